@@ -1,0 +1,131 @@
+/*
+ * oracle.h -- CPU restatement of the reference's draw3d pipeline and of the
+ * north-star ray-tracing path.  TEST INFRASTRUCTURE ONLY.
+ *
+ * Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may
+ * load liboracle.so, and only as the checker / CPU baseline.  The product
+ * (skybox_rt_amd/) never links or calls anything here.
+ *
+ * Parity pinning (see DESIGN.md "Oracle"):
+ *   - raster path: pinned against the reference's committed golden images
+ *     tests/regression/draw3d/triangle_ref_{8..128}.png, tekkaman_ref_128.png,
+ *     box_ref_128.png and tests/regression/raster/triangle_ref_*.png (copied as
+ *     data into tests/golden/).  The reference itself cannot be built here
+ *     (cocogfx/softfloat/ramulator submodules are empty, no RISC-V toolchain).
+ *   - ray-tracing path (MT visibility, shadow, bounce): NO REFERENCE EXISTS
+ *      -> "parity unpinned" beyond primary visibility,
+ *     which is cross-checked against the pinned raster path.
+ *
+ * Numerics: compiled with -ffp-contract=off; every fused multiply-add is an
+ * explicit fmaf() so the HIP kernel (which uses the same explicit fmaf()s)
+ * can be compared bit-for-bit.
+ */
+#ifndef ORACLE_H
+#define ORACLE_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---- flattened scene (produced by oracle/cgltrace.py) -------------------- */
+typedef struct {
+  int32_t prim_offset, prim_count;
+  int32_t tex_slot;                 /* index into textures[], -1 = none */
+  float   znear, zfar;
+  int32_t color_enabled;
+  uint32_t color_writemask;
+  int32_t depth_test, depth_writemask, depth_func;
+  int32_t stencil_test, stencil_func, stencil_zpass, stencil_zfail, stencil_fail;
+  int32_t stencil_ref, stencil_mask, stencil_writemask;
+  int32_t texture_enabled, texture_envmode, texture_minfilter, texture_magfilter;
+  int32_t texture_addressU, texture_addressV;
+  int32_t blend_enabled, blend_src, blend_dst;
+} orc_drawcall_t;
+
+typedef struct {
+  int32_t format, width, height, pad;
+  int64_t offset;                   /* byte offset into texels blob */
+} orc_texture_t;
+
+typedef struct {
+  int32_t num_drawcalls;
+  const orc_drawcall_t* drawcalls;
+  int32_t num_prims;
+  const float* prim_verts;          /* [num_prims][3][10]: xyzw rgba uv */
+  int32_t num_textures;
+  const orc_texture_t* textures;
+  const uint8_t* texels;
+} orc_scene_t;
+
+/* ---- fixed-point primitive record: graphics.h:38-64 rast_prim_t (120 B) --- */
+typedef struct {
+  int32_t edges[3][3];              /* Q15.16, [edge][a,b,c] */
+  int32_t attribs[7][3];            /* Q7.24,  [z,r,g,b,a,u,v][x=a0-a2, y=a1-a2, z=a2] */
+} orc_rast_prim_t;
+
+/* Setup one primitive at W x H (gfxutil.cpp:171-274).  Returns 0 = ok,
+ * 1 = degenerate (rejected), 2 = outside the viewport (rejected by bbox).
+ * bbox = {left, right, top, bottom} in pixels when status != 1. */
+int orc_setup_prim(const float* v /*[3][10]*/, uint32_t width, uint32_t height,
+                   float znear, float zfar, orc_rast_prim_t* out, int32_t bbox[4]);
+
+/* Full draw3d software path (Binning + Rasterizer + shader + OM) over all
+ * drawcalls; color/depth must be pre-cleared by the caller (0xff000000 /
+ * 0xffffffff in the reference, draw3d/main.cpp:47-48).  Row 0 = NDC y=-1.
+ * pid_out (optional): per-pixel global primitive index of the last fragment
+ * that passed the depth/stencil test and was written, -1 if none. */
+int orc_raster_render(const orc_scene_t* scene, uint32_t width, uint32_t height,
+                      uint32_t tile_logsize, uint32_t* color, uint32_t* depth,
+                      int32_t* pid_out);
+
+/* ---- ray tracing -------------------------------------------------------- */
+typedef struct {
+  uint32_t width, height;
+  uint32_t flags;                   /* RT_FLAG_* below */
+  float    light[3];                /* point light in clip (x,y,w) space */
+  uint32_t clear_color;
+  uint32_t bounces;                 /* path-trace depth for RT_FLAG_BOUNCE */
+  uint32_t seed;
+  uint32_t nthreads;                /* CPU worker threads (timing baseline) */
+  uint32_t row_begin, row_end;      /* render rows [begin,end) (0,0 = all) */
+  uint32_t row_step;                /* every row_step-th row (0/1 = all) */
+} orc_rt_params_t;
+
+#define ORC_RT_SHADOWS 0x1u
+
+typedef struct {
+  uint64_t primary_rays, shadow_rays, geometry_hits, occluded;
+  uint64_t node_visits, tri_tests, layer_tests, shaded, texel_bytes;
+} orc_rt_counters_t;
+
+/* BVH in the device layout produced by the product's builder
+ * (skybox_rt_amd/csrc/app/bvh.cpp, DESIGN.md "BVH layout"). */
+typedef struct {
+  int32_t num_nodes;
+  const float* nodes;               /* [num_nodes][16] (4 x float4) */
+  int32_t num_tris;
+  const float* tris;                /* [num_tris][12]  (v0,pid | e1,- | e2,-) */
+} orc_bvh_t;
+
+/* Brute-force (no BVH) reference: closest hit over every geometry triangle,
+ * any-hit shadows.  pid/t optional (may be NULL). */
+int orc_rt_render_bruteforce(const orc_scene_t* scene, const orc_rt_params_t* p,
+                             uint32_t* color, int32_t* pid, float* t,
+                             orc_rt_counters_t* counters);
+
+/* BVH traversal restatement of the HIP kernel's traversal order (for the
+ * algorithmic byte counts and the multi-threaded CPU baseline). */
+int orc_rt_render_bvh(const orc_scene_t* scene, const orc_bvh_t* bvh,
+                      const orc_rt_params_t* p, uint32_t* color, int32_t* pid,
+                      float* t, orc_rt_counters_t* counters);
+
+/* Möller–Trumbore as used by both sides (exposed for unit tests). */
+int orc_mt(const float o[3], const float d[3], const float v0[3],
+           const float e1[3], const float e2[3], float tmin, float* t_out);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,202 @@
+"""ctypes front-end of liboracle.so -- TEST INFRASTRUCTURE ONLY.
+
+Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may
+import this module (see oracle/oracle.h).  It never touches the product.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import subprocess
+
+import numpy as np
+
+from . import cgltrace  # noqa: F401  (re-exported for callers)
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "_build", "liboracle.so")
+
+CLEAR_COLOR = 0xFF000000  # draw3d/main.cpp:47
+CLEAR_DEPTH = 0xFFFFFFFF  # draw3d/main.cpp:48
+RT_SHADOWS = 0x1
+
+
+class DrawcallC(C.Structure):
+    _fields_ = [(n, C.c_int32) for n in ("prim_offset", "prim_count", "tex_slot")] + [
+        ("znear", C.c_float), ("zfar", C.c_float), ("color_enabled", C.c_int32),
+        ("color_writemask", C.c_uint32)] + [(n, C.c_int32) for n in (
+            "depth_test", "depth_writemask", "depth_func", "stencil_test",
+            "stencil_func", "stencil_zpass", "stencil_zfail", "stencil_fail",
+            "stencil_ref", "stencil_mask", "stencil_writemask", "texture_enabled",
+            "texture_envmode", "texture_minfilter", "texture_magfilter",
+            "texture_addressU", "texture_addressV", "blend_enabled", "blend_src",
+            "blend_dst")]
+
+
+class TextureC(C.Structure):
+    _fields_ = [("format", C.c_int32), ("width", C.c_int32), ("height", C.c_int32),
+                ("pad", C.c_int32), ("offset", C.c_int64)]
+
+
+class SceneC(C.Structure):
+    _fields_ = [("num_drawcalls", C.c_int32), ("drawcalls", C.POINTER(DrawcallC)),
+                ("num_prims", C.c_int32), ("prim_verts", C.POINTER(C.c_float)),
+                ("num_textures", C.c_int32), ("textures", C.POINTER(TextureC)),
+                ("texels", C.POINTER(C.c_uint8))]
+
+
+class RtParamsC(C.Structure):
+    _fields_ = [("width", C.c_uint32), ("height", C.c_uint32), ("flags", C.c_uint32),
+                ("light", C.c_float * 3), ("clear_color", C.c_uint32),
+                ("bounces", C.c_uint32), ("seed", C.c_uint32), ("nthreads", C.c_uint32),
+                ("row_begin", C.c_uint32), ("row_end", C.c_uint32), ("row_step", C.c_uint32)]
+
+
+class RtCountersC(C.Structure):
+    _fields_ = [(n, C.c_uint64) for n in (
+        "primary_rays", "shadow_rays", "geometry_hits", "occluded", "node_visits",
+        "tri_tests", "layer_tests", "shaded", "texel_bytes")]
+
+    def as_dict(self):
+        return {n: int(getattr(self, n)) for n, _ in self._fields_}
+
+
+class BvhC(C.Structure):
+    _fields_ = [("num_nodes", C.c_int32), ("nodes", C.POINTER(C.c_float)),
+                ("num_tris", C.c_int32), ("tris", C.POINTER(C.c_float))]
+
+
+def build():
+    subprocess.check_call(["make", "-s", "-C", HERE])
+
+
+_lib = None
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            build()
+        _lib = C.CDLL(LIB_PATH)
+        _lib.orc_raster_render.argtypes = [C.POINTER(SceneC), C.c_uint32, C.c_uint32, C.c_uint32,
+                                           C.c_void_p, C.c_void_p, C.c_void_p]
+        for fn in (_lib.orc_rt_render_bruteforce,):
+            fn.argtypes = [C.POINTER(SceneC), C.POINTER(RtParamsC), C.c_void_p, C.c_void_p,
+                           C.c_void_p, C.POINTER(RtCountersC)]
+        _lib.orc_rt_render_bvh.argtypes = [C.POINTER(SceneC), C.POINTER(BvhC), C.POINTER(RtParamsC),
+                                           C.c_void_p, C.c_void_p, C.c_void_p,
+                                           C.POINTER(RtCountersC)]
+        _lib.orc_setup_prim.argtypes = [C.c_void_p, C.c_uint32, C.c_uint32, C.c_float, C.c_float,
+                                        C.c_void_p, C.c_void_p]
+        _lib.orc_mt.argtypes = [C.c_void_p] * 5 + [C.c_float, C.POINTER(C.c_float)]
+    return _lib
+
+
+def _ptr(a, ctype):
+    return a.ctypes.data_as(C.POINTER(ctype))
+
+
+class OracleScene:
+    """Keeps the numpy buffers alive for the C structs."""
+
+    def __init__(self, scene):
+        self.scene = scene
+        tex_ids = sorted(scene.textures)
+        slot = {tid: i for i, tid in enumerate(tex_ids)}
+        blobs, texs, off = [], [], 0
+        for tid in tex_ids:
+            fmt, w, h, data = scene.textures[tid]
+            texs.append(TextureC(fmt, w, h, 0, off))
+            blobs.append(np.frombuffer(data, np.uint8))
+            off += len(data)
+        self.texels = np.concatenate(blobs) if blobs else np.zeros(1, np.uint8)
+        self.tex_arr = (TextureC * max(1, len(texs)))(*texs)
+        dcs = []
+        for dc in scene.drawcalls:
+            s = dc.states
+            dcs.append(DrawcallC(
+                prim_offset=dc.prim_offset, prim_count=dc.prim_count,
+                tex_slot=slot.get(dc.texture_id, -1) if s["texture_enabled"] else -1,
+                znear=dc.viewport["near"], zfar=dc.viewport["far"],
+                color_enabled=s["color_enabled"], color_writemask=s["color_writemask"] & 0xFFFFFFFF,
+                **{k: s[k] for k in (
+                    "depth_test", "depth_writemask", "depth_func", "stencil_test",
+                    "stencil_func", "stencil_zpass", "stencil_zfail", "stencil_fail",
+                    "stencil_ref", "stencil_mask", "stencil_writemask", "texture_enabled",
+                    "texture_envmode", "texture_minfilter", "texture_magfilter",
+                    "texture_addressU", "texture_addressV", "blend_enabled", "blend_src",
+                    "blend_dst")}))
+        self.dc_arr = (DrawcallC * max(1, len(dcs)))(*dcs)
+        self.verts = np.ascontiguousarray(scene.prim_verts, dtype=np.float32).reshape(-1)
+        if self.verts.size == 0:
+            self.verts = np.zeros(30, np.float32)
+        self.c = SceneC(len(dcs), self.dc_arr, scene.num_prims, _ptr(self.verts, C.c_float),
+                        len(texs), self.tex_arr, _ptr(self.texels, C.c_uint8))
+
+
+def raster_render(oscene: OracleScene, width: int, height: int, tile_logsize: int = 5):
+    color = np.full(width * height, CLEAR_COLOR, np.uint32)
+    depth = np.full(width * height, CLEAR_DEPTH, np.uint32)
+    pid = np.empty(width * height, np.int32)
+    rc = lib().orc_raster_render(C.byref(oscene.c), width, height, tile_logsize,
+                                 color.ctypes.data, depth.ctypes.data, pid.ctypes.data)
+    if rc != 0:
+        raise RuntimeError(f"orc_raster_render failed: {rc}")
+    return (color.reshape(height, width), depth.reshape(height, width),
+            pid.reshape(height, width))
+
+
+def rt_params(width, height, shadows=True, light=(0.0, 60.0, 80.0), nthreads=1,
+              clear_color=CLEAR_COLOR, row_begin=0, row_end=0, row_step=0):
+    p = RtParamsC()
+    p.width, p.height = width, height
+    p.flags = RT_SHADOWS if shadows else 0
+    p.light[:] = [float(np.float32(x)) for x in light]
+    p.clear_color = clear_color
+    p.nthreads = nthreads
+    p.row_begin, p.row_end, p.row_step = row_begin, row_end, row_step
+    return p
+
+
+def rt_render(oscene: OracleScene, params: RtParamsC, bvh=None):
+    """bvh: None (brute force) or (nodes float32[N,16], tris float32[M,12])."""
+    n = params.width * params.height
+    color = np.zeros(n, np.uint32)
+    pid = np.full(n, -1, np.int32)
+    t = np.zeros(n, np.float32)
+    cnt = RtCountersC()
+    if bvh is None:
+        rc = lib().orc_rt_render_bruteforce(C.byref(oscene.c), C.byref(params), color.ctypes.data,
+                                            pid.ctypes.data, t.ctypes.data, C.byref(cnt))
+    else:
+        nodes = np.ascontiguousarray(bvh[0], np.float32)
+        tris = np.ascontiguousarray(bvh[1], np.float32)
+        b = BvhC(nodes.shape[0], _ptr(nodes, C.c_float), tris.shape[0], _ptr(tris, C.c_float))
+        rc = lib().orc_rt_render_bvh(C.byref(oscene.c), C.byref(b), C.byref(params),
+                                     color.ctypes.data, pid.ctypes.data, t.ctypes.data,
+                                     C.byref(cnt))
+    if rc != 0:
+        raise RuntimeError(f"oracle rt render failed: {rc}")
+    h, w = params.height, params.width
+    return color.reshape(h, w), pid.reshape(h, w), t.reshape(h, w), cnt.as_dict()
+
+
+def argb_to_rgba_image(fb: np.ndarray) -> np.ndarray:
+    """ARGB8888 framebuffer (row 0 = bottom) -> RGBA uint8 image, top-down
+    (the reference saves with a negative pitch, draw3d/main.cpp:385-386)."""
+    fb = np.asarray(fb, np.uint32)[::-1]
+    out = np.empty(fb.shape + (4,), np.uint8)
+    out[..., 0] = (fb >> 16) & 0xFF
+    out[..., 1] = (fb >> 8) & 0xFF
+    out[..., 2] = fb & 0xFF
+    out[..., 3] = (fb >> 24) & 0xFF
+    return out
+
+
+def compare_images(a: np.ndarray, b: np.ndarray, tol: int = 0) -> int:
+    """Pixels whose max per-channel |difference| exceeds `tol` (the reference
+    calls cocogfx CompareImages(out, ref, A8R8G8B8, tol): draw3d/main.cpp:507;
+    cocogfx is not vendored, this is the documented interpretation)."""
+    d = np.abs(a.astype(np.int32) - b.astype(np.int32)).max(axis=-1)
+    return int((d > tol).sum())

@@ -1,0 +1,382 @@
+/*
+ * rt.c -- oracle restatement of the north-star ray-tracing path:
+ * per-pixel primary ray generation, Möller–Trumbore closest hit, screen
+ * layers, raster-parity shading of the hit, any-hit shadow rays.
+ * TEST INFRASTRUCTURE ONLY (see oracle.h).
+ *
+ * There is NO reference implementation of this path:
+ * parity of the RT-specific parts is unpinned; primary visibility is
+ * cross-checked against the raster restatement (raster.c), which is pinned by
+ * the reference's golden images.  Anchors used:
+ *   - pixel centres / framebuffer orientation: gfxutil.cpp:190-214 and
+ *     draw3d/main.cpp:385-386 (row 0 = NDC y = -1);
+ *   - MT == homogeneous edge functions for eye rays: gfxutil.cpp:35-75;
+ *   - inclusive coverage (no top-left rule): graphics.cpp:813-825;
+ *   - closest hit with ties -> first drawn (LESS) : graphics.cpp:564-596 with
+ *     per-tile ascending pid order gpu_sw.h:46-60;
+ *   - layers (depth_test off) painted in order: draw3d/main.cpp:239-242;
+ *   - shading of a hit = draw3d shader (kernel.cpp:232-279) evaluated with
+ *     the hit primitive's fixed-point edge functions at the pixel centre.
+ */
+#include <pthread.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include "gfx.h"
+
+/* ---- vector helpers: explicit fmaf, identical op order to the kernel ---- */
+static inline void cross3(float r[3], const float a[3], const float b[3]) {
+  r[0] = fmaf(a[1], b[2], -(a[2] * b[1]));
+  r[1] = fmaf(a[2], b[0], -(a[0] * b[2]));
+  r[2] = fmaf(a[0], b[1], -(a[1] * b[0]));
+}
+static inline float dot3(const float a[3], const float b[3]) {
+  return fmaf(a[2], b[2], fmaf(a[1], b[1], a[0] * b[0]));
+}
+
+/* MT with the reference's inclusive coverage: hit iff det != 0, u >= 0,
+ * v >= 0, u + v <= det (after sign normalisation) and t > tmin.  The single
+ * division is IEEE-correctly-rounded (the kernel uses the same). */
+static inline int mt_hit(const float o[3], const float d[3], const float v0[3],
+                         const float e1[3], const float e2[3], float tmin, float* t_out) {
+  float pvec[3], tvec[3], qvec[3];
+  cross3(pvec, d, e2);
+  const float det = dot3(e1, pvec);
+  tvec[0] = o[0] - v0[0]; tvec[1] = o[1] - v0[1]; tvec[2] = o[2] - v0[2];
+  float u = dot3(tvec, pvec);
+  cross3(qvec, tvec, e1);
+  float v = dot3(d, qvec);
+  float adet = det;
+  if (det < 0.0f) { adet = -det; u = -u; v = -v; }
+  if (!(adet > 0.0f) || u < 0.0f || v < 0.0f || u + v > adet) return 0;
+  const float t = dot3(e2, qvec) / det;
+  if (!(t > tmin)) return 0;
+  *t_out = t;
+  return 1;
+}
+
+int orc_mt(const float o[3], const float d[3], const float v0[3],
+           const float e1[3], const float e2[3], float tmin, float* t_out) {
+  return mt_hit(o, d, v0, e1, e2, tmin, t_out);
+}
+
+/* ---- scene preparation --------------------------------------------------- */
+typedef struct {
+  const orc_scene_t* scene;
+  const orc_bvh_t* bvh;           /* NULL = brute force */
+  orc_rt_params_t p;
+  orc_rast_prim_t* rp;            /* [num_prims] setup at W x H */
+  int* rp_ok;                     /* non-degenerate */
+  int* prim_dc;                   /* drawcall of each prim */
+  orc_dcstate_t* dcst;            /* [num_drawcalls] */
+  float* tri;                     /* [num_prims][9] v0,e1,e2 (clip x,y,w) */
+  int32_t* geom;                  /* geometry prim ids, ascending */
+  int num_geom;
+  int tie_high;                   /* LEQUAL: ties -> highest pid */
+  float sx, sy;
+  uint32_t* color; int32_t* pid; float* tout;
+  orc_rt_counters_t cnt;
+  pthread_mutex_t mu;
+  int next_row;
+} rt_ctx_t;
+
+static int rt_prepare(rt_ctx_t* c, const orc_scene_t* s, const orc_rt_params_t* p) {
+  memset(c, 0, sizeof(*c));
+  c->scene = s;
+  c->p = *p;
+  const int np = s->num_prims > 0 ? s->num_prims : 1;
+  c->rp = (orc_rast_prim_t*)calloc(np, sizeof(orc_rast_prim_t));
+  c->rp_ok = (int*)calloc(np, sizeof(int));
+  c->prim_dc = (int*)calloc(np, sizeof(int));
+  c->tri = (float*)calloc((size_t)np * 9, sizeof(float));
+  c->geom = (int32_t*)calloc(np, sizeof(int32_t));
+  c->dcst = (orc_dcstate_t*)calloc(s->num_drawcalls > 0 ? s->num_drawcalls : 1, sizeof(orc_dcstate_t));
+  int seen_geom = 0, geom_func = -1;
+  for (int d = 0; d < s->num_drawcalls; ++d) {
+    const orc_drawcall_t* dc = &s->drawcalls[d];
+    orc_dcstate_init(&c->dcst[d], s, dc);
+    /* RT-path restrictions (DESIGN.md "Scope"): layers before geometry, one
+     * depth function, no blending/stencil, full colour writes. */
+    if (dc->blend_enabled || dc->stencil_test || (dc->color_writemask & 0xf) != 0xf) return -2;
+    if (dc->depth_test) {
+      const uint32_t f = cgl_to_vx_compare(dc->depth_func);
+      if (f != VX_OM_DEPTH_FUNC_LESS && f != VX_OM_DEPTH_FUNC_LEQUAL) return -2;
+      if (geom_func >= 0 && (int)f != geom_func) return -2;
+      geom_func = (int)f;
+      seen_geom = 1;
+    } else if (seen_geom) {
+      return -2;
+    }
+    for (int i = 0; i < dc->prim_count; ++i) {
+      const int g = dc->prim_offset + i;
+      const float* v = s->prim_verts + (size_t)g * 30;
+      int32_t bb[4];
+      c->rp_ok[g] = orc_setup_prim(v, p->width, p->height, dc->znear, dc->zfar, &c->rp[g], bb) != 1;
+      c->prim_dc[g] = d;
+      float* t = c->tri + (size_t)g * 9;
+      /* clip-space (x, y, w) triangle: v0, e1 = v1 - v0, e2 = v2 - v0 */
+      t[0] = v[0]; t[1] = v[1]; t[2] = v[3];
+      t[3] = v[10] - v[0]; t[4] = v[11] - v[1]; t[5] = v[13] - v[3];
+      t[6] = v[20] - v[0]; t[7] = v[21] - v[1]; t[8] = v[23] - v[3];
+      if (dc->depth_test && c->rp_ok[g]) c->geom[c->num_geom++] = g;
+    }
+  }
+  c->tie_high = (geom_func == VX_OM_DEPTH_FUNC_LEQUAL);
+  c->sx = 2.0f / (float)p->width;
+  c->sy = 2.0f / (float)p->height;
+  pthread_mutex_init(&c->mu, NULL);
+  return 0;
+}
+
+static void rt_release(rt_ctx_t* c) {
+  free(c->rp); free(c->rp_ok); free(c->prim_dc); free(c->tri); free(c->geom); free(c->dcst);
+  pthread_mutex_destroy(&c->mu);
+}
+
+static inline int better(const rt_ctx_t* c, float t, int pid, float bt, int bpid) {
+  if (t < bt) return 1;
+  if (t == bt) return c->tie_high ? (pid > bpid) : (pid < bpid);
+  return 0;
+}
+
+/* ---- BVH traversal: restatement of the kernel's loop -------------------- */
+#define BVH_EMPTY (-1)
+#define BVH_STACK 64
+
+typedef struct { float inv[3], oi[3]; } ray_pre_t;
+
+static inline float safe_dir(float d) {
+  return fabsf(d) < 1e-20f ? (d < 0.0f ? -1e-20f : 1e-20f) : d;
+}
+static inline void ray_pre(ray_pre_t* r, const float o[3], const float d[3]) {
+  for (int k = 0; k < 3; ++k) {
+    r->inv[k] = 1.0f / safe_dir(d[k]);
+    r->oi[k] = o[k] * r->inv[k];
+  }
+}
+/* slab test of child `ch` of a node; returns hit and tnear */
+static inline int slab(const float* n, int ch, const ray_pre_t* r, float tmin, float tmax, float* tnear) {
+  float lo[3], hi[3];
+  for (int k = 0; k < 3; ++k) {
+    lo[k] = fmaf(n[4 * k + 2 * ch + 0], r->inv[k], -r->oi[k]);
+    hi[k] = fmaf(n[4 * k + 2 * ch + 1], r->inv[k], -r->oi[k]);
+  }
+  const float t0 = fminf(lo[0], hi[0]), t1 = fminf(lo[1], hi[1]), t2 = fminf(lo[2], hi[2]);
+  const float u0 = fmaxf(lo[0], hi[0]), u1 = fmaxf(lo[1], hi[1]), u2 = fmaxf(lo[2], hi[2]);
+  const float tn = fmaxf(fmaxf(t0, t1), fmaxf(t2, tmin));
+  const float tf = fminf(fminf(u0, u1), fminf(u2, tmax));
+  *tnear = tn;
+  return tn <= tf;
+}
+
+static inline int32_t node_ref(const float* n, int ch) {
+  int32_t r;
+  memcpy(&r, &n[12 + ch], 4);
+  return r;
+}
+
+/* closest (anyhit=0) or any (anyhit=1) hit; returns hit pid or -1 */
+static int bvh_trace(const rt_ctx_t* c, const float o[3], const float d[3], float tmin,
+                     float tmax, int anyhit, int skip_pid, float* t_out,
+                     uint64_t* visits, uint64_t* tests) {
+  const orc_bvh_t* b = c->bvh;
+  if (b->num_nodes <= 0) return -1;
+  ray_pre_t rp;
+  ray_pre(&rp, o, d);
+  int32_t stack[BVH_STACK];
+  int sp = 0;
+  int32_t ref = 0;
+  float bt = tmax;
+  int bpid = -1;
+  for (;;) {
+    if (ref >= 0) {
+      const float* n = b->nodes + (size_t)ref * 16;
+      ++*visits;
+      const int32_t c0 = node_ref(n, 0), c1 = node_ref(n, 1);
+      float tn0 = 0.0f, tn1 = 0.0f;
+      const float lim = anyhit ? tmax : bt;
+      const int h0 = (c0 != BVH_EMPTY) && slab(n, 0, &rp, tmin, lim, &tn0);
+      const int h1 = (c1 != BVH_EMPTY) && slab(n, 1, &rp, tmin, lim, &tn1);
+      if (h0 && h1) {
+        int32_t near = c0, far = c1;
+        if (tn1 < tn0) { near = c1; far = c0; }
+        if (sp < BVH_STACK) stack[sp++] = far;
+        ref = near;
+        continue;
+      } else if (h0) { ref = c0; continue; }
+      else if (h1) { ref = c1; continue; }
+    } else {
+      const uint32_t lr = (uint32_t)ref;
+      const uint32_t first = (lr >> 4) & 0x07ffffffu, count = (lr & 15u) + 1u;
+      for (uint32_t k = 0; k < count; ++k) {
+        const float* tr = b->tris + (size_t)(first + k) * 12;
+        int32_t pid;
+        memcpy(&pid, &tr[3], 4);
+        ++*tests;
+        if (pid == skip_pid) continue;
+        /* the BVH supplies structure only; vertices come from the oracle's own
+         * setup so a wrong device triangle record cannot hide here */
+        const float* tv = c->tri + (size_t)pid * 9;
+        float t;
+        if (!mt_hit(o, d, tv, tv + 3, tv + 6, tmin, &t)) continue;
+        if (anyhit) {
+          if (t < tmax) { *t_out = t; return pid; }
+          continue;
+        }
+        if (better(c, t, pid, bt, bpid)) { bt = t; bpid = pid; }
+      }
+    }
+    if (sp == 0) break;
+    ref = stack[--sp];
+  }
+  if (bpid >= 0) *t_out = bt;
+  return bpid;
+}
+
+/* brute force over the geometry list (ascending pid) */
+static int brute_trace(const rt_ctx_t* c, const float o[3], const float d[3], float tmin,
+                       float tmax, int anyhit, int skip_pid, float* t_out, uint64_t* tests) {
+  float bt = tmax;
+  int bpid = -1;
+  for (int k = 0; k < c->num_geom; ++k) {
+    const int g = c->geom[k];
+    ++*tests;
+    if (g == skip_pid) continue;
+    const float* tr = c->tri + (size_t)g * 9;
+    float t;
+    if (!mt_hit(o, d, tr, tr + 3, tr + 6, tmin, &t)) continue;
+    if (anyhit) {
+      if (t < tmax) { *t_out = t; return g; }
+      continue;
+    }
+    if (better(c, t, g, bt, bpid)) { bt = t; bpid = g; }
+  }
+  if (bpid >= 0) *t_out = bt;
+  return bpid;
+}
+
+static inline uint32_t shadow_attenuate(uint32_t c) {
+  return (c & 0xff000000u) | ((c >> 1) & 0x007f7f7fu);
+}
+
+static uint32_t shade_at(const rt_ctx_t* c, int g, uint32_t x, uint32_t y, orc_rt_counters_t* k) {
+  const orc_rast_prim_t* p = &c->rp[g];
+  const orc_dcstate_t* st = &c->dcst[c->prim_dc[g]];
+  const int32_t e0 = orc_edge_eval(p->edges[0], x, y);
+  const int32_t e1 = orc_edge_eval(p->edges[1], x, y);
+  const int32_t e2 = orc_edge_eval(p->edges[2], x, y);
+  uint32_t z;
+  ++k->shaded;
+  if (st->tex_enabled)
+    k->texel_bytes += (st->tex_filter == VX_TEX_FILTER_BILINEAR ? 4u : 1u) * vx_format_stride((int)st->tex_format);
+  return orc_shade(st, p, e0, e1, e2, &z);
+}
+
+static void rt_row(rt_ctx_t* c, uint32_t y, orc_rt_counters_t* k) {
+  const orc_scene_t* s = c->scene;
+  const uint32_t W = c->p.width;
+  for (uint32_t x = 0; x < W; ++x) {
+    const float o[3] = {0.0f, 0.0f, 0.0f};
+    const float d[3] = {fmaf((float)x + 0.5f, c->sx, -1.0f),
+                        fmaf((float)y + 0.5f, c->sy, -1.0f), 1.0f};
+    ++k->primary_rays;
+    float t = 0.0f;
+    const int hit = c->bvh ? bvh_trace(c, o, d, 0.0f, INFINITY, 0, -1, &t, &k->node_visits, &k->tri_tests)
+                           : brute_trace(c, o, d, 0.0f, INFINITY, 0, -1, &t, &k->tri_tests);
+    uint32_t col = c->p.clear_color;
+    int32_t opid = -1;
+    if (hit >= 0) {
+      ++k->geometry_hits;
+      col = shade_at(c, hit, x, y, k);
+      opid = hit;
+      if (c->p.flags & ORC_RT_SHADOWS) {
+        /* origin pulled toward the eye by 2^-12 of t, segment to the light */
+        const float tt = t * 0.999755859375f;
+        const float so[3] = {d[0] * tt, d[1] * tt, d[2] * tt};
+        const float sd[3] = {c->p.light[0] - so[0], c->p.light[1] - so[1], c->p.light[2] - so[2]};
+        float ts;
+        ++k->shadow_rays;
+        const int occ = c->bvh ? bvh_trace(c, so, sd, 0.0f, 1.0f, 1, hit, &ts, &k->node_visits, &k->tri_tests)
+                               : brute_trace(c, so, sd, 0.0f, 1.0f, 1, hit, &ts, &k->tri_tests);
+        if (occ >= 0) { ++k->occluded; col = shadow_attenuate(col); }
+      }
+    } else {
+      /* screen layers (depth_test off): painter order, last covering pid */
+      int lpid = -1;
+      for (int dd = 0; dd < s->num_drawcalls; ++dd) {
+        const orc_drawcall_t* dc = &s->drawcalls[dd];
+        if (dc->depth_test) continue;
+        for (int i = dc->prim_count - 1; i >= 0; --i) {
+          const int g = dc->prim_offset + i;
+          if (!c->rp_ok[g]) continue;
+          ++k->layer_tests;
+          const float* tr = c->tri + (size_t)g * 9;
+          float tl;
+          if (mt_hit(o, d, tr, tr + 3, tr + 6, 0.0f, &tl)) { lpid = g; break; }
+        }
+      }
+      if (lpid >= 0) { col = shade_at(c, lpid, x, y, k); opid = lpid; }
+    }
+    const uint64_t px = (uint64_t)y * W + x;
+    c->color[px] = col;
+    if (c->pid) c->pid[px] = opid;
+    if (c->tout) c->tout[px] = hit >= 0 ? t : 0.0f;
+  }
+}
+
+static void* rt_worker(void* arg) {
+  rt_ctx_t* c = (rt_ctx_t*)arg;
+  orc_rt_counters_t k;
+  memset(&k, 0, sizeof(k));
+  const uint32_t r0 = c->p.row_begin, r1 = c->p.row_end ? c->p.row_end : c->p.height;
+  const uint32_t step = c->p.row_step > 1 ? c->p.row_step : 1;
+  for (;;) {
+    pthread_mutex_lock(&c->mu);
+    const int i = c->next_row++;
+    pthread_mutex_unlock(&c->mu);
+    const uint64_t y = r0 + (uint64_t)i * step;
+    if (y >= r1) break;
+    rt_row(c, (uint32_t)y, &k);
+  }
+  pthread_mutex_lock(&c->mu);
+  uint64_t* dst = (uint64_t*)&c->cnt;
+  const uint64_t* src = (const uint64_t*)&k;
+  for (size_t i = 0; i < sizeof(k) / sizeof(uint64_t); ++i) dst[i] += src[i];
+  pthread_mutex_unlock(&c->mu);
+  return NULL;
+}
+
+static int rt_run(const orc_scene_t* scene, const orc_bvh_t* bvh, const orc_rt_params_t* p,
+                  uint32_t* color, int32_t* pid, float* t, orc_rt_counters_t* counters) {
+  if (!scene || !p || !color || p->width == 0 || p->height == 0) return -1;
+  rt_ctx_t c;
+  int err = rt_prepare(&c, scene, p);
+  if (err) { rt_release(&c); return err; }
+  c.bvh = bvh;
+  c.color = color; c.pid = pid; c.tout = t;
+  const uint32_t nt = p->nthreads > 1 ? p->nthreads : 1;
+  if (nt == 1) {
+    rt_worker(&c);
+  } else {
+    pthread_t* th = (pthread_t*)malloc(sizeof(pthread_t) * nt);
+    for (uint32_t i = 0; i < nt; ++i) pthread_create(&th[i], NULL, rt_worker, &c);
+    for (uint32_t i = 0; i < nt; ++i) pthread_join(th[i], NULL);
+    free(th);
+  }
+  if (counters) *counters = c.cnt;
+  rt_release(&c);
+  return 0;
+}
+
+int orc_rt_render_bruteforce(const orc_scene_t* scene, const orc_rt_params_t* p,
+                             uint32_t* color, int32_t* pid, float* t,
+                             orc_rt_counters_t* counters) {
+  return rt_run(scene, NULL, p, color, pid, t, counters);
+}
+
+int orc_rt_render_bvh(const orc_scene_t* scene, const orc_bvh_t* bvh,
+                      const orc_rt_params_t* p, uint32_t* color, int32_t* pid,
+                      float* t, orc_rt_counters_t* counters) {
+  if (!bvh) return -1;
+  return rt_run(scene, bvh, p, color, pid, t, counters);
+}
