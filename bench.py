@@ -1,0 +1,229 @@
+#!/usr/bin/env python3
+"""bench.py -- headline benchmark: Mrays/s of the MI355X ray-tracing hot path.
+
+Workload (BASELINE.json configs[2], the metric's config): tekkaman.cgltrace,
+1024x1024, one primary ray per pixel + one any-hit shadow ray per geometry
+hit, BVH traversal with the per-wave LDS stack.  A "step" is one full frame:
+vx_start + vx_ready_wait of the RT kernel image through libvortex-hip.so
+(inputs already resident in HBM).  With N GPUs (torchrun, one rank per GPU)
+the frame grows to ~1024*sqrt(N) on a side (weak scaling: ~1M pixels per
+GPU), 32x32 tiles are dealt tile t -> rank t % N, and each step ends with an
+RCCL gather of the compact tile buffers to rank 0 plus a de-interleave there
+(SURVEY.md 8(e)).
+
+Rank 0 prints one JSON line.  Everything else goes to stderr.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import math
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+SCENE = os.path.join(ROOT, "tests", "golden", "scenes", "tekkaman.cgltrace")
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
+NODE_BYTES, TRI_BYTES, PIXEL_BYTES = 64, 36, 4
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def algorithmic_bytes(st: dict, pixels: int) -> int:
+    """node bytes x nodes visited + 36 B x triangles tested
+    (BVH leaves and screen layers) + texel bytes per shaded pixel + 4 B per
+    pixel written.  Counts come from the instrumented kernel variant, whose
+    counters tests/test_gpu_rt.py checks equal to the oracle's traversal."""
+    return (NODE_BYTES * st["node_visits"] + TRI_BYTES * (st["tri_tests"] + st["layer_tests"])
+            + st["texel_bytes"] + PIXEL_BYTES * pixels)
+
+
+def frame_side(n_gpus: int, base: int) -> int:
+    return max(32, int(round(base * math.sqrt(n_gpus) / 32.0)) * 32)
+
+
+def cpu_baseline(shadows: bool, side: int, light, budget_s: float):
+    """Oracle (C port of the same algorithm, oracle/rt.c) on the host cores,
+    BVH traversal identical to the kernel's, full frames until budget_s."""
+    from oracle import py_oracle as po
+    from skybox_rt_amd import rt as rtmod
+    cores = max(1, min(16, os.cpu_count() or 1))
+    osc = po.OracleScene(po.cgltrace.load(SCENE))
+    bvh = rtmod.Scene.load(SCENE).bvh()
+    p = po.rt_params(side, side, shadows=shadows, light=light, nthreads=cores)
+    frames, rays, t0 = 0, 0, time.perf_counter()
+    while True:
+        _, _, _, k = po.rt_render(osc, p, bvh=bvh)
+        frames += 1
+        rays += k["primary_rays"] + k["shadow_rays"]
+        el = time.perf_counter() - t0
+        if el >= budget_s:
+            break
+    return {"value": rays / el / 1e6, "unit": "Mrays/s", "cores": cores, "kind": "port",
+            "sample": f"{frames} full {side}x{side} frames of the same workload "
+                      f"({el:.1f} s, oracle/rt.c BVH traversal, {cores} threads)"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--size", type=int, default=1024)
+    ap.add_argument("--no-shadows", action="store_true")
+    ap.add_argument("--cpu-budget", type=float, default=10.0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    n_gpus = max(world, 1)
+    dist = None
+    import torch
+    if world > 1:
+        import torch.distributed as dist
+        torch.cuda.set_device(local_rank)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+    from skybox_rt_amd import rt
+
+    shadows = not args.no_shadows
+    light = rt.DEFAULT_LIGHT
+    side = args.size if n_gpus == 1 else frame_side(n_gpus, args.size)
+    scene = rt.Scene.load(SCENE)
+    info = scene.info()
+    r = rt.Renderer(scene)
+
+    # algorithmic bytes per launch from the instrumented variant (untimed)
+    r.configure(side, side, shadows=shadows, light=light, shard_index=rank, shard_count=n_gpus,
+                instrumented=True)
+    r.render()
+    inst = r.stats()
+    pixels_local = inst["primary_rays"]
+    alg_bytes = algorithmic_bytes(inst, pixels_local)
+
+    r.configure(side, side, shadows=shadows, light=light, shard_index=rank, shard_count=n_gpus)
+    gather = None
+    if world > 1:
+        import ctypes
+        hip = ctypes.CDLL("libamdhip64.so.7")  # torch's runtime, already loaded
+        tiles_x = (side + 31) // 32
+        total_tiles = tiles_x * tiles_x
+        max_local = (total_tiles + n_gpus - 1) // n_gpus
+        local = torch.empty(max_local * 1024, dtype=torch.int32, device="cuda")
+        parts = [torch.empty_like(local) for _ in range(n_gpus)] if rank == 0 else None
+        # de-interleave map on rank 0: image index for every (rank, local tile, task)
+        if rank == 0:
+            g = np.arange(n_gpus)[:, None, None]
+            lt = np.arange(max_local)[None, :, None]
+            t = np.arange(1024)[None, None, :]
+            gt = g + lt * n_gpus
+            blk, ln = t >> 6, t & 63
+            y = (gt // tiles_x) * 32 + (blk >> 2) * 8 + (ln >> 3)
+            x = (gt % tiles_x) * 32 + (blk & 3) * 8 + (ln & 7)
+            valid = (gt < total_tiles) & (x < side) & (y < side)
+            src = np.nonzero(valid.reshape(-1))[0]
+            dst = (y * side + x).reshape(-1)[src]
+            src_t = torch.from_numpy(src).cuda()
+            dst_t = torch.from_numpy(dst).cuda()
+            image = torch.empty(side * side, dtype=torch.int32, device="cuda")
+        dev_ptr, nbytes = r.framebuffer_device()
+
+        def gather():
+            hip.hipMemcpy(ctypes.c_void_p(local.data_ptr()), ctypes.c_void_p(dev_ptr),
+                          ctypes.c_size_t(nbytes), 3)
+            dist.gather(local, parts, dst=0)
+            if rank == 0:
+                image[dst_t] = torch.stack(parts).reshape(-1)[src_t]
+
+    def step():
+        r.render()
+        if gather is not None:
+            gather()
+
+    for _ in range(args.warmup):
+        step()
+    if dist is not None:
+        dist.barrier()
+    torch.cuda.synchronize()
+    kernel_ms = []
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+        kernel_ms.append(r.stats()["kernel_ms"])
+    torch.cuda.synchronize()
+    if dist is not None:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    st = r.stats()
+    rays_local = st["primary_rays"] + st["shadow_rays"]
+    if dist is not None:
+        t = torch.tensor([elapsed, float(rays_local)], dtype=torch.float64, device="cuda")
+        mx = t.clone()
+        dist.all_reduce(mx, op=dist.ReduceOp.MAX)
+        sm = t.clone()
+        dist.all_reduce(sm, op=dist.ReduceOp.SUM)
+        elapsed, rays_total = float(mx[0]), float(sm[1])
+    else:
+        rays_total = float(rays_local)
+    ms_per_step = elapsed / args.steps * 1e3
+    value = rays_total * args.steps / elapsed / 1e6
+    avg_kernel_ms = float(np.mean(kernel_ms))
+    achieved = alg_bytes / (avg_kernel_ms * 1e-3) / 1e9
+    if rank != 0:
+        dist.destroy_process_group()
+        return
+    out = {
+        "metric": "Mrays/sec per GPU + achieved HBM GB/s, 1024^2 primary+shadow tekkaman",
+        "value": round(value, 3),
+        "unit": "Mrays/s",
+        "n_gpus": n_gpus,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(ms_per_step, 5),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f32",
+        "data": "tekkaman.cgltrace from the reference's regression data (tests/golden/scenes)",
+        "config": {
+            "workload": f"{side}x{side} {'primary+shadow' if shadows else 'primary'} rays, "
+                        f"tekkaman.cgltrace, BVH2 + LDS stack",
+            "scene": "tekkaman.cgltrace", "width": side, "height": side,
+            "shadow_rays": shadows, "light_clip_xyw": list(light),
+            "parallelism": f"tiles32 mod {n_gpus}" + (" + rccl gather" if n_gpus > 1 else ""),
+            "bvh_nodes": info["bvh_nodes"], "bvh_depth": info["bvh_depth"],
+            "grid": st["grid"], "block": st["block"],
+            "rays_per_frame": int(rays_total),
+            "mrays_per_s_per_gpu": round(value / n_gpus, 3),
+            "kernel_ms": round(avg_kernel_ms, 5),
+            "kernel_mrays_per_s": round(rays_local / (avg_kernel_ms * 1e-3) / 1e6, 3),
+        },
+        "roofline": {
+            "bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
+            "algorithmic_bytes_per_launch": int(alg_bytes),
+            "counts": {k: int(inst[k]) for k in ("node_visits", "tri_tests", "layer_tests",
+                                                 "texel_bytes", "primary_rays", "shadow_rays")},
+        },
+        "cpu_baseline": None,
+    }
+    if n_gpus == 1 and not args.no_cpu_baseline:
+        try:
+            out["cpu_baseline"] = cpu_baseline(shadows, side, light, args.cpu_budget)
+        except Exception as e:  # the baseline is reported, not required
+            log(f"cpu baseline failed: {e}")
+    print(json.dumps(out), flush=True)
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,32 @@
+/*
+ * vortex_hip.h -- HIP-driver extensions beyond the reference ABI.
+ *
+ * These are NOT part of runtime/include/vortex.h; they exist so a host app can
+ * hand device buffers to PyTorch/RCCL (framebuffer gather) and
+ * read per-launch device timing.  Resolve them through vx_driver_symbol()
+ * (exported by libvortex.so) so the driver stays a plain dlopen plugin.
+ */
+#ifndef VX_VORTEX_HIP_H
+#define VX_VORTEX_HIP_H
+
+#include "vortex.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* libvortex.so: dlsym() in the loaded driver (NULL if absent). */
+void* vx_driver_symbol(const char* name);
+
+/* libvortex-hip.so extensions */
+typedef int (*vx_hip_mem_ptr_t)(vx_buffer_h hbuffer, void** device_ptr);
+typedef int (*vx_hip_stream_t)(vx_device_h hdevice, void** hip_stream);
+typedef int (*vx_hip_last_run_t)(vx_device_h hdevice, double* kernel_ms,
+                                 uint32_t* grid, uint32_t* block);
+typedef int (*vx_hip_device_id_t)(vx_device_h hdevice, int* device_id);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif

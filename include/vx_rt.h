@@ -1,0 +1,90 @@
+/*
+ * vx_rt.h -- C-ABI of the ray-tracing host app (librtapp.so).
+ *
+ * This is the host side of the north-star "tests/regression RT app": the
+ * analog of tests/regression/draw3d/main.cpp (scene load, per-frame state
+ * setup, upload, vx_start/vx_ready_wait, framebuffer read-back), built on the
+ * public vortex.h API and therefore on whatever driver VORTEX_DRIVER selects
+ * (libvortex-hip.so on MI355X).  The rtapp executable is its CLI with
+ * draw3d's flags; Python (skybox_rt_amd.rt) and bench.py bind it via ctypes.
+ *
+ * All functions return 0 on success and a negative value on error; the last
+ * error message of the calling thread is available from rt_last_error().
+ */
+#ifndef VX_RT_H
+#define VX_RT_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct rt_scene* rt_scene_h;
+typedef struct rt_renderer* rt_renderer_h;
+
+typedef struct {
+  uint32_t num_drawcalls, num_prims, num_geometry, num_layer, num_textures;
+  uint32_t bvh_nodes, bvh_tris, bvh_leaves, bvh_depth;
+  uint32_t pad;
+  double parse_ms, bvh_ms;
+} rt_scene_info_t;
+
+#define RT_RENDER_SHADOWS 0x1u
+#define RT_RENDER_INSTRUMENTED 0x100u  /* use the counting kernel variant */
+
+typedef struct {
+  uint32_t width, height;
+  uint32_t flags;             /* RT_RENDER_* */
+  float light[3];             /* point light, clip (x, y, w) space */
+  uint32_t clear_color;       /* ARGB8888, 0xff000000 in draw3d */
+  uint32_t shard_index;       /* this device renders 32x32 tiles t with */
+  uint32_t shard_count;       /*   t % shard_count == shard_index */
+} rt_render_params_t;
+
+typedef struct {
+  uint64_t primary_rays, shadow_rays, geometry_hits, occluded;
+  uint64_t node_visits, tri_tests, layer_tests, shaded, texel_bytes; /* instrumented only */
+  uint64_t tasks;             /* VX_CSR_MINSTRET */
+  double kernel_ms;           /* HIP-event time of the last launch */
+  uint32_t grid, block;       /* launch geometry chosen by the driver */
+  uint32_t num_tasks, local_tiles;
+} rt_stats_t;
+
+const char* rt_last_error(void);
+
+int rt_scene_load(const char* path, rt_scene_h* out);
+int rt_scene_free(rt_scene_h scene);
+int rt_scene_info(rt_scene_h scene, rt_scene_info_t* info);
+/* flattened triangles, float[num_prims][3][10] (x,y,z,w, r,g,b,a, u,v) */
+int rt_scene_export_prims(rt_scene_h scene, float* out, uint64_t count);
+/* BVH arrays: float[bvh_nodes][16], float[bvh_tris][12] */
+int rt_scene_export_bvh(rt_scene_h scene, float* nodes, float* tris);
+/* fixed-point shading records (rt_prim_t) at width x height: int32[num_prims][32] */
+int rt_scene_setup_prims(rt_scene_h scene, uint32_t width, uint32_t height, int32_t* out,
+                         uint64_t count);
+
+/* kernel_dir: directory holding rt_kernel.vxbin / rt_kernel_stats.vxbin
+ * (NULL = next to librtapp.so).  Opens its own vortex device. */
+int rt_renderer_create(rt_scene_h scene, const char* kernel_dir, rt_renderer_h* out);
+int rt_renderer_free(rt_renderer_h r);
+int rt_renderer_configure(rt_renderer_h r, const rt_render_params_t* params);
+int rt_render_start(rt_renderer_h r);
+int rt_render_wait(rt_renderer_h r);
+int rt_render(rt_renderer_h r);  /* start + wait */
+int rt_render_stats(rt_renderer_h r, rt_stats_t* stats);
+/* linear W*H framebuffer (shard_count == 1) or compact tile buffer
+ * (local_tiles * 1024 pixels in task order) */
+int rt_read_framebuffer(rt_renderer_h r, uint32_t* out, uint64_t count);
+
+/* device pointer + byte size of the output buffer (for RCCL gathers) and the
+ * HIP stream the kernel runs on (for stream-ordered consumers) */
+int rt_framebuffer_device(rt_renderer_h r, void** device_ptr, uint64_t* bytes);
+int rt_device_stream(rt_renderer_h r, void** hip_stream);
+int rt_device_caps(rt_renderer_h r, uint64_t caps[8]);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* VX_RT_H */

@@ -118,7 +118,9 @@ static int rt_prepare(rt_ctx_t* c, const orc_scene_t* s, const orc_rt_params_t* 
       t[0] = v[0]; t[1] = v[1]; t[2] = v[3];
       t[3] = v[10] - v[0]; t[4] = v[11] - v[1]; t[5] = v[13] - v[3];
       t[6] = v[20] - v[0]; t[7] = v[21] - v[1]; t[8] = v[23] - v[3];
-      if (dc->depth_test && c->rp_ok[g]) c->geom[c->num_geom++] = g;
+      /* every depth-tested triangle is geometry: MT rejects degenerate ones
+       * (det == 0) by itself, exactly like the kernel */
+      if (dc->depth_test) c->geom[c->num_geom++] = g;
     }
   }
   c->tie_high = (geom_func == VX_OM_DEPTH_FUNC_LEQUAL);
@@ -308,7 +310,6 @@ static void rt_row(rt_ctx_t* c, uint32_t y, orc_rt_counters_t* k) {
         if (dc->depth_test) continue;
         for (int i = dc->prim_count - 1; i >= 0; --i) {
           const int g = dc->prim_offset + i;
-          if (!c->rp_ok[g]) continue;
           ++k->layer_tests;
           const float* tr = c->tri + (size_t)g * 9;
           float tl;

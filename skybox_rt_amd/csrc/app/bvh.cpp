@@ -1,0 +1,190 @@
+// bvh.cpp -- see bvh.h.
+#include "bvh.h"
+
+#include <algorithm>
+#include <array>
+#include <cmath>
+#include <cstring>
+
+namespace rt {
+namespace {
+
+struct Box {
+  float lo[3] = {INFINITY, INFINITY, INFINITY};
+  float hi[3] = {-INFINITY, -INFINITY, -INFINITY};
+  void grow(const float* p) {
+    for (int k = 0; k < 3; ++k) {
+      lo[k] = std::min(lo[k], p[k]);
+      hi[k] = std::max(hi[k], p[k]);
+    }
+  }
+  void grow(const Box& b) {
+    for (int k = 0; k < 3; ++k) {
+      lo[k] = std::min(lo[k], b.lo[k]);
+      hi[k] = std::max(hi[k], b.hi[k]);
+    }
+  }
+  double area() const {
+    if (lo[0] > hi[0]) return 0.0;
+    const double dx = (double)hi[0] - lo[0], dy = (double)hi[1] - lo[1], dz = (double)hi[2] - lo[2];
+    return 2.0 * (dx * dy + dy * dz + dz * dx);
+  }
+};
+
+class Builder {
+ public:
+  Builder(const std::vector<BuildTri>& t, Bvh* out) : t_(t), out_(out) {
+    box_.resize(t.size());
+    cen_.resize(t.size());
+    float ext = 0.0f;
+    for (size_t i = 0; i < t.size(); ++i) {
+      for (int c = 0; c < 3; ++c) {
+        box_[i].grow(t[i].v[c]);
+        for (int k = 0; k < 3; ++k) ext = std::max(ext, std::fabs(t[i].v[c][k]));
+      }
+      for (int k = 0; k < 3; ++k) cen_[i][k] = (box_[i].lo[k] + box_[i].hi[k]) * 0.5f;
+    }
+    pad_ = std::max(ext * (1.0f / 65536.0f), 1e-6f);
+    idx_.resize(t.size());
+    for (size_t i = 0; i < t.size(); ++i) idx_[i] = (uint32_t)i;
+  }
+
+  void run() {
+    out_->nodes.clear();
+    out_->tris.clear();
+    out_->depth = 0;
+    out_->leaves = 0;
+    if (t_.empty()) return;
+    if (t_.size() <= kBvhLeafSize) {  // root must be internal: leaf + empty child
+      out_->nodes.resize(1);
+      Box b = range_box(0, (uint32_t)t_.size());
+      const int32_t leaf = make_leaf(0, (uint32_t)t_.size());
+      set_child(0, 0, b, leaf);
+      set_child(0, 1, Box(), RT_EMPTY_REF);
+      out_->depth = 1;
+      return;
+    }
+    build(0, (uint32_t)t_.size(), 1);
+  }
+
+ private:
+  Box range_box(uint32_t b, uint32_t e) const {
+    Box r;
+    for (uint32_t i = b; i < e; ++i) r.grow(box_[idx_[i]]);
+    return r;
+  }
+
+  int32_t make_leaf(uint32_t b, uint32_t e) {
+    const uint32_t first = (uint32_t)out_->tris.size();
+    for (uint32_t i = b; i < e; ++i) {
+      const BuildTri& s = t_[idx_[i]];
+      rt_tri_t r;
+      std::memset(&r, 0, sizeof(r));
+      // v0, e1 = v1 - v0, e2 = v2 - v0 in fp32 (same as oracle/rt.c)
+      for (int k = 0; k < 3; ++k) {
+        r.v[k] = s.v[0][k];
+        r.v[4 + k] = s.v[1][k] - s.v[0][k];
+        r.v[8 + k] = s.v[2][k] - s.v[0][k];
+      }
+      std::memcpy(&r.v[3], &s.pid, 4);
+      out_->tris.push_back(r);
+    }
+    ++out_->leaves;
+    return (int32_t)(RT_LEAF_FLAG | (first << 4) | (e - b - 1));
+  }
+
+  void set_child(uint32_t node, int ch, const Box& b, int32_t ref) {
+    rt_node_t& n = out_->nodes[node];
+    for (int k = 0; k < 3; ++k) {
+      const bool empty = ref == RT_EMPTY_REF;
+      n.v[4 * k + 2 * ch + 0] = empty ? 0.0f : b.lo[k] - pad_;
+      n.v[4 * k + 2 * ch + 1] = empty ? 0.0f : b.hi[k] + pad_;
+    }
+    std::memcpy(&n.v[12 + ch], &ref, 4);
+  }
+
+  // returns the child reference for range [b, e)
+  int32_t build(uint32_t b, uint32_t e, uint32_t depth) {
+    const uint32_t n = e - b;
+    if (n <= kBvhLeafSize) return make_leaf(b, e);
+    out_->depth = std::max(out_->depth, depth);
+    const uint32_t node = (uint32_t)out_->nodes.size();
+    out_->nodes.emplace_back();
+    std::memset(&out_->nodes[node], 0, sizeof(rt_node_t));
+    const uint32_t mid = split(b, e);
+    const Box lb = range_box(b, mid), rb = range_box(mid, e);
+    const int32_t l = build(b, mid, depth + 1);
+    const int32_t r = build(mid, e, depth + 1);
+    set_child(node, 0, lb, l);
+    set_child(node, 1, rb, r);
+    return (int32_t)node;
+  }
+
+  // binned SAH over centroids on the widest centroid axis; stable partition
+  uint32_t split(uint32_t b, uint32_t e) {
+    float cl[3] = {INFINITY, INFINITY, INFINITY}, ch[3] = {-INFINITY, -INFINITY, -INFINITY};
+    for (uint32_t i = b; i < e; ++i)
+      for (int k = 0; k < 3; ++k) {
+        cl[k] = std::min(cl[k], cen_[idx_[i]][k]);
+        ch[k] = std::max(ch[k], cen_[idx_[i]][k]);
+      }
+    int axis = 0;
+    for (int k = 1; k < 3; ++k)
+      if (ch[k] - cl[k] > ch[axis] - cl[axis]) axis = k;
+    const float ext = ch[axis] - cl[axis];
+    const uint32_t median = b + (e - b) / 2;
+    if (!(ext > 0.0f)) return median;
+    auto bin_of = [&](uint32_t t) {
+      int bi = (int)((cen_[t][axis] - cl[axis]) * ((float)kBvhBins / ext));
+      return std::min(std::max(bi, 0), (int)kBvhBins - 1);
+    };
+    Box bb[kBvhBins];
+    uint32_t cnt[kBvhBins] = {};
+    for (uint32_t i = b; i < e; ++i) {
+      const int bi = bin_of(idx_[i]);
+      bb[bi].grow(box_[idx_[i]]);
+      ++cnt[bi];
+    }
+    double best = INFINITY;
+    uint32_t best_s = 0;
+    for (uint32_t s = 1; s < kBvhBins; ++s) {
+      Box l, r;
+      uint32_t nl = 0, nr = 0;
+      for (uint32_t i = 0; i < s; ++i) { l.grow(bb[i]); nl += cnt[i]; }
+      for (uint32_t i = s; i < kBvhBins; ++i) { r.grow(bb[i]); nr += cnt[i]; }
+      if (nl == 0 || nr == 0) continue;
+      const double c = nl * l.area() + nr * r.area();
+      if (c < best) { best = c; best_s = s; }
+    }
+    if (best_s == 0) return median;
+    auto mid_it = std::stable_partition(idx_.begin() + b, idx_.begin() + e,
+                                        [&](uint32_t t) { return (uint32_t)bin_of(t) < best_s; });
+    return (uint32_t)(mid_it - idx_.begin());
+  }
+
+  const std::vector<BuildTri>& t_;
+  Bvh* out_;
+  std::vector<Box> box_;
+  std::vector<std::array<float, 3>> cen_;
+  std::vector<uint32_t> idx_;
+  float pad_ = 0.0f;
+};
+
+}  // namespace
+
+int BuildBvh(const std::vector<BuildTri>& tris, Bvh* out, std::string* error) {
+  if (out == nullptr) return -1;
+  if (tris.size() >= (1u << 26)) {
+    if (error) *error = "too many triangles for the 27-bit leaf index";
+    return -1;
+  }
+  Builder b(tris, out);
+  b.run();
+  if (out->depth > RT_MAX_STACK) {
+    if (error) *error = "BVH deeper than RT_MAX_STACK";
+    return -1;
+  }
+  return 0;
+}
+
+}  // namespace rt

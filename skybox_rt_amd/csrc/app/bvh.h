@@ -1,0 +1,36 @@
+// bvh.h -- deterministic binned-SAH BVH2 builder (host).
+//
+// NO REFERENCE: the reference has no ray tracer; its
+// acceleration structure for the same scenes is the screen-tile binning of
+// gfxutil.cpp:237-290.  The BVH is built once per scene in clip (x, y, w)
+// space, so it is independent of the render resolution.  Boxes are padded by
+// 2^-16 of the scene extent so that fp32 slab tests are conservative for every
+// hit the (inclusive) Möller–Trumbore test can report.
+#pragma once
+
+#include <cstdint>
+#include <string>
+#include <vector>
+
+#include "../kernels/rt_common.h"
+
+namespace rt {
+
+struct BuildTri {
+  float v[3][3];  // clip-space (x, y, w) of the three corners
+  int32_t pid;    // global primitive id
+};
+
+struct Bvh {
+  std::vector<rt_node_t> nodes;  // root = 0 (empty if no triangles)
+  std::vector<rt_tri_t> tris;    // leaf order
+  uint32_t depth = 0;            // internal levels on the deepest path
+  uint32_t leaves = 0;
+};
+
+constexpr uint32_t kBvhLeafSize = 4;
+constexpr uint32_t kBvhBins = 16;
+
+int BuildBvh(const std::vector<BuildTri>& tris, Bvh* out, std::string* error);
+
+}  // namespace rt

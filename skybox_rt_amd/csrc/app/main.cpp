@@ -1,0 +1,121 @@
+// main.cpp -- rtapp: command-line RT regression app.
+//
+// Flag set and output follow tests/regression/draw3d/main.cpp:80-135,
+// :349-378 and :505-514 (-t trace, -w/-h size, -o output, -r reference with
+// tolerance-1 compare, "PASSED!"/"FAILED!"), plus -S (shadow rays),
+// -L x,y,w (light), -n N (repeat launches for timing), -k dir (kernel images).
+#include <getopt.h>
+
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "png.h"
+#include "vx_rt.h"
+
+namespace {
+
+const char* trace_file = "triangle.cgltrace";
+const char* output_file = "output.png";
+const char* reference_file = nullptr;
+const char* kernel_dir = nullptr;
+uint32_t width = 128, height = 128, repeat = 1;
+bool shadows = false;
+float light[3] = {0.0f, 60.0f, 80.0f};
+
+void usage() {
+  std::printf("Skybox MI355X ray-tracing test.\n"
+              "Usage: [-t trace] [-o output|null] [-r reference] [-w width] [-h height]"
+              " [-S shadows] [-L x,y,w] [-n repeat] [-k kernel_dir]\n");
+}
+
+#define RT_CHECK(_expr)                                                       \
+  do {                                                                        \
+    int _ret = (_expr);                                                       \
+    if (_ret == 0) break;                                                     \
+    std::printf("Error: '%s' returned %d! (%s)\n", #_expr, _ret, rt_last_error()); \
+    std::exit(-1);                                                            \
+  } while (false)
+
+}  // namespace
+
+int main(int argc, char** argv) {
+  int c;
+  while ((c = getopt(argc, argv, "t:o:r:w:h:n:k:L:S?")) != -1) {
+    switch (c) {
+    case 't': trace_file = optarg; break;
+    case 'o': output_file = optarg; break;
+    case 'r': reference_file = optarg; break;
+    case 'w': width = (uint32_t)std::atoi(optarg); break;
+    case 'h': height = (uint32_t)std::atoi(optarg); break;
+    case 'n': repeat = (uint32_t)std::atoi(optarg); break;
+    case 'k': kernel_dir = optarg; break;
+    case 'S': shadows = true; break;
+    case 'L': std::sscanf(optarg, "%f,%f,%f", &light[0], &light[1], &light[2]); break;
+    case '?': usage(); return 0;
+    default: usage(); return -1;
+    }
+  }
+  if (std::strcmp(output_file, "null") == 0 && reference_file) {
+    std::printf("Error: the output file is missing for reference validation!\n");
+    return 1;
+  }
+  rt_scene_h scene = nullptr;
+  RT_CHECK(rt_scene_load(trace_file, &scene));
+  rt_scene_info_t info;
+  RT_CHECK(rt_scene_info(scene, &info));
+  std::printf("CGL Trace: drawcalls=%u, primitives=%u, geometry=%u, layers=%u, textures=%u\n",
+              info.num_drawcalls, info.num_prims, info.num_geometry, info.num_layer,
+              info.num_textures);
+  std::printf("BVH: nodes=%u, leaves=%u, depth=%u, build=%.3f ms (parse %.3f ms)\n",
+              info.bvh_nodes, info.bvh_leaves, info.bvh_depth, info.bvh_ms, info.parse_ms);
+  rt_renderer_h r = nullptr;
+  RT_CHECK(rt_renderer_create(scene, kernel_dir, &r));
+  rt_render_params_t p;
+  std::memset(&p, 0, sizeof(p));
+  p.width = width;
+  p.height = height;
+  p.flags = shadows ? RT_RENDER_SHADOWS : 0;
+  std::memcpy(p.light, light, sizeof(light));
+  p.clear_color = 0xff000000u;
+  p.shard_count = 1;
+  RT_CHECK(rt_renderer_configure(r, &p));
+  double total = 0.0;
+  rt_stats_t st;
+  for (uint32_t i = 0; i < repeat; ++i) {
+    RT_CHECK(rt_render(r));
+    RT_CHECK(rt_render_stats(r, &st));
+    total += st.kernel_ms;
+  }
+  const double rays = (double)(st.primary_rays + st.shadow_rays);
+  std::printf("Elapsed time: %.4f ms/frame (grid %u x %u), rays=%.0f (primary %llu, shadow %llu, "
+              "occluded %llu), %.1f Mrays/s\n",
+              total / repeat, st.grid, st.block, rays, (unsigned long long)st.primary_rays,
+              (unsigned long long)st.shadow_rays, (unsigned long long)st.occluded,
+              rays / (total / repeat) * 1e-3);
+  int errors = 0;
+  if (std::strcmp(output_file, "null") != 0) {
+    std::vector<uint32_t> fb((size_t)width * height);
+    RT_CHECK(rt_read_framebuffer(r, fb.data(), fb.size()));
+    RT_CHECK(rt::SavePngARGB(output_file, fb.data(), width, height));
+    if (reference_file) {
+      std::vector<uint32_t> out, ref;
+      uint32_t ow, oh, rw, rh;
+      RT_CHECK(rt::LoadPngARGB(output_file, &out, &ow, &oh));
+      RT_CHECK(rt::LoadPngARGB(reference_file, &ref, &rw, &rh));
+      if (ow != rw || oh != rh) {
+        std::printf("FAILED! size mismatch\n");
+        errors = -1;
+      } else {
+        errors = (int)rt::CompareARGB(out.data(), ref.data(), out.size(), 1);
+        if (errors == 0) std::printf("PASSED!\n");
+        else std::printf("FAILED! %d errors.\n", errors);
+      }
+    }
+  }
+  rt_renderer_free(r);
+  rt_scene_free(scene);
+  return errors;
+}

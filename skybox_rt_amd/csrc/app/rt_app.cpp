@@ -1,0 +1,399 @@
+// rt_app.cpp -- librtapp.so: the RT host app behind include/vx_rt.h.
+//
+// Mirrors the host structure of tests/regression/draw3d/main.cpp:
+//   scene load (:428-455) -> kernel upload (:459) -> buffer allocation and
+//   clears (:461-490) -> per-frame state + kernel_arg upload (:179-347) ->
+//   vx_start / vx_ready_wait (:349-361) -> vx_mpm_query (:367-372) ->
+//   framebuffer read-back (:380-387).
+// The acceleration structure differs (BVH over clip space instead of
+// per-frame screen-tile binning, gfxutil.cpp:103-276): the BVH is built once
+// per scene at load time and is resolution independent.
+#include <dlfcn.h>
+
+#include <algorithm>
+#include <chrono>
+#include <map>
+#include <cstring>
+#include <memory>
+#include <string>
+#include <vector>
+
+#include "VX_types.h"
+#include "bvh.h"
+#include "cgltrace.h"
+#include "setup.h"
+#include "vortex.h"
+#include "vortex_hip.h"
+#include "vx_rt.h"
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(const std::string& m, int code = -1) {
+  g_err = m;
+  return code;
+}
+
+std::string lib_dir() {
+  Dl_info info;
+  if (dladdr((void*)&lib_dir, &info) && info.dli_fname) {
+    std::string p(info.dli_fname);
+    auto pos = p.rfind('/');
+    if (pos != std::string::npos) return p.substr(0, pos);
+  }
+  return ".";
+}
+
+double ms_since(std::chrono::steady_clock::time_point t0) {
+  return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+}
+
+}  // namespace
+
+struct rt_scene {
+  rt::Scene scene;
+  rt::Bvh bvh;
+  std::vector<int32_t> geometry;  // depth-tested prims (BVH input), ascending
+  std::vector<int32_t> layers;    // screen-layer prims, descending pid
+  std::string unsupported;        // non-empty: the RT path cannot render it
+  bool tie_high = false;
+  double parse_ms = 0, bvh_ms = 0;
+};
+
+struct rt_renderer {
+  rt_scene* sc = nullptr;
+  vx_device_h dev = nullptr;
+  vx_buffer_h krnl[2] = {nullptr, nullptr};
+  vx_buffer_h nodes = nullptr, tris = nullptr, layers = nullptr, dcs = nullptr, tex = nullptr;
+  vx_buffer_h prims = nullptr, cbuf = nullptr, args = nullptr;
+  uint64_t cbuf_bytes = 0;
+  rt_render_params_t params{};
+  rt_kernel_arg_t arg{};
+  bool configured = false;
+  uint32_t local_tiles = 0;
+  vx_hip_mem_ptr_t mem_ptr = nullptr;
+  vx_hip_stream_t stream = nullptr;
+  vx_hip_last_run_t last_run = nullptr;
+
+  ~rt_renderer() {
+    vx_buffer_h* bufs[] = {&krnl[0], &krnl[1], &nodes, &tris, &layers, &dcs, &tex, &prims, &cbuf, &args};
+    for (auto* b : bufs) {
+      if (*b) vx_mem_free(*b);
+      *b = nullptr;
+    }
+    if (dev) vx_dev_close(dev);
+  }
+};
+
+extern "C" {
+
+const char* rt_last_error(void) { return g_err.c_str(); }
+
+int rt_scene_load(const char* path, rt_scene_h* out) {
+  if (path == nullptr || out == nullptr) return fail("null argument");
+  auto sc = std::make_unique<rt_scene>();
+  auto t0 = std::chrono::steady_clock::now();
+  std::string err;
+  if (rt::LoadCGLTrace(path, &sc->scene, &err) != 0) return fail(err);
+  sc->parse_ms = ms_since(t0);
+  // classify drawcalls (DESIGN.md "Scope"): screen layers (depth test off)
+  // must precede geometry; geometry shares one LESS/LEQUAL depth function.
+  bool seen_geom = false;
+  int geom_func = -1;
+  std::vector<rt::BuildTri> build;
+  for (size_t d = 0; d < sc->scene.drawcalls.size(); ++d) {
+    const rt::DrawCall& dc = sc->scene.drawcalls[d];
+    const rt::States& st = dc.states;
+    if (st.blend_enabled || st.stencil_test || (st.color_writemask & 0xf) != 0xf)
+      sc->unsupported = "drawcall " + std::to_string(d) + " uses blending/stencil/partial writes";
+    if (st.depth_test) {
+      const int f = (int)rt::ToVXCompare(st.depth_func);
+      if (f != VX_OM_DEPTH_FUNC_LESS && f != VX_OM_DEPTH_FUNC_LEQUAL)
+        sc->unsupported = "depth function other than LESS/LEQUAL";
+      if (geom_func >= 0 && f != geom_func) sc->unsupported = "mixed depth functions";
+      geom_func = f;
+      seen_geom = true;
+    } else if (seen_geom) {
+      sc->unsupported = "screen layer drawn after depth-tested geometry";
+    }
+    for (uint32_t i = 0; i < dc.prim_count; ++i) {
+      const int32_t g = (int32_t)(dc.prim_offset + i);
+      if (st.depth_test) {
+        rt::BuildTri bt;
+        const auto& p = sc->scene.prims[g];
+        for (int c = 0; c < 3; ++c) {
+          bt.v[c][0] = p[c].pos[0];
+          bt.v[c][1] = p[c].pos[1];
+          bt.v[c][2] = p[c].pos[3];  // clip (x, y, w)
+        }
+        bt.pid = g;
+        build.push_back(bt);
+        sc->geometry.push_back(g);
+      } else {
+        sc->layers.push_back(g);
+      }
+    }
+  }
+  std::reverse(sc->layers.begin(), sc->layers.end());
+  sc->tie_high = geom_func == VX_OM_DEPTH_FUNC_LEQUAL;
+  t0 = std::chrono::steady_clock::now();
+  if (rt::BuildBvh(build, &sc->bvh, &err) != 0) return fail(err);
+  sc->bvh_ms = ms_since(t0);
+  *out = sc.release();
+  return 0;
+}
+
+int rt_scene_free(rt_scene_h s) {
+  delete s;
+  return 0;
+}
+
+int rt_scene_info(rt_scene_h s, rt_scene_info_t* info) {
+  if (!s || !info) return fail("null argument");
+  std::memset(info, 0, sizeof(*info));
+  info->num_drawcalls = (uint32_t)s->scene.drawcalls.size();
+  info->num_prims = (uint32_t)s->scene.prims.size();
+  info->num_geometry = (uint32_t)s->geometry.size();
+  info->num_layer = (uint32_t)s->layers.size();
+  info->num_textures = (uint32_t)s->scene.textures.size();
+  info->bvh_nodes = (uint32_t)s->bvh.nodes.size();
+  info->bvh_tris = (uint32_t)s->bvh.tris.size();
+  info->bvh_leaves = s->bvh.leaves;
+  info->bvh_depth = s->bvh.depth;
+  info->parse_ms = s->parse_ms;
+  info->bvh_ms = s->bvh_ms;
+  return 0;
+}
+
+int rt_scene_export_prims(rt_scene_h s, float* out, uint64_t count) {
+  if (!s || !out) return fail("null argument");
+  if (count < s->scene.prims.size()) return fail("buffer too small");
+  for (size_t i = 0; i < s->scene.prims.size(); ++i)
+    for (int c = 0; c < 3; ++c) {
+      const rt::Vertex& v = s->scene.prims[i][c];
+      float* o = out + (i * 3 + c) * 10;
+      std::memcpy(o, v.pos, 16);
+      std::memcpy(o + 4, v.color, 16);
+      std::memcpy(o + 8, v.uv, 8);
+    }
+  return 0;
+}
+
+int rt_scene_export_bvh(rt_scene_h s, float* nodes, float* tris) {
+  if (!s) return fail("null argument");
+  if (nodes) std::memcpy(nodes, s->bvh.nodes.data(), s->bvh.nodes.size() * sizeof(rt_node_t));
+  if (tris) std::memcpy(tris, s->bvh.tris.data(), s->bvh.tris.size() * sizeof(rt_tri_t));
+  return 0;
+}
+
+static int upload(vx_device_h dev, const void* data, uint64_t size, vx_buffer_h* buf, uint64_t* addr) {
+  const uint64_t sz = size ? size : 64;
+  if (*buf) vx_mem_free(*buf);
+  *buf = nullptr;
+  if (vx_mem_alloc(dev, sz, VX_MEM_READ, buf) != 0) return fail("vx_mem_alloc failed");
+  if (size && vx_copy_to_dev(*buf, data, 0, size) != 0) return fail("vx_copy_to_dev failed");
+  return vx_mem_address(*buf, addr) == 0 ? 0 : fail("vx_mem_address failed");
+}
+
+int rt_renderer_create(rt_scene_h s, const char* kernel_dir, rt_renderer_h* out) {
+  if (!s || !out) return fail("null argument");
+  if (!s->unsupported.empty()) return fail("scene not supported by the RT path: " + s->unsupported, -2);
+  auto r = std::make_unique<rt_renderer>();
+  r->sc = s;
+  if (vx_dev_open(&r->dev) != 0) {
+    r->dev = nullptr;
+    return fail("vx_dev_open failed (no GPU or driver missing)");
+  }
+  const std::string dir = kernel_dir ? kernel_dir : lib_dir();
+  const char* names[2] = {"rt_kernel.vxbin", "rt_kernel_stats.vxbin"};
+  for (int i = 0; i < 2; ++i)
+    if (vx_upload_kernel_file(r->dev, (dir + "/" + names[i]).c_str(), &r->krnl[i]) != 0)
+      return fail("cannot upload kernel " + dir + "/" + names[i]);
+  r->mem_ptr = (vx_hip_mem_ptr_t)vx_driver_symbol("vx_hip_mem_ptr");
+  r->stream = (vx_hip_stream_t)vx_driver_symbol("vx_hip_stream");
+  r->last_run = (vx_hip_last_run_t)vx_driver_symbol("vx_hip_last_run");
+  rt_kernel_arg_t& a = r->arg;
+  std::memset(&a, 0, sizeof(a));
+  const rt::Bvh& bvh = s->bvh;
+  if (upload(r->dev, bvh.nodes.data(), bvh.nodes.size() * sizeof(rt_node_t), &r->nodes, &a.nodes_addr) ||
+      upload(r->dev, bvh.tris.data(), bvh.tris.size() * sizeof(rt_tri_t), &r->tris, &a.tris_addr))
+    return -1;
+  a.num_nodes = (uint32_t)bvh.nodes.size();
+  // screen layers, highest pid first
+  std::vector<rt_tri_t> lt(s->layers.size());
+  for (size_t i = 0; i < s->layers.size(); ++i) {
+    const auto& p = s->scene.prims[s->layers[i]];
+    std::memset(&lt[i], 0, sizeof(rt_tri_t));
+    const float v0[3] = {p[0].pos[0], p[0].pos[1], p[0].pos[3]};
+    for (int k = 0; k < 3; ++k) {
+      const int src = k == 2 ? 3 : k;
+      lt[i].v[k] = v0[k];
+      lt[i].v[4 + k] = p[1].pos[src] - v0[k];
+      lt[i].v[8 + k] = p[2].pos[src] - v0[k];
+    }
+    std::memcpy(&lt[i].v[3], &s->layers[i], 4);
+  }
+  if (upload(r->dev, lt.data(), lt.size() * sizeof(rt_tri_t), &r->layers, &a.layers_addr)) return -1;
+  a.num_layer_tris = (uint32_t)lt.size();
+  // textures: one buffer, each texture 256-B aligned
+  std::vector<uint8_t> texels;
+  std::map<int32_t, uint64_t> tex_off;
+  for (auto& kv : s->scene.textures) {
+    tex_off[kv.first] = texels.size();
+    texels.insert(texels.end(), kv.second.pixels.begin(), kv.second.pixels.end());
+    texels.resize((texels.size() + 255) & ~size_t(255));
+  }
+  uint64_t tex_addr = 0;
+  if (upload(r->dev, texels.data(), texels.size(), &r->tex, &tex_addr)) return -1;
+  std::vector<rt_dcstate_t> dcs;
+  for (const rt::DrawCall& dc : s->scene.drawcalls) {
+    rt_dcstate_t st = rt::DrawcallState(dc, s->scene);
+    if (st.flags & RT_DC_TEX) st.tex_addr = tex_addr + tex_off[dc.texture_id];
+    dcs.push_back(st);
+  }
+  if (upload(r->dev, dcs.data(), dcs.size() * sizeof(rt_dcstate_t), &r->dcs, &a.dcs_addr)) return -1;
+  *out = r.release();
+  return 0;
+}
+
+int rt_renderer_free(rt_renderer_h r) {
+  delete r;
+  return 0;
+}
+
+int rt_scene_setup_prims(rt_scene_h s, uint32_t width, uint32_t height, int32_t* out,
+                         uint64_t count) {
+  if (!s || !out || width == 0 || height == 0) return fail("bad argument");
+  if (count < s->scene.prims.size()) return fail("buffer too small");
+  for (size_t d = 0; d < s->scene.drawcalls.size(); ++d) {
+    const rt::DrawCall& dc = s->scene.drawcalls[d];
+    for (uint32_t i = 0; i < dc.prim_count; ++i) {
+      rt_prim_t p;
+      rt::PrimSetup(s->scene.prims[dc.prim_offset + i], width, height, dc.viewport[4],
+                    dc.viewport[5], &p);
+      p.dc = (uint32_t)d;
+      std::memcpy(out + (size_t)(dc.prim_offset + i) * 32, &p, sizeof(p));
+    }
+  }
+  return 0;
+}
+
+int rt_renderer_configure(rt_renderer_h r, const rt_render_params_t* p) {
+  if (!r || !p) return fail("null argument");
+  if (p->width == 0 || p->height == 0 || p->width > 32768 || p->height > 32768)
+    return fail("bad resolution");
+  const uint32_t shards = p->shard_count ? p->shard_count : 1;
+  if (p->shard_index >= shards) return fail("shard_index >= shard_count");
+  const rt_scene* s = r->sc;
+  r->params = *p;
+  r->params.shard_count = shards;
+  rt_kernel_arg_t& a = r->arg;
+  // per-resolution shading records (rast_prim_t + drawcall id)
+  std::vector<rt_prim_t> prims(s->scene.prims.size());
+  for (size_t d = 0; d < s->scene.drawcalls.size(); ++d) {
+    const rt::DrawCall& dc = s->scene.drawcalls[d];
+    for (uint32_t i = 0; i < dc.prim_count; ++i) {
+      rt_prim_t& q = prims[dc.prim_offset + i];
+      rt::PrimSetup(s->scene.prims[dc.prim_offset + i], p->width, p->height, dc.viewport[4],
+                    dc.viewport[5], &q);
+      q.dc = (uint32_t)d;
+    }
+  }
+  if (upload(r->dev, prims.data(), prims.size() * sizeof(rt_prim_t), &r->prims, &a.prims_addr))
+    return -1;
+  a.width = p->width;
+  a.height = p->height;
+  a.tiles_y = (p->height + 31) >> RT_TILE_LOG;
+  a.tiles_x = (p->width + 31) >> RT_TILE_LOG;
+  const uint32_t tiles = a.tiles_x * a.tiles_y;
+  r->local_tiles = (tiles > p->shard_index) ? (tiles - p->shard_index + shards - 1) / shards : 0;
+  a.num_tasks = r->local_tiles * RT_TILE_PIXELS;
+  a.shard_index = p->shard_index;
+  a.shard_count = shards;
+  a.flags = ((p->flags & RT_RENDER_SHADOWS) ? RT_FLAG_SHADOWS : 0u) |
+            (s->tie_high ? RT_FLAG_TIE_HIGH : 0u) | (shards > 1 ? RT_FLAG_COMPACT : 0u);
+  a.clear_color = p->clear_color;
+  a.sx = 2.0f / (float)p->width;
+  a.sy = 2.0f / (float)p->height;
+  a.light[0] = p->light[0];
+  a.light[1] = p->light[1];
+  a.light[2] = p->light[2];
+  // output buffer, pre-filled with the clear colour (draw3d/main.cpp:485-490)
+  const uint64_t npx = shards > 1 ? (uint64_t)a.num_tasks : (uint64_t)p->width * p->height;
+  std::vector<uint32_t> clear(npx ? npx : 1, p->clear_color);
+  if (upload(r->dev, clear.data(), npx * 4, &r->cbuf, &a.cbuf_addr)) return -1;
+  r->cbuf_bytes = npx * 4;
+  uint64_t args_addr = 0;
+  if (upload(r->dev, &a, sizeof(a), &r->args, &args_addr)) return -1;
+  r->configured = true;
+  return 0;
+}
+
+int rt_render_start(rt_renderer_h r) {
+  if (!r || !r->configured) return fail("renderer not configured");
+  const int k = (r->params.flags & RT_RENDER_INSTRUMENTED) ? 1 : 0;
+  return vx_start(r->dev, r->krnl[k], r->args) == 0 ? 0 : fail("vx_start failed");
+}
+
+int rt_render_wait(rt_renderer_h r) {
+  if (!r) return fail("null argument");
+  return vx_ready_wait(r->dev, VX_MAX_TIMEOUT) == 0 ? 0 : fail("vx_ready_wait failed");
+}
+
+int rt_render(rt_renderer_h r) {
+  int e = rt_render_start(r);
+  return e ? e : rt_render_wait(r);
+}
+
+int rt_render_stats(rt_renderer_h r, rt_stats_t* st) {
+  if (!r || !st) return fail("null argument");
+  std::memset(st, 0, sizeof(*st));
+  uint64_t v[RT_STAT_COUNT] = {};
+  for (int i = 0; i <= RT_STAT_TEXEL_BYTES; ++i)
+    if (vx_mpm_query(r->dev, VX_CSR_MPM_BASE + RT_MPM_USER + i, 0, &v[i]) != 0)
+      return fail("vx_mpm_query failed");
+  st->primary_rays = v[RT_STAT_PRIMARY];
+  st->shadow_rays = v[RT_STAT_SHADOW];
+  st->geometry_hits = v[RT_STAT_HITS];
+  st->occluded = v[RT_STAT_OCCLUDED];
+  st->node_visits = v[RT_STAT_NODE_VISITS];
+  st->tri_tests = v[RT_STAT_TRI_TESTS];
+  st->layer_tests = v[RT_STAT_LAYER_TESTS];
+  st->shaded = v[RT_STAT_SHADED];
+  st->texel_bytes = v[RT_STAT_TEXEL_BYTES];
+  vx_mpm_query(r->dev, VX_CSR_MINSTRET, 0, &st->tasks);
+  uint64_t ns = 0;
+  vx_mpm_query(r->dev, VX_CSR_MCYCLE, 0, &ns);
+  st->kernel_ms = (double)ns * 1e-6;
+  if (r->last_run) r->last_run(r->dev, &st->kernel_ms, &st->grid, &st->block);
+  st->num_tasks = r->arg.num_tasks;
+  st->local_tiles = r->local_tiles;
+  return 0;
+}
+
+int rt_read_framebuffer(rt_renderer_h r, uint32_t* out, uint64_t count) {
+  if (!r || !out || !r->configured) return fail("renderer not configured");
+  if (count * 4 < r->cbuf_bytes) return fail("buffer too small");
+  return vx_copy_from_dev(out, r->cbuf, 0, r->cbuf_bytes) == 0 ? 0 : fail("vx_copy_from_dev failed");
+}
+
+int rt_framebuffer_device(rt_renderer_h r, void** ptr, uint64_t* bytes) {
+  if (!r || !ptr || !r->configured || !r->mem_ptr) return fail("not available");
+  if (bytes) *bytes = r->cbuf_bytes;
+  return r->mem_ptr(r->cbuf, ptr) == 0 ? 0 : fail("vx_hip_mem_ptr failed");
+}
+
+int rt_device_stream(rt_renderer_h r, void** stream) {
+  if (!r || !stream || !r->stream) return fail("not available");
+  return r->stream(r->dev, stream) == 0 ? 0 : fail("vx_hip_stream failed");
+}
+
+int rt_device_caps(rt_renderer_h r, uint64_t caps[8]) {
+  if (!r || !caps) return fail("null argument");
+  for (uint32_t i = 0; i < 8; ++i)
+    if (vx_dev_caps(r->dev, i, &caps[i]) != 0) return fail("vx_dev_caps failed");
+  return 0;
+}
+
+}  // extern "C"

@@ -1,0 +1,73 @@
+// rt_common.h -- data layout shared by the RT host app and the HIP kernel.
+//
+// Everything the kernel reads lives in the driver's HBM arena and is addressed
+// by the device addresses the app got from vx_mem_alloc (see DESIGN.md
+// "Data layout in HBM"):
+//   nodes   [num_nodes]  rt_node_t   64 B  BVH2 node = both children's boxes
+//   tris    [num_tris]   rt_tri_t    48 B  clip-space v0,e1,e2 + pid (leaf order)
+//   layers  [num_layer]  rt_tri_t    48 B  screen layers, highest pid first
+//   prims   [num_prims]  rt_prim_t  128 B  fixed-point shading record
+//   dcs     [num_dc]     rt_dcstate_t 64 B per-drawcall shading state
+//   cbuf    W*H*4 (linear, row 0 = NDC y=-1) or tiles*1024*4 (compact shard)
+#pragma once
+
+#include <stdint.h>
+
+#define RT_BLOCK_THREADS 256
+#define RT_MAX_STACK 24          // BVH depth bound checked by the host builder
+#define RT_TILE_LOG 5            // RASTER_TILE_LOGSIZE (VX_config.vh:477-479)
+#define RT_TILE_PIXELS 1024
+
+#define RT_FLAG_SHADOWS  0x1u
+#define RT_FLAG_TIE_HIGH 0x2u    // LEQUAL geometry: equal t -> highest pid
+#define RT_FLAG_COMPACT  0x4u    // shard output: compact tile buffer
+
+#define RT_DC_DEPTH   0x1u
+#define RT_DC_COLOR   0x2u
+#define RT_DC_TEX     0x4u
+#define RT_DC_MODULATE 0x8u
+
+#define RT_LEAF_FLAG 0x80000000u
+#define RT_EMPTY_REF (-1)
+
+// statistics: user MPM counters, vx_mpm_query(VX_CSR_MPM_BASE + RT_MPM_USER + slot)
+#define RT_MPM_USER 3
+enum {
+  RT_STAT_PRIMARY = 0, RT_STAT_SHADOW, RT_STAT_HITS, RT_STAT_OCCLUDED,
+  RT_STAT_NODE_VISITS, RT_STAT_TRI_TESTS, RT_STAT_LAYER_TESTS, RT_STAT_SHADED,
+  RT_STAT_TEXEL_BYTES, RT_STAT_COUNT = 16
+};
+
+// rt_node_t: 4 x float4 =
+//   (b0lo.x, b0hi.x, b1lo.x, b1hi.x), (.. y ..), (.. z ..), (c0, c1, 0, 0)
+// child ref c: >= 0 internal node index; -1 empty; otherwise a leaf:
+//   (c & 0x7fffffff) >> 4 = first triangle, (c & 15) + 1 = triangle count.
+typedef struct { float v[16]; } rt_node_t;
+
+// rt_tri_t: (v0.x, v0.y, v0.w, pid), (e1.xyw, 0), (e2.xyw, 0) -- clip (x,y,w)
+typedef struct { float v[12]; } rt_tri_t;
+
+typedef struct {
+  int32_t edges[3][3];     // Q15.16 (graphics.h:61-64)
+  int32_t attribs[7][3];   // Q7.24  z,r,g,b,a,u,v x (a0-a2, a1-a2, a2)
+  uint32_t dc;             // drawcall index
+  uint32_t pad;
+} rt_prim_t;
+
+typedef struct {
+  uint32_t flags;          // RT_DC_*
+  uint32_t tex_logw, tex_logh, tex_format, tex_filter, tex_wrapu, tex_wrapv, tex_stride;
+  uint64_t tex_addr;
+  uint32_t pad[6];
+} rt_dcstate_t;
+
+typedef struct {
+  uint64_t cbuf_addr, nodes_addr, tris_addr, layers_addr, prims_addr, dcs_addr;
+  uint64_t pad0[2];
+  uint32_t width, height, tiles_x, tiles_y;
+  uint32_t num_tasks, num_nodes, num_layer_tris, flags;
+  uint32_t clear_color, shard_index, shard_count, pad1;
+  float sx, sy;            // 2/W, 2/H
+  float light[3];
+  uint32_t pad2[3];
+} rt_kernel_arg_t;

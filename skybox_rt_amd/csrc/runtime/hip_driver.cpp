@@ -1,0 +1,452 @@
+// hip_driver.cpp -- libvortex-hip.so: the MI355X driver plugin.
+//
+// Implements the 16-entry callbacks_t ABI (callbacks.h; reference
+// runtime/common/callbacks.h:23-75 and callbacks.inc:20-225) on HIP.  It takes
+// the place of the simx driver (runtime/simx/vortex.cpp:32-246):
+//   * device memory   = one hipMalloc'd HBM arena + ArenaAllocator; device
+//                       addresses are arena offsets >= USER_BASE_ADDR;
+//   * kernel image    = vxbin header + gfx950 code object; start() loads it
+//                       once (hipModuleLoadData, cached) and launches
+//                       `vx_main` over the resident grid;
+//   * DCRs            = host store, mirrored into the module's __vx_dcrs
+//                       constant block at every start();
+//   * start/ready_wait = asynchronous launch on the driver's stream, bracketed
+//                       by HIP events; ready_wait polls the stop event with a
+//                       timeout (the simx driver polls a std::future at 1 s);
+//   * mpm_query       = event-timed device ns (MCYCLE) and task count
+//                       (MINSTRET) of the last run.
+// Error behaviour mirrors callbacks.inc: null handles / zero sizes / ranges
+// past the buffer -> -1; unknown caps id -> -1 (simx aborts).
+#include <hip/hip_runtime.h>
+
+#include <chrono>
+#include <cstdlib>
+#include <cstring>
+#include <map>
+#include <thread>
+#include <vector>
+
+#include "VX_types.h"
+#include "arena.h"
+#include "callbacks.h"
+#include "common.h"
+#include "vortex_hip.h"
+
+#define HIP_CHECK(_expr)                                                              \
+  do {                                                                                \
+    hipError_t _e = (_expr);                                                          \
+    if (_e != hipSuccess) {                                                           \
+      std::printf("[VXDRV] HIP error: '%s' -> %s\n", #_expr, hipGetErrorString(_e));  \
+      return -1;                                                                      \
+    }                                                                                 \
+  } while (false)
+
+namespace {
+
+constexpr uint64_t kBlockSize = 256;      // allocation granule (>= 64 B DCR blocks)
+constexpr uint64_t kDefaultArenaMB = 4096;
+
+uint64_t env_u64(const char* name, uint64_t dflt) {
+  const char* s = std::getenv(name);
+  return (s && *s) ? std::strtoull(s, nullptr, 0) : dflt;
+}
+
+uint64_t fnv1a(const uint8_t* p, size_t n) {
+  uint64_t h = 1469598103934665603ull;
+  for (size_t i = 0; i < n; ++i) h = (h ^ p[i]) * 1099511628211ull;
+  return h;
+}
+
+struct Module {
+  hipModule_t module = nullptr;
+  hipFunction_t entry = nullptr;
+  hipDeviceptr_t dcrs = nullptr, mem_base = nullptr, mpm = nullptr;
+  size_t dcrs_size = 0, mpm_size = 0;
+  uint32_t block = 0, grid = 0;
+};
+
+}  // namespace
+
+class vx_device {
+ public:
+  vx_device() : alloc_(0, 0, kBlockSize) {}
+
+  ~vx_device() {
+    if (running_) (void)hipEventSynchronize(ev_stop_);
+    for (auto& kv : modules_) (void)hipModuleUnload(kv.second.module);
+    if (ev_start_) (void)hipEventDestroy(ev_start_);
+    if (ev_stop_) (void)hipEventDestroy(ev_stop_);
+    if (stream_) (void)hipStreamDestroy(stream_);
+    if (arena_) (void)hipFree(arena_);
+  }
+
+  int init() {
+    int ndev = 0;
+    HIP_CHECK(hipGetDeviceCount(&ndev));
+    if (ndev <= 0) {
+      std::printf("[VXDRV] no HIP device visible\n");
+      return -1;
+    }
+    int dev = -1;
+    if (const char* s = std::getenv("VX_HIP_DEVICE")) dev = std::atoi(s);
+    else if (const char* s = std::getenv("LOCAL_RANK")) dev = std::atoi(s) % ndev;
+    if (dev < 0) HIP_CHECK(hipGetDevice(&dev));
+    device_id_ = dev;
+    HIP_CHECK(hipSetDevice(dev));
+    HIP_CHECK(hipGetDeviceProperties(&props_, dev));
+    const uint64_t arena_bytes = env_u64("VX_HIP_ARENA_MB", kDefaultArenaMB) << 20;
+    HIP_CHECK(hipMalloc(&arena_, arena_bytes));
+    arena_size_ = arena_bytes;
+    alloc_ = ArenaAllocator(USER_BASE_ADDR, arena_bytes - USER_BASE_ADDR, kBlockSize);
+    HIP_CHECK(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking));
+    HIP_CHECK(hipEventCreate(&ev_start_));
+    HIP_CHECK(hipEventCreate(&ev_stop_));
+    return 0;
+  }
+
+  int get_caps(uint32_t id, uint64_t* v) {
+    switch (id) {
+    case VX_CAPS_VERSION: *v = 1; break;
+    case VX_CAPS_NUM_THREADS: *v = 64; break;  // wave64
+    case VX_CAPS_NUM_WARPS:
+      *v = (uint64_t)props_.maxThreadsPerMultiProcessor / 64;  // 32 waves per CU
+      break;
+    case VX_CAPS_NUM_CORES: *v = (uint64_t)props_.multiProcessorCount; break;  // 256 CUs
+    case VX_CAPS_CACHE_LINE_SIZE: *v = 128; break;
+    case VX_CAPS_GLOBAL_MEM_SIZE: *v = arena_size_; break;
+    case VX_CAPS_LOCAL_MEM_SIZE: *v = (uint64_t)props_.maxSharedMemoryPerMultiProcessor; break;
+    case VX_CAPS_ISA_FLAGS:
+      // XLEN 64 (log2(64)-4 = 2 at bit 30); caches, local memory and the
+      // graphics extensions (provided by the device library of vx_gfx.h)
+      *v = (2ull << 30) | VX_ISA_EXT_ICACHE | VX_ISA_EXT_DCACHE | VX_ISA_EXT_L2CACHE |
+           VX_ISA_EXT_L3CACHE | VX_ISA_EXT_LMEM | VX_ISA_EXT_TEX | VX_ISA_EXT_RASTER |
+           VX_ISA_EXT_OM;
+      break;
+    default:
+      std::printf("[VXDRV] invalid caps id: %u\n", id);
+      return -1;
+    }
+    return 0;
+  }
+
+  int mem_alloc(uint64_t size, int flags, uint64_t* addr) {
+    if (alloc_.allocate(size, addr) != 0) return -1;
+    acl_[*addr] = flags;
+    return 0;
+  }
+  int mem_reserve(uint64_t addr, uint64_t size, int flags) {
+    if (addr + size > arena_size_) return -1;
+    if (alloc_.reserve(addr, size) != 0) return -1;
+    acl_[addr] = flags;
+    shadow_[addr].assign(size, 0);  // kernel images: keep a host copy to load
+    return 0;
+  }
+  int mem_free(uint64_t addr) {
+    acl_.erase(addr);
+    shadow_.erase(addr);
+    return alloc_.release(addr);
+  }
+  int mem_access(uint64_t addr, uint64_t size, int flags) {
+    uint64_t start = 0;
+    const uint64_t asz = alloc_.find(addr, &start);
+    if (asz == 0 || addr + size > start + asz) return -1;
+    acl_[addr] = flags;  // bookkeeping only: gfx950 has no per-range ACL
+    return 0;
+  }
+  int mem_info(uint64_t* fr, uint64_t* used) const {
+    if (fr) *fr = alloc_.free_bytes();
+    if (used) *used = alloc_.used_bytes();
+    return 0;
+  }
+
+  int upload(uint64_t addr, const void* src, uint64_t size) {
+    if (addr + size > arena_size_) return -1;
+    if (size == 0) return 0;
+    wait_idle();
+    HIP_CHECK(hipMemcpyAsync(arena_ + addr, src, size, hipMemcpyHostToDevice, stream_));
+    HIP_CHECK(hipStreamSynchronize(stream_));
+    for (auto& kv : shadow_) {  // keep kernel-image shadows coherent
+      const uint64_t a = kv.first, e = a + kv.second.size();
+      if (addr >= a && addr + size <= e)
+        std::memcpy(kv.second.data() + (addr - a), src, size);
+    }
+    return 0;
+  }
+  int download(void* dst, uint64_t addr, uint64_t size) {
+    if (addr + size > arena_size_) return -1;
+    if (size == 0) return 0;
+    wait_idle();
+    HIP_CHECK(hipMemcpyAsync(dst, arena_ + addr, size, hipMemcpyDeviceToHost, stream_));
+    HIP_CHECK(hipStreamSynchronize(stream_));
+    return 0;
+  }
+
+  int start(uint64_t krnl_addr, uint64_t args_addr) {
+    wait_idle();
+    dcr_set(VX_DCR_BASE_STARTUP_ADDR0, (uint32_t)(krnl_addr & 0xffffffffu));
+    dcr_set(VX_DCR_BASE_STARTUP_ADDR1, (uint32_t)(krnl_addr >> 32));
+    dcr_set(VX_DCR_BASE_STARTUP_ARG0, (uint32_t)(args_addr & 0xffffffffu));
+    dcr_set(VX_DCR_BASE_STARTUP_ARG1, (uint32_t)(args_addr >> 32));
+    Module* m = nullptr;
+    if (load_module(krnl_addr, &m) != 0) return -1;
+    const uint64_t base = (uint64_t)(uintptr_t)arena_;
+    HIP_CHECK(hipMemcpyHtoDAsync(m->dcrs, dcrs_, sizeof(dcrs_), stream_));
+    HIP_CHECK(hipMemcpyHtoDAsync(m->mem_base, (void*)&base, sizeof(base), stream_));
+    HIP_CHECK(hipMemsetAsync(m->mpm, 0, m->mpm_size, stream_));
+    HIP_CHECK(hipEventRecord(ev_start_, stream_));
+    HIP_CHECK(hipModuleLaunchKernel(m->entry, m->grid, 1, 1, m->block, 1, 1, 0, stream_,
+                                    nullptr, nullptr));
+    HIP_CHECK(hipEventRecord(ev_stop_, stream_));
+    running_ = true;
+    last_module_ = m;
+    last_grid_ = m->grid;
+    last_block_ = m->block;
+    return 0;
+  }
+
+  int ready_wait(uint64_t timeout_ms) {
+    if (!running_) return 0;
+    const auto t0 = std::chrono::steady_clock::now();
+    for (uint32_t spin = 0;; ++spin) {
+      hipError_t e = hipEventQuery(ev_stop_);
+      if (e == hipSuccess) break;
+      if (e != hipErrorNotReady) {
+        std::printf("[VXDRV] kernel failed: %s\n", hipGetErrorString(e));
+        running_ = false;
+        return -1;
+      }
+      const auto dt = std::chrono::steady_clock::now() - t0;
+      if ((uint64_t)std::chrono::duration_cast<std::chrono::milliseconds>(dt).count() > timeout_ms)
+        return -1;
+      if (spin > 1024) std::this_thread::sleep_for(std::chrono::microseconds(20));
+    }
+    running_ = false;
+    float ms = 0.0f;
+    HIP_CHECK(hipEventElapsedTime(&ms, ev_start_, ev_stop_));
+    last_ms_ = ms;
+    if (last_module_) {
+      HIP_CHECK(hipMemcpyAsync(mpm_, last_module_->mpm, sizeof(mpm_), hipMemcpyDeviceToHost,
+                               stream_));
+      HIP_CHECK(hipStreamSynchronize(stream_));
+    }
+    return 0;
+  }
+
+  int dcr_write(uint32_t addr, uint32_t value) {
+    if (addr >= VX_DCR_MIRROR_SIZE) return -1;
+    wait_idle();  // simx: ensure the prior run completed (vortex.cpp:211-214)
+    dcr_set(addr, value);
+    return 0;
+  }
+  int dcr_read(uint32_t addr, uint32_t* value) const {
+    if (addr >= VX_DCR_MIRROR_SIZE || !dcr_valid_[addr]) return -1;
+    *value = dcrs_[addr];
+    return 0;
+  }
+
+  int mpm_query(uint32_t addr, uint32_t core_id, uint64_t* value) {
+    const uint32_t off = addr - VX_CSR_MPM_BASE;
+    if (off >= VX_MPM_COUNT) return -1;
+    if (core_id != 0) { *value = 0; return 0; }  // device totals live on core 0
+    if (addr == VX_CSR_MCYCLE) *value = (uint64_t)(last_ms_ * 1.0e6 + 0.5);
+    else *value = mpm_[off];
+    return 0;
+  }
+
+  // ---- extensions (vortex_hip.h) ----
+  void* mem_ptr(uint64_t addr) { return arena_ + addr; }
+  hipStream_t stream() const { return stream_; }
+  int device_id() const { return device_id_; }
+  double last_ms() const { return last_ms_; }
+  uint32_t last_grid() const { return last_grid_; }
+  uint32_t last_block() const { return last_block_; }
+
+ private:
+  void dcr_set(uint32_t addr, uint32_t v) {
+    dcrs_[addr] = v;
+    dcr_valid_[addr] = true;
+  }
+  void wait_idle() {
+    if (running_) ready_wait(VX_MAX_TIMEOUT);
+  }
+
+  int load_module(uint64_t krnl_addr, Module** out) {
+    auto it = shadow_.find(krnl_addr);
+    if (it == shadow_.end()) {
+      std::printf("[VXDRV] no kernel image at 0x%llx (use vx_upload_kernel_*)\n",
+                  (unsigned long long)krnl_addr);
+      return -1;
+    }
+    const std::vector<uint8_t>& img = it->second;
+    const uint64_t key = fnv1a(img.data(), img.size()) ^ krnl_addr;
+    auto mit = modules_.find(key);
+    if (mit != modules_.end()) {
+      *out = &mit->second;
+      return 0;
+    }
+    Module m;
+    HIP_CHECK(hipModuleLoadData(&m.module, img.data()));
+    HIP_CHECK(hipModuleGetFunction(&m.entry, m.module, "vx_main"));
+    HIP_CHECK(hipModuleGetGlobal(&m.dcrs, &m.dcrs_size, m.module, "__vx_dcrs"));
+    size_t sz = 0;
+    HIP_CHECK(hipModuleGetGlobal(&m.mem_base, &sz, m.module, "__vx_mem_base"));
+    HIP_CHECK(hipModuleGetGlobal(&m.mpm, &m.mpm_size, m.module, "__vx_mpm"));
+    int max_threads = 0;
+    HIP_CHECK(hipFuncGetAttribute(&max_threads, HIP_FUNC_ATTRIBUTE_MAX_THREADS_PER_BLOCK, m.entry));
+    m.block = (uint32_t)(max_threads > 0 ? max_threads : 256);
+    int per_cu = 0;
+    HIP_CHECK(hipModuleOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, m.entry, (int)m.block, 0));
+    if (const char* s = std::getenv("VX_HIP_BLOCKS_PER_CU")) per_cu = std::atoi(s);
+    if (per_cu < 1) per_cu = 1;
+    m.grid = (uint32_t)(props_.multiProcessorCount * per_cu);
+    auto ins = modules_.emplace(key, m);
+    *out = &ins.first->second;
+    return 0;
+  }
+
+  hipDeviceProp_t props_{};
+  int device_id_ = 0;
+  uint8_t* arena_ = nullptr;
+  uint64_t arena_size_ = 0;
+  ArenaAllocator alloc_;
+  std::map<uint64_t, int> acl_;
+  std::map<uint64_t, std::vector<uint8_t>> shadow_;
+  std::map<uint64_t, Module> modules_;
+  hipStream_t stream_ = nullptr;
+  hipEvent_t ev_start_ = nullptr, ev_stop_ = nullptr;
+  bool running_ = false;
+  Module* last_module_ = nullptr;
+  double last_ms_ = 0.0;
+  uint32_t last_grid_ = 0, last_block_ = 0;
+  uint32_t dcrs_[VX_DCR_MIRROR_SIZE] = {};
+  bool dcr_valid_[VX_DCR_MIRROR_SIZE] = {};
+  unsigned long long mpm_[VX_MPM_COUNT] = {};
+};
+
+struct vx_buffer {
+  vx_device* device;
+  uint64_t addr;
+  uint64_t size;
+};
+
+extern "C" {
+
+__attribute__((visibility("default"))) int vx_dev_init(callbacks_t* cb) {
+  if (cb == nullptr) return -1;
+  cb->dev_open = [](vx_device_h* hdevice) -> int {
+    if (hdevice == nullptr) return -1;
+    auto* d = new vx_device();
+    VX_CHECK_ERR(d->init(), { delete d; return err; });
+    *hdevice = d;
+    return 0;
+  };
+  cb->dev_close = [](vx_device_h hdevice) -> int {
+    if (hdevice == nullptr) return -1;
+    delete (vx_device*)hdevice;
+    return 0;
+  };
+  cb->dev_caps = [](vx_device_h hdevice, uint32_t id, uint64_t* value) -> int {
+    if (hdevice == nullptr || value == nullptr) return -1;
+    return ((vx_device*)hdevice)->get_caps(id, value);
+  };
+  cb->mem_alloc = [](vx_device_h hdevice, uint64_t size, int flags, vx_buffer_h* hbuf) -> int {
+    if (hdevice == nullptr || hbuf == nullptr || size == 0) return -1;
+    auto* d = (vx_device*)hdevice;
+    uint64_t addr = 0;
+    VX_CHECK_ERR(d->mem_alloc(size, flags, &addr), { return err; });
+    *hbuf = new vx_buffer{d, addr, size};
+    return 0;
+  };
+  cb->mem_reserve = [](vx_device_h hdevice, uint64_t address, uint64_t size, int flags,
+                       vx_buffer_h* hbuf) -> int {
+    if (hdevice == nullptr || hbuf == nullptr || size == 0) return -1;
+    auto* d = (vx_device*)hdevice;
+    VX_CHECK_ERR(d->mem_reserve(address, size, flags), { return err; });
+    *hbuf = new vx_buffer{d, address, size};
+    return 0;
+  };
+  cb->mem_free = [](vx_buffer_h hbuf) -> int {
+    if (hbuf == nullptr) return 0;
+    auto* b = (vx_buffer*)hbuf;
+    const int err = b->device->mem_free(b->addr);
+    delete b;
+    return err;
+  };
+  cb->mem_access = [](vx_buffer_h hbuf, uint64_t off, uint64_t size, int flags) -> int {
+    if (hbuf == nullptr) return -1;
+    auto* b = (vx_buffer*)hbuf;
+    if (off + size > b->size) return -1;
+    return b->device->mem_access(b->addr + off, size, flags);
+  };
+  cb->mem_address = [](vx_buffer_h hbuf, uint64_t* address) -> int {
+    if (hbuf == nullptr || address == nullptr) return -1;
+    *address = ((vx_buffer*)hbuf)->addr;
+    return 0;
+  };
+  cb->mem_info = [](vx_device_h hdevice, uint64_t* fr, uint64_t* used) -> int {
+    if (hdevice == nullptr) return -1;
+    return ((vx_device*)hdevice)->mem_info(fr, used);
+  };
+  cb->copy_to_dev = [](vx_buffer_h hbuf, const void* src, uint64_t off, uint64_t size) -> int {
+    if (hbuf == nullptr || src == nullptr) return -1;
+    auto* b = (vx_buffer*)hbuf;
+    if (off + size > b->size) return -1;
+    return b->device->upload(b->addr + off, src, size);
+  };
+  cb->copy_from_dev = [](void* dst, vx_buffer_h hbuf, uint64_t off, uint64_t size) -> int {
+    if (hbuf == nullptr || dst == nullptr) return -1;
+    auto* b = (vx_buffer*)hbuf;
+    if (off + size > b->size) return -1;
+    return b->device->download(dst, b->addr + off, size);
+  };
+  cb->start = [](vx_device_h hdevice, vx_buffer_h hkernel, vx_buffer_h hargs) -> int {
+    if (hdevice == nullptr || hkernel == nullptr || hargs == nullptr) return -1;
+    return ((vx_device*)hdevice)->start(((vx_buffer*)hkernel)->addr, ((vx_buffer*)hargs)->addr);
+  };
+  cb->ready_wait = [](vx_device_h hdevice, uint64_t timeout) -> int {
+    if (hdevice == nullptr) return -1;
+    return ((vx_device*)hdevice)->ready_wait(timeout);
+  };
+  cb->dcr_read = [](vx_device_h hdevice, uint32_t addr, uint32_t* value) -> int {
+    if (hdevice == nullptr || value == nullptr) return -1;
+    return ((vx_device*)hdevice)->dcr_read(addr, value);
+  };
+  cb->dcr_write = [](vx_device_h hdevice, uint32_t addr, uint32_t value) -> int {
+    if (hdevice == nullptr) return -1;
+    return ((vx_device*)hdevice)->dcr_write(addr, value);
+  };
+  cb->mpm_query = [](vx_device_h hdevice, uint32_t addr, uint32_t core, uint64_t* value) -> int {
+    if (hdevice == nullptr || value == nullptr) return -1;
+    return ((vx_device*)hdevice)->mpm_query(addr, core, value);
+  };
+  return 0;
+}
+
+// ---- extensions (vortex_hip.h) ----
+__attribute__((visibility("default"))) int vx_hip_mem_ptr(vx_buffer_h hbuf, void** ptr) {
+  if (hbuf == nullptr || ptr == nullptr) return -1;
+  auto* b = (vx_buffer*)hbuf;
+  *ptr = b->device->mem_ptr(b->addr);
+  return 0;
+}
+__attribute__((visibility("default"))) int vx_hip_stream(vx_device_h hdevice, void** stream) {
+  if (hdevice == nullptr || stream == nullptr) return -1;
+  *stream = (void*)((vx_device*)hdevice)->stream();
+  return 0;
+}
+__attribute__((visibility("default"))) int vx_hip_last_run(vx_device_h hdevice, double* ms,
+                                                           uint32_t* grid, uint32_t* block) {
+  if (hdevice == nullptr) return -1;
+  auto* d = (vx_device*)hdevice;
+  if (ms) *ms = d->last_ms();
+  if (grid) *grid = d->last_grid();
+  if (block) *block = d->last_block();
+  return 0;
+}
+__attribute__((visibility("default"))) int vx_hip_device_id(vx_device_h hdevice, int* id) {
+  if (hdevice == nullptr || id == nullptr) return -1;
+  *id = ((vx_device*)hdevice)->device_id();
+  return 0;
+}
+
+}  // extern "C"

@@ -1,0 +1,258 @@
+// stub.cpp -- libvortex.so: the public vortex.h API.
+//
+// Same role as the reference's runtime/stub/vortex.cpp:25-183 (driver loader,
+// DCR initialisation, call forwarding, multi-core mpm summation) and
+// runtime/stub/utils.cpp:25-155,807-836 (VORTEX_PROFILING, kernel/arg upload
+// helpers, occupancy).  The driver is libvortex-${VORTEX_DRIVER}.so; the
+// default here is "hip".  Besides the normal dlopen search path, the stub also
+// looks next to itself so an in-tree build works without LD_LIBRARY_PATH.
+#include <dlfcn.h>
+
+#include <cstdlib>
+#include <cstring>
+#include <fstream>
+#include <iostream>
+#include <string>
+#include <vector>
+
+#include "VX_types.h"
+#include "callbacks.h"
+#include "common.h"
+#include "vortex_hip.h"
+
+namespace {
+
+callbacks_t g_callbacks;
+void* g_drv_handle = nullptr;
+int g_open_devices = 0;
+
+int get_profiling_mode() {  // utils.cpp:25-47
+  const char* s = std::getenv("VORTEX_PROFILING");
+  return s ? std::atoi(s) : 0;
+}
+
+std::string self_dir() {
+  Dl_info info;
+  if (dladdr((void*)&get_profiling_mode, &info) && info.dli_fname) {
+    std::string p(info.dli_fname);
+    auto pos = p.rfind('/');
+    if (pos != std::string::npos) return p.substr(0, pos + 1);
+  }
+  return "";
+}
+
+int load_driver() {
+  if (g_drv_handle) return 0;
+  const char* name = std::getenv("VORTEX_DRIVER");
+  std::string lib = std::string("libvortex-") + (name ? name : "hip") + ".so";
+  void* h = dlopen((self_dir() + lib).c_str(), RTLD_LAZY | RTLD_LOCAL);
+  if (h == nullptr) h = dlopen(lib.c_str(), RTLD_LAZY | RTLD_LOCAL);
+  if (h == nullptr) {
+    std::cerr << "Cannot open library: " << dlerror() << std::endl;
+    return 1;
+  }
+  auto init = (int (*)(callbacks_t*))dlsym(h, "vx_dev_init");
+  if (init == nullptr) {
+    std::cerr << "Cannot load symbol 'vx_dev_init': " << dlerror() << std::endl;
+    dlclose(h);
+    return 1;
+  }
+  if (init(&g_callbacks) != 0) {
+    dlclose(h);
+    return 1;
+  }
+  g_drv_handle = h;
+  return 0;
+}
+
+int dcr_initialize(vx_device_h hdevice) {  // vortex.cpp:25-49
+  const uint64_t startup = STARTUP_ADDR;
+  VX_CHECK_ERR(vx_dcr_write(hdevice, VX_DCR_BASE_STARTUP_ADDR0, (uint32_t)(startup & 0xffffffffu)),
+               { return err; });
+  VX_CHECK_ERR(vx_dcr_write(hdevice, VX_DCR_BASE_STARTUP_ADDR1, (uint32_t)(startup >> 32)),
+               { return err; });
+  VX_CHECK_ERR(vx_dcr_write(hdevice, VX_DCR_BASE_STARTUP_ARG0, 0), { return err; });
+  VX_CHECK_ERR(vx_dcr_write(hdevice, VX_DCR_BASE_STARTUP_ARG1, 0), { return err; });
+  VX_CHECK_ERR(vx_dcr_write(hdevice, VX_DCR_BASE_MPM_CLASS, 0), { return err; });
+  return 0;
+}
+
+bool read_file(const char* filename, std::vector<char>* out) {
+  std::ifstream ifs(filename, std::ios::binary);
+  if (!ifs) {
+    std::cout << "error: " << filename << " not found" << std::endl;
+    return false;
+  }
+  ifs.seekg(0, ifs.end);
+  auto size = ifs.tellg();
+  ifs.seekg(0, ifs.beg);
+  out->resize((size_t)size);
+  ifs.read(out->data(), size);
+  return true;
+}
+
+}  // namespace
+
+#define VX_API extern "C" __attribute__((visibility("default")))
+
+VX_API int vx_dev_open(vx_device_h* hdevice) {
+  if (hdevice == nullptr) return -1;
+  if (load_driver() != 0) return 1;
+  vx_device_h h = nullptr;
+  VX_CHECK_ERR(g_callbacks.dev_open(&h), { return err; });
+  VX_CHECK_ERR(dcr_initialize(h), { g_callbacks.dev_close(h); return err; });
+  ++g_open_devices;
+  *hdevice = h;
+  return 0;
+}
+
+VX_API int vx_dev_close(vx_device_h hdevice) {
+  if (hdevice == nullptr || g_drv_handle == nullptr) return -1;
+  if (std::getenv("VX_DUMP_PERF")) vx_dump_perf(hdevice, stdout);
+  const int ret = g_callbacks.dev_close(hdevice);
+  // the driver stays loaded: closing a HIP runtime user mid-process is unsafe
+  --g_open_devices;
+  return ret;
+}
+
+VX_API int vx_dev_caps(vx_device_h h, uint32_t id, uint64_t* v) {
+  return g_drv_handle ? g_callbacks.dev_caps(h, id, v) : -1;
+}
+VX_API int vx_mem_alloc(vx_device_h h, uint64_t size, int flags, vx_buffer_h* b) {
+  return g_drv_handle ? g_callbacks.mem_alloc(h, size, flags, b) : -1;
+}
+VX_API int vx_mem_reserve(vx_device_h h, uint64_t addr, uint64_t size, int flags, vx_buffer_h* b) {
+  return g_drv_handle ? g_callbacks.mem_reserve(h, addr, size, flags, b) : -1;
+}
+VX_API int vx_mem_free(vx_buffer_h b) {
+  if (b == nullptr) return 0;
+  return g_drv_handle ? g_callbacks.mem_free(b) : -1;
+}
+VX_API int vx_mem_access(vx_buffer_h b, uint64_t off, uint64_t size, int flags) {
+  return g_drv_handle ? g_callbacks.mem_access(b, off, size, flags) : -1;
+}
+VX_API int vx_mem_address(vx_buffer_h b, uint64_t* addr) {
+  return g_drv_handle ? g_callbacks.mem_address(b, addr) : -1;
+}
+VX_API int vx_mem_info(vx_device_h h, uint64_t* fr, uint64_t* used) {
+  return g_drv_handle ? g_callbacks.mem_info(h, fr, used) : -1;
+}
+VX_API int vx_copy_to_dev(vx_buffer_h b, const void* src, uint64_t off, uint64_t size) {
+  return g_drv_handle ? g_callbacks.copy_to_dev(b, src, off, size) : -1;
+}
+VX_API int vx_copy_from_dev(void* dst, vx_buffer_h b, uint64_t off, uint64_t size) {
+  return g_drv_handle ? g_callbacks.copy_from_dev(dst, b, off, size) : -1;
+}
+VX_API int vx_start(vx_device_h h, vx_buffer_h k, vx_buffer_h a) {
+  if (!g_drv_handle) return -1;
+  const int mode = get_profiling_mode();
+  if (mode != 0) {
+    VX_CHECK_ERR(vx_dcr_write(h, VX_DCR_BASE_MPM_CLASS, (uint32_t)mode), { return err; });
+  }
+  return g_callbacks.start(h, k, a);
+}
+VX_API int vx_ready_wait(vx_device_h h, uint64_t timeout) {
+  return g_drv_handle ? g_callbacks.ready_wait(h, timeout) : -1;
+}
+VX_API int vx_dcr_read(vx_device_h h, uint32_t addr, uint32_t* v) {
+  return g_drv_handle ? g_callbacks.dcr_read(h, addr, v) : -1;
+}
+VX_API int vx_dcr_write(vx_device_h h, uint32_t addr, uint32_t v) {
+  return g_drv_handle ? g_callbacks.dcr_write(h, addr, v) : -1;
+}
+VX_API int vx_mpm_query(vx_device_h h, uint32_t addr, uint32_t core_id, uint64_t* value) {
+  if (!g_drv_handle || value == nullptr) return -1;
+  if (core_id == 0xffffffffu) {  // vortex.cpp:164-183: sum over all cores
+    uint64_t num_cores = 0, sum = 0, cur = 0;
+    VX_CHECK_ERR(g_callbacks.dev_caps(h, VX_CAPS_NUM_CORES, &num_cores), { return err; });
+    for (uint32_t i = 0; i < num_cores; ++i) {
+      VX_CHECK_ERR(g_callbacks.mpm_query(h, addr, i, &cur), { return err; });
+      sum += cur;
+    }
+    *value = sum;
+    return 0;
+  }
+  return g_callbacks.mpm_query(h, addr, core_id, value);
+}
+
+// ---- utilities (utils.cpp:49-155) ----
+VX_API int vx_upload_kernel_bytes(vx_device_h h, const void* content, uint64_t size,
+                                  vx_buffer_h* hbuffer) {
+  if (h == nullptr || content == nullptr || size <= 16 || hbuffer == nullptr) return -1;
+  uint64_t hdr[2];
+  std::memcpy(hdr, content, sizeof(hdr));
+  const uint64_t min_vma = hdr[0], max_vma = hdr[1];
+  const uint64_t bin_size = size - 16;
+  if (max_vma <= min_vma || max_vma - min_vma < bin_size) return -1;
+  const uint64_t runtime_size = max_vma - min_vma;
+  vx_buffer_h b = nullptr;
+  VX_CHECK_ERR(vx_mem_reserve(h, min_vma, runtime_size, 0, &b), { return err; });
+  VX_CHECK_ERR(vx_mem_access(b, 0, bin_size, VX_MEM_READ), { vx_mem_free(b); return err; });
+  if (runtime_size > bin_size) {
+    VX_CHECK_ERR(vx_mem_access(b, bin_size, runtime_size - bin_size, VX_MEM_READ_WRITE),
+                 { vx_mem_free(b); return err; });
+  }
+  VX_CHECK_ERR(vx_copy_to_dev(b, (const uint8_t*)content + 16, 0, bin_size),
+               { vx_mem_free(b); return err; });
+  *hbuffer = b;
+  return 0;
+}
+
+VX_API int vx_upload_kernel_file(vx_device_h h, const char* filename, vx_buffer_h* hbuffer) {
+  if (h == nullptr || filename == nullptr || hbuffer == nullptr) return -1;
+  std::vector<char> content;
+  if (!read_file(filename, &content)) return -1;
+  VX_CHECK_ERR(vx_upload_kernel_bytes(h, content.data(), content.size(), hbuffer), { return err; });
+  return 0;
+}
+
+VX_API int vx_upload_bytes(vx_device_h h, const void* content, uint64_t size, vx_buffer_h* hbuffer) {
+  if (h == nullptr || content == nullptr || size == 0 || hbuffer == nullptr) return -1;
+  vx_buffer_h b = nullptr;
+  VX_CHECK_ERR(vx_mem_alloc(h, size, VX_MEM_READ, &b), { return err; });
+  VX_CHECK_ERR(vx_copy_to_dev(b, content, 0, size), { vx_mem_free(b); return err; });
+  *hbuffer = b;
+  return 0;
+}
+
+VX_API int vx_upload_file(vx_device_h h, const char* filename, vx_buffer_h* hbuffer) {
+  if (h == nullptr || filename == nullptr || hbuffer == nullptr) return -1;
+  std::vector<char> content;
+  if (!read_file(filename, &content)) return -1;
+  VX_CHECK_ERR(vx_upload_bytes(h, content.data(), content.size(), hbuffer), { return err; });
+  return 0;
+}
+
+VX_API int vx_check_occupancy(vx_device_h h, uint32_t group_size, uint32_t* max_localmem) {
+  uint64_t warps = 0, threads = 0;  // utils.cpp:807-836
+  VX_CHECK_ERR(vx_dev_caps(h, VX_CAPS_NUM_WARPS, &warps), { return err; });
+  VX_CHECK_ERR(vx_dev_caps(h, VX_CAPS_NUM_THREADS, &threads), { return err; });
+  const uint64_t threads_per_core = warps * threads;
+  if (group_size == 0 || group_size > threads_per_core) {
+    std::printf("Error: cannot schedule kernel with group_size > threads_per_core (%u,%llu)\n",
+                group_size, (unsigned long long)threads_per_core);
+    return -1;
+  }
+  const uint64_t warps_per_group = (group_size + threads - 1) / threads;
+  const uint64_t groups_per_core = warps / warps_per_group;
+  if (max_localmem) {
+    uint64_t lmem = 0;
+    VX_CHECK_ERR(vx_dev_caps(h, VX_CAPS_LOCAL_MEM_SIZE, &lmem), { return err; });
+    *max_localmem = (uint32_t)(lmem / groups_per_core);
+  }
+  return 0;
+}
+
+VX_API int vx_dump_perf(vx_device_h h, FILE* stream) {
+  uint64_t ns = 0, tasks = 0;
+  VX_CHECK_ERR(vx_mpm_query(h, VX_CSR_MCYCLE, 0, &ns), { return err; });
+  VX_CHECK_ERR(vx_mpm_query(h, VX_CSR_MINSTRET, 0, &tasks), { return err; });
+  std::fprintf(stream, "PERF: device_ns=%llu, tasks=%llu\n", (unsigned long long)ns,
+               (unsigned long long)tasks);
+  return 0;
+}
+
+VX_API void* vx_driver_symbol(const char* name) {
+  if (g_drv_handle == nullptr || name == nullptr) return nullptr;
+  return dlsym(g_drv_handle, name);
+}

@@ -1,0 +1,238 @@
+"""ctypes binding of include/vx_rt.h (librtapp.so): the RT regression app.
+
+    scene = Scene.load("tekkaman.cgltrace")
+    r = Renderer(scene)
+    r.configure(1024, 1024, shadows=True)
+    r.render()
+    fb = r.framebuffer()          # uint32 ARGB8888 [H, W], row 0 = NDC y=-1
+    stats = r.stats()
+
+All work runs through the native library and the HIP driver; there is no
+fallback.  Errors raise RtError with the library's message.
+"""
+from __future__ import annotations
+
+import ctypes as C
+
+import numpy as np
+
+from . import _lib
+
+RT_RENDER_SHADOWS = 0x1
+RT_RENDER_INSTRUMENTED = 0x100
+CLEAR_COLOR = 0xFF000000               # draw3d/main.cpp:47
+DEFAULT_LIGHT = (0.0, 60.0, 80.0)      # clip (x, y, w), SURVEY.md 8(d) config 3
+TILE = 32                              # RASTER_TILE_LOGSIZE = 5
+
+
+class SceneInfo(C.Structure):
+    _fields_ = [(n, C.c_uint32) for n in (
+        "num_drawcalls", "num_prims", "num_geometry", "num_layer", "num_textures",
+        "bvh_nodes", "bvh_tris", "bvh_leaves", "bvh_depth", "pad")] + [
+        ("parse_ms", C.c_double), ("bvh_ms", C.c_double)]
+
+
+class RenderParams(C.Structure):
+    _fields_ = [("width", C.c_uint32), ("height", C.c_uint32), ("flags", C.c_uint32),
+                ("light", C.c_float * 3), ("clear_color", C.c_uint32),
+                ("shard_index", C.c_uint32), ("shard_count", C.c_uint32)]
+
+
+class Stats(C.Structure):
+    _fields_ = [(n, C.c_uint64) for n in (
+        "primary_rays", "shadow_rays", "geometry_hits", "occluded", "node_visits",
+        "tri_tests", "layer_tests", "shaded", "texel_bytes", "tasks")] + [
+        ("kernel_ms", C.c_double), ("grid", C.c_uint32), ("block", C.c_uint32),
+        ("num_tasks", C.c_uint32), ("local_tiles", C.c_uint32)]
+
+    def as_dict(self):
+        return {n: getattr(self, n) for n, _ in self._fields_}
+
+
+class RtError(RuntimeError):
+    pass
+
+
+_h = None
+
+
+def lib():
+    global _h
+    if _h is None:
+        h = _lib.load("librtapp.so")
+        vp, u32, u64 = C.c_void_p, C.c_uint32, C.c_uint64
+        sig = {
+            "rt_scene_load": [C.c_char_p, C.POINTER(vp)],
+            "rt_scene_free": [vp],
+            "rt_scene_info": [vp, C.POINTER(SceneInfo)],
+            "rt_scene_export_prims": [vp, vp, u64],
+            "rt_scene_export_bvh": [vp, vp, vp],
+            "rt_renderer_create": [vp, C.c_char_p, C.POINTER(vp)],
+            "rt_renderer_free": [vp],
+            "rt_renderer_configure": [vp, C.POINTER(RenderParams)],
+            "rt_render_start": [vp],
+            "rt_render_wait": [vp],
+            "rt_render": [vp],
+            "rt_render_stats": [vp, C.POINTER(Stats)],
+            "rt_read_framebuffer": [vp, vp, u64],
+            "rt_scene_setup_prims": [vp, u32, u32, vp, u64],
+            "rt_framebuffer_device": [vp, C.POINTER(vp), C.POINTER(u64)],
+            "rt_device_stream": [vp, C.POINTER(vp)],
+            "rt_device_caps": [vp, C.POINTER(u64)],
+        }
+        for name, argtypes in sig.items():
+            fn = getattr(h, name)
+            fn.argtypes = argtypes
+            fn.restype = C.c_int
+        h.rt_last_error.restype = C.c_char_p
+        h.rt_last_error.argtypes = []
+        _h = h
+    return _h
+
+
+def _check(rc: int, what: str) -> None:
+    if rc != 0:
+        raise RtError(f"{what} failed ({rc}): {lib().rt_last_error().decode(errors='replace')}")
+
+
+class Scene:
+    def __init__(self, handle):
+        self._h = handle
+
+    @classmethod
+    def load(cls, path: str) -> "Scene":
+        h = C.c_void_p()
+        _check(lib().rt_scene_load(str(path).encode(), C.byref(h)), f"rt_scene_load({path})")
+        return cls(h)
+
+    def info(self) -> dict:
+        i = SceneInfo()
+        _check(lib().rt_scene_info(self._h, C.byref(i)), "rt_scene_info")
+        return {n: getattr(i, n) for n, _ in i._fields_ if n != "pad"}
+
+    def prims(self) -> np.ndarray:
+        n = self.info()["num_prims"]
+        out = np.zeros((max(n, 1), 3, 10), np.float32)
+        _check(lib().rt_scene_export_prims(self._h, out.ctypes.data, n), "rt_scene_export_prims")
+        return out[:n]
+
+    def bvh(self):
+        info = self.info()
+        nodes = np.zeros((max(info["bvh_nodes"], 1), 16), np.float32)
+        tris = np.zeros((max(info["bvh_tris"], 1), 12), np.float32)
+        _check(lib().rt_scene_export_bvh(self._h, nodes.ctypes.data, tris.ctypes.data),
+               "rt_scene_export_bvh")
+        return nodes[:info["bvh_nodes"]], tris[:info["bvh_tris"]]
+
+    def setup_prims(self, width: int, height: int) -> np.ndarray:
+        """rt_prim_t shading records (int32[P, 32]) at width x height."""
+        n = self.info()["num_prims"]
+        out = np.zeros((max(n, 1), 32), np.int32)
+        _check(lib().rt_scene_setup_prims(self._h, width, height, out.ctypes.data, n),
+               "rt_scene_setup_prims")
+        return out[:n]
+
+    def close(self) -> None:
+        if self._h:
+            lib().rt_scene_free(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+class Renderer:
+    """One vortex device running the RT kernel for one scene."""
+
+    def __init__(self, scene: Scene, kernel_dir: str = None):
+        self.scene = scene
+        h = C.c_void_p()
+        _check(lib().rt_renderer_create(scene._h, kernel_dir.encode() if kernel_dir else None,
+                                        C.byref(h)), "rt_renderer_create")
+        self._h = h
+        self.params = None
+
+    def configure(self, width: int, height: int, shadows: bool = True, light=DEFAULT_LIGHT,
+                  clear_color: int = CLEAR_COLOR, shard_index: int = 0, shard_count: int = 1,
+                  instrumented: bool = False) -> None:
+        p = RenderParams()
+        p.width, p.height = width, height
+        p.flags = (RT_RENDER_SHADOWS if shadows else 0) | (RT_RENDER_INSTRUMENTED if instrumented else 0)
+        p.light[:] = [float(np.float32(x)) for x in light]
+        p.clear_color = clear_color
+        p.shard_index, p.shard_count = shard_index, shard_count
+        _check(lib().rt_renderer_configure(self._h, C.byref(p)), "rt_renderer_configure")
+        self.params = p
+
+    def render(self) -> None:
+        _check(lib().rt_render(self._h), "rt_render")
+
+    def start(self) -> None:
+        _check(lib().rt_render_start(self._h), "rt_render_start")
+
+    def wait(self) -> None:
+        _check(lib().rt_render_wait(self._h), "rt_render_wait")
+
+    def stats(self) -> dict:
+        s = Stats()
+        _check(lib().rt_render_stats(self._h, C.byref(s)), "rt_render_stats")
+        return s.as_dict()
+
+    def framebuffer(self) -> np.ndarray:
+        p = self.params
+        if p.shard_count > 1:
+            n = self.stats()["num_tasks"]
+            out = np.zeros(max(n, 1), np.uint32)
+            _check(lib().rt_read_framebuffer(self._h, out.ctypes.data, n), "rt_read_framebuffer")
+            return out[:n]
+        out = np.zeros((p.height, p.width), np.uint32)
+        _check(lib().rt_read_framebuffer(self._h, out.ctypes.data, out.size), "rt_read_framebuffer")
+        return out
+
+    def framebuffer_device(self):
+        ptr, nbytes = C.c_void_p(), C.c_uint64()
+        _check(lib().rt_framebuffer_device(self._h, C.byref(ptr), C.byref(nbytes)),
+               "rt_framebuffer_device")
+        return ptr.value, nbytes.value
+
+    def device_stream(self) -> int:
+        s = C.c_void_p()
+        _check(lib().rt_device_stream(self._h, C.byref(s)), "rt_device_stream")
+        return s.value
+
+    def caps(self):
+        c = (C.c_uint64 * 8)()
+        _check(lib().rt_device_caps(self._h, c), "rt_device_caps")
+        return list(c)
+
+    def close(self) -> None:
+        if self._h:
+            lib().rt_renderer_free(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def deinterleave_tiles(shards, width: int, height: int) -> np.ndarray:
+    """Assemble per-rank compact tile buffers (rank r holds tiles t with
+    t % G == r, each 32x32 in 8x8-block/lane task order) into a W x H image."""
+    G = len(shards)
+    tx, ty = (width + TILE - 1) // TILE, (height + TILE - 1) // TILE
+    img = np.zeros((ty * TILE, tx * TILE), np.uint32)
+    for r, buf in enumerate(shards):
+        tiles = np.asarray(buf, np.uint32).reshape(-1, 4, 4, 8, 8)  # [lt][by][bx][y][x]
+        tiles = tiles.transpose(0, 1, 3, 2, 4).reshape(-1, TILE, TILE)
+        for lt, tile in enumerate(tiles):
+            gt = r + lt * G
+            if gt >= tx * ty:
+                break
+            y0, x0 = (gt // tx) * TILE, (gt % tx) * TILE
+            img[y0:y0 + TILE, x0:x0 + TILE] = tile
+    return img[:height, :width]
