@@ -6,23 +6,25 @@
  * A kernel program is one HIP translation unit compiled for gfx950 into a
  * code object, wrapped in the reference's 16-byte vxbin header
  * (kernel/scripts/vxbin.py:54-78) and uploaded with vx_upload_kernel_file().
- * vx_start() launches its `vx_main` entry over the whole device.  Like the
- * reference's main(), VX_MAIN's body reads its argument pointer from the
- * STARTUP_ARG DCRs (the reference reads MSCRATCH, draw3d/kernel.cpp:287) and
- * calls vx_spawn_threads()/vx_spawn_tasks(), which call the per-task
+ * vx_start() launches its `vx_main` entry over a resident persistent grid.
+ * Like the reference's main(), VX_MAIN's body reads its argument pointer from
+ * the STARTUP_ARG DCRs (the reference reads MSCRATCH, draw3d/kernel.cpp:287)
+ * and calls vx_spawn_threads()/vx_spawn_tasks(), which call the per-task
  * callback `kernel_body` once per task.
  *
  * Differences forced by the hardware (documented in DESIGN.md):
  *  - A GPU has no thread-local storage and HIP reserves the name `blockIdx`,
  *    so the task coordinates (the reference's __thread blockIdx/threadIdx,
  *    vx_spawn.c:26-27,75-80) reach the callback as an explicit `vx_task_t`.
- *  - VX_MAIN's body runs SPMD on every hardware thread (64-lane wave
- *    granularity); the reference runs main() per core and wspawns warps.
- *  - Tasks are dealt to hardware threads round-robin (task = k*T + tid,
- *    T = resident hardware threads), so the 64 lanes of a wave always take 64
- *    consecutive task ids (coalesced, and an 8x8 pixel tile for the RT app);
- *    the reference deals contiguous per-core chunks.  Every task still runs
- *    exactly once with blockIdx = the vx_spawn.c:75-80 decomposition.
+ *  - VX_MAIN's body runs SPMD on every hardware thread (64-lane waves); the
+ *    reference runs main() per core and wspawns warps.
+ *  - Scheduling: tasks are handed out in chunks of 64 consecutive ids, one
+ *    chunk per wave (one task per lane: coalesced, and an 8x8 pixel block in
+ *    the RT app), dynamically: chunk c belongs to queue c % 8, a wave starts
+ *    on the queue of its XCD (HW_REG_XCC_ID) and moves on when it runs dry.
+ *    The reference deals static per-core ranges (vx_spawn.c:247-316).  Every
+ *    task still runs exactly once with blockIdx = the vx_spawn.c:75-80
+ *    decomposition; the queues are zeroed by the driver before each launch.
  *  - group_size > 1 (vx_spawn.c:187-246) is not supported yet: returns -1.
  */
 #ifndef VX_SPAWN_H
@@ -33,14 +35,24 @@
 
 #include "VX_types.h"
 
+#define VX_SCHED_QUEUES 8
+#define VX_SCHED_STRIDE 16   /* one 64-B line per queue counter */
+#define VX_CHUNK 64          /* tasks per wave-level dequeue */
+
+/* per-launch device state, zeroed by the driver before every launch */
+typedef struct {
+  unsigned long long mpm[VX_MPM_COUNT];                 /* perf counters (vx_mpm_query) */
+  uint32_t sched[VX_SCHED_QUEUES * VX_SCHED_STRIDE];    /* task-queue heads */
+} vx_state_t;
+
 /* Filled by the driver before every launch (hip_driver.cpp, start()). */
 extern "C" {
 __constant__ uint32_t __vx_dcrs[VX_DCR_MIRROR_SIZE];     /* DCR mirror */
 __constant__ uint64_t __vx_mem_base;                     /* arena base VA */
-__device__ unsigned long long __vx_mpm[VX_MPM_COUNT];    /* perf counters */
+__device__ vx_state_t __vx_state;
 }
 
-#define VX_MPM_TASKS 2  /* __vx_mpm slot for VX_CSR_MINSTRET (tasks run) */
+#define VX_MPM_TASKS 2  /* mpm slot for VX_CSR_MINSTRET (tasks run) */
 
 typedef struct { uint32_t x, y, z; } vx_dim3_t;
 
@@ -65,6 +77,11 @@ __device__ __forceinline__ uint32_t vx_warp_id() { return threadIdx.x >> 6; }
 __device__ __forceinline__ uint32_t vx_num_warps() { return blockDim.x >> 6; }
 __device__ __forceinline__ uint32_t vx_thread_id() { return threadIdx.x & 63u; }
 __device__ __forceinline__ uint32_t vx_num_threads() { return 64u; }
+__device__ __forceinline__ uint32_t vx_xcc_id() {
+  uint32_t x;
+  asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(x));
+  return x & (VX_SCHED_QUEUES - 1);
+}
 
 __device__ __forceinline__ uint32_t __vx_wave_sum(uint32_t v) {
 #pragma unroll
@@ -72,13 +89,49 @@ __device__ __forceinline__ uint32_t __vx_wave_sum(uint32_t v) {
   return v;
 }
 
+/* mpm counter add, one atomic per wave (all 64 lanes must call it) */
+__device__ __forceinline__ void vx_mpm_add(int slot, uint32_t v) {
+  const uint32_t s = __vx_wave_sum(v);
+  if ((threadIdx.x & 63u) == 0 && s) atomicAdd(&__vx_state.mpm[slot], (unsigned long long)s);
+}
+
+/* Wave-level dequeue of the next 64-task chunk (called by all 64 lanes with
+ * wave-uniform q/tried); returns the chunk index or UINT32_MAX when every
+ * queue is exhausted (the loop's exit condition, reached by every wave). */
+__device__ __forceinline__ uint32_t __vx_next_chunk(uint32_t nchunks, uint32_t& q, uint32_t& tried) {
+  while (tried < VX_SCHED_QUEUES) {
+    uint32_t c = 0xffffffffu;
+    if ((threadIdx.x & 63u) == 0) {
+      uint32_t* ctr = &__vx_state.sched[q * VX_SCHED_STRIDE];
+      const uint32_t cur = __hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (cur * VX_SCHED_QUEUES + q < nchunks) {
+        const uint32_t ch = atomicAdd(ctr, 1u) * VX_SCHED_QUEUES + q;
+        if (ch < nchunks) c = ch;
+      }
+    }
+    c = __shfl(c, 0, 64);
+    if (c != 0xffffffffu) return c;
+    q = (q + 1) & (VX_SCHED_QUEUES - 1);
+    ++tried;
+  }
+  return 0xffffffffu;
+}
+
+struct __vx_no_epilogue {
+  template <typename Arg>
+  __device__ __forceinline__ void operator()(bool, Arg*) const {}
+};
+
 /* vx_spawn_threads(dimension, grid_dim, block_dim, kernel_func, arg):
- * calls kernel_func(task, arg) once per grid cell.  `kernel_func` is a
- * __device__ function (inlined); returns 0, or -1 for unsupported shapes. */
-template <typename F, typename Arg>
-__device__ __forceinline__ int vx_spawn_threads(uint32_t dimension, const uint32_t* grid_dim,
-                                                const uint32_t* block_dim, F kernel_func,
-                                                Arg* arg) {
+ * calls kernel_func(task, arg) once per grid cell.  `epilogue(final, arg)` is
+ * called by all 64 lanes of a wave after each chunk (final = false) and once
+ * when the wave runs out of work (final = true): the hook a kernel uses for
+ * wave-level work such as compacted secondary rays.  Returns 0, or -1 for
+ * unsupported shapes. */
+template <typename F, typename E, typename Arg>
+__device__ __forceinline__ int vx_spawn_threads_ex(uint32_t dimension, const uint32_t* grid_dim,
+                                                   const uint32_t* block_dim, F kernel_func,
+                                                   E epilogue, Arg* arg) {
   uint32_t gd[3], num_groups = 1, group_size = 1;
 #pragma unroll
   for (int i = 0; i < 3; ++i) {
@@ -88,37 +141,58 @@ __device__ __forceinline__ int vx_spawn_threads(uint32_t dimension, const uint32
     group_size *= bd;
   }
   if (group_size != 1) return -1;
-  const uint32_t T = gridDim.x * blockDim.x;
-  const uint32_t tid = blockIdx.x * blockDim.x + threadIdx.x;
-  uint32_t ran = 0;
+  const uint32_t nchunks = (num_groups + VX_CHUNK - 1) / VX_CHUNK;
+  uint32_t q = vx_xcc_id(), tried = 0, ran = 0;
   vx_task_t task;
   task.threadIdx.x = task.threadIdx.y = task.threadIdx.z = 0;
-  for (uint32_t t = tid; t < num_groups; t += T) {
-    task.task_id = t;
-    task.blockIdx.x = t % gd[0];
-    task.blockIdx.y = (t / gd[0]) % gd[1];
-    task.blockIdx.z = t / (gd[0] * gd[1]);
-    kernel_func(task, arg);
-    ++ran;
+  for (;;) {
+    const uint32_t c = __vx_next_chunk(nchunks, q, tried);
+    if (c == 0xffffffffu) break;
+    const uint32_t t = c * VX_CHUNK + (threadIdx.x & 63u);
+    if (t < num_groups) {
+      task.task_id = t;
+      task.blockIdx.x = t % gd[0];
+      task.blockIdx.y = (t / gd[0]) % gd[1];
+      task.blockIdx.z = t / (gd[0] * gd[1]);
+      kernel_func(task, arg);
+      ++ran;
+    }
+    epilogue(false, arg);
   }
-  const uint32_t wsum = __vx_wave_sum(ran);
-  if ((threadIdx.x & 63u) == 0 && wsum)
-    atomicAdd(&__vx_mpm[VX_MPM_TASKS], (unsigned long long)wsum);
+  epilogue(true, arg);
+  vx_mpm_add(VX_MPM_TASKS, ran);
   return 0;
 }
 
-/* 1-D convenience form (the north star's vx_spawn_tasks) */
+template <typename F, typename Arg>
+__device__ __forceinline__ int vx_spawn_threads(uint32_t dimension, const uint32_t* grid_dim,
+                                                const uint32_t* block_dim, F kernel_func,
+                                                Arg* arg) {
+  return vx_spawn_threads_ex(dimension, grid_dim, block_dim, kernel_func, __vx_no_epilogue(), arg);
+}
+
+/* 1-D convenience forms (the north star's vx_spawn_tasks) */
 template <typename F, typename Arg>
 __device__ __forceinline__ int vx_spawn_tasks(uint32_t num_tasks, F kernel_func, Arg* arg) {
   return vx_spawn_threads(1u, &num_tasks, (const uint32_t*)nullptr, kernel_func, arg);
+}
+template <typename F, typename E, typename Arg>
+__device__ __forceinline__ int vx_spawn_tasks_ex(uint32_t num_tasks, F kernel_func, E epilogue,
+                                                 Arg* arg) {
+  return vx_spawn_threads_ex(1u, &num_tasks, (const uint32_t*)nullptr, kernel_func, epilogue, arg);
 }
 
 /* VX_MAIN(ArgT, arg, block_threads) { ... return vx_spawn_tasks(...); }
  * defines the `vx_main` entry the driver launches with `block_threads`
  * threads per workgroup (must be a multiple of 64). */
-#define VX_MAIN(ArgT, argname, block_threads)                                        \
+#define VX_MAIN(ArgT, argname, block_threads) \
+  VX_MAIN_BOUNDS(ArgT, argname, __launch_bounds__(block_threads))
+/* same, asking the compiler for `waves_per_eu` resident waves per SIMD */
+#define VX_MAIN_OCC(ArgT, argname, block_threads, waves_per_eu) \
+  VX_MAIN_BOUNDS(ArgT, argname, __launch_bounds__(block_threads, waves_per_eu))
+#define VX_MAIN_BOUNDS(ArgT, argname, bounds)                                        \
   static __device__ __forceinline__ int __vx_main_body(ArgT* argname);               \
-  extern "C" __global__ void __launch_bounds__(block_threads) vx_main() {            \
+  extern "C" __global__ void bounds vx_main() {                                      \
     const uint64_t a = ((uint64_t)__vx_dcrs[VX_DCR_BASE_STARTUP_ARG1] << 32) |       \
                        (uint64_t)__vx_dcrs[VX_DCR_BASE_STARTUP_ARG0];                \
     (void)__vx_main_body(vx_ptr<ArgT>(a));                                           \

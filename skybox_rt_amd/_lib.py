@@ -22,7 +22,8 @@ LIB_DIR = os.path.join(PKG_DIR, "lib")
 CSRC_DIR = os.path.join(PKG_DIR, "csrc")
 
 REQUIRED = ("libvortex.so", "libvortex-hip.so", "librtapp.so", "rtapp",
-            "rt_kernel.vxbin", "rt_kernel_stats.vxbin", "spawn_test.vxbin")
+            "rt_kernel.vxbin", "rt_kernel_stats.vxbin", "rt_kernel_deep.vxbin",
+            "rt_kernel_deep_stats.vxbin", "spawn_test.vxbin")
 
 
 class NativeLibraryMissing(RuntimeError):

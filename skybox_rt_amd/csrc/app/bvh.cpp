@@ -180,8 +180,8 @@ int BuildBvh(const std::vector<BuildTri>& tris, Bvh* out, std::string* error) {
   }
   Builder b(tris, out);
   b.run();
-  if (out->depth > RT_MAX_STACK) {
-    if (error) *error = "BVH deeper than RT_MAX_STACK";
+  if (out->depth > RT_STACK_DEEP) {
+    if (error) *error = "BVH deeper than RT_STACK_DEEP";
     return -1;
   }
   return 0;

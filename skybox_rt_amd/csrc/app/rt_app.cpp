@@ -206,7 +206,11 @@ int rt_renderer_create(rt_scene_h s, const char* kernel_dir, rt_renderer_h* out)
     return fail("vx_dev_open failed (no GPU or driver missing)");
   }
   const std::string dir = kernel_dir ? kernel_dir : lib_dir();
-  const char* names[2] = {"rt_kernel.vxbin", "rt_kernel_stats.vxbin"};
+  // the regular image's LDS stack covers BVH depth <= 16; deeper trees use the
+  // deep image (32 entries, lower occupancy)
+  const bool deep = s->bvh.depth > RT_STACK_SHALLOW;
+  const char* names[2] = {deep ? "rt_kernel_deep.vxbin" : "rt_kernel.vxbin",
+                          deep ? "rt_kernel_deep_stats.vxbin" : "rt_kernel_stats.vxbin"};
   for (int i = 0; i < 2; ++i)
     if (vx_upload_kernel_file(r->dev, (dir + "/" + names[i]).c_str(), &r->krnl[i]) != 0)
       return fail("cannot upload kernel " + dir + "/" + names[i]);

@@ -14,7 +14,14 @@
 #include <stdint.h>
 
 #define RT_BLOCK_THREADS 256
-#define RT_MAX_STACK 24          // BVH depth bound checked by the host builder
+// per-wave LDS traversal stack depth: the regular image covers BVHs of depth
+// <= 16 (keeps 24 waves/CU resident), the deep image up to 32; the host picks
+// the image from the built BVH's depth
+#define RT_STACK_SHALLOW 16
+#define RT_STACK_DEEP 32
+#ifndef RT_MAX_STACK
+#define RT_MAX_STACK RT_STACK_SHALLOW
+#endif
 #define RT_TILE_LOG 5            // RASTER_TILE_LOGSIZE (VX_config.vh:477-479)
 #define RT_TILE_PIXELS 1024
 

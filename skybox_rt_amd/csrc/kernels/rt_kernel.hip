@@ -23,6 +23,10 @@ namespace {
 
 constexpr int kWaves = RT_BLOCK_THREADS / 64;
 
+#ifndef RT_SHADOW_QUEUE
+#define RT_SHADOW_QUEUE 1
+#endif
+
 struct Counters {
   uint32_t primary = 0, shadow = 0, hits = 0, occluded = 0;
 #ifdef RT_INSTRUMENT
@@ -164,46 +168,91 @@ __device__ __forceinline__ uint32_t shade_prim(const rt_kernel_arg_t* a, int32_t
   return gfx::shade(p, s, x, y);
 }
 
-__device__ __forceinline__ void kernel_body(const vx_task_t& task, const rt_kernel_arg_t* a,
-                                            int32_t* stack, Counters& cnt) {
-  // task -> (shard-local 32x32 tile, 8x8 block, lane) -> pixel
-  const uint32_t t = task.blockIdx.x;
+// task -> (shard-local 32x32 tile, 8x8 block, lane) -> pixel
+__device__ __forceinline__ void task_pixel(const rt_kernel_arg_t* a, uint32_t t, uint32_t* x,
+                                           uint32_t* y) {
   const uint32_t lt = t >> 10, blk = (t >> 6) & 15u, ln = t & 63u;
   const uint32_t gt = a->shard_index + lt * a->shard_count;
   const uint32_t tx = gt % a->tiles_x, ty = gt / a->tiles_x;
-  const uint32_t x = (tx << RT_TILE_LOG) + ((blk & 3u) << 3) + (ln & 7u);
-  const uint32_t y = (ty << RT_TILE_LOG) + ((blk >> 2) << 3) + (ln >> 3);
-  if (x >= a->width || y >= a->height) return;
+  *x = (tx << RT_TILE_LOG) + ((blk & 3u) << 3) + (ln & 7u);
+  *y = (ty << RT_TILE_LOG) + ((blk >> 2) << 3) + (ln >> 3);
+}
 
-  Ray r;
+__device__ __forceinline__ void primary_dir(const rt_kernel_arg_t* a, uint32_t x, uint32_t y, Ray& r) {
   r.o[0] = 0.0f; r.o[1] = 0.0f; r.o[2] = 0.0f;
   r.d[0] = fmaf((float)x + 0.5f, a->sx, -1.0f);
   r.d[1] = fmaf((float)y + 0.5f, a->sy, -1.0f);
   r.d[2] = 1.0f;
+}
+
+// shadow segment from the (eye-ward nudged) hit point to the light
+__device__ __forceinline__ void shadow_ray(const rt_kernel_arg_t* a, const Ray& p, float th, Ray& s) {
+  const float tt = th * 0.999755859375f;  // origin pulled toward the eye by 2^-12 of t
+  s.o[0] = p.d[0] * tt; s.o[1] = p.d[1] * tt; s.o[2] = p.d[2] * tt;
+  s.d[0] = a->light[0] - s.o[0];
+  s.d[1] = a->light[1] - s.o[1];
+  s.d[2] = a->light[2] - s.o[2];
+  ray_setup(s);
+}
+
+__device__ __forceinline__ uint32_t shadowed(uint32_t c) {
+  return (c & 0xff000000u) | ((c >> 1) & 0x007f7f7fu);
+}
+
+__device__ __forceinline__ void store_pixel(const rt_kernel_arg_t* a, uint32_t t, uint32_t x,
+                                            uint32_t y, uint32_t color) {
+  if (a->flags & RT_FLAG_COMPACT)
+    vx_ptr<uint32_t>(a->cbuf_addr)[t] = color;
+  else
+    vx_ptr<uint32_t>(a->cbuf_addr)[(uint64_t)y * a->width + x] = color;
+}
+
+// Wave-private LDS: traversal stack (stack[depth][lane]: conflict-free
+// ds_read/write_b32) and the compaction queue of deferred shadow rays.
+#define RT_QUEUE 128
+struct WaveLds {
+  int32_t stack[RT_MAX_STACK][64];
+#if RT_SHADOW_QUEUE
+  uint32_t q_task[RT_QUEUE];
+  float q_t[RT_QUEUE];
+  int32_t q_pid[RT_QUEUE];
+  uint32_t q_color[RT_QUEUE];
+  uint32_t q_count;
+#endif
+};
+
+__device__ __forceinline__ void kernel_body(const vx_task_t& task, const rt_kernel_arg_t* a,
+                                            WaveLds& w, Counters& cnt) {
+  const uint32_t t = task.blockIdx.x;
+  uint32_t x, y;
+  task_pixel(a, t, &x, &y);
+  if (x >= a->width || y >= a->height) return;
+  int32_t* stack = &w.stack[0][threadIdx.x & 63u];
+  Ray r;
+  primary_dir(a, x, y, r);
   ray_setup(r);
   ++cnt.primary;
   const bool tie_high = (a->flags & RT_FLAG_TIE_HIGH) != 0;
   float th = 0.0f;
   const int32_t hit = trace<false>(a, r, 0.0f, INFINITY, -1, tie_high, &th, stack, cnt);
   uint32_t color = a->clear_color;
+  bool defer = false;
   if (hit >= 0) {
     ++cnt.hits;
     color = shade_prim(a, hit, x, y, cnt);
     if (a->flags & RT_FLAG_SHADOWS) {
-      // origin pulled toward the eye by 2^-12 of t; segment to the light
-      const float tt = th * 0.999755859375f;
+#if RT_SHADOW_QUEUE
+      defer = true;
+#else
       Ray s;
-      s.o[0] = r.d[0] * tt; s.o[1] = r.d[1] * tt; s.o[2] = r.d[2] * tt;
-      s.d[0] = a->light[0] - s.o[0];
-      s.d[1] = a->light[1] - s.o[1];
-      s.d[2] = a->light[2] - s.o[2];
-      ray_setup(s);
+      shadow_ray(a, r, th, s);
       ++cnt.shadow;
       float ts;
       if (trace<true>(a, s, 0.0f, 1.0f, hit, tie_high, &ts, stack, cnt) >= 0) {
         ++cnt.occluded;
-        color = (color & 0xff000000u) | ((color >> 1) & 0x007f7f7fu);
+        color = shadowed(color);
       }
+#endif
     }
   } else if (a->num_layer_tris) {
     // screen layers: highest pid first, first covering triangle wins
@@ -220,29 +269,99 @@ __device__ __forceinline__ void kernel_body(const vx_task_t& task, const rt_kern
       }
     }
   }
-  if (a->flags & RT_FLAG_COMPACT)
-    vx_ptr<uint32_t>(a->cbuf_addr)[t] = color;
-  else
-    vx_ptr<uint32_t>(a->cbuf_addr)[(uint64_t)y * a->width + x] = color;
+#if RT_SHADOW_QUEUE
+  // wave64 compaction: lanes with a pending shadow ray append it to the
+  // wave's LDS queue at ballot/mbcnt-assigned slots
+  const uint64_t m = __ballot(defer);
+  if (m) {
+    const uint32_t base = w.q_count;
+    if (defer) {
+      const uint32_t rank = __builtin_amdgcn_mbcnt_hi(
+          (uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+      const uint32_t slot = base + rank;
+      w.q_task[slot] = t;
+      w.q_t[slot] = th;
+      w.q_pid[slot] = hit;
+      w.q_color[slot] = color;
+    }
+    __builtin_amdgcn_wave_barrier();
+    if (threadIdx.x == (uint32_t)__builtin_amdgcn_readfirstlane(threadIdx.x))
+      w.q_count = base + (uint32_t)__popcll(m);
+    __builtin_amdgcn_wave_barrier();
+  }
+  if (!defer) store_pixel(a, t, x, y, color);
+#else
+  (void)defer;
+  store_pixel(a, t, x, y, color);
+#endif
 }
+
+#if RT_SHADOW_QUEUE
+// Called by all 64 lanes after every chunk: trace full waves of 64 shadow
+// rays while the queue holds >= 64 (or whatever is left at the end).
+__device__ __forceinline__ void shadow_drain(bool final, const rt_kernel_arg_t* a, WaveLds& w,
+                                             Counters& cnt) {
+  const uint32_t lane = threadIdx.x & 63u;
+  uint32_t n = w.q_count;
+  if (!(a->flags & RT_FLAG_SHADOWS)) return;
+  const bool tie_high = (a->flags & RT_FLAG_TIE_HIGH) != 0;
+  int32_t* stack = &w.stack[0][lane];
+  while (n >= 64 || (final && n > 0)) {
+    const uint32_t take = n < 64 ? n : 64;
+    const uint32_t base = n - take;
+    if (lane < take) {
+      const uint32_t slot = base + lane;
+      const uint32_t t = w.q_task[slot];
+      uint32_t x, y;
+      task_pixel(a, t, &x, &y);
+      Ray p, s;
+      primary_dir(a, x, y, p);
+      shadow_ray(a, p, w.q_t[slot], s);
+      ++cnt.shadow;
+      uint32_t color = w.q_color[slot];
+      float ts;
+      if (trace<true>(a, s, 0.0f, 1.0f, w.q_pid[slot], tie_high, &ts, stack, cnt) >= 0) {
+        ++cnt.occluded;
+        color = shadowed(color);
+      }
+      store_pixel(a, t, x, y, color);
+    }
+    n = base;
+  }
+  __builtin_amdgcn_wave_barrier();
+  if (lane == 0) w.q_count = n;
+  __builtin_amdgcn_wave_barrier();
+}
+#endif
 
 // RT statistics go to the user MPM counters (VX_CSR_MPM_USER = 0xB03 + slot),
 // which the driver zeroes before every launch and vx_mpm_query() reads back.
-__device__ __forceinline__ void flush(int slot, uint32_t v) {
-  const uint32_t s = __vx_wave_sum(v);
-  if ((threadIdx.x & 63u) == 0 && s) atomicAdd(&__vx_mpm[RT_MPM_USER + slot], (unsigned long long)s);
-}
+__device__ __forceinline__ void flush(int slot, uint32_t v) { vx_mpm_add(RT_MPM_USER + slot, v); }
 
 }  // namespace
 
+#ifdef RT_WAVES_PER_EU
+VX_MAIN_OCC(rt_kernel_arg_t, arg, RT_BLOCK_THREADS, RT_WAVES_PER_EU) {
+#else
 VX_MAIN(rt_kernel_arg_t, arg, RT_BLOCK_THREADS) {
-  __shared__ int32_t s_stack[kWaves][RT_MAX_STACK][64];
-  int32_t* stack = &s_stack[threadIdx.x >> 6][0][threadIdx.x & 63];
+#endif
+  __shared__ WaveLds s_wave[kWaves];
+  WaveLds& w = s_wave[threadIdx.x >> 6];
   Counters cnt;
+#if RT_SHADOW_QUEUE
+  if ((threadIdx.x & 63u) == 0) w.q_count = 0;
+  __builtin_amdgcn_wave_barrier();
+  const int rc = vx_spawn_tasks_ex(
+      arg->num_tasks,
+      [&](const vx_task_t& task, const rt_kernel_arg_t* a) { kernel_body(task, a, w, cnt); },
+      [&](bool final, const rt_kernel_arg_t* a) { shadow_drain(final, a, w, cnt); },
+      (const rt_kernel_arg_t*)arg);
+#else
   const int rc = vx_spawn_tasks(
       arg->num_tasks,
-      [&](const vx_task_t& task, const rt_kernel_arg_t* a) { kernel_body(task, a, stack, cnt); },
+      [&](const vx_task_t& task, const rt_kernel_arg_t* a) { kernel_body(task, a, w, cnt); },
       (const rt_kernel_arg_t*)arg);
+#endif
   flush(RT_STAT_PRIMARY, cnt.primary);
   flush(RT_STAT_SHADOW, cnt.shadow);
   flush(RT_STAT_HITS, cnt.hits);
