@@ -157,7 +157,7 @@ def main():
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step()
-        kernel_ms.append(r.stats()["kernel_ms"])
+        kernel_ms.append(r.kernel_ms())
     torch.cuda.synchronize()
     if dist is not None:
         dist.barrier()

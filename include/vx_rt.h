@@ -73,6 +73,8 @@ int rt_render_start(rt_renderer_h r);
 int rt_render_wait(rt_renderer_h r);
 int rt_render(rt_renderer_h r);  /* start + wait */
 int rt_render_stats(rt_renderer_h r, rt_stats_t* stats);
+/* HIP-event duration of the last launch only (no counter read-back) */
+int rt_render_kernel_ms(rt_renderer_h r, double* kernel_ms);
 /* linear W*H framebuffer (shard_count == 1) or compact tile buffer
  * (local_tiles * 1024 pixels in task order) */
 int rt_read_framebuffer(rt_renderer_h r, uint32_t* out, uint64_t count);

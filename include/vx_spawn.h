@@ -39,6 +39,14 @@
 #define VX_SCHED_STRIDE 16   /* one 64-B line per queue counter */
 #define VX_CHUNK 64          /* tasks per wave-level dequeue */
 
+/* task scheduling policy of vx_spawn_threads (see the header comment) */
+#define VX_POLICY_STATIC 0   /* wave w takes chunks w, w + W, w + 2W, ... */
+#define VX_POLICY_QUEUES 1   /* 8 XCD-affine dynamic queues */
+#define VX_POLICY_HYBRID 2   /* per-block contiguous strip + global pool */
+#ifndef VX_SPAWN_POLICY
+#define VX_SPAWN_POLICY VX_POLICY_STATIC
+#endif
+
 /* per-launch device state, zeroed by the driver before every launch */
 typedef struct {
   unsigned long long mpm[VX_MPM_COUNT];                 /* perf counters (vx_mpm_query) */
@@ -69,6 +77,57 @@ __device__ __forceinline__ T* vx_ptr(uint64_t addr) {
 }
 
 __device__ __forceinline__ uint32_t vx_dcr(uint32_t addr) { return __vx_dcrs[addr]; }
+
+/* The arena as one buffer resource (V#): device addresses below 4 GiB are
+ * 32-bit buffer offsets, so hot loops use buffer_load/store with an SGPR
+ * descriptor instead of 64-bit flat addressing (flat loads also count on
+ * lgkmcnt and so serialise with LDS traffic).  Out-of-range offsets read 0. */
+struct vx_arena {
+  __amdgpu_buffer_rsrc_t r;
+  uint64_t base;
+  __device__ __forceinline__ static vx_arena get() {
+    const uint64_t b = __vx_mem_base;
+    const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)b);
+    const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(b >> 32));
+    vx_arena a;
+    a.base = ((uint64_t)hi << 32) | lo;
+    a.r = __builtin_amdgcn_make_buffer_rsrc((void*)a.base, 0, (int)0xffffffffu, 0x00020000);
+    return a;
+  }
+  /* Wave-uniform loads through the scalar cache (s_load into SGPRs): one
+   * instruction per record for the whole wave instead of 64 lanes' worth of
+   * vector-cache data return.  `off` must be the same in every lane (it is
+   * taken from the first active lane); the data must not change during the
+   * launch (scene records, never the framebuffer). */
+  template <typename T>
+  __device__ __forceinline__ T sld(uint32_t off) const {
+    const uint32_t o = __builtin_amdgcn_readfirstlane(off);
+    return *(const __attribute__((address_space(4))) T*)(base + o);
+  }
+  __device__ __forceinline__ float4 sld_f4(uint32_t off) const { return sld<float4>(off); }
+  __device__ __forceinline__ uint4 sld_u4(uint32_t off) const { return sld<uint4>(off); }
+  __device__ __forceinline__ float4 ld_f4(uint32_t off) const {
+    const auto v = __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0);
+    return make_float4(__uint_as_float(v[0]), __uint_as_float(v[1]), __uint_as_float(v[2]),
+                       __uint_as_float(v[3]));
+  }
+  __device__ __forceinline__ uint4 ld_u4(uint32_t off) const {
+    const auto v = __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0);
+    return make_uint4(v[0], v[1], v[2], v[3]);
+  }
+  __device__ __forceinline__ uint32_t ld_u32(uint32_t off) const {
+    return __builtin_amdgcn_raw_buffer_load_b32(r, off, 0, 0);
+  }
+  __device__ __forceinline__ uint32_t ld_u16(uint32_t off) const {
+    return __builtin_amdgcn_raw_buffer_load_b16(r, off, 0, 0);
+  }
+  __device__ __forceinline__ uint32_t ld_u8(uint32_t off) const {
+    return __builtin_amdgcn_raw_buffer_load_b8(r, off, 0, 0);
+  }
+  __device__ __forceinline__ void st_u32(uint32_t off, uint32_t v) const {
+    __builtin_amdgcn_raw_buffer_store_b32(v, r, off, 0, 0);
+  }
+};
 
 /* hardware identity (vx_intrinsics.h vx_core_id/vx_warp_id/vx_thread_id) */
 __device__ __forceinline__ uint32_t vx_core_id() { return blockIdx.x; }
@@ -145,9 +204,39 @@ __device__ __forceinline__ int vx_spawn_threads_ex(uint32_t dimension, const uin
   uint32_t q = vx_xcc_id(), tried = 0, ran = 0;
   vx_task_t task;
   task.threadIdx.x = task.threadIdx.y = task.threadIdx.z = 0;
+#if VX_SPAWN_POLICY == VX_POLICY_STATIC
+  const uint32_t nwaves = gridDim.x * (blockDim.x >> 6);
+  uint32_t c = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+  (void)q; (void)tried;
+  for (; c < nchunks; c += nwaves) {
+#elif VX_SPAWN_POLICY == VX_POLICY_HYBRID
+  // block b owns a contiguous strip of R chunks (locality: the block's waves
+  // walk neighbouring pixels through one L1); what is left over is a global
+  // pool the early finishers drain (balance)
+  __shared__ uint32_t __vx_block_head;
+  const uint32_t R = (nchunks * 3u / 4u) / gridDim.x;
+  if (threadIdx.x == 0) __vx_block_head = 0;
+  __syncthreads();
+  (void)q;
+  (void)tried;
+  for (;;) {
+    uint32_t c = 0xffffffffu;
+    if ((threadIdx.x & 63u) == 0) {
+      const uint32_t i = atomicAdd(&__vx_block_head, 1u);  // LDS atomic
+      if (i < R) {
+        c = blockIdx.x * R + i;
+      } else {
+        const uint32_t p = gridDim.x * R + atomicAdd(&__vx_state.sched[0], 1u);
+        if (p < nchunks) c = p;
+      }
+    }
+    c = __shfl(c, 0, 64);
+    if (c == 0xffffffffu) break;
+#else
   for (;;) {
     const uint32_t c = __vx_next_chunk(nchunks, q, tried);
     if (c == 0xffffffffu) break;
+#endif
     const uint32_t t = c * VX_CHUNK + (threadIdx.x & 63u);
     if (t < num_groups) {
       task.task_id = t;

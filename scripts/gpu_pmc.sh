@@ -1,0 +1,22 @@
+# PMC passes over scripts/prof_rt.py (one rocprofv3 --pmc pass per counter group).
+set -o pipefail
+cd "$GRAFT_REPO_ROOT"
+export TMPDIR=/tmp
+TAG=${TAG:-pmc}; mkdir -p gpurun_out/$TAG
+run() {  # name, counters...
+  local name=$1; shift
+  timeout -k 10 180 rocprofv3 --pmc "$@" -d gpurun_out/$TAG/$name -o run --output-format csv -- python3 scripts/prof_rt.py --frames 10 > gpurun_out/$TAG/$name.log 2>&1
+  local rc=$?
+  echo "pass $name rc=$rc"
+  case $rc in 124|134|137|139) exit $rc;; esac
+  return 0
+}
+timeout -k 10 180 rocprofv3 --kernel-trace --stats -d gpurun_out/$TAG/trace -o run --output-format csv -- python3 scripts/prof_rt.py --frames 20 > gpurun_out/$TAG/trace.log 2>&1 || exit $?
+run p1 SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY GRBM_GUI_ACTIVE
+run p2 SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_VMEM_RD SQ_INSTS_LDS SQ_INSTS_SMEM SQ_INSTS_VMEM_WR
+run p3 SQ_ACTIVE_INST_VALU SQ_THREAD_CYCLES_VALU SQ_ACTIVE_INST_LDS SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT
+run p4 TCP_TOTAL_CACHE_ACCESSES_sum TCP_TCC_READ_REQ_sum TCC_HIT_sum TCC_MISS_sum
+run p5 FETCH_SIZE
+run p6 WRITE_SIZE
+run p7 TA_BUSY_avr TA_TA_BUSY_sum TD_TD_BUSY_sum SQ_INSTS_FLAT
+ls gpurun_out/$TAG

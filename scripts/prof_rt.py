@@ -1,0 +1,29 @@
+#!/usr/bin/env python3
+"""Render N frames of the benchmark workload (for rocprofv3 passes)."""
+import argparse
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--size", type=int, default=1024)
+    ap.add_argument("--frames", type=int, default=20)
+    ap.add_argument("--no-shadows", action="store_true")
+    ap.add_argument("--kernel-dir", default=None)
+    args = ap.parse_args()
+    import torch  # noqa: F401
+    from skybox_rt_amd import rt
+    s = rt.Scene.load(os.path.join(ROOT, "tests/golden/scenes/tekkaman.cgltrace"))
+    r = rt.Renderer(s, kernel_dir=args.kernel_dir)
+    r.configure(args.size, args.size, shadows=not args.no_shadows)
+    for _ in range(args.frames):
+        r.render()
+    print(r.stats(), file=sys.stderr)
+
+
+if __name__ == "__main__":
+    main()

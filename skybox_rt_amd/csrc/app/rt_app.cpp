@@ -193,7 +193,11 @@ static int upload(vx_device_h dev, const void* data, uint64_t size, vx_buffer_h*
   *buf = nullptr;
   if (vx_mem_alloc(dev, sz, VX_MEM_READ, buf) != 0) return fail("vx_mem_alloc failed");
   if (size && vx_copy_to_dev(*buf, data, 0, size) != 0) return fail("vx_copy_to_dev failed");
-  return vx_mem_address(*buf, addr) == 0 ? 0 : fail("vx_mem_address failed");
+  if (vx_mem_address(*buf, addr) != 0) return fail("vx_mem_address failed");
+  // the kernel addresses every buffer with 32-bit offsets into one arena
+  // descriptor (vx_arena in vx_spawn.h)
+  if (*addr + sz > (1ull << 32)) return fail("buffer beyond the 4 GiB kernel address range");
+  return 0;
 }
 
 int rt_renderer_create(rt_scene_h s, const char* kernel_dir, rt_renderer_h* out) {
@@ -220,8 +224,12 @@ int rt_renderer_create(rt_scene_h s, const char* kernel_dir, rt_renderer_h* out)
   rt_kernel_arg_t& a = r->arg;
   std::memset(&a, 0, sizeof(a));
   const rt::Bvh& bvh = s->bvh;
+  // 3 padding records: the kernel fetches all 4 slots of a leaf at once
+  std::vector<rt_tri_t> tris(bvh.tris);
+  tris.resize(tris.size() + 3);
+  std::memset(tris.data() + bvh.tris.size(), 0, 3 * sizeof(rt_tri_t));
   if (upload(r->dev, bvh.nodes.data(), bvh.nodes.size() * sizeof(rt_node_t), &r->nodes, &a.nodes_addr) ||
-      upload(r->dev, bvh.tris.data(), bvh.tris.size() * sizeof(rt_tri_t), &r->tris, &a.tris_addr))
+      upload(r->dev, tris.data(), tris.size() * sizeof(rt_tri_t), &r->tris, &a.tris_addr))
     return -1;
   a.num_nodes = (uint32_t)bvh.nodes.size();
   // screen layers, highest pid first
@@ -373,6 +381,14 @@ int rt_render_stats(rt_renderer_h r, rt_stats_t* st) {
   if (r->last_run) r->last_run(r->dev, &st->kernel_ms, &st->grid, &st->block);
   st->num_tasks = r->arg.num_tasks;
   st->local_tiles = r->local_tiles;
+  return 0;
+}
+
+int rt_render_kernel_ms(rt_renderer_h r, double* kernel_ms) {
+  if (!r || !kernel_ms) return fail("null argument");
+  uint32_t grid = 0, block = 0;
+  if (!r->last_run || r->last_run(r->dev, kernel_ms, &grid, &block) != 0)
+    return fail("vx_hip_last_run failed");
   return 0;
 }
 

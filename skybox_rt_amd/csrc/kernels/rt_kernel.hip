@@ -1,31 +1,63 @@
 // rt_kernel.hip -- the north-star hot path as a Vortex kernel program for
-// gfx950: per-pixel ray generation, BVH2 traversal with an LDS-resident
-// per-wave stack, Möller–Trumbore closest hit, screen layers, draw3d-exact
-// shading of the hit and an any-hit shadow ray per geometry hit.
+// gfx950: per-pixel ray generation, BVH2 traversal, Möller–Trumbore closest
+// hit, screen layers, draw3d-exact shading of the hit and an any-hit shadow
+// ray per geometry hit, with the shadow rays compacted into full waves
+// (ballot + mbcnt into an LDS queue).
 //
 // Launched by libvortex-hip.so (vx_start) as `vx_main`; the body reads its
-// rt_kernel_arg_t from the STARTUP_ARG DCRs and calls vx_spawn_tasks() with
-// one task per pixel (64 consecutive tasks = one wave = an 8x8 pixel block,
-// 16 waves = one 32x32 raster tile, the reference's tile unit).
+// rt_kernel_arg_t from the STARTUP_ARG DCRs and calls vx_spawn_tasks_ex()
+// with one task per pixel (64 consecutive tasks = one wave = an 8x8 pixel
+// block, 16 waves = one 32x32 raster tile, the reference's tile unit).
 //
-// Numerics are bit-identical to the oracle (oracle/rt.c): every fused
-// multiply-add is an explicit fmaf, everything else is compiled with
-// -ffp-contract=off, divisions are IEEE (correctly rounded).
-// Build with -DRT_INSTRUMENT for the counting variant (node visits, triangle
-// tests, shading bytes) used to derive the algorithmic byte count.
+// Two traversal forms, identical results (tests/test_gpu_rt.py):
+//  * wave packet (default image): the 64 rays of a wave walk the BVH
+//    together.  Node and triangle records are wave-uniform, so they come in
+//    through the scalar cache (s_load into SGPRs, one instruction per record
+//    per wave), each lane tests its own ray, ballots decide where the packet
+//    goes, and the traversal stack is wave-uniform: entry i lives in lane i
+//    of three VGPRs (readlane / writelane, no memory traffic).  Every lane
+//    keeps its own closest (t, pid) and culls with it, so the hit found is
+//    exactly the per-ray one: boxes are conservative and the closest-hit
+//    order is total (t, then pid by the tie rule).
+//  * per ray (RT_PACKET=0, and the RT_INSTRUMENT counting image): each lane
+//    walks alone with its stack in LDS, stack[depth][lane], conflict-free.
+//    Its node-visit / triangle-test counts are the per-ray traversal work the
+//    oracle (oracle/rt.c bvh_trace) restates, the basis of the algorithmic
+//    byte count of SURVEY.md 8(d).
+//
+// Scene reads are buffer / scalar loads through one arena descriptor
+// (vx_arena): 32-bit offsets, no FLAT loads.  Numerics are bit-identical to
+// the oracle (oracle/rt.c): every fused multiply-add is an explicit fmaf,
+// everything else is compiled with -ffp-contract=off, divisions are IEEE.
+//
+// The packet code needs all 64 lanes of a wave present (it never returns
+// early per lane): vx_spawn hands out whole 64-task chunks and the RT app's
+// task count is a multiple of 1024.
 #include <hip/hip_runtime.h>
 
 #include "gfx_device.h"
 #include "rt_common.h"
 #include "vx_spawn.h"
 
-namespace {
-
-constexpr int kWaves = RT_BLOCK_THREADS / 64;
-
 #ifndef RT_SHADOW_QUEUE
 #define RT_SHADOW_QUEUE 1
 #endif
+#ifndef RT_PACKET
+#ifdef RT_INSTRUMENT
+#define RT_PACKET 0
+#else
+#define RT_PACKET 1
+#endif
+#endif
+// distinct primitives per wave shaded from SGPR records before the rest of
+// the wave falls back to per-lane (vector) record loads
+#ifndef RT_SHADE_UNIFORM
+#define RT_SHADE_UNIFORM 2
+#endif
+
+namespace {
+
+constexpr int kWaves = RT_BLOCK_THREADS / 64;
 
 struct Counters {
   uint32_t primary = 0, shadow = 0, hits = 0, occluded = 0;
@@ -33,6 +65,46 @@ struct Counters {
   uint32_t visits = 0, tests = 0, layer_tests = 0, shaded = 0, texel_bytes = 0;
 #endif
 };
+
+// Kernel arguments in scalar registers; buffer addresses become 32-bit
+// arena offsets (rt_app checks every buffer lies below 4 GiB).
+struct Scene {
+  vx_arena A;
+  uint32_t nodes, tris, layers, prims, dcs, cbuf;
+  uint32_t num_nodes, num_layer, flags, width, height;
+  uint32_t shard_index, shard_count, tiles_x, clear_color;
+  float sx, sy, light[3];
+};
+
+__device__ __forceinline__ Scene load_scene(const rt_kernel_arg_t* a) {
+  Scene s;
+  s.A = vx_arena::get();
+  s.nodes = (uint32_t)a->nodes_addr;
+  s.tris = (uint32_t)a->tris_addr;
+  s.layers = (uint32_t)a->layers_addr;
+  s.prims = (uint32_t)a->prims_addr;
+  s.dcs = (uint32_t)a->dcs_addr;
+  s.cbuf = (uint32_t)a->cbuf_addr;
+  s.num_nodes = a->num_nodes;
+  s.num_layer = a->num_layer_tris;
+  s.flags = a->flags;
+  s.width = a->width;
+  s.height = a->height;
+  s.shard_index = a->shard_index;
+  s.shard_count = a->shard_count;
+  s.tiles_x = a->tiles_x;
+  s.clear_color = a->clear_color;
+  s.sx = a->sx;
+  s.sy = a->sy;
+  s.light[0] = a->light[0];
+  s.light[1] = a->light[1];
+  s.light[2] = a->light[2];
+  return s;
+}
+
+__device__ __forceinline__ uint32_t lane_id() {
+  return __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
+}
 
 struct Ray {
   float o[3], d[3];
@@ -95,23 +167,128 @@ __device__ __forceinline__ bool slab(float lox, float hix, float loy, float hiy,
   return tn <= tf;
 }
 
-// Closest hit (ANY = false) or any hit excluding `skip` (ANY = true).
-// Traversal order and culling are restated exactly by oracle/rt.c bvh_trace.
+// closest-hit order: t, then pid by the drawcall's depth-compare tie rule
+__device__ __forceinline__ bool closer(float t, int32_t pid, float bt, int32_t bpid, bool tie_high) {
+  return (t < bt) || (t == bt && (tie_high ? pid > bpid : pid < bpid));
+}
+
+#if RT_PACKET
+// v[lane] = val, for wave-uniform val and lane (v_writelane ignores EXEC)
+template <typename T>
+__device__ __forceinline__ void writelane(T& v, T val, int lane) {
+  asm volatile("v_writelane_b32 %0, %1, m0" : "+v"(v) : "s"(val), "{m0}"(lane));
+}
+
+// Wave-packet traversal: closest hit (ANY = false) or any hit excluding
+// `skip` (ANY = true) for every lane with `active`; all 64 lanes call it.
 template <bool ANY>
-__device__ __forceinline__ int32_t trace(const rt_kernel_arg_t* a, const Ray& r, float tmin,
-                                         float tmax, int32_t skip, bool tie_high, float* t_out,
+__device__ __forceinline__ int32_t ptrace(const Scene& S, const Ray& r, float tmin, float tmax,
+                                          int32_t skip, bool tie_high, bool active,
+                                          float* t_out) {
+  const uint64_t bit = 1ull << lane_id();
+  uint64_t M = __ballot(active);
+  float bt = tmax;
+  int32_t bpid = -1;
+  if (S.num_nodes == 0 || M == 0) return -1;
+  int32_t st_ref = 0;             // stack entry i = lane i
+  uint32_t st_lo = 0, st_hi = 0;  // lanes that entered the pushed child's box
+  int sp = 0;
+  int32_t ref = 0;
+  uint64_t done = 0;  // ANY: lanes already occluded
+  for (;;) {
+    const bool mine = (M & bit) != 0;
+    if (ref >= 0) {
+      const uint32_t no = S.nodes + 64u * (uint32_t)ref;
+      const float4 n0 = S.A.sld_f4(no), n1 = S.A.sld_f4(no + 16);
+      const float4 n2 = S.A.sld_f4(no + 32), n3 = S.A.sld_f4(no + 48);
+      const int32_t c0 = __float_as_int(n3.x), c1 = __float_as_int(n3.y);
+      const float lim = ANY ? tmax : bt;
+      float tn0 = 0.0f, tn1 = 0.0f;
+      const bool h0 = mine && c0 != RT_EMPTY_REF &&
+                      slab(n0.x, n0.y, n1.x, n1.y, n2.x, n2.y, r, tmin, lim, &tn0);
+      const bool h1 = mine && c1 != RT_EMPTY_REF &&
+                      slab(n0.z, n0.w, n1.z, n1.w, n2.z, n2.w, r, tmin, lim, &tn1);
+      const uint64_t m0 = __ballot(h0), m1 = __ballot(h1);
+      if (m0 && m1) {
+        // near child first, by majority of the lanes entering both
+        const uint64_t w1 = __ballot(h0 && h1 && tn1 < tn0);
+        const uint64_t w0 = __ballot(h0 && h1 && !(tn1 < tn0));
+        const bool first1 = __popcll(w1) > __popcll(w0);
+        const int32_t far_ref = first1 ? c0 : c1;
+        const uint64_t far_m = first1 ? m0 : m1;
+        if (sp < 64) {
+          writelane(st_ref, far_ref, sp);
+          writelane(st_lo, (uint32_t)far_m, sp);
+          writelane(st_hi, (uint32_t)(far_m >> 32), sp);
+          ++sp;
+        }
+        ref = first1 ? c1 : c0;
+        M = first1 ? m1 : m0;
+        continue;
+      }
+      if (m0) { ref = c0; M = m0; continue; }
+      if (m1) { ref = c1; M = m1; continue; }
+    } else {
+      const uint32_t lr = (uint32_t)ref;
+      const uint32_t first = (lr >> 4) & 0x07ffffffu, count = (lr & 15u) + 1u;
+      const uint32_t to = S.tris + 48u * first;
+      bool found = false;
+#pragma unroll
+      for (uint32_t k = 0; k < 4; ++k) {
+        if (k < count) {
+          const float4 ta = S.A.sld_f4(to + 48u * k);
+          const float4 tb = S.A.sld_f4(to + 48u * k + 16);
+          const float4 tc = S.A.sld_f4(to + 48u * k + 32);
+          const int32_t pid = __float_as_int(ta.w);
+          float t;
+          if (mine && !found && pid != skip && mt_hit(r, ta, tb, tc, tmin, &t)) {
+            if (ANY) {
+              if (t < tmax) { found = true; bt = t; bpid = pid; }
+            } else if (closer(t, pid, bt, bpid, tie_high)) {
+              bt = t;
+              bpid = pid;
+            }
+          }
+        }
+      }
+      if (ANY) {
+        done |= __ballot(found);
+        M &= ~done;
+        if ((__ballot(active) & ~done) == 0) break;
+      }
+    }
+    // pop the next subtree some lane still needs
+    bool empty = true;
+    while (sp > 0) {
+      --sp;
+      ref = __builtin_amdgcn_readlane(st_ref, sp);
+      M = (((uint64_t)__builtin_amdgcn_readlane(st_hi, sp) << 32) |
+           (uint64_t)__builtin_amdgcn_readlane(st_lo, sp)) & ~done;
+      if (M) { empty = false; break; }
+    }
+    if (empty) break;
+  }
+  if (bpid >= 0) *t_out = bt;
+  return bpid;
+}
+#else
+// Per-ray traversal with the LDS stack (oracle/rt.c bvh_trace restates it
+// exactly, counters included).  A leaf's (up to 4) triangles are fetched in
+// one batch -- the tris array carries 3 padding records.
+template <bool ANY>
+__device__ __forceinline__ int32_t trace(const Scene& S, const Ray& r, float tmin, float tmax,
+                                         int32_t skip, bool tie_high, float* t_out,
                                          int32_t* stack, Counters& cnt) {
-  if (a->num_nodes == 0) return -1;
-  const float4* nodes = vx_ptr<const float4>(a->nodes_addr);
-  const float4* tris = vx_ptr<const float4>(a->tris_addr);
+  if (S.num_nodes == 0) return -1;
   int sp = 0;
   int32_t ref = 0;
   float bt = tmax;
   int32_t bpid = -1;
   for (;;) {
     if (ref >= 0) {
-      const float4 n0 = nodes[4 * ref + 0], n1 = nodes[4 * ref + 1];
-      const float4 n2 = nodes[4 * ref + 2], n3 = nodes[4 * ref + 3];
+      const uint32_t no = S.nodes + 64u * (uint32_t)ref;
+      const float4 n0 = S.A.ld_f4(no), n1 = S.A.ld_f4(no + 16);
+      const float4 n2 = S.A.ld_f4(no + 32), n3 = S.A.ld_f4(no + 48);
 #ifdef RT_INSTRUMENT
       ++cnt.visits;
 #endif
@@ -132,22 +309,31 @@ __device__ __forceinline__ int32_t trace(const rt_kernel_arg_t* a, const Ray& r,
     } else {
       const uint32_t lr = (uint32_t)ref;
       const uint32_t first = (lr >> 4) & 0x07ffffffu, count = (lr & 15u) + 1u;
-      for (uint32_t k = 0; k < count; ++k) {
-        const float4 ta = tris[3 * (first + k) + 0];
-        const int32_t pid = __float_as_int(ta.w);
+      const uint32_t to = S.tris + 48u * first;
+      float4 ta[4], tb[4], tc[4];
+#pragma unroll
+      for (uint32_t k = 0; k < 4; ++k) {
+        ta[k] = S.A.ld_f4(to + 48u * k);
+        tb[k] = S.A.ld_f4(to + 48u * k + 16);
+        tc[k] = S.A.ld_f4(to + 48u * k + 32);
+      }
+#pragma unroll
+      for (uint32_t k = 0; k < 4; ++k) {
+        if (k < count) {
+          const int32_t pid = __float_as_int(ta[k].w);
 #ifdef RT_INSTRUMENT
-        ++cnt.tests;
+          ++cnt.tests;
 #endif
-        if (pid == skip) continue;
-        const float4 tb = tris[3 * (first + k) + 1], tc = tris[3 * (first + k) + 2];
-        float t;
-        if (!mt_hit(r, ta, tb, tc, tmin, &t)) continue;
-        if (ANY) {
-          if (t < tmax) { *t_out = t; return pid; }
-          continue;
+          float t;
+          if (pid != skip && mt_hit(r, ta[k], tb[k], tc[k], tmin, &t)) {
+            if (ANY) {
+              if (t < tmax) { *t_out = t; return pid; }
+            } else if (closer(t, pid, bt, bpid, tie_high)) {
+              bt = t;
+              bpid = pid;
+            }
+          }
         }
-        const bool better = (t < bt) || (t == bt && (tie_high ? pid > bpid : pid < bpid));
-        if (better) { bt = t; bpid = pid; }
       }
     }
     if (sp == 0) break;
@@ -156,42 +342,67 @@ __device__ __forceinline__ int32_t trace(const rt_kernel_arg_t* a, const Ray& r,
   if (bpid >= 0) *t_out = bt;
   return bpid;
 }
+#endif
 
-__device__ __forceinline__ uint32_t shade_prim(const rt_kernel_arg_t* a, int32_t pid, uint32_t x,
+// shade primitive `pid` at (x, y) from per-lane (vector) record loads
+__device__ __forceinline__ uint32_t shade_lane(const Scene& S, int32_t pid, uint32_t x,
                                                uint32_t y, Counters& cnt) {
-  const rt_prim_t& p = vx_ptr<const rt_prim_t>(a->prims_addr)[pid];
-  const rt_dcstate_t& s = vx_ptr<const rt_dcstate_t>(a->dcs_addr)[p.dc];
+  gfx::Prim p;
+  gfx::load_prim(S.A, S.prims + 128u * (uint32_t)pid, p);
+  const gfx::DcState s = gfx::load_dcstate(S.A, S.dcs + 64u * p.dc());
 #ifdef RT_INSTRUMENT
   ++cnt.shaded;
-  if (s.flags & RT_DC_TEX) cnt.texel_bytes += (s.tex_filter == VX_TEX_FILTER_BILINEAR ? 4u : 1u) * s.tex_stride;
+  if (s.flags & RT_DC_TEX) cnt.texel_bytes += (s.filter == VX_TEX_FILTER_BILINEAR ? 4u : 1u) * s.stride;
 #endif
-  return gfx::shade(p, s, x, y);
+  return gfx::shade(S.A, p, s, x, y);
+}
+
+// Shade every lane with spid >= 0 (all 64 lanes call it): the wave's most
+// common primitives first from SGPR records (s_load, one per wave), then
+// whatever is left from per-lane record loads.
+__device__ __forceinline__ uint32_t shade_wave(const Scene& S, int32_t spid, uint32_t x,
+                                               uint32_t y, uint32_t color, Counters& cnt) {
+#if RT_PACKET
+  uint64_t need = __ballot(spid >= 0);
+#pragma unroll 1
+  for (int it = 0; need != 0 && it < RT_SHADE_UNIFORM; ++it) {
+    const int32_t u = __builtin_amdgcn_readlane(spid, (int)__builtin_ctzll(need));
+    gfx::Prim p;
+    gfx::load_prim<true>(S.A, S.prims + 128u * (uint32_t)u, p);
+    const gfx::DcState s = gfx::load_dcstate<true>(S.A, S.dcs + 64u * p.dc());
+    if (spid == u) color = gfx::shade(S.A, p, s, x, y);
+    need &= ~__ballot(spid == u);
+  }
+  if (need != 0 && (need & (1ull << lane_id())) != 0) color = shade_lane(S, spid, x, y, cnt);
+  return color;
+#else
+  return spid >= 0 ? shade_lane(S, spid, x, y, cnt) : color;
+#endif
 }
 
 // task -> (shard-local 32x32 tile, 8x8 block, lane) -> pixel
-__device__ __forceinline__ void task_pixel(const rt_kernel_arg_t* a, uint32_t t, uint32_t* x,
-                                           uint32_t* y) {
+__device__ __forceinline__ void task_pixel(const Scene& S, uint32_t t, uint32_t* x, uint32_t* y) {
   const uint32_t lt = t >> 10, blk = (t >> 6) & 15u, ln = t & 63u;
-  const uint32_t gt = a->shard_index + lt * a->shard_count;
-  const uint32_t tx = gt % a->tiles_x, ty = gt / a->tiles_x;
+  const uint32_t gt = S.shard_index + lt * S.shard_count;
+  const uint32_t tx = gt % S.tiles_x, ty = gt / S.tiles_x;
   *x = (tx << RT_TILE_LOG) + ((blk & 3u) << 3) + (ln & 7u);
   *y = (ty << RT_TILE_LOG) + ((blk >> 2) << 3) + (ln >> 3);
 }
 
-__device__ __forceinline__ void primary_dir(const rt_kernel_arg_t* a, uint32_t x, uint32_t y, Ray& r) {
+__device__ __forceinline__ void primary_dir(const Scene& S, uint32_t x, uint32_t y, Ray& r) {
   r.o[0] = 0.0f; r.o[1] = 0.0f; r.o[2] = 0.0f;
-  r.d[0] = fmaf((float)x + 0.5f, a->sx, -1.0f);
-  r.d[1] = fmaf((float)y + 0.5f, a->sy, -1.0f);
+  r.d[0] = fmaf((float)x + 0.5f, S.sx, -1.0f);
+  r.d[1] = fmaf((float)y + 0.5f, S.sy, -1.0f);
   r.d[2] = 1.0f;
 }
 
 // shadow segment from the (eye-ward nudged) hit point to the light
-__device__ __forceinline__ void shadow_ray(const rt_kernel_arg_t* a, const Ray& p, float th, Ray& s) {
+__device__ __forceinline__ void shadow_ray(const Scene& S, const Ray& p, float th, Ray& s) {
   const float tt = th * 0.999755859375f;  // origin pulled toward the eye by 2^-12 of t
   s.o[0] = p.d[0] * tt; s.o[1] = p.d[1] * tt; s.o[2] = p.d[2] * tt;
-  s.d[0] = a->light[0] - s.o[0];
-  s.d[1] = a->light[1] - s.o[1];
-  s.d[2] = a->light[2] - s.o[2];
+  s.d[0] = S.light[0] - s.o[0];
+  s.d[1] = S.light[1] - s.o[1];
+  s.d[2] = S.light[2] - s.o[2];
   ray_setup(s);
 }
 
@@ -199,19 +410,19 @@ __device__ __forceinline__ uint32_t shadowed(uint32_t c) {
   return (c & 0xff000000u) | ((c >> 1) & 0x007f7f7fu);
 }
 
-__device__ __forceinline__ void store_pixel(const rt_kernel_arg_t* a, uint32_t t, uint32_t x,
-                                            uint32_t y, uint32_t color) {
-  if (a->flags & RT_FLAG_COMPACT)
-    vx_ptr<uint32_t>(a->cbuf_addr)[t] = color;
-  else
-    vx_ptr<uint32_t>(a->cbuf_addr)[(uint64_t)y * a->width + x] = color;
+__device__ __forceinline__ void store_pixel(const Scene& S, uint32_t t, uint32_t x, uint32_t y,
+                                            uint32_t color) {
+  const uint32_t idx = (S.flags & RT_FLAG_COMPACT) ? t : y * S.width + x;
+  S.A.st_u32(S.cbuf + 4u * idx, color);
 }
 
-// Wave-private LDS: traversal stack (stack[depth][lane]: conflict-free
-// ds_read/write_b32) and the compaction queue of deferred shadow rays.
+// Wave-private LDS: the per-ray traversal stack (stack[depth][lane]) and the
+// compaction queue of deferred shadow rays.
 #define RT_QUEUE 128
 struct WaveLds {
+#if !RT_PACKET
   int32_t stack[RT_MAX_STACK][64];
+#endif
 #if RT_SHADOW_QUEUE
   uint32_t q_task[RT_QUEUE];
   float q_t[RT_QUEUE];
@@ -221,61 +432,73 @@ struct WaveLds {
 #endif
 };
 
-__device__ __forceinline__ void kernel_body(const vx_task_t& task, const rt_kernel_arg_t* a,
-                                            WaveLds& w, Counters& cnt) {
+// closest / any hit for lanes with `active` (all 64 lanes call these)
+__device__ __forceinline__ int32_t trace_closest(const Scene& S, const Ray& r, bool tie_high,
+                                                 bool active, float* th, WaveLds& w,
+                                                 Counters& cnt) {
+#if RT_PACKET
+  (void)w; (void)cnt;
+  return ptrace<false>(S, r, 0.0f, INFINITY, -1, tie_high, active, th);
+#else
+  if (!active) return -1;
+  return trace<false>(S, r, 0.0f, INFINITY, -1, tie_high, th, &w.stack[0][lane_id()], cnt);
+#endif
+}
+__device__ __forceinline__ bool occluded(const Scene& S, const Ray& s, int32_t skip, bool tie_high,
+                                         bool active, WaveLds& w, Counters& cnt) {
+  float ts;
+#if RT_PACKET
+  (void)w; (void)cnt;
+  return ptrace<true>(S, s, 0.0f, 1.0f, skip, tie_high, active, &ts) >= 0;
+#else
+  if (!active) return false;
+  return trace<true>(S, s, 0.0f, 1.0f, skip, tie_high, &ts, &w.stack[0][lane_id()], cnt) >= 0;
+#endif
+}
+
+__device__ __forceinline__ void kernel_body(const vx_task_t& task, const Scene& S, WaveLds& w,
+                                            Counters& cnt) {
   const uint32_t t = task.blockIdx.x;
   uint32_t x, y;
-  task_pixel(a, t, &x, &y);
-  if (x >= a->width || y >= a->height) return;
-  int32_t* stack = &w.stack[0][threadIdx.x & 63u];
+  task_pixel(S, t, &x, &y);
+  const bool in = x < S.width && y < S.height;  // edge tiles overhang the image
   Ray r;
-  primary_dir(a, x, y, r);
+  primary_dir(S, x, y, r);
   ray_setup(r);
-  ++cnt.primary;
-  const bool tie_high = (a->flags & RT_FLAG_TIE_HIGH) != 0;
+  cnt.primary += in;
+  const bool tie_high = (S.flags & RT_FLAG_TIE_HIGH) != 0;
   float th = 0.0f;
-  const int32_t hit = trace<false>(a, r, 0.0f, INFINITY, -1, tie_high, &th, stack, cnt);
-  uint32_t color = a->clear_color;
-  bool defer = false;
-  if (hit >= 0) {
-    ++cnt.hits;
-    color = shade_prim(a, hit, x, y, cnt);
-    if (a->flags & RT_FLAG_SHADOWS) {
-#if RT_SHADOW_QUEUE
-      defer = true;
+  const int32_t hit = trace_closest(S, r, tie_high, in, &th, w, cnt);
+  cnt.hits += hit >= 0;
+  // screen layers where no geometry was hit: highest pid first, first
+  // covering triangle wins (one wave-uniform triangle per step)
+  int32_t spid = hit;
+  uint64_t pend = __ballot(in && hit < 0);
+  for (uint32_t k = 0; pend != 0 && k < S.num_layer; ++k) {
+    const uint32_t lo = S.layers + 48u * k;
+#if RT_PACKET
+    const float4 ta = S.A.sld_f4(lo), tb = S.A.sld_f4(lo + 16), tc = S.A.sld_f4(lo + 32);
 #else
-      Ray s;
-      shadow_ray(a, r, th, s);
-      ++cnt.shadow;
-      float ts;
-      if (trace<true>(a, s, 0.0f, 1.0f, hit, tie_high, &ts, stack, cnt) >= 0) {
-        ++cnt.occluded;
-        color = shadowed(color);
-      }
+    const float4 ta = S.A.ld_f4(lo), tb = S.A.ld_f4(lo + 16), tc = S.A.ld_f4(lo + 32);
 #endif
-    }
-  } else if (a->num_layer_tris) {
-    // screen layers: highest pid first, first covering triangle wins
-    const float4* lt4 = vx_ptr<const float4>(a->layers_addr);
-    for (uint32_t k = 0; k < a->num_layer_tris; ++k) {
-      const float4 ta = lt4[3 * k], tb = lt4[3 * k + 1], tc = lt4[3 * k + 2];
+    const bool mine = (pend & (1ull << lane_id())) != 0;
 #ifdef RT_INSTRUMENT
-      ++cnt.layer_tests;
+    cnt.layer_tests += mine;
 #endif
-      float tl;
-      if (mt_hit(r, ta, tb, tc, 0.0f, &tl)) {
-        color = shade_prim(a, __float_as_int(ta.w), x, y, cnt);
-        break;
-      }
-    }
+    float tl;
+    const bool f = mine && mt_hit(r, ta, tb, tc, 0.0f, &tl);
+    if (f) spid = __float_as_int(ta.w);
+    pend &= ~__ballot(f);
   }
+  uint32_t color = shade_wave(S, spid, x, y, S.clear_color, cnt);
+  const bool shadow = hit >= 0 && (S.flags & RT_FLAG_SHADOWS) != 0;
 #if RT_SHADOW_QUEUE
   // wave64 compaction: lanes with a pending shadow ray append it to the
   // wave's LDS queue at ballot/mbcnt-assigned slots
-  const uint64_t m = __ballot(defer);
+  const uint64_t m = __ballot(shadow);
   if (m) {
     const uint32_t base = w.q_count;
-    if (defer) {
+    if (shadow) {
       const uint32_t rank = __builtin_amdgcn_mbcnt_hi(
           (uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
       const uint32_t slot = base + rank;
@@ -285,47 +508,49 @@ __device__ __forceinline__ void kernel_body(const vx_task_t& task, const rt_kern
       w.q_color[slot] = color;
     }
     __builtin_amdgcn_wave_barrier();
-    if (threadIdx.x == (uint32_t)__builtin_amdgcn_readfirstlane(threadIdx.x))
-      w.q_count = base + (uint32_t)__popcll(m);
+    if (lane_id() == 0) w.q_count = base + (uint32_t)__popcll(m);
     __builtin_amdgcn_wave_barrier();
   }
-  if (!defer) store_pixel(a, t, x, y, color);
+  if (in && !shadow) store_pixel(S, t, x, y, color);
 #else
-  (void)defer;
-  store_pixel(a, t, x, y, color);
+  Ray s;
+  shadow_ray(S, r, th, s);
+  cnt.shadow += shadow;
+  if (occluded(S, s, hit, tie_high, shadow, w, cnt)) {
+    ++cnt.occluded;
+    color = shadowed(color);
+  }
+  if (in) store_pixel(S, t, x, y, color);
 #endif
 }
 
 #if RT_SHADOW_QUEUE
 // Called by all 64 lanes after every chunk: trace full waves of 64 shadow
 // rays while the queue holds >= 64 (or whatever is left at the end).
-__device__ __forceinline__ void shadow_drain(bool final, const rt_kernel_arg_t* a, WaveLds& w,
+__device__ __forceinline__ void shadow_drain(bool final, const Scene& S, WaveLds& w,
                                              Counters& cnt) {
-  const uint32_t lane = threadIdx.x & 63u;
+  if (!(S.flags & RT_FLAG_SHADOWS)) return;
+  const uint32_t lane = lane_id();
   uint32_t n = w.q_count;
-  if (!(a->flags & RT_FLAG_SHADOWS)) return;
-  const bool tie_high = (a->flags & RT_FLAG_TIE_HIGH) != 0;
-  int32_t* stack = &w.stack[0][lane];
+  const bool tie_high = (S.flags & RT_FLAG_TIE_HIGH) != 0;
   while (n >= 64 || (final && n > 0)) {
     const uint32_t take = n < 64 ? n : 64;
     const uint32_t base = n - take;
-    if (lane < take) {
-      const uint32_t slot = base + lane;
-      const uint32_t t = w.q_task[slot];
-      uint32_t x, y;
-      task_pixel(a, t, &x, &y);
-      Ray p, s;
-      primary_dir(a, x, y, p);
-      shadow_ray(a, p, w.q_t[slot], s);
-      ++cnt.shadow;
-      uint32_t color = w.q_color[slot];
-      float ts;
-      if (trace<true>(a, s, 0.0f, 1.0f, w.q_pid[slot], tie_high, &ts, stack, cnt) >= 0) {
-        ++cnt.occluded;
-        color = shadowed(color);
-      }
-      store_pixel(a, t, x, y, color);
+    const bool active = lane < take;
+    const uint32_t slot = base + lane;  // < RT_QUEUE for every lane
+    const uint32_t t = w.q_task[slot];
+    uint32_t x, y;
+    task_pixel(S, t, &x, &y);
+    Ray p, s;
+    primary_dir(S, x, y, p);
+    shadow_ray(S, p, w.q_t[slot], s);
+    cnt.shadow += active;
+    uint32_t color = w.q_color[slot];
+    if (occluded(S, s, w.q_pid[slot], tie_high, active, w, cnt)) {
+      ++cnt.occluded;
+      color = shadowed(color);
     }
+    if (active) store_pixel(S, t, x, y, color);
     n = base;
   }
   __builtin_amdgcn_wave_barrier();
@@ -348,19 +573,18 @@ VX_MAIN(rt_kernel_arg_t, arg, RT_BLOCK_THREADS) {
   __shared__ WaveLds s_wave[kWaves];
   WaveLds& w = s_wave[threadIdx.x >> 6];
   Counters cnt;
+  const Scene S = load_scene(arg);
 #if RT_SHADOW_QUEUE
   if ((threadIdx.x & 63u) == 0) w.q_count = 0;
   __builtin_amdgcn_wave_barrier();
   const int rc = vx_spawn_tasks_ex(
       arg->num_tasks,
-      [&](const vx_task_t& task, const rt_kernel_arg_t* a) { kernel_body(task, a, w, cnt); },
-      [&](bool final, const rt_kernel_arg_t* a) { shadow_drain(final, a, w, cnt); },
-      (const rt_kernel_arg_t*)arg);
+      [&](const vx_task_t& task, const Scene* s) { kernel_body(task, *s, w, cnt); },
+      [&](bool final, const Scene* s) { shadow_drain(final, *s, w, cnt); }, &S);
 #else
   const int rc = vx_spawn_tasks(
       arg->num_tasks,
-      [&](const vx_task_t& task, const rt_kernel_arg_t* a) { kernel_body(task, a, w, cnt); },
-      (const rt_kernel_arg_t*)arg);
+      [&](const vx_task_t& task, const Scene* s) { kernel_body(task, *s, w, cnt); }, &S);
 #endif
   flush(RT_STAT_PRIMARY, cnt.primary);
   flush(RT_STAT_SHADOW, cnt.shadow);

@@ -74,6 +74,7 @@ def lib():
             "rt_render_wait": [vp],
             "rt_render": [vp],
             "rt_render_stats": [vp, C.POINTER(Stats)],
+            "rt_render_kernel_ms": [vp, C.POINTER(C.c_double)],
             "rt_read_framebuffer": [vp, vp, u64],
             "rt_scene_setup_prims": [vp, u32, u32, vp, u64],
             "rt_framebuffer_device": [vp, C.POINTER(vp), C.POINTER(u64)],
@@ -180,6 +181,12 @@ class Renderer:
         s = Stats()
         _check(lib().rt_render_stats(self._h, C.byref(s)), "rt_render_stats")
         return s.as_dict()
+
+    def kernel_ms(self) -> float:
+        """HIP-event duration of the last launch (cheap: no counter read-back)."""
+        ms = C.c_double()
+        _check(lib().rt_render_kernel_ms(self._h, C.byref(ms)), "rt_render_kernel_ms")
+        return ms.value
 
     def framebuffer(self) -> np.ndarray:
         p = self.params
