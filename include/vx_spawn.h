@@ -36,7 +36,7 @@
 #include "VX_types.h"
 
 #define VX_SCHED_QUEUES 8
-#define VX_SCHED_STRIDE 16   /* one 64-B line per queue counter */
+#define VX_SCHED_STRIDE 64   /* one 256-B row per queue counter */
 #define VX_CHUNK 64          /* tasks per wave-level dequeue */
 
 /* task scheduling policy of vx_spawn_threads (see the header comment) */
@@ -47,9 +47,16 @@
 #define VX_SPAWN_POLICY VX_POLICY_STATIC
 #endif
 
+/* Perf counters are sharded: a wave adds into shard (global wave id % 64),
+ * each shard on its own 256-B row, and vx_mpm_query sums the shards.  One
+ * counter word per launch would take every wave's atomic on ONE line, which
+ * the memory side serialises (~90 atomics/us per line: thousands of waves x
+ * a few counters = hundreds of us). */
+#define VX_MPM_SHARDS 64
+
 /* per-launch device state, zeroed by the driver before every launch */
 typedef struct {
-  unsigned long long mpm[VX_MPM_COUNT];                 /* perf counters (vx_mpm_query) */
+  unsigned long long mpm[VX_MPM_SHARDS][VX_MPM_COUNT];  /* perf counters (vx_mpm_query) */
   uint32_t sched[VX_SCHED_QUEUES * VX_SCHED_STRIDE];    /* task-queue heads */
 } vx_state_t;
 
@@ -148,10 +155,14 @@ __device__ __forceinline__ uint32_t __vx_wave_sum(uint32_t v) {
   return v;
 }
 
-/* mpm counter add, one atomic per wave (all 64 lanes must call it) */
+/* mpm counter add, one atomic per wave into the wave's shard (all 64 lanes
+ * must call it) */
 __device__ __forceinline__ void vx_mpm_add(int slot, uint32_t v) {
   const uint32_t s = __vx_wave_sum(v);
-  if ((threadIdx.x & 63u) == 0 && s) atomicAdd(&__vx_state.mpm[slot], (unsigned long long)s);
+  const uint32_t shard = (blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)) & (VX_MPM_SHARDS - 1);
+  if ((threadIdx.x & 63u) == 0 && s)
+    __hip_atomic_fetch_add(&__vx_state.mpm[shard][slot], (unsigned long long)s, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
 }
 
 /* Wave-level dequeue of the next 64-task chunk (called by all 64 lanes with

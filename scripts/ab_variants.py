@@ -1,8 +1,13 @@
 #!/usr/bin/env python3
-"""Interleaved A/B timing of kernel-image variants (skybox_rt_amd/lib/variants/*)
-in one process on one GPU (cdna_hip_programming.md section 5.4 rule 24).
-Each variant must render the identical framebuffer (checked against the
-first); prints median / min kernel ms per variant."""
+"""Interleaved A/B timing of kernel-image variants in one process on one GPU
+(cdna_hip_programming.md section 5.4 rule 24).
+
+A variant is `label=dir[:ENV=VAL[:ENV=VAL...]]`, where `dir` is `default`
+(skybox_rt_amd/lib) or a directory name under skybox_rt_amd/lib/variants and
+the ENV settings are applied while that variant's device is opened (e.g.
+VX_HIP_BLOCKS_PER_CU).  A bare name means `name=name`.  Every variant must
+render the identical framebuffer (checked against the first); prints median /
+min kernel ms per variant as one JSON line."""
 import argparse
 import json
 import os
@@ -12,6 +17,15 @@ import numpy as np
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
+
+
+def parse(spec):
+    label, _, rest = spec.partition("=")
+    if not rest:
+        rest = label
+    parts = rest.split(":")
+    env = dict(p.split("=", 1) for p in parts[1:])
+    return label, parts[0], env
 
 
 def main():
@@ -25,28 +39,38 @@ def main():
     args = ap.parse_args()
     import torch  # noqa: F401  (one HIP runtime)
     from skybox_rt_amd import rt
-    vdir = os.path.join(ROOT, "skybox_rt_amd", "lib", "variants")
-    names = args.variants.split(",") if args.variants else sorted(os.listdir(vdir))
+    lib = os.path.join(ROOT, "skybox_rt_amd", "lib")
+    vdir = os.path.join(lib, "variants")
+    specs = args.variants.split(",") if args.variants else sorted(os.listdir(vdir))
     scene = rt.Scene.load(args.scene)
-    rs, ref = {}, None
-    for n in names:
-        r = rt.Renderer(scene, kernel_dir=os.path.join(vdir, n))
+    rs, ref, names = {}, None, []
+    for spec in specs:
+        label, d, env = parse(spec)
+        saved = {k: os.environ.get(k) for k in env}
+        os.environ.update(env)
+        r = rt.Renderer(scene, kernel_dir=lib if d == "default" else os.path.join(vdir, d))
         r.configure(args.size, args.size, shadows=not args.no_shadows)
-        r.render()
+        r.render()  # the driver reads its launch env when it loads the image
+        for k, v in saved.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
         fb = r.framebuffer()
         if ref is None:
             ref = fb
         same = bool(np.array_equal(fb, ref))
-        print(f"{n}: identical={same} stats={r.stats()}", file=sys.stderr)
-        rs[n] = r
+        print(f"{label}: identical={same} stats={r.stats()}", file=sys.stderr)
+        rs[label] = r
+        names.append(label)
     times = {n: [] for n in names}
     for _ in range(args.rounds):
         for n in names:
             r = rs[n]
             for _ in range(args.frames):
                 r.render()
-                times[n].append(r.stats()["kernel_ms"])
-    out = {n: {"median_ms": float(np.median(t)), "min_ms": float(np.min(t)),
+                times[n].append(r.kernel_ms())
+    out = {n: {"median_ms": round(float(np.median(t)), 5), "min_ms": round(float(np.min(t)), 5),
                "grid": rs[n].stats()["grid"]} for n, t in times.items()}
     print(json.dumps(out))
 

@@ -9,30 +9,20 @@
 // with one task per pixel (64 consecutive tasks = one wave = an 8x8 pixel
 // block, 16 waves = one 32x32 raster tile, the reference's tile unit).
 //
-// Two traversal forms, identical results (tests/test_gpu_rt.py):
-//  * wave packet (default image): the 64 rays of a wave walk the BVH
-//    together.  Node and triangle records are wave-uniform, so they come in
-//    through the scalar cache (s_load into SGPRs, one instruction per record
-//    per wave), each lane tests its own ray, ballots decide where the packet
-//    goes, and the traversal stack is wave-uniform: entry i lives in lane i
-//    of three VGPRs (readlane / writelane, no memory traffic).  Every lane
-//    keeps its own closest (t, pid) and culls with it, so the hit found is
-//    exactly the per-ray one: boxes are conservative and the closest-hit
-//    order is total (t, then pid by the tie rule).
-//  * per ray (RT_PACKET=0, and the RT_INSTRUMENT counting image): each lane
-//    walks alone with its stack in LDS, stack[depth][lane], conflict-free.
-//    Its node-visit / triangle-test counts are the per-ray traversal work the
-//    oracle (oracle/rt.c bvh_trace) restates, the basis of the algorithmic
-//    byte count of SURVEY.md 8(d).
+// Traversal: each lane walks the BVH alone (near child first) with its
+// stack in LDS, stack[depth][lane] (conflict-free, no VGPR cost); a leaf's
+// triangles come in as one batch of 16-B loads.  The node-visit /
+// triangle-test counts of the RT_INSTRUMENT image are exactly the per-ray
+// traversal work the oracle (oracle/rt.c bvh_trace) restates, the basis of
+// the algorithmic byte count of SURVEY.md 8(d).  (A wave-packet form --
+// scalar-cache node loads, ballot-steered shared stack -- measured 20-25 %
+// slower on tekkaman and was dropped.)
 //
-// Scene reads are buffer / scalar loads through one arena descriptor
+// Scene reads are buffer loads through one arena descriptor
 // (vx_arena): 32-bit offsets, no FLAT loads.  Numerics are bit-identical to
 // the oracle (oracle/rt.c): every fused multiply-add is an explicit fmaf,
 // everything else is compiled with -ffp-contract=off, divisions are IEEE.
 //
-// The packet code needs all 64 lanes of a wave present (it never returns
-// early per lane): vx_spawn hands out whole 64-task chunks and the RT app's
-// task count is a multiple of 1024.
 #include <hip/hip_runtime.h>
 
 #include "gfx_device.h"
@@ -41,18 +31,6 @@
 
 #ifndef RT_SHADOW_QUEUE
 #define RT_SHADOW_QUEUE 1
-#endif
-#ifndef RT_PACKET
-#ifdef RT_INSTRUMENT
-#define RT_PACKET 0
-#else
-#define RT_PACKET 1
-#endif
-#endif
-// distinct primitives per wave shaded from SGPR records before the rest of
-// the wave falls back to per-lane (vector) record loads
-#ifndef RT_SHADE_UNIFORM
-#define RT_SHADE_UNIFORM 2
 #endif
 
 namespace {
@@ -172,106 +150,6 @@ __device__ __forceinline__ bool closer(float t, int32_t pid, float bt, int32_t b
   return (t < bt) || (t == bt && (tie_high ? pid > bpid : pid < bpid));
 }
 
-#if RT_PACKET
-// v[lane] = val, for wave-uniform val and lane (v_writelane ignores EXEC)
-template <typename T>
-__device__ __forceinline__ void writelane(T& v, T val, int lane) {
-  asm volatile("v_writelane_b32 %0, %1, m0" : "+v"(v) : "s"(val), "{m0}"(lane));
-}
-
-// Wave-packet traversal: closest hit (ANY = false) or any hit excluding
-// `skip` (ANY = true) for every lane with `active`; all 64 lanes call it.
-template <bool ANY>
-__device__ __forceinline__ int32_t ptrace(const Scene& S, const Ray& r, float tmin, float tmax,
-                                          int32_t skip, bool tie_high, bool active,
-                                          float* t_out) {
-  const uint64_t bit = 1ull << lane_id();
-  uint64_t M = __ballot(active);
-  float bt = tmax;
-  int32_t bpid = -1;
-  if (S.num_nodes == 0 || M == 0) return -1;
-  int32_t st_ref = 0;             // stack entry i = lane i
-  uint32_t st_lo = 0, st_hi = 0;  // lanes that entered the pushed child's box
-  int sp = 0;
-  int32_t ref = 0;
-  uint64_t done = 0;  // ANY: lanes already occluded
-  for (;;) {
-    const bool mine = (M & bit) != 0;
-    if (ref >= 0) {
-      const uint32_t no = S.nodes + 64u * (uint32_t)ref;
-      const float4 n0 = S.A.sld_f4(no), n1 = S.A.sld_f4(no + 16);
-      const float4 n2 = S.A.sld_f4(no + 32), n3 = S.A.sld_f4(no + 48);
-      const int32_t c0 = __float_as_int(n3.x), c1 = __float_as_int(n3.y);
-      const float lim = ANY ? tmax : bt;
-      float tn0 = 0.0f, tn1 = 0.0f;
-      const bool h0 = mine && c0 != RT_EMPTY_REF &&
-                      slab(n0.x, n0.y, n1.x, n1.y, n2.x, n2.y, r, tmin, lim, &tn0);
-      const bool h1 = mine && c1 != RT_EMPTY_REF &&
-                      slab(n0.z, n0.w, n1.z, n1.w, n2.z, n2.w, r, tmin, lim, &tn1);
-      const uint64_t m0 = __ballot(h0), m1 = __ballot(h1);
-      if (m0 && m1) {
-        // near child first, by majority of the lanes entering both
-        const uint64_t w1 = __ballot(h0 && h1 && tn1 < tn0);
-        const uint64_t w0 = __ballot(h0 && h1 && !(tn1 < tn0));
-        const bool first1 = __popcll(w1) > __popcll(w0);
-        const int32_t far_ref = first1 ? c0 : c1;
-        const uint64_t far_m = first1 ? m0 : m1;
-        if (sp < 64) {
-          writelane(st_ref, far_ref, sp);
-          writelane(st_lo, (uint32_t)far_m, sp);
-          writelane(st_hi, (uint32_t)(far_m >> 32), sp);
-          ++sp;
-        }
-        ref = first1 ? c1 : c0;
-        M = first1 ? m1 : m0;
-        continue;
-      }
-      if (m0) { ref = c0; M = m0; continue; }
-      if (m1) { ref = c1; M = m1; continue; }
-    } else {
-      const uint32_t lr = (uint32_t)ref;
-      const uint32_t first = (lr >> 4) & 0x07ffffffu, count = (lr & 15u) + 1u;
-      const uint32_t to = S.tris + 48u * first;
-      bool found = false;
-#pragma unroll
-      for (uint32_t k = 0; k < 4; ++k) {
-        if (k < count) {
-          const float4 ta = S.A.sld_f4(to + 48u * k);
-          const float4 tb = S.A.sld_f4(to + 48u * k + 16);
-          const float4 tc = S.A.sld_f4(to + 48u * k + 32);
-          const int32_t pid = __float_as_int(ta.w);
-          float t;
-          if (mine && !found && pid != skip && mt_hit(r, ta, tb, tc, tmin, &t)) {
-            if (ANY) {
-              if (t < tmax) { found = true; bt = t; bpid = pid; }
-            } else if (closer(t, pid, bt, bpid, tie_high)) {
-              bt = t;
-              bpid = pid;
-            }
-          }
-        }
-      }
-      if (ANY) {
-        done |= __ballot(found);
-        M &= ~done;
-        if ((__ballot(active) & ~done) == 0) break;
-      }
-    }
-    // pop the next subtree some lane still needs
-    bool empty = true;
-    while (sp > 0) {
-      --sp;
-      ref = __builtin_amdgcn_readlane(st_ref, sp);
-      M = (((uint64_t)__builtin_amdgcn_readlane(st_hi, sp) << 32) |
-           (uint64_t)__builtin_amdgcn_readlane(st_lo, sp)) & ~done;
-      if (M) { empty = false; break; }
-    }
-    if (empty) break;
-  }
-  if (bpid >= 0) *t_out = bt;
-  return bpid;
-}
-#else
 // Per-ray traversal with the LDS stack (oracle/rt.c bvh_trace restates it
 // exactly, counters included).  A leaf's (up to 4) triangles are fetched in
 // one batch -- the tris array carries 3 padding records.
@@ -342,7 +220,6 @@ __device__ __forceinline__ int32_t trace(const Scene& S, const Ray& r, float tmi
   if (bpid >= 0) *t_out = bt;
   return bpid;
 }
-#endif
 
 // shade primitive `pid` at (x, y) from per-lane (vector) record loads
 __device__ __forceinline__ uint32_t shade_lane(const Scene& S, int32_t pid, uint32_t x,
@@ -362,22 +239,7 @@ __device__ __forceinline__ uint32_t shade_lane(const Scene& S, int32_t pid, uint
 // whatever is left from per-lane record loads.
 __device__ __forceinline__ uint32_t shade_wave(const Scene& S, int32_t spid, uint32_t x,
                                                uint32_t y, uint32_t color, Counters& cnt) {
-#if RT_PACKET
-  uint64_t need = __ballot(spid >= 0);
-#pragma unroll 1
-  for (int it = 0; need != 0 && it < RT_SHADE_UNIFORM; ++it) {
-    const int32_t u = __builtin_amdgcn_readlane(spid, (int)__builtin_ctzll(need));
-    gfx::Prim p;
-    gfx::load_prim<true>(S.A, S.prims + 128u * (uint32_t)u, p);
-    const gfx::DcState s = gfx::load_dcstate<true>(S.A, S.dcs + 64u * p.dc());
-    if (spid == u) color = gfx::shade(S.A, p, s, x, y);
-    need &= ~__ballot(spid == u);
-  }
-  if (need != 0 && (need & (1ull << lane_id())) != 0) color = shade_lane(S, spid, x, y, cnt);
-  return color;
-#else
   return spid >= 0 ? shade_lane(S, spid, x, y, cnt) : color;
-#endif
 }
 
 // task -> (shard-local 32x32 tile, 8x8 block, lane) -> pixel
@@ -420,9 +282,7 @@ __device__ __forceinline__ void store_pixel(const Scene& S, uint32_t t, uint32_t
 // compaction queue of deferred shadow rays.
 #define RT_QUEUE 128
 struct WaveLds {
-#if !RT_PACKET
   int32_t stack[RT_MAX_STACK][64];
-#endif
 #if RT_SHADOW_QUEUE
   uint32_t q_task[RT_QUEUE];
   float q_t[RT_QUEUE];
@@ -436,24 +296,14 @@ struct WaveLds {
 __device__ __forceinline__ int32_t trace_closest(const Scene& S, const Ray& r, bool tie_high,
                                                  bool active, float* th, WaveLds& w,
                                                  Counters& cnt) {
-#if RT_PACKET
-  (void)w; (void)cnt;
-  return ptrace<false>(S, r, 0.0f, INFINITY, -1, tie_high, active, th);
-#else
   if (!active) return -1;
   return trace<false>(S, r, 0.0f, INFINITY, -1, tie_high, th, &w.stack[0][lane_id()], cnt);
-#endif
 }
 __device__ __forceinline__ bool occluded(const Scene& S, const Ray& s, int32_t skip, bool tie_high,
                                          bool active, WaveLds& w, Counters& cnt) {
   float ts;
-#if RT_PACKET
-  (void)w; (void)cnt;
-  return ptrace<true>(S, s, 0.0f, 1.0f, skip, tie_high, active, &ts) >= 0;
-#else
   if (!active) return false;
   return trace<true>(S, s, 0.0f, 1.0f, skip, tie_high, &ts, &w.stack[0][lane_id()], cnt) >= 0;
-#endif
 }
 
 __device__ __forceinline__ void kernel_body(const vx_task_t& task, const Scene& S, WaveLds& w,
@@ -476,11 +326,7 @@ __device__ __forceinline__ void kernel_body(const vx_task_t& task, const Scene& 
   uint64_t pend = __ballot(in && hit < 0);
   for (uint32_t k = 0; pend != 0 && k < S.num_layer; ++k) {
     const uint32_t lo = S.layers + 48u * k;
-#if RT_PACKET
-    const float4 ta = S.A.sld_f4(lo), tb = S.A.sld_f4(lo + 16), tc = S.A.sld_f4(lo + 32);
-#else
     const float4 ta = S.A.ld_f4(lo), tb = S.A.ld_f4(lo + 16), tc = S.A.ld_f4(lo + 32);
-#endif
     const bool mine = (pend & (1ull << lane_id())) != 0;
 #ifdef RT_INSTRUMENT
     cnt.layer_tests += mine;

@@ -47,6 +47,10 @@ namespace {
 
 constexpr uint64_t kBlockSize = 256;      // allocation granule (>= 64 B DCR blocks)
 constexpr uint64_t kDefaultArenaMB = 4096;
+// __vx_state layout (include/vx_spawn.h): mpm[kMpmShards][VX_MPM_COUNT] u64,
+// then the scheduler queue heads
+constexpr uint32_t kMpmShards = 64;
+constexpr int kGridBlocksPerCU = 16;
 
 uint64_t env_u64(const char* name, uint64_t dflt) {
   const char* s = std::getenv(name);
@@ -149,6 +153,7 @@ class vx_device {
   int mem_free(uint64_t addr) {
     acl_.erase(addr);
     shadow_.erase(addr);
+    image_key_.erase(addr);
     return alloc_.release(addr);
   }
   int mem_access(uint64_t addr, uint64_t size, int flags) {
@@ -172,8 +177,10 @@ class vx_device {
     HIP_CHECK(hipStreamSynchronize(stream_));
     for (auto& kv : shadow_) {  // keep kernel-image shadows coherent
       const uint64_t a = kv.first, e = a + kv.second.size();
-      if (addr >= a && addr + size <= e)
+      if (addr >= a && addr + size <= e) {
         std::memcpy(kv.second.data() + (addr - a), src, size);
+        image_key_.erase(a);
+      }
     }
     return 0;
   }
@@ -263,10 +270,14 @@ class vx_device {
       return 0;
     }
     wait_idle();
-    if (mpm_dirty_) {
-      HIP_CHECK(hipMemcpyAsync(mpm_, last_module_->mpm, sizeof(mpm_), hipMemcpyDeviceToHost,
-                               stream_));
+    if (mpm_dirty_) {  // sum the counter shards (vx_spawn.h VX_MPM_SHARDS)
+      HIP_CHECK(hipMemcpyAsync(mpm_shards_, last_module_->mpm, sizeof(mpm_shards_),
+                               hipMemcpyDeviceToHost, stream_));
       HIP_CHECK(hipStreamSynchronize(stream_));
+      for (uint32_t i = 0; i < VX_MPM_COUNT; ++i) {
+        mpm_[i] = 0;
+        for (uint32_t sh = 0; sh < kMpmShards; ++sh) mpm_[i] += mpm_shards_[sh][i];
+      }
       mpm_dirty_ = false;
     }
     *value = mpm_[off];
@@ -297,13 +308,19 @@ class vx_device {
                   (unsigned long long)krnl_addr);
       return -1;
     }
-    const std::vector<uint8_t>& img = it->second;
-    const uint64_t key = fnv1a(img.data(), img.size()) ^ krnl_addr;
+    // the image is hashed only after an upload touched it (not per launch)
+    auto hit = image_key_.find(krnl_addr);
+    if (hit == image_key_.end()) {
+      const std::vector<uint8_t>& img = it->second;
+      hit = image_key_.emplace(krnl_addr, fnv1a(img.data(), img.size()) ^ krnl_addr).first;
+    }
+    const uint64_t key = hit->second;
     auto mit = modules_.find(key);
     if (mit != modules_.end()) {
       *out = &mit->second;
       return 0;
     }
+    const std::vector<uint8_t>& img = it->second;
     Module m;
     HIP_CHECK(hipModuleLoadData(&m.module, img.data()));
     HIP_CHECK(hipModuleGetFunction(&m.entry, m.module, "vx_main"));
@@ -314,8 +331,11 @@ class vx_device {
     int max_threads = 0;
     HIP_CHECK(hipFuncGetAttribute(&max_threads, HIP_FUNC_ATTRIBUTE_MAX_THREADS_PER_BLOCK, m.entry));
     m.block = (uint32_t)(max_threads > 0 ? max_threads : 256);
-    int per_cu = 0;
-    HIP_CHECK(hipModuleOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, m.entry, (int)m.block, 0));
+    // Grid = kGridBlocksPerCU blocks per CU, several times what is resident:
+    // vx_spawn deals 64-task chunks to waves by global wave id, so the blocks
+    // waiting for a slot are the load balancer (the hardware dispatcher hands
+    // a CU its next block when one retires, as simx's cores pull warps).
+    int per_cu = kGridBlocksPerCU;
     if (const char* s = std::getenv("VX_HIP_BLOCKS_PER_CU")) per_cu = std::atoi(s);
     if (per_cu < 1) per_cu = 1;
     m.grid = (uint32_t)(props_.multiProcessorCount * per_cu);
@@ -332,6 +352,7 @@ class vx_device {
   std::map<uint64_t, int> acl_;
   std::map<uint64_t, std::vector<uint8_t>> shadow_;
   std::map<uint64_t, Module> modules_;
+  std::map<uint64_t, uint64_t> image_key_;  // image address -> module key
   hipStream_t stream_ = nullptr;
   hipEvent_t ev_start_ = nullptr, ev_stop_ = nullptr;
   bool running_ = false;
@@ -342,6 +363,7 @@ class vx_device {
   uint32_t dcrs_[VX_DCR_MIRROR_SIZE] = {};
   bool dcr_valid_[VX_DCR_MIRROR_SIZE] = {};
   unsigned long long mpm_[VX_MPM_COUNT] = {};
+  unsigned long long mpm_shards_[kMpmShards][VX_MPM_COUNT] = {};
 };
 
 struct vx_buffer {
