@@ -45,6 +45,25 @@ def algorithmic_bytes(st: dict, pixels: int) -> int:
             + st["texel_bytes"] + PIXEL_BYTES * pixels)
 
 
+def pmc_traffic(side: int, shadows: bool):
+    """HBM bytes per launch from the committed rocprofv3 PMC summary
+    (scripts/pmc_traffic.sh -> profiles/pmc_traffic.json), used only when it
+    was taken on this same kernel image and workload; else None."""
+    import hashlib
+    path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    co = os.path.join(ROOT, "skybox_rt_amd", "lib", "rt_kernel.co")
+    try:
+        with open(path) as fh:
+            t = json.load(fh)
+        md5 = hashlib.md5(open(co, "rb").read()).hexdigest()
+    except (OSError, ValueError):
+        return None
+    if (t.get("kernel_md5") != md5 or t.get("width") != side or t.get("height") != side
+            or t.get("shadows") != shadows):
+        return None
+    return int(t["traffic_bytes"])
+
+
 def frame_side(n_gpus: int, base: int) -> int:
     return max(32, int(round(base * math.sqrt(n_gpus) / 32.0)) * 32)
 
@@ -208,7 +227,7 @@ def main():
         },
         "roofline": {
             "bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-            "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
+            "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": pmc_traffic(side, shadows),
             "algorithmic_bytes_per_launch": int(alg_bytes),
             "counts": {k: int(inst[k]) for k in ("node_visits", "tri_tests", "layer_tests",
                                                  "texel_bytes", "primary_rays", "shadow_rays")},

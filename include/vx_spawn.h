@@ -20,11 +20,16 @@
  *    reference runs main() per core and wspawns warps.
  *  - Scheduling: tasks are handed out in chunks of 64 consecutive ids, one
  *    chunk per wave (one task per lane: coalesced, and an 8x8 pixel block in
- *    the RT app), dynamically: chunk c belongs to queue c % 8, a wave starts
- *    on the queue of its XCD (HW_REG_XCC_ID) and moves on when it runs dry.
- *    The reference deals static per-core ranges (vx_spawn.c:247-316).  Every
- *    task still runs exactly once with blockIdx = the vx_spawn.c:75-80
- *    decomposition; the queues are zeroed by the driver before each launch.
+ *    the RT app); wave w of the grid takes chunks w, w + W, w + 2W, ...  The
+ *    driver launches several times more blocks than are resident, so the
+ *    hardware dispatcher, which hands a CU a new block whenever one retires,
+ *    is the load balancer (the reference deals static per-core ranges,
+ *    vx_spawn.c:247-316).  Atomic work queues (per-XCD heads) measured 2x
+ *    slower than this on the RT kernel and were dropped.  Every task runs
+ *    exactly once with blockIdx = the vx_spawn.c:75-80 decomposition.
+ *  - Perf counters (vx_mpm_add): LDS counters per block, written as one
+ *    64-B row per block at block exit (plain stores, no global atomics, no
+ *    per-launch memset); vx_mpm_query sums the rows of the last launch.
  *  - group_size > 1 (vx_spawn.c:187-246) is not supported yet: returns -1.
  */
 #ifndef VX_SPAWN_H
@@ -35,29 +40,15 @@
 
 #include "VX_types.h"
 
-#define VX_SCHED_QUEUES 8
-#define VX_SCHED_STRIDE 64   /* one 256-B row per queue counter */
-#define VX_CHUNK 64          /* tasks per wave-level dequeue */
+#define VX_CHUNK 64          /* tasks per wave */
+#define VX_MAX_GRID 16384    /* blocks per launch (rows of the counter slab) */
 
-/* task scheduling policy of vx_spawn_threads (see the header comment) */
-#define VX_POLICY_STATIC 0   /* wave w takes chunks w, w + W, w + 2W, ... */
-#define VX_POLICY_QUEUES 1   /* 8 XCD-affine dynamic queues */
-#define VX_POLICY_HYBRID 2   /* per-block contiguous strip + global pool */
-#ifndef VX_SPAWN_POLICY
-#define VX_SPAWN_POLICY VX_POLICY_STATIC
-#endif
-
-/* Perf counters are sharded: a wave adds into shard (global wave id % 64),
- * each shard on its own 256-B row, and vx_mpm_query sums the shards.  One
- * counter word per launch would take every wave's atomic on ONE line, which
- * the memory side serialises (~90 atomics/us per line: thousands of waves x
- * a few counters = hundreds of us). */
-#define VX_MPM_SHARDS 64
-
-/* per-launch device state, zeroed by the driver before every launch */
+/* per-launch device state: one 64-B row of the first VX_MPM_ROW u32 mpm
+ * counters per block, each written by its block at exit (kernel programs
+ * count into slots < VX_MPM_ROW; vx_mpm_query reads the others as 0) */
+#define VX_MPM_ROW 16
 typedef struct {
-  unsigned long long mpm[VX_MPM_SHARDS][VX_MPM_COUNT];  /* perf counters (vx_mpm_query) */
-  uint32_t sched[VX_SCHED_QUEUES * VX_SCHED_STRIDE];    /* task-queue heads */
+  uint32_t mpm[VX_MAX_GRID][VX_MPM_ROW];
 } vx_state_t;
 
 /* Filled by the driver before every launch (hip_driver.cpp, start()). */
@@ -66,6 +57,8 @@ __constant__ uint32_t __vx_dcrs[VX_DCR_MIRROR_SIZE];     /* DCR mirror */
 __constant__ uint64_t __vx_mem_base;                     /* arena base VA */
 __device__ vx_state_t __vx_state;
 }
+/* this block's counters (zeroed / written back by VX_MAIN) */
+__shared__ uint32_t __vx_mpm_lds[VX_MPM_ROW];
 
 #define VX_MPM_TASKS 2  /* mpm slot for VX_CSR_MINSTRET (tasks run) */
 
@@ -146,7 +139,7 @@ __device__ __forceinline__ uint32_t vx_num_threads() { return 64u; }
 __device__ __forceinline__ uint32_t vx_xcc_id() {
   uint32_t x;
   asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(x));
-  return x & (VX_SCHED_QUEUES - 1);
+  return x & 7u;
 }
 
 __device__ __forceinline__ uint32_t __vx_wave_sum(uint32_t v) {
@@ -155,36 +148,11 @@ __device__ __forceinline__ uint32_t __vx_wave_sum(uint32_t v) {
   return v;
 }
 
-/* mpm counter add, one atomic per wave into the wave's shard (all 64 lanes
- * must call it) */
+/* mpm counter add: wave sum, then one LDS atomic per wave into the block's
+ * row (all 64 lanes must call it) */
 __device__ __forceinline__ void vx_mpm_add(int slot, uint32_t v) {
   const uint32_t s = __vx_wave_sum(v);
-  const uint32_t shard = (blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)) & (VX_MPM_SHARDS - 1);
-  if ((threadIdx.x & 63u) == 0 && s)
-    __hip_atomic_fetch_add(&__vx_state.mpm[shard][slot], (unsigned long long)s, __ATOMIC_RELAXED,
-                           __HIP_MEMORY_SCOPE_AGENT);
-}
-
-/* Wave-level dequeue of the next 64-task chunk (called by all 64 lanes with
- * wave-uniform q/tried); returns the chunk index or UINT32_MAX when every
- * queue is exhausted (the loop's exit condition, reached by every wave). */
-__device__ __forceinline__ uint32_t __vx_next_chunk(uint32_t nchunks, uint32_t& q, uint32_t& tried) {
-  while (tried < VX_SCHED_QUEUES) {
-    uint32_t c = 0xffffffffu;
-    if ((threadIdx.x & 63u) == 0) {
-      uint32_t* ctr = &__vx_state.sched[q * VX_SCHED_STRIDE];
-      const uint32_t cur = __hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      if (cur * VX_SCHED_QUEUES + q < nchunks) {
-        const uint32_t ch = atomicAdd(ctr, 1u) * VX_SCHED_QUEUES + q;
-        if (ch < nchunks) c = ch;
-      }
-    }
-    c = __shfl(c, 0, 64);
-    if (c != 0xffffffffu) return c;
-    q = (q + 1) & (VX_SCHED_QUEUES - 1);
-    ++tried;
-  }
-  return 0xffffffffu;
+  if ((threadIdx.x & 63u) == 0 && s && slot < VX_MPM_ROW) atomicAdd(&__vx_mpm_lds[slot], s);
 }
 
 struct __vx_no_epilogue {
@@ -212,42 +180,12 @@ __device__ __forceinline__ int vx_spawn_threads_ex(uint32_t dimension, const uin
   }
   if (group_size != 1) return -1;
   const uint32_t nchunks = (num_groups + VX_CHUNK - 1) / VX_CHUNK;
-  uint32_t q = vx_xcc_id(), tried = 0, ran = 0;
+  const uint32_t nwaves = gridDim.x * (blockDim.x >> 6);
+  uint32_t ran = 0;
   vx_task_t task;
   task.threadIdx.x = task.threadIdx.y = task.threadIdx.z = 0;
-#if VX_SPAWN_POLICY == VX_POLICY_STATIC
-  const uint32_t nwaves = gridDim.x * (blockDim.x >> 6);
-  uint32_t c = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
-  (void)q; (void)tried;
-  for (; c < nchunks; c += nwaves) {
-#elif VX_SPAWN_POLICY == VX_POLICY_HYBRID
-  // block b owns a contiguous strip of R chunks (locality: the block's waves
-  // walk neighbouring pixels through one L1); what is left over is a global
-  // pool the early finishers drain (balance)
-  __shared__ uint32_t __vx_block_head;
-  const uint32_t R = (nchunks * 3u / 4u) / gridDim.x;
-  if (threadIdx.x == 0) __vx_block_head = 0;
-  __syncthreads();
-  (void)q;
-  (void)tried;
-  for (;;) {
-    uint32_t c = 0xffffffffu;
-    if ((threadIdx.x & 63u) == 0) {
-      const uint32_t i = atomicAdd(&__vx_block_head, 1u);  // LDS atomic
-      if (i < R) {
-        c = blockIdx.x * R + i;
-      } else {
-        const uint32_t p = gridDim.x * R + atomicAdd(&__vx_state.sched[0], 1u);
-        if (p < nchunks) c = p;
-      }
-    }
-    c = __shfl(c, 0, 64);
-    if (c == 0xffffffffu) break;
-#else
-  for (;;) {
-    const uint32_t c = __vx_next_chunk(nchunks, q, tried);
-    if (c == 0xffffffffu) break;
-#endif
+  for (uint32_t c = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6); c < nchunks;
+       c += nwaves) {
     const uint32_t t = c * VX_CHUNK + (threadIdx.x & 63u);
     if (t < num_groups) {
       task.task_id = t;
@@ -293,9 +231,14 @@ __device__ __forceinline__ int vx_spawn_tasks_ex(uint32_t num_tasks, F kernel_fu
 #define VX_MAIN_BOUNDS(ArgT, argname, bounds)                                        \
   static __device__ __forceinline__ int __vx_main_body(ArgT* argname);               \
   extern "C" __global__ void bounds vx_main() {                                      \
+    if (threadIdx.x < VX_MPM_ROW) __vx_mpm_lds[threadIdx.x] = 0;                     \
+    __syncthreads();                                                                 \
     const uint64_t a = ((uint64_t)__vx_dcrs[VX_DCR_BASE_STARTUP_ARG1] << 32) |       \
                        (uint64_t)__vx_dcrs[VX_DCR_BASE_STARTUP_ARG0];                \
     (void)__vx_main_body(vx_ptr<ArgT>(a));                                           \
+    __syncthreads();                                                                 \
+    if (threadIdx.x < VX_MPM_ROW && blockIdx.x < VX_MAX_GRID)                        \
+      __vx_state.mpm[blockIdx.x][threadIdx.x] = __vx_mpm_lds[threadIdx.x];           \
   }                                                                                  \
   static __device__ __forceinline__ int __vx_main_body(ArgT* argname)
 

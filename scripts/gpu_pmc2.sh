@@ -1,0 +1,23 @@
+# PMC passes (one rocprofv3 --pmc pass per counter group) over prof_rt.py,
+# plus the host-overhead breakdown.  TAG names the output directory.
+set -o pipefail
+cd "$GRAFT_REPO_ROOT"
+export TMPDIR=/tmp
+TAG=${TAG:-pmc}; mkdir -p gpurun_out/$TAG
+timeout -k 10 120 python scripts/host_overhead.py > gpurun_out/$TAG/host.json 2> gpurun_out/$TAG/host.err || exit $?
+cat gpurun_out/$TAG/host.json
+run() {  # name, counters...
+  local name=$1; shift
+  timeout -k 10 180 rocprofv3 --pmc "$@" -d gpurun_out/$TAG/$name -o run --output-format csv -- python3 scripts/prof_rt.py --frames 10 > gpurun_out/$TAG/$name.log 2>&1
+  local rc=$?
+  echo "pass $name rc=$rc"
+  case $rc in 124|134|137|139) exit $rc;; esac
+  return 0
+}
+run p1 SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY GRBM_GUI_ACTIVE
+run p2 SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_VMEM_RD SQ_INSTS_LDS SQ_INSTS_SMEM SQ_INSTS_VMEM_WR
+run p3 SQ_ACTIVE_INST_VALU SQ_THREAD_CYCLES_VALU SQ_ACTIVE_INST_LDS SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT
+run p4 TCP_TOTAL_CACHE_ACCESSES_sum TCP_TCC_READ_REQ_sum TCC_HIT_sum TCC_MISS_sum
+run p5 FETCH_SIZE
+run p6 WRITE_SIZE
+run p7 TA_BUSY_avr TA_TA_BUSY_sum TD_TD_BUSY_sum SQ_INSTS_FLAT

@@ -32,6 +32,16 @@
 #ifndef RT_SHADOW_QUEUE
 #define RT_SHADOW_QUEUE 1
 #endif
+// 1: wave-uniform node / leaf records through the scalar cache (trace());
+// measured 3-4 % slower than per-lane loads on tekkaman, so off by default
+#ifndef RT_SCALAR
+#define RT_SCALAR 0
+#endif
+// distinct primitives per wave shaded from SGPR records (shade_wave());
+// measured neutral, off by default
+#ifndef RT_SHADE_UNIFORM
+#define RT_SHADE_UNIFORM 0
+#endif
 
 namespace {
 
@@ -151,8 +161,32 @@ __device__ __forceinline__ bool closer(float t, int32_t pid, float bt, int32_t b
 }
 
 // Per-ray traversal with the LDS stack (oracle/rt.c bvh_trace restates it
-// exactly, counters included).  A leaf's (up to 4) triangles are fetched in
-// one batch -- the tris array carries 3 padding records.
+// exactly, counters included).  Each step first checks whether every active
+// lane is at the same node / leaf -- the common case for the coherent rays of
+// an 8x8 pixel wave -- and then reads the record ONCE for the wave through
+// the scalar cache into SGPRs (s_load) instead of 64 lanes x 16 B of
+// vector-memory data return per load (the L1 -> VGPR return path, 64 B/clk
+// per CU, was the busiest unit of the all-vector form).  Divergent steps use
+// per-lane buffer loads.  Both forms compute identical values.
+struct NodeStep {
+  int32_t c0, c1;
+  float tn0, tn1;
+  bool h0, h1;
+};
+
+__device__ __forceinline__ NodeStep node_step(const float4& n0, const float4& n1, const float4& n2,
+                                              const float4& n3, const Ray& r, float tmin,
+                                              float lim) {
+  NodeStep o;
+  o.c0 = __float_as_int(n3.x);
+  o.c1 = __float_as_int(n3.y);
+  o.tn0 = 0.0f;
+  o.tn1 = 0.0f;
+  o.h0 = (o.c0 != RT_EMPTY_REF) && slab(n0.x, n0.y, n1.x, n1.y, n2.x, n2.y, r, tmin, lim, &o.tn0);
+  o.h1 = (o.c1 != RT_EMPTY_REF) && slab(n0.z, n0.w, n1.z, n1.w, n2.z, n2.w, r, tmin, lim, &o.tn1);
+  return o;
+}
+
 template <bool ANY>
 __device__ __forceinline__ int32_t trace(const Scene& S, const Ray& r, float tmin, float tmax,
                                          int32_t skip, bool tie_high, float* t_out,
@@ -163,52 +197,86 @@ __device__ __forceinline__ int32_t trace(const Scene& S, const Ray& r, float tmi
   float bt = tmax;
   int32_t bpid = -1;
   for (;;) {
+    const int32_t r0 = __builtin_amdgcn_readfirstlane(ref);
+    const bool uni = RT_SCALAR && __ballot(ref != r0) == 0;  // wave-uniform branch
     if (ref >= 0) {
-      const uint32_t no = S.nodes + 64u * (uint32_t)ref;
-      const float4 n0 = S.A.ld_f4(no), n1 = S.A.ld_f4(no + 16);
-      const float4 n2 = S.A.ld_f4(no + 32), n3 = S.A.ld_f4(no + 48);
 #ifdef RT_INSTRUMENT
       ++cnt.visits;
 #endif
-      const int32_t c0 = __float_as_int(n3.x), c1 = __float_as_int(n3.y);
       const float lim = ANY ? tmax : bt;
-      float tn0 = 0.0f, tn1 = 0.0f;
-      const bool h0 = (c0 != RT_EMPTY_REF) && slab(n0.x, n0.y, n1.x, n1.y, n2.x, n2.y, r, tmin, lim, &tn0);
-      const bool h1 = (c1 != RT_EMPTY_REF) && slab(n0.z, n0.w, n1.z, n1.w, n2.z, n2.w, r, tmin, lim, &tn1);
-      if (h0 && h1) {
-        const bool swap = tn1 < tn0;
-        const int32_t near_ref = swap ? c1 : c0, far_ref = swap ? c0 : c1;
+      NodeStep st;
+      if (uni) {
+        const uint32_t no = S.nodes + 64u * (uint32_t)r0;
+        st = node_step(S.A.sld_f4(no), S.A.sld_f4(no + 16), S.A.sld_f4(no + 32),
+                       S.A.sld_f4(no + 48), r, tmin, lim);
+      } else {
+        const uint32_t no = S.nodes + 64u * (uint32_t)ref;
+        st = node_step(S.A.ld_f4(no), S.A.ld_f4(no + 16), S.A.ld_f4(no + 32),
+                       S.A.ld_f4(no + 48), r, tmin, lim);
+      }
+      if (st.h0 && st.h1) {
+        const bool swap = st.tn1 < st.tn0;
+        const int32_t near_ref = swap ? st.c1 : st.c0, far_ref = swap ? st.c0 : st.c1;
         if (sp < RT_MAX_STACK) stack[64 * sp++] = far_ref;
         ref = near_ref;
         continue;
       }
-      if (h0) { ref = c0; continue; }
-      if (h1) { ref = c1; continue; }
+      if (st.h0) { ref = st.c0; continue; }
+      if (st.h1) { ref = st.c1; continue; }
     } else {
       const uint32_t lr = (uint32_t)ref;
       const uint32_t first = (lr >> 4) & 0x07ffffffu, count = (lr & 15u) + 1u;
-      const uint32_t to = S.tris + 48u * first;
-      float4 ta[4], tb[4], tc[4];
+      if (uni) {
+        // one leaf for the whole wave: triangle records in SGPRs, one by one
+        const uint32_t to = S.tris + 48u * first;
+        bool done = false;
 #pragma unroll
-      for (uint32_t k = 0; k < 4; ++k) {
-        ta[k] = S.A.ld_f4(to + 48u * k);
-        tb[k] = S.A.ld_f4(to + 48u * k + 16);
-        tc[k] = S.A.ld_f4(to + 48u * k + 32);
-      }
-#pragma unroll
-      for (uint32_t k = 0; k < 4; ++k) {
-        if (k < count) {
-          const int32_t pid = __float_as_int(ta[k].w);
+        for (uint32_t k = 0; k < 4; ++k) {
+          if (k < count && !done) {
+            const float4 ta = S.A.sld_f4(to + 48u * k), tb = S.A.sld_f4(to + 48u * k + 16);
+            const float4 tc = S.A.sld_f4(to + 48u * k + 32);
+            const int32_t pid = __float_as_int(ta.w);
 #ifdef RT_INSTRUMENT
-          ++cnt.tests;
+            ++cnt.tests;
 #endif
-          float t;
-          if (pid != skip && mt_hit(r, ta[k], tb[k], tc[k], tmin, &t)) {
-            if (ANY) {
-              if (t < tmax) { *t_out = t; return pid; }
-            } else if (closer(t, pid, bt, bpid, tie_high)) {
-              bt = t;
-              bpid = pid;
+            float t;
+            if (pid != skip && mt_hit(r, ta, tb, tc, tmin, &t)) {
+              if (ANY) {
+                if (t < tmax) { bt = t; bpid = pid; done = true; }
+              } else if (closer(t, pid, bt, bpid, tie_high)) {
+                bt = t;
+                bpid = pid;
+              }
+            }
+          }
+        }
+        if (ANY && done) { *t_out = bt; return bpid; }
+      } else {
+        // A leaf's (up to 4) triangles are fetched in one batch -- the tris
+        // array carries 3 padding records.
+        const uint32_t to = S.tris + 48u * first;
+        float4 ta[4], tb[4], tc[4];
+#pragma unroll
+        for (uint32_t k = 0; k < 4; ++k) {
+          ta[k] = S.A.ld_f4(to + 48u * k);
+          tb[k] = S.A.ld_f4(to + 48u * k + 16);
+          tc[k] = S.A.ld_f4(to + 48u * k + 32);
+        }
+#pragma unroll
+        for (uint32_t k = 0; k < 4; ++k) {
+          if (k < count) {
+            const int32_t pid = __float_as_int(ta[k].w);
+#ifdef RT_INSTRUMENT
+            ++cnt.tests;
+#endif
+            float t;
+            if (pid != skip && mt_hit(r, ta[k], tb[k], tc[k], tmin, &t)) {
+              if (ANY) {
+                if (t < tmax) { *t_out = t; return pid; }
+              } else if (closer(t, pid, bt, bpid, tie_high)) {
+                bt = t;
+                bpid = pid;
+              }
             }
           }
         }
@@ -234,12 +302,30 @@ __device__ __forceinline__ uint32_t shade_lane(const Scene& S, int32_t pid, uint
   return gfx::shade(S.A, p, s, x, y);
 }
 
-// Shade every lane with spid >= 0 (all 64 lanes call it): the wave's most
-// common primitives first from SGPR records (s_load, one per wave), then
-// whatever is left from per-lane record loads.
+// Shade every lane with spid >= 0: the wave's most common primitives first
+// from SGPR records (s_load, one record read per wave -- the background
+// layer's two triangles cover most waves), then whatever is left from
+// per-lane record loads.
 __device__ __forceinline__ uint32_t shade_wave(const Scene& S, int32_t spid, uint32_t x,
                                                uint32_t y, uint32_t color, Counters& cnt) {
-  return spid >= 0 ? shade_lane(S, spid, x, y, cnt) : color;
+  uint64_t need = __ballot(spid >= 0);
+#pragma unroll 1
+  for (int it = 0; need != 0 && it < RT_SHADE_UNIFORM; ++it) {
+    const int32_t u = __builtin_amdgcn_readlane(spid, (int)__builtin_ctzll(need));
+    gfx::Prim p;
+    gfx::load_prim<true>(S.A, S.prims + 128u * (uint32_t)u, p);
+    const gfx::DcState s = gfx::load_dcstate<true>(S.A, S.dcs + 64u * p.dc());
+    if (spid == u) {
+      color = gfx::shade(S.A, p, s, x, y);
+#ifdef RT_INSTRUMENT
+      ++cnt.shaded;
+      if (s.flags & RT_DC_TEX) cnt.texel_bytes += (s.filter == VX_TEX_FILTER_BILINEAR ? 4u : 1u) * s.stride;
+#endif
+    }
+    need &= ~__ballot(spid == u);
+  }
+  if (need != 0 && (need & (1ull << lane_id())) != 0) color = shade_lane(S, spid, x, y, cnt);
+  return color;
 }
 
 // task -> (shard-local 32x32 tile, 8x8 block, lane) -> pixel
@@ -324,9 +410,12 @@ __device__ __forceinline__ void kernel_body(const vx_task_t& task, const Scene& 
   // covering triangle wins (one wave-uniform triangle per step)
   int32_t spid = hit;
   uint64_t pend = __ballot(in && hit < 0);
+#ifdef RT_ABLATE_LAYERS  // timing-only ablation (scripts/ab_variants.py)
+  pend = 0;
+#endif
   for (uint32_t k = 0; pend != 0 && k < S.num_layer; ++k) {
     const uint32_t lo = S.layers + 48u * k;
-    const float4 ta = S.A.ld_f4(lo), tb = S.A.ld_f4(lo + 16), tc = S.A.ld_f4(lo + 32);
+    const float4 ta = S.A.sld_f4(lo), tb = S.A.sld_f4(lo + 16), tc = S.A.sld_f4(lo + 32);
     const bool mine = (pend & (1ull << lane_id())) != 0;
 #ifdef RT_INSTRUMENT
     cnt.layer_tests += mine;
@@ -336,7 +425,11 @@ __device__ __forceinline__ void kernel_body(const vx_task_t& task, const Scene& 
     if (f) spid = __float_as_int(ta.w);
     pend &= ~__ballot(f);
   }
+#ifdef RT_ABLATE_SHADE  // timing-only ablation (scripts/ab_variants.py)
+  uint32_t color = 0xff000000u | (uint32_t)spid;
+#else
   uint32_t color = shade_wave(S, spid, x, y, S.clear_color, cnt);
+#endif
   const bool shadow = hit >= 0 && (S.flags & RT_FLAG_SHADOWS) != 0;
 #if RT_SHADOW_QUEUE
   // wave64 compaction: lanes with a pending shadow ray append it to the

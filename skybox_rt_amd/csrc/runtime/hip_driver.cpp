@@ -7,7 +7,8 @@
 //                       addresses are arena offsets >= USER_BASE_ADDR;
 //   * kernel image    = vxbin header + gfx950 code object; start() loads it
 //                       once (hipModuleLoadData, cached) and launches
-//                       `vx_main` over the resident grid;
+//                       `vx_main` over an oversubscribed grid (16 blocks per
+//                       CU: the hardware dispatcher balances the load);
 //   * DCRs            = host store, mirrored into the module's __vx_dcrs
 //                       constant block at every start();
 //   * start/ready_wait = asynchronous launch on the driver's stream, bracketed
@@ -15,8 +16,8 @@
 //                       timeout (the simx driver polls a std::future at 1 s);
 //   * mpm_query       = event-timed device ns (MCYCLE) and task count
 //                       (MINSTRET) of the last run;
-//   * __vx_state      = per-launch device state (perf counters + the task
-//                       queues of vx_spawn.h), zeroed before every launch.
+//   * __vx_state      = per-launch device state: one counter row per block,
+//                       written by the block at exit (no per-launch memset).
 // Error behaviour mirrors callbacks.inc: null handles / zero sizes / ranges
 // past the buffer -> -1; unknown caps id -> -1 (simx aborts).
 #include <hip/hip_runtime.h>
@@ -47,10 +48,11 @@ namespace {
 
 constexpr uint64_t kBlockSize = 256;      // allocation granule (>= 64 B DCR blocks)
 constexpr uint64_t kDefaultArenaMB = 4096;
-// __vx_state layout (include/vx_spawn.h): mpm[kMpmShards][VX_MPM_COUNT] u64,
-// then the scheduler queue heads
-constexpr uint32_t kMpmShards = 64;
-constexpr int kGridBlocksPerCU = 16;
+// __vx_state layout (include/vx_spawn.h): uint32 mpm[kMaxGrid][kMpmRow],
+// one row of the first kMpmRow counters per block, written at block exit
+constexpr uint32_t kMaxGrid = 16384;
+constexpr uint32_t kMpmRow = 16;
+constexpr int kGridWavesPerCU = 64;  // 4x the 16 resident waves/CU of the RT kernel
 
 uint64_t env_u64(const char* name, uint64_t dflt) {
   const char* s = std::getenv(name);
@@ -213,7 +215,6 @@ class vx_device {
       HIP_CHECK(hipMemcpyHtoDAsync(m->dcrs, m->dcrs_sent, sizeof(dcrs_), stream_));
       m->dcrs_set = true;
     }
-    HIP_CHECK(hipMemsetAsync(m->mpm, 0, m->mpm_size, stream_));
     HIP_CHECK(hipEventRecord(ev_start_, stream_));
     HIP_CHECK(hipModuleLaunchKernel(m->entry, m->grid, 1, 1, m->block, 1, 1, 0, stream_,
                                     nullptr, nullptr));
@@ -239,7 +240,10 @@ class vx_device {
       const auto dt = std::chrono::steady_clock::now() - t0;
       if ((uint64_t)std::chrono::duration_cast<std::chrono::milliseconds>(dt).count() > timeout_ms)
         return -1;
-      if (spin > 1024) std::this_thread::sleep_for(std::chrono::microseconds(20));
+      // spin (a frame is ~0.1 ms; a sleep costs its timer slack, ~60 us),
+      // back off to sleeping only for long runs
+      if (spin > 1024 && dt > std::chrono::milliseconds(5))
+        std::this_thread::sleep_for(std::chrono::microseconds(50));
     }
     running_ = false;
     float ms = 0.0f;
@@ -270,14 +274,14 @@ class vx_device {
       return 0;
     }
     wait_idle();
-    if (mpm_dirty_) {  // sum the counter shards (vx_spawn.h VX_MPM_SHARDS)
-      HIP_CHECK(hipMemcpyAsync(mpm_shards_, last_module_->mpm, sizeof(mpm_shards_),
+    if (mpm_dirty_) {  // sum the per-block counter rows of the last launch
+      rows_.resize((size_t)last_grid_ * kMpmRow);
+      HIP_CHECK(hipMemcpyAsync(rows_.data(), last_module_->mpm, rows_.size() * sizeof(uint32_t),
                                hipMemcpyDeviceToHost, stream_));
       HIP_CHECK(hipStreamSynchronize(stream_));
-      for (uint32_t i = 0; i < VX_MPM_COUNT; ++i) {
-        mpm_[i] = 0;
-        for (uint32_t sh = 0; sh < kMpmShards; ++sh) mpm_[i] += mpm_shards_[sh][i];
-      }
+      for (uint32_t i = 0; i < VX_MPM_COUNT; ++i) mpm_[i] = 0;
+      for (size_t b = 0; b < last_grid_; ++b)
+        for (uint32_t i = 0; i < kMpmRow; ++i) mpm_[i] += rows_[b * kMpmRow + i];
       mpm_dirty_ = false;
     }
     *value = mpm_[off];
@@ -331,14 +335,19 @@ class vx_device {
     int max_threads = 0;
     HIP_CHECK(hipFuncGetAttribute(&max_threads, HIP_FUNC_ATTRIBUTE_MAX_THREADS_PER_BLOCK, m.entry));
     m.block = (uint32_t)(max_threads > 0 ? max_threads : 256);
-    // Grid = kGridBlocksPerCU blocks per CU, several times what is resident:
+    // Grid = kGridWavesPerCU waves per CU, several times what is resident:
     // vx_spawn deals 64-task chunks to waves by global wave id, so the blocks
     // waiting for a slot are the load balancer (the hardware dispatcher hands
     // a CU its next block when one retires, as simx's cores pull warps).
-    int per_cu = kGridBlocksPerCU;
+    int per_cu = kGridWavesPerCU / (int)((m.block + 63) / 64);
     if (const char* s = std::getenv("VX_HIP_BLOCKS_PER_CU")) per_cu = std::atoi(s);
     if (per_cu < 1) per_cu = 1;
     m.grid = (uint32_t)(props_.multiProcessorCount * per_cu);
+    if (m.grid > kMaxGrid) m.grid = kMaxGrid;
+    if (m.mpm_size < (size_t)m.grid * kMpmRow * sizeof(uint32_t)) {
+      std::printf("[VXDRV] kernel image has no per-block counter slab\n");
+      return -1;
+    }
     auto ins = modules_.emplace(key, m);
     *out = &ins.first->second;
     return 0;
@@ -363,7 +372,7 @@ class vx_device {
   uint32_t dcrs_[VX_DCR_MIRROR_SIZE] = {};
   bool dcr_valid_[VX_DCR_MIRROR_SIZE] = {};
   unsigned long long mpm_[VX_MPM_COUNT] = {};
-  unsigned long long mpm_shards_[kMpmShards][VX_MPM_COUNT] = {};
+  std::vector<uint32_t> rows_;
 };
 
 struct vx_buffer {
