@@ -31,6 +31,7 @@ typedef struct {
 } rt_scene_info_t;
 
 #define RT_RENDER_SHADOWS 0x1u
+#define RT_RENDER_PATH 0x8u            /* diffuse path trace (pt_kernel), `bounces` segments */
 #define RT_RENDER_INSTRUMENTED 0x100u  /* use the counting kernel variant */
 
 typedef struct {
@@ -40,6 +41,8 @@ typedef struct {
   uint32_t clear_color;       /* ARGB8888, 0xff000000 in draw3d */
   uint32_t shard_index;       /* this device renders 32x32 tiles t with */
   uint32_t shard_count;       /*   t % shard_count == shard_index */
+  uint32_t bounces;           /* RT_RENDER_PATH: bounce segments per path (config 4: 4) */
+  uint32_t seed;              /* RT_RENDER_PATH: RNG seed (config 4: 0x5EED) */
 } rt_render_params_t;
 
 typedef struct {
@@ -49,6 +52,7 @@ typedef struct {
   double kernel_ms;           /* HIP-event time of the last launch */
   uint32_t grid, block;       /* launch geometry chosen by the driver */
   uint32_t num_tasks, local_tiles;
+  uint64_t bounce_rays;       /* RT_RENDER_PATH: bounce segments traced */
 } rt_stats_t;
 
 const char* rt_last_error(void);

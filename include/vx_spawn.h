@@ -220,6 +220,33 @@ __device__ __forceinline__ int vx_spawn_tasks_ex(uint32_t num_tasks, F kernel_fu
   return vx_spawn_threads_ex(1u, &num_tasks, (const uint32_t*)nullptr, kernel_func, epilogue, arg);
 }
 
+/* Block-synchronous form for kernels that cooperate across the waves of a
+ * workgroup (e.g. compaction queues in LDS): the block takes blockDim.x
+ * consecutive tasks per step (wave w: tasks step*blockDim + 64w ..+63, the
+ * same 64-task chunks as above), steps are block-uniform, and every thread
+ * calls kernel_func(task, valid, arg) -- valid = false past num_tasks -- and
+ * then block_epilogue(arg), which may use __syncthreads(). */
+template <typename F, typename E, typename Arg>
+__device__ __forceinline__ int vx_spawn_tasks_block(uint32_t num_tasks, F kernel_func,
+                                                    E block_epilogue, Arg* arg) {
+  const uint32_t nsteps = (num_tasks + blockDim.x - 1) / blockDim.x;
+  uint32_t ran = 0;
+  vx_task_t task;
+  task.threadIdx.x = task.threadIdx.y = task.threadIdx.z = 0;
+  task.blockIdx.y = task.blockIdx.z = 0;
+  for (uint32_t st = blockIdx.x; st < nsteps; st += gridDim.x) {
+    const uint32_t t = st * blockDim.x + threadIdx.x;
+    task.task_id = t;
+    task.blockIdx.x = t;
+    const bool valid = t < num_tasks;
+    kernel_func(task, valid, arg);
+    ran += valid;
+    block_epilogue(arg);
+  }
+  vx_mpm_add(VX_MPM_TASKS, ran);
+  return 0;
+}
+
 /* VX_MAIN(ArgT, arg, block_threads) { ... return vx_spawn_tasks(...); }
  * defines the `vx_main` entry the driver launches with `block_threads`
  * threads per workgroup (must be a multiple of 64). */

@@ -346,6 +346,11 @@ uint32_t orc_shade(const orc_dcstate_t* s, const orc_rast_prim_t* p,
   const float r = 1.0f / (f0 + f1 + f2);
   const int32_t dx = fx_from_float_dev(r * f0, 24);
   const int32_t dy = fx_from_float_dev(r * f1, 24);
+  return orc_shade_weights(s, p, dx, dy, depth);
+}
+
+uint32_t orc_shade_weights(const orc_dcstate_t* s, const orc_rast_prim_t* p,
+                           int32_t dx, int32_t dy, uint32_t* depth) {
   int32_t z = 0, cr = 1 << 24, cg = 1 << 24, cb = 1 << 24, ca = 1 << 24, u = 0, v = 0;
   if (s->depth_enabled) z = interp(p->attribs[0], dx, dy);
   if (s->color_enabled) {

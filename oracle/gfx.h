@@ -149,6 +149,12 @@ void orc_dcstate_init(orc_dcstate_t* s, const orc_scene_t* scene,
 uint32_t orc_shade(const orc_dcstate_t* s, const orc_rast_prim_t* p,
                    int32_t F0, int32_t F1, int32_t F2, uint32_t* depth);
 
+/* The same shader from explicit Q.24 barycentric weights dx (vertex 0) and
+ * dy (vertex 1) -- the INTERPOLATE/TEXTURING/MODULATE tail of
+ * draw3d/kernel.cpp:48-79; used for path-trace bounce hits. */
+uint32_t orc_shade_weights(const orc_dcstate_t* s, const orc_rast_prim_t* p,
+                           int32_t dx, int32_t dy, uint32_t* depth);
+
 /* OutputMerger::write (gpu_sw.h:100-168) on one pixel. Returns 1 if the
  * depth/stencil test passed (and colour was written if enabled). */
 int orc_om_write(const orc_dcstate_t* s, uint32_t* cbuf_px, uint32_t* zbuf_px,

@@ -94,11 +94,18 @@ typedef struct {
 } orc_rt_params_t;
 
 #define ORC_RT_SHADOWS 0x1u
+#define ORC_RT_PATH    0x8u   /* diffuse path trace, `bounces` segments */
 
 typedef struct {
   uint64_t primary_rays, shadow_rays, geometry_hits, occluded;
   uint64_t node_visits, tri_tests, layer_tests, shaded, texel_bytes;
+  uint64_t bounce_rays;
 } orc_rt_counters_t;
+
+/* path-trace constants (synthetic: the reference has no lights or
+ * materials) -- identical in the HIP kernel */
+#define ORC_PT_SKY 0.25f        /* radiance of an escaped bounce ray */
+#define ORC_PT_TRIES 8          /* disk rejection-sampling attempts */
 
 /* BVH in the device layout produced by the product's builder
  * (skybox_rt_amd/csrc/app/bvh.cpp, DESIGN.md "BVH layout"). */

@@ -19,6 +19,8 @@ LIB_PATH = os.path.join(HERE, "_build", "liboracle.so")
 CLEAR_COLOR = 0xFF000000  # draw3d/main.cpp:47
 CLEAR_DEPTH = 0xFFFFFFFF  # draw3d/main.cpp:48
 RT_SHADOWS = 0x1
+RT_PATH = 0x8
+PT_SEED = 0x5EED
 
 
 class DrawcallC(C.Structure):
@@ -55,7 +57,7 @@ class RtParamsC(C.Structure):
 class RtCountersC(C.Structure):
     _fields_ = [(n, C.c_uint64) for n in (
         "primary_rays", "shadow_rays", "geometry_hits", "occluded", "node_visits",
-        "tri_tests", "layer_tests", "shaded", "texel_bytes")]
+        "tri_tests", "layer_tests", "shaded", "texel_bytes", "bounce_rays")]
 
     def as_dict(self):
         return {n: int(getattr(self, n)) for n, _ in self._fields_}
@@ -148,10 +150,12 @@ def raster_render(oscene: OracleScene, width: int, height: int, tile_logsize: in
 
 
 def rt_params(width, height, shadows=True, light=(0.0, 60.0, 80.0), nthreads=1,
-              clear_color=CLEAR_COLOR, row_begin=0, row_end=0, row_step=0):
+              clear_color=CLEAR_COLOR, row_begin=0, row_end=0, row_step=0,
+              path=False, bounces=4, seed=PT_SEED):
     p = RtParamsC()
     p.width, p.height = width, height
-    p.flags = RT_SHADOWS if shadows else 0
+    p.flags = (RT_SHADOWS if shadows else 0) | (RT_PATH if path else 0)
+    p.bounces, p.seed = bounces, seed
     p.light[:] = [float(np.float32(x)) for x in light]
     p.clear_color = clear_color
     p.nthreads = nthreads

@@ -274,6 +274,132 @@ static uint32_t shade_at(const rt_ctx_t* c, int g, uint32_t x, uint32_t y, orc_r
   return orc_shade(st, p, e0, e1, e2, &z);
 }
 
+/* ---- diffuse path trace -------------------
+ * NO REFERENCE: the reference has no lights, normals or materials.  The
+ * estimator is the build's own documented choice (DESIGN.md "Path tracing"),
+ * restated here op for op as the HIP kernel (kernels/pt_kernel.hip) runs it:
+ * at every path vertex one shadow ray to the point light (direct term
+ * T * max(0, cos)), then -- for `bounces` segments -- a cosine-weighted bounce
+ * about the geometric normal; an escaped ray adds T * ORC_PT_SKY; a bounce hit
+ * multiplies T by the draw3d shader's colour at the hit's barycentrics.
+ * Only +, -, *, /, sqrt and integer hashing: bit-exact across CPU and GPU. */
+static inline uint32_t pcg_hash(uint32_t v) {
+  const uint32_t state = v * 747796405u + 2891336453u;
+  const uint32_t word = ((state >> ((state >> 28u) + 4u)) ^ state) * 277803737u;
+  return (word >> 22u) ^ word;
+}
+static inline uint32_t pt_key(uint32_t seed, uint32_t px, uint32_t v) {
+  return pcg_hash(px ^ pcg_hash(seed ^ (0x9E3779B9u * (v + 1u))));
+}
+static inline float pt_u11(uint32_t h) { return (float)(h >> 8) * 0x1p-23f - 1.0f; }
+
+/* cosine-weighted direction about unit normal n: uniform point in the unit
+ * disk by bounded rejection sampling, lifted to the hemisphere (Malley), in
+ * the Duff et al. (2017) orthonormal basis of n */
+static void pt_bounce_dir(const float n[3], uint32_t key, float dir[3]) {
+  float x = 0.0f, y = 0.0f;
+  for (uint32_t i = 0; i < ORC_PT_TRIES; ++i) {
+    const float a = pt_u11(pcg_hash(key + 2u * i)), b = pt_u11(pcg_hash(key + 2u * i + 1u));
+    if (fmaf(a, a, b * b) < 1.0f) { x = a; y = b; break; }
+  }
+  const float z = sqrtf(1.0f - fmaf(x, x, y * y));
+  const float sgn = n[2] >= 0.0f ? 1.0f : -1.0f;
+  const float a = -1.0f / (sgn + n[2]);
+  const float b = (n[0] * n[1]) * a;
+  const float t1[3] = {fmaf(sgn * (n[0] * n[0]), a, 1.0f), sgn * b, -(sgn * n[0])};
+  const float t2[3] = {b, fmaf(n[1] * n[1], a, sgn), -n[1]};
+  for (int k = 0; k < 3; ++k) dir[k] = fmaf(x, t1[k], fmaf(y, t2[k], z * n[k]));
+}
+
+/* unit geometric normal of triangle (v0, e1, e2), facing against din */
+static void pt_normal(const float* tri, const float din[3], float n[3]) {
+  cross3(n, tri + 3, tri + 6);
+  const float len = sqrtf(dot3(n, n));
+  n[0] = n[0] / len; n[1] = n[1] / len; n[2] = n[2] / len;
+  if (dot3(n, din) > 0.0f) { n[0] = -n[0]; n[1] = -n[1]; n[2] = -n[2]; }
+}
+
+/* barycentric weights of the MT hit (b1 = vertex 1, b2 = vertex 2): the
+ * same numerators as mt_hit, divided by |det| */
+static void mt_bary(const float o[3], const float d[3], const float* tri, float* b1, float* b2) {
+  float pvec[3], tvec[3], qvec[3];
+  cross3(pvec, d, tri + 6);
+  const float det = dot3(tri + 3, pvec);
+  tvec[0] = o[0] - tri[0]; tvec[1] = o[1] - tri[1]; tvec[2] = o[2] - tri[2];
+  float u = dot3(tvec, pvec);
+  cross3(qvec, tvec, tri + 3);
+  float v = dot3(d, qvec);
+  float adet = det;
+  if (det < 0.0f) { adet = -det; u = -u; v = -v; }
+  *b1 = u / adet;
+  *b2 = v / adet;
+}
+
+static inline uint32_t pt_to8(float x) {
+  return x >= 1.0f ? 255u : (x > 0.0f ? (uint32_t)fmaf(x, 255.0f, 0.5f) : 0u);
+}
+
+static int trace_any(const rt_ctx_t* c, const float o[3], const float d[3], float tmin,
+                     float tmax, int anyhit, int skip, float* t, orc_rt_counters_t* k) {
+  return c->bvh ? bvh_trace(c, o, d, tmin, tmax, anyhit, skip, t, &k->node_visits, &k->tri_tests)
+                : brute_trace(c, o, d, tmin, tmax, anyhit, skip, t, &k->tri_tests);
+}
+
+static uint32_t path_trace(const rt_ctx_t* c, uint32_t px, const float d0[3], float t0, int g,
+                           uint32_t alb0, orc_rt_counters_t* k) {
+  const float k255 = 1.0f / 255.0f;
+  float T[3] = {(float)((alb0 >> 16) & 0xffu) * k255, (float)((alb0 >> 8) & 0xffu) * k255,
+                (float)(alb0 & 0xffu) * k255};
+  float L[3] = {0.0f, 0.0f, 0.0f};
+  float o[3] = {0.0f, 0.0f, 0.0f}, dir[3] = {d0[0], d0[1], d0[2]};
+  float th = t0;
+  int pid = g;
+  for (uint32_t v = 0;; ++v) {
+    float n[3], P[3];
+    pt_normal(c->tri + (size_t)pid * 9, dir, n);
+    const float tt = th * 0.999755859375f;
+    for (int i = 0; i < 3; ++i) P[i] = fmaf(dir[i], tt, o[i]);
+    /* direct light: shadow segment P -> light */
+    const float sd[3] = {c->p.light[0] - P[0], c->p.light[1] - P[1], c->p.light[2] - P[2]};
+    float ts;
+    ++k->shadow_rays;
+    if (trace_any(c, P, sd, 0.0f, 1.0f, 1, pid, &ts, k) >= 0) {
+      ++k->occluded;
+    } else {
+      const float cosl = dot3(n, sd) / sqrtf(dot3(sd, sd));
+      if (cosl > 0.0f)
+        for (int i = 0; i < 3; ++i) L[i] = fmaf(T[i], cosl, L[i]);
+    }
+    if (v == c->p.bounces) break;
+    /* bounce */
+    float nd[3], nt = 0.0f;
+    pt_bounce_dir(n, pt_key(c->p.seed, px, v), nd);
+    ++k->bounce_rays;
+    const int np = trace_any(c, P, nd, 0.0f, INFINITY, 0, pid, &nt, k);
+    if (np < 0) {
+      for (int i = 0; i < 3; ++i) L[i] = fmaf(T[i], ORC_PT_SKY, L[i]);
+      break;
+    }
+    float b1, b2;
+    mt_bary(P, nd, c->tri + (size_t)np * 9, &b1, &b2);
+    const int32_t dx = fx_from_float_dev((1.0f - b1) - b2, 24);
+    const int32_t dy = fx_from_float_dev(b1, 24);
+    const orc_dcstate_t* st = &c->dcst[c->prim_dc[np]];
+    uint32_t z;
+    ++k->shaded;
+    if (st->tex_enabled)
+      k->texel_bytes += (st->tex_filter == VX_TEX_FILTER_BILINEAR ? 4u : 1u) * vx_format_stride((int)st->tex_format);
+    const uint32_t a = orc_shade_weights(st, &c->rp[np], dx, dy, &z);
+    T[0] = T[0] * ((float)((a >> 16) & 0xffu) * k255);
+    T[1] = T[1] * ((float)((a >> 8) & 0xffu) * k255);
+    T[2] = T[2] * ((float)(a & 0xffu) * k255);
+    for (int i = 0; i < 3; ++i) { o[i] = P[i]; dir[i] = nd[i]; }
+    th = nt;
+    pid = np;
+  }
+  return (alb0 & 0xff000000u) | (pt_to8(L[0]) << 16) | (pt_to8(L[1]) << 8) | pt_to8(L[2]);
+}
+
 static void rt_row(rt_ctx_t* c, uint32_t y, orc_rt_counters_t* k) {
   const orc_scene_t* s = c->scene;
   const uint32_t W = c->p.width;
@@ -291,7 +417,9 @@ static void rt_row(rt_ctx_t* c, uint32_t y, orc_rt_counters_t* k) {
       ++k->geometry_hits;
       col = shade_at(c, hit, x, y, k);
       opid = hit;
-      if (c->p.flags & ORC_RT_SHADOWS) {
+      if (c->p.flags & ORC_RT_PATH) {
+        col = path_trace(c, y * W + x, d, t, hit, col, k);
+      } else if (c->p.flags & ORC_RT_SHADOWS) {
         /* origin pulled toward the eye by 2^-12 of t, segment to the light */
         const float tt = t * 0.999755859375f;
         const float so[3] = {d[0] * tt, d[1] * tt, d[2] * tt};

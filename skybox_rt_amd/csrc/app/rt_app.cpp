@@ -64,8 +64,9 @@ struct rt_scene {
 struct rt_renderer {
   rt_scene* sc = nullptr;
   vx_device_h dev = nullptr;
-  vx_buffer_h krnl[2] = {nullptr, nullptr};
+  vx_buffer_h krnl[3] = {nullptr, nullptr, nullptr};  // rt, rt instrumented, path trace
   vx_buffer_h nodes = nullptr, tris = nullptr, layers = nullptr, dcs = nullptr, tex = nullptr;
+  vx_buffer_h ptris = nullptr;
   vx_buffer_h prims = nullptr, cbuf = nullptr, args = nullptr;
   uint64_t cbuf_bytes = 0;
   rt_render_params_t params{};
@@ -77,7 +78,8 @@ struct rt_renderer {
   vx_hip_last_run_t last_run = nullptr;
 
   ~rt_renderer() {
-    vx_buffer_h* bufs[] = {&krnl[0], &krnl[1], &nodes, &tris, &layers, &dcs, &tex, &prims, &cbuf, &args};
+    vx_buffer_h* bufs[] = {&krnl[0], &krnl[1], &krnl[2], &nodes, &tris, &layers, &dcs, &tex,
+                           &ptris, &prims, &cbuf, &args};
     for (auto* b : bufs) {
       if (*b) vx_mem_free(*b);
       *b = nullptr;
@@ -213,9 +215,10 @@ int rt_renderer_create(rt_scene_h s, const char* kernel_dir, rt_renderer_h* out)
   // the regular image's LDS stack covers BVH depth <= 16; deeper trees use the
   // deep image (32 entries, lower occupancy)
   const bool deep = s->bvh.depth > RT_STACK_SHALLOW;
-  const char* names[2] = {deep ? "rt_kernel_deep.vxbin" : "rt_kernel.vxbin",
-                          deep ? "rt_kernel_deep_stats.vxbin" : "rt_kernel_stats.vxbin"};
-  for (int i = 0; i < 2; ++i)
+  const char* names[3] = {deep ? "rt_kernel_deep.vxbin" : "rt_kernel.vxbin",
+                          deep ? "rt_kernel_deep_stats.vxbin" : "rt_kernel_stats.vxbin",
+                          deep ? "pt_kernel_deep.vxbin" : "pt_kernel.vxbin"};
+  for (int i = 0; i < 3; ++i)
     if (vx_upload_kernel_file(r->dev, (dir + "/" + names[i]).c_str(), &r->krnl[i]) != 0)
       return fail("cannot upload kernel " + dir + "/" + names[i]);
   r->mem_ptr = (vx_hip_mem_ptr_t)vx_driver_symbol("vx_hip_mem_ptr");
@@ -247,6 +250,21 @@ int rt_renderer_create(rt_scene_h s, const char* kernel_dir, rt_renderer_h* out)
     std::memcpy(&lt[i].v[3], &s->layers[i], 4);
   }
   if (upload(r->dev, lt.data(), lt.size() * sizeof(rt_tri_t), &r->layers, &a.layers_addr)) return -1;
+  // every primitive's clip-space triangle by pid (path-trace bounce hits)
+  std::vector<rt_tri_t> pt(s->scene.prims.size());
+  for (size_t g = 0; g < pt.size(); ++g) {
+    const auto& p = s->scene.prims[g];
+    std::memset(&pt[g], 0, sizeof(rt_tri_t));
+    for (int k = 0; k < 3; ++k) {
+      const int src = k == 2 ? 3 : k;
+      pt[g].v[k] = p[0].pos[src];
+      pt[g].v[4 + k] = p[1].pos[src] - p[0].pos[src];
+      pt[g].v[8 + k] = p[2].pos[src] - p[0].pos[src];
+    }
+    const int32_t pid = (int32_t)g;
+    std::memcpy(&pt[g].v[3], &pid, 4);
+  }
+  if (upload(r->dev, pt.data(), pt.size() * sizeof(rt_tri_t), &r->ptris, &a.ptris_addr)) return -1;
   a.num_layer_tris = (uint32_t)lt.size();
   // textures: one buffer, each texture 256-B aligned
   std::vector<uint8_t> texels;
@@ -324,7 +342,10 @@ int rt_renderer_configure(rt_renderer_h r, const rt_render_params_t* p) {
   a.shard_index = p->shard_index;
   a.shard_count = shards;
   a.flags = ((p->flags & RT_RENDER_SHADOWS) ? RT_FLAG_SHADOWS : 0u) |
+            ((p->flags & RT_RENDER_PATH) ? RT_FLAG_PATH : 0u) |
             (s->tie_high ? RT_FLAG_TIE_HIGH : 0u) | (shards > 1 ? RT_FLAG_COMPACT : 0u);
+  a.bounces = p->bounces;
+  a.seed = p->seed;
   a.clear_color = p->clear_color;
   a.sx = 2.0f / (float)p->width;
   a.sy = 2.0f / (float)p->height;
@@ -344,7 +365,8 @@ int rt_renderer_configure(rt_renderer_h r, const rt_render_params_t* p) {
 
 int rt_render_start(rt_renderer_h r) {
   if (!r || !r->configured) return fail("renderer not configured");
-  const int k = (r->params.flags & RT_RENDER_INSTRUMENTED) ? 1 : 0;
+  const int k = (r->params.flags & RT_RENDER_PATH) ? 2
+                : (r->params.flags & RT_RENDER_INSTRUMENTED) ? 1 : 0;
   return vx_start(r->dev, r->krnl[k], r->args) == 0 ? 0 : fail("vx_start failed");
 }
 
@@ -362,7 +384,7 @@ int rt_render_stats(rt_renderer_h r, rt_stats_t* st) {
   if (!r || !st) return fail("null argument");
   std::memset(st, 0, sizeof(*st));
   uint64_t v[RT_STAT_COUNT] = {};
-  for (int i = 0; i <= RT_STAT_TEXEL_BYTES; ++i)
+  for (int i = 0; i <= RT_STAT_BOUNCE; ++i)
     if (vx_mpm_query(r->dev, VX_CSR_MPM_BASE + RT_MPM_USER + i, 0, &v[i]) != 0)
       return fail("vx_mpm_query failed");
   st->primary_rays = v[RT_STAT_PRIMARY];
@@ -374,6 +396,7 @@ int rt_render_stats(rt_renderer_h r, rt_stats_t* st) {
   st->layer_tests = v[RT_STAT_LAYER_TESTS];
   st->shaded = v[RT_STAT_SHADED];
   st->texel_bytes = v[RT_STAT_TEXEL_BYTES];
+  st->bounce_rays = v[RT_STAT_BOUNCE];
   vx_mpm_query(r->dev, VX_CSR_MINSTRET, 0, &st->tasks);
   uint64_t ns = 0;
   vx_mpm_query(r->dev, VX_CSR_MCYCLE, 0, &ns);

@@ -188,17 +188,11 @@ __device__ __forceinline__ int32_t edge_eval(const int32_t* e, uint32_t x, uint3
   return (int32_t)((uint32_t)e[0] * x + (uint32_t)e[1] * y + (uint32_t)e[2]);
 }
 
-// draw3d shader for one fragment at pixel (x, y) of primitive p
-// (draw3d/kernel.cpp:232-279; GRADIENTS_SW reinterprets Q15.16 as Q7.24).
-__device__ __forceinline__ uint32_t shade(const vx_arena& A, const Prim& p, const DcState& s,
-                                          uint32_t x, uint32_t y) {
-  const int32_t F0 = edge_eval(p.edge(0), x, y);
-  const int32_t F1 = edge_eval(p.edge(1), x, y);
-  const int32_t F2 = edge_eval(p.edge(2), x, y);
-  const float f0 = fx_to_float(F0, 24), f1 = fx_to_float(F1, 24), f2 = fx_to_float(F2, 24);
-  const float r = 1.0f / (f0 + f1 + f2);
-  const int32_t dx = fx_from_float_dev(r * f0, 24);
-  const int32_t dy = fx_from_float_dev(r * f1, 24);
+// The shader's tail from Q.24 barycentric weights dx (vertex 0), dy (vertex 1):
+// INTERPOLATE / TEXTURING / MODULATE (draw3d/kernel.cpp:48-79).  Path-trace
+// bounce hits enter here with MT barycentrics (oracle/gfx.c orc_shade_weights).
+__device__ __forceinline__ uint32_t shade_weights(const vx_arena& A, const Prim& p,
+                                                  const DcState& s, int32_t dx, int32_t dy) {
   int32_t cr = 1 << 24, cg = 1 << 24, cb = 1 << 24, ca = 1 << 24;
   if (s.flags & RT_DC_COLOR) {
     cr = interp(p.attr(1), dx, dy);
@@ -217,6 +211,18 @@ __device__ __forceinline__ uint32_t shade(const vx_arena& A, const Prim& p, cons
     return tc;
   }
   return (mul8(ca, 255) << 24) | (mul8(cr, 255) << 16) | (mul8(cg, 255) << 8) | mul8(cb, 255);
+}
+
+// draw3d shader for one fragment at pixel (x, y) of primitive p
+// (draw3d/kernel.cpp:232-279; GRADIENTS_SW reinterprets Q15.16 as Q7.24).
+__device__ __forceinline__ uint32_t shade(const vx_arena& A, const Prim& p, const DcState& s,
+                                          uint32_t x, uint32_t y) {
+  const int32_t F0 = edge_eval(p.edge(0), x, y);
+  const int32_t F1 = edge_eval(p.edge(1), x, y);
+  const int32_t F2 = edge_eval(p.edge(2), x, y);
+  const float f0 = fx_to_float(F0, 24), f1 = fx_to_float(F1, 24), f2 = fx_to_float(F2, 24);
+  const float r = 1.0f / (f0 + f1 + f2);
+  return shade_weights(A, p, s, fx_from_float_dev(r * f0, 24), fx_from_float_dev(r * f1, 24));
 }
 
 }  // namespace gfx

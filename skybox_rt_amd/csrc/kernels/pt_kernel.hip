@@ -1,0 +1,306 @@
+// pt_kernel.hip -- diffuse path tracing on the RT hot path (SURVEY.md 8(a)
+// row A7, BASELINE config 4: 1024^2, 4-bounce diffuse, wave64 active-ray
+// compaction).  NO REFERENCE EXISTS for this row; the estimator is the build's
+// own documented choice (DESIGN.md "Path tracing"), restated op for op by the
+// oracle (oracle/rt.c path_trace), against which the output is bit-exact.
+//
+// Per pixel: the primary ray, screen layers and draw3d shading exactly as in
+// rt_kernel.hip.  A pixel whose primary ray hits geometry starts a path:
+// throughput T = its shaded colour, radiance L = 0.  At every path vertex:
+// one any-hit shadow ray to the point light (direct term T * max(0, cos)),
+// then -- for `bounces` segments -- a cosine-weighted bounce about the
+// geometric normal (PCG-hash RNG keyed by pixel, vertex and seed; disk
+// rejection sampling, no transcendentals); a miss adds T * sky and ends the
+// path, a hit multiplies T by the draw3d shader's colour at the hit's
+// barycentrics.  The pixel gets clamp(L) (alpha of the primary colour).
+//
+// Wave64 compaction: a 256-thread workgroup (4 waves, 256 pixels) keeps its
+// live paths in an LDS queue.  After each vertex the surviving paths are
+// appended to the other queue at ballot + mbcnt slots, so bounce k runs on
+// ceil(live/64) full waves while the other waves of the block skip it --
+// the paths that escape (most of them, tekkaman is an open scene) stop
+// costing lanes.
+#include <hip/hip_runtime.h>
+
+#include "rt_trace.h"
+
+#define PT_BLOCK 256
+#define PT_SKY 0.25f     // radiance of an escaped bounce ray (oracle ORC_PT_SKY)
+#define PT_TRIES 8u      // disk rejection-sampling attempts (ORC_PT_TRIES)
+
+namespace {
+
+using namespace rtk;
+
+constexpr int kWaves = PT_BLOCK / 64;
+
+__device__ __forceinline__ uint32_t pcg_hash(uint32_t v) {
+  const uint32_t state = v * 747796405u + 2891336453u;
+  const uint32_t word = ((state >> ((state >> 28u) + 4u)) ^ state) * 277803737u;
+  return (word >> 22u) ^ word;
+}
+__device__ __forceinline__ uint32_t pt_key(uint32_t seed, uint32_t px, uint32_t v) {
+  return pcg_hash(px ^ pcg_hash(seed ^ (0x9E3779B9u * (v + 1u))));
+}
+__device__ __forceinline__ float pt_u11(uint32_t h) {
+  return (float)(h >> 8) * 0x1p-23f - 1.0f;
+}
+
+// cosine-weighted direction about unit normal n (oracle pt_bounce_dir)
+__device__ __forceinline__ void bounce_dir(const float n[3], uint32_t key, float dir[3]) {
+  float x = 0.0f, y = 0.0f;
+  for (uint32_t i = 0; i < PT_TRIES; ++i) {
+    const float a = pt_u11(pcg_hash(key + 2u * i)), b = pt_u11(pcg_hash(key + 2u * i + 1u));
+    if (fmaf(a, a, b * b) < 1.0f) { x = a; y = b; break; }
+  }
+  const float z = sqrtf(1.0f - fmaf(x, x, y * y));
+  const float sgn = n[2] >= 0.0f ? 1.0f : -1.0f;
+  const float a = -1.0f / (sgn + n[2]);
+  const float b = (n[0] * n[1]) * a;
+  const float t1[3] = {fmaf(sgn * (n[0] * n[0]), a, 1.0f), sgn * b, -(sgn * n[0])};
+  const float t2[3] = {b, fmaf(n[1] * n[1], a, sgn), -n[1]};
+#pragma unroll
+  for (int k = 0; k < 3; ++k) dir[k] = fmaf(x, t1[k], fmaf(y, t2[k], z * n[k]));
+}
+
+__device__ __forceinline__ void load_tri(const Scene& S, int32_t pid, float v0[3], float e1[3],
+                                         float e2[3]) {
+  const uint32_t o = S.ptris + 48u * (uint32_t)pid;
+  const float4 a = S.A.ld_f4(o), b = S.A.ld_f4(o + 16), c = S.A.ld_f4(o + 32);
+  v0[0] = a.x; v0[1] = a.y; v0[2] = a.z;
+  e1[0] = b.x; e1[1] = b.y; e1[2] = b.z;
+  e2[0] = c.x; e2[1] = c.y; e2[2] = c.z;
+}
+
+// unit geometric normal facing against din (oracle pt_normal)
+__device__ __forceinline__ void tri_normal(const float e1[3], const float e2[3], const float din[3],
+                                           float n[3]) {
+  cross3(n, e1, e2);
+  const float len = sqrtf(dot3(n, n));
+  n[0] = n[0] / len; n[1] = n[1] / len; n[2] = n[2] / len;
+  if (dot3(n, din) > 0.0f) { n[0] = -n[0]; n[1] = -n[1]; n[2] = -n[2]; }
+}
+
+// MT barycentrics of vertex 1 and 2 (oracle mt_bary)
+__device__ __forceinline__ void mt_bary(const float o[3], const float d[3], const float v0[3],
+                                        const float e1[3], const float e2[3], float* b1,
+                                        float* b2) {
+  float pvec[3], tvec[3], qvec[3];
+  cross3(pvec, d, e2);
+  const float det = dot3(e1, pvec);
+  tvec[0] = o[0] - v0[0]; tvec[1] = o[1] - v0[1]; tvec[2] = o[2] - v0[2];
+  float u = dot3(tvec, pvec);
+  cross3(qvec, tvec, e1);
+  float v = dot3(d, qvec);
+  float adet = det;
+  if (det < 0.0f) { adet = -det; u = -u; v = -v; }
+  *b1 = u / adet;
+  *b2 = v / adet;
+}
+
+__device__ __forceinline__ uint32_t to8(float x) {
+  return x >= 1.0f ? 255u : (x > 0.0f ? (uint32_t)fmaf(x, 255.0f, 0.5f) : 0u);
+}
+
+// A live path at a vertex: the ray that reached it (o, d, hit t, hit pid),
+// its throughput T and radiance L so far, its pixel task and vertex index
+// (implicit: the bounce loop's), the primary colour's alpha.  SoA in LDS.
+struct PathQueue {
+  uint32_t task[PT_BLOCK], alpha[PT_BLOCK];
+  int32_t pid[PT_BLOCK];
+  float t[PT_BLOCK];
+  float o[3][PT_BLOCK], d[3][PT_BLOCK], T[3][PT_BLOCK], L[3][PT_BLOCK];
+};
+
+struct PtLds {
+  int32_t stack[kWaves][RT_MAX_STACK][64];
+  PathQueue q[2];
+  uint32_t n[2];
+};
+
+// append this lane's path (if `want`) to queue q at a ballot/mbcnt slot
+__device__ __forceinline__ void enqueue(PtLds& L, int qi, bool want, uint32_t task, uint32_t alpha,
+                                        int32_t pid, float t, const float o[3], const float d[3],
+                                        const float T[3], const float Lr[3]) {
+  const uint64_t m = __ballot(want);
+  if (m == 0) return;
+  uint32_t base = 0;
+  if (lane_id() == (uint32_t)__builtin_ctzll(m)) base = atomicAdd(&L.n[qi], (uint32_t)__popcll(m));
+  base = __builtin_amdgcn_readlane(base, (int)__builtin_ctzll(m));
+  if (!want) return;
+  const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
+                                                  __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+  const uint32_t s = base + rank;
+  PathQueue& q = L.q[qi];
+  q.task[s] = task;
+  q.alpha[s] = alpha;
+  q.pid[s] = pid;
+  q.t[s] = t;
+#pragma unroll
+  for (int k = 0; k < 3; ++k) {
+    q.o[k][s] = o[k];
+    q.d[k][s] = d[k];
+    q.T[k][s] = T[k];
+    q.L[k][s] = Lr[k];
+  }
+}
+
+// primary phase of one task (every thread of the block calls it)
+__device__ __forceinline__ void primary(const vx_task_t& task, bool valid, const Scene& S,
+                                        PtLds& L, Counters& cnt) {
+  const uint32_t t = task.blockIdx.x;
+  uint32_t x = 0, y = 0;
+  if (valid) task_pixel(S, t, &x, &y);
+  const bool in = valid && x < S.width && y < S.height;
+  Ray r;
+  primary_dir(S, x, y, r);
+  ray_setup(r);
+  cnt.primary += in;
+  const bool tie_high = (S.flags & RT_FLAG_TIE_HIGH) != 0;
+  float th = 0.0f;
+  int32_t* stack = &L.stack[threadIdx.x >> 6][0][lane_id()];
+  const int32_t hit = in ? trace<false>(S, r, 0.0f, INFINITY, -1, tie_high, &th, stack, cnt) : -1;
+  cnt.hits += hit >= 0;
+  const int32_t spid = resolve_layers(S, r, in && hit < 0, hit, cnt);
+  const uint32_t color = shade_wave(S, spid, x, y, S.clear_color, cnt);
+  const bool path = hit >= 0;
+  const float k255 = 1.0f / 255.0f;
+  const float T[3] = {(float)((color >> 16) & 0xffu) * k255, (float)((color >> 8) & 0xffu) * k255,
+                      (float)(color & 0xffu) * k255};
+  const float Lr[3] = {0.0f, 0.0f, 0.0f};
+  enqueue(L, 0, path, t, color & 0xff000000u, hit, th, r.o, r.d, T, Lr);
+  if (in && !path) store_pixel(S, t, x, y, color);
+}
+
+// one path vertex for queue entry i (lanes with i < n; whole waves past n skip)
+__device__ __forceinline__ void vertex(const Scene& S, PtLds& L, int qi, uint32_t v, uint32_t n,
+                                       Counters& cnt) {
+  const uint32_t i = threadIdx.x;
+  const bool act = i < n;
+  const PathQueue& q = L.q[qi];
+  const uint32_t j = act ? i : 0u;
+  const uint32_t task = q.task[j], alpha = q.alpha[j];
+  const int32_t pid = q.pid[j];
+  const float th = q.t[j];
+  float o[3], d[3], T[3], Lr[3];
+#pragma unroll
+  for (int k = 0; k < 3; ++k) {
+    o[k] = q.o[k][j];
+    d[k] = q.d[k][j];
+    T[k] = q.T[k][j];
+    Lr[k] = q.L[k][j];
+  }
+  const bool tie_high = (S.flags & RT_FLAG_TIE_HIGH) != 0;
+  int32_t* stack = &L.stack[threadIdx.x >> 6][0][lane_id()];
+  float v0[3], e1[3], e2[3], nrm[3], P[3];
+  load_tri(S, act ? pid : 0, v0, e1, e2);
+  tri_normal(e1, e2, d, nrm);
+  const float tt = th * 0.999755859375f;
+#pragma unroll
+  for (int k = 0; k < 3; ++k) P[k] = fmaf(d[k], tt, o[k]);
+  // direct light: shadow segment P -> light
+  Ray s;
+  s.o[0] = P[0]; s.o[1] = P[1]; s.o[2] = P[2];
+  s.d[0] = S.light[0] - P[0];
+  s.d[1] = S.light[1] - P[1];
+  s.d[2] = S.light[2] - P[2];
+  ray_setup(s);
+  cnt.shadow += act;
+  float ts;
+  const bool occ = act && trace<true>(S, s, 0.0f, 1.0f, pid, tie_high, &ts, stack, cnt) >= 0;
+  cnt.occluded += occ;
+  if (act && !occ) {
+    const float cosl = dot3(nrm, s.d) / sqrtf(dot3(s.d, s.d));
+    if (cosl > 0.0f) {
+#pragma unroll
+      for (int k = 0; k < 3; ++k) Lr[k] = fmaf(T[k], cosl, Lr[k]);
+    }
+  }
+  bool alive = act && v < S.bounces;
+  int32_t np = -1;
+  float nt = 0.0f;
+  Ray b;
+  if (alive) {
+    b.o[0] = P[0]; b.o[1] = P[1]; b.o[2] = P[2];
+    uint32_t x, y;
+    task_pixel(S, task, &x, &y);
+    bounce_dir(nrm, pt_key(S.seed, y * S.width + x, v), b.d);  // keyed by pixel, not task
+    ray_setup(b);
+    cnt.bounce += 1;
+    np = trace<false>(S, b, 0.0f, INFINITY, pid, tie_high, &nt, stack, cnt);
+    if (np < 0) {
+#pragma unroll
+      for (int k = 0; k < 3; ++k) Lr[k] = fmaf(T[k], PT_SKY, Lr[k]);
+      alive = false;
+    }
+  }
+  if (alive) {
+    // albedo at the bounce hit: the draw3d shader at its MT barycentrics
+    float w0[3], f1[3], f2[3], b1, b2;
+    load_tri(S, np, w0, f1, f2);
+    mt_bary(b.o, b.d, w0, f1, f2, &b1, &b2);
+    gfx::Prim p;
+    gfx::load_prim(S.A, S.prims + 128u * (uint32_t)np, p);
+    const gfx::DcState st = gfx::load_dcstate(S.A, S.dcs + 64u * p.dc());
+    const uint32_t a = gfx::shade_weights(S.A, p, st, gfx::fx_from_float_dev((1.0f - b1) - b2, 24),
+                                          gfx::fx_from_float_dev(b1, 24));
+    const float k255 = 1.0f / 255.0f;
+    T[0] = T[0] * ((float)((a >> 16) & 0xffu) * k255);
+    T[1] = T[1] * ((float)((a >> 8) & 0xffu) * k255);
+    T[2] = T[2] * ((float)(a & 0xffu) * k255);
+  }
+  enqueue(L, qi ^ 1, alive, task, alpha, np, nt, P, b.d, T, Lr);
+  if (act && !alive) {
+    uint32_t x, y;
+    task_pixel(S, task, &x, &y);
+    store_pixel(S, task, x, y, alpha | (to8(Lr[0]) << 16) | (to8(Lr[1]) << 8) | to8(Lr[2]));
+  }
+}
+
+// after each block step: run the path vertices of the queued paths, bounce
+// by bounce, on compacted waves
+__device__ __forceinline__ void bounces(const Scene& S, PtLds& L, Counters& cnt) {
+  __syncthreads();  // primary enqueues complete
+  int qi = 0;
+  for (uint32_t v = 0;; ++v) {
+    const uint32_t n = L.n[qi];
+    __syncthreads();  // every thread has read n before anyone resets it
+    if (threadIdx.x == 0) L.n[qi ^ 1] = 0;
+    __syncthreads();
+    if (n == 0) break;
+    if ((threadIdx.x & ~63u) < n) vertex(S, L, qi, v, n, cnt);  // wave-uniform skip
+    __syncthreads();  // next queue complete
+    qi ^= 1;
+  }
+  if (threadIdx.x == 0) { L.n[0] = 0; L.n[1] = 0; }
+  __syncthreads();
+}
+
+__device__ __forceinline__ void flush(int slot, uint32_t v) { vx_mpm_add(RT_MPM_USER + slot, v); }
+
+}  // namespace
+
+VX_MAIN(rt_kernel_arg_t, arg, PT_BLOCK) {
+  __shared__ PtLds s_pt;
+  Counters cnt;
+  const Scene S = load_scene(arg);
+  if (threadIdx.x == 0) { s_pt.n[0] = 0; s_pt.n[1] = 0; }
+  __syncthreads();
+  const int rc = vx_spawn_tasks_block(
+      arg->num_tasks,
+      [&](const vx_task_t& task, bool valid, const Scene* s) { primary(task, valid, *s, s_pt, cnt); },
+      [&](const Scene* s) { bounces(*s, s_pt, cnt); }, &S);
+  flush(RT_STAT_PRIMARY, cnt.primary);
+  flush(RT_STAT_SHADOW, cnt.shadow);
+  flush(RT_STAT_HITS, cnt.hits);
+  flush(RT_STAT_OCCLUDED, cnt.occluded);
+  flush(RT_STAT_BOUNCE, cnt.bounce);
+#ifdef RT_INSTRUMENT
+  flush(RT_STAT_NODE_VISITS, cnt.visits);
+  flush(RT_STAT_TRI_TESTS, cnt.tests);
+  flush(RT_STAT_LAYER_TESTS, cnt.layer_tests);
+  flush(RT_STAT_SHADED, cnt.shaded);
+  flush(RT_STAT_TEXEL_BYTES, cnt.texel_bytes);
+#endif
+  return rc;
+}

@@ -8,6 +8,7 @@
 //   layers  [num_layer]  rt_tri_t    48 B  screen layers, highest pid first
 //   prims   [num_prims]  rt_prim_t  128 B  fixed-point shading record
 //   dcs     [num_dc]     rt_dcstate_t 64 B per-drawcall shading state
+//   ptris   [num_prims]  rt_tri_t    48 B  clip-space triangle by pid
 //   cbuf    W*H*4 (linear, row 0 = NDC y=-1) or tiles*1024*4 (compact shard)
 #pragma once
 
@@ -33,6 +34,7 @@
 #define RT_FLAG_SHADOWS  0x1u
 #define RT_FLAG_TIE_HIGH 0x2u    // LEQUAL geometry: equal t -> highest pid
 #define RT_FLAG_COMPACT  0x4u    // shard output: compact tile buffer
+#define RT_FLAG_PATH     0x8u    // diffuse path trace (pt_kernel.hip)
 
 #define RT_DC_DEPTH   0x1u
 #define RT_DC_COLOR   0x2u
@@ -47,7 +49,7 @@
 enum {
   RT_STAT_PRIMARY = 0, RT_STAT_SHADOW, RT_STAT_HITS, RT_STAT_OCCLUDED,
   RT_STAT_NODE_VISITS, RT_STAT_TRI_TESTS, RT_STAT_LAYER_TESTS, RT_STAT_SHADED,
-  RT_STAT_TEXEL_BYTES, RT_STAT_COUNT = 16
+  RT_STAT_TEXEL_BYTES, RT_STAT_BOUNCE, RT_STAT_COUNT = 16
 };
 
 // rt_node_t: 4 x float4 =
@@ -75,11 +77,13 @@ typedef struct {
 
 typedef struct {
   uint64_t cbuf_addr, nodes_addr, tris_addr, layers_addr, prims_addr, dcs_addr;
-  uint64_t pad0[2];
+  uint64_t ptris_addr;     // rt_tri_t per pid (path trace: bounce-hit barycentrics)
+  uint64_t pad0;
   uint32_t width, height, tiles_x, tiles_y;
   uint32_t num_tasks, num_nodes, num_layer_tris, flags;
-  uint32_t clear_color, shard_index, shard_count, pad1;
+  uint32_t clear_color, shard_index, shard_count, bounces;
   float sx, sy;            // 2/W, 2/H
   float light[3];
-  uint32_t pad2[3];
+  uint32_t seed;           // path-trace RNG seed
+  uint32_t pad2[2];
 } rt_kernel_arg_t;

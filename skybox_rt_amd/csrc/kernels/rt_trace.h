@@ -1,0 +1,373 @@
+// rt_trace.h -- device pieces shared by the RT kernel programs
+// (rt_kernel.hip: primary + shadow rays; pt_kernel.hip: diffuse path trace):
+// scene arguments, ray setup, Möller–Trumbore, slab test, BVH traversal with
+// the per-lane LDS stack, draw3d-exact shading, pixel addressing.  Numerics
+// are bit-identical to the oracle (oracle/rt.c): every fused multiply-add is
+// an explicit fmaf, everything else is compiled with -ffp-contract=off,
+// divisions and square roots are IEEE (correctly rounded).
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include "gfx_device.h"
+#include "rt_common.h"
+#include "vx_spawn.h"
+
+// 1: wave-uniform node / leaf records through the scalar cache (trace());
+// measured 3-4 % slower than per-lane loads on tekkaman, so off by default
+#ifndef RT_SCALAR
+#define RT_SCALAR 0
+#endif
+// distinct primitives per wave shaded from SGPR records (shade_wave());
+// measured neutral, off by default
+#ifndef RT_SHADE_UNIFORM
+#define RT_SHADE_UNIFORM 0
+#endif
+
+namespace rtk {
+
+
+struct Counters {
+  uint32_t primary = 0, shadow = 0, hits = 0, occluded = 0, bounce = 0;
+#ifdef RT_INSTRUMENT
+  uint32_t visits = 0, tests = 0, layer_tests = 0, shaded = 0, texel_bytes = 0;
+#endif
+};
+
+// Kernel arguments in scalar registers; buffer addresses become 32-bit
+// arena offsets (rt_app checks every buffer lies below 4 GiB).
+struct Scene {
+  vx_arena A;
+  uint32_t nodes, tris, layers, prims, dcs, cbuf, ptris;
+  uint32_t num_nodes, num_layer, flags, width, height;
+  uint32_t shard_index, shard_count, tiles_x, clear_color, bounces, seed;
+  float sx, sy, light[3];
+};
+
+__device__ __forceinline__ Scene load_scene(const rt_kernel_arg_t* a) {
+  Scene s;
+  s.A = vx_arena::get();
+  s.nodes = (uint32_t)a->nodes_addr;
+  s.tris = (uint32_t)a->tris_addr;
+  s.layers = (uint32_t)a->layers_addr;
+  s.prims = (uint32_t)a->prims_addr;
+  s.dcs = (uint32_t)a->dcs_addr;
+  s.cbuf = (uint32_t)a->cbuf_addr;
+  s.ptris = (uint32_t)a->ptris_addr;
+  s.bounces = a->bounces;
+  s.seed = a->seed;
+  s.num_nodes = a->num_nodes;
+  s.num_layer = a->num_layer_tris;
+  s.flags = a->flags;
+  s.width = a->width;
+  s.height = a->height;
+  s.shard_index = a->shard_index;
+  s.shard_count = a->shard_count;
+  s.tiles_x = a->tiles_x;
+  s.clear_color = a->clear_color;
+  s.sx = a->sx;
+  s.sy = a->sy;
+  s.light[0] = a->light[0];
+  s.light[1] = a->light[1];
+  s.light[2] = a->light[2];
+  return s;
+}
+
+__device__ __forceinline__ uint32_t lane_id() {
+  return __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
+}
+
+struct Ray {
+  float o[3], d[3];
+  float inv[3], oi[3];
+};
+
+__device__ __forceinline__ float safe_dir(float d) {
+  return fabsf(d) < 1e-20f ? (d < 0.0f ? -1e-20f : 1e-20f) : d;
+}
+
+__device__ __forceinline__ void ray_setup(Ray& r) {
+#pragma unroll
+  for (int k = 0; k < 3; ++k) {
+    r.inv[k] = 1.0f / safe_dir(r.d[k]);
+    r.oi[k] = r.o[k] * r.inv[k];
+  }
+}
+
+__device__ __forceinline__ void cross3(float* r, const float* a, const float* b) {
+  r[0] = fmaf(a[1], b[2], -(a[2] * b[1]));
+  r[1] = fmaf(a[2], b[0], -(a[0] * b[2]));
+  r[2] = fmaf(a[0], b[1], -(a[1] * b[0]));
+}
+__device__ __forceinline__ float dot3(const float* a, const float* b) {
+  return fmaf(a[2], b[2], fmaf(a[1], b[1], a[0] * b[0]));
+}
+
+// Möller–Trumbore with the reference's inclusive coverage (oracle/rt.c mt_hit)
+__device__ __forceinline__ bool mt_hit(const Ray& r, const float4& a, const float4& b,
+                                       const float4& c, float tmin, float* t_out) {
+  const float v0[3] = {a.x, a.y, a.z}, e1[3] = {b.x, b.y, b.z}, e2[3] = {c.x, c.y, c.z};
+  float pvec[3], tvec[3], qvec[3];
+  cross3(pvec, r.d, e2);
+  const float det = dot3(e1, pvec);
+  tvec[0] = r.o[0] - v0[0];
+  tvec[1] = r.o[1] - v0[1];
+  tvec[2] = r.o[2] - v0[2];
+  float u = dot3(tvec, pvec);
+  cross3(qvec, tvec, e1);
+  float v = dot3(r.d, qvec);
+  float adet = det;
+  if (det < 0.0f) { adet = -det; u = -u; v = -v; }
+  if (!(adet > 0.0f) || u < 0.0f || v < 0.0f || u + v > adet) return false;
+  const float t = dot3(e2, qvec) / det;
+  if (!(t > tmin)) return false;
+  *t_out = t;
+  return true;
+}
+
+// slab test of one child; box planes interleaved as in rt_node_t
+__device__ __forceinline__ bool slab(float lox, float hix, float loy, float hiy, float loz,
+                                     float hiz, const Ray& r, float tmin, float tmax,
+                                     float* tnear) {
+  const float ax = fmaf(lox, r.inv[0], -r.oi[0]), bx = fmaf(hix, r.inv[0], -r.oi[0]);
+  const float ay = fmaf(loy, r.inv[1], -r.oi[1]), by = fmaf(hiy, r.inv[1], -r.oi[1]);
+  const float az = fmaf(loz, r.inv[2], -r.oi[2]), bz = fmaf(hiz, r.inv[2], -r.oi[2]);
+  const float tn = fmaxf(fmaxf(fminf(ax, bx), fminf(ay, by)), fmaxf(fminf(az, bz), tmin));
+  const float tf = fminf(fminf(fmaxf(ax, bx), fmaxf(ay, by)), fminf(fmaxf(az, bz), tmax));
+  *tnear = tn;
+  return tn <= tf;
+}
+
+// closest-hit order: t, then pid by the drawcall's depth-compare tie rule
+__device__ __forceinline__ bool closer(float t, int32_t pid, float bt, int32_t bpid, bool tie_high) {
+  return (t < bt) || (t == bt && (tie_high ? pid > bpid : pid < bpid));
+}
+
+// Per-ray traversal with the LDS stack (oracle/rt.c bvh_trace restates it
+// exactly, counters included).  Each step first checks whether every active
+// lane is at the same node / leaf -- the common case for the coherent rays of
+// an 8x8 pixel wave -- and then reads the record ONCE for the wave through
+// the scalar cache into SGPRs (s_load) instead of 64 lanes x 16 B of
+// vector-memory data return per load (the L1 -> VGPR return path, 64 B/clk
+// per CU, was the busiest unit of the all-vector form).  Divergent steps use
+// per-lane buffer loads.  Both forms compute identical values.
+struct NodeStep {
+  int32_t c0, c1;
+  float tn0, tn1;
+  bool h0, h1;
+};
+
+__device__ __forceinline__ NodeStep node_step(const float4& n0, const float4& n1, const float4& n2,
+                                              const float4& n3, const Ray& r, float tmin,
+                                              float lim) {
+  NodeStep o;
+  o.c0 = __float_as_int(n3.x);
+  o.c1 = __float_as_int(n3.y);
+  o.tn0 = 0.0f;
+  o.tn1 = 0.0f;
+  o.h0 = (o.c0 != RT_EMPTY_REF) && slab(n0.x, n0.y, n1.x, n1.y, n2.x, n2.y, r, tmin, lim, &o.tn0);
+  o.h1 = (o.c1 != RT_EMPTY_REF) && slab(n0.z, n0.w, n1.z, n1.w, n2.z, n2.w, r, tmin, lim, &o.tn1);
+  return o;
+}
+
+template <bool ANY>
+__device__ __forceinline__ int32_t trace(const Scene& S, const Ray& r, float tmin, float tmax,
+                                         int32_t skip, bool tie_high, float* t_out,
+                                         int32_t* stack, Counters& cnt) {
+  if (S.num_nodes == 0) return -1;
+  int sp = 0;
+  int32_t ref = 0;
+  float bt = tmax;
+  int32_t bpid = -1;
+  for (;;) {
+    const int32_t r0 = __builtin_amdgcn_readfirstlane(ref);
+    const bool uni = RT_SCALAR && __ballot(ref != r0) == 0;  // wave-uniform branch
+    if (ref >= 0) {
+#ifdef RT_INSTRUMENT
+      ++cnt.visits;
+#endif
+      const float lim = ANY ? tmax : bt;
+      NodeStep st;
+      if (uni) {
+        const uint32_t no = S.nodes + 64u * (uint32_t)r0;
+        st = node_step(S.A.sld_f4(no), S.A.sld_f4(no + 16), S.A.sld_f4(no + 32),
+                       S.A.sld_f4(no + 48), r, tmin, lim);
+      } else {
+        const uint32_t no = S.nodes + 64u * (uint32_t)ref;
+        st = node_step(S.A.ld_f4(no), S.A.ld_f4(no + 16), S.A.ld_f4(no + 32),
+                       S.A.ld_f4(no + 48), r, tmin, lim);
+      }
+      if (st.h0 && st.h1) {
+        const bool swap = st.tn1 < st.tn0;
+        const int32_t near_ref = swap ? st.c1 : st.c0, far_ref = swap ? st.c0 : st.c1;
+        if (sp < RT_MAX_STACK) stack[64 * sp++] = far_ref;
+        ref = near_ref;
+        continue;
+      }
+      if (st.h0) { ref = st.c0; continue; }
+      if (st.h1) { ref = st.c1; continue; }
+    } else {
+      const uint32_t lr = (uint32_t)ref;
+      const uint32_t first = (lr >> 4) & 0x07ffffffu, count = (lr & 15u) + 1u;
+      if (uni) {
+        // one leaf for the whole wave: triangle records in SGPRs, one by one
+        const uint32_t to = S.tris + 48u * first;
+        bool done = false;
+#pragma unroll
+        for (uint32_t k = 0; k < 4; ++k) {
+          if (k < count && !done) {
+            const float4 ta = S.A.sld_f4(to + 48u * k), tb = S.A.sld_f4(to + 48u * k + 16);
+            const float4 tc = S.A.sld_f4(to + 48u * k + 32);
+            const int32_t pid = __float_as_int(ta.w);
+#ifdef RT_INSTRUMENT
+            ++cnt.tests;
+#endif
+            float t;
+            if (pid != skip && mt_hit(r, ta, tb, tc, tmin, &t)) {
+              if (ANY) {
+                if (t < tmax) { bt = t; bpid = pid; done = true; }
+              } else if (closer(t, pid, bt, bpid, tie_high)) {
+                bt = t;
+                bpid = pid;
+              }
+            }
+          }
+        }
+        if (ANY && done) { *t_out = bt; return bpid; }
+      } else {
+        // A leaf's (up to 4) triangles are fetched in one batch -- the tris
+        // array carries 3 padding records.
+        const uint32_t to = S.tris + 48u * first;
+        float4 ta[4], tb[4], tc[4];
+#pragma unroll
+        for (uint32_t k = 0; k < 4; ++k) {
+          ta[k] = S.A.ld_f4(to + 48u * k);
+          tb[k] = S.A.ld_f4(to + 48u * k + 16);
+          tc[k] = S.A.ld_f4(to + 48u * k + 32);
+        }
+#pragma unroll
+        for (uint32_t k = 0; k < 4; ++k) {
+          if (k < count) {
+            const int32_t pid = __float_as_int(ta[k].w);
+#ifdef RT_INSTRUMENT
+            ++cnt.tests;
+#endif
+            float t;
+            if (pid != skip && mt_hit(r, ta[k], tb[k], tc[k], tmin, &t)) {
+              if (ANY) {
+                if (t < tmax) { *t_out = t; return pid; }
+              } else if (closer(t, pid, bt, bpid, tie_high)) {
+                bt = t;
+                bpid = pid;
+              }
+            }
+          }
+        }
+      }
+    }
+    if (sp == 0) break;
+    ref = stack[64 * --sp];
+  }
+  if (bpid >= 0) *t_out = bt;
+  return bpid;
+}
+
+// shade primitive `pid` at (x, y) from per-lane (vector) record loads
+__device__ __forceinline__ uint32_t shade_lane(const Scene& S, int32_t pid, uint32_t x,
+                                               uint32_t y, Counters& cnt) {
+  gfx::Prim p;
+  gfx::load_prim(S.A, S.prims + 128u * (uint32_t)pid, p);
+  const gfx::DcState s = gfx::load_dcstate(S.A, S.dcs + 64u * p.dc());
+#ifdef RT_INSTRUMENT
+  ++cnt.shaded;
+  if (s.flags & RT_DC_TEX) cnt.texel_bytes += (s.filter == VX_TEX_FILTER_BILINEAR ? 4u : 1u) * s.stride;
+#endif
+  return gfx::shade(S.A, p, s, x, y);
+}
+
+// Shade every lane with spid >= 0: the wave's most common primitives first
+// from SGPR records (s_load, one record read per wave -- the background
+// layer's two triangles cover most waves), then whatever is left from
+// per-lane record loads.
+__device__ __forceinline__ uint32_t shade_wave(const Scene& S, int32_t spid, uint32_t x,
+                                               uint32_t y, uint32_t color, Counters& cnt) {
+  uint64_t need = __ballot(spid >= 0);
+#pragma unroll 1
+  for (int it = 0; need != 0 && it < RT_SHADE_UNIFORM; ++it) {
+    const int32_t u = __builtin_amdgcn_readlane(spid, (int)__builtin_ctzll(need));
+    gfx::Prim p;
+    gfx::load_prim<true>(S.A, S.prims + 128u * (uint32_t)u, p);
+    const gfx::DcState s = gfx::load_dcstate<true>(S.A, S.dcs + 64u * p.dc());
+    if (spid == u) {
+      color = gfx::shade(S.A, p, s, x, y);
+#ifdef RT_INSTRUMENT
+      ++cnt.shaded;
+      if (s.flags & RT_DC_TEX) cnt.texel_bytes += (s.filter == VX_TEX_FILTER_BILINEAR ? 4u : 1u) * s.stride;
+#endif
+    }
+    need &= ~__ballot(spid == u);
+  }
+  if (need != 0 && (need & (1ull << lane_id())) != 0) color = shade_lane(S, spid, x, y, cnt);
+  return color;
+}
+
+// Screen layers for lanes with `need` (no geometry hit): highest pid first,
+// the first covering triangle wins (oracle/rt.c rt_row); one wave-uniform
+// triangle per step, its record through the scalar cache.  Returns the pid
+// to shade (layer pid, or `spid` unchanged).
+__device__ __forceinline__ int32_t resolve_layers(const Scene& S, const Ray& r, bool need,
+                                                  int32_t spid, Counters& cnt) {
+  uint64_t pend = __ballot(need);
+  for (uint32_t k = 0; pend != 0 && k < S.num_layer; ++k) {
+    const uint32_t lo = S.layers + 48u * k;
+    const float4 ta = S.A.sld_f4(lo), tb = S.A.sld_f4(lo + 16), tc = S.A.sld_f4(lo + 32);
+    const bool mine = (pend & (1ull << lane_id())) != 0;
+#ifdef RT_INSTRUMENT
+    cnt.layer_tests += mine;
+#endif
+    float tl;
+    const bool f = mine && mt_hit(r, ta, tb, tc, 0.0f, &tl);
+    if (f) spid = __float_as_int(ta.w);
+    pend &= ~__ballot(f);
+  }
+  return spid;
+}
+
+// task -> (shard-local 32x32 tile, 8x8 block, lane) -> pixel
+__device__ __forceinline__ void task_pixel(const Scene& S, uint32_t t, uint32_t* x, uint32_t* y) {
+  const uint32_t lt = t >> 10, blk = (t >> 6) & 15u, ln = t & 63u;
+  const uint32_t gt = S.shard_index + lt * S.shard_count;
+  const uint32_t tx = gt % S.tiles_x, ty = gt / S.tiles_x;
+  *x = (tx << RT_TILE_LOG) + ((blk & 3u) << 3) + (ln & 7u);
+  *y = (ty << RT_TILE_LOG) + ((blk >> 2) << 3) + (ln >> 3);
+}
+
+__device__ __forceinline__ void primary_dir(const Scene& S, uint32_t x, uint32_t y, Ray& r) {
+  r.o[0] = 0.0f; r.o[1] = 0.0f; r.o[2] = 0.0f;
+  r.d[0] = fmaf((float)x + 0.5f, S.sx, -1.0f);
+  r.d[1] = fmaf((float)y + 0.5f, S.sy, -1.0f);
+  r.d[2] = 1.0f;
+}
+
+// shadow segment from the (eye-ward nudged) hit point to the light
+__device__ __forceinline__ void shadow_ray(const Scene& S, const Ray& p, float th, Ray& s) {
+  const float tt = th * 0.999755859375f;  // origin pulled toward the eye by 2^-12 of t
+  s.o[0] = p.d[0] * tt; s.o[1] = p.d[1] * tt; s.o[2] = p.d[2] * tt;
+  s.d[0] = S.light[0] - s.o[0];
+  s.d[1] = S.light[1] - s.o[1];
+  s.d[2] = S.light[2] - s.o[2];
+  ray_setup(s);
+}
+
+__device__ __forceinline__ uint32_t shadowed(uint32_t c) {
+  return (c & 0xff000000u) | ((c >> 1) & 0x007f7f7fu);
+}
+
+__device__ __forceinline__ void store_pixel(const Scene& S, uint32_t t, uint32_t x, uint32_t y,
+                                            uint32_t color) {
+  const uint32_t idx = (S.flags & RT_FLAG_COMPACT) ? t : y * S.width + x;
+  S.A.st_u32(S.cbuf + 4u * idx, color);
+}
+
+
+}  // namespace rtk

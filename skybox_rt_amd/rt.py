@@ -19,6 +19,8 @@ import numpy as np
 from . import _lib
 
 RT_RENDER_SHADOWS = 0x1
+RT_RENDER_PATH = 0x8
+PT_SEED = 0x5EED
 RT_RENDER_INSTRUMENTED = 0x100
 CLEAR_COLOR = 0xFF000000               # draw3d/main.cpp:47
 DEFAULT_LIGHT = (0.0, 60.0, 80.0)      # clip (x, y, w), SURVEY.md 8(d) config 3
@@ -35,7 +37,8 @@ class SceneInfo(C.Structure):
 class RenderParams(C.Structure):
     _fields_ = [("width", C.c_uint32), ("height", C.c_uint32), ("flags", C.c_uint32),
                 ("light", C.c_float * 3), ("clear_color", C.c_uint32),
-                ("shard_index", C.c_uint32), ("shard_count", C.c_uint32)]
+                ("shard_index", C.c_uint32), ("shard_count", C.c_uint32),
+                ("bounces", C.c_uint32), ("seed", C.c_uint32)]
 
 
 class Stats(C.Structure):
@@ -43,7 +46,7 @@ class Stats(C.Structure):
         "primary_rays", "shadow_rays", "geometry_hits", "occluded", "node_visits",
         "tri_tests", "layer_tests", "shaded", "texel_bytes", "tasks")] + [
         ("kernel_ms", C.c_double), ("grid", C.c_uint32), ("block", C.c_uint32),
-        ("num_tasks", C.c_uint32), ("local_tiles", C.c_uint32)]
+        ("num_tasks", C.c_uint32), ("local_tiles", C.c_uint32), ("bounce_rays", C.c_uint64)]
 
     def as_dict(self):
         return {n: getattr(self, n) for n, _ in self._fields_}
@@ -158,10 +161,15 @@ class Renderer:
 
     def configure(self, width: int, height: int, shadows: bool = True, light=DEFAULT_LIGHT,
                   clear_color: int = CLEAR_COLOR, shard_index: int = 0, shard_count: int = 1,
-                  instrumented: bool = False) -> None:
+                  instrumented: bool = False, path: bool = False, bounces: int = 4,
+                  seed: int = PT_SEED) -> None:
+        """path=True: diffuse path trace (pt_kernel; `bounces` segments per
+        path, RNG `seed`) instead of primary + shadow rays."""
         p = RenderParams()
         p.width, p.height = width, height
-        p.flags = (RT_RENDER_SHADOWS if shadows else 0) | (RT_RENDER_INSTRUMENTED if instrumented else 0)
+        p.flags = ((RT_RENDER_SHADOWS if shadows else 0) | (RT_RENDER_INSTRUMENTED if instrumented else 0)
+                   | (RT_RENDER_PATH if path else 0))
+        p.bounces, p.seed = bounces, seed
         p.light[:] = [float(np.float32(x)) for x in light]
         p.clear_color = clear_color
         p.shard_index, p.shard_count = shard_index, shard_count

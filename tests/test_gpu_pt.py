@@ -1,0 +1,82 @@
+"""GPU parity tests of the path tracer (pt_kernel.hip; SURVEY.md 8(a) row A7,
+BASELINE config 4) through the C-ABI against the oracle's restatement
+(oracle/rt.c path_trace): framebuffers and ray counters bit-exact.  No
+reference exists for this row (parity unpinned beyond the oracle)."""
+import numpy as np
+import pytest
+
+from conftest import scene_path
+
+pytestmark = pytest.mark.gpu
+
+from skybox_rt_amd import rt  # noqa: E402
+
+_cache = {}
+
+
+def setup(po, name):
+    if name not in _cache:
+        s = rt.Scene.load(scene_path(name))
+        _cache[name] = (s, rt.Renderer(s), po.OracleScene(po.cgltrace.load(scene_path(name))),
+                        s.bvh())
+    return _cache[name]
+
+
+@pytest.fixture(scope="module")
+def po(oracle_lib):
+    return oracle_lib
+
+
+CASES = [("tekkaman", 128, 4, 0x5EED), ("tekkaman", 256, 4, 0x5EED), ("tekkaman", 1024, 4, 0x5EED),
+         ("tekkaman", 333, 4, 0x5EED), ("tekkaman", 256, 0, 0x5EED), ("tekkaman", 256, 1, 99),
+         ("tekkaman", 256, 8, 3), ("box", 128, 4, 0x5EED), ("scene", 256, 4, 0x5EED),
+         ("carnival", 128, 4, 0x5EED), ("triangle", 64, 4, 0x5EED)]
+
+
+@pytest.mark.parametrize("name,size,bounces,seed", CASES)
+def test_pt_kernel_bit_exact_vs_oracle(po, name, size, bounces, seed):
+    s, r, osc, bvh = setup(po, name)
+    r.configure(size, size, path=True, bounces=bounces, seed=seed)
+    r.render()
+    fb = r.framebuffer()
+    st = r.stats()
+    c, _, _, k = po.rt_render(osc, po.rt_params(size, size, path=True, bounces=bounces, seed=seed,
+                                                nthreads=8), bvh=bvh)
+    assert np.array_equal(fb, c), f"{int((fb != c).sum())} pixels differ"
+    assert st["primary_rays"] == k["primary_rays"] == size * size
+    for key in ("geometry_hits", "shadow_rays", "occluded", "bounce_rays"):
+        assert st[key] == k[key], key
+    assert st["tasks"] == st["num_tasks"]
+
+
+def test_pt_sharded_reassembles(po):
+    s, r, _, _ = setup(po, "tekkaman")
+    W = H = 384
+    r.configure(W, H, path=True)
+    r.render()
+    full = r.framebuffer()
+    parts, rays = [], 0
+    for i in range(3):
+        r.configure(W, H, path=True, shard_index=i, shard_count=3)
+        r.render()
+        parts.append(r.framebuffer().copy())
+        rays += r.stats()["bounce_rays"]
+    r.configure(W, H, path=True)
+    r.render()
+    assert rays == r.stats()["bounce_rays"]
+    assert np.array_equal(rt.deinterleave_tiles(parts, W, H), full)
+
+
+def test_pt_repeatable_and_primary_mode_unaffected(po):
+    s, r, _, _ = setup(po, "tekkaman")
+    r.configure(512, 512, shadows=True)
+    r.render()
+    a = r.framebuffer()
+    r.configure(512, 512, path=True)
+    r.render()
+    p1 = r.framebuffer()
+    r.render()
+    assert np.array_equal(p1, r.framebuffer())
+    r.configure(512, 512, shadows=True)
+    r.render()
+    assert np.array_equal(a, r.framebuffer())
