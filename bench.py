@@ -68,7 +68,8 @@ def frame_side(n_gpus: int, base: int) -> int:
     return max(32, int(round(base * math.sqrt(n_gpus) / 32.0)) * 32)
 
 
-def cpu_baseline(shadows: bool, side: int, light, budget_s: float):
+def cpu_baseline(shadows: bool, side: int, light, budget_s: float, path: bool = False,
+                 bounces: int = 4):
     """Oracle (C port of the same algorithm, oracle/rt.c) on the host cores,
     BVH traversal identical to the kernel's, full frames until budget_s."""
     from oracle import py_oracle as po
@@ -76,12 +77,13 @@ def cpu_baseline(shadows: bool, side: int, light, budget_s: float):
     cores = max(1, min(16, os.cpu_count() or 1))
     osc = po.OracleScene(po.cgltrace.load(SCENE))
     bvh = rtmod.Scene.load(SCENE).bvh()
-    p = po.rt_params(side, side, shadows=shadows, light=light, nthreads=cores)
+    p = po.rt_params(side, side, shadows=shadows, light=light, nthreads=cores, path=path,
+                     bounces=bounces)
     frames, rays, t0 = 0, 0, time.perf_counter()
     while True:
         _, _, _, k = po.rt_render(osc, p, bvh=bvh)
         frames += 1
-        rays += k["primary_rays"] + k["shadow_rays"]
+        rays += k["primary_rays"] + k["shadow_rays"] + k["bounce_rays"]
         el = time.perf_counter() - t0
         if el >= budget_s:
             break
@@ -99,7 +101,12 @@ def main():
     ap.add_argument("--no-shadows", action="store_true")
     ap.add_argument("--cpu-budget", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--workload", choices=("shadow", "path"), default="shadow",
+                    help="shadow: BASELINE config 3 (the metric's config, default); "
+                         "path: config 4, 4-bounce diffuse path trace")
+    ap.add_argument("--bounces", type=int, default=4)
     args = ap.parse_args()
+    path = args.workload == "path"
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -122,13 +129,14 @@ def main():
 
     # algorithmic bytes per launch from the instrumented variant (untimed)
     r.configure(side, side, shadows=shadows, light=light, shard_index=rank, shard_count=n_gpus,
-                instrumented=True)
+                instrumented=True, path=path, bounces=args.bounces)
     r.render()
     inst = r.stats()
     pixels_local = inst["primary_rays"]
     alg_bytes = algorithmic_bytes(inst, pixels_local)
 
-    r.configure(side, side, shadows=shadows, light=light, shard_index=rank, shard_count=n_gpus)
+    r.configure(side, side, shadows=shadows, light=light, shard_index=rank, shard_count=n_gpus,
+                path=path, bounces=args.bounces)
     gather = None
     if world > 1:
         import ctypes
@@ -182,7 +190,7 @@ def main():
         dist.barrier()
     elapsed = time.perf_counter() - t0
     st = r.stats()
-    rays_local = st["primary_rays"] + st["shadow_rays"]
+    rays_local = st["primary_rays"] + st["shadow_rays"] + st["bounce_rays"]
     if dist is not None:
         t = torch.tensor([elapsed, float(rays_local)], dtype=torch.float64, device="cuda")
         mx = t.clone()
@@ -199,8 +207,14 @@ def main():
     if rank != 0:
         dist.destroy_process_group()
         return
+    metric = "Mrays/sec per GPU + achieved HBM GB/s, 1024^2 primary+shadow tekkaman"
+    kind = "primary+shadow rays"
+    if path:
+        metric = (f"Mrays/sec per GPU + achieved HBM GB/s, 1024^2 {args.bounces}-bounce diffuse "
+                  f"path trace tekkaman (BASELINE config 4)")
+        kind = f"{args.bounces}-bounce diffuse path trace (primary + bounce + shadow rays)"
     out = {
-        "metric": "Mrays/sec per GPU + achieved HBM GB/s, 1024^2 primary+shadow tekkaman",
+        "metric": metric,
         "value": round(value, 3),
         "unit": "Mrays/s",
         "n_gpus": n_gpus,
@@ -213,8 +227,9 @@ def main():
         "dtype": "f32",
         "data": "tekkaman.cgltrace from the reference's regression data (tests/golden/scenes)",
         "config": {
-            "workload": f"{side}x{side} {'primary+shadow' if shadows else 'primary'} rays, "
-                        f"tekkaman.cgltrace, BVH2 + LDS stack",
+            "workload": (f"{side}x{side} {kind}, tekkaman.cgltrace, BVH2 + LDS stack" if path else
+                         f"{side}x{side} {'primary+shadow' if shadows else 'primary'} rays, "
+                         f"tekkaman.cgltrace, BVH2 + LDS stack"),
             "scene": "tekkaman.cgltrace", "width": side, "height": side,
             "shadow_rays": shadows, "light_clip_xyw": list(light),
             "parallelism": f"tiles32 mod {n_gpus}" + (" + rccl gather" if n_gpus > 1 else ""),
@@ -227,16 +242,19 @@ def main():
         },
         "roofline": {
             "bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-            "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": pmc_traffic(side, shadows),
+            "frac": round(achieved / HBM_PEAK_GBS, 4),
+            "traffic": None if path else pmc_traffic(side, shadows),
             "algorithmic_bytes_per_launch": int(alg_bytes),
             "counts": {k: int(inst[k]) for k in ("node_visits", "tri_tests", "layer_tests",
-                                                 "texel_bytes", "primary_rays", "shadow_rays")},
+                                                 "texel_bytes", "primary_rays", "shadow_rays",
+                                                 "bounce_rays")},
         },
         "cpu_baseline": None,
     }
     if n_gpus == 1 and not args.no_cpu_baseline:
         try:
-            out["cpu_baseline"] = cpu_baseline(shadows, side, light, args.cpu_budget)
+            out["cpu_baseline"] = cpu_baseline(shadows, side, light, args.cpu_budget, path,
+                                               args.bounces)
         except Exception as e:  # the baseline is reported, not required
             log(f"cpu baseline failed: {e}")
     print(json.dumps(out), flush=True)

@@ -64,7 +64,8 @@ struct rt_scene {
 struct rt_renderer {
   rt_scene* sc = nullptr;
   vx_device_h dev = nullptr;
-  vx_buffer_h krnl[3] = {nullptr, nullptr, nullptr};  // rt, rt instrumented, path trace
+  // rt, rt instrumented, path trace, path trace instrumented
+  vx_buffer_h krnl[4] = {nullptr, nullptr, nullptr, nullptr};
   vx_buffer_h nodes = nullptr, tris = nullptr, layers = nullptr, dcs = nullptr, tex = nullptr;
   vx_buffer_h ptris = nullptr;
   vx_buffer_h prims = nullptr, cbuf = nullptr, args = nullptr;
@@ -78,7 +79,7 @@ struct rt_renderer {
   vx_hip_last_run_t last_run = nullptr;
 
   ~rt_renderer() {
-    vx_buffer_h* bufs[] = {&krnl[0], &krnl[1], &krnl[2], &nodes, &tris, &layers, &dcs, &tex,
+    vx_buffer_h* bufs[] = {&krnl[0], &krnl[1], &krnl[2], &krnl[3], &nodes, &tris, &layers, &dcs, &tex,
                            &ptris, &prims, &cbuf, &args};
     for (auto* b : bufs) {
       if (*b) vx_mem_free(*b);
@@ -215,10 +216,11 @@ int rt_renderer_create(rt_scene_h s, const char* kernel_dir, rt_renderer_h* out)
   // the regular image's LDS stack covers BVH depth <= 16; deeper trees use the
   // deep image (32 entries, lower occupancy)
   const bool deep = s->bvh.depth > RT_STACK_SHALLOW;
-  const char* names[3] = {deep ? "rt_kernel_deep.vxbin" : "rt_kernel.vxbin",
+  const char* names[4] = {deep ? "rt_kernel_deep.vxbin" : "rt_kernel.vxbin",
                           deep ? "rt_kernel_deep_stats.vxbin" : "rt_kernel_stats.vxbin",
-                          deep ? "pt_kernel_deep.vxbin" : "pt_kernel.vxbin"};
-  for (int i = 0; i < 3; ++i)
+                          deep ? "pt_kernel_deep.vxbin" : "pt_kernel.vxbin",
+                          deep ? "pt_kernel_deep_stats.vxbin" : "pt_kernel_stats.vxbin"};
+  for (int i = 0; i < 4; ++i)
     if (vx_upload_kernel_file(r->dev, (dir + "/" + names[i]).c_str(), &r->krnl[i]) != 0)
       return fail("cannot upload kernel " + dir + "/" + names[i]);
   r->mem_ptr = (vx_hip_mem_ptr_t)vx_driver_symbol("vx_hip_mem_ptr");
@@ -365,8 +367,8 @@ int rt_renderer_configure(rt_renderer_h r, const rt_render_params_t* p) {
 
 int rt_render_start(rt_renderer_h r) {
   if (!r || !r->configured) return fail("renderer not configured");
-  const int k = (r->params.flags & RT_RENDER_PATH) ? 2
-                : (r->params.flags & RT_RENDER_INSTRUMENTED) ? 1 : 0;
+  const int k = ((r->params.flags & RT_RENDER_PATH) ? 2 : 0) +
+                ((r->params.flags & RT_RENDER_INSTRUMENTED) ? 1 : 0);
   return vx_start(r->dev, r->krnl[k], r->args) == 0 ? 0 : fail("vx_start failed");
 }
 

@@ -242,6 +242,11 @@ __device__ __forceinline__ void vertex(const Scene& S, PtLds& L, int qi, uint32_
     gfx::Prim p;
     gfx::load_prim(S.A, S.prims + 128u * (uint32_t)np, p);
     const gfx::DcState st = gfx::load_dcstate(S.A, S.dcs + 64u * p.dc());
+#ifdef RT_INSTRUMENT
+    ++cnt.shaded;
+    if (st.flags & RT_DC_TEX)
+      cnt.texel_bytes += (st.filter == VX_TEX_FILTER_BILINEAR ? 4u : 1u) * st.stride;
+#endif
     const uint32_t a = gfx::shade_weights(S.A, p, st, gfx::fx_from_float_dev((1.0f - b1) - b2, 24),
                                           gfx::fx_from_float_dev(b1, 24));
     const float k255 = 1.0f / 255.0f;

@@ -80,3 +80,16 @@ def test_pt_repeatable_and_primary_mode_unaffected(po):
     r.configure(512, 512, shadows=True)
     r.render()
     assert np.array_equal(a, r.framebuffer())
+
+
+def test_pt_instrumented_counters_equal_oracle_traversal(po):
+    s, r, osc, bvh = setup(po, "tekkaman")
+    for size in (256, 1024):
+        r.configure(size, size, path=True, instrumented=True)
+        r.render()
+        st = r.stats()
+        c, _, _, k = po.rt_render(osc, po.rt_params(size, size, path=True, nthreads=8), bvh=bvh)
+        for key in ("node_visits", "tri_tests", "layer_tests", "shaded", "texel_bytes",
+                    "shadow_rays", "bounce_rays", "occluded"):
+            assert st[key] == k[key], key
+        assert np.array_equal(r.framebuffer(), c)
