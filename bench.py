@@ -105,6 +105,8 @@ def main():
                     help="shadow: BASELINE config 3 (the metric's config, default); "
                          "path: config 4, 4-bounce diffuse path trace")
     ap.add_argument("--bounces", type=int, default=4)
+    ap.add_argument("--verify-gather", action="store_true",
+                    help="N>1: rank 0 checks the gathered frame against its own full render")
     args = ap.parse_args()
     path = args.workload == "path"
 
@@ -114,10 +116,19 @@ def main():
     n_gpus = max(world, 1)
     dist = None
     import torch
+    # RCCL ("nccl") between the GPUs; BENCH_DIST_BACKEND=gloo rehearses the
+    # multi-rank flow with host-staged gathers (e.g. several ranks on one GPU)
+    backend = os.environ.get("BENCH_DIST_BACKEND", "nccl")
+    coll_dev = torch.device("cpu")
     if world > 1:
         import torch.distributed as dist
-        torch.cuda.set_device(local_rank)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+        dev_index = local_rank % max(1, torch.cuda.device_count())
+        torch.cuda.set_device(dev_index)
+        if backend == "nccl":
+            coll_dev = torch.device("cuda", dev_index)
+            dist.init_process_group("nccl", device_id=coll_dev)
+        else:
+            dist.init_process_group(backend)
     from skybox_rt_amd import rt
 
     shadows = not args.no_shadows
@@ -140,35 +151,17 @@ def main():
     gather = None
     if world > 1:
         import ctypes
+        from skybox_rt_amd.shard import FrameGather
         hip = ctypes.CDLL("libamdhip64.so.7")  # torch's runtime, already loaded
-        tiles_x = (side + 31) // 32
-        total_tiles = tiles_x * tiles_x
-        max_local = (total_tiles + n_gpus - 1) // n_gpus
-        local = torch.empty(max_local * 1024, dtype=torch.int32, device="cuda")
-        parts = [torch.empty_like(local) for _ in range(n_gpus)] if rank == 0 else None
-        # de-interleave map on rank 0: image index for every (rank, local tile, task)
-        if rank == 0:
-            g = np.arange(n_gpus)[:, None, None]
-            lt = np.arange(max_local)[None, :, None]
-            t = np.arange(1024)[None, None, :]
-            gt = g + lt * n_gpus
-            blk, ln = t >> 6, t & 63
-            y = (gt // tiles_x) * 32 + (blk >> 2) * 8 + (ln >> 3)
-            x = (gt % tiles_x) * 32 + (blk & 3) * 8 + (ln & 7)
-            valid = (gt < total_tiles) & (x < side) & (y < side)
-            src = np.nonzero(valid.reshape(-1))[0]
-            dst = (y * side + x).reshape(-1)[src]
-            src_t = torch.from_numpy(src).cuda()
-            dst_t = torch.from_numpy(dst).cuda()
-            image = torch.empty(side * side, dtype=torch.int32, device="cuda")
+        fg = FrameGather(dist, side, side, coll_dev)
         dev_ptr, nbytes = r.framebuffer_device()
+        kind = 3 if coll_dev.type == "cuda" else 2  # hipMemcpyDeviceToDevice / ToHost
 
         def gather():
-            hip.hipMemcpy(ctypes.c_void_p(local.data_ptr()), ctypes.c_void_p(dev_ptr),
-                          ctypes.c_size_t(nbytes), 3)
-            dist.gather(local, parts, dst=0)
-            if rank == 0:
-                image[dst_t] = torch.stack(parts).reshape(-1)[src_t]
+            # copy of the compact tile buffer into the gather's buffer, then the gather
+            hip.hipMemcpy(ctypes.c_void_p(fg.local.data_ptr()), ctypes.c_void_p(dev_ptr),
+                          ctypes.c_size_t(nbytes), kind)
+            fg()
 
     def step():
         r.render()
@@ -192,7 +185,7 @@ def main():
     st = r.stats()
     rays_local = st["primary_rays"] + st["shadow_rays"] + st["bounce_rays"]
     if dist is not None:
-        t = torch.tensor([elapsed, float(rays_local)], dtype=torch.float64, device="cuda")
+        t = torch.tensor([elapsed, float(rays_local)], dtype=torch.float64, device=coll_dev)
         mx = t.clone()
         dist.all_reduce(mx, op=dist.ReduceOp.MAX)
         sm = t.clone()
@@ -204,6 +197,13 @@ def main():
     value = rays_total * args.steps / elapsed / 1e6
     avg_kernel_ms = float(np.mean(kernel_ms))
     achieved = alg_bytes / (avg_kernel_ms * 1e-3) / 1e9
+    gather_ok = None
+    if gather is not None and args.verify_gather and rank == 0:
+        r.configure(side, side, shadows=shadows, light=light, path=path, bounces=args.bounces)
+        r.render()
+        full = r.framebuffer().reshape(-1).view(np.int32)
+        gather_ok = bool(np.array_equal(fg.image.cpu().numpy(), full))
+        log(f"gathered frame == full render: {gather_ok}")
     if rank != 0:
         dist.destroy_process_group()
         return
@@ -232,7 +232,8 @@ def main():
                          f"tekkaman.cgltrace, BVH2 + LDS stack"),
             "scene": "tekkaman.cgltrace", "width": side, "height": side,
             "shadow_rays": shadows, "light_clip_xyw": list(light),
-            "parallelism": f"tiles32 mod {n_gpus}" + (" + rccl gather" if n_gpus > 1 else ""),
+            "parallelism": f"tiles32 mod {n_gpus}" + (f" + {'rccl' if backend == 'nccl' else backend} "
+                                                      f"gather" if n_gpus > 1 else ""),
             "bvh_nodes": info["bvh_nodes"], "bvh_depth": info["bvh_depth"],
             "grid": st["grid"], "block": st["block"],
             "rays_per_frame": int(rays_total),
@@ -251,6 +252,8 @@ def main():
         },
         "cpu_baseline": None,
     }
+    if gather_ok is not None:
+        out["config"]["gather_verified"] = gather_ok
     if n_gpus == 1 and not args.no_cpu_baseline:
         try:
             out["cpu_baseline"] = cpu_baseline(shadows, side, light, args.cpu_budget, path,

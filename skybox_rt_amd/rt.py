@@ -238,16 +238,5 @@ class Renderer:
 def deinterleave_tiles(shards, width: int, height: int) -> np.ndarray:
     """Assemble per-rank compact tile buffers (rank r holds tiles t with
     t % G == r, each 32x32 in 8x8-block/lane task order) into a W x H image."""
-    G = len(shards)
-    tx, ty = (width + TILE - 1) // TILE, (height + TILE - 1) // TILE
-    img = np.zeros((ty * TILE, tx * TILE), np.uint32)
-    for r, buf in enumerate(shards):
-        tiles = np.asarray(buf, np.uint32).reshape(-1, 4, 4, 8, 8)  # [lt][by][bx][y][x]
-        tiles = tiles.transpose(0, 1, 3, 2, 4).reshape(-1, TILE, TILE)
-        for lt, tile in enumerate(tiles):
-            gt = r + lt * G
-            if gt >= tx * ty:
-                break
-            y0, x0 = (gt // tx) * TILE, (gt % tx) * TILE
-            img[y0:y0 + TILE, x0:x0 + TILE] = tile
-    return img[:height, :width]
+    from .shard import deinterleave_tiles as _d
+    return _d(shards, width, height)
