@@ -69,7 +69,7 @@ def frame_side(n_gpus: int, base: int) -> int:
 
 
 def cpu_baseline(shadows: bool, side: int, light, budget_s: float, path: bool = False,
-                 bounces: int = 4):
+                 bounces: int = 4, flat: bool = False):
     """Oracle (C port of the same algorithm, oracle/rt.c) on the host cores,
     BVH traversal identical to the kernel's, full frames until budget_s."""
     from oracle import py_oracle as po
@@ -81,7 +81,7 @@ def cpu_baseline(shadows: bool, side: int, light, budget_s: float, path: bool = 
                      bounces=bounces)
     frames, rays, t0 = 0, 0, time.perf_counter()
     while True:
-        _, _, _, k = po.rt_render(osc, p, bvh=bvh)
+        _, _, _, k = po.rt_render(osc, p, bvh=None if flat else bvh)
         frames += 1
         rays += k["primary_rays"] + k["shadow_rays"] + k["bounce_rays"]
         el = time.perf_counter() - t0
@@ -89,7 +89,8 @@ def cpu_baseline(shadows: bool, side: int, light, budget_s: float, path: bool = 
             break
     return {"value": rays / el / 1e6, "unit": "Mrays/s", "cores": cores, "kind": "port",
             "sample": f"{frames} full {side}x{side} frames of the same workload "
-                      f"({el:.1f} s, oracle/rt.c BVH traversal, {cores} threads)"}
+                      f"({el:.1f} s, oracle/rt.c {'brute force' if flat else 'BVH traversal'}, "
+                      f"{cores} threads)"}
 
 
 def main():
@@ -101,15 +102,20 @@ def main():
     ap.add_argument("--no-shadows", action="store_true")
     ap.add_argument("--cpu-budget", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--workload", choices=("shadow", "path"), default="shadow",
+    ap.add_argument("--workload", choices=("shadow", "path", "flat"), default="shadow",
                     help="shadow: BASELINE config 3 (the metric's config, default); "
-                         "path: config 4, 4-bounce diffuse path trace")
+                         "path: config 4, 4-bounce diffuse path trace; "
+                         "flat: config 2, 256^2 primary rays over the flat triangle list")
     ap.add_argument("--bounces", type=int, default=4)
     ap.add_argument("--verify-gather", action="store_true",
                     help="N>1: rank 0 checks the gathered frame against its own full render")
     args = ap.parse_args()
     path = args.workload == "path"
-
+    flat = args.workload == "flat"
+    if flat and args.size == 1024:
+        args.size = 256  # config 2 resolution
+    if flat:
+        args.no_shadows = True
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
@@ -140,14 +146,14 @@ def main():
 
     # algorithmic bytes per launch from the instrumented variant (untimed)
     r.configure(side, side, shadows=shadows, light=light, shard_index=rank, shard_count=n_gpus,
-                instrumented=True, path=path, bounces=args.bounces)
+                instrumented=True, path=path, bounces=args.bounces, flat=flat)
     r.render()
     inst = r.stats()
     pixels_local = inst["primary_rays"]
     alg_bytes = algorithmic_bytes(inst, pixels_local)
 
     r.configure(side, side, shadows=shadows, light=light, shard_index=rank, shard_count=n_gpus,
-                path=path, bounces=args.bounces)
+                path=path, bounces=args.bounces, flat=flat)
     gather = None
     if world > 1:
         import ctypes
@@ -199,7 +205,8 @@ def main():
     achieved = alg_bytes / (avg_kernel_ms * 1e-3) / 1e9
     gather_ok = None
     if gather is not None and args.verify_gather and rank == 0:
-        r.configure(side, side, shadows=shadows, light=light, path=path, bounces=args.bounces)
+        r.configure(side, side, shadows=shadows, light=light, path=path, bounces=args.bounces,
+                    flat=flat)
         r.render()
         full = r.framebuffer().reshape(-1).view(np.int32)
         gather_ok = bool(np.array_equal(fg.image.cpu().numpy(), full))
@@ -213,6 +220,10 @@ def main():
         metric = (f"Mrays/sec per GPU + achieved HBM GB/s, 1024^2 {args.bounces}-bounce diffuse "
                   f"path trace tekkaman (BASELINE config 4)")
         kind = f"{args.bounces}-bounce diffuse path trace (primary + bounce + shadow rays)"
+    if flat:
+        metric = (f"Mrays/sec per GPU + achieved HBM GB/s, {side}^2 primary rays, tekkaman flat "
+                  f"triangle list, no BVH (BASELINE config 2)")
+        kind = "primary rays, flat triangle list (no BVH, LDS-staged)"
     out = {
         "metric": metric,
         "value": round(value, 3),
@@ -227,7 +238,8 @@ def main():
         "dtype": "f32",
         "data": "tekkaman.cgltrace from the reference's regression data (tests/golden/scenes)",
         "config": {
-            "workload": (f"{side}x{side} {kind}, tekkaman.cgltrace, BVH2 + LDS stack" if path else
+            "workload": (f"{side}x{side} {kind}, tekkaman.cgltrace" if flat else
+                         f"{side}x{side} {kind}, tekkaman.cgltrace, BVH2 + LDS stack" if path else
                          f"{side}x{side} {'primary+shadow' if shadows else 'primary'} rays, "
                          f"tekkaman.cgltrace, BVH2 + LDS stack"),
             "scene": "tekkaman.cgltrace", "width": side, "height": side,
@@ -244,7 +256,7 @@ def main():
         "roofline": {
             "bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBS, 4),
-            "traffic": None if path else pmc_traffic(side, shadows),
+            "traffic": None if (path or flat) else pmc_traffic(side, shadows),
             "algorithmic_bytes_per_launch": int(alg_bytes),
             "counts": {k: int(inst[k]) for k in ("node_visits", "tri_tests", "layer_tests",
                                                  "texel_bytes", "primary_rays", "shadow_rays",
@@ -257,7 +269,7 @@ def main():
     if n_gpus == 1 and not args.no_cpu_baseline:
         try:
             out["cpu_baseline"] = cpu_baseline(shadows, side, light, args.cpu_budget, path,
-                                               args.bounces)
+                                               args.bounces, flat)
         except Exception as e:  # the baseline is reported, not required
             log(f"cpu baseline failed: {e}")
     print(json.dumps(out), flush=True)

@@ -32,6 +32,7 @@ typedef struct {
 
 #define RT_RENDER_SHADOWS 0x1u
 #define RT_RENDER_PATH 0x8u            /* diffuse path trace (pt_kernel), `bounces` segments */
+#define RT_RENDER_FLAT 0x10u           /* flat triangle list, no BVH (config 2; rt_flat) */
 #define RT_RENDER_INSTRUMENTED 0x100u  /* use the counting kernel variant */
 
 typedef struct {

@@ -64,10 +64,11 @@ struct rt_scene {
 struct rt_renderer {
   rt_scene* sc = nullptr;
   vx_device_h dev = nullptr;
-  // rt, rt instrumented, path trace, path trace instrumented
-  vx_buffer_h krnl[4] = {nullptr, nullptr, nullptr, nullptr};
+  // kernel images [mode][instrumented]: mode 0 = primary+shadow (BVH),
+  // 1 = path trace, 2 = flat list
+  vx_buffer_h krnl[3][2] = {};
   vx_buffer_h nodes = nullptr, tris = nullptr, layers = nullptr, dcs = nullptr, tex = nullptr;
-  vx_buffer_h ptris = nullptr;
+  vx_buffer_h ptris = nullptr, geom = nullptr;
   vx_buffer_h prims = nullptr, cbuf = nullptr, args = nullptr;
   uint64_t cbuf_bytes = 0;
   rt_render_params_t params{};
@@ -79,8 +80,9 @@ struct rt_renderer {
   vx_hip_last_run_t last_run = nullptr;
 
   ~rt_renderer() {
-    vx_buffer_h* bufs[] = {&krnl[0], &krnl[1], &krnl[2], &krnl[3], &nodes, &tris, &layers, &dcs, &tex,
-                           &ptris, &prims, &cbuf, &args};
+    vx_buffer_h* bufs[] = {&krnl[0][0], &krnl[0][1], &krnl[1][0], &krnl[1][1], &krnl[2][0],
+                           &krnl[2][1], &nodes, &tris, &layers, &dcs, &tex, &ptris, &geom,
+                           &prims, &cbuf, &args};
     for (auto* b : bufs) {
       if (*b) vx_mem_free(*b);
       *b = nullptr;
@@ -216,13 +218,16 @@ int rt_renderer_create(rt_scene_h s, const char* kernel_dir, rt_renderer_h* out)
   // the regular image's LDS stack covers BVH depth <= 16; deeper trees use the
   // deep image (32 entries, lower occupancy)
   const bool deep = s->bvh.depth > RT_STACK_SHALLOW;
-  const char* names[4] = {deep ? "rt_kernel_deep.vxbin" : "rt_kernel.vxbin",
-                          deep ? "rt_kernel_deep_stats.vxbin" : "rt_kernel_stats.vxbin",
-                          deep ? "pt_kernel_deep.vxbin" : "pt_kernel.vxbin",
-                          deep ? "pt_kernel_deep_stats.vxbin" : "pt_kernel_stats.vxbin"};
-  for (int i = 0; i < 4; ++i)
-    if (vx_upload_kernel_file(r->dev, (dir + "/" + names[i]).c_str(), &r->krnl[i]) != 0)
-      return fail("cannot upload kernel " + dir + "/" + names[i]);
+  const char* names[3][2] = {
+      {deep ? "rt_kernel_deep.vxbin" : "rt_kernel.vxbin",
+       deep ? "rt_kernel_deep_stats.vxbin" : "rt_kernel_stats.vxbin"},
+      {deep ? "pt_kernel_deep.vxbin" : "pt_kernel.vxbin",
+       deep ? "pt_kernel_deep_stats.vxbin" : "pt_kernel_stats.vxbin"},
+      {"rt_flat.vxbin", "rt_flat_stats.vxbin"}};
+  for (int m = 0; m < 3; ++m)
+    for (int i = 0; i < 2; ++i)
+      if (vx_upload_kernel_file(r->dev, (dir + "/" + names[m][i]).c_str(), &r->krnl[m][i]) != 0)
+        return fail("cannot upload kernel " + dir + "/" + names[m][i]);
   r->mem_ptr = (vx_hip_mem_ptr_t)vx_driver_symbol("vx_hip_mem_ptr");
   r->stream = (vx_hip_stream_t)vx_driver_symbol("vx_hip_stream");
   r->last_run = (vx_hip_last_run_t)vx_driver_symbol("vx_hip_last_run");
@@ -267,6 +272,11 @@ int rt_renderer_create(rt_scene_h s, const char* kernel_dir, rt_renderer_h* out)
     std::memcpy(&pt[g].v[3], &pid, 4);
   }
   if (upload(r->dev, pt.data(), pt.size() * sizeof(rt_tri_t), &r->ptris, &a.ptris_addr)) return -1;
+  // the geometry triangles in ascending pid order (flat-list mode)
+  std::vector<rt_tri_t> gl;
+  for (int32_t g : s->geometry) gl.push_back(pt[g]);
+  if (upload(r->dev, gl.data(), gl.size() * sizeof(rt_tri_t), &r->geom, &a.geom_addr)) return -1;
+  a.num_geom = (uint32_t)gl.size();
   a.num_layer_tris = (uint32_t)lt.size();
   // textures: one buffer, each texture 256-B aligned
   std::vector<uint8_t> texels;
@@ -316,6 +326,8 @@ int rt_renderer_configure(rt_renderer_h r, const rt_render_params_t* p) {
   if (p->width == 0 || p->height == 0 || p->width > 32768 || p->height > 32768)
     return fail("bad resolution");
   const uint32_t shards = p->shard_count ? p->shard_count : 1;
+  if ((p->flags & RT_RENDER_PATH) && (p->flags & RT_RENDER_FLAT))
+    return fail("RT_RENDER_PATH and RT_RENDER_FLAT are exclusive");
   if (p->shard_index >= shards) return fail("shard_index >= shard_count");
   const rt_scene* s = r->sc;
   r->params = *p;
@@ -345,6 +357,7 @@ int rt_renderer_configure(rt_renderer_h r, const rt_render_params_t* p) {
   a.shard_count = shards;
   a.flags = ((p->flags & RT_RENDER_SHADOWS) ? RT_FLAG_SHADOWS : 0u) |
             ((p->flags & RT_RENDER_PATH) ? RT_FLAG_PATH : 0u) |
+            ((p->flags & RT_RENDER_FLAT) ? RT_FLAG_FLAT : 0u) |
             (s->tie_high ? RT_FLAG_TIE_HIGH : 0u) | (shards > 1 ? RT_FLAG_COMPACT : 0u);
   a.bounces = p->bounces;
   a.seed = p->seed;
@@ -367,9 +380,10 @@ int rt_renderer_configure(rt_renderer_h r, const rt_render_params_t* p) {
 
 int rt_render_start(rt_renderer_h r) {
   if (!r || !r->configured) return fail("renderer not configured");
-  const int k = ((r->params.flags & RT_RENDER_PATH) ? 2 : 0) +
-                ((r->params.flags & RT_RENDER_INSTRUMENTED) ? 1 : 0);
-  return vx_start(r->dev, r->krnl[k], r->args) == 0 ? 0 : fail("vx_start failed");
+  const uint32_t f = r->params.flags;
+  const int mode = (f & RT_RENDER_PATH) ? 1 : (f & RT_RENDER_FLAT) ? 2 : 0;
+  const int k = (f & RT_RENDER_INSTRUMENTED) ? 1 : 0;
+  return vx_start(r->dev, r->krnl[mode][k], r->args) == 0 ? 0 : fail("vx_start failed");
 }
 
 int rt_render_wait(rt_renderer_h r) {

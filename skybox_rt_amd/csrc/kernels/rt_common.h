@@ -9,6 +9,7 @@
 //   prims   [num_prims]  rt_prim_t  128 B  fixed-point shading record
 //   dcs     [num_dc]     rt_dcstate_t 64 B per-drawcall shading state
 //   ptris   [num_prims]  rt_tri_t    48 B  clip-space triangle by pid
+//   geom    [num_geom]   rt_tri_t    48 B  geometry triangles, ascending pid (flat)
 //   cbuf    W*H*4 (linear, row 0 = NDC y=-1) or tiles*1024*4 (compact shard)
 #pragma once
 
@@ -35,6 +36,7 @@
 #define RT_FLAG_TIE_HIGH 0x2u    // LEQUAL geometry: equal t -> highest pid
 #define RT_FLAG_COMPACT  0x4u    // shard output: compact tile buffer
 #define RT_FLAG_PATH     0x8u    // diffuse path trace (pt_kernel.hip)
+#define RT_FLAG_FLAT     0x10u   // flat triangle list, no BVH (BASELINE config 2)
 
 #define RT_DC_DEPTH   0x1u
 #define RT_DC_COLOR   0x2u
@@ -78,12 +80,13 @@ typedef struct {
 typedef struct {
   uint64_t cbuf_addr, nodes_addr, tris_addr, layers_addr, prims_addr, dcs_addr;
   uint64_t ptris_addr;     // rt_tri_t per pid (path trace: bounce-hit barycentrics)
-  uint64_t pad0;
+  uint64_t geom_addr;      // rt_tri_t of the geometry prims, ascending pid (flat mode)
   uint32_t width, height, tiles_x, tiles_y;
   uint32_t num_tasks, num_nodes, num_layer_tris, flags;
   uint32_t clear_color, shard_index, shard_count, bounces;
   float sx, sy;            // 2/W, 2/H
   float light[3];
   uint32_t seed;           // path-trace RNG seed
-  uint32_t pad2[2];
+  uint32_t num_geom;       // geometry triangles (flat mode)
+  uint32_t pad2;
 } rt_kernel_arg_t;

@@ -28,8 +28,14 @@
 #include "rt_trace.h"
 
 
+// RT_FLAT: config-2 image -- brute force over the LDS-staged geometry list
+// instead of the BVH (no traversal stack, no shadow queue)
+#ifndef RT_FLAT
+#define RT_FLAT 0
+#endif
+#define RT_FLAT_CAP 1024  // triangles staged in LDS (48 KB); longer lists stream via s_load
 #ifndef RT_SHADOW_QUEUE
-#define RT_SHADOW_QUEUE 1
+#define RT_SHADOW_QUEUE (!RT_FLAT)
 #endif
 
 namespace {
@@ -42,7 +48,9 @@ constexpr int kWaves = RT_BLOCK_THREADS / 64;
 // compaction queue of deferred shadow rays.
 #define RT_QUEUE 128
 struct WaveLds {
+#if !RT_FLAT
   int32_t stack[RT_MAX_STACK][64];
+#endif
 #if RT_SHADOW_QUEUE
   uint32_t q_task[RT_QUEUE];
   float q_t[RT_QUEUE];
@@ -52,18 +60,34 @@ struct WaveLds {
 #endif
 };
 
+#if RT_FLAT
+__shared__ float4 s_geom[RT_FLAT_CAP * 3];
+// staged geometry list, or nullptr when it does not fit
+__device__ __forceinline__ const float4* flat_list(const Scene& S) {
+  return S.num_geom <= RT_FLAT_CAP ? s_geom : nullptr;
+}
+#endif
+
 // closest / any hit for lanes with `active` (all 64 lanes call these)
 __device__ __forceinline__ int32_t trace_closest(const Scene& S, const Ray& r, bool tie_high,
                                                  bool active, float* th, WaveLds& w,
                                                  Counters& cnt) {
   if (!active) return -1;
+#if RT_FLAT
+  return trace_flat<false>(S, r, 0.0f, INFINITY, -1, tie_high, th, flat_list(S), cnt);
+#else
   return trace<false>(S, r, 0.0f, INFINITY, -1, tie_high, th, &w.stack[0][lane_id()], cnt);
+#endif
 }
 __device__ __forceinline__ bool occluded(const Scene& S, const Ray& s, int32_t skip, bool tie_high,
                                          bool active, WaveLds& w, Counters& cnt) {
   float ts;
   if (!active) return false;
+#if RT_FLAT
+  return trace_flat<true>(S, s, 0.0f, 1.0f, skip, tie_high, &ts, flat_list(S), cnt) >= 0;
+#else
   return trace<true>(S, s, 0.0f, 1.0f, skip, tie_high, &ts, &w.stack[0][lane_id()], cnt) >= 0;
+#endif
 }
 
 __device__ __forceinline__ void kernel_body(const vx_task_t& task, const Scene& S, WaveLds& w,
@@ -173,6 +197,15 @@ VX_MAIN(rt_kernel_arg_t, arg, RT_BLOCK_THREADS) {
   WaveLds& w = s_wave[threadIdx.x >> 6];
   Counters cnt;
   const Scene S = load_scene(arg);
+#if RT_FLAT
+  // stage the geometry list once per workgroup (workgroups past the last
+  // task chunk have nothing to render and skip it)
+  if (S.num_geom <= RT_FLAT_CAP && blockIdx.x * blockDim.x < arg->num_tasks) {
+    for (uint32_t i = threadIdx.x; i < 3u * S.num_geom; i += blockDim.x)
+      s_geom[i] = S.A.ld_f4(S.geom + 16u * i);
+  }
+  __syncthreads();
+#endif
 #if RT_SHADOW_QUEUE
   if ((threadIdx.x & 63u) == 0) w.q_count = 0;
   __builtin_amdgcn_wave_barrier();

@@ -38,8 +38,8 @@ struct Counters {
 // arena offsets (rt_app checks every buffer lies below 4 GiB).
 struct Scene {
   vx_arena A;
-  uint32_t nodes, tris, layers, prims, dcs, cbuf, ptris;
-  uint32_t num_nodes, num_layer, flags, width, height;
+  uint32_t nodes, tris, layers, prims, dcs, cbuf, ptris, geom;
+  uint32_t num_nodes, num_layer, num_geom, flags, width, height;
   uint32_t shard_index, shard_count, tiles_x, clear_color, bounces, seed;
   float sx, sy, light[3];
 };
@@ -54,6 +54,8 @@ __device__ __forceinline__ Scene load_scene(const rt_kernel_arg_t* a) {
   s.dcs = (uint32_t)a->dcs_addr;
   s.cbuf = (uint32_t)a->cbuf_addr;
   s.ptris = (uint32_t)a->ptris_addr;
+  s.geom = (uint32_t)a->geom_addr;
+  s.num_geom = a->num_geom;
   s.bounces = a->bounces;
   s.seed = a->seed;
   s.num_nodes = a->num_nodes;
@@ -267,6 +269,45 @@ __device__ __forceinline__ int32_t trace(const Scene& S, const Ray& r, float tmi
     }
     if (sp == 0) break;
     ref = stack[64 * --sp];
+  }
+  if (bpid >= 0) *t_out = bt;
+  return bpid;
+}
+
+// Flat triangle list, no BVH (BASELINE config 2; the oracle's brute_trace):
+// every lane tests every geometry triangle in ascending pid order -- the
+// same triangle in all lanes at once, so the records come from LDS (`lds`,
+// staged once per workgroup) as broadcast reads, or through the scalar cache
+// when the list does not fit (`lds` == nullptr).  Counters count every
+// triangle visited, as brute_trace does.
+template <bool ANY>
+__device__ __forceinline__ int32_t trace_flat(const Scene& S, const Ray& r, float tmin, float tmax,
+                                              int32_t skip, bool tie_high, float* t_out,
+                                              const float4* lds, Counters& cnt) {
+  float bt = tmax;
+  int32_t bpid = -1;
+  for (uint32_t k = 0; k < S.num_geom; ++k) {
+    float4 ta, tb, tc;
+    if (lds) {
+      ta = lds[3 * k]; tb = lds[3 * k + 1]; tc = lds[3 * k + 2];
+    } else {
+      const uint32_t o = S.geom + 48u * k;
+      ta = S.A.sld_f4(o); tb = S.A.sld_f4(o + 16); tc = S.A.sld_f4(o + 32);
+    }
+    const int32_t pid = __float_as_int(ta.w);
+#ifdef RT_INSTRUMENT
+    ++cnt.tests;
+#endif
+    if (pid == skip) continue;
+    float t;
+    if (mt_hit(r, ta, tb, tc, tmin, &t)) {
+      if (ANY) {
+        if (t < tmax) { *t_out = t; return pid; }
+      } else if (closer(t, pid, bt, bpid, tie_high)) {
+        bt = t;
+        bpid = pid;
+      }
+    }
   }
   if (bpid >= 0) *t_out = bt;
   return bpid;

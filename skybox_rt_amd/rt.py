@@ -20,6 +20,7 @@ from . import _lib
 
 RT_RENDER_SHADOWS = 0x1
 RT_RENDER_PATH = 0x8
+RT_RENDER_FLAT = 0x10
 PT_SEED = 0x5EED
 RT_RENDER_INSTRUMENTED = 0x100
 CLEAR_COLOR = 0xFF000000               # draw3d/main.cpp:47
@@ -162,13 +163,14 @@ class Renderer:
     def configure(self, width: int, height: int, shadows: bool = True, light=DEFAULT_LIGHT,
                   clear_color: int = CLEAR_COLOR, shard_index: int = 0, shard_count: int = 1,
                   instrumented: bool = False, path: bool = False, bounces: int = 4,
-                  seed: int = PT_SEED) -> None:
+                  seed: int = PT_SEED, flat: bool = False) -> None:
         """path=True: diffuse path trace (pt_kernel; `bounces` segments per
-        path, RNG `seed`) instead of primary + shadow rays."""
+        path, RNG `seed`) instead of primary + shadow rays.  flat=True: the
+        flat triangle list without BVH (BASELINE config 2)."""
         p = RenderParams()
         p.width, p.height = width, height
         p.flags = ((RT_RENDER_SHADOWS if shadows else 0) | (RT_RENDER_INSTRUMENTED if instrumented else 0)
-                   | (RT_RENDER_PATH if path else 0))
+                   | (RT_RENDER_PATH if path else 0) | (RT_RENDER_FLAT if flat else 0))
         p.bounces, p.seed = bounces, seed
         p.light[:] = [float(np.float32(x)) for x in light]
         p.clear_color = clear_color
