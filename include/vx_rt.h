@@ -33,6 +33,8 @@ typedef struct {
 #define RT_RENDER_SHADOWS 0x1u
 #define RT_RENDER_PATH 0x8u            /* diffuse path trace (pt_kernel), `bounces` segments */
 #define RT_RENDER_FLAT 0x10u           /* flat triangle list, no BVH (config 2; rt_flat) */
+#define RT_RENDER_RASTER 0x20u         /* the draw3d raster pipeline (raster_kernel): any
+                                          scene incl. blending/stencil; shard_count 1 */
 #define RT_RENDER_INSTRUMENTED 0x100u  /* use the counting kernel variant */
 
 typedef struct {
@@ -70,7 +72,9 @@ int rt_scene_setup_prims(rt_scene_h scene, uint32_t width, uint32_t height, int3
                          uint64_t count);
 
 /* kernel_dir: directory holding rt_kernel.vxbin / rt_kernel_stats.vxbin
- * (NULL = next to librtapp.so).  Opens its own vortex device. */
+ * (NULL = next to librtapp.so).  Opens its own vortex device.  Scenes the
+ * RT path cannot trace (blending, stencil, layers after geometry) get a
+ * renderer that accepts only RT_RENDER_RASTER. */
 int rt_renderer_create(rt_scene_h scene, const char* kernel_dir, rt_renderer_h* out);
 int rt_renderer_free(rt_renderer_h r);
 int rt_renderer_configure(rt_renderer_h r, const rt_render_params_t* params);
@@ -83,6 +87,9 @@ int rt_render_kernel_ms(rt_renderer_h r, double* kernel_ms);
 /* linear W*H framebuffer (shard_count == 1) or compact tile buffer
  * (local_tiles * 1024 pixels in task order) */
 int rt_read_framebuffer(rt_renderer_h r, uint32_t* out, uint64_t count);
+
+/* RT_RENDER_RASTER: the depth/stencil buffer (stencil << 24 | depth), W*H */
+int rt_read_depthbuffer(rt_renderer_h r, uint32_t* out, uint64_t count);
 
 /* device pointer + byte size of the output buffer (for RCCL gathers) and the
  * HIP stream the kernel runs on (for stream-ordered consumers) */

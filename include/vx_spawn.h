@@ -225,7 +225,8 @@ __device__ __forceinline__ int vx_spawn_tasks_ex(uint32_t num_tasks, F kernel_fu
  * consecutive tasks per step (wave w: tasks step*blockDim + 64w ..+63, the
  * same 64-task chunks as above), steps are block-uniform, and every thread
  * calls kernel_func(task, valid, arg) -- valid = false past num_tasks -- and
- * then block_epilogue(arg), which may use __syncthreads(). */
+ * then block_epilogue(step, arg), which may use __syncthreads() (step =
+ * the block step: tasks step * blockDim.x ...). */
 template <typename F, typename E, typename Arg>
 __device__ __forceinline__ int vx_spawn_tasks_block(uint32_t num_tasks, F kernel_func,
                                                     E block_epilogue, Arg* arg) {
@@ -241,7 +242,7 @@ __device__ __forceinline__ int vx_spawn_tasks_block(uint32_t num_tasks, F kernel
     const bool valid = t < num_tasks;
     kernel_func(task, valid, arg);
     ran += valid;
-    block_epilogue(arg);
+    block_epilogue(st, arg);
   }
   vx_mpm_add(VX_MPM_TASKS, ran);
   return 0;

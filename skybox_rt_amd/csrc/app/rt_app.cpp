@@ -11,6 +11,7 @@
 #include <dlfcn.h>
 
 #include <algorithm>
+#include <cstdio>
 #include <chrono>
 #include <map>
 #include <cstring>
@@ -65,10 +66,10 @@ struct rt_renderer {
   rt_scene* sc = nullptr;
   vx_device_h dev = nullptr;
   // kernel images [mode][instrumented]: mode 0 = primary+shadow (BVH),
-  // 1 = path trace, 2 = flat list
-  vx_buffer_h krnl[3][2] = {};
+  // 1 = path trace, 2 = flat list, 3 = raster (no instrumented image)
+  vx_buffer_h krnl[4][2] = {};
   vx_buffer_h nodes = nullptr, tris = nullptr, layers = nullptr, dcs = nullptr, tex = nullptr;
-  vx_buffer_h ptris = nullptr, geom = nullptr;
+  vx_buffer_h ptris = nullptr, geom = nullptr, oms = nullptr, bbox = nullptr, zbuf = nullptr;
   vx_buffer_h prims = nullptr, cbuf = nullptr, args = nullptr;
   uint64_t cbuf_bytes = 0;
   rt_render_params_t params{};
@@ -81,8 +82,8 @@ struct rt_renderer {
 
   ~rt_renderer() {
     vx_buffer_h* bufs[] = {&krnl[0][0], &krnl[0][1], &krnl[1][0], &krnl[1][1], &krnl[2][0],
-                           &krnl[2][1], &nodes, &tris, &layers, &dcs, &tex, &ptris, &geom,
-                           &prims, &cbuf, &args};
+                           &krnl[2][1], &krnl[3][0], &nodes, &tris, &layers, &dcs, &tex,
+                           &ptris, &geom, &oms, &bbox, &zbuf, &prims, &cbuf, &args};
     for (auto* b : bufs) {
       if (*b) vx_mem_free(*b);
       *b = nullptr;
@@ -207,7 +208,6 @@ static int upload(vx_device_h dev, const void* data, uint64_t size, vx_buffer_h*
 
 int rt_renderer_create(rt_scene_h s, const char* kernel_dir, rt_renderer_h* out) {
   if (!s || !out) return fail("null argument");
-  if (!s->unsupported.empty()) return fail("scene not supported by the RT path: " + s->unsupported, -2);
   auto r = std::make_unique<rt_renderer>();
   r->sc = s;
   if (vx_dev_open(&r->dev) != 0) {
@@ -218,16 +218,24 @@ int rt_renderer_create(rt_scene_h s, const char* kernel_dir, rt_renderer_h* out)
   // the regular image's LDS stack covers BVH depth <= 16; deeper trees use the
   // deep image (32 entries, lower occupancy)
   const bool deep = s->bvh.depth > RT_STACK_SHALLOW;
-  const char* names[3][2] = {
+  const char* names[4][2] = {
       {deep ? "rt_kernel_deep.vxbin" : "rt_kernel.vxbin",
        deep ? "rt_kernel_deep_stats.vxbin" : "rt_kernel_stats.vxbin"},
       {deep ? "pt_kernel_deep.vxbin" : "pt_kernel.vxbin",
        deep ? "pt_kernel_deep_stats.vxbin" : "pt_kernel_stats.vxbin"},
-      {"rt_flat.vxbin", "rt_flat_stats.vxbin"}};
-  for (int m = 0; m < 3; ++m)
-    for (int i = 0; i < 2; ++i)
-      if (vx_upload_kernel_file(r->dev, (dir + "/" + names[m][i]).c_str(), &r->krnl[m][i]) != 0)
-        return fail("cannot upload kernel " + dir + "/" + names[m][i]);
+      {"rt_flat.vxbin", "rt_flat_stats.vxbin"},
+      {"raster_kernel.vxbin", nullptr}};
+  // images missing from kernel_dir (e.g. an A/B variant directory holding
+  // only rt_kernel*) come from the library directory
+  for (int m = 0; m < 4; ++m)
+    for (int i = 0; i < 2; ++i) {
+      if (!names[m][i]) continue;
+      std::string path = dir + "/" + names[m][i];
+      if (FILE* f = std::fopen(path.c_str(), "rb")) std::fclose(f);
+      else path = lib_dir() + "/" + names[m][i];
+      if (vx_upload_kernel_file(r->dev, path.c_str(), &r->krnl[m][i]) != 0)
+        return fail("cannot upload kernel " + path);
+    }
   r->mem_ptr = (vx_hip_mem_ptr_t)vx_driver_symbol("vx_hip_mem_ptr");
   r->stream = (vx_hip_stream_t)vx_driver_symbol("vx_hip_stream");
   r->last_run = (vx_hip_last_run_t)vx_driver_symbol("vx_hip_last_run");
@@ -295,6 +303,11 @@ int rt_renderer_create(rt_scene_h s, const char* kernel_dir, rt_renderer_h* out)
     dcs.push_back(st);
   }
   if (upload(r->dev, dcs.data(), dcs.size() * sizeof(rt_dcstate_t), &r->dcs, &a.dcs_addr)) return -1;
+  // output-merger state per drawcall (raster pipeline)
+  std::vector<rt_omstate_t> oms;
+  for (const rt::DrawCall& dc : s->scene.drawcalls) oms.push_back(rt::OmState(dc));
+  if (upload(r->dev, oms.data(), oms.size() * sizeof(rt_omstate_t), &r->oms, &a.oms_addr)) return -1;
+  a.num_drawcalls = (uint32_t)oms.size();
   *out = r.release();
   return 0;
 }
@@ -326,8 +339,13 @@ int rt_renderer_configure(rt_renderer_h r, const rt_render_params_t* p) {
   if (p->width == 0 || p->height == 0 || p->width > 32768 || p->height > 32768)
     return fail("bad resolution");
   const uint32_t shards = p->shard_count ? p->shard_count : 1;
-  if ((p->flags & RT_RENDER_PATH) && (p->flags & RT_RENDER_FLAT))
-    return fail("RT_RENDER_PATH and RT_RENDER_FLAT are exclusive");
+  const uint32_t modes = p->flags & (RT_RENDER_PATH | RT_RENDER_FLAT | RT_RENDER_RASTER);
+  if (modes & (modes - 1)) return fail("RT_RENDER_PATH / FLAT / RASTER are exclusive");
+  const bool raster = (p->flags & RT_RENDER_RASTER) != 0;
+  if (!raster && !r->sc->unsupported.empty())
+    return fail("scene not supported by the RT path (use RT_RENDER_RASTER): " + r->sc->unsupported, -2);
+  if (raster && (shards > 1 || (p->flags & RT_RENDER_INSTRUMENTED)))
+    return fail("RT_RENDER_RASTER renders whole frames, uninstrumented");
   if (p->shard_index >= shards) return fail("shard_index >= shard_count");
   const rt_scene* s = r->sc;
   r->params = *p;
@@ -346,18 +364,38 @@ int rt_renderer_configure(rt_renderer_h r, const rt_render_params_t* p) {
   }
   if (upload(r->dev, prims.data(), prims.size() * sizeof(rt_prim_t), &r->prims, &a.prims_addr))
     return -1;
+  if (raster) {
+    // per-resolution screen boxes; degenerate / culled primitives get an
+    // empty box and are never binned (gfxutil.cpp:195-232)
+    std::vector<rt_bbox_t> bb(s->scene.prims.size());
+    for (size_t d = 0; d < s->scene.drawcalls.size(); ++d) {
+      const rt::DrawCall& dc = s->scene.drawcalls[d];
+      for (uint32_t i = 0; i < dc.prim_count; ++i) {
+        const uint32_t g = dc.prim_offset + i;
+        rt_prim_t tmp;
+        const bool degen = rt::PrimSetup(s->scene.prims[g], p->width, p->height, dc.viewport[4],
+                                         dc.viewport[5], &tmp) == rt::kSetupDegenerate;
+        if (rt::PrimBBox(s->scene.prims[g], p->width, p->height, &bb[g]) != rt::kSetupOk || degen)
+          bb[g].x = bb[g].y = 0;
+      }
+    }
+    if (upload(r->dev, bb.data(), bb.size() * sizeof(rt_bbox_t), &r->bbox, &a.bbox_addr)) return -1;
+    std::vector<uint32_t> zclear((size_t)p->width * p->height, 0xffffffffu);  // main.cpp:48
+    if (upload(r->dev, zclear.data(), zclear.size() * 4, &r->zbuf, &a.zbuf_addr)) return -1;
+  }
   a.width = p->width;
   a.height = p->height;
   a.tiles_y = (p->height + 31) >> RT_TILE_LOG;
   a.tiles_x = (p->width + 31) >> RT_TILE_LOG;
   const uint32_t tiles = a.tiles_x * a.tiles_y;
   r->local_tiles = (tiles > p->shard_index) ? (tiles - p->shard_index + shards - 1) / shards : 0;
-  a.num_tasks = r->local_tiles * RT_TILE_PIXELS;
+  a.num_tasks = r->local_tiles * (raster ? RT_TILE_PIXELS / 4 : RT_TILE_PIXELS);  // raster: 2x2 quads
   a.shard_index = p->shard_index;
   a.shard_count = shards;
   a.flags = ((p->flags & RT_RENDER_SHADOWS) ? RT_FLAG_SHADOWS : 0u) |
             ((p->flags & RT_RENDER_PATH) ? RT_FLAG_PATH : 0u) |
             ((p->flags & RT_RENDER_FLAT) ? RT_FLAG_FLAT : 0u) |
+            (raster ? RT_FLAG_RASTER : 0u) |
             (s->tie_high ? RT_FLAG_TIE_HIGH : 0u) | (shards > 1 ? RT_FLAG_COMPACT : 0u);
   a.bounces = p->bounces;
   a.seed = p->seed;
@@ -381,8 +419,8 @@ int rt_renderer_configure(rt_renderer_h r, const rt_render_params_t* p) {
 int rt_render_start(rt_renderer_h r) {
   if (!r || !r->configured) return fail("renderer not configured");
   const uint32_t f = r->params.flags;
-  const int mode = (f & RT_RENDER_PATH) ? 1 : (f & RT_RENDER_FLAT) ? 2 : 0;
-  const int k = (f & RT_RENDER_INSTRUMENTED) ? 1 : 0;
+  const int mode = (f & RT_RENDER_PATH) ? 1 : (f & RT_RENDER_FLAT) ? 2 : (f & RT_RENDER_RASTER) ? 3 : 0;
+  const int k = (f & RT_RENDER_INSTRUMENTED) && mode != 3 ? 1 : 0;
   return vx_start(r->dev, r->krnl[mode][k], r->args) == 0 ? 0 : fail("vx_start failed");
 }
 
@@ -435,6 +473,14 @@ int rt_read_framebuffer(rt_renderer_h r, uint32_t* out, uint64_t count) {
   if (!r || !out || !r->configured) return fail("renderer not configured");
   if (count * 4 < r->cbuf_bytes) return fail("buffer too small");
   return vx_copy_from_dev(out, r->cbuf, 0, r->cbuf_bytes) == 0 ? 0 : fail("vx_copy_from_dev failed");
+}
+
+int rt_read_depthbuffer(rt_renderer_h r, uint32_t* out, uint64_t count) {
+  if (!r || !out || !r->configured) return fail("renderer not configured");
+  if (!r->zbuf || !(r->params.flags & RT_RENDER_RASTER)) return fail("no depth buffer (raster mode only)");
+  const uint64_t n = (uint64_t)r->params.width * r->params.height;
+  if (count < n) return fail("buffer too small");
+  return vx_copy_from_dev(out, r->zbuf, 0, n * 4) == 0 ? 0 : fail("vx_copy_from_dev failed");
 }
 
 int rt_framebuffer_device(rt_renderer_h r, void** ptr, uint64_t* bytes) {

@@ -141,4 +141,113 @@ rt_dcstate_t DrawcallState(const DrawCall& dc, const Scene& scene) {
   return s;
 }
 
+int PrimBBox(const std::array<Vertex, 3>& v, uint32_t width, uint32_t height, rt_bbox_t* out) {
+  const Viewport vp = MakeViewport(width, height, 0.0f, 1.0f);
+  float l = 0, r = 0, t = 0, b = 0;
+  for (int i = 0; i < 3; ++i) {  // ClipToScreen x, y (oracle clip_to_screen)
+    const float* p = v[i].pos;
+    const float rhw = 1.0f / p[3];
+    const float x = (p[0] * rhw) * vp.sx + vp.cx, y = (p[1] * rhw) * vp.sy + vp.cy;
+    if (i == 0) {
+      l = r = x;
+      t = b = y;
+    } else {
+      l = std::fmin(l, x); r = std::fmax(r, x);
+      t = std::fmin(t, y); b = std::fmax(b, y);
+    }
+  }
+  int32_t L = (int32_t)std::floor(l), R = (int32_t)std::ceil(r);
+  int32_t T = (int32_t)std::floor(t), B = (int32_t)std::ceil(b);
+  L = L > 0 ? L : 0;
+  R = R < (int32_t)width ? R : (int32_t)width;
+  T = T > 0 ? T : 0;
+  B = B < (int32_t)height ? B : (int32_t)height;
+  if (R <= L || B <= T) {
+    out->x = out->y = 0;
+    return kSetupCulled;
+  }
+  out->x = (uint32_t)L | ((uint32_t)R << 16);
+  out->y = (uint32_t)T | ((uint32_t)B << 16);
+  return kSetupOk;
+}
+
+namespace {
+uint32_t ToVXStencilOp(int32_t c) {  // gfxutil.cpp:353-366
+  static const uint32_t m[6] = {VX_OM_STENCIL_OP_KEEP, VX_OM_STENCIL_OP_REPLACE,
+                                VX_OM_STENCIL_OP_INCR, VX_OM_STENCIL_OP_DECR,
+                                VX_OM_STENCIL_OP_ZERO, VX_OM_STENCIL_OP_INVERT};
+  return (c >= 0 && c < 6) ? m[c] : VX_OM_STENCIL_OP_KEEP;
+}
+uint32_t ToVXBlend(int32_t c) {  // gfxutil.cpp:368-386
+  static const uint32_t m[11] = {VX_OM_BLEND_FUNC_ZERO, VX_OM_BLEND_FUNC_ONE,
+                                 VX_OM_BLEND_FUNC_SRC_RGB, VX_OM_BLEND_FUNC_ONE_MINUS_SRC_RGB,
+                                 VX_OM_BLEND_FUNC_SRC_A, VX_OM_BLEND_FUNC_ONE_MINUS_SRC_A,
+                                 VX_OM_BLEND_FUNC_DST_A, VX_OM_BLEND_FUNC_ONE_MINUS_DST_A,
+                                 VX_OM_BLEND_FUNC_DST_RGB, VX_OM_BLEND_FUNC_ONE_MINUS_DST_RGB,
+                                 VX_OM_BLEND_FUNC_ALPHA_SAT};
+  return (c >= 0 && c < 11) ? m[c] : VX_OM_BLEND_FUNC_ONE;
+}
+}  // namespace
+
+rt_omstate_t OmState(const DrawCall& dc) {
+  // draw3d/main.cpp:223-284 DCR writes, then DepthTencil / Blender configure
+  // (graphics.cpp:534-620) and OutputMerger::configure (gpu_sw.h:78-98)
+  rt_omstate_t s;
+  std::memset(&s, 0, sizeof(s));
+  const States& st = dc.states;
+  uint32_t depth_func = VX_OM_DEPTH_FUNC_ALWAYS, depth_wm = 0;
+  if (st.depth_test) {
+    depth_func = ToVXCompare(st.depth_func);
+    depth_wm = (uint32_t)st.depth_writemask & 1u;
+  }
+  uint32_t sf = VX_OM_DEPTH_FUNC_ALWAYS, szp = VX_OM_STENCIL_OP_KEEP, szf = 0;
+  uint32_t sfail = VX_OM_STENCIL_OP_KEEP, sref = 0, smask = VX_OM_STENCIL_MASK, swm = 0;
+  if (st.stencil_test) {
+    sf = ToVXCompare(st.stencil_func);
+    szp = ToVXStencilOp(st.stencil_zfail);  // quirk: ZPASS written twice, ZFAIL never (:251-260)
+    szf = 0;
+    sfail = ToVXStencilOp(st.stencil_fail);
+    sref = (uint32_t)st.stencil_ref;
+    smask = (uint32_t)st.stencil_mask;
+    swm = (uint32_t)st.stencil_writemask;
+  }
+  uint32_t blend_func = (VX_OM_BLEND_FUNC_ZERO << 24) | (VX_OM_BLEND_FUNC_ZERO << 16) |
+                        (VX_OM_BLEND_FUNC_ONE << 8) | VX_OM_BLEND_FUNC_ONE;
+  if (st.blend_enabled) {
+    const uint32_t bs = ToVXBlend(st.blend_src), bd = ToVXBlend(st.blend_dst);
+    blend_func = (bd << 24) | (bd << 16) | (bs << 8) | bs;
+  }
+  s.depth_func = depth_func;
+  s.depth_writemask = depth_wm;
+  s.depth_test_on = !((depth_func == VX_OM_DEPTH_FUNC_ALWAYS) && !depth_wm);
+  s.stencil_func = sf & 0xffff;
+  s.stencil_zpass = szp & 0xffff;
+  s.stencil_zfail = szf & 0xffff;
+  s.stencil_fail = sfail & 0xffff;
+  s.stencil_ref = sref & 0xffff;
+  s.stencil_mask = smask & 0xffff;
+  s.stencil_writemask = swm & 0xffff;
+  s.stencil_on = !((s.stencil_func == VX_OM_DEPTH_FUNC_ALWAYS) &&
+                   (s.stencil_zpass == VX_OM_STENCIL_OP_KEEP) &&
+                   (s.stencil_zfail == VX_OM_STENCIL_OP_KEEP));
+  s.blend_mode_rgb = VX_OM_BLEND_MODE_ADD;
+  s.blend_mode_a = VX_OM_BLEND_MODE_ADD;
+  s.blend_src_rgb = blend_func & 0xff;
+  s.blend_src_a = (blend_func >> 8) & 0xff;
+  s.blend_dst_rgb = (blend_func >> 16) & 0xff;
+  s.blend_dst_a = (blend_func >> 24) & 0xff;
+  s.blend_const = 0;
+  s.logic_op = 0;
+  s.blend_on = !((s.blend_src_rgb == VX_OM_BLEND_FUNC_ONE) && (s.blend_src_a == VX_OM_BLEND_FUNC_ONE) &&
+                 (s.blend_dst_rgb == VX_OM_BLEND_FUNC_ZERO) && (s.blend_dst_a == VX_OM_BLEND_FUNC_ZERO));
+  const uint32_t wm = st.color_writemask & 0xf;
+  s.cbuf_writemask = ((wm >> 0) & 1) * 0x000000ffu | ((wm >> 1) & 1) * 0x0000ff00u |
+                     ((wm >> 2) & 1) * 0x00ff0000u | ((wm >> 3) & 1) * 0xff000000u;
+  s.color_read = wm != 0xf;
+  s.color_write = wm != 0x0;
+  s.prim_offset = dc.prim_offset;
+  s.prim_count = dc.prim_count;
+  return s;
+}
+
 }  // namespace rt

@@ -36,4 +36,11 @@ int PrimSetup(const std::array<Vertex, 3>& v, uint32_t width, uint32_t height, f
 // Shading state of a drawcall (texture address filled by the caller).
 rt_dcstate_t DrawcallState(const DrawCall& dc, const Scene& scene);
 
+// Screen bounding box of a triangle at width x height (gfxutil.cpp:209-232);
+// returns kSetupCulled (and an empty box) when it misses the viewport.
+int PrimBBox(const std::array<Vertex, 3>& v, uint32_t width, uint32_t height, rt_bbox_t* out);
+
+// Output-merger state of a drawcall (raster pipeline).
+rt_omstate_t OmState(const DrawCall& dc);
+
 }  // namespace rt

@@ -192,7 +192,9 @@ __device__ __forceinline__ int32_t edge_eval(const int32_t* e, uint32_t x, uint3
 // INTERPOLATE / TEXTURING / MODULATE (draw3d/kernel.cpp:48-79).  Path-trace
 // bounce hits enter here with MT barycentrics (oracle/gfx.c orc_shade_weights).
 __device__ __forceinline__ uint32_t shade_weights(const vx_arena& A, const Prim& p,
-                                                  const DcState& s, int32_t dx, int32_t dy) {
+                                                  const DcState& s, int32_t dx, int32_t dy,
+                                                  uint32_t* depth = nullptr) {
+  if (depth) *depth = (s.flags & RT_DC_DEPTH) ? (uint32_t)interp(p.attr(0), dx, dy) : 0u;
   int32_t cr = 1 << 24, cg = 1 << 24, cb = 1 << 24, ca = 1 << 24;
   if (s.flags & RT_DC_COLOR) {
     cr = interp(p.attr(1), dx, dy);
@@ -215,14 +217,160 @@ __device__ __forceinline__ uint32_t shade_weights(const vx_arena& A, const Prim&
 
 // draw3d shader for one fragment at pixel (x, y) of primitive p
 // (draw3d/kernel.cpp:232-279; GRADIENTS_SW reinterprets Q15.16 as Q7.24).
-__device__ __forceinline__ uint32_t shade(const vx_arena& A, const Prim& p, const DcState& s,
-                                          uint32_t x, uint32_t y) {
-  const int32_t F0 = edge_eval(p.edge(0), x, y);
-  const int32_t F1 = edge_eval(p.edge(1), x, y);
-  const int32_t F2 = edge_eval(p.edge(2), x, y);
+// ... from the three raw Q15.16 edge values at the fragment (GRADIENTS_SW,
+// draw3d/kernel.cpp:37-44); *depth = interpolated Q7.24 z word
+__device__ __forceinline__ uint32_t shade_edges(const vx_arena& A, const Prim& p, const DcState& s,
+                                                int32_t F0, int32_t F1, int32_t F2,
+                                                uint32_t* depth = nullptr) {
   const float f0 = fx_to_float(F0, 24), f1 = fx_to_float(F1, 24), f2 = fx_to_float(F2, 24);
   const float r = 1.0f / (f0 + f1 + f2);
-  return shade_weights(A, p, s, fx_from_float_dev(r * f0, 24), fx_from_float_dev(r * f1, 24));
+  return shade_weights(A, p, s, fx_from_float_dev(r * f0, 24), fx_from_float_dev(r * f1, 24),
+                       depth);
+}
+__device__ __forceinline__ uint32_t shade(const vx_arena& A, const Prim& p, const DcState& s,
+                                          uint32_t x, uint32_t y) {
+  return shade_edges(A, p, s, edge_eval(p.edge(0), x, y), edge_eval(p.edge(1), x, y),
+                     edge_eval(p.edge(2), x, y));
+}
+
+// ---- output merger: graphics.cpp:320-636 + gpu_sw.h:100-168 (oracle/gfx.c
+// orc_om_write), for a pixel whose colour and depth/stencil words live in
+// registers of the thread that owns the pixel ----
+__device__ __forceinline__ bool om_compare(uint32_t func, uint32_t a, uint32_t b) {
+  switch (func) {
+  case VX_OM_DEPTH_FUNC_NEVER: return false;
+  case VX_OM_DEPTH_FUNC_LESS: return a < b;
+  case VX_OM_DEPTH_FUNC_EQUAL: return a == b;
+  case VX_OM_DEPTH_FUNC_LEQUAL: return a <= b;
+  case VX_OM_DEPTH_FUNC_GREATER: return a > b;
+  case VX_OM_DEPTH_FUNC_NOTEQUAL: return a != b;
+  case VX_OM_DEPTH_FUNC_GEQUAL: return a >= b;
+  default: return true;
+  }
+}
+__device__ __forceinline__ uint32_t om_stencil_op(uint32_t op, uint32_t ref, uint32_t val) {
+  switch (op) {
+  case VX_OM_STENCIL_OP_ZERO: return 0;
+  case VX_OM_STENCIL_OP_REPLACE: return ref;
+  case VX_OM_STENCIL_OP_INCR: return (val < 0xff) ? (val + 1) : val;
+  case VX_OM_STENCIL_OP_DECR: return (val > 0) ? (val - 1) : val;
+  case VX_OM_STENCIL_OP_INVERT: return ~val;
+  case VX_OM_STENCIL_OP_INCR_WRAP: return (val + 1) & 0xff;
+  case VX_OM_STENCIL_OP_DECR_WRAP: return (val - 1) & 0xff;
+  default: return val;
+  }
+}
+__device__ __forceinline__ uint32_t div255(int x) { return (uint32_t)((x + (x >> 8)) >> 8); }
+struct Argb {
+  uint32_t a, r, g, b;
+};
+__device__ __forceinline__ Argb argb(uint32_t v) { return {v >> 24, (v >> 16) & 0xff, (v >> 8) & 0xff, v & 0xff}; }
+__device__ __forceinline__ Argb mk(uint32_t a, uint32_t r, uint32_t g, uint32_t b) {
+  return {a & 0xff, r & 0xff, g & 0xff, b & 0xff};
+}
+__device__ __forceinline__ Argb blend_factor(uint32_t f, Argb s, Argb d, Argb c) {
+  switch (f) {
+  case VX_OM_BLEND_FUNC_ZERO: return mk(0, 0, 0, 0);
+  case VX_OM_BLEND_FUNC_ONE: return mk(0xff, 0xff, 0xff, 0xff);
+  case VX_OM_BLEND_FUNC_SRC_RGB: return s;
+  case VX_OM_BLEND_FUNC_ONE_MINUS_SRC_RGB: return mk(0xff - s.a, 0xff - s.r, 0xff - s.g, 0xff - s.b);
+  case VX_OM_BLEND_FUNC_DST_RGB: return d;
+  case VX_OM_BLEND_FUNC_ONE_MINUS_DST_RGB: return mk(0xff - d.a, 0xff - d.r, 0xff - d.g, 0xff - d.b);
+  case VX_OM_BLEND_FUNC_SRC_A: return mk(s.a, s.a, s.a, s.a);
+  case VX_OM_BLEND_FUNC_ONE_MINUS_SRC_A: return mk(0xff - s.a, 0xff - s.a, 0xff - s.a, 0xff - s.a);
+  case VX_OM_BLEND_FUNC_DST_A: return mk(d.a, d.a, d.a, d.a);
+  case VX_OM_BLEND_FUNC_ONE_MINUS_DST_A: return mk(0xff - d.a, 0xff - d.a, 0xff - d.a, 0xff - d.a);
+  case VX_OM_BLEND_FUNC_CONST_RGB: return c;
+  case VX_OM_BLEND_FUNC_ONE_MINUS_CONST_RGB: return mk(0xff - c.a, 0xff - c.r, 0xff - c.g, 0xff - c.b);
+  case VX_OM_BLEND_FUNC_CONST_A: return mk(c.a, c.a, c.a, c.a);
+  case VX_OM_BLEND_FUNC_ONE_MINUS_CONST_A: return mk(0xff - c.a, 0xff - c.r, 0xff - c.g, 0xff - c.b);
+  case VX_OM_BLEND_FUNC_ALPHA_SAT: {
+    const uint32_t f2 = s.a < (0xff - d.a) ? s.a : (0xff - d.a);
+    return mk(0xff, f2, f2, f2);
+  }
+  default: return mk(0, 0, 0, 0);
+  }
+}
+__device__ __forceinline__ uint32_t logic_op(uint32_t op, uint32_t s, uint32_t d) {
+  switch (op) {
+  case 0: return 0; case 1: return s & d; case 2: return s & ~d; case 3: return s;
+  case 4: return ~s & d; case 5: return d; case 6: return s ^ d; case 7: return s | d;
+  case 8: return ~(s | d); case 9: return ~(s ^ d); case 10: return ~d;
+  case 11: return s | ~d; case 12: return ~s; case 13: return ~s | d;
+  case 14: return ~(s & d); default: return 0xffffffffu;
+  }
+}
+__device__ __forceinline__ int imin(int a, int b) { return a < b ? a : b; }
+__device__ __forceinline__ int imax(int a, int b) { return a > b ? a : b; }
+__device__ __forceinline__ Argb blend_mode(uint32_t mode, uint32_t lop, Argb src, Argb dst, Argb s,
+                                           Argb d, uint32_t srcv, uint32_t dstv) {
+  switch (mode) {
+  case VX_OM_BLEND_MODE_SUB:
+    return mk(div255(imax((int)(src.a * s.a) - (int)(dst.a * d.a) + 0x80, 0)),
+              div255(imax((int)(src.r * s.r) - (int)(dst.r * d.r) + 0x80, 0)),
+              div255(imax((int)(src.g * s.g) - (int)(dst.g * d.g) + 0x80, 0)),
+              div255(imax((int)(src.b * s.b) - (int)(dst.b * d.b) + 0x80, 0)));
+  case VX_OM_BLEND_MODE_REV_SUB:
+    return mk(div255(imax((int)(dst.a * d.a) - (int)(src.a * s.a) + 0x80, 0)),
+              div255(imax((int)(dst.r * d.r) - (int)(src.r * s.r) + 0x80, 0)),
+              div255(imax((int)(dst.g * d.g) - (int)(src.g * s.g) + 0x80, 0)),
+              div255(imax((int)(dst.b * d.b) - (int)(src.b * s.b) + 0x80, 0)));
+  case VX_OM_BLEND_MODE_MIN:
+    return mk(imin(src.a, dst.a), imin(src.r, dst.r), imin(src.g, dst.g), imin(src.b, dst.b));
+  case VX_OM_BLEND_MODE_MAX:
+    return mk(imax(src.a, dst.a), imax(src.r, dst.r), imax(src.g, dst.g), imax(src.b, dst.b));
+  case VX_OM_BLEND_MODE_LOGICOP:
+    return argb(logic_op(lop, srcv, dstv));
+  default:  // ADD
+    return mk(div255(imin((int)(src.a * s.a + dst.a * d.a) + 0x80, 0xFF00)),
+              div255(imin((int)(src.r * s.r + dst.r * d.r) + 0x80, 0xFF00)),
+              div255(imin((int)(src.g * s.g + dst.g * d.g) + 0x80, 0xFF00)),
+              div255(imin((int)(src.b * s.b + dst.b * d.b) + 0x80, 0xFF00)));
+  }
+}
+
+// OutputMerger::write on register-resident pixel state (color, ds =
+// stencil << 24 | depth); returns whether the depth/stencil test passed
+__device__ __forceinline__ bool om_write(const rt_omstate_t& s, uint32_t& cbuf, uint32_t& ds_buf,
+                                         uint32_t color, uint32_t depth) {
+  const bool depth_on = s.depth_test_on != 0, stencil_on = s.stencil_on != 0;
+  const bool blend_on = s.blend_on != 0;
+  const uint32_t dst_ds = (depth_on || stencil_on) ? ds_buf : 0u;
+  const uint32_t dst_color = (s.color_write && (s.color_read || blend_on)) ? cbuf : 0u;
+  bool passed = true;
+  uint32_t ds = 0;
+  if (depth_on || stencil_on) {  // DepthTencil::test (graphics.cpp:564-596)
+    const uint32_t depth_val = dst_ds & VX_OM_DEPTH_MASK;
+    const uint32_t stencil_val = dst_ds >> VX_OM_DEPTH_BITS;
+    const uint32_t depth_ref = depth & VX_OM_DEPTH_MASK;
+    const uint32_t ref_m = s.stencil_ref & s.stencil_mask;
+    const uint32_t val_m = stencil_val & s.stencil_mask;
+    uint32_t op;
+    passed = om_compare(s.stencil_func, ref_m, val_m);
+    if (passed) {
+      passed = om_compare(s.depth_func, depth_ref, depth_val);
+      op = passed ? s.stencil_zpass : s.stencil_zfail;
+    } else {
+      op = s.stencil_fail;
+    }
+    const uint32_t sres = om_stencil_op(op, s.stencil_ref, stencil_val);
+    ds = (sres << VX_OM_DEPTH_BITS) | depth_ref;
+  }
+  if (blend_on && passed) {  // Blender (graphics.cpp:622-636)
+    const Argb src = argb(color), dst = argb(dst_color), cst = argb(s.blend_const);
+    const Argb s_rgb = blend_factor(s.blend_src_rgb, src, dst, cst);
+    const Argb s_a = blend_factor(s.blend_src_a, src, dst, cst);
+    const Argb d_rgb = blend_factor(s.blend_dst_rgb, src, dst, cst);
+    const Argb d_a = blend_factor(s.blend_dst_a, src, dst, cst);
+    const Argb rgb = blend_mode(s.blend_mode_rgb, s.logic_op, src, dst, s_rgb, d_rgb, color, dst_color);
+    const Argb a = blend_mode(s.blend_mode_a, s.logic_op, src, dst, s_a, d_a, color, dst_color);
+    color = (a.a << 24) | (rgb.r << 16) | (rgb.g << 8) | rgb.b;
+  }
+  const uint32_t ds_wm = ((depth_on && passed && s.depth_writemask) ? VX_OM_DEPTH_MASK : 0u) |
+                         (stencil_on ? (s.stencil_writemask << VX_OM_DEPTH_BITS) : 0u);
+  if (ds_wm != 0) ds_buf = (dst_ds & ~ds_wm) | (ds & ds_wm);
+  if (s.color_write && passed) cbuf = (dst_color & ~s.cbuf_writemask) | (color & s.cbuf_writemask);
+  return passed;
 }
 
 }  // namespace gfx

@@ -294,7 +294,7 @@ VX_MAIN(rt_kernel_arg_t, arg, PT_BLOCK) {
   const int rc = vx_spawn_tasks_block(
       arg->num_tasks,
       [&](const vx_task_t& task, bool valid, const Scene* s) { primary(task, valid, *s, s_pt, cnt); },
-      [&](const Scene* s) { bounces(*s, s_pt, cnt); }, &S);
+      [&](uint32_t, const Scene* s) { bounces(*s, s_pt, cnt); }, &S);
   flush(RT_STAT_PRIMARY, cnt.primary);
   flush(RT_STAT_SHADOW, cnt.shadow);
   flush(RT_STAT_HITS, cnt.hits);

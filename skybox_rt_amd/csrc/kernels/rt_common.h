@@ -37,6 +37,7 @@
 #define RT_FLAG_COMPACT  0x4u    // shard output: compact tile buffer
 #define RT_FLAG_PATH     0x8u    // diffuse path trace (pt_kernel.hip)
 #define RT_FLAG_FLAT     0x10u   // flat triangle list, no BVH (BASELINE config 2)
+#define RT_FLAG_RASTER   0x20u   // draw3d raster pipeline (raster_kernel.hip)
 
 #define RT_DC_DEPTH   0x1u
 #define RT_DC_COLOR   0x2u
@@ -77,6 +78,28 @@ typedef struct {
   uint32_t pad[6];
 } rt_dcstate_t;
 
+// Output-merger state of a drawcall for the raster pipeline (raster_kernel):
+// DepthTencil / Blender / OutputMerger configuration derived from the
+// draw3d DCR writes (draw3d/main.cpp:223-284 -> graphics.cpp:534-620,
+// gpu_sw.h:78-98), quirks included.  32 words.
+typedef struct {
+  uint32_t depth_func, depth_writemask, depth_test_on;
+  uint32_t stencil_func, stencil_zpass, stencil_zfail, stencil_fail;
+  uint32_t stencil_ref, stencil_mask, stencil_writemask, stencil_on;
+  uint32_t blend_mode_rgb, blend_mode_a, blend_src_rgb, blend_src_a, blend_dst_rgb, blend_dst_a;
+  uint32_t blend_const, logic_op, blend_on;
+  uint32_t cbuf_writemask, color_read, color_write;
+  uint32_t prim_offset, prim_count;   // the drawcall's primitives (global pids)
+  uint32_t pad[7];
+} rt_omstate_t;
+
+// screen bounding box of a primitive in pixels (gfxutil.cpp:209-232, clamped
+// to the viewport): x in [lo & 0xffff, lo >> 16), y in [hi & 0xffff, hi >> 16);
+// empty (x0 == x1) for degenerate or culled primitives
+typedef struct {
+  uint32_t x, y;
+} rt_bbox_t;
+
 typedef struct {
   uint64_t cbuf_addr, nodes_addr, tris_addr, layers_addr, prims_addr, dcs_addr;
   uint64_t ptris_addr;     // rt_tri_t per pid (path trace: bounce-hit barycentrics)
@@ -88,5 +111,9 @@ typedef struct {
   float light[3];
   uint32_t seed;           // path-trace RNG seed
   uint32_t num_geom;       // geometry triangles (flat mode)
-  uint32_t pad2;
+  uint32_t num_drawcalls;  // raster mode
+  uint64_t zbuf_addr;      // raster mode: depth/stencil buffer, W*H u32
+  uint64_t oms_addr;       // raster mode: rt_omstate_t per drawcall
+  uint64_t bbox_addr;      // raster mode: rt_bbox_t per pid
+  uint64_t pad3;
 } rt_kernel_arg_t;

@@ -23,6 +23,10 @@
 #ifndef RT_SHADE_UNIFORM
 #define RT_SHADE_UNIFORM 0
 #endif
+// leaf triangles fetched per batch (1, 2 or 4): register pressure vs overlap
+#ifndef RT_LEAF_BATCH
+#define RT_LEAF_BATCH 4
+#endif
 
 namespace rtk {
 
@@ -237,25 +241,31 @@ __device__ __forceinline__ int32_t trace(const Scene& S, const Ray& r, float tmi
         }
         if (ANY && done) { *t_out = bt; return bpid; }
       } else {
-        // A leaf's (up to 4) triangles are fetched in one batch -- the tris
-        // array carries 3 padding records.
+        // A leaf's (up to 4) triangles are fetched RT_LEAF_BATCH at a time
+        // (all slots unconditionally: the tris array carries 3 padding
+        // records), so their loads overlap.
         const uint32_t to = S.tris + 48u * first;
-        float4 ta[4], tb[4], tc[4];
 #pragma unroll
-        for (uint32_t k = 0; k < 4; ++k) {
-          ta[k] = S.A.ld_f4(to + 48u * k);
-          tb[k] = S.A.ld_f4(to + 48u * k + 16);
-          tc[k] = S.A.ld_f4(to + 48u * k + 32);
+        for (uint32_t k0 = 0; k0 < 4; k0 += RT_LEAF_BATCH) {
+          if (k0 >= count) break;
+        float4 ta[RT_LEAF_BATCH], tb[RT_LEAF_BATCH], tc[RT_LEAF_BATCH];
+#pragma unroll
+        for (uint32_t j = 0; j < RT_LEAF_BATCH; ++j) {
+          const uint32_t k = k0 + j;
+          ta[j] = S.A.ld_f4(to + 48u * k);
+          tb[j] = S.A.ld_f4(to + 48u * k + 16);
+          tc[j] = S.A.ld_f4(to + 48u * k + 32);
         }
 #pragma unroll
-        for (uint32_t k = 0; k < 4; ++k) {
+        for (uint32_t j = 0; j < RT_LEAF_BATCH; ++j) {
+          const uint32_t k = k0 + j;
           if (k < count) {
-            const int32_t pid = __float_as_int(ta[k].w);
+            const int32_t pid = __float_as_int(ta[j].w);
 #ifdef RT_INSTRUMENT
             ++cnt.tests;
 #endif
             float t;
-            if (pid != skip && mt_hit(r, ta[k], tb[k], tc[k], tmin, &t)) {
+            if (pid != skip && mt_hit(r, ta[j], tb[j], tc[j], tmin, &t)) {
               if (ANY) {
                 if (t < tmax) { *t_out = t; return pid; }
               } else if (closer(t, pid, bt, bpid, tie_high)) {
@@ -264,6 +274,7 @@ __device__ __forceinline__ int32_t trace(const Scene& S, const Ray& r, float tmi
               }
             }
           }
+        }
         }
       }
     }

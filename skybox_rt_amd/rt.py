@@ -21,6 +21,7 @@ from . import _lib
 RT_RENDER_SHADOWS = 0x1
 RT_RENDER_PATH = 0x8
 RT_RENDER_FLAT = 0x10
+RT_RENDER_RASTER = 0x20
 PT_SEED = 0x5EED
 RT_RENDER_INSTRUMENTED = 0x100
 CLEAR_COLOR = 0xFF000000               # draw3d/main.cpp:47
@@ -80,6 +81,7 @@ def lib():
             "rt_render_stats": [vp, C.POINTER(Stats)],
             "rt_render_kernel_ms": [vp, C.POINTER(C.c_double)],
             "rt_read_framebuffer": [vp, vp, u64],
+            "rt_read_depthbuffer": [vp, vp, u64],
             "rt_scene_setup_prims": [vp, u32, u32, vp, u64],
             "rt_framebuffer_device": [vp, C.POINTER(vp), C.POINTER(u64)],
             "rt_device_stream": [vp, C.POINTER(vp)],
@@ -163,14 +165,16 @@ class Renderer:
     def configure(self, width: int, height: int, shadows: bool = True, light=DEFAULT_LIGHT,
                   clear_color: int = CLEAR_COLOR, shard_index: int = 0, shard_count: int = 1,
                   instrumented: bool = False, path: bool = False, bounces: int = 4,
-                  seed: int = PT_SEED, flat: bool = False) -> None:
+                  seed: int = PT_SEED, flat: bool = False, raster: bool = False) -> None:
         """path=True: diffuse path trace (pt_kernel; `bounces` segments per
         path, RNG `seed`) instead of primary + shadow rays.  flat=True: the
-        flat triangle list without BVH (BASELINE config 2)."""
+        flat triangle list without BVH (BASELINE config 2).  raster=True:
+        the draw3d raster pipeline (any scene; depth/stencil/blend)."""
         p = RenderParams()
         p.width, p.height = width, height
         p.flags = ((RT_RENDER_SHADOWS if shadows else 0) | (RT_RENDER_INSTRUMENTED if instrumented else 0)
-                   | (RT_RENDER_PATH if path else 0) | (RT_RENDER_FLAT if flat else 0))
+                   | (RT_RENDER_PATH if path else 0) | (RT_RENDER_FLAT if flat else 0)
+                   | (RT_RENDER_RASTER if raster else 0))
         p.bounces, p.seed = bounces, seed
         p.light[:] = [float(np.float32(x)) for x in light]
         p.clear_color = clear_color
@@ -207,6 +211,13 @@ class Renderer:
             return out[:n]
         out = np.zeros((p.height, p.width), np.uint32)
         _check(lib().rt_read_framebuffer(self._h, out.ctypes.data, out.size), "rt_read_framebuffer")
+        return out
+
+    def depthbuffer(self) -> np.ndarray:
+        """RT_RENDER_RASTER: uint32 [H, W] depth/stencil words (stencil << 24 | depth)."""
+        p = self.params
+        out = np.zeros((p.height, p.width), np.uint32)
+        _check(lib().rt_read_depthbuffer(self._h, out.ctypes.data, out.size), "rt_read_depthbuffer")
         return out
 
     def framebuffer_device(self):
