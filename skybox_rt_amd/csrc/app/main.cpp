@@ -3,7 +3,10 @@
 // Flag set and output follow tests/regression/draw3d/main.cpp:80-135,
 // :349-378 and :505-514 (-t trace, -w/-h size, -o output, -r reference with
 // tolerance-1 compare, "PASSED!"/"FAILED!"), plus -S (shadow rays),
-// -L x,y,w (light), -n N (repeat launches for timing), -k dir (kernel images).
+// -L x,y,w (light), -n N (repeat launches for timing), -k dir (kernel images),
+// and the mode: default ray tracing (primary [+ shadow]), -R the draw3d
+// raster pipeline (draw3d's own default path), -P N path tracing with N
+// bounces, -F the flat triangle list (no BVH).
 #include <getopt.h>
 
 #include <cstdio>
@@ -22,13 +25,15 @@ const char* output_file = "output.png";
 const char* reference_file = nullptr;
 const char* kernel_dir = nullptr;
 uint32_t width = 128, height = 128, repeat = 1;
-bool shadows = false;
+bool shadows = false, raster = false, flat = false;
+int bounces = -1;  // >= 0: path tracing
 float light[3] = {0.0f, 60.0f, 80.0f};
 
 void usage() {
   std::printf("Skybox MI355X ray-tracing test.\n"
               "Usage: [-t trace] [-o output|null] [-r reference] [-w width] [-h height]"
-              " [-S shadows] [-L x,y,w] [-n repeat] [-k kernel_dir]\n");
+              " [-S shadows] [-L x,y,w] [-n repeat] [-k kernel_dir]"
+              " [-R raster | -P bounces | -F flat]\n");
 }
 
 #define RT_CHECK(_expr)                                                       \
@@ -43,7 +48,7 @@ void usage() {
 
 int main(int argc, char** argv) {
   int c;
-  while ((c = getopt(argc, argv, "t:o:r:w:h:n:k:L:S?")) != -1) {
+  while ((c = getopt(argc, argv, "t:o:r:w:h:n:k:L:P:SRF?")) != -1) {
     switch (c) {
     case 't': trace_file = optarg; break;
     case 'o': output_file = optarg; break;
@@ -53,6 +58,9 @@ int main(int argc, char** argv) {
     case 'n': repeat = (uint32_t)std::atoi(optarg); break;
     case 'k': kernel_dir = optarg; break;
     case 'S': shadows = true; break;
+    case 'R': raster = true; break;
+    case 'F': flat = true; break;
+    case 'P': bounces = std::atoi(optarg); break;
     case 'L': std::sscanf(optarg, "%f,%f,%f", &light[0], &light[1], &light[2]); break;
     case '?': usage(); return 0;
     default: usage(); return -1;
@@ -77,7 +85,10 @@ int main(int argc, char** argv) {
   std::memset(&p, 0, sizeof(p));
   p.width = width;
   p.height = height;
-  p.flags = shadows ? RT_RENDER_SHADOWS : 0;
+  p.flags = (shadows ? RT_RENDER_SHADOWS : 0u) | (raster ? RT_RENDER_RASTER : 0u) |
+            (flat ? RT_RENDER_FLAT : 0u) | (bounces >= 0 ? RT_RENDER_PATH : 0u);
+  p.bounces = bounces >= 0 ? (uint32_t)bounces : 0u;
+  p.seed = 0x5EED;
   std::memcpy(p.light, light, sizeof(light));
   p.clear_color = 0xff000000u;
   p.shard_count = 1;
@@ -89,12 +100,19 @@ int main(int argc, char** argv) {
     RT_CHECK(rt_render_stats(r, &st));
     total += st.kernel_ms;
   }
-  const double rays = (double)(st.primary_rays + st.shadow_rays);
-  std::printf("Elapsed time: %.4f ms/frame (grid %u x %u), rays=%.0f (primary %llu, shadow %llu, "
-              "occluded %llu), %.1f Mrays/s\n",
-              total / repeat, st.grid, st.block, rays, (unsigned long long)st.primary_rays,
-              (unsigned long long)st.shadow_rays, (unsigned long long)st.occluded,
-              rays / (total / repeat) * 1e-3);
+  if (raster) {
+    std::printf("Elapsed time: %.4f ms/frame (grid %u x %u), pixels=%llu, fragments=%llu, "
+                "%.1f Mpixels/s\n",
+                total / repeat, st.grid, st.block, (unsigned long long)st.primary_rays,
+                (unsigned long long)st.shaded, (double)st.primary_rays / (total / repeat) * 1e-3);
+  } else {
+    const double rays = (double)(st.primary_rays + st.shadow_rays + st.bounce_rays);
+    std::printf("Elapsed time: %.4f ms/frame (grid %u x %u), rays=%.0f (primary %llu, shadow %llu, "
+                "bounce %llu, occluded %llu), %.1f Mrays/s\n",
+                total / repeat, st.grid, st.block, rays, (unsigned long long)st.primary_rays,
+                (unsigned long long)st.shadow_rays, (unsigned long long)st.bounce_rays,
+                (unsigned long long)st.occluded, rays / (total / repeat) * 1e-3);
+  }
   int errors = 0;
   if (std::strcmp(output_file, "null") != 0) {
     std::vector<uint32_t> fb((size_t)width * height);

@@ -67,6 +67,18 @@ def test_raster_tekkaman_1024_reference_render(po):
     assert po.compare_images(po.argb_to_rgba_image(r.framebuffer()), ref, tol=0) == 0
 
 
+def test_rtapp_cli_raster_mode_against_golden():
+    import os
+    import subprocess
+    from skybox_rt_amd import _lib
+    exe = os.path.join(_lib.LIB_DIR, "rtapp")
+    out = subprocess.run([exe, "-R", "-t", scene_path("vase"), "-w", "128", "-h", "128", "-o",
+                          "/tmp/rtapp_vase128.png", "-r", f"{GOLDEN}/draw3d/vase_ref_128.png"],
+                         capture_output=True, text=True, timeout=300)
+    assert out.returncode == 0, out.stdout + out.stderr
+    assert "PASSED!" in out.stdout
+
+
 def test_raster_repeatable_and_rt_modes_rejected_on_blend_scenes(po):
     _, r, _ = setup(po, "vase")
     r.configure(128, 128, raster=True)
