@@ -36,6 +36,7 @@ def main():
     ap.add_argument("--scene", default=os.path.join(ROOT, "tests/golden/scenes/tekkaman.cgltrace"))
     ap.add_argument("--variants", default="")
     ap.add_argument("--no-shadows", action="store_true")
+    ap.add_argument("--mode", choices=("shadow", "path", "flat", "raster"), default="shadow")
     args = ap.parse_args()
     import torch  # noqa: F401  (one HIP runtime)
     from skybox_rt_amd import rt
@@ -49,7 +50,8 @@ def main():
         saved = {k: os.environ.get(k) for k in env}
         os.environ.update(env)
         r = rt.Renderer(scene, kernel_dir=lib if d == "default" else os.path.join(vdir, d))
-        r.configure(args.size, args.size, shadows=not args.no_shadows)
+        r.configure(args.size, args.size, shadows=not args.no_shadows, path=args.mode == "path",
+                    flat=args.mode == "flat", raster=args.mode == "raster")
         r.render()  # the driver reads its launch env when it loads the image
         for k, v in saved.items():
             if v is None:

@@ -12,6 +12,7 @@
 
 #include <algorithm>
 #include <cstdio>
+#include <cstdlib>
 #include <chrono>
 #include <map>
 #include <cstring>
@@ -385,11 +386,19 @@ int rt_renderer_configure(rt_renderer_h r, const rt_render_params_t* p) {
   }
   a.width = p->width;
   a.height = p->height;
-  a.tiles_y = (p->height + 31) >> RT_TILE_LOG;
-  a.tiles_x = (p->width + 31) >> RT_TILE_LOG;
+  // raster workgroups own 2^log x 2^log tiles (16x16 by default; env
+  // RT_RASTER_TILE_LOG=5 selects the reference's 32x32), 256 tasks each
+  uint32_t tlog = RT_TILE_LOG;
+  if (raster) {
+    tlog = RT_RASTER_TILE_LOG;
+    if (const char* e = std::getenv("RT_RASTER_TILE_LOG")) tlog = std::atoi(e) == 5 ? 5u : 4u;
+  }
+  a.raster_tile_log = tlog;
+  a.tiles_y = (p->height + (1u << tlog) - 1) >> tlog;
+  a.tiles_x = (p->width + (1u << tlog) - 1) >> tlog;
   const uint32_t tiles = a.tiles_x * a.tiles_y;
   r->local_tiles = (tiles > p->shard_index) ? (tiles - p->shard_index + shards - 1) / shards : 0;
-  a.num_tasks = r->local_tiles * (raster ? RT_TILE_PIXELS / 4 : RT_TILE_PIXELS);  // raster: 2x2 quads
+  a.num_tasks = r->local_tiles * (raster ? 256u : RT_TILE_PIXELS);
   a.shard_index = p->shard_index;
   a.shard_count = shards;
   a.flags = ((p->flags & RT_RENDER_SHADOWS) ? RT_FLAG_SHADOWS : 0u) |

@@ -5,9 +5,14 @@
 // merger (depth/stencil test, blending, write masks), pixel-exact with the
 // reference's golden images through the oracle (oracle/raster.c).
 //
-// MI355X mapping: one 256-thread workgroup per 32x32 raster tile (the
-// reference's RASTER_TILE_LOGSIZE = 5 unit), each thread owning one 2x2 quad
-// (the reference's stamp, graphics.cpp:840, kernel.cpp:73-79).  A pixel's
+// MI355X mapping: one 256-thread workgroup per raster tile -- 16x16 pixels,
+// one per thread (RT_RASTER_TILE_LOG, default), or the reference's 32x32
+// (RASTER_TILE_LOGSIZE = 5) with each thread owning a 2x2 quad (the
+// reference's stamp, graphics.cpp:840, kernel.cpp:73-79).  Results do not
+// depend on the tile size (per-pixel semantics; the oracle's tile-size
+// invariance test); 16x16 gives 4x the workgroups and a 4x shorter
+// per-thread pixel loop at 1024^2, where the 32x32 form ran one round of
+// 1024 workgroups bound by its heaviest tile.  A pixel's
 // colour and depth/stencil words stay in the owning thread's registers for
 // the whole frame -- initialised to draw3d's clear values, written once -- so the order-dependent OM
 // semantics of the reference (per-tile ascending primitive order,
@@ -33,16 +38,32 @@ __device__ __forceinline__ uint32_t lane_id() {
   return __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
 }
 
+#ifndef RS_STAGE
+#define RS_STAGE 1  // 1: listed primitives' records staged in LDS during binning
+#endif
+
 struct RsLds {
   uint32_t list[RS_BLOCK];   // the tile's primitives (global pids) of one chunk, in order
   uint32_t wave_n[kWaves];
+#if RS_STAGE
+  uint4 rec[RS_BLOCK][8];    // their rt_prim_t records (128 B each), same order
+#endif
 };
 
 struct Frame {
   vx_arena A;
   uint32_t prims, dcs, oms, bbox, cbuf, zbuf;
-  uint32_t width, height, tiles_x, num_dc, clear_color, clear_depth;
+  uint32_t width, height, tiles_x, num_dc, clear_color, clear_depth, tile_log;
 };
+
+// thread -> its pixel group: g x g pixels at (gx, gy), g = tile side / 16
+__device__ __forceinline__ void thread_pixels(const Frame& F, uint32_t tile, uint32_t t,
+                                              uint32_t* gx, uint32_t* gy, uint32_t* g) {
+  const uint32_t gs = 1u << (F.tile_log - 4);
+  *g = gs;
+  *gx = ((tile % F.tiles_x) << F.tile_log) + gs * (t & 15u);
+  *gy = ((tile / F.tiles_x) << F.tile_log) + gs * (t >> 4);
+}
 
 __device__ __forceinline__ rt_omstate_t load_om(const vx_arena& A, uint32_t off) {
   rt_omstate_t s;
@@ -58,10 +79,12 @@ __device__ __forceinline__ rt_omstate_t load_om(const vx_arena& A, uint32_t off)
 // the frame's drawcalls over one tile; col/ds = this thread's quad
 __device__ __forceinline__ void render_tile(const Frame& F, uint32_t tile, RsLds& L, uint32_t col[4],
                                             uint32_t ds[4], uint32_t& frags) {
-  const uint32_t tx = tile % F.tiles_x, ty = tile / F.tiles_x;
-  const uint32_t x0 = tx << RT_TILE_LOG, y0 = ty << RT_TILE_LOG;
-  const uint32_t q = threadIdx.x;
-  const uint32_t qx = x0 + 2u * (q & 15u), qy = y0 + 2u * (q >> 4);
+  const uint32_t x0 = (tile % F.tiles_x) << F.tile_log, y0 = (tile / F.tiles_x) << F.tile_log;
+  const uint32_t bx_lo = x0 & ~31u, bx_hi = bx_lo + 32u;  // enclosing RASTER_TILE_LOGSIZE tile
+  const uint32_t by_lo = y0 & ~31u, by_hi = by_lo + 32u;
+  uint32_t qx, qy, gs;
+  thread_pixels(F, tile, threadIdx.x, &qx, &qy, &gs);
+  const uint32_t npx = gs * gs;
   const uint32_t w = threadIdx.x >> 6;
   for (uint32_t d = 0; d < F.num_dc; ++d) {
     const rt_omstate_t om = load_om(F.A, F.oms + 128u * d);
@@ -75,7 +98,11 @@ __device__ __forceinline__ void render_tile(const Frame& F, uint32_t tile, RsLds
         g = om.prim_offset + i;
         const uint2 bb = make_uint2(F.A.ld_u32(F.bbox + 8u * g), F.A.ld_u32(F.bbox + 8u * g + 4));
         const uint32_t bx0 = bb.x & 0xffffu, bx1 = bb.x >> 16, by0 = bb.y & 0xffffu, by1 = bb.y >> 16;
-        ov = bx0 < bx1 && bx0 < x0 + 32u && bx1 > x0 && by0 < y0 + 32u && by1 > y0;
+        // binned at the reference's 32x32 granularity whatever this
+        // workgroup's tile size: fixed-point coverage can reach a few pixels
+        // past the float bbox, and the reference covers those pixels iff
+        // they lie in a 32x32 tile the primitive was binned to
+        ov = bx0 < bx1 && bx0 < bx_hi && bx1 > bx_lo && by0 < by_hi && by1 > by_lo;
       }
       const uint64_t m = __ballot(ov);
       if (lane_id() == 0) L.wave_n[w] = (uint32_t)__popcll(m);
@@ -91,15 +118,28 @@ __device__ __forceinline__ void render_tile(const Frame& F, uint32_t tile, RsLds
         const uint32_t r = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
                                                      __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
         L.list[pre + r] = g;
+#if RS_STAGE
+#pragma unroll
+        for (int k = 0; k < 8; ++k) L.rec[pre + r][k] = F.A.ld_u4(F.prims + 128u * g + 16u * k);
+#endif
       }
       __syncthreads();
       // rasterize the listed primitives in order
       for (uint32_t k = 0; k < n; ++k) {
-        const uint32_t pg = L.list[k];
         gfx::Prim p;
-        gfx::load_prim<true>(F.A, F.prims + 128u * pg, p);
+#if RS_STAGE
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {  // broadcast LDS reads
+          const uint4 v = L.rec[k][i];
+          p.w[4 * i + 0] = (int32_t)v.x; p.w[4 * i + 1] = (int32_t)v.y;
+          p.w[4 * i + 2] = (int32_t)v.z; p.w[4 * i + 3] = (int32_t)v.w;
+        }
+#else
+        gfx::load_prim<true>(F.A, F.prims + 128u * L.list[k], p);
+#endif
 #pragma unroll
         for (uint32_t j = 0; j < 4; ++j) {
+          if (j >= npx) break;
           const uint32_t x = qx + (j & 1u), y = qy + (j >> 1);
           const int32_t e0 = gfx::edge_eval(p.edge(0), x, y);
           const int32_t e1 = gfx::edge_eval(p.edge(1), x, y);
@@ -139,15 +179,16 @@ VX_MAIN(rt_kernel_arg_t, arg, RS_BLOCK) {
   F.num_dc = arg->num_drawcalls;
   F.clear_color = arg->clear_color;
   F.clear_depth = 0xffffffffu;
+  F.tile_log = arg->raster_tile_log;
   uint32_t frags = 0, pixels = 0;
-  uint32_t col[4], ds[4], qx = 0, qy = 0;
-  // task = one 2x2 quad (the reference's stamp); a workgroup step = one tile
+  uint32_t col[4], ds[4], qx = 0, qy = 0, npx = 1;
+  // task = one thread's pixel group; a workgroup step = one tile
   const int rc = vx_spawn_tasks_block(
       arg->num_tasks,
       [&](const vx_task_t& task, bool valid, const Frame* f) {
-        const uint32_t tile = task.blockIdx.x / RS_BLOCK, q = task.blockIdx.x % RS_BLOCK;
-        qx = ((tile % f->tiles_x) << RT_TILE_LOG) + 2u * (q & 15u);
-        qy = ((tile / f->tiles_x) << RT_TILE_LOG) + 2u * (q >> 4);
+        uint32_t gs;
+        thread_pixels(*f, task.blockIdx.x / RS_BLOCK, task.blockIdx.x % RS_BLOCK, &qx, &qy, &gs);
+        npx = gs * gs;
         // the frame starts from draw3d's clears (main.cpp:478-490: colour
         // 0xff000000, depth/stencil 0xffffffff), fused here: no read-back
 #pragma unroll
@@ -155,7 +196,7 @@ VX_MAIN(rt_kernel_arg_t, arg, RS_BLOCK) {
           const uint32_t px = qx + (j & 1u), py = qy + (j >> 1);
           col[j] = f->clear_color;
           ds[j] = f->clear_depth;
-          pixels += valid && px < f->width && py < f->height;
+          pixels += j < npx && valid && px < f->width && py < f->height;
         }
       },
       [&](uint32_t step, const Frame* f) {
@@ -163,7 +204,7 @@ VX_MAIN(rt_kernel_arg_t, arg, RS_BLOCK) {
 #pragma unroll
         for (uint32_t j = 0; j < 4; ++j) {  // ... and written once
           const uint32_t px = qx + (j & 1u), py = qy + (j >> 1);
-          if (px < f->width && py < f->height) {
+          if (j < npx && px < f->width && py < f->height) {
             const uint32_t o = 4u * (py * f->width + px);
             f->A.st_u32(f->cbuf + o, col[j]);
             f->A.st_u32(f->zbuf + o, ds[j]);

@@ -31,6 +31,7 @@
 #endif
 #define RT_TILE_LOG 5            // RASTER_TILE_LOGSIZE (VX_config.vh:477-479)
 #define RT_TILE_PIXELS 1024
+#define RT_RASTER_TILE_LOG 4     // raster workgroup tile: 16x16 pixels, one per thread
 
 #define RT_FLAG_SHADOWS  0x1u
 #define RT_FLAG_TIE_HIGH 0x2u    // LEQUAL geometry: equal t -> highest pid
@@ -112,8 +113,9 @@ typedef struct {
   uint32_t seed;           // path-trace RNG seed
   uint32_t num_geom;       // geometry triangles (flat mode)
   uint32_t num_drawcalls;  // raster mode
+  uint32_t raster_tile_log;  // raster mode: tile side 2^log (4: 16x16 px, 1 px/thread; 5: 32x32, 2x2/thread)
+  uint32_t pad4;
   uint64_t zbuf_addr;      // raster mode: depth/stencil buffer, W*H u32
   uint64_t oms_addr;       // raster mode: rt_omstate_t per drawcall
   uint64_t bbox_addr;      // raster mode: rt_bbox_t per pid
-  uint64_t pad3;
 } rt_kernel_arg_t;

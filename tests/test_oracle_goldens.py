@@ -57,3 +57,18 @@ def test_raster_oracle_matches_tekkaman_1024(oracle_lib):
     color, _, _ = po.raster_render(sc, 1024, 1024)
     ref = _png(f"{GOLDEN}/draw3d/tekkaman_1024x1024.png")
     assert po.compare_images(po.argb_to_rgba_image(color), ref, tol=0) == 0
+
+
+def test_raster_binning_granularity_is_semantic(oracle_lib):
+    """Fixed-point coverage can reach past a primitive's float bbox; the
+    reference covers such a pixel only inside a 32x32 tile the primitive was
+    binned to.  The oracle reproduces that (mouse at 128^2 differs in one pixel
+    with 16x16 binning), so the GPU raster binning always uses the 32x32
+    granularity whatever its workgroup tile (raster_kernel.hip)."""
+    po = oracle_lib
+    sc = po.OracleScene(po.cgltrace.load(scene_path("mouse")))
+    a, _, _ = po.raster_render(sc, 128, 128, 5)
+    b, _, _ = po.raster_render(sc, 128, 128, 4)
+    assert int((a != b).sum()) == 1
+    ref = _png(f"{GOLDEN}/draw3d/mouse_ref_128.png")
+    assert po.compare_images(po.argb_to_rgba_image(a), ref, tol=0) == 0
