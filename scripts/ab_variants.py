@@ -37,6 +37,7 @@ def main():
     ap.add_argument("--variants", default="")
     ap.add_argument("--no-shadows", action="store_true")
     ap.add_argument("--mode", choices=("shadow", "path", "flat", "raster"), default="shadow")
+    ap.add_argument("--bounces", type=int, default=4)
     args = ap.parse_args()
     import torch  # noqa: F401  (one HIP runtime)
     from skybox_rt_amd import rt
@@ -51,7 +52,7 @@ def main():
         os.environ.update(env)
         r = rt.Renderer(scene, kernel_dir=lib if d == "default" else os.path.join(vdir, d))
         r.configure(args.size, args.size, shadows=not args.no_shadows, path=args.mode == "path",
-                    flat=args.mode == "flat", raster=args.mode == "raster")
+                    flat=args.mode == "flat", raster=args.mode == "raster", bounces=args.bounces)
         r.render()  # the driver reads its launch env when it loads the image
         for k, v in saved.items():
             if v is None:

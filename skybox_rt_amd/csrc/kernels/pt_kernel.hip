@@ -24,7 +24,29 @@
 
 #include "rt_trace.h"
 
+// PT_MODE 1 (default image pt_kernel): every lane runs its own path to the
+// end in registers (one-wave workgroups, no queue): divergent, but waves
+// never wait on each other and the oversubscribed grid keeps the CUs fed.
+// PT_MODE 0 (image pt_compact): block-level wave64 compaction of live paths
+// through LDS queues (256-thread workgroups, barrier-separated vertex
+// phases).  Measured on tekkaman 1024^2, 4 bounces: 0.39 ms (mode 1) vs
+// 0.47 ms (mode 0) -- the time is the per-vertex latency chain of the
+// deepest paths (each extra bounce level adds ~0.08 ms whatever the number
+// of live paths), which compaction does not shorten and its barriers
+// lengthen.  Both images are parity-tested.
+#ifndef PT_MODE
+#define PT_MODE 1
+#endif
+#ifndef RT_LDS_SCENE
+#define RT_LDS_SCENE 0
+#endif
+#if PT_MODE == 0
 #define PT_BLOCK 256
+#elif RT_LDS_SCENE
+#define PT_BLOCK 1024  // one workgroup per CU shares the staged BVH
+#else
+#define PT_BLOCK 64
+#endif
 #define PT_SKY 0.25f     // radiance of an escaped bounce ray (oracle ORC_PT_SKY)
 #define PT_TRIES 8u      // disk rejection-sampling attempts (ORC_PT_TRIES)
 
@@ -114,10 +136,13 @@ struct PathQueue {
 
 struct PtLds {
   int32_t stack[kWaves][RT_MAX_STACK][64];
+#if PT_MODE == 0
   PathQueue q[2];
   uint32_t n[2];
+#endif
 };
 
+#if PT_MODE == 0
 // append this lane's path (if `want`) to queue q at a ballot/mbcnt slot
 __device__ __forceinline__ void enqueue(PtLds& L, int qi, bool want, uint32_t task, uint32_t alpha,
                                         int32_t pid, float t, const float o[3], const float d[3],
@@ -172,32 +197,30 @@ __device__ __forceinline__ void primary(const vx_task_t& task, bool valid, const
   if (in && !path) store_pixel(S, t, x, y, color);
 }
 
-// one path vertex for queue entry i (lanes with i < n; whole waves past n skip)
-__device__ __forceinline__ void vertex(const Scene& S, PtLds& L, int qi, uint32_t v, uint32_t n,
-                                       Counters& cnt) {
-  const uint32_t i = threadIdx.x;
-  const bool act = i < n;
-  const PathQueue& q = L.q[qi];
-  const uint32_t j = act ? i : 0u;
-  const uint32_t task = q.task[j], alpha = q.alpha[j];
-  const int32_t pid = q.pid[j];
-  const float th = q.t[j];
-  float o[3], d[3], T[3], Lr[3];
-#pragma unroll
-  for (int k = 0; k < 3; ++k) {
-    o[k] = q.o[k][j];
-    d[k] = q.d[k][j];
-    T[k] = q.T[k][j];
-    Lr[k] = q.L[k][j];
-  }
+#endif
+
+// A path at a vertex: the ray that reached it (o, d, hit t, hit pid), its
+// throughput T and radiance L so far, its pixel task, the primary alpha.
+struct PathState {
+  uint32_t task, alpha;
+  int32_t pid;
+  float t;
+  float o[3], d[3], T[3], L[3];
+};
+
+// One path vertex for an active lane: direct light through a shadow ray,
+// then (v < bounces) the bounce; returns whether the path continues (st then
+// describes the next vertex), else the pixel is final.  Every lane of the
+// wave calls it; `act` masks the work.
+__device__ __forceinline__ bool path_step(const Scene& S, int32_t* stack, PathState& st, uint32_t v,
+                                          bool act, Counters& cnt) {
   const bool tie_high = (S.flags & RT_FLAG_TIE_HIGH) != 0;
-  int32_t* stack = &L.stack[threadIdx.x >> 6][0][lane_id()];
   float v0[3], e1[3], e2[3], nrm[3], P[3];
-  load_tri(S, act ? pid : 0, v0, e1, e2);
-  tri_normal(e1, e2, d, nrm);
-  const float tt = th * 0.999755859375f;
+  load_tri(S, act ? st.pid : 0, v0, e1, e2);
+  tri_normal(e1, e2, st.d, nrm);
+  const float tt = st.t * 0.999755859375f;
 #pragma unroll
-  for (int k = 0; k < 3; ++k) P[k] = fmaf(d[k], tt, o[k]);
+  for (int k = 0; k < 3; ++k) P[k] = fmaf(st.d[k], tt, st.o[k]);
   // direct light: shadow segment P -> light
   Ray s;
   s.o[0] = P[0]; s.o[1] = P[1]; s.o[2] = P[2];
@@ -207,13 +230,13 @@ __device__ __forceinline__ void vertex(const Scene& S, PtLds& L, int qi, uint32_
   ray_setup(s);
   cnt.shadow += act;
   float ts;
-  const bool occ = act && trace<true>(S, s, 0.0f, 1.0f, pid, tie_high, &ts, stack, cnt) >= 0;
+  const bool occ = act && trace<true>(S, s, 0.0f, 1.0f, st.pid, tie_high, &ts, stack, cnt) >= 0;
   cnt.occluded += occ;
   if (act && !occ) {
     const float cosl = dot3(nrm, s.d) / sqrtf(dot3(s.d, s.d));
     if (cosl > 0.0f) {
 #pragma unroll
-      for (int k = 0; k < 3; ++k) Lr[k] = fmaf(T[k], cosl, Lr[k]);
+      for (int k = 0; k < 3; ++k) st.L[k] = fmaf(st.T[k], cosl, st.L[k]);
     }
   }
   bool alive = act && v < S.bounces;
@@ -223,14 +246,14 @@ __device__ __forceinline__ void vertex(const Scene& S, PtLds& L, int qi, uint32_
   if (alive) {
     b.o[0] = P[0]; b.o[1] = P[1]; b.o[2] = P[2];
     uint32_t x, y;
-    task_pixel(S, task, &x, &y);
+    task_pixel(S, st.task, &x, &y);
     bounce_dir(nrm, pt_key(S.seed, y * S.width + x, v), b.d);  // keyed by pixel, not task
     ray_setup(b);
     cnt.bounce += 1;
-    np = trace<false>(S, b, 0.0f, INFINITY, pid, tie_high, &nt, stack, cnt);
+    np = trace<false>(S, b, 0.0f, INFINITY, st.pid, tie_high, &nt, stack, cnt);
     if (np < 0) {
 #pragma unroll
-      for (int k = 0; k < 3; ++k) Lr[k] = fmaf(T[k], PT_SKY, Lr[k]);
+      for (int k = 0; k < 3; ++k) st.L[k] = fmaf(st.T[k], PT_SKY, st.L[k]);
       alive = false;
     }
   }
@@ -241,25 +264,60 @@ __device__ __forceinline__ void vertex(const Scene& S, PtLds& L, int qi, uint32_
     mt_bary(b.o, b.d, w0, f1, f2, &b1, &b2);
     gfx::Prim p;
     gfx::load_prim(S.A, S.prims + 128u * (uint32_t)np, p);
-    const gfx::DcState st = gfx::load_dcstate(S.A, S.dcs + 64u * p.dc());
+    const gfx::DcState dst = gfx::load_dcstate(S.A, S.dcs + 64u * p.dc());
 #ifdef RT_INSTRUMENT
     ++cnt.shaded;
-    if (st.flags & RT_DC_TEX)
-      cnt.texel_bytes += (st.filter == VX_TEX_FILTER_BILINEAR ? 4u : 1u) * st.stride;
+    if (dst.flags & RT_DC_TEX)
+      cnt.texel_bytes += (dst.filter == VX_TEX_FILTER_BILINEAR ? 4u : 1u) * dst.stride;
 #endif
-    const uint32_t a = gfx::shade_weights(S.A, p, st, gfx::fx_from_float_dev((1.0f - b1) - b2, 24),
+    const uint32_t a = gfx::shade_weights(S.A, p, dst, gfx::fx_from_float_dev((1.0f - b1) - b2, 24),
                                           gfx::fx_from_float_dev(b1, 24));
     const float k255 = 1.0f / 255.0f;
-    T[0] = T[0] * ((float)((a >> 16) & 0xffu) * k255);
-    T[1] = T[1] * ((float)((a >> 8) & 0xffu) * k255);
-    T[2] = T[2] * ((float)(a & 0xffu) * k255);
+    st.T[0] = st.T[0] * ((float)((a >> 16) & 0xffu) * k255);
+    st.T[1] = st.T[1] * ((float)((a >> 8) & 0xffu) * k255);
+    st.T[2] = st.T[2] * ((float)(a & 0xffu) * k255);
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+      st.o[k] = P[k];
+      st.d[k] = b.d[k];
+    }
+    st.pid = np;
+    st.t = nt;
   }
-  enqueue(L, qi ^ 1, alive, task, alpha, np, nt, P, b.d, T, Lr);
-  if (act && !alive) {
-    uint32_t x, y;
-    task_pixel(S, task, &x, &y);
-    store_pixel(S, task, x, y, alpha | (to8(Lr[0]) << 16) | (to8(Lr[1]) << 8) | to8(Lr[2]));
+  return alive;
+}
+
+__device__ __forceinline__ void store_path_pixel(const Scene& S, const PathState& st) {
+  uint32_t x, y;
+  task_pixel(S, st.task, &x, &y);
+  store_pixel(S, st.task, x, y,
+              st.alpha | (to8(st.L[0]) << 16) | (to8(st.L[1]) << 8) | to8(st.L[2]));
+}
+
+#if PT_MODE == 0
+// one path vertex for queue entry i (lanes with i < n; whole waves past n skip)
+__device__ __forceinline__ void vertex(const Scene& S, PtLds& L, int qi, uint32_t v, uint32_t n,
+                                       Counters& cnt) {
+  const uint32_t i = threadIdx.x;
+  const bool act = i < n;
+  const PathQueue& q = L.q[qi];
+  const uint32_t j = act ? i : 0u;
+  PathState st;
+  st.task = q.task[j];
+  st.alpha = q.alpha[j];
+  st.pid = q.pid[j];
+  st.t = q.t[j];
+#pragma unroll
+  for (int k = 0; k < 3; ++k) {
+    st.o[k] = q.o[k][j];
+    st.d[k] = q.d[k][j];
+    st.T[k] = q.T[k][j];
+    st.L[k] = q.L[k][j];
   }
+  int32_t* stack = &L.stack[threadIdx.x >> 6][0][lane_id()];
+  const bool alive = path_step(S, stack, st, v, act, cnt);
+  enqueue(L, qi ^ 1, alive, st.task, st.alpha, st.pid, st.t, st.o, st.d, st.T, st.L);
+  if (act && !alive) store_path_pixel(S, st);
 }
 
 // after each block step: run the path vertices of the queued paths, bounce
@@ -281,6 +339,50 @@ __device__ __forceinline__ void bounces(const Scene& S, PtLds& L, Counters& cnt)
   __syncthreads();
 }
 
+#else  // PT_MODE == 1
+
+// one pixel's whole path on its own lane (no compaction)
+__device__ __forceinline__ void lane_path(const vx_task_t& task, const Scene& S, int32_t* stack,
+                                          Counters& cnt) {
+  const uint32_t t = task.blockIdx.x;
+  uint32_t x, y;
+  task_pixel(S, t, &x, &y);
+  const bool in = x < S.width && y < S.height;
+  Ray r;
+  primary_dir(S, x, y, r);
+  ray_setup(r);
+  cnt.primary += in;
+  const bool tie_high = (S.flags & RT_FLAG_TIE_HIGH) != 0;
+  float th = 0.0f;
+  const int32_t hit = in ? trace<false>(S, r, 0.0f, INFINITY, -1, tie_high, &th, stack, cnt) : -1;
+  cnt.hits += hit >= 0;
+  const int32_t spid = resolve_layers(S, r, in && hit < 0, hit, cnt);
+  const uint32_t color = shade_wave(S, spid, x, y, S.clear_color, cnt);
+  if (hit < 0) {
+    if (in) store_pixel(S, t, x, y, color);
+    return;
+  }
+  const float k255 = 1.0f / 255.0f;
+  PathState st;
+  st.task = t;
+  st.alpha = color & 0xff000000u;
+  st.pid = hit;
+  st.t = th;
+  st.T[0] = (float)((color >> 16) & 0xffu) * k255;
+  st.T[1] = (float)((color >> 8) & 0xffu) * k255;
+  st.T[2] = (float)(color & 0xffu) * k255;
+#pragma unroll
+  for (int k = 0; k < 3; ++k) {
+    st.o[k] = r.o[k];
+    st.d[k] = r.d[k];
+    st.L[k] = 0.0f;
+  }
+  for (uint32_t v = 0; path_step(S, stack, st, v, true, cnt); ++v) {
+  }
+  store_path_pixel(S, st);
+}
+#endif
+
 __device__ __forceinline__ void flush(int slot, uint32_t v) { vx_mpm_add(RT_MPM_USER + slot, v); }
 
 }  // namespace
@@ -288,13 +390,25 @@ __device__ __forceinline__ void flush(int slot, uint32_t v) { vx_mpm_add(RT_MPM_
 VX_MAIN(rt_kernel_arg_t, arg, PT_BLOCK) {
   __shared__ PtLds s_pt;
   Counters cnt;
-  const Scene S = load_scene(arg);
+  Scene S = load_scene(arg);
+#if PT_MODE == 0
   if (threadIdx.x == 0) { s_pt.n[0] = 0; s_pt.n[1] = 0; }
   __syncthreads();
   const int rc = vx_spawn_tasks_block(
       arg->num_tasks,
       [&](const vx_task_t& task, bool valid, const Scene* s) { primary(task, valid, *s, s_pt, cnt); },
       [&](uint32_t, const Scene* s) { bounces(*s, s_pt, cnt); }, &S);
+#else
+#if RT_LDS_SCENE
+  __shared__ float4 s_scene[RT_LDS_SCENE_F4];
+  stage_scene(S, S.num_geom, s_scene);
+  __syncthreads();
+#endif
+  int32_t* stack = &s_pt.stack[threadIdx.x >> 6][0][lane_id()];
+  const int rc = vx_spawn_tasks(
+      arg->num_tasks,
+      [&](const vx_task_t& task, const Scene* s) { lane_path(task, *s, stack, cnt); }, &S);
+#endif
   flush(RT_STAT_PRIMARY, cnt.primary);
   flush(RT_STAT_SHADOW, cnt.shadow);
   flush(RT_STAT_HITS, cnt.hits);

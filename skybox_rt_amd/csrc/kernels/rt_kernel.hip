@@ -34,6 +34,10 @@
 #define RT_FLAT 0
 #endif
 #define RT_FLAT_CAP 1024  // triangles staged in LDS (48 KB); longer lists stream via s_load
+// RT_LDS_SCENE: the BVH is staged in LDS per workgroup (1024-thread images)
+#ifndef RT_LDS_SCENE
+#define RT_LDS_SCENE 0
+#endif
 #ifndef RT_SHADOW_QUEUE
 #define RT_SHADOW_QUEUE (!RT_FLAT)
 #endif
@@ -196,7 +200,15 @@ VX_MAIN(rt_kernel_arg_t, arg, RT_BLOCK_THREADS) {
   __shared__ WaveLds s_wave[kWaves];
   WaveLds& w = s_wave[threadIdx.x >> 6];
   Counters cnt;
-  const Scene S = load_scene(arg);
+  Scene S = load_scene(arg);
+#if RT_LDS_SCENE
+  // the whole BVH (nodes + leaf triangles) staged once per workgroup:
+  // traversal then reads LDS (broadcast-friendly, ~100-cycle latency)
+  // instead of the vector-memory path
+  __shared__ float4 s_scene[RT_LDS_SCENE_F4];
+  stage_scene(S, S.num_geom, s_scene);
+  __syncthreads();
+#endif
 #if RT_FLAT
   // stage the geometry list once per workgroup (workgroups past the last
   // task chunk have nothing to render and skip it)

@@ -46,7 +46,31 @@ struct Scene {
   uint32_t num_nodes, num_layer, num_geom, flags, width, height;
   uint32_t shard_index, shard_count, tiles_x, clear_color, bounces, seed;
   float sx, sy, light[3];
+  // the BVH staged in LDS by the workgroup (RT_LDS_SCENE images), or null
+  const float4* lnodes = nullptr;
+  const float4* ltris = nullptr;
 };
+
+// LDS budget (float4 slots) for a workgroup-staged BVH: nodes + leaf
+// triangles (+3 padding records); larger scenes stay in global memory
+#ifndef RT_LDS_SCENE_F4
+#define RT_LDS_SCENE_F4 4096
+#endif
+__device__ __forceinline__ uint32_t lds_scene_f4(const Scene& S, uint32_t num_tris) {
+  return 4u * S.num_nodes + 3u * (num_tris + 3u);
+}
+// cooperative copy of nodes + tris into `dst` (all threads of the
+// workgroup; caller syncs); returns whether the scene fits
+__device__ __forceinline__ bool stage_scene(Scene& S, uint32_t num_tris, float4* dst) {
+  const uint32_t n4 = lds_scene_f4(S, num_tris);
+  if (n4 > RT_LDS_SCENE_F4) return false;
+  const uint32_t nn = 4u * S.num_nodes;
+  for (uint32_t i = threadIdx.x; i < n4; i += blockDim.x)
+    dst[i] = S.A.ld_f4(i < nn ? S.nodes + 16u * i : S.tris + 16u * (i - nn));
+  S.lnodes = dst;
+  S.ltris = dst + nn;
+  return true;
+}
 
 __device__ __forceinline__ Scene load_scene(const rt_kernel_arg_t* a) {
   Scene s;
@@ -198,6 +222,9 @@ __device__ __forceinline__ int32_t trace(const Scene& S, const Ray& r, float tmi
         const uint32_t no = S.nodes + 64u * (uint32_t)r0;
         st = node_step(S.A.sld_f4(no), S.A.sld_f4(no + 16), S.A.sld_f4(no + 32),
                        S.A.sld_f4(no + 48), r, tmin, lim);
+      } else if (S.lnodes) {
+        const float4* n = S.lnodes + 4u * (uint32_t)ref;
+        st = node_step(n[0], n[1], n[2], n[3], r, tmin, lim);
       } else {
         const uint32_t no = S.nodes + 64u * (uint32_t)ref;
         st = node_step(S.A.ld_f4(no), S.A.ld_f4(no + 16), S.A.ld_f4(no + 32),
@@ -252,9 +279,14 @@ __device__ __forceinline__ int32_t trace(const Scene& S, const Ray& r, float tmi
 #pragma unroll
         for (uint32_t j = 0; j < RT_LEAF_BATCH; ++j) {
           const uint32_t k = k0 + j;
-          ta[j] = S.A.ld_f4(to + 48u * k);
-          tb[j] = S.A.ld_f4(to + 48u * k + 16);
-          tc[j] = S.A.ld_f4(to + 48u * k + 32);
+          if (S.ltris) {
+            const float4* tr = S.ltris + 3u * (first + k);
+            ta[j] = tr[0]; tb[j] = tr[1]; tc[j] = tr[2];
+          } else {
+            ta[j] = S.A.ld_f4(to + 48u * k);
+            tb[j] = S.A.ld_f4(to + 48u * k + 16);
+            tc[j] = S.A.ld_f4(to + 48u * k + 32);
+          }
         }
 #pragma unroll
         for (uint32_t j = 0; j < RT_LEAF_BATCH; ++j) {

@@ -93,3 +93,23 @@ def test_pt_instrumented_counters_equal_oracle_traversal(po):
                     "shadow_rays", "bounce_rays", "occluded"):
             assert st[key] == k[key], key
         assert np.array_equal(r.framebuffer(), c)
+
+
+@pytest.mark.parametrize("size,bounces", [(256, 4), (1024, 4), (333, 2)])
+def test_pt_compact_image_bit_exact_vs_oracle(po, size, bounces):
+    """The block-compacted path tracer (PT_MODE 0, lib/pt_compact/) renders
+    the same frame as the default per-lane image and the oracle."""
+    import os
+    from skybox_rt_amd import _lib
+    s, _, osc, bvh = setup(po, "tekkaman")
+    r = rt.Renderer(s, kernel_dir=os.path.join(_lib.LIB_DIR, "pt_compact"))
+    r.configure(size, size, path=True, bounces=bounces)
+    r.render()
+    st = r.stats()
+    c, _, _, k = po.rt_render(osc, po.rt_params(size, size, path=True, bounces=bounces, nthreads=8),
+                              bvh=bvh)
+    assert np.array_equal(r.framebuffer(), c)
+    for key in ("geometry_hits", "shadow_rays", "occluded", "bounce_rays"):
+        assert st[key] == k[key], key
+    assert st["block"] == 256                              # the compacting image ran
+    r.close()
