@@ -91,6 +91,10 @@ int rt_read_framebuffer(rt_renderer_h r, uint32_t* out, uint64_t count);
 /* RT_RENDER_RASTER: the depth/stencil buffer (stencil << 24 | depth), W*H */
 int rt_read_depthbuffer(rt_renderer_h r, uint32_t* out, uint64_t count);
 
+/* raw per-workgroup counter rows of the last launch (16 u32 each; the
+ * RT_STAMPS diagnostic images put wave timestamps in slots 12-15) */
+int rt_launch_rows(rt_renderer_h r, uint32_t* rows, uint64_t max_rows, uint64_t* nrows);
+
 /* device pointer + byte size of the output buffer (for RCCL gathers) and the
  * HIP stream the kernel runs on (for stream-ordered consumers) */
 int rt_framebuffer_device(rt_renderer_h r, void** device_ptr, uint64_t* bytes);

@@ -1,0 +1,65 @@
+#!/usr/bin/env python3
+"""Per-wave timeline of one RT frame from the RT_STAMPS diagnostic image
+(skybox_rt_amd/lib/variants/stamp): every one-wave workgroup records its start
+(s_memrealtime, 100 MHz), duration and placement in its counter row.  Prints a
+JSON summary: kernel span, wave-lifetime distribution, slot utilisation over
+time, the tail, and the lifetime of model vs background waves.  Timing-only
+diagnostic; the stamps never reach an output value."""
+import json
+import os
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def main():
+    size = int(sys.argv[1]) if len(sys.argv) > 1 else 1024
+    import torch  # noqa: F401
+    from skybox_rt_amd import rt
+    s = rt.Scene.load(os.path.join(ROOT, "tests/golden/scenes/tekkaman.cgltrace"))
+    r = rt.Renderer(s, kernel_dir=os.path.join(ROOT, "skybox_rt_amd/lib/variants/stamp"))
+    r.configure(size, size, shadows=True)
+    for _ in range(5):
+        r.render()
+    rows = r.launch_rows().astype(np.int64)
+    kms = r.kernel_ms()
+    base = rows[:, 12].min()
+    t0 = rows[:, 12] - base
+    end = rows[:, 13] - base
+    dur = end - t0
+    prim = rows[:, 14] - rows[:, 12]           # start -> primary traced
+    drain = np.where(rows[:, 15] > 0, rows[:, 13] - rows[:, 15], 0)  # final shadow drain
+    span = end.max()
+    # slot utilisation: waves alive per 1 us bucket
+    nb = int(span // 100) + 1
+    alive = np.zeros(nb)
+    for a, b in zip(t0, end):
+        alive[a // 100:(b // 100) + 1] += 1
+    q = lambda x, p: float(np.percentile(x, p))  # noqa: E731
+    n = len(dur)
+    # wave w renders chunk w (one chunk per wave): the model waves are the
+    # slow ones; report the lifetime by chunk decile of duration
+    out = {
+        "size": size, "waves": int(n), "event_kernel_us": round(kms * 1e3, 1),
+        "stamp_span_us": round(span / 100.0, 1),
+        "wave_us": {"p10": q(dur, 10) / 100, "p50": q(dur, 50) / 100, "p90": q(dur, 90) / 100,
+                    "p99": q(dur, 99) / 100, "max": float(dur.max()) / 100},
+        "start_us": {"p50": q(t0, 50) / 100, "p90": q(t0, 90) / 100, "max": float(t0.max()) / 100},
+        "alive_per_us": [int(x) for x in alive[::max(1, nb // 40)]],
+        "sum_wave_us_over_span": round(float(dur.sum()) / float(span), 1),
+        "last_start_to_end_us": round(float(span - t0.max()) / 100, 1),
+    }
+    slow = np.argsort(dur)[-50:]
+    out["slowest50"] = {"wave_us": float(dur[slow].mean()) / 100,
+                        "primary_us": float(prim[slow].mean()) / 100,
+                        "shadow_drain_us": float(drain[slow].mean()) / 100,
+                        "start_us": float(t0[slow].mean()) / 100}
+    out["all"] = {"primary_us": float(prim.mean()) / 100, "shadow_drain_us": float(drain.mean()) / 100}
+    print(json.dumps(out))
+
+
+if __name__ == "__main__":
+    main()

@@ -71,6 +71,7 @@ struct rt_renderer {
   vx_buffer_h krnl[4][2] = {};
   vx_buffer_h nodes = nullptr, tris = nullptr, layers = nullptr, dcs = nullptr, tex = nullptr;
   vx_buffer_h ptris = nullptr, geom = nullptr, oms = nullptr, bbox = nullptr, zbuf = nullptr;
+  vx_buffer_h order = nullptr;
   vx_buffer_h prims = nullptr, cbuf = nullptr, args = nullptr;
   uint64_t cbuf_bytes = 0;
   rt_render_params_t params{};
@@ -80,11 +81,12 @@ struct rt_renderer {
   vx_hip_mem_ptr_t mem_ptr = nullptr;
   vx_hip_stream_t stream = nullptr;
   vx_hip_last_run_t last_run = nullptr;
+  vx_hip_mpm_rows_t mpm_rows = nullptr;
 
   ~rt_renderer() {
     vx_buffer_h* bufs[] = {&krnl[0][0], &krnl[0][1], &krnl[1][0], &krnl[1][1], &krnl[2][0],
                            &krnl[2][1], &krnl[3][0], &nodes, &tris, &layers, &dcs, &tex,
-                           &ptris, &geom, &oms, &bbox, &zbuf, &prims, &cbuf, &args};
+                           &ptris, &geom, &oms, &bbox, &zbuf, &order, &prims, &cbuf, &args};
     for (auto* b : bufs) {
       if (*b) vx_mem_free(*b);
       *b = nullptr;
@@ -240,6 +242,7 @@ int rt_renderer_create(rt_scene_h s, const char* kernel_dir, rt_renderer_h* out)
   r->mem_ptr = (vx_hip_mem_ptr_t)vx_driver_symbol("vx_hip_mem_ptr");
   r->stream = (vx_hip_stream_t)vx_driver_symbol("vx_hip_stream");
   r->last_run = (vx_hip_last_run_t)vx_driver_symbol("vx_hip_last_run");
+  r->mpm_rows = (vx_hip_mpm_rows_t)vx_driver_symbol("vx_hip_mpm_rows");
   rt_kernel_arg_t& a = r->arg;
   std::memset(&a, 0, sizeof(a));
   const rt::Bvh& bvh = s->bvh;
@@ -401,6 +404,33 @@ int rt_renderer_configure(rt_renderer_h r, const rt_render_params_t* p) {
   a.num_tasks = r->local_tiles * (raster ? 256u : RT_TILE_PIXELS);
   a.shard_index = p->shard_index;
   a.shard_count = shards;
+  // Work order of this shard's 32x32 tiles: heaviest first (longest
+  // processing time first) -- weight = geometry primitives whose screen box
+  // touches the tile -- so the long model waves start with the frame rather
+  // than trailing it.  Output is order independent.  RT_TILE_ORDER=0: identity.
+  a.order_addr = 0;
+  if (!raster && r->local_tiles > 0 && !(std::getenv("RT_TILE_ORDER") &&
+                                         std::atoi(std::getenv("RT_TILE_ORDER")) == 0)) {
+    std::vector<uint32_t> weight(tiles, 0);
+    for (size_t d = 0; d < s->scene.drawcalls.size(); ++d) {
+      const rt::DrawCall& dc = s->scene.drawcalls[d];
+      if (!dc.states.depth_test) continue;  // screen layers cost the same everywhere
+      for (uint32_t i = 0; i < dc.prim_count; ++i) {
+        rt_bbox_t bb;
+        if (rt::PrimBBox(s->scene.prims[dc.prim_offset + i], p->width, p->height, &bb) != rt::kSetupOk)
+          continue;
+        const uint32_t tx0 = (bb.x & 0xffffu) >> RT_TILE_LOG, tx1 = ((bb.x >> 16) + 31u) >> RT_TILE_LOG;
+        const uint32_t ty0 = (bb.y & 0xffffu) >> RT_TILE_LOG, ty1 = ((bb.y >> 16) + 31u) >> RT_TILE_LOG;
+        for (uint32_t ty = ty0; ty < ty1 && ty < a.tiles_y; ++ty)
+          for (uint32_t tx = tx0; tx < tx1 && tx < a.tiles_x; ++tx) ++weight[ty * a.tiles_x + tx];
+      }
+    }
+    std::vector<uint32_t> ord(r->local_tiles);
+    for (uint32_t i = 0; i < r->local_tiles; ++i) ord[i] = i;
+    auto w = [&](uint32_t lt) { return weight[p->shard_index + lt * shards]; };
+    std::stable_sort(ord.begin(), ord.end(), [&](uint32_t x, uint32_t y) { return w(x) > w(y); });
+    if (upload(r->dev, ord.data(), ord.size() * 4, &r->order, &a.order_addr)) return -1;
+  }
   a.flags = ((p->flags & RT_RENDER_SHADOWS) ? RT_FLAG_SHADOWS : 0u) |
             ((p->flags & RT_RENDER_PATH) ? RT_FLAG_PATH : 0u) |
             ((p->flags & RT_RENDER_FLAT) ? RT_FLAG_FLAT : 0u) |
@@ -490,6 +520,11 @@ int rt_read_depthbuffer(rt_renderer_h r, uint32_t* out, uint64_t count) {
   const uint64_t n = (uint64_t)r->params.width * r->params.height;
   if (count < n) return fail("buffer too small");
   return vx_copy_from_dev(out, r->zbuf, 0, n * 4) == 0 ? 0 : fail("vx_copy_from_dev failed");
+}
+
+int rt_launch_rows(rt_renderer_h r, uint32_t* rows, uint64_t max_rows, uint64_t* nrows) {
+  if (!r || !r->mpm_rows) return fail("not available");
+  return r->mpm_rows(r->dev, rows, max_rows, nrows) == 0 ? 0 : fail("vx_hip_mpm_rows failed");
 }
 
 int rt_framebuffer_device(rt_renderer_h r, void** ptr, uint64_t* bytes) {

@@ -118,4 +118,6 @@ typedef struct {
   uint64_t zbuf_addr;      // raster mode: depth/stencil buffer, W*H u32
   uint64_t oms_addr;       // raster mode: rt_omstate_t per drawcall
   uint64_t bbox_addr;      // raster mode: rt_bbox_t per pid
+  uint64_t order_addr;     // RT modes: u32 per local tile, the order tiles are worked in
+                           // (heaviest first; 0 = identity), see rt_app.cpp TileOrder
 } rt_kernel_arg_t;

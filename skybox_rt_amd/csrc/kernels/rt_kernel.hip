@@ -107,6 +107,9 @@ __device__ __forceinline__ void kernel_body(const vx_task_t& task, const Scene& 
   const bool tie_high = (S.flags & RT_FLAG_TIE_HIGH) != 0;
   float th = 0.0f;
   const int32_t hit = trace_closest(S, r, tie_high, in, &th, w, cnt);
+#ifdef RT_STAMPS
+  if (lane_id() == 0) __vx_mpm_lds[14] = (uint32_t)__builtin_amdgcn_s_memrealtime();
+#endif
   cnt.hits += hit >= 0;
 #ifdef RT_ABLATE_LAYERS  // timing-only ablation (scripts/ab_variants.py)
   const int32_t spid = hit;
@@ -156,6 +159,9 @@ __device__ __forceinline__ void kernel_body(const vx_task_t& task, const Scene& 
 // rays while the queue holds >= 64 (or whatever is left at the end).
 __device__ __forceinline__ void shadow_drain(bool final, const Scene& S, WaveLds& w,
                                              Counters& cnt) {
+#ifdef RT_STAMPS
+  if (final && lane_id() == 0) __vx_mpm_lds[15] = (uint32_t)__builtin_amdgcn_s_memrealtime();
+#endif
   if (!(S.flags & RT_FLAG_SHADOWS)) return;
   const uint32_t lane = lane_id();
   uint32_t n = w.q_count;
@@ -199,6 +205,9 @@ VX_MAIN(rt_kernel_arg_t, arg, RT_BLOCK_THREADS) {
 #endif
   __shared__ WaveLds s_wave[kWaves];
   WaveLds& w = s_wave[threadIdx.x >> 6];
+#ifdef RT_STAMPS
+  const uint64_t t_stamp0 = __builtin_amdgcn_s_memrealtime();
+#endif
   Counters cnt;
   Scene S = load_scene(arg);
 #if RT_LDS_SCENE
@@ -229,6 +238,14 @@ VX_MAIN(rt_kernel_arg_t, arg, RT_BLOCK_THREADS) {
   const int rc = vx_spawn_tasks(
       arg->num_tasks,
       [&](const vx_task_t& task, const Scene* s) { kernel_body(task, *s, w, cnt); }, &S);
+#endif
+#ifdef RT_STAMPS  // diagnostic image: per-wave phase timestamps
+  if (threadIdx.x == 0) {
+    // 12: start, 13: end, 14: primary traced, 15: shadow drain begins
+    // (low 32 bits of s_memrealtime, 100 MHz)
+    __vx_mpm_lds[12] = (uint32_t)t_stamp0;
+    __vx_mpm_lds[13] = (uint32_t)__builtin_amdgcn_s_memrealtime();
+  }
 #endif
   flush(RT_STAT_PRIMARY, cnt.primary);
   flush(RT_STAT_SHADOW, cnt.shadow);

@@ -42,7 +42,7 @@ struct Counters {
 // arena offsets (rt_app checks every buffer lies below 4 GiB).
 struct Scene {
   vx_arena A;
-  uint32_t nodes, tris, layers, prims, dcs, cbuf, ptris, geom;
+  uint32_t nodes, tris, layers, prims, dcs, cbuf, ptris, geom, order;
   uint32_t num_nodes, num_layer, num_geom, flags, width, height;
   uint32_t shard_index, shard_count, tiles_x, clear_color, bounces, seed;
   float sx, sy, light[3];
@@ -83,6 +83,7 @@ __device__ __forceinline__ Scene load_scene(const rt_kernel_arg_t* a) {
   s.cbuf = (uint32_t)a->cbuf_addr;
   s.ptris = (uint32_t)a->ptris_addr;
   s.geom = (uint32_t)a->geom_addr;
+  s.order = (uint32_t)a->order_addr;
   s.num_geom = a->num_geom;
   s.bounces = a->bounces;
   s.seed = a->seed;
@@ -418,8 +419,15 @@ __device__ __forceinline__ int32_t resolve_layers(const Scene& S, const Ray& r, 
 }
 
 // task -> (shard-local 32x32 tile, 8x8 block, lane) -> pixel
+// Tasks are worked in the host's tile order (heaviest 32x32 tiles first, so
+// the long waves start at once instead of trailing the frame); `local_tile`
+// maps a task to the shard-local tile it renders.
+__device__ __forceinline__ uint32_t local_tile(const Scene& S, uint32_t t) {
+  return S.order ? S.A.ld_u32(S.order + 4u * (t >> 10)) : (t >> 10);
+}
+
 __device__ __forceinline__ void task_pixel(const Scene& S, uint32_t t, uint32_t* x, uint32_t* y) {
-  const uint32_t lt = t >> 10, blk = (t >> 6) & 15u, ln = t & 63u;
+  const uint32_t lt = local_tile(S, t), blk = (t >> 6) & 15u, ln = t & 63u;
   const uint32_t gt = S.shard_index + lt * S.shard_count;
   const uint32_t tx = gt % S.tiles_x, ty = gt / S.tiles_x;
   *x = (tx << RT_TILE_LOG) + ((blk & 3u) << 3) + (ln & 7u);
@@ -449,7 +457,9 @@ __device__ __forceinline__ uint32_t shadowed(uint32_t c) {
 
 __device__ __forceinline__ void store_pixel(const Scene& S, uint32_t t, uint32_t x, uint32_t y,
                                             uint32_t color) {
-  const uint32_t idx = (S.flags & RT_FLAG_COMPACT) ? t : y * S.width + x;
+  // compact shard buffers stay in local-tile order whatever the work order
+  const uint32_t idx = (S.flags & RT_FLAG_COMPACT) ? (local_tile(S, t) << 10) | (t & 1023u)
+                                                   : y * S.width + x;
   S.A.st_u32(S.cbuf + 4u * idx, color);
 }
 

@@ -289,6 +289,16 @@ class vx_device {
   }
 
   // ---- extensions (vortex_hip.h) ----
+  int mpm_rows(uint32_t* rows, uint64_t max_rows, uint64_t* nrows) {
+    wait_idle();
+    if (nrows) *nrows = last_grid_;
+    if (!last_module_ || !rows) return last_module_ ? 0 : -1;
+    const uint64_t n = max_rows < last_grid_ ? max_rows : last_grid_;
+    HIP_CHECK(hipMemcpyAsync(rows, last_module_->mpm, n * kMpmRow * sizeof(uint32_t),
+                             hipMemcpyDeviceToHost, stream_));
+    HIP_CHECK(hipStreamSynchronize(stream_));
+    return 0;
+  }
   void* mem_ptr(uint64_t addr) { return arena_ + addr; }
   hipStream_t stream() const { return stream_; }
   int device_id() const { return device_id_; }
@@ -494,6 +504,11 @@ __attribute__((visibility("default"))) int vx_hip_last_run(vx_device_h hdevice, 
   if (grid) *grid = d->last_grid();
   if (block) *block = d->last_block();
   return 0;
+}
+__attribute__((visibility("default"))) int vx_hip_mpm_rows(vx_device_h hdevice, uint32_t* rows,
+                                                           uint64_t max_rows, uint64_t* nrows) {
+  if (hdevice == nullptr) return -1;
+  return ((vx_device*)hdevice)->mpm_rows(rows, max_rows, nrows);
 }
 __attribute__((visibility("default"))) int vx_hip_device_id(vx_device_h hdevice, int* id) {
   if (hdevice == nullptr || id == nullptr) return -1;

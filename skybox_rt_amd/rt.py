@@ -82,6 +82,7 @@ def lib():
             "rt_render_kernel_ms": [vp, C.POINTER(C.c_double)],
             "rt_read_framebuffer": [vp, vp, u64],
             "rt_read_depthbuffer": [vp, vp, u64],
+            "rt_launch_rows": [vp, vp, u64, C.POINTER(u64)],
             "rt_scene_setup_prims": [vp, u32, u32, vp, u64],
             "rt_framebuffer_device": [vp, C.POINTER(vp), C.POINTER(u64)],
             "rt_device_stream": [vp, C.POINTER(vp)],
@@ -212,6 +213,14 @@ class Renderer:
         out = np.zeros((p.height, p.width), np.uint32)
         _check(lib().rt_read_framebuffer(self._h, out.ctypes.data, out.size), "rt_read_framebuffer")
         return out
+
+    def launch_rows(self) -> np.ndarray:
+        """uint32 [grid, 16]: the last launch's per-workgroup counter rows."""
+        n = C.c_uint64()
+        _check(lib().rt_launch_rows(self._h, None, 0, C.byref(n)), "rt_launch_rows")
+        out = np.zeros((max(n.value, 1), 16), np.uint32)
+        _check(lib().rt_launch_rows(self._h, out.ctypes.data, n.value, C.byref(n)), "rt_launch_rows")
+        return out[:n.value]
 
     def depthbuffer(self) -> np.ndarray:
         """RT_RENDER_RASTER: uint32 [H, W] depth/stencil words (stencil << 24 | depth)."""
