@@ -30,18 +30,19 @@ sys.path.insert(0, ROOT)
 SCENE = os.path.join(ROOT, "tests", "golden", "scenes", "tekkaman.cgltrace")
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
 NODE_BYTES, TRI_BYTES, PIXEL_BYTES = 64, 36, 4
+NODE4_BYTES = 112      # BVH4 node: 6 SoA box float4 + the child-ref float4 (pad not read)
 
 
 def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
-def algorithmic_bytes(st: dict, pixels: int) -> int:
-    """node bytes x nodes visited + 36 B x triangles tested
+def algorithmic_bytes(st: dict, pixels: int, node_bytes: int = NODE_BYTES) -> int:
+    """node bytes (64 B BVH2, 112 B BVH4) x nodes visited + 36 B x triangles tested
     (BVH leaves and screen layers) + texel bytes per shaded pixel + 4 B per
     pixel written.  Counts come from the instrumented kernel variant, whose
     counters tests/test_gpu_rt.py checks equal to the oracle's traversal."""
-    return (NODE_BYTES * st["node_visits"] + TRI_BYTES * (st["tri_tests"] + st["layer_tests"])
+    return (node_bytes * st["node_visits"] + TRI_BYTES * (st["tri_tests"] + st["layer_tests"])
             + st["texel_bytes"] + PIXEL_BYTES * pixels)
 
 
@@ -69,14 +70,15 @@ def frame_side(n_gpus: int, base: int) -> int:
 
 
 def cpu_baseline(shadows: bool, side: int, light, budget_s: float, path: bool = False,
-                 bounces: int = 4, flat: bool = False):
+                 bounces: int = 4, flat: bool = False, bvh4: bool = True):
     """Oracle (C port of the same algorithm, oracle/rt.c) on the host cores,
     BVH traversal identical to the kernel's, full frames until budget_s."""
     from oracle import py_oracle as po
     from skybox_rt_amd import rt as rtmod
     cores = max(1, min(16, os.cpu_count() or 1))
     osc = po.OracleScene(po.cgltrace.load(SCENE))
-    bvh = rtmod.Scene.load(SCENE).bvh()
+    sc = rtmod.Scene.load(SCENE)
+    bvh = sc.bvh() + ((sc.bvh4(),) if bvh4 else ())
     p = po.rt_params(side, side, shadows=shadows, light=light, nthreads=cores, path=path,
                      bounces=bounces)
     frames, rays, t0 = 0, 0, time.perf_counter()
@@ -89,7 +91,7 @@ def cpu_baseline(shadows: bool, side: int, light, budget_s: float, path: bool = 
             break
     return {"value": rays / el / 1e6, "unit": "Mrays/s", "cores": cores, "kind": "port",
             "sample": f"{frames} full {side}x{side} frames of the same workload "
-                      f"({el:.1f} s, oracle/rt.c {'brute force' if flat else 'BVH traversal'}, "
+                      f"({el:.1f} s, oracle/rt.c {'brute force' if flat else ('BVH4' if bvh4 else 'BVH2') + ' traversal'}, "
                       f"{cores} threads)"}
 
 
@@ -150,7 +152,8 @@ def main():
     r.render()
     inst = r.stats()
     pixels_local = inst["primary_rays"]
-    alg_bytes = algorithmic_bytes(inst, pixels_local)
+    bvh_kind = "BVH4" if r.bvh4 else "BVH2"
+    alg_bytes = algorithmic_bytes(inst, pixels_local, NODE4_BYTES if r.bvh4 else NODE_BYTES)
 
     r.configure(side, side, shadows=shadows, light=light, shard_index=rank, shard_count=n_gpus,
                 path=path, bounces=args.bounces, flat=flat)
@@ -239,14 +242,15 @@ def main():
         "data": "tekkaman.cgltrace from the reference's regression data (tests/golden/scenes)",
         "config": {
             "workload": (f"{side}x{side} {kind}, tekkaman.cgltrace" if flat else
-                         f"{side}x{side} {kind}, tekkaman.cgltrace, BVH2 + LDS stack" if path else
+                         f"{side}x{side} {kind}, tekkaman.cgltrace, {bvh_kind} + LDS stack" if path else
                          f"{side}x{side} {'primary+shadow' if shadows else 'primary'} rays, "
-                         f"tekkaman.cgltrace, BVH2 + LDS stack"),
+                         f"tekkaman.cgltrace, {bvh_kind} + LDS stack"),
             "scene": "tekkaman.cgltrace", "width": side, "height": side,
             "shadow_rays": shadows, "light_clip_xyw": list(light),
             "parallelism": f"tiles32 mod {n_gpus}" + (f" + {'rccl' if backend == 'nccl' else backend} "
                                                       f"gather" if n_gpus > 1 else ""),
-            "bvh_nodes": info["bvh_nodes"], "bvh_depth": info["bvh_depth"],
+            "bvh_nodes": info["bvh4_nodes" if r.bvh4 else "bvh_nodes"],
+            "bvh_depth": info["bvh4_depth" if r.bvh4 else "bvh_depth"],
             "grid": st["grid"], "block": st["block"],
             "rays_per_frame": int(rays_total),
             "mrays_per_s_per_gpu": round(value / n_gpus, 3),
@@ -269,7 +273,7 @@ def main():
     if n_gpus == 1 and not args.no_cpu_baseline:
         try:
             out["cpu_baseline"] = cpu_baseline(shadows, side, light, args.cpu_budget, path,
-                                               args.bounces, flat)
+                                               args.bounces, flat, r.bvh4)
         except Exception as e:  # the baseline is reported, not required
             log(f"cpu baseline failed: {e}")
     print(json.dumps(out), flush=True)

@@ -26,7 +26,7 @@ typedef struct rt_renderer* rt_renderer_h;
 typedef struct {
   uint32_t num_drawcalls, num_prims, num_geometry, num_layer, num_textures;
   uint32_t bvh_nodes, bvh_tris, bvh_leaves, bvh_depth;
-  uint32_t pad;
+  uint32_t bvh4_nodes, bvh4_depth, bvh4_stack;  /* the 4-wide BVH collapsed from it */
   double parse_ms, bvh_ms;
 } rt_scene_info_t;
 
@@ -35,6 +35,8 @@ typedef struct {
 #define RT_RENDER_FLAT 0x10u           /* flat triangle list, no BVH (config 2; rt_flat) */
 #define RT_RENDER_RASTER 0x20u         /* the draw3d raster pipeline (raster_kernel): any
                                           scene incl. blending/stencil; shard_count 1 */
+#define RT_RENDER_BVH2 0x40u           /* traverse the binary BVH (default: the 4-wide one;
+                                          env RT_BVH_WIDTH=2 flips the default) */
 #define RT_RENDER_INSTRUMENTED 0x100u  /* use the counting kernel variant */
 
 typedef struct {
@@ -67,6 +69,8 @@ int rt_scene_info(rt_scene_h scene, rt_scene_info_t* info);
 int rt_scene_export_prims(rt_scene_h scene, float* out, uint64_t count);
 /* BVH arrays: float[bvh_nodes][16], float[bvh_tris][12] */
 int rt_scene_export_bvh(rt_scene_h scene, float* nodes, float* tris);
+/* 4-wide BVH nodes: float[bvh4_nodes][32] (rt_node4_t); leaves index the same tris */
+int rt_scene_export_bvh4(rt_scene_h scene, float* nodes4);
 /* fixed-point shading records (rt_prim_t) at width x height: int32[num_prims][32] */
 int rt_scene_setup_prims(rt_scene_h scene, uint32_t width, uint32_t height, int32_t* out,
                          uint64_t count);

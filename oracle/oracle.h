@@ -114,6 +114,9 @@ typedef struct {
   const float* nodes;               /* [num_nodes][16] (4 x float4) */
   int32_t num_tris;
   const float* tris;                /* [num_tris][12]  (v0,pid | e1,- | e2,-) */
+  int32_t num_nodes4;               /* > 0: traverse the 4-wide BVH instead */
+  const float* nodes4;              /* [num_nodes4][32] (lo.x[4] hi.x[4] lo.y hi.y lo.z hi.z
+                                       child[4] pad[4]) */
 } orc_bvh_t;
 
 /* Brute-force (no BVH) reference: closest hit over every geometry triangle,

@@ -65,7 +65,8 @@ class RtCountersC(C.Structure):
 
 class BvhC(C.Structure):
     _fields_ = [("num_nodes", C.c_int32), ("nodes", C.POINTER(C.c_float)),
-                ("num_tris", C.c_int32), ("tris", C.POINTER(C.c_float))]
+                ("num_tris", C.c_int32), ("tris", C.POINTER(C.c_float)),
+                ("num_nodes4", C.c_int32), ("nodes4", C.POINTER(C.c_float))]
 
 
 def build():
@@ -164,7 +165,8 @@ def rt_params(width, height, shadows=True, light=(0.0, 60.0, 80.0), nthreads=1,
 
 
 def rt_render(oscene: OracleScene, params: RtParamsC, bvh=None):
-    """bvh: None (brute force) or (nodes float32[N,16], tris float32[M,12])."""
+    """bvh: None (brute force), (nodes float32[N,16], tris float32[M,12]) or
+    (nodes, tris, nodes4 float32[N4,32]) -- the last traverses the 4-wide BVH."""
     n = params.width * params.height
     color = np.zeros(n, np.uint32)
     pid = np.full(n, -1, np.int32)
@@ -176,7 +178,11 @@ def rt_render(oscene: OracleScene, params: RtParamsC, bvh=None):
     else:
         nodes = np.ascontiguousarray(bvh[0], np.float32)
         tris = np.ascontiguousarray(bvh[1], np.float32)
-        b = BvhC(nodes.shape[0], _ptr(nodes, C.c_float), tris.shape[0], _ptr(tris, C.c_float))
+        b = BvhC(nodes.shape[0], _ptr(nodes, C.c_float), tris.shape[0], _ptr(tris, C.c_float), 0,
+                 None)
+        if len(bvh) > 2 and bvh[2] is not None:
+            nodes4 = np.ascontiguousarray(bvh[2], np.float32)
+            b.num_nodes4, b.nodes4 = nodes4.shape[0], _ptr(nodes4, C.c_float)
         rc = lib().orc_rt_render_bvh(C.byref(oscene.c), C.byref(b), C.byref(params),
                                      color.ctypes.data, pid.ctypes.data, t.ctypes.data,
                                      C.byref(cnt))

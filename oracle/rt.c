@@ -18,6 +18,7 @@
  *   - shading of a hit = draw3d shader (kernel.cpp:232-279) evaluated with
  *     the hit primitive's fixed-point edge functions at the pixel centre.
  */
+#include <float.h>
 #include <pthread.h>
 #include <stdlib.h>
 #include <string.h>
@@ -177,6 +178,45 @@ static inline int32_t node_ref(const float* n, int ch) {
   return r;
 }
 
+/* BVH4 node step (the kernel's rt_trace.h trace(), RT_FLAG_BVH4 branch):
+ * slab-test the 4 children, order the hits by tnear with the same 5-exchange
+ * sorting network (strict <, misses keyed +inf, hit keys clamped to FLT_MAX),
+ * continue with the nearest and push the others farthest first.  Returns the
+ * next ref, or BVH_EMPTY when nothing was hit. */
+static int32_t bvh4_step(const float* n, const ray_pre_t* r, float tmin, float lim,
+                         int32_t* stack, int* sp) {
+  float key[4];
+  int32_t ref[4];
+  int cnt = 0;
+  for (int i = 0; i < 4; ++i) {
+    memcpy(&ref[i], &n[24 + i], 4);
+    float lo[3], hi[3];
+    for (int k = 0; k < 3; ++k) {
+      lo[k] = fmaf(n[8 * k + i], r->inv[k], -r->oi[k]);
+      hi[k] = fmaf(n[8 * k + 4 + i], r->inv[k], -r->oi[k]);
+    }
+    const float t0 = fminf(lo[0], hi[0]), t1 = fminf(lo[1], hi[1]), t2 = fminf(lo[2], hi[2]);
+    const float u0 = fmaxf(lo[0], hi[0]), u1 = fmaxf(lo[1], hi[1]), u2 = fmaxf(lo[2], hi[2]);
+    const float tn = fmaxf(fmaxf(t0, t1), fmaxf(t2, tmin));
+    const float tf = fminf(fminf(u0, u1), fminf(u2, lim));
+    const int h = ref[i] != BVH_EMPTY && tn <= tf;
+    key[i] = h ? fminf(tn, FLT_MAX) : INFINITY;
+    cnt += h;
+  }
+  static const int net[5][2] = {{0, 1}, {2, 3}, {0, 2}, {1, 3}, {1, 2}};
+  for (int e = 0; e < 5; ++e) {
+    const int a = net[e][0], b = net[e][1];
+    if (key[b] < key[a]) {
+      const float tk = key[a]; key[a] = key[b]; key[b] = tk;
+      const int32_t tr = ref[a]; ref[a] = ref[b]; ref[b] = tr;
+    }
+  }
+  if (cnt == 0) return BVH_EMPTY;
+  for (int i = cnt - 1; i >= 1; --i)
+    if (*sp < BVH_STACK) stack[(*sp)++] = ref[i];
+  return ref[0];
+}
+
 /* closest (anyhit=0) or any (anyhit=1) hit; returns hit pid or -1 */
 static int bvh_trace(const rt_ctx_t* c, const float o[3], const float d[3], float tmin,
                      float tmax, int anyhit, int skip_pid, float* t_out,
@@ -191,7 +231,12 @@ static int bvh_trace(const rt_ctx_t* c, const float o[3], const float d[3], floa
   float bt = tmax;
   int bpid = -1;
   for (;;) {
-    if (ref >= 0) {
+    if (ref >= 0 && b->num_nodes4 > 0) {
+      ++*visits;
+      const int32_t nx = bvh4_step(b->nodes4 + (size_t)ref * 32, &rp, tmin, anyhit ? tmax : bt,
+                                   stack, &sp);
+      if (nx != BVH_EMPTY) { ref = nx; continue; }
+    } else if (ref >= 0) {
       const float* n = b->nodes + (size_t)ref * 16;
       ++*visits;
       const int32_t c0 = node_ref(n, 0), c1 = node_ref(n, 1);

@@ -170,6 +170,94 @@ class Builder {
   float pad_ = 0.0f;
 };
 
+// Collapse the BVH2 into a BVH4: a node's children are repeatedly replaced
+// by the children of its largest-area internal child (in place, so the order
+// stays left to right) until it has 4 or none is internal.  Boxes are copied
+// verbatim from the BVH2 nodes that stored them.
+class Collapser {
+ public:
+  explicit Collapser(Bvh* b) : b_(b) {}
+  void run() {
+    b_->nodes4.clear();
+    b_->depth4 = 0;
+    b_->stack4 = 0;
+    if (b_->nodes.empty()) return;
+    uint32_t st = 0;
+    collapse(0, 1, &st);
+    b_->stack4 = st;
+  }
+
+ private:
+  struct Child {
+    float lo[3], hi[3];
+    int32_t ref;
+  };
+  Child child_of(uint32_t n, int ch) const {
+    const rt_node_t& nd = b_->nodes[n];
+    Child c;
+    for (int k = 0; k < 3; ++k) {
+      c.lo[k] = nd.v[4 * k + 2 * ch + 0];
+      c.hi[k] = nd.v[4 * k + 2 * ch + 1];
+    }
+    std::memcpy(&c.ref, &nd.v[12 + ch], 4);
+    return c;
+  }
+  static double area(const Child& c) {
+    const double dx = (double)c.hi[0] - c.lo[0], dy = (double)c.hi[1] - c.lo[1],
+                 dz = (double)c.hi[2] - c.lo[2];
+    return 2.0 * (dx * dy + dy * dz + dz * dx);
+  }
+  // returns the BVH4 index of BVH2 node n; *stack = worst-case stack
+  // entries needed below (and including) this node
+  uint32_t collapse(uint32_t n, uint32_t depth, uint32_t* stack) {
+    b_->depth4 = std::max(b_->depth4, depth);
+    std::vector<Child> cs;
+    for (int ch = 0; ch < 2; ++ch) {
+      const Child c = child_of(n, ch);
+      if (c.ref != RT_EMPTY_REF) cs.push_back(c);
+    }
+    while (cs.size() < 4) {
+      int best = -1;
+      double ba = -1.0;
+      for (size_t i = 0; i < cs.size(); ++i)
+        if (cs[i].ref >= 0 && area(cs[i]) > ba) { ba = area(cs[i]); best = (int)i; }
+      if (best < 0) break;
+      const uint32_t m = (uint32_t)cs[best].ref;
+      std::vector<Child> sub;
+      for (int ch = 0; ch < 2; ++ch) {
+        const Child c = child_of(m, ch);
+        if (c.ref != RT_EMPTY_REF) sub.push_back(c);
+      }
+      cs.erase(cs.begin() + best);
+      cs.insert(cs.begin() + best, sub.begin(), sub.end());
+    }
+    const uint32_t idx = (uint32_t)b_->nodes4.size();
+    b_->nodes4.emplace_back();
+    uint32_t below = 0;
+    for (size_t i = 0; i < cs.size(); ++i)
+      if (cs[i].ref >= 0) {
+        uint32_t st = 0;
+        cs[i].ref = (int32_t)collapse((uint32_t)cs[i].ref, depth + 1, &st);
+        below = std::max(below, st);
+      }
+    rt_node4_t& o = b_->nodes4[idx];
+    std::memset(&o, 0, sizeof(o));
+    for (int i = 0; i < 4; ++i) {
+      const bool used = i < (int)cs.size();
+      for (int k = 0; k < 3; ++k) {
+        o.v[8 * k + i] = used ? cs[i].lo[k] : 0.0f;
+        o.v[8 * k + 4 + i] = used ? cs[i].hi[k] : 0.0f;
+      }
+      const int32_t ref = used ? cs[i].ref : RT_EMPTY_REF;
+      std::memcpy(&o.v[24 + i], &ref, 4);
+    }
+    // descending into one child pushes at most the other (cs.size() - 1)
+    *stack = (uint32_t)(cs.empty() ? 0 : cs.size() - 1) + below;
+    return idx;
+  }
+  Bvh* b_;
+};
+
 }  // namespace
 
 int BuildBvh(const std::vector<BuildTri>& tris, Bvh* out, std::string* error) {
@@ -180,6 +268,7 @@ int BuildBvh(const std::vector<BuildTri>& tris, Bvh* out, std::string* error) {
   }
   Builder b(tris, out);
   b.run();
+  Collapser(out).run();
   if (out->depth > RT_STACK_DEEP) {
     if (error) *error = "BVH deeper than RT_STACK_DEEP";
     return -1;

@@ -26,6 +26,10 @@ struct Bvh {
   std::vector<rt_tri_t> tris;    // leaf order
   uint32_t depth = 0;            // internal levels on the deepest path
   uint32_t leaves = 0;
+  // BVH4 collapsed from `nodes` (same leaves and padded boxes); root = 0
+  std::vector<rt_node4_t> nodes4;
+  uint32_t depth4 = 0;
+  uint32_t stack4 = 0;           // worst-case traversal stack entries (near-first, BVH4)
 };
 
 constexpr uint32_t kBvhLeafSize = 4;

@@ -69,7 +69,7 @@ struct rt_renderer {
   // kernel images [mode][instrumented]: mode 0 = primary+shadow (BVH),
   // 1 = path trace, 2 = flat list, 3 = raster (no instrumented image)
   vx_buffer_h krnl[4][2] = {};
-  vx_buffer_h nodes = nullptr, tris = nullptr, layers = nullptr, dcs = nullptr, tex = nullptr;
+  vx_buffer_h nodes = nullptr, nodes4 = nullptr, tris = nullptr, layers = nullptr, dcs = nullptr, tex = nullptr;
   vx_buffer_h ptris = nullptr, geom = nullptr, oms = nullptr, bbox = nullptr, zbuf = nullptr;
   vx_buffer_h order = nullptr;
   vx_buffer_h prims = nullptr, cbuf = nullptr, args = nullptr;
@@ -85,7 +85,7 @@ struct rt_renderer {
 
   ~rt_renderer() {
     vx_buffer_h* bufs[] = {&krnl[0][0], &krnl[0][1], &krnl[1][0], &krnl[1][1], &krnl[2][0],
-                           &krnl[2][1], &krnl[3][0], &nodes, &tris, &layers, &dcs, &tex,
+                           &krnl[2][1], &krnl[3][0], &nodes, &nodes4, &tris, &layers, &dcs, &tex,
                            &ptris, &geom, &oms, &bbox, &zbuf, &order, &prims, &cbuf, &args};
     for (auto* b : bufs) {
       if (*b) vx_mem_free(*b);
@@ -170,6 +170,9 @@ int rt_scene_info(rt_scene_h s, rt_scene_info_t* info) {
   info->bvh_tris = (uint32_t)s->bvh.tris.size();
   info->bvh_leaves = s->bvh.leaves;
   info->bvh_depth = s->bvh.depth;
+  info->bvh4_nodes = (uint32_t)s->bvh.nodes4.size();
+  info->bvh4_depth = s->bvh.depth4;
+  info->bvh4_stack = s->bvh.stack4;
   info->parse_ms = s->parse_ms;
   info->bvh_ms = s->bvh_ms;
   return 0;
@@ -196,6 +199,12 @@ int rt_scene_export_bvh(rt_scene_h s, float* nodes, float* tris) {
   return 0;
 }
 
+int rt_scene_export_bvh4(rt_scene_h s, float* nodes4) {
+  if (!s || !nodes4) return fail("null argument");
+  std::memcpy(nodes4, s->bvh.nodes4.data(), s->bvh.nodes4.size() * sizeof(rt_node4_t));
+  return 0;
+}
+
 static int upload(vx_device_h dev, const void* data, uint64_t size, vx_buffer_h* buf, uint64_t* addr) {
   const uint64_t sz = size ? size : 64;
   if (*buf) vx_mem_free(*buf);
@@ -218,9 +227,12 @@ int rt_renderer_create(rt_scene_h s, const char* kernel_dir, rt_renderer_h* out)
     return fail("vx_dev_open failed (no GPU or driver missing)");
   }
   const std::string dir = kernel_dir ? kernel_dir : lib_dir();
-  // the regular image's LDS stack covers BVH depth <= 16; deeper trees use the
-  // deep image (32 entries, lower occupancy)
-  const bool deep = s->bvh.depth > RT_STACK_SHALLOW;
+  // the regular image's LDS stack holds RT_STACK_SHALLOW (24) entries; a BVH whose traversal may
+  // need more (BVH2: its depth, BVH4: its stack bound) uses the deep image
+  // (32 entries, lower occupancy)
+  const bool deep = std::max(s->bvh.depth, s->bvh.stack4) > RT_STACK_SHALLOW;
+  if (std::max(s->bvh.depth, s->bvh.stack4) > RT_STACK_DEEP)
+    return fail("BVH too deep for the traversal stack");
   const char* names[4][2] = {
       {deep ? "rt_kernel_deep.vxbin" : "rt_kernel.vxbin",
        deep ? "rt_kernel_deep_stats.vxbin" : "rt_kernel_stats.vxbin"},
@@ -251,9 +263,12 @@ int rt_renderer_create(rt_scene_h s, const char* kernel_dir, rt_renderer_h* out)
   tris.resize(tris.size() + 3);
   std::memset(tris.data() + bvh.tris.size(), 0, 3 * sizeof(rt_tri_t));
   if (upload(r->dev, bvh.nodes.data(), bvh.nodes.size() * sizeof(rt_node_t), &r->nodes, &a.nodes_addr) ||
+      upload(r->dev, bvh.nodes4.data(), bvh.nodes4.size() * sizeof(rt_node4_t), &r->nodes4,
+             &a.nodes4_addr) ||
       upload(r->dev, tris.data(), tris.size() * sizeof(rt_tri_t), &r->tris, &a.tris_addr))
     return -1;
   a.num_nodes = (uint32_t)bvh.nodes.size();
+  a.num_nodes4 = (uint32_t)bvh.nodes4.size();
   // screen layers, highest pid first
   std::vector<rt_tri_t> lt(s->layers.size());
   for (size_t i = 0; i < s->layers.size(); ++i) {
@@ -431,11 +446,14 @@ int rt_renderer_configure(rt_renderer_h r, const rt_render_params_t* p) {
     std::stable_sort(ord.begin(), ord.end(), [&](uint32_t x, uint32_t y) { return w(x) > w(y); });
     if (upload(r->dev, ord.data(), ord.size() * 4, &r->order, &a.order_addr)) return -1;
   }
+  bool use_bvh4 = !(p->flags & RT_RENDER_BVH2);
+  if (const char* e = std::getenv("RT_BVH_WIDTH")) use_bvh4 = use_bvh4 && std::atoi(e) != 2;
   a.flags = ((p->flags & RT_RENDER_SHADOWS) ? RT_FLAG_SHADOWS : 0u) |
             ((p->flags & RT_RENDER_PATH) ? RT_FLAG_PATH : 0u) |
             ((p->flags & RT_RENDER_FLAT) ? RT_FLAG_FLAT : 0u) |
             (raster ? RT_FLAG_RASTER : 0u) |
-            (s->tie_high ? RT_FLAG_TIE_HIGH : 0u) | (shards > 1 ? RT_FLAG_COMPACT : 0u);
+            (s->tie_high ? RT_FLAG_TIE_HIGH : 0u) | (shards > 1 ? RT_FLAG_COMPACT : 0u) |
+            (use_bvh4 ? RT_FLAG_BVH4 : 0u);
   a.bounces = p->bounces;
   a.seed = p->seed;
   a.clear_color = p->clear_color;

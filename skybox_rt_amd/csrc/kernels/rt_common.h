@@ -21,10 +21,12 @@
 #ifndef RT_BLOCK_THREADS
 #define RT_BLOCK_THREADS 64
 #endif
-// per-wave LDS traversal stack depth: the regular image covers BVHs of depth
-// <= 16 (keeps 24 waves/CU resident), the deep image up to 32; the host picks
-// the image from the built BVH's depth
-#define RT_STACK_SHALLOW 16
+// per-wave LDS traversal stack depth: the regular image holds 24 entries
+// (6 KB per wave: LDS still fits more waves than the VGPR budget allows),
+// the deep image 32; the host picks the image from the built BVH's
+// worst-case stack (BVH2: its depth; BVH4: stack4, e.g. 16-17 for the
+// reference scenes)
+#define RT_STACK_SHALLOW 24
 #define RT_STACK_DEEP 32
 #ifndef RT_MAX_STACK
 #define RT_MAX_STACK RT_STACK_SHALLOW
@@ -39,6 +41,7 @@
 #define RT_FLAG_PATH     0x8u    // diffuse path trace (pt_kernel.hip)
 #define RT_FLAG_FLAT     0x10u   // flat triangle list, no BVH (BASELINE config 2)
 #define RT_FLAG_RASTER   0x20u   // draw3d raster pipeline (raster_kernel.hip)
+#define RT_FLAG_BVH4     0x40u   // traverse the 4-wide BVH (nodes4) instead of the BVH2
 
 #define RT_DC_DEPTH   0x1u
 #define RT_DC_COLOR   0x2u
@@ -61,6 +64,12 @@ enum {
 // child ref c: >= 0 internal node index; -1 empty; otherwise a leaf:
 //   (c & 0x7fffffff) >> 4 = first triangle, (c & 15) + 1 = triangle count.
 typedef struct { float v[16]; } rt_node_t;
+
+// rt_node4_t (BVH4, 128 B): SoA over the 4 children --
+//   lo.x[4], hi.x[4], lo.y[4], hi.y[4], lo.z[4], hi.z[4], child[4], pad[4];
+// child refs as in rt_node_t (unused slots -1).  Collapsed from the BVH2
+// (bvh.cpp): same leaves, same padded boxes, half the levels.
+typedef struct { float v[32]; } rt_node4_t;
 
 // rt_tri_t: (v0.x, v0.y, v0.w, pid), (e1.xyw, 0), (e2.xyw, 0) -- clip (x,y,w)
 typedef struct { float v[12]; } rt_tri_t;
@@ -118,6 +127,8 @@ typedef struct {
   uint64_t zbuf_addr;      // raster mode: depth/stencil buffer, W*H u32
   uint64_t oms_addr;       // raster mode: rt_omstate_t per drawcall
   uint64_t bbox_addr;      // raster mode: rt_bbox_t per pid
+  uint64_t nodes4_addr;    // rt_node4_t BVH4 (images built with RT_BVH4)
+  uint32_t num_nodes4, pad5;
   uint64_t order_addr;     // RT modes: u32 per local tile, the order tiles are worked in
                            // (heaviest first; 0 = identity), see rt_app.cpp TileOrder
 } rt_kernel_arg_t;

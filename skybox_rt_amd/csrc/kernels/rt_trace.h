@@ -42,7 +42,7 @@ struct Counters {
 // arena offsets (rt_app checks every buffer lies below 4 GiB).
 struct Scene {
   vx_arena A;
-  uint32_t nodes, tris, layers, prims, dcs, cbuf, ptris, geom, order;
+  uint32_t nodes, nodes4, tris, layers, prims, dcs, cbuf, ptris, geom, order;
   uint32_t num_nodes, num_layer, num_geom, flags, width, height;
   uint32_t shard_index, shard_count, tiles_x, clear_color, bounces, seed;
   float sx, sy, light[3];
@@ -76,6 +76,7 @@ __device__ __forceinline__ Scene load_scene(const rt_kernel_arg_t* a) {
   Scene s;
   s.A = vx_arena::get();
   s.nodes = (uint32_t)a->nodes_addr;
+  s.nodes4 = (uint32_t)a->nodes4_addr;
   s.tris = (uint32_t)a->tris_addr;
   s.layers = (uint32_t)a->layers_addr;
   s.prims = (uint32_t)a->prims_addr;
@@ -201,6 +202,54 @@ __device__ __forceinline__ NodeStep node_step(const float4& n0, const float4& n1
   return o;
 }
 
+// BVH4 node step (RT_FLAG_BVH4; oracle/rt.c bvh4_step restates it): 7
+// per-lane 16-B loads (boxes SoA over the 4 children + child refs), 4 slab
+// tests, the hits ordered by tnear with a 5-exchange sorting network (strict
+// <, misses keyed +inf, hit keys clamped to FLT_MAX so they sort first); the
+// nearest is returned, the other hits are pushed farthest first.  Halves the
+// dependent load -> test -> branch steps of a root-to-leaf walk vs BVH2.
+__device__ __forceinline__ int32_t node4_step(const Scene& S, uint32_t ref, const Ray& r,
+                                              float tmin, float lim, int32_t* stack, int& sp) {
+  const uint32_t no = S.nodes4 + 128u * ref;
+  const float4 lx = S.A.ld_f4(no), hx = S.A.ld_f4(no + 16), ly = S.A.ld_f4(no + 32);
+  const float4 hy = S.A.ld_f4(no + 48), lz = S.A.ld_f4(no + 64), hz = S.A.ld_f4(no + 80);
+  const float4 cf = S.A.ld_f4(no + 96);
+  const float alx[4] = {lx.x, lx.y, lx.z, lx.w}, ahx[4] = {hx.x, hx.y, hx.z, hx.w};
+  const float aly[4] = {ly.x, ly.y, ly.z, ly.w}, ahy[4] = {hy.x, hy.y, hy.z, hy.w};
+  const float alz[4] = {lz.x, lz.y, lz.z, lz.w}, ahz[4] = {hz.x, hz.y, hz.z, hz.w};
+  int32_t c[4] = {__float_as_int(cf.x), __float_as_int(cf.y), __float_as_int(cf.z),
+                  __float_as_int(cf.w)};
+  float k[4];
+  int n = 0;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    float tn = 0.0f;
+    const bool h = c[i] != RT_EMPTY_REF &&
+                   slab(alx[i], ahx[i], aly[i], ahy[i], alz[i], ahz[i], r, tmin, lim, &tn);
+    k[i] = h ? fminf(tn, 3.402823466e38f) : __builtin_inff();
+    n += h ? 1 : 0;
+  }
+  auto cx = [&](int a, int b) {
+    const bool s = k[b] < k[a];
+    const float ka = k[a], kb = k[b];
+    const int32_t ca = c[a], cb = c[b];
+    k[a] = s ? kb : ka;
+    k[b] = s ? ka : kb;
+    c[a] = s ? cb : ca;
+    c[b] = s ? ca : cb;
+  };
+  cx(0, 1);
+  cx(2, 3);
+  cx(0, 2);
+  cx(1, 3);
+  cx(1, 2);
+  if (n == 0) return RT_EMPTY_REF;
+  if (n >= 4 && sp < RT_MAX_STACK) stack[64 * sp++] = c[3];
+  if (n >= 3 && sp < RT_MAX_STACK) stack[64 * sp++] = c[2];
+  if (n >= 2 && sp < RT_MAX_STACK) stack[64 * sp++] = c[1];
+  return c[0];
+}
+
 template <bool ANY>
 __device__ __forceinline__ int32_t trace(const Scene& S, const Ray& r, float tmin, float tmax,
                                          int32_t skip, bool tie_high, float* t_out,
@@ -218,6 +267,10 @@ __device__ __forceinline__ int32_t trace(const Scene& S, const Ray& r, float tmi
       ++cnt.visits;
 #endif
       const float lim = ANY ? tmax : bt;
+      if (S.flags & RT_FLAG_BVH4) {
+        const int32_t nx = node4_step(S, (uint32_t)ref, r, tmin, lim, stack, sp);
+        if (nx != RT_EMPTY_REF) { ref = nx; continue; }
+      } else {
       NodeStep st;
       if (uni) {
         const uint32_t no = S.nodes + 64u * (uint32_t)r0;
@@ -240,6 +293,7 @@ __device__ __forceinline__ int32_t trace(const Scene& S, const Ray& r, float tmi
       }
       if (st.h0) { ref = st.c0; continue; }
       if (st.h1) { ref = st.c1; continue; }
+      }
     } else {
       const uint32_t lr = (uint32_t)ref;
       const uint32_t first = (lr >> 4) & 0x07ffffffu, count = (lr & 15u) + 1u;

@@ -13,6 +13,7 @@ fallback.  Errors raise RtError with the library's message.
 from __future__ import annotations
 
 import ctypes as C
+import os
 
 import numpy as np
 
@@ -22,6 +23,7 @@ RT_RENDER_SHADOWS = 0x1
 RT_RENDER_PATH = 0x8
 RT_RENDER_FLAT = 0x10
 RT_RENDER_RASTER = 0x20
+RT_RENDER_BVH2 = 0x40
 PT_SEED = 0x5EED
 RT_RENDER_INSTRUMENTED = 0x100
 CLEAR_COLOR = 0xFF000000               # draw3d/main.cpp:47
@@ -32,7 +34,8 @@ TILE = 32                              # RASTER_TILE_LOGSIZE = 5
 class SceneInfo(C.Structure):
     _fields_ = [(n, C.c_uint32) for n in (
         "num_drawcalls", "num_prims", "num_geometry", "num_layer", "num_textures",
-        "bvh_nodes", "bvh_tris", "bvh_leaves", "bvh_depth", "pad")] + [
+        "bvh_nodes", "bvh_tris", "bvh_leaves", "bvh_depth", "bvh4_nodes", "bvh4_depth",
+        "bvh4_stack")] + [
         ("parse_ms", C.c_double), ("bvh_ms", C.c_double)]
 
 
@@ -72,6 +75,7 @@ def lib():
             "rt_scene_info": [vp, C.POINTER(SceneInfo)],
             "rt_scene_export_prims": [vp, vp, u64],
             "rt_scene_export_bvh": [vp, vp, vp],
+            "rt_scene_export_bvh4": [vp, vp],
             "rt_renderer_create": [vp, C.c_char_p, C.POINTER(vp)],
             "rt_renderer_free": [vp],
             "rt_renderer_configure": [vp, C.POINTER(RenderParams)],
@@ -132,6 +136,13 @@ class Scene:
                "rt_scene_export_bvh")
         return nodes[:info["bvh_nodes"]], tris[:info["bvh_tris"]]
 
+    def bvh4(self):
+        """The 4-wide BVH nodes (float32[N4, 32], rt_node4_t); leaves index bvh()'s tris."""
+        n = self.info()["bvh4_nodes"]
+        nodes4 = np.zeros((max(n, 1), 32), np.float32)
+        _check(lib().rt_scene_export_bvh4(self._h, nodes4.ctypes.data), "rt_scene_export_bvh4")
+        return nodes4[:n]
+
     def setup_prims(self, width: int, height: int) -> np.ndarray:
         """rt_prim_t shading records (int32[P, 32]) at width x height."""
         n = self.info()["num_prims"]
@@ -166,22 +177,26 @@ class Renderer:
     def configure(self, width: int, height: int, shadows: bool = True, light=DEFAULT_LIGHT,
                   clear_color: int = CLEAR_COLOR, shard_index: int = 0, shard_count: int = 1,
                   instrumented: bool = False, path: bool = False, bounces: int = 4,
-                  seed: int = PT_SEED, flat: bool = False, raster: bool = False) -> None:
+                  seed: int = PT_SEED, flat: bool = False, raster: bool = False,
+                  bvh_width: int = 0) -> None:
         """path=True: diffuse path trace (pt_kernel; `bounces` segments per
         path, RNG `seed`) instead of primary + shadow rays.  flat=True: the
         flat triangle list without BVH (BASELINE config 2).  raster=True:
-        the draw3d raster pipeline (any scene; depth/stencil/blend)."""
+        the draw3d raster pipeline (any scene; depth/stencil/blend).
+        bvh_width: 2 = traverse the binary BVH, 0 = the default (the 4-wide
+        BVH unless env RT_BVH_WIDTH=2)."""
         p = RenderParams()
         p.width, p.height = width, height
         p.flags = ((RT_RENDER_SHADOWS if shadows else 0) | (RT_RENDER_INSTRUMENTED if instrumented else 0)
                    | (RT_RENDER_PATH if path else 0) | (RT_RENDER_FLAT if flat else 0)
-                   | (RT_RENDER_RASTER if raster else 0))
+                   | (RT_RENDER_RASTER if raster else 0) | (RT_RENDER_BVH2 if bvh_width == 2 else 0))
         p.bounces, p.seed = bounces, seed
         p.light[:] = [float(np.float32(x)) for x in light]
         p.clear_color = clear_color
         p.shard_index, p.shard_count = shard_index, shard_count
         _check(lib().rt_renderer_configure(self._h, C.byref(p)), "rt_renderer_configure")
         self.params = p
+        self.bvh4 = bvh_width != 2 and os.environ.get("RT_BVH_WIDTH", "4") != "2"
 
     def render(self) -> None:
         _check(lib().rt_render(self._h), "rt_render")

@@ -18,7 +18,7 @@ def setup(po, name):
     if name not in _cache:
         s = rt.Scene.load(scene_path(name))
         _cache[name] = (s, rt.Renderer(s), po.OracleScene(po.cgltrace.load(scene_path(name))),
-                        s.bvh())
+                        s.bvh() + (s.bvh4(),))
     return _cache[name]
 
 
@@ -82,13 +82,15 @@ def test_pt_repeatable_and_primary_mode_unaffected(po):
     assert np.array_equal(a, r.framebuffer())
 
 
-def test_pt_instrumented_counters_equal_oracle_traversal(po):
+@pytest.mark.parametrize("width", (0, 2))
+def test_pt_instrumented_counters_equal_oracle_traversal(po, width):
     s, r, osc, bvh = setup(po, "tekkaman")
     for size in (256, 1024):
-        r.configure(size, size, path=True, instrumented=True)
+        r.configure(size, size, path=True, instrumented=True, bvh_width=width)
         r.render()
         st = r.stats()
-        c, _, _, k = po.rt_render(osc, po.rt_params(size, size, path=True, nthreads=8), bvh=bvh)
+        c, _, _, k = po.rt_render(osc, po.rt_params(size, size, path=True, nthreads=8),
+                                  bvh=bvh if r.bvh4 else bvh[:2])
         for key in ("node_visits", "tri_tests", "layer_tests", "shaded", "texel_bytes",
                     "shadow_rays", "bounce_rays", "occluded"):
             assert st[key] == k[key], key

@@ -107,10 +107,14 @@ CASES = [("tekkaman", 128, False), ("tekkaman", 128, True), ("tekkaman", 256, Tr
          ("carnival", 128, True)]
 
 
-@pytest.mark.parametrize("name,size,shadows", CASES)
-def test_rt_kernel_bit_exact_vs_oracle(po, name, size, shadows):
+@pytest.mark.parametrize("name,size,shadows,width",
+                         [c + (0,) for c in CASES] +
+                         [("tekkaman", 1024, True, 2), ("scene", 256, True, 2), ("box", 128, True, 2)])
+def test_rt_kernel_bit_exact_vs_oracle(po, name, size, shadows, width):
+    """Both traversals (4-wide default, binary with width=2) against the
+    brute-force oracle: the BVH may only change the work, never the frame."""
     s, r = renderer(name)
-    r.configure(size, size, shadows=shadows)
+    r.configure(size, size, shadows=shadows, bvh_width=width)
     r.render()
     fb = r.framebuffer()
     st = r.stats()
@@ -124,14 +128,16 @@ def test_rt_kernel_bit_exact_vs_oracle(po, name, size, shadows):
     assert st["tasks"] == st["num_tasks"]
 
 
-def test_rt_instrumented_counters_equal_oracle_traversal(po):
+@pytest.mark.parametrize("width", (0, 2))
+def test_rt_instrumented_counters_equal_oracle_traversal(po, width):
     s, r = renderer("tekkaman")
     for size in (256, 1024):
-        r.configure(size, size, shadows=True, instrumented=True)
+        r.configure(size, size, shadows=True, instrumented=True, bvh_width=width)
         r.render()
         st = r.stats()
         _, _, _, k = po.rt_render(oracle_scene(po, "tekkaman"),
-                                  po.rt_params(size, size, shadows=True, nthreads=8), bvh=s.bvh())
+                                  po.rt_params(size, size, shadows=True, nthreads=8),
+                                  bvh=s.bvh() + ((s.bvh4(),) if r.bvh4 else ()))
         for key in ("node_visits", "tri_tests", "layer_tests", "shaded", "texel_bytes",
                     "shadow_rays", "occluded"):
             assert st[key] == k[key], key

@@ -155,6 +155,80 @@ def test_bvh_traversal_equals_bruteforce(oracle_lib, name, size, shadows):
     assert kv["tri_tests"] < kb["tri_tests"]
 
 
+def _check_bvh4(nodes4, nodes, tris, stack_bound):
+    """The 4-wide BVH holds exactly the BVH2's leaves, under the same padded
+    boxes, and the host's stack bound covers every root-to-leaf walk."""
+    leaves4, leaves2 = [], []
+
+    def walk2(ref):
+        if ref >= 0:
+            for ch in range(2):
+                c = int(nodes[ref][12:14].view(np.int32)[ch])
+                if c != -1:
+                    walk2(c)
+        else:
+            leaves2.append(ref)
+
+    def walk4(ref, lo, hi):
+        n = nodes4[ref]
+        refs = n[24:28].view(np.int32)
+        used = [i for i in range(4) if refs[i] != -1]
+        assert used == list(range(len(used))) and (len(used) >= 2 or ref == 0)
+        need = 0
+        for i in used:
+            clo = n[[i, 8 + i, 16 + i]]
+            chi = n[[4 + i, 12 + i, 20 + i]]
+            assert np.all(clo <= chi)
+            if lo is not None:                      # BVH2 nesting: child box inside parent's
+                assert np.all(clo >= lo - 1e-3) and np.all(chi <= hi + 1e-3)
+            c = int(refs[i])
+            if c >= 0:
+                need = max(need, walk4(c, clo, chi))
+            else:
+                leaves4.append(c)
+        return len(used) - 1 + need
+
+    walk2(0)
+    st = walk4(0, None, None)
+    assert sorted(leaves4) == sorted(leaves2)
+    assert st == stack_bound
+
+
+@pytest.mark.parametrize("name", ["tekkaman", "scene", "box", "carnival"])
+def test_bvh4_collapse_structure(name):
+    s = rt.Scene.load(scene_path(name))
+    info = s.info()
+    nodes, tris = s.bvh()
+    nodes4 = s.bvh4()
+    assert info["bvh4_nodes"] == len(nodes4) and 0 < len(nodes4) <= len(nodes)
+    assert info["bvh4_depth"] <= info["bvh_depth"]
+    if len(nodes) > 100:
+        assert len(nodes4) < len(nodes) / 2 and info["bvh4_depth"] < info["bvh_depth"]
+    _check_bvh4(nodes4, nodes, tris, info["bvh4_stack"])
+    assert info["bvh4_stack"] <= 32
+
+
+@pytest.mark.parametrize("name,size,shadows,path", [
+    ("tekkaman", 256, True, False), ("tekkaman", 1024, True, False), ("scene", 256, False, False),
+    ("box", 128, True, False), ("carnival", 200, True, False), ("tekkaman", 128, False, True)])
+def test_bvh4_traversal_equals_bvh2(oracle_lib, name, size, shadows, path):
+    """Any traversal order gives the same closest hit (t, then the depth
+    test's pid tie rule) and the same any-hit verdict: the BVH4 restatement
+    reproduces the BVH2 renders exactly, with fewer node visits."""
+    po = oracle_lib
+    s = rt.Scene.load(scene_path(name))
+    osc = po.OracleScene(po.cgltrace.load(scene_path(name)))
+    p = po.rt_params(size, size, shadows=shadows, nthreads=8, path=path, bounces=3)
+    nodes, tris = s.bvh()
+    c2, p2, t2, k2 = po.rt_render(osc, p, bvh=(nodes, tris))
+    c4, p4, t4, k4 = po.rt_render(osc, p, bvh=(nodes, tris, s.bvh4()))
+    assert np.array_equal(c2, c4) and np.array_equal(p2, p4)
+    assert np.array_equal(t2.view(np.uint32), t4.view(np.uint32))
+    for key in ("occluded", "geometry_hits", "shadow_rays", "bounce_rays"):
+        assert k2[key] == k4[key], key
+    assert k4["node_visits"] < k2["node_visits"] or len(nodes) == 1
+
+
 def test_rt_primary_visibility_matches_pinned_raster(oracle_lib):
     """Primary rays vs the golden-pinned raster path: the hit primitive agrees
     except on a bounded set of silhouette pixels (fixed16 edges vs fp32 MT),
