@@ -50,7 +50,9 @@ def main():
         label, d, env = parse(spec)
         saved = {k: os.environ.get(k) for k in env}
         os.environ.update(env)
-        r = rt.Renderer(scene, kernel_dir=lib if d == "default" else os.path.join(vdir, d))
+        # the scene (and its BVH: RT_BVH_* build knobs) is built under the variant's env
+        sc = rt.Scene.load(args.scene) if any(k.startswith("RT_BVH_") for k in env) else scene
+        r = rt.Renderer(sc, kernel_dir=lib if d == "default" else os.path.join(vdir, d))
         r.configure(args.size, args.size, shadows=not args.no_shadows, path=args.mode == "path",
                     flat=args.mode == "flat", raster=args.mode == "raster", bounces=args.bounces)
         r.render()  # the driver reads its launch env when it loads the image

@@ -4,6 +4,7 @@
 #include <algorithm>
 #include <array>
 #include <cmath>
+#include <cstdlib>
 #include <cstring>
 
 namespace rt {
@@ -33,7 +34,8 @@ struct Box {
 
 class Builder {
  public:
-  Builder(const std::vector<BuildTri>& t, Bvh* out) : t_(t), out_(out) {
+  Builder(const std::vector<BuildTri>& t, Bvh* out, const BvhParams& bp)
+      : t_(t), out_(out), leaf_(bp.leaf_size), bins_(bp.bins), all_axes_(bp.all_axes) {
     box_.resize(t.size());
     cen_.resize(t.size());
     float ext = 0.0f;
@@ -55,7 +57,7 @@ class Builder {
     out_->depth = 0;
     out_->leaves = 0;
     if (t_.empty()) return;
-    if (t_.size() <= kBvhLeafSize) {  // root must be internal: leaf + empty child
+    if (t_.size() <= leaf_) {  // root must be internal: leaf + empty child
       out_->nodes.resize(1);
       Box b = range_box(0, (uint32_t)t_.size());
       const int32_t leaf = make_leaf(0, (uint32_t)t_.size());
@@ -106,7 +108,7 @@ class Builder {
   // returns the child reference for range [b, e)
   int32_t build(uint32_t b, uint32_t e, uint32_t depth) {
     const uint32_t n = e - b;
-    if (n <= kBvhLeafSize) return make_leaf(b, e);
+    if (n <= leaf_) return make_leaf(b, e);
     out_->depth = std::max(out_->depth, depth);
     const uint32_t node = (uint32_t)out_->nodes.size();
     out_->nodes.emplace_back();
@@ -120,7 +122,8 @@ class Builder {
     return (int32_t)node;
   }
 
-  // binned SAH over centroids on the widest centroid axis; stable partition
+  // binned SAH over centroids (the widest centroid axis, or every axis with
+  // all_axes); stable partition
   uint32_t split(uint32_t b, uint32_t e) {
     float cl[3] = {INFINITY, INFINITY, INFINITY}, ch[3] = {-INFINITY, -INFINITY, -INFINITY};
     for (uint32_t i = b; i < e; ++i)
@@ -128,37 +131,54 @@ class Builder {
         cl[k] = std::min(cl[k], cen_[idx_[i]][k]);
         ch[k] = std::max(ch[k], cen_[idx_[i]][k]);
       }
-    int axis = 0;
+    int wide = 0;
     for (int k = 1; k < 3; ++k)
-      if (ch[k] - cl[k] > ch[axis] - cl[axis]) axis = k;
-    const float ext = ch[axis] - cl[axis];
+      if (ch[k] - cl[k] > ch[wide] - cl[wide]) wide = k;
     const uint32_t median = b + (e - b) / 2;
-    if (!(ext > 0.0f)) return median;
-    auto bin_of = [&](uint32_t t) {
-      int bi = (int)((cen_[t][axis] - cl[axis]) * ((float)kBvhBins / ext));
-      return std::min(std::max(bi, 0), (int)kBvhBins - 1);
+    const uint32_t nb = bins_;
+    auto bin_of = [&](uint32_t t, int axis) {
+      const float ext = ch[axis] - cl[axis];
+      int bi = (int)((cen_[t][axis] - cl[axis]) * ((float)nb / ext));
+      return std::min(std::max(bi, 0), (int)nb - 1);
     };
-    Box bb[kBvhBins];
-    uint32_t cnt[kBvhBins] = {};
-    for (uint32_t i = b; i < e; ++i) {
-      const int bi = bin_of(idx_[i]);
-      bb[bi].grow(box_[idx_[i]]);
-      ++cnt[bi];
-    }
     double best = INFINITY;
     uint32_t best_s = 0;
-    for (uint32_t s = 1; s < kBvhBins; ++s) {
-      Box l, r;
-      uint32_t nl = 0, nr = 0;
-      for (uint32_t i = 0; i < s; ++i) { l.grow(bb[i]); nl += cnt[i]; }
-      for (uint32_t i = s; i < kBvhBins; ++i) { r.grow(bb[i]); nr += cnt[i]; }
-      if (nl == 0 || nr == 0) continue;
-      const double c = nl * l.area() + nr * r.area();
-      if (c < best) { best = c; best_s = s; }
+    int best_axis = -1;
+    for (int axis = 0; axis < 3; ++axis) {
+      if (!all_axes_ && axis != wide) continue;
+      if (!(ch[axis] - cl[axis] > 0.0f)) continue;
+      Box bb[kBvhMaxBins];
+      uint32_t cnt[kBvhMaxBins] = {};
+      for (uint32_t i = b; i < e; ++i) {
+        const int bi = bin_of(idx_[i], axis);
+        bb[bi].grow(box_[idx_[i]]);
+        ++cnt[bi];
+      }
+      // suffix sweep: right boxes/counts for every split position
+      Box rs[kBvhMaxBins];
+      uint32_t rc[kBvhMaxBins] = {};
+      Box acc;
+      uint32_t na = 0;
+      for (uint32_t s = nb; s-- > 1;) {
+        acc.grow(bb[s]);
+        na += cnt[s];
+        rs[s] = acc;
+        rc[s] = na;
+      }
+      Box l;
+      uint32_t nl = 0;
+      for (uint32_t s = 1; s < nb; ++s) {
+        l.grow(bb[s - 1]);
+        nl += cnt[s - 1];
+        if (nl == 0 || rc[s] == 0) continue;
+        const double c = nl * l.area() + rc[s] * rs[s].area();
+        if (c < best) { best = c; best_s = s; best_axis = axis; }
+      }
     }
-    if (best_s == 0) return median;
-    auto mid_it = std::stable_partition(idx_.begin() + b, idx_.begin() + e,
-                                        [&](uint32_t t) { return (uint32_t)bin_of(t) < best_s; });
+    if (best_axis < 0) return median;
+    auto mid_it = std::stable_partition(idx_.begin() + b, idx_.begin() + e, [&](uint32_t t) {
+      return (uint32_t)bin_of(t, best_axis) < best_s;
+    });
     return (uint32_t)(mid_it - idx_.begin());
   }
 
@@ -168,6 +188,8 @@ class Builder {
   std::vector<std::array<float, 3>> cen_;
   std::vector<uint32_t> idx_;
   float pad_ = 0.0f;
+  uint32_t leaf_, bins_;
+  bool all_axes_;
 };
 
 // Collapse the BVH2 into a BVH4: a node's children are repeatedly replaced
@@ -266,7 +288,16 @@ int BuildBvh(const std::vector<BuildTri>& tris, Bvh* out, std::string* error) {
     if (error) *error = "too many triangles for the 27-bit leaf index";
     return -1;
   }
-  Builder b(tris, out);
+  BvhParams bp;
+  // build knobs for A/B runs (defaults are the measured best)
+  if (const char* v = std::getenv("RT_BVH_LEAF")) bp.leaf_size = (uint32_t)std::atoi(v);
+  if (const char* v = std::getenv("RT_BVH_BINS")) bp.bins = (uint32_t)std::atoi(v);
+  if (const char* v = std::getenv("RT_BVH_AXES")) bp.all_axes = std::atoi(v) == 3;
+  if (bp.leaf_size < 1 || bp.leaf_size > 4 || bp.bins < 2 || bp.bins > kBvhMaxBins) {
+    if (error) *error = "bad BVH build parameters (leaf 1..4, bins 2..64)";
+    return -1;
+  }
+  Builder b(tris, out, bp);
   b.run();
   Collapser(out).run();
   if (out->depth > RT_STACK_DEEP) {

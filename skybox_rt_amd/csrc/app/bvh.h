@@ -32,8 +32,15 @@ struct Bvh {
   uint32_t stack4 = 0;           // worst-case traversal stack entries (near-first, BVH4)
 };
 
-constexpr uint32_t kBvhLeafSize = 4;
+constexpr uint32_t kBvhLeafSize = 4;   // the kernel fetches at most 4 triangles per leaf
 constexpr uint32_t kBvhBins = 16;
+constexpr uint32_t kBvhMaxBins = 64;
+
+struct BvhParams {
+  uint32_t leaf_size = kBvhLeafSize;   // max triangles per leaf (1..4)
+  uint32_t bins = kBvhBins;            // SAH bins per axis (2..64)
+  bool all_axes = false;               // SAH over x, y and w, not only the widest axis
+};
 
 int BuildBvh(const std::vector<BuildTri>& tris, Bvh* out, std::string* error);
 
