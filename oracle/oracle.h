@@ -23,6 +23,7 @@
 #ifndef ORACLE_H
 #define ORACLE_H
 
+#include <stddef.h>
 #include <stdint.h>
 
 #ifdef __cplusplus
@@ -134,6 +135,20 @@ int orc_rt_render_bvh(const orc_scene_t* scene, const orc_bvh_t* bvh,
 /* Möller–Trumbore as used by both sides (exposed for unit tests). */
 int orc_mt(const float o[3], const float d[3], const float v0[3],
            const float e1[3], const float e2[3], float tmin, float* t_out);
+
+/* ---- texture regression app (tests/regression/tex; oracle/tex.c) ------ */
+/* LoadImage format conversion of one A8R8G8B8 pixel (VX_TEX_FORMAT_*) */
+uint32_t orc_tex_encode(uint32_t argb, uint32_t format);
+/* converted image + mip chain; out NULL = size query; mipoff[16] */
+size_t orc_tex_build(const uint32_t* argb, uint32_t w, uint32_t h, uint32_t format, uint8_t* out,
+                     uint32_t* mipoff, uint32_t* levels);
+/* tex/kernel.cpp main(): lod + blend fraction for a dst size */
+void orc_tex_lod(uint32_t logw, uint32_t logh, uint32_t dst_w, uint32_t dst_h, uint32_t* lod,
+                 uint32_t* frac);
+/* tex/kernel.cpp kernel_body over every task; filter 0/1/2 = -g */
+void orc_tex_render(const uint8_t* tex, const uint32_t* mipoff, uint32_t logw, uint32_t logh,
+                    uint32_t format, uint32_t wrap, uint32_t filter, uint32_t dst_w, uint32_t dst_h,
+                    uint32_t num_tasks, uint32_t* dst);
 
 #ifdef __cplusplus
 }

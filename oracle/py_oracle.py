@@ -93,6 +93,13 @@ def lib():
         _lib.orc_setup_prim.argtypes = [C.c_void_p, C.c_uint32, C.c_uint32, C.c_float, C.c_float,
                                         C.c_void_p, C.c_void_p]
         _lib.orc_mt.argtypes = [C.c_void_p] * 5 + [C.c_float, C.POINTER(C.c_float)]
+        _lib.orc_tex_encode.argtypes = [C.c_uint32, C.c_uint32]
+        _lib.orc_tex_encode.restype = C.c_uint32
+        _lib.orc_tex_build.argtypes = [C.c_void_p, C.c_uint32, C.c_uint32, C.c_uint32, C.c_void_p,
+                                       C.c_void_p, C.c_void_p]
+        _lib.orc_tex_build.restype = C.c_size_t
+        _lib.orc_tex_lod.argtypes = [C.c_uint32] * 4 + [C.POINTER(C.c_uint32)] * 2
+        _lib.orc_tex_render.argtypes = [C.c_void_p, C.c_void_p] + [C.c_uint32] * 8 + [C.c_void_p]
     return _lib
 
 
@@ -210,3 +217,56 @@ def compare_images(a: np.ndarray, b: np.ndarray, tol: int = 0) -> int:
     cocogfx is not vendored, this is the documented interpretation)."""
     d = np.abs(a.astype(np.int32) - b.astype(np.int32)).max(axis=-1)
     return int((d > tol).sum())
+
+
+# ---- texture regression app (tests/regression/tex; oracle/tex.c) ---------
+TEX_FORMATS = ("A8R8G8B8", "R5G6B5", "A1R5G5B5", "A4R4G4B4", "A8L8", "L8", "A8")
+
+
+def load_png_argb(path) -> np.ndarray:
+    """PNG -> ARGB8888 uint32[h, w], row 0 = top (cocogfx LoadImage with
+    FORMAT_A8R8G8B8; RGB images get alpha 0xff)."""
+    from PIL import Image
+    a = np.array(Image.open(path).convert("RGBA"), np.uint32)
+    return (a[..., 3] << 24) | (a[..., 0] << 16) | (a[..., 1] << 8) | a[..., 2]
+
+
+def argb_to_rgba_topdown(fb: np.ndarray) -> np.ndarray:
+    """ARGB8888 image already top-down (tex/main.cpp saves with +pitch) -> RGBA."""
+    fb = np.asarray(fb, np.uint32)
+    return np.stack([(fb >> 16) & 0xFF, (fb >> 8) & 0xFF, fb & 0xFF, fb >> 24], -1).astype(np.uint8)
+
+
+def tex_build(argb: np.ndarray, fmt: int):
+    """-> (texels uint8[], mipoff uint32[16], levels)"""
+    argb = np.ascontiguousarray(argb, np.uint32)
+    h, w = argb.shape
+    mip = np.zeros(16, np.uint32)
+    lv = C.c_uint32()
+    n = lib().orc_tex_build(argb.ctypes.data, w, h, fmt, None, mip.ctypes.data, C.byref(lv))
+    out = np.zeros(max(n, 1), np.uint8)
+    lib().orc_tex_build(argb.ctypes.data, w, h, fmt, out.ctypes.data, mip.ctypes.data, C.byref(lv))
+    return out[:n], mip, lv.value
+
+
+def tex_lod(logw, logh, dst_w, dst_h):
+    lod, frac = C.c_uint32(), C.c_uint32()
+    lib().orc_tex_lod(logw, logh, dst_w, dst_h, C.byref(lod), C.byref(frac))
+    return lod.value, frac.value
+
+
+def tex_render(argb: np.ndarray, fmt: int = 0, wrap: int = 0, filt: int = 0, scale: float = 1.0,
+               num_tasks: int = 0) -> np.ndarray:
+    """The whole tex app on the CPU: dst = (uint32)(src * scale) per side,
+    ARGB8888 rows top-down.  num_tasks 0 = one task per row (the reference's
+    min(cores x warps x threads, dst_height) on any device with at least
+    dst_height hardware threads)."""
+    h, w = argb.shape
+    texels, mip, _ = tex_build(argb, fmt)
+    dw, dh = int(np.float32(w) * np.float32(scale)), int(np.float32(h) * np.float32(scale))
+    dst = np.zeros((dh, dw), np.uint32)
+    nt = num_tasks or dh
+    lib().orc_tex_render(texels.ctypes.data, mip.ctypes.data, int(w).bit_length() - 1,
+                         int(h).bit_length() - 1, fmt, wrap, filt, dw, dh, min(nt, dh),
+                         dst.ctypes.data)
+    return dst

@@ -26,7 +26,8 @@ REQUIRED = ("libvortex.so", "libvortex-hip.so", "librtapp.so", "rtapp",
             "rt_kernel_deep_stats.vxbin", "spawn_test.vxbin", "pt_kernel.vxbin",
             "pt_kernel_deep.vxbin", "pt_kernel_stats.vxbin", "pt_kernel_deep_stats.vxbin",
             "rt_flat.vxbin", "rt_flat_stats.vxbin", "raster_kernel.vxbin",
-            "pt_compact/pt_kernel.vxbin", "pt_compact/pt_kernel_stats.vxbin")
+            "pt_compact/pt_kernel.vxbin", "pt_compact/pt_kernel_stats.vxbin",
+            "tex_kernel.vxbin", "texapp")
 
 
 class NativeLibraryMissing(RuntimeError):

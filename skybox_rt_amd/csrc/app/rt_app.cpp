@@ -21,6 +21,7 @@
 #include <vector>
 
 #include "VX_types.h"
+#include "app_util.h"
 #include "bvh.h"
 #include "cgltrace.h"
 #include "setup.h"
@@ -52,6 +53,11 @@ double ms_since(std::chrono::steady_clock::time_point t0) {
 }
 
 }  // namespace
+
+namespace rtapp {
+int set_error(const std::string& message, int code) { return fail(message, code); }
+std::string library_dir() { return lib_dir(); }
+}  // namespace rtapp
 
 struct rt_scene {
   rt::Scene scene;
