@@ -41,7 +41,7 @@ typedef struct {
 int rt_tex_build_image(const uint32_t* argb, uint32_t width, uint32_t height, uint32_t format,
                        uint8_t* out, uint64_t* size, uint32_t mipoff[16], uint32_t* levels);
 
-/* kernel_dir: directory holding tex_kernel.vxbin (NULL = next to librtapp.so) */
+/* kernel_dir: directory holding tex_kernel_f{0,1,2}.vxbin (NULL = next to librtapp.so) */
 int rt_tex_create(const char* kernel_dir, rt_tex_h* out);
 int rt_tex_free(rt_tex_h t);
 /* source: A8R8G8B8, power-of-two sides, rows top-down */

@@ -155,14 +155,14 @@ int rt_tex_build_image(const uint32_t* argb, uint32_t w, uint32_t h, uint32_t fo
 
 struct rt_tex {
   vx_device_h dev = nullptr;
-  vx_buffer_h krnl = nullptr, tex = nullptr, dst = nullptr, utab = nullptr, vtab = nullptr,
+  vx_buffer_h krnl[3] = {nullptr, nullptr, nullptr}, tex = nullptr, dst = nullptr, utab = nullptr, vtab = nullptr,
               args = nullptr;
   tex_kernel_arg_t arg{};
   rt_tex_stats_t st{};
   bool configured = false;
   vx_hip_last_run_t last_run = nullptr;
   ~rt_tex() {
-    for (vx_buffer_h* b : {&krnl, &tex, &dst, &utab, &vtab, &args}) {
+    for (vx_buffer_h* b : {&krnl[0], &krnl[1], &krnl[2], &tex, &dst, &utab, &vtab, &args}) {
       if (*b) vx_mem_free(*b);
       *b = nullptr;
     }
@@ -196,9 +196,11 @@ int rt_tex_create(const char* kernel_dir, rt_tex_h* out) {
   if (vx_dev_caps(t->dev, VX_CAPS_ISA_FLAGS, &isa) != 0 || !(isa & VX_ISA_EXT_TEX))
     return set_error("texture extension not supported");  // tex/main.cpp:200-206
   const std::string dir = kernel_dir ? kernel_dir : rtapp::library_dir();
-  const std::string path = dir + "/tex_kernel.vxbin";
-  if (vx_upload_kernel_file(t->dev, path.c_str(), &t->krnl) != 0)
-    return set_error("cannot upload kernel " + path);
+  for (int f = 0; f < 3; ++f) {  // one image per filter (-g 0/1/2)
+    const std::string path = dir + "/tex_kernel_f" + std::to_string(f) + ".vxbin";
+    if (vx_upload_kernel_file(t->dev, path.c_str(), &t->krnl[f]) != 0)
+      return set_error("cannot upload kernel " + path);
+  }
   t->last_run = (vx_hip_last_run_t)vx_driver_symbol("vx_hip_last_run");
   *out = t.release();
   return 0;
@@ -244,8 +246,9 @@ int rt_tex_configure(rt_tex_h t, const uint32_t* argb, uint32_t w, uint32_t h,
     a.frac = (uint32_t)((j - (int32_t)(1u << (a.lod + 16))) >> (a.lod + 16 - 8));
   }
   const float dX = 1.0f / (float)dw, dY = 1.0f / (float)dh;
-  const uint32_t qpr = (dw + TEX_PIXELS_PER_TASK - 1) / TEX_PIXELS_PER_TASK;
-  std::vector<int32_t> ut(qpr * TEX_PIXELS_PER_TASK, 0), vt(dh);
+  const uint32_t grp = TEX_GROUP(p->filter);
+  const uint32_t gpr = (dw + grp - 1) / grp;  // groups per row
+  std::vector<int32_t> ut(gpr * grp, 0), vt(dh);
   float fu = (0 + 0.5f) * dX;
   for (uint32_t x = 0; x < dw; ++x, fu += dX) ut[x] = fx_dev(fu, VX_TEX_FXD_FRAC);
   const uint32_t tile_h = (dh + ntasks - 1) / ntasks;
@@ -274,7 +277,7 @@ int rt_tex_configure(rt_tex_h t, const uint32_t* argb, uint32_t w, uint32_t h,
   a.logh = logh;
   a.format = p->format;
   a.wrap = p->wrap;
-  a.num_tasks = dh * qpr;
+  a.num_tasks = dh * gpr * 64;
   uint64_t args_addr = 0;
   if (upload(t->dev, &a, sizeof(a), VX_MEM_READ, &t->args, &args_addr)) return -1;
   std::memset(&t->st, 0, sizeof(t->st));
@@ -291,7 +294,7 @@ int rt_tex_configure(rt_tex_h t, const uint32_t* argb, uint32_t w, uint32_t h,
 
 int rt_tex_render(rt_tex_h t) {
   if (!t || !t->configured) return set_error("texture app not configured");
-  if (vx_start(t->dev, t->krnl, t->args) != 0) return set_error("vx_start failed");
+  if (vx_start(t->dev, t->krnl[t->arg.filter], t->args) != 0) return set_error("vx_start failed");
   return vx_ready_wait(t->dev, VX_MAX_TIMEOUT) == 0 ? 0 : set_error("vx_ready_wait failed");
 }
 

@@ -1,6 +1,6 @@
 """Python binding of the texture regression app (include/vx_tex.h,
 librtapp.so): the reference's tests/regression/tex host (image conversion,
-mip chain, TEX state, launch, read-back) with tex_kernel.vxbin on MI355X.
+mip chain, TEX state, launch, read-back) with tex_kernel_f{0,1,2}.vxbin on MI355X.
 No CPU fallback: every call goes through the native library."""
 from __future__ import annotations
 
@@ -75,7 +75,7 @@ def build_image(argb: np.ndarray, fmt: int):
 
 
 class TexApp:
-    """One device + tex_kernel.vxbin; configure() uploads a texture and the
+    """One device + the tex_kernel_f* images; configure() uploads a texture and the
     destination state, render() runs one launch."""
 
     def __init__(self, kernel_dir: str | None = None):
