@@ -249,6 +249,12 @@ VX_API int vx_dump_perf(vx_device_h h, FILE* stream) {
   VX_CHECK_ERR(vx_mpm_query(h, VX_CSR_MINSTRET, 0, &tasks), { return err; });
   std::fprintf(stream, "PERF: device_ns=%llu, tasks=%llu\n", (unsigned long long)ns,
                (unsigned long long)tasks);
+  // the reference's per-class hardware counters (VORTEX_PROFILING 1-5,
+  // utils.cpp:262-800) are the GPU's PMC counters on MI355X: collected
+  // out of process by rocprofv3, printed in this format by scripts/vx_perf.py
+  if (const int cls = get_profiling_mode())
+    std::fprintf(stream, "PERF: class %d counters: python scripts/vx_perf.py --class %d -- <app>\n",
+                 cls, cls);
   return 0;
 }
 
