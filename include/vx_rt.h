@@ -95,6 +95,20 @@ int rt_read_framebuffer(rt_renderer_h r, uint32_t* out, uint64_t count);
 /* RT_RENDER_RASTER: the depth/stencil buffer (stencil << 24 | depth), W*H */
 int rt_read_depthbuffer(rt_renderer_h r, uint32_t* out, uint64_t count);
 
+/* Build the BVH on the device (Morton codes, radix
+ * sort, binary radix tree, bottom-up boxes -- kernels/bvh_build.hip) from
+ * the scene's triangles and make it this renderer's tree (binary traversal;
+ * a configured renderer is reconfigured).  Stats optional. */
+typedef struct {
+  uint32_t nodes, depth, launches, pad;
+  double build_ms;      /* host wall time of the whole build (upload + launches) */
+  double kernel_ms;     /* sum of the build kernels' HIP-event times */
+} rt_bvh_build_stats_t;
+int rt_renderer_build_bvh(rt_renderer_h r, rt_bvh_build_stats_t* stats);
+/* the renderer's current BVH (float[num_nodes][16], float[num_tris][12]) */
+int rt_renderer_export_bvh(rt_renderer_h r, float* nodes, float* tris, uint32_t* num_nodes,
+                           uint32_t* num_tris);
+
 /* raw per-workgroup counter rows of the last launch (16 u32 each; the
  * RT_STAMPS diagnostic images put wave timestamps in slots 12-15) */
 int rt_launch_rows(rt_renderer_h r, uint32_t* rows, uint64_t max_rows, uint64_t* nrows);

@@ -136,6 +136,12 @@ int orc_rt_render_bvh(const orc_scene_t* scene, const orc_bvh_t* bvh,
 int orc_mt(const float o[3], const float d[3], const float v0[3],
            const float e1[3], const float e2[3], float tmin, float* t_out);
 
+/* ---- linear BVH (oracle/lbvh.c, restating kernels/bvh_build.hip) -------- */
+/* verts: [n][3][3] clip (x, y, w); geom: [n][12] rt_tri_t records of the same
+ * triangles; out: nodes [max(n-1,1)][16], tris [n+3][12], depth. */
+int orc_lbvh_build(const float* verts, const float* geom, uint32_t n, float* nodes, float* tris,
+                   uint32_t* depth);
+
 /* ---- texture regression app (tests/regression/tex; oracle/tex.c) ------ */
 /* LoadImage format conversion of one A8R8G8B8 pixel (VX_TEX_FORMAT_*) */
 uint32_t orc_tex_encode(uint32_t argb, uint32_t format);

@@ -93,6 +93,8 @@ def lib():
         _lib.orc_setup_prim.argtypes = [C.c_void_p, C.c_uint32, C.c_uint32, C.c_float, C.c_float,
                                         C.c_void_p, C.c_void_p]
         _lib.orc_mt.argtypes = [C.c_void_p] * 5 + [C.c_float, C.POINTER(C.c_float)]
+        _lib.orc_lbvh_build.argtypes = [C.c_void_p, C.c_void_p, C.c_uint32, C.c_void_p, C.c_void_p,
+                                        C.POINTER(C.c_uint32)]
         _lib.orc_tex_encode.argtypes = [C.c_uint32, C.c_uint32]
         _lib.orc_tex_encode.restype = C.c_uint32
         _lib.orc_tex_build.argtypes = [C.c_void_p, C.c_uint32, C.c_uint32, C.c_uint32, C.c_void_p,
@@ -270,3 +272,20 @@ def tex_render(argb: np.ndarray, fmt: int = 0, wrap: int = 0, filt: int = 0, sca
                          int(h).bit_length() - 1, fmt, wrap, filt, dw, dh, min(nt, dh),
                          dst.ctypes.data)
     return dst
+
+
+# ---- linear BVH (oracle/lbvh.c) -------------------------------------------
+def lbvh_build(verts: np.ndarray, geom: np.ndarray):
+    """verts float32[n, 3, 3] clip (x, y, w) corners, geom float32[n, 12] their
+    rt_tri_t records -> (nodes float32[max(n-1,1), 16], tris float32[n, 12], depth)."""
+    verts = np.ascontiguousarray(verts, np.float32)
+    geom = np.ascontiguousarray(geom, np.float32)
+    n = verts.shape[0]
+    nodes = np.zeros((max(n - 1, 1), 16), np.float32)
+    tris = np.zeros((n + 3, 12), np.float32)
+    depth = C.c_uint32()
+    rc = lib().orc_lbvh_build(verts.ctypes.data, geom.ctypes.data, n, nodes.ctypes.data,
+                              tris.ctypes.data, C.byref(depth))
+    if rc != 0:
+        raise RuntimeError(f"orc_lbvh_build failed: {rc}")
+    return nodes, tris[:n], depth.value

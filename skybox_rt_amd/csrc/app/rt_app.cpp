@@ -23,6 +23,7 @@
 #include "VX_types.h"
 #include "app_util.h"
 #include "bvh.h"
+#include "bvh_common.h"
 #include "cgltrace.h"
 #include "setup.h"
 #include "vortex.h"
@@ -88,6 +89,10 @@ struct rt_renderer {
   vx_hip_stream_t stream = nullptr;
   vx_hip_last_run_t last_run = nullptr;
   vx_hip_mpm_rows_t mpm_rows = nullptr;
+  std::string kdir;         // kernel directory (images missing there come from lib_dir)
+  bool deep = false;        // RT/PT images with the 32-entry traversal stack
+  bool gpu_bvh = false;     // nodes/tris were built on the device (rt_renderer_build_bvh)
+  uint32_t num_tris = 0;    // leaf triangle records (without the 3 padding records)
 
   ~rt_renderer() {
     vx_buffer_h* bufs[] = {&krnl[0][0], &krnl[0][1], &krnl[1][0], &krnl[1][1], &krnl[2][0],
@@ -216,7 +221,7 @@ static int upload(vx_device_h dev, const void* data, uint64_t size, vx_buffer_h*
   if (*buf) vx_mem_free(*buf);
   *buf = nullptr;
   if (vx_mem_alloc(dev, sz, VX_MEM_READ, buf) != 0) return fail("vx_mem_alloc failed");
-  if (size && vx_copy_to_dev(*buf, data, 0, size) != 0) return fail("vx_copy_to_dev failed");
+  if (data && size && vx_copy_to_dev(*buf, data, 0, size) != 0) return fail("vx_copy_to_dev failed");
   if (vx_mem_address(*buf, addr) != 0) return fail("vx_mem_address failed");
   // the kernel addresses every buffer with 32-bit offsets into one arena
   // descriptor (vx_arena in vx_spawn.h)
@@ -233,12 +238,14 @@ int rt_renderer_create(rt_scene_h s, const char* kernel_dir, rt_renderer_h* out)
     return fail("vx_dev_open failed (no GPU or driver missing)");
   }
   const std::string dir = kernel_dir ? kernel_dir : lib_dir();
+  r->kdir = dir;
   // the regular image's LDS stack holds RT_STACK_SHALLOW (24) entries; a BVH whose traversal may
   // need more (BVH2: its depth, BVH4: its stack bound) uses the deep image
   // (32 entries, lower occupancy)
   const bool deep = std::max(s->bvh.depth, s->bvh.stack4) > RT_STACK_SHALLOW;
   if (std::max(s->bvh.depth, s->bvh.stack4) > RT_STACK_DEEP)
     return fail("BVH too deep for the traversal stack");
+  r->deep = deep;
   const char* names[4][2] = {
       {deep ? "rt_kernel_deep.vxbin" : "rt_kernel.vxbin",
        deep ? "rt_kernel_deep_stats.vxbin" : "rt_kernel_stats.vxbin"},
@@ -275,6 +282,7 @@ int rt_renderer_create(rt_scene_h s, const char* kernel_dir, rt_renderer_h* out)
     return -1;
   a.num_nodes = (uint32_t)bvh.nodes.size();
   a.num_nodes4 = (uint32_t)bvh.nodes4.size();
+  r->num_tris = (uint32_t)bvh.tris.size();
   // screen layers, highest pid first
   std::vector<rt_tri_t> lt(s->layers.size());
   for (size_t i = 0; i < s->layers.size(); ++i) {
@@ -452,7 +460,7 @@ int rt_renderer_configure(rt_renderer_h r, const rt_render_params_t* p) {
     std::stable_sort(ord.begin(), ord.end(), [&](uint32_t x, uint32_t y) { return w(x) > w(y); });
     if (upload(r->dev, ord.data(), ord.size() * 4, &r->order, &a.order_addr)) return -1;
   }
-  bool use_bvh4 = !(p->flags & RT_RENDER_BVH2);
+  bool use_bvh4 = !(p->flags & RT_RENDER_BVH2) && !r->gpu_bvh;
   if (const char* e = std::getenv("RT_BVH_WIDTH")) use_bvh4 = use_bvh4 && std::atoi(e) != 2;
   a.flags = ((p->flags & RT_RENDER_SHADOWS) ? RT_FLAG_SHADOWS : 0u) |
             ((p->flags & RT_RENDER_PATH) ? RT_FLAG_PATH : 0u) |
@@ -570,3 +578,166 @@ int rt_device_caps(rt_renderer_h r, uint64_t caps[8]) {
 }
 
 }  // extern "C"
+
+// ---- GPU BVH build (kernels/bvh_build.hip) --------
+
+namespace {
+
+int load_image(rt_renderer* r, const std::string& name, vx_buffer_h* out) {
+  std::string path = r->kdir + "/" + name;
+  if (FILE* f = std::fopen(path.c_str(), "rb")) std::fclose(f);
+  else path = lib_dir() + "/" + name;
+  if (*out) vx_mem_free(*out);
+  *out = nullptr;
+  return vx_upload_kernel_file(r->dev, path.c_str(), out) == 0 ? 0 : fail("cannot upload kernel " + path);
+}
+
+struct DevBuf {  // scratch buffer freed at scope exit
+  vx_buffer_h h = nullptr;
+  uint64_t addr = 0;
+  ~DevBuf() {
+    if (h) vx_mem_free(h);
+  }
+};
+
+int alloc_buf(vx_device_h dev, uint64_t size, DevBuf* b, const void* init = nullptr) {
+  return upload(dev, init, size, &b->h, &b->addr);
+}
+
+}  // namespace
+
+int rt_renderer_build_bvh(rt_renderer_h r, rt_bvh_build_stats_t* st) {
+  if (!r) return fail("null argument");
+  rt_scene* s = r->sc;
+  const uint32_t n = (uint32_t)s->geometry.size();
+  if (n == 0) return fail("no depth-tested geometry to build a BVH over");
+  const auto t0 = std::chrono::steady_clock::now();
+  vx_buffer_h krnl = nullptr;
+  if (load_image(r, "bvh_build.vxbin", &krnl)) return -1;
+  DevBuf kimg;
+  kimg.h = krnl;
+  // ingestion: the clip-space (x, y, w) corners, one float4 each
+  std::vector<float> verts((size_t)n * 12, 0.0f);
+  for (uint32_t i = 0; i < n; ++i) {
+    const auto& p = s->scene.prims[s->geometry[i]];
+    for (int c = 0; c < 3; ++c) {
+      verts[(size_t)i * 12 + 4 * c + 0] = p[c].pos[0];
+      verts[(size_t)i * 12 + 4 * c + 1] = p[c].pos[1];
+      verts[(size_t)i * 12 + 4 * c + 2] = p[c].pos[3];
+    }
+  }
+  const uint32_t nblocks = (n + BVHB_ITEMS - 1) / BVHB_ITEMS;
+  const uint32_t bounds_init[8] = {~0u, ~0u, ~0u, 0, 0, 0, 0, 0};
+  DevBuf vb, cen, keys[2], vals[2], hist, bounds, parent, flags, boxes, range, child, argb;
+  vx_buffer_h nodes_h = nullptr, tris_h = nullptr;
+  uint64_t nodes_addr = 0, tris_addr = 0;
+  const uint32_t nn = n > 1 ? n - 1 : 1;
+  if (alloc_buf(r->dev, verts.size() * 4, &vb, verts.data()) ||
+      alloc_buf(r->dev, (uint64_t)n * 16, &cen) || alloc_buf(r->dev, (uint64_t)n * 4, &keys[0]) ||
+      alloc_buf(r->dev, (uint64_t)n * 4, &keys[1]) || alloc_buf(r->dev, (uint64_t)n * 4, &vals[0]) ||
+      alloc_buf(r->dev, (uint64_t)n * 4, &vals[1]) ||
+      alloc_buf(r->dev, (uint64_t)256 * nblocks * 4, &hist) ||
+      alloc_buf(r->dev, sizeof(bounds_init), &bounds, bounds_init) ||
+      alloc_buf(r->dev, (uint64_t)n * 8, &parent) || alloc_buf(r->dev, (uint64_t)n * 4, &flags) ||
+      alloc_buf(r->dev, (uint64_t)n * 64, &boxes) || alloc_buf(r->dev, (uint64_t)n * 8, &range) ||
+      alloc_buf(r->dev, (uint64_t)n * 8, &child) ||
+      alloc_buf(r->dev, sizeof(bvh_build_arg_t), &argb) ||
+      upload(r->dev, nullptr, (uint64_t)nn * sizeof(rt_node_t), &nodes_h, &nodes_addr) ||
+      upload(r->dev, nullptr, (uint64_t)(n + 3) * sizeof(rt_tri_t), &tris_h, &tris_addr)) {
+    if (nodes_h) vx_mem_free(nodes_h);
+    if (tris_h) vx_mem_free(tris_h);
+    return -1;
+  }
+  DevBuf nodes_out, tris_out;  // owned here until handed to the renderer
+  nodes_out.h = nodes_h;
+  tris_out.h = tris_h;
+  bvh_build_arg_t a;
+  std::memset(&a, 0, sizeof(a));
+  a.verts_addr = vb.addr;
+  a.geom_addr = r->arg.geom_addr;
+  a.cen_addr = cen.addr;
+  a.keys_addr[0] = keys[0].addr;
+  a.keys_addr[1] = keys[1].addr;
+  a.vals_addr[0] = vals[0].addr;
+  a.vals_addr[1] = vals[1].addr;
+  a.hist_addr = hist.addr;
+  a.bounds_addr = bounds.addr;
+  a.parent_addr = parent.addr;
+  a.flags_addr = flags.addr;
+  a.boxes_addr = boxes.addr;
+  a.range_addr = range.addr;
+  a.child_addr = child.addr;
+  a.nodes_addr = nodes_addr;
+  a.tris_addr = tris_addr;
+  a.n = n;
+  a.nblocks = nblocks;
+  double kernel_ms = 0.0;
+  uint32_t launches = 0;
+  auto launch = [&](uint32_t phase, uint32_t pass) -> int {
+    a.phase = phase;
+    a.pass = pass;
+    if (vx_copy_to_dev(argb.h, &a, 0, sizeof(a)) != 0) return fail("vx_copy_to_dev failed");
+    if (vx_start(r->dev, krnl, argb.h) != 0) return fail("vx_start failed");
+    if (vx_ready_wait(r->dev, VX_MAX_TIMEOUT) != 0) return fail("vx_ready_wait failed");
+    double ms = 0.0;
+    uint32_t g = 0, b = 0;
+    if (r->last_run && r->last_run(r->dev, &ms, &g, &b) == 0) kernel_ms += ms;
+    ++launches;
+    return 0;
+  };
+  if (launch(BVHB_BOUNDS, 0) || launch(BVHB_MORTON, 0)) return -1;
+  for (uint32_t pass = 0; pass < 4; ++pass)  // 30-bit codes: 4 passes of 8 bits
+    if (launch(BVHB_HIST, pass) || launch(BVHB_SCAN, pass) || launch(BVHB_SCATTER, pass)) return -1;
+  if (launch(BVHB_TREE, 0) || launch(BVHB_BOXES, 0) || launch(BVHB_EMIT, 0)) return -1;
+  uint32_t bres[8];
+  if (vx_copy_from_dev(bres, bounds.h, 0, sizeof(bres)) != 0) return fail("vx_copy_from_dev failed");
+  const uint32_t depth = bres[7];
+  if (depth == 0 || depth > RT_STACK_DEEP) return fail("GPU BVH deeper than the traversal stack");
+  // traversal images with a stack deep enough for this tree
+  if (depth > RT_STACK_SHALLOW && !r->deep) {
+    if (load_image(r, "rt_kernel_deep.vxbin", &r->krnl[0][0]) ||
+        load_image(r, "rt_kernel_deep_stats.vxbin", &r->krnl[0][1]) ||
+        load_image(r, "pt_kernel_deep.vxbin", &r->krnl[1][0]) ||
+        load_image(r, "pt_kernel_deep_stats.vxbin", &r->krnl[1][1]))
+      return -1;
+    r->deep = true;
+  }
+  if (r->nodes) vx_mem_free(r->nodes);
+  if (r->tris) vx_mem_free(r->tris);
+  r->nodes = nodes_out.h;
+  r->tris = tris_out.h;
+  nodes_out.h = tris_out.h = nullptr;
+  r->arg.nodes_addr = nodes_addr;
+  r->arg.tris_addr = tris_addr;
+  r->arg.num_nodes = nn;
+  r->num_tris = n;
+  r->gpu_bvh = true;
+  if (st) {
+    std::memset(st, 0, sizeof(*st));
+    st->nodes = nn;
+    st->depth = depth;
+    st->launches = launches;
+    st->kernel_ms = kernel_ms;
+    st->build_ms = ms_since(t0);
+  }
+  // a configured renderer picks up the new tree (and the BVH2 traversal) now
+  if (r->configured) {
+    const rt_render_params_t p = r->params;
+    return rt_renderer_configure(r, &p);
+  }
+  return 0;
+}
+
+int rt_renderer_export_bvh(rt_renderer_h r, float* nodes, float* tris, uint32_t* num_nodes,
+                           uint32_t* num_tris) {
+  if (!r) return fail("null argument");
+  if (num_nodes) *num_nodes = r->arg.num_nodes;
+  if (num_tris) *num_tris = r->num_tris;
+  if (nodes && r->arg.num_nodes &&
+      vx_copy_from_dev(nodes, r->nodes, 0, (uint64_t)r->arg.num_nodes * sizeof(rt_node_t)) != 0)
+    return fail("vx_copy_from_dev failed");
+  if (tris && r->num_tris &&
+      vx_copy_from_dev(tris, r->tris, 0, (uint64_t)r->num_tris * sizeof(rt_tri_t)) != 0)
+    return fail("vx_copy_from_dev failed");
+  return 0;
+}

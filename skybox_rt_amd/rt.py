@@ -39,6 +39,14 @@ class SceneInfo(C.Structure):
         ("parse_ms", C.c_double), ("bvh_ms", C.c_double)]
 
 
+class BvhBuildStats(C.Structure):
+    _fields_ = [("nodes", C.c_uint32), ("depth", C.c_uint32), ("launches", C.c_uint32),
+                ("pad", C.c_uint32), ("build_ms", C.c_double), ("kernel_ms", C.c_double)]
+
+    def as_dict(self):
+        return {n: getattr(self, n) for n, _ in self._fields_ if n != "pad"}
+
+
 class RenderParams(C.Structure):
     _fields_ = [("width", C.c_uint32), ("height", C.c_uint32), ("flags", C.c_uint32),
                 ("light", C.c_float * 3), ("clear_color", C.c_uint32),
@@ -76,6 +84,8 @@ def lib():
             "rt_scene_export_prims": [vp, vp, u64],
             "rt_scene_export_bvh": [vp, vp, vp],
             "rt_scene_export_bvh4": [vp, vp],
+            "rt_renderer_build_bvh": [vp, C.POINTER(BvhBuildStats)],
+            "rt_renderer_export_bvh": [vp, vp, vp, C.POINTER(u32), C.POINTER(u32)],
             "rt_renderer_create": [vp, C.c_char_p, C.POINTER(vp)],
             "rt_renderer_free": [vp],
             "rt_renderer_configure": [vp, C.POINTER(RenderParams)],
@@ -173,6 +183,7 @@ class Renderer:
                                         C.byref(h)), "rt_renderer_create")
         self._h = h
         self.params = None
+        self.gpu_bvh = False
 
     def configure(self, width: int, height: int, shadows: bool = True, light=DEFAULT_LIGHT,
                   clear_color: int = CLEAR_COLOR, shard_index: int = 0, shard_count: int = 1,
@@ -196,7 +207,29 @@ class Renderer:
         p.shard_index, p.shard_count = shard_index, shard_count
         _check(lib().rt_renderer_configure(self._h, C.byref(p)), "rt_renderer_configure")
         self.params = p
-        self.bvh4 = bvh_width != 2 and os.environ.get("RT_BVH_WIDTH", "4") != "2"
+        self.bvh4 = (bvh_width != 2 and os.environ.get("RT_BVH_WIDTH", "4") != "2"
+                     and not self.gpu_bvh)
+
+    def build_bvh(self) -> dict:
+        """Build the BVH on the device (kernels/bvh_build.hip) and trace over it
+        from now on (binary traversal); returns the build statistics."""
+        st = BvhBuildStats()
+        _check(lib().rt_renderer_build_bvh(self._h, C.byref(st)), "rt_renderer_build_bvh")
+        self.gpu_bvh = True
+        if self.params is not None:
+            self.bvh4 = False
+        return st.as_dict()
+
+    def export_bvh(self):
+        """The renderer's current BVH: (nodes float32[N, 16], tris float32[M, 12])."""
+        nn, nt = C.c_uint32(), C.c_uint32()
+        _check(lib().rt_renderer_export_bvh(self._h, None, None, C.byref(nn), C.byref(nt)),
+               "rt_renderer_export_bvh")
+        nodes = np.zeros((max(nn.value, 1), 16), np.float32)
+        tris = np.zeros((max(nt.value, 1), 12), np.float32)
+        _check(lib().rt_renderer_export_bvh(self._h, nodes.ctypes.data, tris.ctypes.data,
+                                            C.byref(nn), C.byref(nt)), "rt_renderer_export_bvh")
+        return nodes[:nn.value], tris[:nt.value]
 
     def render(self) -> None:
         _check(lib().rt_render(self._h), "rt_render")
