@@ -4,8 +4,9 @@
 // scatter ranked with wave ballots), the binary radix tree of Karras 2012
 // over the sorted 62-bit keys (code << 32 | index: unique, so the tree is
 // well defined with duplicate codes), boxes bottom-up (the second child to
-// arrive at a node -- agent-scope acq_rel counter -- builds its box and
-// climbs; nobody waits), and the rt_node_t / rt_tri_t records the traversal
+// arrive at a node builds its box and climbs -- in LDS inside a workgroup's
+// window of leaves, through agent-scope acq_rel counters above it; nobody
+// waits), and the rt_node_t / rt_tri_t records the traversal
 // reads, subtrees of <= 4 triangles emitted as leaves.  Deterministic: the
 // oracle (oracle/lbvh.c) restates every phase and the tests compare the
 // emitted arrays bit for bit.
@@ -72,6 +73,7 @@ __device__ void phase_bounds(const bvh_build_arg_t* a) {
   float4* cen = vx_ptr<float4>(a->cen_addr);
   uint32_t* bounds = vx_ptr<uint32_t>(a->bounds_addr);
   __shared__ float red[kWaves][7];
+  if (blockIdx.x * BVHB_BLOCK >= a->n) return;  // no triangles: no atomics (uniform exit)
   float mn[3] = {INFINITY, INFINITY, INFINITY}, mx[3] = {-INFINITY, -INFINITY, -INFINITY};
   float am = 0.0f;
   for (uint32_t t = blockIdx.x * BVHB_BLOCK + threadIdx.x; t < a->n; t += gridDim.x * BVHB_BLOCK) {
@@ -142,30 +144,33 @@ __device__ void phase_hist(const bvh_build_arg_t* a) {
   }
 }
 
-// exclusive scan of hist[256][nblocks] (digit-major) by workgroup 0
+// exclusive scan of hist[256][nblocks] (digit-major) by workgroup 0: each
+// thread sums a contiguous chunk (independent loads), one workgroup scan of
+// the 256 chunk sums, then each thread rewrites its chunk
 __device__ void phase_scan(const bvh_build_arg_t* a) {
   if (blockIdx.x != 0) return;
   uint32_t* hist = vx_ptr<uint32_t>(a->hist_addr);
   __shared__ uint32_t s[BVHB_BLOCK];
-  __shared__ uint32_t carry;
-  if (threadIdx.x == 0) carry = 0;
   const uint32_t total = 256u * a->nblocks;
-  for (uint32_t base = 0; base < total; base += BVHB_BLOCK) {
-    const uint32_t i = base + threadIdx.x;
-    const uint32_t x = i < total ? hist[i] : 0u;
-    s[threadIdx.x] = x;
+  const uint32_t chunk = (total + BVHB_BLOCK - 1) / BVHB_BLOCK;
+  const uint32_t b0 = threadIdx.x * chunk;
+  const uint32_t b1 = b0 + chunk < total ? b0 + chunk : total;
+  uint32_t sum = 0;
+#pragma unroll 8
+  for (uint32_t i = b0; i < b1; ++i) sum += hist[i];
+  s[threadIdx.x] = sum;
+  __syncthreads();
+  for (uint32_t o = 1; o < BVHB_BLOCK; o <<= 1) {  // Hillis-Steele inclusive scan
+    const uint32_t y = threadIdx.x >= o ? s[threadIdx.x - o] : 0u;
     __syncthreads();
-    for (uint32_t o = 1; o < BVHB_BLOCK; o <<= 1) {  // Hillis-Steele inclusive scan
-      const uint32_t y = threadIdx.x >= o ? s[threadIdx.x - o] : 0u;
-      __syncthreads();
-      s[threadIdx.x] += y;
-      __syncthreads();
-    }
-    const uint32_t c = carry;
-    if (i < total) hist[i] = c + s[threadIdx.x] - x;
+    s[threadIdx.x] += y;
     __syncthreads();
-    if (threadIdx.x == BVHB_BLOCK - 1) carry = c + s[threadIdx.x];
-    __syncthreads();
+  }
+  uint32_t run = s[threadIdx.x] - sum;
+  for (uint32_t i = b0; i < b1; ++i) {
+    const uint32_t x = hist[i];
+    hist[i] = run;
+    run += x;
   }
 }
 
@@ -266,34 +271,83 @@ __device__ void phase_tree(const bvh_build_arg_t* a) {
   if (blockIdx.x == 0 && threadIdx.x == 0) parent[0] = -1;
 }
 
+// Boxes bottom-up.  Workgroup b owns the sorted leaves [256b, 256b + 256):
+// internal nodes whose leaf range lies inside that window ("local" -- their
+// index is one of their range's ends, so also inside it) are completed in
+// LDS with workgroup-scope counters; a thread that climbs out of the window
+// carries its subtree's box on through global memory with agent-scope
+// acq_rel counters (the second child to arrive builds the node; nobody waits).
+__device__ __forceinline__ float4 fmin4(float4 a, float4 b) {
+  return make_float4(fminf(a.x, b.x), fminf(a.y, b.y), fminf(a.z, b.z), 0.0f);
+}
+__device__ __forceinline__ float4 fmax4(float4 a, float4 b) {
+  return make_float4(fmaxf(a.x, b.x), fmaxf(a.y, b.y), fmaxf(a.z, b.z), 0.0f);
+}
+
 __device__ void phase_boxes(const bvh_build_arg_t* a) {
   const float4* v = vx_ptr<const float4>(a->verts_addr);
   const uint32_t* vals = vx_ptr<const uint32_t>(a->vals_addr[0]);
   const int32_t* parent = vx_ptr<const int32_t>(a->parent_addr);
   const int32_t* child = vx_ptr<const int32_t>(a->child_addr);
+  const uint32_t* range = vx_ptr<const uint32_t>(a->range_addr);
   uint32_t* flags = vx_ptr<uint32_t>(a->flags_addr);
   float4* boxes = vx_ptr<float4>(a->boxes_addr);
+  __shared__ float4 llo[2 * BVHB_BLOCK], lhi[2 * BVHB_BLOCK];  // [leaf slot | internal slot]
+  __shared__ uint32_t lcnt[BVHB_BLOCK];
   const int n = (int)a->n;
-  for (int k = blockIdx.x * BVHB_BLOCK + threadIdx.x; k < n; k += gridDim.x * BVHB_BLOCK) {
-    float lo[3], hi[3];
-    tri_box(v, vals[k], lo, hi);
-    boxes[2 * (n + k)] = make_float4(lo[0], lo[1], lo[2], 0.0f);
-    boxes[2 * (n + k) + 1] = make_float4(hi[0], hi[1], hi[2], 0.0f);
-    if (n < 2) continue;
-    int p = parent[n + k];
-    // climb while this thread is the second to arrive (bounded by the depth)
-    for (int guard = 0; p >= 0 && guard < 4096; ++guard) {
+  const int nwin = (n + BVHB_BLOCK - 1) / BVHB_BLOCK;
+  for (int b = blockIdx.x; b < nwin; b += gridDim.x) {
+    const int L0 = b * BVHB_BLOCK, L1 = L0 + BVHB_BLOCK < n ? L0 + BVHB_BLOCK : n;
+    const int k = L0 + (int)threadIdx.x;
+    const bool valid = k < L1;
+    lcnt[threadIdx.x] = 0;
+    float4 lo = make_float4(0, 0, 0, 0), hi = lo;
+    if (valid) {
+      float l[3], h[3];
+      tri_box(v, vals[k], l, h);
+      lo = make_float4(l[0], l[1], l[2], 0.0f);
+      hi = make_float4(h[0], h[1], h[2], 0.0f);
+      boxes[2 * (n + k)] = lo;
+      boxes[2 * (n + k) + 1] = hi;
+      llo[threadIdx.x] = lo;
+      lhi[threadIdx.x] = hi;
+    }
+    __syncthreads();
+    int p = (valid && n >= 2) ? parent[n + k] : -1;
+    bool alive = p >= 0;
+    // local climb: LDS boxes, workgroup-scope counters
+    while (alive && (int)range[2 * p] >= L0 && (int)range[2 * p + 1] < L1) {
+      const uint32_t old = __hip_atomic_fetch_add(&lcnt[p - L0], 1u, __ATOMIC_ACQ_REL,
+                                                  __HIP_MEMORY_SCOPE_WORKGROUP);
+      if (old == 0) {
+        alive = false;
+        break;
+      }
+      const int c0 = child[2 * p], c1 = child[2 * p + 1];
+      const int s0 = c0 >= 0 ? BVHB_BLOCK + c0 - L0 : ~c0 - L0;
+      const int s1 = c1 >= 0 ? BVHB_BLOCK + c1 - L0 : ~c1 - L0;
+      lo = fmin4(llo[s0], llo[s1]);
+      hi = fmax4(lhi[s0], lhi[s1]);
+      llo[BVHB_BLOCK + p - L0] = lo;
+      lhi[BVHB_BLOCK + p - L0] = hi;
+      boxes[2 * p] = lo;
+      boxes[2 * p + 1] = hi;
+      p = parent[p];
+      alive = p >= 0;
+    }
+    // global climb from the first node outside the window
+    for (int guard = 0; alive && guard < 4096; ++guard) {
       const uint32_t old = __hip_atomic_fetch_add(&flags[p], 1u, __ATOMIC_ACQ_REL,
                                                   __HIP_MEMORY_SCOPE_AGENT);
       if (old == 0) break;
       const int c0 = child[2 * p], c1 = child[2 * p + 1];
       const int i0 = c0 >= 0 ? c0 : n + ~c0, i1 = c1 >= 0 ? c1 : n + ~c1;
-      const float4 l0 = boxes[2 * i0], h0 = boxes[2 * i0 + 1];
-      const float4 l1 = boxes[2 * i1], h1 = boxes[2 * i1 + 1];
-      boxes[2 * p] = make_float4(fminf(l0.x, l1.x), fminf(l0.y, l1.y), fminf(l0.z, l1.z), 0.0f);
-      boxes[2 * p + 1] = make_float4(fmaxf(h0.x, h1.x), fmaxf(h0.y, h1.y), fmaxf(h0.z, h1.z), 0.0f);
+      boxes[2 * p] = fmin4(boxes[2 * i0], boxes[2 * i1]);
+      boxes[2 * p + 1] = fmax4(boxes[2 * i0 + 1], boxes[2 * i1 + 1]);
       p = parent[p];
+      alive = p >= 0;
     }
+    __syncthreads();
   }
 }
 
@@ -344,6 +398,7 @@ __device__ void phase_emit(const bvh_build_arg_t* a) {
     }
     return;
   }
+  uint32_t maxdepth = 0;
   for (int i = gid; i < n - 1; i += gstride) {
     float* nd = nodes[i].v;
     for (int q = 0; q < 16; ++q) nd[q] = 0.0f;
@@ -365,8 +420,15 @@ __device__ void phase_emit(const bvh_build_arg_t* a) {
     }
     uint32_t depth = 1;
     for (int p = i; p != 0; p = parent[p]) ++depth;
-    atomicMax(&bounds[7], depth);
+    maxdepth = depth > maxdepth ? depth : maxdepth;
   }
+  // one atomic per wave (100k same-address atomics cost ~0.4 ms)
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const uint32_t y = (uint32_t)__shfl_xor((int)maxdepth, o, 64);
+    maxdepth = y > maxdepth ? y : maxdepth;
+  }
+  if (lane() == 0 && maxdepth) atomicMax(&bounds[7], maxdepth);
 }
 
 }  // namespace
