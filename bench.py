@@ -30,6 +30,8 @@ sys.path.insert(0, ROOT)
 SCENE = os.path.join(ROOT, "tests", "golden", "scenes", "tekkaman.cgltrace")
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
 NODE_BYTES, TRI_BYTES, PIXEL_BYTES = 64, 36, 4
+MT_FLOPS = 40          # fp32 ops per Moller-Trumbore test
+FP32_VALU_TFLOPS = 157.3  # MI355X_MICROARCH.md: peak FP32 (vector)
 NODE4_BYTES = 112      # BVH4 node: 6 SoA box float4 + the child-ref float4 (pad not read)
 
 
@@ -268,6 +270,15 @@ def main():
         },
         "cpu_baseline": None,
     }
+    if flat:
+        # the flat list is read from LDS, never from HBM: its bound is the MT
+        # arithmetic -- SURVEY 8(d): ~40 fp32 ops per test, 157.3 TFLOP/s vector peak
+        tflops = MT_FLOPS * (inst["tri_tests"] + inst["layer_tests"]) / (avg_kernel_ms * 1e-3) / 1e12
+        out["roofline"].update({"bound": "valu", "achieved": round(tflops, 3),
+                                "peak": FP32_VALU_TFLOPS, "unit": "TFLOP/s",
+                                "frac": round(tflops / FP32_VALU_TFLOPS, 4),
+                                "lds_bytes_per_launch": int(alg_bytes)})
+        out["roofline"].pop("algorithmic_bytes_per_launch")
     if gather_ok is not None:
         out["config"]["gather_verified"] = gather_ok
     if n_gpus == 1 and not args.no_cpu_baseline:

@@ -248,6 +248,31 @@ __device__ __forceinline__ int vx_spawn_tasks_block(uint32_t num_tasks, F kernel
   return 0;
 }
 
+/* Block-cooperative form: each workgroup step takes ONE 64-task chunk and
+ * every wave of the workgroup sees the same 64 tasks (lane l: task
+ * chunk * 64 + l), so the waves can split the work of each task among them
+ * (e.g. the flat image's triangle list).  kernel_func(task, valid, arg) is
+ * called by every thread; steps are block-uniform (kernel_func may use
+ * __syncthreads()).  Tasks are counted once (by wave 0). */
+template <typename F, typename Arg>
+__device__ __forceinline__ int vx_spawn_chunks_block(uint32_t num_tasks, F kernel_func, Arg* arg) {
+  const uint32_t nchunks = (num_tasks + VX_CHUNK - 1) / VX_CHUNK;
+  uint32_t ran = 0;
+  vx_task_t task;
+  task.threadIdx.x = task.threadIdx.y = task.threadIdx.z = 0;
+  task.blockIdx.y = task.blockIdx.z = 0;
+  for (uint32_t c = blockIdx.x; c < nchunks; c += gridDim.x) {
+    const uint32_t t = c * VX_CHUNK + (threadIdx.x & 63u);
+    task.task_id = t;
+    task.blockIdx.x = t;
+    const bool valid = t < num_tasks;
+    kernel_func(task, valid, arg);
+    ran += valid && threadIdx.x < 64u;
+  }
+  vx_mpm_add(VX_MPM_TASKS, ran);
+  return 0;
+}
+
 /* VX_MAIN(ArgT, arg, block_threads) { ... return vx_spawn_tasks(...); }
  * defines the `vx_main` entry the driver launches with `block_threads`
  * threads per workgroup (must be a multiple of 64). */

@@ -192,6 +192,91 @@ __device__ __forceinline__ void shadow_drain(bool final, const Scene& S, WaveLds
 }
 #endif
 
+#if RT_FLAT
+// Config 2 with every ray's triangle list split across the workgroup's
+// waves: a workgroup step takes one 64-task chunk (vx_spawn_chunks_block),
+// wave w tests list entries [w*m, (w+1)*m) for the chunk's 64 rays, the
+// per-wave closest hits meet in LDS (closer() is a strict order on
+// (t, pid), so the reduction order is immaterial) and wave 0 resolves
+// layers, shades and stores; shadow rays split the same way, the first
+// occluder in list order found by a min over the waves' first hits (which
+// is also brute_trace's test count).  16x shorter dependent chains and 16x
+// more waves than one ray per lane over the whole list.
+struct FlatLds {
+  float t[kWaves][64];
+  int32_t pid[kWaves][64];
+  uint32_t first[kWaves][64];
+};
+
+__device__ __forceinline__ void flat_chunk(const vx_task_t& task, bool valid, const Scene& S,
+                                           FlatLds& L, Counters& cnt) {
+  const uint32_t w = threadIdx.x >> 6, lane = lane_id();
+  const uint32_t t = task.blockIdx.x;
+  uint32_t x = 0, y = 0;
+  if (valid) task_pixel(S, t, &x, &y);
+  const bool in = valid && x < S.width && y < S.height;
+  Ray r;
+  primary_dir(S, x, y, r);
+  ray_setup(r);
+  const bool tie_high = (S.flags & RT_FLAG_TIE_HIGH) != 0;
+  const uint32_t n = S.num_geom, per = (n + kWaves - 1) / kWaves;
+  const uint32_t k0 = w * per < n ? w * per : n, k1 = k0 + per < n ? k0 + per : n;
+  const float4* lds = flat_list(S);
+  float bt = INFINITY;
+  uint32_t f;
+  const int32_t bp = in ? trace_flat_range<false>(S, r, k0, k1, 0.0f, INFINITY, -1, tie_high, &bt,
+                                                  &f, lds)
+                        : -1;
+#ifdef RT_INSTRUMENT
+  cnt.tests += in ? k1 - k0 : 0u;  // the whole list per ray, summed over the waves
+#endif
+  L.t[w][lane] = bt;
+  L.pid[w][lane] = bp;
+  __syncthreads();
+  int32_t hit = -1;
+  float th = INFINITY;
+  for (uint32_t i = 0; i < kWaves; ++i) {
+    const int32_t p = L.pid[i][lane];
+    if (p >= 0 && closer(L.t[i][lane], p, th, hit, tie_high)) {
+      th = L.t[i][lane];
+      hit = p;
+    }
+  }
+  uint32_t color = 0;
+  if (w == 0) {
+    cnt.primary += in;
+    cnt.hits += hit >= 0;
+    const int32_t spid = resolve_layers(S, r, in && hit < 0, hit, cnt);
+    color = shade_wave(S, spid, x, y, S.clear_color, cnt);
+  }
+  const bool shadow = in && hit >= 0 && (S.flags & RT_FLAG_SHADOWS) != 0;
+  if (__ballot(shadow)) {  // block-uniform: every wave holds the same 64 rays
+    Ray sr;
+    shadow_ray(S, r, th, sr);
+    float ts;
+    uint32_t first = 0xffffffffu;
+    if (shadow) trace_flat_range<true>(S, sr, k0, k1, 0.0f, 1.0f, hit, tie_high, &ts, &first, lds);
+    L.first[w][lane] = first;
+  }
+  __syncthreads();
+  if (w == 0) {
+    if (shadow) {
+      uint32_t first = 0xffffffffu;
+      for (uint32_t i = 0; i < kWaves; ++i) first = L.first[i][lane] < first ? L.first[i][lane] : first;
+      cnt.shadow += 1;
+#ifdef RT_INSTRUMENT
+      cnt.tests += first != 0xffffffffu ? first + 1 : n;  // brute_trace stops at the first occluder
+#endif
+      if (first != 0xffffffffu) {
+        ++cnt.occluded;
+        color = shadowed(color);
+      }
+    }
+    if (in) store_pixel(S, t, x, y, color);
+  }
+}
+#endif
+
 // RT statistics go to the user MPM counters (VX_CSR_MPM_USER = 0xB03 + slot),
 // which the driver zeroes before every launch and vx_mpm_query() reads back.
 __device__ __forceinline__ void flush(int slot, uint32_t v) { vx_mpm_add(RT_MPM_USER + slot, v); }
@@ -221,13 +306,20 @@ VX_MAIN(rt_kernel_arg_t, arg, RT_BLOCK_THREADS) {
 #if RT_FLAT
   // stage the geometry list once per workgroup (workgroups past the last
   // task chunk have nothing to render and skip it)
-  if (S.num_geom <= RT_FLAT_CAP && blockIdx.x * blockDim.x < arg->num_tasks) {
+  if (S.num_geom <= RT_FLAT_CAP && blockIdx.x * VX_CHUNK < arg->num_tasks) {  // one chunk per step
     for (uint32_t i = threadIdx.x; i < 3u * S.num_geom; i += blockDim.x)
       s_geom[i] = S.A.ld_f4(S.geom + 16u * i);
   }
   __syncthreads();
 #endif
-#if RT_SHADOW_QUEUE
+#if RT_FLAT
+  __shared__ FlatLds s_flat;
+  (void)w;
+  const int rc = vx_spawn_chunks_block(
+      arg->num_tasks,
+      [&](const vx_task_t& task, bool valid, const Scene* s) { flat_chunk(task, valid, *s, s_flat, cnt); },
+      &S);
+#elif RT_SHADOW_QUEUE
   if ((threadIdx.x & 63u) == 0) w.q_count = 0;
   __builtin_amdgcn_wave_barrier();
   const int rc = vx_spawn_tasks_ex(

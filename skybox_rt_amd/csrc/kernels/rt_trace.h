@@ -411,6 +411,42 @@ __device__ __forceinline__ int32_t trace_flat(const Scene& S, const Ray& r, floa
   return bpid;
 }
 
+// One wave's share [k0, k1) of the flat list (the flat image splits every
+// ray's list across the waves of its workgroup).  Closest hit (ANY = false)
+// or the first hit in list order (ANY = true: *first = its index, else
+// UINT32_MAX).  Counts nothing: the caller accounts the algorithmic tests.
+template <bool ANY>
+__device__ __forceinline__ int32_t trace_flat_range(const Scene& S, const Ray& r, uint32_t k0,
+                                                    uint32_t k1, float tmin, float tmax,
+                                                    int32_t skip, bool tie_high, float* t_out,
+                                                    uint32_t* first, const float4* lds) {
+  float bt = tmax;
+  int32_t bpid = -1;
+  *first = 0xffffffffu;
+  for (uint32_t k = k0; k < k1; ++k) {
+    float4 ta, tb, tc;
+    if (lds) {
+      ta = lds[3 * k]; tb = lds[3 * k + 1]; tc = lds[3 * k + 2];
+    } else {
+      const uint32_t o = S.geom + 48u * k;
+      ta = S.A.sld_f4(o); tb = S.A.sld_f4(o + 16); tc = S.A.sld_f4(o + 32);
+    }
+    const int32_t pid = __float_as_int(ta.w);
+    if (pid == skip) continue;
+    float t;
+    if (mt_hit(r, ta, tb, tc, tmin, &t)) {
+      if (ANY) {
+        if (t < tmax) { *t_out = t; *first = k; return pid; }
+      } else if (closer(t, pid, bt, bpid, tie_high)) {
+        bt = t;
+        bpid = pid;
+      }
+    }
+  }
+  *t_out = bt;
+  return bpid;
+}
+
 // shade primitive `pid` at (x, y) from per-lane (vector) record loads
 __device__ __forceinline__ uint32_t shade_lane(const Scene& S, int32_t pid, uint32_t x,
                                                uint32_t y, Counters& cnt) {
