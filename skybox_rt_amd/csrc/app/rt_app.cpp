@@ -438,6 +438,7 @@ int rt_renderer_configure(rt_renderer_h r, const rt_render_params_t* p) {
   // touches the tile -- so the long model waves start with the frame rather
   // than trailing it.  Output is order independent.  RT_TILE_ORDER=0: identity.
   a.order_addr = 0;
+  a.split_tiles = 0;
   if (!raster && r->local_tiles > 0 && !(std::getenv("RT_TILE_ORDER") &&
                                          std::atoi(std::getenv("RT_TILE_ORDER")) == 0)) {
     std::vector<uint32_t> weight(tiles, 0);
@@ -459,6 +460,18 @@ int rt_renderer_configure(rt_renderer_h r, const rt_render_params_t* p) {
     auto w = [&](uint32_t lt) { return weight[p->shard_index + lt * shards]; };
     std::stable_sort(ord.begin(), ord.end(), [&](uint32_t x, uint32_t y) { return w(x) > w(y); });
     if (upload(r->dev, ord.data(), ord.size() * 4, &r->order, &a.order_addr)) return -1;
+    // path tracing: tiles geometry touches (first in `ord`) run 32 pixels
+    // per wave (task_map in rt_trace.h): 0.34 -> 0.30 ms at 1024^2; for
+    // primary + shadow rays it measured slower (0.071 -> 0.086 ms: the
+    // shadow rays then also trace in half-empty waves), so off there.
+    // RT_SPLIT_TILES=n overrides the count, 0 disables.
+    uint32_t heavy = 0;
+    if (p->flags & RT_RENDER_PATH)
+      while (heavy < r->local_tiles && w(ord[heavy]) > 0) ++heavy;
+    if (const char* e = std::getenv("RT_SPLIT_TILES"))
+      heavy = std::min<uint32_t>((uint32_t)std::atoi(e), r->local_tiles);
+    a.split_tiles = heavy;
+    a.num_tasks += heavy * RT_TILE_PIXELS;
   }
   bool use_bvh4 = !(p->flags & RT_RENDER_BVH2) && !r->gpu_bvh;
   if (const char* e = std::getenv("RT_BVH_WIDTH")) use_bvh4 = use_bvh4 && std::atoi(e) != 2;
@@ -477,7 +490,8 @@ int rt_renderer_configure(rt_renderer_h r, const rt_render_params_t* p) {
   a.light[1] = p->light[1];
   a.light[2] = p->light[2];
   // output buffer, pre-filled with the clear colour (draw3d/main.cpp:485-490)
-  const uint64_t npx = shards > 1 ? (uint64_t)a.num_tasks : (uint64_t)p->width * p->height;
+  const uint64_t npx = shards > 1 ? (uint64_t)r->local_tiles * RT_TILE_PIXELS
+                                  : (uint64_t)p->width * p->height;
   std::vector<uint32_t> clear(npx ? npx : 1, p->clear_color);
   if (upload(r->dev, clear.data(), npx * 4, &r->cbuf, &a.cbuf_addr)) return -1;
   r->cbuf_bytes = npx * 4;

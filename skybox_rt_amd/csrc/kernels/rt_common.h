@@ -128,7 +128,8 @@ typedef struct {
   uint64_t oms_addr;       // raster mode: rt_omstate_t per drawcall
   uint64_t bbox_addr;      // raster mode: rt_bbox_t per pid
   uint64_t nodes4_addr;    // rt_node4_t BVH4 (images built with RT_BVH4)
-  uint32_t num_nodes4, pad5;
+  uint32_t num_nodes4;
+  uint32_t split_tiles;    // the first split_tiles tiles of the work order run 32 pixels per wave
   uint64_t order_addr;     // RT modes: u32 per local tile, the order tiles are worked in
                            // (heaviest first; 0 = identity), see rt_app.cpp TileOrder
 } rt_kernel_arg_t;

@@ -44,7 +44,7 @@ struct Scene {
   vx_arena A;
   uint32_t nodes, nodes4, tris, layers, prims, dcs, cbuf, ptris, geom, order;
   uint32_t num_nodes, num_layer, num_geom, flags, width, height;
-  uint32_t shard_index, shard_count, tiles_x, clear_color, bounces, seed;
+  uint32_t shard_index, shard_count, tiles_x, clear_color, bounces, seed, split_tiles;
   float sx, sy, light[3];
   // the BVH staged in LDS by the workgroup (RT_LDS_SCENE images), or null
   const float4* lnodes = nullptr;
@@ -88,6 +88,7 @@ __device__ __forceinline__ Scene load_scene(const rt_kernel_arg_t* a) {
   s.num_geom = a->num_geom;
   s.bounces = a->bounces;
   s.seed = a->seed;
+  s.split_tiles = a->split_tiles;
   s.num_nodes = a->num_nodes;
   s.num_layer = a->num_layer_tris;
   s.flags = a->flags;
@@ -508,20 +509,44 @@ __device__ __forceinline__ int32_t resolve_layers(const Scene& S, const Ray& r, 
   return spid;
 }
 
-// task -> (shard-local 32x32 tile, 8x8 block, lane) -> pixel
+// task -> (shard-local 32x32 tile, pixel of the tile) -> pixel
 // Tasks are worked in the host's tile order (heaviest 32x32 tiles first, so
-// the long waves start at once instead of trailing the frame); `local_tile`
-// maps a task to the shard-local tile it renders.
-__device__ __forceinline__ uint32_t local_tile(const Scene& S, uint32_t t) {
-  return S.order ? S.A.ld_u32(S.order + 4u * (t >> 10)) : (t >> 10);
+// the long waves start at once instead of trailing the frame).  A tile is
+// 16 chunks of 64 tasks, one 8x8 pixel block each -- except the first
+// `split_tiles` tiles of the order (the ones geometry touches), which take
+// 32 chunks of 64 tasks with only lanes 0-31 live, one 8x4 half-block each:
+// half as many divergent rays per wave where the per-wave union of BVH
+// paths is widest, which shortens the frame's critical path.
+struct TaskPix {
+  uint32_t lt;   // shard-local tile
+  uint32_t idx;  // pixel of the tile in block order: (8x8 block) * 64 + lane of the block
+  bool live;
+};
+__device__ __forceinline__ TaskPix task_map(const Scene& S, uint32_t t) {
+  TaskPix m;
+  const uint32_t hs = S.split_tiles << 11;
+  uint32_t pos;
+  if (t < hs) {
+    const uint32_t c = (t >> 6) & 31u, ln = t & 63u;
+    pos = t >> 11;
+    m.idx = ((c >> 1) << 6) + (ln & 31u) + ((c & 1u) << 5);
+    m.live = ln < 32u;
+  } else {
+    pos = S.split_tiles + ((t - hs) >> 10);
+    m.idx = t & 1023u;
+    m.live = true;
+  }
+  m.lt = S.order ? S.A.ld_u32(S.order + 4u * pos) : pos;
+  return m;
 }
 
 __device__ __forceinline__ void task_pixel(const Scene& S, uint32_t t, uint32_t* x, uint32_t* y) {
-  const uint32_t lt = local_tile(S, t), blk = (t >> 6) & 15u, ln = t & 63u;
-  const uint32_t gt = S.shard_index + lt * S.shard_count;
+  const TaskPix m = task_map(S, t);
+  const uint32_t blk = m.idx >> 6, ln = m.idx & 63u;
+  const uint32_t gt = S.shard_index + m.lt * S.shard_count;
   const uint32_t tx = gt % S.tiles_x, ty = gt / S.tiles_x;
-  *x = (tx << RT_TILE_LOG) + ((blk & 3u) << 3) + (ln & 7u);
-  *y = (ty << RT_TILE_LOG) + ((blk >> 2) << 3) + (ln >> 3);
+  *x = m.live ? (tx << RT_TILE_LOG) + ((blk & 3u) << 3) + (ln & 7u) : 0xffffffffu;  // dead lane:
+  *y = (ty << RT_TILE_LOG) + ((blk >> 2) << 3) + (ln >> 3);                          // off-image
 }
 
 __device__ __forceinline__ void primary_dir(const Scene& S, uint32_t x, uint32_t y, Ray& r) {
@@ -548,8 +573,11 @@ __device__ __forceinline__ uint32_t shadowed(uint32_t c) {
 __device__ __forceinline__ void store_pixel(const Scene& S, uint32_t t, uint32_t x, uint32_t y,
                                             uint32_t color) {
   // compact shard buffers stay in local-tile order whatever the work order
-  const uint32_t idx = (S.flags & RT_FLAG_COMPACT) ? (local_tile(S, t) << 10) | (t & 1023u)
-                                                   : y * S.width + x;
+  uint32_t idx = y * S.width + x;
+  if (S.flags & RT_FLAG_COMPACT) {
+    const TaskPix m = task_map(S, t);
+    idx = (m.lt << 10) | m.idx;
+  }
   S.A.st_u32(S.cbuf + 4u * idx, color);
 }
 

@@ -254,7 +254,7 @@ class Renderer:
     def framebuffer(self) -> np.ndarray:
         p = self.params
         if p.shard_count > 1:
-            n = self.stats()["num_tasks"]
+            n = self.stats()["local_tiles"] * TILE * TILE
             out = np.zeros(max(n, 1), np.uint32)
             _check(lib().rt_read_framebuffer(self._h, out.ctypes.data, n), "rt_read_framebuffer")
             return out[:n]
