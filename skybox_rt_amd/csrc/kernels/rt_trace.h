@@ -209,12 +209,16 @@ __device__ __forceinline__ NodeStep node_step(const float4& n0, const float4& n1
 // <, misses keyed +inf, hit keys clamped to FLT_MAX so they sort first); the
 // nearest is returned, the other hits are pushed farthest first.  Halves the
 // dependent load -> test -> branch steps of a root-to-leaf walk vs BVH2.
+template <bool SCALAR>
 __device__ __forceinline__ int32_t node4_step(const Scene& S, uint32_t ref, const Ray& r,
                                               float tmin, float lim, int32_t* stack, int& sp) {
   const uint32_t no = S.nodes4 + 128u * ref;
-  const float4 lx = S.A.ld_f4(no), hx = S.A.ld_f4(no + 16), ly = S.A.ld_f4(no + 32);
-  const float4 hy = S.A.ld_f4(no + 48), lz = S.A.ld_f4(no + 64), hz = S.A.ld_f4(no + 80);
-  const float4 cf = S.A.ld_f4(no + 96);
+  // SCALAR: every active lane is at this node -- one scalar-cache load per
+  // record for the wave instead of 64 lanes of vector data return
+  auto ld = [&](uint32_t o) { return SCALAR ? S.A.sld_f4(o) : S.A.ld_f4(o); };
+  const float4 lx = ld(no), hx = ld(no + 16), ly = ld(no + 32);
+  const float4 hy = ld(no + 48), lz = ld(no + 64), hz = ld(no + 80);
+  const float4 cf = ld(no + 96);
   const float alx[4] = {lx.x, lx.y, lx.z, lx.w}, ahx[4] = {hx.x, hx.y, hx.z, hx.w};
   const float aly[4] = {ly.x, ly.y, ly.z, ly.w}, ahy[4] = {hy.x, hy.y, hy.z, hy.w};
   const float alz[4] = {lz.x, lz.y, lz.z, lz.w}, ahz[4] = {hz.x, hz.y, hz.z, hz.w};
@@ -269,7 +273,8 @@ __device__ __forceinline__ int32_t trace(const Scene& S, const Ray& r, float tmi
 #endif
       const float lim = ANY ? tmax : bt;
       if (S.flags & RT_FLAG_BVH4) {
-        const int32_t nx = node4_step(S, (uint32_t)ref, r, tmin, lim, stack, sp);
+        const int32_t nx = uni ? node4_step<true>(S, (uint32_t)r0, r, tmin, lim, stack, sp)
+                               : node4_step<false>(S, (uint32_t)ref, r, tmin, lim, stack, sp);
         if (nx != RT_EMPTY_REF) { ref = nx; continue; }
       } else {
       NodeStep st;
