@@ -168,11 +168,18 @@ def main():
         dev_ptr, nbytes = r.framebuffer_device()
         kind = 3 if coll_dev.type == "cuda" else 2  # hipMemcpyDeviceToDevice / ToHost
 
+        nsteps = [0]
+
         def gather():
-            # copy of the compact tile buffer into the gather's buffer, then the gather
-            hip.hipMemcpy(ctypes.c_void_p(fg.local.data_ptr()), ctypes.c_void_p(dev_ptr),
+            # copy of the compact tile buffer into a free gather slot, then the
+            # gather + frame assembly enqueued asynchronously: frame k's
+            # exchange overlaps frame k+1's render (two slots in flight)
+            slot = nsteps[0] % 2
+            nsteps[0] += 1
+            fg.finish(slot)
+            hip.hipMemcpy(ctypes.c_void_p(fg.locals[slot].data_ptr()), ctypes.c_void_p(dev_ptr),
                           ctypes.c_size_t(nbytes), kind)
-            fg()
+            fg.start(slot)
 
     def step():
         r.render()
@@ -181,6 +188,9 @@ def main():
 
     for _ in range(args.warmup):
         step()
+    if gather is not None:
+        fg.finish(0)
+        fg.finish(1)
     if dist is not None:
         dist.barrier()
     torch.cuda.synchronize()
@@ -189,6 +199,9 @@ def main():
     for _ in range(args.steps):
         step()
         kernel_ms.append(r.kernel_ms())
+    if gather is not None:  # every frame gathered and assembled inside the timed region
+        fg.finish(0)
+        fg.finish(1)
     torch.cuda.synchronize()
     if dist is not None:
         dist.barrier()

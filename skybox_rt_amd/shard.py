@@ -54,30 +54,45 @@ def deinterleave_tiles(shards, width: int, height: int) -> np.ndarray:
 
 
 class FrameGather:
-    """Gather the ranks' compact tile buffers to rank 0 and scatter them into
-    the frame.  Buffers are padded to the largest rank's size so one
-    dist.gather moves them; on RCCL a gather to one root is point-to-point
-    sends to it, each peer over its own xGMI link (no ring all-gather)."""
+    """Gather the ranks' compact tile buffers to rank 0 and assemble the
+    frame there.  Buffers are padded to the largest rank's size so one
+    dist.gather moves them, straight into views of one receive buffer (on
+    RCCL a gather to one root is point-to-point sends to it, each peer over
+    its own xGMI link -- no ring all-gather); the frame is then ONE index
+    gather through a precomputed permutation (frame pixel i <- slot perm[i]).
 
-    def __init__(self, dist, width: int, height: int, device):
+    Synchronous:  image = g(local)
+    Pipelined:    g.start(slot) after filling g.locals[slot] -- the gather
+    and the frame assembly are enqueued (async_op) so they overlap the next
+    frame's render; g.finish(slot) (or the next start on the same slot)
+    waits for them before the buffer is reused.  Two slots."""
+
+    def __init__(self, dist, width: int, height: int, device, slots: int = 2):
         import torch
         self.dist = dist
         self.rank, self.world = dist.get_rank(), dist.get_world_size()
         self.width, self.height = width, height
+        self.device = device
         self.max_local = local_tiles(width, height, 0, self.world) * TILE * TILE
-        self.local = torch.zeros(self.max_local, dtype=torch.int32, device=device)
-        self.parts = None
+        self.locals = [torch.zeros(self.max_local, dtype=torch.int32, device=device)
+                       for _ in range(slots)]
+        self.local = self.locals[0]
+        self.works = [None] * slots
+        self.recv = self.parts = self.perm = self.image = None
         if self.rank == 0:
-            self.parts = [torch.empty_like(self.local) for _ in range(self.world)]
-            src, dst = [], []
+            self.recv = torch.empty(self.world * self.max_local, dtype=torch.int32, device=device)
+            self.parts = list(self.recv.split(self.max_local))
+            perm = np.empty(width * height, np.int64)
             for r in range(self.world):
                 idx = task_pixel_index(width, height, r, self.world)
                 ok = np.nonzero(idx >= 0)[0]
-                src.append(ok + r * self.max_local)
-                dst.append(idx[ok])
-            self.src = torch.from_numpy(np.concatenate(src)).to(device)
-            self.dst = torch.from_numpy(np.concatenate(dst)).to(device)
+                perm[idx[ok]] = ok + r * self.max_local
+            self.perm = torch.from_numpy(perm).to(device)
             self.image = torch.zeros(width * height, dtype=torch.int32, device=device)
+
+    def _assemble(self):
+        import torch
+        torch.index_select(self.recv, 0, self.perm, out=self.image)
 
     def __call__(self, local=None):
         """local: this rank's compact buffer (int32 tensor); None = use
@@ -87,6 +102,24 @@ class FrameGather:
         self.dist.gather(self.local, self.parts, dst=0)
         if self.rank != 0:
             return None
-        import torch
-        self.image[self.dst] = torch.cat(self.parts)[self.src]
+        self._assemble()
         return self.image
+
+    def start(self, slot: int) -> None:
+        """Enqueue the gather of self.locals[slot] (+ the assembly on rank 0)."""
+        self.finish(slot)
+        w = self.dist.gather(self.locals[slot], self.parts, dst=0, async_op=True)
+        if self.rank == 0:
+            w.wait()          # the current stream waits for the gather (the host does not)
+            self._assemble()
+        self.works[slot] = w
+
+    def finish(self, slot: int) -> None:
+        """Block until the gather from self.locals[slot] has completed."""
+        import torch
+        w = self.works[slot]
+        if w is not None:
+            w.wait()
+            if self.device.type == "cuda":
+                torch.cuda.current_stream().synchronize()
+            self.works[slot] = None

@@ -37,8 +37,16 @@ def _worker(rank, world, port, w, h, q):
         local = np.where(idx >= 0, frame[np.maximum(idx, 0)], 0).astype(np.int32)
         g = FrameGatherCPU(w, h)
         img = g(torch.from_numpy(local))
+        ok = rank != 0 or bool(np.array_equal(img.numpy(), frame))
+        # the pipelined form bench.py runs: two slots in flight
+        for step in range(3):
+            slot = step % 2
+            g.locals[slot][:local.size].copy_(torch.from_numpy(local))
+            g.start(slot)
+        g.finish(0)
+        g.finish(1)
         if rank == 0:
-            q.put(bool(np.array_equal(img.numpy(), frame)))
+            q.put(ok and bool(np.array_equal(g.image.numpy(), frame)))
         dist.barrier()
     finally:
         dist.destroy_process_group()
