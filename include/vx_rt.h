@@ -88,6 +88,11 @@ int rt_render(rt_renderer_h r);  /* start + wait */
 int rt_render_stats(rt_renderer_h r, rt_stats_t* stats);
 /* HIP-event duration of the last launch only (no counter read-back) */
 int rt_render_kernel_ms(rt_renderer_h r, double* kernel_ms);
+/* waits for every started frame, then the summed HIP-event kernel time and
+ * the number of launches since the renderer's device opened: back-to-back
+ * rt_render_start calls queue behind the in-flight frame (the driver's
+ * VX_HIP_QUEUE_DEPTH), and this gives their per-launch average */
+int rt_render_run_totals(rt_renderer_h r, double* kernel_ms_sum, uint64_t* launches);
 /* linear W*H framebuffer (shard_count == 1) or compact tile buffer
  * (local_tiles * 1024 pixels in task order) */
 int rt_read_framebuffer(rt_renderer_h r, uint32_t* out, uint64_t count);

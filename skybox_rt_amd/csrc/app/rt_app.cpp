@@ -89,6 +89,7 @@ struct rt_renderer {
   vx_hip_stream_t stream = nullptr;
   vx_hip_last_run_t last_run = nullptr;
   vx_hip_mpm_rows_t mpm_rows = nullptr;
+  vx_hip_run_totals_t run_totals = nullptr;
   std::string kdir;         // kernel directory (images missing there come from lib_dir)
   bool deep = false;        // RT/PT images with the 32-entry traversal stack
   bool gpu_bvh = false;     // nodes/tris were built on the device (rt_renderer_build_bvh)
@@ -268,6 +269,7 @@ int rt_renderer_create(rt_scene_h s, const char* kernel_dir, rt_renderer_h* out)
   r->stream = (vx_hip_stream_t)vx_driver_symbol("vx_hip_stream");
   r->last_run = (vx_hip_last_run_t)vx_driver_symbol("vx_hip_last_run");
   r->mpm_rows = (vx_hip_mpm_rows_t)vx_driver_symbol("vx_hip_mpm_rows");
+  r->run_totals = (vx_hip_run_totals_t)vx_driver_symbol("vx_hip_run_totals");
   rt_kernel_arg_t& a = r->arg;
   std::memset(&a, 0, sizeof(a));
   const rt::Bvh& bvh = s->bvh;
@@ -551,6 +553,13 @@ int rt_render_kernel_ms(rt_renderer_h r, double* kernel_ms) {
   uint32_t grid = 0, block = 0;
   if (!r->last_run || r->last_run(r->dev, kernel_ms, &grid, &block) != 0)
     return fail("vx_hip_last_run failed");
+  return 0;
+}
+
+int rt_render_run_totals(rt_renderer_h r, double* kernel_ms_sum, uint64_t* launches) {
+  if (!r || !kernel_ms_sum || !launches) return fail("null argument");
+  if (!r->run_totals || r->run_totals(r->dev, kernel_ms_sum, launches) != 0)
+    return fail("vx_hip_run_totals failed");
   return 0;
 }
 

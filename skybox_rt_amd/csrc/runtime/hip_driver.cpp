@@ -13,7 +13,15 @@
 //                       constant block at every start();
 //   * start/ready_wait = asynchronous launch on the driver's stream, bracketed
 //                       by HIP events; ready_wait polls the stop event with a
-//                       timeout (the simx driver polls a std::future at 1 s);
+//                       timeout (the simx driver polls a std::future at 1 s).
+//                       simx's start() first waits for the in-flight run
+//                       (vortex.cpp:174-176); here a start() behind a run
+//                       queues on the stream instead -- the device still runs
+//                       them one after the other, the host just does not
+//                       idle between them (VX_HIP_QUEUE_DEPTH runs in flight,
+//                       default 2; 1 = simx's synchronous behaviour).  Every
+//                       call that touches memory, DCRs or counters still
+//                       waits for all of them first;
 //   * mpm_query       = event-timed device ns (MCYCLE) and task count
 //                       (MINSTRET) of the last run;
 //   * __vx_state      = per-launch device state: one counter row per block,
@@ -78,15 +86,25 @@ struct Module {
 
 }  // namespace
 
+// hip/hip_ext.h's launch templates need the HIP compiler; this file is
+// host C++, so the one extension used is declared here (libamdhip64 exports it)
+extern "C" hipError_t hipExtModuleLaunchKernel(hipFunction_t f, uint32_t gx, uint32_t gy,
+                                               uint32_t gz, uint32_t lx, uint32_t ly, uint32_t lz,
+                                               size_t shmem, hipStream_t stream, void** params,
+                                               void** extra, hipEvent_t start, hipEvent_t stop,
+                                               uint32_t flags);
+
 class vx_device {
  public:
   vx_device() : alloc_(0, 0, kBlockSize) {}
 
   ~vx_device() {
-    if (running_) (void)hipEventSynchronize(ev_stop_);
+    if (stream_) (void)hipStreamSynchronize(stream_);
     for (auto& kv : modules_) (void)hipModuleUnload(kv.second.module);
-    if (ev_start_) (void)hipEventDestroy(ev_start_);
-    if (ev_stop_) (void)hipEventDestroy(ev_stop_);
+    for (int i = 0; i < kMaxQueue; ++i) {
+      if (ev_start_[i]) (void)hipEventDestroy(ev_start_[i]);
+      if (ev_stop_[i]) (void)hipEventDestroy(ev_stop_[i]);
+    }
     if (stream_) (void)hipStreamDestroy(stream_);
     if (arena_) (void)hipFree(arena_);
   }
@@ -110,8 +128,13 @@ class vx_device {
     arena_size_ = arena_bytes;
     alloc_ = ArenaAllocator(USER_BASE_ADDR, arena_bytes - USER_BASE_ADDR, kBlockSize);
     HIP_CHECK(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking));
-    HIP_CHECK(hipEventCreate(&ev_start_));
-    HIP_CHECK(hipEventCreate(&ev_stop_));
+    for (int i = 0; i < kMaxQueue; ++i) {
+      HIP_CHECK(hipEventCreate(&ev_start_[i]));
+      HIP_CHECK(hipEventCreate(&ev_stop_[i]));
+    }
+    const uint64_t qd = env_u64("VX_HIP_QUEUE_DEPTH", 2);
+    depth_ = qd < 1 ? 1 : qd > (uint64_t)kMaxQueue ? kMaxQueue : (int)qd;
+    ext_launch_ = env_u64("VX_HIP_EXT_LAUNCH", 1) != 0;
     return 0;
   }
 
@@ -153,6 +176,7 @@ class vx_device {
     return 0;
   }
   int mem_free(uint64_t addr) {
+    wait_idle();  // a queued run may still read it
     acl_.erase(addr);
     shadow_.erase(addr);
     image_key_.erase(addr);
@@ -196,7 +220,10 @@ class vx_device {
   }
 
   int start(uint64_t krnl_addr, uint64_t args_addr) {
-    wait_idle();
+    // DCR writes already waited for the device (dcr_write); the STARTUP
+    // words below only differ from the in-flight run's when another image
+    // or argument block is started, which the constant upload check catches
+    if (depth_ <= 1) wait_idle();
     dcr_set(VX_DCR_BASE_STARTUP_ADDR0, (uint32_t)(krnl_addr & 0xffffffffu));
     dcr_set(VX_DCR_BASE_STARTUP_ADDR1, (uint32_t)(krnl_addr >> 32));
     dcr_set(VX_DCR_BASE_STARTUP_ARG0, (uint32_t)(args_addr & 0xffffffffu));
@@ -205,6 +232,13 @@ class vx_device {
     if (load_module(krnl_addr, &m) != 0) return -1;
     // constant blocks are only re-sent when they changed since this module's
     // last launch (a steady-state frame loop issues memset + launch only)
+    const bool upload = !m->base_set || !m->dcrs_set ||
+                        std::memcmp(m->dcrs_sent, dcrs_, sizeof(dcrs_)) != 0;
+    // constant uploads read host memory: only with the device idle
+    if (upload) wait_idle();
+    // bounded queue: retire the oldest run when depth_ are in flight
+    if (issued_ - retired_ >= (uint64_t)depth_ && retire(retired_ + 1, VX_MAX_TIMEOUT) != 0)
+      return -1;
     if (!m->base_set) {
       m->base_value = (uint64_t)(uintptr_t)arena_;
       HIP_CHECK(hipMemcpyHtoDAsync(m->mem_base, (void*)&m->base_value, sizeof(m->base_value), stream_));
@@ -215,26 +249,42 @@ class vx_device {
       HIP_CHECK(hipMemcpyHtoDAsync(m->dcrs, m->dcrs_sent, sizeof(dcrs_), stream_));
       m->dcrs_set = true;
     }
-    HIP_CHECK(hipEventRecord(ev_start_, stream_));
-    HIP_CHECK(hipModuleLaunchKernel(m->entry, m->grid, 1, 1, m->block, 1, 1, 0, stream_,
-                                    nullptr, nullptr));
-    HIP_CHECK(hipEventRecord(ev_stop_, stream_));
-    running_ = true;
+    const int slot = (int)(issued_ % kMaxQueue);
+    if (ext_launch_) {
+      // the dispatch packet itself carries the start/stop timestamps: no
+      // separate event packets between back-to-back frames
+      HIP_CHECK(hipExtModuleLaunchKernel(m->entry, m->grid * m->block, 1, 1, m->block, 1, 1, 0,
+                                         stream_, nullptr, nullptr, ev_start_[slot],
+                                         ev_stop_[slot], 0));
+    } else {
+      HIP_CHECK(hipEventRecord(ev_start_[slot], stream_));
+      HIP_CHECK(hipModuleLaunchKernel(m->entry, m->grid, 1, 1, m->block, 1, 1, 0, stream_,
+                                      nullptr, nullptr));
+      HIP_CHECK(hipEventRecord(ev_stop_[slot], stream_));
+    }
+    ++issued_;
+    mpm_dirty_ = true;  // read back lazily by mpm_query (after wait_idle)
     last_module_ = m;
     last_grid_ = m->grid;
     last_block_ = m->block;
     return 0;
   }
 
-  int ready_wait(uint64_t timeout_ms) {
-    if (!running_) return 0;
+  int ready_wait(uint64_t timeout_ms) { return retire(issued_, timeout_ms); }
+
+  // wait until run number `upto` (1-based issue count) has finished, then
+  // retire every run up to it: per-run event time into last_ms_ and the
+  // running totals (vx_hip_run_totals)
+  int retire(uint64_t upto, uint64_t timeout_ms) {
+    if (upto <= retired_) return 0;
+    hipEvent_t stop = ev_stop_[(upto - 1) % kMaxQueue];
     const auto t0 = std::chrono::steady_clock::now();
     for (uint32_t spin = 0;; ++spin) {
-      hipError_t e = hipEventQuery(ev_stop_);
+      hipError_t e = hipEventQuery(stop);
       if (e == hipSuccess) break;
       if (e != hipErrorNotReady) {
         std::printf("[VXDRV] kernel failed: %s\n", hipGetErrorString(e));
-        running_ = false;
+        retired_ = issued_;
         return -1;
       }
       const auto dt = std::chrono::steady_clock::now() - t0;
@@ -245,11 +295,14 @@ class vx_device {
       if (spin > 1024 && dt > std::chrono::milliseconds(5))
         std::this_thread::sleep_for(std::chrono::microseconds(50));
     }
-    running_ = false;
-    float ms = 0.0f;
-    HIP_CHECK(hipEventElapsedTime(&ms, ev_start_, ev_stop_));
-    last_ms_ = ms;
-    mpm_dirty_ = last_module_ != nullptr;  // read back lazily by mpm_query
+    for (; retired_ < upto; ++retired_) {
+      const int slot = (int)(retired_ % kMaxQueue);
+      float ms = 0.0f;
+      HIP_CHECK(hipEventElapsedTime(&ms, ev_start_[slot], ev_stop_[slot]));
+      last_ms_ = ms;
+      run_ms_total_ += ms;
+      ++runs_total_;
+    }
     return 0;
   }
 
@@ -269,11 +322,11 @@ class vx_device {
     const uint32_t off = addr - VX_CSR_MPM_BASE;
     if (off >= VX_MPM_COUNT) return -1;
     if (core_id != 0) { *value = 0; return 0; }  // device totals live on core 0
+    wait_idle();
     if (addr == VX_CSR_MCYCLE) {
       *value = (uint64_t)(last_ms_ * 1.0e6 + 0.5);
       return 0;
     }
-    wait_idle();
     if (mpm_dirty_) {  // sum the per-block counter rows of the last launch
       rows_.resize((size_t)last_grid_ * kMpmRow);
       HIP_CHECK(hipMemcpyAsync(rows_.data(), last_module_->mpm, rows_.size() * sizeof(uint32_t),
@@ -303,6 +356,11 @@ class vx_device {
   hipStream_t stream() const { return stream_; }
   int device_id() const { return device_id_; }
   double last_ms() const { return last_ms_; }
+  void run_totals(double* ms, uint64_t* runs) {
+    wait_idle();
+    if (ms) *ms = run_ms_total_;
+    if (runs) *runs = runs_total_;
+  }
   uint32_t last_grid() const { return last_grid_; }
   uint32_t last_block() const { return last_block_; }
 
@@ -312,7 +370,7 @@ class vx_device {
     dcr_valid_[addr] = true;
   }
   void wait_idle() {
-    if (running_) ready_wait(VX_MAX_TIMEOUT);
+    if (issued_ > retired_) ready_wait(VX_MAX_TIMEOUT);
   }
 
   int load_module(uint64_t krnl_addr, Module** out) {
@@ -373,8 +431,13 @@ class vx_device {
   std::map<uint64_t, Module> modules_;
   std::map<uint64_t, uint64_t> image_key_;  // image address -> module key
   hipStream_t stream_ = nullptr;
-  hipEvent_t ev_start_ = nullptr, ev_stop_ = nullptr;
-  bool running_ = false;
+  static constexpr int kMaxQueue = 8;
+  hipEvent_t ev_start_[kMaxQueue] = {}, ev_stop_[kMaxQueue] = {};
+  uint64_t issued_ = 0, retired_ = 0;  // runs started / retired (events read)
+  int depth_ = 2;
+  bool ext_launch_ = true;  // hipExtModuleLaunchKernel with packet timestamps
+  double run_ms_total_ = 0.0;
+  uint64_t runs_total_ = 0;
   Module* last_module_ = nullptr;
   bool mpm_dirty_ = false;
   double last_ms_ = 0.0;
@@ -500,9 +563,16 @@ __attribute__((visibility("default"))) int vx_hip_last_run(vx_device_h hdevice, 
                                                            uint32_t* grid, uint32_t* block) {
   if (hdevice == nullptr) return -1;
   auto* d = (vx_device*)hdevice;
+  d->run_totals(nullptr, nullptr);  // retires every queued run
   if (ms) *ms = d->last_ms();
   if (grid) *grid = d->last_grid();
   if (block) *block = d->last_block();
+  return 0;
+}
+__attribute__((visibility("default"))) int vx_hip_run_totals(vx_device_h hdevice, double* ms,
+                                                             uint64_t* runs) {
+  if (hdevice == nullptr) return -1;
+  ((vx_device*)hdevice)->run_totals(ms, runs);
   return 0;
 }
 __attribute__((visibility("default"))) int vx_hip_mpm_rows(vx_device_h hdevice, uint32_t* rows,
