@@ -124,13 +124,16 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     n_gpus = max(world, 1)
+    # BENCH_FORCE_GATHER=1 (under torch.distributed.run): the N>1 exchange
+    # path even at world size 1 -- RCCL on one GPU, to test its stream order
+    use_gather = world > 1 or os.environ.get("BENCH_FORCE_GATHER") == "1"
     dist = None
     import torch
     # RCCL ("nccl") between the GPUs; BENCH_DIST_BACKEND=gloo rehearses the
     # multi-rank flow with host-staged gathers (e.g. several ranks on one GPU)
     backend = os.environ.get("BENCH_DIST_BACKEND", "nccl")
     coll_dev = torch.device("cpu")
-    if world > 1:
+    if use_gather:
         import torch.distributed as dist
         dev_index = local_rank % max(1, torch.cuda.device_count())
         torch.cuda.set_device(dev_index)
@@ -158,13 +161,14 @@ def main():
     alg_bytes = algorithmic_bytes(inst, pixels_local, NODE4_BYTES if r.bvh4 else NODE_BYTES)
 
     r.configure(side, side, shadows=shadows, light=light, shard_index=rank, shard_count=n_gpus,
-                path=path, bounces=args.bounces, flat=flat)
+                path=path, bounces=args.bounces, flat=flat, compact=use_gather)
     gather = None
-    if world > 1:
+    if use_gather:
         import ctypes
         from skybox_rt_amd.shard import FrameGather
         hip = ctypes.CDLL("libamdhip64.so.7")  # torch's runtime, already loaded
-        fg = FrameGather(dist, side, side, coll_dev)
+        fg_slots = 4
+        fg = FrameGather(dist, side, side, coll_dev, slots=fg_slots)
         dev_ptr, nbytes = r.framebuffer_device()
         kind = 3 if coll_dev.type == "cuda" else 2  # hipMemcpyDeviceToDevice / ToHost
 
@@ -177,22 +181,23 @@ def main():
         def gather():
             # frame k's compact tile buffer -> a free gather slot, then the
             # gather + frame assembly enqueued asynchronously: frame k's
-            # exchange overlaps frame k+1's render (two slots in flight).
+            # exchange overlaps the next frames' renders (4 slots in flight).
             # RCCL: the copy is queued on the driver's stream right behind
-            # frame k's kernel (the host does not wait for the frame), and
-            # torch's stream -- which the gather follows -- waits for it
-            slot = nsteps[0] % 2
+            # frame k's kernel (the host does not wait for the frame) and the
+            # gather follows that stream; a slot is reclaimed on the host
+            # once its gather of 4 frames ago has completed
+            slot = nsteps[0] % fg_slots
             nsteps[0] += 1
-            fg.finish(slot)  # gather k-2 has released the slot
+            fg.reclaim(slot)
             if kind == 3:
                 hip.hipMemcpyAsync(fg.locals[slot].data_ptr(), dev_ptr, nbytes, kind,
                                    drv_stream.cuda_stream)
-                torch.cuda.current_stream().wait_stream(drv_stream)
+                fg.start(slot, stream=drv_stream)
             else:  # host-staged rehearsal (gloo): the frame must be complete
                 r.wait()
                 hip.hipMemcpy(ctypes.c_void_p(fg.locals[slot].data_ptr()),
                               ctypes.c_void_p(dev_ptr), ctypes.c_size_t(nbytes), kind)
-            fg.start(slot)
+                fg.start(slot)
 
     # a step = one frame: vx_start queues the launch behind the in-flight
     # frame (driver VX_HIP_QUEUE_DEPTH, default 2) so the host's launch and
@@ -216,8 +221,8 @@ def main():
         step()
     r.wait()
     if gather is not None:
-        fg.finish(0)
-        fg.finish(1)
+        for slot in range(fg_slots):
+            fg.reclaim(slot)
     if dist is not None:
         dist.barrier()
     torch.cuda.synchronize()
@@ -227,8 +232,8 @@ def main():
         step()
     r.wait()
     if gather is not None:  # every frame gathered and assembled inside the timed region
-        fg.finish(0)
-        fg.finish(1)
+        for slot in range(fg_slots):
+            fg.reclaim(slot)
     torch.cuda.synchronize()
     if dist is not None:
         dist.barrier()

@@ -38,6 +38,8 @@ typedef struct {
 #define RT_RENDER_BVH2 0x40u           /* traverse the binary BVH (default: the 4-wide one;
                                           env RT_BVH_WIDTH=2 flips the default) */
 #define RT_RENDER_INSTRUMENTED 0x100u  /* use the counting kernel variant */
+#define RT_RENDER_COMPACT 0x200u       /* compact tile-order output (the shard layout,
+                                          implied by shard_count > 1) for one shard too */
 
 typedef struct {
   uint32_t width, height;

@@ -379,7 +379,8 @@ int rt_renderer_configure(rt_renderer_h r, const rt_render_params_t* p) {
   const bool raster = (p->flags & RT_RENDER_RASTER) != 0;
   if (!raster && !r->sc->unsupported.empty())
     return fail("scene not supported by the RT path (use RT_RENDER_RASTER): " + r->sc->unsupported, -2);
-  if (raster && (shards > 1 || (p->flags & RT_RENDER_INSTRUMENTED)))
+  const bool compact = shards > 1 || (p->flags & RT_RENDER_COMPACT);
+  if (raster && (compact || (p->flags & RT_RENDER_INSTRUMENTED)))
     return fail("RT_RENDER_RASTER renders whole frames, uninstrumented");
   if (p->shard_index >= shards) return fail("shard_index >= shard_count");
   const rt_scene* s = r->sc;
@@ -481,7 +482,7 @@ int rt_renderer_configure(rt_renderer_h r, const rt_render_params_t* p) {
             ((p->flags & RT_RENDER_PATH) ? RT_FLAG_PATH : 0u) |
             ((p->flags & RT_RENDER_FLAT) ? RT_FLAG_FLAT : 0u) |
             (raster ? RT_FLAG_RASTER : 0u) |
-            (s->tie_high ? RT_FLAG_TIE_HIGH : 0u) | (shards > 1 ? RT_FLAG_COMPACT : 0u) |
+            (s->tie_high ? RT_FLAG_TIE_HIGH : 0u) | (compact ? RT_FLAG_COMPACT : 0u) |
             (use_bvh4 ? RT_FLAG_BVH4 : 0u);
   a.bounces = p->bounces;
   a.seed = p->seed;
@@ -492,7 +493,7 @@ int rt_renderer_configure(rt_renderer_h r, const rt_render_params_t* p) {
   a.light[1] = p->light[1];
   a.light[2] = p->light[2];
   // output buffer, pre-filled with the clear colour (draw3d/main.cpp:485-490)
-  const uint64_t npx = shards > 1 ? (uint64_t)r->local_tiles * RT_TILE_PIXELS
+  const uint64_t npx = compact ? (uint64_t)r->local_tiles * RT_TILE_PIXELS
                                   : (uint64_t)p->width * p->height;
   std::vector<uint32_t> clear(npx ? npx : 1, p->clear_color);
   if (upload(r->dev, clear.data(), npx * 4, &r->cbuf, &a.cbuf_addr)) return -1;

@@ -62,10 +62,15 @@ class FrameGather:
     gather through a precomputed permutation (frame pixel i <- slot perm[i]).
 
     Synchronous:  image = g(local)
-    Pipelined:    g.start(slot) after filling g.locals[slot] -- the gather
-    and the frame assembly are enqueued (async_op) so they overlap the next
-    frame's render; g.finish(slot) (or the next start on the same slot)
-    waits for them before the buffer is reused.  Two slots."""
+    Pipelined:    g.start(slot[, stream]) after filling g.locals[slot] --
+    the gather (and on rank 0 the frame assembly) is enqueued (async_op) so
+    it overlaps the next frames' renders.  Every slot has its own send and
+    receive buffers, so frames in flight never share memory; before a slot
+    is refilled, g.reclaim(slot) waits ON THE HOST until that slot's
+    previous gather and assembly have completed -- normally long done, so
+    the frame loop puts no cross-stream waits on the render stream.  On
+    GPUs the gather follows `stream` (the stream that filled the slot) and
+    the assembly runs on a stream of its own.  g.finish(slot) = reclaim."""
 
     def __init__(self, dist, width: int, height: int, device, slots: int = 2):
         import torch
@@ -73,15 +78,21 @@ class FrameGather:
         self.rank, self.world = dist.get_rank(), dist.get_world_size()
         self.width, self.height = width, height
         self.device = device
+        self.cuda = getattr(device, "type", str(device)) == "cuda"
         self.max_local = local_tiles(width, height, 0, self.world) * TILE * TILE
         self.locals = [torch.zeros(self.max_local, dtype=torch.int32, device=device)
                        for _ in range(slots)]
         self.local = self.locals[0]
         self.works = [None] * slots
+        self.asm_done = [None] * slots
+        self.recvs = self.parts_s = None
         self.recv = self.parts = self.perm = self.image = None
+        self.asm_stream = torch.cuda.Stream(device) if self.cuda and self.rank == 0 else None
         if self.rank == 0:
-            self.recv = torch.empty(self.world * self.max_local, dtype=torch.int32, device=device)
-            self.parts = list(self.recv.split(self.max_local))
+            self.recvs = [torch.empty(self.world * self.max_local, dtype=torch.int32, device=device)
+                          for _ in range(slots)]
+            self.parts_s = [list(r.split(self.max_local)) for r in self.recvs]
+            self.recv, self.parts = self.recvs[0], self.parts_s[0]
             perm = np.empty(width * height, np.int64)
             for r in range(self.world):
                 idx = task_pixel_index(width, height, r, self.world)
@@ -90,36 +101,58 @@ class FrameGather:
             self.perm = torch.from_numpy(perm).to(device)
             self.image = torch.zeros(width * height, dtype=torch.int32, device=device)
 
-    def _assemble(self):
+    def _assemble(self, slot: int = 0):
         import torch
-        torch.index_select(self.recv, 0, self.perm, out=self.image)
+        torch.index_select(self.recvs[slot], 0, self.perm, out=self.image)
 
     def __call__(self, local=None):
         """local: this rank's compact buffer (int32 tensor); None = use
         self.local (filled by the caller, e.g. by a device copy)."""
+        self.reclaim(0)
         if local is not None:
             self.local[:local.numel()].copy_(local.reshape(-1))
         self.dist.gather(self.local, self.parts, dst=0)
         if self.rank != 0:
             return None
-        self._assemble()
+        self._assemble(0)
         return self.image
 
-    def start(self, slot: int) -> None:
-        """Enqueue the gather of self.locals[slot] (+ the assembly on rank 0)."""
-        self.finish(slot)
-        w = self.dist.gather(self.locals[slot], self.parts, dst=0, async_op=True)
+    def start(self, slot: int, stream=None) -> None:
+        """Enqueue the gather of self.locals[slot] (+ the assembly on rank 0).
+        stream: the CUDA stream that filled the slot (default: current)."""
+        import contextlib
+        import torch
+        self.reclaim(slot)
+        parts = self.parts_s[slot] if self.rank == 0 else None
+        ctx = torch.cuda.stream(stream) if (self.cuda and stream is not None) else contextlib.nullcontext()
+        with ctx:
+            w = self.dist.gather(self.locals[slot], parts, dst=0, async_op=True)
         if self.rank == 0:
-            w.wait()          # the current stream waits for the gather (the host does not)
-            self._assemble()
+            if self.asm_stream is not None:
+                with torch.cuda.stream(self.asm_stream):
+                    w.wait()  # the assembly stream waits for the gather (the host does not)
+                    self._assemble(slot)
+                    ev = torch.cuda.Event()
+                    ev.record(self.asm_stream)
+                    self.asm_done[slot] = ev
+            else:
+                w.wait()
+                self._assemble(slot)
         self.works[slot] = w
 
-    def finish(self, slot: int) -> None:
-        """Block until the gather from self.locals[slot] has completed."""
-        import torch
-        w = self.works[slot]
+    def reclaim(self, slot: int) -> None:
+        """Host wait until the slot's previous gather (and assembly) are done."""
+        import time
+        w, ev = self.works[slot], self.asm_done[slot]
         if w is not None:
-            w.wait()
-            if self.device.type == "cuda":
-                torch.cuda.current_stream().synchronize()
+            if self.cuda:
+                while not w.is_completed():
+                    time.sleep(0)
+            else:
+                w.wait()
             self.works[slot] = None
+        if ev is not None:
+            ev.synchronize()
+            self.asm_done[slot] = None
+
+    finish = reclaim

@@ -200,6 +200,37 @@ def test_render_is_deterministic_and_repeatable():
     assert r.stats()["kernel_ms"] > 0
 
 
+def test_compact_single_shard_is_the_shard_layout():
+    _, r = renderer("tekkaman")
+    W = H = 200  # edge tiles overhang the image
+    r.configure(W, H, shadows=True)
+    r.render()
+    full = r.framebuffer()
+    r.configure(W, H, shadows=True, compact=True)
+    r.render()
+    part = r.framebuffer()
+    assert part.size == 7 * 7 * 1024
+    assert np.array_equal(rt.deinterleave_tiles([part], W, H), full)
+
+
+@pytest.mark.parametrize("path", (False, True))
+def test_queued_frames_equal_synchronous_frames(path):
+    # back-to-back vx_start calls queue behind the in-flight frame (driver
+    # VX_HIP_QUEUE_DEPTH); every queued frame is a complete, identical render
+    _, r = renderer("tekkaman")
+    r.configure(512, 512, shadows=True, path=path)
+    r.render()
+    ref = r.framebuffer()
+    ms0, n0 = r.run_totals()
+    for _ in range(7):
+        r.start()
+    r.wait()
+    ms1, n1 = r.run_totals()
+    assert n1 - n0 == 7 and ms1 > ms0
+    assert np.array_equal(r.framebuffer(), ref)
+    assert r.stats()["primary_rays"] == 512 * 512
+
+
 def test_rtapp_cli_against_golden():
     exe = os.path.join(_lib.LIB_DIR, "rtapp")
     out = subprocess.run([exe, "-t", scene_path("triangle"), "-w", "64", "-h", "64", "-o",
