@@ -287,6 +287,108 @@ __device__ __forceinline__ bool path_step(const Scene& S, int32_t* stack, PathSt
   return alive;
 }
 
+// Paired form of path_step for a wave whose upper 32 lanes hold no pixel
+// (the 32-pixel waves of geometry tiles, task_map): lane l < 32 owns a path,
+// lane l + 32 traces that path's shadow ray while lane l traces its bounce
+// ray -- one traversal loop for both (trace_mixed), so a vertex costs the
+// longer of the two traversals instead of their sum.  Same rays, same
+// arithmetic, same order of the radiance updates as path_step: the output
+// and every counter are identical.  All 64 lanes call it.
+#ifndef PT_PAIR
+#define PT_PAIR 1
+#endif
+__device__ __forceinline__ bool path_step_pair(const Scene& S, int32_t* stack, PathState& st,
+                                               uint32_t v, bool act, Counters& cnt) {
+  const bool tie_high = (S.flags & RT_FLAG_TIE_HIGH) != 0;
+  const int32_t ln = (int32_t)lane_id();
+  const bool owner = ln < 32;
+  float v0[3], e1[3], e2[3], nrm[3], P[3];
+  load_tri(S, act ? st.pid : 0, v0, e1, e2);
+  tri_normal(e1, e2, st.d, nrm);
+  const float tt = st.t * 0.999755859375f;
+#pragma unroll
+  for (int k = 0; k < 3; ++k) P[k] = fmaf(st.d[k], tt, st.o[k]);
+  float sd[3] = {S.light[0] - P[0], S.light[1] - P[1], S.light[2] - P[2]};
+  bool alive = act && v < S.bounces;
+  Ray b;
+  b.o[0] = P[0]; b.o[1] = P[1]; b.o[2] = P[2];
+  if (alive) {
+    uint32_t x, y;
+    task_pixel(S, st.task, &x, &y);
+    bounce_dir(nrm, pt_key(S.seed, y * S.width + x, v), b.d);  // keyed by pixel, not task
+  } else {
+    b.d[0] = 1.0f; b.d[1] = 1.0f; b.d[2] = 1.0f;
+  }
+  // the helper lane receives its owner's vertex and shadow direction (the
+  // cross-lane reads run with all 64 lanes active: a bpermute from an
+  // inactive lane returns 0)
+  const int src = ln ^ 32;
+  const bool h_act = __shfl((int)act, src) != 0;
+  const int32_t h_pid = __shfl(st.pid, src);
+  Ray r;
+#pragma unroll
+  for (int k = 0; k < 3; ++k) {
+    const float ho = __shfl(P[k], src), hd = __shfl(sd[k], src);
+    r.o[k] = owner ? b.o[k] : ho;
+    r.d[k] = owner ? b.d[k] : hd;
+  }
+  ray_setup(r);
+  const bool tracing = owner ? alive : h_act;
+  float tr = 0.0f;
+  const int32_t res = tracing ? trace_mixed(S, r, 0.0f, owner ? INFINITY : 1.0f,
+                                            owner ? st.pid : h_pid, tie_high, &tr, stack, cnt,
+                                            !owner)
+                              : -1;
+  const bool h_occ = __shfl((int)(res >= 0), src) != 0;  // the helper's verdict (all lanes)
+  const bool occ = act && h_occ;
+  cnt.shadow += act;
+  cnt.occluded += occ;
+  if (act && !occ) {
+    const float cosl = dot3(nrm, sd) / sqrtf(dot3(sd, sd));
+    if (cosl > 0.0f) {
+#pragma unroll
+      for (int k = 0; k < 3; ++k) st.L[k] = fmaf(st.T[k], cosl, st.L[k]);
+    }
+  }
+  const int32_t np = res;
+  const float nt = tr;
+  if (alive) {
+    cnt.bounce += 1;
+    if (np < 0) {
+#pragma unroll
+      for (int k = 0; k < 3; ++k) st.L[k] = fmaf(st.T[k], PT_SKY, st.L[k]);
+      alive = false;
+    }
+  }
+  if (alive) {
+    float w0[3], f1[3], f2[3], b1, b2;
+    load_tri(S, np, w0, f1, f2);
+    mt_bary(b.o, b.d, w0, f1, f2, &b1, &b2);
+    gfx::Prim p;
+    gfx::load_prim(S.A, S.prims + 128u * (uint32_t)np, p);
+    const gfx::DcState dst = gfx::load_dcstate(S.A, S.dcs + 64u * p.dc());
+#ifdef RT_INSTRUMENT
+    ++cnt.shaded;
+    if (dst.flags & RT_DC_TEX)
+      cnt.texel_bytes += (dst.filter == VX_TEX_FILTER_BILINEAR ? 4u : 1u) * dst.stride;
+#endif
+    const uint32_t a = gfx::shade_weights(S.A, p, dst, gfx::fx_from_float_dev((1.0f - b1) - b2, 24),
+                                          gfx::fx_from_float_dev(b1, 24));
+    const float k255 = 1.0f / 255.0f;
+    st.T[0] = st.T[0] * ((float)((a >> 16) & 0xffu) * k255);
+    st.T[1] = st.T[1] * ((float)((a >> 8) & 0xffu) * k255);
+    st.T[2] = st.T[2] * ((float)(a & 0xffu) * k255);
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+      st.o[k] = P[k];
+      st.d[k] = b.d[k];
+    }
+    st.pid = np;
+    st.t = nt;
+  }
+  return alive;
+}
+
 __device__ __forceinline__ void store_path_pixel(const Scene& S, const PathState& st) {
   uint32_t x, y;
   task_pixel(S, st.task, &x, &y);
@@ -348,6 +450,9 @@ __device__ __forceinline__ void lane_path(const vx_task_t& task, const Scene& S,
   uint32_t x, y;
   task_pixel(S, t, &x, &y);
   const bool in = x < S.width && y < S.height;
+  // paired vertices (path_step_pair) when the whole wave is here and its
+  // upper 32 lanes hold no pixel -- wave-uniform
+  const bool pair = PT_PAIR && __ballot(1) == ~0ull && (__ballot(in) >> 32) == 0;
   Ray r;
   primary_dir(S, x, y, r);
   ray_setup(r);
@@ -358,10 +463,8 @@ __device__ __forceinline__ void lane_path(const vx_task_t& task, const Scene& S,
   cnt.hits += hit >= 0;
   const int32_t spid = resolve_layers(S, r, in && hit < 0, hit, cnt);
   const uint32_t color = shade_wave(S, spid, x, y, S.clear_color, cnt);
-  if (hit < 0) {
-    if (in) store_pixel(S, t, x, y, color);
-    return;
-  }
+  if (hit < 0 && in) store_pixel(S, t, x, y, color);
+  if (hit < 0 && !pair) return;
   const float k255 = 1.0f / 255.0f;
   PathState st;
   st.task = t;
@@ -376,6 +479,14 @@ __device__ __forceinline__ void lane_path(const vx_task_t& task, const Scene& S,
     st.o[k] = r.o[k];
     st.d[k] = r.d[k];
     st.L[k] = 0.0f;
+  }
+  if (pair) {
+    // every lane stays in the loop (helpers trace their owner's shadow ray)
+    bool act = hit >= 0;
+    const bool own = act;
+    for (uint32_t v = 0; __ballot(act) != 0; ++v) act = path_step_pair(S, stack, st, v, act, cnt);
+    if (own) store_path_pixel(S, st);
+    return;
   }
   for (uint32_t v = 0; path_step(S, stack, st, v, true, cnt); ++v) {
   }

@@ -299,10 +299,15 @@ __device__ __forceinline__ int32_t node4_step(const Scene& S, uint32_t ref, cons
   return c[0];
 }
 
-template <bool ANY>
-__device__ __forceinline__ int32_t trace(const Scene& S, const Ray& r, float tmin, float tmax,
-                                         int32_t skip, bool tie_high, float* t_out,
-                                         int32_t* stack, Counters& cnt) {
+// MODE 0: closest hit, 1: any hit (first occluder below tmax), 2: chosen
+// per lane by `any_rt` -- lanes of one wave tracing different ray kinds in
+// the same traversal loop (the path tracer's paired shadow + bounce rays).
+// Per ray, every mode visits the same nodes and returns the same result.
+template <int MODE>
+__device__ __forceinline__ int32_t trace_impl(const Scene& S, const Ray& r, float tmin, float tmax,
+                                              int32_t skip, bool tie_high, float* t_out,
+                                              int32_t* stack, Counters& cnt, bool any_rt) {
+  const bool ANY = MODE == 1 || (MODE == 2 && any_rt);
   if (S.num_nodes == 0) return -1;
   LaneStack lst(stack);
   int32_t ref = 0;
@@ -419,6 +424,19 @@ __device__ __forceinline__ int32_t trace(const Scene& S, const Ray& r, float tmi
   }
   if (bpid >= 0) *t_out = bt;
   return bpid;
+}
+
+template <bool ANY>
+__device__ __forceinline__ int32_t trace(const Scene& S, const Ray& r, float tmin, float tmax,
+                                         int32_t skip, bool tie_high, float* t_out,
+                                         int32_t* stack, Counters& cnt) {
+  return trace_impl<ANY ? 1 : 0>(S, r, tmin, tmax, skip, tie_high, t_out, stack, cnt, ANY);
+}
+
+__device__ __forceinline__ int32_t trace_mixed(const Scene& S, const Ray& r, float tmin, float tmax,
+                                               int32_t skip, bool tie_high, float* t_out,
+                                               int32_t* stack, Counters& cnt, bool any) {
+  return trace_impl<2>(S, r, tmin, tmax, skip, tie_high, t_out, stack, cnt, any);
 }
 
 // Flat triangle list, no BVH (BASELINE config 2; the oracle's brute_trace):
