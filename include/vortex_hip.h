@@ -24,11 +24,13 @@ typedef int (*vx_hip_stream_t)(vx_device_h hdevice, void** hip_stream);
 typedef int (*vx_hip_last_run_t)(vx_device_h hdevice, double* kernel_ms,
                                  uint32_t* grid, uint32_t* block);
 typedef int (*vx_hip_device_id_t)(vx_device_h hdevice, int* device_id);
-/* waits for every queued run, then the sum of their event-timed kernel
- * durations and their count since the device opened (a start() behind an
- * in-flight run queues instead of blocking: VX_HIP_QUEUE_DEPTH, default 2) */
+/* waits for every queued run, then, since the device opened: the summed
+ * event-timed kernel durations, the number of timed runs and of all runs.
+ * A start() behind an in-flight run queues instead of blocking
+ * (VX_HIP_QUEUE_DEPTH, default 2); queued runs are timed one in
+ * VX_HIP_TIME_EVERY (default 4), a run started on an idle queue always. */
 typedef int (*vx_hip_run_totals_t)(vx_device_h hdevice, double* kernel_ms_sum,
-                                   uint64_t* runs);
+                                   uint64_t* timed_runs, uint64_t* runs);
 /* the last launch's raw per-workgroup counter rows (vx_spawn.h: 16 u32 per
  * workgroup, in blockIdx order): copies min(grid, max_rows) rows to `rows`,
  * *nrows = grid.  Diagnostics (e.g. in-kernel timestamps). */

@@ -90,11 +90,13 @@ int rt_render(rt_renderer_h r);  /* start + wait */
 int rt_render_stats(rt_renderer_h r, rt_stats_t* stats);
 /* HIP-event duration of the last launch only (no counter read-back) */
 int rt_render_kernel_ms(rt_renderer_h r, double* kernel_ms);
-/* waits for every started frame, then the summed HIP-event kernel time and
- * the number of launches since the renderer's device opened: back-to-back
- * rt_render_start calls queue behind the in-flight frame (the driver's
- * VX_HIP_QUEUE_DEPTH), and this gives their per-launch average */
-int rt_render_run_totals(rt_renderer_h r, double* kernel_ms_sum, uint64_t* launches);
+/* waits for every started frame, then, since the renderer's device opened:
+ * the summed HIP-event kernel time of the timed launches, their number, and
+ * the number of all launches.  Back-to-back rt_render_start calls queue
+ * behind the in-flight frame (the driver's VX_HIP_QUEUE_DEPTH) and are timed
+ * one in VX_HIP_TIME_EVERY: kernel_ms_sum / timed is their average. */
+int rt_render_run_totals(rt_renderer_h r, double* kernel_ms_sum, uint64_t* timed,
+                         uint64_t* launches);
 /* linear W*H framebuffer (shard_count == 1) or compact tile buffer
  * (local_tiles * 1024 pixels in task order) */
 int rt_read_framebuffer(rt_renderer_h r, uint32_t* out, uint64_t count);

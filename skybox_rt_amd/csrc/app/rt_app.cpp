@@ -557,9 +557,10 @@ int rt_render_kernel_ms(rt_renderer_h r, double* kernel_ms) {
   return 0;
 }
 
-int rt_render_run_totals(rt_renderer_h r, double* kernel_ms_sum, uint64_t* launches) {
-  if (!r || !kernel_ms_sum || !launches) return fail("null argument");
-  if (!r->run_totals || r->run_totals(r->dev, kernel_ms_sum, launches) != 0)
+int rt_render_run_totals(rt_renderer_h r, double* kernel_ms_sum, uint64_t* timed,
+                         uint64_t* launches) {
+  if (!r || !kernel_ms_sum || !timed || !launches) return fail("null argument");
+  if (!r->run_totals || r->run_totals(r->dev, kernel_ms_sum, timed, launches) != 0)
     return fail("vx_hip_run_totals failed");
   return 0;
 }

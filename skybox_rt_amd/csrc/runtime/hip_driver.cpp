@@ -21,7 +21,9 @@
 //                       idle between them (VX_HIP_QUEUE_DEPTH runs in flight,
 //                       default 2; 1 = simx's synchronous behaviour).  Every
 //                       call that touches memory, DCRs or counters still
-//                       waits for all of them first;
+//                       waits for all of them first.  Queued runs carry HIP
+//                       events (kernel time) one in VX_HIP_TIME_EVERY (4);
+//                       a run started on an idle queue always does;
 //   * mpm_query       = event-timed device ns (MCYCLE) and task count
 //                       (MINSTRET) of the last run;
 //   * __vx_state      = per-launch device state: one counter row per block,
@@ -133,8 +135,10 @@ class vx_device {
       HIP_CHECK(hipEventCreate(&ev_stop_[i]));
     }
     const uint64_t qd = env_u64("VX_HIP_QUEUE_DEPTH", 2);
-    depth_ = qd < 1 ? 1 : qd > (uint64_t)kMaxQueue ? kMaxQueue : (int)qd;
-    ext_launch_ = env_u64("VX_HIP_EXT_LAUNCH", 1) != 0;
+    depth_ = qd < 1 ? 1 : qd > 16 ? 16 : (int)qd;
+    const uint64_t te = env_u64("VX_HIP_TIME_EVERY", 4);
+    time_every_ = te < 1 ? 1 : te > 16 ? 16 : (int)te;
+    launch_mode_ = (int)env_u64("VX_HIP_EXT_LAUNCH", 1);
     return 0;
   }
 
@@ -236,9 +240,13 @@ class vx_device {
                         std::memcmp(m->dcrs_sent, dcrs_, sizeof(dcrs_)) != 0;
     // constant uploads read host memory: only with the device idle
     if (upload) wait_idle();
-    // bounded queue: retire the oldest run when depth_ are in flight
-    if (issued_ - retired_ >= (uint64_t)depth_ && retire(retired_ + 1, VX_MAX_TIMEOUT) != 0)
-      return -1;
+    // bounded queue: with depth_ + time_every_ - 1 runs in flight, retire up
+    // to the oldest timed one (at least depth_ - 1 stay queued behind it)
+    while (launch_mode_ != 2 && issued_ - retired_ >= (uint64_t)(depth_ + time_every_ - 1)) {
+      uint64_t j = retired_ + 1;
+      while (j <= issued_ && !timed_[(j - 1) % kMaxQueue]) ++j;
+      if (retire(j <= issued_ ? j : issued_, VX_MAX_TIMEOUT) != 0) return -1;
+    }
     if (!m->base_set) {
       m->base_value = (uint64_t)(uintptr_t)arena_;
       HIP_CHECK(hipMemcpyHtoDAsync(m->mem_base, (void*)&m->base_value, sizeof(m->base_value), stream_));
@@ -250,7 +258,18 @@ class vx_device {
       m->dcrs_set = true;
     }
     const int slot = (int)(issued_ % kMaxQueue);
-    if (ext_launch_) {
+    // a run is timed (events) when it starts on an idle queue -- every run of
+    // a start + wait loop -- and then every time_every_-th run: an event
+    // costs ~5 us of idle device between back-to-back runs (measured)
+    const bool timed = launch_mode_ != 2 && (issued_ == retired_ || issued_ % time_every_ == 0);
+    timed_[slot] = timed;
+    if (!timed) {
+      HIP_CHECK(hipExtModuleLaunchKernel(m->entry, m->grid * m->block, 1, 1, m->block, 1, 1, 0,
+                                         stream_, nullptr, nullptr, nullptr, nullptr, 0));
+    } else if (launch_mode_ == 2) {
+      HIP_CHECK(hipExtModuleLaunchKernel(m->entry, m->grid * m->block, 1, 1, m->block, 1, 1, 0,
+                                         stream_, nullptr, nullptr, nullptr, nullptr, 0));
+    } else if (launch_mode_ == 1) {
       // the dispatch packet itself carries the start/stop timestamps: no
       // separate event packets between back-to-back frames
       HIP_CHECK(hipExtModuleLaunchKernel(m->entry, m->grid * m->block, 1, 1, m->block, 1, 1, 0,
@@ -277,10 +296,13 @@ class vx_device {
   // running totals (vx_hip_run_totals)
   int retire(uint64_t upto, uint64_t timeout_ms) {
     if (upto <= retired_) return 0;
+    // an untimed run has no event: its completion is the stream's
+    const bool by_event = timed_[(upto - 1) % kMaxQueue];
+    if (!by_event) upto = issued_;
     hipEvent_t stop = ev_stop_[(upto - 1) % kMaxQueue];
     const auto t0 = std::chrono::steady_clock::now();
     for (uint32_t spin = 0;; ++spin) {
-      hipError_t e = hipEventQuery(stop);
+      hipError_t e = by_event ? hipEventQuery(stop) : hipStreamQuery(stream_);
       if (e == hipSuccess) break;
       if (e != hipErrorNotReady) {
         std::printf("[VXDRV] kernel failed: %s\n", hipGetErrorString(e));
@@ -297,11 +319,13 @@ class vx_device {
     }
     for (; retired_ < upto; ++retired_) {
       const int slot = (int)(retired_ % kMaxQueue);
+      ++runs_total_;
+      if (!timed_[slot]) continue;
       float ms = 0.0f;
       HIP_CHECK(hipEventElapsedTime(&ms, ev_start_[slot], ev_stop_[slot]));
       last_ms_ = ms;
       run_ms_total_ += ms;
-      ++runs_total_;
+      ++runs_timed_;
     }
     return 0;
   }
@@ -356,9 +380,10 @@ class vx_device {
   hipStream_t stream() const { return stream_; }
   int device_id() const { return device_id_; }
   double last_ms() const { return last_ms_; }
-  void run_totals(double* ms, uint64_t* runs) {
+  void run_totals(double* ms, uint64_t* timed, uint64_t* runs) {
     wait_idle();
     if (ms) *ms = run_ms_total_;
+    if (timed) *timed = runs_timed_;
     if (runs) *runs = runs_total_;
   }
   uint32_t last_grid() const { return last_grid_; }
@@ -431,11 +456,17 @@ class vx_device {
   std::map<uint64_t, Module> modules_;
   std::map<uint64_t, uint64_t> image_key_;  // image address -> module key
   hipStream_t stream_ = nullptr;
-  static constexpr int kMaxQueue = 8;
+  static constexpr int kMaxQueue = 32;  // >= depth_ + time_every_
   hipEvent_t ev_start_[kMaxQueue] = {}, ev_stop_[kMaxQueue] = {};
+  bool timed_[kMaxQueue] = {};
+  int time_every_ = 4;
+  uint64_t runs_timed_ = 0;
   uint64_t issued_ = 0, retired_ = 0;  // runs started / retired (events read)
   int depth_ = 2;
-  bool ext_launch_ = true;  // hipExtModuleLaunchKernel with packet timestamps
+  // 0: hipModuleLaunchKernel between two hipEventRecord packets;
+  // 1: hipExtModuleLaunchKernel, start/stop timestamps on the dispatch packet;
+  // 2: diagnostic -- every run untimed (no events, no queue bound)
+  int launch_mode_ = 1;
   double run_ms_total_ = 0.0;
   uint64_t runs_total_ = 0;
   Module* last_module_ = nullptr;
@@ -563,16 +594,16 @@ __attribute__((visibility("default"))) int vx_hip_last_run(vx_device_h hdevice, 
                                                            uint32_t* grid, uint32_t* block) {
   if (hdevice == nullptr) return -1;
   auto* d = (vx_device*)hdevice;
-  d->run_totals(nullptr, nullptr);  // retires every queued run
+  d->run_totals(nullptr, nullptr, nullptr);  // retires every queued run
   if (ms) *ms = d->last_ms();
   if (grid) *grid = d->last_grid();
   if (block) *block = d->last_block();
   return 0;
 }
 __attribute__((visibility("default"))) int vx_hip_run_totals(vx_device_h hdevice, double* ms,
-                                                             uint64_t* runs) {
+                                                             uint64_t* timed, uint64_t* runs) {
   if (hdevice == nullptr) return -1;
-  ((vx_device*)hdevice)->run_totals(ms, runs);
+  ((vx_device*)hdevice)->run_totals(ms, timed, runs);
   return 0;
 }
 __attribute__((visibility("default"))) int vx_hip_mpm_rows(vx_device_h hdevice, uint32_t* rows,

@@ -95,7 +95,8 @@ def lib():
             "rt_render": [vp],
             "rt_render_stats": [vp, C.POINTER(Stats)],
             "rt_render_kernel_ms": [vp, C.POINTER(C.c_double)],
-            "rt_render_run_totals": [vp, C.POINTER(C.c_double), C.POINTER(C.c_uint64)],
+            "rt_render_run_totals": [vp, C.POINTER(C.c_double), C.POINTER(C.c_uint64),
+                                     C.POINTER(C.c_uint64)],
             "rt_read_framebuffer": [vp, vp, u64],
             "rt_read_depthbuffer": [vp, vp, u64],
             "rt_launch_rows": [vp, vp, u64, C.POINTER(u64)],
@@ -256,11 +257,12 @@ class Renderer:
         return ms.value
 
     def run_totals(self):
-        """(summed kernel ms, launches) since the device opened; waits for
-        every queued frame first."""
-        ms, n = C.c_double(), C.c_uint64()
-        _check(lib().rt_render_run_totals(self._h, C.byref(ms), C.byref(n)), "rt_render_run_totals")
-        return ms.value, n.value
+        """(summed kernel ms of the timed launches, timed launches, all
+        launches) since the device opened; waits for every queued frame."""
+        ms, nt, n = C.c_double(), C.c_uint64(), C.c_uint64()
+        _check(lib().rt_render_run_totals(self._h, C.byref(ms), C.byref(nt), C.byref(n)),
+               "rt_render_run_totals")
+        return ms.value, nt.value, n.value
 
     def framebuffer(self) -> np.ndarray:
         p = self.params

@@ -221,12 +221,12 @@ def test_queued_frames_equal_synchronous_frames(path):
     r.configure(512, 512, shadows=True, path=path)
     r.render()
     ref = r.framebuffer()
-    ms0, n0 = r.run_totals()
+    ms0, nt0, n0 = r.run_totals()
     for _ in range(7):
         r.start()
     r.wait()
-    ms1, n1 = r.run_totals()
-    assert n1 - n0 == 7 and ms1 > ms0
+    ms1, nt1, n1 = r.run_totals()
+    assert n1 - n0 == 7 and nt1 > nt0 and ms1 > ms0
     assert np.array_equal(r.framebuffer(), ref)
     assert r.stats()["primary_rays"] == 512 * 512
 
