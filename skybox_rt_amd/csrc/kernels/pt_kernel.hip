@@ -498,7 +498,11 @@ __device__ __forceinline__ void flush(int slot, uint32_t v) { vx_mpm_add(RT_MPM_
 
 }  // namespace
 
+#ifdef PT_WAVES_PER_EU
+VX_MAIN_OCC(rt_kernel_arg_t, arg, PT_BLOCK, PT_WAVES_PER_EU) {
+#else
 VX_MAIN(rt_kernel_arg_t, arg, PT_BLOCK) {
+#endif
   __shared__ PtLds s_pt;
   Counters cnt;
   Scene S = load_scene(arg);
