@@ -33,6 +33,7 @@ NODE_BYTES, TRI_BYTES, PIXEL_BYTES = 64, 36, 4
 MT_FLOPS = 40          # fp32 ops per Moller-Trumbore test
 FP32_VALU_TFLOPS = 157.3  # MI355X_MICROARCH.md: peak FP32 (vector)
 NODE4_BYTES = 112      # BVH4 node: 6 SoA box float4 + the child-ref float4 (pad not read)
+NODE4H_BYTES = 64      # BVH4 node with binary16 planes (rt_node4h_t): 48 B of planes + 16 B refs
 
 
 def log(*a):
@@ -40,7 +41,7 @@ def log(*a):
 
 
 def algorithmic_bytes(st: dict, pixels: int, node_bytes: int = NODE_BYTES) -> int:
-    """node bytes (64 B BVH2, 112 B BVH4) x nodes visited + 36 B x triangles tested
+    """node bytes (64 B BVH2, 112 B BVH4, 64 B binary16 BVH4) x nodes visited + 36 B x triangles tested
     (BVH leaves and screen layers) + texel bytes per shaded pixel + 4 B per
     pixel written.  Counts come from the instrumented kernel variant, whose
     counters tests/test_gpu_rt.py checks equal to the oracle's traversal."""
@@ -163,8 +164,9 @@ def main():
     r.render()
     inst = r.stats()
     pixels_local = inst["primary_rays"]
-    bvh_kind = "BVH4" if r.bvh4 else "BVH2"
-    alg_bytes = algorithmic_bytes(inst, pixels_local, NODE4_BYTES if r.bvh4 else NODE_BYTES)
+    bvh_kind = ("BVH4 (binary16 boxes)" if r.bvh4_f16 else "BVH4") if r.bvh4 else "BVH2"
+    alg_bytes = algorithmic_bytes(inst, pixels_local, (NODE4H_BYTES if r.bvh4_f16 else NODE4_BYTES)
+                                  if r.bvh4 else NODE_BYTES)
 
     r.configure(side, side, shadows=shadows, light=light, shard_index=rank, shard_count=n_gpus,
                 path=path, bounces=args.bounces, flat=flat, compact=use_gather)

@@ -27,6 +27,7 @@ typedef struct {
   uint32_t num_drawcalls, num_prims, num_geometry, num_layer, num_textures;
   uint32_t bvh_nodes, bvh_tris, bvh_leaves, bvh_depth;
   uint32_t bvh4_nodes, bvh4_depth, bvh4_stack;  /* the 4-wide BVH collapsed from it */
+  uint32_t bvh4_f16;  /* 1: BVH4 boxes rounded outward to binary16, the kernel reads 64-B nodes */
   double parse_ms, bvh_ms;
 } rt_scene_info_t;
 

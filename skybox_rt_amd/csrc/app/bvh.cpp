@@ -10,6 +10,54 @@
 namespace rt {
 namespace {
 
+// --- binary16 box planes (rt_node4h_t) ------------------------------------
+// The nearest binary16-representable value below (dir < 0) or above
+// (dir > 0) x, as a float: x scaled by the binary16 quantum of its binade is
+// an exact float, floor/ceil of it is exact, and so is scaling back.  Beyond
+// the binary16 range a lower bound saturates to -/+65504 or -inf and an upper
+// bound to +/-65504 or +inf -- always outward, so a rounded box contains the
+// original one and the slab test (monotone in the planes under round-to-
+// nearest arithmetic) accepts every ray the unrounded box accepted.
+float HalfRound(float x, int dir) {
+  if (std::isnan(x) || std::isinf(x) || x == 0.0f) return x;
+  const float kMax = 65504.0f;
+  if (x > kMax) return dir < 0 ? kMax : INFINITY;
+  if (x < -kMax) return dir < 0 ? -INFINITY : -kMax;
+  int e;
+  std::frexp(std::fabs(x), &e);                     // |x| in [2^(e-1), 2^e)
+  const int q = std::max(e - 1, -14) - 10;          // quantum 2^q (subnormals: 2^-24)
+  const float m = std::ldexp(x, -q);                // exact
+  const float r = dir < 0 ? std::floor(m) : std::ceil(m);
+  const float v = std::ldexp(r, q);                 // exact (|r| <= 2048)
+  return v > kMax ? INFINITY : (v < -kMax ? -INFINITY : v);
+}
+
+// binary16 encoding of a float that is exactly representable in binary16
+uint16_t HalfBits(float v) {
+  uint32_t u;
+  std::memcpy(&u, &v, 4);
+  const uint16_t sign = (uint16_t)((u >> 16) & 0x8000u);
+  const float a = std::fabs(v);
+  if (a == 0.0f) return sign;
+  if (std::isinf(a)) return (uint16_t)(sign | 0x7c00u);
+  int e;
+  const float m = std::frexp(a, &e);               // a = m 2^e, m in [0.5, 1)
+  if (e - 1 >= -14)
+    return (uint16_t)(sign | ((uint32_t)(e - 1 + 15) << 10) |
+                      (uint32_t)std::ldexp(2.0f * m - 1.0f, 10));
+  return (uint16_t)(sign | (uint32_t)std::ldexp(a, 24));  // subnormal: a = f 2^-24
+}
+
+float HalfValue(uint16_t h) {
+  const int ex = (h >> 10) & 31, f = h & 1023;
+  float v;
+  if (ex == 31) v = f ? NAN : INFINITY;
+  else if (ex == 0) v = std::ldexp((float)f, -24);
+  else v = std::ldexp((float)(1024 + f), ex - 25);
+  return (h & 0x8000u) ? -v : v;
+}
+
+
 struct Box {
   float lo[3] = {INFINITY, INFINITY, INFINITY};
   float hi[3] = {-INFINITY, -INFINITY, -INFINITY};
@@ -300,6 +348,32 @@ int BuildBvh(const std::vector<BuildTri>& tris, Bvh* out, std::string* error) {
   Builder b(tris, out, bp);
   b.run();
   Collapser(out).run();
+  // binary16 box planes: round every BVH4 box outward (RT_BVH_F16=0 keeps
+  // the fp32 planes, rt_node4h_t is then not uploaded), pack rt_node4h_t and
+  // check that it decodes to exactly rt_node4_t's planes
+  if (const char* v = std::getenv("RT_BVH_F16")) bp.f16_boxes = std::atoi(v) != 0;
+  out->nodes4h.clear();
+  if (bp.f16_boxes) {
+    out->nodes4h.resize(out->nodes4.size());
+    for (size_t n = 0; n < out->nodes4.size(); ++n) {
+      rt_node4_t& o = out->nodes4[n];
+      rt_node4h_t& h = out->nodes4h[n];
+      for (int k = 0; k < 3; ++k)
+        for (int i = 0; i < 4; ++i) {
+          float& lo = o.v[8 * k + i];
+          float& hi = o.v[8 * k + 4 + i];
+          lo = HalfRound(lo, -1);
+          hi = HalfRound(hi, +1);
+          h.b[8 * k + i] = HalfBits(lo);
+          h.b[8 * k + 4 + i] = HalfBits(hi);
+          if (HalfValue(h.b[8 * k + i]) != lo || HalfValue(h.b[8 * k + 4 + i]) != hi) {
+            if (error) *error = "binary16 box packing mismatch";
+            return -1;
+          }
+        }
+      std::memcpy(h.child, &o.v[24], 16);
+    }
+  }
   if (out->depth > RT_STACK_DEEP) {
     if (error) *error = "BVH deeper than RT_STACK_DEEP";
     return -1;

@@ -26,8 +26,10 @@ struct Bvh {
   std::vector<rt_tri_t> tris;    // leaf order
   uint32_t depth = 0;            // internal levels on the deepest path
   uint32_t leaves = 0;
-  // BVH4 collapsed from `nodes` (same leaves and padded boxes); root = 0
+  // BVH4 collapsed from `nodes` (same leaves; the padded boxes rounded outward
+  // to binary16-representable values, see f16_boxes); root = 0
   std::vector<rt_node4_t> nodes4;
+  std::vector<rt_node4h_t> nodes4h;  // the same nodes, binary16 boxes (the kernel's form)
   uint32_t depth4 = 0;
   uint32_t stack4 = 0;           // worst-case traversal stack entries (near-first, BVH4)
 };
@@ -40,6 +42,7 @@ struct BvhParams {
   uint32_t leaf_size = kBvhLeafSize;   // max triangles per leaf (1..4)
   uint32_t bins = kBvhBins;            // SAH bins per axis (2..64)
   bool all_axes = false;               // SAH over x, y and w, not only the widest axis
+  bool f16_boxes = true;               // BVH4 boxes rounded outward to binary16 values
 };
 
 int BuildBvh(const std::vector<BuildTri>& tris, Bvh* out, std::string* error);

@@ -185,6 +185,7 @@ int rt_scene_info(rt_scene_h s, rt_scene_info_t* info) {
   info->bvh4_nodes = (uint32_t)s->bvh.nodes4.size();
   info->bvh4_depth = s->bvh.depth4;
   info->bvh4_stack = s->bvh.stack4;
+  info->bvh4_f16 = s->bvh.nodes4h.empty() ? 0u : 1u;
   info->parse_ms = s->parse_ms;
   info->bvh_ms = s->bvh_ms;
   return 0;
@@ -277,9 +278,17 @@ int rt_renderer_create(rt_scene_h s, const char* kernel_dir, rt_renderer_h* out)
   std::vector<rt_tri_t> tris(bvh.tris);
   tris.resize(tris.size() + 3);
   std::memset(tris.data() + bvh.tris.size(), 0, 3 * sizeof(rt_tri_t));
+  // BVH4: rt_node4_t array, then (binary16 boxes) the rt_node4h_t array
+  std::vector<uint8_t> nodes4(bvh.nodes4.size() * sizeof(rt_node4_t) +
+                              bvh.nodes4h.size() * sizeof(rt_node4h_t));
+  if (!bvh.nodes4.empty()) {
+    std::memcpy(nodes4.data(), bvh.nodes4.data(), bvh.nodes4.size() * sizeof(rt_node4_t));
+    if (!bvh.nodes4h.empty())
+      std::memcpy(nodes4.data() + bvh.nodes4.size() * sizeof(rt_node4_t), bvh.nodes4h.data(),
+                  bvh.nodes4h.size() * sizeof(rt_node4h_t));
+  }
   if (upload(r->dev, bvh.nodes.data(), bvh.nodes.size() * sizeof(rt_node_t), &r->nodes, &a.nodes_addr) ||
-      upload(r->dev, bvh.nodes4.data(), bvh.nodes4.size() * sizeof(rt_node4_t), &r->nodes4,
-             &a.nodes4_addr) ||
+      upload(r->dev, nodes4.data(), nodes4.size(), &r->nodes4, &a.nodes4_addr) ||
       upload(r->dev, tris.data(), tris.size() * sizeof(rt_tri_t), &r->tris, &a.tris_addr))
     return -1;
   a.num_nodes = (uint32_t)bvh.nodes.size();
@@ -483,7 +492,8 @@ int rt_renderer_configure(rt_renderer_h r, const rt_render_params_t* p) {
             ((p->flags & RT_RENDER_FLAT) ? RT_FLAG_FLAT : 0u) |
             (raster ? RT_FLAG_RASTER : 0u) |
             (s->tie_high ? RT_FLAG_TIE_HIGH : 0u) | (compact ? RT_FLAG_COMPACT : 0u) |
-            (use_bvh4 ? RT_FLAG_BVH4 : 0u);
+            (use_bvh4 ? RT_FLAG_BVH4 : 0u) |
+            (use_bvh4 && !s->bvh.nodes4h.empty() ? RT_FLAG_BVH4H : 0u);
   a.bounces = p->bounces;
   a.seed = p->seed;
   a.clear_color = p->clear_color;

@@ -42,6 +42,7 @@
 #define RT_FLAG_FLAT     0x10u   // flat triangle list, no BVH (BASELINE config 2)
 #define RT_FLAG_RASTER   0x20u   // draw3d raster pipeline (raster_kernel.hip)
 #define RT_FLAG_BVH4     0x40u   // traverse the 4-wide BVH (nodes4) instead of the BVH2
+#define RT_FLAG_BVH4H    0x80u   // BVH4 node steps read the binary16 rt_node4h_t form
 
 #define RT_DC_DEPTH   0x1u
 #define RT_DC_COLOR   0x2u
@@ -70,6 +71,15 @@ typedef struct { float v[16]; } rt_node_t;
 // child refs as in rt_node_t (unused slots -1).  Collapsed from the BVH2
 // (bvh.cpp): same leaves, same padded boxes, half the levels.
 typedef struct { float v[32]; } rt_node4_t;
+
+// rt_node4h_t (BVH4, 64 B): the same node with its 24 box planes as IEEE
+// binary16 in rt_node4_t's order (lo.x[4], hi.x[4], lo.y[4], ...), then the
+// 4 child refs.  The host rounds every BVH4 box outward to binary16-
+// representable values (bvh.cpp RoundBoxes4), so rt_node4_t holds exactly the
+// values this form decodes to and both describe one tree.  The kernel reads
+// this form (4 loads of 16 B per node step instead of 7); it is uploaded right
+// behind the rt_node4_t array (nodes4_addr + 128 * num_nodes4).
+typedef struct { uint16_t b[24]; int32_t child[4]; } rt_node4h_t;
 
 // rt_tri_t: (v0.x, v0.y, v0.w, pid), (e1.xyw, 0), (e2.xyw, 0) -- clip (x,y,w)
 typedef struct { float v[12]; } rt_tri_t;

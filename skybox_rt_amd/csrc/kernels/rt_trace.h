@@ -49,7 +49,7 @@ struct Counters {
 struct Scene {
   vx_arena A;
   uint32_t nodes, nodes4, tris, layers, prims, dcs, cbuf, ptris, geom, order;
-  uint32_t num_nodes, num_layer, num_geom, flags, width, height;
+  uint32_t num_nodes, num_nodes4, num_layer, num_geom, flags, width, height;
   uint32_t shard_index, shard_count, tiles_x, clear_color, bounces, seed, split_tiles;
   float sx, sy, light[3];
   // the BVH staged in LDS by the workgroup (RT_LDS_SCENE images), or null
@@ -96,6 +96,7 @@ __device__ __forceinline__ Scene load_scene(const rt_kernel_arg_t* a) {
   s.seed = a->seed;
   s.split_tiles = a->split_tiles;
   s.num_nodes = a->num_nodes;
+  s.num_nodes4 = a->num_nodes4;
   s.num_layer = a->num_layer_tris;
   s.flags = a->flags;
   s.width = a->width;
@@ -259,16 +260,35 @@ struct LaneStack {
 // <, misses keyed +inf, hit keys clamped to FLT_MAX so they sort first); the
 // nearest is returned, the other hits are pushed farthest first.  Halves the
 // dependent load -> test -> branch steps of a root-to-leaf walk vs BVH2.
-template <bool SCALAR>
+template <bool SCALAR, bool F16>
 __device__ __forceinline__ int32_t node4_step(const Scene& S, uint32_t ref, const Ray& r,
                                               float tmin, float lim, LaneStack& st) {
-  const uint32_t no = S.nodes4 + 128u * ref;
   // SCALAR: every active lane is at this node -- one scalar-cache load per
   // record for the wave instead of 64 lanes of vector data return
   auto ld = [&](uint32_t o) { return SCALAR ? S.A.sld_f4(o) : S.A.ld_f4(o); };
-  const float4 lx = ld(no), hx = ld(no + 16), ly = ld(no + 32);
-  const float4 hy = ld(no + 48), lz = ld(no + 64), hz = ld(no + 80);
-  const float4 cf = ld(no + 96);
+  float4 lx, hx, ly, hy, lz, hz, cf;
+  if (F16) {
+    // binary16 planes: 3 + 1 loads of 16 B; the conversions are exact, so the
+    // planes equal rt_node4_t's (the host rounded those to binary16 values),
+    // and each folds into its slab FMA (v_fma_mix_f32: f16 operand, f32 math)
+    // -- the layout is a template parameter so no phi separates them
+    const uint32_t no = S.nodes4 + 128u * S.num_nodes4 + 64u * ref;
+    const float4 px = ld(no), py = ld(no + 16), pz = ld(no + 32);
+    cf = ld(no + 48);
+    auto h2 = [](float w, float& a, float& b) {
+      const uint32_t u = __float_as_uint(w);
+      a = (float)__builtin_bit_cast(_Float16, (uint16_t)(u & 0xffffu));
+      b = (float)__builtin_bit_cast(_Float16, (uint16_t)(u >> 16));
+    };
+    h2(px.x, lx.x, lx.y); h2(px.y, lx.z, lx.w); h2(px.z, hx.x, hx.y); h2(px.w, hx.z, hx.w);
+    h2(py.x, ly.x, ly.y); h2(py.y, ly.z, ly.w); h2(py.z, hy.x, hy.y); h2(py.w, hy.z, hy.w);
+    h2(pz.x, lz.x, lz.y); h2(pz.y, lz.z, lz.w); h2(pz.z, hz.x, hz.y); h2(pz.w, hz.z, hz.w);
+  } else {
+    const uint32_t no = S.nodes4 + 128u * ref;
+    lx = ld(no); hx = ld(no + 16); ly = ld(no + 32);
+    hy = ld(no + 48); lz = ld(no + 64); hz = ld(no + 80);
+    cf = ld(no + 96);
+  }
   const float alx[4] = {lx.x, lx.y, lx.z, lx.w}, ahx[4] = {hx.x, hx.y, hx.z, hx.w};
   const float aly[4] = {ly.x, ly.y, ly.z, ly.w}, ahy[4] = {hy.x, hy.y, hy.z, hy.w};
   const float alz[4] = {lz.x, lz.y, lz.z, lz.w}, ahz[4] = {hz.x, hz.y, hz.z, hz.w};
@@ -326,9 +346,12 @@ __device__ __forceinline__ int32_t trace_impl(const Scene& S, const Ray& r, floa
     ++cnt.visits;
 #endif
     const float lim = ANY ? tmax : bt;
+    if (S.flags & RT_FLAG_BVH4H)
+      return uni ? node4_step<true, true>(S, (uint32_t)r0, r, tmin, lim, lst)
+                 : node4_step<false, true>(S, (uint32_t)ref, r, tmin, lim, lst);
     if (S.flags & RT_FLAG_BVH4)
-      return uni ? node4_step<true>(S, (uint32_t)r0, r, tmin, lim, lst)
-                 : node4_step<false>(S, (uint32_t)ref, r, tmin, lim, lst);
+      return uni ? node4_step<true, false>(S, (uint32_t)r0, r, tmin, lim, lst)
+                 : node4_step<false, false>(S, (uint32_t)ref, r, tmin, lim, lst);
     NodeStep st;
     if (uni) {
       const uint32_t no = S.nodes + 64u * (uint32_t)r0;

@@ -36,7 +36,7 @@ class SceneInfo(C.Structure):
     _fields_ = [(n, C.c_uint32) for n in (
         "num_drawcalls", "num_prims", "num_geometry", "num_layer", "num_textures",
         "bvh_nodes", "bvh_tris", "bvh_leaves", "bvh_depth", "bvh4_nodes", "bvh4_depth",
-        "bvh4_stack")] + [
+        "bvh4_stack", "bvh4_f16")] + [
         ("parse_ms", C.c_double), ("bvh_ms", C.c_double)]
 
 
@@ -214,6 +214,8 @@ class Renderer:
         self.params = p
         self.bvh4 = (bvh_width != 2 and os.environ.get("RT_BVH_WIDTH", "4") != "2"
                      and not self.gpu_bvh)
+        # BVH4 node steps read 64-B binary16 nodes (rt_node4h_t) when the scene has them
+        self.bvh4_f16 = self.bvh4 and bool(self.scene.info()["bvh4_f16"])
 
     def build_bvh(self) -> dict:
         """Build the BVH on the device (kernels/bvh_build.hip) and trace over it
@@ -222,7 +224,7 @@ class Renderer:
         _check(lib().rt_renderer_build_bvh(self._h, C.byref(st)), "rt_renderer_build_bvh")
         self.gpu_bvh = True
         if self.params is not None:
-            self.bvh4 = False
+            self.bvh4 = self.bvh4_f16 = False
         return st.as_dict()
 
     def export_bvh(self):

@@ -147,6 +147,38 @@ def test_rt_instrumented_counters_equal_oracle_traversal(po, width):
         assert np.array_equal(fb, r.framebuffer())   # both variants render the same image
 
 
+def test_rt_fp32_bvh4_layout_equals_oracle(po, monkeypatch):
+    """RT_BVH_F16=0: unrounded BVH4 boxes in the 128-B fp32 node layout
+    (the kernel's other node4_step form) -- frame == brute-force oracle,
+    counters == the oracle's traversal of that tree, and the frame equals the
+    default binary16-node render."""
+    monkeypatch.setenv("RT_BVH_F16", "0")
+    s = rt.Scene.load(scene_path("tekkaman"))
+    assert s.info()["bvh4_f16"] == 0
+    r = rt.Renderer(s)
+    try:
+        for size in (256, 1024):
+            r.configure(size, size, shadows=True, instrumented=True)
+            assert r.bvh4 and not r.bvh4_f16
+            r.render()
+            st = r.stats()
+            fb = r.framebuffer()
+            c, _, _, k = po.rt_render(oracle_scene(po, "tekkaman"),
+                                      po.rt_params(size, size, shadows=True, nthreads=8),
+                                      bvh=s.bvh() + (s.bvh4(),))
+            assert np.array_equal(fb, c)
+            for key in ("node_visits", "tri_tests", "layer_tests", "shadow_rays", "occluded"):
+                assert st[key] == k[key], key
+            _, rd = renderer("tekkaman")
+            rd.configure(size, size, shadows=True)
+            assert rd.bvh4_f16
+            rd.render()
+            assert np.array_equal(fb, rd.framebuffer())
+    finally:
+        r.close()
+        s.close()
+
+
 @pytest.mark.parametrize("n", (8, 16, 32, 64, 128))
 def test_rt_triangle_matches_draw3d_golden(n):
     _, r = renderer("triangle")

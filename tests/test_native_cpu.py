@@ -210,6 +210,32 @@ def test_bvh4_collapse_structure(name):
     assert info["bvh4_stack"] <= 32
 
 
+@pytest.mark.parametrize("name", ["tekkaman", "scene", "box", "carnival"])
+def test_bvh4_binary16_boxes_are_outward(name, monkeypatch):
+    """rt_node4h_t (the kernel's 64-B node): every BVH4 box plane is a
+    binary16 value (so the kernel's exact f16->f32 conversion reproduces the
+    exported fp32 planes the oracle traverses), each rounded box contains the
+    unrounded one (RT_BVH_F16=0), and the tree is otherwise the same."""
+    s = rt.Scene.load(scene_path(name))
+    assert s.info()["bvh4_f16"] == 1
+    n16 = s.bvh4()
+    monkeypatch.setenv("RT_BVH_F16", "0")
+    s32 = rt.Scene.load(scene_path(name))
+    assert s32.info()["bvh4_f16"] == 0
+    n32 = s32.bvh4()
+    assert n16.shape == n32.shape
+    planes = n16[:, :24]
+    assert np.array_equal(planes.astype(np.float16).astype(np.float32), planes)
+    assert np.array_equal(n16[:, 24:].view(np.int32), n32[:, 24:].view(np.int32))
+    for k in range(3):
+        assert np.all(n16[:, 8 * k:8 * k + 4] <= n32[:, 8 * k:8 * k + 4])
+        assert np.all(n16[:, 8 * k + 4:8 * k + 8] >= n32[:, 8 * k + 4:8 * k + 8])
+        # outward by at most one binary16 quantum (2^-10 relative, 2^-24 absolute)
+        for sl in (slice(8 * k, 8 * k + 4), slice(8 * k + 4, 8 * k + 8)):
+            d = np.abs(n16[:, sl].astype(np.float64) - n32[:, sl])
+            assert np.all(d <= np.maximum(np.abs(n32[:, sl]) * 2.0 ** -10, 2.0 ** -24))
+
+
 @pytest.mark.parametrize("name,size,shadows,path", [
     ("tekkaman", 256, True, False), ("tekkaman", 1024, True, False), ("scene", 256, False, False),
     ("box", 128, True, False), ("carnival", 200, True, False), ("tekkaman", 128, False, True)])
