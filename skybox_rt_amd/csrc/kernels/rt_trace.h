@@ -27,6 +27,11 @@
 #ifndef RT_LEAF_BATCH
 #define RT_LEAF_BATCH 4
 #endif
+// 1: a leaf's loads are issued only for its own triangle slots (lanes of
+// shorter leaves masked off) instead of all 4 slots unconditionally
+#ifndef RT_LEAF_MASKED
+#define RT_LEAF_MASKED 0
+#endif
 // 1: while-while traversal loop (trace_impl, default: A/B r01_v9 -5.7 % for
 // primary+shadow, -3.4 % for the path tracer); 0: if-if (node step or leaf
 // per iteration)
@@ -439,10 +444,12 @@ __device__ __forceinline__ int32_t trace_impl(const Scene& S, const Ray& r, floa
           if (S.ltris) {
             const float4* tr = S.ltris + 3u * (first + k);
             ta[j] = tr[0]; tb[j] = tr[1]; tc[j] = tr[2];
-          } else {
+          } else if (!RT_LEAF_MASKED || k < count) {
             ta[j] = S.A.ld_f4(to + 48u * k);
             tb[j] = S.A.ld_f4(to + 48u * k + 16);
             tc[j] = S.A.ld_f4(to + 48u * k + 32);
+          } else {
+            ta[j] = tb[j] = tc[j] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
           }
         }
 #pragma unroll
