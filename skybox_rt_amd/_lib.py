@@ -27,7 +27,8 @@ REQUIRED = ("libvortex.so", "libvortex-hip.so", "librtapp.so", "rtapp",
             "pt_kernel_deep.vxbin", "pt_kernel_stats.vxbin", "pt_kernel_deep_stats.vxbin",
             "rt_flat.vxbin", "rt_flat_stats.vxbin", "raster_kernel.vxbin",
             "pt_compact/pt_kernel.vxbin", "pt_compact/pt_kernel_stats.vxbin",
-            "tex_kernel_f0.vxbin", "tex_kernel_f1.vxbin", "tex_kernel_f2.vxbin", "texapp", "bvh_build.vxbin")
+            "tex_kernel_f0.vxbin", "tex_kernel_f1.vxbin", "tex_kernel_f2.vxbin", "texapp", "bvh_build.vxbin",
+            "libframe_assemble.so")
 
 
 class NativeLibraryMissing(RuntimeError):

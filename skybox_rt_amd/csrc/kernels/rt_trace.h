@@ -692,11 +692,13 @@ __device__ __forceinline__ uint32_t shadowed(uint32_t c) {
 
 __device__ __forceinline__ void store_pixel(const Scene& S, uint32_t t, uint32_t x, uint32_t y,
                                             uint32_t color) {
-  // compact shard buffers stay in local-tile order whatever the work order
+  // compact shard buffers stay in local-tile order whatever the work order,
+  // each tile row-major (32 rows of 128 B), so the frame assembly on rank 0
+  // moves whole 128-B tile rows (runtime/frame_assemble.hip)
   uint32_t idx = y * S.width + x;
   if (S.flags & RT_FLAG_COMPACT) {
     const TaskPix m = task_map(S, t);
-    idx = (m.lt << 10) | m.idx;
+    idx = (m.lt << 10) | ((y & 31u) << 5) | (x & 31u);
   }
   S.A.st_u32(S.cbuf + 4u * idx, color);
 }

@@ -1,16 +1,20 @@
 """Multi-GPU frame sharding: 32x32 tiles dealt round-robin,
 tile t -> rank t % G (the reference's raster-unit striding,
 sim/simx/raster_unit.cpp:109-111, 224-227); every rank renders its tiles into
-a compact buffer in task order (the RT kernels' task_pixel mapping: tile,
-then 8x8 block, then lane); one gather to rank 0 -- over RCCL (backend
-"nccl") on the GPUs, gloo in the CPU tests -- and a de-interleave scatter
-there.  That gather is the only exchange of the path: the frame shards with
+a compact buffer of its local tiles (local tile lt = global tile
+rank + lt * G, each tile row-major: slot = lt * 1024 + 32 * (y % 32) + x % 32,
+the RT kernels' store_pixel); one gather to rank 0 -- over RCCL (backend
+"nccl") on the GPUs, gloo in the CPU tests -- and the frame assembly there
+(on the GPU the HIP kernel runtime/frame_assemble.hip behind
+include/rt_shard.h, on the CPU rehearsal a numpy/torch index gather).  That gather is the only exchange of the path: the frame shards with
 no data-path collective.
 
     g = FrameGather(dist, width, height, device)
     image = g(local)   # rank 0: int32[H*W] image, other ranks: None
 """
 from __future__ import annotations
+
+import ctypes
 
 import numpy as np
 
@@ -30,14 +34,14 @@ def local_tiles(width: int, height: int, rank: int, world: int) -> int:
 def task_pixel_index(width: int, height: int, rank: int, world: int) -> np.ndarray:
     """Image index (y * W + x) of every slot of rank's compact buffer, -1 for
     the slots of edge tiles that overhang the image.  Restates the kernels'
-    task_pixel (kernels/rt_trace.h)."""
+    store_pixel compact index (kernels/rt_trace.h)."""
     tx, _ = tiles_of(width, height)
     n = local_tiles(width, height, rank, world)
     t = np.arange(n * TILE * TILE, dtype=np.int64)
-    lt, blk, ln = t >> 10, (t >> 6) & 15, t & 63
+    lt, row, col = t >> 10, (t >> 5) & 31, t & 31
     gt = rank + lt * world
-    x = (gt % tx) * TILE + (blk & 3) * 8 + (ln & 7)
-    y = (gt // tx) * TILE + (blk >> 2) * 8 + (ln >> 3)
+    x = (gt % tx) * TILE + col
+    y = (gt // tx) * TILE + row
     return np.where((x < width) & (y < height), y * width + x, -1)
 
 
@@ -58,8 +62,9 @@ class FrameGather:
     frame there.  Buffers are padded to the largest rank's size so one
     dist.gather moves them, straight into views of one receive buffer (on
     RCCL a gather to one root is point-to-point sends to it, each peer over
-    its own xGMI link -- no ring all-gather); the frame is then ONE index
-    gather through a precomputed permutation (frame pixel i <- slot perm[i]).
+    its own xGMI link -- no ring all-gather); the frame is then assembled by
+    ONE HIP kernel (rt_frame_assemble: arithmetic tile -> rank mapping,
+    coalesced 128-B tile rows; 8 B of HBM traffic per pixel, no index array).
 
     Synchronous:  image = g(local)
     Pipelined:    g.start(slot[, stream]) after filling g.locals[slot] --
@@ -93,17 +98,35 @@ class FrameGather:
                           for _ in range(slots)]
             self.parts_s = [list(r.split(self.max_local)) for r in self.recvs]
             self.recv, self.parts = self.recvs[0], self.parts_s[0]
-            perm = np.empty(width * height, np.int64)
-            for r in range(self.world):
-                idx = task_pixel_index(width, height, r, self.world)
-                ok = np.nonzero(idx >= 0)[0]
-                perm[idx[ok]] = ok + r * self.max_local
-            self.perm = torch.from_numpy(perm).to(device)
             self.image = torch.zeros(width * height, dtype=torch.int32, device=device)
+            if self.cuda:
+                # the HIP assembly kernel (include/rt_shard.h); no torch fallback
+                from . import _lib
+                self._asm = _lib.load("libframe_assemble.so").rt_frame_assemble
+                self._asm.restype = ctypes.c_int
+                self._asm.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32,
+                                      ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint64,
+                                      ctypes.c_void_p]
+            else:
+                # host-staged rehearsal (gloo): one index gather through the
+                # permutation frame pixel i <- slot perm[i]
+                perm = np.empty(width * height, np.int64)
+                for r in range(self.world):
+                    idx = task_pixel_index(width, height, r, self.world)
+                    ok = np.nonzero(idx >= 0)[0]
+                    perm[idx[ok]] = ok + r * self.max_local
+                self.perm = torch.from_numpy(perm)
 
     def _assemble(self, slot: int = 0):
         import torch
-        torch.index_select(self.recvs[slot], 0, self.perm, out=self.image)
+        if self.cuda:
+            rc = self._asm(self.image.data_ptr(), self.recvs[slot].data_ptr(), self.width,
+                           self.height, self.world, self.max_local,
+                           torch.cuda.current_stream(self.device).cuda_stream)
+            if rc != 0:
+                raise RuntimeError(f"rt_frame_assemble failed ({rc})")
+        else:
+            torch.index_select(self.recvs[slot], 0, self.perm, out=self.image)
 
     def __call__(self, local=None):
         """local: this rank's compact buffer (int32 tensor); None = use

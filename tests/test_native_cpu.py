@@ -35,11 +35,12 @@ def native_built():
 
 
 @pytest.mark.parametrize("header,lib", [("vortex.h", "libvortex.so"), ("vx_rt.h", "librtapp.so"),
-                                        ("vx_tex.h", "librtapp.so")])
+                                        ("vx_tex.h", "librtapp.so"),
+                                        ("rt_shard.h", "libframe_assemble.so")])
 def test_c_abi_exports_every_declared_symbol(header, lib):
     h = C.CDLL(os.path.join(_lib.LIB_DIR, lib))
     names = _declared(header)
-    assert len(names) >= {"vortex.h": 22, "vx_rt.h": 15, "vx_tex.h": 7}[header]
+    assert len(names) >= {"vortex.h": 22, "vx_rt.h": 15, "vx_tex.h": 7, "rt_shard.h": 1}[header]
     for n in names:
         assert hasattr(h, n), f"{lib} does not export {n} declared in include/{header}"
 
