@@ -110,11 +110,20 @@ int rt_read_depthbuffer(rt_renderer_h r, uint32_t* out, uint64_t count);
  * the scene's triangles and make it this renderer's tree (binary traversal;
  * a configured renderer is reconfigured).  Stats optional. */
 typedef struct {
-  uint32_t nodes, depth, launches, pad;
+  uint32_t nodes, depth, launches;
+  uint32_t stack4;      /* worst-case stack of the device BVH4 collapse (traversed by the
+                           RT/PT kernels), RT_BVH_STACK4_UNUSED if it exceeds the deep
+                           images' stack and the BVH2 is traversed instead */
   double build_ms;      /* host wall time of the whole build (upload + launches) */
   double kernel_ms;     /* sum of the build kernels' HIP-event times */
 } rt_bvh_build_stats_t;
 int rt_renderer_build_bvh(rt_renderer_h r, rt_bvh_build_stats_t* stats);
+#define RT_BVH_STACK4_UNUSED 0xFFFFFFFFu
+/* the renderer's current BVH4 (float[num_nodes4][32], rt_node4_t: the host
+ * tree's collapse, or after rt_renderer_build_bvh the device collapse --
+ * BVH4 node i at the BVH2 index of every even-depth internal node, zeros
+ * elsewhere).  NO REFERENCE. */
+int rt_renderer_export_bvh4(rt_renderer_h r, float* nodes4, uint32_t* num_nodes4);
 /* the renderer's current BVH (float[num_nodes][16], float[num_tris][12]) */
 int rt_renderer_export_bvh(rt_renderer_h r, float* nodes, float* tris, uint32_t* num_nodes,
                            uint32_t* num_tris);

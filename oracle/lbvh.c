@@ -213,3 +213,74 @@ int orc_lbvh_build(const float* verts, const float* geom, uint32_t n_, float* no
   free(range);
   return 0;
 }
+
+/* ---- BVH4 collapse (bvh_build.hip phase_collapse) --------------------------
+ * Restated top-down: a DFS from the root over internal refs carries each
+ * node's depth and the stack its BVH4 ancestors have pushed; the device
+ * decides per node by walking parent links instead -- same nodes, same slots,
+ * same bound. */
+static int ref_of(const float* nd, int ch) {
+  int32_t r;
+  memcpy(&r, &nd[12 + ch], 4);
+  return r;
+}
+
+static int collapse_slots(const float* nodes, int i, float* o) {
+  int cnt = 0;
+  const float* nd = nodes + 16 * (size_t)i;
+  for (int ch = 0; ch < 2; ++ch) {
+    const int32_t r = ref_of(nd, ch);
+    if (r == EMPTY_REF) continue;
+    const float* src = nd;
+    int g0 = ch, g1 = ch;
+    if (r >= 0) { src = nodes + 16 * (size_t)r; g0 = 0; g1 = 1; }
+    for (int g = g0; g <= g1; ++g) {
+      const int32_t rr = ref_of(src, g);
+      if (rr == EMPTY_REF) continue;
+      if (o) {
+        for (int k = 0; k < 3; ++k) {
+          o[8 * k + cnt] = src[4 * k + 2 * g];
+          o[8 * k + 4 + cnt] = src[4 * k + 2 * g + 1];
+        }
+        memcpy(&o[24 + cnt], &rr, 4);
+      }
+      ++cnt;
+    }
+  }
+  return cnt;
+}
+
+int orc_lbvh_collapse4(const float* nodes, uint32_t nn, float* nodes4, uint32_t* stack_out) {
+  if (nn == 0) return -1;
+  memset(nodes4, 0, sizeof(float) * 32 * (size_t)nn);
+  /* explicit DFS stack: (node, depth, pushes of the BVH4 ancestors) */
+  int* st = (int*)malloc(sizeof(int) * 3 * (size_t)(nn + 1));
+  if (!st) return -2;
+  int sp = 0;
+  uint32_t worst = 0;
+  st[0] = 0; st[1] = 0; st[2] = 0; sp = 1;
+  while (sp) {
+    --sp;
+    const int i = st[3 * sp], d = st[3 * sp + 1], acc = st[3 * sp + 2];
+    int acc2 = acc;
+    if ((d & 1) == 0) {
+      float* o = nodes4 + 32 * (size_t)i;
+      const int32_t e = EMPTY_REF;
+      for (int q = 0; q < 4; ++q) memcpy(&o[24 + q], &e, 4);
+      const int cnt = collapse_slots(nodes, i, o);
+      acc2 = acc + (cnt > 0 ? cnt - 1 : 0);
+      if ((uint32_t)acc2 > worst) worst = (uint32_t)acc2;
+    }
+    const float* nd = nodes + 16 * (size_t)i;
+    for (int ch = 0; ch < 2; ++ch) {
+      const int32_t r = ref_of(nd, ch);
+      if (r >= 0 && (uint32_t)r < nn) {
+        st[3 * sp] = r; st[3 * sp + 1] = d + 1; st[3 * sp + 2] = acc2;
+        ++sp;
+      }
+    }
+  }
+  free(st);
+  *stack_out = worst;
+  return 0;
+}

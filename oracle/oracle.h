@@ -141,6 +141,12 @@ int orc_mt(const float o[3], const float d[3], const float v0[3],
  * triangles; out: nodes [max(n-1,1)][16], tris [n+3][12], depth. */
 int orc_lbvh_build(const float* verts, const float* geom, uint32_t n, float* nodes, float* tris,
                    uint32_t* depth);
+/* BVH4 collapse of an LBVH node array (bvh_build.hip phase_collapse): every
+ * reachable internal node at even depth becomes a BVH4 node at its own index
+ * with its internal (odd-depth) children replaced by their children; nodes:
+ * [nn][16] rt_node_t, out nodes4 [nn][32] rt_node4_t (zeros elsewhere) and
+ * the worst-case near-first traversal stack. */
+int orc_lbvh_collapse4(const float* nodes, uint32_t nn, float* nodes4, uint32_t* stack);
 
 /* ---- texture regression app (tests/regression/tex; oracle/tex.c) ------ */
 /* LoadImage format conversion of one A8R8G8B8 pixel (VX_TEX_FORMAT_*) */

@@ -95,6 +95,8 @@ def lib():
         _lib.orc_mt.argtypes = [C.c_void_p] * 5 + [C.c_float, C.POINTER(C.c_float)]
         _lib.orc_lbvh_build.argtypes = [C.c_void_p, C.c_void_p, C.c_uint32, C.c_void_p, C.c_void_p,
                                         C.POINTER(C.c_uint32)]
+        _lib.orc_lbvh_collapse4.argtypes = [C.c_void_p, C.c_uint32, C.c_void_p,
+                                            C.POINTER(C.c_uint32)]
         _lib.orc_tex_encode.argtypes = [C.c_uint32, C.c_uint32]
         _lib.orc_tex_encode.restype = C.c_uint32
         _lib.orc_tex_build.argtypes = [C.c_void_p, C.c_uint32, C.c_uint32, C.c_uint32, C.c_void_p,
@@ -289,3 +291,16 @@ def lbvh_build(verts: np.ndarray, geom: np.ndarray):
     if rc != 0:
         raise RuntimeError(f"orc_lbvh_build failed: {rc}")
     return nodes, tris[:n], depth.value
+
+
+def lbvh_collapse4(nodes: np.ndarray):
+    """BVH4 collapse of an LBVH node array (oracle/lbvh.c) -> (nodes4
+    float32[nn, 32], worst-case traversal stack)."""
+    nodes = np.ascontiguousarray(nodes, np.float32)
+    nn = nodes.shape[0]
+    nodes4 = np.zeros((nn, 32), np.float32)
+    stack = C.c_uint32()
+    rc = lib().orc_lbvh_collapse4(nodes.ctypes.data, nn, nodes4.ctypes.data, C.byref(stack))
+    if rc != 0:
+        raise RuntimeError(f"orc_lbvh_collapse4 failed: {rc}")
+    return nodes4, stack.value

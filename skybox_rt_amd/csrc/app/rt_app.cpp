@@ -93,6 +93,7 @@ struct rt_renderer {
   std::string kdir;         // kernel directory (images missing there come from lib_dir)
   bool deep = false;        // RT/PT images with the 32-entry traversal stack
   bool gpu_bvh = false;     // nodes/tris were built on the device (rt_renderer_build_bvh)
+  bool gpu_bvh4 = false;    // ... and collapsed to a BVH4 there whose stack fits the images
   uint32_t num_tris = 0;    // leaf triangle records (without the 3 padding records)
 
   ~rt_renderer() {
@@ -485,7 +486,7 @@ int rt_renderer_configure(rt_renderer_h r, const rt_render_params_t* p) {
     a.split_tiles = heavy;
     a.num_tasks += heavy * RT_TILE_PIXELS;
   }
-  bool use_bvh4 = !(p->flags & RT_RENDER_BVH2) && !r->gpu_bvh;
+  bool use_bvh4 = !(p->flags & RT_RENDER_BVH2) && (!r->gpu_bvh || r->gpu_bvh4);
   if (const char* e = std::getenv("RT_BVH_WIDTH")) use_bvh4 = use_bvh4 && std::atoi(e) != 2;
   a.flags = ((p->flags & RT_RENDER_SHADOWS) ? RT_FLAG_SHADOWS : 0u) |
             ((p->flags & RT_RENDER_PATH) ? RT_FLAG_PATH : 0u) |
@@ -493,7 +494,7 @@ int rt_renderer_configure(rt_renderer_h r, const rt_render_params_t* p) {
             (raster ? RT_FLAG_RASTER : 0u) |
             (s->tie_high ? RT_FLAG_TIE_HIGH : 0u) | (compact ? RT_FLAG_COMPACT : 0u) |
             (use_bvh4 ? RT_FLAG_BVH4 : 0u) |
-            (use_bvh4 && !s->bvh.nodes4h.empty() ? RT_FLAG_BVH4H : 0u);
+            (use_bvh4 && !r->gpu_bvh && !s->bvh.nodes4h.empty() ? RT_FLAG_BVH4H : 0u);
   a.bounces = p->bounces;
   a.seed = p->seed;
   a.clear_color = p->clear_color;
@@ -662,10 +663,10 @@ int rt_renderer_build_bvh(rt_renderer_h r, rt_bvh_build_stats_t* st) {
     }
   }
   const uint32_t nblocks = (n + BVHB_ITEMS - 1) / BVHB_ITEMS;
-  const uint32_t bounds_init[8] = {~0u, ~0u, ~0u, 0, 0, 0, 0, 0};
+  const uint32_t bounds_init[10] = {~0u, ~0u, ~0u, 0, 0, 0, 0, 0, 0, 0};
   DevBuf vb, cen, keys[2], vals[2], hist, bounds, parent, flags, boxes, range, child, argb;
-  vx_buffer_h nodes_h = nullptr, tris_h = nullptr;
-  uint64_t nodes_addr = 0, tris_addr = 0;
+  vx_buffer_h nodes_h = nullptr, tris_h = nullptr, nodes4_h = nullptr;
+  uint64_t nodes_addr = 0, tris_addr = 0, nodes4_addr = 0;
   const uint32_t nn = n > 1 ? n - 1 : 1;
   if (alloc_buf(r->dev, verts.size() * 4, &vb, verts.data()) ||
       alloc_buf(r->dev, (uint64_t)n * 16, &cen) || alloc_buf(r->dev, (uint64_t)n * 4, &keys[0]) ||
@@ -678,14 +679,17 @@ int rt_renderer_build_bvh(rt_renderer_h r, rt_bvh_build_stats_t* st) {
       alloc_buf(r->dev, (uint64_t)n * 8, &child) ||
       alloc_buf(r->dev, sizeof(bvh_build_arg_t), &argb) ||
       upload(r->dev, nullptr, (uint64_t)nn * sizeof(rt_node_t), &nodes_h, &nodes_addr) ||
-      upload(r->dev, nullptr, (uint64_t)(n + 3) * sizeof(rt_tri_t), &tris_h, &tris_addr)) {
+      upload(r->dev, nullptr, (uint64_t)(n + 3) * sizeof(rt_tri_t), &tris_h, &tris_addr) ||
+      upload(r->dev, nullptr, (uint64_t)nn * sizeof(rt_node4_t), &nodes4_h, &nodes4_addr)) {
     if (nodes_h) vx_mem_free(nodes_h);
     if (tris_h) vx_mem_free(tris_h);
+    if (nodes4_h) vx_mem_free(nodes4_h);
     return -1;
   }
-  DevBuf nodes_out, tris_out;  // owned here until handed to the renderer
+  DevBuf nodes_out, tris_out, nodes4_out;  // owned here until handed to the renderer
   nodes_out.h = nodes_h;
   tris_out.h = tris_h;
+  nodes4_out.h = nodes4_h;
   bvh_build_arg_t a;
   std::memset(&a, 0, sizeof(a));
   a.verts_addr = vb.addr;
@@ -704,6 +708,7 @@ int rt_renderer_build_bvh(rt_renderer_h r, rt_bvh_build_stats_t* st) {
   a.child_addr = child.addr;
   a.nodes_addr = nodes_addr;
   a.tris_addr = tris_addr;
+  a.nodes4_addr = nodes4_addr;
   a.n = n;
   a.nblocks = nblocks;
   double kernel_ms = 0.0;
@@ -723,13 +728,18 @@ int rt_renderer_build_bvh(rt_renderer_h r, rt_bvh_build_stats_t* st) {
   if (launch(BVHB_BOUNDS, 0) || launch(BVHB_MORTON, 0)) return -1;
   for (uint32_t pass = 0; pass < 4; ++pass)  // 30-bit codes: 4 passes of 8 bits
     if (launch(BVHB_HIST, pass) || launch(BVHB_SCAN, pass) || launch(BVHB_SCATTER, pass)) return -1;
-  if (launch(BVHB_TREE, 0) || launch(BVHB_BOXES, 0) || launch(BVHB_EMIT, 0)) return -1;
-  uint32_t bres[8];
+  if (launch(BVHB_TREE, 0) || launch(BVHB_BOXES, 0) || launch(BVHB_EMIT, 0) ||
+      launch(BVHB_COLLAPSE, 0))
+    return -1;
+  uint32_t bres[10];
   if (vx_copy_from_dev(bres, bounds.h, 0, sizeof(bres)) != 0) return fail("vx_copy_from_dev failed");
-  const uint32_t depth = bres[7];
+  const uint32_t depth = bres[7], stack4 = bres[8];
   if (depth == 0 || depth > RT_STACK_DEEP) return fail("GPU BVH deeper than the traversal stack");
+  // the device BVH4 is traversed when its worst-case stack fits the deep
+  // images (else the BVH2, whose depth bound was just checked)
+  const bool use4 = stack4 <= RT_STACK_DEEP;
   // traversal images with a stack deep enough for this tree
-  if (depth > RT_STACK_SHALLOW && !r->deep) {
+  if (std::max(depth, use4 ? stack4 : 0u) > RT_STACK_SHALLOW && !r->deep) {
     if (load_image(r, "rt_kernel_deep.vxbin", &r->krnl[0][0]) ||
         load_image(r, "rt_kernel_deep_stats.vxbin", &r->krnl[0][1]) ||
         load_image(r, "pt_kernel_deep.vxbin", &r->krnl[1][0]) ||
@@ -739,18 +749,24 @@ int rt_renderer_build_bvh(rt_renderer_h r, rt_bvh_build_stats_t* st) {
   }
   if (r->nodes) vx_mem_free(r->nodes);
   if (r->tris) vx_mem_free(r->tris);
+  if (r->nodes4) vx_mem_free(r->nodes4);
   r->nodes = nodes_out.h;
   r->tris = tris_out.h;
-  nodes_out.h = tris_out.h = nullptr;
+  r->nodes4 = nodes4_out.h;
+  nodes_out.h = tris_out.h = nodes4_out.h = nullptr;
   r->arg.nodes_addr = nodes_addr;
   r->arg.tris_addr = tris_addr;
   r->arg.num_nodes = nn;
+  r->arg.nodes4_addr = nodes4_addr;
+  r->arg.num_nodes4 = nn;
   r->num_tris = n;
   r->gpu_bvh = true;
+  r->gpu_bvh4 = use4;
   if (st) {
     std::memset(st, 0, sizeof(*st));
     st->nodes = nn;
     st->depth = depth;
+    st->stack4 = use4 ? stack4 : RT_BVH_STACK4_UNUSED;
     st->launches = launches;
     st->kernel_ms = kernel_ms;
     st->build_ms = ms_since(t0);
@@ -760,6 +776,17 @@ int rt_renderer_build_bvh(rt_renderer_h r, rt_bvh_build_stats_t* st) {
     const rt_render_params_t p = r->params;
     return rt_renderer_configure(r, &p);
   }
+  return 0;
+}
+
+int rt_renderer_export_bvh4(rt_renderer_h r, float* nodes4, uint32_t* num_nodes4) {
+  if (!r) return fail("null argument");
+  if (num_nodes4) *num_nodes4 = r->arg.num_nodes4;
+  // the fp32 rt_node4_t records (a host tree's buffer carries its binary16
+  // copy behind them)
+  if (nodes4 && r->arg.num_nodes4 &&
+      vx_copy_from_dev(nodes4, r->nodes4, 0, (uint64_t)r->arg.num_nodes4 * sizeof(rt_node4_t)) != 0)
+    return fail("vx_copy_from_dev failed");
   return 0;
 }
 

@@ -431,6 +431,95 @@ __device__ void phase_emit(const bvh_build_arg_t* a) {
   if (lane() == 0 && maxdepth) atomicMax(&bounds[7], maxdepth);
 }
 
+// BVH4 collapse of the emitted BVH2 (bvh_build.hip's own rule, restated by
+// oracle/lbvh.c orc_lbvh_collapse4): every reachable internal node at even
+// depth (root = 0) becomes a BVH4 node at its own index, its children being
+// its BVH2 children with each internal child (odd depth) replaced by that
+// child's two children -- slots in order, leaves and even-depth nodes kept as
+// refs, boxes copied from the emitted rt_node_t records (already padded).
+// No allocation or ordering pass: every node decides alone.  Also the
+// worst-case traversal stack (near-first BVH4 pushes slots - 1 per node):
+// the max over nodes of the sum of (slots - 1) over its BVH4 ancestors and
+// itself, into bounds[8].
+struct Slots4 {
+  int count;
+  int32_t ref[4];
+  float lo[4][3], hi[4][3];
+};
+
+__device__ __forceinline__ Slots4 slots4_of(const rt_node_t* nodes, int i) {
+  Slots4 s;
+  s.count = 0;
+  const float* nd = nodes[i].v;
+  for (int ch = 0; ch < 2; ++ch) {
+    const int32_t r = __float_as_int(nd[12 + ch]);
+    if (r == RT_EMPTY_REF) continue;
+    if (r < 0) {
+      for (int k = 0; k < 3; ++k) {
+        s.lo[s.count][k] = nd[4 * k + 2 * ch];
+        s.hi[s.count][k] = nd[4 * k + 2 * ch + 1];
+      }
+      s.ref[s.count++] = r;
+      continue;
+    }
+    const float* cd = nodes[r].v;
+    for (int g = 0; g < 2; ++g) {
+      const int32_t r2 = __float_as_int(cd[12 + g]);
+      if (r2 == RT_EMPTY_REF) continue;
+      for (int k = 0; k < 3; ++k) {
+        s.lo[s.count][k] = cd[4 * k + 2 * g];
+        s.hi[s.count][k] = cd[4 * k + 2 * g + 1];
+      }
+      s.ref[s.count++] = r2;
+    }
+  }
+  return s;
+}
+
+__device__ void phase_collapse(const bvh_build_arg_t* a) {
+  const int32_t* parent = vx_ptr<const int32_t>(a->parent_addr);
+  const uint32_t* range = vx_ptr<const uint32_t>(a->range_addr);
+  const rt_node_t* nodes = vx_ptr<const rt_node_t>(a->nodes_addr);
+  rt_node4_t* nodes4 = vx_ptr<rt_node4_t>(a->nodes4_addr);
+  uint32_t* bounds = vx_ptr<uint32_t>(a->bounds_addr);
+  const int n = (int)a->n, nn = n > 1 ? n - 1 : 1;
+  const int gid = blockIdx.x * BVHB_BLOCK + threadIdx.x, gstride = gridDim.x * BVHB_BLOCK;
+  uint32_t maxstack = 0;
+  for (int i = gid; i < nn; i += gstride) {
+    float* o = nodes4[i].v;
+    for (int q = 0; q < 32; ++q) o[q] = 0.0f;
+    const bool reach = i == 0 || (n > BVHB_LEAF_MAX && range[2 * i + 1] - range[2 * i] + 1 > BVHB_LEAF_MAX);
+    if (!reach) continue;
+    int depth = 0;
+    if (n > BVHB_LEAF_MAX)
+      for (int p = i; p != 0; p = parent[p]) ++depth;
+    if (depth & 1) continue;
+    const Slots4 s = slots4_of(nodes, i);
+    for (int q = 0; q < 4; ++q) {
+      const bool used = q < s.count;
+      for (int k = 0; k < 3; ++k) {
+        o[8 * k + q] = used ? s.lo[q][k] : 0.0f;
+        o[8 * k + 4 + q] = used ? s.hi[q][k] : 0.0f;
+      }
+      o[24 + q] = __int_as_float(used ? s.ref[q] : RT_EMPTY_REF);
+    }
+    uint32_t st = (uint32_t)(s.count > 0 ? s.count - 1 : 0);
+    if (n > BVHB_LEAF_MAX)
+      for (int p = i; p != 0;) {
+        p = parent[parent[p]];  // the BVH4 parent (two BVH2 levels up)
+        const int c = slots4_of(nodes, p).count;
+        st += (uint32_t)(c > 0 ? c - 1 : 0);
+      }
+    maxstack = st > maxstack ? st : maxstack;
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const uint32_t y = (uint32_t)__shfl_xor((int)maxstack, o, 64);
+    maxstack = y > maxstack ? y : maxstack;
+  }
+  if (lane() == 0 && maxstack) atomicMax(&bounds[8], maxstack);
+}
+
 }  // namespace
 
 VX_MAIN(bvh_build_arg_t, arg, BVHB_BLOCK) {
@@ -442,6 +531,7 @@ VX_MAIN(bvh_build_arg_t, arg, BVHB_BLOCK) {
     case BVHB_SCATTER: phase_scatter(arg); break;
     case BVHB_TREE: phase_tree(arg); break;
     case BVHB_BOXES: phase_boxes(arg); break;
+    case BVHB_COLLAPSE: phase_collapse(arg); break;
     default: phase_emit(arg); break;
   }
   return 0;

@@ -23,6 +23,7 @@ enum {
   BVHB_TREE = 5,     // binary radix tree (internal nodes: ranges, children, parents)
   BVHB_BOXES = 6,    // bottom-up boxes (agent-scope counters, no spinning)
   BVHB_EMIT = 7,     // rt_node_t / rt_tri_t records, depth
+  BVHB_COLLAPSE = 8, // rt_node4_t: every even-depth node absorbs its internal children
 };
 
 typedef struct {
@@ -32,7 +33,8 @@ typedef struct {
   uint64_t keys_addr[2];  // u32 [n] Morton codes (ping-pong)
   uint64_t vals_addr[2];  // u32 [n] triangle indices
   uint64_t hist_addr;     // u32 [256][nblocks]
-  uint64_t bounds_addr;   // u32 [8]: ordered-uint min xyz, max xyz, max |coord|, depth
+  uint64_t bounds_addr;   // u32 [10]: ordered-uint min xyz, max xyz, max |coord|, depth,
+                          //   BVH4 worst-case traversal stack, pad
   uint64_t parent_addr;   // i32 [2n]: parent of internal node i at [i], of leaf k at [n + k]
   uint64_t flags_addr;    // u32 [n]: arrival counters of the bottom-up pass
   uint64_t boxes_addr;    // float4 [2n][2]: lo, hi of internal node i at [i], of leaf k at [n + k]
@@ -40,5 +42,7 @@ typedef struct {
   uint64_t child_addr;    // i32 [n][2]: children (>= 0 internal, else ~leaf)
   uint64_t nodes_addr;    // rt_node_t [max(n - 1, 1)]
   uint64_t tris_addr;     // rt_tri_t [n + 3]
+  uint64_t nodes4_addr;   // rt_node4_t [max(n - 1, 1)]: BVH4 node at the BVH2 index of
+                          //   every even-depth internal node, zeros elsewhere
   uint32_t n, phase, pass, nblocks;
 } bvh_build_arg_t;

@@ -27,6 +27,7 @@ RT_RENDER_BVH2 = 0x40
 PT_SEED = 0x5EED
 RT_RENDER_INSTRUMENTED = 0x100
 RT_RENDER_COMPACT = 0x200
+RT_BVH_STACK4_UNUSED = 0xFFFFFFFF
 CLEAR_COLOR = 0xFF000000               # draw3d/main.cpp:47
 DEFAULT_LIGHT = (0.0, 60.0, 80.0)      # clip (x, y, w), SURVEY.md 8(d) config 3
 TILE = 32                              # RASTER_TILE_LOGSIZE = 5
@@ -42,7 +43,7 @@ class SceneInfo(C.Structure):
 
 class BvhBuildStats(C.Structure):
     _fields_ = [("nodes", C.c_uint32), ("depth", C.c_uint32), ("launches", C.c_uint32),
-                ("pad", C.c_uint32), ("build_ms", C.c_double), ("kernel_ms", C.c_double)]
+                ("stack4", C.c_uint32), ("build_ms", C.c_double), ("kernel_ms", C.c_double)]
 
     def as_dict(self):
         return {n: getattr(self, n) for n, _ in self._fields_ if n != "pad"}
@@ -87,6 +88,7 @@ def lib():
             "rt_scene_export_bvh4": [vp, vp],
             "rt_renderer_build_bvh": [vp, C.POINTER(BvhBuildStats)],
             "rt_renderer_export_bvh": [vp, vp, vp, C.POINTER(u32), C.POINTER(u32)],
+            "rt_renderer_export_bvh4": [vp, vp, C.POINTER(u32)],
             "rt_renderer_create": [vp, C.c_char_p, C.POINTER(vp)],
             "rt_renderer_free": [vp],
             "rt_renderer_configure": [vp, C.POINTER(RenderParams)],
@@ -186,7 +188,7 @@ class Renderer:
                                         C.byref(h)), "rt_renderer_create")
         self._h = h
         self.params = None
-        self.gpu_bvh = False
+        self.gpu_bvh = self.gpu_bvh4 = False
 
     def configure(self, width: int, height: int, shadows: bool = True, light=DEFAULT_LIGHT,
                   clear_color: int = CLEAR_COLOR, shard_index: int = 0, shard_count: int = 1,
@@ -213,9 +215,9 @@ class Renderer:
         _check(lib().rt_renderer_configure(self._h, C.byref(p)), "rt_renderer_configure")
         self.params = p
         self.bvh4 = (bvh_width != 2 and os.environ.get("RT_BVH_WIDTH", "4") != "2"
-                     and not self.gpu_bvh)
+                     and (not self.gpu_bvh or self.gpu_bvh4))
         # BVH4 node steps read 64-B binary16 nodes (rt_node4h_t) when the scene has them
-        self.bvh4_f16 = self.bvh4 and bool(self.scene.info()["bvh4_f16"])
+        self.bvh4_f16 = self.bvh4 and not self.gpu_bvh and bool(self.scene.info()["bvh4_f16"])
 
     def build_bvh(self) -> dict:
         """Build the BVH on the device (kernels/bvh_build.hip) and trace over it
@@ -223,9 +225,20 @@ class Renderer:
         st = BvhBuildStats()
         _check(lib().rt_renderer_build_bvh(self._h, C.byref(st)), "rt_renderer_build_bvh")
         self.gpu_bvh = True
+        self.gpu_bvh4 = st.stack4 != RT_BVH_STACK4_UNUSED
         if self.params is not None:
-            self.bvh4 = self.bvh4_f16 = False
+            self.bvh4 = self.gpu_bvh4 and not self.params.flags & RT_RENDER_BVH2
+            self.bvh4_f16 = False
         return st.as_dict()
+
+    def export_bvh4(self):
+        """The renderer's current BVH4 nodes (float32[N4, 32], rt_node4_t)."""
+        n = C.c_uint32()
+        _check(lib().rt_renderer_export_bvh4(self._h, None, C.byref(n)), "rt_renderer_export_bvh4")
+        nodes4 = np.zeros((max(n.value, 1), 32), np.float32)
+        _check(lib().rt_renderer_export_bvh4(self._h, nodes4.ctypes.data, C.byref(n)),
+               "rt_renderer_export_bvh4")
+        return nodes4[:n.value]
 
     def export_bvh(self):
         """The renderer's current BVH: (nodes float32[N, 16], tris float32[M, 12])."""

@@ -37,20 +37,27 @@ def test_gpu_bvh_equals_oracle_build(oracle_lib, synth, name):
     assert st["depth"] == od and st["nodes"] == len(on)
     assert np.array_equal(nodes.view(np.uint32), on.view(np.uint32))
     assert np.array_equal(tris.view(np.uint32), ot.view(np.uint32))
-    assert st["launches"] == 17
+    assert st["launches"] == 18
+    # the device BVH4 collapse == oracle/lbvh.c orc_lbvh_collapse4, bit for bit
+    o4, ostack = po.lbvh_collapse4(on)
+    assert np.array_equal(r.export_bvh4().view(np.uint32), o4.view(np.uint32))
+    assert st["stack4"] == ostack and r.gpu_bvh4
 
 
-@pytest.mark.parametrize("name,size,mode", [("tekkaman", 1024, "shadow"), ("tekkaman", 256, "path"),
-                                            ("scene", 256, "shadow"), ("box", 128, "shadow"),
-                                            ("synth20k", 192, "shadow")])
-def test_frames_over_gpu_bvh_equal_bruteforce(oracle_lib, synth, name, size, mode):
+@pytest.mark.parametrize("name,size,mode,width", [
+    ("tekkaman", 1024, "shadow", 0), ("tekkaman", 256, "path", 0), ("scene", 256, "shadow", 0),
+    ("box", 128, "shadow", 0), ("synth20k", 192, "shadow", 0), ("tekkaman", 1024, "shadow", 2),
+    ("synth20k", 192, "path", 2)])
+def test_frames_over_gpu_bvh_equal_bruteforce(oracle_lib, synth, name, size, mode, width):
+    """Frames over the device-built tree -- its BVH4 collapse by default,
+    its BVH2 with width=2 -- equal the brute-force oracle."""
     po = oracle_lib
     path = _scene(name, synth)
     s = rt.Scene.load(path)
     r = rt.Renderer(s)
-    r.configure(size, size, shadows=True, path=mode == "path")
+    r.configure(size, size, shadows=True, path=mode == "path", bvh_width=width)
     r.build_bvh()                       # reconfigures the renderer onto the new tree
-    assert not r.bvh4
+    assert r.bvh4 == (width != 2) and not r.bvh4_f16
     r.render()
     osc = po.OracleScene(po.cgltrace.load(path))
     c, _, _, k = po.rt_render(osc, po.rt_params(size, size, shadows=True, nthreads=8,
@@ -70,8 +77,10 @@ def test_instrumented_counts_over_gpu_bvh_equal_oracle_traversal(oracle_lib):
     r.render()
     st = r.stats()
     nodes, tris = r.export_bvh()
+    assert r.bvh4
     _, _, _, k = po.rt_render(po.OracleScene(po.cgltrace.load(scene_path("tekkaman"))),
-                              po.rt_params(512, 512, shadows=True, nthreads=8), bvh=(nodes, tris))
+                              po.rt_params(512, 512, shadows=True, nthreads=8),
+                              bvh=(nodes, tris, r.export_bvh4()))
     for key in ("node_visits", "tri_tests", "shadow_rays", "occluded"):
         assert st[key] == k[key], key
 

@@ -292,6 +292,28 @@ def lbvh_inputs(s):
 
 
 @pytest.mark.parametrize("name", ["tekkaman", "scene", "box", "carnival"])
+def test_lbvh_collapse4_oracle_structure_and_traversal(oracle_lib, name):
+    """The device BVH4 collapse restated (oracle/lbvh.c orc_lbvh_collapse4):
+    every leaf of the LBVH exactly once under nested boxes, >= 2 children per
+    node, the reported stack bound equal to the worst root-to-leaf push count,
+    and BVH4 traversal over it reproduces the BVH2 frames bit for bit."""
+    po = oracle_lib
+    s = rt.Scene.load(scene_path(name))
+    verts, geom, _ = lbvh_inputs(s)
+    nodes, tris, depth = po.lbvh_build(verts, geom)
+    nodes4, stack = po.lbvh_collapse4(nodes)
+    _check_bvh4(nodes4, nodes, tris, stack)
+    assert stack <= 3 * ((depth + 1) // 2)
+    osc = po.OracleScene(po.cgltrace.load(scene_path(name)))
+    p = po.rt_params(160, 160, shadows=True, nthreads=8)
+    c2, p2, t2, k2 = po.rt_render(osc, p, bvh=(nodes, tris))
+    c4, p4, t4, k4 = po.rt_render(osc, p, bvh=(nodes, tris, nodes4))
+    assert np.array_equal(c2, c4) and np.array_equal(p2, p4)
+    assert np.array_equal(t2.view(np.uint32), t4.view(np.uint32))
+    assert k4["occluded"] == k2["occluded"] and k4["node_visits"] <= k2["node_visits"]
+
+
+@pytest.mark.parametrize("name", ["tekkaman", "scene", "box", "carnival"])
 def test_lbvh_oracle_structure_and_traversal(oracle_lib, name):
     """The linear-BVH restatement (oracle/lbvh.c) builds a valid tree -- every
     triangle in exactly one leaf, inside its padded boxes, depth within the
