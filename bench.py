@@ -101,8 +101,8 @@ def cpu_baseline(shadows: bool, side: int, light, budget_s: float, path: bool = 
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=200)
-    ap.add_argument("--warmup", type=int, default=20)
+    ap.add_argument("--steps", type=int, default=2000)
+    ap.add_argument("--warmup", type=int, default=50)
     ap.add_argument("--size", type=int, default=1024)
     ap.add_argument("--no-shadows", action="store_true")
     ap.add_argument("--cpu-budget", type=float, default=10.0)
