@@ -33,7 +33,7 @@
 #ifndef RT_FLAT
 #define RT_FLAT 0
 #endif
-#define RT_FLAT_CAP 1024  // triangles staged in LDS (48 KB); longer lists stream via s_load
+#define RT_FLAT_CAP 1024  // triangles staged in LDS (64 KB); longer lists stream via s_load
 // RT_LDS_SCENE: the BVH is staged in LDS per workgroup (1024-thread images)
 #ifndef RT_LDS_SCENE
 #define RT_LDS_SCENE 0
@@ -65,7 +65,9 @@ struct WaveLds {
 };
 
 #if RT_FLAT
-__shared__ float4 s_geom[RT_FLAT_CAP * 3];
+// the geometry list staged as origin-0 MT records (mt_precompute_o0, 4 float4
+// per triangle) for the primary rays; shadow rays read the plain records
+__shared__ float4 s_geom[RT_FLAT_CAP * 4];
 // staged geometry list, or nullptr when it does not fit
 __device__ __forceinline__ const float4* flat_list(const Scene& S) {
   return S.num_geom <= RT_FLAT_CAP ? s_geom : nullptr;
@@ -78,7 +80,7 @@ __device__ __forceinline__ int32_t trace_closest(const Scene& S, const Ray& r, b
                                                  Counters& cnt) {
   if (!active) return -1;
 #if RT_FLAT
-  return trace_flat<false>(S, r, 0.0f, INFINITY, -1, tie_high, th, flat_list(S), cnt);
+  return trace_flat<false>(S, r, 0.0f, INFINITY, -1, tie_high, th, nullptr, cnt);
 #else
   return trace<false>(S, r, 0.0f, INFINITY, -1, tie_high, th, &w.stack[0][lane_id()], cnt);
 #endif
@@ -88,7 +90,7 @@ __device__ __forceinline__ bool occluded(const Scene& S, const Ray& s, int32_t s
   float ts;
   if (!active) return false;
 #if RT_FLAT
-  return trace_flat<true>(S, s, 0.0f, 1.0f, skip, tie_high, &ts, flat_list(S), cnt) >= 0;
+  return trace_flat<true>(S, s, 0.0f, 1.0f, skip, tie_high, &ts, nullptr, cnt) >= 0;
 #else
   return trace<true>(S, s, 0.0f, 1.0f, skip, tie_high, &ts, &w.stack[0][lane_id()], cnt) >= 0;
 #endif
@@ -224,9 +226,10 @@ __device__ __forceinline__ void flat_chunk(const vx_task_t& task, bool valid, co
   const float4* lds = flat_list(S);
   float bt = INFINITY;
   uint32_t f;
-  const int32_t bp = in ? trace_flat_range<false>(S, r, k0, k1, 0.0f, INFINITY, -1, tie_high, &bt,
-                                                  &f, lds)
-                        : -1;
+  const int32_t bp = !in ? -1
+                   : lds ? trace_flat_range_o0(r, k0, k1, 0.0f, INFINITY, tie_high, &bt, lds)
+                         : trace_flat_range<false>(S, r, k0, k1, 0.0f, INFINITY, -1, tie_high, &bt,
+                                                   &f, nullptr);
 #ifdef RT_INSTRUMENT
   cnt.tests += in ? k1 - k0 : 0u;  // the whole list per ray, summed over the waves
 #endif
@@ -255,7 +258,7 @@ __device__ __forceinline__ void flat_chunk(const vx_task_t& task, bool valid, co
     shadow_ray(S, r, th, sr);
     float ts;
     uint32_t first = 0xffffffffu;
-    if (shadow) trace_flat_range<true>(S, sr, k0, k1, 0.0f, 1.0f, hit, tie_high, &ts, &first, lds);
+    if (shadow) trace_flat_range<true>(S, sr, k0, k1, 0.0f, 1.0f, hit, tie_high, &ts, &first, nullptr);
     L.first[w][lane] = first;
   }
   __syncthreads();
@@ -307,8 +310,9 @@ VX_MAIN(rt_kernel_arg_t, arg, RT_BLOCK_THREADS) {
   // stage the geometry list once per workgroup (workgroups past the last
   // task chunk have nothing to render and skip it)
   if (S.num_geom <= RT_FLAT_CAP && blockIdx.x * VX_CHUNK < arg->num_tasks) {  // one chunk per step
-    for (uint32_t i = threadIdx.x; i < 3u * S.num_geom; i += blockDim.x)
-      s_geom[i] = S.A.ld_f4(S.geom + 16u * i);
+    for (uint32_t i = threadIdx.x; i < S.num_geom; i += blockDim.x)
+      mt_precompute_o0(S.A.ld_f4(S.geom + 48u * i), S.A.ld_f4(S.geom + 48u * i + 16),
+                       S.A.ld_f4(S.geom + 48u * i + 32), &s_geom[4u * i]);
   }
   __syncthreads();
 #endif

@@ -170,6 +170,46 @@ __device__ __forceinline__ bool mt_hit(const Ray& r, const float4& a, const floa
   return true;
 }
 
+// Möller–Trumbore for a ray whose origin is exactly (0, 0, 0) -- every
+// primary ray (primary_dir) -- against a triangle record whose ray-
+// independent terms were precomputed by mt_precompute_o0 with mt_hit's own
+// operations: tvec = 0 - v0, qvec = tvec x e1, tq = e2 . qvec.  Bit-identical
+// to mt_hit(r, ...) with r.o == 0; 4 LDS records of 16 B per triangle:
+// (e1, pid), (e2, tq), (tvec, 0), (qvec, 0).  Saves the per-ray cross product,
+// the subtractions and the t dot product.
+__device__ __forceinline__ void mt_precompute_o0(const float4& a, const float4& b, const float4& c,
+                                                 float4* out) {
+  const float e1[3] = {b.x, b.y, b.z}, e2[3] = {c.x, c.y, c.z};
+  float tvec[3], qvec[3];
+  tvec[0] = 0.0f - a.x;
+  tvec[1] = 0.0f - a.y;
+  tvec[2] = 0.0f - a.z;
+  cross3(qvec, tvec, e1);
+  out[0] = make_float4(b.x, b.y, b.z, a.w);
+  out[1] = make_float4(c.x, c.y, c.z, dot3(e2, qvec));
+  out[2] = make_float4(tvec[0], tvec[1], tvec[2], 0.0f);
+  out[3] = make_float4(qvec[0], qvec[1], qvec[2], 0.0f);
+}
+
+__device__ __forceinline__ bool mt_hit_o0(const Ray& r, const float4& A, const float4& B,
+                                          const float4& C, const float4& D, float tmin,
+                                          float* t_out) {
+  const float e1[3] = {A.x, A.y, A.z}, e2[3] = {B.x, B.y, B.z};
+  const float tvec[3] = {C.x, C.y, C.z}, qvec[3] = {D.x, D.y, D.z};
+  float pvec[3];
+  cross3(pvec, r.d, e2);
+  const float det = dot3(e1, pvec);
+  float u = dot3(tvec, pvec);
+  float v = dot3(r.d, qvec);
+  float adet = det;
+  if (det < 0.0f) { adet = -det; u = -u; v = -v; }
+  if (!(adet > 0.0f) || u < 0.0f || v < 0.0f || u + v > adet) return false;
+  const float t = B.w / det;
+  if (!(t > tmin)) return false;
+  *t_out = t;
+  return true;
+}
+
 // slab test of one child; box planes interleaved as in rt_node_t
 __device__ __forceinline__ bool slab(float lox, float hix, float loy, float hiy, float loz,
                                      float hiz, const Ray& r, float tmin, float tmax,
@@ -562,6 +602,26 @@ __device__ __forceinline__ int32_t trace_flat_range(const Scene& S, const Ray& r
         bt = t;
         bpid = pid;
       }
+    }
+  }
+  *t_out = bt;
+  return bpid;
+}
+
+// trace_flat_range for origin-0 (primary) rays over mt_precompute_o0
+// records in LDS (4 float4 per triangle): closest hit only
+__device__ __forceinline__ int32_t trace_flat_range_o0(const Ray& r, uint32_t k0, uint32_t k1,
+                                                       float tmin, float tmax, bool tie_high,
+                                                       float* t_out, const float4* lds4) {
+  float bt = tmax;
+  int32_t bpid = -1;
+  for (uint32_t k = k0; k < k1; ++k) {
+    const float4 A = lds4[4 * k], B = lds4[4 * k + 1], C = lds4[4 * k + 2], D = lds4[4 * k + 3];
+    const int32_t pid = __float_as_int(A.w);
+    float t;
+    if (mt_hit_o0(r, A, B, C, D, tmin, &t) && closer(t, pid, bt, bpid, tie_high)) {
+      bt = t;
+      bpid = pid;
     }
   }
   *t_out = bt;
