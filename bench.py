@@ -49,13 +49,16 @@ def algorithmic_bytes(st: dict, pixels: int, node_bytes: int = NODE_BYTES) -> in
             + st["texel_bytes"] + PIXEL_BYTES * pixels)
 
 
-def pmc_traffic(side: int, shadows: bool):
+def pmc_traffic(side: int, shadows: bool, mode: str = "shadow"):
     """HBM bytes per launch from the committed rocprofv3 PMC summary
-    (scripts/pmc_traffic.sh -> profiles/pmc_traffic.json), used only when it
-    was taken on this same kernel image and workload; else None."""
+    (scripts/pmc_traffic.sh -> profiles/pmc_traffic[_path|_flat].json), used
+    only when it was taken on this same kernel image and workload; else None."""
     import hashlib
-    path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
-    co = os.path.join(ROOT, "skybox_rt_amd", "lib", "rt_kernel.co")
+    name, image = {"shadow": ("pmc_traffic.json", "rt_kernel.co"),
+                   "path": ("pmc_traffic_path.json", "pt_kernel.co"),
+                   "flat": ("pmc_traffic_flat.json", "rt_flat.co")}[mode]
+    path = os.path.join(ROOT, "profiles", name)
+    co = os.path.join(ROOT, "skybox_rt_amd", "lib", image)
     try:
         with open(path) as fh:
             t = json.load(fh)
@@ -92,10 +95,33 @@ def cpu_baseline(shadows: bool, side: int, light, budget_s: float, path: bool = 
         el = time.perf_counter() - t0
         if el >= budget_s:
             break
-    return {"value": rays / el / 1e6, "unit": "Mrays/s", "cores": cores, "kind": "port",
+    value = rays / el / 1e6
+    # the same port on ONE thread (single-threaded and all
+    # cores; outputs are bit-identical for any thread count), a quarter of
+    # the budget, at least one frame
+    p1 = po.rt_params(side, side, shadows=shadows, light=light, nthreads=1, path=path,
+                      bounces=bounces)
+    frames1, rays1, t1 = 0, 0, time.perf_counter()
+    while True:
+        _, _, _, k = po.rt_render(osc, p1, bvh=None if flat else bvh)
+        frames1 += 1
+        rays1 += k["primary_rays"] + k["shadow_rays"] + k["bounce_rays"]
+        el1 = time.perf_counter() - t1
+        if el1 >= budget_s / 4:
+            break
+    cpu_model = "unknown"
+    try:
+        with open("/proc/cpuinfo") as fh:
+            cpu_model = next((ln.split(":", 1)[1].strip() for ln in fh if ln.startswith("model name")),
+                             cpu_model)
+    except OSError:
+        pass
+    return {"value": value, "unit": "Mrays/s", "cores": cores, "kind": "port",
             "sample": f"{frames} full {side}x{side} frames of the same workload "
                       f"({el:.1f} s, oracle/rt.c {'brute force' if flat else ('BVH4' if bvh4 else 'BVH2') + ' traversal'}, "
-                      f"{cores} threads)"}
+                      f"{cores} threads; single thread: {frames1} frames in {el1:.1f} s)",
+            "single_thread_value": rays1 / el1 / 1e6, "cpu_model": cpu_model,
+            "host_cpus": os.cpu_count()}
 
 
 def main():
@@ -324,7 +350,7 @@ def main():
         "roofline": {
             "bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBS, 4),
-            "traffic": None if (path or flat) else pmc_traffic(side, shadows),
+            "traffic": pmc_traffic(side, shadows, "path" if path else ("flat" if flat else "shadow")),
             "algorithmic_bytes_per_launch": int(alg_bytes),
             "counts": {k: int(inst[k]) for k in ("node_visits", "tri_tests", "layer_tests",
                                                  "texel_bytes", "primary_rays", "shadow_rays",

@@ -8,7 +8,7 @@ Correction (MI355X_MICROARCH.md, HBM section): on gfx950 FETCH_SIZE counts
 64 B per 128-B memory-side read request, i.e. exactly half of the bytes of a
 wide coalesced read, so the read side is doubled; WRITE_SIZE is taken as is.
 Both are in KB.  Usage: pmc_traffic.py <fetch_dir> <write_dir> <out.json>
-<width> <height> <shadows 0|1> <kernel .co>"""
+<width> <height> <shadows 0|1> <kernel .co> [mode: shadow|path|flat]"""
 import csv
 import glob
 import hashlib
@@ -30,13 +30,15 @@ def per_dispatch(d, counter):
 
 def main():
     fdir, wdir, out, w, h, sh, co = sys.argv[1:8]
+    mode = sys.argv[8] if len(sys.argv) > 8 else "shadow"
     f = per_dispatch(fdir, "FETCH_SIZE")
     wr = per_dispatch(wdir, "WRITE_SIZE")
     if not f or not wr:
         sys.exit("no vx_main dispatches with FETCH_SIZE / WRITE_SIZE")
     f_kb, w_kb = sum(f) / len(f), sum(wr) / len(wr)
     res = {
-        "kernel": "vx_main", "width": int(w), "height": int(h), "shadows": bool(int(sh)),
+        "kernel": "vx_main", "mode": mode, "width": int(w), "height": int(h),
+        "shadows": bool(int(sh)),
         "kernel_md5": hashlib.md5(open(co, "rb").read()).hexdigest(),
         "dispatches": [len(f), len(wr)],
         "fetch_size_kb": round(f_kb, 1), "write_size_kb": round(w_kb, 1),

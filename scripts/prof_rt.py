@@ -14,12 +14,16 @@ def main():
     ap.add_argument("--frames", type=int, default=20)
     ap.add_argument("--no-shadows", action="store_true")
     ap.add_argument("--kernel-dir", default=None)
+    ap.add_argument("--mode", choices=("shadow", "path", "flat"), default="shadow")
     args = ap.parse_args()
     import torch  # noqa: F401
     from skybox_rt_amd import rt
     s = rt.Scene.load(os.path.join(ROOT, "tests/golden/scenes/tekkaman.cgltrace"))
     r = rt.Renderer(s, kernel_dir=args.kernel_dir)
-    r.configure(args.size, args.size, shadows=not args.no_shadows)
+    flat = args.mode == "flat"
+    size = 256 if flat and args.size == 1024 else args.size   # bench.py's config-2 size
+    r.configure(size, size, shadows=not (args.no_shadows or flat), path=args.mode == "path",
+                flat=flat)
     for _ in range(args.frames):
         r.render()
     print(r.stats(), file=sys.stderr)
