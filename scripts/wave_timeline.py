@@ -17,11 +17,13 @@ sys.path.insert(0, ROOT)
 
 def main():
     size = int(sys.argv[1]) if len(sys.argv) > 1 else 1024
+    path = len(sys.argv) > 2 and sys.argv[2] == "path"   # pt_kernel (variants/ptstamp)
     import torch  # noqa: F401
     from skybox_rt_amd import rt
     s = rt.Scene.load(os.path.join(ROOT, "tests/golden/scenes/tekkaman.cgltrace"))
-    r = rt.Renderer(s, kernel_dir=os.path.join(ROOT, "skybox_rt_amd/lib/variants/stamp"))
-    r.configure(size, size, shadows=True)
+    r = rt.Renderer(s, kernel_dir=os.path.join(ROOT, "skybox_rt_amd/lib/variants",
+                                               "ptstamp" if path else "stamp"))
+    r.configure(size, size, shadows=True, path=path)
     for _ in range(5):
         r.render()
     rows = r.launch_rows().astype(np.int64)
@@ -43,7 +45,7 @@ def main():
     # wave w renders chunk w (one chunk per wave): the model waves are the
     # slow ones; report the lifetime by chunk decile of duration
     out = {
-        "size": size, "waves": int(n), "event_kernel_us": round(kms * 1e3, 1),
+        "size": size, "mode": "path" if path else "shadow", "waves": int(n), "event_kernel_us": round(kms * 1e3, 1),
         "stamp_span_us": round(span / 100.0, 1),
         "wave_us": {"p10": q(dur, 10) / 100, "p50": q(dur, 50) / 100, "p90": q(dur, 90) / 100,
                     "p99": q(dur, 99) / 100, "max": float(dur.max()) / 100},
@@ -58,6 +60,20 @@ def main():
                         "shadow_drain_us": float(drain[slow].mean()) / 100,
                         "start_us": float(t0[slow].mean()) / 100}
     out["all"] = {"primary_us": float(prim.mean()) / 100, "shadow_drain_us": float(drain.mean()) / 100}
+    # background (short) waves: where their time goes -- start -> primary
+    # traced (prologue, task map, traversal) and primary traced -> end
+    # (layers, shading, store, counter flush)
+    fast = dur <= np.percentile(dur, 50)
+    out["short_waves"] = {"n": int(fast.sum()), "wave_us": float(dur[fast].mean()) / 100,
+                          "to_primary_us": float(prim[fast].mean()) / 100,
+                          "after_primary_us": float((dur - prim)[fast].mean()) / 100}
+    if not path:  # stamp image slots 10 (scene loaded) and 11 (pixel shaded)
+        pro = rows[:, 10] - rows[:, 12]
+        shd = rows[:, 11] - rows[:, 14]
+        out["short_waves"].update({"prologue_us": float(pro[fast].mean()) / 100,
+                                   "trace_us": float((prim - pro)[fast].mean()) / 100,
+                                   "layers_shade_us": float(shd[fast].mean()) / 100,
+                                   "store_flush_us": float((rows[:, 13] - rows[:, 11])[fast].mean()) / 100})
     print(json.dumps(out))
 
 

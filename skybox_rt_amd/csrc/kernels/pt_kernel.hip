@@ -504,6 +504,9 @@ VX_MAIN_OCC(rt_kernel_arg_t, arg, PT_BLOCK, PT_WAVES_PER_EU) {
 VX_MAIN(rt_kernel_arg_t, arg, PT_BLOCK) {
 #endif
   __shared__ PtLds s_pt;
+#ifdef RT_STAMPS  // diagnostic image: per-wave start/end timestamps (scripts/wave_timeline.py)
+  const uint64_t t_stamp0 = __builtin_amdgcn_s_memrealtime();
+#endif
   Counters cnt;
   Scene S = load_scene(arg);
 #if PT_MODE == 0
@@ -529,6 +532,14 @@ VX_MAIN(rt_kernel_arg_t, arg, PT_BLOCK) {
   flush(RT_STAT_HITS, cnt.hits);
   flush(RT_STAT_OCCLUDED, cnt.occluded);
   flush(RT_STAT_BOUNCE, cnt.bounce);
+#ifdef RT_STAMPS
+  if (threadIdx.x == 0) {
+    __vx_mpm_lds[12] = (uint32_t)t_stamp0;
+    __vx_mpm_lds[13] = (uint32_t)__builtin_amdgcn_s_memrealtime();
+    __vx_mpm_lds[14] = (uint32_t)t_stamp0;
+    __vx_mpm_lds[15] = 0;
+  }
+#endif
 #ifdef RT_INSTRUMENT
   flush(RT_STAT_NODE_VISITS, cnt.visits);
   flush(RT_STAT_TRI_TESTS, cnt.tests);

@@ -99,6 +99,10 @@ __device__ __forceinline__ bool occluded(const Scene& S, const Ray& s, int32_t s
 __device__ __forceinline__ void kernel_body(const vx_task_t& task, const Scene& S, WaveLds& w,
                                             Counters& cnt) {
   const uint32_t t = task.blockIdx.x;
+#if RT_LAYER_PREFETCH && !RT_FLAT
+  LayerPre lp;
+  if (S.num_layer) load_layers(S, lp);
+#endif
   uint32_t x, y;
   task_pixel(S, t, &x, &y);
   const bool in = x < S.width && y < S.height;  // edge tiles overhang the image
@@ -116,12 +120,19 @@ __device__ __forceinline__ void kernel_body(const vx_task_t& task, const Scene& 
 #ifdef RT_ABLATE_LAYERS  // timing-only ablation (scripts/ab_variants.py)
   const int32_t spid = hit;
 #else
+#if RT_LAYER_PREFETCH && !RT_FLAT
+  const int32_t spid = resolve_layers(S, r, in && hit < 0, hit, cnt, &lp);
+#else
   const int32_t spid = resolve_layers(S, r, in && hit < 0, hit, cnt);
+#endif
 #endif
 #ifdef RT_ABLATE_SHADE  // timing-only ablation (scripts/ab_variants.py)
   uint32_t color = 0xff000000u | (uint32_t)spid;
 #else
   uint32_t color = shade_wave(S, spid, x, y, S.clear_color, cnt);
+#endif
+#ifdef RT_STAMPS
+  if (lane_id() == 0) __vx_mpm_lds[11] = (uint32_t)__builtin_amdgcn_s_memrealtime();
 #endif
   const bool shadow = hit >= 0 && (S.flags & RT_FLAG_SHADOWS) != 0;
 #if RT_SHADOW_QUEUE
@@ -298,6 +309,9 @@ VX_MAIN(rt_kernel_arg_t, arg, RT_BLOCK_THREADS) {
 #endif
   Counters cnt;
   Scene S = load_scene(arg);
+#ifdef RT_STAMPS
+  if (threadIdx.x == 0) __vx_mpm_lds[10] = (uint32_t)__builtin_amdgcn_s_memrealtime();
+#endif
 #if RT_LDS_SCENE
   // the whole BVH (nodes + leaf triangles) staged once per workgroup:
   // traversal then reads LDS (broadcast-friendly, ~100-cycle latency)

@@ -38,6 +38,19 @@
 #ifndef RT_WW
 #define RT_WW 1
 #endif
+// 1: the first node step of every walk (all lanes at the root) reads the root
+// through the scalar cache -- one load per wave instead of 64 lanes of vector
+// data, and the root is where every background ray's walk ends
+#ifndef RT_ROOT_SCALAR
+#define RT_ROOT_SCALAR 1
+#endif
+// 1: rt_kernel issues the first screen-layer records' scalar loads before the
+// primary walk, so a background wave's layer tests do not wait for them
+// (A/B r01_v12: neutral to +1 % -- off; the root step alone: neutral for
+// primary+shadow, -1.4 % for the path tracer, and 64x less root data traffic)
+#ifndef RT_LAYER_PREFETCH
+#define RT_LAYER_PREFETCH 0
+#endif
 
 namespace rtk {
 
@@ -419,6 +432,15 @@ __device__ __forceinline__ int32_t trace_impl(const Scene& S, const Ray& r, floa
     if (st.h1) return st.c1;
     return RT_EMPTY_REF;
   };
+#if RT_WW && RT_ROOT_SCALAR
+  {
+    // every lane starts at the root: one wave-uniform (scalar) step; a walk
+    // whose root step hits no child has pushed nothing and is over
+    const int32_t nx = node_next(true, 0);
+    if (nx == RT_EMPTY_REF) return -1;
+    ref = nx;
+  }
+#endif
   for (;;) {
 #if RT_WW
     // while-while (Aila & Laine 2009): a lane steps through inner nodes until
@@ -671,12 +693,33 @@ __device__ __forceinline__ uint32_t shade_wave(const Scene& S, int32_t spid, uin
 // the first covering triangle wins (oracle/rt.c rt_row); one wave-uniform
 // triangle per step, its record through the scalar cache.  Returns the pid
 // to shade (layer pid, or `spid` unchanged).
+// the first kLayerPre layer records, loaded (scalar) ahead of their use
+constexpr uint32_t kLayerPre = 2;
+struct LayerPre {
+  float4 rec[kLayerPre][3];
+};
+__device__ __forceinline__ void load_layers(const Scene& S, LayerPre& L) {
+#pragma unroll
+  for (uint32_t k = 0; k < kLayerPre; ++k) {
+    const uint32_t lo = S.layers + 48u * (k < S.num_layer ? k : 0u);
+    L.rec[k][0] = S.A.sld_f4(lo);
+    L.rec[k][1] = S.A.sld_f4(lo + 16);
+    L.rec[k][2] = S.A.sld_f4(lo + 32);
+  }
+}
+
 __device__ __forceinline__ int32_t resolve_layers(const Scene& S, const Ray& r, bool need,
-                                                  int32_t spid, Counters& cnt) {
+                                                  int32_t spid, Counters& cnt,
+                                                  const LayerPre* pre = nullptr) {
   uint64_t pend = __ballot(need);
   for (uint32_t k = 0; pend != 0 && k < S.num_layer; ++k) {
     const uint32_t lo = S.layers + 48u * k;
-    const float4 ta = S.A.sld_f4(lo), tb = S.A.sld_f4(lo + 16), tc = S.A.sld_f4(lo + 32);
+    float4 ta, tb, tc;
+    if (pre && k < kLayerPre) {
+      ta = pre->rec[k][0]; tb = pre->rec[k][1]; tc = pre->rec[k][2];
+    } else {
+      ta = S.A.sld_f4(lo); tb = S.A.sld_f4(lo + 16); tc = S.A.sld_f4(lo + 32);
+    }
     const bool mine = (pend & (1ull << lane_id())) != 0;
 #ifdef RT_INSTRUMENT
     cnt.layer_tests += mine;
