@@ -41,7 +41,7 @@
 #include "VX_types.h"
 
 #define VX_CHUNK 64          /* tasks per wave */
-#define VX_MAX_GRID 16384    /* blocks per launch (rows of the counter slab) */
+#define VX_MAX_GRID 32768    /* blocks per launch (rows of the counter slab) */
 
 /* per-launch device state: one 64-B row of the first VX_MPM_ROW u32 mpm
  * counters per block, each written by its block at exit (kernel programs

@@ -60,7 +60,7 @@ constexpr uint64_t kBlockSize = 256;      // allocation granule (>= 64 B DCR blo
 constexpr uint64_t kDefaultArenaMB = 4096;
 // __vx_state layout (include/vx_spawn.h): uint32 mpm[kMaxGrid][kMpmRow],
 // one row of the first kMpmRow counters per block, written at block exit
-constexpr uint32_t kMaxGrid = 16384;
+constexpr uint32_t kMaxGrid = 32768;
 constexpr uint32_t kMpmRow = 16;
 constexpr int kGridWavesPerCU = 64;  // 4x the 16 resident waves/CU of the RT kernel
 
@@ -433,6 +433,17 @@ class vx_device {
     // waiting for a slot are the load balancer (the hardware dispatcher hands
     // a CU its next block when one retires, as simx's cores pull warps).
     int per_cu = kGridWavesPerCU / (int)((m.block + 63) / 64);
+    // an image may carry its own measured grid (u32 __vx_grid_per_cu, in
+    // 64-thread blocks per CU); the env knob still overrides it
+    hipDeviceptr_t gp = nullptr;
+    size_t gsz = 0;
+    if (hipModuleGetGlobal(&gp, &gsz, m.module, "__vx_grid_per_cu") == hipSuccess && gsz == 4) {
+      uint32_t v = 0;
+      HIP_CHECK(hipMemcpyDtoH(&v, gp, 4));
+      if (v > 0) per_cu = (int)v;
+    } else {
+      (void)hipGetLastError();
+    }
     if (const char* s = std::getenv("VX_HIP_BLOCKS_PER_CU")) per_cu = std::atoi(s);
     if (per_cu < 1) per_cu = 1;
     m.grid = (uint32_t)(props_.multiProcessorCount * per_cu);
