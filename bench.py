@@ -1,24 +1,33 @@
 #!/usr/bin/env python3
 """bench.py -- headline benchmark: Mrays/s of the MI355X ray-tracing hot path.
 
-Workload (BASELINE.json configs[2], the metric's config): tekkaman.cgltrace,
-1024x1024, one primary ray per pixel + one any-hit shadow ray per geometry
-hit, BVH traversal with the per-wave LDS stack.  A "step" is one full frame:
-vx_start + vx_ready_wait of the RT kernel image through libvortex-hip.so
-(inputs already resident in HBM).  With N GPUs (torchrun, one rank per GPU)
-the frame grows to ~1024*sqrt(N) on a side (weak scaling: ~1M pixels per
-GPU), 32x32 tiles are dealt tile t -> rank t % N, and each step ends with an
-RCCL gather of the compact tile buffers to rank 0 plus a de-interleave there
-(SURVEY.md 8(e)).
+Workload at N = 1 (BASELINE.json configs[2], the metric's config):
+tekkaman.cgltrace, 1024x1024, one primary ray per pixel + one any-hit shadow
+ray per geometry hit, BVH traversal with the per-wave LDS stack.  A "step" is
+one full frame: vx_start + vx_ready_wait of the RT kernel image through
+libvortex-hip.so (inputs already resident in HBM).
+
+With N > 1 GPUs (one rank per GPU over RCCL) the default workload is
+BASELINE config 5: ONE 4096x4096 frame whose 32x32 tiles are dealt
+tile t -> rank t % N (sim/simx/raster_unit.cpp:109-111 striding), each step
+ending with an RCCL gather of the ranks' compact tile buffers to rank 0 and
+the frame assembly there -- strong scaling (fixed total
+work).  `--gpus N` without WORLD_SIZE launches the N ranks itself
+(torch.distributed.run, before anything touches a GPU).  Every line also
+carries `series`: the same render at 4096^2 on these N GPUs (strong) and at
+~1024^2 * sqrt(N) (weak, ~1M pixels per GPU).
 
 Rank 0 prints one JSON line.  Everything else goes to stderr.
 """
 from __future__ import annotations
 
 import argparse
+import gc
 import json
 import math
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -34,6 +43,11 @@ MT_FLOPS = 40          # fp32 ops per Moller-Trumbore test
 FP32_VALU_TFLOPS = 157.3  # MI355X_MICROARCH.md: peak FP32 (vector)
 NODE4_BYTES = 112      # BVH4 node: 6 SoA box float4 + the child-ref float4 (pad not read)
 NODE4H_BYTES = 64      # BVH4 node with binary16 planes (rt_node4h_t): 48 B of planes + 16 B refs
+# VALU issue peak: 1024 SIMDs, one wave64 VALU instruction per 2 cycles per
+# SIMD (MI355X_MICROARCH.md "issues each VALU instruction over 2 cycles"),
+# at the 2.4 GHz peak engine clock
+VALU_ISSUE_PEAK_GIPS = 1024 * 2.4 / 2.0
+CONFIG5_SIDE = 4096    # BASELINE config 5
 
 
 def log(*a):
@@ -49,66 +63,120 @@ def algorithmic_bytes(st: dict, pixels: int, node_bytes: int = NODE_BYTES) -> in
             + st["texel_bytes"] + PIXEL_BYTES * pixels)
 
 
-def pmc_traffic(side: int, shadows: bool, mode: str = "shadow"):
-    """HBM bytes per launch from the committed rocprofv3 PMC summary
-    (scripts/pmc_traffic.sh -> profiles/pmc_traffic[_path|_flat].json), used
-    only when it was taken on this same kernel image and workload; else None."""
+PMC_IMAGES = {"shadow": "rt_kernel.co", "path": "pt_kernel.co", "flat": "rt_flat.co"}
+
+
+def pmc_record(mode: str, side: int):
+    """The committed rocprofv3 PMC record of this workload's kernel image
+    (scripts/pmc_profile.sh -> profiles/pmc_<mode>.json): HBM traffic per
+    launch (FETCH_SIZE x2 + WRITE_SIZE, the guide's gfx950 correction) and
+    the SQ/TCP counters.  Returns (record or None, stale): stale = a record
+    exists but was taken on another kernel image or size."""
     import hashlib
-    name, image = {"shadow": ("pmc_traffic.json", "rt_kernel.co"),
-                   "path": ("pmc_traffic_path.json", "pt_kernel.co"),
-                   "flat": ("pmc_traffic_flat.json", "rt_flat.co")}[mode]
-    path = os.path.join(ROOT, "profiles", name)
-    co = os.path.join(ROOT, "skybox_rt_amd", "lib", image)
+    path = os.path.join(ROOT, "profiles", f"pmc_{mode}.json")
+    co = os.path.join(ROOT, "skybox_rt_amd", "lib", PMC_IMAGES[mode])
     try:
         with open(path) as fh:
             t = json.load(fh)
-        md5 = hashlib.md5(open(co, "rb").read()).hexdigest()
     except (OSError, ValueError):
-        return None
-    if (t.get("kernel_md5") != md5 or t.get("width") != side or t.get("height") != side
-            or t.get("shadows") != shadows):
-        return None
-    return int(t["traffic_bytes"])
+        return None, False
+    try:
+        md5 = hashlib.md5(open(co, "rb").read()).hexdigest()
+    except OSError:
+        return None, True
+    if t.get("kernel_md5") != md5 or t.get("width") != side or t.get("height") != side:
+        return None, True
+    return t, False
 
 
 def frame_side(n_gpus: int, base: int) -> int:
     return max(32, int(round(base * math.sqrt(n_gpus) / 32.0)) * 32)
 
 
+def physical_cores(cpus) -> int:
+    """Distinct (package, core) pairs among `cpus` (/proc/cpuinfo)."""
+    try:
+        pairs, cur = set(), {}
+        with open("/proc/cpuinfo") as fh:
+            for ln in list(fh) + [""]:
+                if not ln.strip():
+                    if cur.get("processor") is not None and int(cur["processor"]) in cpus:
+                        pairs.add((cur.get("physical id"), cur.get("core id")))
+                    cur = {}
+                    continue
+                k, _, v = ln.partition(":")
+                cur[k.strip()] = v.strip()
+        return len(pairs) or len(cpus)
+    except OSError:
+        return len(cpus)
+
+
+def cgroup_cpus():
+    """CPU bandwidth quota of this cgroup in CPUs (cpu.max), or None."""
+    try:
+        q, p = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        return None if q == "max" else round(int(q) / int(p), 2)
+    except (OSError, ValueError):
+        return None
+
+
 def cpu_baseline(shadows: bool, side: int, light, budget_s: float, path: bool = False,
                  bounces: int = 4, flat: bool = False, bvh4: bool = True):
     """Oracle (C port of the same algorithm, oracle/rt.c) on the host cores,
-    BVH traversal identical to the kernel's, full frames until budget_s."""
+    BVH traversal identical to the kernel's: threads = every CPU this process
+    may run on (SURVEY.md 8(d) / BASELINE.md: all host cores) -- the CPUs of
+    its affinity set, capped by its cgroup's CPU quota when one is set (a GPU
+    box job sees 256 CPUs but is granted 16: 256 threads there run slower
+    than 16, so that rate is reported beside it) -- median of 5 timed runs
+    of whole frames after a warm-up frame; the 1-thread frame must equal the
+    N-thread frame bit for bit."""
     from oracle import py_oracle as po
     from skybox_rt_amd import rt as rtmod
-    cores = max(1, min(16, os.cpu_count() or 1))
+    cpus = sorted(os.sched_getaffinity(0))
+    quota = cgroup_cpus()
+    threads = len(cpus) if quota is None else max(1, min(len(cpus), int(quota)))
     osc = po.OracleScene(po.cgltrace.load(SCENE))
     sc = rtmod.Scene.load(SCENE)
-    bvh = sc.bvh() + ((sc.bvh4(),) if bvh4 else ())
-    p = po.rt_params(side, side, shadows=shadows, light=light, nthreads=cores, path=path,
-                     bounces=bounces)
-    frames, rays, t0 = 0, 0, time.perf_counter()
-    while True:
-        _, _, _, k = po.rt_render(osc, p, bvh=None if flat else bvh)
-        frames += 1
-        rays += k["primary_rays"] + k["shadow_rays"] + k["bounce_rays"]
-        el = time.perf_counter() - t0
-        if el >= budget_s:
-            break
-    value = rays / el / 1e6
-    # the same port on ONE thread (SURVEY.md 8(d): single-threaded and all
-    # cores; outputs are bit-identical for any thread count), a quarter of
-    # the budget, at least one frame
-    p1 = po.rt_params(side, side, shadows=shadows, light=light, nthreads=1, path=path,
-                      bounces=bounces)
-    frames1, rays1, t1 = 0, 0, time.perf_counter()
-    while True:
-        _, _, _, k = po.rt_render(osc, p1, bvh=None if flat else bvh)
-        frames1 += 1
-        rays1 += k["primary_rays"] + k["shadow_rays"] + k["bounce_rays"]
-        el1 = time.perf_counter() - t1
-        if el1 >= budget_s / 4:
-            break
+    bvh = None if flat else (sc.bvh() + ((sc.bvh4(),) if bvh4 else ()))
+
+    def params(nt):
+        return po.rt_params(side, side, shadows=shadows, light=light, nthreads=nt, path=path,
+                            bounces=bounces)
+
+    def rays_of(k):
+        return k["primary_rays"] + k["shadow_rays"] + k["bounce_rays"]
+
+    pn, p1 = params(threads), params(1)
+    t = time.perf_counter()
+    c1, _, _, k1 = po.rt_render(osc, p1, bvh=bvh)            # one single-thread frame
+    el1 = time.perf_counter() - t
+    cn, _, _, kn = po.rt_render(osc, pn, bvh=bvh)            # warm-up, all threads
+    identical = bool(np.array_equal(c1, cn)) and k1 == kn
+    runs = []
+    frames_total = 0
+    for _ in range(5):
+        frames, rays, t0 = 0, 0, time.perf_counter()
+        while True:
+            _, _, _, k = po.rt_render(osc, pn, bvh=bvh)
+            frames += 1
+            rays += rays_of(k)
+            el = time.perf_counter() - t0
+            if el >= budget_s / 5:
+                break
+        frames_total += frames
+        runs.append(rays / el / 1e6)
+    all_aff = None
+    if threads < len(cpus):  # one run with a thread per affinity CPU, for the record
+        pa = params(len(cpus))
+        frames, rays, t0 = 0, 0, time.perf_counter()
+        while True:
+            _, _, _, k = po.rt_render(osc, pa, bvh=bvh)
+            frames += 1
+            rays += rays_of(k)
+            el = time.perf_counter() - t0
+            if el >= budget_s / 5:
+                break
+        all_aff = rays / el / 1e6
     cpu_model = "unknown"
     try:
         with open("/proc/cpuinfo") as fh:
@@ -116,99 +184,74 @@ def cpu_baseline(shadows: bool, side: int, light, budget_s: float, path: bool = 
                              cpu_model)
     except OSError:
         pass
-    return {"value": value, "unit": "Mrays/s", "cores": cores, "kind": "port",
-            "sample": f"{frames} full {side}x{side} frames of the same workload "
-                      f"({el:.1f} s, oracle/rt.c {'brute force' if flat else ('BVH4' if bvh4 else 'BVH2') + ' traversal'}, "
-                      f"{cores} threads; single thread: {frames1} frames in {el1:.1f} s)",
-            "single_thread_value": rays1 / el1 / 1e6, "cpu_model": cpu_model,
-            "host_cpus": os.cpu_count()}
+    return {"value": float(np.median(runs)), "unit": "Mrays/s", "cores": threads, "kind": "port",
+            "sample": f"median of 5 timed runs ({frames_total} full {side}x{side} frames of the same "
+                      f"workload in ~{budget_s:.0f} s; oracle/rt.c "
+                      f"{'brute force' if flat else ('BVH4' if bvh4 else 'BVH2') + ' traversal'}, "
+                      f"{threads} threads = every CPU granted to this process: {len(cpus)} in the "
+                      f"affinity set, cgroup quota {quota}) after a warm-up frame",
+            "runs_mrays_per_s": [round(x, 3) for x in runs],
+            "threads": threads, "affinity_cpus": len(cpus),
+            "physical_cores": physical_cores(set(cpus)), "cgroup_cpu_quota": quota,
+            "all_affinity_threads_value": all_aff,
+            "single_thread_value": rays_of(k1) / el1 / 1e6,
+            "one_vs_all_threads_bit_identical": identical,
+            "cpu_model": cpu_model, "host_cpus": os.cpu_count()}
 
 
-def main():
-    ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=2000)
-    ap.add_argument("--warmup", type=int, default=50)
-    ap.add_argument("--size", type=int, default=1024)
-    ap.add_argument("--no-shadows", action="store_true")
-    ap.add_argument("--cpu-budget", type=float, default=10.0)
-    ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--workload", choices=("shadow", "path", "flat"), default="shadow",
-                    help="shadow: BASELINE config 3 (the metric's config, default); "
-                         "path: config 4, 4-bounce diffuse path trace; "
-                         "flat: config 2, 256^2 primary rays over the flat triangle list")
-    ap.add_argument("--bounces", type=int, default=4)
-    ap.add_argument("--verify-gather", action="store_true",
-                    help="N>1: rank 0 checks the gathered frame against its own full render")
-    args = ap.parse_args()
-    # stdout carries exactly ONE line, the JSON result: anything else the
-    # native libraries write to fd 1 (e.g. RCCL's version banner) goes to
-    # stderr
-    sys.stdout.flush()
-    json_fd = os.dup(1)
-    os.dup2(2, 1)
-    path = args.workload == "path"
-    flat = args.workload == "flat"
-    if flat and args.size == 1024:
-        args.size = 256  # config 2 resolution
-    if flat:
-        args.no_shadows = True
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    n_gpus = max(world, 1)
-    # BENCH_FORCE_GATHER=1 (under torch.distributed.run): the N>1 exchange
-    # path even at world size 1 -- RCCL on one GPU, to test its stream order
-    use_gather = world > 1 or os.environ.get("BENCH_FORCE_GATHER") == "1"
-    dist = None
-    import torch
-    # RCCL ("nccl") between the GPUs; BENCH_DIST_BACKEND=gloo rehearses the
-    # multi-rank flow with host-staged gathers (e.g. several ranks on one GPU)
-    backend = os.environ.get("BENCH_DIST_BACKEND", "nccl")
-    coll_dev = torch.device("cpu")
-    if use_gather:
-        import torch.distributed as dist
-        dev_index = local_rank % max(1, torch.cuda.device_count())
-        torch.cuda.set_device(dev_index)
-        if backend == "nccl":
-            coll_dev = torch.device("cuda", dev_index)
-            dist.init_process_group("nccl", device_id=coll_dev)
-        else:
-            dist.init_process_group(backend)
-    from skybox_rt_amd import rt
+def free_port() -> int:
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
 
-    shadows = not args.no_shadows
-    light = rt.DEFAULT_LIGHT
-    side = args.size if n_gpus == 1 else frame_side(n_gpus, args.size)
-    scene = rt.Scene.load(SCENE)
-    info = scene.info()
-    r = rt.Renderer(scene)
 
-    # algorithmic bytes per launch from the instrumented variant (untimed)
-    r.configure(side, side, shadows=shadows, light=light, shard_index=rank, shard_count=n_gpus,
-                instrumented=True, path=path, bounces=args.bounces, flat=flat)
-    r.render()
-    inst = r.stats()
-    pixels_local = inst["primary_rays"]
-    bvh_kind = ("BVH4 (binary16 boxes)" if r.bvh4_f16 else "BVH4") if r.bvh4 else "BVH2"
-    alg_bytes = algorithmic_bytes(inst, pixels_local, (NODE4H_BYTES if r.bvh4_f16 else NODE4_BYTES)
-                                  if r.bvh4 else NODE_BYTES)
+def launch_ranks(n: int) -> int:
+    """`--gpus N` outside a launcher: start N ranks (one per GPU) with
+    torch.distributed.run as CHILD processes -- this process never touches a
+    GPU -- and return their exit status."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr", "127.0.0.1", "--master-port", str(free_port()),
+           os.path.abspath(__file__)] + sys.argv[1:]
+    log("bench.py: launching", " ".join(cmd))
+    env = dict(os.environ, BENCH_LAUNCHED="1")
+    return subprocess.call(cmd, env=env)
 
-    r.configure(side, side, shadows=shadows, light=light, shard_index=rank, shard_count=n_gpus,
-                path=path, bounces=args.bounces, flat=flat, compact=use_gather)
-    gather = None
-    if use_gather:
+
+class Run:
+    """One timed configuration of the renderer (+ the RCCL gather at N > 1)."""
+
+    def __init__(self, r, rt, dist, coll_dev, rank, n_gpus, side, shadows, light, path, flat,
+                 bounces, use_gather):
+        self.r, self.side, self.n = r, side, n_gpus
+        self.kw = dict(shadows=shadows, light=light, shard_index=rank, shard_count=n_gpus,
+                       path=path, bounces=bounces, flat=flat)
+        # algorithmic bytes per launch and rays per frame from the instrumented
+        # variant (untimed; its counters equal the oracle's traversal,
+        # tests/test_gpu_rt.py): the timed product image writes no counters
+        r.configure(side, side, instrumented=True, **self.kw)
+        r.render()
+        self.inst = r.stats()
+        self.rays_local = (self.inst["primary_rays"] + self.inst["shadow_rays"]
+                           + self.inst["bounce_rays"])
+        r.configure(side, side, compact=use_gather, counters=False, **self.kw)
+        self.gather = None
+        self.fg = None
+        if use_gather:
+            self._setup_gather(dist, coll_dev)
+
+    def _setup_gather(self, dist, coll_dev):
         import ctypes
+        import torch
         from skybox_rt_amd.shard import FrameGather
+        r = self.r
         hip = ctypes.CDLL("libamdhip64.so.7")  # torch's runtime, already loaded
-        fg_slots = 4
-        fg = FrameGather(dist, side, side, coll_dev, slots=fg_slots)
+        self.slots = 4
+        fg = FrameGather(dist, self.side, self.side, coll_dev, slots=self.slots)
+        self.fg = fg
         dev_ptr, nbytes = r.framebuffer_device()
         kind = 3 if coll_dev.type == "cuda" else 2  # hipMemcpyDeviceToDevice / ToHost
-
         nsteps = [0]
-        if kind == 3:
-            drv_stream = torch.cuda.ExternalStream(r.device_stream())
+        drv_stream = torch.cuda.ExternalStream(r.device_stream()) if kind == 3 else None
         hip.hipMemcpyAsync.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t,
                                        ctypes.c_int, ctypes.c_void_p]
 
@@ -220,7 +263,7 @@ def main():
             # frame k's kernel (the host does not wait for the frame) and the
             # gather follows that stream; a slot is reclaimed on the host
             # once its gather of 4 frames ago has completed
-            slot = nsteps[0] % fg_slots
+            slot = nsteps[0] % self.slots
             nsteps[0] += 1
             fg.reclaim(slot)
             if kind == 3:
@@ -232,77 +275,208 @@ def main():
                 hip.hipMemcpy(ctypes.c_void_p(fg.locals[slot].data_ptr()),
                               ctypes.c_void_p(dev_ptr), ctypes.c_size_t(nbytes), kind)
                 fg.start(slot)
+        self.gather = gather
 
+    def step(self):
+        self.r.start()
+        if self.gather is not None:
+            self.gather()
+
+    def drain(self):
+        self.r.wait()
+        if self.fg is not None:
+            for slot in range(self.slots):
+                self.fg.reclaim(slot)
+
+    def timed(self, steps, warmup, dist):
+        """W untimed steps, then EXACTLY `steps` steps between barrier +
+        synchronize on both sides; returns (elapsed s, kernel ms avg, timed
+        launches)."""
+        import torch
+        for _ in range(warmup):
+            self.step()
+        self.drain()
+        if dist is not None:
+            dist.barrier()
+        torch.cuda.synchronize()
+        ms0, nt0, n0 = self.r.run_totals()
+        gc.disable()  # no collector pause inside the timed region
+        try:
+            t0 = time.perf_counter()
+            for _ in range(steps):
+                self.step()
+            self.drain()  # every frame rendered (and gathered + assembled) inside the region
+            torch.cuda.synchronize()
+            if dist is not None:
+                dist.barrier()
+            elapsed = time.perf_counter() - t0
+        finally:
+            gc.enable()
+        ms1, nt1, n1 = self.r.run_totals()
+        assert n1 - n0 == steps and nt1 > nt0, (n0, n1, nt0, nt1)
+        return elapsed, (ms1 - ms0) / (nt1 - nt0), nt1 - nt0
+
+
+def reduce_max_sum(dist, coll_dev, elapsed, rays):
+    import torch
+    if dist is None:
+        return elapsed, float(rays)
+    t = torch.tensor([elapsed, float(rays)], dtype=torch.float64, device=coll_dev)
+    mx, sm = t.clone(), t.clone()
+    dist.all_reduce(mx, op=dist.ReduceOp.MAX)
+    dist.all_reduce(sm, op=dist.ReduceOp.SUM)
+    return float(mx[0]), float(sm[1])
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=2000)
+    ap.add_argument("--warmup", type=int, default=50)
+    ap.add_argument("--size", type=int, default=None,
+                    help="frame side (default: 1024 at N=1, config 3; 4096 at N>1, config 5)")
+    ap.add_argument("--no-shadows", action="store_true")
+    ap.add_argument("--cpu-budget", type=float, default=15.0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-series", action="store_true",
+                    help="skip the strong/weak scaling series runs")
+    ap.add_argument("--workload", choices=("shadow", "path", "flat"), default="shadow",
+                    help="shadow: BASELINE config 3 (the metric's config, default); "
+                         "path: config 4, 4-bounce diffuse path trace; "
+                         "flat: config 2, 256^2 primary rays over the flat triangle list")
+    ap.add_argument("--bounces", type=int, default=4)
+    ap.add_argument("--verify-gather", action="store_true",
+                    help="N>1: rank 0 checks the gathered frame against its own full render")
+    ap.add_argument("--plumbing-check", action="store_true",
+                    help="stop after the ranks have joined the communicator: rank 0 prints "
+                         "n_gpus / ranks_seen (CPU rehearsal of --gpus with BENCH_DIST_BACKEND=gloo)")
+    args = ap.parse_args()
+    world_env = os.environ.get("WORLD_SIZE")
+    if args.gpus > 1 and world_env is None:
+        sys.exit(launch_ranks(args.gpus))
+    world = int(world_env or "1")
+    if args.gpus > 1 and world != args.gpus:
+        log(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}")
+        sys.exit(2)
+    # stdout carries exactly ONE line, the JSON result: anything else the
+    # native libraries write to fd 1 (e.g. RCCL's version banner) goes to
+    # stderr
+    sys.stdout.flush()
+    json_fd = os.dup(1)
+    os.dup2(2, 1)
+    path = args.workload == "path"
+    flat = args.workload == "flat"
+    n_gpus = max(world, 1)
+    if args.size is None:
+        args.size = 256 if flat else (CONFIG5_SIDE if n_gpus > 1 else 1024)
+    if flat:
+        args.no_shadows = True
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    # BENCH_FORCE_GATHER=1 (under torch.distributed.run): the N>1 exchange
+    # path even at world size 1 -- RCCL on one GPU, to test its stream order
+    use_gather = world > 1 or os.environ.get("BENCH_FORCE_GATHER") == "1" or args.plumbing_check
+    dist = None
+    import torch
+    # RCCL ("nccl") between the GPUs; BENCH_DIST_BACKEND=gloo rehearses the
+    # multi-rank flow with host-staged gathers (e.g. several ranks on one GPU)
+    backend = os.environ.get("BENCH_DIST_BACKEND", "nccl")
+    coll_dev = torch.device("cpu")
+    ranks_seen = 1
+    if use_gather:
+        import torch.distributed as dist
+        ndev = torch.cuda.device_count()
+        dev_index = local_rank % max(1, ndev)
+        if ndev:
+            torch.cuda.set_device(dev_index)
+        if backend == "nccl":
+            coll_dev = torch.device("cuda", dev_index)
+            dist.init_process_group("nccl", device_id=coll_dev)
+        else:
+            dist.init_process_group(backend)
+        one = torch.ones(1, dtype=torch.float64, device=coll_dev)
+        dist.all_reduce(one)  # ranks the communicator actually connects
+        ranks_seen = int(one.item())
+        if ranks_seen != world:
+            log(f"bench.py: communicator sees {ranks_seen} ranks, WORLD_SIZE={world}")
+            sys.exit(3)
+    if args.plumbing_check:
+        if rank == 0:
+            os.write(json_fd, (json.dumps({"n_gpus": n_gpus, "ranks_seen": ranks_seen,
+                                           "backend": backend, "plumbing_check": True}) + "\n").encode())
+        if dist is not None:
+            dist.destroy_process_group()
+        return
+    from skybox_rt_amd import rt
+
+    shadows = not args.no_shadows
+    light = rt.DEFAULT_LIGHT
+    side = args.size
+    scene = rt.Scene.load(SCENE)
+    info = scene.info()
+    r = rt.Renderer(scene)
+
+    def make_run(s):
+        return Run(r, rt, dist, coll_dev, rank, n_gpus, s, shadows, light, path, flat,
+                   args.bounces, use_gather)
+
+    run = make_run(side)
+    inst = run.inst
+    bvh_kind = ("BVH4 (binary16 boxes)" if r.bvh4_f16 else "BVH4") if r.bvh4 else "BVH2"
+    alg_bytes = algorithmic_bytes(inst, inst["primary_rays"], (NODE4H_BYTES if r.bvh4_f16 else NODE4_BYTES)
+                                  if r.bvh4 else NODE_BYTES)
+    # synchronous frames first (start + wait per frame, simx's blocking
+    # start): reported beside the pipelined rate, not as `value`
+    sync_ms = None
+    if not use_gather:
+        sync_n = max(5, min(args.steps, 50))
+        for _ in range(2):
+            r.render()
+        t_s = time.perf_counter()
+        for _ in range(sync_n):
+            r.render()
+        sync_ms = (time.perf_counter() - t_s) / sync_n * 1e3
     # a step = one frame: vx_start queues the launch behind the in-flight
     # frame (driver VX_HIP_QUEUE_DEPTH, default 2) so the host's launch and
     # completion-poll overhead overlaps the previous frame; every frame is
-    # complete before the timed region ends (wait + synchronize below)
-    def step():
-        r.start()
-        if gather is not None:
-            gather()
-
-    # synchronous frames first (start + wait per frame, simx's blocking
-    # start): reported beside the pipelined rate, not as `value`
-    sync_n = max(5, min(args.steps, 50))
-    for _ in range(2):
-        r.render()
-    t_s = time.perf_counter()
-    for _ in range(sync_n):
-        r.render()
-    sync_ms = (time.perf_counter() - t_s) / sync_n * 1e3
-    for _ in range(args.warmup):
-        step()
-    r.wait()
-    if gather is not None:
-        for slot in range(fg_slots):
-            fg.reclaim(slot)
-    if dist is not None:
-        dist.barrier()
-    torch.cuda.synchronize()
-    ms0, nt0, n0 = r.run_totals()
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        step()
-    r.wait()
-    if gather is not None:  # every frame gathered and assembled inside the timed region
-        for slot in range(fg_slots):
-            fg.reclaim(slot)
-    torch.cuda.synchronize()
-    if dist is not None:
-        dist.barrier()
-    elapsed = time.perf_counter() - t0
-    ms1, nt1, n1 = r.run_totals()
-    assert n1 - n0 == args.steps and nt1 > nt0, (n0, n1, nt0, nt1)
+    # complete before the timed region ends
+    elapsed, avg_kernel_ms, timed_launches = run.timed(args.steps, args.warmup, dist)
     st = r.stats()
-    rays_local = st["primary_rays"] + st["shadow_rays"] + st["bounce_rays"]
-    if dist is not None:
-        t = torch.tensor([elapsed, float(rays_local)], dtype=torch.float64, device=coll_dev)
-        mx = t.clone()
-        dist.all_reduce(mx, op=dist.ReduceOp.MAX)
-        sm = t.clone()
-        dist.all_reduce(sm, op=dist.ReduceOp.SUM)
-        elapsed, rays_total = float(mx[0]), float(sm[1])
-    else:
-        rays_total = float(rays_local)
+    elapsed, rays_total = reduce_max_sum(dist, coll_dev, elapsed, run.rays_local)
     ms_per_step = elapsed / args.steps * 1e3
     value = rays_total * args.steps / elapsed / 1e6
-    # HIP-event time of the timed launches of the timed region (one in
-    # VX_HIP_TIME_EVERY of the queued frames carries events)
-    avg_kernel_ms = (ms1 - ms0) / (nt1 - nt0)
-    timed_launches = nt1 - nt0
     achieved = alg_bytes / (avg_kernel_ms * 1e-3) / 1e9
     gather_ok = None
-    if gather is not None and args.verify_gather and rank == 0:
+    if use_gather and args.verify_gather:
+        image = run.fg.image.cpu().numpy() if rank == 0 else None
         r.configure(side, side, shadows=shadows, light=light, path=path, bounces=args.bounces,
                     flat=flat)
-        r.render()
-        full = r.framebuffer().reshape(-1).view(np.int32)
-        gather_ok = bool(np.array_equal(fg.image.cpu().numpy(), full))
-        log(f"gathered frame == full render: {gather_ok}")
+        if rank == 0:
+            r.render()
+            full = r.framebuffer().reshape(-1).view(np.int32)
+            gather_ok = bool(np.array_equal(image, full))
+            log(f"gathered frame == full render: {gather_ok}")
+    # scaling series: the same render at 4096^2 on these N GPUs (strong) and
+    # at ~1024^2 * sqrt(N) (weak); short runs, reported beside `value`
+    series = {}
+    if not args.no_series and not flat:
+        series_steps = max(20, min(args.steps, 200))
+        for name, s in (("strong_4096", CONFIG5_SIDE), ("weak_1024_sqrtN", frame_side(n_gpus, 1024))):
+            if s == side:
+                series[name] = {"side": s, "value": round(value, 3), "ms_per_step": round(ms_per_step, 5),
+                                "same_as": "value"}
+                continue
+            sr = make_run(s)
+            e2, k2, _ = sr.timed(series_steps, 10, dist)
+            e2, rays2 = reduce_max_sum(dist, coll_dev, e2, sr.rays_local)
+            series[name] = {"side": s, "steps": series_steps,
+                            "value": round(rays2 * series_steps / e2 / 1e6, 3),
+                            "ms_per_step": round(e2 / series_steps * 1e3, 5),
+                            "kernel_ms": round(k2, 5), "rays_per_frame": int(rays2)}
     if rank != 0:
         dist.destroy_process_group()
         return
+    config5 = n_gpus > 1 and side == CONFIG5_SIDE
     metric = "Mrays/sec per GPU + achieved HBM GB/s, 1024^2 primary+shadow tekkaman"
     kind = "primary+shadow rays"
     if path:
@@ -313,6 +487,20 @@ def main():
         metric = (f"Mrays/sec per GPU + achieved HBM GB/s, {side}^2 primary rays, tekkaman flat "
                   f"triangle list, no BVH (BASELINE config 2)")
         kind = "primary rays, flat triangle list (no BVH, LDS-staged)"
+    if flat:
+        workload = f"{side}x{side} {kind}, tekkaman.cgltrace"
+    elif path:
+        workload = f"{side}x{side} {kind}, tekkaman.cgltrace, {bvh_kind} + LDS stack"
+    else:
+        workload = (f"{side}x{side} {'primary+shadow' if shadows else 'primary'} rays, "
+                    f"tekkaman.cgltrace, {bvh_kind} + LDS stack")
+    if n_gpus > 1:
+        workload += (f", tile-sharded over {n_gpus} GPUs (32x32 tile t -> rank t mod {n_gpus}) + "
+                     f"{'RCCL' if backend == 'nccl' else backend} gather to rank 0"
+                     + (" (BASELINE config 5)" if config5 else ""))
+    mode = "path" if path else ("flat" if flat else "shadow")
+    rec, stale = pmc_record(mode, side) if n_gpus == 1 else (None, False)
+    traffic = rec["traffic_bytes"] if rec else None
     out = {
         "metric": metric,
         "value": round(value, 3),
@@ -322,19 +510,17 @@ def main():
         "warmup": args.warmup,
         "ms_per_step": round(ms_per_step, 5),
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": "strong" if n_gpus > 1 else "weak",
         "vs_baseline": None,
         "dtype": "f32",
         "data": "tekkaman.cgltrace from the reference's regression data (tests/golden/scenes)",
         "config": {
-            "workload": (f"{side}x{side} {kind}, tekkaman.cgltrace" if flat else
-                         f"{side}x{side} {kind}, tekkaman.cgltrace, {bvh_kind} + LDS stack" if path else
-                         f"{side}x{side} {'primary+shadow' if shadows else 'primary'} rays, "
-                         f"tekkaman.cgltrace, {bvh_kind} + LDS stack"),
+            "workload": workload,
             "scene": "tekkaman.cgltrace", "width": side, "height": side,
             "shadow_rays": shadows, "light_clip_xyw": list(light),
             "parallelism": f"tiles32 mod {n_gpus}" + (f" + {'rccl' if backend == 'nccl' else backend} "
                                                       f"gather" if n_gpus > 1 else ""),
+            "ranks_seen": ranks_seen,
             "bvh_nodes": info["bvh4_nodes" if r.bvh4 else "bvh_nodes"],
             "bvh_depth": info["bvh4_depth" if r.bvh4 else "bvh_depth"],
             "grid": st["grid"], "block": st["block"],
@@ -344,13 +530,15 @@ def main():
             "frames": "queued (vx_start behind the in-flight frame, depth "
                       f"{os.environ.get('VX_HIP_QUEUE_DEPTH', '2')}); kernel_ms = HIP events on "
                       f"{timed_launches} of the {args.steps} timed launches",
-            "sync_ms_per_step": round(sync_ms, 5),
-            "kernel_mrays_per_s": round(rays_local / (avg_kernel_ms * 1e-3) / 1e6, 3),
+            "sync_ms_per_step": round(sync_ms, 5) if sync_ms is not None else None,
+            "kernel_mrays_per_s": round(run.rays_local / (avg_kernel_ms * 1e-3) / 1e6, 3),
+            "counters": "off in the timed frames (rays per frame from the instrumented pre-run)",
         },
+        "series": series,
         "roofline": {
             "bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBS, 4),
-            "traffic": pmc_traffic(side, shadows, "path" if path else ("flat" if flat else "shadow")),
+            "traffic": traffic,
             "algorithmic_bytes_per_launch": int(alg_bytes),
             "counts": {k: int(inst[k]) for k in ("node_visits", "tri_tests", "layer_tests",
                                                  "texel_bytes", "primary_rays", "shadow_rays",
@@ -358,6 +546,28 @@ def main():
         },
         "cpu_baseline": None,
     }
+    if stale:
+        out["roofline"]["traffic_stale"] = True
+    if rec:
+        # measured HBM bytes per launch over the same kernel time: the share of
+        # the HBM peak the kernel physically uses (the scene is cache-resident)
+        out["roofline"]["measured_hbm_gbs"] = round(traffic / (avg_kernel_ms * 1e-3) / 1e9, 2)
+        out["roofline"]["measured_hbm_frac"] = round(traffic / (avg_kernel_ms * 1e-3) / 1e9
+                                                     / HBM_PEAK_GBS, 4)
+        out["roofline"]["pmc_source"] = f"profiles/pmc_{mode}.json"
+        d = rec.get("derived", {})
+        if rec.get("sq", {}).get("SQ_INSTS_VALU"):
+            # the binding resource: VALU issue (and what the waves wait on)
+            gips = rec["sq"]["SQ_INSTS_VALU"] / (avg_kernel_ms * 1e-3) / 1e9
+            out["roofline_issue"] = {
+                "bound": "valu_issue", "achieved": round(gips, 2), "peak": VALU_ISSUE_PEAK_GIPS,
+                "unit": "G wave-instr/s", "frac": round(gips / VALU_ISSUE_PEAK_GIPS, 4),
+                "valu_insts_per_launch": int(rec["sq"]["SQ_INSTS_VALU"]),
+                **{k: d[k] for k in ("wait_any_frac", "wait_inst_any_frac", "active_inst_any_frac",
+                                     "active_inst_valu_frac", "valu_lane_utilisation",
+                                     "l1_hit_rate", "l2_hit_rate") if k in d},
+                "source": f"profiles/pmc_{mode}.json (rocprofv3 --pmc passes, scripts/pmc_profile.sh)",
+            }
     if flat:
         # the flat list is read from LDS, never from HBM: its bound is the MT
         # arithmetic -- SURVEY 8(d): ~40 fp32 ops per test, 157.3 TFLOP/s vector peak

@@ -130,6 +130,9 @@
 
 /* DCR mirror size shipped to every launch (covers 0x000..0x03F) */
 #define VX_DCR_MIRROR_SIZE 64
+/* HIP-driver word of the device DCR mirror (beyond the reference's DCRs):
+ * nonzero = kernels write their per-block counter rows (vx_spawn.h) */
+#define VX_DCR_HIP_MPM_ROWS 0x03F
 
 /* ---- performance counters (VX_types.vh:71-77) ---- */
 #define VX_CSR_MPM_BASE  0xB00

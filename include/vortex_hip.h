@@ -36,6 +36,12 @@ typedef int (*vx_hip_run_totals_t)(vx_device_h hdevice, double* kernel_ms_sum,
  * *nrows = grid.  Diagnostics (e.g. in-kernel timestamps). */
 typedef int (*vx_hip_mpm_rows_t)(vx_device_h hdevice, uint32_t* rows, uint64_t max_rows,
                                  uint64_t* nrows);
+/* per-block counter rows on (1) / off (0, the default): with them off a
+ * launch writes no counters -- vx_mpm_query returns its spawned task count
+ * for VX_CSR_MINSTRET, device time for VX_CSR_MCYCLE and 0 otherwise.
+ * VORTEX_PROFILING (the stub's MPM_CLASS DCR) or env VX_HIP_COUNTERS=1 turn
+ * them on as well. */
+typedef int (*vx_hip_set_counters_t)(vx_device_h hdevice, int enable);
 
 #ifdef __cplusplus
 }

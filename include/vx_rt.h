@@ -41,6 +41,10 @@ typedef struct {
 #define RT_RENDER_INSTRUMENTED 0x100u  /* use the counting kernel variant */
 #define RT_RENDER_COMPACT 0x200u       /* compact tile-order output (the shard layout,
                                           implied by shard_count > 1) for one shard too */
+#define RT_RENDER_COUNTERS 0x400u      /* per-workgroup counter rows on (vx_hip_set_counters):
+                                          rt_render_stats' ray / hit counts; implied by
+                                          RT_RENDER_INSTRUMENTED.  Off, a frame writes only
+                                          its framebuffer (and one task-count word) */
 
 typedef struct {
   uint32_t width, height;
@@ -54,7 +58,7 @@ typedef struct {
 } rt_render_params_t;
 
 typedef struct {
-  uint64_t primary_rays, shadow_rays, geometry_hits, occluded;
+  uint64_t primary_rays, shadow_rays, geometry_hits, occluded;      /* RT_RENDER_COUNTERS */
   uint64_t node_visits, tri_tests, layer_tests, shaded, texel_bytes; /* instrumented only */
   uint64_t tasks;             /* VX_CSR_MINSTRET */
   double kernel_ms;           /* HIP-event time of the last launch */

@@ -29,7 +29,9 @@
  *    exactly once with blockIdx = the vx_spawn.c:75-80 decomposition.
  *  - Perf counters (vx_mpm_add): LDS counters per block, written as one
  *    64-B row per block at block exit (plain stores, no global atomics, no
- *    per-launch memset); vx_mpm_query sums the rows of the last launch.
+ *    per-launch memset) when the driver enables counters; vx_mpm_query
+ *    sums the rows of the last launch.  Without counters a launch writes
+ *    one word (the task count) beside its output.
  *  - group_size > 1 (vx_spawn.c:187-246) is not supported yet: returns -1.
  */
 #ifndef VX_SPAWN_H
@@ -44,11 +46,17 @@
 #define VX_MAX_GRID 32768    /* blocks per launch (rows of the counter slab) */
 
 /* per-launch device state: one 64-B row of the first VX_MPM_ROW u32 mpm
- * counters per block, each written by its block at exit (kernel programs
- * count into slots < VX_MPM_ROW; vx_mpm_query reads the others as 0) */
+ * counters per block, each written by its block at exit -- only when the
+ * driver asks for counters (DCR mirror word VX_DCR_HIP_MPM_ROWS: profiling
+ * requested, as VORTEX_PROFILING gates the reference's perf classes,
+ * runtime/stub/utils.cpp:25-47); kernel programs count into slots <
+ * VX_MPM_ROW, vx_mpm_query reads the others as 0.  `tasks` = the task count
+ * the launch spawned, one word written by block 0 every launch
+ * (vx_mpm_query(MINSTRET) without counter rows). */
 #define VX_MPM_ROW 16
 typedef struct {
   uint32_t mpm[VX_MAX_GRID][VX_MPM_ROW];
+  uint32_t tasks;
 } vx_state_t;
 
 /* Filled by the driver before every launch (hip_driver.cpp, start()). */
@@ -155,6 +163,11 @@ __device__ __forceinline__ void vx_mpm_add(int slot, uint32_t v) {
   if ((threadIdx.x & 63u) == 0 && s && slot < VX_MPM_ROW) atomicAdd(&__vx_mpm_lds[slot], s);
 }
 
+/* block 0 records how many tasks the launch spawns (all lanes may call) */
+__device__ __forceinline__ void __vx_declare_tasks(uint32_t n) {
+  if (blockIdx.x == 0 && threadIdx.x == 0) __vx_state.tasks = n;
+}
+
 struct __vx_no_epilogue {
   template <typename Arg>
   __device__ __forceinline__ void operator()(bool, Arg*) const {}
@@ -179,6 +192,7 @@ __device__ __forceinline__ int vx_spawn_threads_ex(uint32_t dimension, const uin
     group_size *= bd;
   }
   if (group_size != 1) return -1;
+  __vx_declare_tasks(num_groups);
   const uint32_t nchunks = (num_groups + VX_CHUNK - 1) / VX_CHUNK;
   const uint32_t nwaves = gridDim.x * (blockDim.x >> 6);
   uint32_t ran = 0;
@@ -231,6 +245,7 @@ template <typename F, typename E, typename Arg>
 __device__ __forceinline__ int vx_spawn_tasks_block(uint32_t num_tasks, F kernel_func,
                                                     E block_epilogue, Arg* arg) {
   const uint32_t nsteps = (num_tasks + blockDim.x - 1) / blockDim.x;
+  __vx_declare_tasks(num_tasks);
   uint32_t ran = 0;
   vx_task_t task;
   task.threadIdx.x = task.threadIdx.y = task.threadIdx.z = 0;
@@ -257,6 +272,7 @@ __device__ __forceinline__ int vx_spawn_tasks_block(uint32_t num_tasks, F kernel
 template <typename F, typename Arg>
 __device__ __forceinline__ int vx_spawn_chunks_block(uint32_t num_tasks, F kernel_func, Arg* arg) {
   const uint32_t nchunks = (num_tasks + VX_CHUNK - 1) / VX_CHUNK;
+  __vx_declare_tasks(num_tasks);
   uint32_t ran = 0;
   vx_task_t task;
   task.threadIdx.x = task.threadIdx.y = task.threadIdx.z = 0;
@@ -290,7 +306,8 @@ __device__ __forceinline__ int vx_spawn_chunks_block(uint32_t num_tasks, F kerne
                        (uint64_t)__vx_dcrs[VX_DCR_BASE_STARTUP_ARG0];                \
     (void)__vx_main_body(vx_ptr<ArgT>(a));                                           \
     __syncthreads();                                                                 \
-    if (threadIdx.x < VX_MPM_ROW && blockIdx.x < VX_MAX_GRID)                        \
+    if (__vx_dcrs[VX_DCR_HIP_MPM_ROWS] && threadIdx.x < VX_MPM_ROW &&                \
+        blockIdx.x < VX_MAX_GRID)                                                    \
       __vx_state.mpm[blockIdx.x][threadIdx.x] = __vx_mpm_lds[threadIdx.x];           \
   }                                                                                  \
   static __device__ __forceinline__ int __vx_main_body(ArgT* argname)

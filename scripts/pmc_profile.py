@@ -1,0 +1,86 @@
+#!/usr/bin/env python3
+"""Reduce the rocprofv3 --pmc passes of scripts/pmc_profile.sh for one mode to
+the record bench.py reports (profiles/pmc_<mode>.json): per-launch means over
+the vx_main dispatches of every counter, HBM traffic and derived ratios.
+
+HBM correction (MI355X_MICROARCH.md, HBM section): on gfx950 FETCH_SIZE counts
+64 B per 128-B memory-side read request, i.e. half of the bytes of a wide
+coalesced read, so the read side is doubled; WRITE_SIZE is taken as is.  Both
+are in KB.  SQ_WAVE_CYCLES / SQ_WAIT_* / SQ_ACTIVE_INST_* count quad-cycles
+(summed over waves), so their ratios are what is meaningful.
+Usage: pmc_profile.py <tag_dir> <mode> <side> <kernel .co> <out.json>"""
+import csv
+import glob
+import hashlib
+import json
+import os
+import sys
+from collections import defaultdict
+
+
+def means(d):
+    """counter -> mean over dispatches of vx_main (values summed per dispatch)."""
+    per = defaultdict(lambda: defaultdict(float))
+    for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
+        with open(f) as fh:
+            for row in csv.DictReader(fh):
+                if row["Kernel_Name"] != "vx_main":
+                    continue
+                per[row["Counter_Name"]][row["Dispatch_Id"]] += float(row["Counter_Value"])
+    return {c: sum(v.values()) / len(v) for c, v in per.items() if v}, \
+        {c: len(v) for c, v in per.items()}
+
+
+def main():
+    tag, mode, side, co, out = sys.argv[1:6]
+    side = int(side)
+    m, nd = {}, {}
+    for d in sorted(glob.glob(os.path.join(tag, f"{mode}_*"))):
+        if os.path.isdir(d):
+            a, b = means(d)
+            m.update(a)
+            nd.update(b)
+    if "FETCH_SIZE" not in m or "WRITE_SIZE" not in m:
+        sys.exit("no vx_main dispatches with FETCH_SIZE / WRITE_SIZE")
+    g = m.get
+    der = {}
+    wc = g("SQ_WAVE_CYCLES")
+    if wc:
+        for k, n in (("SQ_WAIT_ANY", "wait_any_frac"), ("SQ_WAIT_INST_ANY", "wait_inst_any_frac"),
+                     ("SQ_ACTIVE_INST_ANY", "active_inst_any_frac"),
+                     ("SQ_ACTIVE_INST_VALU", "active_inst_valu_frac"),
+                     ("SQ_ACTIVE_INST_LDS", "active_inst_lds_frac"),
+                     ("SQ_WAIT_INST_LDS", "wait_inst_lds_frac")):
+            if g(k) is not None:
+                der[n] = round(m[k] / wc, 4)
+    if g("SQ_WAVES"):
+        for k in ("SQ_INSTS_VALU", "SQ_INSTS_SALU", "SQ_INSTS_VMEM_RD", "SQ_INSTS_LDS",
+                  "SQ_INSTS_SMEM", "SQ_INSTS_VMEM_WR"):
+            if g(k) is not None:
+                der[k.lower().replace("sq_insts_", "") + "_insts_per_wave"] = round(m[k] / m["SQ_WAVES"], 1)
+    if g("SQ_THREAD_CYCLES_VALU") and g("SQ_ACTIVE_INST_VALU"):
+        der["valu_lane_utilisation"] = round(m["SQ_THREAD_CYCLES_VALU"] / (64 * m["SQ_ACTIVE_INST_VALU"]), 4)
+    if g("TCC_HIT_sum") is not None and g("TCC_MISS_sum") is not None and m["TCC_HIT_sum"] + m["TCC_MISS_sum"]:
+        der["l2_hit_rate"] = round(m["TCC_HIT_sum"] / (m["TCC_HIT_sum"] + m["TCC_MISS_sum"]), 4)
+    if g("TCP_TOTAL_CACHE_ACCESSES_sum") and g("TCP_TCC_READ_REQ_sum") is not None:
+        der["l1_hit_rate"] = round(1.0 - m["TCP_TCC_READ_REQ_sum"] / m["TCP_TOTAL_CACHE_ACCESSES_sum"], 4)
+    f_kb, w_kb = m["FETCH_SIZE"], m["WRITE_SIZE"]
+    res = {
+        "kernel": "vx_main", "mode": mode, "width": side, "height": side,
+        "kernel_image": os.path.basename(co),
+        "kernel_md5": hashlib.md5(open(co, "rb").read()).hexdigest(),
+        "dispatches": nd,
+        "fetch_size_kb": round(f_kb, 1), "write_size_kb": round(w_kb, 1),
+        "correction": "read bytes = 2 x FETCH_SIZE x 1024 (gfx950 half-count), write = WRITE_SIZE x 1024",
+        "traffic_bytes": int(2 * f_kb * 1024 + w_kb * 1024),
+        "sq": {k: round(v, 1) for k, v in sorted(m.items()) if k not in ("FETCH_SIZE", "WRITE_SIZE")},
+        "derived": der,
+        "source": "scripts/pmc_profile.sh (rocprofv3 --pmc, one pass per counter group)",
+    }
+    with open(out, "w") as fh:
+        json.dump(res, fh, indent=1)
+    print(json.dumps(res))
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,32 @@
+# rocprofv3 PMC record of one bench workload's kernel image: HBM traffic
+# (FETCH_SIZE and WRITE_SIZE, separate passes) and the SQ / TCP / TCC counters
+# that name the binding resource, one --pmc pass per counter group within the
+# per-block limits (8 SQ, 4 TCC, 4 TCP, 2 GRBM), each over
+# scripts/prof_rt.py (the product configuration: counters off), reduced by
+# scripts/pmc_profile.py into gpurun_out/$TAG/pmc_<mode>.json.
+# MODE = shadow (config 3, default), path (config 4) or flat (config 2).
+set -o pipefail
+cd "$GRAFT_REPO_ROOT"
+export TMPDIR=/tmp
+TAG=${TAG:-pmc}; mkdir -p gpurun_out/$TAG
+MODE=${MODE:-shadow}
+case $MODE in
+  shadow) CO=rt_kernel.co; SZ=1024 ;;
+  path)   CO=pt_kernel.co; SZ=1024 ;;
+  flat)   CO=rt_flat.co;   SZ=256 ;;
+  *) echo "bad MODE $MODE"; exit 2 ;;
+esac
+pass() {  # name, counters...
+  local name=$1; shift
+  timeout -s KILL 90 rocprofv3 --pmc "$@" -d gpurun_out/$TAG/${MODE}_$name -o run --output-format csv -- python3 scripts/prof_rt.py --mode $MODE --frames 10 > gpurun_out/$TAG/${MODE}_$name.log 2>&1
+  local rc=$?
+  echo "pmc $MODE $name rc=$rc"
+  return $rc
+}
+pass fetch FETCH_SIZE || exit $?
+pass write WRITE_SIZE || exit $?
+pass sq1 SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY GRBM_GUI_ACTIVE || exit $?
+pass sq2 SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_VMEM_RD SQ_INSTS_LDS SQ_INSTS_SMEM SQ_INSTS_VMEM_WR || exit $?
+pass sq3 SQ_ACTIVE_INST_VALU SQ_THREAD_CYCLES_VALU SQ_ACTIVE_INST_LDS SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT || exit $?
+pass mem TCP_TOTAL_CACHE_ACCESSES_sum TCP_TCC_READ_REQ_sum TCC_HIT_sum TCC_MISS_sum || exit $?
+python3 scripts/pmc_profile.py gpurun_out/$TAG $MODE $SZ skybox_rt_amd/lib/$CO gpurun_out/$TAG/pmc_$MODE.json

@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""Summarize rocprofv3 --pmc passes (scripts/gpu_pmc.sh layout) for one kernel:
+"""Summarize rocprofv3 --pmc passes (scripts/pmc_profile.sh layout) for one kernel:
 mean value of every counter over that kernel's dispatches, plus derived
 ratios.  Usage: pmc_summary.py gpurun_out/<TAG> [kernel_name]"""
 import csv

@@ -15,6 +15,8 @@ def main():
     ap.add_argument("--no-shadows", action="store_true")
     ap.add_argument("--kernel-dir", default=None)
     ap.add_argument("--mode", choices=("shadow", "path", "flat"), default="shadow")
+    ap.add_argument("--counters", action="store_true",
+                    help="counter rows on (default off: the timed product configuration)")
     args = ap.parse_args()
     import torch  # noqa: F401
     from skybox_rt_amd import rt
@@ -23,7 +25,7 @@ def main():
     flat = args.mode == "flat"
     size = 256 if flat and args.size == 1024 else args.size   # bench.py's config-2 size
     r.configure(size, size, shadows=not (args.no_shadows or flat), path=args.mode == "path",
-                flat=flat)
+                flat=flat, counters=args.counters)
     for _ in range(args.frames):
         r.render()
     print(r.stats(), file=sys.stderr)

@@ -86,7 +86,8 @@ int main(int argc, char** argv) {
   p.width = width;
   p.height = height;
   p.flags = (shadows ? RT_RENDER_SHADOWS : 0u) | (raster ? RT_RENDER_RASTER : 0u) |
-            (flat ? RT_RENDER_FLAT : 0u) | (bounces >= 0 ? RT_RENDER_PATH : 0u);
+            (flat ? RT_RENDER_FLAT : 0u) | (bounces >= 0 ? RT_RENDER_PATH : 0u) |
+            RT_RENDER_COUNTERS;  // the CLI prints ray counts
   p.bounces = bounces >= 0 ? (uint32_t)bounces : 0u;
   p.seed = 0x5EED;
   std::memcpy(p.light, light, sizeof(light));

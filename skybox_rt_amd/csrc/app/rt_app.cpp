@@ -90,6 +90,7 @@ struct rt_renderer {
   vx_hip_last_run_t last_run = nullptr;
   vx_hip_mpm_rows_t mpm_rows = nullptr;
   vx_hip_run_totals_t run_totals = nullptr;
+  vx_hip_set_counters_t set_counters = nullptr;
   std::string kdir;         // kernel directory (images missing there come from lib_dir)
   bool deep = false;        // RT/PT images with the 32-entry traversal stack
   bool gpu_bvh = false;     // nodes/tris were built on the device (rt_renderer_build_bvh)
@@ -272,6 +273,7 @@ int rt_renderer_create(rt_scene_h s, const char* kernel_dir, rt_renderer_h* out)
   r->last_run = (vx_hip_last_run_t)vx_driver_symbol("vx_hip_last_run");
   r->mpm_rows = (vx_hip_mpm_rows_t)vx_driver_symbol("vx_hip_mpm_rows");
   r->run_totals = (vx_hip_run_totals_t)vx_driver_symbol("vx_hip_run_totals");
+  r->set_counters = (vx_hip_set_counters_t)vx_driver_symbol("vx_hip_set_counters");
   rt_kernel_arg_t& a = r->arg;
   std::memset(&a, 0, sizeof(a));
   const rt::Bvh& bvh = s->bvh;
@@ -520,6 +522,10 @@ int rt_render_start(rt_renderer_h r) {
   const uint32_t f = r->params.flags;
   const int mode = (f & RT_RENDER_PATH) ? 1 : (f & RT_RENDER_FLAT) ? 2 : (f & RT_RENDER_RASTER) ? 3 : 0;
   const int k = (f & RT_RENDER_INSTRUMENTED) && mode != 3 ? 1 : 0;
+  // counter rows only when the caller wants rt_render_stats' counts
+  if (r->set_counters &&
+      r->set_counters(r->dev, (f & (RT_RENDER_COUNTERS | RT_RENDER_INSTRUMENTED)) ? 1 : 0) != 0)
+    return fail("vx_hip_set_counters failed");
   return vx_start(r->dev, r->krnl[mode][k], r->args) == 0 ? 0 : fail("vx_start failed");
 }
 

@@ -202,6 +202,8 @@ int rt_tex_create(const char* kernel_dir, rt_tex_h* out) {
       return set_error("cannot upload kernel " + path);
   }
   t->last_run = (vx_hip_last_run_t)vx_driver_symbol("vx_hip_last_run");
+  // the tex app reports its pixel counter (rt_tex_stats): counter rows on
+  if (auto sc = (vx_hip_set_counters_t)vx_driver_symbol("vx_hip_set_counters")) sc(t->dev, 1);
   *out = t.release();
   return 0;
 }

@@ -27,7 +27,13 @@
 //   * mpm_query       = event-timed device ns (MCYCLE) and task count
 //                       (MINSTRET) of the last run;
 //   * __vx_state      = per-launch device state: one counter row per block,
-//                       written by the block at exit (no per-launch memset).
+//                       written by the block at exit (no per-launch memset)
+//                       only while counters are on -- VORTEX_PROFILING set
+//                       (the stub's MPM_CLASS DCR, as the reference gates its
+//                       perf classes, runtime/stub/utils.cpp:25-47), env
+//                       VX_HIP_COUNTERS=1 or vx_hip_set_counters(); without
+//                       them a launch writes only its task count (MINSTRET)
+//                       and the other counters read 0.
 // Error behaviour mirrors callbacks.inc: null handles / zero sizes / ranges
 // past the buffer -> -1; unknown caps id -> -1 (simx aborts).
 #include <hip/hip_runtime.h>
@@ -62,6 +68,7 @@ constexpr uint64_t kDefaultArenaMB = 4096;
 // one row of the first kMpmRow counters per block, written at block exit
 constexpr uint32_t kMaxGrid = 32768;
 constexpr uint32_t kMpmRow = 16;
+constexpr size_t kTasksOffset = (size_t)kMaxGrid * kMpmRow * sizeof(uint32_t);  // vx_state_t::tasks
 constexpr int kGridWavesPerCU = 64;  // 4x the 16 resident waves/CU of the RT kernel
 
 uint64_t env_u64(const char* name, uint64_t dflt) {
@@ -139,6 +146,7 @@ class vx_device {
     const uint64_t te = env_u64("VX_HIP_TIME_EVERY", 4);
     time_every_ = te < 1 ? 1 : te > 16 ? 16 : (int)te;
     launch_mode_ = (int)env_u64("VX_HIP_EXT_LAUNCH", 1);
+    counters_env_ = env_u64("VX_HIP_COUNTERS", 0) != 0;
     return 0;
   }
 
@@ -232,6 +240,10 @@ class vx_device {
     dcr_set(VX_DCR_BASE_STARTUP_ADDR1, (uint32_t)(krnl_addr >> 32));
     dcr_set(VX_DCR_BASE_STARTUP_ARG0, (uint32_t)(args_addr & 0xffffffffu));
     dcr_set(VX_DCR_BASE_STARTUP_ARG1, (uint32_t)(args_addr >> 32));
+    // per-block counter rows only when counters are wanted (vx_spawn.h)
+    const bool rows = counters_ || counters_env_ ||
+                      (dcr_valid_[VX_DCR_BASE_MPM_CLASS] && dcrs_[VX_DCR_BASE_MPM_CLASS] != 0);
+    dcr_set(VX_DCR_HIP_MPM_ROWS, rows ? 1u : 0u);
     Module* m = nullptr;
     if (load_module(krnl_addr, &m) != 0) return -1;
     // constant blocks are only re-sent when they changed since this module's
@@ -283,6 +295,7 @@ class vx_device {
     }
     ++issued_;
     mpm_dirty_ = true;  // read back lazily by mpm_query (after wait_idle)
+    last_rows_ = rows;
     last_module_ = m;
     last_grid_ = m->grid;
     last_block_ = m->block;
@@ -351,14 +364,22 @@ class vx_device {
       *value = (uint64_t)(last_ms_ * 1.0e6 + 0.5);
       return 0;
     }
-    if (mpm_dirty_) {  // sum the per-block counter rows of the last launch
-      rows_.resize((size_t)last_grid_ * kMpmRow);
-      HIP_CHECK(hipMemcpyAsync(rows_.data(), last_module_->mpm, rows_.size() * sizeof(uint32_t),
-                               hipMemcpyDeviceToHost, stream_));
-      HIP_CHECK(hipStreamSynchronize(stream_));
+    if (mpm_dirty_ && last_module_) {
       for (uint32_t i = 0; i < VX_MPM_COUNT; ++i) mpm_[i] = 0;
-      for (size_t b = 0; b < last_grid_; ++b)
-        for (uint32_t i = 0; i < kMpmRow; ++i) mpm_[i] += rows_[b * kMpmRow + i];
+      if (last_rows_) {  // sum the per-block counter rows of the last launch
+        rows_.resize((size_t)last_grid_ * kMpmRow);
+        HIP_CHECK(hipMemcpyAsync(rows_.data(), last_module_->mpm, rows_.size() * sizeof(uint32_t),
+                                 hipMemcpyDeviceToHost, stream_));
+        HIP_CHECK(hipStreamSynchronize(stream_));
+        for (size_t b = 0; b < last_grid_; ++b)
+          for (uint32_t i = 0; i < kMpmRow; ++i) mpm_[i] += rows_[b * kMpmRow + i];
+      } else {  // counters off: the task count the launch declared
+        uint32_t tasks = 0;
+        HIP_CHECK(hipMemcpyAsync(&tasks, (uint8_t*)last_module_->mpm + kTasksOffset, 4,
+                                 hipMemcpyDeviceToHost, stream_));
+        HIP_CHECK(hipStreamSynchronize(stream_));
+        mpm_[VX_CSR_MINSTRET - VX_CSR_MPM_BASE] = tasks;
+      }
       mpm_dirty_ = false;
     }
     *value = mpm_[off];
@@ -376,6 +397,8 @@ class vx_device {
     HIP_CHECK(hipStreamSynchronize(stream_));
     return 0;
   }
+  void set_counters(bool on) { counters_ = on; }  // applies from the next start()
+  bool counters() const { return counters_ || counters_env_; }
   void* mem_ptr(uint64_t addr) { return arena_ + addr; }
   hipStream_t stream() const { return stream_; }
   int device_id() const { return device_id_; }
@@ -448,7 +471,7 @@ class vx_device {
     if (per_cu < 1) per_cu = 1;
     m.grid = (uint32_t)(props_.multiProcessorCount * per_cu);
     if (m.grid > kMaxGrid) m.grid = kMaxGrid;
-    if (m.mpm_size < (size_t)m.grid * kMpmRow * sizeof(uint32_t)) {
+    if (m.mpm_size < kTasksOffset + sizeof(uint32_t)) {
       std::printf("[VXDRV] kernel image has no per-block counter slab\n");
       return -1;
     }
@@ -482,6 +505,7 @@ class vx_device {
   uint64_t runs_total_ = 0;
   Module* last_module_ = nullptr;
   bool mpm_dirty_ = false;
+  bool counters_ = false, counters_env_ = false, last_rows_ = false;
   double last_ms_ = 0.0;
   uint32_t last_grid_ = 0, last_block_ = 0;
   uint32_t dcrs_[VX_DCR_MIRROR_SIZE] = {};
@@ -621,6 +645,11 @@ __attribute__((visibility("default"))) int vx_hip_mpm_rows(vx_device_h hdevice, 
                                                            uint64_t max_rows, uint64_t* nrows) {
   if (hdevice == nullptr) return -1;
   return ((vx_device*)hdevice)->mpm_rows(rows, max_rows, nrows);
+}
+__attribute__((visibility("default"))) int vx_hip_set_counters(vx_device_h hdevice, int enable) {
+  if (hdevice == nullptr) return -1;
+  ((vx_device*)hdevice)->set_counters(enable != 0);
+  return 0;
 }
 __attribute__((visibility("default"))) int vx_hip_device_id(vx_device_h hdevice, int* id) {
   if (hdevice == nullptr || id == nullptr) return -1;

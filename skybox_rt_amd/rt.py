@@ -27,6 +27,7 @@ RT_RENDER_BVH2 = 0x40
 PT_SEED = 0x5EED
 RT_RENDER_INSTRUMENTED = 0x100
 RT_RENDER_COMPACT = 0x200
+RT_RENDER_COUNTERS = 0x400
 RT_BVH_STACK4_UNUSED = 0xFFFFFFFF
 CLEAR_COLOR = 0xFF000000               # draw3d/main.cpp:47
 DEFAULT_LIGHT = (0.0, 60.0, 80.0)      # clip (x, y, w), SURVEY.md 8(d) config 3
@@ -194,20 +195,22 @@ class Renderer:
                   clear_color: int = CLEAR_COLOR, shard_index: int = 0, shard_count: int = 1,
                   instrumented: bool = False, path: bool = False, bounces: int = 4,
                   seed: int = PT_SEED, flat: bool = False, raster: bool = False,
-                  bvh_width: int = 0, compact: bool = False) -> None:
+                  bvh_width: int = 0, compact: bool = False, counters: bool = True) -> None:
         """path=True: diffuse path trace (pt_kernel; `bounces` segments per
         path, RNG `seed`) instead of primary + shadow rays.  flat=True: the
         flat triangle list without BVH (BASELINE config 2).  raster=True:
         the draw3d raster pipeline (any scene; depth/stencil/blend).
         bvh_width: 2 = traverse the binary BVH, 0 = the default (the 4-wide
         BVH unless env RT_BVH_WIDTH=2).  compact=True: the shard layout
-        (tile order, as for shard_count > 1) for a single shard too."""
+        (tile order, as for shard_count > 1) for a single shard too.
+        counters=False: no per-workgroup counter rows (the timed product
+        configuration; stats() then has the task count and kernel time only)."""
         p = RenderParams()
         p.width, p.height = width, height
         p.flags = ((RT_RENDER_SHADOWS if shadows else 0) | (RT_RENDER_INSTRUMENTED if instrumented else 0)
                    | (RT_RENDER_PATH if path else 0) | (RT_RENDER_FLAT if flat else 0)
                    | (RT_RENDER_RASTER if raster else 0) | (RT_RENDER_BVH2 if bvh_width == 2 else 0)
-                   | (RT_RENDER_COMPACT if compact else 0))
+                   | (RT_RENDER_COMPACT if compact else 0) | (RT_RENDER_COUNTERS if counters else 0))
         p.bounces, p.seed = bounces, seed
         p.light[:] = [float(np.float32(x)) for x in light]
         p.clear_color = clear_color

@@ -1,0 +1,99 @@
+"""BASELINE config 5 at full size on one GPU: a 4096x4096 tekkaman frame
+(primary + shadow rays) rendered as the 8 tile shards of an 8-GPU node
+(32x32 tile t -> shard t % 8, sim/simx/raster_unit.cpp:109-111 striding),
+the shards' compact buffers laid side by side as the RCCL gather leaves them
+in rank 0's receive buffer and assembled by rt_frame_assemble -- which must
+give the full single-launch 4096^2 render, which must equal the oracle bit
+for bit.  Also the FrameGather path itself at world size 1 (RCCL to self):
+compact render -> gather -> assembly == the full render.  Exercises the
+arena addressing and compact-tile indexing at config 5's 64 MiB framebuffer."""
+import ctypes
+import os
+import socket
+
+import numpy as np
+import pytest
+
+from conftest import scene_path
+
+pytestmark = pytest.mark.gpu
+
+from skybox_rt_amd import _lib, rt, shard  # noqa: E402
+
+W = H = 4096
+SHARDS = 8
+
+
+@pytest.fixture(scope="module")
+def tek():
+    s = rt.Scene.load(scene_path("tekkaman"))
+    r = rt.Renderer(s)
+    r.configure(W, H, shadows=True)
+    r.render()
+    full = r.framebuffer().copy()
+    yield s, r, full
+    r.close()
+    s.close()
+
+
+def test_config5_full_frame_equals_oracle(tek, oracle_lib):
+    po = oracle_lib
+    _, _, full = tek
+    c, _, _, k = po.rt_render(po.OracleScene(po.cgltrace.load(scene_path("tekkaman"))),
+                              po.rt_params(W, H, shadows=True, nthreads=min(16, os.cpu_count() or 1)))
+    bad = int((full != c).sum())
+    assert bad == 0, f"{bad} of {W * H} pixels differ from the oracle at 4096^2"
+    assert k["primary_rays"] == W * H
+
+
+def test_config5_eight_shards_assemble_to_the_full_frame(tek):
+    import torch
+    _, r, full = tek
+    per = shard.local_tiles(W, H, 0, SHARDS) * 1024
+    recv = torch.zeros(SHARDS * per, dtype=torch.int32, device="cuda")
+    rays = 0
+    for i in range(SHARDS):
+        r.configure(W, H, shadows=True, shard_index=i, shard_count=SHARDS)
+        r.render()
+        part = r.framebuffer()
+        assert part.size == shard.local_tiles(W, H, i, SHARDS) * 1024
+        recv[i * per:i * per + part.size] = torch.from_numpy(part.view(np.int32)).cuda()
+        rays += r.stats()["primary_rays"]
+    assert rays == W * H
+    f = _lib.load("libframe_assemble.so").rt_frame_assemble
+    f.restype = ctypes.c_int
+    f.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint32,
+                  ctypes.c_uint32, ctypes.c_uint64, ctypes.c_void_p]
+    img = torch.full((W * H,), -1, dtype=torch.int32, device="cuda")
+    assert f(img.data_ptr(), recv.data_ptr(), W, H, SHARDS, per,
+             torch.cuda.current_stream().cuda_stream) == 0
+    torch.cuda.synchronize()
+    got = img.cpu().numpy().view(np.uint32).reshape(H, W)
+    assert np.array_equal(got, full)
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def test_config5_frame_gather_world_size_1(tek):
+    """The bench's exchange code (FrameGather over RCCL) at world size 1."""
+    import torch
+    import torch.distributed as dist
+    from skybox_rt_amd.shard import FrameGather
+    _, r, full = tek
+    dev = torch.device("cuda", torch.cuda.current_device())
+    dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{_free_port()}", rank=0,
+                            world_size=1, device_id=dev)
+    try:
+        r.configure(W, H, shadows=True, compact=True)
+        r.render()
+        local = torch.from_numpy(r.framebuffer().view(np.int32)).to(dev)
+        fg = FrameGather(dist, W, H, dev)
+        image = fg(local)
+        torch.cuda.synchronize()
+        assert np.array_equal(image.cpu().numpy().view(np.uint32).reshape(H, W), full)
+    finally:
+        dist.destroy_process_group()

@@ -270,3 +270,21 @@ def test_rtapp_cli_against_golden():
                          capture_output=True, text=True, timeout=300)
     assert out.returncode == 0, out.stdout + out.stderr
     assert "PASSED!" in out.stdout
+
+
+def test_counters_off_writes_no_counter_rows():
+    """The timed product configuration (counters=False) writes no per-block
+    counter rows: the user counters read 0 and MINSTRET is the launch's
+    declared task count; with counters on they are the real counts."""
+    _, r = renderer("tekkaman")
+    r.configure(256, 256, shadows=True, counters=True)
+    r.render()
+    on = r.stats()
+    fb_on = r.framebuffer()
+    r.configure(256, 256, shadows=True, counters=False)
+    r.render()
+    off = r.stats()
+    assert on["primary_rays"] == 256 * 256 and on["shadow_rays"] > 0
+    assert off["primary_rays"] == 0 and off["shadow_rays"] == 0
+    assert off["tasks"] == off["num_tasks"] == on["tasks"]
+    assert np.array_equal(r.framebuffer(), fb_on)
