@@ -81,6 +81,13 @@ int rt_scene_export_bvh4(rt_scene_h scene, float* nodes4);
 /* fixed-point shading records (rt_prim_t) at width x height: int32[num_prims][32] */
 int rt_scene_setup_prims(rt_scene_h scene, uint32_t width, uint32_t height, int32_t* out,
                          uint64_t count);
+/* primary-visibility record of every primitive at width x height (the RT
+ * kernels' raster-exact primary rays, rt_common.h): uint32[num_prims][3] =
+ * covered-pixel rectangle x0 | x1 << 16, y0 | y1 << 16 (inclusive; empty:
+ * 0x0000ffff) and the lower bound of its 24-bit depth word.  NO REFERENCE
+ * (derived from draw3d's coverage rule; oracle/vis.c restates it). */
+int rt_scene_setup_vis(rt_scene_h scene, uint32_t width, uint32_t height, uint32_t* out,
+                       uint64_t count);
 
 /* kernel_dir: directory holding rt_kernel.vxbin / rt_kernel_stats.vxbin
  * (NULL = next to librtapp.so).  Opens its own vortex device.  Scenes the

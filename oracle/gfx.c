@@ -349,6 +349,17 @@ uint32_t orc_shade(const orc_dcstate_t* s, const orc_rast_prim_t* p,
   return orc_shade_weights(s, p, dx, dy, depth);
 }
 
+/* the depth word the shader computes (GRADIENTS_SW + INTERPOLATE z,
+ * draw3d/kernel.cpp:37-59), masked to VX_OM_DEPTH_BITS: what the depth test
+ * compares (graphics.cpp:564-596) */
+uint32_t orc_vis_depth(const orc_rast_prim_t* p, int32_t F0, int32_t F1, int32_t F2) {
+  const float f0 = fx_to_float(F0, 24), f1 = fx_to_float(F1, 24), f2 = fx_to_float(F2, 24);
+  const float r = 1.0f / (f0 + f1 + f2);
+  const int32_t dx = fx_from_float_dev(r * f0, 24);
+  const int32_t dy = fx_from_float_dev(r * f1, 24);
+  return (uint32_t)interp(p->attribs[0], dx, dy) & VX_OM_DEPTH_MASK;
+}
+
 uint32_t orc_shade_weights(const orc_dcstate_t* s, const orc_rast_prim_t* p,
                            int32_t dx, int32_t dy, uint32_t* depth) {
   int32_t z = 0, cr = 1 << 24, cg = 1 << 24, cb = 1 << 24, ca = 1 << 24, u = 0, v = 0;

@@ -155,6 +155,23 @@ uint32_t orc_shade(const orc_dcstate_t* s, const orc_rast_prim_t* p,
 uint32_t orc_shade_weights(const orc_dcstate_t* s, const orc_rast_prim_t* p,
                            int32_t dx, int32_t dy, uint32_t* depth);
 
+/* the masked 24-bit depth word of a fragment with edge values F0..F2 */
+uint32_t orc_vis_depth(const orc_rast_prim_t* p, int32_t F0, int32_t F1, int32_t F2);
+
+/* primary visibility of one primitive at W x H (oracle/vis.c): covered-pixel
+ * rectangle (x0 | x1 << 16, y0 | y1 << 16, inclusive; empty 0x0000ffff) and
+ * depth-word lower bound */
+typedef struct {
+  uint32_t rx, ry, zmin;
+  int any;
+} orc_vis_prim_t;
+void orc_vis_prim_compute(const orc_rast_prim_t* p, int ok, const int32_t bbox[4], uint32_t width,
+                          uint32_t height, orc_vis_prim_t* out);
+/* rt_vnode_t words ([n][16]: rx[4] ry[4] zmin[4] child[4]) over a tree given
+ * by child references refs[n][4] (leaf refs index leaf_pids) */
+int orc_vis_nodes(const int32_t* refs, uint32_t n, const int32_t* leaf_pids, uint32_t m,
+                  const orc_vis_prim_t* by_pid, uint32_t np, uint32_t* vnodes);
+
 /* OutputMerger::write (gpu_sw.h:100-168) on one pixel. Returns 1 if the
  * depth/stencil test passed (and colour was written if enabled). */
 int orc_om_write(const orc_dcstate_t* s, uint32_t* cbuf_px, uint32_t* zbuf_px,

@@ -132,6 +132,12 @@ int orc_rt_render_bvh(const orc_scene_t* scene, const orc_bvh_t* bvh,
                       const orc_rt_params_t* p, uint32_t* color, int32_t* pid,
                       float* t, orc_rt_counters_t* counters);
 
+/* Primary visibility (vis.c): per primitive at W x H, out[num_prims][3] =
+ * covered-pixel rectangle x0|x1<<16, y0|y1<<16 (inclusive; empty 0x0000ffff)
+ * and depth-word lower bound -- the product's rt_scene_setup_vis restated
+ * by brute force over the binned tiles. */
+int orc_vis_prims(const orc_scene_t* scene, uint32_t width, uint32_t height, uint32_t* out);
+
 /* Möller–Trumbore as used by both sides (exposed for unit tests). */
 int orc_mt(const float o[3], const float d[3], const float v0[3],
            const float e1[3], const float e2[3], float tmin, float* t_out);

@@ -93,6 +93,7 @@ def lib():
         _lib.orc_setup_prim.argtypes = [C.c_void_p, C.c_uint32, C.c_uint32, C.c_float, C.c_float,
                                         C.c_void_p, C.c_void_p]
         _lib.orc_mt.argtypes = [C.c_void_p] * 5 + [C.c_float, C.POINTER(C.c_float)]
+        _lib.orc_vis_prims.argtypes = [C.POINTER(SceneC), C.c_uint32, C.c_uint32, C.c_void_p]
         _lib.orc_lbvh_build.argtypes = [C.c_void_p, C.c_void_p, C.c_uint32, C.c_void_p, C.c_void_p,
                                         C.POINTER(C.c_uint32)]
         _lib.orc_lbvh_collapse4.argtypes = [C.c_void_p, C.c_uint32, C.c_void_p,
@@ -159,6 +160,17 @@ def raster_render(oscene: OracleScene, width: int, height: int, tile_logsize: in
         raise RuntimeError(f"orc_raster_render failed: {rc}")
     return (color.reshape(height, width), depth.reshape(height, width),
             pid.reshape(height, width))
+
+
+def vis_prims(oscene: OracleScene, width: int, height: int) -> np.ndarray:
+    """uint32[P, 3]: every primitive's covered-pixel rectangle (x0|x1<<16,
+    y0|y1<<16, inclusive) and depth-word lower bound, by brute force (vis.c)."""
+    n = oscene.scene.num_prims
+    out = np.zeros((max(n, 1), 3), np.uint32)
+    rc = lib().orc_vis_prims(C.byref(oscene.c), width, height, out.ctypes.data)
+    if rc != 0:
+        raise RuntimeError(f"orc_vis_prims failed: {rc}")
+    return out[:n]
 
 
 def rt_params(width, height, shadows=True, light=(0.0, 60.0, 80.0), nthreads=1,

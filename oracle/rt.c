@@ -12,8 +12,14 @@
  *     draw3d/main.cpp:385-386 (row 0 = NDC y = -1);
  *   - MT == homogeneous edge functions for eye rays: gfxutil.cpp:35-75;
  *   - inclusive coverage (no top-left rule): graphics.cpp:813-825;
- *   - closest hit with ties -> first drawn (LESS) : graphics.cpp:564-596 with
- *     per-tile ascending pid order gpu_sw.h:46-60;
+ *   - PRIMARY rays are raster-exact (vis.c; the kernels' trace_primary):
+ *     coverage = the Q15.16 edge test inside the binned tiles
+ *     (graphics.cpp:813-825, gfxutil.cpp:237-271), closest hit = the depth
+ *     test's winner on the 24-bit word (graphics.cpp:564-596, ties to the
+ *     first drawn for LESS / last drawn for LEQUAL, gpu_sw.h:46-60), found
+ *     by a BVH walk over per-node pixel rectangles + depth bounds;
+ *   - SECONDARY rays (shadow, bounce): Möller–Trumbore, closest hit with
+ *     ties -> lowest pid (LESS) / highest (LEQUAL);
  *   - layers (depth_test off) painted in order: draw3d/main.cpp:239-242;
  *   - shading of a hit = draw3d shader (kernel.cpp:232-279) evaluated with
  *     the hit primitive's fixed-point edge functions at the pixel centre.
@@ -70,6 +76,9 @@ typedef struct {
   int* rp_ok;                     /* non-degenerate */
   int* prim_dc;                   /* drawcall of each prim */
   orc_dcstate_t* dcst;            /* [num_drawcalls] */
+  orc_vis_prim_t* vis;            /* [num_prims] primary visibility (vis.c) */
+  uint32_t* vnodes;               /* [num vnodes][16] over the traversed tree */
+  uint32_t num_vnodes;
   float* tri;                     /* [num_prims][9] v0,e1,e2 (clip x,y,w) */
   int32_t* geom;                  /* geometry prim ids, ascending */
   int num_geom;
@@ -92,6 +101,7 @@ static int rt_prepare(rt_ctx_t* c, const orc_scene_t* s, const orc_rt_params_t* 
   c->tri = (float*)calloc((size_t)np * 9, sizeof(float));
   c->geom = (int32_t*)calloc(np, sizeof(int32_t));
   c->dcst = (orc_dcstate_t*)calloc(s->num_drawcalls > 0 ? s->num_drawcalls : 1, sizeof(orc_dcstate_t));
+  c->vis = (orc_vis_prim_t*)calloc(np, sizeof(orc_vis_prim_t));
   int seen_geom = 0, geom_func = -1;
   for (int d = 0; d < s->num_drawcalls; ++d) {
     const orc_drawcall_t* dc = &s->drawcalls[d];
@@ -103,6 +113,7 @@ static int rt_prepare(rt_ctx_t* c, const orc_scene_t* s, const orc_rt_params_t* 
       const uint32_t f = cgl_to_vx_compare(dc->depth_func);
       if (f != VX_OM_DEPTH_FUNC_LESS && f != VX_OM_DEPTH_FUNC_LEQUAL) return -2;
       if (geom_func >= 0 && (int)f != geom_func) return -2;
+      if (!(dc->depth_writemask & 1)) return -2;  /* the winner must write its depth */
       geom_func = (int)f;
       seen_geom = 1;
     } else if (seen_geom) {
@@ -112,7 +123,9 @@ static int rt_prepare(rt_ctx_t* c, const orc_scene_t* s, const orc_rt_params_t* 
       const int g = dc->prim_offset + i;
       const float* v = s->prim_verts + (size_t)g * 30;
       int32_t bb[4];
-      c->rp_ok[g] = orc_setup_prim(v, p->width, p->height, dc->znear, dc->zfar, &c->rp[g], bb) != 1;
+      const int st = orc_setup_prim(v, p->width, p->height, dc->znear, dc->zfar, &c->rp[g], bb);
+      c->rp_ok[g] = st != 1;
+      orc_vis_prim_compute(&c->rp[g], st == 0, bb, p->width, p->height, &c->vis[g]);
       c->prim_dc[g] = d;
       float* t = c->tri + (size_t)g * 9;
       /* clip-space (x, y, w) triangle: v0, e1 = v1 - v0, e2 = v2 - v0 */
@@ -133,6 +146,7 @@ static int rt_prepare(rt_ctx_t* c, const orc_scene_t* s, const orc_rt_params_t* 
 
 static void rt_release(rt_ctx_t* c) {
   free(c->rp); free(c->rp_ok); free(c->prim_dc); free(c->tri); free(c->geom); free(c->dcst);
+  free(c->vis); free(c->vnodes);
   pthread_mutex_destroy(&c->mu);
 }
 
@@ -302,6 +316,130 @@ static int brute_trace(const rt_ctx_t* c, const float o[3], const float d[3], fl
   return bpid;
 }
 
+/* ---- primary visibility: restatement of the kernels' trace_primary ------ */
+static inline int rect_in(uint32_t r, uint32_t p) { return p >= (r & 0xffffu) && p <= (r >> 16); }
+
+static inline int vis_better(uint32_t z, int pid, uint32_t bz, int bpid, int tie_high) {
+  return z < bz || (z == bz && (tie_high ? pid > bpid : (bpid >= 0 && pid < bpid)));
+}
+
+/* one candidate primitive at pixel (px, py): draw3d's coverage (the binned
+ * rectangle + inclusive edge test) and depth test against (bz, bpid) */
+static inline void vis_test(const rt_ctx_t* c, int pid, uint32_t px, uint32_t py, uint32_t* bz,
+                            int* bpid) {
+  const orc_vis_prim_t* v = &c->vis[pid];
+  if (!rect_in(v->rx, px) || !rect_in(v->ry, py) || v->zmin > *bz) return;
+  const orc_rast_prim_t* p = &c->rp[pid];
+  const int32_t e0 = orc_edge_eval(p->edges[0], px, py);
+  const int32_t e1 = orc_edge_eval(p->edges[1], px, py);
+  const int32_t e2 = orc_edge_eval(p->edges[2], px, py);
+  if (e0 < 0 || e1 < 0 || e2 < 0) return;
+  const uint32_t z = orc_vis_depth(p, e0, e1, e2);
+  if (vis_better(z, pid, *bz, *bpid, c->tie_high)) { *bz = z; *bpid = pid; }
+}
+
+/* rt_vnode_t step (kernels' vnode_step): children whose rectangle holds the
+ * pixel and whose depth bound can still win, sorted by that bound with the
+ * 5-exchange network, nearest returned, the others pushed farthest first */
+static int32_t vnode_step(const uint32_t* n, uint32_t px, uint32_t py, uint32_t bz,
+                          int32_t* stack, int* sp) {
+  uint32_t key[4];
+  int32_t ref[4];
+  int cnt = 0;
+  for (int i = 0; i < 4; ++i) {
+    ref[i] = (int32_t)n[12 + i];
+    const int h = ref[i] != BVH_EMPTY && rect_in(n[i], px) && rect_in(n[4 + i], py) && n[8 + i] <= bz;
+    key[i] = h ? n[8 + i] : 0xffffffffu;
+    cnt += h;
+  }
+  static const int net[5][2] = {{0, 1}, {2, 3}, {0, 2}, {1, 3}, {1, 2}};
+  for (int e = 0; e < 5; ++e) {
+    const int a = net[e][0], b = net[e][1];
+    if (key[b] < key[a]) {
+      const uint32_t tk = key[a]; key[a] = key[b]; key[b] = tk;
+      const int32_t tr = ref[a]; ref[a] = ref[b]; ref[b] = tr;
+    }
+  }
+  if (cnt == 0) return BVH_EMPTY;
+  for (int i = cnt - 1; i >= 1; --i)
+    if (*sp < BVH_STACK) stack[(*sp)++] = ref[i];
+  return ref[0];
+}
+
+static int vis_trace(const rt_ctx_t* c, uint32_t px, uint32_t py, uint64_t* visits, uint64_t* tests) {
+  const orc_bvh_t* b = c->bvh;
+  if (c->num_vnodes == 0) return -1;
+  int32_t stack[BVH_STACK];
+  int sp = 0;
+  int32_t ref = 0;
+  uint32_t bz = VX_OM_DEPTH_MASK;
+  int bpid = -1;
+  for (;;) {
+    if (ref >= 0) {
+      ++*visits;
+      const int32_t nx = vnode_step(c->vnodes + (size_t)ref * 16, px, py, bz, stack, &sp);
+      if (nx != BVH_EMPTY) { ref = nx; continue; }
+    } else {
+      const uint32_t lr = (uint32_t)ref;
+      const uint32_t first = (lr >> 4) & 0x07ffffffu, count = (lr & 15u) + 1u;
+      for (uint32_t k = 0; k < count; ++k) {
+        int32_t pid;
+        memcpy(&pid, &b->tris[(size_t)(first + k) * 12 + 3], 4);
+        ++*tests;
+        vis_test(c, pid, px, py, &bz, &bpid);
+      }
+    }
+    if (sp == 0) break;
+    ref = stack[--sp];
+  }
+  return bpid;
+}
+
+/* flat list: every geometry primitive, ascending pid */
+static int vis_brute(const rt_ctx_t* c, uint32_t px, uint32_t py, uint64_t* tests) {
+  uint32_t bz = VX_OM_DEPTH_MASK;
+  int bpid = -1;
+  for (int k = 0; k < c->num_geom; ++k) {
+    ++*tests;
+    vis_test(c, c->geom[k], px, py, &bz, &bpid);
+  }
+  return bpid;
+}
+
+/* the primary ray's parameter at the winner's plane: MT's t without the
+ * coverage test (the kernels' plane_t) */
+static float plane_t(const float o[3], const float d[3], const float* tri) {
+  float pvec[3], tvec[3], qvec[3];
+  cross3(pvec, d, tri + 6);
+  const float det = dot3(tri + 3, pvec);
+  tvec[0] = o[0] - tri[0]; tvec[1] = o[1] - tri[1]; tvec[2] = o[2] - tri[2];
+  cross3(qvec, tvec, tri + 3);
+  return dot3(tri + 6, qvec) / det;
+}
+
+static void vis_build_nodes(rt_ctx_t* c) {
+  const orc_bvh_t* b = c->bvh;
+  if (!b || b->num_nodes <= 0) return;
+  const uint32_t n = (uint32_t)(b->num_nodes4 > 0 ? b->num_nodes4 : b->num_nodes);
+  int32_t* refs = (int32_t*)malloc(sizeof(int32_t) * 4 * n);
+  for (uint32_t i = 0; i < n; ++i)
+    for (int k = 0; k < 4; ++k) {
+      int32_t r = BVH_EMPTY;
+      if (b->num_nodes4 > 0) memcpy(&r, &b->nodes4[(size_t)i * 32 + 24 + k], 4);
+      else if (k < 2) memcpy(&r, &b->nodes[(size_t)i * 16 + 12 + k], 4);
+      refs[i * 4 + k] = r;
+    }
+  int32_t* pids = (int32_t*)malloc(sizeof(int32_t) * (b->num_tris > 0 ? b->num_tris : 1));
+  for (int k = 0; k < b->num_tris; ++k) memcpy(&pids[k], &b->tris[(size_t)k * 12 + 3], 4);
+  c->vnodes = (uint32_t*)malloc(sizeof(uint32_t) * 16 * n);
+  c->num_vnodes = n;
+  if (orc_vis_nodes(refs, n, pids, (uint32_t)b->num_tris, c->vis, (uint32_t)c->scene->num_prims,
+                    c->vnodes) != 0)
+    c->num_vnodes = 0;
+  free(refs);
+  free(pids);
+}
+
 static inline uint32_t shadow_attenuate(uint32_t c) {
   return (c & 0xff000000u) | ((c >> 1) & 0x007f7f7fu);
 }
@@ -453,18 +591,22 @@ static void rt_row(rt_ctx_t* c, uint32_t y, orc_rt_counters_t* k) {
     const float d[3] = {fmaf((float)x + 0.5f, c->sx, -1.0f),
                         fmaf((float)y + 0.5f, c->sy, -1.0f), 1.0f};
     ++k->primary_rays;
-    float t = 0.0f;
-    const int hit = c->bvh ? bvh_trace(c, o, d, 0.0f, INFINITY, 0, -1, &t, &k->node_visits, &k->tri_tests)
-                           : brute_trace(c, o, d, 0.0f, INFINITY, 0, -1, &t, &k->tri_tests);
+    /* primary visibility: the raster's winner at this pixel */
+    const int hit = c->bvh ? vis_trace(c, x, y, &k->node_visits, &k->tri_tests)
+                           : vis_brute(c, x, y, &k->tri_tests);
     uint32_t col = c->p.clear_color;
     int32_t opid = -1;
+    float t = 0.0f;
     if (hit >= 0) {
       ++k->geometry_hits;
       col = shade_at(c, hit, x, y, k);
       opid = hit;
-      if (c->p.flags & ORC_RT_PATH) {
+      /* secondary rays start at the winner's plane (none if edge-on) */
+      t = plane_t(o, d, c->tri + (size_t)hit * 9);
+      const int sec = t > 0.0f && t < INFINITY;
+      if (sec && (c->p.flags & ORC_RT_PATH)) {
         col = path_trace(c, y * W + x, d, t, hit, col, k);
-      } else if (c->p.flags & ORC_RT_SHADOWS) {
+      } else if (sec && (c->p.flags & ORC_RT_SHADOWS)) {
         /* origin pulled toward the eye by 2^-12 of t, segment to the light */
         const float tt = t * 0.999755859375f;
         const float so[3] = {d[0] * tt, d[1] * tt, d[2] * tt};
@@ -476,17 +618,20 @@ static void rt_row(rt_ctx_t* c, uint32_t y, orc_rt_counters_t* k) {
         if (occ >= 0) { ++k->occluded; col = shadow_attenuate(col); }
       }
     } else {
-      /* screen layers (depth_test off): painter order, last covering pid */
+      /* screen layers (depth_test off): painter order, the last drawn
+       * (highest) covering pid, by draw3d's coverage rule */
       int lpid = -1;
-      for (int dd = 0; dd < s->num_drawcalls; ++dd) {
+      for (int dd = s->num_drawcalls - 1; dd >= 0 && lpid < 0; --dd) {
         const orc_drawcall_t* dc = &s->drawcalls[dd];
         if (dc->depth_test) continue;
         for (int i = dc->prim_count - 1; i >= 0; --i) {
           const int g = dc->prim_offset + i;
           ++k->layer_tests;
-          const float* tr = c->tri + (size_t)g * 9;
-          float tl;
-          if (mt_hit(o, d, tr, tr + 3, tr + 6, 0.0f, &tl)) { lpid = g; break; }
+          const orc_vis_prim_t* v = &c->vis[g];
+          if (!rect_in(v->rx, x) || !rect_in(v->ry, y)) continue;
+          const orc_rast_prim_t* p = &c->rp[g];
+          if (orc_edge_eval(p->edges[0], x, y) >= 0 && orc_edge_eval(p->edges[1], x, y) >= 0 &&
+              orc_edge_eval(p->edges[2], x, y) >= 0) { lpid = g; break; }
         }
       }
       if (lpid >= 0) { col = shade_at(c, lpid, x, y, k); opid = lpid; }
@@ -527,6 +672,7 @@ static int rt_run(const orc_scene_t* scene, const orc_bvh_t* bvh, const orc_rt_p
   int err = rt_prepare(&c, scene, p);
   if (err) { rt_release(&c); return err; }
   c.bvh = bvh;
+  vis_build_nodes(&c);
   c.color = color; c.pid = pid; c.tout = t;
   const uint32_t nt = p->nthreads > 1 ? p->nthreads : 1;
   if (nt == 1) {

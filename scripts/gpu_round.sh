@@ -20,5 +20,5 @@ fi
 step "bench"; timeout -k 10 300 python bench.py > gpurun_out/${T}_bench.json 2> gpurun_out/${T}_bench.err; rc=$?; cat gpurun_out/${T}_bench.json; tail -2 gpurun_out/${T}_bench.err; [ $rc -eq 0 ] || exit $rc
 step "bench path"; timeout -k 10 300 python bench.py --workload path --cpu-budget 5 > gpurun_out/${T}_bench_path.json 2> gpurun_out/${T}_bench_path.err; rc=$?; cat gpurun_out/${T}_bench_path.json; tail -2 gpurun_out/${T}_bench_path.err; [ $rc -eq 0 ] || exit $rc
 step "bench flat"; timeout -k 10 300 python bench.py --workload flat --cpu-budget 5 > gpurun_out/${T}_bench_flat.json 2> gpurun_out/${T}_bench_flat.err; rc=$?; cat gpurun_out/${T}_bench_flat.json; tail -2 gpurun_out/${T}_bench_flat.err; [ $rc -eq 0 ] || exit $rc
-step "rocprof"; timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/${T}_prof -o ${T} --output-format csv -- python3 bench.py --no-cpu-baseline > gpurun_out/${T}_prof.log 2>&1; rc=$?; tail -1 gpurun_out/${T}_prof.log; [ $rc -eq 0 ] || exit $rc
+step "rocprof"; timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/${T}_prof -o ${T} --output-format csv -- python3 bench.py --no-cpu-baseline --no-series > gpurun_out/${T}_prof.log 2>&1; rc=$?; tail -1 gpurun_out/${T}_prof.log; [ $rc -eq 0 ] || exit $rc
 if [ -n "$AB" ]; then step "ab"; timeout -k 10 250 python scripts/ab_variants.py --rounds 8 --variants "$AB" > gpurun_out/${T}_ab.json 2> gpurun_out/${T}_ab.err; rc=$?; cat gpurun_out/${T}_ab.json; exit $rc; fi

@@ -26,6 +26,7 @@
 #include "bvh_common.h"
 #include "cgltrace.h"
 #include "setup.h"
+#include "vis.h"
 #include "vortex.h"
 #include "vortex_hip.h"
 #include "vx_rt.h"
@@ -79,6 +80,7 @@ struct rt_renderer {
   vx_buffer_h nodes = nullptr, nodes4 = nullptr, tris = nullptr, layers = nullptr, dcs = nullptr, tex = nullptr;
   vx_buffer_h ptris = nullptr, geom = nullptr, oms = nullptr, bbox = nullptr, zbuf = nullptr;
   vx_buffer_h order = nullptr;
+  vx_buffer_h vnodes = nullptr, vtris = nullptr, vlayers = nullptr, vgeom = nullptr;
   vx_buffer_h prims = nullptr, cbuf = nullptr, args = nullptr;
   uint64_t cbuf_bytes = 0;
   rt_render_params_t params{};
@@ -100,7 +102,8 @@ struct rt_renderer {
   ~rt_renderer() {
     vx_buffer_h* bufs[] = {&krnl[0][0], &krnl[0][1], &krnl[1][0], &krnl[1][1], &krnl[2][0],
                            &krnl[2][1], &krnl[3][0], &nodes, &nodes4, &tris, &layers, &dcs, &tex,
-                           &ptris, &geom, &oms, &bbox, &zbuf, &order, &prims, &cbuf, &args};
+                           &ptris, &geom, &oms, &bbox, &zbuf, &order, &vnodes, &vtris, &vlayers,
+                           &vgeom, &prims, &cbuf, &args};
     for (auto* b : bufs) {
       if (*b) vx_mem_free(*b);
       *b = nullptr;
@@ -131,6 +134,9 @@ int rt_scene_load(const char* path, rt_scene_h* out) {
     if (st.blend_enabled || st.stencil_test || (st.color_writemask & 0xf) != 0xf)
       sc->unsupported = "drawcall " + std::to_string(d) + " uses blending/stencil/partial writes";
     if (st.depth_test) {
+      // the depth test's winner is the closest hit only while every
+      // geometry fragment that passes also writes its depth
+      if (!(st.depth_writemask & 1)) sc->unsupported = "depth-tested drawcall without depth writes";
       const int f = (int)rt::ToVXCompare(st.depth_func);
       if (f != VX_OM_DEPTH_FUNC_LESS && f != VX_OM_DEPTH_FUNC_LEQUAL)
         sc->unsupported = "depth function other than LESS/LEQUAL";
@@ -297,21 +303,6 @@ int rt_renderer_create(rt_scene_h s, const char* kernel_dir, rt_renderer_h* out)
   a.num_nodes = (uint32_t)bvh.nodes.size();
   a.num_nodes4 = (uint32_t)bvh.nodes4.size();
   r->num_tris = (uint32_t)bvh.tris.size();
-  // screen layers, highest pid first
-  std::vector<rt_tri_t> lt(s->layers.size());
-  for (size_t i = 0; i < s->layers.size(); ++i) {
-    const auto& p = s->scene.prims[s->layers[i]];
-    std::memset(&lt[i], 0, sizeof(rt_tri_t));
-    const float v0[3] = {p[0].pos[0], p[0].pos[1], p[0].pos[3]};
-    for (int k = 0; k < 3; ++k) {
-      const int src = k == 2 ? 3 : k;
-      lt[i].v[k] = v0[k];
-      lt[i].v[4 + k] = p[1].pos[src] - v0[k];
-      lt[i].v[8 + k] = p[2].pos[src] - v0[k];
-    }
-    std::memcpy(&lt[i].v[3], &s->layers[i], 4);
-  }
-  if (upload(r->dev, lt.data(), lt.size() * sizeof(rt_tri_t), &r->layers, &a.layers_addr)) return -1;
   // every primitive's clip-space triangle by pid (path-trace bounce hits)
   std::vector<rt_tri_t> pt(s->scene.prims.size());
   for (size_t g = 0; g < pt.size(); ++g) {
@@ -332,7 +323,7 @@ int rt_renderer_create(rt_scene_h s, const char* kernel_dir, rt_renderer_h* out)
   for (int32_t g : s->geometry) gl.push_back(pt[g]);
   if (upload(r->dev, gl.data(), gl.size() * sizeof(rt_tri_t), &r->geom, &a.geom_addr)) return -1;
   a.num_geom = (uint32_t)gl.size();
-  a.num_layer_tris = (uint32_t)lt.size();
+  a.num_layer_tris = (uint32_t)s->layers.size();
   // textures: one buffer, each texture 256-B aligned
   std::vector<uint8_t> texels;
   std::map<int32_t, uint64_t> tex_off;
@@ -381,6 +372,103 @@ int rt_scene_setup_prims(rt_scene_h s, uint32_t width, uint32_t height, int32_t*
   return 0;
 }
 
+int rt_scene_setup_vis(rt_scene_h s, uint32_t width, uint32_t height, uint32_t* out,
+                       uint64_t count) {
+  if (!s || !out || width == 0 || height == 0) return fail("bad argument");
+  if (count < s->scene.prims.size()) return fail("buffer too small");
+  for (size_t d = 0; d < s->scene.drawcalls.size(); ++d) {
+    const rt::DrawCall& dc = s->scene.drawcalls[d];
+    for (uint32_t i = 0; i < dc.prim_count; ++i) {
+      const uint32_t g = dc.prim_offset + i;
+      rt_prim_t p;
+      rt_bbox_t bb{0, 0};
+      const bool ok = rt::PrimSetup(s->scene.prims[g], width, height, dc.viewport[4],
+                                    dc.viewport[5], &p) == rt::kSetupOk &&
+                      rt::PrimBBox(s->scene.prims[g], width, height, &bb) == rt::kSetupOk;
+      const rt::VisPrim v = rt::ComputeVisPrim(p, ok, bb, width, height);
+      out[3 * g + 0] = v.rx;
+      out[3 * g + 1] = v.ry;
+      out[3 * g + 2] = v.zmin;
+    }
+  }
+  return 0;
+}
+
+// Per-resolution primary-visibility records (app/vis.h): every primitive's
+// covered-pixel rectangle and depth bound, the leaf / layer / flat-list
+// rt_vtri_t records and the rt_vnode_t of the tree the kernels traverse
+// (host tree, or the device tree read back).
+static int configure_vis(rt_renderer* r, const rt_render_params_t* p,
+                         const std::vector<rt_prim_t>& prims, const std::vector<uint8_t>& setup_ok,
+                         bool use_bvh4) {
+  const rt_scene* s = r->sc;
+  rt_kernel_arg_t& a = r->arg;
+  std::vector<rt::VisPrim> vis(prims.size());
+  for (size_t g = 0; g < prims.size(); ++g) {
+    rt_bbox_t bb{0, 0};
+    const bool ok = setup_ok[g] &&
+                    rt::PrimBBox(s->scene.prims[g], p->width, p->height, &bb) == rt::kSetupOk;
+    vis[g] = rt::ComputeVisPrim(prims[g], ok, bb, p->width, p->height);
+  }
+  // the traversed tree's child references and the leaf records' pids
+  std::vector<std::array<int32_t, 4>> refs;
+  std::vector<int32_t> leaf_pids;
+  std::vector<rt_node4_t> n4;
+  std::vector<rt_node_t> n2;
+  std::vector<rt_tri_t> tr;
+  if (r->gpu_bvh) {
+    tr.resize(r->num_tris);
+    if (r->num_tris && vx_copy_from_dev(tr.data(), r->tris, 0, tr.size() * sizeof(rt_tri_t)) != 0)
+      return fail("vx_copy_from_dev failed");
+    if (use_bvh4) {
+      n4.resize(a.num_nodes4);
+      if (!n4.empty() && vx_copy_from_dev(n4.data(), r->nodes4, 0, n4.size() * sizeof(rt_node4_t)) != 0)
+        return fail("vx_copy_from_dev failed");
+    } else {
+      n2.resize(a.num_nodes);
+      if (!n2.empty() && vx_copy_from_dev(n2.data(), r->nodes, 0, n2.size() * sizeof(rt_node_t)) != 0)
+        return fail("vx_copy_from_dev failed");
+    }
+  } else {
+    tr = s->bvh.tris;
+    if (use_bvh4) n4 = s->bvh.nodes4;
+    else n2 = s->bvh.nodes;
+  }
+  for (const rt_tri_t& t : tr) {
+    int32_t pid;
+    std::memcpy(&pid, &t.v[3], 4);
+    leaf_pids.push_back(pid);
+  }
+  if (use_bvh4) {
+    for (const rt_node4_t& n : n4) {
+      std::array<int32_t, 4> c;
+      std::memcpy(c.data(), &n.v[24], 16);
+      refs.push_back(c);
+    }
+  } else {
+    for (const rt_node_t& n : n2) {
+      std::array<int32_t, 4> c = {RT_EMPTY_REF, RT_EMPTY_REF, RT_EMPTY_REF, RT_EMPTY_REF};
+      std::memcpy(c.data(), &n.v[12], 8);
+      refs.push_back(c);
+    }
+  }
+  std::vector<rt_vnode_t> vnodes;
+  if (rt::BuildVisNodes(refs, leaf_pids, vis, &vnodes) != 0) return fail("malformed BVH");
+  std::vector<rt_vtri_t> vtris;
+  for (int32_t pid : leaf_pids) vtris.push_back(rt::MakeVisTri(prims[pid], vis[pid], pid));
+  for (int i = 0; i < 3; ++i)  // padding: the kernel loads all 4 slots of a leaf
+    vtris.push_back(rt::MakeVisTri(rt_prim_t{}, rt::VisPrim{}, -1));
+  std::vector<rt_vtri_t> vl, vg;
+  for (int32_t g : s->layers) vl.push_back(rt::MakeVisTri(prims[g], vis[g], g));
+  for (int32_t g : s->geometry) vg.push_back(rt::MakeVisTri(prims[g], vis[g], g));
+  if (upload(r->dev, vnodes.data(), vnodes.size() * sizeof(rt_vnode_t), &r->vnodes, &a.vnodes_addr) ||
+      upload(r->dev, vtris.data(), vtris.size() * sizeof(rt_vtri_t), &r->vtris, &a.vtris_addr) ||
+      upload(r->dev, vl.data(), vl.size() * sizeof(rt_vtri_t), &r->vlayers, &a.vlayers_addr) ||
+      upload(r->dev, vg.data(), vg.size() * sizeof(rt_vtri_t), &r->vgeom, &a.vgeom_addr))
+    return -1;
+  return 0;
+}
+
 int rt_renderer_configure(rt_renderer_h r, const rt_render_params_t* p) {
   if (!r || !p) return fail("null argument");
   if (p->width == 0 || p->height == 0 || p->width > 32768 || p->height > 32768)
@@ -401,13 +489,15 @@ int rt_renderer_configure(rt_renderer_h r, const rt_render_params_t* p) {
   rt_kernel_arg_t& a = r->arg;
   // per-resolution shading records (rast_prim_t + drawcall id)
   std::vector<rt_prim_t> prims(s->scene.prims.size());
+  std::vector<uint8_t> setup_ok(prims.size(), 0);
   for (size_t d = 0; d < s->scene.drawcalls.size(); ++d) {
     const rt::DrawCall& dc = s->scene.drawcalls[d];
     for (uint32_t i = 0; i < dc.prim_count; ++i) {
       rt_prim_t& q = prims[dc.prim_offset + i];
-      rt::PrimSetup(s->scene.prims[dc.prim_offset + i], p->width, p->height, dc.viewport[4],
-                    dc.viewport[5], &q);
+      const int st = rt::PrimSetup(s->scene.prims[dc.prim_offset + i], p->width, p->height,
+                                   dc.viewport[4], dc.viewport[5], &q);
       q.dc = (uint32_t)d;
+      setup_ok[dc.prim_offset + i] = st == rt::kSetupOk;
     }
   }
   if (upload(r->dev, prims.data(), prims.size() * sizeof(rt_prim_t), &r->prims, &a.prims_addr))
@@ -497,6 +587,7 @@ int rt_renderer_configure(rt_renderer_h r, const rt_render_params_t* p) {
             (s->tie_high ? RT_FLAG_TIE_HIGH : 0u) | (compact ? RT_FLAG_COMPACT : 0u) |
             (use_bvh4 ? RT_FLAG_BVH4 : 0u) |
             (use_bvh4 && !r->gpu_bvh && !s->bvh.nodes4h.empty() ? RT_FLAG_BVH4H : 0u);
+  if (!raster && configure_vis(r, p, prims, setup_ok, use_bvh4) != 0) return -1;
   a.bounces = p->bounces;
   a.seed = p->seed;
   a.clear_color = p->clear_color;

@@ -4,8 +4,9 @@
 // own documented choice (DESIGN.md "Path tracing"), restated op for op by the
 // oracle (oracle/rt.c path_trace), against which the output is bit-exact.
 //
-// Per pixel: the primary ray, screen layers and draw3d shading exactly as in
-// rt_kernel.hip.  A pixel whose primary ray hits geometry starts a path:
+// Per pixel: the primary ray (raster-exact, trace_primary), screen layers and
+// draw3d shading exactly as in rt_kernel.hip.  A pixel whose primary ray
+// hits geometry starts a path at the hit's plane intersection:
 // throughput T = its shaded colour, radiance L = 0.  At every path vertex:
 // one any-hit shadow ray to the point light (direct term T * max(0, cos)),
 // then -- for `bounces` segments -- a cosine-weighted bounce about the
@@ -177,18 +178,18 @@ __device__ __forceinline__ void primary(const vx_task_t& task, bool valid, const
   uint32_t x = 0, y = 0;
   if (valid) task_pixel(S, t, &x, &y);
   const bool in = valid && x < S.width && y < S.height;
-  Ray r;
-  primary_dir(S, x, y, r);
-  ray_setup(r);
   cnt.primary += in;
   const bool tie_high = (S.flags & RT_FLAG_TIE_HIGH) != 0;
-  float th = 0.0f;
   int32_t* stack = &L.stack[threadIdx.x >> 6][0][lane_id()];
-  const int32_t hit = in ? trace<false>(S, r, 0.0f, INFINITY, -1, tie_high, &th, stack, cnt) : -1;
+  // primary visibility: the raster's winner at this pixel (trace_primary)
+  const int32_t hit = in ? trace_primary(S, x, y, tie_high, stack, cnt) : -1;
   cnt.hits += hit >= 0;
-  const int32_t spid = resolve_layers(S, r, in && hit < 0, hit, cnt);
+  const int32_t spid = resolve_layers(S, x, y, in && hit < 0, hit, cnt);
   const uint32_t color = shade_wave(S, spid, x, y, S.clear_color, cnt);
-  const bool path = hit >= 0;
+  Ray r;
+  primary_dir(S, x, y, r);
+  const float th = hit >= 0 ? plane_t(S, r, hit) : 0.0f;
+  const bool path = hit >= 0 && secondary_ok(th);
   const float k255 = 1.0f / 255.0f;
   const float T[3] = {(float)((color >> 16) & 0xffu) * k255, (float)((color >> 8) & 0xffu) * k255,
                       (float)(color & 0xffu) * k255};
@@ -453,18 +454,19 @@ __device__ __forceinline__ void lane_path(const vx_task_t& task, const Scene& S,
   // paired vertices (path_step_pair) when the whole wave is here and its
   // upper 32 lanes hold no pixel -- wave-uniform
   const bool pair = PT_PAIR && __ballot(1) == ~0ull && (__ballot(in) >> 32) == 0;
-  Ray r;
-  primary_dir(S, x, y, r);
-  ray_setup(r);
   cnt.primary += in;
   const bool tie_high = (S.flags & RT_FLAG_TIE_HIGH) != 0;
-  float th = 0.0f;
-  const int32_t hit = in ? trace<false>(S, r, 0.0f, INFINITY, -1, tie_high, &th, stack, cnt) : -1;
+  // primary visibility: the raster's winner at this pixel (trace_primary)
+  const int32_t hit = in ? trace_primary(S, x, y, tie_high, stack, cnt) : -1;
   cnt.hits += hit >= 0;
-  const int32_t spid = resolve_layers(S, r, in && hit < 0, hit, cnt);
+  const int32_t spid = resolve_layers(S, x, y, in && hit < 0, hit, cnt);
   const uint32_t color = shade_wave(S, spid, x, y, S.clear_color, cnt);
-  if (hit < 0 && in) store_pixel(S, t, x, y, color);
-  if (hit < 0 && !pair) return;
+  Ray r;
+  primary_dir(S, x, y, r);
+  const float th = hit >= 0 ? plane_t(S, r, hit) : 0.0f;
+  const bool path = hit >= 0 && secondary_ok(th);  // a path starts at the winner's plane
+  if (!path && in) store_pixel(S, t, x, y, color);
+  if (!path && !pair) return;
   const float k255 = 1.0f / 255.0f;
   PathState st;
   st.task = t;
@@ -482,7 +484,7 @@ __device__ __forceinline__ void lane_path(const vx_task_t& task, const Scene& S,
   }
   if (pair) {
     // every lane stays in the loop (helpers trace their owner's shadow ray)
-    bool act = hit >= 0;
+    bool act = path;
     const bool own = act;
     for (uint32_t v = 0; __ballot(act) != 0; ++v) act = path_step_pair(S, stack, st, v, act, cnt);
     if (own) store_path_pixel(S, st);

@@ -5,7 +5,10 @@
 // "Data layout in HBM"):
 //   nodes   [num_nodes]  rt_node_t   64 B  BVH2 node = both children's boxes
 //   tris    [num_tris]   rt_tri_t    48 B  clip-space v0,e1,e2 + pid (leaf order)
-//   layers  [num_layer]  rt_tri_t    48 B  screen layers, highest pid first
+//   vnodes  [num nodes]  rt_vnode_t  64 B  primary visibility per traversed node
+//   vtris   [num_tris]   rt_vtri_t   64 B  primary visibility per leaf record
+//   vlayers [num_layer]  rt_vtri_t   64 B  screen layers, highest pid first
+//   vgeom   [num_geom]   rt_vtri_t   64 B  geometry, ascending pid (flat mode)
 //   prims   [num_prims]  rt_prim_t  128 B  fixed-point shading record
 //   dcs     [num_dc]     rt_dcstate_t 64 B per-drawcall shading state
 //   ptris   [num_prims]  rt_tri_t    48 B  clip-space triangle by pid
@@ -84,6 +87,39 @@ typedef struct { uint16_t b[24]; int32_t child[4]; } rt_node4h_t;
 // rt_tri_t: (v0.x, v0.y, v0.w, pid), (e1.xyw, 0), (e2.xyw, 0) -- clip (x,y,w)
 typedef struct { float v[12]; } rt_tri_t;
 
+// ---- primary visibility (raster-exact primary rays, app/vis.cpp) ----------
+// A primary ray through pixel (x, y) hits primitive p exactly where draw3d's
+// rasterizer covers (x, y) with p: all three Q15.16 edge values >= 0
+// (graphics.cpp:813-825, int32 wrap) inside a 32x32 tile p was binned to
+// (gfxutil.cpp:237-271), and the closest hit is the draw3d depth test's
+// winner: the smallest 24-bit depth word (graphics.cpp:564-596), ties to the
+// first drawn (LESS) or last drawn (LEQUAL) primitive.  Per resolution the
+// host computes every primitive's covered-pixel rectangle (exact, integer)
+// and a lower bound of its depth word, and the BVH's nodes get the union /
+// minimum over their subtrees: primary traversal is a 2D point-in-rect walk
+// with depth culling, then the exact fixed-point test at the leaves.
+// Pixel rectangles: x0 | x1 << 16 and y0 | y1 << 16, inclusive; an empty
+// rectangle is x0 = 0xffff, x1 = 0.
+#define RT_VIS_EMPTY_RECT 0x0000ffffu
+#define RT_VIS_ZMIN_NONE 0xffffffffu
+// rt_vnode_t (64 B), index-aligned with the traversed tree's nodes (BVH4, or
+// BVH2 in slots 0-1): per child its covered-pixel rectangle, depth lower
+// bound and reference (RT_EMPTY_REF when the child covers no pixel)
+typedef struct {
+  uint32_t rx[4], ry[4], zmin[4];
+  int32_t child[4];
+} rt_vnode_t;
+// rt_vtri_t (64 B), index-aligned with the leaf triangle records (tris):
+// edges[3][3] Q15.16, covered rectangle, pid, the z attribute (Q7.24
+// a0-a2, a1-a2, a2) and the depth lower bound
+typedef struct {
+  int32_t edges[9];
+  uint32_t rx, ry;
+  int32_t pid;
+  int32_t z[3];
+  uint32_t zmin;
+} rt_vtri_t;
+
 typedef struct {
   int32_t edges[3][3];     // Q15.16 (graphics.h:61-64)
   int32_t attribs[7][3];   // Q7.24  z,r,g,b,a,u,v x (a0-a2, a1-a2, a2)
@@ -121,7 +157,7 @@ typedef struct {
 } rt_bbox_t;
 
 typedef struct {
-  uint64_t cbuf_addr, nodes_addr, tris_addr, layers_addr, prims_addr, dcs_addr;
+  uint64_t cbuf_addr, nodes_addr, tris_addr, vlayers_addr, prims_addr, dcs_addr;
   uint64_t ptris_addr;     // rt_tri_t per pid (path trace: bounce-hit barycentrics)
   uint64_t geom_addr;      // rt_tri_t of the geometry prims, ascending pid (flat mode)
   uint32_t width, height, tiles_x, tiles_y;
@@ -142,4 +178,7 @@ typedef struct {
   uint32_t split_tiles;    // the first split_tiles tiles of the work order run 32 pixels per wave
   uint64_t order_addr;     // RT modes: u32 per local tile, the order tiles are worked in
                            // (heaviest first; 0 = identity), see rt_app.cpp TileOrder
+  uint64_t vnodes_addr;    // rt_vnode_t per node of the traversed tree (primary visibility)
+  uint64_t vtris_addr;     // rt_vtri_t per leaf triangle record (+3 padding records)
+  uint64_t vgeom_addr;     // rt_vtri_t per geometry primitive, ascending pid (flat mode)
 } rt_kernel_arg_t;

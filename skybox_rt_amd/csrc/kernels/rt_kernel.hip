@@ -1,8 +1,10 @@
 // rt_kernel.hip -- the north-star hot path as a Vortex kernel program for
-// gfx950: per-pixel ray generation, BVH2 traversal, Möller–Trumbore closest
-// hit, screen layers, draw3d-exact shading of the hit and an any-hit shadow
-// ray per geometry hit, with the shadow rays compacted into full waves
-// (ballot + mbcnt into an LDS queue).
+// gfx950: per-pixel primary rays resolved raster-exactly over the BVH
+// (trace_primary: 2D point-in-rect node walk with depth-bound culling, the
+// draw3d fixed-point coverage + 24-bit depth test at the leaves), screen
+// layers, draw3d-exact shading of the winner, and an any-hit Möller–Trumbore
+// shadow ray per geometry hit, with the shadow rays compacted into full
+// waves (ballot + mbcnt into an LDS queue).
 //
 // Launched by libvortex-hip.so (vx_start) as `vx_main`; the body reads its
 // rt_kernel_arg_t from the STARTUP_ARG DCRs and calls vx_spawn_tasks_ex()
@@ -13,10 +15,8 @@
 // stack in LDS, stack[depth][lane] (conflict-free, no VGPR cost); a leaf's
 // triangles come in as one batch of 16-B loads.  The node-visit /
 // triangle-test counts of the RT_INSTRUMENT image are exactly the per-ray
-// traversal work the oracle (oracle/rt.c bvh_trace) restates, the basis of
-// the algorithmic byte count of SURVEY.md 8(d).  (A wave-packet form --
-// scalar-cache node loads, ballot-steered shared stack -- measured 20-25 %
-// slower on tekkaman and was dropped.)
+// traversal work the oracle (oracle/rt.c vis_trace / bvh_trace) restates, the
+// basis of the algorithmic byte count of SURVEY.md 8(d).
 //
 // Scene reads are buffer loads through one arena descriptor
 // (vx_arena): 32-bit offsets, no FLAT loads.  Numerics are bit-identical to
@@ -33,11 +33,7 @@
 #ifndef RT_FLAT
 #define RT_FLAT 0
 #endif
-#define RT_FLAT_CAP 1024  // triangles staged in LDS (64 KB); longer lists stream via s_load
-// RT_LDS_SCENE: the BVH is staged in LDS per workgroup (1024-thread images)
-#ifndef RT_LDS_SCENE
-#define RT_LDS_SCENE 0
-#endif
+#define RT_FLAT_CAP 1024  // primitives staged in LDS (64 KB); longer lists stream via s_load
 #ifndef RT_SHADOW_QUEUE
 #define RT_SHADOW_QUEUE (!RT_FLAT)
 #endif
@@ -65,26 +61,14 @@ struct WaveLds {
 };
 
 #if RT_FLAT
-// the geometry list staged as origin-0 MT records (mt_precompute_o0, 4 float4
-// per triangle) for the primary rays; shadow rays read the plain records
-__shared__ float4 s_geom[RT_FLAT_CAP * 4];
-// staged geometry list, or nullptr when it does not fit
-__device__ __forceinline__ const float4* flat_list(const Scene& S) {
+// the geometry list staged as rt_vtri_t records (4 x 16 B per primitive) for
+// the primary rays; the shadow rays read the MT records (rt_tri_t) of S.geom
+__shared__ uint4 s_geom[RT_FLAT_CAP * 4];
+__device__ __forceinline__ const uint4* flat_list(const Scene& S) {
   return S.num_geom <= RT_FLAT_CAP ? s_geom : nullptr;
 }
 #endif
 
-// closest / any hit for lanes with `active` (all 64 lanes call these)
-__device__ __forceinline__ int32_t trace_closest(const Scene& S, const Ray& r, bool tie_high,
-                                                 bool active, float* th, WaveLds& w,
-                                                 Counters& cnt) {
-  if (!active) return -1;
-#if RT_FLAT
-  return trace_flat<false>(S, r, 0.0f, INFINITY, -1, tie_high, th, nullptr, cnt);
-#else
-  return trace<false>(S, r, 0.0f, INFINITY, -1, tie_high, th, &w.stack[0][lane_id()], cnt);
-#endif
-}
 __device__ __forceinline__ bool occluded(const Scene& S, const Ray& s, int32_t skip, bool tie_high,
                                          bool active, WaveLds& w, Counters& cnt) {
   float ts;
@@ -96,23 +80,17 @@ __device__ __forceinline__ bool occluded(const Scene& S, const Ray& s, int32_t s
 #endif
 }
 
+#if !RT_FLAT
 __device__ __forceinline__ void kernel_body(const vx_task_t& task, const Scene& S, WaveLds& w,
                                             Counters& cnt) {
   const uint32_t t = task.blockIdx.x;
-#if RT_LAYER_PREFETCH && !RT_FLAT
-  LayerPre lp;
-  if (S.num_layer) load_layers(S, lp);
-#endif
   uint32_t x, y;
   task_pixel(S, t, &x, &y);
   const bool in = x < S.width && y < S.height;  // edge tiles overhang the image
-  Ray r;
-  primary_dir(S, x, y, r);
-  ray_setup(r);
   cnt.primary += in;
   const bool tie_high = (S.flags & RT_FLAG_TIE_HIGH) != 0;
-  float th = 0.0f;
-  const int32_t hit = trace_closest(S, r, tie_high, in, &th, w, cnt);
+  // primary visibility: the raster's winner at this pixel
+  const int32_t hit = in ? trace_primary(S, x, y, tie_high, &w.stack[0][lane_id()], cnt) : -1;
 #ifdef RT_STAMPS
   if (lane_id() == 0) __vx_mpm_lds[14] = (uint32_t)__builtin_amdgcn_s_memrealtime();
 #endif
@@ -120,11 +98,7 @@ __device__ __forceinline__ void kernel_body(const vx_task_t& task, const Scene& 
 #ifdef RT_ABLATE_LAYERS  // timing-only ablation (scripts/ab_variants.py)
   const int32_t spid = hit;
 #else
-#if RT_LAYER_PREFETCH && !RT_FLAT
-  const int32_t spid = resolve_layers(S, r, in && hit < 0, hit, cnt, &lp);
-#else
-  const int32_t spid = resolve_layers(S, r, in && hit < 0, hit, cnt);
-#endif
+  const int32_t spid = resolve_layers(S, x, y, in && hit < 0, hit, cnt);
 #endif
 #ifdef RT_ABLATE_SHADE  // timing-only ablation (scripts/ab_variants.py)
   uint32_t color = 0xff000000u | (uint32_t)spid;
@@ -134,7 +108,10 @@ __device__ __forceinline__ void kernel_body(const vx_task_t& task, const Scene& 
 #ifdef RT_STAMPS
   if (lane_id() == 0) __vx_mpm_lds[11] = (uint32_t)__builtin_amdgcn_s_memrealtime();
 #endif
-  const bool shadow = hit >= 0 && (S.flags & RT_FLAG_SHADOWS) != 0;
+  Ray r;
+  primary_dir(S, x, y, r);
+  const float th = hit >= 0 ? plane_t(S, r, hit) : 0.0f;
+  const bool shadow = hit >= 0 && secondary_ok(th) && (S.flags & RT_FLAG_SHADOWS) != 0;
 #if RT_SHADOW_QUEUE
   // wave64 compaction: lanes with a pending shadow ray append it to the
   // wave's LDS queue at ballot/mbcnt-assigned slots
@@ -166,6 +143,7 @@ __device__ __forceinline__ void kernel_body(const vx_task_t& task, const Scene& 
   if (in) store_pixel(S, t, x, y, color);
 #endif
 }
+#endif
 
 #if RT_SHADOW_QUEUE
 // Called by all 64 lanes after every chunk: trace full waves of 64 shadow
@@ -206,20 +184,25 @@ __device__ __forceinline__ void shadow_drain(bool final, const Scene& S, WaveLds
 #endif
 
 #if RT_FLAT
-// Config 2 with every ray's triangle list split across the workgroup's
+// Config 2 with every ray's primitive list split across the workgroup's
 // waves: a workgroup step takes one 64-task chunk (vx_spawn_chunks_block),
-// wave w tests list entries [w*m, (w+1)*m) for the chunk's 64 rays, the
-// per-wave closest hits meet in LDS (closer() is a strict order on
-// (t, pid), so the reduction order is immaterial) and wave 0 resolves
-// layers, shades and stores; shadow rays split the same way, the first
-// occluder in list order found by a min over the waves' first hits (which
-// is also brute_trace's test count).  16x shorter dependent chains and 16x
-// more waves than one ray per lane over the whole list.
+// wave w tests list entries [w*m, (w+1)*m) for the chunk's 64 pixels
+// (rt_vtri_t records from LDS: one broadcast 16-B read of a record's pixel
+// rectangle first, the edges and depth only when a lane of the wave lies in
+// it), the per-wave winners meet in LDS (vis_better is a strict order on
+// (depth word, pid), so the reduction order is immaterial) and wave 0
+// shades and stores; shadow rays split the same way, the first occluder in
+// list order found by a min over the waves' first hits (which is also
+// brute_trace's test count).
 struct FlatLds {
-  float t[kWaves][64];
+  uint32_t z[kWaves][64];
   int32_t pid[kWaves][64];
   uint32_t first[kWaves][64];
 };
+
+__device__ __forceinline__ uint4 flat_rec(const Scene& S, const uint4* lds, uint32_t k, uint32_t q) {
+  return lds ? lds[4u * k + q] : S.A.sld_u4(S.vgeom + 64u * k + 16u * q);
+}
 
 __device__ __forceinline__ void flat_chunk(const vx_task_t& task, bool valid, const Scene& S,
                                            FlatLds& L, Counters& cnt) {
@@ -228,31 +211,31 @@ __device__ __forceinline__ void flat_chunk(const vx_task_t& task, bool valid, co
   uint32_t x = 0, y = 0;
   if (valid) task_pixel(S, t, &x, &y);
   const bool in = valid && x < S.width && y < S.height;
-  Ray r;
-  primary_dir(S, x, y, r);
-  ray_setup(r);
+  const uint32_t px = in ? x : 0xffffffffu;  // outside every pixel rectangle
   const bool tie_high = (S.flags & RT_FLAG_TIE_HIGH) != 0;
   const uint32_t n = S.num_geom, per = (n + kWaves - 1) / kWaves;
   const uint32_t k0 = w * per < n ? w * per : n, k1 = k0 + per < n ? k0 + per : n;
-  const float4* lds = flat_list(S);
-  float bt = INFINITY;
-  uint32_t f;
-  const int32_t bp = !in ? -1
-                   : lds ? trace_flat_range_o0(r, k0, k1, 0.0f, INFINITY, tie_high, &bt, lds)
-                         : trace_flat_range<false>(S, r, k0, k1, 0.0f, INFINITY, -1, tie_high, &bt,
-                                                   &f, nullptr);
+  const uint4* lds = flat_list(S);
+  uint32_t bz = VX_OM_DEPTH_MASK;
+  int32_t bp = -1;
+  for (uint32_t k = k0; k < k1; ++k) {
+    const uint4 C = flat_rec(S, lds, k, 2);
+    if (__ballot(rect_in(C.y, px) && rect_in(C.z, y)) == 0) continue;  // wave-uniform skip
+    vis_test(flat_rec(S, lds, k, 0), flat_rec(S, lds, k, 1), C, flat_rec(S, lds, k, 3), px, y,
+             tie_high, bz, bp);
+  }
 #ifdef RT_INSTRUMENT
   cnt.tests += in ? k1 - k0 : 0u;  // the whole list per ray, summed over the waves
 #endif
-  L.t[w][lane] = bt;
+  L.z[w][lane] = bz;
   L.pid[w][lane] = bp;
   __syncthreads();
   int32_t hit = -1;
-  float th = INFINITY;
+  uint32_t hz = VX_OM_DEPTH_MASK;
   for (uint32_t i = 0; i < kWaves; ++i) {
     const int32_t p = L.pid[i][lane];
-    if (p >= 0 && closer(L.t[i][lane], p, th, hit, tie_high)) {
-      th = L.t[i][lane];
+    if (p >= 0 && vis_better(L.z[i][lane], p, hz, hit, tie_high)) {
+      hz = L.z[i][lane];
       hit = p;
     }
   }
@@ -260,10 +243,13 @@ __device__ __forceinline__ void flat_chunk(const vx_task_t& task, bool valid, co
   if (w == 0) {
     cnt.primary += in;
     cnt.hits += hit >= 0;
-    const int32_t spid = resolve_layers(S, r, in && hit < 0, hit, cnt);
+    const int32_t spid = resolve_layers(S, x, y, in && hit < 0, hit, cnt);
     color = shade_wave(S, spid, x, y, S.clear_color, cnt);
   }
-  const bool shadow = in && hit >= 0 && (S.flags & RT_FLAG_SHADOWS) != 0;
+  Ray r;
+  primary_dir(S, x, y, r);
+  const float th = hit >= 0 ? plane_t(S, r, hit) : 0.0f;
+  const bool shadow = in && hit >= 0 && secondary_ok(th) && (S.flags & RT_FLAG_SHADOWS) != 0;
   if (__ballot(shadow)) {  // block-uniform: every wave holds the same 64 rays
     Ray sr;
     shadow_ray(S, r, th, sr);
@@ -324,9 +310,8 @@ VX_MAIN(rt_kernel_arg_t, arg, RT_BLOCK_THREADS) {
   // stage the geometry list once per workgroup (workgroups past the last
   // task chunk have nothing to render and skip it)
   if (S.num_geom <= RT_FLAT_CAP && blockIdx.x * VX_CHUNK < arg->num_tasks) {  // one chunk per step
-    for (uint32_t i = threadIdx.x; i < S.num_geom; i += blockDim.x)
-      mt_precompute_o0(S.A.ld_f4(S.geom + 48u * i), S.A.ld_f4(S.geom + 48u * i + 16),
-                       S.A.ld_f4(S.geom + 48u * i + 32), &s_geom[4u * i]);
+    for (uint32_t i = threadIdx.x; i < 4u * S.num_geom; i += blockDim.x)
+      s_geom[i] = S.A.ld_u4(S.vgeom + 16u * i);
   }
   __syncthreads();
 #endif

@@ -44,13 +44,6 @@
 #ifndef RT_ROOT_SCALAR
 #define RT_ROOT_SCALAR 1
 #endif
-// 1: rt_kernel issues the first screen-layer records' scalar loads before the
-// primary walk, so a background wave's layer tests do not wait for them
-// (A/B r01_v12: neutral to +1 % -- off; the root step alone: neutral for
-// primary+shadow, -1.4 % for the path tracer, and 64x less root data traffic)
-#ifndef RT_LAYER_PREFETCH
-#define RT_LAYER_PREFETCH 0
-#endif
 
 namespace rtk {
 
@@ -66,7 +59,8 @@ struct Counters {
 // arena offsets (rt_app checks every buffer lies below 4 GiB).
 struct Scene {
   vx_arena A;
-  uint32_t nodes, nodes4, tris, layers, prims, dcs, cbuf, ptris, geom, order;
+  uint32_t nodes, nodes4, tris, prims, dcs, cbuf, ptris, geom, order;
+  uint32_t vnodes, vtris, vlayers, vgeom;  // primary visibility records (rt_common.h)
   uint32_t num_nodes, num_nodes4, num_layer, num_geom, flags, width, height;
   uint32_t shard_index, shard_count, tiles_x, clear_color, bounces, seed, split_tiles;
   float sx, sy, light[3];
@@ -102,7 +96,10 @@ __device__ __forceinline__ Scene load_scene(const rt_kernel_arg_t* a) {
   s.nodes = (uint32_t)a->nodes_addr;
   s.nodes4 = (uint32_t)a->nodes4_addr;
   s.tris = (uint32_t)a->tris_addr;
-  s.layers = (uint32_t)a->layers_addr;
+  s.vnodes = (uint32_t)a->vnodes_addr;
+  s.vtris = (uint32_t)a->vtris_addr;
+  s.vlayers = (uint32_t)a->vlayers_addr;
+  s.vgeom = (uint32_t)a->vgeom_addr;
   s.prims = (uint32_t)a->prims_addr;
   s.dcs = (uint32_t)a->dcs_addr;
   s.cbuf = (uint32_t)a->cbuf_addr;
@@ -178,46 +175,6 @@ __device__ __forceinline__ bool mt_hit(const Ray& r, const float4& a, const floa
   if (det < 0.0f) { adet = -det; u = -u; v = -v; }
   if (!(adet > 0.0f) || u < 0.0f || v < 0.0f || u + v > adet) return false;
   const float t = dot3(e2, qvec) / det;
-  if (!(t > tmin)) return false;
-  *t_out = t;
-  return true;
-}
-
-// Möller–Trumbore for a ray whose origin is exactly (0, 0, 0) -- every
-// primary ray (primary_dir) -- against a triangle record whose ray-
-// independent terms were precomputed by mt_precompute_o0 with mt_hit's own
-// operations: tvec = 0 - v0, qvec = tvec x e1, tq = e2 . qvec.  Bit-identical
-// to mt_hit(r, ...) with r.o == 0; 4 LDS records of 16 B per triangle:
-// (e1, pid), (e2, tq), (tvec, 0), (qvec, 0).  Saves the per-ray cross product,
-// the subtractions and the t dot product.
-__device__ __forceinline__ void mt_precompute_o0(const float4& a, const float4& b, const float4& c,
-                                                 float4* out) {
-  const float e1[3] = {b.x, b.y, b.z}, e2[3] = {c.x, c.y, c.z};
-  float tvec[3], qvec[3];
-  tvec[0] = 0.0f - a.x;
-  tvec[1] = 0.0f - a.y;
-  tvec[2] = 0.0f - a.z;
-  cross3(qvec, tvec, e1);
-  out[0] = make_float4(b.x, b.y, b.z, a.w);
-  out[1] = make_float4(c.x, c.y, c.z, dot3(e2, qvec));
-  out[2] = make_float4(tvec[0], tvec[1], tvec[2], 0.0f);
-  out[3] = make_float4(qvec[0], qvec[1], qvec[2], 0.0f);
-}
-
-__device__ __forceinline__ bool mt_hit_o0(const Ray& r, const float4& A, const float4& B,
-                                          const float4& C, const float4& D, float tmin,
-                                          float* t_out) {
-  const float e1[3] = {A.x, A.y, A.z}, e2[3] = {B.x, B.y, B.z};
-  const float tvec[3] = {C.x, C.y, C.z}, qvec[3] = {D.x, D.y, D.z};
-  float pvec[3];
-  cross3(pvec, r.d, e2);
-  const float det = dot3(e1, pvec);
-  float u = dot3(tvec, pvec);
-  float v = dot3(r.d, qvec);
-  float adet = det;
-  if (det < 0.0f) { adet = -det; u = -u; v = -v; }
-  if (!(adet > 0.0f) || u < 0.0f || v < 0.0f || u + v > adet) return false;
-  const float t = B.w / det;
   if (!(t > tmin)) return false;
   *t_out = t;
   return true;
@@ -630,26 +587,6 @@ __device__ __forceinline__ int32_t trace_flat_range(const Scene& S, const Ray& r
   return bpid;
 }
 
-// trace_flat_range for origin-0 (primary) rays over mt_precompute_o0
-// records in LDS (4 float4 per triangle): closest hit only
-__device__ __forceinline__ int32_t trace_flat_range_o0(const Ray& r, uint32_t k0, uint32_t k1,
-                                                       float tmin, float tmax, bool tie_high,
-                                                       float* t_out, const float4* lds4) {
-  float bt = tmax;
-  int32_t bpid = -1;
-  for (uint32_t k = k0; k < k1; ++k) {
-    const float4 A = lds4[4 * k], B = lds4[4 * k + 1], C = lds4[4 * k + 2], D = lds4[4 * k + 3];
-    const int32_t pid = __float_as_int(A.w);
-    float t;
-    if (mt_hit_o0(r, A, B, C, D, tmin, &t) && closer(t, pid, bt, bpid, tie_high)) {
-      bt = t;
-      bpid = pid;
-    }
-  }
-  *t_out = bt;
-  return bpid;
-}
-
 // shade primitive `pid` at (x, y) from per-lane (vector) record loads
 __device__ __forceinline__ uint32_t shade_lane(const Scene& S, int32_t pid, uint32_t x,
                                                uint32_t y, Counters& cnt) {
@@ -689,44 +626,197 @@ __device__ __forceinline__ uint32_t shade_wave(const Scene& S, int32_t spid, uin
   return color;
 }
 
-// Screen layers for lanes with `need` (no geometry hit): highest pid first,
-// the first covering triangle wins (oracle/rt.c rt_row); one wave-uniform
-// triangle per step, its record through the scalar cache.  Returns the pid
-// to shade (layer pid, or `spid` unchanged).
-// the first kLayerPre layer records, loaded (scalar) ahead of their use
-constexpr uint32_t kLayerPre = 2;
-struct LayerPre {
-  float4 rec[kLayerPre][3];
-};
-__device__ __forceinline__ void load_layers(const Scene& S, LayerPre& L) {
-#pragma unroll
-  for (uint32_t k = 0; k < kLayerPre; ++k) {
-    const uint32_t lo = S.layers + 48u * (k < S.num_layer ? k : 0u);
-    L.rec[k][0] = S.A.sld_f4(lo);
-    L.rec[k][1] = S.A.sld_f4(lo + 16);
-    L.rec[k][2] = S.A.sld_f4(lo + 32);
+// ---- primary visibility (rt_common.h "primary visibility"; app/vis.cpp) ----
+// A primary ray through pixel (px, py) is resolved the way draw3d's raster
+// resolves that pixel: coverage by the Q15.16 edge functions inside the
+// primitive's binned tiles, closest hit = the depth test's winner on the
+// 24-bit depth word.  Exact, so the RT frame equals the reference's raster
+// frame; the BVH only narrows the candidates (2D point-in-rect per child,
+// culled by the children's depth lower bounds).
+__device__ __forceinline__ bool rect_in(uint32_t r, uint32_t p) {
+  return p >= (r & 0xffffu) && p <= (r >> 16);
+}
+
+// the depth word draw3d's shader computes from the three edge values
+// (GRADIENTS + INTERPOLATE z, draw3d/kernel.cpp:37-59; gfx::shade_edges)
+__device__ __forceinline__ uint32_t vis_depth(int32_t E0, int32_t E1, int32_t E2, const int32_t z[3]) {
+  const float f0 = gfx::fx_to_float(E0, 24), f1 = gfx::fx_to_float(E1, 24),
+              f2 = gfx::fx_to_float(E2, 24);
+  const float r = 1.0f / (f0 + f1 + f2);
+  const int32_t dx = gfx::fx_from_float_dev(r * f0, 24), dy = gfx::fx_from_float_dev(r * f1, 24);
+  return (uint32_t)gfx::interp(z, dx, dy) & VX_OM_DEPTH_MASK;
+}
+
+// DepthTencil::test against the winner so far (graphics.cpp:564-596; per-tile
+// ascending pid order gpu_sw.h:46-60): LESS keeps the first drawn of equal
+// words and never beats the cleared word 0xffffff; LEQUAL takes the last
+// drawn.  (bz, bpid) start at (0xffffff, -1), the cleared depth buffer.
+__device__ __forceinline__ bool vis_better(uint32_t z, int32_t pid, uint32_t bz, int32_t bpid,
+                                           bool tie_high) {
+  return z < bz || (z == bz && (tie_high ? pid > bpid : (bpid >= 0 && pid < bpid)));
+}
+
+// one rt_vtri_t candidate; updates (bz, bpid)
+__device__ __forceinline__ void vis_test(const uint4& A, const uint4& B, const uint4& C, const uint4& D,
+                                         uint32_t px, uint32_t py, bool tie_high, uint32_t& bz,
+                                         int32_t& bpid) {
+  if (!rect_in(C.y, px) || !rect_in(C.z, py) || D.w > bz) return;
+  const int32_t e0[3] = {(int32_t)A.x, (int32_t)A.y, (int32_t)A.z};
+  const int32_t e1[3] = {(int32_t)A.w, (int32_t)B.x, (int32_t)B.y};
+  const int32_t e2[3] = {(int32_t)B.z, (int32_t)B.w, (int32_t)C.x};
+  const int32_t E0 = gfx::edge_eval(e0, px, py), E1 = gfx::edge_eval(e1, px, py),
+                E2 = gfx::edge_eval(e2, px, py);
+  if (E0 < 0 || E1 < 0 || E2 < 0) return;
+  const int32_t z3[3] = {(int32_t)D.x, (int32_t)D.y, (int32_t)D.z};
+  const uint32_t z = vis_depth(E0, E1, E2, z3);
+  const int32_t pid = (int32_t)C.w;
+  if (vis_better(z, pid, bz, bpid, tie_high)) {
+    bz = z;
+    bpid = pid;
   }
 }
 
-__device__ __forceinline__ int32_t resolve_layers(const Scene& S, const Ray& r, bool need,
-                                                  int32_t spid, Counters& cnt,
-                                                  const LayerPre* pre = nullptr) {
+// rt_vnode_t step: children whose pixel rectangle holds (px, py) and whose
+// depth bound can still win, ordered by that bound (the same 5-exchange
+// network as node4_step, unsigned keys, misses last); the nearest is
+// returned, the others pushed farthest first.  SCALAR: every active lane is
+// at this node (s_load into SGPRs).
+template <bool SCALAR>
+__device__ __forceinline__ int32_t vnode_step(const Scene& S, uint32_t ref, uint32_t px, uint32_t py,
+                                              uint32_t bz, LaneStack& st) {
+  auto ld = [&](uint32_t o) { return SCALAR ? S.A.sld_u4(o) : S.A.ld_u4(o); };
+  const uint32_t o = S.vnodes + 64u * ref;
+  const uint4 rx = ld(o), ry = ld(o + 16), zm = ld(o + 32), cf = ld(o + 48);
+  const uint32_t arx[4] = {rx.x, rx.y, rx.z, rx.w}, ary[4] = {ry.x, ry.y, ry.z, ry.w};
+  const uint32_t azm[4] = {zm.x, zm.y, zm.z, zm.w};
+  int32_t c[4] = {(int32_t)cf.x, (int32_t)cf.y, (int32_t)cf.z, (int32_t)cf.w};
+  uint32_t k[4];
+  int n = 0;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const bool h = c[i] != RT_EMPTY_REF && rect_in(arx[i], px) && rect_in(ary[i], py) && azm[i] <= bz;
+    k[i] = h ? azm[i] : 0xffffffffu;
+    n += h ? 1 : 0;
+  }
+  auto cx = [&](int a, int b) {
+    const bool s = k[b] < k[a];
+    const uint32_t ka = k[a], kb = k[b];
+    const int32_t ca = c[a], cb = c[b];
+    k[a] = s ? kb : ka;
+    k[b] = s ? ka : kb;
+    c[a] = s ? cb : ca;
+    c[b] = s ? ca : cb;
+  };
+  cx(0, 1);
+  cx(2, 3);
+  cx(0, 2);
+  cx(1, 3);
+  cx(1, 2);
+  if (n == 0) return RT_EMPTY_REF;
+  if (n >= 4) st.push(c[3]);
+  if (n >= 3) st.push(c[2]);
+  if (n >= 2) st.push(c[1]);
+  return c[0];
+}
+
+// The primary ray's hit: the draw3d depth-test winner among the geometry
+// primitives covering (px, py), or -1 (oracle/rt.c vis_trace restates it,
+// counters included).  While-while loop as trace_impl.
+__device__ __forceinline__ int32_t trace_primary(const Scene& S, uint32_t px, uint32_t py,
+                                                 bool tie_high, int32_t* stack, Counters& cnt) {
+  if (S.num_nodes == 0 && S.num_nodes4 == 0) return -1;
+  LaneStack lst(stack);
+  uint32_t bz = VX_OM_DEPTH_MASK;
+  int32_t bpid = -1;
+  int32_t ref;
+  {  // every lane starts at the root: one wave-uniform (scalar) step
+#ifdef RT_INSTRUMENT
+    ++cnt.visits;
+#endif
+    ref = vnode_step<true>(S, 0u, px, py, bz, lst);
+    if (ref == RT_EMPTY_REF) return -1;
+  }
+  for (;;) {
+    bool dry = false;
+    while (ref >= 0) {
+#ifdef RT_INSTRUMENT
+      ++cnt.visits;
+#endif
+      const int32_t nx = vnode_step<false>(S, (uint32_t)ref, px, py, bz, lst);
+      if (nx != RT_EMPTY_REF) { ref = nx; continue; }
+      if (!lst.pop(ref)) { dry = true; break; }
+    }
+    if (dry) break;
+    const uint32_t lr = (uint32_t)ref;
+    const uint32_t first = (lr >> 4) & 0x07ffffffu, count = (lr & 15u) + 1u;
+    const uint32_t to = S.vtris + 64u * first;
+#pragma unroll
+    for (uint32_t k0 = 0; k0 < 4; k0 += RT_LEAF_BATCH) {
+      if (k0 >= count) break;
+      uint4 a[RT_LEAF_BATCH], b[RT_LEAF_BATCH], c[RT_LEAF_BATCH], d[RT_LEAF_BATCH];
+#pragma unroll
+      for (uint32_t j = 0; j < RT_LEAF_BATCH; ++j) {
+        const uint32_t o = to + 64u * (k0 + j);
+        a[j] = S.A.ld_u4(o); b[j] = S.A.ld_u4(o + 16); c[j] = S.A.ld_u4(o + 32); d[j] = S.A.ld_u4(o + 48);
+      }
+#pragma unroll
+      for (uint32_t j = 0; j < RT_LEAF_BATCH; ++j) {
+        if (k0 + j < count) {
+#ifdef RT_INSTRUMENT
+          ++cnt.tests;
+#endif
+          vis_test(a[j], b[j], c[j], d[j], px, py, tie_high, bz, bpid);
+        }
+      }
+    }
+    if (!lst.pop(ref)) break;
+  }
+  return bpid;
+}
+
+// ray parameter of the primary ray's intersection with the plane of
+// triangle `pid` (rt_tri_t by pid in ptris): MT's t without the coverage
+// test (mt_hit's operations); the origin of the shadow ray / path.  Not
+// finite or <= 0 (a plane edge-on to the ray): no secondary rays.
+__device__ __forceinline__ float plane_t(const Scene& S, const Ray& r, int32_t pid) {
+  const uint32_t o = S.ptris + 48u * (uint32_t)pid;
+  const float4 a = S.A.ld_f4(o), b = S.A.ld_f4(o + 16), c = S.A.ld_f4(o + 32);
+  const float e1[3] = {b.x, b.y, b.z}, e2[3] = {c.x, c.y, c.z};
+  float pvec[3], tvec[3], qvec[3];
+  cross3(pvec, r.d, e2);
+  const float det = dot3(e1, pvec);
+  tvec[0] = r.o[0] - a.x;
+  tvec[1] = r.o[1] - a.y;
+  tvec[2] = r.o[2] - a.z;
+  cross3(qvec, tvec, e1);
+  return dot3(e2, qvec) / det;
+}
+__device__ __forceinline__ bool secondary_ok(float t) { return t > 0.0f && t < INFINITY; }
+
+// Screen layers (depth test off) for lanes with `need` (no geometry
+// winner): painter order, the highest covering pid wins (layers drawn in
+// order, each overwriting; draw3d/main.cpp:179 + gpu_sw.h:38-61); one
+// wave-uniform rt_vtri_t per step through the scalar cache.  Returns the pid
+// to shade (layer pid, or `spid` unchanged).
+__device__ __forceinline__ int32_t resolve_layers(const Scene& S, uint32_t px, uint32_t py, bool need,
+                                                  int32_t spid, Counters& cnt) {
   uint64_t pend = __ballot(need);
   for (uint32_t k = 0; pend != 0 && k < S.num_layer; ++k) {
-    const uint32_t lo = S.layers + 48u * k;
-    float4 ta, tb, tc;
-    if (pre && k < kLayerPre) {
-      ta = pre->rec[k][0]; tb = pre->rec[k][1]; tc = pre->rec[k][2];
-    } else {
-      ta = S.A.sld_f4(lo); tb = S.A.sld_f4(lo + 16); tc = S.A.sld_f4(lo + 32);
-    }
+    const uint32_t lo = S.vlayers + 64u * k;
+    const uint4 A = S.A.sld_u4(lo), B = S.A.sld_u4(lo + 16), C = S.A.sld_u4(lo + 32);
     const bool mine = (pend & (1ull << lane_id())) != 0;
 #ifdef RT_INSTRUMENT
     cnt.layer_tests += mine;
 #endif
-    float tl;
-    const bool f = mine && mt_hit(r, ta, tb, tc, 0.0f, &tl);
-    if (f) spid = __float_as_int(ta.w);
+    bool f = false;
+    if (mine && rect_in(C.y, px) && rect_in(C.z, py)) {
+      const int32_t e0[3] = {(int32_t)A.x, (int32_t)A.y, (int32_t)A.z};
+      const int32_t e1[3] = {(int32_t)A.w, (int32_t)B.x, (int32_t)B.y};
+      const int32_t e2[3] = {(int32_t)B.z, (int32_t)B.w, (int32_t)C.x};
+      f = gfx::edge_eval(e0, px, py) >= 0 && gfx::edge_eval(e1, px, py) >= 0 &&
+          gfx::edge_eval(e2, px, py) >= 0;
+    }
+    if (f) spid = (int32_t)C.w;
     pend &= ~__ballot(f);
   }
   return spid;

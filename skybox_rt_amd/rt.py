@@ -104,6 +104,7 @@ def lib():
             "rt_read_depthbuffer": [vp, vp, u64],
             "rt_launch_rows": [vp, vp, u64, C.POINTER(u64)],
             "rt_scene_setup_prims": [vp, u32, u32, vp, u64],
+            "rt_scene_setup_vis": [vp, u32, u32, vp, u64],
             "rt_framebuffer_device": [vp, C.POINTER(vp), C.POINTER(u64)],
             "rt_device_stream": [vp, C.POINTER(vp)],
             "rt_device_caps": [vp, C.POINTER(u64)],
@@ -165,6 +166,15 @@ class Scene:
         out = np.zeros((max(n, 1), 32), np.int32)
         _check(lib().rt_scene_setup_prims(self._h, width, height, out.ctypes.data, n),
                "rt_scene_setup_prims")
+        return out[:n]
+
+    def setup_vis(self, width: int, height: int) -> np.ndarray:
+        """Primary-visibility records (uint32[P, 3]: covered-pixel rectangle
+        x0|x1<<16, y0|y1<<16 inclusive, depth-word lower bound) at width x height."""
+        n = self.info()["num_prims"]
+        out = np.zeros((max(n, 1), 3), np.uint32)
+        _check(lib().rt_scene_setup_vis(self._h, width, height, out.ctypes.data, n),
+               "rt_scene_setup_vis")
         return out[:n]
 
     def close(self) -> None:
