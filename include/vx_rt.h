@@ -88,6 +88,13 @@ int rt_scene_setup_prims(rt_scene_h scene, uint32_t width, uint32_t height, int3
  * (derived from draw3d's coverage rule; oracle/vis.c restates it). */
 int rt_scene_setup_vis(rt_scene_h scene, uint32_t width, uint32_t height, uint32_t* out,
                        uint64_t count);
+/* the screen-space BVH4 the primary rays walk at width x height (what
+ * rt_renderer_configure builds; depth_scale 0 = the default 2D SAH):
+ * int32 refs[num_nodes][4], leaf_pids[num_leaf], worst-case stack; NULL
+ * arrays = counts only.  NO REFERENCE. */
+int rt_scene_vis_tree(rt_scene_h scene, uint32_t width, uint32_t height, float depth_scale,
+                      int32_t* refs, uint32_t* num_nodes, int32_t* leaf_pids, uint32_t* num_leaf,
+                      uint32_t* stack4);
 
 /* kernel_dir: directory holding rt_kernel.vxbin / rt_kernel_stats.vxbin
  * (NULL = next to librtapp.so).  Opens its own vortex device.  Scenes the
@@ -139,9 +146,26 @@ int rt_renderer_export_bvh4(rt_renderer_h r, float* nodes4, uint32_t* num_nodes4
 int rt_renderer_export_bvh(rt_renderer_h r, float* nodes, float* tris, uint32_t* num_nodes,
                            uint32_t* num_tris);
 
+/* the primary rays' tree of the current configuration (NO REFERENCE): child
+ * references int32[num_nodes][4] (rt_node4_t child encoding; leaf refs index
+ * leaf_pids) and the pid of every leaf record -- by default a per-resolution
+ * screen-space BVH4 over the covered-pixel rectangles (app/vis.h
+ * BuildScreenTree).  NULL arrays: counts only. */
+int rt_renderer_export_vis_tree(rt_renderer_h r, int32_t* refs, uint32_t* num_nodes,
+                                int32_t* leaf_pids, uint32_t* num_leaf);
+
 /* raw per-workgroup counter rows of the last launch (16 u32 each; the
  * RT_STAMPS diagnostic images put wave timestamps in slots 12-15) */
 int rt_launch_rows(rt_renderer_h r, uint32_t* rows, uint64_t max_rows, uint64_t* nrows);
+
+/* Multi-GPU frame exchange for C hosts (include/rt_shard.h, librt_shard.so,
+ * RCCL): after rt_render, gather every rank's compact tile buffer to rank 0
+ * and assemble the frame there, on the renderer's stream; rank 0 copies it
+ * to `image` (W*H ARGB8888, row 0 = NDC y = -1) when not NULL.  The
+ * renderer must be configured with shard_index / shard_count = the
+ * communicator's rank / size.  Collective.  NO REFERENCE. */
+struct rt_shard_comm;
+int rt_render_gather(rt_renderer_h r, struct rt_shard_comm* comm, uint32_t* image);
 
 /* device pointer + byte size of the output buffer (for RCCL gathers) and the
  * HIP stream the kernel runs on (for stream-ordered consumers) */

@@ -92,6 +92,9 @@ typedef struct {
   uint32_t nthreads;                /* CPU worker threads (timing baseline) */
   uint32_t row_begin, row_end;      /* render rows [begin,end) (0,0 = all) */
   uint32_t row_step;                /* every row_step-th row (0/1 = all) */
+  uint32_t vis_per_lane;            /* BVH mode: 1 = primary rays walk the tree one pixel
+                                       at a time (RT_VIS_PACKET=0 images), 0 = per wave packet
+                                       (the default images; full frames only) */
 } orc_rt_params_t;
 
 #define ORC_RT_SHADOWS 0x1u
@@ -118,6 +121,12 @@ typedef struct {
   int32_t num_nodes4;               /* > 0: traverse the 4-wide BVH instead */
   const float* nodes4;              /* [num_nodes4][32] (lo.x[4] hi.x[4] lo.y hi.y lo.z hi.z
                                        child[4] pad[4]) */
+  /* the primary rays' tree (rt_renderer_export_vis_tree; NULL / 0: walk the
+   * BVH above): child refs [num_vis_nodes][4], leaf record pids [num_vis_leaves] */
+  int32_t num_vis_nodes;
+  const int32_t* vis_refs;
+  int32_t num_vis_leaves;
+  const int32_t* vis_pids;
 } orc_bvh_t;
 
 /* Brute-force (no BVH) reference: closest hit over every geometry triangle,

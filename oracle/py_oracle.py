@@ -51,7 +51,8 @@ class RtParamsC(C.Structure):
     _fields_ = [("width", C.c_uint32), ("height", C.c_uint32), ("flags", C.c_uint32),
                 ("light", C.c_float * 3), ("clear_color", C.c_uint32),
                 ("bounces", C.c_uint32), ("seed", C.c_uint32), ("nthreads", C.c_uint32),
-                ("row_begin", C.c_uint32), ("row_end", C.c_uint32), ("row_step", C.c_uint32)]
+                ("row_begin", C.c_uint32), ("row_end", C.c_uint32), ("row_step", C.c_uint32),
+                ("vis_per_lane", C.c_uint32)]
 
 
 class RtCountersC(C.Structure):
@@ -66,7 +67,9 @@ class RtCountersC(C.Structure):
 class BvhC(C.Structure):
     _fields_ = [("num_nodes", C.c_int32), ("nodes", C.POINTER(C.c_float)),
                 ("num_tris", C.c_int32), ("tris", C.POINTER(C.c_float)),
-                ("num_nodes4", C.c_int32), ("nodes4", C.POINTER(C.c_float))]
+                ("num_nodes4", C.c_int32), ("nodes4", C.POINTER(C.c_float)),
+                ("num_vis_nodes", C.c_int32), ("vis_refs", C.POINTER(C.c_int32)),
+                ("num_vis_leaves", C.c_int32), ("vis_pids", C.POINTER(C.c_int32))]
 
 
 def build():
@@ -175,8 +178,9 @@ def vis_prims(oscene: OracleScene, width: int, height: int) -> np.ndarray:
 
 def rt_params(width, height, shadows=True, light=(0.0, 60.0, 80.0), nthreads=1,
               clear_color=CLEAR_COLOR, row_begin=0, row_end=0, row_step=0,
-              path=False, bounces=4, seed=PT_SEED):
+              path=False, bounces=4, seed=PT_SEED, vis_per_lane=False):
     p = RtParamsC()
+    p.vis_per_lane = 1 if vis_per_lane else 0
     p.width, p.height = width, height
     p.flags = (RT_SHADOWS if shadows else 0) | (RT_PATH if path else 0)
     p.bounces, p.seed = bounces, seed
@@ -187,9 +191,12 @@ def rt_params(width, height, shadows=True, light=(0.0, 60.0, 80.0), nthreads=1,
     return p
 
 
-def rt_render(oscene: OracleScene, params: RtParamsC, bvh=None):
+def rt_render(oscene: OracleScene, params: RtParamsC, bvh=None, vis_tree=None):
     """bvh: None (brute force), (nodes float32[N,16], tris float32[M,12]) or
-    (nodes, tris, nodes4 float32[N4,32]) -- the last traverses the 4-wide BVH."""
+    (nodes, tris, nodes4 float32[N4,32]) -- the last traverses the 4-wide BVH.
+    vis_tree: the primary rays' tree (refs int32[N,4], leaf pids int32[M]) as
+    the product exports it (Renderer.export_vis_tree); None = walk the BVH
+    (the frame is the same either way, the traversal counters are not)."""
     n = params.width * params.height
     color = np.zeros(n, np.uint32)
     pid = np.full(n, -1, np.int32)
@@ -206,6 +213,11 @@ def rt_render(oscene: OracleScene, params: RtParamsC, bvh=None):
         if len(bvh) > 2 and bvh[2] is not None:
             nodes4 = np.ascontiguousarray(bvh[2], np.float32)
             b.num_nodes4, b.nodes4 = nodes4.shape[0], _ptr(nodes4, C.c_float)
+        if vis_tree is not None and len(vis_tree[0]):
+            vrefs = np.ascontiguousarray(vis_tree[0], np.int32)
+            vpids = np.ascontiguousarray(vis_tree[1], np.int32)
+            b.num_vis_nodes, b.vis_refs = vrefs.shape[0], _ptr(vrefs, C.c_int32)
+            b.num_vis_leaves, b.vis_pids = vpids.shape[0], _ptr(vpids, C.c_int32)
         rc = lib().orc_rt_render_bvh(C.byref(oscene.c), C.byref(b), C.byref(params),
                                      color.ctypes.data, pid.ctypes.data, t.ctypes.data,
                                      C.byref(cnt))

@@ -77,8 +77,11 @@ typedef struct {
   int* prim_dc;                   /* drawcall of each prim */
   orc_dcstate_t* dcst;            /* [num_drawcalls] */
   orc_vis_prim_t* vis;            /* [num_prims] primary visibility (vis.c) */
-  uint32_t* vnodes;               /* [num vnodes][16] over the traversed tree */
+  uint32_t* vnodes;               /* [num vnodes][16] over the primary rays' tree */
+  int32_t* vpids;                 /* its leaf records' pids */
   uint32_t num_vnodes;
+  int32_t* vhit;                  /* [W*H] primary winner per pixel (packet pre-pass) */
+  int next_tile_row;
   float* tri;                     /* [num_prims][9] v0,e1,e2 (clip x,y,w) */
   int32_t* geom;                  /* geometry prim ids, ascending */
   int num_geom;
@@ -146,7 +149,7 @@ static int rt_prepare(rt_ctx_t* c, const orc_scene_t* s, const orc_rt_params_t* 
 
 static void rt_release(rt_ctx_t* c) {
   free(c->rp); free(c->rp_ok); free(c->prim_dc); free(c->tri); free(c->geom); free(c->dcst);
-  free(c->vis); free(c->vnodes);
+  free(c->vis); free(c->vnodes); free(c->vpids); free(c->vhit);
   pthread_mutex_destroy(&c->mu);
 }
 
@@ -195,9 +198,11 @@ static inline int32_t node_ref(const float* n, int ch) {
 /* BVH4 node step (the kernel's rt_trace.h trace(), RT_FLAG_BVH4 branch):
  * slab-test the 4 children, order the hits by tnear with the same 5-exchange
  * sorting network (strict <, misses keyed +inf, hit keys clamped to FLT_MAX),
- * continue with the nearest and push the others farthest first.  Returns the
- * next ref, or BVH_EMPTY when nothing was hit. */
-static int32_t bvh4_step(const float* n, const ray_pre_t* r, float tmin, float lim,
+ * continue with the nearest and push the others farthest first.  Any-hit
+ * walks (anyhit) key the hits by slot: fixed slot order (rt_trace.h
+ * node4_step `any`, the order of the kernels' shadow packets,
+ * occluded_packet).  Returns the next ref, or BVH_EMPTY when nothing was hit. */
+static int32_t bvh4_step(const float* n, const ray_pre_t* r, float tmin, float lim, int anyhit,
                          int32_t* stack, int* sp) {
   float key[4];
   int32_t ref[4];
@@ -214,7 +219,7 @@ static int32_t bvh4_step(const float* n, const ray_pre_t* r, float tmin, float l
     const float tn = fmaxf(fmaxf(t0, t1), fmaxf(t2, tmin));
     const float tf = fminf(fminf(u0, u1), fminf(u2, lim));
     const int h = ref[i] != BVH_EMPTY && tn <= tf;
-    key[i] = h ? fminf(tn, FLT_MAX) : INFINITY;
+    key[i] = h ? (anyhit ? (float)i : fminf(tn, FLT_MAX)) : INFINITY;
     cnt += h;
   }
   static const int net[5][2] = {{0, 1}, {2, 3}, {0, 2}, {1, 3}, {1, 2}};
@@ -248,7 +253,7 @@ static int bvh_trace(const rt_ctx_t* c, const float o[3], const float d[3], floa
     if (ref >= 0 && b->num_nodes4 > 0) {
       ++*visits;
       const int32_t nx = bvh4_step(b->nodes4 + (size_t)ref * 32, &rp, tmin, anyhit ? tmax : bt,
-                                   stack, &sp);
+                                   anyhit, stack, &sp);
       if (nx != BVH_EMPTY) { ref = nx; continue; }
     } else if (ref >= 0) {
       const float* n = b->nodes + (size_t)ref * 16;
@@ -260,7 +265,7 @@ static int bvh_trace(const rt_ctx_t* c, const float o[3], const float d[3], floa
       const int h1 = (c1 != BVH_EMPTY) && slab(n, 1, &rp, tmin, lim, &tn1);
       if (h0 && h1) {
         int32_t near = c0, far = c1;
-        if (tn1 < tn0) { near = c1; far = c0; }
+        if (!anyhit && tn1 < tn0) { near = c1; far = c0; }  /* any-hit: slot order */
         if (sp < BVH_STACK) stack[sp++] = far;
         ref = near;
         continue;
@@ -367,7 +372,6 @@ static int32_t vnode_step(const uint32_t* n, uint32_t px, uint32_t py, uint32_t 
 }
 
 static int vis_trace(const rt_ctx_t* c, uint32_t px, uint32_t py, uint64_t* visits, uint64_t* tests) {
-  const orc_bvh_t* b = c->bvh;
   if (c->num_vnodes == 0) return -1;
   int32_t stack[BVH_STACK];
   int sp = 0;
@@ -383,16 +387,138 @@ static int vis_trace(const rt_ctx_t* c, uint32_t px, uint32_t py, uint64_t* visi
       const uint32_t lr = (uint32_t)ref;
       const uint32_t first = (lr >> 4) & 0x07ffffffu, count = (lr & 15u) + 1u;
       for (uint32_t k = 0; k < count; ++k) {
-        int32_t pid;
-        memcpy(&pid, &b->tris[(size_t)(first + k) * 12 + 3], 4);
         ++*tests;
-        vis_test(c, pid, px, py, &bz, &bpid);
+        vis_test(c, c->vpids[first + k], px, py, &bz, &bpid);
       }
     }
     if (sp == 0) break;
     ref = stack[--sp];
   }
   return bpid;
+}
+
+/* Packet form (the kernels' trace_primary_packet, RT_VIS_PACKET): the
+ * wave's pixels walk the tree together -- a child is entered when some
+ * lane's pixel lies in its rectangle with a bound that can still beat that
+ * lane's best; entered children sorted by bound, nearest taken, the others
+ * pushed farthest first; every lane tests every leaf primitive of the walk.
+ * n lanes at (px[i], py[i]); out[i] = winner.  Visits and tests count once
+ * per packet. */
+#define PK_LANES 64
+static void vis_trace_packet(const rt_ctx_t* c, int n, const uint32_t* px, const uint32_t* py,
+                             int32_t* out, uint64_t* visits, uint64_t* tests) {
+  uint32_t bz[PK_LANES];
+  int bpid[PK_LANES];
+  for (int i = 0; i < n; ++i) { bz[i] = VX_OM_DEPTH_MASK; bpid[i] = -1; out[i] = -1; }
+  if (c->num_vnodes == 0 || n == 0) return;
+  int32_t stack[BVH_STACK];
+  int sp = 0;
+  int32_t ref = 0;
+  for (;;) {
+    if (ref >= 0) {
+      ++*visits;
+      const uint32_t* nd = c->vnodes + (size_t)ref * 16;
+      uint32_t key[4];
+      int32_t r[4];
+      int cnt = 0;
+      for (int k = 0; k < 4; ++k) {
+        r[k] = (int32_t)nd[12 + k];
+        int need = 0;
+        if (r[k] != BVH_EMPTY)
+          for (int i = 0; i < n && !need; ++i)
+            need = rect_in(nd[k], px[i]) && rect_in(nd[4 + k], py[i]) && nd[8 + k] <= bz[i];
+        key[k] = need ? nd[8 + k] : 0xffffffffu;
+        cnt += need;
+      }
+      static const int net[5][2] = {{0, 1}, {2, 3}, {0, 2}, {1, 3}, {1, 2}};
+      for (int e = 0; e < 5; ++e) {
+        const int a = net[e][0], b = net[e][1];
+        if (key[b] < key[a]) {
+          const uint32_t tk = key[a]; key[a] = key[b]; key[b] = tk;
+          const int32_t tr = r[a]; r[a] = r[b]; r[b] = tr;
+        }
+      }
+      if (cnt > 0) {
+        for (int i = cnt - 1; i >= 1; --i)
+          if (sp < BVH_STACK) stack[sp++] = r[i];
+        ref = r[0];
+        continue;
+      }
+    } else {
+      const uint32_t lr = (uint32_t)ref;
+      const uint32_t first = (lr >> 4) & 0x07ffffffu, count = (lr & 15u) + 1u;
+      for (uint32_t k = 0; k < count; ++k) {
+        ++*tests;
+        for (int i = 0; i < n; ++i) vis_test(c, c->vpids[first + k], px[i], py[i], &bz[i], &bpid[i]);
+      }
+    }
+    if (sp == 0) break;
+    ref = stack[--sp];
+  }
+  for (int i = 0; i < n; ++i) out[i] = bpid[i];
+}
+
+/* tile (tx, ty) runs as 32-pixel waves (8x4 half blocks) in the path tracer
+ * iff some geometry primitive covers a pixel of it (the host's split rule,
+ * rt_app.cpp: tiles any covered-pixel rectangle reaches) */
+static int tile_split(const rt_ctx_t* c, uint32_t tx, uint32_t ty) {
+  if (!(c->p.flags & ORC_RT_PATH)) return 0;
+  const uint32_t x0 = tx * 32, x1 = x0 + 31, y0 = ty * 32, y1 = y0 + 31;
+  for (int k = 0; k < c->num_geom; ++k) {
+    const orc_vis_prim_t* v = &c->vis[c->geom[k]];
+    if (!v->any) continue;
+    if ((v->rx & 0xffffu) <= x1 && (v->rx >> 16) >= x0 && (v->ry & 0xffffu) <= y1 && (v->ry >> 16) >= y0)
+      return 1;
+  }
+  return 0;
+}
+
+/* the primary pre-pass over one row of 32x32 tiles: every wave's packet
+ * (8x8 blocks, or 8x4 halves in split tiles, the kernels' task_map) */
+static void vis_tile_row(rt_ctx_t* c, uint32_t ty, orc_rt_counters_t* k) {
+  const uint32_t W = c->p.width, H = c->p.height;
+  const uint32_t ntx = (W + 31) / 32;
+  uint32_t px[PK_LANES], py[PK_LANES];
+  int32_t out[PK_LANES];
+  int32_t idx[PK_LANES];
+  for (uint32_t tx = 0; tx < ntx; ++tx) {
+    const int split = tile_split(c, tx, ty);
+    const int waves = split ? 32 : 16, lanes = split ? 32 : 64;
+    for (int wv = 0; wv < waves; ++wv) {
+      int n = 0;
+      for (int ln = 0; ln < lanes; ++ln) {
+        const uint32_t ti = split ? (((uint32_t)wv >> 1) << 6) + (uint32_t)ln + (((uint32_t)wv & 1u) << 5)
+                                  : ((uint32_t)wv << 6) + (uint32_t)ln;
+        const uint32_t blk = ti >> 6, l = ti & 63u;
+        const uint32_t x = tx * 32 + (blk & 3u) * 8 + (l & 7u), y = ty * 32 + (blk >> 2) * 8 + (l >> 3);
+        if (x >= W || y >= H) continue;
+        px[n] = x; py[n] = y; idx[n] = (int32_t)(y * W + x);
+        ++n;
+      }
+      if (n == 0) continue;
+      vis_trace_packet(c, n, px, py, out, &k->node_visits, &k->tri_tests);
+      for (int i = 0; i < n; ++i) c->vhit[idx[i]] = out[i];
+    }
+  }
+}
+
+static void* vis_worker(void* arg) {
+  rt_ctx_t* c = (rt_ctx_t*)arg;
+  orc_rt_counters_t k;
+  memset(&k, 0, sizeof(k));
+  const uint32_t nty = (c->p.height + 31) / 32;
+  for (;;) {
+    pthread_mutex_lock(&c->mu);
+    const int i = c->next_tile_row++;
+    pthread_mutex_unlock(&c->mu);
+    if ((uint32_t)i >= nty) break;
+    vis_tile_row(c, (uint32_t)i, &k);
+  }
+  pthread_mutex_lock(&c->mu);
+  c->cnt.node_visits += k.node_visits;
+  c->cnt.tri_tests += k.tri_tests;
+  pthread_mutex_unlock(&c->mu);
+  return NULL;
 }
 
 /* flat list: every geometry primitive, ascending pid */
@@ -419,25 +545,37 @@ static float plane_t(const float o[3], const float d[3], const float* tri) {
 
 static void vis_build_nodes(rt_ctx_t* c) {
   const orc_bvh_t* b = c->bvh;
-  if (!b || b->num_nodes <= 0) return;
-  const uint32_t n = (uint32_t)(b->num_nodes4 > 0 ? b->num_nodes4 : b->num_nodes);
-  int32_t* refs = (int32_t*)malloc(sizeof(int32_t) * 4 * n);
-  for (uint32_t i = 0; i < n; ++i)
-    for (int k = 0; k < 4; ++k) {
-      int32_t r = BVH_EMPTY;
-      if (b->num_nodes4 > 0) memcpy(&r, &b->nodes4[(size_t)i * 32 + 24 + k], 4);
-      else if (k < 2) memcpy(&r, &b->nodes[(size_t)i * 16 + 12 + k], 4);
-      refs[i * 4 + k] = r;
-    }
-  int32_t* pids = (int32_t*)malloc(sizeof(int32_t) * (b->num_tris > 0 ? b->num_tris : 1));
-  for (int k = 0; k < b->num_tris; ++k) memcpy(&pids[k], &b->tris[(size_t)k * 12 + 3], 4);
+  if (!b) return;
+  uint32_t n, m;
+  int32_t *refs, *pids;
+  if (b->vis_refs && b->num_vis_nodes > 0) {  /* the product's primary tree */
+    n = (uint32_t)b->num_vis_nodes;
+    m = (uint32_t)b->num_vis_leaves;
+    refs = (int32_t*)malloc(sizeof(int32_t) * 4 * n);
+    pids = (int32_t*)malloc(sizeof(int32_t) * (m ? m : 1));
+    memcpy(refs, b->vis_refs, sizeof(int32_t) * 4 * n);
+    memcpy(pids, b->vis_pids, sizeof(int32_t) * m);
+  } else {                                     /* the secondary rays' BVH */
+    if (b->num_nodes <= 0) return;
+    n = (uint32_t)(b->num_nodes4 > 0 ? b->num_nodes4 : b->num_nodes);
+    m = (uint32_t)b->num_tris;
+    refs = (int32_t*)malloc(sizeof(int32_t) * 4 * n);
+    for (uint32_t i = 0; i < n; ++i)
+      for (int k = 0; k < 4; ++k) {
+        int32_t r = BVH_EMPTY;
+        if (b->num_nodes4 > 0) memcpy(&r, &b->nodes4[(size_t)i * 32 + 24 + k], 4);
+        else if (k < 2) memcpy(&r, &b->nodes[(size_t)i * 16 + 12 + k], 4);
+        refs[i * 4 + k] = r;
+      }
+    pids = (int32_t*)malloc(sizeof(int32_t) * (m ? m : 1));
+    for (uint32_t k = 0; k < m; ++k) memcpy(&pids[k], &b->tris[(size_t)k * 12 + 3], 4);
+  }
   c->vnodes = (uint32_t*)malloc(sizeof(uint32_t) * 16 * n);
+  c->vpids = pids;
   c->num_vnodes = n;
-  if (orc_vis_nodes(refs, n, pids, (uint32_t)b->num_tris, c->vis, (uint32_t)c->scene->num_prims,
-                    c->vnodes) != 0)
+  if (orc_vis_nodes(refs, n, pids, m, c->vis, (uint32_t)c->scene->num_prims, c->vnodes) != 0)
     c->num_vnodes = 0;
   free(refs);
-  free(pids);
 }
 
 static inline uint32_t shadow_attenuate(uint32_t c) {
@@ -592,8 +730,9 @@ static void rt_row(rt_ctx_t* c, uint32_t y, orc_rt_counters_t* k) {
                         fmaf((float)y + 0.5f, c->sy, -1.0f), 1.0f};
     ++k->primary_rays;
     /* primary visibility: the raster's winner at this pixel */
-    const int hit = c->bvh ? vis_trace(c, x, y, &k->node_visits, &k->tri_tests)
-                           : vis_brute(c, x, y, &k->tri_tests);
+    const int hit = c->vhit ? c->vhit[(uint64_t)y * W + x]
+                 : c->bvh ? vis_trace(c, x, y, &k->node_visits, &k->tri_tests)
+                          : vis_brute(c, x, y, &k->tri_tests);
     uint32_t col = c->p.clear_color;
     int32_t opid = -1;
     float t = 0.0f;
@@ -675,6 +814,19 @@ static int rt_run(const orc_scene_t* scene, const orc_bvh_t* bvh, const orc_rt_p
   vis_build_nodes(&c);
   c.color = color; c.pid = pid; c.tout = t;
   const uint32_t nt = p->nthreads > 1 ? p->nthreads : 1;
+  if (bvh && !p->vis_per_lane && p->row_begin == 0 && p->row_end == 0 && p->row_step <= 1) {
+    /* primary visibility as the kernels walk it: one packet per wave */
+    c.vhit = (int32_t*)malloc(sizeof(int32_t) * (size_t)p->width * p->height);
+    c.next_tile_row = 0;
+    if (nt == 1) {
+      vis_worker(&c);
+    } else {
+      pthread_t* th = (pthread_t*)malloc(sizeof(pthread_t) * nt);
+      for (uint32_t i = 0; i < nt; ++i) pthread_create(&th[i], NULL, vis_worker, &c);
+      for (uint32_t i = 0; i < nt; ++i) pthread_join(th[i], NULL);
+      free(th);
+    }
+  }
   if (nt == 1) {
     rt_worker(&c);
   } else {

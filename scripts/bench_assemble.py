@@ -16,7 +16,7 @@ sys.path.insert(0, ROOT)
 def main():
     import torch
     from skybox_rt_amd import _lib, shard
-    f = _lib.load("libframe_assemble.so").rt_frame_assemble
+    f = _lib.load("librt_shard.so").rt_frame_assemble
     f.restype = ctypes.c_int
     f.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint32,
                   ctypes.c_uint32, ctypes.c_uint64, ctypes.c_void_p]

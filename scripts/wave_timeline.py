@@ -28,6 +28,11 @@ def main():
         r.render()
     rows = r.launch_rows().astype(np.int64)
     kms = r.kernel_ms()
+    # the same frame through the instrumented image: per-wave sums of the
+    # lanes' node visits (slot 3 + RT_STAT_NODE_VISITS) and triangle tests
+    r.configure(size, size, shadows=True, path=path, instrumented=True)
+    r.render()
+    irows = r.launch_rows().astype(np.int64)
     base = rows[:, 12].min()
     t0 = rows[:, 12] - base
     end = rows[:, 13] - base
@@ -60,6 +65,24 @@ def main():
                         "shadow_drain_us": float(drain[slow].mean()) / 100,
                         "start_us": float(t0[slow].mean()) / 100}
     out["all"] = {"primary_us": float(prim.mean()) / 100, "shadow_drain_us": float(drain.mean()) / 100}
+    # wave-level loop iterations (RT_WAVE_ITER): primary node steps (slot 7),
+    # primary leaf rounds (8), secondary-ray node steps + leaf rounds (9)
+    it = rows[:, 7:10]
+    out["slowest50"].update({"primary_node_iters": float(it[slow, 0].mean()),
+                             "primary_leaf_iters": float(it[slow, 1].mean()),
+                             "secondary_iters": float(it[slow, 2].mean()),
+                             "us_per_iter": float(dur[slow].mean() / 100 / max(1.0, it[slow].sum(1).mean())),
+                             "lane_visits_avg": float(irows[slow, 7].mean()) / 64,
+                             "lane_tri_tests_avg": float(irows[slow, 8].mean()) / 64})
+    if not path:  # phase stamps (RT_STAMPS rt_kernel): 3 before primary, 14 primary done,
+        # 4 layers done, 11 shaded, 5 queued/stored, 6 non-final drain start, 15 final drain
+        ph = lambda a, b: float((rows[slow, b] - rows[slow, a]).mean()) / 100  # noqa: E731
+        out["slowest50"]["phases_us"] = {
+            "to_primary": ph(12, 3), "primary": ph(3, 14), "layers": ph(14, 4), "shade": ph(4, 11),
+            "plane_queue": ph(11, 5), "to_final_drain": ph(5, 15), "final_drain": ph(15, 13),
+            "nonfinal_drains": int((rows[slow, 6] > 0).sum())}
+    out["all"].update({"primary_node_iters": float(it[:, 0].mean()), "primary_leaf_iters": float(it[:, 1].mean()),
+                       "secondary_iters": float(it[:, 2].mean())})
     # background (short) waves: where their time goes -- start -> primary
     # traced (prologue, task map, traversal) and primary traced -> end
     # (layers, shading, store, counter flush)

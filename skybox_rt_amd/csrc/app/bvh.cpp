@@ -341,6 +341,17 @@ int BuildBvh(const std::vector<BuildTri>& tris, Bvh* out, std::string* error) {
   if (const char* v = std::getenv("RT_BVH_LEAF")) bp.leaf_size = (uint32_t)std::atoi(v);
   if (const char* v = std::getenv("RT_BVH_BINS")) bp.bins = (uint32_t)std::atoi(v);
   if (const char* v = std::getenv("RT_BVH_AXES")) bp.all_axes = std::atoi(v) == 3;
+  if (const char* v = std::getenv("RT_BVH_F16")) bp.f16_boxes = std::atoi(v) != 0;
+  return BuildBvhWith(tris, bp, out, error);
+}
+
+int BuildBvhWith(const std::vector<BuildTri>& tris, const BvhParams& bp, Bvh* out,
+                 std::string* error) {
+  if (out == nullptr) return -1;
+  if (tris.size() >= (1u << 26)) {
+    if (error) *error = "too many triangles for the 27-bit leaf index";
+    return -1;
+  }
   if (bp.leaf_size < 1 || bp.leaf_size > 4 || bp.bins < 2 || bp.bins > kBvhMaxBins) {
     if (error) *error = "bad BVH build parameters (leaf 1..4, bins 2..64)";
     return -1;
@@ -351,7 +362,6 @@ int BuildBvh(const std::vector<BuildTri>& tris, Bvh* out, std::string* error) {
   // binary16 box planes: round every BVH4 box outward (RT_BVH_F16=0 keeps
   // the fp32 planes, rt_node4h_t is then not uploaded), pack rt_node4h_t and
   // check that it decodes to exactly rt_node4_t's planes
-  if (const char* v = std::getenv("RT_BVH_F16")) bp.f16_boxes = std::atoi(v) != 0;
   out->nodes4h.clear();
   if (bp.f16_boxes) {
     out->nodes4h.resize(out->nodes4.size());

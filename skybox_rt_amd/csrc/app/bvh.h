@@ -46,5 +46,7 @@ struct BvhParams {
 };
 
 int BuildBvh(const std::vector<BuildTri>& tris, Bvh* out, std::string* error);
+// the same with explicit parameters (no environment knobs)
+int BuildBvhWith(const std::vector<BuildTri>& tris, const BvhParams& bp, Bvh* out, std::string* error);
 
 }  // namespace rt

@@ -7,6 +7,11 @@
 // and the mode: default ray tracing (primary [+ shadow]), -R the draw3d
 // raster pipeline (draw3d's own default path), -P N path tracing with N
 // bounces, -F the flat triangle list (no BVH).
+// Multi-GPU (one process per GPU, C host over librt_shard.so / RCCL):
+// -G rank,ranks -I idfile: this process renders 32x32 tiles t with
+// t % ranks == rank, rank 0 writes the RCCL communicator id to `idfile` (the
+// other ranks wait for it), every frame ends with rt_render_gather to rank
+// 0, which writes / checks the assembled frame.
 #include <getopt.h>
 
 #include <cstdio>
@@ -15,7 +20,15 @@
 #include <string>
 #include <vector>
 
+#include <sys/stat.h>
+#include <unistd.h>
+
+#include <chrono>
+#include <fstream>
+#include <thread>
+
 #include "png.h"
+#include "rt_shard.h"
 #include "vx_rt.h"
 
 namespace {
@@ -28,12 +41,14 @@ uint32_t width = 128, height = 128, repeat = 1;
 bool shadows = false, raster = false, flat = false;
 int bounces = -1;  // >= 0: path tracing
 float light[3] = {0.0f, 60.0f, 80.0f};
+int rank = -1, ranks = 1;            // -G rank,ranks
+const char* id_file = "rt_shard.id";  // -I
 
 void usage() {
   std::printf("Skybox MI355X ray-tracing test.\n"
               "Usage: [-t trace] [-o output|null] [-r reference] [-w width] [-h height]"
               " [-S shadows] [-L x,y,w] [-n repeat] [-k kernel_dir]"
-              " [-R raster | -P bounces | -F flat]\n");
+              " [-R raster | -P bounces | -F flat] [-G rank,ranks [-I idfile]]\n");
 }
 
 #define RT_CHECK(_expr)                                                       \
@@ -48,7 +63,7 @@ void usage() {
 
 int main(int argc, char** argv) {
   int c;
-  while ((c = getopt(argc, argv, "t:o:r:w:h:n:k:L:P:SRF?")) != -1) {
+  while ((c = getopt(argc, argv, "t:o:r:w:h:n:k:L:P:G:I:SRF?")) != -1) {
     switch (c) {
     case 't': trace_file = optarg; break;
     case 'o': output_file = optarg; break;
@@ -62,6 +77,8 @@ int main(int argc, char** argv) {
     case 'F': flat = true; break;
     case 'P': bounces = std::atoi(optarg); break;
     case 'L': std::sscanf(optarg, "%f,%f,%f", &light[0], &light[1], &light[2]); break;
+    case 'G': std::sscanf(optarg, "%d,%d", &rank, &ranks); break;
+    case 'I': id_file = optarg; break;
     case '?': usage(); return 0;
     default: usage(); return -1;
     }
@@ -69,6 +86,34 @@ int main(int argc, char** argv) {
   if (std::strcmp(output_file, "null") == 0 && reference_file) {
     std::printf("Error: the output file is missing for reference validation!\n");
     return 1;
+  }
+  const bool sharded = rank >= 0;
+  if (sharded && (ranks < 1 || rank >= ranks || raster)) {
+    std::printf("Error: -G rank,ranks needs 0 <= rank < ranks (ray-tracing modes)\n");
+    return 1;
+  }
+  int device = 0;
+  rt_shard_comm_h comm = nullptr;
+  uint8_t id[RT_SHARD_ID_BYTES] = {};
+  if (sharded) {
+    // one process per GPU: rank r on device r % (visible devices)
+    const int ndev = rt_shard_device_count();
+    device = ndev > 0 ? rank % ndev : 0;
+    setenv("VX_HIP_DEVICE", std::to_string(device).c_str(), 0);
+    device = std::atoi(std::getenv("VX_HIP_DEVICE"));
+    if (rank == 0) {  // the communicator id, published atomically
+      RT_CHECK(rt_shard_unique_id(id));
+      const std::string tmp = std::string(id_file) + ".tmp";
+      std::ofstream(tmp, std::ios::binary).write((const char*)id, RT_SHARD_ID_BYTES);
+      RT_CHECK(std::rename(tmp.c_str(), id_file));
+    } else {
+      struct stat sb;
+      for (int i = 0; stat(id_file, &sb) != 0 || sb.st_size < RT_SHARD_ID_BYTES; ++i) {
+        if (i > 6000) { std::printf("Error: no communicator id in %s\n", id_file); return 1; }
+        std::this_thread::sleep_for(std::chrono::milliseconds(10));
+      }
+      std::ifstream(id_file, std::ios::binary).read((char*)id, RT_SHARD_ID_BYTES);
+    }
   }
   rt_scene_h scene = nullptr;
   RT_CHECK(rt_scene_load(trace_file, &scene));
@@ -93,13 +138,26 @@ int main(int argc, char** argv) {
   std::memcpy(p.light, light, sizeof(light));
   p.clear_color = 0xff000000u;
   p.shard_count = 1;
+  if (sharded) {
+    p.shard_index = (uint32_t)rank;
+    p.shard_count = (uint32_t)ranks;
+    p.flags |= RT_RENDER_COMPACT;
+    RT_CHECK(rt_shard_comm_init(&comm, id, (uint32_t)rank, (uint32_t)ranks, device));
+    uint32_t seen = 0;
+    RT_CHECK(rt_shard_comm_info(comm, nullptr, &seen));
+    std::printf("Shard: rank %d of %d on device %d (communicator: %u ranks)\n", rank, ranks, device,
+                seen);
+  }
   RT_CHECK(rt_renderer_configure(r, &p));
   double total = 0.0;
   rt_stats_t st;
+  std::vector<uint32_t> gathered;
+  if (sharded && rank == 0) gathered.resize((size_t)width * height);
   for (uint32_t i = 0; i < repeat; ++i) {
     RT_CHECK(rt_render(r));
     RT_CHECK(rt_render_stats(r, &st));
     total += st.kernel_ms;
+    if (sharded) RT_CHECK(rt_render_gather(r, comm, rank == 0 ? gathered.data() : nullptr));
   }
   if (raster) {
     std::printf("Elapsed time: %.4f ms/frame (grid %u x %u), pixels=%llu, fragments=%llu, "
@@ -115,9 +173,10 @@ int main(int argc, char** argv) {
                 (unsigned long long)st.occluded, rays / (total / repeat) * 1e-3);
   }
   int errors = 0;
-  if (std::strcmp(output_file, "null") != 0) {
+  if (std::strcmp(output_file, "null") != 0 && (!sharded || rank == 0)) {
     std::vector<uint32_t> fb((size_t)width * height);
-    RT_CHECK(rt_read_framebuffer(r, fb.data(), fb.size()));
+    if (sharded) fb = gathered;  // the frame assembled from every rank's tiles
+    else RT_CHECK(rt_read_framebuffer(r, fb.data(), fb.size()));
     RT_CHECK(rt::SavePngARGB(output_file, fb.data(), width, height));
     if (reference_file) {
       std::vector<uint32_t> out, ref;
@@ -136,5 +195,6 @@ int main(int argc, char** argv) {
   }
   rt_renderer_free(r);
   rt_scene_free(scene);
+  if (comm) rt_shard_comm_free(comm);
   return errors;
 }

@@ -28,6 +28,7 @@
 #include "setup.h"
 #include "vis.h"
 #include "vortex.h"
+#include "rt_shard.h"
 #include "vortex_hip.h"
 #include "vx_rt.h"
 
@@ -81,6 +82,7 @@ struct rt_renderer {
   vx_buffer_h ptris = nullptr, geom = nullptr, oms = nullptr, bbox = nullptr, zbuf = nullptr;
   vx_buffer_h order = nullptr;
   vx_buffer_h vnodes = nullptr, vtris = nullptr, vlayers = nullptr, vgeom = nullptr;
+  vx_buffer_h gather_recv = nullptr, gather_image = nullptr;  // rank 0 of rt_render_gather
   vx_buffer_h prims = nullptr, cbuf = nullptr, args = nullptr;
   uint64_t cbuf_bytes = 0;
   rt_render_params_t params{};
@@ -95,6 +97,9 @@ struct rt_renderer {
   vx_hip_set_counters_t set_counters = nullptr;
   std::string kdir;         // kernel directory (images missing there come from lib_dir)
   bool deep = false;        // RT/PT images with the 32-entry traversal stack
+  // the primary rays' tree of the current configuration (rt_renderer_export_vis_tree)
+  std::vector<std::array<int32_t, 4>> vis_refs;
+  std::vector<int32_t> vis_pids;
   bool gpu_bvh = false;     // nodes/tris were built on the device (rt_renderer_build_bvh)
   bool gpu_bvh4 = false;    // ... and collapsed to a BVH4 there whose stack fits the images
   uint32_t num_tris = 0;    // leaf triangle records (without the 3 padding records)
@@ -103,7 +108,7 @@ struct rt_renderer {
     vx_buffer_h* bufs[] = {&krnl[0][0], &krnl[0][1], &krnl[1][0], &krnl[1][1], &krnl[2][0],
                            &krnl[2][1], &krnl[3][0], &nodes, &nodes4, &tris, &layers, &dcs, &tex,
                            &ptris, &geom, &oms, &bbox, &zbuf, &order, &vnodes, &vtris, &vlayers,
-                           &vgeom, &prims, &cbuf, &args};
+                           &vgeom, &gather_recv, &gather_image, &prims, &cbuf, &args};
     for (auto* b : bufs) {
       if (*b) vx_mem_free(*b);
       *b = nullptr;
@@ -350,6 +355,17 @@ int rt_renderer_create(rt_scene_h s, const char* kernel_dir, rt_renderer_h* out)
   return 0;
 }
 
+int rt_renderer_export_vis_tree(rt_renderer_h r, int32_t* refs, uint32_t* num_nodes,
+                                int32_t* leaf_pids, uint32_t* num_leaf) {
+  if (!r || !r->configured) return fail("renderer not configured");
+  if (num_nodes) *num_nodes = (uint32_t)r->vis_refs.size();
+  if (num_leaf) *num_leaf = (uint32_t)r->vis_pids.size();
+  if (refs && !r->vis_refs.empty()) std::memcpy(refs, r->vis_refs.data(), r->vis_refs.size() * 16);
+  if (leaf_pids && !r->vis_pids.empty())
+    std::memcpy(leaf_pids, r->vis_pids.data(), r->vis_pids.size() * 4);
+  return 0;
+}
+
 int rt_renderer_free(rt_renderer_h r) {
   delete r;
   return 0;
@@ -394,64 +410,128 @@ int rt_scene_setup_vis(rt_scene_h s, uint32_t width, uint32_t height, uint32_t* 
   return 0;
 }
 
+int rt_scene_vis_tree(rt_scene_h s, uint32_t width, uint32_t height, float depth_scale,
+                      int32_t* refs, uint32_t* num_nodes, int32_t* leaf_pids, uint32_t* num_leaf,
+                      uint32_t* stack4) {
+  if (!s || width == 0 || height == 0) return fail("bad argument");
+  std::vector<rt::VisPrim> vis(s->scene.prims.size());
+  for (size_t d = 0; d < s->scene.drawcalls.size(); ++d) {
+    const rt::DrawCall& dc = s->scene.drawcalls[d];
+    for (uint32_t i = 0; i < dc.prim_count; ++i) {
+      const uint32_t g = dc.prim_offset + i;
+      rt_prim_t p;
+      rt_bbox_t bb{0, 0};
+      const bool ok = rt::PrimSetup(s->scene.prims[g], width, height, dc.viewport[4],
+                                    dc.viewport[5], &p) == rt::kSetupOk &&
+                      rt::PrimBBox(s->scene.prims[g], width, height, &bb) == rt::kSetupOk;
+      vis[g] = rt::ComputeVisPrim(p, ok, bb, width, height);
+    }
+  }
+  std::vector<std::array<int32_t, 4>> rf;
+  std::vector<int32_t> lp;
+  uint32_t st = 0;
+  if (rt::BuildScreenTree(vis, s->geometry, depth_scale, &rf, &lp, &st) != 0)
+    return fail("screen tree build failed");
+  if (num_nodes) *num_nodes = (uint32_t)rf.size();
+  if (num_leaf) *num_leaf = (uint32_t)lp.size();
+  if (stack4) *stack4 = st;
+  if (refs && !rf.empty()) std::memcpy(refs, rf.data(), rf.size() * 16);
+  if (leaf_pids && !lp.empty()) std::memcpy(leaf_pids, lp.data(), lp.size() * 4);
+  return 0;
+}
+
+namespace {
+
+int load_image(rt_renderer* r, const std::string& name, vx_buffer_h* out) {
+  std::string path = r->kdir + "/" + name;
+  if (FILE* f = std::fopen(path.c_str(), "rb")) std::fclose(f);
+  else path = lib_dir() + "/" + name;
+  if (*out) vx_mem_free(*out);
+  *out = nullptr;
+  return vx_upload_kernel_file(r->dev, path.c_str(), out) == 0 ? 0 : fail("cannot upload kernel " + path);
+}
+
+// the RT / PT images with the 32-entry traversal stack
+int load_deep_images(rt_renderer* r) {
+  if (load_image(r, "rt_kernel_deep.vxbin", &r->krnl[0][0]) ||
+      load_image(r, "rt_kernel_deep_stats.vxbin", &r->krnl[0][1]) ||
+      load_image(r, "pt_kernel_deep.vxbin", &r->krnl[1][0]) ||
+      load_image(r, "pt_kernel_deep_stats.vxbin", &r->krnl[1][1]))
+    return -1;
+  r->deep = true;
+  return 0;
+}
+
+}  // namespace
+
 // Per-resolution primary-visibility records (app/vis.h): every primitive's
 // covered-pixel rectangle and depth bound, the leaf / layer / flat-list
 // rt_vtri_t records and the rt_vnode_t of the tree the kernels traverse
 // (host tree, or the device tree read back).
-static int configure_vis(rt_renderer* r, const rt_render_params_t* p,
-                         const std::vector<rt_prim_t>& prims, const std::vector<uint8_t>& setup_ok,
-                         bool use_bvh4) {
+static int configure_vis(rt_renderer* r, const std::vector<rt_prim_t>& prims,
+                         const std::vector<rt::VisPrim>& vis, bool use_bvh4) {
   const rt_scene* s = r->sc;
   rt_kernel_arg_t& a = r->arg;
-  std::vector<rt::VisPrim> vis(prims.size());
-  for (size_t g = 0; g < prims.size(); ++g) {
-    rt_bbox_t bb{0, 0};
-    const bool ok = setup_ok[g] &&
-                    rt::PrimBBox(s->scene.prims[g], p->width, p->height, &bb) == rt::kSetupOk;
-    vis[g] = rt::ComputeVisPrim(prims[g], ok, bb, p->width, p->height);
-  }
-  // the traversed tree's child references and the leaf records' pids
+  // the primary rays' tree: the secondary rays' tree (the host tree or the
+  // device tree read back), whose nodes get the pixel rectangles and depth
+  // bounds of their subtrees.  Env RT_VIS_TREE=screen: a per-resolution
+  // screen-space BVH4 over the rectangles (rt::BuildScreenTree) -- fewer
+  // visits per ray (tekkaman 1024^2: 8.6 vs 9.3) but measured 6 % slower
+  // (profiles/r02f_ab.json)
   std::vector<std::array<int32_t, 4>> refs;
   std::vector<int32_t> leaf_pids;
-  std::vector<rt_node4_t> n4;
-  std::vector<rt_node_t> n2;
-  std::vector<rt_tri_t> tr;
-  if (r->gpu_bvh) {
-    tr.resize(r->num_tris);
-    if (r->num_tris && vx_copy_from_dev(tr.data(), r->tris, 0, tr.size() * sizeof(rt_tri_t)) != 0)
-      return fail("vx_copy_from_dev failed");
-    if (use_bvh4) {
-      n4.resize(a.num_nodes4);
-      if (!n4.empty() && vx_copy_from_dev(n4.data(), r->nodes4, 0, n4.size() * sizeof(rt_node4_t)) != 0)
+  const char* vt = std::getenv("RT_VIS_TREE");
+  if (vt && std::string(vt) == "screen") {
+    float dscale = 0.0f;
+    if (const char* e = std::getenv("RT_VIS_DEPTH_SCALE")) dscale = (float)std::atof(e);
+    uint32_t stack = 0;
+    if (rt::BuildScreenTree(vis, s->geometry, dscale, &refs, &leaf_pids, &stack) != 0)
+      return fail("screen tree build failed");
+    if (stack > RT_STACK_DEEP) return fail("screen tree deeper than the traversal stack");
+    if (stack > RT_STACK_SHALLOW && !r->deep && load_deep_images(r) != 0) return -1;
+  } else {
+    std::vector<rt_node4_t> n4;
+    std::vector<rt_node_t> n2;
+    std::vector<rt_tri_t> tr;
+    if (r->gpu_bvh) {
+      tr.resize(r->num_tris);
+      if (r->num_tris && vx_copy_from_dev(tr.data(), r->tris, 0, tr.size() * sizeof(rt_tri_t)) != 0)
         return fail("vx_copy_from_dev failed");
+      if (use_bvh4) {
+        n4.resize(a.num_nodes4);
+        if (!n4.empty() && vx_copy_from_dev(n4.data(), r->nodes4, 0, n4.size() * sizeof(rt_node4_t)) != 0)
+          return fail("vx_copy_from_dev failed");
+      } else {
+        n2.resize(a.num_nodes);
+        if (!n2.empty() && vx_copy_from_dev(n2.data(), r->nodes, 0, n2.size() * sizeof(rt_node_t)) != 0)
+          return fail("vx_copy_from_dev failed");
+      }
     } else {
-      n2.resize(a.num_nodes);
-      if (!n2.empty() && vx_copy_from_dev(n2.data(), r->nodes, 0, n2.size() * sizeof(rt_node_t)) != 0)
-        return fail("vx_copy_from_dev failed");
+      tr = s->bvh.tris;
+      if (use_bvh4) n4 = s->bvh.nodes4;
+      else n2 = s->bvh.nodes;
     }
-  } else {
-    tr = s->bvh.tris;
-    if (use_bvh4) n4 = s->bvh.nodes4;
-    else n2 = s->bvh.nodes;
-  }
-  for (const rt_tri_t& t : tr) {
-    int32_t pid;
-    std::memcpy(&pid, &t.v[3], 4);
-    leaf_pids.push_back(pid);
-  }
-  if (use_bvh4) {
-    for (const rt_node4_t& n : n4) {
-      std::array<int32_t, 4> c;
-      std::memcpy(c.data(), &n.v[24], 16);
-      refs.push_back(c);
+    for (const rt_tri_t& t : tr) {
+      int32_t pid;
+      std::memcpy(&pid, &t.v[3], 4);
+      leaf_pids.push_back(pid);
     }
-  } else {
-    for (const rt_node_t& n : n2) {
-      std::array<int32_t, 4> c = {RT_EMPTY_REF, RT_EMPTY_REF, RT_EMPTY_REF, RT_EMPTY_REF};
-      std::memcpy(c.data(), &n.v[12], 8);
-      refs.push_back(c);
+    if (use_bvh4) {
+      for (const rt_node4_t& n : n4) {
+        std::array<int32_t, 4> c;
+        std::memcpy(c.data(), &n.v[24], 16);
+        refs.push_back(c);
+      }
+    } else {
+      for (const rt_node_t& n : n2) {
+        std::array<int32_t, 4> c = {RT_EMPTY_REF, RT_EMPTY_REF, RT_EMPTY_REF, RT_EMPTY_REF};
+        std::memcpy(c.data(), &n.v[12], 8);
+        refs.push_back(c);
+      }
     }
   }
+  r->vis_refs = refs;
+  r->vis_pids = leaf_pids;
   std::vector<rt_vnode_t> vnodes;
   if (rt::BuildVisNodes(refs, leaf_pids, vis, &vnodes) != 0) return fail("malformed BVH");
   std::vector<rt_vtri_t> vtris;
@@ -461,6 +541,7 @@ static int configure_vis(rt_renderer* r, const rt_render_params_t* p,
   std::vector<rt_vtri_t> vl, vg;
   for (int32_t g : s->layers) vl.push_back(rt::MakeVisTri(prims[g], vis[g], g));
   for (int32_t g : s->geometry) vg.push_back(rt::MakeVisTri(prims[g], vis[g], g));
+  a.num_vnodes = (uint32_t)vnodes.size();
   if (upload(r->dev, vnodes.data(), vnodes.size() * sizeof(rt_vnode_t), &r->vnodes, &a.vnodes_addr) ||
       upload(r->dev, vtris.data(), vtris.size() * sizeof(rt_vtri_t), &r->vtris, &a.vtris_addr) ||
       upload(r->dev, vl.data(), vl.size() * sizeof(rt_vtri_t), &r->vlayers, &a.vlayers_addr) ||
@@ -486,6 +567,8 @@ int rt_renderer_configure(rt_renderer_h r, const rt_render_params_t* p) {
   const rt_scene* s = r->sc;
   r->params = *p;
   r->params.shard_count = shards;
+  for (vx_buffer_h* b : {&r->gather_recv, &r->gather_image})  // sized per configuration
+    if (*b) { vx_mem_free(*b); *b = nullptr; }
   rt_kernel_arg_t& a = r->arg;
   // per-resolution shading records (rast_prim_t + drawcall id)
   std::vector<rt_prim_t> prims(s->scene.prims.size());
@@ -502,6 +585,17 @@ int rt_renderer_configure(rt_renderer_h r, const rt_render_params_t* p) {
   }
   if (upload(r->dev, prims.data(), prims.size() * sizeof(rt_prim_t), &r->prims, &a.prims_addr))
     return -1;
+  // primary visibility per primitive (app/vis.h): covered-pixel rectangle + depth bound
+  std::vector<rt::VisPrim> vis;
+  if (!raster) {
+    vis.resize(prims.size());
+    for (size_t g = 0; g < prims.size(); ++g) {
+      rt_bbox_t bb{0, 0};
+      const bool ok = setup_ok[g] &&
+                      rt::PrimBBox(s->scene.prims[g], p->width, p->height, &bb) == rt::kSetupOk;
+      vis[g] = rt::ComputeVisPrim(prims[g], ok, bb, p->width, p->height);
+    }
+  }
   if (raster) {
     // per-resolution screen boxes; degenerate / culled primitives get an
     // empty box and are never binned (gfxutil.cpp:195-232)
@@ -539,34 +633,31 @@ int rt_renderer_configure(rt_renderer_h r, const rt_render_params_t* p) {
   a.shard_index = p->shard_index;
   a.shard_count = shards;
   // Work order of this shard's 32x32 tiles: heaviest first (longest
-  // processing time first) -- weight = geometry primitives whose screen box
-  // touches the tile -- so the long model waves start with the frame rather
-  // than trailing it.  Output is order independent.  RT_TILE_ORDER=0: identity.
+  // processing time first) -- weight = geometry primitives whose
+  // covered-pixel rectangle reaches the tile -- so the long model waves start
+  // with the frame rather than trailing it.  Output is order independent.
+  // RT_TILE_ORDER=0: identity.
   a.order_addr = 0;
   a.split_tiles = 0;
   if (!raster && r->local_tiles > 0 && !(std::getenv("RT_TILE_ORDER") &&
                                          std::atoi(std::getenv("RT_TILE_ORDER")) == 0)) {
     std::vector<uint32_t> weight(tiles, 0);
-    for (size_t d = 0; d < s->scene.drawcalls.size(); ++d) {
-      const rt::DrawCall& dc = s->scene.drawcalls[d];
-      if (!dc.states.depth_test) continue;  // screen layers cost the same everywhere
-      for (uint32_t i = 0; i < dc.prim_count; ++i) {
-        rt_bbox_t bb;
-        if (rt::PrimBBox(s->scene.prims[dc.prim_offset + i], p->width, p->height, &bb) != rt::kSetupOk)
-          continue;
-        const uint32_t tx0 = (bb.x & 0xffffu) >> RT_TILE_LOG, tx1 = ((bb.x >> 16) + 31u) >> RT_TILE_LOG;
-        const uint32_t ty0 = (bb.y & 0xffffu) >> RT_TILE_LOG, ty1 = ((bb.y >> 16) + 31u) >> RT_TILE_LOG;
-        for (uint32_t ty = ty0; ty < ty1 && ty < a.tiles_y; ++ty)
-          for (uint32_t tx = tx0; tx < tx1 && tx < a.tiles_x; ++tx) ++weight[ty * a.tiles_x + tx];
-      }
+    for (int32_t g : s->geometry) {
+      const rt::VisPrim& v = vis[g];
+      if (!v.any) continue;
+      const uint32_t tx0 = (v.rx & 0xffffu) >> RT_TILE_LOG, tx1 = (v.rx >> 16) >> RT_TILE_LOG;
+      const uint32_t ty0 = (v.ry & 0xffffu) >> RT_TILE_LOG, ty1 = (v.ry >> 16) >> RT_TILE_LOG;
+      for (uint32_t ty = ty0; ty <= ty1 && ty < a.tiles_y; ++ty)
+        for (uint32_t tx = tx0; tx <= tx1 && tx < a.tiles_x; ++tx) ++weight[ty * a.tiles_x + tx];
     }
     std::vector<uint32_t> ord(r->local_tiles);
     for (uint32_t i = 0; i < r->local_tiles; ++i) ord[i] = i;
     auto w = [&](uint32_t lt) { return weight[p->shard_index + lt * shards]; };
     std::stable_sort(ord.begin(), ord.end(), [&](uint32_t x, uint32_t y) { return w(x) > w(y); });
     if (upload(r->dev, ord.data(), ord.size() * 4, &r->order, &a.order_addr)) return -1;
-    // path tracing: tiles geometry touches (first in `ord`) run 32 pixels
-    // per wave (task_map in rt_trace.h): 0.34 -> 0.30 ms at 1024^2; for
+    // path tracing: tiles geometry covers (first in `ord`; oracle/rt.c
+    // tile_split restates the rule) run 32 pixels per wave (task_map in
+    // rt_trace.h): 0.34 -> 0.30 ms at 1024^2; for
     // primary + shadow rays it measured slower (0.071 -> 0.086 ms: the
     // shadow rays then also trace in half-empty waves), so off there.
     // RT_SPLIT_TILES=n overrides the count, 0 disables.
@@ -577,6 +668,12 @@ int rt_renderer_configure(rt_renderer_h r, const rt_render_params_t* p) {
       heavy = std::min<uint32_t>((uint32_t)std::atoi(e), r->local_tiles);
     a.split_tiles = heavy;
     a.num_tasks += heavy * RT_TILE_PIXELS;
+    // timing probe only (the frame is incomplete): render just the first n
+    // tiles of the work order, e.g. the geometry tiles without the background
+    if (const char* e = std::getenv("RT_TILE_LIMIT")) {
+      const uint32_t n = std::min<uint32_t>((uint32_t)std::atoi(e), r->local_tiles);
+      a.num_tasks = std::min(a.num_tasks, n * RT_TILE_PIXELS + std::min(n, heavy) * RT_TILE_PIXELS);
+    }
   }
   bool use_bvh4 = !(p->flags & RT_RENDER_BVH2) && (!r->gpu_bvh || r->gpu_bvh4);
   if (const char* e = std::getenv("RT_BVH_WIDTH")) use_bvh4 = use_bvh4 && std::atoi(e) != 2;
@@ -587,7 +684,7 @@ int rt_renderer_configure(rt_renderer_h r, const rt_render_params_t* p) {
             (s->tie_high ? RT_FLAG_TIE_HIGH : 0u) | (compact ? RT_FLAG_COMPACT : 0u) |
             (use_bvh4 ? RT_FLAG_BVH4 : 0u) |
             (use_bvh4 && !r->gpu_bvh && !s->bvh.nodes4h.empty() ? RT_FLAG_BVH4H : 0u);
-  if (!raster && configure_vis(r, p, prims, setup_ok, use_bvh4) != 0) return -1;
+  if (!raster && configure_vis(r, prims, vis, use_bvh4) != 0) return -1;
   a.bounces = p->bounces;
   a.seed = p->seed;
   a.clear_color = p->clear_color;
@@ -692,6 +789,50 @@ int rt_launch_rows(rt_renderer_h r, uint32_t* rows, uint64_t max_rows, uint64_t*
   return r->mpm_rows(r->dev, rows, max_rows, nrows) == 0 ? 0 : fail("vx_hip_mpm_rows failed");
 }
 
+int rt_render_gather(rt_renderer_h r, struct rt_shard_comm* comm, uint32_t* image) {
+  if (!r || !comm || !r->configured || !r->mem_ptr || !r->stream) return fail("renderer not configured");
+  // librt_shard.so (HIP + RCCL) is loaded on first use: librtapp itself
+  // does not depend on RCCL
+  static void* lib = nullptr;
+  using gather_fn = int (*)(rt_shard_comm_h, const uint32_t*, uint32_t*, uint64_t, uint32_t*, uint32_t,
+                            uint32_t, void*);
+  using info_fn = int (*)(rt_shard_comm_h, uint32_t*, uint32_t*);
+  using sync_fn = int (*)(void*);
+  if (!lib) lib = dlopen((lib_dir() + "/librt_shard.so").c_str(), RTLD_NOW | RTLD_GLOBAL);
+  if (!lib) return fail(std::string("cannot load librt_shard.so: ") + dlerror());
+  auto gather = (gather_fn)dlsym(lib, "rt_frame_gather");
+  auto info = (info_fn)dlsym(lib, "rt_shard_comm_info");
+  auto sync = (sync_fn)dlsym(lib, "rt_shard_stream_sync");
+  if (!gather || !info || !sync) return fail("librt_shard.so lacks the gather API");
+  uint32_t rank = 0, world = 0;
+  if (info(comm, &rank, &world) != 0) return fail("rt_shard_comm_info failed");
+  const rt_render_params_t& p = r->params;
+  if (rank != p.shard_index || world != p.shard_count || !(r->arg.flags & RT_FLAG_COMPACT))
+    return fail("renderer shard (index/count, compact output) does not match the communicator");
+  const uint64_t ntiles = (uint64_t)r->arg.tiles_x * r->arg.tiles_y;
+  const uint64_t slots = ((ntiles + world - 1) / world) * RT_TILE_PIXELS;  // rank 0's buffer
+  void *local = nullptr, *recv = nullptr, *img = nullptr, *stream = nullptr;
+  if (r->mem_ptr(r->cbuf, &local) != 0 || r->stream(r->dev, &stream) != 0)
+    return fail("driver extension failed");
+  if (rank == 0) {
+    uint64_t a1 = 0, a2 = 0;
+    const uint64_t rbytes = world * slots * 4, ibytes = (uint64_t)p.width * p.height * 4;
+    if (!r->gather_recv && upload(r->dev, nullptr, rbytes, &r->gather_recv, &a1)) return -1;
+    if (!r->gather_image && upload(r->dev, nullptr, ibytes, &r->gather_image, &a2)) return -1;
+    if (r->mem_ptr(r->gather_recv, &recv) != 0 || r->mem_ptr(r->gather_image, &img) != 0)
+      return fail("driver extension failed");
+  }
+  // every render this host started is on the stream ahead of the exchange
+  if (gather(comm, (const uint32_t*)local, (uint32_t*)recv, slots, (uint32_t*)img, p.width, p.height,
+             stream) != 0)
+    return fail("rt_frame_gather failed");
+  if (sync(stream) != 0) return fail("stream synchronize failed");
+  if (rank == 0 && image &&
+      vx_copy_from_dev(image, r->gather_image, 0, (uint64_t)p.width * p.height * 4) != 0)
+    return fail("vx_copy_from_dev failed");
+  return 0;
+}
+
 int rt_framebuffer_device(rt_renderer_h r, void** ptr, uint64_t* bytes) {
   if (!r || !ptr || !r->configured || !r->mem_ptr) return fail("not available");
   if (bytes) *bytes = r->cbuf_bytes;
@@ -715,15 +856,6 @@ int rt_device_caps(rt_renderer_h r, uint64_t caps[8]) {
 // ---- GPU BVH build (kernels/bvh_build.hip) --------
 
 namespace {
-
-int load_image(rt_renderer* r, const std::string& name, vx_buffer_h* out) {
-  std::string path = r->kdir + "/" + name;
-  if (FILE* f = std::fopen(path.c_str(), "rb")) std::fclose(f);
-  else path = lib_dir() + "/" + name;
-  if (*out) vx_mem_free(*out);
-  *out = nullptr;
-  return vx_upload_kernel_file(r->dev, path.c_str(), out) == 0 ? 0 : fail("cannot upload kernel " + path);
-}
 
 struct DevBuf {  // scratch buffer freed at scope exit
   vx_buffer_h h = nullptr;
@@ -836,14 +968,8 @@ int rt_renderer_build_bvh(rt_renderer_h r, rt_bvh_build_stats_t* st) {
   // images (else the BVH2, whose depth bound was just checked)
   const bool use4 = stack4 <= RT_STACK_DEEP;
   // traversal images with a stack deep enough for this tree
-  if (std::max(depth, use4 ? stack4 : 0u) > RT_STACK_SHALLOW && !r->deep) {
-    if (load_image(r, "rt_kernel_deep.vxbin", &r->krnl[0][0]) ||
-        load_image(r, "rt_kernel_deep_stats.vxbin", &r->krnl[0][1]) ||
-        load_image(r, "pt_kernel_deep.vxbin", &r->krnl[1][0]) ||
-        load_image(r, "pt_kernel_deep_stats.vxbin", &r->krnl[1][1]))
-      return -1;
-    r->deep = true;
-  }
+  if (std::max(depth, use4 ? stack4 : 0u) > RT_STACK_SHALLOW && !r->deep && load_deep_images(r) != 0)
+    return -1;
   if (r->nodes) vx_mem_free(r->nodes);
   if (r->tris) vx_mem_free(r->tris);
   if (r->nodes4) vx_mem_free(r->nodes4);

@@ -3,6 +3,9 @@
 
 #include <algorithm>
 #include <cstring>
+#include <string>
+
+#include "bvh.h"
 
 namespace rt {
 namespace {
@@ -200,6 +203,47 @@ int BuildVisNodes(const std::vector<std::array<int32_t, 4>>& refs,
   NodeBuilder b{refs, leaf_pids, by_pid, out};
   b.of(0, 0);
   return b.err;
+}
+
+int BuildScreenTree(const std::vector<VisPrim>& by_pid, const std::vector<int32_t>& geometry,
+                    float depth_scale, std::vector<std::array<int32_t, 4>>* refs,
+                    std::vector<int32_t>* leaf_pids, uint32_t* stack4) {
+  refs->clear();
+  leaf_pids->clear();
+  *stack4 = 0;
+  std::vector<BuildTri> bt;
+  for (int32_t g : geometry) {
+    const VisPrim& v = by_pid[g];
+    if (!v.any) continue;
+    // a degenerate "triangle" spanning the rectangle [x0, x1 + 1) x [y0, y1 + 1)
+    // at depth z: its box is the rectangle, so the builder's SAH is on area
+    const float z = depth_scale * (float)v.zmin * (1.0f / 16777216.0f);
+    BuildTri t;
+    t.v[0][0] = (float)(v.rx & 0xffffu); t.v[0][1] = (float)(v.ry & 0xffffu); t.v[0][2] = z;
+    t.v[1][0] = (float)((v.rx >> 16) + 1); t.v[1][1] = (float)((v.ry >> 16) + 1); t.v[1][2] = z;
+    t.v[2][0] = t.v[0][0]; t.v[2][1] = t.v[0][1]; t.v[2][2] = z;
+    t.pid = g;
+    bt.push_back(t);
+  }
+  if (bt.empty()) return 0;
+  BvhParams bp;
+  bp.f16_boxes = false;
+  bp.all_axes = true;
+  Bvh b;
+  std::string err;
+  if (BuildBvhWith(bt, bp, &b, &err) != 0) return -1;
+  for (const rt_node4_t& n : b.nodes4) {
+    std::array<int32_t, 4> c;
+    std::memcpy(c.data(), &n.v[24], 16);
+    refs->push_back(c);
+  }
+  for (const rt_tri_t& t : b.tris) {
+    int32_t pid;
+    std::memcpy(&pid, &t.v[3], 4);
+    leaf_pids->push_back(pid);
+  }
+  *stack4 = b.stack4;
+  return 0;
 }
 
 }  // namespace rt

@@ -47,4 +47,13 @@ int BuildVisNodes(const std::vector<std::array<int32_t, 4>>& refs,
                   const std::vector<int32_t>& leaf_pids, const std::vector<VisPrim>& by_pid,
                   std::vector<rt_vnode_t>* out);
 
+// The primary rays' own tree, per resolution: a 4-wide BVH over the
+// geometry primitives' covered-pixel rectangles (binned SAH on screen area,
+// optionally with the depth bound as a third axis scaled by depth_scale
+// pixels per 2^24; primitives covering no pixel are left out), in the
+// layout BuildVisNodes takes.  stack4 = its worst-case traversal stack.
+int BuildScreenTree(const std::vector<VisPrim>& by_pid, const std::vector<int32_t>& geometry,
+                    float depth_scale, std::vector<std::array<int32_t, 4>>* refs,
+                    std::vector<int32_t>* leaf_pids, uint32_t* stack4);
+
 }  // namespace rt

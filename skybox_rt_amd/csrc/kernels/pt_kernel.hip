@@ -182,7 +182,7 @@ __device__ __forceinline__ void primary(const vx_task_t& task, bool valid, const
   const bool tie_high = (S.flags & RT_FLAG_TIE_HIGH) != 0;
   int32_t* stack = &L.stack[threadIdx.x >> 6][0][lane_id()];
   // primary visibility: the raster's winner at this pixel (trace_primary)
-  const int32_t hit = in ? trace_primary(S, x, y, tie_high, stack, cnt) : -1;
+  const int32_t hit = trace_primary(S, x, y, in, tie_high, stack, cnt);
   cnt.hits += hit >= 0;
   const int32_t spid = resolve_layers(S, x, y, in && hit < 0, hit, cnt);
   const uint32_t color = shade_wave(S, spid, x, y, S.clear_color, cnt);
@@ -298,6 +298,9 @@ __device__ __forceinline__ bool path_step(const Scene& S, int32_t* stack, PathSt
 #ifndef PT_PAIR
 #define PT_PAIR 1
 #endif
+// (Shadow rays as wave packets, occluded_packet, then the bounce rays per
+// lane: 0.31 ms vs 0.22 ms, measured -- a path's later shadow rays are
+// incoherent and the two traversals no longer overlap.)
 __device__ __forceinline__ bool path_step_pair(const Scene& S, int32_t* stack, PathState& st,
                                                uint32_t v, bool act, Counters& cnt) {
   const bool tie_high = (S.flags & RT_FLAG_TIE_HIGH) != 0;
@@ -334,8 +337,8 @@ __device__ __forceinline__ bool path_step_pair(const Scene& S, int32_t* stack, P
     r.d[k] = owner ? b.d[k] : hd;
   }
   ray_setup(r);
-  const bool tracing = owner ? alive : h_act;
   float tr = 0.0f;
+  const bool tracing = owner ? alive : h_act;
   const int32_t res = tracing ? trace_mixed(S, r, 0.0f, owner ? INFINITY : 1.0f,
                                             owner ? st.pid : h_pid, tie_high, &tr, stack, cnt,
                                             !owner)
@@ -457,7 +460,7 @@ __device__ __forceinline__ void lane_path(const vx_task_t& task, const Scene& S,
   cnt.primary += in;
   const bool tie_high = (S.flags & RT_FLAG_TIE_HIGH) != 0;
   // primary visibility: the raster's winner at this pixel (trace_primary)
-  const int32_t hit = in ? trace_primary(S, x, y, tie_high, stack, cnt) : -1;
+  const int32_t hit = trace_primary(S, x, y, in, tie_high, stack, cnt);
   cnt.hits += hit >= 0;
   const int32_t spid = resolve_layers(S, x, y, in && hit < 0, hit, cnt);
   const uint32_t color = shade_wave(S, spid, x, y, S.clear_color, cnt);

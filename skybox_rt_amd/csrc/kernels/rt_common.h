@@ -169,7 +169,7 @@ typedef struct {
   uint32_t num_geom;       // geometry triangles (flat mode)
   uint32_t num_drawcalls;  // raster mode
   uint32_t raster_tile_log;  // raster mode: tile side 2^log (4: 16x16 px, 1 px/thread; 5: 32x32, 2x2/thread)
-  uint32_t pad4;
+  uint32_t num_vnodes;     // rt_vnode_t records (0: no primitive covers a pixel)
   uint64_t zbuf_addr;      // raster mode: depth/stencil buffer, W*H u32
   uint64_t oms_addr;       // raster mode: rt_omstate_t per drawcall
   uint64_t bbox_addr;      // raster mode: rt_bbox_t per pid

@@ -37,6 +37,11 @@
 #ifndef RT_SHADOW_QUEUE
 #define RT_SHADOW_QUEUE (!RT_FLAT)
 #endif
+// 1: the queued shadow rays of a wave walk the binary16 BVH4 as one packet
+// (occluded_packet in rt_trace.h; same verdicts and per-ray counts)
+#ifndef RT_SHADOW_PACKET
+#define RT_SHADOW_PACKET 1
+#endif
 
 namespace {
 
@@ -89,8 +94,11 @@ __device__ __forceinline__ void kernel_body(const vx_task_t& task, const Scene& 
   const bool in = x < S.width && y < S.height;  // edge tiles overhang the image
   cnt.primary += in;
   const bool tie_high = (S.flags & RT_FLAG_TIE_HIGH) != 0;
+#ifdef RT_STAMPS
+  if (lane_id() == 0) __vx_mpm_lds[3] = (uint32_t)__builtin_amdgcn_s_memrealtime();
+#endif
   // primary visibility: the raster's winner at this pixel
-  const int32_t hit = in ? trace_primary(S, x, y, tie_high, &w.stack[0][lane_id()], cnt) : -1;
+  const int32_t hit = trace_primary(S, x, y, in, tie_high, &w.stack[0][lane_id()], cnt);
 #ifdef RT_STAMPS
   if (lane_id() == 0) __vx_mpm_lds[14] = (uint32_t)__builtin_amdgcn_s_memrealtime();
 #endif
@@ -99,6 +107,9 @@ __device__ __forceinline__ void kernel_body(const vx_task_t& task, const Scene& 
   const int32_t spid = hit;
 #else
   const int32_t spid = resolve_layers(S, x, y, in && hit < 0, hit, cnt);
+#endif
+#ifdef RT_STAMPS
+  if (lane_id() == 0) __vx_mpm_lds[4] = (uint32_t)__builtin_amdgcn_s_memrealtime();
 #endif
 #ifdef RT_ABLATE_SHADE  // timing-only ablation (scripts/ab_variants.py)
   uint32_t color = 0xff000000u | (uint32_t)spid;
@@ -132,6 +143,9 @@ __device__ __forceinline__ void kernel_body(const vx_task_t& task, const Scene& 
     __builtin_amdgcn_wave_barrier();
   }
   if (in && !shadow) store_pixel(S, t, x, y, color);
+#ifdef RT_STAMPS
+  if (lane_id() == 0) __vx_mpm_lds[5] = (uint32_t)__builtin_amdgcn_s_memrealtime();
+#endif
 #else
   Ray s;
   shadow_ray(S, r, th, s);
@@ -152,6 +166,8 @@ __device__ __forceinline__ void shadow_drain(bool final, const Scene& S, WaveLds
                                              Counters& cnt) {
 #ifdef RT_STAMPS
   if (final && lane_id() == 0) __vx_mpm_lds[15] = (uint32_t)__builtin_amdgcn_s_memrealtime();
+  if (!final && w.q_count >= 64 && lane_id() == 0)
+    __vx_mpm_lds[6] = (uint32_t)__builtin_amdgcn_s_memrealtime();
 #endif
   if (!(S.flags & RT_FLAG_SHADOWS)) return;
   const uint32_t lane = lane_id();
@@ -170,7 +186,14 @@ __device__ __forceinline__ void shadow_drain(bool final, const Scene& S, WaveLds
     shadow_ray(S, p, w.q_t[slot], s);
     cnt.shadow += active;
     uint32_t color = w.q_color[slot];
+#if RT_SHADOW_PACKET
+    const bool occ = (S.flags & RT_FLAG_BVH4H)
+                         ? occluded_packet(S, s, active, w.q_pid[slot], 1.0f, &w.stack[0][lane], cnt)
+                         : occluded(S, s, w.q_pid[slot], tie_high, active, w, cnt);
+    if (occ) {
+#else
     if (occluded(S, s, w.q_pid[slot], tie_high, active, w, cnt)) {
+#endif
       ++cnt.occluded;
       color = shadowed(color);
     }
@@ -342,10 +365,12 @@ VX_MAIN(rt_kernel_arg_t, arg, RT_BLOCK_THREADS) {
     __vx_mpm_lds[13] = (uint32_t)__builtin_amdgcn_s_memrealtime();
   }
 #endif
+#ifndef RT_STAMPS  // the stamp image keeps slots 3-9 for phase stamps / iteration counts
   flush(RT_STAT_PRIMARY, cnt.primary);
   flush(RT_STAT_SHADOW, cnt.shadow);
   flush(RT_STAT_HITS, cnt.hits);
   flush(RT_STAT_OCCLUDED, cnt.occluded);
+#endif
 #ifdef RT_INSTRUMENT
   flush(RT_STAT_NODE_VISITS, cnt.visits);
   flush(RT_STAT_TRI_TESTS, cnt.tests);

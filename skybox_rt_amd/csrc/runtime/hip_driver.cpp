@@ -461,8 +461,11 @@ class vx_device {
     hipDeviceptr_t gp = nullptr;
     size_t gsz = 0;
     if (hipModuleGetGlobal(&gp, &gsz, m.module, "__vx_grid_per_cu") == hipSuccess && gsz == 4) {
+      // read on the driver's stream (frames of another image may be queued
+      // on it; the null stream would not be ordered with them)
       uint32_t v = 0;
-      HIP_CHECK(hipMemcpyDtoH(&v, gp, 4));
+      HIP_CHECK(hipMemcpyAsync(&v, gp, 4, hipMemcpyDeviceToHost, stream_));
+      HIP_CHECK(hipStreamSynchronize(stream_));
       if (v > 0) per_cu = (int)v;
     } else {
       (void)hipGetLastError();

@@ -90,6 +90,7 @@ def lib():
             "rt_renderer_build_bvh": [vp, C.POINTER(BvhBuildStats)],
             "rt_renderer_export_bvh": [vp, vp, vp, C.POINTER(u32), C.POINTER(u32)],
             "rt_renderer_export_bvh4": [vp, vp, C.POINTER(u32)],
+            "rt_renderer_export_vis_tree": [vp, vp, C.POINTER(u32), vp, C.POINTER(u32)],
             "rt_renderer_create": [vp, C.c_char_p, C.POINTER(vp)],
             "rt_renderer_free": [vp],
             "rt_renderer_configure": [vp, C.POINTER(RenderParams)],
@@ -105,9 +106,12 @@ def lib():
             "rt_launch_rows": [vp, vp, u64, C.POINTER(u64)],
             "rt_scene_setup_prims": [vp, u32, u32, vp, u64],
             "rt_scene_setup_vis": [vp, u32, u32, vp, u64],
+            "rt_scene_vis_tree": [vp, u32, u32, C.c_float, vp, C.POINTER(u32), vp, C.POINTER(u32),
+                                  C.POINTER(u32)],
             "rt_framebuffer_device": [vp, C.POINTER(vp), C.POINTER(u64)],
             "rt_device_stream": [vp, C.POINTER(vp)],
             "rt_device_caps": [vp, C.POINTER(u64)],
+            "rt_render_gather": [vp, vp, vp],
         }
         for name, argtypes in sig.items():
             fn = getattr(h, name)
@@ -176,6 +180,19 @@ class Scene:
         _check(lib().rt_scene_setup_vis(self._h, width, height, out.ctypes.data, n),
                "rt_scene_setup_vis")
         return out[:n]
+
+    def vis_tree(self, width: int, height: int, depth_scale: float = 0.0):
+        """The primary rays' screen-space BVH4 at width x height: (refs
+        int32[N, 4], leaf_pids int32[M], worst-case stack)."""
+        nn, nl, st = C.c_uint32(), C.c_uint32(), C.c_uint32()
+        _check(lib().rt_scene_vis_tree(self._h, width, height, depth_scale, None, C.byref(nn), None,
+                                       C.byref(nl), C.byref(st)), "rt_scene_vis_tree")
+        refs = np.zeros((max(nn.value, 1), 4), np.int32)
+        pids = np.zeros(max(nl.value, 1), np.int32)
+        _check(lib().rt_scene_vis_tree(self._h, width, height, depth_scale, refs.ctypes.data,
+                                       C.byref(nn), pids.ctypes.data, C.byref(nl), C.byref(st)),
+               "rt_scene_vis_tree")
+        return refs[:nn.value], pids[:nl.value], st.value
 
     def close(self) -> None:
         if self._h:
@@ -253,6 +270,19 @@ class Renderer:
                "rt_renderer_export_bvh4")
         return nodes4[:n.value]
 
+    def export_vis_tree(self):
+        """The primary rays' tree of the current configuration: (refs
+        int32[N, 4] child references, leaf_pids int32[M])."""
+        nn, nl = C.c_uint32(), C.c_uint32()
+        _check(lib().rt_renderer_export_vis_tree(self._h, None, C.byref(nn), None, C.byref(nl)),
+               "rt_renderer_export_vis_tree")
+        refs = np.zeros((max(nn.value, 1), 4), np.int32)
+        pids = np.zeros(max(nl.value, 1), np.int32)
+        _check(lib().rt_renderer_export_vis_tree(self._h, refs.ctypes.data, C.byref(nn),
+                                                 pids.ctypes.data, C.byref(nl)),
+               "rt_renderer_export_vis_tree")
+        return refs[:nn.value], pids[:nl.value]
+
     def export_bvh(self):
         """The renderer's current BVH: (nodes float32[N, 16], tris float32[M, 12])."""
         nn, nt = C.c_uint32(), C.c_uint32()
@@ -310,6 +340,17 @@ class Renderer:
         out = np.zeros((max(n.value, 1), 16), np.uint32)
         _check(lib().rt_launch_rows(self._h, out.ctypes.data, n.value, C.byref(n)), "rt_launch_rows")
         return out[:n.value]
+
+    def gather(self, comm) -> np.ndarray:
+        """rt_render_gather over a shard.ShardComm: this rank's compact tiles
+        to rank 0 (RCCL), assembled there; rank 0 gets the uint32 [H, W]
+        frame, other ranks None."""
+        p = self.params
+        rank, _ = comm.info()
+        out = np.zeros((p.height, p.width), np.uint32) if rank == 0 else None
+        _check(lib().rt_render_gather(self._h, comm.handle, out.ctypes.data if out is not None else None),
+               "rt_render_gather")
+        return out
 
     def depthbuffer(self) -> np.ndarray:
         """RT_RENDER_RASTER: uint32 [H, W] depth/stencil words (stencil << 24 | depth)."""

@@ -102,7 +102,7 @@ class FrameGather:
             if self.cuda:
                 # the HIP assembly kernel (include/rt_shard.h); no torch fallback
                 from . import _lib
-                self._asm = _lib.load("libframe_assemble.so").rt_frame_assemble
+                self._asm = _lib.load("librt_shard.so").rt_frame_assemble
                 self._asm.restype = ctypes.c_int
                 self._asm.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32,
                                       ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint64,
@@ -179,3 +179,48 @@ class FrameGather:
             self.asm_done[slot] = None
 
     finish = reclaim
+
+
+class ShardComm:
+    """ctypes binding of include/rt_shard.h's RCCL communicator
+    (librt_shard.so): the C-ABI frame exchange a C host uses without torch
+    (rtapp -G rank,ranks).  Renderer.gather(comm) runs rt_render_gather."""
+    ID_BYTES = 128
+
+    @staticmethod
+    def _lib():
+        from . import _lib
+        h = _lib.load("librt_shard.so")
+        h.rt_shard_unique_id.argtypes = [ctypes.c_char_p]
+        h.rt_shard_comm_init.argtypes = [ctypes.POINTER(ctypes.c_void_p), ctypes.c_char_p,
+                                         ctypes.c_uint32, ctypes.c_uint32, ctypes.c_int]
+        h.rt_shard_comm_free.argtypes = [ctypes.c_void_p]
+        h.rt_shard_comm_info.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_uint32),
+                                         ctypes.POINTER(ctypes.c_uint32)]
+        h.rt_shard_local_words.argtypes = [ctypes.c_uint32] * 4
+        h.rt_shard_local_words.restype = ctypes.c_uint64
+        return h
+
+    @classmethod
+    def unique_id(cls) -> bytes:
+        buf = ctypes.create_string_buffer(cls.ID_BYTES)
+        if cls._lib().rt_shard_unique_id(buf) != 0:
+            raise RuntimeError("rt_shard_unique_id failed")
+        return buf.raw
+
+    def __init__(self, uid: bytes, rank: int, world: int, device: int = 0):
+        self.handle = ctypes.c_void_p()
+        if self._lib().rt_shard_comm_init(ctypes.byref(self.handle), uid, rank, world, device) != 0:
+            raise RuntimeError("rt_shard_comm_init failed")
+
+    def info(self):
+        r, w = ctypes.c_uint32(), ctypes.c_uint32()
+        if self._lib().rt_shard_comm_info(self.handle, ctypes.byref(r), ctypes.byref(w)) != 0:
+            raise RuntimeError("rt_shard_comm_info failed")
+        return r.value, w.value
+
+    def close(self):
+        if self.handle:
+            self._lib().rt_shard_comm_free(self.handle)
+            self.handle = None
+

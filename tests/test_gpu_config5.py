@@ -60,7 +60,7 @@ def test_config5_eight_shards_assemble_to_the_full_frame(tek):
         recv[i * per:i * per + part.size] = torch.from_numpy(part.view(np.int32)).cuda()
         rays += r.stats()["primary_rays"]
     assert rays == W * H
-    f = _lib.load("libframe_assemble.so").rt_frame_assemble
+    f = _lib.load("librt_shard.so").rt_frame_assemble
     f.restype = ctypes.c_int
     f.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint32,
                   ctypes.c_uint32, ctypes.c_uint64, ctypes.c_void_p]
@@ -97,3 +97,32 @@ def test_config5_frame_gather_world_size_1(tek):
         assert np.array_equal(image.cpu().numpy().view(np.uint32).reshape(H, W), full)
     finally:
         dist.destroy_process_group()
+
+
+def test_c_abi_gather_world_size_1(tek):
+    """The C-ABI exchange (include/rt_shard.h over RCCL, no torch):
+    rt_render_gather at world size 1 == the full frame, at 4096^2."""
+    from skybox_rt_amd.shard import ShardComm
+    _, r, full = tek
+    comm = ShardComm(ShardComm.unique_id(), 0, 1, 0)
+    try:
+        assert comm.info() == (0, 1)
+        r.configure(W, H, shadows=True, shard_index=0, shard_count=1, compact=True)
+        r.render()
+        assert np.array_equal(r.gather(comm), full)
+    finally:
+        comm.close()
+
+
+def test_rtapp_rank_mode_world_size_1(tmp_path):
+    """rtapp -G 0,1: the C host's multi-GPU mode (render its shard, RCCL
+    gather, assemble on rank 0) reproduces the reference's golden image."""
+    import subprocess
+    from conftest import GOLDEN
+    exe = os.path.join(_lib.LIB_DIR, "rtapp")
+    out = subprocess.run([exe, "-t", scene_path("tekkaman"), "-w", "128", "-h", "128", "-G", "0,1",
+                          "-I", str(tmp_path / "id"), "-o", str(tmp_path / "o.png"), "-r",
+                          f"{GOLDEN}/draw3d/tekkaman_ref_128.png"],
+                         capture_output=True, text=True, timeout=300)
+    assert out.returncode == 0, out.stdout + out.stderr
+    assert "communicator: 1 ranks" in out.stdout and "PASSED!" in out.stdout

@@ -14,7 +14,7 @@ pytestmark = pytest.mark.gpu
 
 
 def _assemble_fn():
-    f = _lib.load("libframe_assemble.so").rt_frame_assemble
+    f = _lib.load("librt_shard.so").rt_frame_assemble
     f.restype = ctypes.c_int
     f.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint32,
                   ctypes.c_uint32, ctypes.c_uint64, ctypes.c_void_p]

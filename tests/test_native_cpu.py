@@ -36,7 +36,7 @@ def native_built():
 
 @pytest.mark.parametrize("header,lib", [("vortex.h", "libvortex.so"), ("vx_rt.h", "librtapp.so"),
                                         ("vx_tex.h", "librtapp.so"),
-                                        ("rt_shard.h", "libframe_assemble.so")])
+                                        ("rt_shard.h", "librt_shard.so")])
 def test_c_abi_exports_every_declared_symbol(header, lib):
     h = C.CDLL(os.path.join(_lib.LIB_DIR, lib))
     names = _declared(header)
