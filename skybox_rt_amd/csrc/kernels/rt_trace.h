@@ -100,7 +100,25 @@ __device__ __forceinline__ bool stage_scene(Scene& S, uint32_t num_tris, float4*
   return true;
 }
 
-__device__ __forceinline__ Scene load_scene(const rt_kernel_arg_t* a) {
+// The argument block is read through the scalar cache (constant address
+// space, wave-uniform address): the scene's fields then live in SGPRs, and
+// the traversal loops form node / triangle addresses in scalar registers
+// instead of VGPR + readfirstlane.
+#ifndef RT_SCALAR_ARGS
+#define RT_SCALAR_ARGS 1
+#endif
+__device__ __forceinline__ Scene load_scene(const rt_kernel_arg_t* ga) {
+#if RT_SCALAR_ARGS
+  const uint64_t p = (uint64_t)ga;
+  // (readfirstlane returns int: through uint32_t, or the low word sign-extends)
+  const uint32_t lo = (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)p);
+  const uint32_t hi = (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(p >> 32));
+  const uint64_t u = ((uint64_t)hi << 32) | (uint64_t)lo;
+  const __attribute__((address_space(4))) rt_kernel_arg_t* a =
+      (const __attribute__((address_space(4))) rt_kernel_arg_t*)u;
+#else
+  const rt_kernel_arg_t* a = ga;
+#endif
   Scene s;
   s.A = vx_arena::get();
   s.nodes = (uint32_t)a->nodes_addr;
@@ -543,10 +561,21 @@ __device__ __forceinline__ int32_t trace_impl(const Scene& S, const Ray& r, floa
 // (0.0565 -> 0.0514 ms): the heavy tiles' shadow rays are coherent.  Every
 // active lane calls it (any EXEC mask: the stack words are stored by all
 // active lanes and read back with readfirstlane).
+#ifndef RT_PACKET_BRANCHLESS
+#define RT_PACKET_BRANCHLESS 1
+#endif
+// wave priority while walking a packet (0: unchanged): the packet walks are
+// the heavy tiles' latency chains
+#ifndef RT_PACKET_PRIO
+#define RT_PACKET_PRIO 0
+#endif
 __device__ __forceinline__ bool occluded_packet(const Scene& S, const Ray& r, bool act, int32_t skip,
                                                 float tmax, int32_t* stack, Counters& cnt) {
   bool done = !act, occ = false;
   if (S.num_nodes4 == 0 || __ballot(!done) == 0) return false;
+#if RT_PACKET_PRIO
+  __builtin_amdgcn_s_setprio(RT_PACKET_PRIO);
+#endif
   int32_t* ws = stack - lane_id();
   int sp = 0;
   int32_t ref = 0;
@@ -577,8 +606,14 @@ __device__ __forceinline__ bool occluded_packet(const Scene& S, const Ray& r, bo
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         float tn = 0.0f;
+#if RT_PACKET_BRANCHLESS
+        // every lane evaluates the slab (no exec-mask branch per child)
+        const bool hs = slab(lx[i], hx[i], ly[i], hy[i], lz[i], hz[i], r, 0.0f, tmax, &tn);
+        h[i] = hs & live & (c[i] != RT_EMPTY_REF);
+#else
         h[i] = live && c[i] != RT_EMPTY_REF &&
                slab(lx[i], hx[i], ly[i], hy[i], lz[i], hz[i], r, 0.0f, tmax, &tn);
+#endif
         need |= __ballot(h[i]) ? 1u << i : 0u;
       }
       if (need) {
@@ -624,6 +659,9 @@ __device__ __forceinline__ bool occluded_packet(const Scene& S, const Ray& r, bo
     __builtin_amdgcn_wave_barrier();
     ref = __builtin_amdgcn_readfirstlane(ws[64 * sp]);
   }
+#if RT_PACKET_PRIO
+  __builtin_amdgcn_s_setprio(0);
+#endif
   return occ;
 }
 
@@ -922,6 +960,9 @@ __device__ __forceinline__ int32_t trace_primary_packet(const Scene& S, uint32_t
                                                         Counters& cnt) {
   if (S.num_vnodes == 0) return -1;
   if (!act) px = 0xffffffffu;  // in no rectangle
+#if RT_PACKET_PRIO
+  __builtin_amdgcn_s_setprio(RT_PACKET_PRIO);
+#endif
   int32_t* ws = stack - lane_id();  // the wave's column base (lane 0's column)
   const bool l0 = lane_id() == 0;
   uint32_t bz = VX_OM_DEPTH_MASK;
@@ -992,6 +1033,9 @@ __device__ __forceinline__ int32_t trace_primary_packet(const Scene& S, uint32_t
     __builtin_amdgcn_wave_barrier();
     ref = __builtin_amdgcn_readfirstlane(ws[64 * sp]);
   }
+#if RT_PACKET_PRIO
+  __builtin_amdgcn_s_setprio(0);
+#endif
   return bpid;
 }
 
