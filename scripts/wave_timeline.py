@@ -81,6 +81,19 @@ def main():
             "to_primary": ph(12, 3), "primary": ph(3, 14), "layers": ph(14, 4), "shade": ph(4, 11),
             "plane_queue": ph(11, 5), "to_final_drain": ph(5, 15), "final_drain": ph(15, 13),
             "nonfinal_drains": int((rows[slow, 6] > 0).sum())}
+    if path:  # pt stamp image: 10 wave cycles (s_memtime), 4 paired-traversal cycles,
+        # 5 vertex steps, 6 post-traversal (bounce-hit shading) cycles
+        cyc = rows[:, 10].astype(np.float64)
+        ghz = cyc[slow] / (dur[slow] * 10.0)
+        out["slowest50"].update({
+            "clock_ghz": float(ghz.mean()),
+            "vertex_steps": float(rows[slow, 5].mean()),
+            "traversal_frac": float((rows[slow, 4] / np.maximum(cyc[slow], 1)).mean()),
+            "shade_frac": float((rows[slow, 6] / np.maximum(cyc[slow], 1)).mean()),
+            "node_loop_frac": float((rows[slow, 11] / np.maximum(cyc[slow], 1)).mean()),
+            "node_iters": float(rows[slow, 9].mean()),
+            "cycles_per_iter": float((cyc[slow] / np.maximum(it[slow].sum(1), 1)).mean())})
+        out["all"]["clock_ghz"] = float((cyc / np.maximum(dur * 10.0, 1)).mean())
     out["all"].update({"primary_node_iters": float(it[:, 0].mean()), "primary_leaf_iters": float(it[:, 1].mean()),
                        "secondary_iters": float(it[:, 2].mean())})
     # background (short) waves: where their time goes -- start -> primary

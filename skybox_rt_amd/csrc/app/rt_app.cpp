@@ -639,6 +639,7 @@ int rt_renderer_configure(rt_renderer_h r, const rt_render_params_t* p) {
   // RT_TILE_ORDER=0: identity.
   a.order_addr = 0;
   a.split_tiles = 0;
+  a.split_log = 5;
   if (!raster && r->local_tiles > 0 && !(std::getenv("RT_TILE_ORDER") &&
                                          std::atoi(std::getenv("RT_TILE_ORDER")) == 0)) {
     std::vector<uint32_t> weight(tiles, 0);
@@ -667,12 +668,15 @@ int rt_renderer_configure(rt_renderer_h r, const rt_render_params_t* p) {
     if (const char* e = std::getenv("RT_SPLIT_TILES"))
       heavy = std::min<uint32_t>((uint32_t)std::atoi(e), r->local_tiles);
     a.split_tiles = heavy;
-    a.num_tasks += heavy * RT_TILE_PIXELS;
+    a.split_log = 5;  // 32 pixels per wave
+    if (const char* e = std::getenv("RT_SPLIT_LOG")) a.split_log = std::min(6u, std::max(3u, (uint32_t)std::atoi(e)));
+    const uint32_t extra = RT_TILE_PIXELS * ((64u >> a.split_log) - 1u);  // per split tile
+    a.num_tasks += heavy * extra;
     // timing probe only (the frame is incomplete): render just the first n
     // tiles of the work order, e.g. the geometry tiles without the background
     if (const char* e = std::getenv("RT_TILE_LIMIT")) {
       const uint32_t n = std::min<uint32_t>((uint32_t)std::atoi(e), r->local_tiles);
-      a.num_tasks = std::min(a.num_tasks, n * RT_TILE_PIXELS + std::min(n, heavy) * RT_TILE_PIXELS);
+      a.num_tasks = std::min(a.num_tasks, n * RT_TILE_PIXELS + std::min(n, heavy) * extra);
     }
   }
   bool use_bvh4 = !(p->flags & RT_RENDER_BVH2) && (!r->gpu_bvh || r->gpu_bvh4);

@@ -41,12 +41,14 @@
 #ifndef RT_LDS_SCENE
 #define RT_LDS_SCENE 0
 #endif
+#ifndef PT_BLOCK
 #if PT_MODE == 0
 #define PT_BLOCK 256
 #elif RT_LDS_SCENE
 #define PT_BLOCK 1024  // one workgroup per CU shares the staged BVH
 #else
 #define PT_BLOCK 64
+#endif
 #endif
 #define PT_SKY 0.25f     // radiance of an escaped bounce ray (oracle ORC_PT_SKY)
 #define PT_TRIES 8u      // disk rejection-sampling attempts (ORC_PT_TRIES)
@@ -298,9 +300,27 @@ __device__ __forceinline__ bool path_step(const Scene& S, int32_t* stack, PathSt
 #ifndef PT_PAIR
 #define PT_PAIR 1
 #endif
+#ifndef PT_PRIO
+#define PT_PRIO 0
+#endif
+// >0: stage up to this many binary16 BVH4 nodes in LDS per workgroup
+#ifndef PT_LDS_NODES
+#define PT_LDS_NODES 0
+#endif
 // (Shadow rays as wave packets, occluded_packet, then the bounce rays per
 // lane: 0.31 ms vs 0.22 ms, measured -- a path's later shadow rays are
 // incoherent and the two traversals no longer overlap.)
+#ifdef RT_STAMPS  // diagnostic image: per-wave cycle accumulators (scripts/wave_timeline.py)
+#define PT_CYC() __builtin_amdgcn_s_memtime()
+#define PT_ACC(slot, v)                                                            \
+  do {                                                                             \
+    if (lane_id() == (uint32_t)__builtin_ctzll(__ballot(1)))                      \
+      ((volatile uint32_t*)__vx_mpm_lds)[slot] += (uint32_t)(v);                  \
+  } while (0)
+#else
+#define PT_CYC() 0ull
+#define PT_ACC(slot, v) do {} while (0)
+#endif
 __device__ __forceinline__ bool path_step_pair(const Scene& S, int32_t* stack, PathState& st,
                                                uint32_t v, bool act, Counters& cnt) {
   const bool tie_high = (S.flags & RT_FLAG_TIE_HIGH) != 0;
@@ -339,11 +359,15 @@ __device__ __forceinline__ bool path_step_pair(const Scene& S, int32_t* stack, P
   ray_setup(r);
   float tr = 0.0f;
   const bool tracing = owner ? alive : h_act;
+  const uint64_t c0 = PT_CYC();
   const int32_t res = tracing ? trace_mixed(S, r, 0.0f, owner ? INFINITY : 1.0f,
                                             owner ? st.pid : h_pid, tie_high, &tr, stack, cnt,
                                             !owner)
                               : -1;
   const bool h_occ = __shfl((int)(res >= 0), src) != 0;  // the helper's verdict (all lanes)
+  const uint64_t c1 = PT_CYC();
+  PT_ACC(4, c1 - c0);  // cycles in the paired traversal
+  PT_ACC(5, 1);        // vertex steps
   const bool occ = act && h_occ;
   cnt.shadow += act;
   cnt.occluded += occ;
@@ -390,6 +414,7 @@ __device__ __forceinline__ bool path_step_pair(const Scene& S, int32_t* stack, P
     st.pid = np;
     st.t = nt;
   }
+  PT_ACC(6, PT_CYC() - c1);  // cycles after the traversal (shading the bounce hit)
   return alive;
 }
 
@@ -457,6 +482,9 @@ __device__ __forceinline__ void lane_path(const vx_task_t& task, const Scene& S,
   // paired vertices (path_step_pair) when the whole wave is here and its
   // upper 32 lanes hold no pixel -- wave-uniform
   const bool pair = PT_PAIR && __ballot(1) == ~0ull && (__ballot(in) >> 32) == 0;
+#if PT_PRIO
+  if (pair) __builtin_amdgcn_s_setprio(PT_PRIO);  // geometry-tile waves: the long paths
+#endif
   cnt.primary += in;
   const bool tie_high = (S.flags & RT_FLAG_TIE_HIGH) != 0;
   // primary visibility: the raster's winner at this pixel (trace_primary)
@@ -521,6 +549,7 @@ VX_MAIN(rt_kernel_arg_t, arg, PT_BLOCK) {
   __shared__ PtLds s_pt;
 #ifdef RT_STAMPS  // diagnostic image: per-wave start/end timestamps (scripts/wave_timeline.py)
   const uint64_t t_stamp0 = __builtin_amdgcn_s_memrealtime();
+  const uint64_t t_cyc0 = __builtin_amdgcn_s_memtime();
 #endif
   Counters cnt;
   Scene S = load_scene(arg);
@@ -537,22 +566,35 @@ VX_MAIN(rt_kernel_arg_t, arg, PT_BLOCK) {
   stage_scene(S, S.num_geom, s_scene);
   __syncthreads();
 #endif
+#if PT_LDS_NODES
+  // the binary16 BVH4 nodes (64 B each) staged per workgroup when they fit
+  __shared__ float4 s_nodes4h[4 * PT_LDS_NODES];
+  if (S.num_nodes4 <= PT_LDS_NODES && (S.flags & RT_FLAG_BVH4H)) {
+    for (uint32_t i = threadIdx.x; i < 4u * S.num_nodes4; i += blockDim.x)
+      s_nodes4h[i] = S.A.ld_f4(S.nodes4 + 128u * S.num_nodes4 + 16u * i);
+    S.lnodes4h = s_nodes4h;
+  }
+  __syncthreads();
+#endif
   int32_t* stack = &s_pt.stack[threadIdx.x >> 6][0][lane_id()];
   const int rc = vx_spawn_tasks(
       arg->num_tasks,
       [&](const vx_task_t& task, const Scene* s) { lane_path(task, *s, stack, cnt); }, &S);
 #endif
+#ifndef RT_STAMPS  // the stamp image keeps slots 4-6 for its cycle accumulators
   flush(RT_STAT_PRIMARY, cnt.primary);
   flush(RT_STAT_SHADOW, cnt.shadow);
   flush(RT_STAT_HITS, cnt.hits);
   flush(RT_STAT_OCCLUDED, cnt.occluded);
   flush(RT_STAT_BOUNCE, cnt.bounce);
+#endif
 #ifdef RT_STAMPS
   if (threadIdx.x == 0) {
     __vx_mpm_lds[12] = (uint32_t)t_stamp0;
     __vx_mpm_lds[13] = (uint32_t)__builtin_amdgcn_s_memrealtime();
     __vx_mpm_lds[14] = (uint32_t)t_stamp0;
     __vx_mpm_lds[15] = 0;
+    __vx_mpm_lds[10] = (uint32_t)(__builtin_amdgcn_s_memtime() - t_cyc0);  // wave cycles
   }
 #endif
 #ifdef RT_INSTRUMENT

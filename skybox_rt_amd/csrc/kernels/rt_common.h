@@ -181,4 +181,6 @@ typedef struct {
   uint64_t vnodes_addr;    // rt_vnode_t per node of the traversed tree (primary visibility)
   uint64_t vtris_addr;     // rt_vtri_t per leaf triangle record (+3 padding records)
   uint64_t vgeom_addr;     // rt_vtri_t per geometry primitive, ascending pid (flat mode)
+  uint32_t split_log;      // split tiles run 2^split_log pixels per wave (5: 32, an 8x4 half block)
+  uint32_t pad5;
 } rt_kernel_arg_t;

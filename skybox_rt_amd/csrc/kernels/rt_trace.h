@@ -72,11 +72,12 @@ struct Scene {
   uint32_t nodes, nodes4, tris, prims, dcs, cbuf, ptris, geom, order;
   uint32_t vnodes, vtris, vlayers, vgeom, num_vnodes;  // primary visibility (rt_common.h)
   uint32_t num_nodes, num_nodes4, num_layer, num_geom, flags, width, height;
-  uint32_t shard_index, shard_count, tiles_x, clear_color, bounces, seed, split_tiles;
+  uint32_t shard_index, shard_count, tiles_x, clear_color, bounces, seed, split_tiles, split_log;
   float sx, sy, light[3];
   // the BVH staged in LDS by the workgroup (RT_LDS_SCENE images), or null
   const float4* lnodes = nullptr;
   const float4* ltris = nullptr;
+  const float4* lnodes4h = nullptr;  // the binary16 BVH4 nodes staged in LDS (RT_LDS_NODES4H images)
 };
 
 // LDS budget (float4 slots) for a workgroup-staged BVH: nodes + leaf
@@ -139,6 +140,7 @@ __device__ __forceinline__ Scene load_scene(const rt_kernel_arg_t* ga) {
   s.bounces = a->bounces;
   s.seed = a->seed;
   s.split_tiles = a->split_tiles;
+  s.split_log = a->split_log;
   s.num_nodes = a->num_nodes;
   s.num_nodes4 = a->num_nodes4;
   s.num_layer = a->num_layer_tris;
@@ -172,6 +174,20 @@ __device__ __forceinline__ uint32_t lane_id() {
   } while (0)
 #else
 #define RT_WAVE_ITER(slot) do {} while (0)
+#endif
+// RT_TRACE_CYCLES (path-tracer stamp image only): wave cycles spent in the
+// secondary traversal's node loop (slot 11) and leaf rounds (slot 3)
+#ifdef RT_TRACE_CYCLES
+#define RT_CYC_BEGIN() const uint64_t rt_cyc0 = __builtin_amdgcn_s_memtime()
+#define RT_CYC_END(slot)                                                                  \
+  do {                                                                                    \
+    const uint32_t d = (uint32_t)(__builtin_amdgcn_s_memtime() - rt_cyc0);               \
+    if (lane_id() == (uint32_t)__builtin_ctzll(__ballot(1)))                             \
+      ((volatile uint32_t*)__vx_mpm_lds)[slot] += d;                                      \
+  } while (0)
+#else
+#define RT_CYC_BEGIN() do {} while (0)
+#define RT_CYC_END(slot) do {} while (0)
 #endif
 
 struct Ray {
@@ -277,6 +293,10 @@ __device__ __forceinline__ NodeStep node_step(const float4& n0, const float4& n1
 #ifndef RT_TOS
 #define RT_TOS 0
 #endif
+// 1: BVH4 node steps without a branch per child or per push
+#ifndef RT_NODE_BRANCHLESS
+#define RT_NODE_BRANCHLESS 1
+#endif
 struct LaneStack {
   int32_t* mem;
   int sp = 0;
@@ -296,6 +316,18 @@ struct LaneStack {
 #else
     if (sp < RT_MAX_STACK) mem[64 * sp++] = x;
 #endif
+  }
+  // push the hit children c[1..n-1] of a sorted node step (c[n-1] first, so
+  // c[1] ends on top) -- push()'s order and overflow rule, as predicated
+  // stores instead of a branch per push
+  __device__ __forceinline__ void push_sorted(const int32_t c[4], int n) {
+#pragma unroll
+    for (int j = 1; j < 4; ++j) {
+      const int pos = sp + n - 1 - j;
+      if (j < n && pos < RT_MAX_STACK) mem[64 * pos] = c[j];
+    }
+    const int top = sp + n - 1;
+    sp = top < RT_MAX_STACK ? top : RT_MAX_STACK;
   }
   __device__ __forceinline__ bool pop(int32_t& x) {
 #if RT_TOS
@@ -333,8 +365,14 @@ __device__ __forceinline__ int32_t node4_step(const Scene& S, uint32_t ref, cons
     // and each folds into its slab FMA (v_fma_mix_f32: f16 operand, f32 math)
     // -- the layout is a template parameter so no phi separates them
     const uint32_t no = S.nodes4 + 128u * S.num_nodes4 + 64u * ref;
-    const float4 px = ld(no), py = ld(no + 16), pz = ld(no + 32);
-    cf = ld(no + 48);
+    float4 px, py, pz;
+    if (!SCALAR && S.lnodes4h) {
+      const float4* n = S.lnodes4h + 4u * ref;
+      px = n[0]; py = n[1]; pz = n[2]; cf = n[3];
+    } else {
+      px = ld(no); py = ld(no + 16); pz = ld(no + 32);
+      cf = ld(no + 48);
+    }
     auto h2 = [](float w, float& a, float& b) {
       const uint32_t u = __float_as_uint(w);
       a = (float)__builtin_bit_cast(_Float16, (uint16_t)(u & 0xffffu));
@@ -359,8 +397,14 @@ __device__ __forceinline__ int32_t node4_step(const Scene& S, uint32_t ref, cons
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
     float tn = 0.0f;
+#if RT_NODE_BRANCHLESS
+    // every lane evaluates all four slabs (no exec-mask branch per child)
+    const bool hs = slab(alx[i], ahx[i], aly[i], ahy[i], alz[i], ahz[i], r, tmin, lim, &tn);
+    const bool h = hs & (c[i] != RT_EMPTY_REF);
+#else
     const bool h = c[i] != RT_EMPTY_REF &&
                    slab(alx[i], ahx[i], aly[i], ahy[i], alz[i], ahz[i], r, tmin, lim, &tn);
+#endif
     k[i] = h ? (any ? (float)i : fminf(tn, 3.402823466e38f)) : __builtin_inff();
     n += h ? 1 : 0;
   }
@@ -379,9 +423,13 @@ __device__ __forceinline__ int32_t node4_step(const Scene& S, uint32_t ref, cons
   cx(1, 3);
   cx(1, 2);
   if (n == 0) return RT_EMPTY_REF;
+#if RT_NODE_BRANCHLESS && !RT_TOS
+  st.push_sorted(c, n);
+#else
   if (n >= 4) st.push(c[3]);
   if (n >= 3) st.push(c[2]);
   if (n >= 2) st.push(c[1]);
+#endif
   return c[0];
 }
 
@@ -450,11 +498,15 @@ __device__ __forceinline__ int32_t trace_impl(const Scene& S, const Ray& r, floa
     // once no lane is still in the node loop -- the per-lane sequence of node
     // visits and leaf tests (hence every counter and result) is unchanged
     bool dry = false;
-    while (ref >= 0) {
-      RT_WAVE_ITER(9);
-      const int32_t nx = node_next(false, 0);
-      if (nx != RT_EMPTY_REF) { ref = nx; continue; }
-      if (!lst.pop(ref)) { dry = true; break; }
+    {
+      RT_CYC_BEGIN();
+      while (ref >= 0) {
+        RT_WAVE_ITER(9);
+        const int32_t nx = node_next(false, 0);
+        if (nx != RT_EMPTY_REF) { ref = nx; continue; }
+        if (!lst.pop(ref)) { dry = true; break; }
+      }
+      RT_CYC_END(11);
     }
     if (dry) break;
     const bool uni = false;
@@ -1113,13 +1165,16 @@ struct TaskPix {
 };
 __device__ __forceinline__ TaskPix task_map(const Scene& S, uint32_t t) {
   TaskPix m;
-  const uint32_t hs = S.split_tiles << 11;
+  const uint32_t pl = S.split_log;  // split tiles: 2^pl pixels per wave (pl <= 6)
+  const uint32_t cl = 16u - pl;      // log2 tasks per split tile (1024 >> pl chunks of 64)
+  const uint32_t hs = S.split_tiles << cl;
   uint32_t pos;
   if (t < hs) {
-    const uint32_t c = (t >> 6) & 31u, ln = t & 63u;
-    pos = t >> 11;
-    m.idx = ((c >> 1) << 6) + (ln & 31u) + ((c & 1u) << 5);
-    m.live = ln < 32u;
+    const uint32_t sub = 6u - pl;    // log2 chunks per 8x8 block
+    const uint32_t c = (t >> 6) & ((1024u >> pl) - 1u), ln = t & 63u;
+    pos = t >> cl;
+    m.idx = ((c >> sub) << 6) + ((c & ((1u << sub) - 1u)) << pl) + (ln & ((1u << pl) - 1u));
+    m.live = ln < (1u << pl);
   } else {
     pos = S.split_tiles + ((t - hs) >> 10);
     m.idx = t & 1023u;
