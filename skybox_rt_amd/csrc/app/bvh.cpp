@@ -170,9 +170,45 @@ class Builder {
     return (int32_t)node;
   }
 
+  // full-sweep SAH (bins == 0): every axis, every split position of the
+  // triangles sorted by centroid (ties by index); the range is left sorted
+  // along the chosen axis
+  uint32_t split_sweep(uint32_t b, uint32_t e) {
+    const uint32_t n = e - b;
+    std::vector<uint32_t> ord(n);
+    std::vector<double> left(n);
+    double best = INFINITY;
+    int best_axis = -1;
+    uint32_t best_nl = 0;
+    for (int axis = 0; axis < 3; ++axis) {
+      std::copy(idx_.begin() + b, idx_.begin() + e, ord.begin());
+      std::sort(ord.begin(), ord.end(), [&](uint32_t x, uint32_t y) {
+        return cen_[x][axis] < cen_[y][axis] || (cen_[x][axis] == cen_[y][axis] && x < y);
+      });
+      Box acc;
+      for (uint32_t i = 0; i < n; ++i) {
+        acc.grow(box_[ord[i]]);
+        left[i] = acc.area();
+      }
+      Box r;
+      for (uint32_t i = n; i-- > 1;) {  // right = ord[i..n), left = ord[0..i)
+        r.grow(box_[ord[i]]);
+        const double c = (double)i * left[i - 1] + (double)(n - i) * r.area();
+        if (c < best) { best = c; best_axis = axis; best_nl = i; }
+      }
+    }
+    if (best_axis < 0) return b + n / 2;
+    const int axis = best_axis;
+    std::sort(idx_.begin() + b, idx_.begin() + e, [&](uint32_t x, uint32_t y) {
+      return cen_[x][axis] < cen_[y][axis] || (cen_[x][axis] == cen_[y][axis] && x < y);
+    });
+    return b + best_nl;
+  }
+
   // binned SAH over centroids (the widest centroid axis, or every axis with
   // all_axes); stable partition
   uint32_t split(uint32_t b, uint32_t e) {
+    if (bins_ == 0) return split_sweep(b, e);
     float cl[3] = {INFINITY, INFINITY, INFINITY}, ch[3] = {-INFINITY, -INFINITY, -INFINITY};
     for (uint32_t i = b; i < e; ++i)
       for (int k = 0; k < 3; ++k) {
@@ -352,8 +388,8 @@ int BuildBvhWith(const std::vector<BuildTri>& tris, const BvhParams& bp, Bvh* ou
     if (error) *error = "too many triangles for the 27-bit leaf index";
     return -1;
   }
-  if (bp.leaf_size < 1 || bp.leaf_size > 4 || bp.bins < 2 || bp.bins > kBvhMaxBins) {
-    if (error) *error = "bad BVH build parameters (leaf 1..4, bins 2..64)";
+  if (bp.leaf_size < 1 || bp.leaf_size > 4 || bp.bins == 1 || bp.bins > kBvhMaxBins) {
+    if (error) *error = "bad BVH build parameters (leaf 1..4, bins 0 (sweep) or 2..64)";
     return -1;
   }
   Builder b(tris, out, bp);

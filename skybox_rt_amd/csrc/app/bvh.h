@@ -41,7 +41,7 @@ constexpr uint32_t kBvhMaxBins = 64;
 struct BvhParams {
   uint32_t leaf_size = kBvhLeafSize;   // max triangles per leaf (1..4)
   uint32_t bins = kBvhBins;            // SAH bins per axis (2..64)
-  bool all_axes = false;               // SAH over x, y and w, not only the widest axis
+  bool all_axes = true;                // SAH over x, y and w, not only the widest axis
   bool f16_boxes = true;               // BVH4 boxes rounded outward to binary16 values
 };
 
