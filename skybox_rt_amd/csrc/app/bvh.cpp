@@ -58,6 +58,8 @@ float HalfValue(uint16_t h) {
 }
 
 
+double g_wside = 1.0;
+
 struct Box {
   float lo[3] = {INFINITY, INFINITY, INFINITY};
   float hi[3] = {-INFINITY, -INFINITY, -INFINITY};
@@ -73,10 +75,11 @@ struct Box {
       hi[k] = std::max(hi[k], b.hi[k]);
     }
   }
+  // SAH area; g_wside weighs the faces that extend along w (probe knob)
   double area() const {
     if (lo[0] > hi[0]) return 0.0;
     const double dx = (double)hi[0] - lo[0], dy = (double)hi[1] - lo[1], dz = (double)hi[2] - lo[2];
-    return 2.0 * (dx * dy + dy * dz + dz * dx);
+    return 2.0 * (dx * dy + g_wside * (dy * dz + dz * dx));
   }
 };
 
@@ -378,6 +381,7 @@ int BuildBvh(const std::vector<BuildTri>& tris, Bvh* out, std::string* error) {
   if (const char* v = std::getenv("RT_BVH_BINS")) bp.bins = (uint32_t)std::atoi(v);
   if (const char* v = std::getenv("RT_BVH_AXES")) bp.all_axes = std::atoi(v) == 3;
   if (const char* v = std::getenv("RT_BVH_F16")) bp.f16_boxes = std::atoi(v) != 0;
+  g_wside = std::getenv("RT_BVH_WSIDE") ? std::atof(std::getenv("RT_BVH_WSIDE")) : 1.0;
   return BuildBvhWith(tris, bp, out, error);
 }
 

@@ -41,6 +41,19 @@ std::string self_dir() {
   return "";
 }
 
+// In-process class counters (libvx_perf.so, runtime/vx_perf.cpp): loaded
+// only when VORTEX_PROFILING is set, before the driver starts the HIP
+// runtime -- the counter tool must be registered first.
+void* g_perf_handle = nullptr;
+bool g_perf_ok = false;
+void load_perf(int mode) {
+  if (g_perf_handle != nullptr || mode == 0) return;
+  g_perf_handle = dlopen((self_dir() + "libvx_perf.so").c_str(), RTLD_NOW | RTLD_LOCAL);
+  if (g_perf_handle == nullptr) return;
+  auto init = (int (*)(int))dlsym(g_perf_handle, "vx_perf_init");
+  g_perf_ok = init != nullptr && init(mode) == 0;
+}
+
 int load_driver() {
   if (g_drv_handle) return 0;
   const char* name = std::getenv("VORTEX_DRIVER");
@@ -97,6 +110,7 @@ bool read_file(const char* filename, std::vector<char>* out) {
 
 VX_API int vx_dev_open(vx_device_h* hdevice) {
   if (hdevice == nullptr) return -1;
+  load_perf(get_profiling_mode());
   if (load_driver() != 0) return 1;
   vx_device_h h = nullptr;
   VX_CHECK_ERR(g_callbacks.dev_open(&h), { return err; });
@@ -249,12 +263,18 @@ VX_API int vx_dump_perf(vx_device_h h, FILE* stream) {
   VX_CHECK_ERR(vx_mpm_query(h, VX_CSR_MINSTRET, 0, &tasks), { return err; });
   std::fprintf(stream, "PERF: device_ns=%llu, tasks=%llu\n", (unsigned long long)ns,
                (unsigned long long)tasks);
-  // the reference's per-class hardware counters (VORTEX_PROFILING 1-5,
-  // utils.cpp:262-800) are the GPU's PMC counters on MI355X: collected
-  // out of process by rocprofv3, printed in this format by scripts/vx_perf.py
-  if (const int cls = get_profiling_mode())
-    std::fprintf(stream, "PERF: class %d counters: python scripts/vx_perf.py --class %d -- <app>\n",
-                 cls, cls);
+  // the reference's per-class counters (VORTEX_PROFILING 1-5,
+  // utils.cpp:262-800) are the GPU's hardware counters on MI355X, collected
+  // in process by libvx_perf.so when it could register before the HIP
+  // runtime started; otherwise scripts/vx_perf.py collects them out of process
+  if (const int cls = get_profiling_mode()) {
+    auto dump = g_perf_ok ? (int (*)(FILE*, int))dlsym(g_perf_handle, "vx_perf_dump") : nullptr;
+    if (dump == nullptr || dump(stream, cls) != 0)
+      std::fprintf(stream,
+                   "PERF: class %d counters unavailable in process (HIP runtime started before "
+                   "vx_dev_open?): python scripts/vx_perf.py --class %d -- <app>\n",
+                   cls, cls);
+  }
   return 0;
 }
 

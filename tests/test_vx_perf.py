@@ -39,3 +39,47 @@ def test_report_layout():
     out = io.StringIO()
     vx_perf.report(2, v, out)
     assert "l2cache read misses=10 (hit ratio=90%)" in out.getvalue()
+
+
+def test_in_process_library_exports():
+    """libvx_perf.so (runtime/vx_perf.cpp): the in-process collector the stub
+    loads under VORTEX_PROFILING exports its three entry points."""
+    import ctypes
+    lib = os.path.join(ROOT, "skybox_rt_amd", "lib", "libvx_perf.so")
+    h = ctypes.CDLL(lib)
+    for sym in ("vx_perf_init", "vx_perf_dump", "vx_perf_dispatches"):
+        assert hasattr(h, sym)
+    h.vx_perf_dispatches.restype = ctypes.c_uint64
+    assert h.vx_perf_dispatches() == 0       # nothing collected, no GPU touched
+    assert h.vx_perf_init(9) == -1           # no such class
+
+
+def _perf_lines(out):
+    return [ln for ln in out.splitlines() if ln.startswith("PERF: ")]
+
+
+import pytest  # noqa: E402
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("cls", [1, 2])
+def test_vx_dump_perf_in_process(tmp_path, cls):
+    """VORTEX_PROFILING=<class> + VX_DUMP_PERF: the C host prints the class's
+    hardware counters in process at vx_dev_close (stub.cpp / vx_perf.cpp),
+    the reference's utils.cpp:159-805 report, over all its launches."""
+    import subprocess
+    exe = os.path.join(ROOT, "skybox_rt_amd", "lib", "rtapp")
+    env = dict(os.environ, VORTEX_PROFILING=str(cls), VX_DUMP_PERF="1")
+    scene = os.path.join(ROOT, "tests", "golden", "scenes", "tekkaman.cgltrace")
+    out = subprocess.run([exe, "-t", scene, "-w", "256", "-h", "256", "-S", "-n", "6",
+                          "-o", str(tmp_path / "o.png")], env=env, capture_output=True, text=True,
+                         timeout=120)
+    assert out.returncode == 0, out.stdout + out.stderr
+    lines = _perf_lines(out.stdout)
+    instrs = [ln for ln in lines if ln.startswith("PERF: instrs=")]
+    assert instrs, lines
+    n = int(instrs[0].split("instrs=")[1].split(",")[0])
+    assert n > 0
+    assert any(f"class {cls}: " in ln and "vx_main launches profiled" in ln for ln in lines), lines
+    key = "scheduler idle=" if cls == 1 else "dcache reads="
+    assert any(key in ln for ln in lines), lines
