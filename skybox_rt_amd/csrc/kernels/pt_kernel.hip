@@ -531,12 +531,13 @@ __device__ __forceinline__ void flush(int slot, uint32_t v) { vx_mpm_add(RT_MPM_
 
 }  // namespace
 
-// grid for the driver: 96 64-thread blocks per CU (24576), one 64-task chunk
-// per wave for the split heavy tiles too; 0.2262 -> 0.2222 ms at 1024^2
-// (profiles/r01_v13_grid_sweep.jsonl; 64/CU is best for rt_kernel)
+// grid for the driver: 128 64-thread blocks per CU (32768), one 64-task chunk
+// per wave for the split heavy tiles too (r01: 96/CU, 0.2262 -> 0.2222 ms;
+// r02 after the scalar argument block: 128/CU 0.1765 vs 96/CU 0.1801 ms,
+// profiles/r02/ab_pt_grid.json; 64/CU is best for rt_kernel)
 #if PT_BLOCK == 64
 #ifndef PT_GRID_PER_CU
-#define PT_GRID_PER_CU 96
+#define PT_GRID_PER_CU 128
 #endif
 __device__ __attribute__((used)) uint32_t __vx_grid_per_cu = PT_GRID_PER_CU;
 #endif

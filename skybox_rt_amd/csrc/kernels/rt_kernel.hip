@@ -217,6 +217,9 @@ __device__ __forceinline__ void shadow_drain(bool final, const Scene& S, WaveLds
 // shades and stores; shadow rays split the same way, the first occluder in
 // list order found by a min over the waves' first hits (which is also
 // brute_trace's test count).
+#ifndef RT_FLAT_UNROLL
+#define RT_FLAT_UNROLL 8
+#endif
 struct FlatLds {
   uint32_t z[kWaves][64];
   int32_t pid[kWaves][64];
@@ -241,7 +244,26 @@ __device__ __forceinline__ void flat_chunk(const vx_task_t& task, bool valid, co
   const uint4* lds = flat_list(S);
   uint32_t bz = VX_OM_DEPTH_MASK;
   int32_t bp = -1;
-  for (uint32_t k = k0; k < k1; ++k) {
+  uint32_t k = k0;
+#if RT_FLAT_UNROLL > 1
+  // RT_FLAT_UNROLL rectangle words in flight at once (their LDS reads
+  // overlap), then the candidates among them in ascending order
+  for (; k + RT_FLAT_UNROLL <= k1; k += RT_FLAT_UNROLL) {
+    uint4 C[RT_FLAT_UNROLL];
+#pragma unroll
+    for (int j = 0; j < RT_FLAT_UNROLL; ++j) C[j] = flat_rec(S, lds, k + j, 2);
+    uint32_t cand = 0u;
+#pragma unroll
+    for (int j = 0; j < RT_FLAT_UNROLL; ++j)
+      cand |= __ballot(rect_in(C[j].y, px) && rect_in(C[j].z, y)) ? 1u << j : 0u;
+#pragma unroll
+    for (int j = 0; j < RT_FLAT_UNROLL; ++j)
+      if ((cand >> j) & 1u)  // wave-uniform
+        vis_test(flat_rec(S, lds, k + j, 0), flat_rec(S, lds, k + j, 1), C[j],
+                 flat_rec(S, lds, k + j, 3), px, y, tie_high, bz, bp);
+  }
+#endif
+  for (; k < k1; ++k) {
     const uint4 C = flat_rec(S, lds, k, 2);
     if (__ballot(rect_in(C.y, px) && rect_in(C.z, y)) == 0) continue;  // wave-uniform skip
     vis_test(flat_rec(S, lds, k, 0), flat_rec(S, lds, k, 1), C, flat_rec(S, lds, k, 3), px, y,
