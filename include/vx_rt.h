@@ -142,6 +142,9 @@ int rt_renderer_build_bvh(rt_renderer_h r, rt_bvh_build_stats_t* stats);
  * BVH4 node i at the BVH2 index of every even-depth internal node, zeros
  * elsewhere).  NO REFERENCE. */
 int rt_renderer_export_bvh4(rt_renderer_h r, float* nodes4, uint32_t* num_nodes4);
+/* the same nodes as 64-B rt_node4h_t records (binary16 planes, the layout the
+ * kernels read), num_nodes4 * 64 bytes */
+int rt_renderer_export_bvh4h(rt_renderer_h r, void* nodes4h, uint32_t* num_nodes4);
 /* the renderer's current BVH (float[num_nodes][16], float[num_tris][12]) */
 int rt_renderer_export_bvh(rt_renderer_h r, float* nodes, float* tris, uint32_t* num_nodes,
                            uint32_t* num_tris);

@@ -284,3 +284,56 @@ int orc_lbvh_collapse4(const float* nodes, uint32_t nn, float* nodes4, uint32_t*
   *stack_out = worst;
   return 0;
 }
+
+/* ---- binary16 box planes (the kernels' rt_node4h_t) ----------------------
+ * Restates app/bvh.cpp HalfRound / HalfBits and the device phase
+ * BVHB_HALF (kernels/bvh_build.hip): every plane of a BVH4 node rounded
+ * outward to a binary16-representable value (lower planes down, upper planes
+ * up; exact scaling by the binade's quantum, floor / ceil, saturating
+ * outward past +-65504), the fp32 node rewritten with the rounded values and
+ * the 64-B half record emitted (24 halves in rt_node4_t plane order, then
+ * the 4 child refs). */
+static float half_round(float x, int dir) {
+  if (isnan(x) || isinf(x) || x == 0.0f) return x;
+  const float kmax = 65504.0f;
+  if (x > kmax) return dir < 0 ? kmax : INFINITY;
+  if (x < -kmax) return dir < 0 ? -INFINITY : -kmax;
+  int e;
+  frexpf(fabsf(x), &e);
+  int q = e - 1 > -14 ? e - 1 : -14;
+  q -= 10;
+  const float m = ldexpf(x, -q);
+  const float r = dir < 0 ? floorf(m) : ceilf(m);
+  const float v = ldexpf(r, q);
+  return v > kmax ? INFINITY : (v < -kmax ? -INFINITY : v);
+}
+
+static uint16_t half_bits(float v) {
+  uint32_t u;
+  memcpy(&u, &v, 4);
+  const uint16_t sign = (uint16_t)((u >> 16) & 0x8000u);
+  const float a = fabsf(v);
+  if (a == 0.0f) return sign;
+  if (isinf(a)) return (uint16_t)(sign | 0x7c00u);
+  int e;
+  const float m = frexpf(a, &e);
+  if (e - 1 >= -14)
+    return (uint16_t)(sign | ((uint32_t)(e - 1 + 15) << 10) | (uint32_t)ldexpf(2.0f * m - 1.0f, 10));
+  return (uint16_t)(sign | (uint32_t)ldexpf(a, 24));
+}
+
+int orc_half4(float* nodes4, uint32_t nn, void* half) {
+  uint8_t* out = (uint8_t*)half;
+  for (uint32_t i = 0; i < nn; ++i) {
+    float* n = nodes4 + 32 * (size_t)i;
+    uint16_t b[24];
+    for (int k = 0; k < 24; ++k) {
+      const int upper = (k & 4) != 0; /* lo.x[4] hi.x[4] lo.y[4] hi.y[4] ... */
+      n[k] = half_round(n[k], upper ? 1 : -1);
+      b[k] = half_bits(n[k]);
+    }
+    memcpy(out + 64 * (size_t)i, b, 48);
+    memcpy(out + 64 * (size_t)i + 48, &n[24], 16);
+  }
+  return 0;
+}

@@ -162,6 +162,9 @@ int orc_lbvh_build(const float* verts, const float* geom, uint32_t n, float* nod
  * [nn][16] rt_node_t, out nodes4 [nn][32] rt_node4_t (zeros elsewhere) and
  * the worst-case near-first traversal stack. */
 int orc_lbvh_collapse4(const float* nodes, uint32_t nn, float* nodes4, uint32_t* stack);
+/* binary16 planes of a BVH4 node array: planes rounded outward in place,
+ * 64-B rt_node4h_t records (24 halves + 4 child refs) to `half` (nn * 64 B) */
+int orc_half4(float* nodes4, uint32_t nn, void* half);
 
 /* ---- texture regression app (tests/regression/tex; oracle/tex.c) ------ */
 /* LoadImage format conversion of one A8R8G8B8 pixel (VX_TEX_FORMAT_*) */

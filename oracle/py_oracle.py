@@ -101,6 +101,7 @@ def lib():
                                         C.POINTER(C.c_uint32)]
         _lib.orc_lbvh_collapse4.argtypes = [C.c_void_p, C.c_uint32, C.c_void_p,
                                             C.POINTER(C.c_uint32)]
+        _lib.orc_half4.argtypes = [C.c_void_p, C.c_uint32, C.c_void_p]
         _lib.orc_tex_encode.argtypes = [C.c_uint32, C.c_uint32]
         _lib.orc_tex_encode.restype = C.c_uint32
         _lib.orc_tex_build.argtypes = [C.c_void_p, C.c_uint32, C.c_uint32, C.c_uint32, C.c_void_p,
@@ -328,3 +329,14 @@ def lbvh_collapse4(nodes: np.ndarray):
     if rc != 0:
         raise RuntimeError(f"orc_lbvh_collapse4 failed: {rc}")
     return nodes4, stack.value
+
+
+def half4(nodes4: np.ndarray):
+    """binary16 planes of a BVH4 node array (oracle/lbvh.c orc_half4) ->
+    (the fp32 nodes with every plane rounded outward, uint8[nn, 64]
+    rt_node4h_t records)."""
+    n4 = np.ascontiguousarray(nodes4, np.float32).copy()
+    nn = n4.shape[0]
+    half = np.zeros((nn, 64), np.uint8)
+    lib().orc_half4(n4.ctypes.data, nn, half.ctypes.data)
+    return n4, half

@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""GPU BVH build time (kernels/bvh_build.hip, 18 launches incl. the BVH4 collapse) vs the host
+"""GPU BVH build time (kernels/bvh_build.hip, 19 launches incl. the BVH4 collapse and its binary16 planes) vs the host
 binned-SAH build (app/bvh.cpp) on the same triangles, and the traced frame
 time over each tree.  One JSON line per scene."""
 import json

@@ -687,7 +687,8 @@ int rt_renderer_configure(rt_renderer_h r, const rt_render_params_t* p) {
             (raster ? RT_FLAG_RASTER : 0u) |
             (s->tie_high ? RT_FLAG_TIE_HIGH : 0u) | (compact ? RT_FLAG_COMPACT : 0u) |
             (use_bvh4 ? RT_FLAG_BVH4 : 0u) |
-            (use_bvh4 && !r->gpu_bvh && !s->bvh.nodes4h.empty() ? RT_FLAG_BVH4H : 0u);
+            // binary16 node records: the host tree's, or the device tree's (BVHB_HALF)
+            (use_bvh4 && (r->gpu_bvh || !s->bvh.nodes4h.empty()) ? RT_FLAG_BVH4H : 0u);
   if (!raster && configure_vis(r, prims, vis, use_bvh4) != 0) return -1;
   a.bounces = p->bounces;
   a.seed = p->seed;
@@ -913,7 +914,8 @@ int rt_renderer_build_bvh(rt_renderer_h r, rt_bvh_build_stats_t* st) {
       alloc_buf(r->dev, sizeof(bvh_build_arg_t), &argb) ||
       upload(r->dev, nullptr, (uint64_t)nn * sizeof(rt_node_t), &nodes_h, &nodes_addr) ||
       upload(r->dev, nullptr, (uint64_t)(n + 3) * sizeof(rt_tri_t), &tris_h, &tris_addr) ||
-      upload(r->dev, nullptr, (uint64_t)nn * sizeof(rt_node4_t), &nodes4_h, &nodes4_addr)) {
+      upload(r->dev, nullptr, (uint64_t)nn * (sizeof(rt_node4_t) + sizeof(rt_node4h_t)), &nodes4_h,
+             &nodes4_addr)) {
     if (nodes_h) vx_mem_free(nodes_h);
     if (tris_h) vx_mem_free(tris_h);
     if (nodes4_h) vx_mem_free(nodes4_h);
@@ -962,7 +964,7 @@ int rt_renderer_build_bvh(rt_renderer_h r, rt_bvh_build_stats_t* st) {
   for (uint32_t pass = 0; pass < 4; ++pass)  // 30-bit codes: 4 passes of 8 bits
     if (launch(BVHB_HIST, pass) || launch(BVHB_SCAN, pass) || launch(BVHB_SCATTER, pass)) return -1;
   if (launch(BVHB_TREE, 0) || launch(BVHB_BOXES, 0) || launch(BVHB_EMIT, 0) ||
-      launch(BVHB_COLLAPSE, 0))
+      launch(BVHB_COLLAPSE, 0) || launch(BVHB_HALF, 0))
     return -1;
   uint32_t bres[10];
   if (vx_copy_from_dev(bres, bounds.h, 0, sizeof(bres)) != 0) return fail("vx_copy_from_dev failed");
@@ -1013,6 +1015,18 @@ int rt_renderer_export_bvh4(rt_renderer_h r, float* nodes4, uint32_t* num_nodes4
   // copy behind them)
   if (nodes4 && r->arg.num_nodes4 &&
       vx_copy_from_dev(nodes4, r->nodes4, 0, (uint64_t)r->arg.num_nodes4 * sizeof(rt_node4_t)) != 0)
+    return fail("vx_copy_from_dev failed");
+  return 0;
+}
+
+int rt_renderer_export_bvh4h(rt_renderer_h r, void* nodes4h, uint32_t* num_nodes4) {
+  if (!r) return fail("null argument");
+  if (num_nodes4) *num_nodes4 = r->arg.num_nodes4;
+  // the binary16 records behind the fp32 ones (host tree: BuildBvh; device
+  // tree: BVHB_HALF)
+  const uint64_t n4 = r->arg.num_nodes4;
+  if (nodes4h && n4 &&
+      vx_copy_from_dev(nodes4h, r->nodes4, n4 * sizeof(rt_node4_t), n4 * sizeof(rt_node4h_t)) != 0)
     return fail("vx_copy_from_dev failed");
   return 0;
 }

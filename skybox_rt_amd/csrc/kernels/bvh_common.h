@@ -24,6 +24,8 @@ enum {
   BVHB_BOXES = 6,    // bottom-up boxes (agent-scope counters, no spinning)
   BVHB_EMIT = 7,     // rt_node_t / rt_tri_t records, depth
   BVHB_COLLAPSE = 8, // rt_node4_t: every even-depth node absorbs its internal children
+  BVHB_HALF = 9,     // binary16 planes: rt_node4_t rounded outward in place + rt_node4h_t
+                     //   records right behind the rt_node4_t array
 };
 
 typedef struct {
@@ -43,6 +45,7 @@ typedef struct {
   uint64_t nodes_addr;    // rt_node_t [max(n - 1, 1)]
   uint64_t tris_addr;     // rt_tri_t [n + 3]
   uint64_t nodes4_addr;   // rt_node4_t [max(n - 1, 1)]: BVH4 node at the BVH2 index of
-                          //   every even-depth internal node, zeros elsewhere
+                          //   every even-depth internal node, zeros elsewhere; then
+                          //   rt_node4h_t [max(n - 1, 1)] (BVHB_HALF)
   uint32_t n, phase, pass, nblocks;
 } bvh_build_arg_t;

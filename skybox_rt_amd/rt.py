@@ -90,6 +90,7 @@ def lib():
             "rt_renderer_build_bvh": [vp, C.POINTER(BvhBuildStats)],
             "rt_renderer_export_bvh": [vp, vp, vp, C.POINTER(u32), C.POINTER(u32)],
             "rt_renderer_export_bvh4": [vp, vp, C.POINTER(u32)],
+            "rt_renderer_export_bvh4h": [vp, vp, C.POINTER(u32)],
             "rt_renderer_export_vis_tree": [vp, vp, C.POINTER(u32), vp, C.POINTER(u32)],
             "rt_renderer_create": [vp, C.c_char_p, C.POINTER(vp)],
             "rt_renderer_free": [vp],
@@ -247,7 +248,7 @@ class Renderer:
         self.bvh4 = (bvh_width != 2 and os.environ.get("RT_BVH_WIDTH", "4") != "2"
                      and (not self.gpu_bvh or self.gpu_bvh4))
         # BVH4 node steps read 64-B binary16 nodes (rt_node4h_t) when the scene has them
-        self.bvh4_f16 = self.bvh4 and not self.gpu_bvh and bool(self.scene.info()["bvh4_f16"])
+        self.bvh4_f16 = self.bvh4 and (self.gpu_bvh or bool(self.scene.info()["bvh4_f16"]))
 
     def build_bvh(self) -> dict:
         """Build the BVH on the device (kernels/bvh_build.hip) and trace over it
@@ -258,7 +259,7 @@ class Renderer:
         self.gpu_bvh4 = st.stack4 != RT_BVH_STACK4_UNUSED
         if self.params is not None:
             self.bvh4 = self.gpu_bvh4 and not self.params.flags & RT_RENDER_BVH2
-            self.bvh4_f16 = False
+            self.bvh4_f16 = self.bvh4  # the device tree carries binary16 records (BVHB_HALF)
         return st.as_dict()
 
     def export_bvh4(self):
@@ -269,6 +270,16 @@ class Renderer:
         _check(lib().rt_renderer_export_bvh4(self._h, nodes4.ctypes.data, C.byref(n)),
                "rt_renderer_export_bvh4")
         return nodes4[:n.value]
+
+    def export_bvh4h(self):
+        """The same nodes as rt_node4h_t records (uint8[N4, 64]: 24 binary16
+        planes, 4 child refs) -- what the kernels read."""
+        n = C.c_uint32()
+        _check(lib().rt_renderer_export_bvh4h(self._h, None, C.byref(n)), "rt_renderer_export_bvh4h")
+        out = np.zeros((max(n.value, 1), 64), np.uint8)
+        _check(lib().rt_renderer_export_bvh4h(self._h, out.ctypes.data, C.byref(n)),
+               "rt_renderer_export_bvh4h")
+        return out[:n.value]
 
     def export_vis_tree(self):
         """The primary rays' tree of the current configuration: (refs

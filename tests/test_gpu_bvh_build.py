@@ -37,10 +37,14 @@ def test_gpu_bvh_equals_oracle_build(oracle_lib, synth, name):
     assert st["depth"] == od and st["nodes"] == len(on)
     assert np.array_equal(nodes.view(np.uint32), on.view(np.uint32))
     assert np.array_equal(tris.view(np.uint32), ot.view(np.uint32))
-    assert st["launches"] == 18
-    # the device BVH4 collapse == oracle/lbvh.c orc_lbvh_collapse4, bit for bit
+    assert st["launches"] == 19
+    # the device BVH4 collapse == oracle/lbvh.c orc_lbvh_collapse4, and its
+    # binary16 planes (BVHB_HALF) == orc_half4, bit for bit: the fp32 nodes
+    # with every plane rounded outward and the 64-B half records
     o4, ostack = po.lbvh_collapse4(on)
-    assert np.array_equal(r.export_bvh4().view(np.uint32), o4.view(np.uint32))
+    o4r, oh = po.half4(o4)
+    assert np.array_equal(r.export_bvh4().view(np.uint32), o4r.view(np.uint32))
+    assert np.array_equal(r.export_bvh4h(), oh)
     assert st["stack4"] == ostack and r.gpu_bvh4
 
 
@@ -57,7 +61,7 @@ def test_frames_over_gpu_bvh_equal_bruteforce(oracle_lib, synth, name, size, mod
     r = rt.Renderer(s)
     r.configure(size, size, shadows=True, path=mode == "path", bvh_width=width)
     r.build_bvh()                       # reconfigures the renderer onto the new tree
-    assert r.bvh4 == (width != 2) and not r.bvh4_f16
+    assert r.bvh4 == (width != 2) and r.bvh4_f16 == (width != 2)
     r.render()
     osc = po.OracleScene(po.cgltrace.load(path))
     c, _, _, k = po.rt_render(osc, po.rt_params(size, size, shadows=True, nthreads=8,

@@ -318,3 +318,19 @@ def test_lbvh_oracle_structure_and_traversal(oracle_lib, name):
     cv, pv, tv, kv = po.rt_render(osc, p, bvh=(nodes, tris))
     assert np.array_equal(cb, cv) and np.array_equal(pb, pv)
     assert np.array_equal(tb.view(np.uint32), tv.view(np.uint32))
+
+
+@pytest.mark.parametrize("name", ["tekkaman", "scene", "carnival"])
+def test_oracle_half4_restates_host_rounding(name, oracle_lib):
+    """The host tree's fp32 BVH4 planes are already rounded outward to
+    binary16 values (bvh.cpp HalfRound), so the oracle's restatement
+    (orc_half4, which the device tree's BVHB_HALF phase is checked against)
+    must leave them unchanged, and its half records must decode to them."""
+    po = oracle_lib
+    s = rt.Scene.load(scene_path(name))
+    n4 = s.bvh4()
+    r4, h = po.half4(n4)
+    assert np.array_equal(r4.view(np.uint32), n4.view(np.uint32))
+    halves = h[:, :48].copy().view(np.float16).astype(np.float32)
+    assert np.array_equal(halves, n4[:, :24])
+    assert np.array_equal(h[:, 48:].copy().view(np.int32), n4[:, 24:28].view(np.int32))
