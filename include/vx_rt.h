@@ -45,6 +45,11 @@ typedef struct {
                                           rt_render_stats' ray / hit counts; implied by
                                           RT_RENDER_INSTRUMENTED.  Off, a frame writes only
                                           its framebuffer (and one task-count word) */
+#define RT_RENDER_HOST_SETUP 0x800u    /* build the per-resolution records (shading and
+                                          visibility records, primary tree, tile order,
+                                          clears) with the host loops instead of on the
+                                          device (kernels/rt_setup.hip, the default; env
+                                          RT_SETUP=host does the same) */
 
 typedef struct {
   uint32_t width, height;
@@ -156,6 +161,36 @@ int rt_renderer_export_bvh(rt_renderer_h r, float* nodes, float* tris, uint32_t*
  * BuildScreenTree).  NULL arrays: counts only. */
 int rt_renderer_export_vis_tree(rt_renderer_h r, int32_t* refs, uint32_t* num_nodes,
                                 int32_t* leaf_pids, uint32_t* num_leaf);
+
+/* How the last rt_renderer_configure built its per-resolution records.  The
+ * reference builds them per drawcall on the host (draw3d/main.cpp:179-211 ->
+ * graphics::Binning, gfxutil.cpp:103-276); here kernels/rt_setup.hip builds
+ * them unless RT_RENDER_HOST_SETUP. */
+typedef struct {
+  uint32_t device;        /* 1: device setup, 0: host loops */
+  uint32_t launches;      /* device setup launches */
+  uint32_t heavy_tiles;   /* local tiles whose weight (covering geometry primitives) > 0 */
+  uint32_t pad;
+  double setup_ms;        /* host wall time of the record build (uploads / launches included) */
+  double configure_ms;    /* host wall time of the whole rt_renderer_configure */
+} rt_setup_stats_t;
+int rt_renderer_setup_stats(rt_renderer_h r, rt_setup_stats_t* stats);
+
+/* Read back one per-resolution record array of the current configuration
+ * (layouts: kernels/rt_common.h; NO REFERENCE).  out NULL = size query
+ * (*size = bytes). */
+#define RT_REC_PRIMS 0u     /* rt_prim_t per primitive (128 B) */
+#define RT_REC_BBOX 1u      /* rt_bbox_t per primitive (raster mode or device setup) */
+#define RT_REC_VIS 2u       /* uint32[4] per primitive: rectangle x, y, depth bound, any */
+#define RT_REC_VNODES 3u    /* rt_vnode_t per node of the primary rays' tree */
+#define RT_REC_VTRIS 4u     /* rt_vtri_t per leaf record (+3 pads) */
+#define RT_REC_VLAYERS 5u   /* rt_vtri_t per screen layer, last drawn first */
+#define RT_REC_VGEOM 6u     /* rt_vtri_t per geometry primitive, ascending pid */
+#define RT_REC_ORDER 7u     /* u32 per local tile: the work order */
+#define RT_REC_PTRIS 8u     /* rt_tri_t per primitive (clip v0 + pid, e1, e2) */
+#define RT_REC_GEOM 9u      /* rt_tri_t per geometry primitive */
+int rt_renderer_export_records(rt_renderer_h r, uint32_t which, void* out, uint64_t bytes,
+                               uint64_t* size);
 
 /* raw per-workgroup counter rows of the last launch (16 u32 each; the
  * RT_STAMPS diagnostic images put wave timestamps in slots 12-15) */

@@ -25,6 +25,8 @@
 #include "bvh.h"
 #include "bvh_common.h"
 #include "cgltrace.h"
+#include "rt_internal.h"
+#include "setup_common.h"
 #include "setup.h"
 #include "vis.h"
 #include "vortex.h"
@@ -62,60 +64,9 @@ int set_error(const std::string& message, int code) { return fail(message, code)
 std::string library_dir() { return lib_dir(); }
 }  // namespace rtapp
 
-struct rt_scene {
-  rt::Scene scene;
-  rt::Bvh bvh;
-  std::vector<int32_t> geometry;  // depth-tested prims (BVH input), ascending
-  std::vector<int32_t> layers;    // screen-layer prims, descending pid
-  std::string unsupported;        // non-empty: the RT path cannot render it
-  bool tie_high = false;
-  double parse_ms = 0, bvh_ms = 0;
-};
-
-struct rt_renderer {
-  rt_scene* sc = nullptr;
-  vx_device_h dev = nullptr;
-  // kernel images [mode][instrumented]: mode 0 = primary+shadow (BVH),
-  // 1 = path trace, 2 = flat list, 3 = raster (no instrumented image)
-  vx_buffer_h krnl[4][2] = {};
-  vx_buffer_h nodes = nullptr, nodes4 = nullptr, tris = nullptr, layers = nullptr, dcs = nullptr, tex = nullptr;
-  vx_buffer_h ptris = nullptr, geom = nullptr, oms = nullptr, bbox = nullptr, zbuf = nullptr;
-  vx_buffer_h order = nullptr;
-  vx_buffer_h vnodes = nullptr, vtris = nullptr, vlayers = nullptr, vgeom = nullptr;
-  vx_buffer_h gather_recv = nullptr, gather_image = nullptr;  // rank 0 of rt_render_gather
-  vx_buffer_h prims = nullptr, cbuf = nullptr, args = nullptr;
-  uint64_t cbuf_bytes = 0;
-  rt_render_params_t params{};
-  rt_kernel_arg_t arg{};
-  bool configured = false;
-  uint32_t local_tiles = 0;
-  vx_hip_mem_ptr_t mem_ptr = nullptr;
-  vx_hip_stream_t stream = nullptr;
-  vx_hip_last_run_t last_run = nullptr;
-  vx_hip_mpm_rows_t mpm_rows = nullptr;
-  vx_hip_run_totals_t run_totals = nullptr;
-  vx_hip_set_counters_t set_counters = nullptr;
-  std::string kdir;         // kernel directory (images missing there come from lib_dir)
-  bool deep = false;        // RT/PT images with the 32-entry traversal stack
-  // the primary rays' tree of the current configuration (rt_renderer_export_vis_tree)
-  std::vector<std::array<int32_t, 4>> vis_refs;
-  std::vector<int32_t> vis_pids;
-  bool gpu_bvh = false;     // nodes/tris were built on the device (rt_renderer_build_bvh)
-  bool gpu_bvh4 = false;    // ... and collapsed to a BVH4 there whose stack fits the images
-  uint32_t num_tris = 0;    // leaf triangle records (without the 3 padding records)
-
-  ~rt_renderer() {
-    vx_buffer_h* bufs[] = {&krnl[0][0], &krnl[0][1], &krnl[1][0], &krnl[1][1], &krnl[2][0],
-                           &krnl[2][1], &krnl[3][0], &nodes, &nodes4, &tris, &layers, &dcs, &tex,
-                           &ptris, &geom, &oms, &bbox, &zbuf, &order, &vnodes, &vtris, &vlayers,
-                           &vgeom, &gather_recv, &gather_image, &prims, &cbuf, &args};
-    for (auto* b : bufs) {
-      if (*b) vx_mem_free(*b);
-      *b = nullptr;
-    }
-    if (dev) vx_dev_close(dev);
-  }
-};
+using rtapp::DevBuf;
+using rtapp::load_image;
+using rtapp::upload;
 
 extern "C" {
 
@@ -231,7 +182,10 @@ int rt_scene_export_bvh4(rt_scene_h s, float* nodes4) {
   return 0;
 }
 
-static int upload(vx_device_h dev, const void* data, uint64_t size, vx_buffer_h* buf, uint64_t* addr) {
+}  // extern "C"
+
+int rtapp::upload(vx_device_h dev, const void* data, uint64_t size, vx_buffer_h* buf,
+                  uint64_t* addr) {
   const uint64_t sz = size ? size : 64;
   if (*buf) vx_mem_free(*buf);
   *buf = nullptr;
@@ -243,6 +197,8 @@ static int upload(vx_device_h dev, const void* data, uint64_t size, vx_buffer_h*
   if (*addr + sz > (1ull << 32)) return fail("buffer beyond the 4 GiB kernel address range");
   return 0;
 }
+
+extern "C" {
 
 int rt_renderer_create(rt_scene_h s, const char* kernel_dir, rt_renderer_h* out) {
   if (!s || !out) return fail("null argument");
@@ -308,26 +264,33 @@ int rt_renderer_create(rt_scene_h s, const char* kernel_dir, rt_renderer_h* out)
   a.num_nodes = (uint32_t)bvh.nodes.size();
   a.num_nodes4 = (uint32_t)bvh.nodes4.size();
   r->num_tris = (uint32_t)bvh.tris.size();
-  // every primitive's clip-space triangle by pid (path-trace bounce hits)
-  std::vector<rt_tri_t> pt(s->scene.prims.size());
-  for (size_t g = 0; g < pt.size(); ++g) {
-    const auto& p = s->scene.prims[g];
-    std::memset(&pt[g], 0, sizeof(rt_tri_t));
-    for (int k = 0; k < 3; ++k) {
-      const int src = k == 2 ? 3 : k;
-      pt[g].v[k] = p[0].pos[src];
-      pt[g].v[4 + k] = p[1].pos[src] - p[0].pos[src];
-      pt[g].v[8 + k] = p[2].pos[src] - p[0].pos[src];
+  a.num_geom = (uint32_t)s->geometry.size();
+  // the resolution-independent device-setup inputs, and every primitive's
+  // clip-space triangle by pid (path-trace bounce hits) + the geometry
+  // triangles in ascending pid order (flat-list mode) -- built on the device
+  // unless env RT_SETUP=host
+  const char* sv = std::getenv("RT_SETUP");
+  const bool host_records = sv && std::string(sv) == "host";
+  if (rtapp::device_ingest(r.get(), !host_records) != 0) return -1;
+  if (host_records) {
+    std::vector<rt_tri_t> pt(s->scene.prims.size());
+    for (size_t g = 0; g < pt.size(); ++g) {
+      const auto& p = s->scene.prims[g];
+      std::memset(&pt[g], 0, sizeof(rt_tri_t));
+      for (int k = 0; k < 3; ++k) {
+        const int src = k == 2 ? 3 : k;
+        pt[g].v[k] = p[0].pos[src];
+        pt[g].v[4 + k] = p[1].pos[src] - p[0].pos[src];
+        pt[g].v[8 + k] = p[2].pos[src] - p[0].pos[src];
+      }
+      const int32_t pid = (int32_t)g;
+      std::memcpy(&pt[g].v[3], &pid, 4);
     }
-    const int32_t pid = (int32_t)g;
-    std::memcpy(&pt[g].v[3], &pid, 4);
+    if (upload(r->dev, pt.data(), pt.size() * sizeof(rt_tri_t), &r->ptris, &a.ptris_addr)) return -1;
+    std::vector<rt_tri_t> gl;
+    for (int32_t g : s->geometry) gl.push_back(pt[g]);
+    if (upload(r->dev, gl.data(), gl.size() * sizeof(rt_tri_t), &r->geom, &a.geom_addr)) return -1;
   }
-  if (upload(r->dev, pt.data(), pt.size() * sizeof(rt_tri_t), &r->ptris, &a.ptris_addr)) return -1;
-  // the geometry triangles in ascending pid order (flat-list mode)
-  std::vector<rt_tri_t> gl;
-  for (int32_t g : s->geometry) gl.push_back(pt[g]);
-  if (upload(r->dev, gl.data(), gl.size() * sizeof(rt_tri_t), &r->geom, &a.geom_addr)) return -1;
-  a.num_geom = (uint32_t)gl.size();
   a.num_layer_tris = (uint32_t)s->layers.size();
   // textures: one buffer, each texture 256-B aligned
   std::vector<uint8_t> texels;
@@ -355,15 +318,57 @@ int rt_renderer_create(rt_scene_h s, const char* kernel_dir, rt_renderer_h* out)
   return 0;
 }
 
+static int tree_refs(rt_renderer* r, bool use_bvh4, std::vector<std::array<int32_t, 4>>* out_refs,
+                     std::vector<int32_t>* out_pids);
+
 int rt_renderer_export_vis_tree(rt_renderer_h r, int32_t* refs, uint32_t* num_nodes,
                                 int32_t* leaf_pids, uint32_t* num_leaf) {
   if (!r || !r->configured) return fail("renderer not configured");
+  // a device setup keeps no host copy: the traversed tree's references
+  if (r->setup.device && !(r->params.flags & RT_RENDER_RASTER) && r->vis_refs.empty() &&
+      tree_refs(r, r->use_bvh4, &r->vis_refs, &r->vis_pids) != 0)
+    return -1;
   if (num_nodes) *num_nodes = (uint32_t)r->vis_refs.size();
   if (num_leaf) *num_leaf = (uint32_t)r->vis_pids.size();
   if (refs && !r->vis_refs.empty()) std::memcpy(refs, r->vis_refs.data(), r->vis_refs.size() * 16);
   if (leaf_pids && !r->vis_pids.empty())
     std::memcpy(leaf_pids, r->vis_pids.data(), r->vis_pids.size() * 4);
   return 0;
+}
+
+int rt_renderer_setup_stats(rt_renderer_h r, rt_setup_stats_t* st) {
+  if (!r || !st) return fail("null argument");
+  if (!r->configured) return fail("renderer not configured");
+  *st = r->setup;
+  return 0;
+}
+
+int rt_renderer_export_records(rt_renderer_h r, uint32_t which, void* out, uint64_t bytes,
+                               uint64_t* size) {
+  if (!r || !r->configured) return fail("renderer not configured");
+  const rt_kernel_arg_t& a = r->arg;
+  const bool raster = (r->params.flags & RT_RENDER_RASTER) != 0;
+  const uint64_t np = r->sc->scene.prims.size();
+  vx_buffer_h b = nullptr;
+  uint64_t n = 0;
+  switch (which) {
+    case RT_REC_PRIMS: b = r->prims; n = np * sizeof(rt_prim_t); break;
+    case RT_REC_BBOX: b = r->bbox; n = np * sizeof(rt_bbox_t); break;
+    case RT_REC_VIS: b = raster ? nullptr : r->vis; n = np * 16; break;
+    case RT_REC_VNODES: b = raster ? nullptr : r->vnodes; n = (uint64_t)a.num_vnodes * sizeof(rt_vnode_t); break;
+    case RT_REC_VTRIS: b = raster ? nullptr : r->vtris; n = ((uint64_t)r->num_tris + 3) * sizeof(rt_vtri_t); break;
+    case RT_REC_VLAYERS: b = raster ? nullptr : r->vlayers; n = (uint64_t)r->sc->layers.size() * sizeof(rt_vtri_t); break;
+    case RT_REC_VGEOM: b = raster ? nullptr : r->vgeom; n = (uint64_t)r->sc->geometry.size() * sizeof(rt_vtri_t); break;
+    case RT_REC_ORDER: b = a.order_addr ? r->order : nullptr; n = (uint64_t)r->local_tiles * 4; break;
+    case RT_REC_PTRIS: b = r->ptris; n = np * sizeof(rt_tri_t); break;
+    case RT_REC_GEOM: b = r->geom; n = (uint64_t)r->sc->geometry.size() * sizeof(rt_tri_t); break;
+    default: return fail("unknown record array");
+  }
+  if (!b) return fail("record array not present in this configuration");
+  if (size) *size = n;
+  if (!out) return 0;
+  if (bytes < n) return fail("buffer too small");
+  return (n == 0 || vx_copy_from_dev(out, b, 0, n) == 0) ? 0 : fail("vx_copy_from_dev failed");
 }
 
 int rt_renderer_free(rt_renderer_h r) {
@@ -440,9 +445,9 @@ int rt_scene_vis_tree(rt_scene_h s, uint32_t width, uint32_t height, float depth
   return 0;
 }
 
-namespace {
+}  // extern "C"
 
-int load_image(rt_renderer* r, const std::string& name, vx_buffer_h* out) {
+int rtapp::load_image(rt_renderer* r, const std::string& name, vx_buffer_h* out) {
   std::string path = r->kdir + "/" + name;
   if (FILE* f = std::fopen(path.c_str(), "rb")) std::fclose(f);
   else path = lib_dir() + "/" + name;
@@ -450,6 +455,10 @@ int load_image(rt_renderer* r, const std::string& name, vx_buffer_h* out) {
   *out = nullptr;
   return vx_upload_kernel_file(r->dev, path.c_str(), out) == 0 ? 0 : fail("cannot upload kernel " + path);
 }
+
+extern "C" {
+
+namespace {
 
 // the RT / PT images with the 32-entry traversal stack
 int load_deep_images(rt_renderer* r) {
@@ -463,6 +472,58 @@ int load_deep_images(rt_renderer* r) {
 }
 
 }  // namespace
+
+// child references (4 per node; a BVH2 uses slots 0-1) and leaf-record pids
+// of the tree the kernels traverse: the host tree, or the device tree read back
+static int tree_refs(rt_renderer* r, bool use_bvh4, std::vector<std::array<int32_t, 4>>* out_refs,
+                     std::vector<int32_t>* out_pids) {
+  const rt_scene* s = r->sc;
+  const rt_kernel_arg_t& a = r->arg;
+  std::vector<std::array<int32_t, 4>>& refs = *out_refs;
+  std::vector<int32_t>& leaf_pids = *out_pids;
+  refs.clear();
+  leaf_pids.clear();
+  std::vector<rt_node4_t> n4;
+  std::vector<rt_node_t> n2;
+  std::vector<rt_tri_t> tr;
+  if (r->gpu_bvh) {
+    tr.resize(r->num_tris);
+    if (r->num_tris && vx_copy_from_dev(tr.data(), r->tris, 0, tr.size() * sizeof(rt_tri_t)) != 0)
+      return fail("vx_copy_from_dev failed");
+    if (use_bvh4) {
+      n4.resize(a.num_nodes4);
+      if (!n4.empty() && vx_copy_from_dev(n4.data(), r->nodes4, 0, n4.size() * sizeof(rt_node4_t)) != 0)
+        return fail("vx_copy_from_dev failed");
+    } else {
+      n2.resize(a.num_nodes);
+      if (!n2.empty() && vx_copy_from_dev(n2.data(), r->nodes, 0, n2.size() * sizeof(rt_node_t)) != 0)
+        return fail("vx_copy_from_dev failed");
+    }
+  } else {
+    tr = s->bvh.tris;
+    if (use_bvh4) n4 = s->bvh.nodes4;
+    else n2 = s->bvh.nodes;
+  }
+  for (const rt_tri_t& t : tr) {
+    int32_t pid;
+    std::memcpy(&pid, &t.v[3], 4);
+    leaf_pids.push_back(pid);
+  }
+  if (use_bvh4) {
+    for (const rt_node4_t& n : n4) {
+      std::array<int32_t, 4> c;
+      std::memcpy(c.data(), &n.v[24], 16);
+      refs.push_back(c);
+    }
+  } else {
+    for (const rt_node_t& n : n2) {
+      std::array<int32_t, 4> c = {RT_EMPTY_REF, RT_EMPTY_REF, RT_EMPTY_REF, RT_EMPTY_REF};
+      std::memcpy(c.data(), &n.v[12], 8);
+      refs.push_back(c);
+    }
+  }
+  return 0;
+}
 
 // Per-resolution primary-visibility records (app/vis.h): every primitive's
 // covered-pixel rectangle and depth bound, the leaf / layer / flat-list
@@ -489,46 +550,8 @@ static int configure_vis(rt_renderer* r, const std::vector<rt_prim_t>& prims,
       return fail("screen tree build failed");
     if (stack > RT_STACK_DEEP) return fail("screen tree deeper than the traversal stack");
     if (stack > RT_STACK_SHALLOW && !r->deep && load_deep_images(r) != 0) return -1;
-  } else {
-    std::vector<rt_node4_t> n4;
-    std::vector<rt_node_t> n2;
-    std::vector<rt_tri_t> tr;
-    if (r->gpu_bvh) {
-      tr.resize(r->num_tris);
-      if (r->num_tris && vx_copy_from_dev(tr.data(), r->tris, 0, tr.size() * sizeof(rt_tri_t)) != 0)
-        return fail("vx_copy_from_dev failed");
-      if (use_bvh4) {
-        n4.resize(a.num_nodes4);
-        if (!n4.empty() && vx_copy_from_dev(n4.data(), r->nodes4, 0, n4.size() * sizeof(rt_node4_t)) != 0)
-          return fail("vx_copy_from_dev failed");
-      } else {
-        n2.resize(a.num_nodes);
-        if (!n2.empty() && vx_copy_from_dev(n2.data(), r->nodes, 0, n2.size() * sizeof(rt_node_t)) != 0)
-          return fail("vx_copy_from_dev failed");
-      }
-    } else {
-      tr = s->bvh.tris;
-      if (use_bvh4) n4 = s->bvh.nodes4;
-      else n2 = s->bvh.nodes;
-    }
-    for (const rt_tri_t& t : tr) {
-      int32_t pid;
-      std::memcpy(&pid, &t.v[3], 4);
-      leaf_pids.push_back(pid);
-    }
-    if (use_bvh4) {
-      for (const rt_node4_t& n : n4) {
-        std::array<int32_t, 4> c;
-        std::memcpy(c.data(), &n.v[24], 16);
-        refs.push_back(c);
-      }
-    } else {
-      for (const rt_node_t& n : n2) {
-        std::array<int32_t, 4> c = {RT_EMPTY_REF, RT_EMPTY_REF, RT_EMPTY_REF, RT_EMPTY_REF};
-        std::memcpy(c.data(), &n.v[12], 8);
-        refs.push_back(c);
-      }
-    }
+  } else if (tree_refs(r, use_bvh4, &refs, &leaf_pids) != 0) {
+    return -1;
   }
   r->vis_refs = refs;
   r->vis_pids = leaf_pids;
@@ -550,25 +573,14 @@ static int configure_vis(rt_renderer* r, const std::vector<rt_prim_t>& prims,
   return 0;
 }
 
-int rt_renderer_configure(rt_renderer_h r, const rt_render_params_t* p) {
-  if (!r || !p) return fail("null argument");
-  if (p->width == 0 || p->height == 0 || p->width > 32768 || p->height > 32768)
-    return fail("bad resolution");
-  const uint32_t shards = p->shard_count ? p->shard_count : 1;
-  const uint32_t modes = p->flags & (RT_RENDER_PATH | RT_RENDER_FLAT | RT_RENDER_RASTER);
-  if (modes & (modes - 1)) return fail("RT_RENDER_PATH / FLAT / RASTER are exclusive");
-  const bool raster = (p->flags & RT_RENDER_RASTER) != 0;
-  if (!raster && !r->sc->unsupported.empty())
-    return fail("scene not supported by the RT path (use RT_RENDER_RASTER): " + r->sc->unsupported, -2);
-  const bool compact = shards > 1 || (p->flags & RT_RENDER_COMPACT);
-  if (raster && (compact || (p->flags & RT_RENDER_INSTRUMENTED)))
-    return fail("RT_RENDER_RASTER renders whole frames, uninstrumented");
-  if (p->shard_index >= shards) return fail("shard_index >= shard_count");
+// Tile layout, work order and kernel flags of a configuration; the
+// per-resolution records come from the device setup (device_setup.cpp,
+// kernels/rt_setup.hip; the default) or from the host loops below
+// (RT_RENDER_HOST_SETUP / env RT_SETUP=host, and the RT_VIS_TREE=screen
+// variant, which needs the visibility records on the host).
+static int host_setup(rt_renderer* r, const rt_render_params_t* p, bool raster, bool order_on,
+                      uint32_t* heavy) {
   const rt_scene* s = r->sc;
-  r->params = *p;
-  r->params.shard_count = shards;
-  for (vx_buffer_h* b : {&r->gather_recv, &r->gather_image})  // sized per configuration
-    if (*b) { vx_mem_free(*b); *b = nullptr; }
   rt_kernel_arg_t& a = r->arg;
   // per-resolution shading records (rast_prim_t + drawcall id)
   std::vector<rt_prim_t> prims(s->scene.prims.size());
@@ -585,36 +597,86 @@ int rt_renderer_configure(rt_renderer_h r, const rt_render_params_t* p) {
   }
   if (upload(r->dev, prims.data(), prims.size() * sizeof(rt_prim_t), &r->prims, &a.prims_addr))
     return -1;
-  // primary visibility per primitive (app/vis.h): covered-pixel rectangle + depth bound
-  std::vector<rt::VisPrim> vis;
-  if (!raster) {
-    vis.resize(prims.size());
-    for (size_t g = 0; g < prims.size(); ++g) {
-      rt_bbox_t bb{0, 0};
-      const bool ok = setup_ok[g] &&
-                      rt::PrimBBox(s->scene.prims[g], p->width, p->height, &bb) == rt::kSetupOk;
-      vis[g] = rt::ComputeVisPrim(prims[g], ok, bb, p->width, p->height);
-    }
+  // screen boxes (PrimBBox; degenerate / culled primitives get an empty box
+  // and are never binned, gfxutil.cpp:195-232) and primary visibility per
+  // primitive (app/vis.h): covered-pixel rectangle + depth bound
+  std::vector<rt_bbox_t> bb(prims.size());
+  std::vector<rt::VisPrim> vis(prims.size());
+  for (size_t g = 0; g < prims.size(); ++g) {
+    const bool ok = setup_ok[g] &&
+                    rt::PrimBBox(s->scene.prims[g], p->width, p->height, &bb[g]) == rt::kSetupOk;
+    if (!ok) bb[g].x = bb[g].y = 0;
+    if (!raster) vis[g] = rt::ComputeVisPrim(prims[g], ok, bb[g], p->width, p->height);
   }
   if (raster) {
-    // per-resolution screen boxes; degenerate / culled primitives get an
-    // empty box and are never binned (gfxutil.cpp:195-232)
-    std::vector<rt_bbox_t> bb(s->scene.prims.size());
-    for (size_t d = 0; d < s->scene.drawcalls.size(); ++d) {
-      const rt::DrawCall& dc = s->scene.drawcalls[d];
-      for (uint32_t i = 0; i < dc.prim_count; ++i) {
-        const uint32_t g = dc.prim_offset + i;
-        rt_prim_t tmp;
-        const bool degen = rt::PrimSetup(s->scene.prims[g], p->width, p->height, dc.viewport[4],
-                                         dc.viewport[5], &tmp) == rt::kSetupDegenerate;
-        if (rt::PrimBBox(s->scene.prims[g], p->width, p->height, &bb[g]) != rt::kSetupOk || degen)
-          bb[g].x = bb[g].y = 0;
-      }
-    }
     if (upload(r->dev, bb.data(), bb.size() * sizeof(rt_bbox_t), &r->bbox, &a.bbox_addr)) return -1;
     std::vector<uint32_t> zclear((size_t)p->width * p->height, 0xffffffffu);  // main.cpp:48
     if (upload(r->dev, zclear.data(), zclear.size() * 4, &r->zbuf, &a.zbuf_addr)) return -1;
+  } else {
+    // the visibility records as the device setup keeps them (uint4: rx, ry, zmin, any)
+    std::vector<uint32_t> v4(4 * vis.size());
+    for (size_t g = 0; g < vis.size(); ++g) {
+      v4[4 * g] = vis[g].rx;
+      v4[4 * g + 1] = vis[g].ry;
+      v4[4 * g + 2] = vis[g].zmin;
+      v4[4 * g + 3] = vis[g].any ? 1u : 0u;
+    }
+    uint64_t va = 0;
+    if (upload(r->dev, v4.data(), v4.size() * 4, &r->vis, &va)) return -1;
   }
+  // Work order of this shard's 32x32 tiles: heaviest first (longest
+  // processing time first) -- weight = geometry primitives whose
+  // covered-pixel rectangle reaches the tile, capped at 255 (the device
+  // sort's 8-bit key) -- so the long model waves start with the frame
+  // rather than trailing it.  Output is order independent.
+  *heavy = 0;
+  if (order_on) {
+    std::vector<uint32_t> weight((size_t)a.tiles_x * a.tiles_y, 0);
+    for (int32_t g : s->geometry) {
+      const rt::VisPrim& v = vis[g];
+      if (!v.any) continue;
+      const uint32_t tx0 = (v.rx & 0xffffu) >> RT_TILE_LOG, tx1 = (v.rx >> 16) >> RT_TILE_LOG;
+      const uint32_t ty0 = (v.ry & 0xffffu) >> RT_TILE_LOG, ty1 = (v.ry >> 16) >> RT_TILE_LOG;
+      for (uint32_t ty = ty0; ty <= ty1 && ty < a.tiles_y; ++ty)
+        for (uint32_t tx = tx0; tx <= tx1 && tx < a.tiles_x; ++tx) ++weight[ty * a.tiles_x + tx];
+    }
+    const uint32_t shards = a.shard_count;
+    std::vector<uint32_t> ord(r->local_tiles);
+    for (uint32_t i = 0; i < r->local_tiles; ++i) ord[i] = i;
+    auto w = [&](uint32_t lt) { return std::min(weight[a.shard_index + lt * shards], RTS_WEIGHT_CAP); };
+    std::stable_sort(ord.begin(), ord.end(), [&](uint32_t x, uint32_t y) { return w(x) > w(y); });
+    if (upload(r->dev, ord.data(), ord.size() * 4, &r->order, &a.order_addr)) return -1;
+    while (*heavy < r->local_tiles && w(ord[*heavy]) > 0) ++*heavy;
+  }
+  if (!raster && configure_vis(r, prims, vis, r->use_bvh4) != 0) return -1;
+  // output buffer, pre-filled with the clear colour (draw3d/main.cpp:485-490)
+  std::vector<uint32_t> clear(r->cbuf_bytes / 4 ? r->cbuf_bytes / 4 : 1, p->clear_color);
+  if (upload(r->dev, clear.data(), r->cbuf_bytes, &r->cbuf, &a.cbuf_addr)) return -1;
+  return 0;
+}
+
+int rt_renderer_configure(rt_renderer_h r, const rt_render_params_t* p) {
+  if (!r || !p) return fail("null argument");
+  if (p->width == 0 || p->height == 0 || p->width > 32768 || p->height > 32768)
+    return fail("bad resolution");
+  const auto t0 = std::chrono::steady_clock::now();
+  const uint32_t shards = p->shard_count ? p->shard_count : 1;
+  const uint32_t modes = p->flags & (RT_RENDER_PATH | RT_RENDER_FLAT | RT_RENDER_RASTER);
+  if (modes & (modes - 1)) return fail("RT_RENDER_PATH / FLAT / RASTER are exclusive");
+  const bool raster = (p->flags & RT_RENDER_RASTER) != 0;
+  if (!raster && !r->sc->unsupported.empty())
+    return fail("scene not supported by the RT path (use RT_RENDER_RASTER): " + r->sc->unsupported, -2);
+  const bool compact = shards > 1 || (p->flags & RT_RENDER_COMPACT);
+  if (raster && (compact || (p->flags & RT_RENDER_INSTRUMENTED)))
+    return fail("RT_RENDER_RASTER renders whole frames, uninstrumented");
+  if (p->shard_index >= shards) return fail("shard_index >= shard_count");
+  const rt_scene* s = r->sc;
+  r->configured = false;
+  r->params = *p;
+  r->params.shard_count = shards;
+  for (vx_buffer_h* b : {&r->gather_recv, &r->gather_image})  // sized per configuration
+    if (*b) { vx_mem_free(*b); *b = nullptr; }
+  rt_kernel_arg_t& a = r->arg;
   a.width = p->width;
   a.height = p->height;
   // raster workgroups own 2^log x 2^log tiles (16x16 by default; env
@@ -632,55 +694,14 @@ int rt_renderer_configure(rt_renderer_h r, const rt_render_params_t* p) {
   a.num_tasks = r->local_tiles * (raster ? 256u : RT_TILE_PIXELS);
   a.shard_index = p->shard_index;
   a.shard_count = shards;
-  // Work order of this shard's 32x32 tiles: heaviest first (longest
-  // processing time first) -- weight = geometry primitives whose
-  // covered-pixel rectangle reaches the tile -- so the long model waves start
-  // with the frame rather than trailing it.  Output is order independent.
-  // RT_TILE_ORDER=0: identity.
   a.order_addr = 0;
   a.split_tiles = 0;
   a.split_log = 5;
-  if (!raster && r->local_tiles > 0 && !(std::getenv("RT_TILE_ORDER") &&
-                                         std::atoi(std::getenv("RT_TILE_ORDER")) == 0)) {
-    std::vector<uint32_t> weight(tiles, 0);
-    for (int32_t g : s->geometry) {
-      const rt::VisPrim& v = vis[g];
-      if (!v.any) continue;
-      const uint32_t tx0 = (v.rx & 0xffffu) >> RT_TILE_LOG, tx1 = (v.rx >> 16) >> RT_TILE_LOG;
-      const uint32_t ty0 = (v.ry & 0xffffu) >> RT_TILE_LOG, ty1 = (v.ry >> 16) >> RT_TILE_LOG;
-      for (uint32_t ty = ty0; ty <= ty1 && ty < a.tiles_y; ++ty)
-        for (uint32_t tx = tx0; tx <= tx1 && tx < a.tiles_x; ++tx) ++weight[ty * a.tiles_x + tx];
-    }
-    std::vector<uint32_t> ord(r->local_tiles);
-    for (uint32_t i = 0; i < r->local_tiles; ++i) ord[i] = i;
-    auto w = [&](uint32_t lt) { return weight[p->shard_index + lt * shards]; };
-    std::stable_sort(ord.begin(), ord.end(), [&](uint32_t x, uint32_t y) { return w(x) > w(y); });
-    if (upload(r->dev, ord.data(), ord.size() * 4, &r->order, &a.order_addr)) return -1;
-    // path tracing: tiles geometry covers (first in `ord`; oracle/rt.c
-    // tile_split restates the rule) run 32 pixels per wave (task_map in
-    // rt_trace.h): 0.34 -> 0.30 ms at 1024^2; for
-    // primary + shadow rays it measured slower (0.071 -> 0.086 ms: the
-    // shadow rays then also trace in half-empty waves), so off there.
-    // RT_SPLIT_TILES=n overrides the count, 0 disables.
-    uint32_t heavy = 0;
-    if (p->flags & RT_RENDER_PATH)
-      while (heavy < r->local_tiles && w(ord[heavy]) > 0) ++heavy;
-    if (const char* e = std::getenv("RT_SPLIT_TILES"))
-      heavy = std::min<uint32_t>((uint32_t)std::atoi(e), r->local_tiles);
-    a.split_tiles = heavy;
-    a.split_log = 5;  // 32 pixels per wave
-    if (const char* e = std::getenv("RT_SPLIT_LOG")) a.split_log = std::min(6u, std::max(3u, (uint32_t)std::atoi(e)));
-    const uint32_t extra = RT_TILE_PIXELS * ((64u >> a.split_log) - 1u);  // per split tile
-    a.num_tasks += heavy * extra;
-    // timing probe only (the frame is incomplete): render just the first n
-    // tiles of the work order, e.g. the geometry tiles without the background
-    if (const char* e = std::getenv("RT_TILE_LIMIT")) {
-      const uint32_t n = std::min<uint32_t>((uint32_t)std::atoi(e), r->local_tiles);
-      a.num_tasks = std::min(a.num_tasks, n * RT_TILE_PIXELS + std::min(n, heavy) * extra);
-    }
-  }
+  const bool order_on = !raster && r->local_tiles > 0 &&
+                        !(std::getenv("RT_TILE_ORDER") && std::atoi(std::getenv("RT_TILE_ORDER")) == 0);
   bool use_bvh4 = !(p->flags & RT_RENDER_BVH2) && (!r->gpu_bvh || r->gpu_bvh4);
   if (const char* e = std::getenv("RT_BVH_WIDTH")) use_bvh4 = use_bvh4 && std::atoi(e) != 2;
+  r->use_bvh4 = use_bvh4;
   a.flags = ((p->flags & RT_RENDER_SHADOWS) ? RT_FLAG_SHADOWS : 0u) |
             ((p->flags & RT_RENDER_PATH) ? RT_FLAG_PATH : 0u) |
             ((p->flags & RT_RENDER_FLAT) ? RT_FLAG_FLAT : 0u) |
@@ -689,7 +710,6 @@ int rt_renderer_configure(rt_renderer_h r, const rt_render_params_t* p) {
             (use_bvh4 ? RT_FLAG_BVH4 : 0u) |
             // binary16 node records: the host tree's, or the device tree's (BVHB_HALF)
             (use_bvh4 && (r->gpu_bvh || !s->bvh.nodes4h.empty()) ? RT_FLAG_BVH4H : 0u);
-  if (!raster && configure_vis(r, prims, vis, use_bvh4) != 0) return -1;
   a.bounces = p->bounces;
   a.seed = p->seed;
   a.clear_color = p->clear_color;
@@ -698,14 +718,54 @@ int rt_renderer_configure(rt_renderer_h r, const rt_render_params_t* p) {
   a.light[0] = p->light[0];
   a.light[1] = p->light[1];
   a.light[2] = p->light[2];
-  // output buffer, pre-filled with the clear colour (draw3d/main.cpp:485-490)
   const uint64_t npx = compact ? (uint64_t)r->local_tiles * RT_TILE_PIXELS
                                   : (uint64_t)p->width * p->height;
-  std::vector<uint32_t> clear(npx ? npx : 1, p->clear_color);
-  if (upload(r->dev, clear.data(), npx * 4, &r->cbuf, &a.cbuf_addr)) return -1;
   r->cbuf_bytes = npx * 4;
+  // the per-resolution records: on the device unless the host path is asked
+  // for (or needed: the screen-space primary tree is built on the host)
+  const char* sv = std::getenv("RT_SETUP");
+  const char* vt = std::getenv("RT_VIS_TREE");
+  const bool device = !(p->flags & RT_RENDER_HOST_SETUP) && !(sv && std::string(sv) == "host") &&
+                      !(!raster && vt && std::string(vt) == "screen");
+  uint32_t heavy = 0, launches = 0;
+  const auto t1 = std::chrono::steady_clock::now();
+  if (device) {
+    r->vis_refs.clear();
+    r->vis_pids.clear();
+    if (rtapp::device_setup(r, raster, order_on, &heavy, &launches) != 0) return -1;
+  } else if (host_setup(r, p, raster, order_on, &heavy) != 0) {
+    return -1;
+  }
+  const double setup_ms = ms_since(t1);
+  if (order_on) {
+    // path tracing: tiles that geometry covers (first in the order;
+    // oracle/rt.c tile_split restates the rule) run 32 pixels per wave
+    // (task_map in rt_trace.h): 0.34 -> 0.30 ms at 1024^2; for primary +
+    // shadow rays it measured slower (0.071 -> 0.086 ms: the shadow rays then
+    // also trace in half-empty waves), so off there.  RT_SPLIT_TILES=n
+    // overrides the count, 0 disables.
+    uint32_t split = (p->flags & RT_RENDER_PATH) ? heavy : 0u;
+    if (const char* e = std::getenv("RT_SPLIT_TILES"))
+      split = std::min<uint32_t>((uint32_t)std::atoi(e), r->local_tiles);
+    a.split_tiles = split;
+    a.split_log = 5;  // 32 pixels per wave
+    if (const char* e = std::getenv("RT_SPLIT_LOG")) a.split_log = std::min(6u, std::max(3u, (uint32_t)std::atoi(e)));
+    const uint32_t extra = RT_TILE_PIXELS * ((64u >> a.split_log) - 1u);  // per split tile
+    a.num_tasks += split * extra;
+    // timing probe only (the frame is incomplete): render just the first n
+    // tiles of the work order, e.g. the geometry tiles without the background
+    if (const char* e = std::getenv("RT_TILE_LIMIT")) {
+      const uint32_t n = std::min<uint32_t>((uint32_t)std::atoi(e), r->local_tiles);
+      a.num_tasks = std::min(a.num_tasks, n * RT_TILE_PIXELS + std::min(n, split) * extra);
+    }
+  }
   uint64_t args_addr = 0;
   if (upload(r->dev, &a, sizeof(a), &r->args, &args_addr)) return -1;
+  r->setup.device = device ? 1u : 0u;
+  r->setup.launches = launches;
+  r->setup.heavy_tiles = heavy;
+  r->setup.setup_ms = setup_ms;
+  r->setup.configure_ms = ms_since(t0);
   r->configured = true;
   return 0;
 }
@@ -861,14 +921,6 @@ int rt_device_caps(rt_renderer_h r, uint64_t caps[8]) {
 // ---- GPU BVH build (kernels/bvh_build.hip) --------
 
 namespace {
-
-struct DevBuf {  // scratch buffer freed at scope exit
-  vx_buffer_h h = nullptr;
-  uint64_t addr = 0;
-  ~DevBuf() {
-    if (h) vx_mem_free(h);
-  }
-};
 
 int alloc_buf(vx_device_h dev, uint64_t size, DevBuf* b, const void* init = nullptr) {
   return upload(dev, init, size, &b->h, &b->addr);

@@ -1,0 +1,108 @@
+// rt_internal.h -- the RT host app's scene / renderer state (librtapp.so
+// internals shared by rt_app.cpp and device_setup.cpp; not part of the ABI).
+#pragma once
+
+#include <array>
+#include <cstdint>
+#include <string>
+#include <vector>
+
+#include "app_util.h"
+#include "bvh.h"
+#include "cgltrace.h"
+#include "rt_common.h"
+#include "vortex.h"
+#include "vortex_hip.h"
+#include "vx_rt.h"
+
+struct rt_scene {
+  rt::Scene scene;
+  rt::Bvh bvh;
+  std::vector<int32_t> geometry;  // depth-tested prims (BVH input), ascending
+  std::vector<int32_t> layers;    // screen-layer prims, descending pid
+  std::string unsupported;        // non-empty: the RT path cannot render it
+  bool tie_high = false;
+  double parse_ms = 0, bvh_ms = 0;
+};
+
+struct rt_renderer {
+  rt_scene* sc = nullptr;
+  vx_device_h dev = nullptr;
+  // kernel images [mode][instrumented]: mode 0 = primary+shadow (BVH),
+  // 1 = path trace, 2 = flat list, 3 = raster (no instrumented image)
+  vx_buffer_h krnl[4][2] = {};
+  vx_buffer_h nodes = nullptr, nodes4 = nullptr, tris = nullptr, layers = nullptr, dcs = nullptr, tex = nullptr;
+  vx_buffer_h ptris = nullptr, geom = nullptr, oms = nullptr, bbox = nullptr, zbuf = nullptr;
+  vx_buffer_h order = nullptr;
+  vx_buffer_h vnodes = nullptr, vtris = nullptr, vlayers = nullptr, vgeom = nullptr;
+  vx_buffer_h gather_recv = nullptr, gather_image = nullptr;  // rank 0 of rt_render_gather
+  vx_buffer_h prims = nullptr, cbuf = nullptr, args = nullptr;
+  // device-side setup (device_setup.cpp, kernels/rt_setup.hip): the image,
+  // the resolution-independent inputs uploaded once at creation, and the
+  // per-primitive visibility records of the current configuration
+  vx_buffer_h setup_krnl = nullptr, verts = nullptr, pdc = nullptr, dcz = nullptr;
+  vx_buffer_h layer_list = nullptr, geometry_list = nullptr, vis = nullptr;
+  uint64_t cbuf_bytes = 0;
+  rt_render_params_t params{};
+  rt_kernel_arg_t arg{};
+  bool configured = false;
+  uint32_t local_tiles = 0;
+  vx_hip_mem_ptr_t mem_ptr = nullptr;
+  vx_hip_stream_t stream = nullptr;
+  vx_hip_last_run_t last_run = nullptr;
+  vx_hip_mpm_rows_t mpm_rows = nullptr;
+  vx_hip_run_totals_t run_totals = nullptr;
+  vx_hip_set_counters_t set_counters = nullptr;
+  std::string kdir;         // kernel directory (images missing there come from lib_dir)
+  bool deep = false;        // RT/PT images with the 32-entry traversal stack
+  // the primary rays' tree of the current configuration (rt_renderer_export_vis_tree;
+  // host setup only -- after a device setup it is read back on request)
+  std::vector<std::array<int32_t, 4>> vis_refs;
+  std::vector<int32_t> vis_pids;
+  bool use_bvh4 = true;     // the configured traversal reads the BVH4
+  bool gpu_bvh = false;     // nodes/tris were built on the device (rt_renderer_build_bvh)
+  bool gpu_bvh4 = false;    // ... and collapsed to a BVH4 there whose stack fits the images
+  uint32_t num_tris = 0;    // leaf triangle records (without the 3 padding records)
+  rt_setup_stats_t setup{};  // the last configuration's setup (rt_renderer_setup_stats)
+
+  ~rt_renderer() {
+    vx_buffer_h* bufs[] = {&krnl[0][0], &krnl[0][1], &krnl[1][0], &krnl[1][1], &krnl[2][0],
+                           &krnl[2][1], &krnl[3][0], &nodes, &nodes4, &tris, &layers, &dcs, &tex,
+                           &ptris, &geom, &oms, &bbox, &zbuf, &order, &vnodes, &vtris, &vlayers,
+                           &vgeom, &gather_recv, &gather_image, &prims, &cbuf, &args,
+                           &setup_krnl, &verts, &pdc, &dcz, &layer_list, &geometry_list, &vis};
+    for (auto* b : bufs) {
+      if (*b) vx_mem_free(*b);
+      *b = nullptr;
+    }
+    if (dev) vx_dev_close(dev);
+  }
+};
+
+namespace rtapp {
+
+// (re)allocate *buf (size bytes, or 64 when 0), copy `data` when given; the
+// device address must lie below 4 GiB (the kernels' 32-bit arena offsets)
+int upload(vx_device_h dev, const void* data, uint64_t size, vx_buffer_h* buf, uint64_t* addr);
+// kernel image `name` from the renderer's kernel directory (else the library's)
+int load_image(rt_renderer* r, const std::string& name, vx_buffer_h* out);
+
+struct DevBuf {  // scratch buffer freed at scope exit
+  vx_buffer_h h = nullptr;
+  uint64_t addr = 0;
+  ~DevBuf() {
+    if (h) vx_mem_free(h);
+  }
+};
+
+// device_setup.cpp: the resolution-independent inputs of the device setup
+// and the triangle records built from them (ptris, geom) at renderer creation
+int device_ingest(rt_renderer* r, bool records);
+// the per-resolution records of rt_renderer_configure on the device: prims
+// (+ bbox, zbuf clear for raster), vis / vtris / vlayers / vgeom / vnodes,
+// the tile order (heavy = local tiles with weight > 0), the cleared cbuf.
+// r->arg holds the layout fields (tiles, shard, flags, the tree); the
+// record buffers are (re)allocated here and their addresses set in r->arg.
+int device_setup(rt_renderer* r, bool raster, bool order_on, uint32_t* heavy, uint32_t* launches);
+
+}  // namespace rtapp

@@ -1,0 +1,627 @@
+// rt_setup.hip -- the per-resolution setup of the RT path on the GPU
+// (the reference's per-drawcall host pre-pass
+// draw3d/main.cpp:179-211 -> graphics::Binning, gfxutil.cpp:103-276).  The
+// records and their layouts are described in setup_common.h; each sub-phase
+// restates one host routine of app/setup.cpp / app/vis.cpp / app/rt_app.cpp
+// operation for operation (fp32 without contraction, IEEE division, x86
+// float -> int32 conversion semantics, exact int64 row solving), so the
+// device records equal the host path's bit for bit.
+#include <hip/hip_runtime.h>
+
+#include "rt_common.h"
+#include "setup_common.h"
+#include "vx_spawn.h"
+
+namespace {
+
+__device__ __forceinline__ uint32_t lane_id() {
+  return __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
+}
+
+// (int32_t)x as the reference's x86 host computes it (cvttss2si: truncation,
+// INT32_MIN for NaN and out-of-range values; the GPU's v_cvt_i32_f32
+// saturates instead)
+__device__ __forceinline__ int32_t cvt_x86(float x) {
+  if (!(x >= -2147483648.0f && x < 2147483648.0f)) return INT32_MIN;
+  return (int32_t)x;
+}
+
+// cocogfx TFixed<frac>(float) on the host (app/setup.cpp FixedHost)
+__device__ __forceinline__ int32_t fixed_host(float f, int frac) {
+  return cvt_x86(f * (float)(1u << frac));
+}
+
+__device__ __forceinline__ int64_t floor_div(int64_t a, int64_t b) {  // b > 0
+  int64_t q = a / b;
+  if (a % b != 0 && a < 0) --q;
+  return q;
+}
+__device__ __forceinline__ int64_t ceil_div(int64_t a, int64_t b) { return -floor_div(-a, b); }
+
+__device__ __forceinline__ int32_t edge_at(const int32_t* e, uint32_t x, uint32_t y) {
+  return (int32_t)((uint32_t)e[0] * x + (uint32_t)e[1] * y + (uint32_t)e[2]);
+}
+
+// app/vis.cpp DepthLowerBound (floor division by 2^24 = arithmetic shift)
+__device__ uint32_t depth_lower_bound(const int32_t* z) {
+  const int64_t T = (int64_t(1) << 24) + 8;
+  const int64_t p0 = (int64_t)z[0] * T, p1 = (int64_t)z[1] * T;
+  const int64_t lo = min(int64_t(0), min(p0, p1)), hi = max(int64_t(0), max(p0, p1));
+  const int64_t zlo = (int64_t)z[2] + (lo >> 24) - 4;
+  const int64_t zhi = (int64_t)z[2] + (hi >> 24) + 4;
+  if ((zlo >> 24) != (zhi >> 24)) return 0u;
+  return (uint32_t)(zlo & 0xffffff);
+}
+
+__device__ __forceinline__ uint32_t wave_min_u32(uint32_t x) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) x = min(x, (uint32_t)__shfl_xor((int)x, o, 64));
+  return x;
+}
+__device__ __forceinline__ uint32_t wave_max_u32(uint32_t x) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) x = max(x, (uint32_t)__shfl_xor((int)x, o, 64));
+  return x;
+}
+
+struct Setup {
+  rt_prim_t prim;
+  uint32_t bx, by;   // rt_bbox_t, 0 when not ok
+  bool ok;           // setup ok and the screen box is not empty
+};
+
+// app/setup.cpp PrimSetup + PrimBBox for primitive g (drawcall dc)
+__device__ void prim_setup(const float* v, uint32_t dc, float zn, float zf, uint32_t W,
+                           uint32_t H, Setup* s) {
+  int32_t* o = reinterpret_cast<int32_t*>(&s->prim);
+  for (int k = 0; k < 32; ++k) o[k] = 0;
+  s->prim.dc = dc;
+  // viewport (0, W, 0, H, near, far): cocogfx ClipToHDC / ClipToScreen
+  const float sx = ((float)W - 0.0f) * 0.5f, cx = ((float)W + 0.0f) * 0.5f;
+  const float sy = ((float)H - 0.0f) * 0.5f, cy = ((float)H + 0.0f) * 0.5f;
+  const float szs = (zf - zn) * 0.5f, szc = (zf + zn) * 0.5f;
+  float hx[3], hy[3], hw[3], sz[3];
+  for (int i = 0; i < 3; ++i) {
+    const float* p = v + 10 * i;
+    hx[i] = p[0] * sx + p[3] * cx;
+    hy[i] = p[1] * sy + p[3] * cy;
+    hw[i] = p[3];
+    const float rhw = 1.0f / p[3];
+    sz[i] = (p[2] * rhw) * szs + szc;
+  }
+  float e[3][3];
+  for (int i = 0; i < 3; ++i) {
+    const int j = (i + 1) % 3, k = (i + 2) % 3;
+    e[i][0] = (hy[j] * hw[k]) - (hy[k] * hw[j]);
+    e[i][1] = (hx[k] * hw[j]) - (hx[j] * hw[k]);
+    e[i][2] = (hx[j] * hy[k]) - (hx[k] * hy[j]);
+  }
+  const float det = e[0][2] * hw[0] + e[1][2] * hw[1] + e[2][2] * hw[2];
+  if (det < 0)
+    for (int i = 0; i < 3; ++i)
+      for (int j = 0; j < 3; ++j) e[i][j] *= -1.0f;
+  bool setup_ok = !(det == 0);
+  if (setup_ok) {
+    for (int i = 0; i < 3; ++i) e[i][2] += e[i][0] * 0.5f + e[i][1] * 0.5f;
+    float m = fabsf(e[0][0]);
+    const float c[5] = {fabsf(e[1][0]), fabsf(e[2][0]), fabsf(e[0][1]), fabsf(e[1][1]),
+                        fabsf(e[2][1])};
+    for (int i = 0; i < 5; ++i) m = (c[i] > m) ? c[i] : m;
+    const float scale = 1.0f / m;
+    for (int i = 0; i < 3; ++i)
+      for (int j = 0; j < 3; ++j) s->prim.edges[i][j] = fixed_host(e[i][j] * scale, 16);
+    float a[7][3];
+    for (int i = 0; i < 3; ++i) {
+      const float* p = v + 10 * i;
+      a[0][i] = sz[i];
+      for (int k = 0; k < 4; ++k) a[1 + k][i] = p[4 + k];
+      a[5][i] = p[8];
+      a[6][i] = p[9];
+    }
+    for (int k = 0; k < 7; ++k) {
+      s->prim.attribs[k][0] = fixed_host(a[k][0] - a[k][2], 24);
+      s->prim.attribs[k][1] = fixed_host(a[k][1] - a[k][2], 24);
+      s->prim.attribs[k][2] = fixed_host(a[k][2], 24);
+    }
+  }
+  // PrimBBox: viewport (0, W, 0, H, 0, 1), x86 fmin / fmax / floor / ceil
+  float l = 0, r = 0, t = 0, b = 0;
+  for (int i = 0; i < 3; ++i) {
+    const float* p = v + 10 * i;
+    const float rhw = 1.0f / p[3];
+    const float x = (p[0] * rhw) * sx + cx, y = (p[1] * rhw) * sy + cy;
+    if (i == 0) {
+      l = r = x;
+      t = b = y;
+    } else {
+      l = fminf(l, x); r = fmaxf(r, x);
+      t = fminf(t, y); b = fmaxf(b, y);
+    }
+  }
+  int32_t L = cvt_x86(floorf(l)), R = cvt_x86(ceilf(r));
+  int32_t T = cvt_x86(floorf(t)), B = cvt_x86(ceilf(b));
+  L = L > 0 ? L : 0;
+  R = R < (int32_t)W ? R : (int32_t)W;
+  T = T > 0 ? T : 0;
+  B = B < (int32_t)H ? B : (int32_t)H;
+  const bool box_ok = !(R <= L || B <= T);
+  s->ok = setup_ok && box_ok;
+  s->bx = s->ok ? ((uint32_t)L | ((uint32_t)R << 16)) : 0u;
+  s->by = s->ok ? ((uint32_t)T | ((uint32_t)B << 16)) : 0u;
+}
+
+// --- sub-phases -------------------------------------------------------------
+
+__device__ void phase_fill(const rt_setup_arg_t* a) {
+  const uint64_t gid = (uint64_t)blockIdx.x * RTS_BLOCK + threadIdx.x;
+  const uint64_t gstride = (uint64_t)gridDim.x * RTS_BLOCK;
+  for (uint32_t f = 0; f < a->nfills && f < RTS_MAX_FILLS; ++f) {
+    const rts_fill_t fl = a->fills[f];
+    uint32_t* dst = vx_ptr<uint32_t>(fl.addr);
+    const uint32_t v = fl.value;
+    const uint64_t n4 = (fl.addr & 15) ? 0 : fl.count / 4;
+    uint4* d4 = reinterpret_cast<uint4*>(dst);
+    for (uint64_t i = gid; i < n4; i += gstride) d4[i] = make_uint4(v, v, v, v);
+    for (uint64_t i = 4 * n4 + gid; i < fl.count; i += gstride) dst[i] = v;
+  }
+}
+
+// wave per primitive: every lane computes the setup (uniform values), lane 0
+// stores the records, the lanes split the rows of the covered-rectangle scan
+// (app/vis.cpp ComputeVisPrim)
+__device__ void phase_primvis(const rt_setup_arg_t* a) {
+  const float* verts = vx_ptr<const float>(a->verts_addr);
+  const uint32_t* pdc = vx_ptr<const uint32_t>(a->pdc_addr);
+  const float* dcz = vx_ptr<const float>(a->dcz_addr);
+  rt_prim_t* prims = vx_ptr<rt_prim_t>(a->prims_addr);
+  rt_bbox_t* bbox = vx_ptr<rt_bbox_t>(a->bbox_addr);
+  uint4* vis = vx_ptr<uint4>(a->vis_addr);
+  const uint32_t W = a->width, H = a->height, l = lane_id();
+  const uint32_t waves = gridDim.x * (RTS_BLOCK / 64);
+  for (uint32_t g = blockIdx.x * (RTS_BLOCK / 64) + (threadIdx.x >> 6); g < a->num_prims; g += waves) {
+    float v[30];
+    const float4* src = reinterpret_cast<const float4*>(verts + 32ull * g);
+#pragma unroll
+    for (int q = 0; q < 7; ++q) {
+      const float4 x = src[q];
+      v[4 * q] = x.x; v[4 * q + 1] = x.y; v[4 * q + 2] = x.z; v[4 * q + 3] = x.w;
+    }
+    {
+      const float2 x = reinterpret_cast<const float2*>(src)[14];
+      v[28] = x.x; v[29] = x.y;
+    }
+    const uint32_t dc = pdc[g];
+    Setup s;
+    prim_setup(v, dc, dcz[2 * dc], dcz[2 * dc + 1], W, H, &s);
+    if (l == 0) {
+      const uint4* pr = reinterpret_cast<const uint4*>(&s.prim);
+      uint4* dst = reinterpret_cast<uint4*>(prims + g);
+#pragma unroll
+      for (int q = 0; q < 8; ++q) dst[q] = pr[q];
+      bbox[g] = rt_bbox_t{s.bx, s.by};
+    }
+    if (a->raster) continue;
+    // covered-pixel rectangle: rows of the binned 32x32 tiles, clipped to the viewport
+    uint32_t xmin = 0xffffffffu, xmax = 0, ymin = 0xffffffffu, ymax = 0;
+    bool all_zero = false;
+    if (s.ok) {
+      const uint32_t L = s.bx & 0xffffu, R = s.bx >> 16, T = s.by & 0xffffu, B = s.by >> 16;
+      const uint32_t X0 = (L >> RT_TILE_LOG) << RT_TILE_LOG;
+      const uint32_t X1 = min(((R + 31u) >> RT_TILE_LOG) << RT_TILE_LOG, W);
+      const uint32_t Y0 = (T >> RT_TILE_LOG) << RT_TILE_LOG;
+      const uint32_t Y1 = min(((B + 31u) >> RT_TILE_LOG) << RT_TILE_LOG, H);
+      const int32_t* e = &s.prim.edges[0][0];
+      for (uint32_t y = Y0 + l; y < Y1; y += 64) {
+        int64_t lo = X0, hi = (int64_t)X1 - 1, d[3] = {0, 0, 0};
+        bool exact = true;
+        for (int i = 0; i < 3 && exact; ++i) {
+          const int64_t ea = e[3 * i];
+          d[i] = (int64_t)e[3 * i + 1] * y + e[3 * i + 2];
+          const int64_t vl = ea * X0 + d[i], vr = ea * ((int64_t)X1 - 1) + d[i];
+          if (vl < INT32_MIN || vl > INT32_MAX || vr < INT32_MIN || vr > INT32_MAX) {
+            exact = false;
+            break;
+          }
+          if (ea > 0) lo = max(lo, ceil_div(-d[i], ea));
+          else if (ea < 0) hi = min(hi, floor_div(d[i], -ea));
+          else if (d[i] < 0) hi = lo - 1;
+        }
+        if (!exact) {  // wrapping edge values: pixel by pixel, as the rasterizer does
+          for (uint32_t x = X0; x < X1; ++x) {
+            const int32_t e0 = edge_at(e, x, y), e1 = edge_at(e + 3, x, y), e2 = edge_at(e + 6, x, y);
+            if (e0 < 0 || e1 < 0 || e2 < 0) continue;
+            xmin = min(xmin, x); xmax = max(xmax, x);
+            ymin = min(ymin, y); ymax = max(ymax, y);
+            all_zero |= (e0 | e1 | e2) == 0;
+          }
+          continue;
+        }
+        if (lo > hi) continue;
+        xmin = min(xmin, (uint32_t)lo); xmax = max(xmax, (uint32_t)hi);
+        ymin = min(ymin, y); ymax = max(ymax, y);
+        int k = 0;
+        while (k < 3 && e[3 * k] == 0) ++k;
+        if (k == 3) {
+          all_zero |= d[0] == 0 && d[1] == 0 && d[2] == 0;
+        } else if ((-d[k]) % e[3 * k] == 0) {
+          const int64_t x = -d[k] / e[3 * k];
+          all_zero |= x >= lo && x <= hi && e[0] * x + d[0] == 0 && e[3] * x + d[1] == 0 &&
+                      e[6] * x + d[2] == 0;
+        }
+      }
+    }
+    xmin = wave_min_u32(xmin); ymin = wave_min_u32(ymin);
+    xmax = wave_max_u32(xmax); ymax = wave_max_u32(ymax);
+    all_zero = __ballot(all_zero) != 0;
+    if (l == 0) {
+      const bool any = xmin != 0xffffffffu;
+      uint4 rec = make_uint4(RT_VIS_EMPTY_RECT, RT_VIS_EMPTY_RECT, RT_VIS_ZMIN_NONE, 0u);
+      if (any)
+        rec = make_uint4(xmin | (xmax << 16), ymin | (ymax << 16),
+                         all_zero ? 0u : depth_lower_bound(s.prim.attribs[0]), 1u);
+      vis[g] = rec;
+    }
+  }
+}
+
+// app/vis.cpp MakeVisTri
+__device__ __forceinline__ void make_vtri(const rt_prim_t* prims, const uint4* vis, int32_t pid,
+                                          rt_vtri_t* out) {
+  rt_vtri_t t;
+  if (pid < 0) {
+    for (int k = 0; k < 9; ++k) t.edges[k] = 0;
+    t.rx = t.ry = RT_VIS_EMPTY_RECT;
+    t.z[0] = t.z[1] = t.z[2] = 0;
+    t.zmin = RT_VIS_ZMIN_NONE;
+  } else {
+    const rt_prim_t& p = prims[pid];
+    const uint4 v = vis[pid];
+    for (int k = 0; k < 9; ++k) t.edges[k] = (&p.edges[0][0])[k];
+    t.rx = v.x;
+    t.ry = v.y;
+    for (int k = 0; k < 3; ++k) t.z[k] = p.attribs[0][k];
+    t.zmin = v.z;
+  }
+  t.pid = pid;
+  const uint4* s = reinterpret_cast<const uint4*>(&t);
+  uint4* d = reinterpret_cast<uint4*>(out);
+#pragma unroll
+  for (int q = 0; q < 4; ++q) d[q] = s[q];
+}
+
+__device__ __forceinline__ int32_t tri_pid(const rt_tri_t* tris, uint32_t k) {
+  return __float_as_int(tris[k].v[3]);
+}
+
+__device__ void phase_vtris(const rt_setup_arg_t* a) {
+  const rt_prim_t* prims = vx_ptr<const rt_prim_t>(a->prims_addr);
+  const uint4* vis = vx_ptr<const uint4>(a->vis_addr);
+  const rt_tri_t* tris = vx_ptr<const rt_tri_t>(a->tris_addr);
+  const int32_t* layers = vx_ptr<const int32_t>(a->layers_addr);
+  const int32_t* geometry = vx_ptr<const int32_t>(a->geometry_addr);
+  uint32_t* status = vx_ptr<uint32_t>(a->status_addr);
+  const uint32_t nt = a->num_tris + 3, nl = a->num_layers, ng = a->num_geom;
+  const uint32_t total = nt + nl + ng;
+  for (uint32_t i = blockIdx.x * RTS_BLOCK + threadIdx.x; i < total; i += gridDim.x * RTS_BLOCK) {
+    int32_t pid;
+    rt_vtri_t* out;
+    if (i < nt) {
+      pid = i < a->num_tris ? tri_pid(tris, i) : -1;
+      out = vx_ptr<rt_vtri_t>(a->vtris_addr) + i;
+    } else if (i < nt + nl) {
+      pid = layers[i - nt];
+      out = vx_ptr<rt_vtri_t>(a->vlayers_addr) + (i - nt);
+    } else {
+      pid = geometry[i - nt - nl];
+      out = vx_ptr<rt_vtri_t>(a->vgeom_addr) + (i - nt - nl);
+    }
+    if (pid >= (int32_t)a->num_prims || (pid < 0 && i < a->num_tris)) {
+      atomicOr(&status[0], RTS_ERR_PID);
+      pid = -1;
+    }
+    make_vtri(prims, vis, pid, out);
+  }
+}
+
+// the 4 child references of node i (BVH4: rt_node4_t slots; BVH2: 2 slots)
+__device__ __forceinline__ void node_refs(const rt_setup_arg_t* a, uint32_t i, int32_t r[4]) {
+  if (a->bvh4) {
+    const int4 c = reinterpret_cast<const int4*>(vx_ptr<const rt_node4_t>(a->nodes_addr) + i)[6];
+    r[0] = c.x; r[1] = c.y; r[2] = c.z; r[3] = c.w;
+  } else {
+    const float4 c = reinterpret_cast<const float4*>(vx_ptr<const rt_node_t>(a->nodes_addr) + i)[3];
+    r[0] = __float_as_int(c.x); r[1] = __float_as_int(c.y);
+    r[2] = r[3] = RT_EMPTY_REF;
+  }
+}
+
+// node references: > 0 internal node, < -1 leaf, -1 empty; 0 (the root is
+// nobody's child: the zero records of the device BVH4's absorbed nodes) empty
+__device__ void phase_link(const rt_setup_arg_t* a) {
+  int32_t* parent = vx_ptr<int32_t>(a->parent_addr);
+  uint32_t* count = vx_ptr<uint32_t>(a->count_addr);
+  uint32_t* status = vx_ptr<uint32_t>(a->status_addr);
+  const uint32_t nn = a->num_nodes;
+  for (uint32_t i = blockIdx.x * RTS_BLOCK + threadIdx.x; i < nn; i += gridDim.x * RTS_BLOCK) {
+    int32_t r[4];
+    node_refs(a, i, r);
+    uint32_t nint = 0;
+    for (int s = 0; s < 4; ++s) {
+      if (r[s] <= 0) continue;
+      if ((uint32_t)r[s] >= nn) {
+        atomicOr(&status[0], RTS_ERR_REF);
+        continue;
+      }
+      parent[r[s]] = (int32_t)(4 * i + s);
+      ++nint;
+    }
+    count[2 * i] = nint;
+    count[2 * i + 1] = 0;
+  }
+}
+
+struct Cover {
+  uint32_t x0, x1, y0, y1, zmin;
+  bool any;
+};
+
+__device__ __forceinline__ void cover_add(Cover* c, uint32_t rx, uint32_t ry, uint32_t zmin) {
+  c->x0 = min(c->x0, rx & 0xffffu); c->x1 = max(c->x1, rx >> 16);
+  c->y0 = min(c->y0, ry & 0xffffu); c->y1 = max(c->y1, ry >> 16);
+  c->zmin = min(c->zmin, zmin);
+  c->any = true;
+}
+
+// bottom-up vnode records (app/vis.cpp BuildVisNodes): each node's slots get
+// the union rectangle / minimum depth bound of the child's subtree; a node's
+// climbing thread computes its leaf slots, its internal slots were written by
+// the children's climbs, and it writes its own union into its parent's slot
+// before the agent-scope acq_rel arrival count -- the last child to arrive
+// climbs on (nobody waits)
+__device__ void phase_climb(const rt_setup_arg_t* a) {
+  const int32_t* parent = vx_ptr<const int32_t>(a->parent_addr);
+  uint32_t* count = vx_ptr<uint32_t>(a->count_addr);
+  const rt_tri_t* tris = vx_ptr<const rt_tri_t>(a->tris_addr);
+  const uint4* vis = vx_ptr<const uint4>(a->vis_addr);
+  rt_vnode_t* vn = vx_ptr<rt_vnode_t>(a->vnodes_addr);
+  uint32_t* status = vx_ptr<uint32_t>(a->status_addr);
+  const uint32_t nn = a->num_nodes;
+  for (uint32_t i = blockIdx.x * RTS_BLOCK + threadIdx.x; i < nn; i += gridDim.x * RTS_BLOCK) {
+    if (count[2 * i] != 0) continue;
+    uint32_t cur = i;
+    for (int guard = 0;; ++guard) {
+      if (guard == 64) {
+        atomicOr(&status[0], RTS_ERR_CLIMB);
+        break;
+      }
+      int32_t r[4];
+      node_refs(a, cur, r);
+      Cover u = {0xffffu, 0u, 0xffffu, 0u, RT_VIS_ZMIN_NONE, false};
+      for (int s = 0; s < 4; ++s) {
+        if (r[s] > 0 && (uint32_t)r[s] < nn) {  // written by the child's climb
+          if (vn[cur].child[s] != RT_EMPTY_REF) cover_add(&u, vn[cur].rx[s], vn[cur].ry[s], vn[cur].zmin[s]);
+          continue;
+        }
+        Cover c = {0xffffu, 0u, 0xffffu, 0u, RT_VIS_ZMIN_NONE, false};
+        if (r[s] < RT_EMPTY_REF) {  // leaf: its triangle records
+          const uint32_t lr = (uint32_t)r[s], first = (lr >> 4) & 0x07ffffffu, cnt = (lr & 15u) + 1u;
+          for (uint32_t k = first; k < first + cnt; ++k) {
+            const int32_t pid = k < a->num_tris ? tri_pid(tris, k) : -1;
+            if (pid < 0 || (uint32_t)pid >= a->num_prims) {
+              atomicOr(&status[0], RTS_ERR_PID);
+              continue;
+            }
+            const uint4 v = vis[pid];
+            if (v.w) cover_add(&c, v.x, v.y, v.z);
+          }
+        }
+        vn[cur].rx[s] = c.any ? (c.x0 | (c.x1 << 16)) : RT_VIS_EMPTY_RECT;
+        vn[cur].ry[s] = c.any ? (c.y0 | (c.y1 << 16)) : RT_VIS_EMPTY_RECT;
+        vn[cur].zmin[s] = c.any ? c.zmin : RT_VIS_ZMIN_NONE;
+        vn[cur].child[s] = c.any ? r[s] : RT_EMPTY_REF;
+        if (c.any) cover_add(&u, vn[cur].rx[s], vn[cur].ry[s], c.zmin);
+      }
+      const int32_t p = parent[cur];
+      if (p < 0) break;
+      const uint32_t pn = (uint32_t)p >> 2, ps = (uint32_t)p & 3u;
+      vn[pn].rx[ps] = u.any ? (u.x0 | (u.x1 << 16)) : RT_VIS_EMPTY_RECT;
+      vn[pn].ry[ps] = u.any ? (u.y0 | (u.y1 << 16)) : RT_VIS_EMPTY_RECT;
+      vn[pn].zmin[ps] = u.any ? u.zmin : RT_VIS_ZMIN_NONE;
+      vn[pn].child[ps] = u.any ? (int32_t)cur : RT_EMPTY_REF;
+      const uint32_t old = __hip_atomic_fetch_add(&count[2 * pn + 1], 1u, __ATOMIC_ACQ_REL,
+                                                  __HIP_MEMORY_SCOPE_AGENT);
+      if (old + 1 != count[2 * pn]) break;
+      cur = pn;
+    }
+  }
+}
+
+// ---- tile order (app/rt_app.cpp configure): weights = geometry primitives
+// whose covered rectangle reaches the tile, as a 2D difference array
+__device__ void phase_weight(const rt_setup_arg_t* a) {
+  const int32_t* geometry = vx_ptr<const int32_t>(a->geometry_addr);
+  const uint4* vis = vx_ptr<const uint4>(a->vis_addr);
+  uint32_t* w = vx_ptr<uint32_t>(a->weight_addr);
+  const uint32_t W1 = a->tiles_x + 1;
+  for (uint32_t j = blockIdx.x * RTS_BLOCK + threadIdx.x; j < a->num_geom; j += gridDim.x * RTS_BLOCK) {
+    const uint4 v = vis[geometry[j]];
+    if (!v.w) continue;
+    const uint32_t tx0 = (v.x & 0xffffu) >> RT_TILE_LOG, tx1 = min((v.x >> 16) >> RT_TILE_LOG, a->tiles_x - 1);
+    const uint32_t ty0 = (v.y & 0xffffu) >> RT_TILE_LOG, ty1 = min((v.y >> 16) >> RT_TILE_LOG, a->tiles_y - 1);
+    if (tx0 > tx1 || ty0 > ty1) continue;
+    atomicAdd(&w[ty0 * W1 + tx0], 1u);
+    atomicAdd(&w[ty0 * W1 + tx1 + 1], 0xffffffffu);
+    atomicAdd(&w[(ty1 + 1) * W1 + tx0], 0xffffffffu);
+    atomicAdd(&w[(ty1 + 1) * W1 + tx1 + 1], 1u);
+  }
+}
+
+__device__ void phase_rowsum(const rt_setup_arg_t* a) {
+  uint32_t* w = vx_ptr<uint32_t>(a->weight_addr);
+  const uint32_t W1 = a->tiles_x + 1;
+  for (uint32_t r = blockIdx.x * RTS_BLOCK + threadIdx.x; r <= a->tiles_y; r += gridDim.x * RTS_BLOCK) {
+    uint32_t run = 0;
+    for (uint32_t x = 0; x < W1; ++x) {
+      run += w[r * W1 + x];
+      w[r * W1 + x] = run;
+    }
+  }
+}
+
+__device__ void phase_colsum(const rt_setup_arg_t* a) {
+  uint32_t* w = vx_ptr<uint32_t>(a->weight_addr);
+  const uint32_t W1 = a->tiles_x + 1;
+  for (uint32_t c = blockIdx.x * RTS_BLOCK + threadIdx.x; c < W1; c += gridDim.x * RTS_BLOCK) {
+    uint32_t run = 0;
+    for (uint32_t y = 0; y <= a->tiles_y; ++y) {
+      run += w[y * W1 + c];
+      w[y * W1 + c] = run;
+    }
+  }
+}
+
+// sort digit of local tile lt: 255 - min(weight, 255) (ascending digit =
+// heaviest first; stable, so equal weights keep the tile order)
+__device__ __forceinline__ uint32_t tile_digit(const rt_setup_arg_t* a, const uint32_t* w, uint32_t lt) {
+  const uint32_t t = a->shard_index + lt * a->shard_count;
+  const uint32_t x = w[(t / a->tiles_x) * (a->tiles_x + 1) + t % a->tiles_x];
+  return RTS_WEIGHT_CAP - min(x, RTS_WEIGHT_CAP);
+}
+
+__device__ void phase_hist(const rt_setup_arg_t* a) {
+  const uint32_t* w = vx_ptr<const uint32_t>(a->weight_addr);
+  uint32_t* hist = vx_ptr<uint32_t>(a->hist_addr);
+  __shared__ uint32_t h[256];
+  for (uint32_t b = blockIdx.x; b < a->nblocks; b += gridDim.x) {
+    h[threadIdx.x] = 0;
+    __syncthreads();
+    for (uint32_t i = 0; i < RTS_ITEMS / RTS_BLOCK; ++i) {
+      const uint32_t lt = b * RTS_ITEMS + i * RTS_BLOCK + threadIdx.x;
+      if (lt < a->local_tiles) atomicAdd(&h[tile_digit(a, w, lt)], 1u);
+    }
+    __syncthreads();
+    hist[threadIdx.x * a->nblocks + b] = h[threadIdx.x];
+    __syncthreads();
+  }
+}
+
+// exclusive scan of hist[256][nblocks] (digit-major) by workgroup 0
+__device__ void phase_scan(const rt_setup_arg_t* a) {
+  if (blockIdx.x != 0) return;
+  uint32_t* hist = vx_ptr<uint32_t>(a->hist_addr);
+  __shared__ uint32_t s[RTS_BLOCK];
+  const uint32_t total = 256u * a->nblocks;
+  const uint32_t chunk = (total + RTS_BLOCK - 1) / RTS_BLOCK;
+  const uint32_t b0 = min(threadIdx.x * chunk, total), b1 = min(b0 + chunk, total);
+  uint32_t sum = 0;
+  for (uint32_t i = b0; i < b1; ++i) sum += hist[i];
+  s[threadIdx.x] = sum;
+  __syncthreads();
+  for (uint32_t o = 1; o < RTS_BLOCK; o <<= 1) {
+    const uint32_t y = threadIdx.x >= o ? s[threadIdx.x - o] : 0u;
+    __syncthreads();
+    s[threadIdx.x] += y;
+    __syncthreads();
+  }
+  uint32_t run = s[threadIdx.x] - sum;
+  for (uint32_t i = b0; i < b1; ++i) {
+    const uint32_t x = hist[i];
+    hist[i] = run;
+    run += x;
+  }
+}
+
+// stable scatter of the local tile indices (rank = digit offset of the block
+// + earlier rounds + earlier waves + lanes below with the same digit)
+__device__ void phase_scatter(const rt_setup_arg_t* a) {
+  const uint32_t* w = vx_ptr<const uint32_t>(a->weight_addr);
+  const uint32_t* hist = vx_ptr<const uint32_t>(a->hist_addr);
+  uint32_t* order = vx_ptr<uint32_t>(a->order_addr);
+  constexpr uint32_t kW = RTS_BLOCK / 64;
+  __shared__ uint32_t base[256];
+  __shared__ uint32_t wcnt[kW][256];
+  const uint32_t wv = threadIdx.x >> 6, l = lane_id();
+  const uint64_t lt_mask = (l == 0) ? 0ull : (~0ull >> (64 - l));
+  for (uint32_t b = blockIdx.x; b < a->nblocks; b += gridDim.x) {
+    base[threadIdx.x] = hist[threadIdx.x * a->nblocks + b];
+    for (uint32_t i = 0; i < kW; ++i) wcnt[i][threadIdx.x] = 0;
+    __syncthreads();
+    for (uint32_t r = 0; r < RTS_ITEMS / RTS_BLOCK; ++r) {
+      const uint32_t lt = b * RTS_ITEMS + r * RTS_BLOCK + threadIdx.x;
+      const bool valid = lt < a->local_tiles;
+      const uint32_t d = valid ? tile_digit(a, w, lt) : 0u;
+      uint64_t peers = __ballot(valid);
+#pragma unroll
+      for (int bit = 0; bit < 8; ++bit) {
+        const uint64_t m = __ballot((d >> bit) & 1u);
+        peers &= ((d >> bit) & 1u) ? m : ~m;
+      }
+      const uint32_t below = (uint32_t)__popcll(peers & lt_mask);
+      if (valid && below == 0) wcnt[wv][d] = (uint32_t)__popcll(peers);
+      __syncthreads();
+      uint32_t off = 0;
+      if (valid)
+        for (uint32_t i = 0; i < wv; ++i) off += wcnt[i][d];
+      const uint32_t dst = base[d] + off + below;
+      __syncthreads();
+      uint32_t sum = 0;
+      for (uint32_t i = 0; i < kW; ++i) {
+        sum += wcnt[i][threadIdx.x];
+        wcnt[i][threadIdx.x] = 0;
+      }
+      base[threadIdx.x] += sum;
+      if (valid) order[dst] = lt;
+      __syncthreads();
+    }
+  }
+}
+
+// renderer creation (app/rt_app.cpp rt_renderer_create): the clip-space
+// triangle of every pid (v0.xyw + pid, e1, e2) and the geometry list's copy
+__device__ __forceinline__ void tri_record(const float* verts, uint32_t g, rt_tri_t* out) {
+  const float* p = verts + 32ull * g;
+  const int src[3] = {0, 1, 3};
+  float r[12];
+  for (int k = 0; k < 3; ++k) {
+    r[k] = p[src[k]];
+    r[4 + k] = p[10 + src[k]] - p[src[k]];
+    r[8 + k] = p[20 + src[k]] - p[src[k]];
+  }
+  r[3] = __int_as_float((int32_t)g);
+  r[7] = r[11] = 0.0f;
+  float4* d = reinterpret_cast<float4*>(out);
+  d[0] = make_float4(r[0], r[1], r[2], r[3]);
+  d[1] = make_float4(r[4], r[5], r[6], r[7]);
+  d[2] = make_float4(r[8], r[9], r[10], r[11]);
+}
+
+__device__ void phase_records(const rt_setup_arg_t* a) {
+  const float* verts = vx_ptr<const float>(a->verts_addr);
+  const int32_t* geometry = vx_ptr<const int32_t>(a->geometry_addr);
+  rt_tri_t* ptris = vx_ptr<rt_tri_t>(a->ptris_addr);
+  rt_tri_t* geom = vx_ptr<rt_tri_t>(a->geom_addr);
+  const uint32_t total = a->num_prims + a->num_geom;
+  for (uint32_t i = blockIdx.x * RTS_BLOCK + threadIdx.x; i < total; i += gridDim.x * RTS_BLOCK) {
+    if (i < a->num_prims) tri_record(verts, i, ptris + i);
+    else tri_record(verts, (uint32_t)geometry[i - a->num_prims], geom + (i - a->num_prims));
+  }
+}
+
+}  // namespace
+
+VX_MAIN(rt_setup_arg_t, arg, RTS_BLOCK) {
+  const uint32_t ph = arg->phases;
+  if (ph & RTS_FILL) phase_fill(arg);
+  if (ph & RTS_PRIMVIS) phase_primvis(arg);
+  if (ph & RTS_VTRIS) phase_vtris(arg);
+  if (ph & RTS_WEIGHT) phase_weight(arg);
+  if (ph & RTS_LINK) phase_link(arg);
+  if (ph & RTS_ROWSUM) phase_rowsum(arg);
+  if (ph & RTS_CLIMB) phase_climb(arg);
+  if (ph & RTS_COLSUM) phase_colsum(arg);
+  if (ph & RTS_HIST) phase_hist(arg);
+  if (ph & RTS_SCAN) phase_scan(arg);
+  if (ph & RTS_SCATTER) phase_scatter(arg);
+  if (ph & RTS_RECORDS) phase_records(arg);
+  return 0;
+}

@@ -1,0 +1,87 @@
+// setup_common.h -- argument block of the device-side per-resolution setup
+// (rt_setup.hip), shared with the host (app/rt_app.cpp device_setup).
+//
+// The reference's host pre-pass per drawcall is draw3d/main.cpp:179-211 ->
+// graphics::Binning (sim/common/gfxutil.cpp:103-276): per primitive the
+// clip -> device transform, edge equations, Q15.16 / Q7.24 fixed-point
+// record (rast_prim_t) and the 32x32 tiles its screen box reaches.  Here the
+// same work runs on the GPU, one launch per row below, in the records the RT
+// kernels read:
+//   prims   rt_prim_t per primitive              (app/setup.cpp PrimSetup)
+//   bbox    rt_bbox_t per primitive              (app/setup.cpp PrimBBox)
+//   vis     uint4 per primitive: covered-pixel rectangle, depth bound, any
+//                                                (app/vis.cpp ComputeVisPrim)
+//   vtris / vlayers / vgeom  rt_vtri_t records   (app/vis.cpp MakeVisTri)
+//   vnodes  rt_vnode_t per tree node, bottom-up  (app/vis.cpp BuildVisNodes)
+//   order   the shard's tiles, heaviest first    (app/rt_app.cpp tile order)
+// and the resolution-independent triangle records at renderer creation
+// (ptris by pid, geom).  Every record equals the host path's bit for bit
+// (tests/test_gpu_setup.py; the host path stays selectable: RT_SETUP=host).
+#pragma once
+
+#include <stdint.h>
+
+#define RTS_BLOCK 256
+#define RTS_ITEMS 1024            // tile-order sort items per block (4 per thread)
+#define RTS_MAX_FILLS 4
+#define RTS_WEIGHT_CAP 255u       // tile-order key: min(weight, 255), one 8-bit digit
+
+// sub-phases, OR-ed into `phases`: a launch runs every selected sub-phase
+// (each independent of the others in the same launch)
+#define RTS_FILL     0x001u  // fills[0..nfills): u32 words = value
+#define RTS_PRIMVIS  0x002u  // wave per primitive: rt_prim_t + rt_bbox_t (+ vis unless raster)
+#define RTS_VTRIS    0x004u  // thread per record: leaf vtris (+3 pads), vlayers, vgeom
+#define RTS_WEIGHT   0x008u  // per geometry primitive: the 4 corners of its tile rectangle
+                             //   in a 2D difference array (tiles_x + 1) x (tiles_y + 1)
+#define RTS_LINK     0x010u  // thread per tree node: parent slot of each internal child,
+                             //   internal-child count, arrival counter 0
+#define RTS_ROWSUM   0x020u  // thread per tile row: prefix sums along x
+#define RTS_CLIMB    0x040u  // thread per node without internal children: vnode rectangles
+                             //   bottom-up (the last child to arrive climbs on)
+#define RTS_COLSUM   0x080u  // thread per tile column: prefix sums along y -> tile weights
+#define RTS_HIST     0x100u  // tile order: per-block histograms of 255 - min(weight, 255)
+#define RTS_SCAN     0x200u  //   exclusive scan (workgroup 0)
+#define RTS_SCATTER  0x400u  //   stable scatter of the local tile indices -> order
+#define RTS_RECORDS  0x800u  // renderer creation: rt_tri_t per pid (ptris), geometry list (geom)
+
+// status words (u32 [4]): [0] malformed-input flags (RTS_ERR_*), [1..3] spare
+#define RTS_ERR_REF   0x1u   // a tree reference out of range
+#define RTS_ERR_PID   0x2u   // a leaf record's pid out of range
+#define RTS_ERR_CLIMB 0x4u   // a climb longer than 64 levels
+
+typedef struct {
+  uint64_t addr;     // u32 words
+  uint64_t count;
+  uint32_t value, pad;
+} rts_fill_t;
+
+typedef struct {
+  uint64_t verts_addr;     // float [P][32]: 3 x (x, y, z, w, r, g, b, a, u, v), 2 pad
+  uint64_t pdc_addr;       // u32 [P]: drawcall of each primitive
+  uint64_t dcz_addr;       // float [num_dc][2]: viewport near, far
+  uint64_t prims_addr;     // rt_prim_t [P]
+  uint64_t bbox_addr;      // rt_bbox_t [P] (empty: degenerate or outside the viewport)
+  uint64_t vis_addr;       // uint4 [P]: rx, ry, zmin, any
+  uint64_t tris_addr;      // rt_tri_t [num_tris]: leaf records (pid bits in v[3])
+  uint64_t nodes_addr;     // the traversed tree: rt_node4_t [num_nodes] (bvh4) or rt_node_t
+  uint64_t vnodes_addr;    // rt_vnode_t [num_nodes]
+  uint64_t vtris_addr;     // rt_vtri_t [num_tris + 3]
+  uint64_t vlayers_addr;   // rt_vtri_t [num_layers]
+  uint64_t vgeom_addr;     // rt_vtri_t [num_geom]
+  uint64_t layers_addr;    // i32 [num_layers]: screen-layer pids, last drawn first
+  uint64_t geometry_addr;  // i32 [num_geom]: depth-tested pids, ascending
+  uint64_t parent_addr;    // i32 [num_nodes]: parent * 4 + slot, -1 for the root / unreached
+  uint64_t count_addr;     // u32 [num_nodes][2]: internal children, arrivals
+  uint64_t weight_addr;    // u32 [(tiles_y + 1) * (tiles_x + 1)]
+  uint64_t hist_addr;      // u32 [256][nblocks]
+  uint64_t order_addr;     // u32 [local_tiles]
+  uint64_t status_addr;    // u32 [4]
+  uint64_t ptris_addr;     // rt_tri_t [P]
+  uint64_t geom_addr;      // rt_tri_t [num_geom]
+  rts_fill_t fills[RTS_MAX_FILLS];
+  uint32_t phases, nfills;
+  uint32_t num_prims, width, height, raster;
+  uint32_t num_tris, num_nodes, bvh4, num_layers, num_geom;
+  uint32_t tiles_x, tiles_y, shard_index, shard_count, local_tiles, nblocks;
+  uint32_t pad[3];
+} rt_setup_arg_t;

@@ -28,6 +28,12 @@ PT_SEED = 0x5EED
 RT_RENDER_INSTRUMENTED = 0x100
 RT_RENDER_COMPACT = 0x200
 RT_RENDER_COUNTERS = 0x400
+RT_RENDER_HOST_SETUP = 0x800
+# rt_renderer_export_records arrays: name -> (id, dtype, words per record)
+RECORDS = {"prims": (0, np.int32, 32), "bbox": (1, np.uint32, 2), "vis": (2, np.uint32, 4),
+           "vnodes": (3, np.uint32, 16), "vtris": (4, np.int32, 16), "vlayers": (5, np.int32, 16),
+           "vgeom": (6, np.int32, 16), "order": (7, np.uint32, 1), "ptris": (8, np.float32, 12),
+           "geom": (9, np.float32, 12)}
 RT_BVH_STACK4_UNUSED = 0xFFFFFFFF
 CLEAR_COLOR = 0xFF000000               # draw3d/main.cpp:47
 DEFAULT_LIGHT = (0.0, 60.0, 80.0)      # clip (x, y, w), SURVEY.md 8(d) config 3
@@ -45,6 +51,14 @@ class SceneInfo(C.Structure):
 class BvhBuildStats(C.Structure):
     _fields_ = [("nodes", C.c_uint32), ("depth", C.c_uint32), ("launches", C.c_uint32),
                 ("stack4", C.c_uint32), ("build_ms", C.c_double), ("kernel_ms", C.c_double)]
+
+    def as_dict(self):
+        return {n: getattr(self, n) for n, _ in self._fields_ if n != "pad"}
+
+
+class SetupStats(C.Structure):
+    _fields_ = [("device", C.c_uint32), ("launches", C.c_uint32), ("heavy_tiles", C.c_uint32),
+                ("pad", C.c_uint32), ("setup_ms", C.c_double), ("configure_ms", C.c_double)]
 
     def as_dict(self):
         return {n: getattr(self, n) for n, _ in self._fields_ if n != "pad"}
@@ -113,6 +127,8 @@ def lib():
             "rt_device_stream": [vp, C.POINTER(vp)],
             "rt_device_caps": [vp, C.POINTER(u64)],
             "rt_render_gather": [vp, vp, vp],
+            "rt_renderer_setup_stats": [vp, C.POINTER(SetupStats)],
+            "rt_renderer_export_records": [vp, u32, vp, u64, C.POINTER(u64)],
         }
         for name, argtypes in sig.items():
             fn = getattr(h, name)
@@ -223,7 +239,8 @@ class Renderer:
                   clear_color: int = CLEAR_COLOR, shard_index: int = 0, shard_count: int = 1,
                   instrumented: bool = False, path: bool = False, bounces: int = 4,
                   seed: int = PT_SEED, flat: bool = False, raster: bool = False,
-                  bvh_width: int = 0, compact: bool = False, counters: bool = True) -> None:
+                  bvh_width: int = 0, compact: bool = False, counters: bool = True,
+                  host_setup: bool = False) -> None:
         """path=True: diffuse path trace (pt_kernel; `bounces` segments per
         path, RNG `seed`) instead of primary + shadow rays.  flat=True: the
         flat triangle list without BVH (BASELINE config 2).  raster=True:
@@ -232,13 +249,16 @@ class Renderer:
         BVH unless env RT_BVH_WIDTH=2).  compact=True: the shard layout
         (tile order, as for shard_count > 1) for a single shard too.
         counters=False: no per-workgroup counter rows (the timed product
-        configuration; stats() then has the task count and kernel time only)."""
+        configuration; stats() then has the task count and kernel time only).
+        host_setup=True: build the per-resolution records with the host loops
+        instead of on the device (kernels/rt_setup.hip)."""
         p = RenderParams()
         p.width, p.height = width, height
         p.flags = ((RT_RENDER_SHADOWS if shadows else 0) | (RT_RENDER_INSTRUMENTED if instrumented else 0)
                    | (RT_RENDER_PATH if path else 0) | (RT_RENDER_FLAT if flat else 0)
                    | (RT_RENDER_RASTER if raster else 0) | (RT_RENDER_BVH2 if bvh_width == 2 else 0)
-                   | (RT_RENDER_COMPACT if compact else 0) | (RT_RENDER_COUNTERS if counters else 0))
+                   | (RT_RENDER_COMPACT if compact else 0) | (RT_RENDER_COUNTERS if counters else 0)
+                   | (RT_RENDER_HOST_SETUP if host_setup else 0))
         p.bounces, p.seed = bounces, seed
         p.light[:] = [float(np.float32(x)) for x in light]
         p.clear_color = clear_color
@@ -249,6 +269,26 @@ class Renderer:
                      and (not self.gpu_bvh or self.gpu_bvh4))
         # BVH4 node steps read 64-B binary16 nodes (rt_node4h_t) when the scene has them
         self.bvh4_f16 = self.bvh4 and (self.gpu_bvh or bool(self.scene.info()["bvh4_f16"]))
+
+    def setup_stats(self) -> dict:
+        """How the last configure built its records (device / host, launches,
+        heavy tiles, setup and configure wall ms)."""
+        st = SetupStats()
+        _check(lib().rt_renderer_setup_stats(self._h, C.byref(st)), "rt_renderer_setup_stats")
+        return st.as_dict()
+
+    def records(self, name: str) -> np.ndarray:
+        """One per-resolution record array of the current configuration
+        (RECORDS: prims, bbox, vis, vnodes, vtris, vlayers, vgeom, order,
+        ptris, geom), as [count, words]."""
+        which, dt, words = RECORDS[name]
+        n = C.c_uint64()
+        _check(lib().rt_renderer_export_records(self._h, which, None, 0, C.byref(n)),
+               f"rt_renderer_export_records({name})")
+        out = np.zeros(max(n.value // 4, 1), dt)
+        _check(lib().rt_renderer_export_records(self._h, which, out.ctypes.data, out.nbytes, C.byref(n)),
+               f"rt_renderer_export_records({name})")
+        return out[:n.value // 4].reshape(-1, words)
 
     def build_bvh(self) -> dict:
         """Build the BVH on the device (kernels/bvh_build.hip) and trace over it

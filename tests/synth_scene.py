@@ -22,16 +22,24 @@ _ITEM = ('<item><first>{i}</first><second><pos><x>{x:.9e}</x><y>{y:.9e}</y><z>{z
          '</texcoord></second></item>')
 
 
-def make_scene(path: str, n: int, seed: int = 1, size: float = 0.03) -> str:
-    """Writes a gzip'd trace of n triangles to `path` (returned)."""
+def make_scene(path: str, n: int, seed: int = 1, size: float = 0.03, w_range=(90.0, 110.0),
+               spread: float = 0.8, w_jitter: float = 0.5, degenerate: int = 0) -> str:
+    """Writes a gzip'd trace of n triangles to `path` (returned): centres
+    uniform in +-spread (NDC), corners +-size around them, w in w_range,
+    each corner's w jittered by +-w_jitter (w_jitter > w_range[0] puts some
+    corners behind the eye); the first `degenerate` triangles repeat their
+    first corner as their last (zero area: the setup's det == 0 exactly)."""
     rng = np.random.default_rng(seed)
-    w = rng.uniform(90.0, 110.0, n)
-    cx, cy = rng.uniform(-0.8, 0.8, n) * w, rng.uniform(-0.8, 0.8, n) * w
+    w = rng.uniform(w_range[0], w_range[1], n)
+    cx, cy = rng.uniform(-spread, spread, n) * w, rng.uniform(-spread, spread, n) * w
     verts = []
     for k in range(3):
         ox, oy = rng.uniform(-size, size, n) * w, rng.uniform(-size, size, n) * w
-        dw = rng.uniform(-0.5, 0.5, n)
+        dw = rng.uniform(-w_jitter, w_jitter, n)
         verts.append((cx + ox, cy + oy, (w + dw) * 0.5, w + dw))
+    if degenerate:
+        verts[2] = tuple(np.concatenate([v0[:degenerate], v2[degenerate:]])
+                         for v0, v2 in zip(verts[0], verts[2]))
     col = rng.uniform(0.2, 1.0, (n, 3))
     items = []
     for t in range(n):
