@@ -139,8 +139,20 @@ typedef struct {
                            images' stack and the BVH2 is traversed instead */
   double build_ms;      /* host wall time of the whole build (upload + launches) */
   double kernel_ms;     /* sum of the build kernels' HIP-event times */
+  uint32_t nodes4;      /* rt_node4_t records (LBVH: one per BVH2 index, zeros at absorbed nodes) */
+  uint32_t depth4;      /* BVH4 depth (SAH build; 0 for the LBVH) */
+  uint32_t method;      /* RT_BVH_BUILD_* */
+  uint32_t pad;
 } rt_bvh_build_stats_t;
-int rt_renderer_build_bvh(rt_renderer_h r, rt_bvh_build_stats_t* stats);
+int rt_renderer_build_bvh(rt_renderer_h r, rt_bvh_build_stats_t* stats);  /* = _ex(LBVH) */
+/* RT_BVH_BUILD_LBVH: Morton codes + radix tree (kernels/bvh_build.hip, 19
+ * launches, fastest build).  RT_BVH_BUILD_SAH: the host builder's binned-SAH
+ * tree, BVH4 collapse and binary16 planes restated on the device
+ * (kernels/bvh_sah.hip, one launch per level + 8): the same arrays as the
+ * scene's host build, bit for bit. */
+#define RT_BVH_BUILD_LBVH 0u
+#define RT_BVH_BUILD_SAH 1u
+int rt_renderer_build_bvh_ex(rt_renderer_h r, uint32_t method, rt_bvh_build_stats_t* stats);
 #define RT_BVH_STACK4_UNUSED 0xFFFFFFFFu
 /* the renderer's current BVH4 (float[num_nodes4][32], rt_node4_t: the host
  * tree's collapse, or after rt_renderer_build_bvh the device collapse --

@@ -26,6 +26,7 @@
 #include "bvh_common.h"
 #include "cgltrace.h"
 #include "rt_internal.h"
+#include "sah_common.h"
 #include "setup_common.h"
 #include "setup.h"
 #include "vis.h"
@@ -928,8 +929,7 @@ int alloc_buf(vx_device_h dev, uint64_t size, DevBuf* b, const void* init = null
 
 }  // namespace
 
-int rt_renderer_build_bvh(rt_renderer_h r, rt_bvh_build_stats_t* st) {
-  if (!r) return fail("null argument");
+static int build_lbvh(rt_renderer_h r, rt_bvh_build_stats_t* st) {
   rt_scene* s = r->sc;
   const uint32_t n = (uint32_t)s->geometry.size();
   if (n == 0) return fail("no depth-tested geometry to build a BVH over");
@@ -1051,6 +1051,8 @@ int rt_renderer_build_bvh(rt_renderer_h r, rt_bvh_build_stats_t* st) {
     st->launches = launches;
     st->kernel_ms = kernel_ms;
     st->build_ms = ms_since(t0);
+    st->nodes4 = nn;
+    st->method = RT_BVH_BUILD_LBVH;
   }
   // a configured renderer picks up the new tree (and the BVH2 traversal) now
   if (r->configured) {
@@ -1058,6 +1060,165 @@ int rt_renderer_build_bvh(rt_renderer_h r, rt_bvh_build_stats_t* st) {
     return rt_renderer_configure(r, &p);
   }
   return 0;
+}
+
+// The host builder (app/bvh.cpp) restated on the device (kernels/bvh_sah.hip):
+// the same binned-SAH tree, BVH4 collapse and binary16 planes bit for bit.
+static int build_sah(rt_renderer_h r, rt_bvh_build_stats_t* st) {
+  rt_scene* s = r->sc;
+  const uint32_t n = (uint32_t)s->geometry.size();
+  const auto t0 = std::chrono::steady_clock::now();
+  vx_buffer_h krnl = nullptr;
+  if (load_image(r, "bvh_sah.vxbin", &krnl)) return -1;
+  DevBuf kimg;
+  kimg.h = krnl;
+  std::vector<float> verts((size_t)n * 12, 0.0f);
+  for (uint32_t i = 0; i < n; ++i) {
+    const auto& p = s->scene.prims[s->geometry[i]];
+    for (int c = 0; c < 3; ++c) {
+      verts[(size_t)i * 12 + 4 * c + 0] = p[c].pos[0];
+      verts[(size_t)i * 12 + 4 * c + 1] = p[c].pos[1];
+      verts[(size_t)i * 12 + 4 * c + 2] = p[c].pos[3];
+    }
+  }
+  std::vector<uint32_t> ctl0(SAH_CTL_WORDS, 0u);
+  DevBuf vb, tbox, cen, idx[2], fin, segs[2], nrec, nbox, cnt, d0, parent, cs, is4, ctl, argb;
+  const uint64_t N = n;
+  if (alloc_buf(r->dev, verts.size() * 4, &vb, verts.data()) || alloc_buf(r->dev, N * 32, &tbox) ||
+      alloc_buf(r->dev, N * 16, &cen) || alloc_buf(r->dev, N * 4, &idx[0]) ||
+      alloc_buf(r->dev, N * 4, &idx[1]) || alloc_buf(r->dev, N * 4, &fin) ||
+      alloc_buf(r->dev, N * 16, &segs[0]) || alloc_buf(r->dev, N * 16, &segs[1]) ||
+      alloc_buf(r->dev, N * 16, &nrec) || alloc_buf(r->dev, N * 64, &nbox) ||
+      alloc_buf(r->dev, (N + 1) * 4, &cnt) || alloc_buf(r->dev, N * 4, &d0) ||
+      alloc_buf(r->dev, N * 4, &parent) || alloc_buf(r->dev, N * 32, &cs) ||
+      alloc_buf(r->dev, (N + 1) * 4, &is4) ||
+      alloc_buf(r->dev, ctl0.size() * 4, &ctl, ctl0.data()) ||
+      alloc_buf(r->dev, sizeof(sah_arg_t), &argb))
+    return -1;
+  sah_arg_t a;
+  std::memset(&a, 0, sizeof(a));
+  a.verts_addr = vb.addr;
+  a.geom_addr = r->arg.geom_addr;
+  a.tbox_addr = tbox.addr;
+  a.cen_addr = cen.addr;
+  a.idx_addr[0] = idx[0].addr;
+  a.idx_addr[1] = idx[1].addr;
+  a.final_addr = fin.addr;
+  a.segs_addr[0] = segs[0].addr;
+  a.segs_addr[1] = segs[1].addr;
+  a.nrec_addr = nrec.addr;
+  a.nbox_addr = nbox.addr;
+  a.cnt_addr = cnt.addr;
+  a.d0_addr = d0.addr;
+  a.parent_addr = parent.addr;
+  a.cs_addr = cs.addr;
+  a.is4_addr = is4.addr;
+  a.ctl_addr = ctl.addr;
+  a.n = n;
+  double kernel_ms = 0.0;
+  uint32_t launches = 0;
+  auto launch = [&](uint32_t phase) -> int {
+    a.phase = phase;
+    if (vx_copy_to_dev(argb.h, &a, 0, sizeof(a)) != 0) return fail("vx_copy_to_dev failed");
+    if (vx_start(r->dev, krnl, argb.h) != 0) return fail("vx_start failed");
+    if (vx_ready_wait(r->dev, VX_MAX_TIMEOUT) != 0) return fail("vx_ready_wait failed");
+    double ms = 0.0;
+    uint32_t g = 0, b = 0;
+    if (r->last_run && r->last_run(r->dev, &ms, &g, &b) == 0) kernel_ms += ms;
+    ++launches;
+    return 0;
+  };
+  uint32_t c[SAH_CTL_WORDS];
+  auto read_ctl = [&]() -> int {
+    return vx_copy_from_dev(c, ctl.h, 0, sizeof(c)) == 0 ? 0 : fail("vx_copy_from_dev failed");
+  };
+  if (launch(SAH_INIT)) return -1;
+  // one launch per tree level, until a level creates no internal node
+  for (uint32_t L = 0;; ++L) {
+    if (L + 1 >= SAH_MAX_LEVELS) return fail("SAH build deeper than its level table");
+    a.level = L;
+    if (launch(SAH_SPLIT) || read_ctl()) return -1;
+    if (c[SAH_CTL_ERR]) return fail("SAH build overflowed its node / segment capacity");
+    if (c[SAH_CTL_SEG + L + 1] == 0) break;
+  }
+  const uint32_t nn = c[SAH_CTL_NODES], depth = c[SAH_CTL_DEPTH];
+  if (depth > RT_STACK_DEEP) return fail("BVH deeper than RT_STACK_DEEP");
+  vx_buffer_h nodes_h = nullptr, tris_h = nullptr, nodes4_h = nullptr;
+  uint64_t nodes_addr = 0, tris_addr = 0, nodes4_addr = 0;
+  DevBuf nodes_out, tris_out, nodes4_out;  // owned here until handed to the renderer
+  if (upload(r->dev, nullptr, (uint64_t)nn * sizeof(rt_node_t), &nodes_h, &nodes_addr)) return -1;
+  nodes_out.h = nodes_h;
+  if (upload(r->dev, nullptr, (N + 3) * sizeof(rt_tri_t), &tris_h, &tris_addr)) return -1;
+  tris_out.h = tris_h;
+  a.nodes_addr = nodes_addr;
+  a.tris_addr = tris_addr;
+  a.nn = nn;
+  a.scan_addr = cnt.addr;
+  a.scan_count = n;
+  if (launch(SAH_NUMBER) || launch(SAH_SCAN) || launch(SAH_EMIT) || launch(SAH_CS) ||
+      launch(SAH_MARK))
+    return -1;
+  a.scan_addr = is4.addr;
+  a.scan_count = nn;
+  if (launch(SAH_SCAN)) return -1;
+  uint32_t nn4 = 0;
+  if (vx_copy_from_dev(&nn4, is4.h, (uint64_t)nn * 4, 4) != 0) return fail("vx_copy_from_dev failed");
+  if (upload(r->dev, nullptr, (uint64_t)nn4 * (sizeof(rt_node4_t) + sizeof(rt_node4h_t)), &nodes4_h,
+             &nodes4_addr))
+    return -1;
+  nodes4_out.h = nodes4_h;
+  a.nodes4_addr = nodes4_addr;
+  a.nn4 = nn4;
+  if (launch(SAH_EMIT4) || launch(SAH_HALF) || read_ctl()) return -1;
+  if (c[SAH_CTL_ERR]) return fail("SAH build: BVH4 walk deeper than its path table");
+  const uint32_t stack4 = c[SAH_CTL_STACK4];
+  const bool use4 = stack4 <= RT_STACK_DEEP;
+  if (std::max(depth, use4 ? stack4 : 0u) > RT_STACK_SHALLOW && !r->deep && load_deep_images(r) != 0)
+    return -1;
+  if (r->nodes) vx_mem_free(r->nodes);
+  if (r->tris) vx_mem_free(r->tris);
+  if (r->nodes4) vx_mem_free(r->nodes4);
+  r->nodes = nodes_out.h;
+  r->tris = tris_out.h;
+  r->nodes4 = nodes4_out.h;
+  nodes_out.h = tris_out.h = nodes4_out.h = nullptr;
+  r->arg.nodes_addr = nodes_addr;
+  r->arg.tris_addr = tris_addr;
+  r->arg.num_nodes = nn;
+  r->arg.nodes4_addr = nodes4_addr;
+  r->arg.num_nodes4 = nn4;
+  r->num_tris = n;
+  r->gpu_bvh = true;
+  r->gpu_bvh4 = use4;
+  if (st) {
+    std::memset(st, 0, sizeof(*st));
+    st->nodes = nn;
+    st->depth = depth;
+    st->stack4 = use4 ? stack4 : RT_BVH_STACK4_UNUSED;
+    st->launches = launches;
+    st->kernel_ms = kernel_ms;
+    st->build_ms = ms_since(t0);
+    st->nodes4 = nn4;
+    st->depth4 = c[SAH_CTL_DEPTH4];
+    st->method = RT_BVH_BUILD_SAH;
+  }
+  if (r->configured) {
+    const rt_render_params_t p = r->params;
+    return rt_renderer_configure(r, &p);
+  }
+  return 0;
+}
+
+int rt_renderer_build_bvh_ex(rt_renderer_h r, uint32_t method, rt_bvh_build_stats_t* st) {
+  if (!r) return fail("null argument");
+  if (r->sc->geometry.empty()) return fail("no depth-tested geometry to build a BVH over");
+  if (method == RT_BVH_BUILD_SAH) return build_sah(r, st);
+  if (method != RT_BVH_BUILD_LBVH) return fail("unknown BVH build method");
+  return build_lbvh(r, st);
+}
+
+int rt_renderer_build_bvh(rt_renderer_h r, rt_bvh_build_stats_t* st) {
+  return rt_renderer_build_bvh_ex(r, RT_BVH_BUILD_LBVH, st);
 }
 
 int rt_renderer_export_bvh4(rt_renderer_h r, float* nodes4, uint32_t* num_nodes4) {

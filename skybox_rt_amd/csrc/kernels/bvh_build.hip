@@ -13,6 +13,7 @@
 #include <hip/hip_runtime.h>
 
 #include "bvh_common.h"
+#include "half4.h"
 #include "rt_common.h"
 #include "vx_spawn.h"
 
@@ -520,58 +521,13 @@ __device__ void phase_collapse(const bvh_build_arg_t* a) {
   if (lane() == 0 && maxstack) atomicMax(&bounds[8], maxstack);
 }
 
-// Binary16 box planes for the device tree (app/bvh.cpp HalfRound /
-// HalfBits, restated by oracle/lbvh.c orc_half4): each plane rounded
-// outward to a binary16 value by exact scaling with its binade's quantum,
-// floor (lower planes) or ceil (upper planes), saturating outward past
-// +-65504 -- so a rounded box contains the original and the slab test
-// accepts every ray the original accepted; the fp32 node keeps the rounded
-// values (both layouts describe one tree) and the 64-B half record goes
-// behind the rt_node4_t array, where the kernels' F16 node step reads it.
-__device__ float half_round(float x, int dir) {
-  if (__builtin_isnan(x) || __builtin_isinf(x) || x == 0.0f) return x;
-  const float kmax = 65504.0f;
-  if (x > kmax) return dir < 0 ? kmax : INFINITY;
-  if (x < -kmax) return dir < 0 ? -INFINITY : -kmax;
-  int e;
-  frexpf(fabsf(x), &e);
-  const int q = (e - 1 > -14 ? e - 1 : -14) - 10;
-  const float m = ldexpf(x, -q);
-  const float r = dir < 0 ? floorf(m) : ceilf(m);
-  const float v = ldexpf(r, q);
-  return v > kmax ? INFINITY : (v < -kmax ? -INFINITY : v);
-}
-
-__device__ uint32_t half_bits(float v) {
-  const uint32_t u = __float_as_uint(v);
-  const uint32_t sign = (u >> 16) & 0x8000u;
-  const float a = fabsf(v);
-  if (a == 0.0f) return sign;
-  if (__builtin_isinf(a)) return sign | 0x7c00u;
-  int e;
-  const float m = frexpf(a, &e);
-  if (e - 1 >= -14) return sign | ((uint32_t)(e - 1 + 15) << 10) | (uint32_t)ldexpf(2.0f * m - 1.0f, 10);
-  return sign | (uint32_t)ldexpf(a, 24);
-}
-
 __device__ void phase_half(const bvh_build_arg_t* a) {
   const int n = (int)a->n, nn = n > 1 ? n - 1 : 1;
   rt_node4_t* nodes4 = vx_ptr<rt_node4_t>(a->nodes4_addr);
   uint32_t* half = vx_ptr<uint32_t>(a->nodes4_addr + 128ull * (uint64_t)nn);
   const int gid = blockIdx.x * BVHB_BLOCK + threadIdx.x, gstride = gridDim.x * BVHB_BLOCK;
   for (int i = gid; i < nn; i += gstride) {
-    float* v = nodes4[i].v;
-    uint32_t* h = half + 16 * i;
-#pragma unroll
-    for (int k = 0; k < 24; k += 2) {
-      const float r0 = half_round(v[k], (k & 4) ? 1 : -1);
-      const float r1 = half_round(v[k + 1], ((k + 1) & 4) ? 1 : -1);
-      v[k] = r0;
-      v[k + 1] = r1;
-      h[k / 2] = half_bits(r0) | (half_bits(r1) << 16);
-    }
-#pragma unroll
-    for (int q = 0; q < 4; ++q) h[12 + q] = __float_as_uint(v[24 + q]);
+    half4_node(nodes4[i].v, half + 16 * i);
   }
 }
 

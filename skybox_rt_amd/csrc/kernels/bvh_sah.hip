@@ -1,0 +1,611 @@
+// bvh_sah.hip -- GPU binned-SAH BVH build that reproduces the host builder
+// (app/bvh.cpp Builder + Collapser + binary16 planes) bit for bit; the
+// phases and the argument block are described in sah_common.h.  Float
+// arithmetic follows the host operation for operation (fp32 without
+// contraction, the SAH cost in double, x86 float -> int conversion), and
+// every reduction is a min / max / count, so no result depends on the
+// order the GPU performs it in.
+#include <hip/hip_runtime.h>
+
+#include "half4.h"
+#include "rt_common.h"
+#include "sah_common.h"
+#include "vx_spawn.h"
+
+namespace {
+
+constexpr uint32_t kWaves = SAH_BLOCK / 64;
+
+__device__ __forceinline__ uint32_t lane_id() {
+  return __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
+}
+
+// float <-> uint preserving the float order (min / max as integer atomics)
+__device__ __forceinline__ uint32_t ord(float f) {
+  const uint32_t b = __float_as_uint(f);
+  return (b & 0x80000000u) ? ~b : (b | 0x80000000u);
+}
+__device__ __forceinline__ float unord(uint32_t u) {
+  return __uint_as_float((u & 0x80000000u) ? (u & 0x7fffffffu) : ~u);
+}
+
+// (int)x as the host's x86 build computes it (cvttss2si)
+__device__ __forceinline__ int cvt_x86(float x) {
+  if (!(x >= -2147483648.0f && x < 2147483648.0f)) return INT32_MIN;
+  return (int)x;
+}
+
+__device__ __forceinline__ float comp(const float4& v, int k) { return k == 0 ? v.x : (k == 1 ? v.y : v.z); }
+
+struct Box {  // app/bvh.cpp Box
+  float lo[3], hi[3];
+  __device__ void empty() {
+    for (int k = 0; k < 3; ++k) {
+      lo[k] = INFINITY;
+      hi[k] = -INFINITY;
+    }
+  }
+  __device__ void grow(const Box& b) {
+    for (int k = 0; k < 3; ++k) {
+      lo[k] = fminf(lo[k], b.lo[k]);
+      hi[k] = fmaxf(hi[k], b.hi[k]);
+    }
+  }
+  __device__ double area() const {  // g_wside = 1 (the default; 1.0 * x == x)
+    if (lo[0] > hi[0]) return 0.0;
+    const double dx = (double)hi[0] - lo[0], dy = (double)hi[1] - lo[1], dz = (double)hi[2] - lo[2];
+    return 2.0 * (dx * dy + (dy * dz + dz * dx));
+  }
+};
+
+__device__ __forceinline__ float scene_pad(const uint32_t* ctl) {
+  const float ext = __uint_as_float(ctl[SAH_CTL_EXT]);
+  return fmaxf(ext * (1.0f / 65536.0f), 1e-6f);
+}
+
+// ---- SAH_INIT --------------------------------------------------------------
+__device__ void phase_init(const sah_arg_t* a) {
+  const float4* v = vx_ptr<const float4>(a->verts_addr);
+  float4* tbox = vx_ptr<float4>(a->tbox_addr);
+  float4* cen = vx_ptr<float4>(a->cen_addr);
+  uint32_t* idx = vx_ptr<uint32_t>(a->idx_addr[0]);
+  uint32_t* cnt = vx_ptr<uint32_t>(a->cnt_addr);
+  uint32_t* d0 = vx_ptr<uint32_t>(a->d0_addr);
+  uint32_t* ctl = vx_ptr<uint32_t>(a->ctl_addr);
+  const uint32_t n = a->n;
+  float ext = 0.0f;
+  for (uint32_t i = blockIdx.x * SAH_BLOCK + threadIdx.x; i <= n; i += gridDim.x * SAH_BLOCK) {
+    cnt[i] = 0;
+    if (i == n) break;
+    d0[i] = 0xffffffffu;
+    idx[i] = i;
+    const float4 p0 = v[3 * i], p1 = v[3 * i + 1], p2 = v[3 * i + 2];
+    const float4 lo = make_float4(fminf(fminf(p0.x, p1.x), p2.x), fminf(fminf(p0.y, p1.y), p2.y),
+                                  fminf(fminf(p0.z, p1.z), p2.z), 0.0f);
+    const float4 hi = make_float4(fmaxf(fmaxf(p0.x, p1.x), p2.x), fmaxf(fmaxf(p0.y, p1.y), p2.y),
+                                  fmaxf(fmaxf(p0.z, p1.z), p2.z), 0.0f);
+    tbox[2 * i] = lo;
+    tbox[2 * i + 1] = hi;
+    cen[i] = make_float4((lo.x + hi.x) * 0.5f, (lo.y + hi.y) * 0.5f, (lo.z + hi.z) * 0.5f, 0.0f);
+    ext = fmaxf(ext, fmaxf(fmaxf(fabsf(p0.x), fabsf(p0.y)), fabsf(p0.z)));
+    ext = fmaxf(ext, fmaxf(fmaxf(fabsf(p1.x), fabsf(p1.y)), fabsf(p1.z)));
+    ext = fmaxf(ext, fmaxf(fmaxf(fabsf(p2.x), fabsf(p2.y)), fabsf(p2.z)));
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) ext = fmaxf(ext, __shfl_xor(ext, o, 64));
+  if (lane_id() == 0 && ext > 0.0f) atomicMax(&ctl[SAH_CTL_EXT], __float_as_uint(ext));
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    sah_seg_t* s0 = vx_ptr<sah_seg_t>(a->segs_addr[0]);
+    s0[0] = sah_seg_t{0, n, 0, 1};
+    ctl[SAH_CTL_SEG + 0] = 1;
+    ctl[SAH_CTL_NODES] = 1;
+    ctl[SAH_CTL_DEPTH] = 1;
+  }
+}
+
+// ---- SAH_SPLIT: one workgroup per segment of level `level` -----------------
+struct SplitLds {
+  uint32_t cb[6];                       // centroid bounds (ordered uints)
+  uint32_t bin[3][SAH_BINS][7];         // lo xyz, hi xyz (ordered), count
+  uint32_t side[2][6];                  // child boxes by reduction (median / root)
+  float box[2][6];                      // child boxes (lo xyz, hi xyz)
+  int axis;
+  uint32_t s, nl;
+  uint32_t wl[kWaves], wr[kWaves], lbase, rbase;
+};
+
+__device__ __forceinline__ int bin_of(float c, float cl, float ext) {
+  const int bi = cvt_x86((c - cl) * ((float)SAH_BINS / ext));
+  return min(max(bi, 0), SAH_BINS - 1);
+}
+
+__device__ void phase_split(const sah_arg_t* a) {
+  const uint32_t L = a->level;
+  uint32_t* ctl = vx_ptr<uint32_t>(a->ctl_addr);
+  const uint32_t nseg = ctl[SAH_CTL_SEG + L];
+  const sah_seg_t* segs = vx_ptr<const sah_seg_t>(a->segs_addr[L & 1]);
+  sah_seg_t* next = vx_ptr<sah_seg_t>(a->segs_addr[(L + 1) & 1]);
+  const uint32_t* idx = vx_ptr<const uint32_t>(a->idx_addr[L & 1]);
+  uint32_t* out = vx_ptr<uint32_t>(a->idx_addr[(L + 1) & 1]);
+  uint32_t* fin = vx_ptr<uint32_t>(a->final_addr);
+  const float4* cen = vx_ptr<const float4>(a->cen_addr);
+  const float4* tbox = vx_ptr<const float4>(a->tbox_addr);
+  uint4* nrec = vx_ptr<uint4>(a->nrec_addr);
+  float4* nbox = vx_ptr<float4>(a->nbox_addr);
+  __shared__ SplitLds S;
+  const uint32_t tid = threadIdx.x, w = tid >> 6, l = lane_id();
+  const uint64_t lt = (l == 0) ? 0ull : (~0ull >> (64 - l));
+  for (uint32_t si = blockIdx.x; si < nseg; si += gridDim.x) {
+    const sah_seg_t sg = segs[si];
+    const uint32_t b = sg.b, e = sg.e, n = e - b;
+    // 1. centroid bounds
+    if (tid < 6) S.cb[tid] = tid < 3 ? ord(INFINITY) : ord(-INFINITY);
+    for (uint32_t k = tid; k < 3 * SAH_BINS * 7; k += SAH_BLOCK) {
+      const uint32_t f = k % 7;
+      (&S.bin[0][0][0])[k] = f < 3 ? ord(INFINITY) : (f < 6 ? ord(-INFINITY) : 0u);
+    }
+    if (tid < 12) (&S.side[0][0])[tid] = (tid % 6) < 3 ? ord(INFINITY) : ord(-INFINITY);
+    if (tid == 0) {
+      S.lbase = S.rbase = 0;
+      S.axis = -1;
+    }
+    __syncthreads();
+    float cl[3] = {INFINITY, INFINITY, INFINITY}, ch[3] = {-INFINITY, -INFINITY, -INFINITY};
+    for (uint32_t i = b + tid; i < e; i += SAH_BLOCK) {
+      const float4 c = cen[idx[i]];
+      cl[0] = fminf(cl[0], c.x); cl[1] = fminf(cl[1], c.y); cl[2] = fminf(cl[2], c.z);
+      ch[0] = fmaxf(ch[0], c.x); ch[1] = fmaxf(ch[1], c.y); ch[2] = fmaxf(ch[2], c.z);
+    }
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) {
+        cl[k] = fminf(cl[k], __shfl_xor(cl[k], o, 64));
+        ch[k] = fmaxf(ch[k], __shfl_xor(ch[k], o, 64));
+      }
+    }
+    if (l == 0)
+      for (int k = 0; k < 3; ++k) {
+        atomicMin(&S.cb[k], ord(cl[k]));
+        atomicMax(&S.cb[3 + k], ord(ch[k]));
+      }
+    __syncthreads();
+    for (int k = 0; k < 3; ++k) {
+      cl[k] = unord(S.cb[k]);
+      ch[k] = unord(S.cb[3 + k]);
+    }
+    const bool split_node = n > SAH_LEAF;
+    // 2. bins over every axis with extent (app/bvh.cpp split)
+    if (split_node)
+      for (uint32_t i = b + tid; i < e; i += SAH_BLOCK) {
+        const uint32_t t = idx[i];
+        const float4 c = cen[t], lo = tbox[2 * t], hi = tbox[2 * t + 1];
+        for (int ax = 0; ax < 3; ++ax) {
+          const float ext = ch[ax] - cl[ax];
+          if (!(ext > 0.0f)) continue;
+          uint32_t* bn = S.bin[ax][bin_of(comp(c, ax), cl[ax], ext)];
+          atomicMin(&bn[0], ord(lo.x)); atomicMin(&bn[1], ord(lo.y)); atomicMin(&bn[2], ord(lo.z));
+          atomicMax(&bn[3], ord(hi.x)); atomicMax(&bn[4], ord(hi.y)); atomicMax(&bn[5], ord(hi.z));
+          atomicAdd(&bn[6], 1u);
+        }
+      }
+    __syncthreads();
+    // 3. the SAH decision, in the host's order (one thread)
+    if (tid == 0 && split_node) {
+      double best = INFINITY;
+      for (int ax = 0; ax < 3; ++ax) {
+        if (!(ch[ax] - cl[ax] > 0.0f)) continue;
+        Box bb[SAH_BINS], rs[SAH_BINS];
+        uint32_t cnt[SAH_BINS], rc[SAH_BINS];
+        for (int q = 0; q < SAH_BINS; ++q) {
+          for (int k = 0; k < 3; ++k) {
+            bb[q].lo[k] = unord(S.bin[ax][q][k]);
+            bb[q].hi[k] = unord(S.bin[ax][q][3 + k]);
+          }
+          cnt[q] = S.bin[ax][q][6];
+        }
+        Box acc;
+        acc.empty();
+        uint32_t na = 0;
+        for (int q = SAH_BINS - 1; q >= 1; --q) {
+          acc.grow(bb[q]);
+          na += cnt[q];
+          rs[q] = acc;
+          rc[q] = na;
+        }
+        Box lb;
+        lb.empty();
+        uint32_t nl = 0;
+        for (int q = 1; q < SAH_BINS; ++q) {
+          lb.grow(bb[q - 1]);
+          nl += cnt[q - 1];
+          if (nl == 0 || rc[q] == 0) continue;
+          const double c = (double)nl * lb.area() + (double)rc[q] * rs[q].area();
+          if (c < best) {
+            best = c;
+            S.axis = ax;
+            S.s = (uint32_t)q;
+            S.nl = nl;
+            for (int k = 0; k < 3; ++k) {
+              S.box[0][k] = lb.lo[k]; S.box[0][3 + k] = lb.hi[k];
+              S.box[1][k] = rs[q].lo[k]; S.box[1][3 + k] = rs[q].hi[k];
+            }
+          }
+        }
+      }
+    }
+    __syncthreads();
+    const int axis = S.axis;
+    // the root of <= 4 triangles: one leaf child and an empty one; no SAH
+    // split: the median, order unchanged
+    const uint32_t nl = !split_node ? n : (axis >= 0 ? S.nl : n / 2);
+    if (axis < 0) {  // child boxes by reduction over the two halves
+      float bl[2][6];
+      for (int q = 0; q < 2; ++q)
+        for (int k = 0; k < 3; ++k) {
+          bl[q][k] = INFINITY;
+          bl[q][3 + k] = -INFINITY;
+        }
+      for (uint32_t i = b + tid; i < e; i += SAH_BLOCK) {
+        const uint32_t t = idx[i];
+        const int q = i < b + nl ? 0 : 1;
+        const float4 lo = tbox[2 * t], hi = tbox[2 * t + 1];
+        for (int k = 0; k < 3; ++k) {
+          bl[q][k] = fminf(bl[q][k], comp(lo, k));
+          bl[q][3 + k] = fmaxf(bl[q][3 + k], comp(hi, k));
+        }
+      }
+      for (int q = 0; q < 2; ++q)
+        for (int k = 0; k < 6; ++k) {
+          float x = bl[q][k];
+#pragma unroll
+          for (int o = 32; o > 0; o >>= 1)
+            x = k < 3 ? fminf(x, __shfl_xor(x, o, 64)) : fmaxf(x, __shfl_xor(x, o, 64));
+          if (l == 0) {
+            if (k < 3) atomicMin(&S.side[q][k], ord(x));
+            else atomicMax(&S.side[q][k], ord(x));
+          }
+        }
+      __syncthreads();
+      if (tid < 12) (&S.box[0][0])[tid] = unord((&S.side[0][0])[tid]);
+    }
+    __syncthreads();
+    const bool leaf0 = nl <= SAH_LEAF, leaf1 = n - nl <= SAH_LEAF;
+    // 4. the children's triangle order: a stable partition by the split bin
+    //    (ballot ranks, rounds of SAH_BLOCK in order), else a copy; leaf
+    //    ranges also go to the final order
+    if (axis >= 0) {
+      const float ext = ch[axis] - cl[axis];
+      for (uint32_t r0 = b; r0 < e; r0 += SAH_BLOCK) {
+        const uint32_t i = r0 + tid;
+        const bool valid = i < e;
+        const uint32_t t = valid ? idx[i] : 0u;
+        const bool f = valid && (uint32_t)bin_of(comp(cen[t], axis), cl[axis], ext) < S.s;
+        const bool g = valid && !f;
+        const uint64_t mL = __ballot(f), mR = __ballot(g);
+        if (l == 0) {
+          S.wl[w] = (uint32_t)__popcll(mL);
+          S.wr[w] = (uint32_t)__popcll(mR);
+        }
+        __syncthreads();
+        uint32_t offL = S.lbase, offR = S.rbase;
+        for (uint32_t k = 0; k < w; ++k) {
+          offL += S.wl[k];
+          offR += S.wr[k];
+        }
+        if (valid) {
+          const uint32_t dst = f ? b + offL + (uint32_t)__popcll(mL & lt)
+                                 : b + nl + offR + (uint32_t)__popcll(mR & lt);
+          out[dst] = t;
+          if (f ? leaf0 : leaf1) fin[dst] = t;
+        }
+        __syncthreads();
+        if (tid == 0)
+          for (uint32_t k = 0; k < kWaves; ++k) {
+            S.lbase += S.wl[k];
+            S.rbase += S.wr[k];
+          }
+        __syncthreads();
+      }
+    } else {
+      for (uint32_t i = b + tid; i < e; i += SAH_BLOCK) {
+        const uint32_t t = idx[i];
+        out[i] = t;
+        if (i < b + nl ? leaf0 : leaf1) fin[i] = t;
+      }
+    }
+    // 5. the node record and the next level's segments
+    if (tid == 0) {
+      int32_t ref[2];
+      const uint32_t cb[2] = {b, b + nl}, ce[2] = {b + nl, e};
+      for (int q = 0; q < 2; ++q) {
+        const uint32_t m = ce[q] - cb[q];
+        if (m == 0) {
+          ref[q] = RT_EMPTY_REF;  // only the small root's second child
+        } else if (m <= SAH_LEAF) {
+          ref[q] = (int32_t)(RT_LEAF_FLAG | (cb[q] << 4) | (m - 1));
+        } else {
+          const uint32_t id = atomicAdd(&ctl[SAH_CTL_NODES], 1u);
+          const uint32_t slot = atomicAdd(&ctl[SAH_CTL_SEG + L + 1], 1u);
+          if (id >= a->n || slot >= a->n || L + 2 >= SAH_MAX_LEVELS) {
+            atomicOr(&ctl[SAH_CTL_ERR], 1u);
+            ref[q] = RT_EMPTY_REF;
+            continue;
+          }
+          next[slot] = sah_seg_t{cb[q], ce[q], id, sg.depth + 1};
+          atomicMax(&ctl[SAH_CTL_DEPTH], sg.depth + 1);
+          ref[q] = (int32_t)id;
+        }
+      }
+      nrec[sg.node] = make_uint4(b, sg.depth, (uint32_t)ref[0], (uint32_t)ref[1]);
+      float4* nb = nbox + 4 * sg.node;
+      nb[0] = make_float4(S.box[0][0], S.box[0][1], S.box[0][2], 0.0f);
+      nb[1] = make_float4(S.box[0][3], S.box[0][4], S.box[0][5], 0.0f);
+      nb[2] = make_float4(S.box[1][0], S.box[1][1], S.box[1][2], 0.0f);
+      nb[3] = make_float4(S.box[1][3], S.box[1][4], S.box[1][5], 0.0f);
+    }
+    __syncthreads();
+  }
+}
+
+// ---- preorder numbering ------------------------------------------------------
+__device__ void phase_number(const sah_arg_t* a) {
+  const uint4* nrec = vx_ptr<const uint4>(a->nrec_addr);
+  uint32_t* cnt = vx_ptr<uint32_t>(a->cnt_addr);
+  uint32_t* d0 = vx_ptr<uint32_t>(a->d0_addr);
+  const uint32_t nodes = vx_ptr<const uint32_t>(a->ctl_addr)[SAH_CTL_NODES];
+  for (uint32_t x = blockIdx.x * SAH_BLOCK + threadIdx.x; x < nodes; x += gridDim.x * SAH_BLOCK) {
+    const uint4 r = nrec[x];
+    atomicAdd(&cnt[r.x], 1u);
+    atomicMin(&d0[r.x], r.y);
+  }
+}
+
+// exclusive scan of u32 [scan_count] in place, total at [scan_count]
+// (workgroup 0: contiguous chunks per thread, a workgroup scan of the chunk sums)
+__device__ void phase_scan(const sah_arg_t* a) {
+  if (blockIdx.x != 0) return;
+  uint32_t* x = vx_ptr<uint32_t>(a->scan_addr);
+  __shared__ uint32_t s[SAH_BLOCK];
+  const uint32_t total = a->scan_count;
+  const uint32_t chunk = (total + SAH_BLOCK - 1) / SAH_BLOCK;
+  const uint32_t b0 = min(threadIdx.x * chunk, total), b1 = min(b0 + chunk, total);
+  uint32_t sum = 0;
+  for (uint32_t i = b0; i < b1; ++i) sum += x[i];
+  s[threadIdx.x] = sum;
+  __syncthreads();
+  for (uint32_t o = 1; o < SAH_BLOCK; o <<= 1) {
+    const uint32_t y = threadIdx.x >= o ? s[threadIdx.x - o] : 0u;
+    __syncthreads();
+    s[threadIdx.x] += y;
+    __syncthreads();
+  }
+  uint32_t run = s[threadIdx.x] - sum;
+  for (uint32_t i = b0; i < b1; ++i) {
+    const uint32_t v = x[i];
+    x[i] = run;
+    run += v;
+  }
+  if (threadIdx.x == SAH_BLOCK - 1) x[total] = s[SAH_BLOCK - 1];
+}
+
+// preorder index of BFS node x: its rank in (first position, depth) order
+__device__ __forceinline__ uint32_t pre_of(const uint4* nrec, const uint32_t* P, const uint32_t* d0,
+                                           uint32_t x) {
+  const uint4 r = nrec[x];
+  return P[r.x] + r.y - d0[r.x];
+}
+
+__device__ void phase_emit(const sah_arg_t* a) {
+  const uint4* nrec = vx_ptr<const uint4>(a->nrec_addr);
+  const float4* nbox = vx_ptr<const float4>(a->nbox_addr);
+  const uint32_t* P = vx_ptr<const uint32_t>(a->cnt_addr);
+  const uint32_t* d0 = vx_ptr<const uint32_t>(a->d0_addr);
+  const uint32_t* ctl = vx_ptr<const uint32_t>(a->ctl_addr);
+  int32_t* parent = vx_ptr<int32_t>(a->parent_addr);
+  float4* nodes = vx_ptr<float4>(a->nodes_addr);
+  const uint32_t nodes_n = ctl[SAH_CTL_NODES];
+  const float pad = scene_pad(ctl);
+  const uint32_t gid = blockIdx.x * SAH_BLOCK + threadIdx.x, gs = gridDim.x * SAH_BLOCK;
+  for (uint32_t x = gid; x < nodes_n; x += gs) {
+    const uint4 r = nrec[x];
+    const uint32_t px = pre_of(nrec, P, d0, x);
+    if (x == 0) parent[px] = -1;
+    int32_t ref[2] = {(int32_t)r.z, (int32_t)r.w};
+    float v[16];
+    for (int q = 0; q < 2; ++q) {
+      const bool empty = ref[q] == RT_EMPTY_REF;
+      const float4 lo = nbox[4 * x + 2 * q], hi = nbox[4 * x + 2 * q + 1];
+      for (int k = 0; k < 3; ++k) {
+        v[4 * k + 2 * q + 0] = empty ? 0.0f : comp(lo, k) - pad;
+        v[4 * k + 2 * q + 1] = empty ? 0.0f : comp(hi, k) + pad;
+      }
+      if (ref[q] >= 0) {
+        const uint32_t py = pre_of(nrec, P, d0, (uint32_t)ref[q]);
+        parent[py] = (int32_t)px;
+        ref[q] = (int32_t)py;
+      }
+      v[12 + q] = __int_as_float(ref[q]);
+    }
+    v[14] = v[15] = 0.0f;
+    float4* o = nodes + 4 * px;
+    for (int q = 0; q < 4; ++q) o[q] = make_float4(v[4 * q], v[4 * q + 1], v[4 * q + 2], v[4 * q + 3]);
+  }
+  // triangle records in leaf order (+3 zero padding records)
+  const uint32_t* fin = vx_ptr<const uint32_t>(a->final_addr);
+  const float4* geom = vx_ptr<const float4>(a->geom_addr);
+  float4* tris = vx_ptr<float4>(a->tris_addr);
+  for (uint32_t i = gid; i < a->n + 3; i += gs) {
+    const bool pad_rec = i >= a->n;
+    const uint32_t t = pad_rec ? 0u : fin[i];
+    for (int q = 0; q < 3; ++q) tris[3 * i + q] = pad_rec ? make_float4(0, 0, 0, 0) : geom[3 * t + q];
+  }
+}
+
+// ---- BVH4 collapse (app/bvh.cpp Collapser) ---------------------------------
+struct Child {
+  float lo[3], hi[3];
+  int32_t ref, src;  // src = BVH2 node << 1 | slot holding the box
+};
+
+__device__ __forceinline__ Child child_of(const float* nodes, uint32_t p, int ch) {
+  const float* v = nodes + 16ull * p;
+  Child c;
+  for (int k = 0; k < 3; ++k) {
+    c.lo[k] = v[4 * k + 2 * ch];
+    c.hi[k] = v[4 * k + 2 * ch + 1];
+  }
+  c.ref = __float_as_int(v[12 + ch]);
+  c.src = (int32_t)(2 * p + ch);
+  return c;
+}
+
+__device__ __forceinline__ double child_area(const Child& c) {
+  const double dx = (double)c.hi[0] - c.lo[0], dy = (double)c.hi[1] - c.lo[1],
+               dz = (double)c.hi[2] - c.lo[2];
+  return 2.0 * (dx * dy + dy * dz + dz * dx);
+}
+
+__device__ void phase_cs(const sah_arg_t* a) {
+  const float* nodes = vx_ptr<const float>(a->nodes_addr);
+  int32_t* cs = vx_ptr<int32_t>(a->cs_addr);
+  for (uint32_t p = blockIdx.x * SAH_BLOCK + threadIdx.x; p < a->nn; p += gridDim.x * SAH_BLOCK) {
+    Child c[4];
+    int m = 0;
+    for (int ch = 0; ch < 2; ++ch) {
+      const Child x = child_of(nodes, p, ch);
+      if (x.ref != RT_EMPTY_REF) c[m++] = x;
+    }
+    while (m < 4) {
+      int best = -1;
+      double ba = -1.0;
+      for (int i = 0; i < m; ++i)
+        if (c[i].ref >= 0 && child_area(c[i]) > ba) {
+          ba = child_area(c[i]);
+          best = i;
+        }
+      if (best < 0) break;
+      const uint32_t q = (uint32_t)c[best].ref;
+      Child sub[2];
+      int ns = 0;
+      for (int ch = 0; ch < 2; ++ch) {
+        const Child x = child_of(nodes, q, ch);
+        if (x.ref != RT_EMPTY_REF) sub[ns++] = x;
+      }
+      // erase c[best], insert sub there (m - 1 + ns <= 4)
+      Child t[4];
+      int k = 0;
+      for (int i = 0; i < best; ++i) t[k++] = c[i];
+      for (int i = 0; i < ns; ++i) t[k++] = sub[i];
+      for (int i = best + 1; i < m; ++i) t[k++] = c[i];
+      for (int i = 0; i < k; ++i) c[i] = t[i];
+      m = k;
+    }
+    int32_t* o = cs + 8ull * p;
+    for (int i = 0; i < 4; ++i) {
+      o[i] = i < m ? c[i].ref : RT_EMPTY_REF;
+      o[4 + i] = i < m ? c[i].src : -1;
+    }
+  }
+}
+
+// BVH4 membership: walk the node's root path down, following the BVH4 node
+// whose expansion the path is in; depth and the worst-case stack (the sum of
+// (children - 1) over the BVH4 nodes of the path) of every BVH4 node
+__device__ void phase_mark(const sah_arg_t* a) {
+  const int32_t* parent = vx_ptr<const int32_t>(a->parent_addr);
+  const int32_t* cs = vx_ptr<const int32_t>(a->cs_addr);
+  uint32_t* is4 = vx_ptr<uint32_t>(a->is4_addr);
+  uint32_t* ctl = vx_ptr<uint32_t>(a->ctl_addr);
+  for (uint32_t m = blockIdx.x * SAH_BLOCK + threadIdx.x; m < a->nn; m += gridDim.x * SAH_BLOCK) {
+    int32_t path[SAH_MAX_LEVELS];
+    int len = 0;
+    int32_t x = (int32_t)m;
+    while (x >= 0 && len < SAH_MAX_LEVELS) {
+      path[len++] = x;
+      x = parent[x];
+    }
+    if (x >= 0) {
+      atomicOr(&ctl[SAH_CTL_ERR], 2u);
+      is4[m] = 0;
+      continue;
+    }
+    auto nch = [&](int32_t p) {
+      int k = 0;
+      while (k < 4 && cs[8 * p + k] != RT_EMPTY_REF) ++k;
+      return (uint32_t)k;
+    };
+    int32_t cur = path[len - 1];  // the root
+    uint32_t depth4 = 1, stack = nch(cur) > 0 ? nch(cur) - 1 : 0;
+    bool member = len == 1;
+    for (int k = len - 2; k >= 0; --k) {
+      const int32_t p = path[k];
+      bool in = false;
+      for (int i = 0; i < 4; ++i) in |= cs[8 * cur + i] == p;
+      if (in) {
+        cur = p;
+        ++depth4;
+        const uint32_t c = nch(p);
+        stack += c > 0 ? c - 1 : 0;
+      }
+      if (k == 0) member = in;
+    }
+    is4[m] = member ? 1u : 0u;
+    if (member) {
+      atomicMax(&ctl[SAH_CTL_DEPTH4], depth4);
+      atomicMax(&ctl[SAH_CTL_STACK4], stack);
+    }
+  }
+}
+
+__device__ void phase_emit4(const sah_arg_t* a) {
+  const float* nodes = vx_ptr<const float>(a->nodes_addr);
+  const int32_t* cs = vx_ptr<const int32_t>(a->cs_addr);
+  const uint32_t* pre4 = vx_ptr<const uint32_t>(a->is4_addr);
+  rt_node4_t* nodes4 = vx_ptr<rt_node4_t>(a->nodes4_addr);
+  for (uint32_t m = blockIdx.x * SAH_BLOCK + threadIdx.x; m < a->nn; m += gridDim.x * SAH_BLOCK) {
+    if (pre4[m + 1] == pre4[m]) continue;  // not a BVH4 node
+    float v[32];
+    for (int i = 0; i < 32; ++i) v[i] = 0.0f;
+    for (int i = 0; i < 4; ++i) {
+      int32_t ref = cs[8 * m + i];
+      const int32_t src = cs[8 * m + 4 + i];
+      if (ref != RT_EMPTY_REF) {
+        const float* s = nodes + 16ull * (uint32_t)(src >> 1);
+        const int ch = src & 1;
+        for (int k = 0; k < 3; ++k) {
+          v[8 * k + i] = s[4 * k + 2 * ch];
+          v[8 * k + 4 + i] = s[4 * k + 2 * ch + 1];
+        }
+        if (ref >= 0) ref = (int32_t)pre4[ref];
+      }
+      v[24 + i] = __int_as_float(ref);
+    }
+    float4* o = reinterpret_cast<float4*>(nodes4 + pre4[m]);
+    for (int q = 0; q < 8; ++q) o[q] = make_float4(v[4 * q], v[4 * q + 1], v[4 * q + 2], v[4 * q + 3]);
+  }
+}
+
+__device__ void phase_half(const sah_arg_t* a) {
+  rt_node4_t* nodes4 = vx_ptr<rt_node4_t>(a->nodes4_addr);
+  uint32_t* half = vx_ptr<uint32_t>(a->nodes4_addr + 128ull * (uint64_t)a->nn4);
+  for (uint32_t i = blockIdx.x * SAH_BLOCK + threadIdx.x; i < a->nn4; i += gridDim.x * SAH_BLOCK)
+    half4_node(nodes4[i].v, half + 16 * i);
+}
+
+}  // namespace
+
+VX_MAIN(sah_arg_t, arg, SAH_BLOCK) {
+  switch (arg->phase) {
+    case SAH_INIT: phase_init(arg); break;
+    case SAH_SPLIT: phase_split(arg); break;
+    case SAH_NUMBER: phase_number(arg); break;
+    case SAH_SCAN: phase_scan(arg); break;
+    case SAH_EMIT: phase_emit(arg); break;
+    case SAH_CS: phase_cs(arg); break;
+    case SAH_MARK: phase_mark(arg); break;
+    case SAH_EMIT4: phase_emit4(arg); break;
+    default: phase_half(arg); break;
+  }
+  return 0;
+}

@@ -50,7 +50,9 @@ class SceneInfo(C.Structure):
 
 class BvhBuildStats(C.Structure):
     _fields_ = [("nodes", C.c_uint32), ("depth", C.c_uint32), ("launches", C.c_uint32),
-                ("stack4", C.c_uint32), ("build_ms", C.c_double), ("kernel_ms", C.c_double)]
+                ("stack4", C.c_uint32), ("build_ms", C.c_double), ("kernel_ms", C.c_double),
+                ("nodes4", C.c_uint32), ("depth4", C.c_uint32), ("method", C.c_uint32),
+                ("pad", C.c_uint32)]
 
     def as_dict(self):
         return {n: getattr(self, n) for n, _ in self._fields_ if n != "pad"}
@@ -102,6 +104,7 @@ def lib():
             "rt_scene_export_bvh": [vp, vp, vp],
             "rt_scene_export_bvh4": [vp, vp],
             "rt_renderer_build_bvh": [vp, C.POINTER(BvhBuildStats)],
+            "rt_renderer_build_bvh_ex": [vp, u32, C.POINTER(BvhBuildStats)],
             "rt_renderer_export_bvh": [vp, vp, vp, C.POINTER(u32), C.POINTER(u32)],
             "rt_renderer_export_bvh4": [vp, vp, C.POINTER(u32)],
             "rt_renderer_export_bvh4h": [vp, vp, C.POINTER(u32)],
@@ -290,11 +293,15 @@ class Renderer:
                f"rt_renderer_export_records({name})")
         return out[:n.value // 4].reshape(-1, words)
 
-    def build_bvh(self) -> dict:
-        """Build the BVH on the device (kernels/bvh_build.hip) and trace over it
-        from now on (binary traversal); returns the build statistics."""
+    def build_bvh(self, method: str = "lbvh") -> dict:
+        """Build the BVH on the device and trace over it from now on; returns
+        the build statistics.  method "lbvh": Morton codes + radix tree
+        (kernels/bvh_build.hip); "sah": the host builder's binned-SAH tree
+        restated on the device (kernels/bvh_sah.hip), equal to the scene's
+        host-built arrays."""
         st = BvhBuildStats()
-        _check(lib().rt_renderer_build_bvh(self._h, C.byref(st)), "rt_renderer_build_bvh")
+        m = {"lbvh": 0, "sah": 1}[method]
+        _check(lib().rt_renderer_build_bvh_ex(self._h, m, C.byref(st)), "rt_renderer_build_bvh_ex")
         self.gpu_bvh = True
         self.gpu_bvh4 = st.stack4 != RT_BVH_STACK4_UNUSED
         if self.params is not None:
