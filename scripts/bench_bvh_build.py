@@ -1,7 +1,10 @@
 #!/usr/bin/env python3
-"""GPU BVH build time (kernels/bvh_build.hip, 19 launches incl. the BVH4 collapse and its binary16 planes) vs the host
-binned-SAH build (app/bvh.cpp) on the same triangles, and the traced frame
-time over each tree.  One JSON line per scene."""
+"""GPU BVH build times -- the LBVH (kernels/bvh_build.hip, 19 launches incl.
+the BVH4 collapse and its binary16 planes) and the binned-SAH restatement of
+the host builder (kernels/bvh_sah.hip, one launch per level + 8; the host's
+arrays bit for bit) -- vs the host binned-SAH build (app/bvh.cpp) on the
+same triangles, and the traced frame time over each tree.  One JSON line per
+scene."""
 import json
 import os
 import sys
@@ -48,6 +51,11 @@ def main():
         r3.build_bvh()
         gpu2_ms = frame_ms(r3)          # over the device BVH2
         b = sorted(builds, key=lambda x: x["build_ms"])[len(builds) // 2]
+        r4 = rt.Renderer(s)
+        r4.configure(1024, 1024, shadows=True)
+        sah = [r4.build_bvh("sah") for _ in range(5)]
+        sah_ms = frame_ms(r4)           # over the device SAH tree (== the host tree)
+        bs = sorted(sah, key=lambda x: x["build_ms"])[len(sah) // 2]
         print(json.dumps({"scene": name, "triangles": info["num_geometry"],
                           "host_sah_build_ms": round(info["bvh_ms"], 3),
                           "gpu_build_ms": round(b["build_ms"], 3),
@@ -58,7 +66,11 @@ def main():
                           "frame_ms_host_bvh4": round(host_ms, 4),
                           "frame_ms_host_bvh2": round(host2_ms, 4),
                           "frame_ms_gpu_lbvh4": round(gpu_ms, 4),
-                          "frame_ms_gpu_lbvh2": round(gpu2_ms, 4)}), flush=True)
+                          "frame_ms_gpu_lbvh2": round(gpu2_ms, 4),
+                          "gpu_sah_build_ms": round(bs["build_ms"], 3),
+                          "gpu_sah_build_kernel_ms": round(bs["kernel_ms"], 3),
+                          "gpu_sah_launches": bs["launches"],
+                          "frame_ms_gpu_sah4": round(sah_ms, 4)}), flush=True)
 
 
 if __name__ == "__main__":

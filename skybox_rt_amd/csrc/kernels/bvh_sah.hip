@@ -109,6 +109,8 @@ struct SplitLds {
   uint32_t bin[3][SAH_BINS][7];         // lo xyz, hi xyz (ordered), count
   uint32_t side[2][6];                  // child boxes by reduction (median / root)
   float box[2][6];                      // child boxes (lo xyz, hi xyz)
+  float rs[SAH_BINS][6];                // SAH sweep: suffix boxes and counts
+  uint32_t rc[SAH_BINS];
   int axis;
   uint32_t s, nl;
   uint32_t wl[kWaves], wr[kWaves], lbase, rbase;
@@ -190,37 +192,42 @@ __device__ void phase_split(const sah_arg_t* a) {
         }
       }
     __syncthreads();
-    // 3. the SAH decision, in the host's order (one thread)
+    // 3. the SAH decision, in the host's order (one thread; the suffix boxes
+    //    go through LDS to keep them out of registers)
     if (tid == 0 && split_node) {
       double best = INFINITY;
       for (int ax = 0; ax < 3; ++ax) {
         if (!(ch[ax] - cl[ax] > 0.0f)) continue;
-        Box bb[SAH_BINS], rs[SAH_BINS];
-        uint32_t cnt[SAH_BINS], rc[SAH_BINS];
-        for (int q = 0; q < SAH_BINS; ++q) {
-          for (int k = 0; k < 3; ++k) {
-            bb[q].lo[k] = unord(S.bin[ax][q][k]);
-            bb[q].hi[k] = unord(S.bin[ax][q][3 + k]);
-          }
-          cnt[q] = S.bin[ax][q][6];
-        }
         Box acc;
         acc.empty();
         uint32_t na = 0;
         for (int q = SAH_BINS - 1; q >= 1; --q) {
-          acc.grow(bb[q]);
-          na += cnt[q];
-          rs[q] = acc;
-          rc[q] = na;
+          for (int k = 0; k < 3; ++k) {
+            acc.lo[k] = fminf(acc.lo[k], unord(S.bin[ax][q][k]));
+            acc.hi[k] = fmaxf(acc.hi[k], unord(S.bin[ax][q][3 + k]));
+            S.rs[q][k] = acc.lo[k];
+            S.rs[q][3 + k] = acc.hi[k];
+          }
+          na += S.bin[ax][q][6];
+          S.rc[q] = na;
         }
         Box lb;
         lb.empty();
         uint32_t nl = 0;
         for (int q = 1; q < SAH_BINS; ++q) {
-          lb.grow(bb[q - 1]);
-          nl += cnt[q - 1];
-          if (nl == 0 || rc[q] == 0) continue;
-          const double c = (double)nl * lb.area() + (double)rc[q] * rs[q].area();
+          for (int k = 0; k < 3; ++k) {
+            lb.lo[k] = fminf(lb.lo[k], unord(S.bin[ax][q - 1][k]));
+            lb.hi[k] = fmaxf(lb.hi[k], unord(S.bin[ax][q - 1][3 + k]));
+          }
+          nl += S.bin[ax][q - 1][6];
+          const uint32_t rc = S.rc[q];
+          if (nl == 0 || rc == 0) continue;
+          Box rb;
+          for (int k = 0; k < 3; ++k) {
+            rb.lo[k] = S.rs[q][k];
+            rb.hi[k] = S.rs[q][3 + k];
+          }
+          const double c = (double)nl * lb.area() + (double)rc * rb.area();
           if (c < best) {
             best = c;
             S.axis = ax;
@@ -228,7 +235,7 @@ __device__ void phase_split(const sah_arg_t* a) {
             S.nl = nl;
             for (int k = 0; k < 3; ++k) {
               S.box[0][k] = lb.lo[k]; S.box[0][3 + k] = lb.hi[k];
-              S.box[1][k] = rs[q].lo[k]; S.box[1][3 + k] = rs[q].hi[k];
+              S.box[1][k] = rb.lo[k]; S.box[1][3 + k] = rb.hi[k];
             }
           }
         }
