@@ -43,12 +43,15 @@ int bounces = -1;  // >= 0: path tracing
 float light[3] = {0.0f, 60.0f, 80.0f};
 int rank = -1, ranks = 1;            // -G rank,ranks
 const char* id_file = "rt_shard.id";  // -I
+const char* build = nullptr;          // -B lbvh|sah: build the BVH on the device
+bool host_setup = false;              // -H: per-resolution records by the host loops
 
 void usage() {
   std::printf("Skybox MI355X ray-tracing test.\n"
               "Usage: [-t trace] [-o output|null] [-r reference] [-w width] [-h height]"
               " [-S shadows] [-L x,y,w] [-n repeat] [-k kernel_dir]"
-              " [-R raster | -P bounces | -F flat] [-G rank,ranks [-I idfile]]\n");
+              " [-R raster | -P bounces | -F flat] [-G rank,ranks [-I idfile]]"
+              " [-B lbvh|sah device BVH build] [-H host setup]\n");
 }
 
 #define RT_CHECK(_expr)                                                       \
@@ -63,7 +66,7 @@ void usage() {
 
 int main(int argc, char** argv) {
   int c;
-  while ((c = getopt(argc, argv, "t:o:r:w:h:n:k:L:P:G:I:SRF?")) != -1) {
+  while ((c = getopt(argc, argv, "t:o:r:w:h:n:k:L:P:G:I:B:SRFH?")) != -1) {
     switch (c) {
     case 't': trace_file = optarg; break;
     case 'o': output_file = optarg; break;
@@ -79,6 +82,8 @@ int main(int argc, char** argv) {
     case 'L': std::sscanf(optarg, "%f,%f,%f", &light[0], &light[1], &light[2]); break;
     case 'G': std::sscanf(optarg, "%d,%d", &rank, &ranks); break;
     case 'I': id_file = optarg; break;
+    case 'B': build = optarg; break;
+    case 'H': host_setup = true; break;
     case '?': usage(); return 0;
     default: usage(); return -1;
     }
@@ -126,13 +131,22 @@ int main(int argc, char** argv) {
               info.bvh_nodes, info.bvh_leaves, info.bvh_depth, info.bvh_ms, info.parse_ms);
   rt_renderer_h r = nullptr;
   RT_CHECK(rt_renderer_create(scene, kernel_dir, &r));
+  if (build) {
+    const uint32_t m = std::strcmp(build, "sah") == 0 ? RT_BVH_BUILD_SAH : RT_BVH_BUILD_LBVH;
+    rt_bvh_build_stats_t bs;
+    RT_CHECK(rt_renderer_build_bvh_ex(r, m, &bs));
+    std::printf("Device BVH (%s): nodes=%u, depth=%u, bvh4 nodes=%u, stack4=%u, %u launches, "
+                "%.3f ms (kernels %.3f ms)\n", m == RT_BVH_BUILD_SAH ? "sah" : "lbvh", bs.nodes,
+                bs.depth, bs.nodes4, bs.stack4, bs.launches, bs.build_ms, bs.kernel_ms);
+  }
   rt_render_params_t p;
   std::memset(&p, 0, sizeof(p));
   p.width = width;
   p.height = height;
   p.flags = (shadows ? RT_RENDER_SHADOWS : 0u) | (raster ? RT_RENDER_RASTER : 0u) |
             (flat ? RT_RENDER_FLAT : 0u) | (bounces >= 0 ? RT_RENDER_PATH : 0u) |
-            RT_RENDER_COUNTERS;  // the CLI prints ray counts
+            RT_RENDER_COUNTERS |  // the CLI prints ray counts
+            (host_setup ? RT_RENDER_HOST_SETUP : 0u);
   p.bounces = bounces >= 0 ? (uint32_t)bounces : 0u;
   p.seed = 0x5EED;
   std::memcpy(p.light, light, sizeof(light));
@@ -149,6 +163,10 @@ int main(int argc, char** argv) {
                 seen);
   }
   RT_CHECK(rt_renderer_configure(r, &p));
+  rt_setup_stats_t ss;
+  RT_CHECK(rt_renderer_setup_stats(r, &ss));
+  std::printf("Setup (%s): %.3f ms, configure %.3f ms\n", ss.device ? "device" : "host", ss.setup_ms,
+              ss.configure_ms);
   double total = 0.0;
   rt_stats_t st;
   std::vector<uint32_t> gathered;

@@ -300,6 +300,21 @@ def test_rtapp_cli_against_golden():
     assert "PASSED!" in out.stdout
 
 
+@pytest.mark.parametrize("flags", [["-B", "sah"], ["-B", "lbvh"], ["-H"], ["-B", "sah", "-H"]])
+def test_rtapp_cli_device_build_and_host_setup(flags):
+    """rtapp -B sah|lbvh (device BVH build) and -H (host-loop setup) render
+    draw3d's tekkaman golden exactly (primary rays are raster-exact)."""
+    exe = os.path.join(_lib.LIB_DIR, "rtapp")
+    out = subprocess.run([exe, "-t", scene_path("tekkaman"), "-w", "128", "-h", "128", "-o",
+                          "/tmp/rtapp_tek128.png", "-r", f"{GOLDEN}/draw3d/tekkaman_ref_128.png"] + flags,
+                         capture_output=True, text=True, timeout=300)
+    assert out.returncode == 0, out.stdout + out.stderr
+    assert "PASSED!" in out.stdout
+    assert ("Setup (host)" if "-H" in flags else "Setup (device)") in out.stdout
+    if "-B" in flags:
+        assert f"Device BVH ({flags[1]})" in out.stdout
+
+
 def test_counters_off_writes_no_counter_rows():
     """The timed product configuration (counters=False) writes no per-block
     counter rows: the user counters read 0 and MINSTRET is the launch's
