@@ -616,6 +616,13 @@ __device__ __forceinline__ int32_t trace_impl(const Scene& S, const Ray& r, floa
 #ifndef RT_PACKET_BRANCHLESS
 #define RT_PACKET_BRANCHLESS 1
 #endif
+// packet leaves: this many triangle records loaded before any is tested
+// (1: one record at a time).  A/B (profiles/r02/ab_packet_leaf_hoist.json,
+// tekkaman 1024^2 primary + shadow): 1 0.0450 ms, 2 0.0426, 4 0.0436 (4
+// spills twice the SGPRs); the path tracer is neutral (0.179 / 0.177 / 0.178)
+#ifndef RT_PACKET_LEAF_HOIST
+#define RT_PACKET_LEAF_HOIST 2
+#endif
 // wave priority while walking a packet (0: unchanged): the packet walks are
 // the heavy tiles' latency chains
 #ifndef RT_PACKET_PRIO
@@ -690,6 +697,35 @@ __device__ __forceinline__ bool occluded_packet(const Scene& S, const Ray& r, bo
       const uint32_t first = (lr >> 4) & 0x07ffffffu, count = (lr & 15u) + 1u;
       RT_WAVE_ITER(9);
       bool lv = live;
+#if RT_PACKET_LEAF_HOIST > 1
+      // RT_PACKET_LEAF_HOIST slots in flight at once (3 padding records)
+      constexpr uint32_t H = RT_PACKET_LEAF_HOIST;
+#pragma unroll
+      for (uint32_t q0 = 0; q0 < 4; q0 += H) {
+        if (q0 >= count) break;
+        float4 ta[H], tb[H], tc[H];
+#pragma unroll
+        for (uint32_t j = 0; j < H; ++j) {
+          const uint32_t to = S.tris + 48u * (first + q0 + j);
+          ta[j] = S.A.sld_f4(to); tb[j] = S.A.sld_f4(to + 16); tc[j] = S.A.sld_f4(to + 32);
+        }
+#pragma unroll
+        for (uint32_t j = 0; j < H; ++j) {
+          if (q0 + j < count) {
+#ifdef RT_INSTRUMENT
+            cnt.tests += lv;
+#endif
+            float t;
+            if (lv && __float_as_int(ta[j].w) != skip && mt_hit(r, ta[j], tb[j], tc[j], 0.0f, &t) &&
+                t < tmax) {
+              occ = true;
+              done = true;
+              lv = false;
+            }
+          }
+        }
+      }
+#else
       for (uint32_t q = 0; q < count; ++q) {
         const uint32_t to = S.tris + 48u * (first + q);
         const float4 ta = S.A.sld_f4(to), tb = S.A.sld_f4(to + 16), tc = S.A.sld_f4(to + 32);
@@ -703,6 +739,7 @@ __device__ __forceinline__ bool occluded_packet(const Scene& S, const Ray& r, bo
           lv = false;
         }
       }
+#endif
       if (__ballot(!done) == 0) break;
     }
     if (sp == 0) break;
@@ -1070,6 +1107,32 @@ __device__ __forceinline__ int32_t trace_primary_packet(const Scene& S, uint32_t
       const uint32_t lr = (uint32_t)ref;
       const uint32_t first = (lr >> 4) & 0x07ffffffu, count = (lr & 15u) + 1u;
       RT_WAVE_ITER(8);
+#if RT_PACKET_LEAF_HOIST > 1
+      // RT_PACKET_LEAF_HOIST slots' records in flight at once (the vtris
+      // array carries 3 padding records), then their tests: fewer scalar-load
+      // round trips on the walk's dependent chain
+      constexpr uint32_t H = RT_PACKET_LEAF_HOIST;
+#pragma unroll
+      for (uint32_t k0 = 0; k0 < 4; k0 += H) {
+        if (k0 >= count) break;
+        uint4 A[H], B[H], C[H], D[H];
+#pragma unroll
+        for (uint32_t j = 0; j < H; ++j) {
+          const uint32_t o = S.vtris + 64u * (first + k0 + j);
+          A[j] = S.A.sld_u4(o); B[j] = S.A.sld_u4(o + 16); C[j] = S.A.sld_u4(o + 32);
+          D[j] = S.A.sld_u4(o + 48);
+        }
+#pragma unroll
+        for (uint32_t j = 0; j < H; ++j) {
+          if (k0 + j < count) {
+#ifdef RT_INSTRUMENT
+            cnt.tests += l0;
+#endif
+            vis_test(A[j], B[j], C[j], D[j], px, py, tie_high, bz, bpid);
+          }
+        }
+      }
+#else
       for (uint32_t k = 0; k < count; ++k) {
         const uint32_t o = S.vtris + 64u * (first + k);
         const uint4 A = S.A.sld_u4(o), B = S.A.sld_u4(o + 16), C = S.A.sld_u4(o + 32),
@@ -1079,6 +1142,7 @@ __device__ __forceinline__ int32_t trace_primary_packet(const Scene& S, uint32_t
 #endif
         vis_test(A, B, C, D, px, py, tie_high, bz, bpid);
       }
+#endif
     }
     if (sp == 0) break;
     --sp;
