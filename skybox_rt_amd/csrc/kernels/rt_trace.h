@@ -623,6 +623,20 @@ __device__ __forceinline__ int32_t trace_impl(const Scene& S, const Ray& r, floa
 #ifndef RT_PACKET_LEAF_HOIST
 #define RT_PACKET_LEAF_HOIST 2
 #endif
+// 1: a packet walk's (wave-uniform) stack lives in one VGPR, entry i in lane
+// i (v_writelane / v_readlane: no LDS round trip on the pop -> node-load
+// chain); 0: the wave's LDS stack column
+#ifndef RT_PACKET_VSTACK
+#define RT_PACKET_VSTACK 1
+#endif
+// v_writelane_b32: lane `lane` of v := val (wave-uniform val and lane; EXEC
+// is ignored, so it works under any mask)
+__device__ __forceinline__ int32_t vwritelane(int32_t v, int32_t val, int32_t lane) {
+  const int32_t x = __builtin_amdgcn_readfirstlane(val), l = __builtin_amdgcn_readfirstlane(lane);
+  // lane select through M0 (one constant-bus read per VALU op on gfx9)
+  asm("s_mov_b32 m0, %2\n\tv_writelane_b32 %0, %1, m0" : "+v"(v) : "s"(x), "s"(l) : "m0");
+  return v;
+}
 // wave priority while walking a packet (0: unchanged): the packet walks are
 // the heavy tiles' latency chains
 #ifndef RT_PACKET_PRIO
@@ -636,6 +650,8 @@ __device__ __forceinline__ bool occluded_packet(const Scene& S, const Ray& r, bo
   __builtin_amdgcn_s_setprio(RT_PACKET_PRIO);
 #endif
   int32_t* ws = stack - lane_id();
+  (void)ws;
+  int32_t vstk = 0;  // RT_PACKET_VSTACK: stack entry i in lane i of this VGPR
   int sp = 0;
   int32_t ref = 0;
   bool on = true;     // this lane's ray hit the current node's box (and its ancestors')
@@ -681,7 +697,11 @@ __device__ __forceinline__ bool occluded_packet(const Scene& S, const Ray& r, bo
         for (int i = 3; i >= 1; --i) {
           if ((need >> i) & 1u && (need & ((1u << i) - 1u))) {
             if (sp < RT_MAX_STACK) {
+#if RT_PACKET_VSTACK
+              vstk = vwritelane(vstk, c[i], sp);
+#else
               ws[64 * sp] = c[i];  // every active lane stores the same word
+#endif
               onb = h[i] ? onb | (1u << sp) : onb & ~(1u << sp);
               ++sp;
             }
@@ -745,8 +765,12 @@ __device__ __forceinline__ bool occluded_packet(const Scene& S, const Ray& r, bo
     if (sp == 0) break;
     --sp;
     on = (onb >> sp) & 1u;
+#if RT_PACKET_VSTACK
+    ref = __builtin_amdgcn_readlane(vstk, sp);
+#else
     __builtin_amdgcn_wave_barrier();
     ref = __builtin_amdgcn_readfirstlane(ws[64 * sp]);
+#endif
   }
 #if RT_PACKET_PRIO
   __builtin_amdgcn_s_setprio(0);
@@ -1053,6 +1077,8 @@ __device__ __forceinline__ int32_t trace_primary_packet(const Scene& S, uint32_t
   __builtin_amdgcn_s_setprio(RT_PACKET_PRIO);
 #endif
   int32_t* ws = stack - lane_id();  // the wave's column base (lane 0's column)
+  (void)ws;
+  int32_t vstk = 0;  // RT_PACKET_VSTACK: stack entry i in lane i of this VGPR
   const bool l0 = lane_id() == 0;
   uint32_t bz = VX_OM_DEPTH_MASK;
   int32_t bpid = -1;
@@ -1096,7 +1122,11 @@ __device__ __forceinline__ int32_t trace_primary_packet(const Scene& S, uint32_t
       if (n > 0) {
         for (int i = n - 1; i >= 1; --i) {
           if (sp < RT_MAX_STACK) {
+#if RT_PACKET_VSTACK
+            vstk = vwritelane(vstk, c[i], sp);
+#else
             if (l0) ws[64 * sp] = c[i];
+#endif
             ++sp;
           }
         }
@@ -1146,8 +1176,12 @@ __device__ __forceinline__ int32_t trace_primary_packet(const Scene& S, uint32_t
     }
     if (sp == 0) break;
     --sp;
+#if RT_PACKET_VSTACK
+    ref = __builtin_amdgcn_readlane(vstk, sp);
+#else
     __builtin_amdgcn_wave_barrier();
     ref = __builtin_amdgcn_readfirstlane(ws[64 * sp]);
+#endif
   }
 #if RT_PACKET_PRIO
   __builtin_amdgcn_s_setprio(0);
