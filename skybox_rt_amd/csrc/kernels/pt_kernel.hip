@@ -548,6 +548,12 @@ VX_MAIN_OCC(rt_kernel_arg_t, arg, PT_BLOCK, PT_WAVES_PER_EU) {
 VX_MAIN(rt_kernel_arg_t, arg, PT_BLOCK) {
 #endif
   __shared__ PtLds s_pt;
+#ifdef RT_LDS_PAD_WORDS
+  // occupancy probe (A/B only): LDS padding caps the waves per CU; the store
+  // never runs (no real scene has these flags) but keeps the array allocated
+  __shared__ uint32_t s_occ_pad[RT_LDS_PAD_WORDS];
+  if (arg->flags == 0xffffffffu) ((volatile uint32_t*)s_occ_pad)[threadIdx.x] = 0u;
+#endif
 #ifdef RT_STAMPS  // diagnostic image: per-wave start/end timestamps (scripts/wave_timeline.py)
   const uint64_t t_stamp0 = __builtin_amdgcn_s_memrealtime();
   const uint64_t t_cyc0 = __builtin_amdgcn_s_memtime();
