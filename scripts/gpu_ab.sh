@@ -9,3 +9,4 @@ timeout -k 10 400 python -u -m pytest $FILES -x -q --timeout 120 --timeout-metho
 fi
 if [ -n "$AB_SHADOW" ]; then timeout -k 10 300 python scripts/ab_variants.py --rounds ${ROUNDS:-8} --variants "$AB_SHADOW" > gpurun_out/${T}_shadow.json 2> gpurun_out/${T}_shadow.err || { tail -5 gpurun_out/${T}_shadow.err; exit 1; }; cat gpurun_out/${T}_shadow.json; fi
 if [ -n "$AB_PATH" ]; then timeout -k 10 300 python scripts/ab_variants.py --mode path --rounds ${ROUNDS:-8} --variants "$AB_PATH" > gpurun_out/${T}_path.json 2> gpurun_out/${T}_path.err || { tail -5 gpurun_out/${T}_path.err; exit 1; }; cat gpurun_out/${T}_path.json; fi
+if [ -n "$AB_FLAT" ]; then timeout -k 10 300 python scripts/ab_variants.py --mode flat --size 256 --no-shadows --rounds ${ROUNDS:-8} --variants "$AB_FLAT" > gpurun_out/${T}_flat.json 2> gpurun_out/${T}_flat.err || { tail -5 gpurun_out/${T}_flat.err; exit 1; }; cat gpurun_out/${T}_flat.json; fi

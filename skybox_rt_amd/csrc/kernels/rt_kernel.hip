@@ -66,9 +66,24 @@ struct WaveLds {
 };
 
 #if RT_FLAT
+// RT_FLAT_RECT_LDS 1: only each record's rectangle word (16 B: the word the
+// scan tests for every entry) is staged in LDS, 12 KB for tekkaman instead of
+// 48, so many more workgroups fit a CU; a candidate's other three words come
+// through the scalar cache (wave-uniform).  0: the whole 64-B records.
+// A/B (profiles/r02/ab_flat_rect_lds.json, 256^2): whole records in 1024-
+// thread workgroups (2 per CU by LDS) 0.0479 ms; rectangle words in 256-
+// thread workgroups (8 per CU, 4-way list split) 0.0280 ms -- the default
+// image (Makefile FLATDEFS); 512 threads 0.0302, 128 threads 0.0403
+#ifndef RT_FLAT_RECT_LDS
+#define RT_FLAT_RECT_LDS 0
+#endif
 // the geometry list staged as rt_vtri_t records (4 x 16 B per primitive) for
 // the primary rays; the shadow rays read the MT records (rt_tri_t) of S.geom
+#if RT_FLAT_RECT_LDS
+__shared__ uint4 s_geom[RT_FLAT_CAP];
+#else
 __shared__ uint4 s_geom[RT_FLAT_CAP * 4];
+#endif
 __device__ __forceinline__ const uint4* flat_list(const Scene& S) {
   return S.num_geom <= RT_FLAT_CAP ? s_geom : nullptr;
 }
@@ -227,7 +242,11 @@ struct FlatLds {
 };
 
 __device__ __forceinline__ uint4 flat_rec(const Scene& S, const uint4* lds, uint32_t k, uint32_t q) {
+#if RT_FLAT_RECT_LDS
+  return (lds && q == 2) ? lds[k] : S.A.sld_u4(S.vgeom + 64u * k + 16u * q);
+#else
   return lds ? lds[4u * k + q] : S.A.sld_u4(S.vgeom + 64u * k + 16u * q);
+#endif
 }
 
 __device__ __forceinline__ void flat_chunk(const vx_task_t& task, bool valid, const Scene& S,
@@ -368,8 +387,13 @@ VX_MAIN(rt_kernel_arg_t, arg, RT_BLOCK_THREADS) {
   // stage the geometry list once per workgroup (workgroups past the last
   // task chunk have nothing to render and skip it)
   if (S.num_geom <= RT_FLAT_CAP && blockIdx.x * VX_CHUNK < arg->num_tasks) {  // one chunk per step
+#if RT_FLAT_RECT_LDS
+    for (uint32_t i = threadIdx.x; i < S.num_geom; i += blockDim.x)
+      s_geom[i] = S.A.ld_u4(S.vgeom + 64u * i + 32u);
+#else
     for (uint32_t i = threadIdx.x; i < 4u * S.num_geom; i += blockDim.x)
       s_geom[i] = S.A.ld_u4(S.vgeom + 16u * i);
+#endif
   }
   __syncthreads();
 #endif
