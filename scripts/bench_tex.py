@@ -32,6 +32,8 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--cpu-budget", type=float, default=3.0)
+    ap.add_argument("--ab", default="", help="variant directory under lib/variants: time the "
+                    "default and that variant's images interleaved (kernel ms only)")
     args = ap.parse_args()
     import torch  # noqa: F401  (one HIP runtime)
     from conftest import GOLDEN
@@ -46,6 +48,22 @@ def main():
              ("rainbow256 A8R8G8B8 trilinear x16", rainbow, 0, 2, 0, 16.0),
              ("rainbow256 R5G6B5 bilinear x8 mirror", rainbow, 1, 1, 2, 8.0)]
     a = tex.TexApp()
+    if args.ab:
+        b = tex.TexApp(os.path.join(ROOT, "skybox_rt_amd", "lib", "variants", args.ab))
+        for label, src, fmt, filt, wrap, scale in cases:
+            a.configure(src, fmt=fmt, filt=filt, wrap=wrap, scale=scale)
+            b.configure(src, fmt=fmt, filt=filt, wrap=wrap, scale=scale)
+            ka, kb = [], []
+            for _ in range(8):
+                for app, ks in ((a, ka), (b, kb)):
+                    for _ in range(args.steps // 8 + 1):
+                        app.render()
+                        ks.append(app.stats()["kernel_ms"])
+            same = bool(np.array_equal(a.image(), b.image()))
+            print(json.dumps({"case": label, "default_ms": round(float(np.median(ka)), 5),
+                              args.ab + "_ms": round(float(np.median(kb)), 5),
+                              "identical": same}), flush=True)
+        return
     for label, src, fmt, filt, wrap, scale in cases:
         a.configure(src, fmt=fmt, filt=filt, wrap=wrap, scale=scale)
         for _ in range(5):
