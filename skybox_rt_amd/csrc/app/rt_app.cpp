@@ -1117,6 +1117,7 @@ static int build_sah(rt_renderer_h r, rt_bvh_build_stats_t* st) {
   a.n = n;
   double kernel_ms = 0.0;
   uint32_t launches = 0;
+  const bool trace = std::getenv("RT_SAH_TRACE") != nullptr;  // per-launch times to stderr
   auto launch = [&](uint32_t phase) -> int {
     a.phase = phase;
     if (vx_copy_to_dev(argb.h, &a, 0, sizeof(a)) != 0) return fail("vx_copy_to_dev failed");
@@ -1125,6 +1126,7 @@ static int build_sah(rt_renderer_h r, rt_bvh_build_stats_t* st) {
     double ms = 0.0;
     uint32_t g = 0, b = 0;
     if (r->last_run && r->last_run(r->dev, &ms, &g, &b) == 0) kernel_ms += ms;
+    if (trace) std::fprintf(stderr, "sah phase %u level %u: %.4f ms\n", phase, a.level, ms);
     ++launches;
     return 0;
   };

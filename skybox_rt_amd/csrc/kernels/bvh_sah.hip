@@ -109,8 +109,6 @@ struct SplitLds {
   uint32_t bin[3][SAH_BINS][7];         // lo xyz, hi xyz (ordered), count
   uint32_t side[2][6];                  // child boxes by reduction (median / root)
   float box[2][6];                      // child boxes (lo xyz, hi xyz)
-  float rs[SAH_BINS][6];                // SAH sweep: suffix boxes and counts
-  uint32_t rc[SAH_BINS];
   int axis;
   uint32_t s, nl;
   uint32_t wl[kWaves], wr[kWaves], lbase, rbase;
@@ -192,52 +190,54 @@ __device__ void phase_split(const sah_arg_t* a) {
         }
       }
     __syncthreads();
-    // 3. the SAH decision, in the host's order (one thread; the suffix boxes
-    //    go through LDS to keep them out of registers)
-    if (tid == 0 && split_node) {
-      double best = INFINITY;
-      for (int ax = 0; ax < 3; ++ax) {
-        if (!(ch[ax] - cl[ax] > 0.0f)) continue;
-        Box acc;
-        acc.empty();
-        uint32_t na = 0;
-        for (int q = SAH_BINS - 1; q >= 1; --q) {
-          for (int k = 0; k < 3; ++k) {
-            acc.lo[k] = fminf(acc.lo[k], unord(S.bin[ax][q][k]));
-            acc.hi[k] = fmaxf(acc.hi[k], unord(S.bin[ax][q][3 + k]));
-            S.rs[q][k] = acc.lo[k];
-            S.rs[q][3 + k] = acc.hi[k];
+    // 3. the SAH decision: lane i of wave 0 prices candidate i = axis * 15 +
+    //    (split - 1) -- its prefix / suffix boxes and counts over the bins, the
+    //    cost in the host's double arithmetic -- and the wave takes the
+    //    minimum, ties to the lowest index: the host's sequential scan keeps
+    //    the first strict minimum in (axis, split) order (NaN / inf costs never
+    //    win there, so they are +inf here)
+    if (w == 0 && split_node) {
+      const int ax = (int)l / (SAH_BINS - 1), q = (int)l % (SAH_BINS - 1) + 1;
+      double c = INFINITY;
+      Box lb, rb;
+      lb.empty();
+      rb.empty();
+      uint32_t nl = 0;
+      if (l < 3u * (SAH_BINS - 1) && ch[ax] - cl[ax] > 0.0f) {
+        uint32_t rc = 0;
+        for (int k = 0; k < SAH_BINS; ++k) {
+          Box bb;
+          for (int d = 0; d < 3; ++d) {
+            bb.lo[d] = unord(S.bin[ax][k][d]);
+            bb.hi[d] = unord(S.bin[ax][k][3 + d]);
           }
-          na += S.bin[ax][q][6];
-          S.rc[q] = na;
+          const uint32_t cnt = S.bin[ax][k][6];
+          if (k < q) { lb.grow(bb); nl += cnt; }
+          else { rb.grow(bb); rc += cnt; }
         }
-        Box lb;
-        lb.empty();
-        uint32_t nl = 0;
-        for (int q = 1; q < SAH_BINS; ++q) {
-          for (int k = 0; k < 3; ++k) {
-            lb.lo[k] = fminf(lb.lo[k], unord(S.bin[ax][q - 1][k]));
-            lb.hi[k] = fmaxf(lb.hi[k], unord(S.bin[ax][q - 1][3 + k]));
-          }
-          nl += S.bin[ax][q - 1][6];
-          const uint32_t rc = S.rc[q];
-          if (nl == 0 || rc == 0) continue;
-          Box rb;
-          for (int k = 0; k < 3; ++k) {
-            rb.lo[k] = S.rs[q][k];
-            rb.hi[k] = S.rs[q][3 + k];
-          }
-          const double c = (double)nl * lb.area() + (double)rc * rb.area();
-          if (c < best) {
-            best = c;
-            S.axis = ax;
-            S.s = (uint32_t)q;
-            S.nl = nl;
-            for (int k = 0; k < 3; ++k) {
-              S.box[0][k] = lb.lo[k]; S.box[0][3 + k] = lb.hi[k];
-              S.box[1][k] = rb.lo[k]; S.box[1][3 + k] = rb.hi[k];
-            }
-          }
+        if (nl != 0 && rc != 0) {
+          c = (double)nl * lb.area() + (double)rc * rb.area();
+          if (!(c < INFINITY)) c = INFINITY;  // NaN / overflow: never chosen
+        }
+      }
+      double cm = c;
+      uint32_t im = l;
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) {
+        const double oc = __shfl_xor(cm, o, 64);
+        const uint32_t oi = (uint32_t)__shfl_xor((int)im, o, 64);
+        if (oc < cm || (oc == cm && oi < im)) {
+          cm = oc;
+          im = oi;
+        }
+      }
+      if (cm < INFINITY && l == im) {
+        S.axis = ax;
+        S.s = (uint32_t)q;
+        S.nl = nl;
+        for (int k = 0; k < 3; ++k) {
+          S.box[0][k] = lb.lo[k]; S.box[0][3 + k] = lb.hi[k];
+          S.box[1][k] = rb.lo[k]; S.box[1][3 + k] = rb.hi[k];
         }
       }
     }
