@@ -1082,12 +1082,13 @@ static int build_sah(rt_renderer_h r, rt_bvh_build_stats_t* st) {
     }
   }
   std::vector<uint32_t> ctl0(SAH_CTL_WORDS, 0u);
-  DevBuf vb, tbox, cen, idx[2], fin, segs[2], nrec, nbox, cnt, d0, parent, cs, is4, ctl, argb;
+  DevBuf vb, tbox, cen, idx[2], fin, segs[2], small[2], nrec, nbox, cnt, d0, parent, cs, is4, ctl, argb;
   const uint64_t N = n;
   if (alloc_buf(r->dev, verts.size() * 4, &vb, verts.data()) || alloc_buf(r->dev, N * 32, &tbox) ||
       alloc_buf(r->dev, N * 16, &cen) || alloc_buf(r->dev, N * 4, &idx[0]) ||
       alloc_buf(r->dev, N * 4, &idx[1]) || alloc_buf(r->dev, N * 4, &fin) ||
       alloc_buf(r->dev, N * 16, &segs[0]) || alloc_buf(r->dev, N * 16, &segs[1]) ||
+      alloc_buf(r->dev, N * 16, &small[0]) || alloc_buf(r->dev, N * 16, &small[1]) ||
       alloc_buf(r->dev, N * 16, &nrec) || alloc_buf(r->dev, N * 64, &nbox) ||
       alloc_buf(r->dev, (N + 1) * 4, &cnt) || alloc_buf(r->dev, N * 4, &d0) ||
       alloc_buf(r->dev, N * 4, &parent) || alloc_buf(r->dev, N * 32, &cs) ||
@@ -1106,6 +1107,8 @@ static int build_sah(rt_renderer_h r, rt_bvh_build_stats_t* st) {
   a.final_addr = fin.addr;
   a.segs_addr[0] = segs[0].addr;
   a.segs_addr[1] = segs[1].addr;
+  a.small_addr[0] = small[0].addr;
+  a.small_addr[1] = small[1].addr;
   a.nrec_addr = nrec.addr;
   a.nbox_addr = nbox.addr;
   a.cnt_addr = cnt.addr;
@@ -1141,7 +1144,7 @@ static int build_sah(rt_renderer_h r, rt_bvh_build_stats_t* st) {
     a.level = L;
     if (launch(SAH_SPLIT) || read_ctl()) return -1;
     if (c[SAH_CTL_ERR]) return fail("SAH build overflowed its node / segment capacity");
-    if (c[SAH_CTL_SEG + L + 1] == 0) break;
+    if (c[SAH_CTL_SEG + L + 1] == 0 && c[SAH_CTL_SMALL + L + 1] == 0) break;
   }
   const uint32_t nn = c[SAH_CTL_NODES], depth = c[SAH_CTL_DEPTH];
   if (depth > RT_STACK_DEEP) return fail("BVH deeper than RT_STACK_DEEP");

@@ -104,14 +104,25 @@ __device__ void phase_init(const sah_arg_t* a) {
 }
 
 // ---- SAH_SPLIT: one workgroup per segment of level `level` -----------------
-struct SplitLds {
+struct Decision {  // the SAH split of a segment (axis -1: none, the median)
+  int axis;
+  uint32_t s, nl;
+  float box[2][6];                      // child boxes (lo xyz, hi xyz)
+};
+struct SplitLds {  // a workgroup's segment
   uint32_t cb[6];                       // centroid bounds (ordered uints)
   uint32_t bin[3][SAH_BINS][7];         // lo xyz, hi xyz (ordered), count
   uint32_t side[2][6];                  // child boxes by reduction (median / root)
-  float box[2][6];                      // child boxes (lo xyz, hi xyz)
-  int axis;
-  uint32_t s, nl;
+  Decision dec;
   uint32_t wl[kWaves], wr[kWaves], lbase, rbase;
+};
+struct SmallLds {  // a wave's segment (<= SAH_SMALL triangles)
+  uint32_t bin[3][SAH_BINS][7];
+  Decision dec;
+};
+union SplitShared {  // the two loops of a SAH_SPLIT launch run one after the other
+  SplitLds big;
+  SmallLds small[kWaves];
 };
 
 __device__ __forceinline__ int bin_of(float c, float cl, float ext) {
@@ -119,20 +130,201 @@ __device__ __forceinline__ int bin_of(float c, float cl, float ext) {
   return min(max(bi, 0), SAH_BINS - 1);
 }
 
-__device__ void phase_split(const sah_arg_t* a) {
+// The SAH decision over a segment's bins (all 64 lanes of one wave): lane i
+// prices candidate i = axis * 15 + (split - 1) -- its prefix / suffix boxes
+// and counts over the bins, the cost in the host's double arithmetic -- and
+// the wave takes the minimum, ties to the lowest index: the host's sequential
+// scan keeps the first strict minimum in (axis, split) order (NaN / inf costs
+// never win there, so they are +inf here).  The winning lane writes *d; with
+// no winner *d is left as the caller set it (axis -1).
+__device__ void sah_price(const uint32_t (*bin)[SAH_BINS][7], const float* cl, const float* ch,
+                          uint32_t l, Decision* d) {
+  const int ax = (int)l / (SAH_BINS - 1), q = (int)l % (SAH_BINS - 1) + 1;
+  double c = INFINITY;
+  Box lb, rb;
+  lb.empty();
+  rb.empty();
+  uint32_t nl = 0;
+  if (l < 3u * (SAH_BINS - 1) && ch[ax] - cl[ax] > 0.0f) {
+    uint32_t rc = 0;
+    for (int k = 0; k < SAH_BINS; ++k) {
+      Box bb;
+      for (int e = 0; e < 3; ++e) {
+        bb.lo[e] = unord(bin[ax][k][e]);
+        bb.hi[e] = unord(bin[ax][k][3 + e]);
+      }
+      const uint32_t cnt = bin[ax][k][6];
+      if (k < q) { lb.grow(bb); nl += cnt; }
+      else { rb.grow(bb); rc += cnt; }
+    }
+    if (nl != 0 && rc != 0) {
+      c = (double)nl * lb.area() + (double)rc * rb.area();
+      if (!(c < INFINITY)) c = INFINITY;  // NaN / overflow: never chosen
+    }
+  }
+  double cm = c;
+  uint32_t im = l;
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const double oc = __shfl_xor(cm, o, 64);
+    const uint32_t oi = (uint32_t)__shfl_xor((int)im, o, 64);
+    if (oc < cm || (oc == cm && oi < im)) {
+      cm = oc;
+      im = oi;
+    }
+  }
+  if (cm < INFINITY && l == im) {
+    d->axis = ax;
+    d->s = (uint32_t)q;
+    d->nl = nl;
+    for (int k = 0; k < 3; ++k) {
+      d->box[0][k] = lb.lo[k]; d->box[0][3 + k] = lb.hi[k];
+      d->box[1][k] = rb.lo[k]; d->box[1][3 + k] = rb.hi[k];
+    }
+  }
+}
+
+// The node record of segment sg (split at b + nl; child boxes bx) and its
+// children: <= SAH_LEAF triangles a leaf, <= SAH_SMALL a segment of the
+// next level's wave list, else of its workgroup list (one thread)
+__device__ void emit_node(const sah_arg_t* a, const sah_seg_t& sg, uint32_t nl, const float (*bx)[6]) {
   const uint32_t L = a->level;
   uint32_t* ctl = vx_ptr<uint32_t>(a->ctl_addr);
-  const uint32_t nseg = ctl[SAH_CTL_SEG + L];
-  const sah_seg_t* segs = vx_ptr<const sah_seg_t>(a->segs_addr[L & 1]);
   sah_seg_t* next = vx_ptr<sah_seg_t>(a->segs_addr[(L + 1) & 1]);
+  sah_seg_t* next_small = vx_ptr<sah_seg_t>(a->small_addr[(L + 1) & 1]);
+  int32_t ref[2];
+  const uint32_t b = sg.b, e = sg.e;
+  const uint32_t cb[2] = {b, b + nl}, ce[2] = {b + nl, e};
+  for (int q = 0; q < 2; ++q) {
+    const uint32_t m = ce[q] - cb[q];
+    if (m == 0) {
+      ref[q] = RT_EMPTY_REF;  // only the small root's second child
+    } else if (m <= SAH_LEAF) {
+      ref[q] = (int32_t)(RT_LEAF_FLAG | (cb[q] << 4) | (m - 1));
+    } else {
+      const bool small = m <= SAH_SMALL;
+      const uint32_t id = atomicAdd(&ctl[SAH_CTL_NODES], 1u);
+      const uint32_t slot = atomicAdd(&ctl[(small ? SAH_CTL_SMALL : SAH_CTL_SEG) + L + 1], 1u);
+      if (id >= a->n || slot >= a->n || L + 2 >= SAH_MAX_LEVELS) {
+        atomicOr(&ctl[SAH_CTL_ERR], 1u);
+        ref[q] = RT_EMPTY_REF;
+        continue;
+      }
+      (small ? next_small : next)[slot] = sah_seg_t{cb[q], ce[q], id, sg.depth + 1};
+      atomicMax(&ctl[SAH_CTL_DEPTH], sg.depth + 1);
+      ref[q] = (int32_t)id;
+    }
+  }
+  vx_ptr<uint4>(a->nrec_addr)[sg.node] = make_uint4(b, sg.depth, (uint32_t)ref[0], (uint32_t)ref[1]);
+  float4* nb = vx_ptr<float4>(a->nbox_addr) + 4 * sg.node;
+  nb[0] = make_float4(bx[0][0], bx[0][1], bx[0][2], 0.0f);
+  nb[1] = make_float4(bx[0][3], bx[0][4], bx[0][5], 0.0f);
+  nb[2] = make_float4(bx[1][0], bx[1][1], bx[1][2], 0.0f);
+  nb[3] = make_float4(bx[1][3], bx[1][4], bx[1][5], 0.0f);
+}
+
+__device__ __forceinline__ float wmin(float x) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) x = fminf(x, __shfl_xor(x, o, 64));
+  return x;
+}
+__device__ __forceinline__ float wmax(float x) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) x = fmaxf(x, __shfl_xor(x, o, 64));
+  return x;
+}
+
+// Segments of <= SAH_SMALL (64) triangles, one per wave (the deep levels'
+// thousands of small nodes): a triangle per lane, wave reductions instead of
+// workgroup barriers, the bins in the wave's own LDS; the same decisions,
+// order and records as the workgroup path.
+__device__ void split_small(const sah_arg_t* a, SmallLds& W, uint32_t w, uint32_t l, uint64_t lt) {
+  const uint32_t L = a->level;
+  const uint32_t nseg = vx_ptr<const uint32_t>(a->ctl_addr)[SAH_CTL_SMALL + L];
+  const sah_seg_t* segs = vx_ptr<const sah_seg_t>(a->small_addr[L & 1]);
   const uint32_t* idx = vx_ptr<const uint32_t>(a->idx_addr[L & 1]);
   uint32_t* out = vx_ptr<uint32_t>(a->idx_addr[(L + 1) & 1]);
   uint32_t* fin = vx_ptr<uint32_t>(a->final_addr);
   const float4* cen = vx_ptr<const float4>(a->cen_addr);
   const float4* tbox = vx_ptr<const float4>(a->tbox_addr);
-  uint4* nrec = vx_ptr<uint4>(a->nrec_addr);
-  float4* nbox = vx_ptr<float4>(a->nbox_addr);
-  __shared__ SplitLds S;
+  for (uint32_t si = blockIdx.x * kWaves + w; si < nseg; si += gridDim.x * kWaves) {
+    const sah_seg_t sg = segs[si];
+    const uint32_t b = sg.b, n = sg.e - sg.b;  // 5 .. SAH_SMALL
+    const bool valid = l < n;
+    const uint32_t i = b + l;
+    const uint32_t t = valid ? idx[i] : 0u;
+    const float4 c = cen[t], lo = tbox[2 * t], hi = tbox[2 * t + 1];
+    float cl[3], ch[3];
+    for (int k = 0; k < 3; ++k) {
+      cl[k] = wmin(valid ? comp(c, k) : INFINITY);
+      ch[k] = wmax(valid ? comp(c, k) : -INFINITY);
+    }
+    uint32_t* bins = &W.bin[0][0][0];
+    for (uint32_t k = l; k < 3 * SAH_BINS * 7; k += 64) {
+      const uint32_t f = k % 7;
+      bins[k] = f < 3 ? ord(INFINITY) : (f < 6 ? ord(-INFINITY) : 0u);
+    }
+    if (l == 0) W.dec.axis = -1;
+    __builtin_amdgcn_wave_barrier();  // (one wave: its LDS operations complete in order)
+    if (valid)
+      for (int ax = 0; ax < 3; ++ax) {
+        const float ext = ch[ax] - cl[ax];
+        if (!(ext > 0.0f)) continue;
+        uint32_t* bn = W.bin[ax][bin_of(comp(c, ax), cl[ax], ext)];
+        atomicMin(&bn[0], ord(lo.x)); atomicMin(&bn[1], ord(lo.y)); atomicMin(&bn[2], ord(lo.z));
+        atomicMax(&bn[3], ord(hi.x)); atomicMax(&bn[4], ord(hi.y)); atomicMax(&bn[5], ord(hi.z));
+        atomicAdd(&bn[6], 1u);
+      }
+    __builtin_amdgcn_wave_barrier();
+    sah_price(W.bin, cl, ch, l, &W.dec);
+    __builtin_amdgcn_wave_barrier();
+    const int axis = W.dec.axis;
+    const uint32_t nl = axis >= 0 ? W.dec.nl : n / 2;
+    const bool leaf0 = nl <= SAH_LEAF, leaf1 = n - nl <= SAH_LEAF;
+    float bx[2][6];
+    if (axis >= 0) {
+      for (int q = 0; q < 2; ++q)
+        for (int k = 0; k < 6; ++k) bx[q][k] = W.dec.box[q][k];
+      const float ext = ch[axis] - cl[axis];
+      const bool f = valid && (uint32_t)bin_of(comp(c, axis), cl[axis], ext) < W.dec.s;
+      const bool g = valid && !f;
+      const uint64_t mL = __ballot(f), mR = __ballot(g);
+      if (valid) {
+        const uint32_t dst = f ? b + (uint32_t)__popcll(mL & lt) : b + nl + (uint32_t)__popcll(mR & lt);
+        out[dst] = t;
+        if (f ? leaf0 : leaf1) fin[dst] = t;
+      }
+    } else {  // the median: order unchanged, boxes of the two halves
+      const bool left = l < nl;
+      for (int q = 0; q < 2; ++q) {
+        const bool in = valid && (q == 0) == left;
+        for (int k = 0; k < 3; ++k) {
+          bx[q][k] = wmin(in ? comp(lo, k) : INFINITY);
+          bx[q][3 + k] = wmax(in ? comp(hi, k) : -INFINITY);
+        }
+      }
+      if (valid) {
+        out[i] = t;
+        if (left ? leaf0 : leaf1) fin[i] = t;
+      }
+    }
+    if (l == 0) emit_node(a, sg, nl, bx);
+    __builtin_amdgcn_wave_barrier();  // W is reused by the wave's next segment
+  }
+}
+
+__device__ void phase_split(const sah_arg_t* a) {
+  const uint32_t L = a->level;
+  uint32_t* ctl = vx_ptr<uint32_t>(a->ctl_addr);
+  const uint32_t nseg = ctl[SAH_CTL_SEG + L];
+  const sah_seg_t* segs = vx_ptr<const sah_seg_t>(a->segs_addr[L & 1]);
+  const uint32_t* idx = vx_ptr<const uint32_t>(a->idx_addr[L & 1]);
+  uint32_t* out = vx_ptr<uint32_t>(a->idx_addr[(L + 1) & 1]);
+  uint32_t* fin = vx_ptr<uint32_t>(a->final_addr);
+  const float4* cen = vx_ptr<const float4>(a->cen_addr);
+  const float4* tbox = vx_ptr<const float4>(a->tbox_addr);
+  __shared__ SplitShared U;
+  SplitLds& S = U.big;
   const uint32_t tid = threadIdx.x, w = tid >> 6, l = lane_id();
   const uint64_t lt = (l == 0) ? 0ull : (~0ull >> (64 - l));
   for (uint32_t si = blockIdx.x; si < nseg; si += gridDim.x) {
@@ -147,7 +339,7 @@ __device__ void phase_split(const sah_arg_t* a) {
     if (tid < 12) (&S.side[0][0])[tid] = (tid % 6) < 3 ? ord(INFINITY) : ord(-INFINITY);
     if (tid == 0) {
       S.lbase = S.rbase = 0;
-      S.axis = -1;
+      S.dec.axis = -1;
     }
     __syncthreads();
     float cl[3] = {INFINITY, INFINITY, INFINITY}, ch[3] = {-INFINITY, -INFINITY, -INFINITY};
@@ -190,62 +382,13 @@ __device__ void phase_split(const sah_arg_t* a) {
         }
       }
     __syncthreads();
-    // 3. the SAH decision: lane i of wave 0 prices candidate i = axis * 15 +
-    //    (split - 1) -- its prefix / suffix boxes and counts over the bins, the
-    //    cost in the host's double arithmetic -- and the wave takes the
-    //    minimum, ties to the lowest index: the host's sequential scan keeps
-    //    the first strict minimum in (axis, split) order (NaN / inf costs never
-    //    win there, so they are +inf here)
-    if (w == 0 && split_node) {
-      const int ax = (int)l / (SAH_BINS - 1), q = (int)l % (SAH_BINS - 1) + 1;
-      double c = INFINITY;
-      Box lb, rb;
-      lb.empty();
-      rb.empty();
-      uint32_t nl = 0;
-      if (l < 3u * (SAH_BINS - 1) && ch[ax] - cl[ax] > 0.0f) {
-        uint32_t rc = 0;
-        for (int k = 0; k < SAH_BINS; ++k) {
-          Box bb;
-          for (int d = 0; d < 3; ++d) {
-            bb.lo[d] = unord(S.bin[ax][k][d]);
-            bb.hi[d] = unord(S.bin[ax][k][3 + d]);
-          }
-          const uint32_t cnt = S.bin[ax][k][6];
-          if (k < q) { lb.grow(bb); nl += cnt; }
-          else { rb.grow(bb); rc += cnt; }
-        }
-        if (nl != 0 && rc != 0) {
-          c = (double)nl * lb.area() + (double)rc * rb.area();
-          if (!(c < INFINITY)) c = INFINITY;  // NaN / overflow: never chosen
-        }
-      }
-      double cm = c;
-      uint32_t im = l;
-#pragma unroll
-      for (int o = 32; o > 0; o >>= 1) {
-        const double oc = __shfl_xor(cm, o, 64);
-        const uint32_t oi = (uint32_t)__shfl_xor((int)im, o, 64);
-        if (oc < cm || (oc == cm && oi < im)) {
-          cm = oc;
-          im = oi;
-        }
-      }
-      if (cm < INFINITY && l == im) {
-        S.axis = ax;
-        S.s = (uint32_t)q;
-        S.nl = nl;
-        for (int k = 0; k < 3; ++k) {
-          S.box[0][k] = lb.lo[k]; S.box[0][3 + k] = lb.hi[k];
-          S.box[1][k] = rb.lo[k]; S.box[1][3 + k] = rb.hi[k];
-        }
-      }
-    }
+    // 3. the SAH decision (wave 0)
+    if (w == 0 && split_node) sah_price(S.bin, cl, ch, l, &S.dec);
     __syncthreads();
-    const int axis = S.axis;
+    const int axis = S.dec.axis;
     // the root of <= 4 triangles: one leaf child and an empty one; no SAH
     // split: the median, order unchanged
-    const uint32_t nl = !split_node ? n : (axis >= 0 ? S.nl : n / 2);
+    const uint32_t nl = !split_node ? n : (axis >= 0 ? S.dec.nl : n / 2);
     if (axis < 0) {  // child boxes by reduction over the two halves
       float bl[2][6];
       for (int q = 0; q < 2; ++q)
@@ -274,7 +417,7 @@ __device__ void phase_split(const sah_arg_t* a) {
           }
         }
       __syncthreads();
-      if (tid < 12) (&S.box[0][0])[tid] = unord((&S.side[0][0])[tid]);
+      if (tid < 12) (&S.dec.box[0][0])[tid] = unord((&S.side[0][0])[tid]);
     }
     __syncthreads();
     const bool leaf0 = nl <= SAH_LEAF, leaf1 = n - nl <= SAH_LEAF;
@@ -287,7 +430,7 @@ __device__ void phase_split(const sah_arg_t* a) {
         const uint32_t i = r0 + tid;
         const bool valid = i < e;
         const uint32_t t = valid ? idx[i] : 0u;
-        const bool f = valid && (uint32_t)bin_of(comp(cen[t], axis), cl[axis], ext) < S.s;
+        const bool f = valid && (uint32_t)bin_of(comp(cen[t], axis), cl[axis], ext) < S.dec.s;
         const bool g = valid && !f;
         const uint64_t mL = __ballot(f), mR = __ballot(g);
         if (l == 0) {
@@ -322,37 +465,11 @@ __device__ void phase_split(const sah_arg_t* a) {
       }
     }
     // 5. the node record and the next level's segments
-    if (tid == 0) {
-      int32_t ref[2];
-      const uint32_t cb[2] = {b, b + nl}, ce[2] = {b + nl, e};
-      for (int q = 0; q < 2; ++q) {
-        const uint32_t m = ce[q] - cb[q];
-        if (m == 0) {
-          ref[q] = RT_EMPTY_REF;  // only the small root's second child
-        } else if (m <= SAH_LEAF) {
-          ref[q] = (int32_t)(RT_LEAF_FLAG | (cb[q] << 4) | (m - 1));
-        } else {
-          const uint32_t id = atomicAdd(&ctl[SAH_CTL_NODES], 1u);
-          const uint32_t slot = atomicAdd(&ctl[SAH_CTL_SEG + L + 1], 1u);
-          if (id >= a->n || slot >= a->n || L + 2 >= SAH_MAX_LEVELS) {
-            atomicOr(&ctl[SAH_CTL_ERR], 1u);
-            ref[q] = RT_EMPTY_REF;
-            continue;
-          }
-          next[slot] = sah_seg_t{cb[q], ce[q], id, sg.depth + 1};
-          atomicMax(&ctl[SAH_CTL_DEPTH], sg.depth + 1);
-          ref[q] = (int32_t)id;
-        }
-      }
-      nrec[sg.node] = make_uint4(b, sg.depth, (uint32_t)ref[0], (uint32_t)ref[1]);
-      float4* nb = nbox + 4 * sg.node;
-      nb[0] = make_float4(S.box[0][0], S.box[0][1], S.box[0][2], 0.0f);
-      nb[1] = make_float4(S.box[0][3], S.box[0][4], S.box[0][5], 0.0f);
-      nb[2] = make_float4(S.box[1][0], S.box[1][1], S.box[1][2], 0.0f);
-      nb[3] = make_float4(S.box[1][3], S.box[1][4], S.box[1][5], 0.0f);
-    }
+    if (tid == 0) emit_node(a, sg, nl, S.dec.box);
     __syncthreads();
   }
+  __syncthreads();  // the union's other member from here on
+  split_small(a, U.small[w], w, l, lt);
 }
 
 // ---- preorder numbering ------------------------------------------------------

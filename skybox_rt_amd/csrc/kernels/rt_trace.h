@@ -633,8 +633,9 @@ __device__ __forceinline__ int32_t trace_impl(const Scene& S, const Ray& r, floa
 // is ignored, so it works under any mask)
 __device__ __forceinline__ int32_t vwritelane(int32_t v, int32_t val, int32_t lane) {
   const int32_t x = __builtin_amdgcn_readfirstlane(val), l = __builtin_amdgcn_readfirstlane(lane);
-  // lane select through M0 (one constant-bus read per VALU op on gfx9)
-  asm("s_mov_b32 m0, %2\n\tv_writelane_b32 %0, %1, m0" : "+v"(v) : "s"(x), "s"(l) : "m0");
+  // lane select in M0 (one constant-bus read per VALU op on gfx9; the
+  // compiler loads M0 for the operand and knows it is read)
+  asm("v_writelane_b32 %0, %1, m0" : "+v"(v) : "s"(x), "{m0}"(l));
   return v;
 }
 // wave priority while walking a packet (0: unchanged): the packet walks are

@@ -7,10 +7,11 @@
 // extent; the BVH4 collapse that repeatedly opens the largest-area internal
 // child; binary16 planes) that produces the host's arrays bit for bit:
 //   * top-down, one launch per tree level: a workgroup per node (segment of
-//     the triangle order) computes the centroid bounds, the 3 x 16 bins in
-//     LDS, the SAH decision (one thread, in the host's order and double
-//     arithmetic) and the stable partition (ballot ranks) into the other
-//     triangle-order buffer;
+//     the triangle order; a wave per node of <= 64 triangles) computes the
+//     centroid bounds, the 3 x 16 bins in LDS, the SAH decision (45
+//     candidates priced by 45 lanes in the host's double arithmetic, the
+//     first minimum in the host's order) and the stable partition (ballot
+//     ranks) into the other triangle-order buffer;
 //   * the host numbers nodes in depth-first preorder; an internal node's
 //     preorder index is its rank in (first triangle position, depth) order --
 //     the nodes starting at one position form a chain of left children -- so
@@ -25,6 +26,7 @@
 #define SAH_BLOCK 256
 #define SAH_BINS 16
 #define SAH_LEAF 4
+#define SAH_SMALL 64             // segments up to this many triangles: one wave each
 #define SAH_MAX_LEVELS 64
 
 enum {
@@ -46,8 +48,9 @@ enum {
 #define SAH_CTL_DEPTH4 3   // BVH4 depth
 #define SAH_CTL_STACK4 4   // BVH4 worst-case traversal stack
 #define SAH_CTL_ERR 5      // != 0: capacity / depth overflow
-#define SAH_CTL_SEG 8      // [SAH_CTL_SEG + L]: segments of level L
-#define SAH_CTL_WORDS (SAH_CTL_SEG + SAH_MAX_LEVELS + 1)
+#define SAH_CTL_SEG 8      // [SAH_CTL_SEG + L]: workgroup segments of level L
+#define SAH_CTL_SMALL (SAH_CTL_SEG + SAH_MAX_LEVELS + 1)  // [.. + L]: wave segments of level L
+#define SAH_CTL_WORDS (SAH_CTL_SMALL + SAH_MAX_LEVELS + 1)
 
 typedef struct {
   uint32_t b, e, node, depth;
@@ -60,7 +63,8 @@ typedef struct {
   uint64_t cen_addr;      // float4 [n]: centroid
   uint64_t idx_addr[2];   // u32 [n]: triangle order, ping-pong per level
   uint64_t final_addr;    // u32 [n]: the final order (leaf ranges written when created)
-  uint64_t segs_addr[2];  // sah_seg_t [n]: segments of the current / next level
+  uint64_t segs_addr[2];  // sah_seg_t [n]: workgroup segments of the current / next level
+  uint64_t small_addr[2]; // sah_seg_t [n]: wave segments (<= SAH_SMALL triangles)
   uint64_t nrec_addr;     // u32 [n][4]: BFS node: b, depth, ref0, ref1 (ref: > 0 BFS id,
                           //   < -1 leaf, -1 empty)
   uint64_t nbox_addr;     // float4 [n][4]: child 0 lo, hi, child 1 lo, hi (unpadded)
