@@ -20,9 +20,12 @@ def main():
     path = len(sys.argv) > 2 and sys.argv[2] == "path"   # pt_kernel (variants/ptstamp)
     import torch  # noqa: F401
     from skybox_rt_amd import rt
+    kdir = os.path.join(ROOT, "skybox_rt_amd/lib/variants", "ptstamp" if path else "stamp")
+    image = os.path.join(kdir, "pt_kernel.vxbin" if path else "rt_kernel.vxbin")
+    if not os.path.exists(image):  # the renderer would fall back to the stamp-less product image
+        sys.exit(f"wave_timeline: {image} missing (make -C skybox_rt_amd/csrc diag)")
     s = rt.Scene.load(os.path.join(ROOT, "tests/golden/scenes/tekkaman.cgltrace"))
-    r = rt.Renderer(s, kernel_dir=os.path.join(ROOT, "skybox_rt_amd/lib/variants",
-                                               "ptstamp" if path else "stamp"))
+    r = rt.Renderer(s, kernel_dir=kdir)
     r.configure(size, size, shadows=True, path=path)
     for _ in range(5):
         r.render()
