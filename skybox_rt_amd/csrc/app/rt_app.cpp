@@ -461,7 +461,7 @@ extern "C" {
 
 namespace {
 
-// the RT / PT images with the 32-entry traversal stack
+// the generic RT / PT images: every BVH layout, the 32-entry traversal stack
 int load_deep_images(rt_renderer* r) {
   if (load_image(r, "rt_kernel_deep.vxbin", &r->krnl[0][0]) ||
       load_image(r, "rt_kernel_deep_stats.vxbin", &r->krnl[0][1]) ||
@@ -711,6 +711,12 @@ int rt_renderer_configure(rt_renderer_h r, const rt_render_params_t* p) {
             (use_bvh4 ? RT_FLAG_BVH4 : 0u) |
             // binary16 node records: the host tree's, or the device tree's (BVHB_HALF)
             (use_bvh4 && (r->gpu_bvh || !s->bvh.nodes4h.empty()) ? RT_FLAG_BVH4H : 0u);
+  // the regular RT / PT images walk only the binary16 BVH4 (RT_ONLY_BVH4H);
+  // any other layout runs the generic images (the deep ones: every layout,
+  // 32-entry stack)
+  if (!raster && !(p->flags & RT_RENDER_FLAT) && !(a.flags & RT_FLAG_BVH4H) && !r->deep &&
+      load_deep_images(r) != 0)
+    return -1;
   a.bounces = p->bounces;
   a.seed = p->seed;
   a.clear_color = p->clear_color;

@@ -54,7 +54,7 @@ struct rt_renderer {
   vx_hip_run_totals_t run_totals = nullptr;
   vx_hip_set_counters_t set_counters = nullptr;
   std::string kdir;         // kernel directory (images missing there come from lib_dir)
-  bool deep = false;        // RT/PT images with the 32-entry traversal stack
+  bool deep = false;        // generic RT/PT images (every BVH layout, 32-entry stack)
   // the primary rays' tree of the current configuration (rt_renderer_export_vis_tree;
   // host setup only -- after a device setup it is read back on request)
   std::vector<std::array<int32_t, 4>> vis_refs;

@@ -138,7 +138,7 @@ struct PathQueue {
 };
 
 struct PtLds {
-  int32_t stack[kWaves][RT_MAX_STACK][64];
+  int32_t stack[kWaves][RT_STACK_ROWS][64];
 #if PT_MODE == 0
   PathQueue q[2];
   uint32_t n[2];

@@ -34,6 +34,13 @@
 #ifndef RT_MAX_STACK
 #define RT_MAX_STACK RT_STACK_SHALLOW
 #endif
+// 1: a per-lane BVH4 step writes all three push rows unconditionally (rows at
+// or above the new top hold garbage that is never read); the stack then
+// carries 3 slack rows past its capacity for the writes of a full stack
+#ifndef RT_PUSH_UNCOND
+#define RT_PUSH_UNCOND 0
+#endif
+#define RT_STACK_ROWS (RT_MAX_STACK + (RT_PUSH_UNCOND ? 3 : 0))
 #define RT_TILE_LOG 5            // RASTER_TILE_LOGSIZE (VX_config.vh:477-479)
 #define RT_TILE_PIXELS 1024
 #define RT_RASTER_TILE_LOG 4     // raster workgroup tile: 16x16 pixels, one per thread

@@ -52,9 +52,18 @@ constexpr int kWaves = RT_BLOCK_THREADS / 64;
 // Wave-private LDS: the per-ray traversal stack (stack[depth][lane]) and the
 // compaction queue of deferred shadow rays.
 #define RT_QUEUE 128
+// the per-lane walks' LDS stack: not needed when every walk of the image is
+// a wave packet with its stack in a VGPR (binary16-BVH4-only images)
+#ifndef RT_LANE_STACK
+#define RT_LANE_STACK (!RT_FLAT && !(RT_ONLY_BVH4H && RT_PACKET_VSTACK && RT_VIS_PACKET && \
+                                     RT_SHADOW_PACKET && RT_SHADOW_QUEUE))
+#endif
 struct WaveLds {
-#if !RT_FLAT
-  int32_t stack[RT_MAX_STACK][64];
+#if RT_LANE_STACK
+  int32_t stack[RT_STACK_ROWS][64];
+#define RT_WSTACK(w, lane) (&(w).stack[0][(lane)])
+#else
+#define RT_WSTACK(w, lane) ((int32_t*)nullptr)
 #endif
 #if RT_SHADOW_QUEUE
   uint32_t q_task[RT_QUEUE];
@@ -96,7 +105,7 @@ __device__ __forceinline__ bool occluded(const Scene& S, const Ray& s, int32_t s
 #if RT_FLAT
   return trace_flat<true>(S, s, 0.0f, 1.0f, skip, tie_high, &ts, nullptr, cnt) >= 0;
 #else
-  return trace<true>(S, s, 0.0f, 1.0f, skip, tie_high, &ts, &w.stack[0][lane_id()], cnt) >= 0;
+  return trace<true>(S, s, 0.0f, 1.0f, skip, tie_high, &ts, RT_WSTACK(w, lane_id()), cnt) >= 0;
 #endif
 }
 
@@ -113,7 +122,7 @@ __device__ __forceinline__ void kernel_body(const vx_task_t& task, const Scene& 
   if (lane_id() == 0) __vx_mpm_lds[3] = (uint32_t)__builtin_amdgcn_s_memrealtime();
 #endif
   // primary visibility: the raster's winner at this pixel
-  const int32_t hit = trace_primary(S, x, y, in, tie_high, &w.stack[0][lane_id()], cnt);
+  const int32_t hit = trace_primary(S, x, y, in, tie_high, RT_WSTACK(w, lane_id()), cnt);
 #ifdef RT_STAMPS
   if (lane_id() == 0) __vx_mpm_lds[14] = (uint32_t)__builtin_amdgcn_s_memrealtime();
 #endif
@@ -202,8 +211,8 @@ __device__ __forceinline__ void shadow_drain(bool final, const Scene& S, WaveLds
     cnt.shadow += active;
     uint32_t color = w.q_color[slot];
 #if RT_SHADOW_PACKET
-    const bool occ = (S.flags & RT_FLAG_BVH4H)
-                         ? occluded_packet(S, s, active, w.q_pid[slot], 1.0f, &w.stack[0][lane], cnt)
+    const bool occ = (RT_ONLY_BVH4H || (S.flags & RT_FLAG_BVH4H))
+                         ? occluded_packet(S, s, active, w.q_pid[slot], 1.0f, RT_WSTACK(w, lane), cnt)
                          : occluded(S, s, w.q_pid[slot], tie_high, active, w, cnt);
     if (occ) {
 #else

@@ -51,6 +51,11 @@
 // 1: the first node step of every walk (all lanes at the root) reads the root
 // through the scalar cache -- one load per wave instead of 64 lanes of vector
 // data, and the root is where every background ray's walk ends
+// 1: the image walks only the binary16 BVH4 layout (RT_FLAG_BVH4H, the
+// default build); the host runs the generic image for any other layout
+#ifndef RT_ONLY_BVH4H
+#define RT_ONLY_BVH4H 0
+#endif
 #ifndef RT_ROOT_SCALAR
 #define RT_ROOT_SCALAR 1
 #endif
@@ -321,11 +326,25 @@ struct LaneStack {
   // c[1] ends on top) -- push()'s order and overflow rule, as predicated
   // stores instead of a branch per push
   __device__ __forceinline__ void push_sorted(const int32_t c[4], int n) {
+#if RT_PUSH_UNCOND
+    // the same rows get the same entries (row sp + i holds c[n-1-i]); the
+    // three stores run unconditionally -- rows from the new top up hold
+    // garbage never read, and a full stack's stores land in the slack rows
+    int32_t c1 = c[1], c2 = c[2], c3 = c[3];
+    // opaque register values: keeps the selects below from being folded
+    // into a dynamically indexed (scratch) load of c[]
+    asm("" : "+v"(c1), "+v"(c2), "+v"(c3));
+    int32_t* m = mem + 64 * sp;
+    m[0] = n == 2 ? c1 : (n == 3 ? c2 : c3);
+    m[64] = n == 3 ? c1 : c2;
+    m[128] = c1;
+#else
 #pragma unroll
     for (int j = 1; j < 4; ++j) {
       const int pos = sp + n - 1 - j;
       if (j < n && pos < RT_MAX_STACK) mem[64 * pos] = c[j];
     }
+#endif
     const int top = sp + n - 1;
     sp = top < RT_MAX_STACK ? top : RT_MAX_STACK;
   }
@@ -454,9 +473,10 @@ __device__ __forceinline__ int32_t trace_impl(const Scene& S, const Ray& r, floa
     ++cnt.visits;
 #endif
     const float lim = ANY ? tmax : bt;
-    if (S.flags & RT_FLAG_BVH4H)
+    if (RT_ONLY_BVH4H || (S.flags & RT_FLAG_BVH4H))
       return uni ? node4_step<true, true>(S, (uint32_t)r0, r, tmin, lim, ANY, lst)
                  : node4_step<false, true>(S, (uint32_t)ref, r, tmin, lim, ANY, lst);
+#if !RT_ONLY_BVH4H
     if (S.flags & RT_FLAG_BVH4)
       return uni ? node4_step<true, false>(S, (uint32_t)r0, r, tmin, lim, ANY, lst)
                  : node4_step<false, false>(S, (uint32_t)ref, r, tmin, lim, ANY, lst);
@@ -481,6 +501,7 @@ __device__ __forceinline__ int32_t trace_impl(const Scene& S, const Ray& r, floa
     if (st.h0) return st.c0;
     if (st.h1) return st.c1;
     return RT_EMPTY_REF;
+#endif
   };
 #if RT_WW && RT_ROOT_SCALAR
   {
