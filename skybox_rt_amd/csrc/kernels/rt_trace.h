@@ -635,7 +635,7 @@ __device__ __forceinline__ int32_t trace_impl(const Scene& S, const Ray& r, floa
 // active lane calls it (any EXEC mask: the stack words are stored by all
 // active lanes and read back with readfirstlane).
 #ifndef RT_PACKET_BRANCHLESS
-#define RT_PACKET_BRANCHLESS 1
+#define RT_PACKET_BRANCHLESS 2
 #endif
 // packet leaves: this many triangle records loaded before any is tested
 // (1: one record at a time).  A/B (profiles/r02/ab_packet_leaf_hoist.json,
@@ -703,7 +703,13 @@ __device__ __forceinline__ bool occluded_packet(const Scene& S, const Ray& r, bo
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         float tn = 0.0f;
-#if RT_PACKET_BRANCHLESS
+#if RT_PACKET_BRANCHLESS == 2
+        // lanes off the path and empty slots test against a negative far
+        // limit, which the slab test itself rejects (its near value is >= 0):
+        // h is one compare, the same value as the masked form below
+        const float lim = (live && c[i] != RT_EMPTY_REF) ? tmax : -1.0f;
+        h[i] = slab(lx[i], hx[i], ly[i], hy[i], lz[i], hz[i], r, 0.0f, lim, &tn);
+#elif RT_PACKET_BRANCHLESS
         // every lane evaluates the slab (no exec-mask branch per child)
         const bool hs = slab(lx[i], hx[i], ly[i], hy[i], lz[i], hz[i], r, 0.0f, tmax, &tn);
         h[i] = hs & live & (c[i] != RT_EMPTY_REF);
@@ -1142,8 +1148,11 @@ __device__ __forceinline__ int32_t trace_primary_packet(const Scene& S, uint32_t
       cx(1, 3);
       cx(1, 2);
       if (n > 0) {
-        for (int i = n - 1; i >= 1; --i) {
-          if (sp < RT_MAX_STACK) {
+        // c[n-1] .. c[1] pushed (farthest first); unrolled over the slots so
+        // each c[i] is a fixed register, not a dynamically indexed one
+#pragma unroll
+        for (int i = 3; i >= 1; --i) {
+          if (i < n && sp < RT_MAX_STACK) {
 #if RT_PACKET_VSTACK
             vstk = vwritelane(vstk, c[i], sp);
 #else
