@@ -178,8 +178,8 @@ struct NodeBuilder {
     for (int i = 0; i < 4; ++i) {
       const Cover k = of(refs[ref][i], depth + 1);
       n.child[i] = k.any ? refs[ref][i] : RT_EMPTY_REF;
-      n.rx[i] = k.any ? Pack(k.x0, k.x1) : RT_VIS_EMPTY_RECT;
-      n.ry[i] = k.any ? Pack(k.y0, k.y1) : RT_VIS_EMPTY_RECT;
+      n.lo[i] = k.any ? Pack(k.x0, k.y0) : RT_VIS_EMPTY_RECT;
+      n.hi[i] = k.any ? Pack(k.x1, k.y1) : RT_VIS_EMPTY_RECT;
       n.zmin[i] = k.any ? k.zmin : RT_VIS_ZMIN_NONE;
       c.add(k);
     }
@@ -195,7 +195,7 @@ int BuildVisNodes(const std::vector<std::array<int32_t, 4>>& refs,
   out->assign(refs.size(), rt_vnode_t{});
   for (rt_vnode_t& n : *out)
     for (int i = 0; i < 4; ++i) {
-      n.rx[i] = n.ry[i] = RT_VIS_EMPTY_RECT;
+      n.lo[i] = n.hi[i] = RT_VIS_EMPTY_RECT;
       n.zmin[i] = RT_VIS_ZMIN_NONE;
       n.child[i] = RT_EMPTY_REF;
     }

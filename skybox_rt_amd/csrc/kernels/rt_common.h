@@ -110,10 +110,13 @@ typedef struct { float v[12]; } rt_tri_t;
 #define RT_VIS_EMPTY_RECT 0x0000ffffu
 #define RT_VIS_ZMIN_NONE 0xffffffffu
 // rt_vnode_t (64 B), index-aligned with the traversed tree's nodes (BVH4, or
-// BVH2 in slots 0-1): per child its covered-pixel rectangle, depth lower
-// bound and reference (RT_EMPTY_REF when the child covers no pixel)
+// BVH2 in slots 0-1): per child its covered-pixel rectangle as its corners
+// lo = x0 | y0 << 16 and hi = x1 | y1 << 16 (inclusive: a pixel packed as
+// x | y << 16 is inside iff two packed 16-bit clamps leave it unchanged),
+// depth lower bound and reference (RT_EMPTY_REF when the child covers no
+// pixel; its lo = hi = RT_VIS_EMPTY_RECT)
 typedef struct {
-  uint32_t rx[4], ry[4], zmin[4];
+  uint32_t lo[4], hi[4], zmin[4];
   int32_t child[4];
 } rt_vnode_t;
 // rt_vtri_t (64 B), index-aligned with the leaf triangle records (tris):

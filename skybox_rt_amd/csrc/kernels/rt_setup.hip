@@ -371,6 +371,10 @@ __device__ __forceinline__ void cover_add(Cover* c, uint32_t rx, uint32_t ry, ui
   c->zmin = min(c->zmin, zmin);
   c->any = true;
 }
+// a vnode child's rectangle (corners lo = x0 | y0 << 16, hi = x1 | y1 << 16)
+__device__ __forceinline__ void cover_add_corners(Cover* c, uint32_t lo, uint32_t hi, uint32_t zmin) {
+  cover_add(c, (lo & 0xffffu) | (hi << 16), (lo >> 16) | (hi & 0xffff0000u), zmin);
+}
 
 // bottom-up vnode records (app/vis.cpp BuildVisNodes): each node's slots get
 // the union rectangle / minimum depth bound of the child's subtree; a node's
@@ -399,7 +403,7 @@ __device__ void phase_climb(const rt_setup_arg_t* a) {
       Cover u = {0xffffu, 0u, 0xffffu, 0u, RT_VIS_ZMIN_NONE, false};
       for (int s = 0; s < 4; ++s) {
         if (r[s] > 0 && (uint32_t)r[s] < nn) {  // written by the child's climb
-          if (vn[cur].child[s] != RT_EMPTY_REF) cover_add(&u, vn[cur].rx[s], vn[cur].ry[s], vn[cur].zmin[s]);
+          if (vn[cur].child[s] != RT_EMPTY_REF) cover_add_corners(&u, vn[cur].lo[s], vn[cur].hi[s], vn[cur].zmin[s]);
           continue;
         }
         Cover c = {0xffffu, 0u, 0xffffu, 0u, RT_VIS_ZMIN_NONE, false};
@@ -415,17 +419,17 @@ __device__ void phase_climb(const rt_setup_arg_t* a) {
             if (v.w) cover_add(&c, v.x, v.y, v.z);
           }
         }
-        vn[cur].rx[s] = c.any ? (c.x0 | (c.x1 << 16)) : RT_VIS_EMPTY_RECT;
-        vn[cur].ry[s] = c.any ? (c.y0 | (c.y1 << 16)) : RT_VIS_EMPTY_RECT;
+        vn[cur].lo[s] = c.any ? (c.x0 | (c.y0 << 16)) : RT_VIS_EMPTY_RECT;
+        vn[cur].hi[s] = c.any ? (c.x1 | (c.y1 << 16)) : RT_VIS_EMPTY_RECT;
         vn[cur].zmin[s] = c.any ? c.zmin : RT_VIS_ZMIN_NONE;
         vn[cur].child[s] = c.any ? r[s] : RT_EMPTY_REF;
-        if (c.any) cover_add(&u, vn[cur].rx[s], vn[cur].ry[s], c.zmin);
+        if (c.any) cover_add_corners(&u, vn[cur].lo[s], vn[cur].hi[s], c.zmin);
       }
       const int32_t p = parent[cur];
       if (p < 0) break;
       const uint32_t pn = (uint32_t)p >> 2, ps = (uint32_t)p & 3u;
-      vn[pn].rx[ps] = u.any ? (u.x0 | (u.x1 << 16)) : RT_VIS_EMPTY_RECT;
-      vn[pn].ry[ps] = u.any ? (u.y0 | (u.y1 << 16)) : RT_VIS_EMPTY_RECT;
+      vn[pn].lo[ps] = u.any ? (u.x0 | (u.y0 << 16)) : RT_VIS_EMPTY_RECT;
+      vn[pn].hi[ps] = u.any ? (u.x1 | (u.y1 << 16)) : RT_VIS_EMPTY_RECT;
       vn[pn].zmin[ps] = u.any ? u.zmin : RT_VIS_ZMIN_NONE;
       vn[pn].child[ps] = u.any ? (int32_t)cur : RT_EMPTY_REF;
       const uint32_t old = __hip_atomic_fetch_add(&count[2 * pn + 1], 1u, __ATOMIC_ACQ_REL,

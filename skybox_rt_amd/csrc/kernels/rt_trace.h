@@ -255,6 +255,25 @@ __device__ __forceinline__ bool slab(float lox, float hix, float loy, float hiy,
   *tnear = tn;
   return tn <= tf;
 }
+// the same test, also returning the far value (for a lane-mask compare)
+__device__ __forceinline__ bool slab_nf(float lox, float hix, float loy, float hiy, float loz,
+                                        float hiz, const Ray& r, float tmin, float tmax,
+                                        float* tnear, float* tfar) {
+  const float ax = fmaf(lox, r.inv[0], -r.oi[0]), bx = fmaf(hix, r.inv[0], -r.oi[0]);
+  const float ay = fmaf(loy, r.inv[1], -r.oi[1]), by = fmaf(hiy, r.inv[1], -r.oi[1]);
+  const float az = fmaf(loz, r.inv[2], -r.oi[2]), bz = fmaf(hiz, r.inv[2], -r.oi[2]);
+  const float tn = fmaxf(fmaxf(fminf(ax, bx), fminf(ay, by)), fmaxf(fminf(az, bz), tmin));
+  const float tf = fminf(fminf(fmaxf(ax, bx), fmaxf(ay, by)), fminf(fmaxf(az, bz), tmax));
+  *tnear = tn;
+  *tfar = tf;
+  return tn <= tf;
+}
+// lane masks straight from one v_cmp (inactive lanes 0), instead of a
+// ballot of a combined bool (which the compiler re-materialises with a
+// v_cndmask + v_cmp pair): ordered a <= b, unsigned a == b, unsigned a <= b
+__device__ __forceinline__ uint64_t mask_fle(float a, float b) { return __builtin_amdgcn_fcmp(a, b, 5); }
+__device__ __forceinline__ uint64_t mask_ueq(uint32_t a, uint32_t b) { return __builtin_amdgcn_uicmp(a, b, 32); }
+__device__ __forceinline__ uint64_t mask_ule(uint32_t a, uint32_t b) { return __builtin_amdgcn_uicmp(a, b, 37); }
 
 // closest-hit order: t, then pid by the drawcall's depth-compare tie rule
 __device__ __forceinline__ bool closer(float t, int32_t pid, float bt, int32_t bpid, bool tie_high) {
@@ -708,7 +727,10 @@ __device__ __forceinline__ bool occluded_packet(const Scene& S, const Ray& r, bo
         // limit, which the slab test itself rejects (its near value is >= 0):
         // h is one compare, the same value as the masked form below
         const float lim = (live && c[i] != RT_EMPTY_REF) ? tmax : -1.0f;
-        h[i] = slab(lx[i], hx[i], ly[i], hy[i], lz[i], hz[i], r, 0.0f, lim, &tn);
+        float tf;
+        h[i] = slab_nf(lx[i], hx[i], ly[i], hy[i], lz[i], hz[i], r, 0.0f, lim, &tn, &tf);
+        need |= mask_fle(tn, tf) ? 1u << i : 0u;
+        continue;
 #elif RT_PACKET_BRANCHLESS
         // every lane evaluates the slab (no exec-mask branch per child)
         const bool hs = slab(lx[i], hx[i], ly[i], hy[i], lz[i], hz[i], r, 0.0f, tmax, &tn);
@@ -943,6 +965,16 @@ __device__ __forceinline__ uint32_t shade_wave(const Scene& S, int32_t spid, uin
 __device__ __forceinline__ bool rect_in(uint32_t r, uint32_t p) {
   return p >= (r & 0xffffu) && p <= (r >> 16);
 }
+// pixel p = x | y << 16 inside the rectangle with corners lo, hi (packed the
+// same way, lo <= hi per half): two packed 16-bit clamps (v_pk_max_u16,
+// v_pk_min_u16) and one compare for both axes
+typedef uint16_t rt_u16x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ bool rect2_in(uint32_t lo, uint32_t hi, uint32_t p) {
+  const rt_u16x2 v = __builtin_bit_cast(rt_u16x2, p);
+  const rt_u16x2 c = __builtin_elementwise_min(
+      __builtin_elementwise_max(v, __builtin_bit_cast(rt_u16x2, lo)), __builtin_bit_cast(rt_u16x2, hi));
+  return __builtin_bit_cast(uint32_t, c) == p;
+}
 
 // the depth word draw3d's shader computes from the three edge values
 // (GRADIENTS + INTERPOLATE z, draw3d/kernel.cpp:37-59; gfx::shade_edges)
@@ -993,15 +1025,16 @@ __device__ __forceinline__ int32_t vnode_step(const Scene& S, uint32_t ref, uint
                                               uint32_t bz, LaneStack& st) {
   auto ld = [&](uint32_t o) { return SCALAR ? S.A.sld_u4(o) : S.A.ld_u4(o); };
   const uint32_t o = S.vnodes + 64u * ref;
-  const uint4 rx = ld(o), ry = ld(o + 16), zm = ld(o + 32), cf = ld(o + 48);
-  const uint32_t arx[4] = {rx.x, rx.y, rx.z, rx.w}, ary[4] = {ry.x, ry.y, ry.z, ry.w};
+  const uint4 rl = ld(o), rh = ld(o + 16), zm = ld(o + 32), cf = ld(o + 48);
+  const uint32_t alo[4] = {rl.x, rl.y, rl.z, rl.w}, ahi[4] = {rh.x, rh.y, rh.z, rh.w};
   const uint32_t azm[4] = {zm.x, zm.y, zm.z, zm.w};
   int32_t c[4] = {(int32_t)cf.x, (int32_t)cf.y, (int32_t)cf.z, (int32_t)cf.w};
+  const uint32_t pp = px > 0xffffu ? 0xffffffffu : px | (py << 16);
   uint32_t k[4];
   int n = 0;
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
-    const bool h = c[i] != RT_EMPTY_REF && rect_in(arx[i], px) && rect_in(ary[i], py) && azm[i] <= bz;
+    const bool h = c[i] != RT_EMPTY_REF && rect2_in(alo[i], ahi[i], pp) && azm[i] <= bz;
     k[i] = h ? azm[i] : 0xffffffffu;
     n += h ? 1 : 0;
   }
@@ -1101,6 +1134,7 @@ __device__ __forceinline__ int32_t trace_primary_packet(const Scene& S, uint32_t
                                                         Counters& cnt) {
   if (S.num_vnodes == 0) return -1;
   if (!act) px = 0xffffffffu;  // in no rectangle
+  const uint32_t pp = px > 0xffffu ? 0xffffffffu : px | (py << 16);  // packed pixel (rect2_in)
 #if RT_PACKET_PRIO
   __builtin_amdgcn_s_setprio(RT_PACKET_PRIO);
 #endif
@@ -1119,17 +1153,22 @@ __device__ __forceinline__ int32_t trace_primary_packet(const Scene& S, uint32_t
 #endif
       RT_WAVE_ITER(7);
       const uint32_t o = S.vnodes + 64u * (uint32_t)ref;
-      const uint4 rx = S.A.sld_u4(o), ry = S.A.sld_u4(o + 16), zm = S.A.sld_u4(o + 32),
+      const uint4 rl = S.A.sld_u4(o), rh = S.A.sld_u4(o + 16), zm = S.A.sld_u4(o + 32),
                   cf = S.A.sld_u4(o + 48);
-      const uint32_t arx[4] = {rx.x, rx.y, rx.z, rx.w}, ary[4] = {ry.x, ry.y, ry.z, ry.w};
+      const uint32_t alo[4] = {rl.x, rl.y, rl.z, rl.w}, ahi[4] = {rh.x, rh.y, rh.z, rh.w};
       const uint32_t azm[4] = {zm.x, zm.y, zm.z, zm.w};
       int32_t c[4] = {(int32_t)cf.x, (int32_t)cf.y, (int32_t)cf.z, (int32_t)cf.w};
       uint32_t k[4];
       int n = 0;
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
+        // lanes whose pixel is in the child's rectangle and whose best depth
+        // word can still lose to the child's bound: two lane masks, one AND
+        const rt_u16x2 cl = __builtin_elementwise_min(
+            __builtin_elementwise_max(__builtin_bit_cast(rt_u16x2, pp), __builtin_bit_cast(rt_u16x2, alo[i])),
+            __builtin_bit_cast(rt_u16x2, ahi[i]));
         const bool need = c[i] != RT_EMPTY_REF &&
-                          __ballot(rect_in(arx[i], px) && rect_in(ary[i], py) && azm[i] <= bz) != 0;
+                          (mask_ueq(__builtin_bit_cast(uint32_t, cl), pp) & mask_ule(azm[i], bz)) != 0;
         k[i] = need ? azm[i] : 0xffffffffu;
         n += need ? 1 : 0;
       }
