@@ -250,9 +250,24 @@ struct FlatLds {
   uint32_t first[kWaves][64];
 };
 
+#if RT_FLAT_RECT_LDS
+// a record's rectangle word with its rectangle as packed corners (lo = x0 |
+// y0 << 16, hi = x1 | y1 << 16 in .y / .z; an empty rectangle becomes
+// lo = 0xffffffff, hi = 0xfffefffe, which no pixel matches): the form staged
+// in LDS, so a wave's rectangle test is two packed 16-bit clamps and one
+// compare (rect2_in)
+__device__ __forceinline__ uint4 rect_corners(uint4 c) {
+  const uint32_t rx = c.y, ry = c.z;
+  const bool empty = (rx & 0xffffu) > (rx >> 16) || (ry & 0xffffu) > (ry >> 16);
+  c.y = empty ? 0xffffffffu : (rx & 0xffffu) | (ry << 16);
+  c.z = empty ? 0xfffefffeu : (rx >> 16) | (ry & 0xffff0000u);
+  return c;
+}
+#endif
 __device__ __forceinline__ uint4 flat_rec(const Scene& S, const uint4* lds, uint32_t k, uint32_t q) {
 #if RT_FLAT_RECT_LDS
-  return (lds && q == 2) ? lds[k] : S.A.sld_u4(S.vgeom + 64u * k + 16u * q);
+  if (q == 2) return lds ? lds[k] : rect_corners(S.A.sld_u4(S.vgeom + 64u * k + 32u));
+  return S.A.sld_u4(S.vgeom + 64u * k + 16u * q);
 #else
   return lds ? lds[4u * k + q] : S.A.sld_u4(S.vgeom + 64u * k + 16u * q);
 #endif
@@ -266,6 +281,9 @@ __device__ __forceinline__ void flat_chunk(const vx_task_t& task, bool valid, co
   if (valid) task_pixel(S, t, &x, &y);
   const bool in = valid && x < S.width && y < S.height;
   const uint32_t px = in ? x : 0xffffffffu;  // outside every pixel rectangle
+#if RT_FLAT_RECT_LDS
+  const uint32_t pp = in ? x | (y << 16) : 0xffffffffu;  // packed pixel (rect_corners)
+#endif
   const bool tie_high = (S.flags & RT_FLAG_TIE_HIGH) != 0;
   const uint32_t n = S.num_geom, per = (n + kWaves - 1) / kWaves;
   const uint32_t k0 = w * per < n ? w * per : n, k1 = k0 + per < n ? k0 + per : n;
@@ -281,6 +299,19 @@ __device__ __forceinline__ void flat_chunk(const vx_task_t& task, bool valid, co
 #pragma unroll
     for (int j = 0; j < RT_FLAT_UNROLL; ++j) C[j] = flat_rec(S, lds, k + j, 2);
     uint32_t cand = 0u;
+#if RT_FLAT_RECT_LDS
+    bool inr[RT_FLAT_UNROLL];
+#pragma unroll
+    for (int j = 0; j < RT_FLAT_UNROLL; ++j) {
+      inr[j] = rect2_in(C[j].y, C[j].z, pp);
+      cand |= mask_ueq(rect2_clamp(C[j].y, C[j].z, pp), pp) ? 1u << j : 0u;
+    }
+#pragma unroll
+    for (int j = 0; j < RT_FLAT_UNROLL; ++j)
+      if ((cand >> j) & 1u)  // wave-uniform
+        vis_test_in(flat_rec(S, lds, k + j, 0), flat_rec(S, lds, k + j, 1), C[j],
+                    flat_rec(S, lds, k + j, 3), inr[j], px, y, tie_high, bz, bp);
+#else
 #pragma unroll
     for (int j = 0; j < RT_FLAT_UNROLL; ++j)
       cand |= __ballot(rect_in(C[j].y, px) && rect_in(C[j].z, y)) ? 1u << j : 0u;
@@ -289,13 +320,21 @@ __device__ __forceinline__ void flat_chunk(const vx_task_t& task, bool valid, co
       if ((cand >> j) & 1u)  // wave-uniform
         vis_test(flat_rec(S, lds, k + j, 0), flat_rec(S, lds, k + j, 1), C[j],
                  flat_rec(S, lds, k + j, 3), px, y, tie_high, bz, bp);
+#endif
   }
 #endif
   for (; k < k1; ++k) {
     const uint4 C = flat_rec(S, lds, k, 2);
+#if RT_FLAT_RECT_LDS
+    const bool inr = rect2_in(C.y, C.z, pp);
+    if (__ballot(inr) == 0) continue;  // wave-uniform skip
+    vis_test_in(flat_rec(S, lds, k, 0), flat_rec(S, lds, k, 1), C, flat_rec(S, lds, k, 3), inr, px,
+                y, tie_high, bz, bp);
+#else
     if (__ballot(rect_in(C.y, px) && rect_in(C.z, y)) == 0) continue;  // wave-uniform skip
     vis_test(flat_rec(S, lds, k, 0), flat_rec(S, lds, k, 1), C, flat_rec(S, lds, k, 3), px, y,
              tie_high, bz, bp);
+#endif
   }
 #ifdef RT_INSTRUMENT
   cnt.tests += in ? k1 - k0 : 0u;  // the whole list per ray, summed over the waves
@@ -398,7 +437,7 @@ VX_MAIN(rt_kernel_arg_t, arg, RT_BLOCK_THREADS) {
   if (S.num_geom <= RT_FLAT_CAP && blockIdx.x * VX_CHUNK < arg->num_tasks) {  // one chunk per step
 #if RT_FLAT_RECT_LDS
     for (uint32_t i = threadIdx.x; i < S.num_geom; i += blockDim.x)
-      s_geom[i] = S.A.ld_u4(S.vgeom + 64u * i + 32u);
+      s_geom[i] = rect_corners(S.A.ld_u4(S.vgeom + 64u * i + 32u));
 #else
     for (uint32_t i = threadIdx.x; i < 4u * S.num_geom; i += blockDim.x)
       s_geom[i] = S.A.ld_u4(S.vgeom + 16u * i);

@@ -653,8 +653,10 @@ __device__ __forceinline__ int32_t trace_impl(const Scene& S, const Ray& r, floa
 // (0.0565 -> 0.0514 ms): the heavy tiles' shadow rays are coherent.  Every
 // active lane calls it (any EXEC mask: the stack words are stored by all
 // active lanes and read back with readfirstlane).
+// (2: off-path lanes folded into the slab's far limit and the child mask
+// taken from one v_cmp -- 0.8 % slower than 1 in A/B, ab_packet_fold.json)
 #ifndef RT_PACKET_BRANCHLESS
-#define RT_PACKET_BRANCHLESS 2
+#define RT_PACKET_BRANCHLESS 1
 #endif
 // packet leaves: this many triangle records loaded before any is tested
 // (1: one record at a time).  A/B (profiles/r02/ab_packet_leaf_hoist.json,
@@ -969,11 +971,14 @@ __device__ __forceinline__ bool rect_in(uint32_t r, uint32_t p) {
 // same way, lo <= hi per half): two packed 16-bit clamps (v_pk_max_u16,
 // v_pk_min_u16) and one compare for both axes
 typedef uint16_t rt_u16x2 __attribute__((ext_vector_type(2)));
-__device__ __forceinline__ bool rect2_in(uint32_t lo, uint32_t hi, uint32_t p) {
+__device__ __forceinline__ uint32_t rect2_clamp(uint32_t lo, uint32_t hi, uint32_t p) {
   const rt_u16x2 v = __builtin_bit_cast(rt_u16x2, p);
   const rt_u16x2 c = __builtin_elementwise_min(
       __builtin_elementwise_max(v, __builtin_bit_cast(rt_u16x2, lo)), __builtin_bit_cast(rt_u16x2, hi));
-  return __builtin_bit_cast(uint32_t, c) == p;
+  return __builtin_bit_cast(uint32_t, c);
+}
+__device__ __forceinline__ bool rect2_in(uint32_t lo, uint32_t hi, uint32_t p) {
+  return rect2_clamp(lo, hi, p) == p;
 }
 
 // the depth word draw3d's shader computes from the three edge values
@@ -995,11 +1000,12 @@ __device__ __forceinline__ bool vis_better(uint32_t z, int32_t pid, uint32_t bz,
   return z < bz || (z == bz && (tie_high ? pid > bpid : (bpid >= 0 && pid < bpid)));
 }
 
-// one rt_vtri_t candidate; updates (bz, bpid)
-__device__ __forceinline__ void vis_test(const uint4& A, const uint4& B, const uint4& C, const uint4& D,
-                                         uint32_t px, uint32_t py, bool tie_high, uint32_t& bz,
-                                         int32_t& bpid) {
-  if (!rect_in(C.y, px) || !rect_in(C.z, py) || D.w > bz) return;
+// one rt_vtri_t candidate whose rectangle test is already known (`inr`);
+// updates (bz, bpid)
+__device__ __forceinline__ void vis_test_in(const uint4& A, const uint4& B, const uint4& C,
+                                            const uint4& D, bool inr, uint32_t px, uint32_t py,
+                                            bool tie_high, uint32_t& bz, int32_t& bpid) {
+  if (!inr || D.w > bz) return;
   const int32_t e0[3] = {(int32_t)A.x, (int32_t)A.y, (int32_t)A.z};
   const int32_t e1[3] = {(int32_t)A.w, (int32_t)B.x, (int32_t)B.y};
   const int32_t e2[3] = {(int32_t)B.z, (int32_t)B.w, (int32_t)C.x};
@@ -1013,6 +1019,11 @@ __device__ __forceinline__ void vis_test(const uint4& A, const uint4& B, const u
     bz = z;
     bpid = pid;
   }
+}
+__device__ __forceinline__ void vis_test(const uint4& A, const uint4& B, const uint4& C, const uint4& D,
+                                         uint32_t px, uint32_t py, bool tie_high, uint32_t& bz,
+                                         int32_t& bpid) {
+  vis_test_in(A, B, C, D, rect_in(C.y, px) && rect_in(C.z, py), px, py, tie_high, bz, bpid);
 }
 
 // rt_vnode_t step: children whose pixel rectangle holds (px, py) and whose
