@@ -114,6 +114,17 @@ struct vx_arena {
   }
   __device__ __forceinline__ float4 sld_f4(uint32_t off) const { return sld<float4>(off); }
   __device__ __forceinline__ uint4 sld_u4(uint32_t off) const { return sld<uint4>(off); }
+  /* N consecutive 16-B words of one record from one wave-uniform address:
+   * immediate offsets off one pointer, so the loads merge into wide s_loads
+   * (s_load_dwordx16 for a 64-B record) instead of one per word */
+  template <int N>
+  __device__ __forceinline__ void sld_u4n(uint32_t off, uint4* out) const {
+    const uint32_t o = __builtin_amdgcn_readfirstlane(off);
+    const __attribute__((address_space(4))) uint4* p =
+        (const __attribute__((address_space(4))) uint4*)(base + o);
+#pragma unroll
+    for (int i = 0; i < N; ++i) out[i] = p[i];
+  }
   __device__ __forceinline__ float4 ld_f4(uint32_t off) const {
     const auto v = __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0);
     return make_float4(__uint_as_float(v[0]), __uint_as_float(v[1]), __uint_as_float(v[2]),

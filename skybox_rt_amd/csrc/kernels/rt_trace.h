@@ -271,7 +271,8 @@ __device__ __forceinline__ bool slab_nf(float lox, float hix, float loy, float h
 // lane masks straight from one v_cmp (inactive lanes 0), instead of a
 // ballot of a combined bool (which the compiler re-materialises with a
 // v_cndmask + v_cmp pair): ordered a <= b, unsigned a == b, unsigned a <= b
-__device__ __forceinline__ uint64_t mask_fle(float a, float b) { return __builtin_amdgcn_fcmp(a, b, 5); }
+// (fcmpf: the float form; __builtin_amdgcn_fcmp takes doubles and compares in f64)
+__device__ __forceinline__ uint64_t mask_fle(float a, float b) { return __builtin_amdgcn_fcmpf(a, b, 5); }
 __device__ __forceinline__ uint64_t mask_ueq(uint32_t a, uint32_t b) { return __builtin_amdgcn_uicmp(a, b, 32); }
 __device__ __forceinline__ uint64_t mask_ule(uint32_t a, uint32_t b) { return __builtin_amdgcn_uicmp(a, b, 37); }
 
@@ -680,6 +681,15 @@ __device__ __forceinline__ int32_t vwritelane(int32_t v, int32_t val, int32_t la
   asm("v_writelane_b32 %0, %1, m0" : "+v"(v) : "s"(x), "{m0}"(l));
   return v;
 }
+// 1: packet walks load a node (64 B) or a leaf's hoisted triangle records
+// through one pointer, so they merge into wide s_loads
+#ifndef RT_SLD_WIDE
+#define RT_SLD_WIDE 1
+#endif
+__device__ __forceinline__ float4 u4f(const uint4 u) {
+  return make_float4(__uint_as_float(u.x), __uint_as_float(u.y), __uint_as_float(u.z),
+                     __uint_as_float(u.w));
+}
 // wave priority while walking a packet (0: unchanged): the packet walks are
 // the heavy tiles' latency chains
 #ifndef RT_PACKET_PRIO
@@ -708,8 +718,14 @@ __device__ __forceinline__ bool occluded_packet(const Scene& S, const Ray& r, bo
 #endif
       RT_WAVE_ITER(9);
       const uint32_t no = S.nodes4 + 128u * S.num_nodes4 + 64u * (uint32_t)ref;
+#if RT_SLD_WIDE
+      uint4 nw[4];
+      S.A.sld_u4n<4>(no, nw);  // one s_load_dwordx16
+      const uint4 px = nw[0], py = nw[1], pz = nw[2], cf = nw[3];
+#else
       const uint4 px = S.A.sld_u4(no), py = S.A.sld_u4(no + 16), pz = S.A.sld_u4(no + 32),
                   cf = S.A.sld_u4(no + 48);
+#endif
       float lx[4], hx[4], ly[4], hy[4], lz[4], hz[4];
       auto h2 = [](uint32_t u, float& a, float& b) {
         a = (float)__builtin_bit_cast(_Float16, (uint16_t)(u & 0xffffu));
@@ -721,10 +737,22 @@ __device__ __forceinline__ bool occluded_packet(const Scene& S, const Ray& r, bo
       const int32_t c[4] = {(int32_t)cf.x, (int32_t)cf.y, (int32_t)cf.z, (int32_t)cf.w};
       bool h[4];
       uint32_t need = 0u;  // wave-uniform: children some live lane enters
+#if RT_PACKET_BRANCHLESS == 3
+      const uint64_t lm = __ballot(live);  // once per node, not per child
+#endif
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         float tn = 0.0f;
-#if RT_PACKET_BRANCHLESS == 2
+#if RT_PACKET_BRANCHLESS == 3
+        // the per-lane bit as in 1; the wave's child mask from the slab's own
+        // v_cmp ANDed with the node's live mask (no re-materialised ballot)
+        float tf;
+        const bool hs = slab_nf(lx[i], hx[i], ly[i], hy[i], lz[i], hz[i], r, 0.0f, tmax, &tn, &tf);
+        const bool cv = c[i] != RT_EMPTY_REF;
+        h[i] = hs & live & cv;
+        need |= (mask_fle(tn, tf) & lm & (cv ? ~0ull : 0ull)) != 0 ? 1u << i : 0u;
+        continue;
+#elif RT_PACKET_BRANCHLESS == 2
         // lanes off the path and empty slots test against a negative far
         // limit, which the slab test itself rejects (its near value is >= 0):
         // h is one compare, the same value as the masked form below
@@ -776,11 +804,22 @@ __device__ __forceinline__ bool occluded_packet(const Scene& S, const Ray& r, bo
       for (uint32_t q0 = 0; q0 < 4; q0 += H) {
         if (q0 >= count) break;
         float4 ta[H], tb[H], tc[H];
+#if RT_SLD_WIDE
+        {  // the H consecutive records from one address (wide s_loads)
+          uint4 tw[3 * H];
+          S.A.sld_u4n<3 * H>(S.tris + 48u * (first + q0), tw);
+#pragma unroll
+          for (uint32_t j = 0; j < H; ++j) {
+            ta[j] = u4f(tw[3 * j]); tb[j] = u4f(tw[3 * j + 1]); tc[j] = u4f(tw[3 * j + 2]);
+          }
+        }
+#else
 #pragma unroll
         for (uint32_t j = 0; j < H; ++j) {
           const uint32_t to = S.tris + 48u * (first + q0 + j);
           ta[j] = S.A.sld_f4(to); tb[j] = S.A.sld_f4(to + 16); tc[j] = S.A.sld_f4(to + 32);
         }
+#endif
 #pragma unroll
         for (uint32_t j = 0; j < H; ++j) {
           if (q0 + j < count) {
@@ -1164,8 +1203,14 @@ __device__ __forceinline__ int32_t trace_primary_packet(const Scene& S, uint32_t
 #endif
       RT_WAVE_ITER(7);
       const uint32_t o = S.vnodes + 64u * (uint32_t)ref;
+#if RT_SLD_WIDE
+      uint4 vw[4];
+      S.A.sld_u4n<4>(o, vw);  // one s_load_dwordx16
+      const uint4 rl = vw[0], rh = vw[1], zm = vw[2], cf = vw[3];
+#else
       const uint4 rl = S.A.sld_u4(o), rh = S.A.sld_u4(o + 16), zm = S.A.sld_u4(o + 32),
                   cf = S.A.sld_u4(o + 48);
+#endif
       const uint32_t alo[4] = {rl.x, rl.y, rl.z, rl.w}, ahi[4] = {rh.x, rh.y, rh.z, rh.w};
       const uint32_t azm[4] = {zm.x, zm.y, zm.z, zm.w};
       int32_t c[4] = {(int32_t)cf.x, (int32_t)cf.y, (int32_t)cf.z, (int32_t)cf.w};
@@ -1227,12 +1272,23 @@ __device__ __forceinline__ int32_t trace_primary_packet(const Scene& S, uint32_t
       for (uint32_t k0 = 0; k0 < 4; k0 += H) {
         if (k0 >= count) break;
         uint4 A[H], B[H], C[H], D[H];
+#if RT_SLD_WIDE
+        {  // the H consecutive records from one address (wide s_loads)
+          uint4 tw[4 * H];
+          S.A.sld_u4n<4 * H>(S.vtris + 64u * (first + k0), tw);
+#pragma unroll
+          for (uint32_t j = 0; j < H; ++j) {
+            A[j] = tw[4 * j]; B[j] = tw[4 * j + 1]; C[j] = tw[4 * j + 2]; D[j] = tw[4 * j + 3];
+          }
+        }
+#else
 #pragma unroll
         for (uint32_t j = 0; j < H; ++j) {
           const uint32_t o = S.vtris + 64u * (first + k0 + j);
           A[j] = S.A.sld_u4(o); B[j] = S.A.sld_u4(o + 16); C[j] = S.A.sld_u4(o + 32);
           D[j] = S.A.sld_u4(o + 48);
         }
+#endif
 #pragma unroll
         for (uint32_t j = 0; j < H; ++j) {
           if (k0 + j < count) {
