@@ -84,6 +84,14 @@ def main():
             "to_primary": ph(12, 3), "primary": ph(3, 14), "layers": ph(14, 4), "shade": ph(4, 11),
             "plane_queue": ph(11, 5), "to_final_drain": ph(5, 15), "final_drain": ph(15, 13),
             "nonfinal_drains": int((rows[slow, 6] > 0).sum())}
+        # s_memtime cycles waiting on the packet walks' record loads (slot 0
+        # primary, 1 shadow) per wave, and per loop iteration
+        pi = np.maximum(it[slow, 0] + it[slow, 1], 1)
+        si = np.maximum(it[slow, 2], 1)
+        out["slowest50"]["load_wait_cycles"] = {
+            "primary": float(rows[slow, 0].mean()), "shadow": float(rows[slow, 1].mean()),
+            "primary_per_iter": float((rows[slow, 0] / pi).mean()),
+            "shadow_per_iter": float((rows[slow, 1] / si).mean())}
     if path:  # pt stamp image: 10 wave cycles (s_memtime), 4 paired-traversal cycles,
         # 5 vertex steps, 6 post-traversal (bounce-hit shading) cycles
         cyc = rows[:, 10].astype(np.float64)

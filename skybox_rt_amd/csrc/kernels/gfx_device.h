@@ -27,9 +27,14 @@ struct DcState {
 // SCALAR = true: `off` is wave-uniform and the record lands in SGPRs
 template <bool SCALAR = false>
 __device__ __forceinline__ DcState load_dcstate(const vx_arena& A, uint32_t off) {
-  const uint4 a = SCALAR ? A.sld_u4(off) : A.ld_u4(off);
-  const uint4 b = SCALAR ? A.sld_u4(off + 16) : A.ld_u4(off + 16);
-  const uint4 c = SCALAR ? A.sld_u4(off + 32) : A.ld_u4(off + 32);
+  uint4 a, b, c;
+  if constexpr (SCALAR) {  // one pointer: merged wide s_loads
+    uint4 w[3];
+    A.sld_u4n<3>(off, w);
+    a = w[0]; b = w[1]; c = w[2];
+  } else {
+    a = A.ld_u4(off); b = A.ld_u4(off + 16); c = A.ld_u4(off + 32);
+  }
   DcState s;
   s.flags = a.x; s.logw = a.y; s.logh = a.z; s.format = a.w;
   s.filter = b.x; s.wrapu = b.y; s.wrapv = b.z; s.stride = b.w;
@@ -47,9 +52,12 @@ struct Prim {
 
 template <bool SCALAR = false>
 __device__ __forceinline__ void load_prim(const vx_arena& A, uint32_t off, Prim& p) {
+  uint4 sw[SCALAR ? 8 : 1];
+  if constexpr (SCALAR) A.sld_u4n<8>(off, sw);  // two s_load_dwordx16
 #pragma unroll
   for (int i = 0; i < 8; ++i) {
-    const uint4 v = SCALAR ? A.sld_u4(off + 16 * i) : A.ld_u4(off + 16 * i);
+    uint4 v;
+    if constexpr (SCALAR) v = sw[i]; else v = A.ld_u4(off + 16 * i);
     p.w[4 * i + 0] = (int32_t)v.x; p.w[4 * i + 1] = (int32_t)v.y;
     p.w[4 * i + 2] = (int32_t)v.z; p.w[4 * i + 3] = (int32_t)v.w;
   }

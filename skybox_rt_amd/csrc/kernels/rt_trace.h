@@ -177,8 +177,26 @@ __device__ __forceinline__ uint32_t lane_id() {
     if (lane_id() == (uint32_t)__builtin_ctzll(__ballot(1)))                      \
       ((volatile uint32_t*)__vx_mpm_lds)[slot] += 1u;                             \
   } while (0)
+// cycles from issuing a packet walk's record load to its data (rt stamp
+// image: slot 0 primary packets, slot 1 shadow packets; s_memtime, explicit
+// wait; not in the path tracer's stamp image)
+#ifdef RT_TRACE_CYCLES
+#define RT_LD_BEGIN() do {} while (0)
+#define RT_LD_END(slot) do {} while (0)
+#else
+#define RT_LD_BEGIN() const uint64_t rt_ld0 = __builtin_amdgcn_s_memtime()
+#define RT_LD_END(slot)                                                            \
+  do {                                                                             \
+    __builtin_amdgcn_s_waitcnt(0xC07F);                                            \
+    const uint32_t rt_ldd = (uint32_t)(__builtin_amdgcn_s_memtime() - rt_ld0);     \
+    if (lane_id() == (uint32_t)__builtin_ctzll(__ballot(1)))                      \
+      ((volatile uint32_t*)__vx_mpm_lds)[slot] += rt_ldd;                         \
+  } while (0)
+#endif
 #else
 #define RT_WAVE_ITER(slot) do {} while (0)
+#define RT_LD_BEGIN() do {} while (0)
+#define RT_LD_END(slot) do {} while (0)
 #endif
 // RT_TRACE_CYCLES (path-tracer stamp image only): wave cycles spent in the
 // secondary traversal's node loop (slot 11) and leaf rounds (slot 3)
@@ -720,7 +738,9 @@ __device__ __forceinline__ bool occluded_packet(const Scene& S, const Ray& r, bo
       const uint32_t no = S.nodes4 + 128u * S.num_nodes4 + 64u * (uint32_t)ref;
 #if RT_SLD_WIDE
       uint4 nw[4];
+      RT_LD_BEGIN();
       S.A.sld_u4n<4>(no, nw);  // one s_load_dwordx16
+      RT_LD_END(1);
       const uint4 px = nw[0], py = nw[1], pz = nw[2], cf = nw[3];
 #else
       const uint4 px = S.A.sld_u4(no), py = S.A.sld_u4(no + 16), pz = S.A.sld_u4(no + 32),
@@ -807,7 +827,9 @@ __device__ __forceinline__ bool occluded_packet(const Scene& S, const Ray& r, bo
 #if RT_SLD_WIDE
         {  // the H consecutive records from one address (wide s_loads)
           uint4 tw[3 * H];
+          RT_LD_BEGIN();
           S.A.sld_u4n<3 * H>(S.tris + 48u * (first + q0), tw);
+          RT_LD_END(1);
 #pragma unroll
           for (uint32_t j = 0; j < H; ++j) {
             ta[j] = u4f(tw[3 * j]); tb[j] = u4f(tw[3 * j + 1]); tc[j] = u4f(tw[3 * j + 2]);
@@ -1205,7 +1227,9 @@ __device__ __forceinline__ int32_t trace_primary_packet(const Scene& S, uint32_t
       const uint32_t o = S.vnodes + 64u * (uint32_t)ref;
 #if RT_SLD_WIDE
       uint4 vw[4];
+      RT_LD_BEGIN();
       S.A.sld_u4n<4>(o, vw);  // one s_load_dwordx16
+      RT_LD_END(0);
       const uint4 rl = vw[0], rh = vw[1], zm = vw[2], cf = vw[3];
 #else
       const uint4 rl = S.A.sld_u4(o), rh = S.A.sld_u4(o + 16), zm = S.A.sld_u4(o + 32),
@@ -1275,7 +1299,9 @@ __device__ __forceinline__ int32_t trace_primary_packet(const Scene& S, uint32_t
 #if RT_SLD_WIDE
         {  // the H consecutive records from one address (wide s_loads)
           uint4 tw[4 * H];
+          RT_LD_BEGIN();
           S.A.sld_u4n<4 * H>(S.vtris + 64u * (first + k0), tw);
+          RT_LD_END(0);
 #pragma unroll
           for (uint32_t j = 0; j < H; ++j) {
             A[j] = tw[4 * j]; B[j] = tw[4 * j + 1]; C[j] = tw[4 * j + 2]; D[j] = tw[4 * j + 3];
@@ -1365,8 +1391,9 @@ __device__ __forceinline__ int32_t resolve_layers(const Scene& S, uint32_t px, u
                                                   int32_t spid, Counters& cnt) {
   uint64_t pend = __ballot(need);
   for (uint32_t k = 0; pend != 0 && k < S.num_layer; ++k) {
-    const uint32_t lo = S.vlayers + 64u * k;
-    const uint4 A = S.A.sld_u4(lo), B = S.A.sld_u4(lo + 16), C = S.A.sld_u4(lo + 32);
+    uint4 lw[3];
+    S.A.sld_u4n<3>(S.vlayers + 64u * k, lw);  // one pointer: merged wide s_loads
+    const uint4 A = lw[0], B = lw[1], C = lw[2];
     const bool mine = (pend & (1ull << lane_id())) != 0;
 #ifdef RT_INSTRUMENT
     cnt.layer_tests += mine;
