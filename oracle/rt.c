@@ -344,31 +344,22 @@ static inline void vis_test(const rt_ctx_t* c, int pid, uint32_t px, uint32_t py
 }
 
 /* rt_vnode_t step (kernels' vnode_step): children whose rectangle holds the
- * pixel and whose depth bound can still win, sorted by that bound with the
- * 5-exchange network, nearest returned, the others pushed farthest first */
+ * pixel and whose depth bound can still win, in slot order -- the slots are
+ * stored in ascending depth bound (vis.c / vis.cpp SortSlots) -- the first
+ * returned, the others pushed last slot first */
 static int32_t vnode_step(const uint32_t* n, uint32_t px, uint32_t py, uint32_t bz,
                           int32_t* stack, int* sp) {
-  uint32_t key[4];
-  int32_t ref[4];
+  int idx[4];
   int cnt = 0;
   for (int i = 0; i < 4; ++i) {
-    ref[i] = (int32_t)n[12 + i];
-    const int h = ref[i] != BVH_EMPTY && rect_in(n[i], px) && rect_in(n[4 + i], py) && n[8 + i] <= bz;
-    key[i] = h ? n[8 + i] : 0xffffffffu;
-    cnt += h;
-  }
-  static const int net[5][2] = {{0, 1}, {2, 3}, {0, 2}, {1, 3}, {1, 2}};
-  for (int e = 0; e < 5; ++e) {
-    const int a = net[e][0], b = net[e][1];
-    if (key[b] < key[a]) {
-      const uint32_t tk = key[a]; key[a] = key[b]; key[b] = tk;
-      const int32_t tr = ref[a]; ref[a] = ref[b]; ref[b] = tr;
-    }
+    const int h = (int32_t)n[12 + i] != BVH_EMPTY && rect_in(n[i], px) && rect_in(n[4 + i], py) &&
+                  n[8 + i] <= bz;
+    if (h) idx[cnt++] = i;
   }
   if (cnt == 0) return BVH_EMPTY;
-  for (int i = cnt - 1; i >= 1; --i)
-    if (*sp < BVH_STACK) stack[(*sp)++] = ref[i];
-  return ref[0];
+  for (int j = cnt - 1; j >= 1; --j)
+    if (*sp < BVH_STACK) stack[(*sp)++] = (int32_t)n[12 + idx[j]];
+  return (int32_t)n[12 + idx[0]];
 }
 
 static int vis_trace(const rt_ctx_t* c, uint32_t px, uint32_t py, uint64_t* visits, uint64_t* tests) {
@@ -400,8 +391,8 @@ static int vis_trace(const rt_ctx_t* c, uint32_t px, uint32_t py, uint64_t* visi
 /* Packet form (the kernels' trace_primary_packet, RT_VIS_PACKET): the
  * wave's pixels walk the tree together -- a child is entered when some
  * lane's pixel lies in its rectangle with a bound that can still beat that
- * lane's best; entered children sorted by bound, nearest taken, the others
- * pushed farthest first; every lane tests every leaf primitive of the walk.
+ * lane's best; entered children in slot order (= ascending bound), the
+ * first taken, the others pushed last first; every lane tests every leaf primitive of the walk.
  * n lanes at (px[i], py[i]); out[i] = winner.  Visits and tests count once
  * per packet. */
 #define PK_LANES 64
@@ -418,25 +409,15 @@ static void vis_trace_packet(const rt_ctx_t* c, int n, const uint32_t* px, const
     if (ref >= 0) {
       ++*visits;
       const uint32_t* nd = c->vnodes + (size_t)ref * 16;
-      uint32_t key[4];
       int32_t r[4];
       int cnt = 0;
-      for (int k = 0; k < 4; ++k) {
-        r[k] = (int32_t)nd[12 + k];
+      for (int k = 0; k < 4; ++k) {  /* needed children in slot order (sorted slots) */
+        const int32_t ck = (int32_t)nd[12 + k];
         int need = 0;
-        if (r[k] != BVH_EMPTY)
+        if (ck != BVH_EMPTY)
           for (int i = 0; i < n && !need; ++i)
             need = rect_in(nd[k], px[i]) && rect_in(nd[4 + k], py[i]) && nd[8 + k] <= bz[i];
-        key[k] = need ? nd[8 + k] : 0xffffffffu;
-        cnt += need;
-      }
-      static const int net[5][2] = {{0, 1}, {2, 3}, {0, 2}, {1, 3}, {1, 2}};
-      for (int e = 0; e < 5; ++e) {
-        const int a = net[e][0], b = net[e][1];
-        if (key[b] < key[a]) {
-          const uint32_t tk = key[a]; key[a] = key[b]; key[b] = tk;
-          const int32_t tr = r[a]; r[a] = r[b]; r[b] = tr;
-        }
+        if (need) r[cnt++] = ck;
       }
       if (cnt > 0) {
         for (int i = cnt - 1; i >= 1; --i)

@@ -147,6 +147,12 @@ static cover_t vn_of(vn_ctx_t* c, int32_t ref, int depth) {
     o[12 + i] = k.any ? (uint32_t)cr : 0xffffffffu;
     cover_add(&r, &k);
   }
+  /* slots in ascending depth bound, stable (vis.cpp SortSlots) */
+  for (int i = 1; i < 4; ++i)
+    for (int j = i; j > 0 && o[8 + j] < o[8 + j - 1]; --j)
+      for (int f = 0; f < 16; f += 4) {
+        const uint32_t t = o[f + j]; o[f + j] = o[f + j - 1]; o[f + j - 1] = t;
+      }
   return r;
 }
 

@@ -139,6 +139,19 @@ struct Cover {
   }
 };
 
+// a node's slots in ascending depth bound (stable; empty slots, bound
+// RT_VIS_ZMIN_NONE, last): the order the primary walks enter children, so
+// the kernels take needed children in slot order with no sort per step
+void SortSlots(rt_vnode_t& n) {
+  for (int i = 1; i < 4; ++i)
+    for (int j = i; j > 0 && n.zmin[j] < n.zmin[j - 1]; --j) {
+      std::swap(n.lo[j], n.lo[j - 1]);
+      std::swap(n.hi[j], n.hi[j - 1]);
+      std::swap(n.zmin[j], n.zmin[j - 1]);
+      std::swap(n.child[j], n.child[j - 1]);
+    }
+}
+
 struct NodeBuilder {
   const std::vector<std::array<int32_t, 4>>& refs;
   const std::vector<int32_t>& pids;
@@ -183,6 +196,7 @@ struct NodeBuilder {
       n.zmin[i] = k.any ? k.zmin : RT_VIS_ZMIN_NONE;
       c.add(k);
     }
+    SortSlots(n);
     return c;
   }
 };

@@ -425,6 +425,18 @@ __device__ void phase_climb(const rt_setup_arg_t* a) {
         vn[cur].child[s] = c.any ? r[s] : RT_EMPTY_REF;
         if (c.any) cover_add_corners(&u, vn[cur].lo[s], vn[cur].hi[s], c.zmin);
       }
+      // every slot of cur is final: ascending depth bound, stable (vis.cpp SortSlots)
+      {
+        rt_vnode_t n = vn[cur];
+        for (int i = 1; i < 4; ++i)
+          for (int j = i; j > 0 && n.zmin[j] < n.zmin[j - 1]; --j) {
+            const uint32_t lo = n.lo[j], hi = n.hi[j], zm = n.zmin[j];
+            const int32_t ch = n.child[j];
+            n.lo[j] = n.lo[j - 1]; n.hi[j] = n.hi[j - 1]; n.zmin[j] = n.zmin[j - 1]; n.child[j] = n.child[j - 1];
+            n.lo[j - 1] = lo; n.hi[j - 1] = hi; n.zmin[j - 1] = zm; n.child[j - 1] = ch;
+          }
+        vn[cur] = n;
+      }
       const int32_t p = parent[cur];
       if (p < 0) break;
       const uint32_t pn = (uint32_t)p >> 2, ps = (uint32_t)p & 3u;

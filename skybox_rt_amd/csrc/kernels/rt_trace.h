@@ -1088,9 +1088,10 @@ __device__ __forceinline__ void vis_test(const uint4& A, const uint4& B, const u
 }
 
 // rt_vnode_t step: children whose pixel rectangle holds (px, py) and whose
-// depth bound can still win, ordered by that bound (the same 5-exchange
-// network as node4_step, unsigned keys, misses last); the nearest is
-// returned, the others pushed farthest first.  SCALAR: every active lane is
+// depth bound can still win, in slot order -- the setup stores a node's
+// slots in ascending depth bound (vis.cpp SortSlots), so that is nearest
+// first with no sort per step; the first is returned, the others pushed last
+// slot first.  SCALAR: every active lane is
 // at this node (s_load into SGPRs).
 template <bool SCALAR>
 __device__ __forceinline__ int32_t vnode_step(const Scene& S, uint32_t ref, uint32_t px, uint32_t py,
@@ -1102,33 +1103,18 @@ __device__ __forceinline__ int32_t vnode_step(const Scene& S, uint32_t ref, uint
   const uint32_t azm[4] = {zm.x, zm.y, zm.z, zm.w};
   int32_t c[4] = {(int32_t)cf.x, (int32_t)cf.y, (int32_t)cf.z, (int32_t)cf.w};
   const uint32_t pp = px > 0xffffu ? 0xffffffffu : px | (py << 16);
-  uint32_t k[4];
-  int n = 0;
+  // the slots are stored in ascending depth bound (vis.cpp SortSlots): the
+  // needed children in slot order are nearest first
+  uint32_t need = 0u;
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const bool h = c[i] != RT_EMPTY_REF && rect2_in(alo[i], ahi[i], pp) && azm[i] <= bz;
-    k[i] = h ? azm[i] : 0xffffffffu;
-    n += h ? 1 : 0;
-  }
-  auto cx = [&](int a, int b) {
-    const bool s = k[b] < k[a];
-    const uint32_t ka = k[a], kb = k[b];
-    const int32_t ca = c[a], cb = c[b];
-    k[a] = s ? kb : ka;
-    k[b] = s ? ka : kb;
-    c[a] = s ? cb : ca;
-    c[b] = s ? ca : cb;
-  };
-  cx(0, 1);
-  cx(2, 3);
-  cx(0, 2);
-  cx(1, 3);
-  cx(1, 2);
-  if (n == 0) return RT_EMPTY_REF;
-  if (n >= 4) st.push(c[3]);
-  if (n >= 3) st.push(c[2]);
-  if (n >= 2) st.push(c[1]);
-  return c[0];
+  for (int i = 0; i < 4; ++i)
+    need |= (c[i] != RT_EMPTY_REF && rect2_in(alo[i], ahi[i], pp) && azm[i] <= bz) ? 1u << i : 0u;
+  if (need == 0u) return RT_EMPTY_REF;
+#pragma unroll
+  for (int i = 3; i >= 1; --i)  // the others pushed farthest (last slot) first
+    if ((need >> i) & 1u && (need & ((1u << i) - 1u))) st.push(c[i]);
+  const int f = __builtin_ctz(need);
+  return f == 0 ? c[0] : f == 1 ? c[1] : f == 2 ? c[2] : c[3];
 }
 
 // The primary ray's hit: the draw3d depth-test winner among the geometry
@@ -1191,8 +1177,9 @@ __device__ __forceinline__ int32_t trace_primary_lane(const Scene& S, uint32_t p
 // Packet form (RT_VIS_PACKET): the wave's pixels walk the tree together.
 // A child is entered when, for some lane, the pixel lies in the child's
 // rectangle and the child's depth bound can still beat that lane's best
-// (ballot); the entered children are ordered by their bound (the 5-exchange
-// network on wave-uniform keys) and the others pushed farthest first on the
+// (ballot); the entered children are taken in slot order (= ascending
+// bound, vis.cpp SortSlots: no sorting network per step) and the others
+// pushed farthest first on the
 // wave's LDS stack (entries stride 64 in `stack`, written by lane 0).  Node
 // and leaf records are wave-uniform: scalar loads, one per record for the
 // wave instead of 64 lanes' gathers.  Each lane runs the exact coverage and
@@ -1238,8 +1225,7 @@ __device__ __forceinline__ int32_t trace_primary_packet(const Scene& S, uint32_t
       const uint32_t alo[4] = {rl.x, rl.y, rl.z, rl.w}, ahi[4] = {rh.x, rh.y, rh.z, rh.w};
       const uint32_t azm[4] = {zm.x, zm.y, zm.z, zm.w};
       int32_t c[4] = {(int32_t)cf.x, (int32_t)cf.y, (int32_t)cf.z, (int32_t)cf.w};
-      uint32_t k[4];
-      int n = 0;
+      uint32_t need = 0u;  // wave-uniform: children some lane must enter
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         // lanes whose pixel is in the child's rectangle and whose best depth
@@ -1247,31 +1233,17 @@ __device__ __forceinline__ int32_t trace_primary_packet(const Scene& S, uint32_t
         const rt_u16x2 cl = __builtin_elementwise_min(
             __builtin_elementwise_max(__builtin_bit_cast(rt_u16x2, pp), __builtin_bit_cast(rt_u16x2, alo[i])),
             __builtin_bit_cast(rt_u16x2, ahi[i]));
-        const bool need = c[i] != RT_EMPTY_REF &&
-                          (mask_ueq(__builtin_bit_cast(uint32_t, cl), pp) & mask_ule(azm[i], bz)) != 0;
-        k[i] = need ? azm[i] : 0xffffffffu;
-        n += need ? 1 : 0;
+        need |= (c[i] != RT_EMPTY_REF &&
+                 (mask_ueq(__builtin_bit_cast(uint32_t, cl), pp) & mask_ule(azm[i], bz)) != 0)
+                    ? 1u << i : 0u;
       }
-      auto cx = [&](int a, int b) {
-        const bool s = k[b] < k[a];
-        const uint32_t ka = k[a], kb = k[b];
-        const int32_t ca = c[a], cb = c[b];
-        k[a] = s ? kb : ka;
-        k[b] = s ? ka : kb;
-        c[a] = s ? cb : ca;
-        c[b] = s ? ca : cb;
-      };
-      cx(0, 1);
-      cx(2, 3);
-      cx(0, 2);
-      cx(1, 3);
-      cx(1, 2);
-      if (n > 0) {
-        // c[n-1] .. c[1] pushed (farthest first); unrolled over the slots so
-        // each c[i] is a fixed register, not a dynamically indexed one
+      if (need != 0u) {
+        // the slots are stored in ascending depth bound (vis.cpp SortSlots):
+        // the first needed slot is entered, the others pushed last slot first;
+        // unrolled over the slots so each c[i] is a fixed register
 #pragma unroll
         for (int i = 3; i >= 1; --i) {
-          if (i < n && sp < RT_MAX_STACK) {
+          if ((need >> i) & 1u && (need & ((1u << i) - 1u)) && sp < RT_MAX_STACK) {
 #if RT_PACKET_VSTACK
             vstk = vwritelane(vstk, c[i], sp);
 #else
@@ -1280,7 +1252,8 @@ __device__ __forceinline__ int32_t trace_primary_packet(const Scene& S, uint32_t
             ++sp;
           }
         }
-        ref = c[0];
+        const int f = __builtin_ctz(need);
+        ref = f == 0 ? c[0] : f == 1 ? c[1] : f == 2 ? c[2] : c[3];
         continue;
       }
     } else {
