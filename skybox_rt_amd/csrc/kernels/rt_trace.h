@@ -79,6 +79,7 @@ struct Scene {
   uint32_t num_nodes, num_nodes4, num_layer, num_geom, flags, width, height;
   uint32_t shard_index, shard_count, tiles_x, clear_color, bounces, seed, split_tiles, split_log;
   float sx, sy, light[3];
+  uint64_t argp;  // the argument block (constant address space), for lazy_args
   // the BVH staged in LDS by the workgroup (RT_LDS_SCENE images), or null
   const float4* lnodes = nullptr;
   const float4* ltris = nullptr;
@@ -126,6 +127,7 @@ __device__ __forceinline__ Scene load_scene(const rt_kernel_arg_t* ga) {
   const rt_kernel_arg_t* a = ga;
 #endif
   Scene s;
+  s.argp = (uint64_t)a;
   s.A = vx_arena::get();
   s.nodes = (uint32_t)a->nodes_addr;
   s.nodes4 = (uint32_t)a->nodes4_addr;
@@ -684,6 +686,10 @@ __device__ __forceinline__ int32_t trace_impl(const Scene& S, const Ray& r, floa
 #ifndef RT_PACKET_LEAF_HOIST
 #define RT_PACKET_LEAF_HOIST 2
 #endif
+// the same for the shadow packets' leaves (48-B records)
+#ifndef RT_SHADOW_LEAF_HOIST
+#define RT_SHADOW_LEAF_HOIST RT_PACKET_LEAF_HOIST
+#endif
 // 1: a packet walk's (wave-uniform) stack lives in one VGPR, entry i in lane
 // i (v_writelane / v_readlane: no LDS round trip on the pop -> node-load
 // chain); 0: the wave's LDS stack column
@@ -817,9 +823,9 @@ __device__ __forceinline__ bool occluded_packet(const Scene& S, const Ray& r, bo
       const uint32_t first = (lr >> 4) & 0x07ffffffu, count = (lr & 15u) + 1u;
       RT_WAVE_ITER(9);
       bool lv = live;
-#if RT_PACKET_LEAF_HOIST > 1
-      // RT_PACKET_LEAF_HOIST slots in flight at once (3 padding records)
-      constexpr uint32_t H = RT_PACKET_LEAF_HOIST;
+#if RT_SHADOW_LEAF_HOIST > 1
+      // RT_SHADOW_LEAF_HOIST slots in flight at once (3 padding records)
+      constexpr uint32_t H = RT_SHADOW_LEAF_HOIST;
 #pragma unroll
       for (uint32_t q0 = 0; q0 < 4; q0 += H) {
         if (q0 >= count) break;
@@ -1398,11 +1404,35 @@ struct TaskPix {
   uint32_t idx;  // pixel of the tile in block order: (8x8 block) * 64 + lane of the block
   bool live;
 };
-__device__ __forceinline__ TaskPix task_map(const Scene& S, uint32_t t) {
+// 1: the task-map fields (split, order, shard) are read from the argument
+// block where they are used, through an opaque pointer, instead of living in
+// SGPRs across the walks (the chunk loop keeps loop-invariant values live)
+#ifndef RT_LAZY_TASK_ARGS
+#define RT_LAZY_TASK_ARGS 1
+#endif
+struct TaskArgs {
+  uint32_t split_tiles, split_log, order, shard_index, shard_count, tiles_x;
+};
+__device__ __forceinline__ TaskArgs task_args(const Scene& S) {
+  TaskArgs t;
+#if RT_LAZY_TASK_ARGS
+  uint64_t p = S.argp;
+  asm volatile("" : "+s"(p));  // opaque: re-issued here, not hoisted or CSE'd
+  const __attribute__((address_space(4))) rt_kernel_arg_t* a =
+      (const __attribute__((address_space(4))) rt_kernel_arg_t*)p;
+  t.split_tiles = a->split_tiles; t.split_log = a->split_log; t.order = (uint32_t)a->order_addr;
+  t.shard_index = a->shard_index; t.shard_count = a->shard_count; t.tiles_x = a->tiles_x;
+#else
+  t.split_tiles = S.split_tiles; t.split_log = S.split_log; t.order = S.order;
+  t.shard_index = S.shard_index; t.shard_count = S.shard_count; t.tiles_x = S.tiles_x;
+#endif
+  return t;
+}
+__device__ __forceinline__ TaskPix task_map(const Scene& S, const TaskArgs& T, uint32_t t) {
   TaskPix m;
-  const uint32_t pl = S.split_log;  // split tiles: 2^pl pixels per wave (pl <= 6)
+  const uint32_t pl = T.split_log;  // split tiles: 2^pl pixels per wave (pl <= 6)
   const uint32_t cl = 16u - pl;      // log2 tasks per split tile (1024 >> pl chunks of 64)
-  const uint32_t hs = S.split_tiles << cl;
+  const uint32_t hs = T.split_tiles << cl;
   uint32_t pos;
   if (t < hs) {
     const uint32_t sub = 6u - pl;    // log2 chunks per 8x8 block
@@ -1411,19 +1441,23 @@ __device__ __forceinline__ TaskPix task_map(const Scene& S, uint32_t t) {
     m.idx = ((c >> sub) << 6) + ((c & ((1u << sub) - 1u)) << pl) + (ln & ((1u << pl) - 1u));
     m.live = ln < (1u << pl);
   } else {
-    pos = S.split_tiles + ((t - hs) >> 10);
+    pos = T.split_tiles + ((t - hs) >> 10);
     m.idx = t & 1023u;
     m.live = true;
   }
-  m.lt = S.order ? S.A.ld_u32(S.order + 4u * pos) : pos;
+  m.lt = T.order ? S.A.ld_u32(T.order + 4u * pos) : pos;
   return m;
+}
+__device__ __forceinline__ TaskPix task_map(const Scene& S, uint32_t t) {
+  return task_map(S, task_args(S), t);
 }
 
 __device__ __forceinline__ void task_pixel(const Scene& S, uint32_t t, uint32_t* x, uint32_t* y) {
-  const TaskPix m = task_map(S, t);
+  const TaskArgs T = task_args(S);
+  const TaskPix m = task_map(S, T, t);
   const uint32_t blk = m.idx >> 6, ln = m.idx & 63u;
-  const uint32_t gt = S.shard_index + m.lt * S.shard_count;
-  const uint32_t tx = gt % S.tiles_x, ty = gt / S.tiles_x;
+  const uint32_t gt = T.shard_index + m.lt * T.shard_count;
+  const uint32_t tx = gt % T.tiles_x, ty = gt / T.tiles_x;
   *x = m.live ? (tx << RT_TILE_LOG) + ((blk & 3u) << 3) + (ln & 7u) : 0xffffffffu;  // dead lane:
   *y = (ty << RT_TILE_LOG) + ((blk >> 2) << 3) + (ln >> 3);                          // off-image
 }
