@@ -571,6 +571,51 @@ static int configure_vis(rt_renderer* r, const std::vector<rt_prim_t>& prims,
       upload(r->dev, vl.data(), vl.size() * sizeof(rt_vtri_t), &r->vlayers, &a.vlayers_addr) ||
       upload(r->dev, vg.data(), vg.size() * sizeof(rt_vtri_t), &r->vgeom, &a.vgeom_addr))
     return -1;
+  // experiment (env RT_BLOCK_LISTS=1, RT_BLOCK_LIST images): per 8x8 pixel
+  // block, the geometry primitives whose covered rectangle reaches it, in
+  // ascending depth bound, with the union rectangle of each record and the
+  // ones after it, so a wave can resolve its block's primary visibility by
+  // scanning the list and stop early instead of walking the tree
+  a.blist_nbx = 0;
+  a.blist_addr = a.bidx_addr = a.bsuf_addr = 0;
+  if (std::getenv("RT_BLOCK_LISTS") && std::atoi(std::getenv("RT_BLOCK_LISTS")) != 0) {
+    const uint32_t nbx = (a.width + 7) / 8, nby = (a.height + 7) / 8;
+    std::vector<std::vector<std::pair<uint32_t, uint32_t>>> lists((size_t)nbx * nby);
+    for (uint32_t k = 0; k < (uint32_t)s->geometry.size(); ++k) {
+      const rt::VisPrim& v = vis[s->geometry[k]];
+      if (!v.any) continue;
+      const uint32_t x0 = (v.rx & 0xffffu) >> 3, x1 = (v.rx >> 16) >> 3;
+      const uint32_t y0 = (v.ry & 0xffffu) >> 3, y1 = (v.ry >> 16) >> 3;
+      for (uint32_t by = y0; by <= y1 && by < nby; ++by)
+        for (uint32_t bx = x0; bx <= x1 && bx < nbx; ++bx) lists[(size_t)by * nbx + bx].push_back({v.zmin, k});
+    }
+    std::vector<rt_vtri_t> recs;
+    std::vector<uint32_t> idx, suf;
+    for (auto& l : lists) {
+      std::sort(l.begin(), l.end());
+      idx.push_back((uint32_t)recs.size());
+      idx.push_back((uint32_t)l.size());
+      const size_t base = recs.size();
+      for (auto& e : l) recs.push_back(vg[e.second]);
+      std::vector<uint32_t> lo(l.size()), hi(l.size());
+      uint32_t ux0 = 0xffffu, uy0 = 0xffffu, ux1 = 0, uy1 = 0;
+      for (size_t i = l.size(); i-- > 0;) {
+        const rt_vtri_t& t = recs[base + i];
+        ux0 = std::min(ux0, t.rx & 0xffffu); ux1 = std::max(ux1, t.rx >> 16);
+        uy0 = std::min(uy0, t.ry & 0xffffu); uy1 = std::max(uy1, t.ry >> 16);
+        lo[i] = ux0 | (uy0 << 16);
+        hi[i] = ux1 | (uy1 << 16);
+      }
+      for (size_t i = 0; i < l.size(); ++i) { suf.push_back(lo[i]); suf.push_back(hi[i]); }
+    }
+    recs.push_back(rt::MakeVisTri(rt_prim_t{}, rt::VisPrim{}, -1));  // padding: pairs are loaded
+    suf.push_back(0xffffffffu); suf.push_back(0xfffefffeu);
+    a.blist_nbx = nbx;
+    if (upload(r->dev, recs.data(), recs.size() * sizeof(rt_vtri_t), &r->blist, &a.blist_addr) ||
+        upload(r->dev, idx.data(), idx.size() * 4, &r->bidx, &a.bidx_addr) ||
+        upload(r->dev, suf.data(), suf.size() * 4, &r->bsuf, &a.bsuf_addr))
+      return -1;
+  }
   return 0;
 }
 

@@ -35,6 +35,7 @@ struct rt_renderer {
   vx_buffer_h ptris = nullptr, geom = nullptr, oms = nullptr, bbox = nullptr, zbuf = nullptr;
   vx_buffer_h order = nullptr;
   vx_buffer_h vnodes = nullptr, vtris = nullptr, vlayers = nullptr, vgeom = nullptr;
+  vx_buffer_h blist = nullptr, bidx = nullptr, bsuf = nullptr;  // RT_BLOCK_LISTS experiment
   vx_buffer_h gather_recv = nullptr, gather_image = nullptr;  // rank 0 of rt_render_gather
   vx_buffer_h prims = nullptr, cbuf = nullptr, args = nullptr;
   // device-side setup (device_setup.cpp, kernels/rt_setup.hip): the image,
@@ -70,7 +71,8 @@ struct rt_renderer {
                            &krnl[2][1], &krnl[3][0], &nodes, &nodes4, &tris, &layers, &dcs, &tex,
                            &ptris, &geom, &oms, &bbox, &zbuf, &order, &vnodes, &vtris, &vlayers,
                            &vgeom, &gather_recv, &gather_image, &prims, &cbuf, &args,
-                           &setup_krnl, &verts, &pdc, &dcz, &layer_list, &geometry_list, &vis};
+                           &setup_krnl, &verts, &pdc, &dcz, &layer_list, &geometry_list, &vis,
+                           &blist, &bidx, &bsuf};
     for (auto* b : bufs) {
       if (*b) vx_mem_free(*b);
       *b = nullptr;

@@ -192,5 +192,8 @@ typedef struct {
   uint64_t vtris_addr;     // rt_vtri_t per leaf triangle record (+3 padding records)
   uint64_t vgeom_addr;     // rt_vtri_t per geometry primitive, ascending pid (flat mode)
   uint32_t split_log;      // split tiles run 2^split_log pixels per wave (5: 32, an 8x4 half block)
-  uint32_t pad5;
+  uint32_t blist_nbx;      // experiment (RT_BLOCK_LIST images): 8x8 blocks per row, 0 = no lists
+  uint64_t blist_addr;     // per 8x8 block: its candidate rt_vtri_t records, ascending depth bound
+  uint64_t bidx_addr;      // per block: (first record, count)
+  uint64_t bsuf_addr;      // per list record: union rectangle (lo, hi corners) of it and the rest
 } rt_kernel_arg_t;

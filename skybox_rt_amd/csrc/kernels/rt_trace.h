@@ -80,6 +80,9 @@ struct Scene {
   uint32_t shard_index, shard_count, tiles_x, clear_color, bounces, seed, split_tiles, split_log;
   float sx, sy, light[3];
   uint64_t argp;  // the argument block (constant address space), for lazy_args
+#if RT_BLOCK_LIST
+  uint32_t blist, bidx, bsuf, blist_nbx;  // per-block candidate lists (experiment)
+#endif
   // the BVH staged in LDS by the workgroup (RT_LDS_SCENE images), or null
   const float4* lnodes = nullptr;
   const float4* ltris = nullptr;
@@ -148,6 +151,12 @@ __device__ __forceinline__ Scene load_scene(const rt_kernel_arg_t* ga) {
   s.seed = a->seed;
   s.split_tiles = a->split_tiles;
   s.split_log = a->split_log;
+#if RT_BLOCK_LIST
+  s.blist = (uint32_t)a->blist_addr;
+  s.bidx = (uint32_t)a->bidx_addr;
+  s.bsuf = (uint32_t)a->bsuf_addr;
+  s.blist_nbx = a->blist_nbx;
+#endif
   s.num_nodes = a->num_nodes;
   s.num_nodes4 = a->num_nodes4;
   s.num_layer = a->num_layer_tris;
@@ -705,6 +714,9 @@ __device__ __forceinline__ int32_t vwritelane(int32_t v, int32_t val, int32_t la
   asm("v_writelane_b32 %0, %1, m0" : "+v"(v) : "s"(x), "{m0}"(l));
   return v;
 }
+#ifndef RT_BLOCK_LIST
+#define RT_BLOCK_LIST 0
+#endif
 // 1: packet walks load a node (64 B) or a leaf's hoisted triangle records
 // through one pointer, so they merge into wide s_loads
 #ifndef RT_SLD_WIDE
@@ -1332,8 +1344,39 @@ __device__ __forceinline__ int32_t trace_primary_packet(const Scene& S, uint32_t
 }
 
 // every lane of the wave calls it; lanes with !act get -1
+#if RT_BLOCK_LIST
+// Experiment: the wave's 8x8 block resolved from its candidate list (host
+// built, RT_BLOCK_LISTS=1): records in ascending depth bound, two per round,
+// every lane runs the exact test; the scan stops once no lane can change its
+// winner -- its pixel is outside the union rectangle of the remaining
+// records, or their smallest bound exceeds its best depth word.  Same
+// winners as the walk (vis_better is a strict order); counters not kept.
+__device__ __forceinline__ int32_t block_primary(const Scene& S, uint32_t px, uint32_t py, bool act,
+                                                 bool tie_high) {
+  const uint32_t bx = (uint32_t)__builtin_amdgcn_readfirstlane(px >> 3);
+  const uint32_t by = (uint32_t)__builtin_amdgcn_readfirstlane(py >> 3);
+  if (!act) px = 0xffffffffu;
+  const uint32_t pp = px > 0xffffu ? 0xffffffffu : px | (py << 16);
+  const uint2 oc = S.A.sld<uint2>(S.bidx + 8u * (by * S.blist_nbx + bx));
+  uint32_t bz = VX_OM_DEPTH_MASK;
+  int32_t bpid = -1;
+  for (uint32_t k = 0; k < oc.y; k += 2) {
+    uint4 tw[8];
+    S.A.sld_u4n<8>(S.blist + 64u * (oc.x + k), tw);
+    const uint2 sr = S.A.sld<uint2>(S.bsuf + 8u * (oc.x + k));
+    if (__ballot(rect2_in(sr.x, sr.y, pp) && tw[3].w <= bz) == 0) break;
+    vis_test(tw[0], tw[1], tw[2], tw[3], px, py, tie_high, bz, bpid);
+    if (k + 1 < oc.y) vis_test(tw[4], tw[5], tw[6], tw[7], px, py, tie_high, bz, bpid);
+  }
+  return act ? bpid : -1;
+}
+#endif
+
 __device__ __forceinline__ int32_t trace_primary(const Scene& S, uint32_t px, uint32_t py, bool act,
                                                  bool tie_high, int32_t* stack, Counters& cnt) {
+#if RT_BLOCK_LIST
+  if (S.blist_nbx) return block_primary(S, px, py, act, tie_high);
+#endif
 #if RT_VIS_PACKET
   const int32_t h = trace_primary_packet(S, px, py, act, tie_high, stack, cnt);
   return act ? h : -1;
