@@ -95,6 +95,9 @@ typedef struct {
   uint32_t vis_per_lane;            /* BVH mode: 1 = primary rays walk the tree one pixel
                                        at a time (RT_VIS_PACKET=0 images), 0 = per wave packet
                                        (the default images; full frames only) */
+  uint32_t vis_lists;               /* BVH mode, not path: 1 = primary visibility from the
+                                       per-8x8-block candidate lists (rt_app.cpp
+                                       build_block_lists, the kernels' block_primary) */
 } orc_rt_params_t;
 
 #define ORC_RT_SHADOWS 0x1u

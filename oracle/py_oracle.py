@@ -52,7 +52,7 @@ class RtParamsC(C.Structure):
                 ("light", C.c_float * 3), ("clear_color", C.c_uint32),
                 ("bounces", C.c_uint32), ("seed", C.c_uint32), ("nthreads", C.c_uint32),
                 ("row_begin", C.c_uint32), ("row_end", C.c_uint32), ("row_step", C.c_uint32),
-                ("vis_per_lane", C.c_uint32)]
+                ("vis_per_lane", C.c_uint32), ("vis_lists", C.c_uint32)]
 
 
 class RtCountersC(C.Structure):
@@ -179,9 +179,12 @@ def vis_prims(oscene: OracleScene, width: int, height: int) -> np.ndarray:
 
 def rt_params(width, height, shadows=True, light=(0.0, 60.0, 80.0), nthreads=1,
               clear_color=CLEAR_COLOR, row_begin=0, row_end=0, row_step=0,
-              path=False, bounces=4, seed=PT_SEED, vis_per_lane=False):
+              path=False, bounces=4, seed=PT_SEED, vis_per_lane=False, vis_lists=None):
     p = RtParamsC()
     p.vis_per_lane = 1 if vis_per_lane else 0
+    # the product resolves primary visibility of primary+shadow frames from
+    # per-block candidate lists (its default); path tracing walks the tree
+    p.vis_lists = (0 if (path or vis_per_lane) else 1) if vis_lists is None else int(bool(vis_lists))
     p.width, p.height = width, height
     p.flags = (RT_SHADOWS if shadows else 0) | (RT_PATH if path else 0)
     p.bounces, p.seed = bounces, seed

@@ -78,6 +78,9 @@ typedef struct {
   orc_dcstate_t* dcst;            /* [num_drawcalls] */
   orc_vis_prim_t* vis;            /* [num_prims] primary visibility (vis.c) */
   uint32_t* vnodes;               /* [num vnodes][16] over the primary rays' tree */
+  uint32_t* bl_idx;               /* vis_lists: per 8x8 block (first entry, count) */
+  uint32_t* bl_ent;               /* per entry: geometry pid, suffix union rx, ry */
+  uint32_t bl_nbx;
   int32_t* vpids;                 /* its leaf records' pids */
   uint32_t num_vnodes;
   int32_t* vhit;                  /* [W*H] primary winner per pixel (packet pre-pass) */
@@ -149,6 +152,7 @@ static int rt_prepare(rt_ctx_t* c, const orc_scene_t* s, const orc_rt_params_t* 
 
 static void rt_release(rt_ctx_t* c) {
   free(c->rp); free(c->rp_ok); free(c->prim_dc); free(c->tri); free(c->geom); free(c->dcst);
+  free(c->bl_idx); free(c->bl_ent);
   free(c->vis); free(c->vnodes); free(c->vpids); free(c->vhit);
   pthread_mutex_destroy(&c->mu);
 }
@@ -454,6 +458,89 @@ static int tile_split(const rt_ctx_t* c, uint32_t tx, uint32_t ty) {
   return 0;
 }
 
+/* Per-8x8-block candidate lists (rt_app.cpp build_block_lists): the
+ * geometry primitives whose covered rectangle reaches the block, in
+ * ascending (depth bound, geometry index), each with the union rectangle of
+ * itself and the entries after it. */
+typedef struct { uint32_t zmin, k; } bl_key_t;
+static int bl_cmp(const void* a, const void* b) {
+  const bl_key_t *x = (const bl_key_t*)a, *y = (const bl_key_t*)b;
+  if (x->zmin != y->zmin) return x->zmin < y->zmin ? -1 : 1;
+  return x->k < y->k ? -1 : x->k > y->k;
+}
+static void vis_build_lists(rt_ctx_t* c) {
+  const uint32_t nbx = (c->p.width + 7) / 8, nby = (c->p.height + 7) / 8, nb = nbx * nby;
+  uint32_t* cnt = (uint32_t*)calloc(nb, sizeof(uint32_t));
+  for (int k = 0; k < c->num_geom; ++k) {
+    const orc_vis_prim_t* v = &c->vis[c->geom[k]];
+    if (!v->any) continue;
+    for (uint32_t by = (v->ry & 0xffffu) >> 3; by <= (v->ry >> 16) >> 3 && by < nby; ++by)
+      for (uint32_t bx = (v->rx & 0xffffu) >> 3; bx <= (v->rx >> 16) >> 3 && bx < nbx; ++bx) ++cnt[by * nbx + bx];
+  }
+  c->bl_idx = (uint32_t*)malloc(sizeof(uint32_t) * 2 * nb);
+  uint32_t tot = 0;
+  for (uint32_t b = 0; b < nb; ++b) { c->bl_idx[2 * b] = tot; c->bl_idx[2 * b + 1] = 0; tot += cnt[b]; }
+  bl_key_t* keys = (bl_key_t*)malloc(sizeof(bl_key_t) * (tot ? tot : 1));
+  for (int k = 0; k < c->num_geom; ++k) {
+    const orc_vis_prim_t* v = &c->vis[c->geom[k]];
+    if (!v->any) continue;
+    for (uint32_t by = (v->ry & 0xffffu) >> 3; by <= (v->ry >> 16) >> 3 && by < nby; ++by)
+      for (uint32_t bx = (v->rx & 0xffffu) >> 3; bx <= (v->rx >> 16) >> 3 && bx < nbx; ++bx) {
+        const uint32_t b = by * nbx + bx;
+        bl_key_t* e = &keys[c->bl_idx[2 * b] + c->bl_idx[2 * b + 1]++];
+        e->zmin = v->zmin;
+        e->k = (uint32_t)k;
+      }
+  }
+  c->bl_ent = (uint32_t*)malloc(sizeof(uint32_t) * 3 * (tot ? tot : 1));
+  for (uint32_t b = 0; b < nb; ++b) {
+    const uint32_t o = c->bl_idx[2 * b], n = c->bl_idx[2 * b + 1];
+    qsort(keys + o, n, sizeof(bl_key_t), bl_cmp);
+    uint32_t x0 = 0xffffu, x1 = 0, y0 = 0xffffu, y1 = 0;
+    for (uint32_t i = n; i-- > 0;) {
+      const int32_t pid = c->geom[keys[o + i].k];
+      const orc_vis_prim_t* v = &c->vis[pid];
+      if ((v->rx & 0xffffu) < x0) x0 = v->rx & 0xffffu;
+      if ((v->rx >> 16) > x1) x1 = v->rx >> 16;
+      if ((v->ry & 0xffffu) < y0) y0 = v->ry & 0xffffu;
+      if ((v->ry >> 16) > y1) y1 = v->ry >> 16;
+      c->bl_ent[3 * (o + i)] = (uint32_t)pid;
+      c->bl_ent[3 * (o + i) + 1] = x0 | (x1 << 16);
+      c->bl_ent[3 * (o + i) + 2] = y0 | (y1 << 16);
+    }
+  }
+  c->bl_nbx = nbx;
+  free(keys);
+  free(cnt);
+}
+
+/* the kernels' block_primary: the wave's block list two entries per round,
+ * stopping once no lane's pixel lies in the remaining entries' union with a
+ * bound (the next entry's, the smallest left) not above its best depth word;
+ * tests count once per wave per entry tested */
+static void vis_scan_block(const rt_ctx_t* c, int n, const uint32_t* px, const uint32_t* py,
+                           int32_t* out, uint64_t* tests) {
+  uint32_t bz[PK_LANES];
+  int bpid[PK_LANES];
+  for (int i = 0; i < n; ++i) { bz[i] = VX_OM_DEPTH_MASK; bpid[i] = -1; }
+  const uint32_t b = (py[0] >> 3) * c->bl_nbx + (px[0] >> 3);
+  const uint32_t o = c->bl_idx[2 * b], cnt = c->bl_idx[2 * b + 1];
+  for (uint32_t k = 0; k < cnt; k += 2) {
+    const uint32_t* e = &c->bl_ent[3 * (o + k)];
+    const uint32_t zk = c->vis[e[0]].zmin;
+    int go = 0;
+    for (int i = 0; i < n && !go; ++i)
+      go = rect_in(e[1], px[i]) && rect_in(e[2], py[i]) && zk <= bz[i];
+    if (!go) break;
+    for (uint32_t j = k; j < k + 2 && j < cnt; ++j) {
+      ++*tests;
+      const int32_t pid = (int32_t)c->bl_ent[3 * (o + j)];
+      for (int i = 0; i < n; ++i) vis_test(c, pid, px[i], py[i], &bz[i], &bpid[i]);
+    }
+  }
+  for (int i = 0; i < n; ++i) out[i] = bpid[i];
+}
+
 /* the primary pre-pass over one row of 32x32 tiles: every wave's packet
  * (8x8 blocks, or 8x4 halves in split tiles, the kernels' task_map) */
 static void vis_tile_row(rt_ctx_t* c, uint32_t ty, orc_rt_counters_t* k) {
@@ -477,7 +564,10 @@ static void vis_tile_row(rt_ctx_t* c, uint32_t ty, orc_rt_counters_t* k) {
         ++n;
       }
       if (n == 0) continue;
-      vis_trace_packet(c, n, px, py, out, &k->node_visits, &k->tri_tests);
+      if (c->bl_idx)
+        vis_scan_block(c, n, px, py, out, &k->tri_tests);
+      else
+        vis_trace_packet(c, n, px, py, out, &k->node_visits, &k->tri_tests);
       for (int i = 0; i < n; ++i) c->vhit[idx[i]] = out[i];
     }
   }
@@ -798,6 +888,7 @@ static int rt_run(const orc_scene_t* scene, const orc_bvh_t* bvh, const orc_rt_p
   if (bvh && !p->vis_per_lane && p->row_begin == 0 && p->row_end == 0 && p->row_step <= 1) {
     /* primary visibility as the kernels walk it: one packet per wave */
     c.vhit = (int32_t*)malloc(sizeof(int32_t) * (size_t)p->width * p->height);
+    if (p->vis_lists && !(p->flags & ORC_RT_PATH)) vis_build_lists(&c);
     c.next_tile_row = 0;
     if (nt == 1) {
       vis_worker(&c);

@@ -571,51 +571,57 @@ static int configure_vis(rt_renderer* r, const std::vector<rt_prim_t>& prims,
       upload(r->dev, vl.data(), vl.size() * sizeof(rt_vtri_t), &r->vlayers, &a.vlayers_addr) ||
       upload(r->dev, vg.data(), vg.size() * sizeof(rt_vtri_t), &r->vgeom, &a.vgeom_addr))
     return -1;
-  // experiment (env RT_BLOCK_LISTS=1, RT_BLOCK_LIST images): per 8x8 pixel
-  // block, the geometry primitives whose covered rectangle reaches it, in
-  // ascending depth bound, with the union rectangle of each record and the
-  // ones after it, so a wave can resolve its block's primary visibility by
-  // scanning the list and stop early instead of walking the tree
-  a.blist_nbx = 0;
-  a.blist_addr = a.bidx_addr = a.bsuf_addr = 0;
-  if (std::getenv("RT_BLOCK_LISTS") && std::atoi(std::getenv("RT_BLOCK_LISTS")) != 0) {
-    const uint32_t nbx = (a.width + 7) / 8, nby = (a.height + 7) / 8;
-    std::vector<std::vector<std::pair<uint32_t, uint32_t>>> lists((size_t)nbx * nby);
-    for (uint32_t k = 0; k < (uint32_t)s->geometry.size(); ++k) {
-      const rt::VisPrim& v = vis[s->geometry[k]];
-      if (!v.any) continue;
-      const uint32_t x0 = (v.rx & 0xffffu) >> 3, x1 = (v.rx >> 16) >> 3;
-      const uint32_t y0 = (v.ry & 0xffffu) >> 3, y1 = (v.ry >> 16) >> 3;
-      for (uint32_t by = y0; by <= y1 && by < nby; ++by)
-        for (uint32_t bx = x0; bx <= x1 && bx < nbx; ++bx) lists[(size_t)by * nbx + bx].push_back({v.zmin, k});
-    }
-    std::vector<rt_vtri_t> recs;
-    std::vector<uint32_t> idx, suf;
-    for (auto& l : lists) {
-      std::sort(l.begin(), l.end());
-      idx.push_back((uint32_t)recs.size());
-      idx.push_back((uint32_t)l.size());
-      const size_t base = recs.size();
-      for (auto& e : l) recs.push_back(vg[e.second]);
-      std::vector<uint32_t> lo(l.size()), hi(l.size());
-      uint32_t ux0 = 0xffffu, uy0 = 0xffffu, ux1 = 0, uy1 = 0;
-      for (size_t i = l.size(); i-- > 0;) {
-        const rt_vtri_t& t = recs[base + i];
-        ux0 = std::min(ux0, t.rx & 0xffffu); ux1 = std::max(ux1, t.rx >> 16);
-        uy0 = std::min(uy0, t.ry & 0xffffu); uy1 = std::max(uy1, t.ry >> 16);
-        lo[i] = ux0 | (uy0 << 16);
-        hi[i] = ux1 | (uy1 << 16);
-      }
-      for (size_t i = 0; i < l.size(); ++i) { suf.push_back(lo[i]); suf.push_back(hi[i]); }
-    }
-    recs.push_back(rt::MakeVisTri(rt_prim_t{}, rt::VisPrim{}, -1));  // padding: pairs are loaded
-    suf.push_back(0xffffffffu); suf.push_back(0xfffefffeu);
-    a.blist_nbx = nbx;
-    if (upload(r->dev, recs.data(), recs.size() * sizeof(rt_vtri_t), &r->blist, &a.blist_addr) ||
-        upload(r->dev, idx.data(), idx.size() * 4, &r->bidx, &a.bidx_addr) ||
-        upload(r->dev, suf.data(), suf.size() * 4, &r->bsuf, &a.bsuf_addr))
-      return -1;
+  return 0;
+}
+
+// Per-8x8-block candidate lists for primary visibility (the rt images'
+// block_primary; oracle/rt.c vis_build_lists restates them): per block of
+// the frame, the geometry records whose covered rectangle reaches it, in
+// ascending (depth bound, geometry index), and per record the union
+// rectangle (corners) of it and the records after it, so a wave stops its
+// scan once no lane can change its winner.  Built from the geometry records
+// (the host's, or the device setup's read back), for primary+shadow frames;
+// env RT_BLOCK_LISTS=0 keeps the tree walk.
+static int build_block_lists(rt_renderer* r, const std::vector<rt_vtri_t>& vg) {
+  rt_kernel_arg_t& a = r->arg;
+  const uint32_t nbx = (a.width + 7) / 8, nby = (a.height + 7) / 8;
+  std::vector<std::vector<std::pair<uint32_t, uint32_t>>> lists((size_t)nbx * nby);
+  for (uint32_t k = 0; k < (uint32_t)vg.size(); ++k) {
+    const rt_vtri_t& t = vg[k];
+    const uint32_t x0 = t.rx & 0xffffu, x1 = t.rx >> 16, y0 = t.ry & 0xffffu, y1 = t.ry >> 16;
+    if (x0 > x1 || y0 > y1) continue;  // covers no pixel
+    for (uint32_t by = y0 >> 3; by <= (y1 >> 3) && by < nby; ++by)
+      for (uint32_t bx = x0 >> 3; bx <= (x1 >> 3) && bx < nbx; ++bx)
+        lists[(size_t)by * nbx + bx].push_back({t.zmin, k});
   }
+  std::vector<rt_vtri_t> recs;
+  std::vector<uint32_t> idx, suf;
+  idx.reserve(lists.size() * 2);
+  for (auto& l : lists) {
+    std::sort(l.begin(), l.end());
+    idx.push_back((uint32_t)recs.size());
+    idx.push_back((uint32_t)l.size());
+    const size_t base = recs.size();
+    for (auto& e : l) recs.push_back(vg[e.second]);
+    std::vector<uint32_t> lo(l.size()), hi(l.size());
+    uint32_t ux0 = 0xffffu, uy0 = 0xffffu, ux1 = 0, uy1 = 0;
+    for (size_t i = l.size(); i-- > 0;) {
+      const rt_vtri_t& t = recs[base + i];
+      ux0 = std::min(ux0, t.rx & 0xffffu); ux1 = std::max(ux1, t.rx >> 16);
+      uy0 = std::min(uy0, t.ry & 0xffffu); uy1 = std::max(uy1, t.ry >> 16);
+      lo[i] = ux0 | (uy0 << 16);
+      hi[i] = ux1 | (uy1 << 16);
+    }
+    for (size_t i = 0; i < l.size(); ++i) { suf.push_back(lo[i]); suf.push_back(hi[i]); }
+  }
+  recs.push_back(rt::MakeVisTri(rt_prim_t{}, rt::VisPrim{}, -1));  // padding: pairs are loaded
+  suf.push_back(0xffffffffu);
+  suf.push_back(0xfffefffeu);
+  if (upload(r->dev, recs.data(), recs.size() * sizeof(rt_vtri_t), &r->blist, &a.blist_addr) ||
+      upload(r->dev, idx.data(), idx.size() * 4, &r->bidx, &a.bidx_addr) ||
+      upload(r->dev, suf.data(), suf.size() * 4, &r->bsuf, &a.bsuf_addr))
+    return -1;
+  a.blist_nbx = nbx;
   return 0;
 }
 
@@ -787,6 +793,17 @@ int rt_renderer_configure(rt_renderer_h r, const rt_render_params_t* p) {
     if (rtapp::device_setup(r, raster, order_on, &heavy, &launches) != 0) return -1;
   } else if (host_setup(r, p, raster, order_on, &heavy) != 0) {
     return -1;
+  }
+  // primary+shadow frames: per-block candidate lists (build_block_lists)
+  a.blist_nbx = 0;
+  a.blist_addr = a.bidx_addr = a.bsuf_addr = 0;
+  const char* bl = std::getenv("RT_BLOCK_LISTS");
+  if (!raster && !(p->flags & (RT_RENDER_PATH | RT_RENDER_FLAT)) && !(bl && std::atoi(bl) == 0) &&
+      a.num_geom > 0) {
+    std::vector<rt_vtri_t> vg(a.num_geom);
+    if (vx_copy_from_dev(vg.data(), r->vgeom, 0, vg.size() * sizeof(rt_vtri_t)) != 0)
+      return fail("vx_copy_from_dev failed");
+    if (build_block_lists(r, vg) != 0) return -1;
   }
   const double setup_ms = ms_since(t1);
   if (order_on) {

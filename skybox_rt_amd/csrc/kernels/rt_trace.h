@@ -1345,14 +1345,17 @@ __device__ __forceinline__ int32_t trace_primary_packet(const Scene& S, uint32_t
 
 // every lane of the wave calls it; lanes with !act get -1
 #if RT_BLOCK_LIST
-// Experiment: the wave's 8x8 block resolved from its candidate list (host
-// built, RT_BLOCK_LISTS=1): records in ascending depth bound, two per round,
+// The wave's 8x8 block resolved from its candidate list (rt_app.cpp
+// build_block_lists; oracle/rt.c vis_scan_block): records in ascending depth
+// bound, two per round,
 // every lane runs the exact test; the scan stops once no lane can change its
 // winner -- its pixel is outside the union rectangle of the remaining
 // records, or their smallest bound exceeds its best depth word.  Same
-// winners as the walk (vis_better is a strict order); counters not kept.
+// winners as the walk (vis_better is a strict order).  Tests count once per
+// wave per record tested, as the packet walk's do.
 __device__ __forceinline__ int32_t block_primary(const Scene& S, uint32_t px, uint32_t py, bool act,
-                                                 bool tie_high) {
+                                                 bool tie_high, Counters& cnt) {
+  (void)cnt;
   const uint32_t bx = (uint32_t)__builtin_amdgcn_readfirstlane(px >> 3);
   const uint32_t by = (uint32_t)__builtin_amdgcn_readfirstlane(py >> 3);
   if (!act) px = 0xffffffffu;
@@ -1365,6 +1368,9 @@ __device__ __forceinline__ int32_t block_primary(const Scene& S, uint32_t px, ui
     S.A.sld_u4n<8>(S.blist + 64u * (oc.x + k), tw);
     const uint2 sr = S.A.sld<uint2>(S.bsuf + 8u * (oc.x + k));
     if (__ballot(rect2_in(sr.x, sr.y, pp) && tw[3].w <= bz) == 0) break;
+#ifdef RT_INSTRUMENT
+    cnt.tests += lane_id() == 0 ? (k + 1 < oc.y ? 2u : 1u) : 0u;  // once per wave per record
+#endif
     vis_test(tw[0], tw[1], tw[2], tw[3], px, py, tie_high, bz, bpid);
     if (k + 1 < oc.y) vis_test(tw[4], tw[5], tw[6], tw[7], px, py, tie_high, bz, bpid);
   }
@@ -1375,7 +1381,7 @@ __device__ __forceinline__ int32_t block_primary(const Scene& S, uint32_t px, ui
 __device__ __forceinline__ int32_t trace_primary(const Scene& S, uint32_t px, uint32_t py, bool act,
                                                  bool tie_high, int32_t* stack, Counters& cnt) {
 #if RT_BLOCK_LIST
-  if (S.blist_nbx) return block_primary(S, px, py, act, tie_high);
+  if (S.blist_nbx) return block_primary(S, px, py, act, tie_high, cnt);
 #endif
 #if RT_VIS_PACKET
   const int32_t h = trace_primary_packet(S, px, py, act, tie_high, stack, cnt);

@@ -248,7 +248,8 @@ def test_bvh4_traversal_equals_bvh2(oracle_lib, name, size, shadows, path):
     po = oracle_lib
     s = rt.Scene.load(scene_path(name))
     osc = po.OracleScene(po.cgltrace.load(scene_path(name)))
-    p = po.rt_params(size, size, shadows=shadows, nthreads=8, path=path, bounces=3)
+    # the primary walk too (not the block lists): this compares tree traversals
+    p = po.rt_params(size, size, shadows=shadows, nthreads=8, path=path, bounces=3, vis_lists=False)
     nodes, tris = s.bvh()
     c2, p2, t2, k2 = po.rt_render(osc, p, bvh=(nodes, tris))
     c4, p4, t4, k4 = po.rt_render(osc, p, bvh=(nodes, tris, s.bvh4()))
