@@ -182,9 +182,9 @@ def rt_params(width, height, shadows=True, light=(0.0, 60.0, 80.0), nthreads=1,
               path=False, bounces=4, seed=PT_SEED, vis_per_lane=False, vis_lists=None):
     p = RtParamsC()
     p.vis_per_lane = 1 if vis_per_lane else 0
-    # the product resolves primary visibility from per-block candidate lists
-    # (its default for primary+shadow frames and path tracing)
-    p.vis_lists = (0 if vis_per_lane else 1) if vis_lists is None else int(bool(vis_lists))
+    # the product resolves primary visibility of primary+shadow frames from
+    # per-block candidate lists (its default); path tracing walks the tree
+    p.vis_lists = (0 if (path or vis_per_lane) else 1) if vis_lists is None else int(bool(vis_lists))
     p.width, p.height = width, height
     p.flags = (RT_SHADOWS if shadows else 0) | (RT_PATH if path else 0)
     p.bounces, p.seed = bounces, seed

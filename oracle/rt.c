@@ -888,7 +888,7 @@ static int rt_run(const orc_scene_t* scene, const orc_bvh_t* bvh, const orc_rt_p
   if (bvh && !p->vis_per_lane && p->row_begin == 0 && p->row_end == 0 && p->row_step <= 1) {
     /* primary visibility as the kernels walk it: one packet per wave */
     c.vhit = (int32_t*)malloc(sizeof(int32_t) * (size_t)p->width * p->height);
-    if (p->vis_lists) vis_build_lists(&c);
+    if (p->vis_lists && !(p->flags & ORC_RT_PATH)) vis_build_lists(&c);
     c.next_tile_row = 0;
     if (nt == 1) {
       vis_worker(&c);

@@ -794,11 +794,11 @@ int rt_renderer_configure(rt_renderer_h r, const rt_render_params_t* p) {
   } else if (host_setup(r, p, raster, order_on, &heavy) != 0) {
     return -1;
   }
-  // RT frames (primary+shadow, path): per-block candidate lists (build_block_lists)
+  // primary+shadow frames: per-block candidate lists (build_block_lists)
   a.blist_nbx = 0;
   a.blist_addr = a.bidx_addr = a.bsuf_addr = 0;
   const char* bl = std::getenv("RT_BLOCK_LISTS");
-  if (!raster && !(p->flags & RT_RENDER_FLAT) && !(bl && std::atoi(bl) == 0) &&
+  if (!raster && !(p->flags & (RT_RENDER_PATH | RT_RENDER_FLAT)) && !(bl && std::atoi(bl) == 0) &&
       a.num_geom > 0) {
     std::vector<rt_vtri_t> vg(a.num_geom);
     if (vx_copy_from_dev(vg.data(), r->vgeom, 0, vg.size() * sizeof(rt_vtri_t)) != 0)
