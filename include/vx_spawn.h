@@ -301,16 +301,21 @@ __device__ __forceinline__ int vx_spawn_chunks_block(uint32_t num_tasks, F kerne
 }
 
 /* VX_MAIN(ArgT, arg, block_threads) { ... return vx_spawn_tasks(...); }
- * defines the `vx_main` entry the driver launches with `block_threads`
- * threads per workgroup (must be a multiple of 64). */
+ * defines the entry the driver launches with `block_threads` threads per
+ * workgroup (must be a multiple of 64): `vx_main`, or the image's own name
+ * vx_main_<image> given by -DVX_ENTRY (the driver finds it in the code
+ * object's symbol table, so profiles tell the images apart). */
 #define VX_MAIN(ArgT, argname, block_threads) \
   VX_MAIN_BOUNDS(ArgT, argname, __launch_bounds__(block_threads))
 /* same, asking the compiler for `waves_per_eu` resident waves per SIMD */
 #define VX_MAIN_OCC(ArgT, argname, block_threads, waves_per_eu) \
   VX_MAIN_BOUNDS(ArgT, argname, __launch_bounds__(block_threads, waves_per_eu))
+#ifndef VX_ENTRY
+#define VX_ENTRY vx_main
+#endif
 #define VX_MAIN_BOUNDS(ArgT, argname, bounds)                                        \
   static __device__ __forceinline__ int __vx_main_body(ArgT* argname);               \
-  extern "C" __global__ void bounds vx_main() {                                      \
+  extern "C" __global__ void bounds VX_ENTRY() {                                     \
     if (threadIdx.x < VX_MPM_ROW) __vx_mpm_lds[threadIdx.x] = 0;                     \
     __syncthreads();                                                                 \
     const uint64_t a = ((uint64_t)__vx_dcrs[VX_DCR_BASE_STARTUP_ARG1] << 32) |       \

@@ -15,12 +15,11 @@
 // path, a hit multiplies T by the draw3d shader's colour at the hit's
 // barycentrics.  The pixel gets clamp(L) (alpha of the primary colour).
 //
-// Wave64 compaction: a 256-thread workgroup (4 waves, 256 pixels) keeps its
-// live paths in an LDS queue.  After each vertex the surviving paths are
-// appended to the other queue at ballot + mbcnt slots, so bounce k runs on
-// ceil(live/64) full waves while the other waves of the block skip it --
-// the paths that escape (most of them, tekkaman is an open scene) stop
-// costing lanes.
+// Two images: pt_kernel (PT_MODE 1, the default) runs each path on its own
+// lane, the 32-pixel waves of geometry tiles with paired shadow / bounce
+// lanes; pt_compact (PT_MODE 0) keeps a 256-thread workgroup's live paths in
+// an LDS queue and after each vertex appends the survivors to the other
+// queue at ballot + mbcnt slots (wave64 compaction).
 #include <hip/hip_runtime.h>
 
 #include "rt_trace.h"
@@ -38,17 +37,10 @@
 #ifndef PT_MODE
 #define PT_MODE 1
 #endif
-#ifndef RT_LDS_SCENE
-#define RT_LDS_SCENE 0
-#endif
-#ifndef PT_BLOCK
 #if PT_MODE == 0
 #define PT_BLOCK 256
-#elif RT_LDS_SCENE
-#define PT_BLOCK 1024  // one workgroup per CU shares the staged BVH
 #else
 #define PT_BLOCK 64
-#endif
 #endif
 #define PT_SKY 0.25f     // radiance of an escaped bounce ray (oracle ORC_PT_SKY)
 #define PT_TRIES 8u      // disk rejection-sampling attempts (ORC_PT_TRIES)
@@ -182,9 +174,8 @@ __device__ __forceinline__ void primary(const vx_task_t& task, bool valid, const
   const bool in = valid && x < S.width && y < S.height;
   cnt.primary += in;
   const bool tie_high = (S.flags & RT_FLAG_TIE_HIGH) != 0;
-  int32_t* stack = &L.stack[threadIdx.x >> 6][0][lane_id()];
   // primary visibility: the raster's winner at this pixel (trace_primary)
-  const int32_t hit = trace_primary(S, x, y, in, tie_high, stack, cnt);
+  const int32_t hit = trace_primary(S, x, y, in, tie_high, cnt);
   cnt.hits += hit >= 0;
   const int32_t spid = resolve_layers(S, x, y, in && hit < 0, hit, cnt);
   const uint32_t color = shade_wave(S, spid, x, y, S.clear_color, cnt);
@@ -297,16 +288,6 @@ __device__ __forceinline__ bool path_step(const Scene& S, int32_t* stack, PathSt
 // longer of the two traversals instead of their sum.  Same rays, same
 // arithmetic, same order of the radiance updates as path_step: the output
 // and every counter are identical.  All 64 lanes call it.
-#ifndef PT_PAIR
-#define PT_PAIR 1
-#endif
-#ifndef PT_PRIO
-#define PT_PRIO 0
-#endif
-// >0: stage up to this many binary16 BVH4 nodes in LDS per workgroup
-#ifndef PT_LDS_NODES
-#define PT_LDS_NODES 0
-#endif
 // (Shadow rays as wave packets, occluded_packet, then the bounce rays per
 // lane: 0.31 ms vs 0.22 ms, measured -- a path's later shadow rays are
 // incoherent and the two traversals no longer overlap.)
@@ -481,14 +462,11 @@ __device__ __forceinline__ void lane_path(const vx_task_t& task, const Scene& S,
   const bool in = x < S.width && y < S.height;
   // paired vertices (path_step_pair) when the whole wave is here and its
   // upper 32 lanes hold no pixel -- wave-uniform
-  const bool pair = PT_PAIR && __ballot(1) == ~0ull && (__ballot(in) >> 32) == 0;
-#if PT_PRIO
-  if (pair) __builtin_amdgcn_s_setprio(PT_PRIO);  // geometry-tile waves: the long paths
-#endif
+  const bool pair = __ballot(1) == ~0ull && (__ballot(in) >> 32) == 0;
   cnt.primary += in;
   const bool tie_high = (S.flags & RT_FLAG_TIE_HIGH) != 0;
   // primary visibility: the raster's winner at this pixel (trace_primary)
-  const int32_t hit = trace_primary(S, x, y, in, tie_high, stack, cnt);
+  const int32_t hit = trace_primary(S, x, y, in, tie_high, cnt);
   cnt.hits += hit >= 0;
   const int32_t spid = resolve_layers(S, x, y, in && hit < 0, hit, cnt);
   const uint32_t color = shade_wave(S, spid, x, y, S.clear_color, cnt);
@@ -536,24 +514,12 @@ __device__ __forceinline__ void flush(int slot, uint32_t v) { vx_mpm_add(RT_MPM_
 // r02 after the scalar argument block: 128/CU 0.1765 vs 96/CU 0.1801 ms,
 // profiles/r02/ab_pt_grid.json; 64/CU is best for rt_kernel)
 #if PT_BLOCK == 64
-#ifndef PT_GRID_PER_CU
 #define PT_GRID_PER_CU 128
-#endif
 __device__ __attribute__((used)) uint32_t __vx_grid_per_cu = PT_GRID_PER_CU;
 #endif
 
-#ifdef PT_WAVES_PER_EU
-VX_MAIN_OCC(rt_kernel_arg_t, arg, PT_BLOCK, PT_WAVES_PER_EU) {
-#else
 VX_MAIN(rt_kernel_arg_t, arg, PT_BLOCK) {
-#endif
   __shared__ PtLds s_pt;
-#ifdef RT_LDS_PAD_WORDS
-  // occupancy probe (A/B only): LDS padding caps the waves per CU; the store
-  // never runs (no real scene has these flags) but keeps the array allocated
-  __shared__ uint32_t s_occ_pad[RT_LDS_PAD_WORDS];
-  if (arg->flags == 0xffffffffu) ((volatile uint32_t*)s_occ_pad)[threadIdx.x] = 0u;
-#endif
 #ifdef RT_STAMPS  // diagnostic image: per-wave start/end timestamps (scripts/wave_timeline.py)
   const uint64_t t_stamp0 = __builtin_amdgcn_s_memrealtime();
   const uint64_t t_cyc0 = __builtin_amdgcn_s_memtime();
@@ -568,21 +534,6 @@ VX_MAIN(rt_kernel_arg_t, arg, PT_BLOCK) {
       [&](const vx_task_t& task, bool valid, const Scene* s) { primary(task, valid, *s, s_pt, cnt); },
       [&](uint32_t, const Scene* s) { bounces(*s, s_pt, cnt); }, &S);
 #else
-#if RT_LDS_SCENE
-  __shared__ float4 s_scene[RT_LDS_SCENE_F4];
-  stage_scene(S, S.num_geom, s_scene);
-  __syncthreads();
-#endif
-#if PT_LDS_NODES
-  // the binary16 BVH4 nodes (64 B each) staged per workgroup when they fit
-  __shared__ float4 s_nodes4h[4 * PT_LDS_NODES];
-  if (S.num_nodes4 <= PT_LDS_NODES && (S.flags & RT_FLAG_BVH4H)) {
-    for (uint32_t i = threadIdx.x; i < 4u * S.num_nodes4; i += blockDim.x)
-      s_nodes4h[i] = S.A.ld_f4(S.nodes4 + 128u * S.num_nodes4 + 16u * i);
-    S.lnodes4h = s_nodes4h;
-  }
-  __syncthreads();
-#endif
   int32_t* stack = &s_pt.stack[threadIdx.x >> 6][0][lane_id()];
   const int rc = vx_spawn_tasks(
       arg->num_tasks,

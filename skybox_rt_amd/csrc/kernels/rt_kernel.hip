@@ -1,47 +1,37 @@
 // rt_kernel.hip -- the north-star hot path as a Vortex kernel program for
-// gfx950: per-pixel primary rays resolved raster-exactly over the BVH
-// (trace_primary: 2D point-in-rect node walk with depth-bound culling, the
-// draw3d fixed-point coverage + 24-bit depth test at the leaves), screen
-// layers, draw3d-exact shading of the winner, and an any-hit Möller–Trumbore
-// shadow ray per geometry hit, with the shadow rays compacted into full
-// waves (ballot + mbcnt into an LDS queue).
+// gfx950: per-pixel primary rays resolved raster-exactly (trace_primary: the
+// wave's 8x8 block scans its candidate list, or walks the tree as a packet;
+// the draw3d fixed-point coverage + 24-bit depth test decide), screen layers,
+// draw3d-exact shading of the winner, and an any-hit Möller–Trumbore shadow
+// ray per geometry hit, with the shadow rays compacted into full waves
+// (ballot + mbcnt into an LDS queue) and each full wave walking the binary16
+// BVH4 as one packet (occluded_packet).
 //
-// Launched by libvortex-hip.so (vx_start) as `vx_main`; the body reads its
-// rt_kernel_arg_t from the STARTUP_ARG DCRs and calls vx_spawn_tasks_ex()
-// with one task per pixel (64 consecutive tasks = one wave = an 8x8 pixel
-// block, 16 waves = one 32x32 raster tile, the reference's tile unit).
+// Launched by libvortex-hip.so (vx_start) as its entry (VX_ENTRY); the body
+// reads its rt_kernel_arg_t from the STARTUP_ARG DCRs and calls
+// vx_spawn_tasks_ex() with one task per pixel (64 consecutive tasks = one
+// wave = an 8x8 pixel block, 16 waves = one 32x32 raster tile, the
+// reference's tile unit).  The node-visit / triangle-test counts of the
+// RT_INSTRUMENT image are exactly the traversal work the oracle (oracle/rt.c)
+// restates, the basis of the algorithmic byte count of SURVEY.md 8(d).
 //
-// Traversal: each lane walks the BVH alone (near child first) with its
-// stack in LDS, stack[depth][lane] (conflict-free, no VGPR cost); a leaf's
-// triangles come in as one batch of 16-B loads.  The node-visit /
-// triangle-test counts of the RT_INSTRUMENT image are exactly the per-ray
-// traversal work the oracle (oracle/rt.c vis_trace / bvh_trace) restates, the
-// basis of the algorithmic byte count of SURVEY.md 8(d).
+// Scene reads are buffer loads through one arena descriptor (vx_arena):
+// 32-bit offsets, no FLAT loads.  Numerics are bit-identical to the oracle:
+// every fused multiply-add is an explicit fmaf, everything else is compiled
+// with -ffp-contract=off, divisions are IEEE.
 //
-// Scene reads are buffer loads through one arena descriptor
-// (vx_arena): 32-bit offsets, no FLAT loads.  Numerics are bit-identical to
-// the oracle (oracle/rt.c): every fused multiply-add is an explicit fmaf,
-// everything else is compiled with -ffp-contract=off, divisions are IEEE.
-//
+// Images (Makefile): rt_kernel (binary16 BVH4 only), rt_kernel_deep (every
+// BVH layout: per-lane walks with a 32-entry LDS stack for the layouts the
+// packet walk does not read), rt_flat (RT_FLAT: BASELINE config 2, the flat
+// geometry list, no BVH).
 #include <hip/hip_runtime.h>
 
 #include "rt_trace.h"
 
-
-// RT_FLAT: config-2 image -- brute force over the LDS-staged geometry list
-// instead of the BVH (no traversal stack, no shadow queue)
 #ifndef RT_FLAT
 #define RT_FLAT 0
 #endif
-#define RT_FLAT_CAP 1024  // primitives staged in LDS (64 KB); longer lists stream via s_load
-#ifndef RT_SHADOW_QUEUE
-#define RT_SHADOW_QUEUE (!RT_FLAT)
-#endif
-// 1: the queued shadow rays of a wave walk the binary16 BVH4 as one packet
-// (occluded_packet in rt_trace.h; same verdicts and per-ray counts)
-#ifndef RT_SHADOW_PACKET
-#define RT_SHADOW_PACKET 1
-#endif
+#define RT_FLAT_CAP 1024  // rectangle words staged in LDS (16 KB); longer lists stream via s_load
 
 namespace {
 
@@ -49,15 +39,11 @@ using namespace rtk;
 
 constexpr int kWaves = RT_BLOCK_THREADS / 64;
 
-// Wave-private LDS: the per-ray traversal stack (stack[depth][lane]) and the
-// compaction queue of deferred shadow rays.
+// Wave-private LDS: the compaction queue of deferred shadow rays, and the
+// per-lane walks' stack[depth][lane] (deep images: layouts other than the
+// binary16 BVH4 walk per lane)
 #define RT_QUEUE 128
-// the per-lane walks' LDS stack: not needed when every walk of the image is
-// a wave packet with its stack in a VGPR (binary16-BVH4-only images)
-#ifndef RT_LANE_STACK
-#define RT_LANE_STACK (!RT_FLAT && !(RT_ONLY_BVH4H && RT_PACKET_VSTACK && RT_VIS_PACKET && \
-                                     RT_SHADOW_PACKET && RT_SHADOW_QUEUE))
-#endif
+#define RT_LANE_STACK (!RT_FLAT && !RT_ONLY_BVH4H)
 struct WaveLds {
 #if RT_LANE_STACK
   int32_t stack[RT_STACK_ROWS][64];
@@ -65,7 +51,7 @@ struct WaveLds {
 #else
 #define RT_WSTACK(w, lane) ((int32_t*)nullptr)
 #endif
-#if RT_SHADOW_QUEUE
+#if !RT_FLAT
   uint32_t q_task[RT_QUEUE];
   float q_t[RT_QUEUE];
   int32_t q_pid[RT_QUEUE];
@@ -75,39 +61,19 @@ struct WaveLds {
 };
 
 #if RT_FLAT
-// RT_FLAT_RECT_LDS 1: only each record's rectangle word (16 B: the word the
-// scan tests for every entry) is staged in LDS, 12 KB for tekkaman instead of
-// 48, so many more workgroups fit a CU; a candidate's other three words come
-// through the scalar cache (wave-uniform).  0: the whole 64-B records.
-// A/B (profiles/r02/ab_flat_rect_lds.json, 256^2): whole records in 1024-
-// thread workgroups (2 per CU by LDS) 0.0479 ms; rectangle words in 256-
-// thread workgroups (8 per CU, 4-way list split) 0.0280 ms -- the default
-// image (Makefile FLATDEFS); 512 threads 0.0302, 128 threads 0.0403
-#ifndef RT_FLAT_RECT_LDS
-#define RT_FLAT_RECT_LDS 0
-#endif
-// the geometry list staged as rt_vtri_t records (4 x 16 B per primitive) for
-// the primary rays; the shadow rays read the MT records (rt_tri_t) of S.geom
-#if RT_FLAT_RECT_LDS
+// Only each record's rectangle word (16 B: the word the scan tests for every
+// entry) is staged in LDS, 12 KB for tekkaman, so 8 workgroups fit a CU; a
+// candidate's other three words come through the scalar cache (wave-uniform).
+// A/B (profiles/r02/ab_flat_rect_lds.json, 256^2): whole 64-B records in
+// 1024-thread workgroups (2 per CU by LDS) 0.0479 ms; rectangle words in
+// 256-thread workgroups (8 per CU, 4-way list split) 0.0280 ms; 512 threads
+// 0.0302, 128 threads 0.0403.  The shadow rays read the MT records (rt_tri_t)
+// of S.geom.
 __shared__ uint4 s_geom[RT_FLAT_CAP];
-#else
-__shared__ uint4 s_geom[RT_FLAT_CAP * 4];
-#endif
 __device__ __forceinline__ const uint4* flat_list(const Scene& S) {
   return S.num_geom <= RT_FLAT_CAP ? s_geom : nullptr;
 }
 #endif
-
-__device__ __forceinline__ bool occluded(const Scene& S, const Ray& s, int32_t skip, bool tie_high,
-                                         bool active, WaveLds& w, Counters& cnt) {
-  float ts;
-  if (!active) return false;
-#if RT_FLAT
-  return trace_flat<true>(S, s, 0.0f, 1.0f, skip, tie_high, &ts, nullptr, cnt) >= 0;
-#else
-  return trace<true>(S, s, 0.0f, 1.0f, skip, tie_high, &ts, RT_WSTACK(w, lane_id()), cnt) >= 0;
-#endif
-}
 
 #if !RT_FLAT
 __device__ __forceinline__ void kernel_body(const vx_task_t& task, const Scene& S, WaveLds& w,
@@ -122,24 +88,16 @@ __device__ __forceinline__ void kernel_body(const vx_task_t& task, const Scene& 
   if (lane_id() == 0) __vx_mpm_lds[3] = (uint32_t)__builtin_amdgcn_s_memrealtime();
 #endif
   // primary visibility: the raster's winner at this pixel
-  const int32_t hit = trace_primary(S, x, y, in, tie_high, RT_WSTACK(w, lane_id()), cnt);
+  const int32_t hit = trace_primary(S, x, y, in, tie_high, cnt);
 #ifdef RT_STAMPS
   if (lane_id() == 0) __vx_mpm_lds[14] = (uint32_t)__builtin_amdgcn_s_memrealtime();
 #endif
   cnt.hits += hit >= 0;
-#ifdef RT_ABLATE_LAYERS  // timing-only ablation (scripts/ab_variants.py)
-  const int32_t spid = hit;
-#else
   const int32_t spid = resolve_layers(S, x, y, in && hit < 0, hit, cnt);
-#endif
 #ifdef RT_STAMPS
   if (lane_id() == 0) __vx_mpm_lds[4] = (uint32_t)__builtin_amdgcn_s_memrealtime();
 #endif
-#ifdef RT_ABLATE_SHADE  // timing-only ablation (scripts/ab_variants.py)
-  uint32_t color = 0xff000000u | (uint32_t)spid;
-#else
   uint32_t color = shade_wave(S, spid, x, y, S.clear_color, cnt);
-#endif
 #ifdef RT_STAMPS
   if (lane_id() == 0) __vx_mpm_lds[11] = (uint32_t)__builtin_amdgcn_s_memrealtime();
 #endif
@@ -147,7 +105,6 @@ __device__ __forceinline__ void kernel_body(const vx_task_t& task, const Scene& 
   primary_dir(S, x, y, r);
   const float th = hit >= 0 ? plane_t(S, r, hit) : 0.0f;
   const bool shadow = hit >= 0 && secondary_ok(th) && (S.flags & RT_FLAG_SHADOWS) != 0;
-#if RT_SHADOW_QUEUE
   // wave64 compaction: lanes with a pending shadow ray append it to the
   // wave's LDS queue at ballot/mbcnt-assigned slots
   const uint64_t m = __ballot(shadow);
@@ -170,20 +127,10 @@ __device__ __forceinline__ void kernel_body(const vx_task_t& task, const Scene& 
 #ifdef RT_STAMPS
   if (lane_id() == 0) __vx_mpm_lds[5] = (uint32_t)__builtin_amdgcn_s_memrealtime();
 #endif
-#else
-  Ray s;
-  shadow_ray(S, r, th, s);
-  cnt.shadow += shadow;
-  if (occluded(S, s, hit, tie_high, shadow, w, cnt)) {
-    ++cnt.occluded;
-    color = shadowed(color);
-  }
-  if (in) store_pixel(S, t, x, y, color);
-#endif
 }
 #endif
 
-#if RT_SHADOW_QUEUE
+#if !RT_FLAT
 // Called by all 64 lanes after every chunk: trace full waves of 64 shadow
 // rays while the queue holds >= 64 (or whatever is left at the end).
 __device__ __forceinline__ void shadow_drain(bool final, const Scene& S, WaveLds& w,
@@ -210,14 +157,12 @@ __device__ __forceinline__ void shadow_drain(bool final, const Scene& S, WaveLds
     shadow_ray(S, p, w.q_t[slot], s);
     cnt.shadow += active;
     uint32_t color = w.q_color[slot];
-#if RT_SHADOW_PACKET
+    float ts;
     const bool occ = (RT_ONLY_BVH4H || (S.flags & RT_FLAG_BVH4H))
-                         ? occluded_packet(S, s, active, w.q_pid[slot], 1.0f, RT_WSTACK(w, lane), cnt)
-                         : occluded(S, s, w.q_pid[slot], tie_high, active, w, cnt);
+                         ? occluded_packet(S, s, active, w.q_pid[slot], 1.0f, cnt)
+                         : active && trace<true>(S, s, 0.0f, 1.0f, w.q_pid[slot], tie_high, &ts,
+                                                 RT_WSTACK(w, lane), cnt) >= 0;
     if (occ) {
-#else
-    if (occluded(S, s, w.q_pid[slot], tie_high, active, w, cnt)) {
-#endif
       ++cnt.occluded;
       color = shadowed(color);
     }
@@ -241,16 +186,13 @@ __device__ __forceinline__ void shadow_drain(bool final, const Scene& S, WaveLds
 // shades and stores; shadow rays split the same way, the first occluder in
 // list order found by a min over the waves' first hits (which is also
 // brute_trace's test count).
-#ifndef RT_FLAT_UNROLL
-#define RT_FLAT_UNROLL 8
-#endif
+constexpr int kFlatUnroll = 8;  // rectangle words in flight at once
 struct FlatLds {
   uint32_t z[kWaves][64];
   int32_t pid[kWaves][64];
   uint32_t first[kWaves][64];
 };
 
-#if RT_FLAT_RECT_LDS
 // a record's rectangle word with its rectangle as packed corners (lo = x0 |
 // y0 << 16, hi = x1 | y1 << 16 in .y / .z; an empty rectangle becomes
 // lo = 0xffffffff, hi = 0xfffefffe, which no pixel matches): the form staged
@@ -263,14 +205,9 @@ __device__ __forceinline__ uint4 rect_corners(uint4 c) {
   c.z = empty ? 0xfffefffeu : (rx >> 16) | (ry & 0xffff0000u);
   return c;
 }
-#endif
 __device__ __forceinline__ uint4 flat_rec(const Scene& S, const uint4* lds, uint32_t k, uint32_t q) {
-#if RT_FLAT_RECT_LDS
   if (q == 2) return lds ? lds[k] : rect_corners(S.A.sld_u4(S.vgeom + 64u * k + 32u));
   return S.A.sld_u4(S.vgeom + 64u * k + 16u * q);
-#else
-  return lds ? lds[4u * k + q] : S.A.sld_u4(S.vgeom + 64u * k + 16u * q);
-#endif
 }
 
 __device__ __forceinline__ void flat_chunk(const vx_task_t& task, bool valid, const Scene& S,
@@ -281,9 +218,7 @@ __device__ __forceinline__ void flat_chunk(const vx_task_t& task, bool valid, co
   if (valid) task_pixel(S, t, &x, &y);
   const bool in = valid && x < S.width && y < S.height;
   const uint32_t px = in ? x : 0xffffffffu;  // outside every pixel rectangle
-#if RT_FLAT_RECT_LDS
   const uint32_t pp = in ? x | (y << 16) : 0xffffffffu;  // packed pixel (rect_corners)
-#endif
   const bool tie_high = (S.flags & RT_FLAG_TIE_HIGH) != 0;
   const uint32_t n = S.num_geom, per = (n + kWaves - 1) / kWaves;
   const uint32_t k0 = w * per < n ? w * per : n, k1 = k0 + per < n ? k0 + per : n;
@@ -291,50 +226,31 @@ __device__ __forceinline__ void flat_chunk(const vx_task_t& task, bool valid, co
   uint32_t bz = VX_OM_DEPTH_MASK;
   int32_t bp = -1;
   uint32_t k = k0;
-#if RT_FLAT_UNROLL > 1
-  // RT_FLAT_UNROLL rectangle words in flight at once (their LDS reads
+  // kFlatUnroll rectangle words in flight at once (their LDS reads
   // overlap), then the candidates among them in ascending order
-  for (; k + RT_FLAT_UNROLL <= k1; k += RT_FLAT_UNROLL) {
-    uint4 C[RT_FLAT_UNROLL];
+  for (; k + kFlatUnroll <= k1; k += kFlatUnroll) {
+    uint4 C[kFlatUnroll];
 #pragma unroll
-    for (int j = 0; j < RT_FLAT_UNROLL; ++j) C[j] = flat_rec(S, lds, k + j, 2);
+    for (int j = 0; j < kFlatUnroll; ++j) C[j] = flat_rec(S, lds, k + j, 2);
     uint32_t cand = 0u;
-#if RT_FLAT_RECT_LDS
-    bool inr[RT_FLAT_UNROLL];
+    bool inr[kFlatUnroll];
 #pragma unroll
-    for (int j = 0; j < RT_FLAT_UNROLL; ++j) {
+    for (int j = 0; j < kFlatUnroll; ++j) {
       inr[j] = rect2_in(C[j].y, C[j].z, pp);
       cand |= mask_ueq(rect2_clamp(C[j].y, C[j].z, pp), pp) ? 1u << j : 0u;
     }
 #pragma unroll
-    for (int j = 0; j < RT_FLAT_UNROLL; ++j)
+    for (int j = 0; j < kFlatUnroll; ++j)
       if ((cand >> j) & 1u)  // wave-uniform
         vis_test_in(flat_rec(S, lds, k + j, 0), flat_rec(S, lds, k + j, 1), C[j],
                     flat_rec(S, lds, k + j, 3), inr[j], px, y, tie_high, bz, bp);
-#else
-#pragma unroll
-    for (int j = 0; j < RT_FLAT_UNROLL; ++j)
-      cand |= __ballot(rect_in(C[j].y, px) && rect_in(C[j].z, y)) ? 1u << j : 0u;
-#pragma unroll
-    for (int j = 0; j < RT_FLAT_UNROLL; ++j)
-      if ((cand >> j) & 1u)  // wave-uniform
-        vis_test(flat_rec(S, lds, k + j, 0), flat_rec(S, lds, k + j, 1), C[j],
-                 flat_rec(S, lds, k + j, 3), px, y, tie_high, bz, bp);
-#endif
   }
-#endif
   for (; k < k1; ++k) {
     const uint4 C = flat_rec(S, lds, k, 2);
-#if RT_FLAT_RECT_LDS
     const bool inr = rect2_in(C.y, C.z, pp);
     if (__ballot(inr) == 0) continue;  // wave-uniform skip
     vis_test_in(flat_rec(S, lds, k, 0), flat_rec(S, lds, k, 1), C, flat_rec(S, lds, k, 3), inr, px,
                 y, tie_high, bz, bp);
-#else
-    if (__ballot(rect_in(C.y, px) && rect_in(C.z, y)) == 0) continue;  // wave-uniform skip
-    vis_test(flat_rec(S, lds, k, 0), flat_rec(S, lds, k, 1), C, flat_rec(S, lds, k, 3), px, y,
-             tie_high, bz, bp);
-#endif
   }
 #ifdef RT_INSTRUMENT
   cnt.tests += in ? k1 - k0 : 0u;  // the whole list per ray, summed over the waves
@@ -367,7 +283,7 @@ __device__ __forceinline__ void flat_chunk(const vx_task_t& task, bool valid, co
     shadow_ray(S, r, th, sr);
     float ts;
     uint32_t first = 0xffffffffu;
-    if (shadow) trace_flat_range<true>(S, sr, k0, k1, 0.0f, 1.0f, hit, tie_high, &ts, &first, nullptr);
+    if (shadow) trace_flat_range<true>(S, sr, k0, k1, 0.0f, 1.0f, hit, tie_high, &ts, &first);
     L.first[w][lane] = first;
   }
   __syncthreads();
@@ -409,12 +325,6 @@ VX_MAIN(rt_kernel_arg_t, arg, RT_BLOCK_THREADS) {
 #endif
   __shared__ WaveLds s_wave[kWaves];
   WaveLds& w = s_wave[threadIdx.x >> 6];
-#ifdef RT_LDS_PAD_WORDS
-  // occupancy probe (A/B only): LDS padding caps the waves per CU; the store
-  // never runs (no real scene has these flags) but keeps the array allocated
-  __shared__ uint32_t s_occ_pad[RT_LDS_PAD_WORDS];
-  if (arg->flags == 0xffffffffu) ((volatile uint32_t*)s_occ_pad)[threadIdx.x] = 0u;
-#endif
 #ifdef RT_STAMPS
   const uint64_t t_stamp0 = __builtin_amdgcn_s_memrealtime();
 #endif
@@ -423,46 +333,27 @@ VX_MAIN(rt_kernel_arg_t, arg, RT_BLOCK_THREADS) {
 #ifdef RT_STAMPS
   if (threadIdx.x == 0) __vx_mpm_lds[10] = (uint32_t)__builtin_amdgcn_s_memrealtime();
 #endif
-#if RT_LDS_SCENE
-  // the whole BVH (nodes + leaf triangles) staged once per workgroup:
-  // traversal then reads LDS (broadcast-friendly, ~100-cycle latency)
-  // instead of the vector-memory path
-  __shared__ float4 s_scene[RT_LDS_SCENE_F4];
-  stage_scene(S, S.num_geom, s_scene);
-  __syncthreads();
-#endif
 #if RT_FLAT
   // stage the geometry list once per workgroup (workgroups past the last
   // task chunk have nothing to render and skip it)
   if (S.num_geom <= RT_FLAT_CAP && blockIdx.x * VX_CHUNK < arg->num_tasks) {  // one chunk per step
-#if RT_FLAT_RECT_LDS
     for (uint32_t i = threadIdx.x; i < S.num_geom; i += blockDim.x)
       s_geom[i] = rect_corners(S.A.ld_u4(S.vgeom + 64u * i + 32u));
-#else
-    for (uint32_t i = threadIdx.x; i < 4u * S.num_geom; i += blockDim.x)
-      s_geom[i] = S.A.ld_u4(S.vgeom + 16u * i);
-#endif
   }
   __syncthreads();
-#endif
-#if RT_FLAT
   __shared__ FlatLds s_flat;
   (void)w;
   const int rc = vx_spawn_chunks_block(
       arg->num_tasks,
       [&](const vx_task_t& task, bool valid, const Scene* s) { flat_chunk(task, valid, *s, s_flat, cnt); },
       &S);
-#elif RT_SHADOW_QUEUE
+#else
   if ((threadIdx.x & 63u) == 0) w.q_count = 0;
   __builtin_amdgcn_wave_barrier();
   const int rc = vx_spawn_tasks_ex(
       arg->num_tasks,
       [&](const vx_task_t& task, const Scene* s) { kernel_body(task, *s, w, cnt); },
       [&](bool final, const Scene* s) { shadow_drain(final, *s, w, cnt); }, &S);
-#else
-  const int rc = vx_spawn_tasks(
-      arg->num_tasks,
-      [&](const vx_task_t& task, const Scene* s) { kernel_body(task, *s, w, cnt); }, &S);
 #endif
 #ifdef RT_STAMPS  // diagnostic image: per-wave phase timestamps
   if (threadIdx.x == 0) {

@@ -1,10 +1,22 @@
 // rt_trace.h -- device pieces shared by the RT kernel programs
 // (rt_kernel.hip: primary + shadow rays; pt_kernel.hip: diffuse path trace):
-// scene arguments, ray setup, Möller–Trumbore, slab test, BVH traversal with
-// the per-lane LDS stack, draw3d-exact shading, pixel addressing.  Numerics
-// are bit-identical to the oracle (oracle/rt.c): every fused multiply-add is
-// an explicit fmaf, everything else is compiled with -ffp-contract=off,
+// scene arguments, ray setup, Möller–Trumbore, slab test, the per-lane BVH
+// walk (closest hit / any hit, stack in LDS) and the wave-packet walks
+// (primary visibility, shadow rays; stack in one VGPR), the per-block
+// candidate lists, draw3d-exact shading, pixel addressing.  Numerics are
+// bit-identical to the oracle (oracle/rt.c): every fused multiply-add is an
+// explicit fmaf, everything else is compiled with -ffp-contract=off,
 // divisions and square roots are IEEE (correctly rounded).
+//
+// Image knobs (Makefile per-image defines; DESIGN.md §4 keeps the record of
+// the variants measured and not kept):
+//   RT_ONLY_BVH4H   the image walks only the binary16 BVH4 (the regular
+//                   images); 0: every layout (the deep images)
+//   RT_BLOCK_LIST   primary visibility from the per-block candidate lists
+//   RT_PUSH_UNCOND  per-lane BVH4 pushes as unconditional rows (path tracer)
+//   RT_LAZY_TASK_ARGS  task-map fields re-read from the argument block
+//   RT_INSTRUMENT   algorithmic counters (node visits, tests, texels)
+//   RT_STAMPS / RT_TRACE_CYCLES  diagnostic per-wave stamps
 #pragma once
 
 #include <hip/hip_runtime.h>
@@ -13,51 +25,11 @@
 #include "rt_common.h"
 #include "vx_spawn.h"
 
-// 1: wave-uniform node / leaf records through the scalar cache (trace());
-// measured 3-4 % slower than per-lane loads on tekkaman, so off by default
-#ifndef RT_SCALAR
-#define RT_SCALAR 0
-#endif
-// distinct primitives per wave shaded from SGPR records (shade_wave());
-// measured neutral, off by default
-#ifndef RT_SHADE_UNIFORM
-#define RT_SHADE_UNIFORM 0
-#endif
-// leaf triangles fetched per batch (1, 2 or 4): register pressure vs overlap
-#ifndef RT_LEAF_BATCH
-#define RT_LEAF_BATCH 4
-#endif
-// 1: primary rays walk the tree as a packet (one walk per wave over the
-// union of its pixels, node / leaf records wave-uniform through the scalar
-// cache, one LDS stack per wave); 0: one walk per lane
-#ifndef RT_VIS_PACKET
-#define RT_VIS_PACKET 1
-#endif
-// primary-visibility leaf records (rt_vtri_t, 64 B) fetched per batch
-#ifndef RT_VIS_BATCH
-#define RT_VIS_BATCH 2
-#endif
-// 1: a leaf's loads are issued only for its own triangle slots (lanes of
-// shorter leaves masked off) instead of all 4 slots unconditionally
-#ifndef RT_LEAF_MASKED
-#define RT_LEAF_MASKED 0
-#endif
-// 1: while-while traversal loop (trace_impl, default: A/B r01_v9 -5.7 % for
-// primary+shadow, -3.4 % for the path tracer); 0: if-if (node step or leaf
-// per iteration)
-#ifndef RT_WW
-#define RT_WW 1
-#endif
-// 1: the first node step of every walk (all lanes at the root) reads the root
-// through the scalar cache -- one load per wave instead of 64 lanes of vector
-// data, and the root is where every background ray's walk ends
-// 1: the image walks only the binary16 BVH4 layout (RT_FLAG_BVH4H, the
-// default build); the host runs the generic image for any other layout
 #ifndef RT_ONLY_BVH4H
 #define RT_ONLY_BVH4H 0
 #endif
-#ifndef RT_ROOT_SCALAR
-#define RT_ROOT_SCALAR 1
+#ifndef RT_BLOCK_LIST
+#define RT_BLOCK_LIST 0
 #endif
 
 namespace rtk {
@@ -81,44 +53,15 @@ struct Scene {
   float sx, sy, light[3];
   uint64_t argp;  // the argument block (constant address space), for lazy_args
 #if RT_BLOCK_LIST
-  uint32_t blist, bidx, bsuf, blist_nbx;  // per-block candidate lists (experiment)
+  uint32_t blist, bidx, bsuf, blist_nbx;  // per-block candidate lists
 #endif
-  // the BVH staged in LDS by the workgroup (RT_LDS_SCENE images), or null
-  const float4* lnodes = nullptr;
-  const float4* ltris = nullptr;
-  const float4* lnodes4h = nullptr;  // the binary16 BVH4 nodes staged in LDS (RT_LDS_NODES4H images)
 };
-
-// LDS budget (float4 slots) for a workgroup-staged BVH: nodes + leaf
-// triangles (+3 padding records); larger scenes stay in global memory
-#ifndef RT_LDS_SCENE_F4
-#define RT_LDS_SCENE_F4 4096
-#endif
-__device__ __forceinline__ uint32_t lds_scene_f4(const Scene& S, uint32_t num_tris) {
-  return 4u * S.num_nodes + 3u * (num_tris + 3u);
-}
-// cooperative copy of nodes + tris into `dst` (all threads of the
-// workgroup; caller syncs); returns whether the scene fits
-__device__ __forceinline__ bool stage_scene(Scene& S, uint32_t num_tris, float4* dst) {
-  const uint32_t n4 = lds_scene_f4(S, num_tris);
-  if (n4 > RT_LDS_SCENE_F4) return false;
-  const uint32_t nn = 4u * S.num_nodes;
-  for (uint32_t i = threadIdx.x; i < n4; i += blockDim.x)
-    dst[i] = S.A.ld_f4(i < nn ? S.nodes + 16u * i : S.tris + 16u * (i - nn));
-  S.lnodes = dst;
-  S.ltris = dst + nn;
-  return true;
-}
 
 // The argument block is read through the scalar cache (constant address
 // space, wave-uniform address): the scene's fields then live in SGPRs, and
 // the traversal loops form node / triangle addresses in scalar registers
 // instead of VGPR + readfirstlane.
-#ifndef RT_SCALAR_ARGS
-#define RT_SCALAR_ARGS 1
-#endif
 __device__ __forceinline__ Scene load_scene(const rt_kernel_arg_t* ga) {
-#if RT_SCALAR_ARGS
   const uint64_t p = (uint64_t)ga;
   // (readfirstlane returns int: through uint32_t, or the low word sign-extends)
   const uint32_t lo = (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)p);
@@ -126,9 +69,6 @@ __device__ __forceinline__ Scene load_scene(const rt_kernel_arg_t* ga) {
   const uint64_t u = ((uint64_t)hi << 32) | (uint64_t)lo;
   const __attribute__((address_space(4))) rt_kernel_arg_t* a =
       (const __attribute__((address_space(4))) rt_kernel_arg_t*)u;
-#else
-  const rt_kernel_arg_t* a = ga;
-#endif
   Scene s;
   s.argp = (uint64_t)a;
   s.A = vx_arena::get();
@@ -310,14 +250,8 @@ __device__ __forceinline__ bool closer(float t, int32_t pid, float bt, int32_t b
   return (t < bt) || (t == bt && (tie_high ? pid > bpid : pid < bpid));
 }
 
-// Per-ray traversal with the LDS stack (oracle/rt.c bvh_trace restates it
-// exactly, counters included).  Each step first checks whether every active
-// lane is at the same node / leaf -- the common case for the coherent rays of
-// an 8x8 pixel wave -- and then reads the record ONCE for the wave through
-// the scalar cache into SGPRs (s_load) instead of 64 lanes x 16 B of
-// vector-memory data return per load (the L1 -> VGPR return path, 64 B/clk
-// per CU, was the busiest unit of the all-vector form).  Divergent steps use
-// per-lane buffer loads.  Both forms compute identical values.
+// BVH2 node step (deep images only: RT_RENDER_BVH2 and the LBVH's BVH2):
+// both slabs of an rt_node_t
 struct NodeStep {
   int32_t c0, c1;
   float tn0, tn1;
@@ -337,39 +271,15 @@ __device__ __forceinline__ NodeStep node_step(const float4& n0, const float4& n1
   return o;
 }
 
-// Per-lane traversal stack: LDS column stack[entry][lane] plus, with RT_TOS,
-// the top entry held in a register -- a pop of the entry pushed last (the
-// common case: the second-nearest child) then costs no LDS round trip on
-// the dependent chain pop -> node load.  Same LIFO order and overflow rule
-// either way.  Measured (A/B, r8a): 3 % slower for primary+shadow, neutral
-// for the path tracer (the extra VGPRs and select chains cost more than the
-// LDS round trip they save), so off.
-#ifndef RT_TOS
-#define RT_TOS 0
-#endif
-// 1: BVH4 node steps without a branch per child or per push
-#ifndef RT_NODE_BRANCHLESS
-#define RT_NODE_BRANCHLESS 1
-#endif
+// Per-lane traversal stack: LDS column stack[entry][lane] (conflict-free);
+// a push onto a full stack is dropped -- the oracle's overflow rule
+// (oracle/rt.c bvh_trace)
 struct LaneStack {
   int32_t* mem;
   int sp = 0;
-  int32_t tos = 0;
-  bool htos = false;
   __device__ __forceinline__ explicit LaneStack(int32_t* m) : mem(m) {}
   __device__ __forceinline__ void push(int32_t x) {
-#if RT_TOS
-    // capacity RT_MAX_STACK entries in total, a push onto a full stack is
-    // dropped -- the oracle's overflow rule (oracle/rt.c bvh_trace)
-    if (htos) {
-      if (sp + 1 >= RT_MAX_STACK) return;
-      mem[64 * sp++] = tos;
-    }
-    tos = x;
-    htos = true;
-#else
     if (sp < RT_MAX_STACK) mem[64 * sp++] = x;
-#endif
   }
   // push the hit children c[1..n-1] of a sorted node step (c[n-1] first, so
   // c[1] ends on top) -- push()'s order and overflow rule, as predicated
@@ -398,13 +308,6 @@ struct LaneStack {
     sp = top < RT_MAX_STACK ? top : RT_MAX_STACK;
   }
   __device__ __forceinline__ bool pop(int32_t& x) {
-#if RT_TOS
-    if (htos) {
-      x = tos;
-      htos = false;
-      return true;
-    }
-#endif
     if (sp == 0) return false;
     x = mem[64 * --sp];
     return true;
@@ -433,14 +336,8 @@ __device__ __forceinline__ int32_t node4_step(const Scene& S, uint32_t ref, cons
     // and each folds into its slab FMA (v_fma_mix_f32: f16 operand, f32 math)
     // -- the layout is a template parameter so no phi separates them
     const uint32_t no = S.nodes4 + 128u * S.num_nodes4 + 64u * ref;
-    float4 px, py, pz;
-    if (!SCALAR && S.lnodes4h) {
-      const float4* n = S.lnodes4h + 4u * ref;
-      px = n[0]; py = n[1]; pz = n[2]; cf = n[3];
-    } else {
-      px = ld(no); py = ld(no + 16); pz = ld(no + 32);
-      cf = ld(no + 48);
-    }
+    const float4 px = ld(no), py = ld(no + 16), pz = ld(no + 32);
+    cf = ld(no + 48);
     auto h2 = [](float w, float& a, float& b) {
       const uint32_t u = __float_as_uint(w);
       a = (float)__builtin_bit_cast(_Float16, (uint16_t)(u & 0xffffu));
@@ -465,14 +362,9 @@ __device__ __forceinline__ int32_t node4_step(const Scene& S, uint32_t ref, cons
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
     float tn = 0.0f;
-#if RT_NODE_BRANCHLESS
     // every lane evaluates all four slabs (no exec-mask branch per child)
     const bool hs = slab(alx[i], ahx[i], aly[i], ahy[i], alz[i], ahz[i], r, tmin, lim, &tn);
     const bool h = hs & (c[i] != RT_EMPTY_REF);
-#else
-    const bool h = c[i] != RT_EMPTY_REF &&
-                   slab(alx[i], ahx[i], aly[i], ahy[i], alz[i], ahz[i], r, tmin, lim, &tn);
-#endif
     k[i] = h ? (any ? (float)i : fminf(tn, 3.402823466e38f)) : __builtin_inff();
     n += h ? 1 : 0;
   }
@@ -491,13 +383,7 @@ __device__ __forceinline__ int32_t node4_step(const Scene& S, uint32_t ref, cons
   cx(1, 3);
   cx(1, 2);
   if (n == 0) return RT_EMPTY_REF;
-#if RT_NODE_BRANCHLESS && !RT_TOS
   st.push_sorted(c, n);
-#else
-  if (n >= 4) st.push(c[3]);
-  if (n >= 3) st.push(c[2]);
-  if (n >= 2) st.push(c[1]);
-#endif
   return c[0];
 }
 
@@ -534,9 +420,6 @@ __device__ __forceinline__ int32_t trace_impl(const Scene& S, const Ray& r, floa
       const uint32_t no = S.nodes + 64u * (uint32_t)r0;
       st = node_step(S.A.sld_f4(no), S.A.sld_f4(no + 16), S.A.sld_f4(no + 32),
                      S.A.sld_f4(no + 48), r, tmin, lim);
-    } else if (S.lnodes) {
-      const float4* n = S.lnodes + 4u * (uint32_t)ref;
-      st = node_step(n[0], n[1], n[2], n[3], r, tmin, lim);
     } else {
       const uint32_t no = S.nodes + 64u * (uint32_t)ref;
       st = node_step(S.A.ld_f4(no), S.A.ld_f4(no + 16), S.A.ld_f4(no + 32),
@@ -552,7 +435,6 @@ __device__ __forceinline__ int32_t trace_impl(const Scene& S, const Ray& r, floa
     return RT_EMPTY_REF;
 #endif
   };
-#if RT_WW && RT_ROOT_SCALAR
   {
     // every lane starts at the root: one wave-uniform (scalar) step; a walk
     // whose root step hits no child has pushed nothing and is over
@@ -560,9 +442,7 @@ __device__ __forceinline__ int32_t trace_impl(const Scene& S, const Ray& r, floa
     if (nx == RT_EMPTY_REF) return -1;
     ref = nx;
   }
-#endif
   for (;;) {
-#if RT_WW
     // while-while (Aila & Laine 2009): a lane steps through inner nodes until
     // it reaches a leaf or its stack runs dry, and the wave tests leaves only
     // once no lane is still in the node loop -- the per-lane sequence of node
@@ -579,86 +459,36 @@ __device__ __forceinline__ int32_t trace_impl(const Scene& S, const Ray& r, floa
       RT_CYC_END(11);
     }
     if (dry) break;
-    const bool uni = false;
     {
-#else
-    const int32_t r0 = __builtin_amdgcn_readfirstlane(ref);
-    const bool uni = RT_SCALAR && __ballot(ref != r0) == 0;  // wave-uniform branch
-    if (ref >= 0) {
-      const int32_t nx = node_next(uni, r0);
-      if (nx != RT_EMPTY_REF) { ref = nx; continue; }
-    } else {
-#endif
       const uint32_t lr = (uint32_t)ref;
       const uint32_t first = (lr >> 4) & 0x07ffffffu, count = (lr & 15u) + 1u;
       RT_WAVE_ITER(9);
-      if (uni) {
-        // one leaf for the whole wave: triangle records in SGPRs, one by one
-        const uint32_t to = S.tris + 48u * first;
-        bool done = false;
+      // a leaf's (up to 4) triangles: all 4 slots loaded at once (the tris
+      // array carries 3 padding records), so their loads overlap
+      const uint32_t to = S.tris + 48u * first;
+      float4 ta[4], tb[4], tc[4];
 #pragma unroll
-        for (uint32_t k = 0; k < 4; ++k) {
-          if (k < count && !done) {
-            const float4 ta = S.A.sld_f4(to + 48u * k), tb = S.A.sld_f4(to + 48u * k + 16);
-            const float4 tc = S.A.sld_f4(to + 48u * k + 32);
-            const int32_t pid = __float_as_int(ta.w);
+      for (uint32_t k = 0; k < 4; ++k) {
+        ta[k] = S.A.ld_f4(to + 48u * k);
+        tb[k] = S.A.ld_f4(to + 48u * k + 16);
+        tc[k] = S.A.ld_f4(to + 48u * k + 32);
+      }
+#pragma unroll
+      for (uint32_t k = 0; k < 4; ++k) {
+        if (k < count) {
+          const int32_t pid = __float_as_int(ta[k].w);
 #ifdef RT_INSTRUMENT
-            ++cnt.tests;
+          ++cnt.tests;
 #endif
-            float t;
-            if (pid != skip && mt_hit(r, ta, tb, tc, tmin, &t)) {
-              if (ANY) {
-                if (t < tmax) { bt = t; bpid = pid; done = true; }
-              } else if (closer(t, pid, bt, bpid, tie_high)) {
-                bt = t;
-                bpid = pid;
-              }
+          float t;
+          if (pid != skip && mt_hit(r, ta[k], tb[k], tc[k], tmin, &t)) {
+            if (ANY) {
+              if (t < tmax) { *t_out = t; return pid; }
+            } else if (closer(t, pid, bt, bpid, tie_high)) {
+              bt = t;
+              bpid = pid;
             }
           }
-        }
-        if (ANY && done) { *t_out = bt; return bpid; }
-      } else {
-        // A leaf's (up to 4) triangles are fetched RT_LEAF_BATCH at a time
-        // (all slots unconditionally: the tris array carries 3 padding
-        // records), so their loads overlap.
-        const uint32_t to = S.tris + 48u * first;
-#pragma unroll
-        for (uint32_t k0 = 0; k0 < 4; k0 += RT_LEAF_BATCH) {
-          if (k0 >= count) break;
-        float4 ta[RT_LEAF_BATCH], tb[RT_LEAF_BATCH], tc[RT_LEAF_BATCH];
-#pragma unroll
-        for (uint32_t j = 0; j < RT_LEAF_BATCH; ++j) {
-          const uint32_t k = k0 + j;
-          if (S.ltris) {
-            const float4* tr = S.ltris + 3u * (first + k);
-            ta[j] = tr[0]; tb[j] = tr[1]; tc[j] = tr[2];
-          } else if (!RT_LEAF_MASKED || k < count) {
-            ta[j] = S.A.ld_f4(to + 48u * k);
-            tb[j] = S.A.ld_f4(to + 48u * k + 16);
-            tc[j] = S.A.ld_f4(to + 48u * k + 32);
-          } else {
-            ta[j] = tb[j] = tc[j] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-          }
-        }
-#pragma unroll
-        for (uint32_t j = 0; j < RT_LEAF_BATCH; ++j) {
-          const uint32_t k = k0 + j;
-          if (k < count) {
-            const int32_t pid = __float_as_int(ta[j].w);
-#ifdef RT_INSTRUMENT
-            ++cnt.tests;
-#endif
-            float t;
-            if (pid != skip && mt_hit(r, ta[j], tb[j], tc[j], tmin, &t)) {
-              if (ANY) {
-                if (t < tmax) { *t_out = t; return pid; }
-              } else if (closer(t, pid, bt, bpid, tie_high)) {
-                bt = t;
-                bpid = pid;
-              }
-            }
-          }
-        }
         }
       }
     }
@@ -681,30 +511,13 @@ __device__ __forceinline__ int32_t trace_impl(const Scene& S, const Ray& r, floa
 // box; per stack entry one bit of `onb`) and unfinished.  Measured (A/B,
 // tekkaman 1024^2 primary + shadow): -9 % kernel time vs per-lane walks
 // (0.0565 -> 0.0514 ms): the heavy tiles' shadow rays are coherent.  Every
-// active lane calls it (any EXEC mask: the stack words are stored by all
-// active lanes and read back with readfirstlane).
-// (2: off-path lanes folded into the slab's far limit and the child mask
-// taken from one v_cmp -- 0.8 % slower than 1 in A/B, ab_packet_fold.json)
-#ifndef RT_PACKET_BRANCHLESS
-#define RT_PACKET_BRANCHLESS 1
-#endif
-// packet leaves: this many triangle records loaded before any is tested
-// (1: one record at a time).  A/B (profiles/r02/ab_packet_leaf_hoist.json,
-// tekkaman 1024^2 primary + shadow): 1 0.0450 ms, 2 0.0426, 4 0.0436 (4
-// spills twice the SGPRs); the path tracer is neutral (0.179 / 0.177 / 0.178)
-#ifndef RT_PACKET_LEAF_HOIST
-#define RT_PACKET_LEAF_HOIST 2
-#endif
-// the same for the shadow packets' leaves (48-B records)
-#ifndef RT_SHADOW_LEAF_HOIST
-#define RT_SHADOW_LEAF_HOIST RT_PACKET_LEAF_HOIST
-#endif
-// 1: a packet walk's (wave-uniform) stack lives in one VGPR, entry i in lane
-// i (v_writelane / v_readlane: no LDS round trip on the pop -> node-load
-// chain); 0: the wave's LDS stack column
-#ifndef RT_PACKET_VSTACK
-#define RT_PACKET_VSTACK 1
-#endif
+// active lane calls it (any EXEC mask).  The walk's (wave-uniform) stack
+// lives in one VGPR, entry i in lane i (v_writelane / v_readlane: no LDS
+// round trip on the pop -> node-load chain); a node (64 B) and a leaf's
+// records, two at a time, arrive through one pointer each as wide s_loads.
+// Packet leaves load this many records before testing any (A/B,
+// profiles/r02/ab_packet_leaf_hoist.json: 1 0.0450 ms, 2 0.0426, 4 0.0436)
+constexpr uint32_t kLeafHoist = 2;
 // v_writelane_b32: lane `lane` of v := val (wave-uniform val and lane; EXEC
 // is ignored, so it works under any mask)
 __device__ __forceinline__ int32_t vwritelane(int32_t v, int32_t val, int32_t lane) {
@@ -714,33 +527,15 @@ __device__ __forceinline__ int32_t vwritelane(int32_t v, int32_t val, int32_t la
   asm("v_writelane_b32 %0, %1, m0" : "+v"(v) : "s"(x), "{m0}"(l));
   return v;
 }
-#ifndef RT_BLOCK_LIST
-#define RT_BLOCK_LIST 0
-#endif
-// 1: packet walks load a node (64 B) or a leaf's hoisted triangle records
-// through one pointer, so they merge into wide s_loads
-#ifndef RT_SLD_WIDE
-#define RT_SLD_WIDE 1
-#endif
 __device__ __forceinline__ float4 u4f(const uint4 u) {
   return make_float4(__uint_as_float(u.x), __uint_as_float(u.y), __uint_as_float(u.z),
                      __uint_as_float(u.w));
 }
-// wave priority while walking a packet (0: unchanged): the packet walks are
-// the heavy tiles' latency chains
-#ifndef RT_PACKET_PRIO
-#define RT_PACKET_PRIO 0
-#endif
 __device__ __forceinline__ bool occluded_packet(const Scene& S, const Ray& r, bool act, int32_t skip,
-                                                float tmax, int32_t* stack, Counters& cnt) {
+                                                float tmax, Counters& cnt) {
   bool done = !act, occ = false;
   if (S.num_nodes4 == 0 || __ballot(!done) == 0) return false;
-#if RT_PACKET_PRIO
-  __builtin_amdgcn_s_setprio(RT_PACKET_PRIO);
-#endif
-  int32_t* ws = stack - lane_id();
-  (void)ws;
-  int32_t vstk = 0;  // RT_PACKET_VSTACK: stack entry i in lane i of this VGPR
+  int32_t vstk = 0;  // stack entry i in lane i of this VGPR
   int sp = 0;
   int32_t ref = 0;
   bool on = true;     // this lane's ray hit the current node's box (and its ancestors')
@@ -754,16 +549,11 @@ __device__ __forceinline__ bool occluded_packet(const Scene& S, const Ray& r, bo
 #endif
       RT_WAVE_ITER(9);
       const uint32_t no = S.nodes4 + 128u * S.num_nodes4 + 64u * (uint32_t)ref;
-#if RT_SLD_WIDE
       uint4 nw[4];
       RT_LD_BEGIN();
       S.A.sld_u4n<4>(no, nw);  // one s_load_dwordx16
       RT_LD_END(1);
       const uint4 px = nw[0], py = nw[1], pz = nw[2], cf = nw[3];
-#else
-      const uint4 px = S.A.sld_u4(no), py = S.A.sld_u4(no + 16), pz = S.A.sld_u4(no + 32),
-                  cf = S.A.sld_u4(no + 48);
-#endif
       float lx[4], hx[4], ly[4], hy[4], lz[4], hz[4];
       auto h2 = [](uint32_t u, float& a, float& b) {
         a = (float)__builtin_bit_cast(_Float16, (uint16_t)(u & 0xffffu));
@@ -775,38 +565,12 @@ __device__ __forceinline__ bool occluded_packet(const Scene& S, const Ray& r, bo
       const int32_t c[4] = {(int32_t)cf.x, (int32_t)cf.y, (int32_t)cf.z, (int32_t)cf.w};
       bool h[4];
       uint32_t need = 0u;  // wave-uniform: children some live lane enters
-#if RT_PACKET_BRANCHLESS == 3
-      const uint64_t lm = __ballot(live);  // once per node, not per child
-#endif
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         float tn = 0.0f;
-#if RT_PACKET_BRANCHLESS == 3
-        // the per-lane bit as in 1; the wave's child mask from the slab's own
-        // v_cmp ANDed with the node's live mask (no re-materialised ballot)
-        float tf;
-        const bool hs = slab_nf(lx[i], hx[i], ly[i], hy[i], lz[i], hz[i], r, 0.0f, tmax, &tn, &tf);
-        const bool cv = c[i] != RT_EMPTY_REF;
-        h[i] = hs & live & cv;
-        need |= (mask_fle(tn, tf) & lm & (cv ? ~0ull : 0ull)) != 0 ? 1u << i : 0u;
-        continue;
-#elif RT_PACKET_BRANCHLESS == 2
-        // lanes off the path and empty slots test against a negative far
-        // limit, which the slab test itself rejects (its near value is >= 0):
-        // h is one compare, the same value as the masked form below
-        const float lim = (live && c[i] != RT_EMPTY_REF) ? tmax : -1.0f;
-        float tf;
-        h[i] = slab_nf(lx[i], hx[i], ly[i], hy[i], lz[i], hz[i], r, 0.0f, lim, &tn, &tf);
-        need |= mask_fle(tn, tf) ? 1u << i : 0u;
-        continue;
-#elif RT_PACKET_BRANCHLESS
         // every lane evaluates the slab (no exec-mask branch per child)
         const bool hs = slab(lx[i], hx[i], ly[i], hy[i], lz[i], hz[i], r, 0.0f, tmax, &tn);
         h[i] = hs & live & (c[i] != RT_EMPTY_REF);
-#else
-        h[i] = live && c[i] != RT_EMPTY_REF &&
-               slab(lx[i], hx[i], ly[i], hy[i], lz[i], hz[i], r, 0.0f, tmax, &tn);
-#endif
         need |= __ballot(h[i]) ? 1u << i : 0u;
       }
       if (need) {
@@ -815,11 +579,7 @@ __device__ __forceinline__ bool occluded_packet(const Scene& S, const Ray& r, bo
         for (int i = 3; i >= 1; --i) {
           if ((need >> i) & 1u && (need & ((1u << i) - 1u))) {
             if (sp < RT_MAX_STACK) {
-#if RT_PACKET_VSTACK
               vstk = vwritelane(vstk, c[i], sp);
-#else
-              ws[64 * sp] = c[i];  // every active lane stores the same word
-#endif
               onb = h[i] ? onb | (1u << sp) : onb & ~(1u << sp);
               ++sp;
             }
@@ -835,14 +595,12 @@ __device__ __forceinline__ bool occluded_packet(const Scene& S, const Ray& r, bo
       const uint32_t first = (lr >> 4) & 0x07ffffffu, count = (lr & 15u) + 1u;
       RT_WAVE_ITER(9);
       bool lv = live;
-#if RT_SHADOW_LEAF_HOIST > 1
-      // RT_SHADOW_LEAF_HOIST slots in flight at once (3 padding records)
-      constexpr uint32_t H = RT_SHADOW_LEAF_HOIST;
+      // kLeafHoist slots in flight at once (3 padding records)
+      constexpr uint32_t H = kLeafHoist;
 #pragma unroll
       for (uint32_t q0 = 0; q0 < 4; q0 += H) {
         if (q0 >= count) break;
         float4 ta[H], tb[H], tc[H];
-#if RT_SLD_WIDE
         {  // the H consecutive records from one address (wide s_loads)
           uint4 tw[3 * H];
           RT_LD_BEGIN();
@@ -853,13 +611,6 @@ __device__ __forceinline__ bool occluded_packet(const Scene& S, const Ray& r, bo
             ta[j] = u4f(tw[3 * j]); tb[j] = u4f(tw[3 * j + 1]); tc[j] = u4f(tw[3 * j + 2]);
           }
         }
-#else
-#pragma unroll
-        for (uint32_t j = 0; j < H; ++j) {
-          const uint32_t to = S.tris + 48u * (first + q0 + j);
-          ta[j] = S.A.sld_f4(to); tb[j] = S.A.sld_f4(to + 16); tc[j] = S.A.sld_f4(to + 32);
-        }
-#endif
 #pragma unroll
         for (uint32_t j = 0; j < H; ++j) {
           if (q0 + j < count) {
@@ -876,36 +627,13 @@ __device__ __forceinline__ bool occluded_packet(const Scene& S, const Ray& r, bo
           }
         }
       }
-#else
-      for (uint32_t q = 0; q < count; ++q) {
-        const uint32_t to = S.tris + 48u * (first + q);
-        const float4 ta = S.A.sld_f4(to), tb = S.A.sld_f4(to + 16), tc = S.A.sld_f4(to + 32);
-#ifdef RT_INSTRUMENT
-        cnt.tests += lv;
-#endif
-        float t;
-        if (lv && __float_as_int(ta.w) != skip && mt_hit(r, ta, tb, tc, 0.0f, &t) && t < tmax) {
-          occ = true;
-          done = true;
-          lv = false;
-        }
-      }
-#endif
       if (__ballot(!done) == 0) break;
     }
     if (sp == 0) break;
     --sp;
     on = (onb >> sp) & 1u;
-#if RT_PACKET_VSTACK
     ref = __builtin_amdgcn_readlane(vstk, sp);
-#else
-    __builtin_amdgcn_wave_barrier();
-    ref = __builtin_amdgcn_readfirstlane(ws[64 * sp]);
-#endif
   }
-#if RT_PACKET_PRIO
-  __builtin_amdgcn_s_setprio(0);
-#endif
   return occ;
 }
 
@@ -923,64 +651,23 @@ __device__ __forceinline__ int32_t trace_mixed(const Scene& S, const Ray& r, flo
 }
 
 // Flat triangle list, no BVH (BASELINE config 2; the oracle's brute_trace):
-// every lane tests every geometry triangle in ascending pid order -- the
-// same triangle in all lanes at once, so the records come from LDS (`lds`,
-// staged once per workgroup) as broadcast reads, or through the scalar cache
-// when the list does not fit (`lds` == nullptr).  Counters count every
-// triangle visited, as brute_trace does.
-template <bool ANY>
-__device__ __forceinline__ int32_t trace_flat(const Scene& S, const Ray& r, float tmin, float tmax,
-                                              int32_t skip, bool tie_high, float* t_out,
-                                              const float4* lds, Counters& cnt) {
-  float bt = tmax;
-  int32_t bpid = -1;
-  for (uint32_t k = 0; k < S.num_geom; ++k) {
-    float4 ta, tb, tc;
-    if (lds) {
-      ta = lds[3 * k]; tb = lds[3 * k + 1]; tc = lds[3 * k + 2];
-    } else {
-      const uint32_t o = S.geom + 48u * k;
-      ta = S.A.sld_f4(o); tb = S.A.sld_f4(o + 16); tc = S.A.sld_f4(o + 32);
-    }
-    const int32_t pid = __float_as_int(ta.w);
-#ifdef RT_INSTRUMENT
-    ++cnt.tests;
-#endif
-    if (pid == skip) continue;
-    float t;
-    if (mt_hit(r, ta, tb, tc, tmin, &t)) {
-      if (ANY) {
-        if (t < tmax) { *t_out = t; return pid; }
-      } else if (closer(t, pid, bt, bpid, tie_high)) {
-        bt = t;
-        bpid = pid;
-      }
-    }
-  }
-  if (bpid >= 0) *t_out = bt;
-  return bpid;
-}
-
-// One wave's share [k0, k1) of the flat list (the flat image splits every
-// ray's list across the waves of its workgroup).  Closest hit (ANY = false)
-// or the first hit in list order (ANY = true: *first = its index, else
-// UINT32_MAX).  Counts nothing: the caller accounts the algorithmic tests.
+// one wave's share [k0, k1) of the geometry list in ascending pid order (the
+// flat image splits every ray's list across the waves of its workgroup), the
+// same record in all lanes at once through the scalar cache.  Closest hit
+// (ANY = false) or the first hit in list order (ANY = true: *first = its
+// index, else UINT32_MAX).  Counts nothing: the caller accounts the
+// algorithmic tests.
 template <bool ANY>
 __device__ __forceinline__ int32_t trace_flat_range(const Scene& S, const Ray& r, uint32_t k0,
                                                     uint32_t k1, float tmin, float tmax,
                                                     int32_t skip, bool tie_high, float* t_out,
-                                                    uint32_t* first, const float4* lds) {
+                                                    uint32_t* first) {
   float bt = tmax;
   int32_t bpid = -1;
   *first = 0xffffffffu;
   for (uint32_t k = k0; k < k1; ++k) {
-    float4 ta, tb, tc;
-    if (lds) {
-      ta = lds[3 * k]; tb = lds[3 * k + 1]; tc = lds[3 * k + 2];
-    } else {
-      const uint32_t o = S.geom + 48u * k;
-      ta = S.A.sld_f4(o); tb = S.A.sld_f4(o + 16); tc = S.A.sld_f4(o + 32);
-    }
+    const uint32_t o = S.geom + 48u * k;
+    const float4 ta = S.A.sld_f4(o), tb = S.A.sld_f4(o + 16), tc = S.A.sld_f4(o + 32);
     const int32_t pid = __float_as_int(ta.w);
     if (pid == skip) continue;
     float t;
@@ -1010,28 +697,12 @@ __device__ __forceinline__ uint32_t shade_lane(const Scene& S, int32_t pid, uint
   return gfx::shade(S.A, p, s, x, y);
 }
 
-// Shade every lane with spid >= 0: the wave's most common primitives first
-// from SGPR records (s_load, one record read per wave -- the background
-// layer's two triangles cover most waves), then whatever is left from
-// per-lane record loads.
+// Shade every lane with spid >= 0 from per-lane record loads (wave-uniform
+// records through the scalar cache for the wave's most common primitives
+// measured neutral)
 __device__ __forceinline__ uint32_t shade_wave(const Scene& S, int32_t spid, uint32_t x,
                                                uint32_t y, uint32_t color, Counters& cnt) {
-  uint64_t need = __ballot(spid >= 0);
-#pragma unroll 1
-  for (int it = 0; need != 0 && it < RT_SHADE_UNIFORM; ++it) {
-    const int32_t u = __builtin_amdgcn_readlane(spid, (int)__builtin_ctzll(need));
-    gfx::Prim p;
-    gfx::load_prim<true>(S.A, S.prims + 128u * (uint32_t)u, p);
-    const gfx::DcState s = gfx::load_dcstate<true>(S.A, S.dcs + 64u * p.dc());
-    if (spid == u) {
-      color = gfx::shade(S.A, p, s, x, y);
-#ifdef RT_INSTRUMENT
-      ++cnt.shaded;
-      if (s.flags & RT_DC_TEX) cnt.texel_bytes += (s.filter == VX_TEX_FILTER_BILINEAR ? 4u : 1u) * s.stride;
-#endif
-    }
-    need &= ~__ballot(spid == u);
-  }
+  const uint64_t need = __ballot(spid >= 0);
   if (need != 0 && (need & (1ull << lane_id())) != 0) color = shade_lane(S, spid, x, y, cnt);
   return color;
 }
@@ -1105,100 +776,14 @@ __device__ __forceinline__ void vis_test(const uint4& A, const uint4& B, const u
   vis_test_in(A, B, C, D, rect_in(C.y, px) && rect_in(C.z, py), px, py, tie_high, bz, bpid);
 }
 
-// rt_vnode_t step: children whose pixel rectangle holds (px, py) and whose
-// depth bound can still win, in slot order -- the setup stores a node's
-// slots in ascending depth bound (vis.cpp SortSlots), so that is nearest
-// first with no sort per step; the first is returned, the others pushed last
-// slot first.  SCALAR: every active lane is
-// at this node (s_load into SGPRs).
-template <bool SCALAR>
-__device__ __forceinline__ int32_t vnode_step(const Scene& S, uint32_t ref, uint32_t px, uint32_t py,
-                                              uint32_t bz, LaneStack& st) {
-  auto ld = [&](uint32_t o) { return SCALAR ? S.A.sld_u4(o) : S.A.ld_u4(o); };
-  const uint32_t o = S.vnodes + 64u * ref;
-  const uint4 rl = ld(o), rh = ld(o + 16), zm = ld(o + 32), cf = ld(o + 48);
-  const uint32_t alo[4] = {rl.x, rl.y, rl.z, rl.w}, ahi[4] = {rh.x, rh.y, rh.z, rh.w};
-  const uint32_t azm[4] = {zm.x, zm.y, zm.z, zm.w};
-  int32_t c[4] = {(int32_t)cf.x, (int32_t)cf.y, (int32_t)cf.z, (int32_t)cf.w};
-  const uint32_t pp = px > 0xffffu ? 0xffffffffu : px | (py << 16);
-  // the slots are stored in ascending depth bound (vis.cpp SortSlots): the
-  // needed children in slot order are nearest first
-  uint32_t need = 0u;
-#pragma unroll
-  for (int i = 0; i < 4; ++i)
-    need |= (c[i] != RT_EMPTY_REF && rect2_in(alo[i], ahi[i], pp) && azm[i] <= bz) ? 1u << i : 0u;
-  if (need == 0u) return RT_EMPTY_REF;
-#pragma unroll
-  for (int i = 3; i >= 1; --i)  // the others pushed farthest (last slot) first
-    if ((need >> i) & 1u && (need & ((1u << i) - 1u))) st.push(c[i]);
-  const int f = __builtin_ctz(need);
-  return f == 0 ? c[0] : f == 1 ? c[1] : f == 2 ? c[2] : c[3];
-}
-
 // The primary ray's hit: the draw3d depth-test winner among the geometry
-// primitives covering (px, py), or -1 (oracle/rt.c vis_trace restates it,
-// counters included).  Per-lane walk, while-while loop as trace_impl.
-__device__ __forceinline__ int32_t trace_primary_lane(const Scene& S, uint32_t px, uint32_t py,
-                                                      bool tie_high, int32_t* stack, Counters& cnt) {
-  if (S.num_vnodes == 0) return -1;
-  LaneStack lst(stack);
-  uint32_t bz = VX_OM_DEPTH_MASK;
-  int32_t bpid = -1;
-  int32_t ref;
-  {  // every lane starts at the root: one wave-uniform (scalar) step
-#ifdef RT_INSTRUMENT
-    ++cnt.visits;
-#endif
-    ref = vnode_step<true>(S, 0u, px, py, bz, lst);
-    if (ref == RT_EMPTY_REF) return -1;
-  }
-  for (;;) {
-    bool dry = false;
-    while (ref >= 0) {
-#ifdef RT_INSTRUMENT
-      ++cnt.visits;
-#endif
-      RT_WAVE_ITER(7);
-      const int32_t nx = vnode_step<false>(S, (uint32_t)ref, px, py, bz, lst);
-      if (nx != RT_EMPTY_REF) { ref = nx; continue; }
-      if (!lst.pop(ref)) { dry = true; break; }
-    }
-    if (dry) break;
-    const uint32_t lr = (uint32_t)ref;
-    const uint32_t first = (lr >> 4) & 0x07ffffffu, count = (lr & 15u) + 1u;
-    const uint32_t to = S.vtris + 64u * first;
-    RT_WAVE_ITER(8);
-#pragma unroll
-    for (uint32_t k0 = 0; k0 < 4; k0 += RT_VIS_BATCH) {
-      if (k0 >= count) break;
-      uint4 a[RT_VIS_BATCH], b[RT_VIS_BATCH], c[RT_VIS_BATCH], d[RT_VIS_BATCH];
-#pragma unroll
-      for (uint32_t j = 0; j < RT_VIS_BATCH; ++j) {
-        const uint32_t o = to + 64u * (k0 + j);
-        a[j] = S.A.ld_u4(o); b[j] = S.A.ld_u4(o + 16); c[j] = S.A.ld_u4(o + 32); d[j] = S.A.ld_u4(o + 48);
-      }
-#pragma unroll
-      for (uint32_t j = 0; j < RT_VIS_BATCH; ++j) {
-        if (k0 + j < count) {
-#ifdef RT_INSTRUMENT
-          ++cnt.tests;
-#endif
-          vis_test(a[j], b[j], c[j], d[j], px, py, tie_high, bz, bpid);
-        }
-      }
-    }
-    if (!lst.pop(ref)) break;
-  }
-  return bpid;
-}
-
-// Packet form (RT_VIS_PACKET): the wave's pixels walk the tree together.
+// primitives covering (px, py), or -1.  The wave's pixels walk the tree
+// together (oracle/rt.c vis_trace_packet).
 // A child is entered when, for some lane, the pixel lies in the child's
 // rectangle and the child's depth bound can still beat that lane's best
 // (ballot); the entered children are taken in slot order (= ascending
 // bound, vis.cpp SortSlots: no sorting network per step) and the others
-// pushed farthest first on the
-// wave's LDS stack (entries stride 64 in `stack`, written by lane 0).  Node
+// pushed farthest first on the wave's VGPR stack.  Node
 // and leaf records are wave-uniform: scalar loads, one per record for the
 // wave instead of 64 lanes' gathers.  Each lane runs the exact coverage and
 // depth test on every leaf primitive of the walk, so the result is the
@@ -1207,17 +792,11 @@ __device__ __forceinline__ int32_t trace_primary_lane(const Scene& S, uint32_t p
 // included).  Every lane of the wave must call it; `act` = this lane holds
 // a pixel.
 __device__ __forceinline__ int32_t trace_primary_packet(const Scene& S, uint32_t px, uint32_t py,
-                                                        bool act, bool tie_high, int32_t* stack,
-                                                        Counters& cnt) {
+                                                        bool act, bool tie_high, Counters& cnt) {
   if (S.num_vnodes == 0) return -1;
   if (!act) px = 0xffffffffu;  // in no rectangle
   const uint32_t pp = px > 0xffffu ? 0xffffffffu : px | (py << 16);  // packed pixel (rect2_in)
-#if RT_PACKET_PRIO
-  __builtin_amdgcn_s_setprio(RT_PACKET_PRIO);
-#endif
-  int32_t* ws = stack - lane_id();  // the wave's column base (lane 0's column)
-  (void)ws;
-  int32_t vstk = 0;  // RT_PACKET_VSTACK: stack entry i in lane i of this VGPR
+  int32_t vstk = 0;  // stack entry i in lane i of this VGPR
   const bool l0 = lane_id() == 0;
   uint32_t bz = VX_OM_DEPTH_MASK;
   int32_t bpid = -1;
@@ -1230,16 +809,11 @@ __device__ __forceinline__ int32_t trace_primary_packet(const Scene& S, uint32_t
 #endif
       RT_WAVE_ITER(7);
       const uint32_t o = S.vnodes + 64u * (uint32_t)ref;
-#if RT_SLD_WIDE
       uint4 vw[4];
       RT_LD_BEGIN();
       S.A.sld_u4n<4>(o, vw);  // one s_load_dwordx16
       RT_LD_END(0);
       const uint4 rl = vw[0], rh = vw[1], zm = vw[2], cf = vw[3];
-#else
-      const uint4 rl = S.A.sld_u4(o), rh = S.A.sld_u4(o + 16), zm = S.A.sld_u4(o + 32),
-                  cf = S.A.sld_u4(o + 48);
-#endif
       const uint32_t alo[4] = {rl.x, rl.y, rl.z, rl.w}, ahi[4] = {rh.x, rh.y, rh.z, rh.w};
       const uint32_t azm[4] = {zm.x, zm.y, zm.z, zm.w};
       int32_t c[4] = {(int32_t)cf.x, (int32_t)cf.y, (int32_t)cf.z, (int32_t)cf.w};
@@ -1262,11 +836,7 @@ __device__ __forceinline__ int32_t trace_primary_packet(const Scene& S, uint32_t
 #pragma unroll
         for (int i = 3; i >= 1; --i) {
           if ((need >> i) & 1u && (need & ((1u << i) - 1u)) && sp < RT_MAX_STACK) {
-#if RT_PACKET_VSTACK
             vstk = vwritelane(vstk, c[i], sp);
-#else
-            if (l0) ws[64 * sp] = c[i];
-#endif
             ++sp;
           }
         }
@@ -1278,16 +848,14 @@ __device__ __forceinline__ int32_t trace_primary_packet(const Scene& S, uint32_t
       const uint32_t lr = (uint32_t)ref;
       const uint32_t first = (lr >> 4) & 0x07ffffffu, count = (lr & 15u) + 1u;
       RT_WAVE_ITER(8);
-#if RT_PACKET_LEAF_HOIST > 1
-      // RT_PACKET_LEAF_HOIST slots' records in flight at once (the vtris
-      // array carries 3 padding records), then their tests: fewer scalar-load
+      // kLeafHoist slots' records in flight at once (the vtris array
+      // carries 3 padding records), then their tests: fewer scalar-load
       // round trips on the walk's dependent chain
-      constexpr uint32_t H = RT_PACKET_LEAF_HOIST;
+      constexpr uint32_t H = kLeafHoist;
 #pragma unroll
       for (uint32_t k0 = 0; k0 < 4; k0 += H) {
         if (k0 >= count) break;
         uint4 A[H], B[H], C[H], D[H];
-#if RT_SLD_WIDE
         {  // the H consecutive records from one address (wide s_loads)
           uint4 tw[4 * H];
           RT_LD_BEGIN();
@@ -1298,14 +866,6 @@ __device__ __forceinline__ int32_t trace_primary_packet(const Scene& S, uint32_t
             A[j] = tw[4 * j]; B[j] = tw[4 * j + 1]; C[j] = tw[4 * j + 2]; D[j] = tw[4 * j + 3];
           }
         }
-#else
-#pragma unroll
-        for (uint32_t j = 0; j < H; ++j) {
-          const uint32_t o = S.vtris + 64u * (first + k0 + j);
-          A[j] = S.A.sld_u4(o); B[j] = S.A.sld_u4(o + 16); C[j] = S.A.sld_u4(o + 32);
-          D[j] = S.A.sld_u4(o + 48);
-        }
-#endif
 #pragma unroll
         for (uint32_t j = 0; j < H; ++j) {
           if (k0 + j < count) {
@@ -1316,30 +876,11 @@ __device__ __forceinline__ int32_t trace_primary_packet(const Scene& S, uint32_t
           }
         }
       }
-#else
-      for (uint32_t k = 0; k < count; ++k) {
-        const uint32_t o = S.vtris + 64u * (first + k);
-        const uint4 A = S.A.sld_u4(o), B = S.A.sld_u4(o + 16), C = S.A.sld_u4(o + 32),
-                    D = S.A.sld_u4(o + 48);
-#ifdef RT_INSTRUMENT
-        cnt.tests += l0;
-#endif
-        vis_test(A, B, C, D, px, py, tie_high, bz, bpid);
-      }
-#endif
     }
     if (sp == 0) break;
     --sp;
-#if RT_PACKET_VSTACK
     ref = __builtin_amdgcn_readlane(vstk, sp);
-#else
-    __builtin_amdgcn_wave_barrier();
-    ref = __builtin_amdgcn_readfirstlane(ws[64 * sp]);
-#endif
   }
-#if RT_PACKET_PRIO
-  __builtin_amdgcn_s_setprio(0);
-#endif
   return bpid;
 }
 
@@ -1379,16 +920,12 @@ __device__ __forceinline__ int32_t block_primary(const Scene& S, uint32_t px, ui
 #endif
 
 __device__ __forceinline__ int32_t trace_primary(const Scene& S, uint32_t px, uint32_t py, bool act,
-                                                 bool tie_high, int32_t* stack, Counters& cnt) {
+                                                 bool tie_high, Counters& cnt) {
 #if RT_BLOCK_LIST
   if (S.blist_nbx) return block_primary(S, px, py, act, tie_high, cnt);
 #endif
-#if RT_VIS_PACKET
-  const int32_t h = trace_primary_packet(S, px, py, act, tie_high, stack, cnt);
+  const int32_t h = trace_primary_packet(S, px, py, act, tie_high, cnt);
   return act ? h : -1;
-#else
-  return act ? trace_primary_lane(S, px, py, tie_high, stack, cnt) : -1;
-#endif
 }
 
 // ray parameter of the primary ray's intersection with the plane of

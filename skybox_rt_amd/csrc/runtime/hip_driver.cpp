@@ -38,10 +38,13 @@
 // past the buffer -> -1; unknown caps id -> -1 (simx aborts).
 #include <hip/hip_runtime.h>
 
+#include <elf.h>
+
 #include <chrono>
 #include <cstdlib>
 #include <cstring>
 #include <map>
+#include <string>
 #include <thread>
 #include <vector>
 
@@ -82,9 +85,46 @@ uint64_t fnv1a(const uint8_t* p, size_t n) {
   return h;
 }
 
+// The kernel entry of a code object: every image defines one VX_MAIN entry
+// named vx_main or vx_main_<image> (include/vx_spawn.h VX_ENTRY; distinct
+// names let a rocprofv3 kernel trace tell the images apart).  Read from the
+// ELF symbol table: the kernel descriptor symbol "<entry>.kd".
+std::string entry_name(const std::vector<uint8_t>& img) {
+  const std::string dflt = "vx_main";
+  if (img.size() < sizeof(Elf64_Ehdr) || std::memcmp(img.data(), ELFMAG, SELFMAG) != 0) return dflt;
+  Elf64_Ehdr eh;
+  std::memcpy(&eh, img.data(), sizeof(eh));
+  if (eh.e_shoff == 0 || eh.e_shentsize != sizeof(Elf64_Shdr) ||
+      eh.e_shoff + (uint64_t)eh.e_shnum * sizeof(Elf64_Shdr) > img.size())
+    return dflt;
+  auto shdr = [&](uint32_t i) {
+    Elf64_Shdr sh;
+    std::memcpy(&sh, img.data() + eh.e_shoff + (uint64_t)i * sizeof(Elf64_Shdr), sizeof(sh));
+    return sh;
+  };
+  for (uint32_t i = 0; i < eh.e_shnum; ++i) {
+    const Elf64_Shdr sym = shdr(i);
+    if (sym.sh_type != SHT_SYMTAB || sym.sh_link >= eh.e_shnum) continue;
+    const Elf64_Shdr str = shdr(sym.sh_link);
+    if (sym.sh_offset + sym.sh_size > img.size() || str.sh_offset + str.sh_size > img.size()) continue;
+    for (uint64_t o = 0; o + sizeof(Elf64_Sym) <= sym.sh_size; o += sizeof(Elf64_Sym)) {
+      Elf64_Sym e;
+      std::memcpy(&e, img.data() + sym.sh_offset + o, sizeof(e));
+      if (e.st_name >= str.sh_size) continue;
+      const char* nm = (const char*)img.data() + str.sh_offset + e.st_name;
+      const size_t len = strnlen(nm, str.sh_size - e.st_name);
+      const std::string n(nm, len);
+      if (n.size() > 3 && n.compare(n.size() - 3, 3, ".kd") == 0 && n.rfind("vx_main", 0) == 0)
+        return n.substr(0, n.size() - 3);
+    }
+  }
+  return dflt;
+}
+
 struct Module {
   hipModule_t module = nullptr;
   hipFunction_t entry = nullptr;
+  std::string name;  // the entry's symbol
   hipDeviceptr_t dcrs = nullptr, mem_base = nullptr, mpm = nullptr;
   size_t dcrs_size = 0, mpm_size = 0;
   uint32_t block = 0, grid = 0;
@@ -443,7 +483,8 @@ class vx_device {
     const std::vector<uint8_t>& img = it->second;
     Module m;
     HIP_CHECK(hipModuleLoadData(&m.module, img.data()));
-    HIP_CHECK(hipModuleGetFunction(&m.entry, m.module, "vx_main"));
+    m.name = entry_name(img);
+    HIP_CHECK(hipModuleGetFunction(&m.entry, m.module, m.name.c_str()));
     HIP_CHECK(hipModuleGetGlobal(&m.dcrs, &m.dcrs_size, m.module, "__vx_dcrs"));
     size_t sz = 0;
     HIP_CHECK(hipModuleGetGlobal(&m.mem_base, &sz, m.module, "__vx_mem_base"));

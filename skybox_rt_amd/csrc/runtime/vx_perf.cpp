@@ -76,7 +76,7 @@ State& St() {
 }
 
 bool IsMain(const std::string& name) {
-  return name == "vx_main" || name.rfind("vx_main.", 0) == 0;
+  return name.rfind("vx_main", 0) == 0;  // vx_main, vx_main_<image> (VX_ENTRY)
 }
 
 void CodeObjectCb(rocprofiler_callback_tracing_record_t rec, rocprofiler_user_data_t*, void*) {
