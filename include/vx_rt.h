@@ -182,9 +182,12 @@ typedef struct {
   uint32_t device;        /* 1: device setup, 0: host loops */
   uint32_t launches;      /* device setup launches */
   uint32_t heavy_tiles;   /* local tiles whose weight (covering geometry primitives) > 0 */
-  uint32_t pad;
+  uint32_t blist_blocks;  /* local 8x8 blocks with candidate lists (0: primary rays walk the tree) */
   double setup_ms;        /* host wall time of the record build (uploads / launches included) */
   double configure_ms;    /* host wall time of the whole rt_renderer_configure */
+  uint64_t blist_entries; /* candidate-list entries (0 when not built) */
+  uint32_t blist_max;     /* the longest list */
+  uint32_t pad;
 } rt_setup_stats_t;
 int rt_renderer_setup_stats(rt_renderer_h r, rt_setup_stats_t* stats);
 
@@ -201,6 +204,8 @@ int rt_renderer_setup_stats(rt_renderer_h r, rt_setup_stats_t* stats);
 #define RT_REC_ORDER 7u     /* u32 per local tile: the work order */
 #define RT_REC_PTRIS 8u     /* rt_tri_t per primitive (clip v0 + pid, e1, e2) */
 #define RT_REC_GEOM 9u      /* rt_tri_t per geometry primitive */
+#define RT_REC_BIDX 10u     /* uint32[2] per local 8x8 block: first list entry, count */
+#define RT_REC_BLIST 11u    /* rt_bentry_t per list entry (+2 padding entries) */
 int rt_renderer_export_records(rt_renderer_h r, uint32_t which, void* out, uint64_t bytes,
                                uint64_t* size);
 

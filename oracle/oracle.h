@@ -95,9 +95,9 @@ typedef struct {
   uint32_t vis_per_lane;            /* BVH mode: 1 = primary rays walk the tree one pixel
                                        at a time (RT_VIS_PACKET=0 images), 0 = per wave packet
                                        (the default images; full frames only) */
-  uint32_t vis_lists;               /* BVH mode, not path: 1 = primary visibility from the
-                                       per-8x8-block candidate lists (rt_app.cpp
-                                       build_block_lists, the kernels' block_primary) */
+  uint32_t vis_lists;               /* BVH mode: 1 = primary visibility from the per-8x8-block
+                                       candidate lists (rt_app.cpp build_block_lists, the
+                                       kernels' block_primary) */
 } orc_rt_params_t;
 
 #define ORC_RT_SHADOWS 0x1u
@@ -149,6 +149,13 @@ int orc_rt_render_bvh(const orc_scene_t* scene, const orc_bvh_t* bvh,
  * and depth-word lower bound -- the product's rt_scene_setup_vis restated
  * by brute force over the binned tiles. */
 int orc_vis_prims(const orc_scene_t* scene, uint32_t width, uint32_t height, uint32_t* out);
+
+/* The per-8x8-block candidate lists of one shard (the product's
+ * rt_bentry_t layout, rt.c vis_build_lists): idx [nlb][2] (first entry,
+ * count), ent [total][4] (geometry index, union corners lo, hi, depth
+ * bound); NULL arrays: sizes only. */
+int orc_vis_block_lists(const orc_scene_t* scene, uint32_t width, uint32_t height, uint32_t shard_index,
+                        uint32_t shard_count, uint32_t* idx, uint32_t* ent, uint64_t* total, uint32_t* nlb);
 
 /* Möller–Trumbore as used by both sides (exposed for unit tests). */
 int orc_mt(const float o[3], const float d[3], const float v0[3],

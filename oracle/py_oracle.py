@@ -97,6 +97,8 @@ def lib():
                                         C.c_void_p, C.c_void_p]
         _lib.orc_mt.argtypes = [C.c_void_p] * 5 + [C.c_float, C.POINTER(C.c_float)]
         _lib.orc_vis_prims.argtypes = [C.POINTER(SceneC), C.c_uint32, C.c_uint32, C.c_void_p]
+        _lib.orc_vis_block_lists.argtypes = [C.POINTER(SceneC)] + [C.c_uint32] * 4 + [
+            C.c_void_p, C.c_void_p, C.POINTER(C.c_uint64), C.POINTER(C.c_uint32)]
         _lib.orc_lbvh_build.argtypes = [C.c_void_p, C.c_void_p, C.c_uint32, C.c_void_p, C.c_void_p,
                                         C.POINTER(C.c_uint32)]
         _lib.orc_lbvh_collapse4.argtypes = [C.c_void_p, C.c_uint32, C.c_void_p,
@@ -177,14 +179,32 @@ def vis_prims(oscene: OracleScene, width: int, height: int) -> np.ndarray:
     return out[:n]
 
 
+def vis_block_lists(oscene: OracleScene, width: int, height: int, shard_index: int = 0,
+                    shard_count: int = 1):
+    """The per-8x8-block candidate lists of one shard (oracle/rt.c
+    orc_vis_block_lists, the product's rt_bentry_t layout) -> (idx
+    uint32[nlb, 2]: first entry, count; ent uint32[total, 4]: geometry index,
+    union corners lo, hi, depth bound)."""
+    tot, nlb = C.c_uint64(), C.c_uint32()
+    rc = lib().orc_vis_block_lists(C.byref(oscene.c), width, height, shard_index, shard_count, None,
+                                   None, C.byref(tot), C.byref(nlb))
+    if rc != 0:
+        raise RuntimeError(f"orc_vis_block_lists failed: {rc}")
+    idx = np.zeros((max(nlb.value, 1), 2), np.uint32)
+    ent = np.zeros((max(tot.value, 1), 4), np.uint32)
+    lib().orc_vis_block_lists(C.byref(oscene.c), width, height, shard_index, shard_count,
+                              idx.ctypes.data, ent.ctypes.data, C.byref(tot), C.byref(nlb))
+    return idx[:nlb.value], ent[:tot.value]
+
+
 def rt_params(width, height, shadows=True, light=(0.0, 60.0, 80.0), nthreads=1,
               clear_color=CLEAR_COLOR, row_begin=0, row_end=0, row_step=0,
               path=False, bounces=4, seed=PT_SEED, vis_per_lane=False, vis_lists=None):
     p = RtParamsC()
     p.vis_per_lane = 1 if vis_per_lane else 0
-    # the product resolves primary visibility of primary+shadow frames from
-    # per-block candidate lists (its default); path tracing walks the tree
-    p.vis_lists = (0 if (path or vis_per_lane) else 1) if vis_lists is None else int(bool(vis_lists))
+    # the product resolves primary visibility from per-block candidate lists
+    # (its default, primary+shadow and path frames)
+    p.vis_lists = (0 if vis_per_lane else 1) if vis_lists is None else int(bool(vis_lists))
     p.width, p.height = width, height
     p.flags = (RT_SHADOWS if shadows else 0) | (RT_PATH if path else 0)
     p.bounces, p.seed = bounces, seed

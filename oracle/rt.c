@@ -888,7 +888,7 @@ static int rt_run(const orc_scene_t* scene, const orc_bvh_t* bvh, const orc_rt_p
   if (bvh && !p->vis_per_lane && p->row_begin == 0 && p->row_end == 0 && p->row_step <= 1) {
     /* primary visibility as the kernels walk it: one packet per wave */
     c.vhit = (int32_t*)malloc(sizeof(int32_t) * (size_t)p->width * p->height);
-    if (p->vis_lists && !(p->flags & ORC_RT_PATH)) vis_build_lists(&c);
+    if (p->vis_lists) vis_build_lists(&c);
     c.next_tile_row = 0;
     if (nt == 1) {
       vis_worker(&c);
@@ -923,4 +923,57 @@ int orc_rt_render_bvh(const orc_scene_t* scene, const orc_bvh_t* bvh,
                       float* t, orc_rt_counters_t* counters) {
   if (!bvh) return -1;
   return rt_run(scene, bvh, p, color, pid, t, counters);
+}
+
+/* The candidate lists of one shard's 8x8 blocks in the product's layout
+ * (rt_common.h rt_bentry_t; the device build rt_setup.hip BCOUNT .. BSORT and
+ * the host restatement rt_app.cpp build_block_lists): local block
+ * lb = (t / shard_count) * 16 + (by & 3) * 4 + (bx & 3) for the tiles
+ * t = (by / 4) * tiles_x + bx / 4 with t % shard_count == shard_index; its
+ * list = the full-frame block's (vis_build_lists).  idx [nlb][2] = (first,
+ * count); ent [total][4] = (geometry index, union lo = x0 | y0 << 16,
+ * hi = x1 | y1 << 16, depth bound); NULL = sizes only. */
+int orc_vis_block_lists(const orc_scene_t* scene, uint32_t width, uint32_t height, uint32_t shard_index,
+                        uint32_t shard_count, uint32_t* idx, uint32_t* ent, uint64_t* total, uint32_t* nlb) {
+  if (!scene || width == 0 || height == 0 || shard_count == 0 || shard_index >= shard_count) return -1;
+  orc_rt_params_t p;
+  memset(&p, 0, sizeof(p));
+  p.width = width;
+  p.height = height;
+  rt_ctx_t c;
+  int err = rt_prepare(&c, scene, &p);
+  if (err) { rt_release(&c); return err; }
+  vis_build_lists(&c);
+  int32_t* kof = (int32_t*)malloc(sizeof(int32_t) * (size_t)(scene->num_prims > 0 ? scene->num_prims : 1));
+  for (int k = 0; k < c.num_geom; ++k) kof[c.geom[k]] = k;
+  const uint32_t tx = (width + 31) / 32, ty = (height + 31) / 32, nt = tx * ty;
+  const uint32_t ltiles = nt > shard_index ? (nt - shard_index + shard_count - 1) / shard_count : 0;
+  const uint32_t nbx = (width + 7) / 8, nby = (height + 7) / 8;
+  uint64_t tot = 0;
+  for (uint32_t lt = 0; lt < ltiles; ++lt) {
+    const uint32_t t = shard_index + lt * shard_count;
+    for (uint32_t blk = 0; blk < 16; ++blk) {
+      const uint32_t bx = (t % tx) * 4 + (blk & 3), by = (t / tx) * 4 + (blk >> 2);
+      uint32_t o = 0, n = 0;
+      if (bx < nbx && by < nby) {
+        o = c.bl_idx[2 * (by * nbx + bx)];
+        n = c.bl_idx[2 * (by * nbx + bx) + 1];
+      }
+      if (idx) { idx[2 * (lt * 16 + blk)] = (uint32_t)tot; idx[2 * (lt * 16 + blk) + 1] = n; }
+      for (uint32_t i = 0; ent && i < n; ++i) {
+        const uint32_t* e = &c.bl_ent[3 * (o + i)];
+        uint32_t* d = ent + 4 * (tot + i);
+        d[0] = (uint32_t)kof[e[0]];
+        d[1] = (e[1] & 0xffffu) | (e[2] << 16);
+        d[2] = (e[1] >> 16) | (e[2] & 0xffff0000u);
+        d[3] = c.vis[e[0]].zmin;
+      }
+      tot += n;
+    }
+  }
+  if (total) *total = tot;
+  if (nlb) *nlb = ltiles * 16;
+  free(kof);
+  rt_release(&c);
+  return 0;
 }

@@ -99,7 +99,8 @@ int device_ingest(rt_renderer* r, bool records) {
   return run(r, &argb, g, &launches);
 }
 
-int device_setup(rt_renderer* r, bool raster, bool order_on, uint32_t* heavy, uint32_t* launches) {
+int device_setup(rt_renderer* r, bool raster, bool order_on, bool lists, uint32_t* heavy,
+                 uint32_t* launches) {
   const rt_scene* s = r->sc;
   rt_kernel_arg_t& a = r->arg;
   *heavy = 0;
@@ -142,8 +143,15 @@ int device_setup(rt_renderer* r, bool raster, bool order_on, uint32_t* heavy, ui
       alloc(r, (uint64_t)nn * sizeof(rt_vnode_t), &r->vnodes, &a.vnodes_addr))
     return -1;
   a.num_vnodes = nn;
-  DevBuf parent, count, weight, hist;
+  DevBuf parent, count, weight, hist, bcnt, bpart, btmp;
   if (alloc_tmp(r, (uint64_t)nn * 4, &parent) || alloc_tmp(r, (uint64_t)nn * 8, &count)) return -1;
+  // per-block candidate lists: one count / cursor word and one (first, count)
+  // pair per local 8x8 block, one partial sum per RTS_BLOCKS_PER_PART blocks
+  const uint32_t nblk = lists ? r->local_tiles * 16u : 0u;
+  const uint32_t nbpart = (nblk + RTS_BLOCKS_PER_PART - 1) / RTS_BLOCKS_PER_PART;
+  if (lists && (alloc_tmp(r, (uint64_t)nblk * 4, &bcnt) || alloc_tmp(r, (uint64_t)nbpart * 4, &bpart) ||
+                alloc(r, (uint64_t)nblk * 8, &r->bidx, &a.bidx_addr)))
+    return -1;
   const uint64_t wwords = (uint64_t)(a.tiles_x + 1) * (a.tiles_y + 1);
   const uint32_t nblocks = (r->local_tiles + RTS_ITEMS - 1) / RTS_ITEMS;
   if (order_on && (alloc_tmp(r, wwords * 4, &weight) || alloc_tmp(r, 256ull * nblocks * 4, &hist) ||
@@ -170,21 +178,51 @@ int device_setup(rt_renderer* r, bool raster, bool order_on, uint32_t* heavy, ui
   g.shard_count = a.shard_count;
   g.local_tiles = r->local_tiles;
   g.nblocks = nblocks;
+  g.nblk = nblk;
+  g.nbpart = nbpart;
+  g.bcnt_addr = bcnt.addr;
+  g.bpart_addr = bpart.addr;
+  g.bidx_addr = a.bidx_addr;
   add_fill(&g, parent.addr, nn, 0xffffffffu);
   if (order_on) add_fill(&g, weight.addr, wwords, 0u);
+  if (lists) add_fill(&g, bcnt.addr, nblk, 0u);
   const uint32_t ord = order_on ? 1u : 0u;
+  uint32_t bl = lists ? 1u : 0u;
   const uint32_t steps[] = {
-      RTS_FILL | RTS_PRIMVIS,                 // records, clears
-      RTS_VTRIS | (ord ? RTS_WEIGHT : 0u),    // vtri records; tile-rectangle corners
-      RTS_LINK | (ord ? RTS_ROWSUM : 0u),     // tree parents; weight rows
-      RTS_CLIMB | (ord ? RTS_COLSUM : 0u),    // vnodes bottom-up; weight columns
-      ord ? RTS_HIST : 0u, ord ? RTS_SCAN : 0u, ord ? RTS_SCATTER : 0u};
+      RTS_FILL | RTS_PRIMVIS,                                     // records, clears
+      RTS_VTRIS | (ord ? RTS_WEIGHT : 0u) | (bl ? RTS_BCOUNT : 0u),  // vtris; tile weights; block counts
+      RTS_LINK | (ord ? RTS_ROWSUM : 0u) | (bl ? RTS_BSUM : 0u),     // tree parents; rows; block sums
+      RTS_CLIMB | (ord ? RTS_COLSUM : 0u) | (bl ? RTS_BSCAN : 0u),   // vnodes; columns; sums scanned
+      (ord ? RTS_HIST : 0u) | (bl ? RTS_BOFF : 0u),                // tile histograms; list offsets
+      0u,                                                          // (list sizes read back here)
+      (ord ? RTS_SCAN : 0u) | (bl ? RTS_BFILL : 0u),               // digit scan; list entries
+      (ord ? RTS_SCATTER : 0u) | (bl ? RTS_BSORT : 0u)};           // tile order; lists sorted
+  uint32_t st[4] = {0, 0, 0, 0};
   for (uint32_t ph : steps) {
+    if (ph == 0u && bl) {
+      // the list sizes: the longest list and the entries in total decide
+      // whether the lists are built (else the kernels walk the tree)
+      if (vx_copy_from_dev(st, status.h, 0, sizeof(st)) != 0) return set_error("vx_copy_from_dev failed");
+      r->setup.blist_max = st[1];
+      r->setup.blist_entries = st[2];
+      if (!rtapp::block_lists_fit(st[1], st[2])) {
+        bl = 0u;
+        continue;
+      }
+      const uint64_t total = st[2];
+      if (alloc_tmp(r, total * 16 + 16, &btmp) || alloc(r, (total + 2) * 16, &r->blist, &a.blist_addr))
+        return -1;
+      g.btmp_addr = btmp.addr;
+      g.blist_addr = a.blist_addr;
+      g.blist_entries = st[2];
+      continue;
+    }
+    if (!bl) ph &= ~(RTS_BFILL | RTS_BSORT);
     if (!ph) continue;
     g.phases = ph;
     if (run(r, &argb, g, launches) != 0) return -1;
   }
-  uint32_t st[4] = {0, 0, 0, 0};
+  a.blist_blocks = bl ? nblk : 0u;
   if (vx_copy_from_dev(st, status.h, 0, sizeof(st)) != 0) return set_error("vx_copy_from_dev failed");
   if (st[0] & RTS_ERR_REF) return set_error("malformed BVH (reference out of range)");
   if (st[0] & RTS_ERR_PID) return set_error("malformed BVH (leaf pid out of range)");

@@ -185,6 +185,12 @@ int rt_scene_export_bvh4(rt_scene_h s, float* nodes4) {
 
 }  // extern "C"
 
+bool rtapp::block_lists_fit(uint64_t longest, uint64_t entries) {
+  uint64_t cap = 16ull << 20;
+  if (const char* e = std::getenv("RT_BLIST_MAX_ENTRIES")) cap = std::strtoull(e, nullptr, 0);
+  return longest <= RT_BLIST_MAX_LIST && entries <= cap;
+}
+
 int rtapp::upload(vx_device_h dev, const void* data, uint64_t size, vx_buffer_h* buf,
                   uint64_t* addr) {
   const uint64_t sz = size ? size : 64;
@@ -363,6 +369,11 @@ int rt_renderer_export_records(rt_renderer_h r, uint32_t which, void* out, uint6
     case RT_REC_ORDER: b = a.order_addr ? r->order : nullptr; n = (uint64_t)r->local_tiles * 4; break;
     case RT_REC_PTRIS: b = r->ptris; n = np * sizeof(rt_tri_t); break;
     case RT_REC_GEOM: b = r->geom; n = (uint64_t)r->sc->geometry.size() * sizeof(rt_tri_t); break;
+    case RT_REC_BIDX: b = a.blist_blocks ? r->bidx : nullptr; n = (uint64_t)a.blist_blocks * 8; break;
+    case RT_REC_BLIST:
+      b = a.blist_blocks ? r->blist : nullptr;
+      n = (r->setup.blist_entries + 2) * sizeof(rt_bentry_t);
+      break;
     default: return fail("unknown record array");
   }
   if (!b) return fail("record array not present in this configuration");
@@ -574,54 +585,59 @@ static int configure_vis(rt_renderer* r, const std::vector<rt_prim_t>& prims,
   return 0;
 }
 
-// Per-8x8-block candidate lists for primary visibility (the rt images'
-// block_primary; oracle/rt.c vis_build_lists restates them): per block of
-// the frame, the geometry records whose covered rectangle reaches it, in
-// ascending (depth bound, geometry index), and per record the union
-// rectangle (corners) of it and the records after it, so a wave stops its
-// scan once no lane can change its winner.  Built from the geometry records
-// (the host's, or the device setup's read back), for primary+shadow frames;
-// env RT_BLOCK_LISTS=0 keeps the tree walk.
-static int build_block_lists(rt_renderer* r, const std::vector<rt_vtri_t>& vg) {
+
+// Per-8x8-block candidate lists (rt_common.h rt_bentry_t), the host
+// restatement of the device build (rt_setup.hip BCOUNT .. BSORT; oracle/rt.c
+// vis_build_lists): for every local block of the shard, the geometry
+// primitives whose covered rectangle reaches it, ascending (depth bound,
+// geometry index), each with the union rectangle of itself and the rest.
+static int build_block_lists(rt_renderer* r, const std::vector<rt::VisPrim>& vis) {
+  const rt_scene* s = r->sc;
   rt_kernel_arg_t& a = r->arg;
-  const uint32_t nbx = (a.width + 7) / 8, nby = (a.height + 7) / 8;
-  std::vector<std::vector<std::pair<uint32_t, uint32_t>>> lists((size_t)nbx * nby);
-  for (uint32_t k = 0; k < (uint32_t)vg.size(); ++k) {
-    const rt_vtri_t& t = vg[k];
-    const uint32_t x0 = t.rx & 0xffffu, x1 = t.rx >> 16, y0 = t.ry & 0xffffu, y1 = t.ry >> 16;
-    if (x0 > x1 || y0 > y1) continue;  // covers no pixel
-    for (uint32_t by = y0 >> 3; by <= (y1 >> 3) && by < nby; ++by)
-      for (uint32_t bx = x0 >> 3; bx <= (x1 >> 3) && bx < nbx; ++bx)
-        lists[(size_t)by * nbx + bx].push_back({t.zmin, k});
+  const uint32_t nblk = r->local_tiles * 16u, sc = a.shard_count, si = a.shard_index;
+  std::vector<std::vector<std::pair<uint32_t, uint32_t>>> lists(nblk);  // (zmin, k)
+  for (uint32_t k = 0; k < (uint32_t)s->geometry.size(); ++k) {
+    const rt::VisPrim& v = vis[s->geometry[k]];
+    if (!v.any) continue;
+    for (uint32_t by = (v.ry & 0xffffu) >> 3; by <= (v.ry >> 16) >> 3; ++by)
+      for (uint32_t bx = (v.rx & 0xffffu) >> 3; bx <= (v.rx >> 16) >> 3; ++bx) {
+        const uint32_t t = (by >> 2) * a.tiles_x + (bx >> 2);
+        if (t % sc != si) continue;
+        lists[((t / sc) << 4) | ((by & 3u) << 2) | (bx & 3u)].push_back({v.zmin, k});
+      }
   }
-  std::vector<rt_vtri_t> recs;
-  std::vector<uint32_t> idx, suf;
-  idx.reserve(lists.size() * 2);
+  uint64_t total = 0, longest = 0;
+  for (const auto& l : lists) {
+    total += l.size();
+    longest = std::max<uint64_t>(longest, l.size());
+  }
+  r->setup.blist_max = (uint32_t)longest;
+  r->setup.blist_entries = total;
+  a.blist_blocks = 0;
+  if (!rtapp::block_lists_fit(longest, total)) return 0;
+  std::vector<rt_bentry_t> ent;
+  std::vector<uint32_t> idx;
+  ent.reserve(total + 2);
+  idx.reserve(2 * (size_t)nblk);
   for (auto& l : lists) {
     std::sort(l.begin(), l.end());
-    idx.push_back((uint32_t)recs.size());
+    idx.push_back((uint32_t)ent.size());
     idx.push_back((uint32_t)l.size());
-    const size_t base = recs.size();
-    for (auto& e : l) recs.push_back(vg[e.second]);
-    std::vector<uint32_t> lo(l.size()), hi(l.size());
-    uint32_t ux0 = 0xffffu, uy0 = 0xffffu, ux1 = 0, uy1 = 0;
+    const size_t base = ent.size();
+    ent.resize(base + l.size());
+    uint32_t x0 = 0xffffu, y0 = 0xffffu, x1 = 0, y1 = 0;
     for (size_t i = l.size(); i-- > 0;) {
-      const rt_vtri_t& t = recs[base + i];
-      ux0 = std::min(ux0, t.rx & 0xffffu); ux1 = std::max(ux1, t.rx >> 16);
-      uy0 = std::min(uy0, t.ry & 0xffffu); uy1 = std::max(uy1, t.ry >> 16);
-      lo[i] = ux0 | (uy0 << 16);
-      hi[i] = ux1 | (uy1 << 16);
+      const rt::VisPrim& v = vis[s->geometry[l[i].second]];
+      x0 = std::min(x0, v.rx & 0xffffu); x1 = std::max(x1, v.rx >> 16);
+      y0 = std::min(y0, v.ry & 0xffffu); y1 = std::max(y1, v.ry >> 16);
+      ent[base + i] = rt_bentry_t{l[i].second, x0 | (y0 << 16), x1 | (y1 << 16), l[i].first};
     }
-    for (size_t i = 0; i < l.size(); ++i) { suf.push_back(lo[i]); suf.push_back(hi[i]); }
   }
-  recs.push_back(rt::MakeVisTri(rt_prim_t{}, rt::VisPrim{}, -1));  // padding: pairs are loaded
-  suf.push_back(0xffffffffu);
-  suf.push_back(0xfffefffeu);
-  if (upload(r->dev, recs.data(), recs.size() * sizeof(rt_vtri_t), &r->blist, &a.blist_addr) ||
-      upload(r->dev, idx.data(), idx.size() * 4, &r->bidx, &a.bidx_addr) ||
-      upload(r->dev, suf.data(), suf.size() * 4, &r->bsuf, &a.bsuf_addr))
+  for (int i = 0; i < 2; ++i) ent.push_back(rt_bentry_t{0u, RT_BLIST_PAD_LO, RT_BLIST_PAD_HI, RT_VIS_ZMIN_NONE});
+  if (upload(r->dev, ent.data(), ent.size() * sizeof(rt_bentry_t), &r->blist, &a.blist_addr) ||
+      upload(r->dev, idx.data(), idx.size() * 4, &r->bidx, &a.bidx_addr))
     return -1;
-  a.blist_nbx = nbx;
+  a.blist_blocks = nblk;
   return 0;
 }
 
@@ -630,7 +646,7 @@ static int build_block_lists(rt_renderer* r, const std::vector<rt_vtri_t>& vg) {
 // kernels/rt_setup.hip; the default) or from the host loops below
 // (RT_RENDER_HOST_SETUP / env RT_SETUP=host, and the RT_VIS_TREE=screen
 // variant, which needs the visibility records on the host).
-static int host_setup(rt_renderer* r, const rt_render_params_t* p, bool raster, bool order_on,
+static int host_setup(rt_renderer* r, const rt_render_params_t* p, bool raster, bool order_on, bool lists,
                       uint32_t* heavy) {
   const rt_scene* s = r->sc;
   rt_kernel_arg_t& a = r->arg;
@@ -701,6 +717,7 @@ static int host_setup(rt_renderer* r, const rt_render_params_t* p, bool raster, 
     while (*heavy < r->local_tiles && w(ord[*heavy]) > 0) ++*heavy;
   }
   if (!raster && configure_vis(r, prims, vis, r->use_bvh4) != 0) return -1;
+  if (lists && build_block_lists(r, vis) != 0) return -1;
   // output buffer, pre-filled with the clear colour (draw3d/main.cpp:485-490)
   std::vector<uint32_t> clear(r->cbuf_bytes / 4 ? r->cbuf_bytes / 4 : 1, p->clear_color);
   if (upload(r->dev, clear.data(), r->cbuf_bytes, &r->cbuf, &a.cbuf_addr)) return -1;
@@ -786,24 +803,22 @@ int rt_renderer_configure(rt_renderer_h r, const rt_render_params_t* p) {
   const bool device = !(p->flags & RT_RENDER_HOST_SETUP) && !(sv && std::string(sv) == "host") &&
                       !(!raster && vt && std::string(vt) == "screen");
   uint32_t heavy = 0, launches = 0;
+  // primary visibility of primary+shadow and path frames from per-block
+  // candidate lists (rt_bentry_t; env RT_BLOCK_LISTS=0 keeps the tree walk)
+  const char* bl = std::getenv("RT_BLOCK_LISTS");
+  const bool lists = !raster && !(p->flags & RT_RENDER_FLAT) && !(bl && std::atoi(bl) == 0) &&
+                     a.num_geom > 0 && r->local_tiles > 0;
+  a.blist_blocks = 0;
+  a.blist_addr = a.bidx_addr = 0;
+  r->setup.blist_entries = 0;
+  r->setup.blist_max = 0;
   const auto t1 = std::chrono::steady_clock::now();
   if (device) {
     r->vis_refs.clear();
     r->vis_pids.clear();
-    if (rtapp::device_setup(r, raster, order_on, &heavy, &launches) != 0) return -1;
-  } else if (host_setup(r, p, raster, order_on, &heavy) != 0) {
+    if (rtapp::device_setup(r, raster, order_on, lists, &heavy, &launches) != 0) return -1;
+  } else if (host_setup(r, p, raster, order_on, lists, &heavy) != 0) {
     return -1;
-  }
-  // primary+shadow frames: per-block candidate lists (build_block_lists)
-  a.blist_nbx = 0;
-  a.blist_addr = a.bidx_addr = a.bsuf_addr = 0;
-  const char* bl = std::getenv("RT_BLOCK_LISTS");
-  if (!raster && !(p->flags & (RT_RENDER_PATH | RT_RENDER_FLAT)) && !(bl && std::atoi(bl) == 0) &&
-      a.num_geom > 0) {
-    std::vector<rt_vtri_t> vg(a.num_geom);
-    if (vx_copy_from_dev(vg.data(), r->vgeom, 0, vg.size() * sizeof(rt_vtri_t)) != 0)
-      return fail("vx_copy_from_dev failed");
-    if (build_block_lists(r, vg) != 0) return -1;
   }
   const double setup_ms = ms_since(t1);
   if (order_on) {
@@ -833,6 +848,7 @@ int rt_renderer_configure(rt_renderer_h r, const rt_render_params_t* p) {
   r->setup.device = device ? 1u : 0u;
   r->setup.launches = launches;
   r->setup.heavy_tiles = heavy;
+  r->setup.blist_blocks = a.blist_blocks;
   r->setup.setup_ms = setup_ms;
   r->setup.configure_ms = ms_since(t0);
   r->configured = true;

@@ -35,7 +35,7 @@ struct rt_renderer {
   vx_buffer_h ptris = nullptr, geom = nullptr, oms = nullptr, bbox = nullptr, zbuf = nullptr;
   vx_buffer_h order = nullptr;
   vx_buffer_h vnodes = nullptr, vtris = nullptr, vlayers = nullptr, vgeom = nullptr;
-  vx_buffer_h blist = nullptr, bidx = nullptr, bsuf = nullptr;  // RT_BLOCK_LISTS experiment
+  vx_buffer_h blist = nullptr, bidx = nullptr;  // per-block candidate lists (rt_bentry_t)
   vx_buffer_h gather_recv = nullptr, gather_image = nullptr;  // rank 0 of rt_render_gather
   vx_buffer_h prims = nullptr, cbuf = nullptr, args = nullptr;
   // device-side setup (device_setup.cpp, kernels/rt_setup.hip): the image,
@@ -72,7 +72,7 @@ struct rt_renderer {
                            &ptris, &geom, &oms, &bbox, &zbuf, &order, &vnodes, &vtris, &vlayers,
                            &vgeom, &gather_recv, &gather_image, &prims, &cbuf, &args,
                            &setup_krnl, &verts, &pdc, &dcz, &layer_list, &geometry_list, &vis,
-                           &blist, &bidx, &bsuf};
+                           &blist, &bidx};
     for (auto* b : bufs) {
       if (*b) vx_mem_free(*b);
       *b = nullptr;
@@ -105,6 +105,13 @@ int device_ingest(rt_renderer* r, bool records);
 // the tile order (heavy = local tiles with weight > 0), the cleared cbuf.
 // r->arg holds the layout fields (tiles, shard, flags, the tree); the
 // record buffers are (re)allocated here and their addresses set in r->arg.
-int device_setup(rt_renderer* r, bool raster, bool order_on, uint32_t* heavy, uint32_t* launches);
+// lists: also the per-block candidate lists (rt_bentry_t, the bidx / blist
+// buffers and arg.blist_blocks; 0 when they do not fit, block_lists_fit)
+int device_setup(rt_renderer* r, bool raster, bool order_on, bool lists, uint32_t* heavy,
+                 uint32_t* launches);
+// whether lists with this longest list and this many entries are built
+// (RT_BLIST_MAX_LIST, the device sort's limit; env RT_BLIST_MAX_ENTRIES,
+// default 16 M entries = 512 MiB of list and sort buffers)
+bool block_lists_fit(uint64_t longest, uint64_t entries);
 
 }  // namespace rtapp

@@ -169,13 +169,13 @@ __device__ __forceinline__ void enqueue(PtLds& L, int qi, bool want, uint32_t ta
 __device__ __forceinline__ void primary(const vx_task_t& task, bool valid, const Scene& S,
                                         PtLds& L, Counters& cnt) {
   const uint32_t t = task.blockIdx.x;
-  uint32_t x = 0, y = 0;
-  if (valid) task_pixel(S, t, &x, &y);
+  uint32_t x = 0, y = 0, lb = 0;
+  if (valid) task_pixel(S, t, &x, &y, &lb);
   const bool in = valid && x < S.width && y < S.height;
   cnt.primary += in;
   const bool tie_high = (S.flags & RT_FLAG_TIE_HIGH) != 0;
   // primary visibility: the raster's winner at this pixel (trace_primary)
-  const int32_t hit = trace_primary(S, x, y, in, tie_high, cnt);
+  const int32_t hit = trace_primary(S, lb, x, y, in, tie_high, cnt);
   cnt.hits += hit >= 0;
   const int32_t spid = resolve_layers(S, x, y, in && hit < 0, hit, cnt);
   const uint32_t color = shade_wave(S, spid, x, y, S.clear_color, cnt);
@@ -457,8 +457,8 @@ __device__ __forceinline__ void bounces(const Scene& S, PtLds& L, Counters& cnt)
 __device__ __forceinline__ void lane_path(const vx_task_t& task, const Scene& S, int32_t* stack,
                                           Counters& cnt) {
   const uint32_t t = task.blockIdx.x;
-  uint32_t x, y;
-  task_pixel(S, t, &x, &y);
+  uint32_t x, y, lb;
+  task_pixel(S, t, &x, &y, &lb);
   const bool in = x < S.width && y < S.height;
   // paired vertices (path_step_pair) when the whole wave is here and its
   // upper 32 lanes hold no pixel -- wave-uniform
@@ -466,7 +466,7 @@ __device__ __forceinline__ void lane_path(const vx_task_t& task, const Scene& S,
   cnt.primary += in;
   const bool tie_high = (S.flags & RT_FLAG_TIE_HIGH) != 0;
   // primary visibility: the raster's winner at this pixel (trace_primary)
-  const int32_t hit = trace_primary(S, x, y, in, tie_high, cnt);
+  const int32_t hit = trace_primary(S, lb, x, y, in, tie_high, cnt);
   cnt.hits += hit >= 0;
   const int32_t spid = resolve_layers(S, x, y, in && hit < 0, hit, cnt);
   const uint32_t color = shade_wave(S, spid, x, y, S.clear_color, cnt);

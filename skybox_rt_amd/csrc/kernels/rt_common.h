@@ -192,8 +192,26 @@ typedef struct {
   uint64_t vtris_addr;     // rt_vtri_t per leaf triangle record (+3 padding records)
   uint64_t vgeom_addr;     // rt_vtri_t per geometry primitive, ascending pid (flat mode)
   uint32_t split_log;      // split tiles run 2^split_log pixels per wave (5: 32, an 8x4 half block)
-  uint32_t blist_nbx;      // experiment (RT_BLOCK_LIST images): 8x8 blocks per row, 0 = no lists
-  uint64_t blist_addr;     // per 8x8 block: its candidate rt_vtri_t records, ascending depth bound
-  uint64_t bidx_addr;      // per block: (first record, count)
-  uint64_t bsuf_addr;      // per list record: union rectangle (lo, hi corners) of it and the rest
+  uint32_t blist_blocks;   // per-block candidate lists: local 8x8 blocks (local_tiles * 16), 0 = walk the tree
+  uint64_t blist_addr;     // rt_bentry_t [entries + 2]: every local block's list, concatenated
+  uint64_t bidx_addr;      // uint32[2] per local block lt * 16 + (by & 3) * 4 + (bx & 3): first entry, count
 } rt_kernel_arg_t;
+
+// ---- per-8x8-block candidate lists (primary visibility) -------------------
+// For every 8x8 pixel block of the shard's tiles (local block lb = local
+// tile * 16 + block of the tile), the geometry primitives whose covered-pixel
+// rectangle reaches the block, ascending (depth lower bound, geometry index):
+// the finer-grained form of draw3d's per-tile primitive lists
+// (gfxutil.cpp:237-271).  Each entry carries the union rectangle (corners) of
+// itself and the entries after it, so a wave stops scanning once no lane can
+// change its winner.  Built on the device (rt_setup.hip, BCOUNT .. BSORT) or by
+// the host restatement (rt_app.cpp BuildBlockLists); oracle/rt.c
+// vis_build_lists restates them.
+typedef struct {
+  uint32_t k;              // geometry index (rt_vtri_t vgeom[k])
+  uint32_t lo, hi;         // union rectangle of this entry and the rest: corners x | y << 16
+  uint32_t zmin;           // this entry's depth lower bound (the smallest of the rest)
+} rt_bentry_t;
+#define RT_BLIST_PAD_LO 0xffffffffu   // padding entries: a rectangle no pixel is in
+#define RT_BLIST_PAD_HI 0xfffefffeu
+#define RT_BLIST_MAX_LIST 1024u       // longest list the device sort takes (else: tree walk)

@@ -79,8 +79,8 @@ __device__ __forceinline__ const uint4* flat_list(const Scene& S) {
 __device__ __forceinline__ void kernel_body(const vx_task_t& task, const Scene& S, WaveLds& w,
                                             Counters& cnt) {
   const uint32_t t = task.blockIdx.x;
-  uint32_t x, y;
-  task_pixel(S, t, &x, &y);
+  uint32_t x, y, lb;
+  task_pixel(S, t, &x, &y, &lb);
   const bool in = x < S.width && y < S.height;  // edge tiles overhang the image
   cnt.primary += in;
   const bool tie_high = (S.flags & RT_FLAG_TIE_HIGH) != 0;
@@ -88,7 +88,7 @@ __device__ __forceinline__ void kernel_body(const vx_task_t& task, const Scene& 
   if (lane_id() == 0) __vx_mpm_lds[3] = (uint32_t)__builtin_amdgcn_s_memrealtime();
 #endif
   // primary visibility: the raster's winner at this pixel
-  const int32_t hit = trace_primary(S, x, y, in, tie_high, cnt);
+  const int32_t hit = trace_primary(S, lb, x, y, in, tie_high, cnt);
 #ifdef RT_STAMPS
   if (lane_id() == 0) __vx_mpm_lds[14] = (uint32_t)__builtin_amdgcn_s_memrealtime();
 #endif

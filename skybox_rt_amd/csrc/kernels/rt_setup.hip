@@ -522,29 +522,10 @@ __device__ void phase_hist(const rt_setup_arg_t* a) {
 }
 
 // exclusive scan of hist[256][nblocks] (digit-major) by workgroup 0
+__device__ void scan_excl(uint32_t* v, uint32_t n, uint32_t* total);
 __device__ void phase_scan(const rt_setup_arg_t* a) {
   if (blockIdx.x != 0) return;
-  uint32_t* hist = vx_ptr<uint32_t>(a->hist_addr);
-  __shared__ uint32_t s[RTS_BLOCK];
-  const uint32_t total = 256u * a->nblocks;
-  const uint32_t chunk = (total + RTS_BLOCK - 1) / RTS_BLOCK;
-  const uint32_t b0 = min(threadIdx.x * chunk, total), b1 = min(b0 + chunk, total);
-  uint32_t sum = 0;
-  for (uint32_t i = b0; i < b1; ++i) sum += hist[i];
-  s[threadIdx.x] = sum;
-  __syncthreads();
-  for (uint32_t o = 1; o < RTS_BLOCK; o <<= 1) {
-    const uint32_t y = threadIdx.x >= o ? s[threadIdx.x - o] : 0u;
-    __syncthreads();
-    s[threadIdx.x] += y;
-    __syncthreads();
-  }
-  uint32_t run = s[threadIdx.x] - sum;
-  for (uint32_t i = b0; i < b1; ++i) {
-    const uint32_t x = hist[i];
-    hist[i] = run;
-    run += x;
-  }
+  scan_excl(vx_ptr<uint32_t>(a->hist_addr), 256u * a->nblocks, nullptr);
 }
 
 // stable scatter of the local tile indices (rank = digit offset of the block
@@ -588,6 +569,209 @@ __device__ void phase_scatter(const rt_setup_arg_t* a) {
       base[threadIdx.x] += sum;
       if (valid) order[dst] = lt;
       __syncthreads();
+    }
+  }
+}
+
+// ---- per-block candidate lists (rt_common.h rt_bentry_t; the host
+// restatement is app/rt_app.cpp BuildBlockLists, the oracle's
+// oracle/rt.c vis_build_lists).  The reference bins each primitive's screen
+// box into 32x32 tiles on the host per drawcall (gfxutil.cpp:237-271); here
+// the covered-pixel rectangles are binned into the shard's 8x8 blocks on the
+// device: count, scan, fill, per-block sort.
+
+// wave-uniform load through the scalar cache (the data was written by an
+// earlier launch)
+template <typename T>
+__device__ __forceinline__ T sload(const T* p) {
+  const uint64_t u = (uint64_t)p;
+  const uint32_t lo = (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)u);
+  const uint32_t hi = (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(u >> 32));
+  return *(const __attribute__((address_space(4))) T*)(((uint64_t)hi << 32) | lo);
+}
+
+// the lanes of a wave split the 8x8 blocks of covered rectangle v (vis
+// record: rx, ry) that lie in the shard's tiles; f(local block) for each
+// (tile t = (by >> 2) * tiles_x + (bx >> 2) belongs to shard t % shard_count,
+// local tile t / shard_count)
+template <typename F>
+__device__ __forceinline__ void for_blocks(const rt_setup_arg_t* a, uint4 v, F f) {
+  const uint32_t bx0 = (v.x & 0xffffu) >> 3, bx1 = (v.x >> 16) >> 3;
+  const uint32_t by0 = (v.y & 0xffffu) >> 3, by1 = (v.y >> 16) >> 3;
+  const uint32_t w = bx1 - bx0 + 1, n = w * (by1 - by0 + 1);
+  const uint32_t sc = a->shard_count, si = a->shard_index, tx = a->tiles_x;
+  for (uint32_t i = lane_id(); i < n; i += 64) {
+    const uint32_t bx = bx0 + i % w, by = by0 + i / w;
+    const uint32_t t = (by >> 2) * tx + (bx >> 2);
+    if (t % sc != si) continue;
+    f(((t / sc) << 4) | ((by & 3u) << 2) | (bx & 3u));
+  }
+}
+
+// a wave per geometry primitive: +1 in every block its rectangle reaches
+__device__ void phase_bcount(const rt_setup_arg_t* a) {
+  const int32_t* geometry = vx_ptr<const int32_t>(a->geometry_addr);
+  const uint4* vis = vx_ptr<const uint4>(a->vis_addr);
+  uint32_t* bcnt = vx_ptr<uint32_t>(a->bcnt_addr);
+  const uint32_t waves = gridDim.x * (RTS_BLOCK / 64);
+  for (uint32_t j = blockIdx.x * (RTS_BLOCK / 64) + (threadIdx.x >> 6); j < a->num_geom; j += waves) {
+    const uint4 v = vis[geometry[j]];
+    if (!v.w) continue;
+    for_blocks(a, v, [&](uint32_t lb) { atomicAdd(&bcnt[lb], 1u); });
+  }
+}
+
+// workgroup reduction (sum and max) of one value per thread
+__device__ __forceinline__ void block_sum_max(uint32_t x, uint32_t* sum, uint32_t* mx) {
+  __shared__ uint32_t ss[RTS_BLOCK / 64], sm[RTS_BLOCK / 64];
+  uint32_t s = x, m = x;
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    s += (uint32_t)__shfl_xor((int)s, o, 64);
+    m = max(m, (uint32_t)__shfl_xor((int)m, o, 64));
+  }
+  if (lane_id() == 0) { ss[threadIdx.x >> 6] = s; sm[threadIdx.x >> 6] = m; }
+  __syncthreads();
+  s = 0; m = 0;
+  for (int w = 0; w < RTS_BLOCK / 64; ++w) { s += ss[w]; m = max(m, sm[w]); }
+  *sum = s;
+  *mx = m;
+  __syncthreads();
+}
+
+// per RTS_BLOCKS_PER_PART blocks: their entry sum -> bpart, the longest list -> status[1]
+__device__ void phase_bsum(const rt_setup_arg_t* a) {
+  const uint32_t* bcnt = vx_ptr<const uint32_t>(a->bcnt_addr);
+  uint32_t* bpart = vx_ptr<uint32_t>(a->bpart_addr);
+  uint32_t* status = vx_ptr<uint32_t>(a->status_addr);
+  constexpr uint32_t Q = RTS_BLOCKS_PER_PART / RTS_BLOCK;
+  for (uint32_t b = blockIdx.x; b < a->nbpart; b += gridDim.x) {
+    uint32_t sum = 0, mx = 0;
+    for (uint32_t q = 0; q < Q; ++q) {
+      const uint32_t lb = b * RTS_BLOCKS_PER_PART + threadIdx.x * Q + q;
+      const uint32_t c = lb < a->nblk ? bcnt[lb] : 0u;
+      sum += c;
+      mx = max(mx, c);
+    }
+    uint32_t ts, tm;
+    block_sum_max(sum, &ts, &tm);
+    if (threadIdx.x == 0) {
+      bpart[b] = ts;
+      atomicMax(&status[1], tm);
+    }
+  }
+}
+
+// exclusive scan of v[0, n) in place by one workgroup; the total -> *total
+__device__ void scan_excl(uint32_t* v, uint32_t n, uint32_t* total) {
+  __shared__ uint32_t s[RTS_BLOCK];
+  const uint32_t chunk = (n + RTS_BLOCK - 1) / RTS_BLOCK;
+  const uint32_t b0 = min(threadIdx.x * chunk, n), b1 = min(b0 + chunk, n);
+  uint32_t sum = 0;
+  for (uint32_t i = b0; i < b1; ++i) sum += v[i];
+  s[threadIdx.x] = sum;
+  __syncthreads();
+  for (uint32_t o = 1; o < RTS_BLOCK; o <<= 1) {
+    const uint32_t y = threadIdx.x >= o ? s[threadIdx.x - o] : 0u;
+    __syncthreads();
+    s[threadIdx.x] += y;
+    __syncthreads();
+  }
+  uint32_t run = s[threadIdx.x] - sum;
+  for (uint32_t i = b0; i < b1; ++i) {
+    const uint32_t x = v[i];
+    v[i] = run;
+    run += x;
+  }
+  if (total && threadIdx.x == RTS_BLOCK - 1) *total = s[RTS_BLOCK - 1];
+}
+
+__device__ void phase_bscan(const rt_setup_arg_t* a) {
+  if (blockIdx.x != 0) return;
+  scan_excl(vx_ptr<uint32_t>(a->bpart_addr), a->nbpart, vx_ptr<uint32_t>(a->status_addr) + 2);
+}
+
+// per local block: (first entry, count) -> bidx; the count word zeroed (it
+// becomes the block's fill cursor)
+__device__ void phase_boff(const rt_setup_arg_t* a) {
+  uint32_t* bcnt = vx_ptr<uint32_t>(a->bcnt_addr);
+  const uint32_t* bpart = vx_ptr<const uint32_t>(a->bpart_addr);
+  uint2* bidx = vx_ptr<uint2>(a->bidx_addr);
+  __shared__ uint32_t s[RTS_BLOCK];
+  constexpr uint32_t Q = RTS_BLOCKS_PER_PART / RTS_BLOCK;
+  for (uint32_t b = blockIdx.x; b < a->nbpart; b += gridDim.x) {
+    const uint32_t lb0 = b * RTS_BLOCKS_PER_PART + threadIdx.x * Q;
+    uint32_t c[Q], sum = 0;
+    for (uint32_t q = 0; q < Q; ++q) {
+      c[q] = lb0 + q < a->nblk ? bcnt[lb0 + q] : 0u;
+      sum += c[q];
+    }
+    s[threadIdx.x] = sum;
+    __syncthreads();
+    for (uint32_t o = 1; o < RTS_BLOCK; o <<= 1) {
+      const uint32_t y = threadIdx.x >= o ? s[threadIdx.x - o] : 0u;
+      __syncthreads();
+      s[threadIdx.x] += y;
+      __syncthreads();
+    }
+    uint32_t run = bpart[b] + s[threadIdx.x] - sum;
+    for (uint32_t q = 0; q < Q; ++q) {
+      if (lb0 + q < a->nblk) {
+        bidx[lb0 + q] = make_uint2(run, c[q]);
+        bcnt[lb0 + q] = 0u;
+      }
+      run += c[q];
+    }
+    __syncthreads();
+  }
+}
+
+// a wave per geometry primitive: its (depth bound, index, rectangle) in every
+// block it reaches, at the block's next free slot (order fixed by BSORT)
+__device__ void phase_bfill(const rt_setup_arg_t* a) {
+  const int32_t* geometry = vx_ptr<const int32_t>(a->geometry_addr);
+  const uint4* vis = vx_ptr<const uint4>(a->vis_addr);
+  uint32_t* bcnt = vx_ptr<uint32_t>(a->bcnt_addr);
+  const uint2* bidx = vx_ptr<const uint2>(a->bidx_addr);
+  uint4* btmp = vx_ptr<uint4>(a->btmp_addr);
+  const uint32_t waves = gridDim.x * (RTS_BLOCK / 64);
+  for (uint32_t j = blockIdx.x * (RTS_BLOCK / 64) + (threadIdx.x >> 6); j < a->num_geom; j += waves) {
+    const uint4 v = vis[geometry[j]];
+    if (!v.w) continue;
+    for_blocks(a, v, [&](uint32_t lb) {
+      const uint32_t slot = atomicAdd(&bcnt[lb], 1u);
+      btmp[bidx[lb].x + slot] = make_uint4(v.z, j, v.x, v.y);
+    });
+  }
+}
+
+// a wave per local block: every entry's rank in (depth bound, index) order
+// (the keys are distinct: one entry per primitive) and the union rectangle
+// of the entries at or after it, by one pass over the list per 64 entries
+// (wave-uniform scalar loads); the sorted rt_bentry_t -> blist
+__device__ void phase_bsort(const rt_setup_arg_t* a) {
+  const uint2* bidx = vx_ptr<const uint2>(a->bidx_addr);
+  const uint4* btmp = vx_ptr<const uint4>(a->btmp_addr);
+  uint4* blist = vx_ptr<uint4>(a->blist_addr);
+  const uint32_t waves = gridDim.x * (RTS_BLOCK / 64), l = lane_id();
+  if (blockIdx.x == 0 && threadIdx.x < 2)  // the 2 padding entries (the kernels load pairs ahead)
+    blist[a->blist_entries + threadIdx.x] = make_uint4(0u, RT_BLIST_PAD_LO, RT_BLIST_PAD_HI, RT_VIS_ZMIN_NONE);
+  for (uint32_t lb = blockIdx.x * (RTS_BLOCK / 64) + (threadIdx.x >> 6); lb < a->nblk; lb += waves) {
+    const uint2 oc = sload(bidx + lb);
+    for (uint32_t base = 0; base < oc.y; base += 64) {
+      const uint32_t i = base + l;
+      const uint4 me = btmp[oc.x + (i < oc.y ? i : 0u)];
+      uint32_t rank = 0, x0 = 0xffffu, x1 = 0, y0 = 0xffffu, y1 = 0;
+      for (uint32_t j = 0; j < oc.y; ++j) {
+        const uint4 o = sload(btmp + oc.x + j);
+        const bool before = o.x < me.x || (o.x == me.x && o.y < me.y);
+        rank += before ? 1u : 0u;
+        if (!before) {
+          x0 = min(x0, o.z & 0xffffu); x1 = max(x1, o.z >> 16);
+          y0 = min(y0, o.w & 0xffffu); y1 = max(y1, o.w >> 16);
+        }
+      }
+      if (i < oc.y) blist[oc.x + rank] = make_uint4(me.y, x0 | (y0 << 16), x1 | (y1 << 16), me.x);
     }
   }
 }
@@ -639,5 +823,11 @@ VX_MAIN(rt_setup_arg_t, arg, RTS_BLOCK) {
   if (ph & RTS_SCAN) phase_scan(arg);
   if (ph & RTS_SCATTER) phase_scatter(arg);
   if (ph & RTS_RECORDS) phase_records(arg);
+  if (ph & RTS_BCOUNT) phase_bcount(arg);
+  if (ph & RTS_BSUM) phase_bsum(arg);
+  if (ph & RTS_BSCAN) phase_bscan(arg);
+  if (ph & RTS_BOFF) phase_boff(arg);
+  if (ph & RTS_BFILL) phase_bfill(arg);
+  if (ph & RTS_BSORT) phase_bsort(arg);
   return 0;
 }

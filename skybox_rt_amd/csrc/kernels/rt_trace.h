@@ -12,7 +12,6 @@
 // the variants measured and not kept):
 //   RT_ONLY_BVH4H   the image walks only the binary16 BVH4 (the regular
 //                   images); 0: every layout (the deep images)
-//   RT_BLOCK_LIST   primary visibility from the per-block candidate lists
 //   RT_PUSH_UNCOND  per-lane BVH4 pushes as unconditional rows (path tracer)
 //   RT_LAZY_TASK_ARGS  task-map fields re-read from the argument block
 //   RT_INSTRUMENT   algorithmic counters (node visits, tests, texels)
@@ -27,9 +26,6 @@
 
 #ifndef RT_ONLY_BVH4H
 #define RT_ONLY_BVH4H 0
-#endif
-#ifndef RT_BLOCK_LIST
-#define RT_BLOCK_LIST 0
 #endif
 
 namespace rtk {
@@ -52,9 +48,7 @@ struct Scene {
   uint32_t shard_index, shard_count, tiles_x, clear_color, bounces, seed, split_tiles, split_log;
   float sx, sy, light[3];
   uint64_t argp;  // the argument block (constant address space), for lazy_args
-#if RT_BLOCK_LIST
-  uint32_t blist, bidx, bsuf, blist_nbx;  // per-block candidate lists
-#endif
+  uint32_t blist, bidx, blist_blocks;  // per-block candidate lists (rt_bentry_t)
 };
 
 // The argument block is read through the scalar cache (constant address
@@ -91,12 +85,9 @@ __device__ __forceinline__ Scene load_scene(const rt_kernel_arg_t* ga) {
   s.seed = a->seed;
   s.split_tiles = a->split_tiles;
   s.split_log = a->split_log;
-#if RT_BLOCK_LIST
   s.blist = (uint32_t)a->blist_addr;
   s.bidx = (uint32_t)a->bidx_addr;
-  s.bsuf = (uint32_t)a->bsuf_addr;
-  s.blist_nbx = a->blist_nbx;
-#endif
+  s.blist_blocks = a->blist_blocks;
   s.num_nodes = a->num_nodes;
   s.num_nodes4 = a->num_nodes4;
   s.num_layer = a->num_layer_tris;
@@ -884,46 +875,49 @@ __device__ __forceinline__ int32_t trace_primary_packet(const Scene& S, uint32_t
   return bpid;
 }
 
-// every lane of the wave calls it; lanes with !act get -1
-#if RT_BLOCK_LIST
-// The wave's 8x8 block resolved from its candidate list (rt_app.cpp
-// build_block_lists; oracle/rt.c vis_scan_block): records in ascending depth
-// bound, two per round,
-// every lane runs the exact test; the scan stops once no lane can change its
-// winner -- its pixel is outside the union rectangle of the remaining
-// records, or their smallest bound exceeds its best depth word.  Same
-// winners as the walk (vis_better is a strict order).  Tests count once per
-// wave per record tested, as the packet walk's do.
-__device__ __forceinline__ int32_t block_primary(const Scene& S, uint32_t px, uint32_t py, bool act,
-                                                 bool tie_high, Counters& cnt) {
+// The wave's 8x8 block resolved from its candidate list (rt_common.h
+// rt_bentry_t; oracle/rt.c vis_scan_block): entries in ascending (depth
+// bound, geometry index), two per round; every lane runs the exact test on
+// both records; the scan stops once no lane can change its winner -- its
+// pixel is outside the union rectangle of the remaining entries, or their
+// smallest bound exceeds its best depth word.  Same winners as the tree walk
+// (vis_better is a strict order).  The next round's entries are loaded with
+// this round's records, so a round is one scalar-load round trip.  Tests
+// count once per wave per record tested, as the packet walk's do.  Every
+// lane of the wave calls it with the wave's local block `lb` (uniform);
+// lanes with !act get -1.
+__device__ __forceinline__ int32_t block_primary(const Scene& S, uint32_t lb, uint32_t px, uint32_t py,
+                                                 bool act, bool tie_high, Counters& cnt) {
   (void)cnt;
-  const uint32_t bx = (uint32_t)__builtin_amdgcn_readfirstlane(px >> 3);
-  const uint32_t by = (uint32_t)__builtin_amdgcn_readfirstlane(py >> 3);
   if (!act) px = 0xffffffffu;
   const uint32_t pp = px > 0xffffu ? 0xffffffffu : px | (py << 16);
-  const uint2 oc = S.A.sld<uint2>(S.bidx + 8u * (by * S.blist_nbx + bx));
+  const uint2 oc = S.A.sld<uint2>(S.bidx + 8u * lb);
   uint32_t bz = VX_OM_DEPTH_MASK;
   int32_t bpid = -1;
+  uint4 e[2];
+  S.A.sld_u4n<2>(S.blist + 16u * oc.x, e);  // the list carries 2 padding entries
   for (uint32_t k = 0; k < oc.y; k += 2) {
-    uint4 tw[8];
-    S.A.sld_u4n<8>(S.blist + 64u * (oc.x + k), tw);
-    const uint2 sr = S.A.sld<uint2>(S.bsuf + 8u * (oc.x + k));
-    if (__ballot(rect2_in(sr.x, sr.y, pp) && tw[3].w <= bz) == 0) break;
+    if (__ballot(rect2_in(e[0].y, e[0].z, pp) && e[0].w <= bz) == 0) break;
+    uint4 r0[4], r1[4], en[2];
+    S.A.sld_u4n<4>(S.vgeom + 64u * e[0].x, r0);
+    S.A.sld_u4n<4>(S.vgeom + 64u * e[1].x, r1);
+    S.A.sld_u4n<2>(S.blist + 16u * (oc.x + k + 2), en);
 #ifdef RT_INSTRUMENT
     cnt.tests += lane_id() == 0 ? (k + 1 < oc.y ? 2u : 1u) : 0u;  // once per wave per record
 #endif
-    vis_test(tw[0], tw[1], tw[2], tw[3], px, py, tie_high, bz, bpid);
-    if (k + 1 < oc.y) vis_test(tw[4], tw[5], tw[6], tw[7], px, py, tie_high, bz, bpid);
+    vis_test(r0[0], r0[1], r0[2], r0[3], px, py, tie_high, bz, bpid);
+    if (k + 1 < oc.y) vis_test(r1[0], r1[1], r1[2], r1[3], px, py, tie_high, bz, bpid);
+    e[0] = en[0];
+    e[1] = en[1];
   }
   return act ? bpid : -1;
 }
-#endif
 
-__device__ __forceinline__ int32_t trace_primary(const Scene& S, uint32_t px, uint32_t py, bool act,
-                                                 bool tie_high, Counters& cnt) {
-#if RT_BLOCK_LIST
-  if (S.blist_nbx) return block_primary(S, px, py, act, tie_high, cnt);
-#endif
+// primary visibility of the wave's pixels: the block's candidate list when
+// the host built lists (blist_blocks), else the packet walk of the tree
+__device__ __forceinline__ int32_t trace_primary(const Scene& S, uint32_t lb, uint32_t px, uint32_t py,
+                                                 bool act, bool tie_high, Counters& cnt) {
+  if (S.blist_blocks) return block_primary(S, lb, px, py, act, tie_high, cnt);
   const int32_t h = trace_primary_packet(S, px, py, act, tie_high, cnt);
   return act ? h : -1;
 }
@@ -1038,9 +1032,14 @@ __device__ __forceinline__ TaskPix task_map(const Scene& S, uint32_t t) {
   return task_map(S, task_args(S), t);
 }
 
-__device__ __forceinline__ void task_pixel(const Scene& S, uint32_t t, uint32_t* x, uint32_t* y) {
+// pixel of task t (dead lanes of split tiles: x = 0xffffffff, off-image)
+// and, optionally, its local 8x8 block lt * 16 + block of the tile (the same
+// for every lane of a wave: wave-uniform)
+__device__ __forceinline__ void task_pixel(const Scene& S, uint32_t t, uint32_t* x, uint32_t* y,
+                                           uint32_t* lb = nullptr) {
   const TaskArgs T = task_args(S);
   const TaskPix m = task_map(S, T, t);
+  if (lb) *lb = (uint32_t)__builtin_amdgcn_readfirstlane((m.lt << 4) | (m.idx >> 6));
   const uint32_t blk = m.idx >> 6, ln = m.idx & 63u;
   const uint32_t gt = T.shard_index + m.lt * T.shard_count;
   const uint32_t tx = gt % T.tiles_x, ty = gt / T.tiles_x;

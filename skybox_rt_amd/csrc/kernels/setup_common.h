@@ -14,6 +14,8 @@
 //   vtris / vlayers / vgeom  rt_vtri_t records   (app/vis.cpp MakeVisTri)
 //   vnodes  rt_vnode_t per tree node, bottom-up  (app/vis.cpp BuildVisNodes)
 //   order   the shard's tiles, heaviest first    (app/rt_app.cpp tile order)
+//   bidx / blist  per local 8x8 block its candidate list (rt_bentry_t,
+//           rt_common.h): count, scan, fill, sort    (app/rt_app.cpp BuildBlockLists)
 // and the resolution-independent triangle records at renderer creation
 // (ptris by pid, geom).  Every record equals the host path's bit for bit
 // (tests/test_gpu_setup.py; the host path stays selectable: RT_SETUP=host).
@@ -23,7 +25,7 @@
 
 #define RTS_BLOCK 256
 #define RTS_ITEMS 1024            // tile-order sort items per block (4 per thread)
-#define RTS_MAX_FILLS 4
+#define RTS_MAX_FILLS 6
 #define RTS_WEIGHT_CAP 255u       // tile-order key: min(weight, 255), one 8-bit digit
 
 // sub-phases, OR-ed into `phases`: a launch runs every selected sub-phase
@@ -43,8 +45,18 @@
 #define RTS_SCAN     0x200u  //   exclusive scan (workgroup 0)
 #define RTS_SCATTER  0x400u  //   stable scatter of the local tile indices -> order
 #define RTS_RECORDS  0x800u  // renderer creation: rt_tri_t per pid (ptris), geometry list (geom)
+// per-block candidate lists (rt_bentry_t): a wave per geometry primitive
+// visits the shard's 8x8 blocks its covered rectangle reaches
+#define RTS_BCOUNT   0x1000u // atomic count per local block
+#define RTS_BSUM     0x2000u // per 1024 blocks: sum (-> bpart) and the longest list (status[1])
+#define RTS_BSCAN    0x4000u // exclusive scan of bpart (workgroup 0), total -> status[2]
+#define RTS_BOFF     0x8000u // per local block (first entry, count) -> bidx; counts zeroed
+#define RTS_BFILL    0x10000u // unsorted (zmin, k, rx, ry) per (block, primitive) -> btmp
+#define RTS_BSORT    0x20000u // wave per block: rank + suffix union -> blist (+2 pads)
+#define RTS_BLOCKS_PER_PART 1024u  // blocks summed per bpart word (4 per thread)
 
-// status words (u32 [4]): [0] malformed-input flags (RTS_ERR_*), [1..3] spare
+// status words (u32 [4]): [0] malformed-input flags (RTS_ERR_*), [1] the
+// longest block list, [2] list entries in total, [3] spare
 #define RTS_ERR_REF   0x1u   // a tree reference out of range
 #define RTS_ERR_PID   0x2u   // a leaf record's pid out of range
 #define RTS_ERR_CLIMB 0x4u   // a climb longer than 64 levels
@@ -78,10 +90,16 @@ typedef struct {
   uint64_t status_addr;    // u32 [4]
   uint64_t ptris_addr;     // rt_tri_t [P]
   uint64_t geom_addr;      // rt_tri_t [num_geom]
+  uint64_t bcnt_addr;      // u32 [nblk]: entries per local block (then the fill cursors)
+  uint64_t bpart_addr;     // u32 [nbpart]: per RTS_BLOCKS_PER_PART blocks their sum, then its scan
+  uint64_t bidx_addr;      // uint32[2] [nblk]: first entry, count
+  uint64_t btmp_addr;      // uint4 [entries]: unsorted (zmin, k, rx, ry)
+  uint64_t blist_addr;     // rt_bentry_t [entries + 2]
   rts_fill_t fills[RTS_MAX_FILLS];
   uint32_t phases, nfills;
   uint32_t num_prims, width, height, raster;
   uint32_t num_tris, num_nodes, bvh4, num_layers, num_geom;
   uint32_t tiles_x, tiles_y, shard_index, shard_count, local_tiles, nblocks;
-  uint32_t pad[3];
+  uint32_t nblk, nbpart, blist_entries;  // local 8x8 blocks, bpart words, list entries (BSORT)
+
 } rt_setup_arg_t;

@@ -51,7 +51,10 @@ def _scene(name, tmp_path_factory=None):
 
 
 def _records(r, names):
-    return {n: r.records(n) for n in names}
+    out = {n: r.records(n) for n in names}
+    if r.setup_stats()["blist_blocks"]:  # the per-block candidate lists
+        out.update({n: r.records(n) for n in ("bidx", "blist")})
+    return out
 
 
 def _equal(a, b, what):
@@ -71,7 +74,8 @@ def _device_vs_host(r, w, h, **kw):
     ds = r.setup_stats()
     assert ds["device"] == 1 and hs["device"] == 0
     assert ds["heavy_tiles"] == hs["heavy_tiles"]
-    for n in REC_RT:
+    assert sorted(dev) == sorted(host)
+    for n in dev:
         _equal(dev[n], host[n], n)
     r.render()
     assert np.array_equal(r.framebuffer(), fb_host)
@@ -145,8 +149,8 @@ def test_device_setup_over_device_tree(tmp_path_factory, name, width):
 
 def test_device_setup_frames_equal_oracle_with_counts(oracle_lib):
     """Instrumented frames on device-built records: image and traversal
-    counts == the oracle's (the vnodes' rectangles and depth bounds drive
-    the primary packet walk's visits)."""
+    counts == the oracle's (the block lists drive the primary tests, the
+    BVH4 the shadow rays' visits)."""
     po = oracle_lib
     path = scene_path("tekkaman")
     s = rt.Scene.load(path)
