@@ -621,10 +621,10 @@ __device__ void phase_bcount(const rt_setup_arg_t* a) {
   }
 }
 
-// workgroup reduction (sum and max) of one value per thread
-__device__ __forceinline__ void block_sum_max(uint32_t x, uint32_t* sum, uint32_t* mx) {
+// workgroup reduction: the sum of xs and the max of xm over the threads
+__device__ __forceinline__ void block_sum_max(uint32_t xs, uint32_t xm, uint32_t* sum, uint32_t* mx) {
   __shared__ uint32_t ss[RTS_BLOCK / 64], sm[RTS_BLOCK / 64];
-  uint32_t s = x, m = x;
+  uint32_t s = xs, m = xm;
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) {
     s += (uint32_t)__shfl_xor((int)s, o, 64);
@@ -654,7 +654,7 @@ __device__ void phase_bsum(const rt_setup_arg_t* a) {
       mx = max(mx, c);
     }
     uint32_t ts, tm;
-    block_sum_max(sum, &ts, &tm);
+    block_sum_max(sum, mx, &ts, &tm);
     if (threadIdx.x == 0) {
       bpart[b] = ts;
       atomicMax(&status[1], tm);
