@@ -152,7 +152,13 @@ int rt_renderer_build_bvh(rt_renderer_h r, rt_bvh_build_stats_t* stats);  /* = _
  * scene's host build, bit for bit. */
 #define RT_BVH_BUILD_LBVH 0u
 #define RT_BVH_BUILD_SAH 1u
+#define RT_BVH_BUILD_HOST 2u  /* the scene's host build (app/bvh.cpp) uploaded: env RT_BVH=host */
 int rt_renderer_build_bvh_ex(rt_renderer_h r, uint32_t method, rt_bvh_build_stats_t* stats);
+/* How the renderer's current tree was built: rt_renderer_create builds it on
+ * the device with RT_BVH_BUILD_SAH (the host builder's tree bit for bit;
+ * RT_BVH_BUILD_HOST under env RT_BVH=host or for a scene without geometry),
+ * or the last rt_renderer_build_bvh_ex. */
+int rt_renderer_bvh_stats(rt_renderer_h r, rt_bvh_build_stats_t* stats);
 #define RT_BVH_STACK4_UNUSED 0xFFFFFFFFu
 /* the renderer's current BVH4 (float[num_nodes4][32], rt_node4_t: the host
  * tree's collapse, or after rt_renderer_build_bvh the device collapse --

@@ -123,9 +123,7 @@ int rt_scene_load(const char* path, rt_scene_h* out) {
   }
   std::reverse(sc->layers.begin(), sc->layers.end());
   sc->tie_high = geom_func == VX_OM_DEPTH_FUNC_LEQUAL;
-  t0 = std::chrono::steady_clock::now();
-  if (rt::BuildBvh(build, &sc->bvh, &err) != 0) return fail(err);
-  sc->bvh_ms = ms_since(t0);
+  sc->build_tris = std::move(build);
   *out = sc.release();
   return 0;
 }
@@ -137,6 +135,7 @@ int rt_scene_free(rt_scene_h s) {
 
 int rt_scene_info(rt_scene_h s, rt_scene_info_t* info) {
   if (!s || !info) return fail("null argument");
+  if (rtapp::host_bvh(s) != 0) return -1;
   std::memset(info, 0, sizeof(*info));
   info->num_drawcalls = (uint32_t)s->scene.drawcalls.size();
   info->num_prims = (uint32_t)s->scene.prims.size();
@@ -172,6 +171,7 @@ int rt_scene_export_prims(rt_scene_h s, float* out, uint64_t count) {
 
 int rt_scene_export_bvh(rt_scene_h s, float* nodes, float* tris) {
   if (!s) return fail("null argument");
+  if (rtapp::host_bvh(s) != 0) return -1;
   if (nodes) std::memcpy(nodes, s->bvh.nodes.data(), s->bvh.nodes.size() * sizeof(rt_node_t));
   if (tris) std::memcpy(tris, s->bvh.tris.data(), s->bvh.tris.size() * sizeof(rt_tri_t));
   return 0;
@@ -179,11 +179,22 @@ int rt_scene_export_bvh(rt_scene_h s, float* nodes, float* tris) {
 
 int rt_scene_export_bvh4(rt_scene_h s, float* nodes4) {
   if (!s || !nodes4) return fail("null argument");
+  if (rtapp::host_bvh(s) != 0) return -1;
   std::memcpy(nodes4, s->bvh.nodes4.data(), s->bvh.nodes4.size() * sizeof(rt_node4_t));
   return 0;
 }
 
 }  // extern "C"
+
+int rtapp::host_bvh(rt_scene* s) {
+  if (s->bvh_built) return 0;
+  const auto t0 = std::chrono::steady_clock::now();
+  std::string err;
+  if (rt::BuildBvh(s->build_tris, &s->bvh, &err) != 0) return fail(err);
+  s->bvh_ms = ms_since(t0);
+  s->bvh_built = true;
+  return 0;
+}
 
 bool rtapp::block_lists_fit(uint64_t longest, uint64_t entries) {
   uint64_t cap = 16ull << 20;
@@ -205,6 +216,8 @@ int rtapp::upload(vx_device_h dev, const void* data, uint64_t size, vx_buffer_h*
   return 0;
 }
 
+static int build_sah(rt_renderer_h r, rt_bvh_build_stats_t* st);
+
 extern "C" {
 
 int rt_renderer_create(rt_scene_h s, const char* kernel_dir, rt_renderer_h* out) {
@@ -217,11 +230,19 @@ int rt_renderer_create(rt_scene_h s, const char* kernel_dir, rt_renderer_h* out)
   }
   const std::string dir = kernel_dir ? kernel_dir : lib_dir();
   r->kdir = dir;
+  // the tree: built on the device from the ingested triangles (bvh_sah.hip,
+  // the host builder's binned SAH restated, equal to it bit for bit) unless
+  // env RT_BVH=host asks for the host build (app/bvh.cpp) uploaded
+  const char* bv = std::getenv("RT_BVH");
+  const bool host_tree = (bv && std::string(bv) == "host") || s->geometry.empty();
+  if (host_tree && rtapp::host_bvh(s) != 0) return -1;
+  static const rt::Bvh kEmpty{};
+  const rt::Bvh& bvh = host_tree ? s->bvh : kEmpty;
   // the regular image's LDS stack holds RT_STACK_SHALLOW (24) entries; a BVH whose traversal may
   // need more (BVH2: its depth, BVH4: its stack bound) uses the deep image
-  // (32 entries, lower occupancy)
-  const bool deep = std::max(s->bvh.depth, s->bvh.stack4) > RT_STACK_SHALLOW;
-  if (std::max(s->bvh.depth, s->bvh.stack4) > RT_STACK_DEEP)
+  // (32 entries, lower occupancy); build_sah decides for a device tree
+  const bool deep = std::max(bvh.depth, bvh.stack4) > RT_STACK_SHALLOW;
+  if (std::max(bvh.depth, bvh.stack4) > RT_STACK_DEEP)
     return fail("BVH too deep for the traversal stack");
   r->deep = deep;
   const char* names[4][2] = {
@@ -250,7 +271,6 @@ int rt_renderer_create(rt_scene_h s, const char* kernel_dir, rt_renderer_h* out)
   r->set_counters = (vx_hip_set_counters_t)vx_driver_symbol("vx_hip_set_counters");
   rt_kernel_arg_t& a = r->arg;
   std::memset(&a, 0, sizeof(a));
-  const rt::Bvh& bvh = s->bvh;
   // 3 padding records: the kernel fetches all 4 slots of a leaf at once
   std::vector<rt_tri_t> tris(bvh.tris);
   tris.resize(tris.size() + 3);
@@ -321,7 +341,25 @@ int rt_renderer_create(rt_scene_h s, const char* kernel_dir, rt_renderer_h* out)
   for (const rt::DrawCall& dc : s->scene.drawcalls) oms.push_back(rt::OmState(dc));
   if (upload(r->dev, oms.data(), oms.size() * sizeof(rt_omstate_t), &r->oms, &a.oms_addr)) return -1;
   a.num_drawcalls = (uint32_t)oms.size();
+  std::memset(&r->bvh_stats, 0, sizeof(r->bvh_stats));
+  if (!host_tree) {
+    if (build_sah(r.get(), &r->bvh_stats) != 0) return -1;
+  } else {
+    r->bvh_stats.nodes = (uint32_t)bvh.nodes.size();
+    r->bvh_stats.depth = bvh.depth;
+    r->bvh_stats.stack4 = bvh.stack4;
+    r->bvh_stats.nodes4 = (uint32_t)bvh.nodes4.size();
+    r->bvh_stats.depth4 = bvh.depth4;
+    r->bvh_stats.build_ms = s->bvh_ms;
+    r->bvh_stats.method = RT_BVH_BUILD_HOST;
+  }
   *out = r.release();
+  return 0;
+}
+
+int rt_renderer_bvh_stats(rt_renderer_h r, rt_bvh_build_stats_t* st) {
+  if (!r || !st) return fail("null argument");
+  *st = r->bvh_stats;
   return 0;
 }
 
@@ -512,6 +550,7 @@ static int tree_refs(rt_renderer* r, bool use_bvh4, std::vector<std::array<int32
         return fail("vx_copy_from_dev failed");
     }
   } else {
+    if (rtapp::host_bvh(r->sc) != 0) return -1;
     tr = s->bvh.tris;
     if (use_bvh4) n4 = s->bvh.nodes4;
     else n2 = s->bvh.nodes;
@@ -1301,9 +1340,14 @@ static int build_sah(rt_renderer_h r, rt_bvh_build_stats_t* st) {
 int rt_renderer_build_bvh_ex(rt_renderer_h r, uint32_t method, rt_bvh_build_stats_t* st) {
   if (!r) return fail("null argument");
   if (r->sc->geometry.empty()) return fail("no depth-tested geometry to build a BVH over");
-  if (method == RT_BVH_BUILD_SAH) return build_sah(r, st);
-  if (method != RT_BVH_BUILD_LBVH) return fail("unknown BVH build method");
-  return build_lbvh(r, st);
+  if (method != RT_BVH_BUILD_SAH && method != RT_BVH_BUILD_LBVH) return fail("unknown BVH build method");
+  rt_bvh_build_stats_t tmp;
+  const int rc = method == RT_BVH_BUILD_SAH ? build_sah(r, &tmp) : build_lbvh(r, &tmp);
+  if (rc == 0) {
+    r->bvh_stats = tmp;
+    if (st) *st = tmp;
+  }
+  return rc;
 }
 
 int rt_renderer_build_bvh(rt_renderer_h r, rt_bvh_build_stats_t* st) {

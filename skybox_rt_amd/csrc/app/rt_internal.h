@@ -17,7 +17,9 @@
 
 struct rt_scene {
   rt::Scene scene;
-  rt::Bvh bvh;
+  rt::Bvh bvh;                    // the host build: on request only (host_bvh)
+  std::vector<rt::BuildTri> build_tris;  // its input: the depth-tested triangles, clip (x, y, w)
+  bool bvh_built = false;
   std::vector<int32_t> geometry;  // depth-tested prims (BVH input), ascending
   std::vector<int32_t> layers;    // screen-layer prims, descending pid
   std::string unsupported;        // non-empty: the RT path cannot render it
@@ -65,6 +67,7 @@ struct rt_renderer {
   bool gpu_bvh4 = false;    // ... and collapsed to a BVH4 there whose stack fits the images
   uint32_t num_tris = 0;    // leaf triangle records (without the 3 padding records)
   rt_setup_stats_t setup{};  // the last configuration's setup (rt_renderer_setup_stats)
+  rt_bvh_build_stats_t bvh_stats{};  // how the current tree was built (rt_renderer_bvh_stats)
 
   ~rt_renderer() {
     vx_buffer_h* bufs[] = {&krnl[0][0], &krnl[0][1], &krnl[1][0], &krnl[1][1], &krnl[2][0],
@@ -82,6 +85,10 @@ struct rt_renderer {
 };
 
 namespace rtapp {
+
+// the scene's host BVH (app/bvh.cpp), built on first use: the renderer
+// builds its tree on the device (bvh_sah.hip) unless env RT_BVH=host
+int host_bvh(rt_scene* s);
 
 // (re)allocate *buf (size bytes, or 64 when 0), copy `data` when given; the
 // device address must lie below 4 GiB (the kernels' 32-bit arena offsets)

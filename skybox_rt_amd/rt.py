@@ -35,6 +35,7 @@ RECORDS = {"prims": (0, np.int32, 32), "bbox": (1, np.uint32, 2), "vis": (2, np.
            "vgeom": (6, np.int32, 16), "order": (7, np.uint32, 1), "ptris": (8, np.float32, 12),
            "geom": (9, np.float32, 12), "bidx": (10, np.uint32, 2), "blist": (11, np.uint32, 4)}
 RT_BVH_STACK4_UNUSED = 0xFFFFFFFF
+RT_BVH_BUILD_HOST = 2
 CLEAR_COLOR = 0xFF000000               # draw3d/main.cpp:47
 DEFAULT_LIGHT = (0.0, 60.0, 80.0)      # clip (x, y, w), SURVEY.md 8(d) config 3
 TILE = 32                              # RASTER_TILE_LOGSIZE = 5
@@ -106,6 +107,7 @@ def lib():
             "rt_scene_export_bvh4": [vp, vp],
             "rt_renderer_build_bvh": [vp, C.POINTER(BvhBuildStats)],
             "rt_renderer_build_bvh_ex": [vp, u32, C.POINTER(BvhBuildStats)],
+            "rt_renderer_bvh_stats": [vp, C.POINTER(BvhBuildStats)],
             "rt_renderer_export_bvh": [vp, vp, vp, C.POINTER(u32), C.POINTER(u32)],
             "rt_renderer_export_bvh4": [vp, vp, C.POINTER(u32)],
             "rt_renderer_export_bvh4h": [vp, vp, C.POINTER(u32)],
@@ -237,7 +239,11 @@ class Renderer:
                                         C.byref(h)), "rt_renderer_create")
         self._h = h
         self.params = None
-        self.gpu_bvh = self.gpu_bvh4 = False
+        # the tree rt_renderer_create built: on the device (binned SAH, the
+        # host build's arrays) unless env RT_BVH=host
+        st = self.bvh_stats()
+        self.gpu_bvh = st["method"] != RT_BVH_BUILD_HOST
+        self.gpu_bvh4 = self.gpu_bvh and st["stack4"] != RT_BVH_STACK4_UNUSED
 
     def configure(self, width: int, height: int, shadows: bool = True, light=DEFAULT_LIGHT,
                   clear_color: int = CLEAR_COLOR, shard_index: int = 0, shard_count: int = 1,
@@ -294,6 +300,13 @@ class Renderer:
         _check(lib().rt_renderer_export_records(self._h, which, out.ctypes.data, out.nbytes, C.byref(n)),
                f"rt_renderer_export_records({name})")
         return out[:n.value // 4].reshape(-1, words)
+
+    def bvh_stats(self) -> dict:
+        """How the current tree was built (method: 0 LBVH, 1 SAH on the
+        device, 2 the host build; nodes, depth, stack4, build_ms, ...)."""
+        st = BvhBuildStats()
+        _check(lib().rt_renderer_bvh_stats(self._h, C.byref(st)), "rt_renderer_bvh_stats")
+        return st.as_dict()
 
     def build_bvh(self, method: str = "lbvh") -> dict:
         """Build the BVH on the device and trace over it from now on; returns
