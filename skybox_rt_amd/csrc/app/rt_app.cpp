@@ -232,9 +232,12 @@ int rt_renderer_create(rt_scene_h s, const char* kernel_dir, rt_renderer_h* out)
   r->kdir = dir;
   // the tree: built on the device from the ingested triangles (bvh_sah.hip,
   // the host builder's binned SAH restated, equal to it bit for bit) unless
-  // env RT_BVH=host asks for the host build (app/bvh.cpp) uploaded
+  // env RT_BVH=host asks for the host build (app/bvh.cpp) uploaded; so does
+  // the host builder's fp32-box BVH4 variant (env RT_BVH_F16=0)
   const char* bv = std::getenv("RT_BVH");
-  const bool host_tree = (bv && std::string(bv) == "host") || s->geometry.empty();
+  const char* f16 = std::getenv("RT_BVH_F16");
+  const bool host_tree = (bv && std::string(bv) == "host") || (f16 && std::atoi(f16) == 0) ||
+                         s->geometry.empty();
   if (host_tree && rtapp::host_bvh(s) != 0) return -1;
   static const rt::Bvh kEmpty{};
   const rt::Bvh& bvh = host_tree ? s->bvh : kEmpty;
