@@ -2,10 +2,12 @@
 """bench.py -- headline benchmark: Mrays/s of the MI355X ray-tracing hot path.
 
 Workload at N = 1 (BASELINE.json configs[2], the metric's config):
-tekkaman.cgltrace, 1024x1024, one primary ray per pixel + one any-hit shadow
-ray per geometry hit, BVH traversal with the per-wave LDS stack.  A "step" is
-one full frame: vx_start + vx_ready_wait of the RT kernel image through
-libvortex-hip.so (inputs already resident in HBM).
+tekkaman.cgltrace, 1024x1024, one primary ray per pixel (raster-exact, from
+the per-8x8-block candidate lists built on the device) + one any-hit shadow
+ray per geometry hit (binary16 BVH4, wave packets, ballot/mbcnt-compacted).
+A "step" is one full frame: vx_start of the RT kernel image through
+libvortex-hip.so (inputs already resident in HBM), every frame complete
+inside the timed region.
 
 With N > 1 GPUs (one rank per GPU over RCCL) the default workload is
 BASELINE config 5: ONE 4096x4096 frame whose 32x32 tiles are dealt
@@ -339,7 +341,10 @@ def main():
     ap.add_argument("--cpu-budget", type=float, default=15.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-series", action="store_true",
-                    help="skip the strong/weak scaling series runs")
+                    help="skip the strong/weak scaling series runs (default at N>1)")
+    ap.add_argument("--series", action="store_true",
+                    help="N=1: also run the series (4096^2 strong point, weak 1024^2); off by default "
+                         "so the timed image's rocprof average is the metric's frame size only")
     ap.add_argument("--workload", choices=("shadow", "path", "flat"), default="shadow",
                     help="shadow: BASELINE config 3 (the metric's config, default); "
                          "path: config 4, 4-bounce diffuse path trace; "
@@ -413,14 +418,15 @@ def main():
     light = rt.DEFAULT_LIGHT
     side = args.size
     scene = rt.Scene.load(SCENE)
-    info = scene.info()
     r = rt.Renderer(scene)
+    bvh_st = r.bvh_stats()  # the renderer's tree, built on the device at creation
 
     def make_run(s):
         return Run(r, rt, dist, coll_dev, rank, n_gpus, s, shadows, light, path, flat,
                    args.bounces, use_gather)
 
     run = make_run(side)
+    setup_st = r.setup_stats()  # the timed configuration's records (configure)
     inst = run.inst
     bvh_kind = ("BVH4 (binary16 boxes)" if r.bvh4_f16 else "BVH4") if r.bvh4 else "BVH2"
     alg_bytes = algorithmic_bytes(inst, inst["primary_rays"], (NODE4H_BYTES if r.bvh4_f16 else NODE4_BYTES)
@@ -459,7 +465,7 @@ def main():
     # scaling series: the same render at 4096^2 on these N GPUs (strong) and
     # at ~1024^2 * sqrt(N) (weak); short runs, reported beside `value`
     series = {}
-    if not args.no_series and not flat:
+    if not args.no_series and not flat and (n_gpus > 1 or args.series):
         series_steps = max(20, min(args.steps, 200))
         for name, s in (("strong_4096", CONFIG5_SIDE), ("weak_1024_sqrtN", frame_side(n_gpus, 1024))):
             if s == side:
@@ -487,13 +493,19 @@ def main():
         metric = (f"Mrays/sec per GPU + achieved HBM GB/s, {side}^2 primary rays, tekkaman flat "
                   f"triangle list, no BVH (BASELINE config 2)")
         kind = "primary rays, flat triangle list (no BVH, LDS-staged)"
+    primary = ("primary: 8x8-block candidate lists built on the device (raster-exact)"
+               if setup_st["blist_blocks"] else f"primary: {bvh_kind} packet walk (raster-exact)")
     if flat:
-        workload = f"{side}x{side} {kind}, tekkaman.cgltrace"
+        workload = (f"{side}x{side} {kind}, tekkaman.cgltrace: every ray tests the whole geometry "
+                    f"list (rectangle words in LDS, wave-uniform rectangle skip, exact edge + depth test)")
     elif path:
-        workload = f"{side}x{side} {kind}, tekkaman.cgltrace, {bvh_kind} + LDS stack"
+        workload = (f"{side}x{side} {kind}, tekkaman.cgltrace; {primary}; bounce + shadow rays: "
+                    f"per-lane {bvh_kind} walk, LDS stack, shadow/bounce lanes paired in the "
+                    f"32-pixel waves of geometry tiles")
     else:
         workload = (f"{side}x{side} {'primary+shadow' if shadows else 'primary'} rays, "
-                    f"tekkaman.cgltrace, {bvh_kind} + LDS stack")
+                    f"tekkaman.cgltrace; {primary}; shadow rays: ballot/mbcnt-compacted into full "
+                    f"waves, each wave a {bvh_kind} packet walk (stack in one VGPR)")
     if n_gpus > 1:
         workload += (f", tile-sharded over {n_gpus} GPUs (32x32 tile t -> rank t mod {n_gpus}) + "
                      f"{'RCCL' if backend == 'nccl' else backend} gather to rank 0"
@@ -501,6 +513,7 @@ def main():
     mode = "path" if path else ("flat" if flat else "shadow")
     rec, stale = pmc_record(mode, side) if n_gpus == 1 else (None, False)
     traffic = rec["traffic_bytes"] if rec else None
+    info = scene.info()  # (after the timed region: parse time, host-side counts)
     out = {
         "metric": metric,
         "value": round(value, 3),
@@ -521,8 +534,18 @@ def main():
             "parallelism": f"tiles32 mod {n_gpus}" + (f" + {'rccl' if backend == 'nccl' else backend} "
                                                       f"gather" if n_gpus > 1 else ""),
             "ranks_seen": ranks_seen,
-            "bvh_nodes": info["bvh4_nodes" if r.bvh4 else "bvh_nodes"],
-            "bvh_depth": info["bvh4_depth" if r.bvh4 else "bvh_depth"],
+            "bvh_nodes": bvh_st["nodes4" if r.bvh4 else "nodes"],
+            "bvh_depth": bvh_st["depth4" if r.bvh4 else "depth"],
+            # scene parse, BVH build and per-resolution setup
+            # are reported separately, outside the timed frames
+            "parse_ms": round(info["parse_ms"], 3),
+            "bvh_build_ms": round(bvh_st["build_ms"], 3),
+            "bvh_build": {0: "device LBVH", 1: "device binned SAH (kernels/bvh_sah.hip)",
+                          2: "host binned SAH"}.get(bvh_st["method"], "?"),
+            "configure_ms": round(setup_st["configure_ms"], 3),
+            "setup_ms": round(setup_st["setup_ms"], 3),
+            "setup": ("device" if setup_st["device"] else "host") + f", {setup_st['launches']} launches",
+            "block_list_entries": int(setup_st["blist_entries"]),
             "grid": st["grid"], "block": st["block"],
             "rays_per_frame": int(rays_total),
             "mrays_per_s_per_gpu": round(value / n_gpus, 3),
@@ -549,6 +572,9 @@ def main():
     if stale:
         out["roofline"]["traffic_stale"] = True
     if rec:
+        out["roofline"]["traffic_calibrated"] = bool(rec.get("traffic_calibrated", False))
+        if "traffic_bounds" in rec:
+            out["roofline"]["traffic_bounds"] = rec["traffic_bounds"]
         # measured HBM bytes per launch over the same kernel time: the share of
         # the HBM peak the kernel physically uses (the scene is cache-resident)
         out["roofline"]["measured_hbm_gbs"] = round(traffic / (avg_kernel_ms * 1e-3) / 1e9, 2)
@@ -569,14 +595,24 @@ def main():
                 "source": f"profiles/pmc_{mode}.json (rocprofv3 --pmc passes, scripts/pmc_profile.sh)",
             }
     if flat:
-        # the flat list is read from LDS, never from HBM: its bound is the MT
-        # arithmetic -- SURVEY 8(d): ~40 fp32 ops per test, 157.3 TFLOP/s vector peak
-        tflops = MT_FLOPS * (inst["tri_tests"] + inst["layer_tests"]) / (avg_kernel_ms * 1e-3) / 1e12
-        out["roofline"].update({"bound": "valu", "achieved": round(tflops, 3),
-                                "peak": FP32_VALU_TFLOPS, "unit": "TFLOP/s",
-                                "frac": round(tflops / FP32_VALU_TFLOPS, 4),
-                                "lds_bytes_per_launch": int(alg_bytes)})
+        # the flat list is read from LDS and the scalar cache, never from HBM,
+        # and the kernel prunes with an integer rectangle test: its bound is
+        # VALU issue (measured, profiles/pmc_flat.json).  The work executed per
+        # frame (instrumented image, per wave): rectangle words tested and the
+        # entries some lane lay in (edge + depth tests); the algorithmic list
+        # (every ray x every primitive) is reported beside it
+        work = {"rect_tests_per_wave": int(inst["rect_tests"]), "edge_tests_per_wave": int(inst["edge_tests"]),
+                "list_entries_per_ray_algorithmic": int(inst["tri_tests"])}
         out["roofline"].pop("algorithmic_bytes_per_launch")
+        if "roofline_issue" in out:
+            ri = out.pop("roofline_issue")
+            out["roofline"] = {**ri, "traffic": traffic, "work_executed": work,
+                               "counts": out["roofline"]["counts"]}
+            if rec:
+                out["roofline"]["measured_hbm_gbs"] = round(traffic / (avg_kernel_ms * 1e-3) / 1e9, 2)
+        else:
+            out["roofline"].update({"bound": "valu_issue", "achieved": None, "frac": None,
+                                    "work_executed": work, "note": "no current PMC record"})
     if gather_ok is not None:
         out["config"]["gather_verified"] = gather_ok
     if n_gpus == 1 and not args.no_cpu_baseline:

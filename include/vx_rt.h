@@ -70,6 +70,10 @@ typedef struct {
   uint32_t grid, block;       /* launch geometry chosen by the driver */
   uint32_t num_tasks, local_tiles;
   uint64_t bounce_rays;       /* RT_RENDER_PATH: bounce segments traced */
+  uint64_t rect_tests;        /* RT_RENDER_FLAT, instrumented: list entries whose rectangle a
+                                 wave tested (per wave, the work executed) */
+  uint64_t edge_tests;        /* RT_RENDER_FLAT, instrumented: entries some lane of the wave
+                                 lay in, whose edges and depth the wave evaluated */
 } rt_stats_t;
 
 const char* rt_last_error(void);

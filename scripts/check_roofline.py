@@ -1,0 +1,86 @@
+#!/usr/bin/env python3
+"""Recompute a bench line's roofline numbers from the committed profiles
+(the headline must be reproducible from profiles/ for the
+image actually timed).
+
+Inputs: the bench JSON line (bench.py's stdout, or the driver's BENCH_rNN.json
+whose `parsed` holds it), the rocprofv3 --kernel-trace --stats summary of the
+same command (<prefix>_kernel_stats.csv: one row per kernel name; every
+image's entry is vx_main_<image>, so the timed kernel is its own row), and
+the PMC record the line cites (profiles/pmc_<mode>.json).
+
+Recomputed:
+  roofline.frac            algorithmic bytes per launch / rocprof average
+                           duration of the timed image / 8 TB/s
+  roofline.measured_hbm_frac  PMC traffic per launch / the same duration / 8 TB/s
+  roofline_issue.frac      PMC VALU wave-instructions per launch / duration /
+                           1228.8 G/s
+and compared with the line (which uses the HIP-event average of its own timed
+launches): each must agree within --tol (default 5 %).
+
+Usage: check_roofline.py <bench.json> <kernel_stats.csv> [--pmc profiles/pmc_shadow.json]"""
+import argparse
+import csv
+import json
+import sys
+
+HBM_PEAK_GBS = 8000.0
+VALU_ISSUE_PEAK_GIPS = 1024 * 2.4 / 2.0
+IMAGE_OF = {"shadow": "vx_main_rt_kernel", "path": "vx_main_pt_kernel", "flat": "vx_main_rt_flat"}
+
+
+def load_line(path):
+    d = json.load(open(path))
+    return d.get("parsed", d)
+
+
+def mode_of(line):
+    m = line["metric"]
+    return "path" if "path trace" in m else ("flat" if "flat" in m else "shadow")
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("bench")
+    ap.add_argument("stats")
+    ap.add_argument("--pmc", default=None)
+    ap.add_argument("--tol", type=float, default=0.05)
+    a = ap.parse_args()
+    line = load_line(a.bench)
+    mode = mode_of(line)
+    kname = IMAGE_OF[mode]
+    rows = {r["Name"]: r for r in csv.DictReader(open(a.stats))}
+    if kname not in rows:
+        sys.exit(f"{kname} not in {a.stats} (names: {sorted(rows)})")
+    row = rows[kname]
+    dur_s = float(row["AverageNs"]) * 1e-9
+    pmc = json.load(open(a.pmc or f"profiles/pmc_{mode}.json"))
+    rf = line["roofline"]
+    out = {"kernel": kname, "rocprof_calls": int(row["Calls"]), "rocprof_avg_ms": round(dur_s * 1e3, 5),
+           "line_kernel_ms": line["config"]["kernel_ms"], "checks": {}}
+    ok = True
+
+    def check(name, mine, theirs):
+        nonlocal ok
+        rel = abs(mine - theirs) / theirs if theirs else float("inf")
+        good = rel <= a.tol
+        ok &= good
+        out["checks"][name] = {"recomputed": round(mine, 4), "line": theirs, "rel_diff": round(rel, 4),
+                               "ok": good}
+
+    if mode != "flat":
+        check("roofline.frac", rf["algorithmic_bytes_per_launch"] / dur_s / 1e9 / HBM_PEAK_GBS, rf["frac"])
+    if rf.get("measured_hbm_frac") is not None:
+        check("roofline.measured_hbm_frac", pmc["traffic_bytes"] / dur_s / 1e9 / HBM_PEAK_GBS,
+              rf["measured_hbm_frac"])
+    issue = line.get("roofline_issue") or (rf if rf.get("bound") == "valu_issue" else None)
+    if issue is not None and issue.get("frac") is not None:
+        check("roofline_issue.frac", pmc["sq"]["SQ_INSTS_VALU"] / dur_s / 1e9 / VALU_ISSUE_PEAK_GIPS,
+              issue["frac"])
+    out["ok"] = ok
+    print(json.dumps(out, indent=1))
+    sys.exit(0 if ok else 1)
+
+
+if __name__ == "__main__":
+    main()

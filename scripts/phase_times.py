@@ -6,7 +6,7 @@ import sys
 
 PH = ["bounds", "morton"] + [f"{p}{i}" for i in range(4) for p in ("hist", "scan", "scatter")] + \
      ["tree", "boxes", "emit"]
-rows = [r for r in csv.DictReader(open(sys.argv[1])) if r["Kernel_Name"] == "vx_main"]
+rows = [r for r in csv.DictReader(open(sys.argv[1])) if r["Kernel_Name"] == "vx_main_bvh_build"]
 rows.sort(key=lambda r: int(r["Start_Timestamp"]))
 last = rows[-17:]
 for name, r in zip(PH, last):

@@ -1,14 +1,20 @@
 #!/usr/bin/env python3
 """Reduce the rocprofv3 --pmc passes of scripts/pmc_profile.sh for one mode to
 the record bench.py reports (profiles/pmc_<mode>.json): per-launch means over
-the vx_main dispatches of every counter, HBM traffic and derived ratios.
+the dispatches of the timed image's own entry (vx_main_<image>: the setup
+and instrumented launches of the same process are other kernels) of every
+counter, HBM traffic and derived ratios.
 
-HBM correction (MI355X_MICROARCH.md, HBM section): on gfx950 FETCH_SIZE counts
-64 B per 128-B memory-side read request, i.e. half of the bytes of a wide
-coalesced read, so the read side is doubled; WRITE_SIZE is taken as is.  Both
-are in KB.  SQ_WAVE_CYCLES / SQ_WAIT_* / SQ_ACTIVE_INST_* count quad-cycles
-(summed over waves), so their ratios are what is meaningful.
-Usage: pmc_profile.py <tag_dir> <mode> <side> <kernel .co> <out.json>"""
+HBM bytes, calibrated on known-byte probes (scripts/pmc_calibrate.sh ->
+profiles/r03/pmc_calibration.json): FETCH_SIZE counts a 16-B/lane vector read
+at half its bytes (x2, as MI355X_MICROARCH.md says) but a 64-B s_load_dwordx16
+record read at its bytes (x1); WRITE_SIZE counts the 4-B/lane framebuffer
+stores at their bytes (x1).  The RT kernels read through both paths and the
+memory-side counter cannot tell them apart, so the read side is reported as
+bounds [FETCH x1, FETCH x2] and `traffic_bytes` is the upper bound.  SQ_WAVE_CYCLES
+/ SQ_WAIT_* / SQ_ACTIVE_INST_* count quad-cycles (summed over waves), so their
+ratios are what is meaningful.
+Usage: pmc_profile.py <tag_dir> <mode> <side> <kernel .co> <out.json> [kernel name]"""
 import csv
 import glob
 import hashlib
@@ -18,13 +24,13 @@ import sys
 from collections import defaultdict
 
 
-def means(d):
-    """counter -> mean over dispatches of vx_main (values summed per dispatch)."""
+def means(d, kname):
+    """counter -> mean over dispatches of kernel `kname` (values summed per dispatch)."""
     per = defaultdict(lambda: defaultdict(float))
     for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
         with open(f) as fh:
             for row in csv.DictReader(fh):
-                if row["Kernel_Name"] != "vx_main":
+                if row["Kernel_Name"] != kname:
                     continue
                 per[row["Counter_Name"]][row["Dispatch_Id"]] += float(row["Counter_Value"])
     return {c: sum(v.values()) / len(v) for c, v in per.items() if v}, \
@@ -33,15 +39,17 @@ def means(d):
 
 def main():
     tag, mode, side, co, out = sys.argv[1:6]
+    image = os.path.splitext(os.path.basename(co))[0]
+    kname = sys.argv[6] if len(sys.argv) > 6 else f"vx_main_{image}"
     side = int(side)
     m, nd = {}, {}
     for d in sorted(glob.glob(os.path.join(tag, f"{mode}_*"))):
         if os.path.isdir(d):
-            a, b = means(d)
+            a, b = means(d, kname)
             m.update(a)
             nd.update(b)
     if "FETCH_SIZE" not in m or "WRITE_SIZE" not in m:
-        sys.exit("no vx_main dispatches with FETCH_SIZE / WRITE_SIZE")
+        sys.exit(f"no {kname} dispatches with FETCH_SIZE / WRITE_SIZE")
     g = m.get
     der = {}
     wc = g("SQ_WAVE_CYCLES")
@@ -65,14 +73,19 @@ def main():
     if g("TCP_TOTAL_CACHE_ACCESSES_sum") and g("TCP_TCC_READ_REQ_sum") is not None:
         der["l1_hit_rate"] = round(1.0 - m["TCP_TCC_READ_REQ_sum"] / m["TCP_TOTAL_CACHE_ACCESSES_sum"], 4)
     f_kb, w_kb = m["FETCH_SIZE"], m["WRITE_SIZE"]
+    lo, hi = int(f_kb * 1024 + w_kb * 1024), int(2 * f_kb * 1024 + w_kb * 1024)
     res = {
-        "kernel": "vx_main", "mode": mode, "width": side, "height": side,
+        "kernel": kname, "mode": mode, "width": side, "height": side,
         "kernel_image": os.path.basename(co),
         "kernel_md5": hashlib.md5(open(co, "rb").read()).hexdigest(),
         "dispatches": nd,
         "fetch_size_kb": round(f_kb, 1), "write_size_kb": round(w_kb, 1),
-        "correction": "read bytes = 2 x FETCH_SIZE x 1024 (gfx950 half-count), write = WRITE_SIZE x 1024",
-        "traffic_bytes": int(2 * f_kb * 1024 + w_kb * 1024),
+        "correction": ("calibrated (profiles/r03/pmc_calibration.json): reads FETCH_SIZE x1024 x1 "
+                       "(s_load records) .. x2 (16-B/lane vector loads), writes WRITE_SIZE x1024 x1 "
+                       "(4-B/lane stores)"),
+        "traffic_calibrated": True,
+        "traffic_bounds": [lo, hi],
+        "traffic_bytes": hi,
         "sq": {k: round(v, 1) for k, v in sorted(m.items()) if k not in ("FETCH_SIZE", "WRITE_SIZE")},
         "derived": der,
         "source": "scripts/pmc_profile.sh (rocprofv3 --pmc, one pass per counter group)",

@@ -3,7 +3,8 @@
 # that name the binding resource, one --pmc pass per counter group within the
 # per-block limits (8 SQ, 4 TCC, 4 TCP, 2 GRBM), each over
 # scripts/prof_rt.py (the product configuration: counters off), reduced by
-# scripts/pmc_profile.py into gpurun_out/$TAG/pmc_<mode>.json.
+# scripts/pmc_profile.py into gpurun_out/$TAG/pmc_<mode>.json over the timed
+# image's own entry (vx_main_<image>).
 # MODE = shadow (config 3, default), path (config 4) or flat (config 2).
 set -o pipefail
 cd "$GRAFT_REPO_ROOT"

@@ -11,7 +11,7 @@ from collections import defaultdict
 
 def main():
     root = sys.argv[1]
-    kname = sys.argv[2] if len(sys.argv) > 2 else "vx_main"
+    kname = sys.argv[2] if len(sys.argv) > 2 else "vx_main_rt_kernel"
     vals = defaultdict(list)
     for f in sorted(glob.glob(os.path.join(root, "*", "*counter_collection.csv"))):
         per = defaultdict(float)

@@ -68,7 +68,7 @@ def collect(outdir, passes, cmd, kernel, timeout):
         for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
             with open(f) as fh:
                 for row in csv.DictReader(fh):
-                    if row["Kernel_Name"] != kernel:
+                    if not row["Kernel_Name"].startswith(kernel):
                         continue
                     per[row["Counter_Name"]] += float(row["Counter_Value"])
                     n.add(row["Dispatch_Id"])
@@ -139,7 +139,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--class", dest="cls", type=int, default=int(os.environ.get("VORTEX_PROFILING", "1")),
                     choices=(0, 1, 2, 3, 4, 5))
-    ap.add_argument("--kernel", default="vx_main")
+    ap.add_argument("--kernel", default="vx_main", help="kernel name prefix (every image: vx_main_<image>)")
     ap.add_argument("--out", default="gpurun_out/vx_perf")
     ap.add_argument("--timeout", type=int, default=60)
     ap.add_argument("cmd", nargs=argparse.REMAINDER)

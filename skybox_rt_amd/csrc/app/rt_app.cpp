@@ -923,7 +923,7 @@ int rt_render_stats(rt_renderer_h r, rt_stats_t* st) {
   if (!r || !st) return fail("null argument");
   std::memset(st, 0, sizeof(*st));
   uint64_t v[RT_STAT_COUNT] = {};
-  for (int i = 0; i <= RT_STAT_BOUNCE; ++i)
+  for (int i = 0; i <= RT_STAT_EDGE_TESTS; ++i)
     if (vx_mpm_query(r->dev, VX_CSR_MPM_BASE + RT_MPM_USER + i, 0, &v[i]) != 0)
       return fail("vx_mpm_query failed");
   st->primary_rays = v[RT_STAT_PRIMARY];
@@ -936,6 +936,8 @@ int rt_render_stats(rt_renderer_h r, rt_stats_t* st) {
   st->shaded = v[RT_STAT_SHADED];
   st->texel_bytes = v[RT_STAT_TEXEL_BYTES];
   st->bounce_rays = v[RT_STAT_BOUNCE];
+  st->rect_tests = v[RT_STAT_RECT_TESTS];
+  st->edge_tests = v[RT_STAT_EDGE_TESTS];
   vx_mpm_query(r->dev, VX_CSR_MINSTRET, 0, &st->tasks);
   uint64_t ns = 0;
   vx_mpm_query(r->dev, VX_CSR_MCYCLE, 0, &ns);

@@ -67,7 +67,7 @@
 enum {
   RT_STAT_PRIMARY = 0, RT_STAT_SHADOW, RT_STAT_HITS, RT_STAT_OCCLUDED,
   RT_STAT_NODE_VISITS, RT_STAT_TRI_TESTS, RT_STAT_LAYER_TESTS, RT_STAT_SHADED,
-  RT_STAT_TEXEL_BYTES, RT_STAT_BOUNCE, RT_STAT_COUNT = 16
+  RT_STAT_TEXEL_BYTES, RT_STAT_BOUNCE, RT_STAT_RECT_TESTS, RT_STAT_EDGE_TESTS, RT_STAT_COUNT = 16
 };
 
 // rt_node_t: 4 x float4 =

@@ -234,11 +234,17 @@ __device__ __forceinline__ void flat_chunk(const vx_task_t& task, bool valid, co
     for (int j = 0; j < kFlatUnroll; ++j) C[j] = flat_rec(S, lds, k + j, 2);
     uint32_t cand = 0u;
     bool inr[kFlatUnroll];
+#ifdef RT_INSTRUMENT
+    cnt.rect_tests += lane == 0 ? (uint32_t)kFlatUnroll : 0u;
+#endif
 #pragma unroll
     for (int j = 0; j < kFlatUnroll; ++j) {
       inr[j] = rect2_in(C[j].y, C[j].z, pp);
       cand |= mask_ueq(rect2_clamp(C[j].y, C[j].z, pp), pp) ? 1u << j : 0u;
     }
+#ifdef RT_INSTRUMENT
+    cnt.edge_tests += lane == 0 ? (uint32_t)__popc(cand) : 0u;
+#endif
 #pragma unroll
     for (int j = 0; j < kFlatUnroll; ++j)
       if ((cand >> j) & 1u)  // wave-uniform
@@ -248,7 +254,13 @@ __device__ __forceinline__ void flat_chunk(const vx_task_t& task, bool valid, co
   for (; k < k1; ++k) {
     const uint4 C = flat_rec(S, lds, k, 2);
     const bool inr = rect2_in(C.y, C.z, pp);
+#ifdef RT_INSTRUMENT
+    cnt.rect_tests += lane == 0 ? 1u : 0u;
+#endif
     if (__ballot(inr) == 0) continue;  // wave-uniform skip
+#ifdef RT_INSTRUMENT
+    cnt.edge_tests += lane == 0 ? 1u : 0u;
+#endif
     vis_test_in(flat_rec(S, lds, k, 0), flat_rec(S, lds, k, 1), C, flat_rec(S, lds, k, 3), inr, px,
                 y, tie_high, bz, bp);
   }
@@ -375,6 +387,10 @@ VX_MAIN(rt_kernel_arg_t, arg, RT_BLOCK_THREADS) {
   flush(RT_STAT_LAYER_TESTS, cnt.layer_tests);
   flush(RT_STAT_SHADED, cnt.shaded);
   flush(RT_STAT_TEXEL_BYTES, cnt.texel_bytes);
+#if RT_FLAT
+  flush(RT_STAT_RECT_TESTS, cnt.rect_tests);
+  flush(RT_STAT_EDGE_TESTS, cnt.edge_tests);
+#endif
 #endif
   return rc;
 }

@@ -35,6 +35,7 @@ struct Counters {
   uint32_t primary = 0, shadow = 0, hits = 0, occluded = 0, bounce = 0;
 #ifdef RT_INSTRUMENT
   uint32_t visits = 0, tests = 0, layer_tests = 0, shaded = 0, texel_bytes = 0;
+  uint32_t rect_tests = 0, edge_tests = 0;  // flat image: work executed per wave
 #endif
 };
 

@@ -80,7 +80,8 @@ class Stats(C.Structure):
         "primary_rays", "shadow_rays", "geometry_hits", "occluded", "node_visits",
         "tri_tests", "layer_tests", "shaded", "texel_bytes", "tasks")] + [
         ("kernel_ms", C.c_double), ("grid", C.c_uint32), ("block", C.c_uint32),
-        ("num_tasks", C.c_uint32), ("local_tiles", C.c_uint32), ("bounce_rays", C.c_uint64)]
+        ("num_tasks", C.c_uint32), ("local_tiles", C.c_uint32), ("bounce_rays", C.c_uint64),
+        ("rect_tests", C.c_uint64), ("edge_tests", C.c_uint64)]
 
     def as_dict(self):
         return {n: getattr(self, n) for n, _ in self._fields_}
