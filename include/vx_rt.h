@@ -197,7 +197,8 @@ typedef struct {
   double configure_ms;    /* host wall time of the whole rt_renderer_configure */
   uint64_t blist_entries; /* candidate-list entries (0 when not built) */
   uint32_t blist_max;     /* the longest list */
-  uint32_t pad;
+  uint32_t slist_on;      /* 1: shadow rays test the light-space lists (rt_common.h) */
+  uint64_t slist_entries; /* light-space shadow list entries */
 } rt_setup_stats_t;
 int rt_renderer_setup_stats(rt_renderer_h r, rt_setup_stats_t* stats);
 
@@ -216,6 +217,8 @@ int rt_renderer_setup_stats(rt_renderer_h r, rt_setup_stats_t* stats);
 #define RT_REC_GEOM 9u      /* rt_tri_t per geometry primitive */
 #define RT_REC_BIDX 10u     /* uint32[2] per local 8x8 block: first list entry, count */
 #define RT_REC_BLIST 11u    /* rt_bentry_t per list entry (+2 padding entries) */
+#define RT_REC_SIDX 12u     /* uint32[2] per light-space cell: first entry, count */
+#define RT_REC_SLIST 13u    /* rt_tri_t per light-space list entry (+1 padding record) */
 int rt_renderer_export_records(rt_renderer_h r, uint32_t which, void* out, uint64_t bytes,
                                uint64_t* size);
 

@@ -98,6 +98,8 @@ typedef struct {
   uint32_t vis_lists;               /* BVH mode: 1 = primary visibility from the per-8x8-block
                                        candidate lists (rt_app.cpp build_block_lists, the
                                        kernels' block_primary) */
+  uint32_t shadow_lists;            /* primary+shadow: shadow rays test the light-space cell
+                                       lists (rt.c sl_build, the kernels' occluded_list) */
 } orc_rt_params_t;
 
 #define ORC_RT_SHADOWS 0x1u
@@ -156,6 +158,13 @@ int orc_vis_prims(const orc_scene_t* scene, uint32_t width, uint32_t height, uin
  * bound); NULL arrays: sizes only. */
 int orc_vis_block_lists(const orc_scene_t* scene, uint32_t width, uint32_t height, uint32_t shard_index,
                         uint32_t shard_count, uint32_t* idx, uint32_t* ent, uint64_t* total, uint32_t* nlb);
+
+/* The light-space shadow lists for a point light (rt.c sl_build; the device
+ * build rt_setup.hip SCOUNT .. SSORT): idx [6 * 128 * 128][2] (first entry,
+ * count; cell = (face * 128 + cy) * 128 + cx), ent [total] geometry indices
+ * (ascending within a cell); NULL arrays: total only. */
+int orc_shadow_lists(const orc_scene_t* scene, const float light[3], uint32_t* idx, int32_t* ent,
+                     uint64_t* total);
 
 /* Möller–Trumbore as used by both sides (exposed for unit tests). */
 int orc_mt(const float o[3], const float d[3], const float v0[3],

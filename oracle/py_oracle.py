@@ -52,7 +52,8 @@ class RtParamsC(C.Structure):
                 ("light", C.c_float * 3), ("clear_color", C.c_uint32),
                 ("bounces", C.c_uint32), ("seed", C.c_uint32), ("nthreads", C.c_uint32),
                 ("row_begin", C.c_uint32), ("row_end", C.c_uint32), ("row_step", C.c_uint32),
-                ("vis_per_lane", C.c_uint32), ("vis_lists", C.c_uint32)]
+                ("vis_per_lane", C.c_uint32), ("vis_lists", C.c_uint32),
+                ("shadow_lists", C.c_uint32)]
 
 
 class RtCountersC(C.Structure):
@@ -197,14 +198,38 @@ def vis_block_lists(oscene: OracleScene, width: int, height: int, shard_index: i
     return idx[:nlb.value], ent[:tot.value]
 
 
+SL_N = 128
+
+
+def shadow_lists(oscene: OracleScene, light=(0.0, 60.0, 80.0)):
+    """The light-space shadow lists (oracle/rt.c orc_shadow_lists) -> (idx
+    uint32[6*128*128, 2]: first entry, count; ent int32[total]: geometry
+    indices, ascending within a cell)."""
+    L = (C.c_float * 3)(*[float(np.float32(x)) for x in light])
+    tot = C.c_uint64()
+    lib().orc_shadow_lists.argtypes = [C.POINTER(SceneC), C.c_void_p, C.c_void_p, C.c_void_p,
+                                       C.POINTER(C.c_uint64)]
+    rc = lib().orc_shadow_lists(C.byref(oscene.c), L, None, None, C.byref(tot))
+    if rc != 0:
+        raise RuntimeError(f"orc_shadow_lists failed: {rc}")
+    idx = np.zeros((6 * SL_N * SL_N, 2), np.uint32)
+    ent = np.zeros(max(tot.value, 1), np.int32)
+    lib().orc_shadow_lists(C.byref(oscene.c), L, idx.ctypes.data, ent.ctypes.data, C.byref(tot))
+    return idx, ent[:tot.value]
+
+
 def rt_params(width, height, shadows=True, light=(0.0, 60.0, 80.0), nthreads=1,
               clear_color=CLEAR_COLOR, row_begin=0, row_end=0, row_step=0,
-              path=False, bounces=4, seed=PT_SEED, vis_per_lane=False, vis_lists=None):
+              path=False, bounces=4, seed=PT_SEED, vis_per_lane=False, vis_lists=None,
+              shadow_lists=None):
     p = RtParamsC()
     p.vis_per_lane = 1 if vis_per_lane else 0
     # the product resolves primary visibility from per-block candidate lists
     # (its default, primary+shadow and path frames)
     p.vis_lists = (0 if vis_per_lane else 1) if vis_lists is None else int(bool(vis_lists))
+    # the product's shadow rays of primary+shadow frames test the light-space
+    # lists (its default with the device setup)
+    p.shadow_lists = int(bool(shadows and not path) if shadow_lists is None else bool(shadow_lists))
     p.width, p.height = width, height
     p.flags = (RT_SHADOWS if shadows else 0) | (RT_PATH if path else 0)
     p.bounces, p.seed = bounces, seed

@@ -81,6 +81,8 @@ typedef struct {
   uint32_t* bl_idx;               /* vis_lists: per 8x8 block (first entry, count) */
   uint32_t* bl_ent;               /* per entry: geometry pid, suffix union rx, ry */
   uint32_t bl_nbx;
+  uint32_t* sl_idx;               /* shadow_lists: per light-space cell (first entry, count) */
+  int32_t* sl_ent;                /* per entry: geometry index (c->geom) */
   int32_t* vpids;                 /* its leaf records' pids */
   uint32_t num_vnodes;
   int32_t* vhit;                  /* [W*H] primary winner per pixel (packet pre-pass) */
@@ -153,6 +155,7 @@ static int rt_prepare(rt_ctx_t* c, const orc_scene_t* s, const orc_rt_params_t* 
 static void rt_release(rt_ctx_t* c) {
   free(c->rp); free(c->rp_ok); free(c->prim_dc); free(c->tri); free(c->geom); free(c->dcst);
   free(c->bl_idx); free(c->bl_ent);
+  free(c->sl_idx); free(c->sl_ent);
   free(c->vis); free(c->vnodes); free(c->vpids); free(c->vhit);
   pthread_mutex_destroy(&c->mu);
 }
@@ -792,6 +795,202 @@ static uint32_t path_trace(const rt_ctx_t* c, uint32_t px, const float d0[3], fl
   return (alb0 & 0xff000000u) | (pt_to8(L[0]) << 16) | (pt_to8(L[1]) << 8) | pt_to8(L[2]);
 }
 
+/* ---- light-space shadow lists (the kernels' occluded_list; built on the
+ * device by rt_setup.hip SCOUNT .. SSORT).  Every shadow segment ends at the
+ * one point light, so a ray is identified by its direction from the light,
+ * u = P - L.  The directions are binned on the 6 faces of a cube around the
+ * light (face 2k + (u_k < 0) for the dominant axis k, face coordinates
+ * u_i / |u_k|, u_j / |u_k| in [-1, 1], SL_N x SL_N cells); a cell's list holds
+ * every geometry triangle whose projection from the light reaches the cell:
+ * the triangle clipped to the face's frustum widened by SL_EPS, its projected
+ * polygon's box widened by SL_EPS, then a separating-axis test against the
+ * cell widened by SL_EPS.  Conservative: a triangle MT accepts for a ray meets
+ * the ray's direction, which lies in the ray's cell, and the widening covers
+ * fp32 rounding; the lists only narrow the candidates -- a ray's verdict is
+ * the brute-force any-hit's.  A ray tests its cell's list in ascending
+ * geometry index until the first occluder.  All arithmetic fp32, no
+ * contraction, the device's operation order. */
+#define SL_N 128
+#define SL_EPS (1.0f / 512.0f)
+#define SL_CELLS (6 * SL_N * SL_N)
+static const int sl_ax[3][2] = {{1, 2}, {0, 2}, {0, 1}};
+
+static int sl_clip_plane(float in[][3], int n, int k, float s, int m, float sg, float out[][3]) {
+  const float ke = 1.0f + SL_EPS;
+  int o = 0;
+  for (int q = 0; q < n; ++q) {
+    const float* a = in[q];
+    const float* b = in[(q + 1) % n];
+    const float da = (s * a[k]) * ke - sg * a[m], db = (s * b[k]) * ke - sg * b[m];
+    if (da >= 0.0f) { out[o][0] = a[0]; out[o][1] = a[1]; out[o][2] = a[2]; ++o; }
+    if ((da >= 0.0f) != (db >= 0.0f)) {
+      const float tq = da / (da - db);
+      for (int cc = 0; cc < 3; ++cc) out[o][cc] = a[cc] + (b[cc] - a[cc]) * tq;
+      ++o;
+    }
+  }
+  return o;
+}
+
+/* triangle t9 (v0, e1, e2) on face f: projected polygon (pu, pv, n) and cell
+ * range; returns 0 when the face holds none of it, 2 when the polygon reaches
+ * the light (every cell of the face, no separating-axis test) */
+static int sl_project(const float* t9, const float L[3], int f, float pu[8], float pv[8], int* n,
+                      int rng[4]) {
+  const int k = f >> 1, i = sl_ax[k][0], j = sl_ax[k][1];
+  const float s = (f & 1) ? -1.0f : 1.0f;
+  float A[8][3], B[8][3];
+  for (int cc = 0; cc < 3; ++cc) {
+    A[0][cc] = t9[cc] - L[cc];
+    A[1][cc] = (t9[cc] + t9[3 + cc]) - L[cc];
+    A[2][cc] = (t9[cc] + t9[6 + cc]) - L[cc];
+  }
+  int m = 3;
+  m = sl_clip_plane(A, m, k, s, i, 1.0f, B);
+  if (m) m = sl_clip_plane(B, m, k, s, i, -1.0f, A);
+  if (m) m = sl_clip_plane(A, m, k, s, j, 1.0f, B);
+  if (m) m = sl_clip_plane(B, m, k, s, j, -1.0f, A);
+  if (!m) return 0;
+  const float hn = (float)SL_N * 0.5f;
+  for (int q = 0; q < m; ++q)
+    if (!(s * A[q][k] > 0.0f)) {
+      rng[0] = 0; rng[1] = SL_N - 1; rng[2] = 0; rng[3] = SL_N - 1;
+      *n = 0;
+      return 2;
+    }
+  float u0 = 0, u1 = 0, v0 = 0, v1 = 0;
+  for (int q = 0; q < m; ++q) {
+    const float ck = s * A[q][k];
+    pu[q] = A[q][i] / ck;
+    pv[q] = A[q][j] / ck;
+    if (q == 0 || pu[q] < u0) u0 = pu[q];
+    if (q == 0 || pu[q] > u1) u1 = pu[q];
+    if (q == 0 || pv[q] < v0) v0 = pv[q];
+    if (q == 0 || pv[q] > v1) v1 = pv[q];
+  }
+  *n = m;
+  int x0 = (int)floorf(((u0 - SL_EPS) + 1.0f) * hn), x1 = (int)floorf(((u1 + SL_EPS) + 1.0f) * hn);
+  int y0 = (int)floorf(((v0 - SL_EPS) + 1.0f) * hn), y1 = (int)floorf(((v1 + SL_EPS) + 1.0f) * hn);
+  if (x0 < 0) x0 = 0;
+  if (y0 < 0) y0 = 0;
+  if (x1 > SL_N - 1) x1 = SL_N - 1;
+  if (y1 > SL_N - 1) y1 = SL_N - 1;
+  rng[0] = x0; rng[1] = x1; rng[2] = y0; rng[3] = y1;
+  return x0 <= x1 && y0 <= y1;
+}
+
+/* separating-axis test of the projected polygon against cell (cx, cy)
+ * widened by SL_EPS (the box axes are the cell range's) */
+static int sl_cell_meets(const float* pu, const float* pv, int n, int cx, int cy) {
+  if (n < 3) return 1;
+  const float cw = 2.0f / (float)SL_N;
+  const float rx0 = ((float)cx * cw - 1.0f) - SL_EPS, rx1 = ((float)(cx + 1) * cw - 1.0f) + SL_EPS;
+  const float ry0 = ((float)cy * cw - 1.0f) - SL_EPS, ry1 = ((float)(cy + 1) * cw - 1.0f) + SL_EPS;
+  for (int a = 0; a < n; ++a) {
+    const int b = a + 1 < n ? a + 1 : 0;
+    const float nx = pv[b] - pv[a], ny = pu[a] - pu[b];
+    float p0 = 0, p1 = 0;
+    for (int q = 0; q < n; ++q) {
+      const float d = nx * pu[q] + ny * pv[q];
+      if (q == 0 || d < p0) p0 = d;
+      if (q == 0 || d > p1) p1 = d;
+    }
+    const float c0 = nx * rx0 + ny * ry0, c1 = nx * rx1 + ny * ry0;
+    const float c2 = nx * rx0 + ny * ry1, c3 = nx * rx1 + ny * ry1;
+    const float r0 = fminf(fminf(c0, c1), fminf(c2, c3)), r1 = fmaxf(fmaxf(c0, c1), fmaxf(c2, c3));
+    if (p1 < r0 || p0 > r1) return 0;
+  }
+  return 1;
+}
+
+/* every (cell, geometry index) pair, in (k, face, cy, cx) order: count (ent
+ * NULL) or fill at the cells' cursors */
+static void sl_pairs(const rt_ctx_t* c, const float L[3], uint32_t* cnt, uint32_t* cur, int32_t* ent) {
+  for (int k = 0; k < c->num_geom; ++k) {
+    const float* t9 = c->tri + (size_t)c->geom[k] * 9;
+    for (int f = 0; f < 6; ++f) {
+      float pu[8], pv[8];
+      int n = 0, rng[4];
+      const int r = sl_project(t9, L, f, pu, pv, &n, rng);
+      if (!r) continue;
+      for (int cy = rng[2]; cy <= rng[3]; ++cy)
+        for (int cx = rng[0]; cx <= rng[1]; ++cx) {
+          if (r == 1 && !sl_cell_meets(pu, pv, n, cx, cy)) continue;
+          const uint32_t cell = ((uint32_t)f * SL_N + (uint32_t)cy) * SL_N + (uint32_t)cx;
+          if (ent) ent[cur[cell]++] = k;
+          else ++cnt[cell];
+        }
+    }
+  }
+}
+
+static void sl_build(rt_ctx_t* c) {
+  uint32_t* cnt = (uint32_t*)calloc(SL_CELLS, sizeof(uint32_t));
+  sl_pairs(c, c->p.light, cnt, NULL, NULL);
+  c->sl_idx = (uint32_t*)malloc(sizeof(uint32_t) * 2 * SL_CELLS);
+  uint32_t* cur = (uint32_t*)malloc(sizeof(uint32_t) * SL_CELLS);
+  uint64_t tot = 0;
+  for (uint32_t i = 0; i < SL_CELLS; ++i) {
+    c->sl_idx[2 * i] = (uint32_t)tot;
+    c->sl_idx[2 * i + 1] = cnt[i];
+    cur[i] = (uint32_t)tot;
+    tot += cnt[i];
+  }
+  c->sl_ent = (int32_t*)malloc(sizeof(int32_t) * (tot ? tot : 1));
+  sl_pairs(c, c->p.light, NULL, cur, c->sl_ent);  /* ascending k within each cell */
+  free(cnt);
+  free(cur);
+}
+
+/* the ray's cell: dominant axis of u = -sd (ties to the lower axis) */
+static uint32_t sl_cell_of(const float sd[3]) {
+  const float u[3] = {-sd[0], -sd[1], -sd[2]};
+  int k = 0;
+  float m = fabsf(u[0]);
+  if (fabsf(u[1]) > m) { k = 1; m = fabsf(u[1]); }
+  if (fabsf(u[2]) > m) { k = 2; m = fabsf(u[2]); }
+  if (!(m > 0.0f)) return 0;
+  const int f = 2 * k + (u[k] < 0.0f ? 1 : 0);
+  const float hn = (float)SL_N * 0.5f;
+  int cx = (int)floorf((u[sl_ax[k][0]] / m + 1.0f) * hn), cy = (int)floorf((u[sl_ax[k][1]] / m + 1.0f) * hn);
+  cx = cx < 0 ? 0 : (cx > SL_N - 1 ? SL_N - 1 : cx);
+  cy = cy < 0 ? 0 : (cy > SL_N - 1 ? SL_N - 1 : cy);
+  return ((uint32_t)f * SL_N + (uint32_t)cy) * SL_N + (uint32_t)cx;
+}
+
+/* any-hit over the ray's cell list (t in (0, 1), skip excluded): 1 = occluded */
+static int sl_occluded(const rt_ctx_t* c, const float so[3], const float sd[3], int skip, uint64_t* tests) {
+  const uint32_t cell = sl_cell_of(sd);
+  const uint32_t o = c->sl_idx[2 * cell], n = c->sl_idx[2 * cell + 1];
+  for (uint32_t q = 0; q < n; ++q) {
+    const int g = c->geom[c->sl_ent[o + q]];
+    ++*tests;
+    const float* t9 = c->tri + (size_t)g * 9;
+    float t;
+    if (g != skip && mt_hit(so, sd, t9, t9 + 3, t9 + 6, 0.0f, &t) && t < 1.0f) return 1;
+  }
+  return 0;
+}
+
+int orc_shadow_lists(const orc_scene_t* scene, const float light[3], uint32_t* idx, int32_t* ent,
+                     uint64_t* total) {
+  if (!scene || !light) return -1;
+  orc_rt_params_t p;
+  memset(&p, 0, sizeof(p));
+  p.width = p.height = 64;
+  for (int i = 0; i < 3; ++i) p.light[i] = light[i];
+  rt_ctx_t c;
+  int err = rt_prepare(&c, scene, &p);
+  if (err) { rt_release(&c); return err; }
+  sl_build(&c);
+  const uint64_t tot = (uint64_t)c.sl_idx[2 * (SL_CELLS - 1)] + c.sl_idx[2 * (SL_CELLS - 1) + 1];
+  if (idx) memcpy(idx, c.sl_idx, sizeof(uint32_t) * 2 * SL_CELLS);
+  if (ent) memcpy(ent, c.sl_ent, sizeof(int32_t) * tot);
+  if (total) *total = tot;
+  rt_release(&c);
+  return 0;
+}
+
 static void rt_row(rt_ctx_t* c, uint32_t y, orc_rt_counters_t* k) {
   const orc_scene_t* s = c->scene;
   const uint32_t W = c->p.width;
@@ -823,7 +1022,8 @@ static void rt_row(rt_ctx_t* c, uint32_t y, orc_rt_counters_t* k) {
         const float sd[3] = {c->p.light[0] - so[0], c->p.light[1] - so[1], c->p.light[2] - so[2]};
         float ts;
         ++k->shadow_rays;
-        const int occ = c->bvh ? bvh_trace(c, so, sd, 0.0f, 1.0f, 1, hit, &ts, &k->node_visits, &k->tri_tests)
+        const int occ = c->sl_idx ? (sl_occluded(c, so, sd, hit, &k->tri_tests) ? 0 : -1)
+                      : c->bvh ? bvh_trace(c, so, sd, 0.0f, 1.0f, 1, hit, &ts, &k->node_visits, &k->tri_tests)
                                : brute_trace(c, so, sd, 0.0f, 1.0f, 1, hit, &ts, &k->tri_tests);
         if (occ >= 0) { ++k->occluded; col = shadow_attenuate(col); }
       }
@@ -883,6 +1083,7 @@ static int rt_run(const orc_scene_t* scene, const orc_bvh_t* bvh, const orc_rt_p
   if (err) { rt_release(&c); return err; }
   c.bvh = bvh;
   vis_build_nodes(&c);
+  if (p->shadow_lists && !(p->flags & ORC_RT_PATH) && (p->flags & ORC_RT_SHADOWS)) sl_build(&c);
   c.color = color; c.pid = pid; c.tout = t;
   const uint32_t nt = p->nthreads > 1 ? p->nthreads : 1;
   if (bvh && !p->vis_per_lane && p->row_begin == 0 && p->row_end == 0 && p->row_step <= 1) {

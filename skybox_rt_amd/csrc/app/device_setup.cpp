@@ -235,4 +235,55 @@ int device_setup(rt_renderer* r, bool raster, bool order_on, bool lists, uint32_
   return 0;
 }
 
+int shadow_lists(rt_renderer* r, uint32_t* launches) {
+  rt_kernel_arg_t& a = r->arg;
+  if (r->sl_built && std::memcmp(r->sl_light, a.light, sizeof(a.light)) == 0) {
+    r->setup.slist_entries = r->sl_entries;
+    return 0;
+  }
+  r->sl_built = false;
+  a.slist_on = 0;
+  const uint32_t cells = RT_SLIST_CELLS, nbpart = (cells + RTS_BLOCKS_PER_PART - 1) / RTS_BLOCKS_PER_PART;
+  const uint32_t zero4[4] = {0, 0, 0, 0};
+  DevBuf argb, status, cnt, part, tmp;
+  if (alloc_tmp(r, sizeof(rt_setup_arg_t), &argb) || alloc_tmp(r, sizeof(zero4), &status, zero4) ||
+      alloc_tmp(r, (uint64_t)cells * 4, &cnt) || alloc_tmp(r, (uint64_t)nbpart * 4, &part) ||
+      alloc(r, (uint64_t)cells * 8, &r->sidx, &a.sidx_addr))
+    return -1;
+  rt_setup_arg_t g;
+  base_arg(r, &g);
+  g.geom_addr = a.geom_addr;
+  g.status_addr = status.addr;
+  g.bcnt_addr = cnt.addr;
+  g.bpart_addr = part.addr;
+  g.bidx_addr = a.sidx_addr;
+  g.nblk = cells;
+  g.nbpart = nbpart;
+  for (int i = 0; i < 3; ++i) g.light[i] = a.light[i];
+  add_fill(&g, cnt.addr, cells, 0u);
+  for (uint32_t ph : {RTS_FILL, RTS_SCOUNT, RTS_BSUM, RTS_BSCAN, RTS_BOFF}) {
+    g.phases = ph;
+    if (run(r, &argb, g, launches) != 0) return -1;
+  }
+  uint32_t st[4];
+  if (vx_copy_from_dev(st, status.h, 0, sizeof(st)) != 0) return set_error("vx_copy_from_dev failed");
+  r->sl_entries = st[2];
+  r->setup.slist_entries = st[2];
+  if (!block_lists_fit(st[1], st[2])) return 0;  // the packet walk, as without lists
+  if (alloc_tmp(r, (uint64_t)st[2] * 4 + 4, &tmp) || alloc(r, ((uint64_t)st[2] + 1) * 48, &r->slist, &a.slist_addr))
+    return -1;
+  g.btmp_addr = tmp.addr;
+  g.slist_addr = a.slist_addr;
+  g.blist_entries = st[2];
+  g.nfills = 0;
+  for (uint32_t ph : {RTS_SFILL, RTS_SSORT}) {
+    g.phases = ph;
+    if (run(r, &argb, g, launches) != 0) return -1;
+  }
+  std::memcpy(r->sl_light, a.light, sizeof(a.light));
+  r->sl_built = true;
+  a.slist_on = 1;
+  return 0;
+}
+
 }  // namespace rtapp

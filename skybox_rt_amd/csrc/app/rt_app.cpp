@@ -415,6 +415,8 @@ int rt_renderer_export_records(rt_renderer_h r, uint32_t which, void* out, uint6
       b = a.blist_blocks ? r->blist : nullptr;
       n = (r->setup.blist_entries + 2) * sizeof(rt_bentry_t);
       break;
+    case RT_REC_SIDX: b = a.slist_on ? r->sidx : nullptr; n = (uint64_t)RT_SLIST_CELLS * 8; break;
+    case RT_REC_SLIST: b = a.slist_on ? r->slist : nullptr; n = (r->sl_entries + 1) * sizeof(rt_tri_t); break;
     default: return fail("unknown record array");
   }
   if (!b) return fail("record array not present in this configuration");
@@ -862,6 +864,17 @@ int rt_renderer_configure(rt_renderer_h r, const rt_render_params_t* p) {
   } else if (host_setup(r, p, raster, order_on, lists, &heavy) != 0) {
     return -1;
   }
+  // shadow rays of primary+shadow frames: light-space lists (built on the
+  // device for this light; env RT_SHADOW_LISTS=0 keeps the BVH packet walk;
+  // the host setup path walks the BVH)
+  a.slist_on = 0;
+  r->setup.slist_entries = 0;
+  const char* sle = std::getenv("RT_SHADOW_LISTS");
+  if (device && !raster && !(p->flags & (RT_RENDER_FLAT | RT_RENDER_PATH)) && (p->flags & RT_RENDER_SHADOWS) &&
+      a.num_geom > 0 && !(sle && std::atoi(sle) == 0)) {
+    if (rtapp::shadow_lists(r, &launches) != 0) return -1;
+    a.slist_on = r->sl_built ? 1u : 0u;
+  }
   const double setup_ms = ms_since(t1);
   if (order_on) {
     // path tracing: tiles that geometry covers (first in the order;
@@ -891,6 +904,7 @@ int rt_renderer_configure(rt_renderer_h r, const rt_render_params_t* p) {
   r->setup.launches = launches;
   r->setup.heavy_tiles = heavy;
   r->setup.blist_blocks = a.blist_blocks;
+  r->setup.slist_on = a.slist_on;
   r->setup.setup_ms = setup_ms;
   r->setup.configure_ms = ms_since(t0);
   r->configured = true;

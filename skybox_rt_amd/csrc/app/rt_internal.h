@@ -38,6 +38,10 @@ struct rt_renderer {
   vx_buffer_h order = nullptr;
   vx_buffer_h vnodes = nullptr, vtris = nullptr, vlayers = nullptr, vgeom = nullptr;
   vx_buffer_h blist = nullptr, bidx = nullptr;  // per-block candidate lists (rt_bentry_t)
+  vx_buffer_h sidx = nullptr, slist = nullptr;  // light-space shadow lists (built for sl_light)
+  float sl_light[3] = {0, 0, 0};
+  bool sl_built = false;
+  uint64_t sl_entries = 0;
   vx_buffer_h gather_recv = nullptr, gather_image = nullptr;  // rank 0 of rt_render_gather
   vx_buffer_h prims = nullptr, cbuf = nullptr, args = nullptr;
   // device-side setup (device_setup.cpp, kernels/rt_setup.hip): the image,
@@ -75,7 +79,7 @@ struct rt_renderer {
                            &ptris, &geom, &oms, &bbox, &zbuf, &order, &vnodes, &vtris, &vlayers,
                            &vgeom, &gather_recv, &gather_image, &prims, &cbuf, &args,
                            &setup_krnl, &verts, &pdc, &dcz, &layer_list, &geometry_list, &vis,
-                           &blist, &bidx};
+                           &blist, &bidx, &sidx, &slist};
     for (auto* b : bufs) {
       if (*b) vx_mem_free(*b);
       *b = nullptr;
@@ -116,6 +120,10 @@ int device_ingest(rt_renderer* r, bool records);
 // buffers and arg.blist_blocks; 0 when they do not fit, block_lists_fit)
 int device_setup(rt_renderer* r, bool raster, bool order_on, bool lists, uint32_t* heavy,
                  uint32_t* launches);
+// the light-space shadow lists for a.light (rt_common.h; rt_setup.hip
+// SCOUNT .. SSORT), kept while the light is unchanged: arg.slist_on /
+// sidx_addr / slist_addr (slist_on 0 when they do not fit)
+int shadow_lists(rt_renderer* r, uint32_t* launches);
 // whether lists with this longest list and this many entries are built
 // (RT_BLIST_MAX_LIST, the device sort's limit; env RT_BLIST_MAX_ENTRIES,
 // default 16 M entries = 512 MiB of list and sort buffers)

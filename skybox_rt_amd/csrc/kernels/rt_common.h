@@ -195,7 +195,27 @@ typedef struct {
   uint32_t blist_blocks;   // per-block candidate lists: local 8x8 blocks (local_tiles * 16), 0 = walk the tree
   uint64_t blist_addr;     // rt_bentry_t [entries + 2]: every local block's list, concatenated
   uint64_t bidx_addr;      // uint32[2] per local block lt * 16 + (by & 3) * 4 + (bx & 3): first entry, count
+  uint32_t slist_on;       // light-space shadow lists built for `light` (0: shadow rays walk the BVH)
+  uint32_t pad_sl;
+  uint64_t sidx_addr;      // uint32[2] per light-space cell: first entry, count
+  uint64_t slist_addr;     // rt_tri_t per entry (+1 padding record): every cell's triangles, ascending pid
 } rt_kernel_arg_t;
+
+// ---- light-space shadow lists (shadow rays to the point light) ------------
+// A shadow segment P -> L is identified by its direction from the light,
+// u = P - L, binned on the 6 faces of a cube around the light: face 2k +
+// (u_k < 0) for the dominant axis k (ties to the lower axis), face
+// coordinates (u_i, u_j) / |u_k| in [-1, 1] with (i, j) the other two axes in
+// order, RT_SLIST_N x RT_SLIST_N cells, cell = (face * N + cy) * N + cx.  A
+// cell's list holds every geometry triangle whose projection from the light
+// reaches it (clipped to the face frustum widened by RT_SLIST_EPS, polygon
+// box and separating-axis test against the cell widened by RT_SLIST_EPS):
+// conservative, so any-hit over the list is the brute force's verdict.
+// Built on the device (rt_setup.hip SCOUNT .. SSORT); oracle/rt.c sl_build
+// restates it.
+#define RT_SLIST_N 128
+#define RT_SLIST_EPS (1.0f / 512.0f)
+#define RT_SLIST_CELLS (6u * RT_SLIST_N * RT_SLIST_N)
 
 // ---- per-8x8-block candidate lists (primary visibility) -------------------
 // For every 8x8 pixel block of the shard's tiles (local block lb = local

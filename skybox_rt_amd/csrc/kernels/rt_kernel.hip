@@ -158,7 +158,10 @@ __device__ __forceinline__ void shadow_drain(bool final, const Scene& S, WaveLds
     cnt.shadow += active;
     uint32_t color = w.q_color[slot];
     float ts;
-    const bool occ = (RT_ONLY_BVH4H || (S.flags & RT_FLAG_BVH4H))
+    // the light-space lists when built (occluded_list), else the BVH: the
+    // binary16 BVH4 as one packet, other layouts per lane (deep images)
+    const bool occ = S.slist_on ? occluded_list(S, s, active, w.q_pid[slot], cnt)
+                     : (RT_ONLY_BVH4H || (S.flags & RT_FLAG_BVH4H))
                          ? occluded_packet(S, s, active, w.q_pid[slot], 1.0f, cnt)
                          : active && trace<true>(S, s, 0.0f, 1.0f, w.q_pid[slot], tie_high, &ts,
                                                  RT_WSTACK(w, lane), cnt) >= 0;

@@ -776,6 +776,159 @@ __device__ void phase_bsort(const rt_setup_arg_t* a) {
   }
 }
 
+// ---- light-space shadow lists (rt_common.h; oracle/rt.c sl_build restates
+// them operation for operation: fp32, no contraction, IEEE division)
+
+// clip polygon `in` (n vertices) to s * x_k * (1 + eps) - sg * x_m >= 0
+__device__ __forceinline__ int sl_clip_plane(const float (*in)[3], int n, int k, float s, int m, float sg,
+                                             float (*out)[3]) {
+  const float ke = 1.0f + RT_SLIST_EPS;
+  int o = 0;
+  for (int q = 0; q < n; ++q) {
+    const float* a = in[q];
+    const float* b = in[q + 1 < n ? q + 1 : 0];
+    const float da = (s * a[k]) * ke - sg * a[m], db = (s * b[k]) * ke - sg * b[m];
+    if (da >= 0.0f) { out[o][0] = a[0]; out[o][1] = a[1]; out[o][2] = a[2]; ++o; }
+    if ((da >= 0.0f) != (db >= 0.0f)) {
+      const float tq = da / (da - db);
+      for (int cc = 0; cc < 3; ++cc) out[o][cc] = a[cc] + (b[cc] - a[cc]) * tq;
+      ++o;
+    }
+  }
+  return o;
+}
+
+struct SlFace {
+  float pu[8], pv[8];
+  int n;         // polygon vertices (0 with whole = 1)
+  int whole;     // the polygon reaches the light: every cell, no separating-axis test
+  int x0, x1, y0, y1;
+};
+
+// geometry triangle (rt_tri_t record r) on face f; false: nothing on the face
+__device__ __noinline__ bool sl_project(const rt_tri_t& r, const float L[3], int f, SlFace* F) {
+  const int k = f >> 1, i = k == 0 ? 1 : 0, j = k == 2 ? 1 : 2;
+  const float s = (f & 1) ? -1.0f : 1.0f;
+  float A[8][3], B[8][3];
+  for (int cc = 0; cc < 3; ++cc) {
+    A[0][cc] = r.v[cc] - L[cc];
+    A[1][cc] = (r.v[cc] + r.v[4 + cc]) - L[cc];
+    A[2][cc] = (r.v[cc] + r.v[8 + cc]) - L[cc];
+  }
+  int m = 3;
+  m = sl_clip_plane(A, m, k, s, i, 1.0f, B);
+  if (m) m = sl_clip_plane(B, m, k, s, i, -1.0f, A);
+  if (m) m = sl_clip_plane(A, m, k, s, j, 1.0f, B);
+  if (m) m = sl_clip_plane(B, m, k, s, j, -1.0f, A);
+  if (!m) return false;
+  const float hn = (float)RT_SLIST_N * 0.5f;
+  F->whole = 0;
+  for (int q = 0; q < m; ++q)
+    if (!(s * A[q][k] > 0.0f)) F->whole = 1;
+  if (F->whole) {
+    F->n = 0;
+    F->x0 = F->y0 = 0;
+    F->x1 = F->y1 = RT_SLIST_N - 1;
+    return true;
+  }
+  float u0 = 0, u1 = 0, v0 = 0, v1 = 0;
+  for (int q = 0; q < m; ++q) {
+    const float ck = s * A[q][k];
+    F->pu[q] = A[q][i] / ck;
+    F->pv[q] = A[q][j] / ck;
+    if (q == 0 || F->pu[q] < u0) u0 = F->pu[q];
+    if (q == 0 || F->pu[q] > u1) u1 = F->pu[q];
+    if (q == 0 || F->pv[q] < v0) v0 = F->pv[q];
+    if (q == 0 || F->pv[q] > v1) v1 = F->pv[q];
+  }
+  F->n = m;
+  F->x0 = max((int)floorf(((u0 - RT_SLIST_EPS) + 1.0f) * hn), 0);
+  F->x1 = min((int)floorf(((u1 + RT_SLIST_EPS) + 1.0f) * hn), RT_SLIST_N - 1);
+  F->y0 = max((int)floorf(((v0 - RT_SLIST_EPS) + 1.0f) * hn), 0);
+  F->y1 = min((int)floorf(((v1 + RT_SLIST_EPS) + 1.0f) * hn), RT_SLIST_N - 1);
+  return F->x0 <= F->x1 && F->y0 <= F->y1;
+}
+
+// separating-axis test of the projected polygon against cell (cx, cy)
+// widened by RT_SLIST_EPS
+__device__ __forceinline__ bool sl_cell_meets(const SlFace& F, int cx, int cy) {
+  if (F.n < 3) return true;
+  const float cw = 2.0f / (float)RT_SLIST_N;
+  const float rx0 = ((float)cx * cw - 1.0f) - RT_SLIST_EPS, rx1 = ((float)(cx + 1) * cw - 1.0f) + RT_SLIST_EPS;
+  const float ry0 = ((float)cy * cw - 1.0f) - RT_SLIST_EPS, ry1 = ((float)(cy + 1) * cw - 1.0f) + RT_SLIST_EPS;
+  for (int a = 0; a < F.n; ++a) {
+    const int b = a + 1 < F.n ? a + 1 : 0;
+    const float nx = F.pv[b] - F.pv[a], ny = F.pu[a] - F.pu[b];
+    float p0 = 0, p1 = 0;
+    for (int q = 0; q < F.n; ++q) {
+      const float d = nx * F.pu[q] + ny * F.pv[q];
+      if (q == 0 || d < p0) p0 = d;
+      if (q == 0 || d > p1) p1 = d;
+    }
+    const float c0 = nx * rx0 + ny * ry0, c1 = nx * rx1 + ny * ry0;
+    const float c2 = nx * rx0 + ny * ry1, c3 = nx * rx1 + ny * ry1;
+    const float r0 = fminf(fminf(c0, c1), fminf(c2, c3)), r1 = fmaxf(fmaxf(c0, c1), fmaxf(c2, c3));
+    if (p1 < r0 || p0 > r1) return false;
+  }
+  return true;
+}
+
+// a wave per geometry triangle: f(cell) for every cell of its projection on
+// every face (lanes split a face's cell range)
+template <typename Fn>
+__device__ __forceinline__ void sl_for_cells(const rt_setup_arg_t* a, Fn f) {
+  const rt_tri_t* geom = vx_ptr<const rt_tri_t>(a->geom_addr);
+  const uint32_t waves = gridDim.x * (RTS_BLOCK / 64);
+  for (uint32_t j = blockIdx.x * (RTS_BLOCK / 64) + (threadIdx.x >> 6); j < a->num_geom; j += waves) {
+    const rt_tri_t r = geom[j];
+    for (int fc = 0; fc < 6; ++fc) {
+      SlFace F;
+      if (!sl_project(r, a->light, fc, &F)) continue;
+      const uint32_t w = (uint32_t)(F.x1 - F.x0 + 1), n = w * (uint32_t)(F.y1 - F.y0 + 1);
+      for (uint32_t q = lane_id(); q < n; q += 64) {
+        const int cx = F.x0 + (int)(q % w), cy = F.y0 + (int)(q / w);
+        if (!F.whole && !sl_cell_meets(F, cx, cy)) continue;
+        f(j, ((uint32_t)fc * RT_SLIST_N + (uint32_t)cy) * RT_SLIST_N + (uint32_t)cx);
+      }
+    }
+  }
+}
+
+__device__ void phase_scount(const rt_setup_arg_t* a) {
+  uint32_t* cnt = vx_ptr<uint32_t>(a->bcnt_addr);
+  sl_for_cells(a, [&](uint32_t, uint32_t cell) { atomicAdd(&cnt[cell], 1u); });
+}
+
+__device__ void phase_sfill(const rt_setup_arg_t* a) {
+  uint32_t* cur = vx_ptr<uint32_t>(a->bcnt_addr);
+  const uint2* sidx = vx_ptr<const uint2>(a->bidx_addr);
+  uint32_t* tmp = vx_ptr<uint32_t>(a->btmp_addr);
+  sl_for_cells(a, [&](uint32_t j, uint32_t cell) { tmp[sidx[cell].x + atomicAdd(&cur[cell], 1u)] = j; });
+}
+
+// a wave per cell: every entry's rank by geometry index (distinct), its
+// rt_tri_t copied to that position
+__device__ void phase_ssort(const rt_setup_arg_t* a) {
+  const uint2* sidx = vx_ptr<const uint2>(a->bidx_addr);
+  const uint32_t* tmp = vx_ptr<const uint32_t>(a->btmp_addr);
+  const uint4* geom = vx_ptr<const uint4>(a->geom_addr);
+  uint4* out = vx_ptr<uint4>(a->slist_addr);
+  const uint32_t waves = gridDim.x * (RTS_BLOCK / 64), l = lane_id();
+  if (blockIdx.x == 0 && threadIdx.x < 3)  // padding record (the kernels load pairs ahead)
+    out[3ull * a->blist_entries + threadIdx.x] = make_uint4(0u, 0u, 0u, 0u);
+  for (uint32_t c = blockIdx.x * (RTS_BLOCK / 64) + (threadIdx.x >> 6); c < a->nblk; c += waves) {
+    const uint2 oc = sload(sidx + c);
+    for (uint32_t base = 0; base < oc.y; base += 64) {
+      const uint32_t i = base + l;
+      const uint32_t me = tmp[oc.x + (i < oc.y ? i : 0u)];
+      uint32_t rank = 0;
+      for (uint32_t q = 0; q < oc.y; ++q) rank += sload(tmp + oc.x + q) < me ? 1u : 0u;
+      if (i < oc.y)
+        for (int w = 0; w < 3; ++w) out[3ull * (oc.x + rank) + w] = geom[3ull * me + w];
+    }
+  }
+}
+
 // renderer creation (app/rt_app.cpp rt_renderer_create): the clip-space
 // triangle of every pid (v0.xyw + pid, e1, e2) and the geometry list's copy
 __device__ __forceinline__ void tri_record(const float* verts, uint32_t g, rt_tri_t* out) {
@@ -829,5 +982,8 @@ VX_MAIN(rt_setup_arg_t, arg, RTS_BLOCK) {
   if (ph & RTS_BOFF) phase_boff(arg);
   if (ph & RTS_BFILL) phase_bfill(arg);
   if (ph & RTS_BSORT) phase_bsort(arg);
+  if (ph & RTS_SCOUNT) phase_scount(arg);
+  if (ph & RTS_SFILL) phase_sfill(arg);
+  if (ph & RTS_SSORT) phase_ssort(arg);
   return 0;
 }

@@ -50,6 +50,7 @@ struct Scene {
   float sx, sy, light[3];
   uint64_t argp;  // the argument block (constant address space), for lazy_args
   uint32_t blist, bidx, blist_blocks;  // per-block candidate lists (rt_bentry_t)
+  uint32_t sidx, slist, slist_on;      // light-space shadow lists (rt_common.h)
 };
 
 // The argument block is read through the scalar cache (constant address
@@ -89,6 +90,9 @@ __device__ __forceinline__ Scene load_scene(const rt_kernel_arg_t* ga) {
   s.blist = (uint32_t)a->blist_addr;
   s.bidx = (uint32_t)a->bidx_addr;
   s.blist_blocks = a->blist_blocks;
+  s.sidx = (uint32_t)a->sidx_addr;
+  s.slist = (uint32_t)a->slist_addr;
+  s.slist_on = a->slist_on;
   s.num_nodes = a->num_nodes;
   s.num_nodes4 = a->num_nodes4;
   s.num_layer = a->num_layer_tris;
@@ -627,6 +631,52 @@ __device__ __forceinline__ bool occluded_packet(const Scene& S, const Ray& r, bo
     ref = __builtin_amdgcn_readlane(vstk, sp);
   }
   return occ;
+}
+
+// A shadow segment's any-hit over its light-space cell list (rt_common.h;
+// oracle/rt.c sl_occluded): the cell of its direction from the light, then
+// the cell's triangles in ascending pid order until the first occluder
+// (t in (0, 1), the primary winner `skip` excluded).  Per lane: a lane's
+// chain is its own list, not the wave's union of BVH paths; the records are
+// copies in list order, loaded two ahead.  Tests count per lane.
+__device__ __forceinline__ uint32_t slist_cell(const Ray& s) {
+  const float u0 = -s.d[0], u1 = -s.d[1], u2 = -s.d[2];
+  int k = 0;
+  float m = fabsf(u0);
+  if (fabsf(u1) > m) { k = 1; m = fabsf(u1); }
+  if (fabsf(u2) > m) { k = 2; m = fabsf(u2); }
+  if (!(m > 0.0f)) return 0u;
+  const float uk = k == 0 ? u0 : (k == 1 ? u1 : u2);
+  const float ui = k == 0 ? u1 : u0, uj = k == 2 ? u1 : u2;
+  const int f = 2 * k + (uk < 0.0f ? 1 : 0);
+  const float hn = (float)RT_SLIST_N * 0.5f;
+  const int cx = min(max((int)floorf((ui / m + 1.0f) * hn), 0), RT_SLIST_N - 1);
+  const int cy = min(max((int)floorf((uj / m + 1.0f) * hn), 0), RT_SLIST_N - 1);
+  return ((uint32_t)f * RT_SLIST_N + (uint32_t)cy) * RT_SLIST_N + (uint32_t)cx;
+}
+__device__ __forceinline__ bool occluded_list(const Scene& S, const Ray& s, bool act, int32_t skip,
+                                              Counters& cnt) {
+  if (!act) return false;
+  const uint32_t cell = slist_cell(s);
+  const uint32_t off = S.A.ld_u32(S.sidx + 8u * cell), n = S.A.ld_u32(S.sidx + 8u * cell + 4u);
+  uint32_t o = S.slist + 48u * off;
+  for (uint32_t q = 0; q < n; q += 2, o += 96u) {
+    float4 t[6];
+#pragma unroll
+    for (int w = 0; w < 6; ++w) t[w] = S.A.ld_f4(o + 16u * w);  // 2 records (a padding one at the end)
+#pragma unroll
+    for (int e = 0; e < 2; ++e) {
+      if (q + e >= n) break;
+#ifdef RT_INSTRUMENT
+      ++cnt.tests;
+#endif
+      float th;
+      if (__float_as_int(t[3 * e].w) != skip && mt_hit(s, t[3 * e], t[3 * e + 1], t[3 * e + 2], 0.0f, &th) &&
+          th < 1.0f)
+        return true;
+    }
+  }
+  return false;
 }
 
 template <bool ANY>

@@ -54,6 +54,12 @@
 #define RTS_BFILL    0x10000u // unsorted (zmin, k, rx, ry) per (block, primitive) -> btmp
 #define RTS_BSORT    0x20000u // wave per block: rank + suffix union -> blist (+2 pads)
 #define RTS_BLOCKS_PER_PART 1024u  // blocks summed per bpart word (4 per thread)
+// light-space shadow lists (rt_common.h): a wave per geometry triangle
+// visits the cells of its projection on each cube face; BSUM / BSCAN / BOFF
+// then run over the cells (bcnt = the cell counts, bidx = sidx)
+#define RTS_SCOUNT   0x40000u // atomic count per cell
+#define RTS_SFILL    0x80000u // geometry index per (cell, triangle) -> btmp (u32), unsorted
+#define RTS_SSORT    0x100000u // wave per cell: rank by geometry index -> slist (rt_tri_t copies, +1 pad)
 
 // status words (u32 [4]): [0] malformed-input flags (RTS_ERR_*), [1] the
 // longest block list, [2] list entries in total, [3] spare
@@ -101,5 +107,8 @@ typedef struct {
   uint32_t num_tris, num_nodes, bvh4, num_layers, num_geom;
   uint32_t tiles_x, tiles_y, shard_index, shard_count, local_tiles, nblocks;
   uint32_t nblk, nbpart, blist_entries;  // local 8x8 blocks, bpart words, list entries (BSORT)
+  float light[3];          // shadow lists: the point light (clip x, y, w)
+  uint32_t pad2;
+  uint64_t slist_addr;     // shadow lists: rt_tri_t [entries + 1]
 
 } rt_setup_arg_t;

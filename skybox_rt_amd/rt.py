@@ -33,7 +33,8 @@ RT_RENDER_HOST_SETUP = 0x800
 RECORDS = {"prims": (0, np.int32, 32), "bbox": (1, np.uint32, 2), "vis": (2, np.uint32, 4),
            "vnodes": (3, np.uint32, 16), "vtris": (4, np.int32, 16), "vlayers": (5, np.int32, 16),
            "vgeom": (6, np.int32, 16), "order": (7, np.uint32, 1), "ptris": (8, np.float32, 12),
-           "geom": (9, np.float32, 12), "bidx": (10, np.uint32, 2), "blist": (11, np.uint32, 4)}
+           "geom": (9, np.float32, 12), "bidx": (10, np.uint32, 2), "blist": (11, np.uint32, 4),
+           "sidx": (12, np.uint32, 2), "slist": (13, np.float32, 12)}
 RT_BVH_STACK4_UNUSED = 0xFFFFFFFF
 RT_BVH_BUILD_HOST = 2
 CLEAR_COLOR = 0xFF000000               # draw3d/main.cpp:47
@@ -62,7 +63,8 @@ class BvhBuildStats(C.Structure):
 class SetupStats(C.Structure):
     _fields_ = [("device", C.c_uint32), ("launches", C.c_uint32), ("heavy_tiles", C.c_uint32),
                 ("blist_blocks", C.c_uint32), ("setup_ms", C.c_double), ("configure_ms", C.c_double),
-                ("blist_entries", C.c_uint64), ("blist_max", C.c_uint32), ("pad", C.c_uint32)]
+                ("blist_entries", C.c_uint64), ("blist_max", C.c_uint32), ("slist_on", C.c_uint32),
+                ("slist_entries", C.c_uint64)]
 
     def as_dict(self):
         return {n: getattr(self, n) for n, _ in self._fields_ if n != "pad"}

@@ -154,7 +154,8 @@ def test_list_cap_falls_back_to_the_walk(oracle_lib, host):
         r.render()
         k_gpu = r.stats()
         c, _, _, k = po.rt_render(_oscene(po, "tekkaman"),
-                                  po.rt_params(256, 256, shadows=True, nthreads=8, vis_lists=False),
+                                  po.rt_params(256, 256, shadows=True, nthreads=8, vis_lists=False,
+                                               shadow_lists=False),
                                   bvh=s.bvh() + (s.bvh4(),))
         assert np.array_equal(r.framebuffer(), c)
         assert k_gpu["tri_tests"] == k["tri_tests"] and k_gpu["node_visits"] == k["node_visits"]
@@ -180,3 +181,54 @@ def test_configure_4096_with_lists_is_timed():
     assert best["configure_ms"] < 5.0
     r.close()
     s.close()
+
+
+# ---- light-space shadow lists (rt_common.h; rt_setup.hip SCOUNT .. SSORT) ----
+@pytest.mark.parametrize("name", ["tekkaman", "scene", "box"])
+@pytest.mark.parametrize("light", [(0.0, 60.0, 80.0), (30.0, -20.0, 95.0), (0.0, 0.0, 0.5)])
+def test_shadow_lists_equal_oracle(oracle_lib, name, light):
+    """The device-built light-space lists == the oracle's (every cell's first
+    entry and count, every entry's triangle record in ascending pid order)."""
+    po = oracle_lib
+    s = rt.Scene.load(scene_path(name))
+    r = rt.Renderer(s)
+    r.configure(64, 64, shadows=True, light=light)
+    st = r.setup_stats()
+    assert st["slist_on"] == 1
+    idx, ent = po.shadow_lists(_oscene(po, name), light)
+    didx = r.records("sidx")
+    slist = r.records("slist")
+    assert np.array_equal(didx, idx)
+    assert st["slist_entries"] == len(ent) and slist.shape == (len(ent) + 1, 12)
+    geom = r.records("geom")
+    assert np.array_equal(slist[:-1].view(np.uint32), geom[ent].view(np.uint32))
+    r.close()
+    s.close()
+
+
+@pytest.mark.parametrize("lists", [1, 0])
+@pytest.mark.parametrize("light", [(0.0, 60.0, 80.0), (-200.0, 150.0, 50.0), (5.0, 5.0, 99.5)])
+def test_shadow_lists_frames_equal_oracle_with_counts(oracle_lib, lists, light):
+    """Shadow rays over the light-space lists (or, RT_SHADOW_LISTS=0, the BVH
+    packet walk): frame, occlusions and every count == the oracle's in the
+    same mode; both frames equal."""
+    po = oracle_lib
+    os.environ["RT_SHADOW_LISTS"] = str(lists)
+    try:
+        s = rt.Scene.load(scene_path("tekkaman"))
+        r = rt.Renderer(s)
+        r.configure(512, 512, shadows=True, light=light, instrumented=True)
+        assert r.setup_stats()["slist_on"] == lists
+        r.render()
+        st = r.stats()
+        c, _, _, k = po.rt_render(_oscene(po, "tekkaman"),
+                                  po.rt_params(512, 512, shadows=True, light=light, nthreads=8,
+                                               shadow_lists=bool(lists)),
+                                  bvh=s.bvh() + (s.bvh4(),))
+        assert np.array_equal(r.framebuffer(), c)
+        for key in ("node_visits", "tri_tests", "layer_tests", "shadow_rays", "occluded"):
+            assert st[key] == k[key], key
+        r.close()
+        s.close()
+    finally:
+        del os.environ["RT_SHADOW_LISTS"]
