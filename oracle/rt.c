@@ -1083,7 +1083,8 @@ static int rt_run(const orc_scene_t* scene, const orc_bvh_t* bvh, const orc_rt_p
   if (err) { rt_release(&c); return err; }
   c.bvh = bvh;
   vis_build_nodes(&c);
-  if (p->shadow_lists && !(p->flags & ORC_RT_PATH) && (p->flags & ORC_RT_SHADOWS)) sl_build(&c);
+  /* (BVH mode only: the flat image's shadow rays test the whole list) */
+  if (bvh && p->shadow_lists && !(p->flags & ORC_RT_PATH) && (p->flags & ORC_RT_SHADOWS)) sl_build(&c);
   c.color = color; c.pid = pid; c.tout = t;
   const uint32_t nt = p->nthreads > 1 ? p->nthreads : 1;
   if (bvh && !p->vis_per_lane && p->row_begin == 0 && p->row_end == 0 && p->row_step <= 1) {
