@@ -8,6 +8,8 @@
 // chain of launches of one image (device_setup); app/setup.cpp, app/vis.cpp
 // and rt_app.cpp host_setup remain the host restatement (RT_SETUP=host) that
 // the GPU tests compare against bit for bit.
+#include <algorithm>
+#include <cstdlib>
 #include <cstring>
 #include <vector>
 
@@ -237,13 +239,16 @@ int device_setup(rt_renderer* r, bool raster, bool order_on, bool lists, uint32_
 
 int shadow_lists(rt_renderer* r, uint32_t* launches) {
   rt_kernel_arg_t& a = r->arg;
-  if (r->sl_built && std::memcmp(r->sl_light, a.light, sizeof(a.light)) == 0) {
+  uint32_t N = RT_SLIST_N;
+  if (const char* e = std::getenv("RT_SLIST_N")) N = std::min(1024u, std::max(1u, (uint32_t)std::atoi(e)));
+  if (r->sl_built && std::memcmp(r->sl_light, a.light, sizeof(a.light)) == 0 && a.slist_n == N) {
     r->setup.slist_entries = r->sl_entries;
     return 0;
   }
   r->sl_built = false;
   a.slist_on = 0;
-  const uint32_t cells = RT_SLIST_CELLS, nbpart = (cells + RTS_BLOCKS_PER_PART - 1) / RTS_BLOCKS_PER_PART;
+  a.slist_n = N;
+  const uint32_t cells = 6u * N * N, nbpart = (cells + RTS_BLOCKS_PER_PART - 1) / RTS_BLOCKS_PER_PART;
   const uint32_t zero4[4] = {0, 0, 0, 0};
   DevBuf argb, status, cnt, part, tmp;
   if (alloc_tmp(r, sizeof(rt_setup_arg_t), &argb) || alloc_tmp(r, sizeof(zero4), &status, zero4) ||
@@ -259,6 +264,7 @@ int shadow_lists(rt_renderer* r, uint32_t* launches) {
   g.bidx_addr = a.sidx_addr;
   g.nblk = cells;
   g.nbpart = nbpart;
+  g.slist_n = N;
   for (int i = 0; i < 3; ++i) g.light[i] = a.light[i];
   add_fill(&g, cnt.addr, cells, 0u);
   for (uint32_t ph : {RTS_FILL, RTS_SCOUNT, RTS_BSUM, RTS_BSCAN, RTS_BOFF}) {

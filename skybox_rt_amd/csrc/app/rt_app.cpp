@@ -415,7 +415,7 @@ int rt_renderer_export_records(rt_renderer_h r, uint32_t which, void* out, uint6
       b = a.blist_blocks ? r->blist : nullptr;
       n = (r->setup.blist_entries + 2) * sizeof(rt_bentry_t);
       break;
-    case RT_REC_SIDX: b = a.slist_on ? r->sidx : nullptr; n = (uint64_t)RT_SLIST_CELLS * 8; break;
+    case RT_REC_SIDX: b = a.slist_on ? r->sidx : nullptr; n = 6ull * a.slist_n * a.slist_n * 8; break;
     case RT_REC_SLIST: b = a.slist_on ? r->slist : nullptr; n = (r->sl_entries + 1) * sizeof(rt_tri_t); break;
     default: return fail("unknown record array");
   }

@@ -196,7 +196,7 @@ typedef struct {
   uint64_t blist_addr;     // rt_bentry_t [entries + 2]: every local block's list, concatenated
   uint64_t bidx_addr;      // uint32[2] per local block lt * 16 + (by & 3) * 4 + (bx & 3): first entry, count
   uint32_t slist_on;       // light-space shadow lists built for `light` (0: shadow rays walk the BVH)
-  uint32_t pad_sl;
+  uint32_t slist_n;        // their cells per cube-face side (RT_SLIST_N unless env RT_SLIST_N)
   uint64_t sidx_addr;      // uint32[2] per light-space cell: first entry, count
   uint64_t slist_addr;     // rt_tri_t per entry (+1 padding record): every cell's triangles, ascending pid
 } rt_kernel_arg_t;
@@ -213,9 +213,8 @@ typedef struct {
 // conservative, so any-hit over the list is the brute force's verdict.
 // Built on the device (rt_setup.hip SCOUNT .. SSORT); oracle/rt.c sl_build
 // restates it.
-#define RT_SLIST_N 128
+#define RT_SLIST_N 128              // default cells per face side (the oracle's SL_N)
 #define RT_SLIST_EPS (1.0f / 512.0f)
-#define RT_SLIST_CELLS (6u * RT_SLIST_N * RT_SLIST_N)
 
 // ---- per-8x8-block candidate lists (primary visibility) -------------------
 // For every 8x8 pixel block of the shard's tiles (local block lb = local

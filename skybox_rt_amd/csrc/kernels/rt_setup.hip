@@ -806,7 +806,7 @@ struct SlFace {
 };
 
 // geometry triangle (rt_tri_t record r) on face f; false: nothing on the face
-__device__ __noinline__ bool sl_project(const rt_tri_t& r, const float L[3], int f, SlFace* F) {
+__device__ __noinline__ bool sl_project(const rt_tri_t& r, const float L[3], int f, int N, SlFace* F) {
   const int k = f >> 1, i = k == 0 ? 1 : 0, j = k == 2 ? 1 : 2;
   const float s = (f & 1) ? -1.0f : 1.0f;
   float A[8][3], B[8][3];
@@ -821,14 +821,14 @@ __device__ __noinline__ bool sl_project(const rt_tri_t& r, const float L[3], int
   if (m) m = sl_clip_plane(A, m, k, s, j, 1.0f, B);
   if (m) m = sl_clip_plane(B, m, k, s, j, -1.0f, A);
   if (!m) return false;
-  const float hn = (float)RT_SLIST_N * 0.5f;
+  const float hn = (float)N * 0.5f;
   F->whole = 0;
   for (int q = 0; q < m; ++q)
     if (!(s * A[q][k] > 0.0f)) F->whole = 1;
   if (F->whole) {
     F->n = 0;
     F->x0 = F->y0 = 0;
-    F->x1 = F->y1 = RT_SLIST_N - 1;
+    F->x1 = F->y1 = N - 1;
     return true;
   }
   float u0 = 0, u1 = 0, v0 = 0, v1 = 0;
@@ -843,17 +843,17 @@ __device__ __noinline__ bool sl_project(const rt_tri_t& r, const float L[3], int
   }
   F->n = m;
   F->x0 = max((int)floorf(((u0 - RT_SLIST_EPS) + 1.0f) * hn), 0);
-  F->x1 = min((int)floorf(((u1 + RT_SLIST_EPS) + 1.0f) * hn), RT_SLIST_N - 1);
+  F->x1 = min((int)floorf(((u1 + RT_SLIST_EPS) + 1.0f) * hn), N - 1);
   F->y0 = max((int)floorf(((v0 - RT_SLIST_EPS) + 1.0f) * hn), 0);
-  F->y1 = min((int)floorf(((v1 + RT_SLIST_EPS) + 1.0f) * hn), RT_SLIST_N - 1);
+  F->y1 = min((int)floorf(((v1 + RT_SLIST_EPS) + 1.0f) * hn), N - 1);
   return F->x0 <= F->x1 && F->y0 <= F->y1;
 }
 
 // separating-axis test of the projected polygon against cell (cx, cy)
 // widened by RT_SLIST_EPS
-__device__ __forceinline__ bool sl_cell_meets(const SlFace& F, int cx, int cy) {
+__device__ __forceinline__ bool sl_cell_meets(const SlFace& F, int cx, int cy, int N) {
   if (F.n < 3) return true;
-  const float cw = 2.0f / (float)RT_SLIST_N;
+  const float cw = 2.0f / (float)N;
   const float rx0 = ((float)cx * cw - 1.0f) - RT_SLIST_EPS, rx1 = ((float)(cx + 1) * cw - 1.0f) + RT_SLIST_EPS;
   const float ry0 = ((float)cy * cw - 1.0f) - RT_SLIST_EPS, ry1 = ((float)(cy + 1) * cw - 1.0f) + RT_SLIST_EPS;
   for (int a = 0; a < F.n; ++a) {
@@ -879,16 +879,17 @@ template <typename Fn>
 __device__ __forceinline__ void sl_for_cells(const rt_setup_arg_t* a, Fn f) {
   const rt_tri_t* geom = vx_ptr<const rt_tri_t>(a->geom_addr);
   const uint32_t waves = gridDim.x * (RTS_BLOCK / 64);
+  const int N = (int)a->slist_n;
   for (uint32_t j = blockIdx.x * (RTS_BLOCK / 64) + (threadIdx.x >> 6); j < a->num_geom; j += waves) {
     const rt_tri_t r = geom[j];
     for (int fc = 0; fc < 6; ++fc) {
       SlFace F;
-      if (!sl_project(r, a->light, fc, &F)) continue;
+      if (!sl_project(r, a->light, fc, N, &F)) continue;
       const uint32_t w = (uint32_t)(F.x1 - F.x0 + 1), n = w * (uint32_t)(F.y1 - F.y0 + 1);
       for (uint32_t q = lane_id(); q < n; q += 64) {
         const int cx = F.x0 + (int)(q % w), cy = F.y0 + (int)(q / w);
-        if (!F.whole && !sl_cell_meets(F, cx, cy)) continue;
-        f(j, ((uint32_t)fc * RT_SLIST_N + (uint32_t)cy) * RT_SLIST_N + (uint32_t)cx);
+        if (!F.whole && !sl_cell_meets(F, cx, cy, N)) continue;
+        f(j, ((uint32_t)fc * (uint32_t)N + (uint32_t)cy) * (uint32_t)N + (uint32_t)cx);
       }
     }
   }

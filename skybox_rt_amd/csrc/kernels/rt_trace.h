@@ -50,7 +50,7 @@ struct Scene {
   float sx, sy, light[3];
   uint64_t argp;  // the argument block (constant address space), for lazy_args
   uint32_t blist, bidx, blist_blocks;  // per-block candidate lists (rt_bentry_t)
-  uint32_t sidx, slist, slist_on;      // light-space shadow lists (rt_common.h)
+  uint32_t sidx, slist, slist_on, slist_n;  // light-space shadow lists (rt_common.h)
 };
 
 // The argument block is read through the scalar cache (constant address
@@ -93,6 +93,7 @@ __device__ __forceinline__ Scene load_scene(const rt_kernel_arg_t* ga) {
   s.sidx = (uint32_t)a->sidx_addr;
   s.slist = (uint32_t)a->slist_addr;
   s.slist_on = a->slist_on;
+  s.slist_n = a->slist_n;
   s.num_nodes = a->num_nodes;
   s.num_nodes4 = a->num_nodes4;
   s.num_layer = a->num_layer_tris;
@@ -639,7 +640,7 @@ __device__ __forceinline__ bool occluded_packet(const Scene& S, const Ray& r, bo
 // (t in (0, 1), the primary winner `skip` excluded).  Per lane: a lane's
 // chain is its own list, not the wave's union of BVH paths; the records are
 // copies in list order, loaded two ahead.  Tests count per lane.
-__device__ __forceinline__ uint32_t slist_cell(const Ray& s) {
+__device__ __forceinline__ uint32_t slist_cell(const Ray& s, uint32_t N) {
   const float u0 = -s.d[0], u1 = -s.d[1], u2 = -s.d[2];
   int k = 0;
   float m = fabsf(u0);
@@ -649,15 +650,15 @@ __device__ __forceinline__ uint32_t slist_cell(const Ray& s) {
   const float uk = k == 0 ? u0 : (k == 1 ? u1 : u2);
   const float ui = k == 0 ? u1 : u0, uj = k == 2 ? u1 : u2;
   const int f = 2 * k + (uk < 0.0f ? 1 : 0);
-  const float hn = (float)RT_SLIST_N * 0.5f;
-  const int cx = min(max((int)floorf((ui / m + 1.0f) * hn), 0), RT_SLIST_N - 1);
-  const int cy = min(max((int)floorf((uj / m + 1.0f) * hn), 0), RT_SLIST_N - 1);
-  return ((uint32_t)f * RT_SLIST_N + (uint32_t)cy) * RT_SLIST_N + (uint32_t)cx;
+  const float hn = (float)N * 0.5f;
+  const int cx = min(max((int)floorf((ui / m + 1.0f) * hn), 0), (int)N - 1);
+  const int cy = min(max((int)floorf((uj / m + 1.0f) * hn), 0), (int)N - 1);
+  return ((uint32_t)f * N + (uint32_t)cy) * N + (uint32_t)cx;
 }
 __device__ __forceinline__ bool occluded_list(const Scene& S, const Ray& s, bool act, int32_t skip,
                                               Counters& cnt) {
   if (!act) return false;
-  const uint32_t cell = slist_cell(s);
+  const uint32_t cell = slist_cell(s, S.slist_n);
   const uint32_t off = S.A.ld_u32(S.sidx + 8u * cell), n = S.A.ld_u32(S.sidx + 8u * cell + 4u);
   uint32_t o = S.slist + 48u * off;
   for (uint32_t q = 0; q < n; q += 2, o += 96u) {

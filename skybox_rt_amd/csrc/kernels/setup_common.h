@@ -108,7 +108,7 @@ typedef struct {
   uint32_t tiles_x, tiles_y, shard_index, shard_count, local_tiles, nblocks;
   uint32_t nblk, nbpart, blist_entries;  // local 8x8 blocks, bpart words, list entries (BSORT)
   float light[3];          // shadow lists: the point light (clip x, y, w)
-  uint32_t pad2;
+  uint32_t slist_n;        // shadow lists: cells per cube-face side
   uint64_t slist_addr;     // shadow lists: rt_tri_t [entries + 1]
 
 } rt_setup_arg_t;
