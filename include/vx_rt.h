@@ -50,6 +50,9 @@ typedef struct {
                                           clears) with the host loops instead of on the
                                           device (kernels/rt_setup.hip, the default; env
                                           RT_SETUP=host does the same) */
+#define RT_RENDER_COVERAGE 0x1000u     /* with RT_RENDER_RASTER: the raster regression app's
+                                          coverage image (tests/regression/raster/kernel.cpp:
+                                          covered pixels 0xffffffff, no shading, no OM state) */
 
 typedef struct {
   uint32_t width, height;
@@ -60,6 +63,8 @@ typedef struct {
   uint32_t shard_count;       /*   t % shard_count == shard_index */
   uint32_t bounces;           /* RT_RENDER_PATH: bounce segments per path (config 4: 4) */
   uint32_t seed;              /* RT_RENDER_PATH: RNG seed (config 4: 0x5EED) */
+  uint32_t tile_logsize;      /* RT_RENDER_RASTER: binning tile side 2^k (draw3d / raster -k,
+                                 gfxutil.cpp:237-250; 2..15), 0 = RASTER_TILE_LOGSIZE (5) */
 } rt_render_params_t;
 
 typedef struct {
@@ -79,6 +84,9 @@ typedef struct {
 const char* rt_last_error(void);
 
 int rt_scene_load(const char* path, rt_scene_h* out);
+/* draw3d's -s start / -e end (tests/regression/draw3d/main.cpp:179-181): only
+ * drawcalls start <= d <= end are drawn (rt_scene_load = 0, 0xffffffff) */
+int rt_scene_load_range(const char* path, uint32_t start_draw, uint32_t end_draw, rt_scene_h* out);
 int rt_scene_free(rt_scene_h scene);
 int rt_scene_info(rt_scene_h scene, rt_scene_info_t* info);
 /* flattened triangles, float[num_prims][3][10] (x,y,z,w, r,g,b,a, u,v) */

@@ -123,3 +123,18 @@ def load(path: str) -> Scene:
             assert len(data) == size, (len(data), size)
             scene.textures[tid] = (fmt, w, h, data)
     return scene
+
+
+def select_drawcalls(scene: Scene, keep) -> Scene:
+    """The scene with only drawcalls `keep` (ascending indices), in order:
+    draw3d's -s / -e draw range (tests/regression/draw3d/main.cpp:179-181)."""
+    out = Scene(textures=scene.textures)
+    verts = []
+    for d in keep:
+        dc = scene.drawcalls[d]
+        verts.append(scene.prim_verts[dc.prim_offset:dc.prim_offset + dc.prim_count])
+        out.drawcalls.append(DrawCall(dc.states, dc.texture_id, sum(len(v) for v in verts[:-1]),
+                                      dc.prim_count, dc.viewport))
+    out.prim_verts = (np.concatenate(verts).astype(np.float32) if verts
+                      else np.zeros((0, 3, 10), np.float32))
+    return out

@@ -534,3 +534,80 @@ int orc_om_write(const orc_dcstate_t* s, uint32_t* cbuf_px, uint32_t* zbuf_px,
     *cbuf_px = (dst_color & ~s->cbuf_writemask) | (color & s->cbuf_writemask);
   return passed;
 }
+
+/* ---- the render-output regression app (tests/regression/om) -------------
+ * OutputMerger / DepthTencil / Blender ::configure from the 18 OM DCR words
+ * (dcr[i] = VX_DCR_OM_STATE_BEGIN + i), the stencil face chosen by
+ * `backface` (sim/simx/om_unit.cpp:28-49, graphics.cpp:534-620), then the
+ * kernel (om/kernel.cpp:16-40): num_tasks tasks of ceil(H / num_tasks) rows,
+ * each pixel written once through the unit (om_unit.cpp:55-80) with the
+ * colour (alpha = task * 255 / rows when blending) and depth words.  cbuf /
+ * zbuf hold the host's clears on entry (om/main.cpp:262-283). */
+enum {
+  OM_CBUF_WRITEMASK = 2, OM_DEPTH_FUNC = 5, OM_DEPTH_WRITEMASK = 6, OM_STENCIL_FUNC = 7,
+  OM_STENCIL_ZPASS = 8, OM_STENCIL_ZFAIL = 9, OM_STENCIL_FAIL = 10, OM_STENCIL_REF = 11,
+  OM_STENCIL_MASK = 12, OM_STENCIL_WRITEMASK = 13, OM_BLEND_MODE = 14, OM_BLEND_FUNC = 15,
+  OM_BLEND_CONST = 16, OM_LOGIC_OP = 17
+};
+void orc_om_configure(orc_dcstate_t* s, const uint32_t dcr[18], int backface) {
+  const uint32_t sh = backface ? 16u : 0u;
+  memset(s, 0, sizeof(*s));
+  s->depth_func = dcr[OM_DEPTH_FUNC];
+  s->depth_writemask = dcr[OM_DEPTH_WRITEMASK] & 1u;
+  s->depth_test_on = !((s->depth_func == VX_OM_DEPTH_FUNC_ALWAYS) && !s->depth_writemask);
+  s->stencil_func = (dcr[OM_STENCIL_FUNC] >> sh) & 0xffffu;
+  s->stencil_zpass = (dcr[OM_STENCIL_ZPASS] >> sh) & 0xffffu;
+  s->stencil_zfail = (dcr[OM_STENCIL_ZFAIL] >> sh) & 0xffffu;
+  s->stencil_fail = (dcr[OM_STENCIL_FAIL] >> sh) & 0xffffu;
+  s->stencil_ref = (dcr[OM_STENCIL_REF] >> sh) & 0xffffu;
+  s->stencil_mask = (dcr[OM_STENCIL_MASK] >> sh) & 0xffffu;
+  s->stencil_writemask = (dcr[OM_STENCIL_WRITEMASK] >> sh) & 0xffffu;
+  s->stencil_on = !((s->stencil_func == VX_OM_DEPTH_FUNC_ALWAYS) &&
+                    (s->stencil_zpass == VX_OM_STENCIL_OP_KEEP) &&
+                    (s->stencil_zfail == VX_OM_STENCIL_OP_KEEP));
+  s->blend_mode_rgb = dcr[OM_BLEND_MODE] & 0xffffu;
+  s->blend_mode_a = dcr[OM_BLEND_MODE] >> 16;
+  s->blend_src_rgb = dcr[OM_BLEND_FUNC] & 0xffu;
+  s->blend_src_a = (dcr[OM_BLEND_FUNC] >> 8) & 0xffu;
+  s->blend_dst_rgb = (dcr[OM_BLEND_FUNC] >> 16) & 0xffu;
+  s->blend_dst_a = (dcr[OM_BLEND_FUNC] >> 24) & 0xffu;
+  s->blend_const = dcr[OM_BLEND_CONST];
+  s->logic_op = dcr[OM_LOGIC_OP];
+  s->blend_on = !((s->blend_mode_rgb == VX_OM_BLEND_MODE_ADD) &&
+                  (s->blend_mode_a == VX_OM_BLEND_MODE_ADD) &&
+                  (s->blend_src_rgb == VX_OM_BLEND_FUNC_ONE) &&
+                  (s->blend_src_a == VX_OM_BLEND_FUNC_ONE) &&
+                  (s->blend_dst_rgb == VX_OM_BLEND_FUNC_ZERO) &&
+                  (s->blend_dst_a == VX_OM_BLEND_FUNC_ZERO));
+  {
+    const uint32_t wm = dcr[OM_CBUF_WRITEMASK] & 0xfu;
+    s->cbuf_writemask = ((wm >> 0) & 1u) * 0x000000ffu | ((wm >> 1) & 1u) * 0x0000ff00u |
+                        ((wm >> 2) & 1u) * 0x00ff0000u | ((wm >> 3) & 1u) * 0xff000000u;
+    s->color_read = wm != 0xfu;
+    s->color_write = wm != 0u;
+  }
+}
+
+int orc_om_app(uint32_t width, uint32_t height, uint32_t num_tasks, uint32_t color,
+               uint32_t depth, int backface, int blend_enable, const uint32_t dcr[18],
+               uint32_t* cbuf, uint32_t* zbuf) {
+  orc_dcstate_t s;
+  uint32_t task, tile_h;
+  float alpha_step;
+  if (num_tasks == 0) return -1;
+  orc_om_configure(&s, dcr, backface);
+  tile_h = (height + num_tasks - 1) / num_tasks;          /* kernel.cpp:35-36 */
+  alpha_step = 255.0f / (float)tile_h;
+  for (task = 0; task < num_tasks; ++task) {               /* kernel_body :16-33 */
+    const uint32_t y0 = task * tile_h;
+    const uint32_t y1 = (y0 + tile_h < height) ? y0 + tile_h : height;
+    const uint32_t alpha = blend_enable ? (uint32_t)((float)task * alpha_step) : 0xffu;
+    const uint32_t c = (alpha << 24) | (color & 0x00ffffffu);
+    uint32_t x, y;
+    if (y0 >= height) break;
+    for (y = y0; y < y1; ++y)
+      for (x = 0; x < width; ++x)
+        orc_om_write(&s, &cbuf[(size_t)y * width + x], &zbuf[(size_t)y * width + x], c, depth);
+  }
+  return 0;
+}

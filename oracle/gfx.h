@@ -177,6 +177,13 @@ int orc_vis_nodes(const int32_t* refs, uint32_t n, const int32_t* leaf_pids, uin
 int orc_om_write(const orc_dcstate_t* s, uint32_t* cbuf_px, uint32_t* zbuf_px,
                  uint32_t color, uint32_t depth);
 
+/* The OM regression app (tests/regression/om, see gfx.c): unit state from
+ * the 18 OM DCR words, and the whole kernel over pre-cleared buffers. */
+void orc_om_configure(orc_dcstate_t* s, const uint32_t dcr[18], int backface);
+int orc_om_app(uint32_t width, uint32_t height, uint32_t num_tasks, uint32_t color,
+               uint32_t depth, int backface, int blend_enable, const uint32_t dcr[18],
+               uint32_t* cbuf, uint32_t* zbuf);
+
 /* TextureSampler::read (graphics.cpp:253-314), lod 0. */
 uint32_t orc_tex_read(const orc_dcstate_t* s, int32_t u, int32_t v);
 

@@ -80,6 +80,11 @@ int orc_setup_prim(const float* v /*[3][10]*/, uint32_t width, uint32_t height,
 int orc_raster_render(const orc_scene_t* scene, uint32_t width, uint32_t height,
                       uint32_t tile_logsize, uint32_t* color, uint32_t* depth,
                       int32_t* pid_out);
+/* The raster regression app (tests/regression/raster): the same binning and
+ * coverage, every covered pixel written 0xffffffff over the caller's clear
+ * (0xff000000 in the reference, raster/main.cpp:40,245-250). */
+int orc_raster_coverage(const orc_scene_t* scene, uint32_t width, uint32_t height,
+                        uint32_t tile_logsize, uint32_t* color);
 
 /* ---- ray tracing -------------------------------------------------------- */
 typedef struct {

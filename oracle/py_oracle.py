@@ -169,6 +169,18 @@ def raster_render(oscene: OracleScene, width: int, height: int, tile_logsize: in
             pid.reshape(height, width))
 
 
+def raster_coverage(oscene: OracleScene, width: int, height: int, tile_logsize: int = 5):
+    """The raster regression app's image (ARGB, row 0 = bottom): covered
+    pixels 0xffffffff over the 0xff000000 clear."""
+    L = lib()
+    L.orc_raster_coverage.argtypes = [C.POINTER(SceneC), C.c_uint32, C.c_uint32, C.c_uint32,
+                                      C.c_void_p]
+    color = np.full(width * height, CLEAR_COLOR, np.uint32)
+    if L.orc_raster_coverage(C.byref(oscene.c), width, height, tile_logsize, color.ctypes.data):
+        raise RuntimeError("orc_raster_coverage failed")
+    return color.reshape(height, width)
+
+
 def vis_prims(oscene: OracleScene, width: int, height: int) -> np.ndarray:
     """uint32[P, 3]: every primitive's covered-pixel rectangle (x0|x1<<16,
     y0|y1<<16, inclusive) and depth-word lower bound, by brute force (vis.c)."""
@@ -388,3 +400,32 @@ def half4(nodes4: np.ndarray):
     half = np.zeros((nn, 64), np.uint8)
     lib().orc_half4(n4.ctypes.data, nn, half.ctypes.data)
     return n4, half
+
+
+def om_app(width=128, height=128, num_tasks=256 * 32 * 64, color=0xFFFFFFFF, depth_enable=False,
+           blend=False, backface=False):
+    """The OM regression app (tests/regression/om/main.cpp:130-300 host side,
+    restated: the checkerboard depth clear of :265-275 with TFixed<24>(0.0 /
+    0.99), colour clear 0, the OM DCR words of :153-190) run through the
+    oracle's unit (gfx.c orc_om_app).  Returns the ARGB8888 colour buffer
+    [height, width], row 0 = bottom like the device buffer.  num_tasks
+    defaults to the MI355X driver's cores x warps x threads (256 x 32 x 64)."""
+    L = lib()
+    L.orc_om_app.argtypes = [C.c_uint32] * 5 + [C.c_int, C.c_int, C.c_void_p, C.c_void_p,
+                                                C.c_void_p]
+    fx24 = lambda f: int(np.float32(f) * np.float32(16777216.0))   # truncating TFixed<24>
+    y, x = np.mgrid[0:height, 0:width]
+    zbuf = np.where((x & 1) == (y & 1), fx24(0.0), fx24(0.99)).astype(np.uint32).reshape(-1)
+    cbuf = np.zeros(width * height, np.uint32)
+    dcr = np.zeros(18, np.uint32)          # VX_DCR_OM_STATE_BEGIN + i
+    dcr[2] = 0xF                                                  # CBUF_WRITEMASK
+    dcr[5] = 2 if depth_enable else 0                             # DEPTH_FUNC LESS / ALWAYS
+    dcr[6] = 1 if depth_enable else 0                             # DEPTH_WRITEMASK
+    dcr[12] = 0xFF                                                # STENCIL_MASK
+    dcr[14] = 0                                                   # BLEND_MODE ADD/ADD
+    dcr[15] = ((7 << 24) | (7 << 16) | (1 << 8) | 1) if blend else ((1 << 8) | 1)
+    rc = L.orc_om_app(width, height, num_tasks, color & 0xFFFFFFFF, 0x800000, int(backface),
+                      int(blend), dcr.ctypes.data, cbuf.ctypes.data, zbuf.ctypes.data)
+    if rc != 0:
+        raise RuntimeError(f"orc_om_app failed: {rc}")
+    return cbuf.reshape(height, width)

@@ -10,9 +10,12 @@
 
 #include "gfx.h"
 
-int orc_raster_render(const orc_scene_t* scene, uint32_t width, uint32_t height,
-                      uint32_t tile_logsize, uint32_t* color, uint32_t* depth,
-                      int32_t* pid_out) {
+/* coverage != 0: the raster regression app instead of draw3d
+ * (tests/regression/raster/kernel.cpp:35-45: every covered pixel of every
+ * drawcall written 0xffffffff, no shader, no output-merger state) */
+static int raster_render(const orc_scene_t* scene, uint32_t width, uint32_t height,
+                         uint32_t tile_logsize, int coverage, uint32_t* color, uint32_t* depth,
+                         int32_t* pid_out) {
   if (!scene || !color || !depth || width == 0 || height == 0) return -1;
   if (pid_out)
     for (uint64_t i = 0; i < (uint64_t)width * height; ++i) pid_out[i] = -1;
@@ -74,6 +77,10 @@ int orc_raster_render(const orc_scene_t* scene, uint32_t width, uint32_t height,
             const int32_t e1 = orc_edge_eval(p->edges[1], x, y);
             const int32_t e2 = orc_edge_eval(p->edges[2], x, y);
             if (e0 < 0 || e1 < 0 || e2 < 0) continue;
+            if (coverage) {
+              color[(uint64_t)y * width + x] = 0xffffffffu;
+              continue;
+            }
             uint32_t z;
             const uint32_t c = orc_shade(&st, p, e0, e1, e2, &z);
             const uint64_t px = (uint64_t)y * width + x;
@@ -87,4 +94,17 @@ int orc_raster_render(const orc_scene_t* scene, uint32_t width, uint32_t height,
   }
   free(tile_cnt); free(tile_off);
   return 0;
+}
+
+int orc_raster_render(const orc_scene_t* scene, uint32_t width, uint32_t height,
+                      uint32_t tile_logsize, uint32_t* color, uint32_t* depth,
+                      int32_t* pid_out) {
+  return raster_render(scene, width, height, tile_logsize, 0, color, depth, pid_out);
+}
+
+int orc_raster_coverage(const orc_scene_t* scene, uint32_t width, uint32_t height,
+                        uint32_t tile_logsize, uint32_t* color) {
+  uint32_t dummy = 0;
+  if (!color) return -1;
+  return raster_render(scene, width, height, tile_logsize, 1, color, &dummy, NULL);
 }

@@ -28,7 +28,7 @@ REQUIRED = ("libvortex.so", "libvortex-hip.so", "librtapp.so", "rtapp",
             "rt_flat.vxbin", "rt_flat_stats.vxbin", "raster_kernel.vxbin",
             "pt_compact/pt_kernel.vxbin", "pt_compact/pt_kernel_stats.vxbin",
             "tex_kernel_f0.vxbin", "tex_kernel_f1.vxbin", "tex_kernel_f2.vxbin", "texapp", "bvh_build.vxbin",
-            "librt_shard.so", "rt_setup.vxbin", "bvh_sah.vxbin")
+            "librt_shard.so", "rt_setup.vxbin", "bvh_sah.vxbin", "om.vxbin", "omapp", "rasterapp")
 
 
 class NativeLibraryMissing(RuntimeError):

@@ -74,11 +74,30 @@ extern "C" {
 const char* rt_last_error(void) { return g_err.c_str(); }
 
 int rt_scene_load(const char* path, rt_scene_h* out) {
+  return rt_scene_load_range(path, 0u, 0xffffffffu, out);
+}
+
+int rt_scene_load_range(const char* path, uint32_t start_draw, uint32_t end_draw, rt_scene_h* out) {
   if (path == nullptr || out == nullptr) return fail("null argument");
   auto sc = std::make_unique<rt_scene>();
   auto t0 = std::chrono::steady_clock::now();
   std::string err;
   if (rt::LoadCGLTrace(path, &sc->scene, &err) != 0) return fail(err);
+  if (start_draw != 0u || end_draw != 0xffffffffu) {
+    // draw3d -s / -e (main.cpp:179-181): drawcalls outside [start, end] are
+    // not drawn; the kept ones keep their order (and so every tie rule)
+    rt::Scene all = std::move(sc->scene);
+    sc->scene = rt::Scene();
+    sc->scene.textures = std::move(all.textures);
+    for (uint32_t d = 0; d < (uint32_t)all.drawcalls.size(); ++d) {
+      if (d < start_draw || d > end_draw) continue;
+      rt::DrawCall dc = all.drawcalls[d];
+      dc.prim_offset = (uint32_t)sc->scene.prims.size();
+      sc->scene.prims.insert(sc->scene.prims.end(), all.prims.begin() + all.drawcalls[d].prim_offset,
+                             all.prims.begin() + all.drawcalls[d].prim_offset + dc.prim_count);
+      sc->scene.drawcalls.push_back(dc);
+    }
+  }
   sc->parse_ms = ms_since(t0);
   // classify drawcalls (DESIGN.md "Scope"): screen layers (depth test off)
   // must precede geometry; geometry shares one LESS/LEQUAL depth function.
@@ -800,6 +819,14 @@ int rt_renderer_configure(rt_renderer_h r, const rt_render_params_t* p) {
     if (const char* e = std::getenv("RT_RASTER_TILE_LOG")) tlog = std::atoi(e) == 5 ? 5u : 4u;
   }
   a.raster_tile_log = tlog;
+  // binning granularity (draw3d / raster -k): semantic, fixed-point coverage
+  // reaching past a primitive's bbox counts only inside its binned tiles
+  a.raster_bin_log = p->tile_logsize ? p->tile_logsize : RT_TILE_LOG;
+  if (raster && (a.raster_bin_log < 2 || a.raster_bin_log > 15))
+    return fail("tile_logsize must be in [2, 15] (raster_unit.cpp:92)");
+  if (!raster && a.raster_bin_log != RT_TILE_LOG)
+    return fail("the RT modes bin at RASTER_TILE_LOGSIZE 5; other tile sizes need RT_RENDER_RASTER");
+  if ((p->flags & RT_RENDER_COVERAGE) && !raster) return fail("RT_RENDER_COVERAGE needs RT_RENDER_RASTER");
   a.tiles_y = (p->height + (1u << tlog) - 1) >> tlog;
   a.tiles_x = (p->width + (1u << tlog) - 1) >> tlog;
   const uint32_t tiles = a.tiles_x * a.tiles_y;
@@ -819,6 +846,7 @@ int rt_renderer_configure(rt_renderer_h r, const rt_render_params_t* p) {
             ((p->flags & RT_RENDER_PATH) ? RT_FLAG_PATH : 0u) |
             ((p->flags & RT_RENDER_FLAT) ? RT_FLAG_FLAT : 0u) |
             (raster ? RT_FLAG_RASTER : 0u) |
+            ((p->flags & RT_RENDER_COVERAGE) ? RT_FLAG_COVERAGE : 0u) |
             (s->tie_high ? RT_FLAG_TIE_HIGH : 0u) | (compact ? RT_FLAG_COMPACT : 0u) |
             (use_bvh4 ? RT_FLAG_BVH4 : 0u) |
             // binary16 node records: the host tree's, or the device tree's (BVHB_HALF)

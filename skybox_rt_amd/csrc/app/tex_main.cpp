@@ -13,6 +13,7 @@
 #include <string>
 #include <vector>
 
+#include "assets.h"
 #include "png.h"
 #include "vx_rt.h"
 #include "vx_tex.h"
@@ -74,6 +75,8 @@ int main(int argc, char** argv) {
   }
   std::vector<uint32_t> src;
   uint32_t w = 0, h = 0;
+  input = rt::ResolveAsset(input);  // tex/main.cpp resolves through ASSETS_PATHS too
+  if (!reference.empty()) reference = rt::ResolveAsset(reference);
   if (rt::LoadPngARGB(input, &src, &w, &h) != 0) {
     std::printf("Error: cannot load %s\n", input.c_str());
     return -1;

@@ -44,6 +44,7 @@ __device__ __forceinline__ uint32_t lane_id() {
 
 struct RsLds {
   uint32_t list[RS_BLOCK];   // the tile's primitives (global pids) of one chunk, in order
+  uint2 bb[RS_BLOCK];        // their screen boxes (per-pixel bin test, bins finer than the tile)
   uint32_t wave_n[kWaves];
 #if RS_STAGE
   uint4 rec[RS_BLOCK][8];    // their rt_prim_t records (128 B each), same order
@@ -54,7 +55,17 @@ struct Frame {
   vx_arena A;
   uint32_t prims, dcs, oms, bbox, cbuf, zbuf;
   uint32_t width, height, tiles_x, num_dc, clear_color, clear_depth, tile_log;
+  uint32_t bin_log;          // binning tile side 2^bin_log (RASTER_TILE_LOGSIZE, draw3d -k)
+  bool coverage;             // the raster app: covered pixels white (raster/kernel.cpp:35-45)
 };
+
+// the reference bins a primitive to the tiles its screen box [x0, x1) x
+// [y0, y1) reaches (gfxutil.cpp:237-250); does it reach the region [lo, hi)?
+__device__ __forceinline__ bool bins_to(uint2 bb, uint32_t x_lo, uint32_t x_hi, uint32_t y_lo,
+                                        uint32_t y_hi) {
+  const uint32_t bx0 = bb.x & 0xffffu, bx1 = bb.x >> 16, by0 = bb.y & 0xffffu, by1 = bb.y >> 16;
+  return bx0 < bx1 && bx0 < x_hi && bx1 > x_lo && by0 < y_hi && by1 > y_lo;
+}
 
 // thread -> its pixel group: g x g pixels at (gx, gy), g = tile side / 16
 __device__ __forceinline__ void thread_pixels(const Frame& F, uint32_t tile, uint32_t t,
@@ -80,8 +91,14 @@ __device__ __forceinline__ rt_omstate_t load_om(const vx_arena& A, uint32_t off)
 __device__ __forceinline__ void render_tile(const Frame& F, uint32_t tile, RsLds& L, uint32_t col[4],
                                             uint32_t ds[4], uint32_t& frags) {
   const uint32_t x0 = (tile % F.tiles_x) << F.tile_log, y0 = (tile / F.tiles_x) << F.tile_log;
-  const uint32_t bx_lo = x0 & ~31u, bx_hi = bx_lo + 32u;  // enclosing RASTER_TILE_LOGSIZE tile
-  const uint32_t by_lo = y0 & ~31u, by_hi = by_lo + 32u;
+  // the bins this workgroup tile lies in: the enclosing bin when bins are at
+  // least as large as the tile, else the tile itself (then every pixel also
+  // tests its own bin below)
+  const bool fine_bins = F.bin_log < F.tile_log;
+  const uint32_t bmask = fine_bins ? ((1u << F.tile_log) - 1u) : ((1u << F.bin_log) - 1u);
+  const uint32_t bx_lo = x0 & ~bmask, bx_hi = bx_lo + bmask + 1u;
+  const uint32_t by_lo = y0 & ~bmask, by_hi = by_lo + bmask + 1u;
+  const uint32_t pmask = (1u << F.bin_log) - 1u;
   uint32_t qx, qy, gs;
   thread_pixels(F, tile, threadIdx.x, &qx, &qy, &gs);
   const uint32_t npx = gs * gs;
@@ -94,15 +111,15 @@ __device__ __forceinline__ void render_tile(const Frame& F, uint32_t tile, RsLds
       const uint32_t i = base + threadIdx.x;
       bool ov = false;
       uint32_t g = 0;
+      uint2 bb = make_uint2(0u, 0u);
       if (i < om.prim_count) {
         g = om.prim_offset + i;
-        const uint2 bb = make_uint2(F.A.ld_u32(F.bbox + 8u * g), F.A.ld_u32(F.bbox + 8u * g + 4));
-        const uint32_t bx0 = bb.x & 0xffffu, bx1 = bb.x >> 16, by0 = bb.y & 0xffffu, by1 = bb.y >> 16;
-        // binned at the reference's 32x32 granularity whatever this
-        // workgroup's tile size: fixed-point coverage can reach a few pixels
-        // past the float bbox, and the reference covers those pixels iff
-        // they lie in a 32x32 tile the primitive was binned to
-        ov = bx0 < bx1 && bx0 < bx_hi && bx1 > bx_lo && by0 < by_hi && by1 > by_lo;
+        bb = make_uint2(F.A.ld_u32(F.bbox + 8u * g), F.A.ld_u32(F.bbox + 8u * g + 4));
+        // binned at the reference's granularity whatever this workgroup's
+        // tile size: fixed-point coverage can reach a few pixels past the
+        // float bbox, and the reference covers those pixels iff they lie in
+        // a tile the primitive was binned to
+        ov = bins_to(bb, bx_lo, bx_hi, by_lo, by_hi);
       }
       const uint64_t m = __ballot(ov);
       if (lane_id() == 0) L.wave_n[w] = (uint32_t)__popcll(m);
@@ -118,6 +135,7 @@ __device__ __forceinline__ void render_tile(const Frame& F, uint32_t tile, RsLds
         const uint32_t r = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
                                                      __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
         L.list[pre + r] = g;
+        L.bb[pre + r] = bb;
 #if RS_STAGE
 #pragma unroll
         for (int k = 0; k < 8; ++k) L.rec[pre + r][k] = F.A.ld_u4(F.prims + 128u * g + 16u * k);
@@ -146,10 +164,18 @@ __device__ __forceinline__ void render_tile(const Frame& F, uint32_t tile, RsLds
           const int32_t e2 = gfx::edge_eval(p.edge(2), x, y);
           // inclusive coverage, no top-left rule, viewport scissor
           // (graphics.cpp:813-825)
-          if (x < F.width && y < F.height && e0 >= 0 && e1 >= 0 && e2 >= 0) {
-            uint32_t z;
-            const uint32_t c = gfx::shade_edges(F.A, p, st, e0, e1, e2, &z);
-            gfx::om_write(om, col[j], ds[j], c, z);
+          bool in = x < F.width && y < F.height && e0 >= 0 && e1 >= 0 && e2 >= 0;
+          if (fine_bins)  // the pixel's own bin must be one the primitive was binned to
+            in = in && bins_to(L.bb[k], x & ~pmask, (x & ~pmask) + pmask + 1u, y & ~pmask,
+                               (y & ~pmask) + pmask + 1u);
+          if (in) {
+            if (F.coverage) {
+              col[j] = 0xffffffffu;
+            } else {
+              uint32_t z;
+              const uint32_t c = gfx::shade_edges(F.A, p, st, e0, e1, e2, &z);
+              gfx::om_write(om, col[j], ds[j], c, z);
+            }
             ++frags;
           }
         }
@@ -180,6 +206,8 @@ VX_MAIN(rt_kernel_arg_t, arg, RS_BLOCK) {
   F.clear_color = arg->clear_color;
   F.clear_depth = 0xffffffffu;
   F.tile_log = arg->raster_tile_log;
+  F.bin_log = arg->raster_bin_log;
+  F.coverage = (arg->flags & RT_FLAG_COVERAGE) != 0;
   uint32_t frags = 0, pixels = 0;
   uint32_t col[4], ds[4], qx = 0, qy = 0, npx = 1;
   // task = one thread's pixel group; a workgroup step = one tile

@@ -53,6 +53,7 @@
 #define RT_FLAG_RASTER   0x20u   // draw3d raster pipeline (raster_kernel.hip)
 #define RT_FLAG_BVH4     0x40u   // traverse the 4-wide BVH (nodes4) instead of the BVH2
 #define RT_FLAG_BVH4H    0x80u   // BVH4 node steps read the binary16 rt_node4h_t form
+#define RT_FLAG_COVERAGE 0x100u  // raster mode: covered pixels white, no shading / OM
 
 #define RT_DC_DEPTH   0x1u
 #define RT_DC_COLOR   0x2u
@@ -199,6 +200,8 @@ typedef struct {
   uint32_t slist_n;        // their cells per cube-face side (RT_SLIST_N unless env RT_SLIST_N)
   uint64_t sidx_addr;      // uint32[2] per light-space cell: first entry, count
   uint64_t slist_addr;     // rt_tri_t per entry (+1 padding record): every cell's triangles, ascending pid
+  uint32_t raster_bin_log; // raster mode: binning tile side 2^log (RASTER_TILE_LOGSIZE; draw3d -k)
+  uint32_t pad_bin;
 } rt_kernel_arg_t;
 
 // ---- light-space shadow lists (shadow rays to the point light) ------------

@@ -74,7 +74,7 @@ class RenderParams(C.Structure):
     _fields_ = [("width", C.c_uint32), ("height", C.c_uint32), ("flags", C.c_uint32),
                 ("light", C.c_float * 3), ("clear_color", C.c_uint32),
                 ("shard_index", C.c_uint32), ("shard_count", C.c_uint32),
-                ("bounces", C.c_uint32), ("seed", C.c_uint32)]
+                ("bounces", C.c_uint32), ("seed", C.c_uint32), ("tile_logsize", C.c_uint32)]
 
 
 class Stats(C.Structure):

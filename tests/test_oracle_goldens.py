@@ -72,3 +72,14 @@ def test_raster_binning_granularity_is_semantic(oracle_lib):
     assert int((a != b).sum()) == 1
     ref = _png(f"{GOLDEN}/draw3d/mouse_ref_128.png")
     assert po.compare_images(po.argb_to_rgba_image(a), ref, tol=0) == 0
+
+
+@pytest.mark.parametrize("size,k", [(s, 5) for s in (8, 16, 32, 64, 128)] + [(128, 4), (128, 6)])
+def test_raster_app_coverage_oracle_matches_raster_golden(oracle_lib, size, k):
+    """The raster regression app's own image (white coverage over the
+    0xff000000 clear), at the CI's -k4/-k5/-k6 (ci/regression.sh.in:184-189)."""
+    po = oracle_lib
+    sc = po.OracleScene(po.cgltrace.load(scene_path("triangle")))
+    fb = po.raster_coverage(sc, size, size, k)
+    ref = po.load_png_argb(f"{GOLDEN}/raster/coverage_triangle_ref_{size}.png")
+    assert np.array_equal(fb[::-1], ref)
