@@ -279,9 +279,10 @@ class Run:
                 fg.start(slot)
         self.gather = gather
 
-    def step(self):
-        self.r.start()
-        if self.gather is not None:
+    def step(self, render=True, exchange=True):
+        if render:
+            self.r.start()
+        if exchange and self.gather is not None:
             self.gather()
 
     def drain(self):
@@ -290,13 +291,14 @@ class Run:
             for slot in range(self.slots):
                 self.fg.reclaim(slot)
 
-    def timed(self, steps, warmup, dist):
+    def timed(self, steps, warmup, dist, render=True, exchange=True):
         """W untimed steps, then EXACTLY `steps` steps between barrier +
         synchronize on both sides; returns (elapsed s, kernel ms avg, timed
-        launches)."""
+        launches).  render / exchange = False leave that half out of every
+        step (N > 1: the render and the frame exchange timed apart)."""
         import torch
         for _ in range(warmup):
-            self.step()
+            self.step(render, exchange)
         self.drain()
         if dist is not None:
             dist.barrier()
@@ -306,7 +308,7 @@ class Run:
         try:
             t0 = time.perf_counter()
             for _ in range(steps):
-                self.step()
+                self.step(render, exchange)
             self.drain()  # every frame rendered (and gathered + assembled) inside the region
             torch.cuda.synchronize()
             if dist is not None:
@@ -315,6 +317,8 @@ class Run:
         finally:
             gc.enable()
         ms1, nt1, n1 = self.r.run_totals()
+        if not render:
+            return elapsed, None, 0
         assert n1 - n0 == steps and nt1 > nt0, (n0, n1, nt0, nt1)
         return elapsed, (ms1 - ms0) / (nt1 - nt0), nt1 - nt0
 
@@ -452,6 +456,20 @@ def main():
     ms_per_step = elapsed / args.steps * 1e3
     value = rays_total * args.steps / elapsed / 1e6
     achieved = alg_bytes / (avg_kernel_ms * 1e-3) / 1e9
+    # N > 1: the same steps with only the render, and with only the frame
+    # exchange (gather of the last frame + assembly), max over ranks -- which
+    # half sets the step time at this N
+    split = None
+    if use_gather:
+        split_steps = max(20, min(args.steps, 500))
+        e_r, _, _ = run.timed(split_steps, 5, dist, exchange=False)
+        e_x, _, _ = run.timed(split_steps, 5, dist, render=False)
+        e_r, _ = reduce_max_sum(dist, coll_dev, e_r, 0)
+        e_x, _ = reduce_max_sum(dist, coll_dev, e_x, 0)
+        split = {"steps": split_steps, "render_ms_per_step": round(e_r / split_steps * 1e3, 5),
+                 "exchange_ms_per_step": round(e_x / split_steps * 1e3, 5),
+                 "exchange": "torch.distributed gather (RCCL) of the compact tile buffers + "
+                             "rt_frame_assemble on rank 0, pipelined over 4 slots"}
     gather_ok = None
     if use_gather and args.verify_gather:
         image = run.fg.image.cpu().numpy() if rank == 0 else None
@@ -615,6 +633,8 @@ def main():
                                     "work_executed": work, "note": "no current PMC record"})
     if gather_ok is not None:
         out["config"]["gather_verified"] = gather_ok
+    if split is not None:
+        out["config"]["step_split"] = split
     if n_gpus == 1 and not args.no_cpu_baseline:
         try:
             out["cpu_baseline"] = cpu_baseline(shadows, side, light, args.cpu_budget, path,

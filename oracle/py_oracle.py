@@ -239,9 +239,9 @@ def rt_params(width, height, shadows=True, light=(0.0, 60.0, 80.0), nthreads=1,
     # the product resolves primary visibility from per-block candidate lists
     # (its default, primary+shadow and path frames)
     p.vis_lists = (0 if vis_per_lane else 1) if vis_lists is None else int(bool(vis_lists))
-    # the product's shadow rays of primary+shadow frames test the light-space
-    # lists (its default with the device setup)
-    p.shadow_lists = int(bool(shadows and not path) if shadow_lists is None else bool(shadow_lists))
+    # the product's shadow rays (primary+shadow frames and every path vertex)
+    # test the light-space lists (its default with the device setup)
+    p.shadow_lists = int(bool(shadows or path) if shadow_lists is None else bool(shadow_lists))
     p.width, p.height = width, height
     p.flags = (RT_SHADOWS if shadows else 0) | (RT_PATH if path else 0)
     p.bounces, p.seed = bounces, seed

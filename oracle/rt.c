@@ -740,6 +740,9 @@ static int trace_any(const rt_ctx_t* c, const float o[3], const float d[3], floa
                 : brute_trace(c, o, d, tmin, tmax, anyhit, skip, t, &k->tri_tests);
 }
 
+static int sl_occluded(const rt_ctx_t* c, const float so[3], const float sd[3], int skip,
+                       uint64_t* tests);
+
 static uint32_t path_trace(const rt_ctx_t* c, uint32_t px, const float d0[3], float t0, int g,
                            uint32_t alb0, orc_rt_counters_t* k) {
   const float k255 = 1.0f / 255.0f;
@@ -758,7 +761,9 @@ static uint32_t path_trace(const rt_ctx_t* c, uint32_t px, const float d0[3], fl
     const float sd[3] = {c->p.light[0] - P[0], c->p.light[1] - P[1], c->p.light[2] - P[2]};
     float ts;
     ++k->shadow_rays;
-    if (trace_any(c, P, sd, 0.0f, 1.0f, 1, pid, &ts, k) >= 0) {
+    /* the light-space lists when built (the kernels' occluded_list), else the BVH */
+    if (c->sl_idx ? sl_occluded(c, P, sd, pid, &k->tri_tests)
+                  : trace_any(c, P, sd, 0.0f, 1.0f, 1, pid, &ts, k) >= 0) {
       ++k->occluded;
     } else {
       const float cosl = dot3(n, sd) / sqrtf(dot3(sd, sd));
@@ -1084,7 +1089,7 @@ static int rt_run(const orc_scene_t* scene, const orc_bvh_t* bvh, const orc_rt_p
   c.bvh = bvh;
   vis_build_nodes(&c);
   /* (BVH mode only: the flat image's shadow rays test the whole list) */
-  if (bvh && p->shadow_lists && !(p->flags & ORC_RT_PATH) && (p->flags & ORC_RT_SHADOWS)) sl_build(&c);
+  if (bvh && p->shadow_lists && (p->flags & (ORC_RT_PATH | ORC_RT_SHADOWS))) sl_build(&c);
   c.color = color; c.pid = pid; c.tout = t;
   const uint32_t nt = p->nthreads > 1 ? p->nthreads : 1;
   if (bvh && !p->vis_per_lane && p->row_begin == 0 && p->row_end == 0 && p->row_step <= 1) {

@@ -9,7 +9,8 @@
 // to 0, OM DCR state of :153-190, start, wait, read back, save flipped) and
 // the same verdict lines ("PASSED!" / "FAILED!", exit code = the error count).
 // The default kernel file is om.vxbin beside this executable (the reference's
-// default is kernel.vxbin in the working directory).
+// default is kernel.vxbin in the working directory); the reference image
+// resolves through RT_ASSETS_PATHS like ResolveFilePath (app/assets.h).
 #include <getopt.h>
 #include <unistd.h>
 
@@ -21,6 +22,7 @@
 #include <vector>
 
 #include "VX_types.h"
+#include "assets.h"
 #include "png.h"
 #include "vortex.h"
 
@@ -184,7 +186,7 @@ int main(int argc, char** argv) {
   if (reference_file) {
     std::vector<uint32_t> out, ref;
     uint32_t ow = 0, oh = 0, rw = 0, rh = 0;
-    if (rt::LoadPngARGB(output_file, &out, &ow, &oh) || rt::LoadPngARGB(reference_file, &ref, &rw, &rh) ||
+    if (rt::LoadPngARGB(output_file, &out, &ow, &oh) || rt::LoadPngARGB(rt::ResolveAsset(reference_file), &ref, &rw, &rh) ||
         ow != rw || oh != rh) {
       std::printf("FAILED!\n");
       return -1;

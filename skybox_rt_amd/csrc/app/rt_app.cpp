@@ -892,13 +892,13 @@ int rt_renderer_configure(rt_renderer_h r, const rt_render_params_t* p) {
   } else if (host_setup(r, p, raster, order_on, lists, &heavy) != 0) {
     return -1;
   }
-  // shadow rays of primary+shadow frames: light-space lists (built on the
-  // device for this light; env RT_SHADOW_LISTS=0 keeps the BVH packet walk;
-  // the host setup path walks the BVH)
+  // shadow rays (primary+shadow frames, every path vertex): light-space
+  // lists (built on the device for this light; env RT_SHADOW_LISTS=0 keeps
+  // the BVH walks; the host setup path walks the BVH)
   a.slist_on = 0;
   r->setup.slist_entries = 0;
   const char* sle = std::getenv("RT_SHADOW_LISTS");
-  if (device && !raster && !(p->flags & (RT_RENDER_FLAT | RT_RENDER_PATH)) && (p->flags & RT_RENDER_SHADOWS) &&
+  if (device && !raster && !(p->flags & RT_RENDER_FLAT) && (p->flags & (RT_RENDER_SHADOWS | RT_RENDER_PATH)) &&
       a.num_geom > 0 && !(sle && std::atoi(sle) == 0)) {
     if (rtapp::shadow_lists(r, &launches) != 0) return -1;
     a.slist_on = r->sl_built ? 1u : 0u;

@@ -224,7 +224,9 @@ __device__ __forceinline__ bool path_step(const Scene& S, int32_t* stack, PathSt
   ray_setup(s);
   cnt.shadow += act;
   float ts;
-  const bool occ = act && trace<true>(S, s, 0.0f, 1.0f, st.pid, tie_high, &ts, stack, cnt) >= 0;
+  // the light-space lists when built (occluded_list), else the BVH
+  const bool occ = S.slist_on ? occluded_list(S, s, act, st.pid, cnt)
+                              : act && trace<true>(S, s, 0.0f, 1.0f, st.pid, tie_high, &ts, stack, cnt) >= 0;
   cnt.occluded += occ;
   if (act && !occ) {
     const float cosl = dot3(nrm, s.d) / sqrtf(dot3(s.d, s.d));
@@ -461,8 +463,9 @@ __device__ __forceinline__ void lane_path(const vx_task_t& task, const Scene& S,
   task_pixel(S, t, &x, &y, &lb);
   const bool in = x < S.width && y < S.height;
   // paired vertices (path_step_pair) when the whole wave is here and its
-  // upper 32 lanes hold no pixel -- wave-uniform
-  const bool pair = __ballot(1) == ~0ull && (__ballot(in) >> 32) == 0;
+  // upper 32 lanes hold no pixel -- wave-uniform; not with the light-space
+  // shadow lists (a list scan and a BVH walk cannot share one traversal loop)
+  const bool pair = !S.slist_on && __ballot(1) == ~0ull && (__ballot(in) >> 32) == 0;
   cnt.primary += in;
   const bool tie_high = (S.flags & RT_FLAG_TIE_HIGH) != 0;
   // primary visibility: the raster's winner at this pixel (trace_primary)

@@ -126,3 +126,40 @@ def test_rtapp_rank_mode_world_size_1(tmp_path):
                          capture_output=True, text=True, timeout=300)
     assert out.returncode == 0, out.stdout + out.stderr
     assert "communicator: 1 ranks" in out.stdout and "PASSED!" in out.stdout
+
+
+def test_torch_and_c_abi_exchanges_give_identical_frames():
+    """The two bindings of the frame exchange -- bench.py's torch FrameGather
+    and the C-ABI rt_render_gather C hosts use (librt_shard.so) -- return the
+    same frame, frame after frame (three lights, so the frames differ), at
+    world size 1 over RCCL, and each equals the full render."""
+    import torch
+    import torch.distributed as dist
+    from skybox_rt_amd.shard import FrameGather, ShardComm
+    s = rt.Scene.load(scene_path("tekkaman"))
+    r = rt.Renderer(s)
+    side = 512
+    dev = torch.device("cuda", torch.cuda.current_device())
+    dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{_free_port()}", rank=0,
+                            world_size=1, device_id=dev)
+    comm = ShardComm(ShardComm.unique_id(), 0, 1, 0)
+    try:
+        fg = FrameGather(dist, side, side, dev)
+        for light in ((0.0, 60.0, 80.0), (-40.0, 30.0, 60.0), (25.0, -10.0, 120.0)):
+            r.configure(side, side, shadows=True, light=light)
+            r.render()
+            full = r.framebuffer().copy()
+            r.configure(side, side, shadows=True, light=light, shard_index=0, shard_count=1,
+                        compact=True)
+            r.render()
+            c_img = r.gather(comm)
+            t_img = fg(torch.from_numpy(r.framebuffer().view(np.int32)).to(dev))
+            torch.cuda.synchronize()
+            t_img = t_img.cpu().numpy().view(np.uint32).reshape(side, side)
+            assert np.array_equal(c_img, t_img), light
+            assert np.array_equal(c_img, full), light
+    finally:
+        comm.close()
+        dist.destroy_process_group()
+        r.close()
+        s.close()

@@ -83,3 +83,31 @@ def test_vx_dump_perf_in_process(tmp_path, cls):
     assert any(f"class {cls}: " in ln and "vx_main launches profiled" in ln for ln in lines), lines
     key = "scheduler idle=" if cls == 1 else "dcache reads="
     assert any(key in ln for ln in lines), lines
+
+
+GFX_APPS = {  # the CI's --perf=<class> runs (ci/regression.sh.in:142,165,183)
+    3: ("texapp", ["-i", "soccer.png", "-r", "soccer_ref_g1.png", "-g1"], "tex", "tex memory reads="),
+    4: ("rasterapp", ["-t", "triangle.cgltrace"], "scenes", "rcache read misses="),
+    5: ("omapp", ["-r", "whitebox_128.png"], "om", "om memory writes="),
+}
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("cls", sorted(GFX_APPS))
+def test_vx_dump_perf_graphics_classes(tmp_path, cls):
+    """Classes 3 (TEX), 4 (RASTER), 5 (OM) (runtime/stub/utils.cpp:587-640,
+    725-790) printed in process by the app the reference CI profiles with that
+    class: texapp, rasterapp, omapp."""
+    import subprocess
+    exe, args, sub, key = GFX_APPS[cls]
+    env = dict(os.environ, VORTEX_PROFILING=str(cls), VX_DUMP_PERF="1",
+               RT_ASSETS_PATHS=os.path.join(ROOT, "tests", "golden", sub))
+    out = subprocess.run([os.path.join(ROOT, "skybox_rt_amd", "lib", exe)] + args +
+                         ["-o", str(tmp_path / "o.png")], env=env, capture_output=True, text=True,
+                         timeout=120, cwd=str(tmp_path))
+    assert out.returncode == 0, out.stdout + out.stderr
+    lines = _perf_lines(out.stdout)
+    assert any(key in ln for ln in lines), lines
+    assert any(f"class {cls}: " in ln and "vx_main launches profiled" in ln for ln in lines), lines
+    n = int([ln for ln in lines if ln.startswith("PERF: instrs=")][0].split("instrs=")[1].split(",")[0])
+    assert n > 0
