@@ -42,6 +42,9 @@
 #else
 #define PT_BLOCK 64
 #endif
+#ifndef PT_PAIR
+#define PT_PAIR 1        // 0: no paired-vertex code (the shadow lists never pair)
+#endif
 #define PT_SKY 0.25f     // radiance of an escaped bounce ray (oracle ORC_PT_SKY)
 #define PT_TRIES 8u      // disk rejection-sampling attempts (ORC_PT_TRIES)
 
@@ -465,7 +468,7 @@ __device__ __forceinline__ void lane_path(const vx_task_t& task, const Scene& S,
   // paired vertices (path_step_pair) when the whole wave is here and its
   // upper 32 lanes hold no pixel -- wave-uniform; not with the light-space
   // shadow lists (a list scan and a BVH walk cannot share one traversal loop)
-  const bool pair = !S.slist_on && __ballot(1) == ~0ull && (__ballot(in) >> 32) == 0;
+  const bool pair = PT_PAIR && !S.slist_on && __ballot(1) == ~0ull && (__ballot(in) >> 32) == 0;
   cnt.primary += in;
   const bool tie_high = (S.flags & RT_FLAG_TIE_HIGH) != 0;
   // primary visibility: the raster's winner at this pixel (trace_primary)
@@ -521,7 +524,11 @@ __device__ __forceinline__ void flush(int slot, uint32_t v) { vx_mpm_add(RT_MPM_
 __device__ __attribute__((used)) uint32_t __vx_grid_per_cu = PT_GRID_PER_CU;
 #endif
 
+#ifdef PT_WAVES_PER_EU
+VX_MAIN_OCC(rt_kernel_arg_t, arg, PT_BLOCK, PT_WAVES_PER_EU) {
+#else
 VX_MAIN(rt_kernel_arg_t, arg, PT_BLOCK) {
+#endif
   __shared__ PtLds s_pt;
 #ifdef RT_STAMPS  // diagnostic image: per-wave start/end timestamps (scripts/wave_timeline.py)
   const uint64_t t_stamp0 = __builtin_amdgcn_s_memrealtime();

@@ -326,12 +326,14 @@ __device__ __forceinline__ void flush(int slot, uint32_t v) { vx_mpm_add(RT_MPM_
 
 }  // namespace
 
-// primary + shadow images: registers for 5 waves per SIMD (<= 96 VGPRs, no
-// spills) -- A/B (profiles/r02/ab_occupancy_r02z.json): 0.0418 -> 0.0408 ms;
-// capping occupancy lower (LDS padding to 11 / 7 waves per CU) costs +27 /
-// +80 %: the frame is throughput-bound, not the heavy waves' issue share
+// primary + shadow images: registers for 7 waves per SIMD (<= 72 VGPRs: 67,
+// 22 SGPR spills) -- A/B on the light-space-list image (r03g, same frames):
+// 5 (71 VGPRs, 6-7 resident) 0.02574 ms, 7 0.02470, 8 (64 VGPRs, 39 SGPR
+// spills) 0.02532: the frame is latency-bound with the chip full of waves
+// (DESIGN 4.1), so more resident waves win until the spills cost more.
+// (r02: capping occupancy lower with LDS padding cost +27 / +80 %.)
 #if !defined(RT_WAVES_PER_EU) && !RT_FLAT
-#define RT_WAVES_PER_EU 5
+#define RT_WAVES_PER_EU 7
 #endif
 #ifdef RT_WAVES_PER_EU
 VX_MAIN_OCC(rt_kernel_arg_t, arg, RT_BLOCK_THREADS, RT_WAVES_PER_EU) {

@@ -294,7 +294,8 @@ class vx_device {
     if (upload) wait_idle();
     // bounded queue: with depth_ + time_every_ - 1 runs in flight, retire up
     // to the oldest timed one (at least depth_ - 1 stay queued behind it)
-    while (launch_mode_ != 2 && issued_ - retired_ >= (uint64_t)(depth_ + time_every_ - 1)) {
+    while (launch_mode_ != 2 && group_pos_ == 0 &&
+           issued_ - retired_ >= (uint64_t)(depth_ + time_every_ - 1) * group_n_) {
       uint64_t j = retired_ + 1;
       while (j <= issued_ && !timed_[(j - 1) % kMaxQueue]) ++j;
       if (retire(j <= issued_ ? j : issued_, VX_MAX_TIMEOUT) != 0) return -1;
@@ -312,9 +313,23 @@ class vx_device {
     const int slot = (int)(issued_ % kMaxQueue);
     // a run is timed (events) when it starts on an idle queue -- every run of
     // a start + wait loop -- and then every time_every_-th run: an event
-    // costs ~5 us of idle device between back-to-back runs (measured)
-    const bool timed = launch_mode_ != 2 && (issued_ == retired_ || issued_ % time_every_ == 0);
-    timed_[slot] = timed;
+    // costs ~5 us of idle device between back-to-back runs (measured).  A
+    // run is a group of group_n_ launches (vx_hip_launch_group: one frame of
+    // several kernels): timed as a whole, the start event on its first
+    // launch, the stop event on its last.
+    const bool first = group_pos_ == 0, last = group_pos_ + 1 == group_n_;
+    if (first) {
+      group_timed_ = launch_mode_ != 2 &&
+                     (issued_ == retired_ || (issued_ / group_n_) % time_every_ == 0);
+      group_slot_ = slot;
+      group_mods_.clear();
+    }
+    group_mods_.push_back({m, m->grid, rows});
+    const bool timed = group_timed_;
+    timed_[slot] = timed && last;  // the run completes (and is timed) with its last launch
+    group_last_[slot] = last;
+    group_first_slot_[slot] = group_slot_;
+    group_pos_ = last ? 0 : group_pos_ + 1;
     if (!timed) {
       HIP_CHECK(hipExtModuleLaunchKernel(m->entry, m->grid * m->block, 1, 1, m->block, 1, 1, 0,
                                          stream_, nullptr, nullptr, nullptr, nullptr, 0));
@@ -325,13 +340,14 @@ class vx_device {
       // the dispatch packet itself carries the start/stop timestamps: no
       // separate event packets between back-to-back frames
       HIP_CHECK(hipExtModuleLaunchKernel(m->entry, m->grid * m->block, 1, 1, m->block, 1, 1, 0,
-                                         stream_, nullptr, nullptr, ev_start_[slot],
-                                         ev_stop_[slot], 0));
+                                         stream_, nullptr, nullptr,
+                                         first ? ev_start_[slot] : nullptr,
+                                         last ? ev_stop_[slot] : nullptr, 0));
     } else {
-      HIP_CHECK(hipEventRecord(ev_start_[slot], stream_));
+      if (first) HIP_CHECK(hipEventRecord(ev_start_[slot], stream_));
       HIP_CHECK(hipModuleLaunchKernel(m->entry, m->grid, 1, 1, m->block, 1, 1, 0, stream_,
                                       nullptr, nullptr));
-      HIP_CHECK(hipEventRecord(ev_stop_[slot], stream_));
+      if (last) HIP_CHECK(hipEventRecord(ev_stop_[slot], stream_));
     }
     ++issued_;
     mpm_dirty_ = true;  // read back lazily by mpm_query (after wait_idle)
@@ -372,10 +388,11 @@ class vx_device {
     }
     for (; retired_ < upto; ++retired_) {
       const int slot = (int)(retired_ % kMaxQueue);
+      if (!group_last_[slot]) continue;  // a run = a whole launch group
       ++runs_total_;
       if (!timed_[slot]) continue;
       float ms = 0.0f;
-      HIP_CHECK(hipEventElapsedTime(&ms, ev_start_[slot], ev_stop_[slot]));
+      HIP_CHECK(hipEventElapsedTime(&ms, ev_start_[group_first_slot_[slot]], ev_stop_[slot]));
       last_ms_ = ms;
       run_ms_total_ += ms;
       ++runs_timed_;
@@ -406,19 +423,23 @@ class vx_device {
     }
     if (mpm_dirty_ && last_module_) {
       for (uint32_t i = 0; i < VX_MPM_COUNT; ++i) mpm_[i] = 0;
-      if (last_rows_) {  // sum the per-block counter rows of the last launch
-        rows_.resize((size_t)last_grid_ * kMpmRow);
-        HIP_CHECK(hipMemcpyAsync(rows_.data(), last_module_->mpm, rows_.size() * sizeof(uint32_t),
-                                 hipMemcpyDeviceToHost, stream_));
-        HIP_CHECK(hipStreamSynchronize(stream_));
-        for (size_t b = 0; b < last_grid_; ++b)
-          for (uint32_t i = 0; i < kMpmRow; ++i) mpm_[i] += rows_[b * kMpmRow + i];
-      } else {  // counters off: the task count the launch declared
-        uint32_t tasks = 0;
-        HIP_CHECK(hipMemcpyAsync(&tasks, (uint8_t*)last_module_->mpm + kTasksOffset, 4,
-                                 hipMemcpyDeviceToHost, stream_));
-        HIP_CHECK(hipStreamSynchronize(stream_));
-        mpm_[VX_CSR_MINSTRET - VX_CSR_MPM_BASE] = tasks;
+      // every launch of the last run (launch group): their modules are
+      // distinct images, each with its own counter slab
+      for (const GroupLaunch& g : group_mods_) {
+        if (g.rows) {  // sum the per-block counter rows of the launch
+          rows_.resize((size_t)g.grid * kMpmRow);
+          HIP_CHECK(hipMemcpyAsync(rows_.data(), g.m->mpm, rows_.size() * sizeof(uint32_t),
+                                   hipMemcpyDeviceToHost, stream_));
+          HIP_CHECK(hipStreamSynchronize(stream_));
+          for (size_t b = 0; b < g.grid; ++b)
+            for (uint32_t i = 0; i < kMpmRow; ++i) mpm_[i] += rows_[b * kMpmRow + i];
+        } else {  // counters off: the task count the launch declared
+          uint32_t tasks = 0;
+          HIP_CHECK(hipMemcpyAsync(&tasks, (uint8_t*)g.m->mpm + kTasksOffset, 4,
+                                   hipMemcpyDeviceToHost, stream_));
+          HIP_CHECK(hipStreamSynchronize(stream_));
+          mpm_[VX_CSR_MINSTRET - VX_CSR_MPM_BASE] += tasks;
+        }
       }
       mpm_dirty_ = false;
     }
@@ -438,6 +459,16 @@ class vx_device {
     return 0;
   }
   void set_counters(bool on) { counters_ = on; }  // applies from the next start()
+  // the next runs are groups of n launches (1 = every launch a run); waits
+  // for the queue, so groups never straddle a change
+  int launch_group(uint32_t n) {
+    if (n < 1 || n > 4) return -1;
+    if (n == group_n_ && group_pos_ == 0) return 0;
+    if (group_pos_ != 0) return -1;  // inside a group
+    wait_idle();
+    group_n_ = n;
+    return 0;
+  }
   bool counters() const { return counters_ || counters_env_; }
   void* mem_ptr(uint64_t addr) { return arena_ + addr; }
   hipStream_t stream() const { return stream_; }
@@ -534,9 +565,22 @@ class vx_device {
   std::map<uint64_t, Module> modules_;
   std::map<uint64_t, uint64_t> image_key_;  // image address -> module key
   hipStream_t stream_ = nullptr;
-  static constexpr int kMaxQueue = 32;  // >= depth_ + time_every_
+  static constexpr int kMaxQueue = 64;  // >= (depth_ + time_every_) * group_n_
   hipEvent_t ev_start_[kMaxQueue] = {}, ev_stop_[kMaxQueue] = {};
   bool timed_[kMaxQueue] = {};
+  // launch groups (vx_hip_launch_group): group_n_ consecutive launches form
+  // one run (a frame of several kernels)
+  struct GroupLaunch {
+    Module* m;
+    uint32_t grid;
+    bool rows;
+  };
+  uint32_t group_n_ = 1, group_pos_ = 0;
+  bool group_timed_ = false;
+  int group_slot_ = 0;
+  bool group_last_[kMaxQueue] = {};
+  int group_first_slot_[kMaxQueue] = {};
+  std::vector<GroupLaunch> group_mods_;
   int time_every_ = 4;
   uint64_t runs_timed_ = 0;
   uint64_t issued_ = 0, retired_ = 0;  // runs started / retired (events read)
@@ -694,6 +738,10 @@ __attribute__((visibility("default"))) int vx_hip_set_counters(vx_device_h hdevi
   if (hdevice == nullptr) return -1;
   ((vx_device*)hdevice)->set_counters(enable != 0);
   return 0;
+}
+__attribute__((visibility("default"))) int vx_hip_launch_group(vx_device_h hdevice, uint32_t n) {
+  if (hdevice == nullptr) return -1;
+  return ((vx_device*)hdevice)->launch_group(n);
 }
 __attribute__((visibility("default"))) int vx_hip_device_id(vx_device_h hdevice, int* id) {
   if (hdevice == nullptr || id == nullptr) return -1;
