@@ -207,6 +207,9 @@ typedef struct {
   uint32_t blist_max;     /* the longest list */
   uint32_t slist_on;      /* 1: shadow rays test the light-space lists (rt_common.h) */
   uint64_t slist_entries; /* light-space shadow list entries */
+  uint32_t path_queue;    /* 1: RT_RENDER_PATH runs in two kernels (pt_primary + pt_queue: a
+                             frame is one launch group of 2, vortex_hip.h) */
+  uint32_t pad;
 } rt_setup_stats_t;
 int rt_renderer_setup_stats(rt_renderer_h r, rt_setup_stats_t* stats);
 

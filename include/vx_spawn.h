@@ -146,6 +146,11 @@ struct vx_arena {
   __device__ __forceinline__ void st_u32(uint32_t off, uint32_t v) const {
     __builtin_amdgcn_raw_buffer_store_b32(v, r, off, 0, 0);
   }
+  __device__ __forceinline__ void st_u4(uint32_t off, uint4 v) const {
+    typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+    const u32x4 w = {v.x, v.y, v.z, v.w};
+    __builtin_amdgcn_raw_buffer_store_b128(w, r, off, 0, 0);
+  }
 };
 
 /* hardware identity (vx_intrinsics.h vx_core_id/vx_warp_id/vx_thread_id) */

@@ -105,6 +105,9 @@ typedef struct {
                                        kernels' block_primary) */
   uint32_t shadow_lists;            /* primary+shadow: shadow rays test the light-space cell
                                        lists (rt.c sl_build, the kernels' occluded_list) */
+  uint32_t path_queue;              /* path trace in two kernels (pt_primary + pt_queue): the
+                                       primary pass runs 8x8 blocks everywhere (no 32-pixel
+                                       waves in geometry tiles) */
 } orc_rt_params_t;
 
 #define ORC_RT_SHADOWS 0x1u

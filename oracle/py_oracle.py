@@ -53,7 +53,7 @@ class RtParamsC(C.Structure):
                 ("bounces", C.c_uint32), ("seed", C.c_uint32), ("nthreads", C.c_uint32),
                 ("row_begin", C.c_uint32), ("row_end", C.c_uint32), ("row_step", C.c_uint32),
                 ("vis_per_lane", C.c_uint32), ("vis_lists", C.c_uint32),
-                ("shadow_lists", C.c_uint32)]
+                ("shadow_lists", C.c_uint32), ("path_queue", C.c_uint32)]
 
 
 class RtCountersC(C.Structure):
@@ -233,7 +233,7 @@ def shadow_lists(oscene: OracleScene, light=(0.0, 60.0, 80.0)):
 def rt_params(width, height, shadows=True, light=(0.0, 60.0, 80.0), nthreads=1,
               clear_color=CLEAR_COLOR, row_begin=0, row_end=0, row_step=0,
               path=False, bounces=4, seed=PT_SEED, vis_per_lane=False, vis_lists=None,
-              shadow_lists=None):
+              shadow_lists=None, path_queue=None):
     p = RtParamsC()
     p.vis_per_lane = 1 if vis_per_lane else 0
     # the product resolves primary visibility from per-block candidate lists
@@ -242,6 +242,9 @@ def rt_params(width, height, shadows=True, light=(0.0, 60.0, 80.0), nthreads=1,
     # the product's shadow rays (primary+shadow frames and every path vertex)
     # test the light-space lists (its default with the device setup)
     p.shadow_lists = int(bool(shadows or path) if shadow_lists is None else bool(shadow_lists))
+    # the product path-traces in two kernels (its default with the lists):
+    # the primary pass counts per 8x8 block everywhere
+    p.path_queue = int(bool(path) if path_queue is None else bool(path_queue))
     p.width, p.height = width, height
     p.flags = (RT_SHADOWS if shadows else 0) | (RT_PATH if path else 0)
     p.bounces, p.seed = bounces, seed

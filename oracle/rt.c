@@ -450,7 +450,7 @@ static void vis_trace_packet(const rt_ctx_t* c, int n, const uint32_t* px, const
  * iff some geometry primitive covers a pixel of it (the host's split rule,
  * rt_app.cpp: tiles any covered-pixel rectangle reaches) */
 static int tile_split(const rt_ctx_t* c, uint32_t tx, uint32_t ty) {
-  if (!(c->p.flags & ORC_RT_PATH)) return 0;
+  if (!(c->p.flags & ORC_RT_PATH) || c->p.path_queue) return 0;
   const uint32_t x0 = tx * 32, x1 = x0 + 31, y0 = ty * 32, y1 = y0 + 31;
   for (int k = 0; k < c->num_geom; ++k) {
     const orc_vis_prim_t* v = &c->vis[c->geom[k]];

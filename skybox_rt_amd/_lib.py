@@ -28,7 +28,8 @@ REQUIRED = ("libvortex.so", "libvortex-hip.so", "librtapp.so", "rtapp",
             "rt_flat.vxbin", "rt_flat_stats.vxbin", "raster_kernel.vxbin",
             "pt_compact/pt_kernel.vxbin", "pt_compact/pt_kernel_stats.vxbin",
             "tex_kernel_f0.vxbin", "tex_kernel_f1.vxbin", "tex_kernel_f2.vxbin", "texapp", "bvh_build.vxbin",
-            "librt_shard.so", "rt_setup.vxbin", "bvh_sah.vxbin", "om.vxbin", "omapp", "rasterapp")
+            "librt_shard.so", "rt_setup.vxbin", "bvh_sah.vxbin", "om.vxbin", "omapp", "rasterapp",
+            "pt_primary.vxbin", "pt_primary_stats.vxbin", "pt_queue.vxbin", "pt_queue_stats.vxbin")
 
 
 class NativeLibraryMissing(RuntimeError):

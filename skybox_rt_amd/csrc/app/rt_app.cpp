@@ -291,6 +291,23 @@ int rt_renderer_create(rt_scene_h s, const char* kernel_dir, rt_renderer_h* out)
   r->mpm_rows = (vx_hip_mpm_rows_t)vx_driver_symbol("vx_hip_mpm_rows");
   r->run_totals = (vx_hip_run_totals_t)vx_driver_symbol("vx_hip_run_totals");
   r->set_counters = (vx_hip_set_counters_t)vx_driver_symbol("vx_hip_set_counters");
+  r->launch_group = (vx_hip_launch_group_t)vx_driver_symbol("vx_hip_launch_group");
+  // the two-kernel path tracer's images (binary16 BVH4 only; the others run
+  // the one-kernel pt_kernel images), from the kernel directory itself: a
+  // directory without them (e.g. lib/pt_compact) runs its own pt_kernel
+  if (!deep) {
+    const char* pq_names[2][2] = {{"pt_primary.vxbin", "pt_primary_stats.vxbin"},
+                                  {"pt_queue.vxbin", "pt_queue_stats.vxbin"}};
+    bool all = true;
+    for (int m = 0; m < 2; ++m)
+      for (int i = 0; i < 2; ++i)
+        if (FILE* f = std::fopen((dir + "/" + pq_names[m][i]).c_str(), "rb")) std::fclose(f);
+        else all = false;
+    for (int m = 0; m < 2 && all; ++m)
+      for (int i = 0; i < 2; ++i)
+        if (vx_upload_kernel_file(r->dev, (dir + "/" + pq_names[m][i]).c_str(), &r->krnl_pq[m][i]) != 0)
+          return fail("cannot upload kernel " + dir + "/" + pq_names[m][i]);
+  }
   rt_kernel_arg_t& a = r->arg;
   std::memset(&a, 0, sizeof(a));
   // 3 padding records: the kernel fetches all 4 slots of a leaf at once
@@ -857,6 +874,11 @@ int rt_renderer_configure(rt_renderer_h r, const rt_render_params_t* p) {
   if (!raster && !(p->flags & RT_RENDER_FLAT) && !(a.flags & RT_FLAG_BVH4H) && !r->deep &&
       load_deep_images(r) != 0)
     return -1;
+  // path tracing in two kernels (pt_primary, pt_queue) on the binary16 BVH4
+  // images; env RT_PT_QUEUE=0 keeps the one-kernel pt_kernel
+  const char* pqe = std::getenv("RT_PT_QUEUE");
+  r->pq = (p->flags & RT_RENDER_PATH) && !r->deep && (a.flags & RT_FLAG_BVH4H) && r->krnl_pq[0][0] &&
+          r->launch_group && !(pqe && std::atoi(pqe) == 0);
   a.bounces = p->bounces;
   a.seed = p->seed;
   a.clear_color = p->clear_color;
@@ -911,7 +933,7 @@ int rt_renderer_configure(rt_renderer_h r, const rt_render_params_t* p) {
     // shadow rays it measured slower (0.071 -> 0.086 ms: the shadow rays then
     // also trace in half-empty waves), so off there.  RT_SPLIT_TILES=n
     // overrides the count, 0 disables.
-    uint32_t split = (p->flags & RT_RENDER_PATH) ? heavy : 0u;
+    uint32_t split = (p->flags & RT_RENDER_PATH) && !r->pq ? heavy : 0u;
     if (const char* e = std::getenv("RT_SPLIT_TILES"))
       split = std::min<uint32_t>((uint32_t)std::atoi(e), r->local_tiles);
     a.split_tiles = split;
@@ -927,12 +949,24 @@ int rt_renderer_configure(rt_renderer_h r, const rt_render_params_t* p) {
     }
   }
   uint64_t args_addr = 0;
+  if (r->pq) {  // the path queue (uint4 per path start, at most one per local pixel) + counters
+    const uint32_t zero[16] = {};
+    uint64_t qa = 0, ca = 0;
+    if (upload(r->dev, nullptr, npx * 16, &r->pathq, &qa) ||
+        upload(r->dev, zero, sizeof(zero), &r->pathq_ctr, &ca))
+      return -1;
+    a.pathq_addr = qa;
+    a.pathq_ctr_addr = ca;
+  } else {
+    a.pathq_addr = a.pathq_ctr_addr = 0;
+  }
   if (upload(r->dev, &a, sizeof(a), &r->args, &args_addr)) return -1;
   r->setup.device = device ? 1u : 0u;
   r->setup.launches = launches;
   r->setup.heavy_tiles = heavy;
   r->setup.blist_blocks = a.blist_blocks;
   r->setup.slist_on = a.slist_on;
+  r->setup.path_queue = r->pq ? 1u : 0u;
   r->setup.setup_ms = setup_ms;
   r->setup.configure_ms = ms_since(t0);
   r->configured = true;
@@ -948,6 +982,14 @@ int rt_render_start(rt_renderer_h r) {
   if (r->set_counters &&
       r->set_counters(r->dev, (f & (RT_RENDER_COUNTERS | RT_RENDER_INSTRUMENTED)) ? 1 : 0) != 0)
     return fail("vx_hip_set_counters failed");
+  // a frame of the two-kernel path tracer is one launch group of 2
+  const uint32_t group = (mode == 1 && r->pq) ? 2u : 1u;
+  if (r->launch_group && r->launch_group(r->dev, group) != 0) return fail("vx_hip_launch_group failed");
+  if (group == 2)
+    return vx_start(r->dev, r->krnl_pq[0][k], r->args) == 0 &&
+                   vx_start(r->dev, r->krnl_pq[1][k], r->args) == 0
+               ? 0
+               : fail("vx_start failed");
   return vx_start(r->dev, r->krnl[mode][k], r->args) == 0 ? 0 : fail("vx_start failed");
 }
 

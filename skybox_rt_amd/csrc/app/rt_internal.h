@@ -33,6 +33,12 @@ struct rt_renderer {
   // kernel images [mode][instrumented]: mode 0 = primary+shadow (BVH),
   // 1 = path trace, 2 = flat list, 3 = raster (no instrumented image)
   vx_buffer_h krnl[4][2] = {};
+  // path tracing in two kernels (the default with the binary16 BVH4): [0]
+  // pt_primary (primary pass, path queue), [1] pt_queue (the queued paths);
+  // [.][1] the instrumented images
+  vx_buffer_h krnl_pq[2][2] = {};
+  vx_buffer_h pathq = nullptr, pathq_ctr = nullptr;
+  bool pq = false;          // the configuration runs the two-kernel path tracer
   vx_buffer_h nodes = nullptr, nodes4 = nullptr, tris = nullptr, layers = nullptr, dcs = nullptr, tex = nullptr;
   vx_buffer_h ptris = nullptr, geom = nullptr, oms = nullptr, bbox = nullptr, zbuf = nullptr;
   vx_buffer_h order = nullptr;
@@ -60,6 +66,7 @@ struct rt_renderer {
   vx_hip_mpm_rows_t mpm_rows = nullptr;
   vx_hip_run_totals_t run_totals = nullptr;
   vx_hip_set_counters_t set_counters = nullptr;
+  vx_hip_launch_group_t launch_group = nullptr;
   std::string kdir;         // kernel directory (images missing there come from lib_dir)
   bool deep = false;        // generic RT/PT images (every BVH layout, 32-entry stack)
   // the primary rays' tree of the current configuration (rt_renderer_export_vis_tree;
@@ -79,7 +86,8 @@ struct rt_renderer {
                            &ptris, &geom, &oms, &bbox, &zbuf, &order, &vnodes, &vtris, &vlayers,
                            &vgeom, &gather_recv, &gather_image, &prims, &cbuf, &args,
                            &setup_krnl, &verts, &pdc, &dcz, &layer_list, &geometry_list, &vis,
-                           &blist, &bidx, &sidx, &slist};
+                           &blist, &bidx, &sidx, &slist, &krnl_pq[0][0], &krnl_pq[0][1],
+                           &krnl_pq[1][0], &krnl_pq[1][1], &pathq, &pathq_ctr};
     for (auto* b : bufs) {
       if (*b) vx_mem_free(*b);
       *b = nullptr;

@@ -34,6 +34,9 @@
 // deepest paths (each extra bounce level adds ~0.08 ms whatever the number
 // of live paths), which compaction does not shorten and its barriers
 // lengthen.  Both images are parity-tested.
+// PT_MODE 2 (image pt_queue, with pt_primary): the second kernel of a
+// two-kernel frame -- the compacted path queue the first kernel filled, one
+// path per lane on full waves (rt_trace.h pathq_append).
 #ifndef PT_MODE
 #define PT_MODE 1
 #endif
@@ -456,6 +459,39 @@ __device__ __forceinline__ void bounces(const Scene& S, PtLds& L, Counters& cnt)
   __syncthreads();
 }
 
+#elif PT_MODE == 2
+
+// one queued path (pt_primary appended it: task, plane t, hit pid, primary
+// colour) on its own lane to the end; the other lanes of the wave hold the
+// paths queued next to it
+__device__ __forceinline__ void queued_path(const vx_task_t& task, const Scene& S, uint32_t q,
+                                            int32_t* stack, Counters& cnt) {
+  const uint4 e = S.A.ld_u4(q + 16u * task.task_id);
+  uint32_t x, y;
+  task_pixel(S, e.x, &x, &y);
+  Ray r;
+  primary_dir(S, x, y, r);
+  const uint32_t color = e.w;
+  const float k255 = 1.0f / 255.0f;
+  PathState st;
+  st.task = e.x;
+  st.alpha = color & 0xff000000u;
+  st.pid = (int32_t)e.z;
+  st.t = __uint_as_float(e.y);
+  st.T[0] = (float)((color >> 16) & 0xffu) * k255;
+  st.T[1] = (float)((color >> 8) & 0xffu) * k255;
+  st.T[2] = (float)(color & 0xffu) * k255;
+#pragma unroll
+  for (int k = 0; k < 3; ++k) {
+    st.o[k] = r.o[k];
+    st.d[k] = r.d[k];
+    st.L[k] = 0.0f;
+  }
+  for (uint32_t v = 0; path_step(S, stack, st, v, true, cnt); ++v) {
+  }
+  store_path_pixel(S, st);
+}
+
 #else  // PT_MODE == 1
 
 // one pixel's whole path on its own lane (no compaction)
@@ -519,7 +555,13 @@ __device__ __forceinline__ void flush(int slot, uint32_t v) { vx_mpm_add(RT_MPM_
 // per wave for the split heavy tiles too (r01: 96/CU, 0.2262 -> 0.2222 ms;
 // r02 after the scalar argument block: 128/CU 0.1765 vs 96/CU 0.1801 ms,
 // profiles/r02/ab_pt_grid.json; 64/CU is best for rt_kernel)
-#if PT_BLOCK == 64
+#if PT_MODE == 2
+// pt_queue: the waves that run queued paths are all resident at once (16
+// one-wave blocks per CU = 4 per SIMD at <= 128 VGPRs); a wave takes chunks
+// w, w + W, ... of the queue
+#define PT_GRID_PER_CU 16
+__device__ __attribute__((used)) uint32_t __vx_grid_per_cu = PT_GRID_PER_CU;
+#elif PT_BLOCK == 64
 #define PT_GRID_PER_CU 128
 __device__ __attribute__((used)) uint32_t __vx_grid_per_cu = PT_GRID_PER_CU;
 #endif
@@ -543,6 +585,28 @@ VX_MAIN(rt_kernel_arg_t, arg, PT_BLOCK) {
       arg->num_tasks,
       [&](const vx_task_t& task, bool valid, const Scene* s) { primary(task, valid, *s, s_pt, cnt); },
       [&](uint32_t, const Scene* s) { bounces(*s, s_pt, cnt); }, &S);
+#elif PT_MODE == 2
+  int32_t* stack = &s_pt.stack[threadIdx.x >> 6][0][lane_id()];
+  const PathQ Q = pathq_args(S);
+  // the paths the first kernel queued (a vector load: written by the
+  // previous launch, after this launch's cache invalidation)
+  const uint32_t n = __builtin_amdgcn_readfirstlane(S.A.ld_u32(Q.ctr));
+  const int rc = vx_spawn_tasks(
+      n, [&](const vx_task_t& task, const Scene* s) { queued_path(task, *s, Q.q, stack, cnt); }, &S);
+  // the last worker wave to finish zeroes the counters for the next frame
+  // (no wave waits on another: each counts itself done once)
+  const uint32_t nchunks = (n + VX_CHUNK - 1) / VX_CHUNK;
+  const uint32_t nwaves = gridDim.x * (blockDim.x >> 6);
+  const uint32_t wid = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+  const uint32_t workers = nchunks < nwaves ? nchunks : nwaves;
+  if (wid < workers && lane_id() == 0) {
+    uint32_t* ctr = vx_ptr<uint32_t>(Q.ctr);
+    __threadfence();
+    if (atomicAdd(&ctr[2], 1u) == workers - 1u) {
+      atomicExch(&ctr[0], 0u);
+      atomicExch(&ctr[2], 0u);
+    }
+  }
 #else
   int32_t* stack = &s_pt.stack[threadIdx.x >> 6][0][lane_id()];
   const int rc = vx_spawn_tasks(

@@ -202,6 +202,10 @@ typedef struct {
   uint64_t slist_addr;     // rt_tri_t per entry (+1 padding record): every cell's triangles, ascending pid
   uint32_t raster_bin_log; // raster mode: binning tile side 2^log (RASTER_TILE_LOGSIZE; draw3d -k)
   uint32_t pad_bin;
+  uint64_t pathq_addr;     // path tracing in two kernels (pt_primary + pt_queue): uint4 per path
+                           // start (task, plane t, hit pid, primary colour), compacted
+  uint64_t pathq_ctr_addr; // u32 [4]: [0] paths queued this frame, [2] pt_queue worker waves
+                           // done (the last one zeroes both for the next frame)
 } rt_kernel_arg_t;
 
 // ---- light-space shadow lists (shadow rays to the point light) ------------

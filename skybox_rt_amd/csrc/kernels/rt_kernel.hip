@@ -31,6 +31,9 @@
 #ifndef RT_FLAT
 #define RT_FLAT 0
 #endif
+#ifndef RT_PATHQ
+#define RT_PATHQ 0  // 1: image pt_primary, the path tracer's first kernel (rt_trace.h pathq_append)
+#endif
 #define RT_FLAT_CAP 1024  // rectangle words staged in LDS (16 KB); longer lists stream via s_load
 
 namespace {
@@ -104,6 +107,15 @@ __device__ __forceinline__ void kernel_body(const vx_task_t& task, const Scene& 
   Ray r;
   primary_dir(S, x, y, r);
   const float th = hit >= 0 ? plane_t(S, r, hit) : 0.0f;
+#if RT_PATHQ
+  // path tracing, first kernel: a path starts at the winner's plane; its
+  // pixel is written by pt_queue when the path ends
+  const bool path = hit >= 0 && secondary_ok(th);
+  pathq_append(S, path, t, th, hit, color);
+  if (in && !path) store_pixel(S, t, x, y, color);
+  (void)w;
+  return;
+#endif
   const bool shadow = hit >= 0 && secondary_ok(th) && (S.flags & RT_FLAG_SHADOWS) != 0;
   // wave64 compaction: lanes with a pending shadow ray append it to the
   // wave's LDS queue at ballot/mbcnt-assigned slots

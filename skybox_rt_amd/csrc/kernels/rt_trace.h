@@ -1200,6 +1200,40 @@ __device__ __forceinline__ void shadow_ray(const Scene& S, const Ray& p, float t
   ray_setup(s);
 }
 
+// Path tracing in two kernels (BASELINE config 4's wave64 active-ray
+// compaction): the first pass (pt_primary, rt_kernel.hip built
+// with RT_PATHQ) appends every pixel that starts a path to the frame's path
+// queue -- one atomic per wave, the wave's paths at ballot / mbcnt slots --
+// and pt_queue (pt_kernel.hip PT_MODE 2) runs the queued paths on full
+// waves.  The queue fields are read from the argument block where used.
+struct PathQ {
+  uint32_t q, ctr;
+};
+__device__ __forceinline__ PathQ pathq_args(const Scene& S) {
+  uint64_t p = S.argp;
+  asm volatile("" : "+s"(p));
+  const __attribute__((address_space(4))) rt_kernel_arg_t* a =
+      (const __attribute__((address_space(4))) rt_kernel_arg_t*)p;
+  PathQ o;
+  o.q = (uint32_t)a->pathq_addr;
+  o.ctr = (uint32_t)a->pathq_ctr_addr;
+  return o;
+}
+// every lane of the wave calls it; lanes with `want` append (task, t, pid, colour)
+__device__ __forceinline__ void pathq_append(const Scene& S, bool want, uint32_t task, float t,
+                                             int32_t pid, uint32_t color) {
+  const uint64_t m = __ballot(want);
+  if (m == 0) return;
+  const PathQ Q = pathq_args(S);
+  const int first = __builtin_ctzll(m);
+  uint32_t base = 0;
+  if ((int)lane_id() == first) base = atomicAdd(vx_ptr<uint32_t>(Q.ctr), (uint32_t)__popcll(m));
+  base = __builtin_amdgcn_readlane(base, first);
+  if (!want) return;
+  const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+  S.A.st_u4(Q.q + 16u * (base + rank), make_uint4(task, __float_as_uint(t), (uint32_t)pid, color));
+}
+
 __device__ __forceinline__ uint32_t shadowed(uint32_t c) {
   return (c & 0xff000000u) | ((c >> 1) & 0x007f7f7fu);
 }

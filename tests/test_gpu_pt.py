@@ -89,7 +89,8 @@ def test_pt_instrumented_counters_equal_oracle_traversal(po, width):
         r.configure(size, size, path=True, instrumented=True, bvh_width=width)
         r.render()
         st = r.stats()
-        c, _, _, k = po.rt_render(osc, po.rt_params(size, size, path=True, nthreads=8),
+        c, _, _, k = po.rt_render(osc, po.rt_params(size, size, path=True, nthreads=8,
+                                                    path_queue=r.setup_stats()["path_queue"]),
                                   bvh=bvh if r.bvh4 else bvh[:2])
         for key in ("node_visits", "tri_tests", "layer_tests", "shaded", "texel_bytes",
                     "shadow_rays", "bounce_rays", "occluded"):
@@ -115,3 +116,36 @@ def test_pt_compact_image_bit_exact_vs_oracle(po, size, bounces):
         assert st[key] == k[key], key
     assert st["block"] == 256                              # the compacting image ran
     r.close()
+
+
+@pytest.mark.parametrize("queue", [1, 0])
+@pytest.mark.parametrize("size,bounces", [(1024, 4), (333, 3)])
+def test_pt_two_kernels_and_one_kernel_equal_oracle(po, queue, size, bounces):
+    """Config 4 in two kernels (pt_primary appends path starts to a compacted
+    queue, pt_queue runs them on full waves: one launch group) or, with
+    RT_PT_QUEUE=0, in the one-kernel pt_kernel: the same frame, every count
+    equal to the oracle's in the same mode (the primary pass counts per 8x8
+    block in the two-kernel form), repeatable frame after frame (the queue
+    counters are reset by the last pt_queue wave)."""
+    import os
+    os.environ["RT_PT_QUEUE"] = str(queue)
+    try:
+        s, _, osc, bvh = setup(po, "tekkaman")
+        r = rt.Renderer(s)
+        r.configure(size, size, path=True, bounces=bounces, instrumented=True)
+        assert r.setup_stats()["path_queue"] == queue
+        r.render()
+        st = r.stats()
+        c, _, _, k = po.rt_render(osc, po.rt_params(size, size, path=True, bounces=bounces, nthreads=8,
+                                                    path_queue=bool(queue)), bvh=bvh)
+        assert np.array_equal(r.framebuffer(), c)
+        for key in ("primary_rays", "geometry_hits", "node_visits", "tri_tests", "layer_tests",
+                    "shaded", "texel_bytes", "shadow_rays", "bounce_rays", "occluded"):
+            assert st[key] == k[key], key
+        r.configure(size, size, path=True, bounces=bounces, counters=False)
+        for _ in range(3):
+            r.render()
+            assert np.array_equal(r.framebuffer(), c)
+        r.close()
+    finally:
+        del os.environ["RT_PT_QUEUE"]
