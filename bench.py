@@ -65,10 +65,13 @@ def algorithmic_bytes(st: dict, pixels: int, node_bytes: int = NODE_BYTES) -> in
             + st["texel_bytes"] + PIXEL_BYTES * pixels)
 
 
-PMC_IMAGES = {"shadow": "rt_kernel.co", "path": "pt_kernel.co", "flat": "rt_flat.co"}
+# the kernel images of one frame per workload (config 4: pt_primary + pt_queue,
+# one launch group; pt_kernel when the renderer runs it in one kernel)
+PMC_IMAGES = {"shadow": ("rt_kernel.co",), "path": ("pt_primary.co", "pt_queue.co"),
+              "flat": ("rt_flat.co",)}
 
 
-def pmc_record(mode: str, side: int):
+def pmc_record(mode: str, side: int, images=None):
     """The committed rocprofv3 PMC record of this workload's kernel image
     (scripts/pmc_profile.sh -> profiles/pmc_<mode>.json): HBM traffic per
     launch (FETCH_SIZE x2 + WRITE_SIZE, the guide's gfx950 correction) and
@@ -76,14 +79,16 @@ def pmc_record(mode: str, side: int):
     exists but was taken on another kernel image or size."""
     import hashlib
     path = os.path.join(ROOT, "profiles", f"pmc_{mode}.json")
-    co = os.path.join(ROOT, "skybox_rt_amd", "lib", PMC_IMAGES[mode])
     try:
         with open(path) as fh:
             t = json.load(fh)
     except (OSError, ValueError):
         return None, False
     try:
-        md5 = hashlib.md5(open(co, "rb").read()).hexdigest()
+        h = hashlib.md5()  # the frame's images' bytes concatenated (scripts/pmc_profile.py)
+        for co in images or PMC_IMAGES[mode]:
+            h.update(open(os.path.join(ROOT, "skybox_rt_amd", "lib", co), "rb").read())
+        md5 = h.hexdigest()
     except OSError:
         return None, True
     if t.get("kernel_md5") != md5 or t.get("width") != side or t.get("height") != side:
@@ -516,20 +521,32 @@ def main():
     if flat:
         workload = (f"{side}x{side} {kind}, tekkaman.cgltrace: every ray tests the whole geometry "
                     f"list (rectangle words in LDS, wave-uniform rectangle skip, exact edge + depth test)")
+    elif path and setup_st.get("path_queue"):
+        shadow_how = ("light-space shadow lists" if setup_st["slist_on"] else f"{bvh_kind} walk")
+        workload = (f"{side}x{side} {kind}, tekkaman.cgltrace, two kernels per frame: {primary}, "
+                    f"path starts appended to a compacted queue (wave64: one atomic per wave, "
+                    f"ballot/mbcnt slots); then the queued paths on full waves: bounce rays a "
+                    f"per-lane {bvh_kind} walk (LDS stack), shadow rays on the {shadow_how}")
     elif path:
         workload = (f"{side}x{side} {kind}, tekkaman.cgltrace; {primary}; bounce + shadow rays: "
                     f"per-lane {bvh_kind} walk, LDS stack, shadow/bounce lanes paired in the "
                     f"32-pixel waves of geometry tiles")
     else:
+        shadow_how = ("per lane over its light-space cell list (cube map around the light, built "
+                      "on the device)" if setup_st["slist_on"]
+                      else f"each wave a {bvh_kind} packet walk (stack in one VGPR)")
         workload = (f"{side}x{side} {'primary+shadow' if shadows else 'primary'} rays, "
                     f"tekkaman.cgltrace; {primary}; shadow rays: ballot/mbcnt-compacted into full "
-                    f"waves, each wave a {bvh_kind} packet walk (stack in one VGPR)")
+                    f"waves, {shadow_how}")
     if n_gpus > 1:
         workload += (f", tile-sharded over {n_gpus} GPUs (32x32 tile t -> rank t mod {n_gpus}) + "
                      f"{'RCCL' if backend == 'nccl' else backend} gather to rank 0"
                      + (" (BASELINE config 5)" if config5 else ""))
     mode = "path" if path else ("flat" if flat else "shadow")
-    rec, stale = pmc_record(mode, side) if n_gpus == 1 else (None, False)
+    images = None
+    if path and not setup_st.get("path_queue"):
+        images = ("pt_kernel.co",)  # the one-kernel path tracer (RT_PT_QUEUE=0)
+    rec, stale = pmc_record(mode, side, images) if n_gpus == 1 else (None, False)
     traffic = rec["traffic_bytes"] if rec else None
     info = scene.info()  # (after the timed region: parse time, host-side counts)
     out = {

@@ -42,12 +42,12 @@ typedef int (*vx_hip_mpm_rows_t)(vx_device_h hdevice, uint32_t* rows, uint64_t m
  * VORTEX_PROFILING (the stub's MPM_CLASS DCR) or env VX_HIP_COUNTERS=1 turn
  * them on as well. */
 typedef int (*vx_hip_set_counters_t)(vx_device_h hdevice, int enable);
-/* the following runs are groups of n (1..4) consecutive vx_start launches --
- * one frame made of several kernels on the driver's stream: a group is timed
- * as a whole (start event on its first launch, stop event on its last: the
- * frame's span), counted as one run by vx_hip_run_totals / vx_hip_last_run,
- * and vx_mpm_query sums the counters of all its launches.  1 = the default
- * (every launch a run).  Only between groups; waits for the queue. */
+/* the next n (1..4) vx_start launches form one run -- a frame made of
+ * several kernels on the driver's stream: timed as a whole (start event on
+ * its first launch, stop event on its last: the frame's span), counted as
+ * one run by vx_hip_run_totals / vx_hip_last_run, and vx_mpm_query sums the
+ * counters of all its launches; then launches are single runs again.  Only
+ * between groups (-1 inside one); never waits. */
 typedef int (*vx_hip_launch_group_t)(vx_device_h hdevice, uint32_t n);
 
 #ifdef __cplusplus

@@ -14,7 +14,12 @@ memory-side counter cannot tell them apart, so the read side is reported as
 bounds [FETCH x1, FETCH x2] and `traffic_bytes` is the upper bound.  SQ_WAVE_CYCLES
 / SQ_WAIT_* / SQ_ACTIVE_INST_* count quad-cycles (summed over waves), so their
 ratios are what is meaningful.
-Usage: pmc_profile.py <tag_dir> <mode> <side> <kernel .co> <out.json> [kernel name]"""
+A workload of several kernels per frame (config 4: pt_primary + pt_queue)
+passes its images comma-separated: every counter is the sum over the images
+of their per-dispatch means (one dispatch of each per frame), the record
+carries each image's MD5 and `kernel_md5` = the MD5 of the images' bytes
+concatenated in that order.
+Usage: pmc_profile.py <tag_dir> <mode> <side> <kernel .co[,.co]> <out.json>"""
 import csv
 import glob
 import hashlib
@@ -37,19 +42,32 @@ def means(d, kname):
         {c: len(v) for c, v in per.items()}
 
 
+def images_md5(cos):
+    """MD5 of the images' bytes concatenated in order (one image: its MD5)."""
+    h = hashlib.md5()
+    for co in cos:
+        h.update(open(co, "rb").read())
+    return h.hexdigest()
+
+
 def main():
-    tag, mode, side, co, out = sys.argv[1:6]
-    image = os.path.splitext(os.path.basename(co))[0]
-    kname = sys.argv[6] if len(sys.argv) > 6 else f"vx_main_{image}"
+    tag, mode, side, co_arg, out = sys.argv[1:6]
+    cos = co_arg.split(",")
+    knames = [f"vx_main_{os.path.splitext(os.path.basename(co))[0]}" for co in cos]
     side = int(side)
-    m, nd = {}, {}
-    for d in sorted(glob.glob(os.path.join(tag, f"{mode}_*"))):
-        if os.path.isdir(d):
-            a, b = means(d, kname)
-            m.update(a)
-            nd.update(b)
+    m, nd = defaultdict(float), {}
+    for kname in knames:
+        for d in sorted(glob.glob(os.path.join(tag, f"{mode}_*"))):
+            if os.path.isdir(d):
+                a, b = means(d, kname)
+                for c, v in a.items():
+                    m[c] += v
+                for c, v in b.items():
+                    nd[f"{kname}:{c}"] = v
+    m = dict(m)
     if "FETCH_SIZE" not in m or "WRITE_SIZE" not in m:
-        sys.exit(f"no {kname} dispatches with FETCH_SIZE / WRITE_SIZE")
+        sys.exit(f"no {knames} dispatches with FETCH_SIZE / WRITE_SIZE")
+    kname = "+".join(knames)
     g = m.get
     der = {}
     wc = g("SQ_WAVE_CYCLES")
@@ -76,8 +94,9 @@ def main():
     lo, hi = int(f_kb * 1024 + w_kb * 1024), int(2 * f_kb * 1024 + w_kb * 1024)
     res = {
         "kernel": kname, "mode": mode, "width": side, "height": side,
-        "kernel_image": os.path.basename(co),
-        "kernel_md5": hashlib.md5(open(co, "rb").read()).hexdigest(),
+        "kernel_image": "+".join(os.path.basename(co) for co in cos),
+        "kernel_md5": images_md5(cos),
+        "kernel_md5s": {os.path.basename(co): images_md5([co]) for co in cos},
         "dispatches": nd,
         "fetch_size_kb": round(f_kb, 1), "write_size_kb": round(w_kb, 1),
         "correction": ("calibrated (profiles/r03/pmc_calibration.json): reads FETCH_SIZE x1024 x1 "

@@ -13,7 +13,7 @@ TAG=${TAG:-pmc}; mkdir -p gpurun_out/$TAG
 MODE=${MODE:-shadow}
 case $MODE in
   shadow) CO=rt_kernel.co; SZ=1024 ;;
-  path)   CO=pt_kernel.co; SZ=1024 ;;
+  path)   CO=pt_primary.co,pt_queue.co; SZ=1024 ;;  # one frame = both kernels
   flat)   CO=rt_flat.co;   SZ=256 ;;
   *) echo "bad MODE $MODE"; exit 2 ;;
 esac
@@ -30,4 +30,4 @@ pass sq1 SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_
 pass sq2 SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_VMEM_RD SQ_INSTS_LDS SQ_INSTS_SMEM SQ_INSTS_VMEM_WR || exit $?
 pass sq3 SQ_ACTIVE_INST_VALU SQ_THREAD_CYCLES_VALU SQ_ACTIVE_INST_LDS SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT || exit $?
 pass mem TCP_TOTAL_CACHE_ACCESSES_sum TCP_TCC_READ_REQ_sum TCC_HIT_sum TCC_MISS_sum || exit $?
-python3 scripts/pmc_profile.py gpurun_out/$TAG $MODE $SZ skybox_rt_amd/lib/$CO gpurun_out/$TAG/pmc_$MODE.json
+python3 scripts/pmc_profile.py gpurun_out/$TAG $MODE $SZ $(echo $CO | sed 's#\([^,]*\)#skybox_rt_amd/lib/\1#g') gpurun_out/$TAG/pmc_$MODE.json

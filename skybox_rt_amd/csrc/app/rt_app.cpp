@@ -983,13 +983,13 @@ int rt_render_start(rt_renderer_h r) {
       r->set_counters(r->dev, (f & (RT_RENDER_COUNTERS | RT_RENDER_INSTRUMENTED)) ? 1 : 0) != 0)
     return fail("vx_hip_set_counters failed");
   // a frame of the two-kernel path tracer is one launch group of 2
-  const uint32_t group = (mode == 1 && r->pq) ? 2u : 1u;
-  if (r->launch_group && r->launch_group(r->dev, group) != 0) return fail("vx_hip_launch_group failed");
-  if (group == 2)
+  if (mode == 1 && r->pq) {
+    if (r->launch_group(r->dev, 2) != 0) return fail("vx_hip_launch_group failed");
     return vx_start(r->dev, r->krnl_pq[0][k], r->args) == 0 &&
                    vx_start(r->dev, r->krnl_pq[1][k], r->args) == 0
                ? 0
                : fail("vx_start failed");
+  }
   return vx_start(r->dev, r->krnl[mode][k], r->args) == 0 ? 0 : fail("vx_start failed");
 }
 

@@ -378,10 +378,6 @@ VX_MAIN(rt_kernel_arg_t, arg, RT_BLOCK_THREADS) {
       &S);
 #else
   if ((threadIdx.x & 63u) == 0) w.q_count = 0;
-#if RT_LDS_SHADE
-  stage_shade(S, arg->num_drawcalls);
-  __syncthreads();
-#endif
   __builtin_amdgcn_wave_barrier();
   const int rc = vx_spawn_tasks_ex(
       arg->num_tasks,

@@ -640,9 +640,6 @@ __device__ __forceinline__ bool occluded_packet(const Scene& S, const Ray& r, bo
 // (t in (0, 1), the primary winner `skip` excluded).  Per lane: a lane's
 // chain is its own list, not the wave's union of BVH paths; the records are
 // copies in list order, loaded two ahead.  Tests count per lane.
-#ifndef RT_SLIST_PREFETCH
-#define RT_SLIST_PREFETCH 0
-#endif
 __device__ __forceinline__ uint32_t slist_cell(const Ray& s, uint32_t N) {
   const float u0 = -s.d[0], u1 = -s.d[1], u2 = -s.d[2];
   int k = 0;
@@ -664,34 +661,6 @@ __device__ __forceinline__ bool occluded_list(const Scene& S, const Ray& s, bool
   const uint32_t cell = slist_cell(s, S.slist_n);
   const uint32_t off = S.A.ld_u32(S.sidx + 8u * cell), n = S.A.ld_u32(S.sidx + 8u * cell + 4u);
   uint32_t o = S.slist + 48u * off;
-#if RT_SLIST_PREFETCH
-  // software-pipelined: the next two records' loads are in flight while the
-  // current two are tested (the list carries a padding record; a load past
-  // the arena reads 0)
-  float4 t[6];
-#pragma unroll
-  for (int w = 0; w < 6; ++w) t[w] = S.A.ld_f4(o + 16u * w);
-  for (uint32_t q = 0; q < n; q += 2) {
-    o += 96u;
-    float4 nt[6];
-#pragma unroll
-    for (int w = 0; w < 6; ++w) nt[w] = S.A.ld_f4(o + 16u * w);
-#pragma unroll
-    for (int e = 0; e < 2; ++e) {
-      if (q + e >= n) break;
-#ifdef RT_INSTRUMENT
-      ++cnt.tests;
-#endif
-      float th;
-      if (__float_as_int(t[3 * e].w) != skip && mt_hit(s, t[3 * e], t[3 * e + 1], t[3 * e + 2], 0.0f, &th) &&
-          th < 1.0f)
-        return true;
-    }
-#pragma unroll
-    for (int w = 0; w < 6; ++w) t[w] = nt[w];
-  }
-  return false;
-#endif
   for (uint32_t q = 0; q < n; q += 2, o += 96u) {
     float4 t[6];
 #pragma unroll
@@ -758,65 +727,12 @@ __device__ __forceinline__ int32_t trace_flat_range(const Scene& S, const Ray& r
   return bpid;
 }
 
-// LDS shading-record cache (RT_LDS_SHADE): every workgroup stages the
-// drawcall states and the screen layers' primitive records (the layers are
-// pids 0 .. num_layer-1: they precede the geometry, DESIGN "Scope") once, so
-// a background pixel's shading reads its records from LDS instead of two
-// dependent global round trips (prim -> drawcall state)
-#ifndef RT_LDS_SHADE
-#define RT_LDS_SHADE 0
-#endif
-#if RT_LDS_SHADE
-#define RT_LDS_DCS 8       // drawcall states cached (more: the rest from memory)
-#define RT_LDS_LAYERS 4    // layer primitive records cached
-struct ShadeLds {
-  uint4 dcs[RT_LDS_DCS][3];
-  uint4 prims[RT_LDS_LAYERS][8];
-  uint32_t ndc, nl;
-};
-__shared__ ShadeLds s_shade;
-// every thread of the workgroup calls it; the caller syncs the workgroup
-__device__ __forceinline__ void stage_shade(const Scene& S, uint32_t num_dc) {
-  const uint32_t ndc = num_dc < RT_LDS_DCS ? num_dc : RT_LDS_DCS;
-  const uint32_t nl = S.num_layer < RT_LDS_LAYERS ? S.num_layer : RT_LDS_LAYERS;
-  const uint32_t i = threadIdx.x;
-  if (i < 3 * ndc) s_shade.dcs[i / 3][i % 3] = S.A.ld_u4(S.dcs + 64u * (i / 3) + 16u * (i % 3));
-  else if (i - 3 * ndc < 8 * nl) {
-    const uint32_t j = i - 3 * ndc;
-    s_shade.prims[j / 8][j % 8] = S.A.ld_u4(S.prims + 128u * (j / 8) + 16u * (j % 8));
-  }
-  if (i == 0) { s_shade.ndc = ndc; s_shade.nl = nl; }
-}
-#endif
-
 // shade primitive `pid` at (x, y) from per-lane (vector) record loads
 __device__ __forceinline__ uint32_t shade_lane(const Scene& S, int32_t pid, uint32_t x,
                                                uint32_t y, Counters& cnt) {
   gfx::Prim p;
-#if RT_LDS_SHADE
-  if ((uint32_t)pid < s_shade.nl) {
-#pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      const uint4 v = s_shade.prims[pid][i];
-      p.w[4 * i + 0] = (int32_t)v.x; p.w[4 * i + 1] = (int32_t)v.y;
-      p.w[4 * i + 2] = (int32_t)v.z; p.w[4 * i + 3] = (int32_t)v.w;
-    }
-  } else {
-    gfx::load_prim(S.A, S.prims + 128u * (uint32_t)pid, p);
-  }
-  gfx::DcState s;
-  if (p.dc() < s_shade.ndc) {
-    const uint4 a = s_shade.dcs[p.dc()][0], b = s_shade.dcs[p.dc()][1], c = s_shade.dcs[p.dc()][2];
-    s.flags = a.x; s.logw = a.y; s.logh = a.z; s.format = a.w;
-    s.filter = b.x; s.wrapu = b.y; s.wrapv = b.z; s.stride = b.w;
-    s.tex_off = c.x;
-  } else {
-    s = gfx::load_dcstate(S.A, S.dcs + 64u * p.dc());
-  }
-#else
   gfx::load_prim(S.A, S.prims + 128u * (uint32_t)pid, p);
   const gfx::DcState s = gfx::load_dcstate(S.A, S.dcs + 64u * p.dc());
-#endif
 #ifdef RT_INSTRUMENT
   ++cnt.shaded;
   if (s.flags & RT_DC_TEX) cnt.texel_bytes += (s.filter == VX_TEX_FILTER_BILINEAR ? 4u : 1u) * s.stride;
@@ -1126,6 +1042,9 @@ struct TaskPix {
 #ifndef RT_LAZY_TASK_ARGS
 #define RT_LAZY_TASK_ARGS 1
 #endif
+#ifndef RT_ORDER_SLOAD
+#define RT_ORDER_SLOAD 0
+#endif
 struct TaskArgs {
   uint32_t split_tiles, split_log, order, shard_index, shard_count, tiles_x;
 };
@@ -1161,7 +1080,12 @@ __device__ __forceinline__ TaskPix task_map(const Scene& S, const TaskArgs& T, u
     m.idx = t & 1023u;
     m.live = true;
   }
+#if RT_ORDER_SLOAD
+  // pos is wave-uniform: the work-order word through the scalar cache
+  m.lt = T.order ? S.A.sld<uint32_t>(T.order + 4u * pos) : pos;
+#else
   m.lt = T.order ? S.A.ld_u32(T.order + 4u * pos) : pos;
+#endif
   return m;
 }
 __device__ __forceinline__ TaskPix task_map(const Scene& S, uint32_t t) {

@@ -319,10 +319,10 @@ class vx_device {
     // launch, the stop event on its last.
     const bool first = group_pos_ == 0, last = group_pos_ + 1 == group_n_;
     if (first) {
-      group_timed_ = launch_mode_ != 2 &&
-                     (issued_ == retired_ || (issued_ / group_n_) % time_every_ == 0);
+      group_timed_ = launch_mode_ != 2 && (issued_ == retired_ || runs_issued_ % time_every_ == 0);
       group_slot_ = slot;
       group_mods_.clear();
+      ++runs_issued_;
     }
     group_mods_.push_back({m, m->grid, rows});
     const bool timed = group_timed_;
@@ -330,6 +330,7 @@ class vx_device {
     group_last_[slot] = last;
     group_first_slot_[slot] = group_slot_;
     group_pos_ = last ? 0 : group_pos_ + 1;
+    if (last) group_n_ = 1;  // a group covers the launches it was declared for
     if (!timed) {
       HIP_CHECK(hipExtModuleLaunchKernel(m->entry, m->grid * m->block, 1, 1, m->block, 1, 1, 0,
                                          stream_, nullptr, nullptr, nullptr, nullptr, 0));
@@ -459,13 +460,9 @@ class vx_device {
     return 0;
   }
   void set_counters(bool on) { counters_ = on; }  // applies from the next start()
-  // the next runs are groups of n launches (1 = every launch a run); waits
-  // for the queue, so groups never straddle a change
+  // the next n launches form one run (then single launches again)
   int launch_group(uint32_t n) {
-    if (n < 1 || n > 4) return -1;
-    if (n == group_n_ && group_pos_ == 0) return 0;
-    if (group_pos_ != 0) return -1;  // inside a group
-    wait_idle();
+    if (n < 1 || n > 4 || group_pos_ != 0) return -1;  // not inside a group
     group_n_ = n;
     return 0;
   }
@@ -576,6 +573,7 @@ class vx_device {
     bool rows;
   };
   uint32_t group_n_ = 1, group_pos_ = 0;
+  uint64_t runs_issued_ = 0;
   bool group_timed_ = false;
   int group_slot_ = 0;
   bool group_last_[kMaxQueue] = {};

@@ -12,7 +12,8 @@ import pytest
 from skybox_rt_amd import _lib
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-IMAGES = {"shadow": "rt_kernel.co", "path": "pt_kernel.co", "flat": "rt_flat.co"}
+IMAGES = {"shadow": ("rt_kernel.co",), "path": ("pt_primary.co", "pt_queue.co"),
+          "flat": ("rt_flat.co",)}
 
 
 @pytest.mark.parametrize("mode", sorted(IMAGES))
@@ -22,8 +23,10 @@ def test_pmc_record_matches_built_image(mode):
     rec_path = os.path.join(ROOT, "profiles", f"pmc_{mode}.json")
     assert os.path.exists(rec_path), f"no PMC record for {mode}: run scripts/pmc_profile.sh"
     rec = json.load(open(rec_path))
-    co = os.path.join(_lib.LIB_DIR, IMAGES[mode])
-    md5 = hashlib.md5(open(co, "rb").read()).hexdigest()
+    h = hashlib.md5()  # the frame's images concatenated (scripts/pmc_profile.py)
+    for co in IMAGES[mode]:
+        h.update(open(os.path.join(_lib.LIB_DIR, co), "rb").read())
+    md5 = h.hexdigest()
     assert rec["kernel_md5"] == md5, (
         f"profiles/pmc_{mode}.json was taken on another {IMAGES[mode]} "
         f"({rec['kernel_md5']} != {md5}): regenerate it with scripts/pmc_profile.sh")
