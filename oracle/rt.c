@@ -815,7 +815,7 @@ static uint32_t path_trace(const rt_ctx_t* c, uint32_t px, const float d0[3], fl
  * the brute-force any-hit's.  A ray tests its cell's list in ascending
  * geometry index until the first occluder.  All arithmetic fp32, no
  * contraction, the device's operation order. */
-#define SL_N 128
+#define SL_N 256
 #define SL_EPS (1.0f / 512.0f)
 #define SL_CELLS (6 * SL_N * SL_N)
 static const int sl_ax[3][2] = {{1, 2}, {0, 2}, {0, 1}};

@@ -949,14 +949,25 @@ int rt_renderer_configure(rt_renderer_h r, const rt_render_params_t* p) {
     }
   }
   uint64_t args_addr = 0;
-  if (r->pq) {  // the path queue (uint4 per path start, at most one per local pixel) + counters
-    const uint32_t zero[16] = {};
+  if (r->pq) {
+    // the path queue: RT_PQ_SEGS segments (chunk c -> segment c % RT_PQ_SEGS),
+    // each holding up to 64 paths per chunk it gets; the counters, one 128-B
+    // line each (rt_common.h)
+    const uint32_t chunks = (a.num_tasks + 63u) / 64u;
+    a.pathq_seg_cap = ((chunks + RT_PQ_SEGS - 1) / RT_PQ_SEGS) * 64u;
+    const std::vector<uint32_t> zero(32u * (2u * RT_PQ_SEGS + 1u), 0u);
     uint64_t qa = 0, ca = 0;
-    if (upload(r->dev, nullptr, npx * 16, &r->pathq, &qa) ||
-        upload(r->dev, zero, sizeof(zero), &r->pathq_ctr, &ca))
+    if (upload(r->dev, nullptr, (uint64_t)RT_PQ_SEGS * a.pathq_seg_cap * 16, &r->pathq, &qa) ||
+        upload(r->dev, zero.data(), zero.size() * 4, &r->pathq_ctr, &ca))
       return -1;
     a.pathq_addr = qa;
     a.pathq_ctr_addr = ca;
+    // paths per pt_queue wave (env RT_PQ_LANES: 64, 32 or 16)
+    a.pathq_lanes = 64;
+    if (const char* e = std::getenv("RT_PQ_LANES")) {
+      const uint32_t l = (uint32_t)std::atoi(e);
+      a.pathq_lanes = (l == 16 || l == 32) ? l : 64u;
+    }
   } else {
     a.pathq_addr = a.pathq_ctr_addr = 0;
   }

@@ -464,9 +464,17 @@ __device__ __forceinline__ void bounces(const Scene& S, PtLds& L, Counters& cnt)
 // one queued path (pt_primary appended it: task, plane t, hit pid, primary
 // colour) on its own lane to the end; the other lanes of the wave hold the
 // paths queued next to it
-__device__ __forceinline__ void queued_path(const vx_task_t& task, const Scene& S, uint32_t q,
-                                            int32_t* stack, Counters& cnt) {
-  const uint4 e = S.A.ld_u4(q + 16u * task.task_id);
+// Work item g = task / 64 takes paths [j * lanes, (j + 1) * lanes) of
+// segment s = g % RT_PQ_SEGS, j = g / RT_PQ_SEGS (Q.lanes paths per wave,
+// the rest of the wave idles); nseg = this lane's segment count (lane s
+// holds segment s's)
+__device__ __forceinline__ void queued_path(const vx_task_t& task, const Scene& S, const PathQ& Q,
+                                            uint32_t nseg, int32_t* stack, Counters& cnt) {
+  const uint32_t g = task.task_id >> 6, s = g % RT_PQ_SEGS, j = g / RT_PQ_SEGS;
+  const uint32_t n = __builtin_amdgcn_readlane(nseg, (int)s);
+  const uint32_t i = j * Q.lanes + (task.task_id & 63u);
+  if ((task.task_id & 63u) >= Q.lanes || i >= n) return;
+  const uint4 e = S.A.ld_u4(Q.q + 16u * (s * Q.cap + i));
   uint32_t x, y;
   task_pixel(S, e.x, &x, &y);
   Ray r;
@@ -590,22 +598,38 @@ VX_MAIN(rt_kernel_arg_t, arg, PT_BLOCK) {
   const PathQ Q = pathq_args(S);
   // the paths the first kernel queued (a vector load: written by the
   // previous launch, after this launch's cache invalidation)
-  const uint32_t n = __builtin_amdgcn_readfirstlane(S.A.ld_u32(Q.ctr));
+  // every segment's count, lane s holding segment s's (RT_PQ_SEGS = 64), and
+  // the most waves of Q.lanes paths any segment needs
+  static_assert(RT_PQ_SEGS == 64, "one segment per lane");
+  const uint32_t nseg = S.A.ld_u32(Q.ctr + 128u * lane_id());
+  uint32_t jmax = (nseg + Q.lanes - 1) / Q.lanes;
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) jmax = max(jmax, (uint32_t)__shfl_xor((int)jmax, off, 64));
   const int rc = vx_spawn_tasks(
-      n, [&](const vx_task_t& task, const Scene* s) { queued_path(task, *s, Q.q, stack, cnt); }, &S);
-  // the last worker wave to finish zeroes the counters for the next frame
-  // (no wave waits on another: each counts itself done once)
-  const uint32_t nchunks = (n + VX_CHUNK - 1) / VX_CHUNK;
+      RT_PQ_SEGS * jmax * VX_CHUNK,
+      [&](const vx_task_t& task, const Scene* s) { queued_path(task, *s, Q, nseg, stack, cnt); }, &S);
+  // every wave counts itself done once, on its group's counter (wave id
+  // mod 64: the atomics spread over 64 lines); the wave completing a group
+  // counts the group, and the one completing the last group zeroes every
+  // counter for the next frame -- by then every wave has read them.  Nobody
+  // waits.
   const uint32_t nwaves = gridDim.x * (blockDim.x >> 6);
   const uint32_t wid = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
-  const uint32_t workers = nchunks < nwaves ? nchunks : nwaves;
-  if (wid < workers && lane_id() == 0) {
+  const uint32_t grp = wid % RT_PQ_SEGS;
+  const uint32_t in_grp = nwaves / RT_PQ_SEGS + (grp < nwaves % RT_PQ_SEGS ? 1u : 0u);
+  const uint32_t ngrp = nwaves < RT_PQ_SEGS ? nwaves : RT_PQ_SEGS;
+  uint32_t last = 0;
+  if (lane_id() == 0) {
     uint32_t* ctr = vx_ptr<uint32_t>(Q.ctr);
     __threadfence();
-    if (atomicAdd(&ctr[2], 1u) == workers - 1u) {
-      atomicExch(&ctr[0], 0u);
-      atomicExch(&ctr[2], 0u);
-    }
+    if (atomicAdd(&ctr[32u * (RT_PQ_SEGS + grp)], 1u) == in_grp - 1u &&
+        atomicAdd(&ctr[32u * 2u * RT_PQ_SEGS], 1u) == ngrp - 1u)
+      last = 1;
+  }
+  if (__builtin_amdgcn_readfirstlane(last)) {  // lanes zero segment / group counter l
+    S.A.st_u32(Q.ctr + 128u * lane_id(), 0u);
+    S.A.st_u32(Q.ctr + 128u * (RT_PQ_SEGS + lane_id()), 0u);
+    if (lane_id() == 0) S.A.st_u32(Q.ctr + 128u * 2u * RT_PQ_SEGS, 0u);
   }
 #else
   int32_t* stack = &s_pt.stack[threadIdx.x >> 6][0][lane_id()];

@@ -201,12 +201,20 @@ typedef struct {
   uint64_t sidx_addr;      // uint32[2] per light-space cell: first entry, count
   uint64_t slist_addr;     // rt_tri_t per entry (+1 padding record): every cell's triangles, ascending pid
   uint32_t raster_bin_log; // raster mode: binning tile side 2^log (RASTER_TILE_LOGSIZE; draw3d -k)
-  uint32_t pad_bin;
+  uint32_t pathq_lanes;    // pt_queue: paths per wave (64, 32 or 16; 0 = 64)
   uint64_t pathq_addr;     // path tracing in two kernels (pt_primary + pt_queue): uint4 per path
-                           // start (task, plane t, hit pid, primary colour), compacted
-  uint64_t pathq_ctr_addr; // u32 [4]: [0] paths queued this frame, [2] pt_queue worker waves
-                           // done (the last one zeroes both for the next frame)
+                           // start (task, plane t, hit pid, primary colour), compacted in
+                           // RT_PQ_SEGS segments of pathq_seg_cap entries
+  uint64_t pathq_ctr_addr; // counters, one 128-B line each (u32 word 32 * i): i < RT_PQ_SEGS
+                           // paths queued in segment i; RT_PQ_SEGS + g pt_queue waves done of
+                           // group g; 2 * RT_PQ_SEGS groups done (the last zeroes them all)
+  uint32_t pathq_seg_cap;  // entries per segment
+  uint32_t pad_pq;
 } rt_kernel_arg_t;
+// the path queue is split into segments (a primary chunk c appends to segment
+// c % RT_PQ_SEGS) so its atomics spread over that many counters: one
+// device-scope counter for the whole frame serialised ~1 600 atomics
+#define RT_PQ_SEGS 64
 
 // ---- light-space shadow lists (shadow rays to the point light) ------------
 // A shadow segment P -> L is identified by its direction from the light,
@@ -220,7 +228,7 @@ typedef struct {
 // conservative, so any-hit over the list is the brute force's verdict.
 // Built on the device (rt_setup.hip SCOUNT .. SSORT); oracle/rt.c sl_build
 // restates it.
-#define RT_SLIST_N 128              // default cells per face side (the oracle's SL_N)
+#define RT_SLIST_N 256              // default cells per face side (the oracle's SL_N); A/B r03h: 128 0.02524 ms, 256 0.02476, 512 0.0259 (r03c)
 #define RT_SLIST_EPS (1.0f / 512.0f)
 
 // ---- per-8x8-block candidate lists (primary visibility) -------------------

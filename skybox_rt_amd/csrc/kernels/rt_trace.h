@@ -1131,7 +1131,7 @@ __device__ __forceinline__ void shadow_ray(const Scene& S, const Ray& p, float t
 // and pt_queue (pt_kernel.hip PT_MODE 2) runs the queued paths on full
 // waves.  The queue fields are read from the argument block where used.
 struct PathQ {
-  uint32_t q, ctr;
+  uint32_t q, ctr, lanes, cap;
 };
 __device__ __forceinline__ PathQ pathq_args(const Scene& S) {
   uint64_t p = S.argp;
@@ -1141,6 +1141,8 @@ __device__ __forceinline__ PathQ pathq_args(const Scene& S) {
   PathQ o;
   o.q = (uint32_t)a->pathq_addr;
   o.ctr = (uint32_t)a->pathq_ctr_addr;
+  o.lanes = a->pathq_lanes ? a->pathq_lanes : 64u;
+  o.cap = a->pathq_seg_cap;
   return o;
 }
 // every lane of the wave calls it; lanes with `want` append (task, t, pid, colour)
@@ -1149,13 +1151,16 @@ __device__ __forceinline__ void pathq_append(const Scene& S, bool want, uint32_t
   const uint64_t m = __ballot(want);
   if (m == 0) return;
   const PathQ Q = pathq_args(S);
+  const uint32_t seg = __builtin_amdgcn_readfirstlane(task >> 6) % RT_PQ_SEGS;  // the wave's chunk
   const int first = __builtin_ctzll(m);
   uint32_t base = 0;
-  if ((int)lane_id() == first) base = atomicAdd(vx_ptr<uint32_t>(Q.ctr), (uint32_t)__popcll(m));
+  if ((int)lane_id() == first)
+    base = atomicAdd(vx_ptr<uint32_t>(Q.ctr + 128u * seg), (uint32_t)__popcll(m));
   base = __builtin_amdgcn_readlane(base, first);
   if (!want) return;
   const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
-  S.A.st_u4(Q.q + 16u * (base + rank), make_uint4(task, __float_as_uint(t), (uint32_t)pid, color));
+  S.A.st_u4(Q.q + 16u * (seg * Q.cap + base + rank),
+            make_uint4(task, __float_as_uint(t), (uint32_t)pid, color));
 }
 
 __device__ __forceinline__ uint32_t shadowed(uint32_t c) {
