@@ -45,6 +45,9 @@
 #else
 #define PT_BLOCK 64
 #endif
+#ifndef PT_ILP
+#define PT_ILP 0         // 1: a vertex's bounce walk and shadow-list scan in one loop
+#endif
 #ifndef PT_PAIR
 #define PT_PAIR 1        // 0: no paired-vertex code (the shadow lists never pair)
 #endif
@@ -208,6 +211,36 @@ struct PathState {
   float o[3], d[3], T[3], L[3];
 };
 
+// The next vertex of a path whose bounce ray b from P hit triangle np at t:
+// albedo = the draw3d shader at the hit's MT barycentrics, T *= albedo
+__device__ __forceinline__ void path_hit(const Scene& S, PathState& st, const float P[3], const Ray& b,
+                                         int32_t np, float nt, Counters& cnt) {
+  float w0[3], f1[3], f2[3], b1, b2;
+  load_tri(S, np, w0, f1, f2);
+  mt_bary(b.o, b.d, w0, f1, f2, &b1, &b2);
+  gfx::Prim p;
+  gfx::load_prim(S.A, S.prims + 128u * (uint32_t)np, p);
+  const gfx::DcState dst = gfx::load_dcstate(S.A, S.dcs + 64u * p.dc());
+#ifdef RT_INSTRUMENT
+  ++cnt.shaded;
+  if (dst.flags & RT_DC_TEX)
+    cnt.texel_bytes += (dst.filter == VX_TEX_FILTER_BILINEAR ? 4u : 1u) * dst.stride;
+#endif
+  const uint32_t a = gfx::shade_weights(S.A, p, dst, gfx::fx_from_float_dev((1.0f - b1) - b2, 24),
+                                        gfx::fx_from_float_dev(b1, 24));
+  const float k255 = 1.0f / 255.0f;
+  st.T[0] = st.T[0] * ((float)((a >> 16) & 0xffu) * k255);
+  st.T[1] = st.T[1] * ((float)((a >> 8) & 0xffu) * k255);
+  st.T[2] = st.T[2] * ((float)(a & 0xffu) * k255);
+#pragma unroll
+  for (int k = 0; k < 3; ++k) {
+    st.o[k] = P[k];
+    st.d[k] = b.d[k];
+  }
+  st.pid = np;
+  st.t = nt;
+}
+
 // One path vertex for an active lane: direct light through a shadow ray,
 // then (v < bounces) the bounce; returns whether the path continues (st then
 // describes the next vertex), else the pixel is final.  Every lane of the
@@ -229,6 +262,40 @@ __device__ __forceinline__ bool path_step(const Scene& S, int32_t* stack, PathSt
   s.d[2] = S.light[2] - P[2];
   ray_setup(s);
   cnt.shadow += act;
+#if PT_ILP
+  if (S.slist_on) {  // both rays of the vertex in one loop (trace_bounce_and_list)
+    bool alive = act && v < S.bounces;
+    Ray b;
+    b.o[0] = P[0]; b.o[1] = P[1]; b.o[2] = P[2];
+    b.d[0] = b.d[1] = b.d[2] = 1.0f;
+    if (alive) {
+      uint32_t x, y;
+      task_pixel(S, st.task, &x, &y);
+      bounce_dir(nrm, pt_key(S.seed, y * S.width + x, v), b.d);  // keyed by pixel, not task
+      cnt.bounce += 1;
+    }
+    ray_setup(b);
+    bool occ = false;
+    float nt = 0.0f;
+    const int32_t np = trace_bounce_and_list(S, b, st.pid, tie_high, &nt, stack, cnt, alive, s, st.pid,
+                                             act, &occ);
+    cnt.occluded += occ;
+    if (act && !occ) {
+      const float cosl = dot3(nrm, s.d) / sqrtf(dot3(s.d, s.d));
+      if (cosl > 0.0f) {
+#pragma unroll
+        for (int k = 0; k < 3; ++k) st.L[k] = fmaf(st.T[k], cosl, st.L[k]);
+      }
+    }
+    if (alive && np < 0) {
+#pragma unroll
+      for (int k = 0; k < 3; ++k) st.L[k] = fmaf(st.T[k], PT_SKY, st.L[k]);
+      alive = false;
+    }
+    if (alive) path_hit(S, st, P, b, np, nt, cnt);
+    return alive;
+  }
+#endif
   float ts;
   // the light-space lists when built (occluded_list), else the BVH
   const bool occ = S.slist_on ? occluded_list(S, s, act, st.pid, cnt)
@@ -259,33 +326,7 @@ __device__ __forceinline__ bool path_step(const Scene& S, int32_t* stack, PathSt
       alive = false;
     }
   }
-  if (alive) {
-    // albedo at the bounce hit: the draw3d shader at its MT barycentrics
-    float w0[3], f1[3], f2[3], b1, b2;
-    load_tri(S, np, w0, f1, f2);
-    mt_bary(b.o, b.d, w0, f1, f2, &b1, &b2);
-    gfx::Prim p;
-    gfx::load_prim(S.A, S.prims + 128u * (uint32_t)np, p);
-    const gfx::DcState dst = gfx::load_dcstate(S.A, S.dcs + 64u * p.dc());
-#ifdef RT_INSTRUMENT
-    ++cnt.shaded;
-    if (dst.flags & RT_DC_TEX)
-      cnt.texel_bytes += (dst.filter == VX_TEX_FILTER_BILINEAR ? 4u : 1u) * dst.stride;
-#endif
-    const uint32_t a = gfx::shade_weights(S.A, p, dst, gfx::fx_from_float_dev((1.0f - b1) - b2, 24),
-                                          gfx::fx_from_float_dev(b1, 24));
-    const float k255 = 1.0f / 255.0f;
-    st.T[0] = st.T[0] * ((float)((a >> 16) & 0xffu) * k255);
-    st.T[1] = st.T[1] * ((float)((a >> 8) & 0xffu) * k255);
-    st.T[2] = st.T[2] * ((float)(a & 0xffu) * k255);
-#pragma unroll
-    for (int k = 0; k < 3; ++k) {
-      st.o[k] = P[k];
-      st.d[k] = b.d[k];
-    }
-    st.pid = np;
-    st.t = nt;
-  }
+  if (alive) path_hit(S, st, P, b, np, nt, cnt);
   return alive;
 }
 

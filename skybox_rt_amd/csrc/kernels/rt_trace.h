@@ -680,6 +680,108 @@ __device__ __forceinline__ bool occluded_list(const Scene& S, const Ray& s, bool
   return false;
 }
 
+// A path vertex's two rays in one per-lane loop (path tracer, light-space
+// lists, PT_ILP): the bounce ray's closest-hit walk of the binary16 BVH4
+// (trace_impl's per-lane sequence of node steps and leaf tests) and the
+// shadow ray's cell-list scan (occluded_list's sequence) advance one step
+// each per iteration, so a vertex costs the longer of the two instead of
+// their sum.  Each ray's visits, tests and result are its own walk's.
+// `bact` / `sact`: this lane traces a bounce / shadow ray; *occ = the shadow
+// verdict; returns the bounce hit (-1: none).
+__device__ __forceinline__ int32_t trace_bounce_and_list(const Scene& S, const Ray& r, int32_t skip,
+                                                         bool tie_high, float* t_out, int32_t* stack,
+                                                         Counters& cnt, bool bact, const Ray& sr,
+                                                         int32_t sskip, bool sact, bool* occ_out) {
+  // shadow list state (occluded_list)
+  uint32_t so = 0, sn = 0, sq = 0;
+  bool sdone = !sact, occ = false;
+  if (sact) {
+    const uint32_t cell = slist_cell(sr, S.slist_n);
+    so = S.slist + 48u * S.A.ld_u32(S.sidx + 8u * cell);
+    sn = S.A.ld_u32(S.sidx + 8u * cell + 4u);
+    sdone = sn == 0;
+  }
+  // bounce walk state (trace_impl, closest hit)
+  LaneStack lst(stack);
+  int32_t ref = 0;
+  float bt = INFINITY;
+  int32_t bpid = -1;
+  bool bdone = !bact || S.num_nodes == 0;
+  auto node_next = [&](bool uni, uint32_t at) -> int32_t {
+#ifdef RT_INSTRUMENT
+    ++cnt.visits;
+#endif
+    return uni ? node4_step<true, true>(S, at, r, 0.0f, bt, false, lst)
+               : node4_step<false, true>(S, at, r, 0.0f, bt, false, lst);
+  };
+  if (__ballot(!bdone)) {  // every bouncing lane starts at the root: one scalar step
+    const int32_t nx = node_next(true, 0u);
+    if (!bdone) {
+      if (nx == RT_EMPTY_REF) bdone = true;
+      else ref = nx;
+    }
+  }
+  while (!bdone || !sdone) {
+    if (!bdone) {
+      if (ref >= 0) {  // a node step
+        const int32_t nx = node_next(false, (uint32_t)ref);
+        if (nx != RT_EMPTY_REF) ref = nx;
+        else if (!lst.pop(ref)) bdone = true;
+      } else {  // a leaf's (up to 4) triangles
+        const uint32_t lr = (uint32_t)ref;
+        const uint32_t first = (lr >> 4) & 0x07ffffffu, count = (lr & 15u) + 1u;
+        const uint32_t to = S.tris + 48u * first;
+        float4 ta[4], tb[4], tc[4];
+#pragma unroll
+        for (uint32_t k = 0; k < 4; ++k) {
+          ta[k] = S.A.ld_f4(to + 48u * k);
+          tb[k] = S.A.ld_f4(to + 48u * k + 16);
+          tc[k] = S.A.ld_f4(to + 48u * k + 32);
+        }
+#pragma unroll
+        for (uint32_t k = 0; k < 4; ++k) {
+          if (k < count) {
+            const int32_t pid = __float_as_int(ta[k].w);
+#ifdef RT_INSTRUMENT
+            ++cnt.tests;
+#endif
+            float t;
+            if (pid != skip && mt_hit(r, ta[k], tb[k], tc[k], 0.0f, &t) && closer(t, pid, bt, bpid, tie_high)) {
+              bt = t;
+              bpid = pid;
+            }
+          }
+        }
+        if (!lst.pop(ref)) bdone = true;
+      }
+    }
+    if (!sdone) {  // two records of the cell list
+      float4 t[6];
+#pragma unroll
+      for (int w = 0; w < 6; ++w) t[w] = S.A.ld_f4(so + 48u * sq + 16u * w);
+#pragma unroll
+      for (int e = 0; e < 2; ++e) {
+        if (!sdone && sq + e < sn) {
+#ifdef RT_INSTRUMENT
+          ++cnt.tests;
+#endif
+          float th;
+          if (__float_as_int(t[3 * e].w) != sskip &&
+              mt_hit(sr, t[3 * e], t[3 * e + 1], t[3 * e + 2], 0.0f, &th) && th < 1.0f) {
+            occ = true;
+            sdone = true;
+          }
+        }
+      }
+      sq += 2;
+      if (sq >= sn) sdone = true;
+    }
+  }
+  *occ_out = occ;
+  if (bpid >= 0) *t_out = bt;
+  return bpid;
+}
+
 template <bool ANY>
 __device__ __forceinline__ int32_t trace(const Scene& S, const Ray& r, float tmin, float tmax,
                                          int32_t skip, bool tie_high, float* t_out,
