@@ -1144,9 +1144,6 @@ struct TaskPix {
 #ifndef RT_LAZY_TASK_ARGS
 #define RT_LAZY_TASK_ARGS 1
 #endif
-#ifndef RT_ORDER_SLOAD
-#define RT_ORDER_SLOAD 0
-#endif
 struct TaskArgs {
   uint32_t split_tiles, split_log, order, shard_index, shard_count, tiles_x;
 };
@@ -1182,12 +1179,7 @@ __device__ __forceinline__ TaskPix task_map(const Scene& S, const TaskArgs& T, u
     m.idx = t & 1023u;
     m.live = true;
   }
-#if RT_ORDER_SLOAD
-  // pos is wave-uniform: the work-order word through the scalar cache
-  m.lt = T.order ? S.A.sld<uint32_t>(T.order + 4u * pos) : pos;
-#else
   m.lt = T.order ? S.A.ld_u32(T.order + 4u * pos) : pos;
-#endif
   return m;
 }
 __device__ __forceinline__ TaskPix task_map(const Scene& S, uint32_t t) {
