@@ -65,9 +65,9 @@ def algorithmic_bytes(st: dict, pixels: int, node_bytes: int = NODE_BYTES) -> in
             + st["texel_bytes"] + PIXEL_BYTES * pixels)
 
 
-# the kernel images of one frame per workload (config 4: pt_primary + pt_queue,
-# one launch group; pt_kernel when the renderer runs it in one kernel)
-PMC_IMAGES = {"shadow": ("rt_kernel.co",), "path": ("pt_primary.co", "pt_queue.co"),
+# the kernel images of one frame per workload (config 4: the one-kernel
+# pt_kernel; pt_primary + pt_queue under RT_PT_QUEUE=1)
+PMC_IMAGES = {"shadow": ("rt_kernel.co",), "path": ("pt_kernel.co",),
               "flat": ("rt_flat.co",)}
 
 
@@ -527,6 +527,12 @@ def main():
                     f"path starts appended to a compacted queue (wave64: one atomic per wave, "
                     f"ballot/mbcnt slots); then the queued paths on full waves: bounce rays a "
                     f"per-lane {bvh_kind} walk (LDS stack), shadow rays on the {shadow_how}")
+    elif path and setup_st["slist_on"]:
+        workload = (f"{side}x{side} {kind}, tekkaman.cgltrace, one kernel; {primary}; then each "
+                    f"path on its lane(s): bounce rays a {bvh_kind} walk (LDS stack), shadow rays "
+                    f"on the light-space shadow lists; in the 32-pixel waves of geometry tiles "
+                    f"two lanes per path (children / triangles / list records split two and two, "
+                    f"permlane32 exchanges)")
     elif path:
         workload = (f"{side}x{side} {kind}, tekkaman.cgltrace; {primary}; bounce + shadow rays: "
                     f"per-lane {bvh_kind} walk, LDS stack, shadow/bounce lanes paired in the "
@@ -544,8 +550,8 @@ def main():
                      + (" (BASELINE config 5)" if config5 else ""))
     mode = "path" if path else ("flat" if flat else "shadow")
     images = None
-    if path and not setup_st.get("path_queue"):
-        images = ("pt_kernel.co",)  # the one-kernel path tracer (RT_PT_QUEUE=0)
+    if path and setup_st.get("path_queue"):
+        images = ("pt_primary.co", "pt_queue.co")  # the two-kernel form (RT_PT_QUEUE=1)
     rec, stale = pmc_record(mode, side, images) if n_gpus == 1 else (None, False)
     traffic = rec["traffic_bytes"] if rec else None
     info = scene.info()  # (after the timed region: parse time, host-side counts)

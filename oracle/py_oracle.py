@@ -242,9 +242,10 @@ def rt_params(width, height, shadows=True, light=(0.0, 60.0, 80.0), nthreads=1,
     # the product's shadow rays (primary+shadow frames and every path vertex)
     # test the light-space lists (its default with the device setup)
     p.shadow_lists = int(bool(shadows or path) if shadow_lists is None else bool(shadow_lists))
-    # the product path-traces in two kernels (its default with the lists):
-    # the primary pass counts per 8x8 block everywhere
-    p.path_queue = int(bool(path) if path_queue is None else bool(path_queue))
+    # path_queue: the product's two-kernel path tracer (RT_PT_QUEUE=1; the
+    # primary pass counts per 8x8 block everywhere); default the one-kernel
+    # pt_kernel (32-pixel waves in geometry tiles)
+    p.path_queue = int(bool(path_queue))
     p.width, p.height = width, height
     p.flags = (RT_SHADOWS if shadows else 0) | (RT_PATH if path else 0)
     p.bounces, p.seed = bounces, seed

@@ -26,9 +26,9 @@ import sys
 
 HBM_PEAK_GBS = 8000.0
 VALU_ISSUE_PEAK_GIPS = 1024 * 2.4 / 2.0
-# the kernels of one frame (config 4: two launches, pt_primary + pt_queue; the
-# one-kernel pt_kernel when the summary has no pt_queue row)
-IMAGE_OF = {"shadow": ("vx_main_rt_kernel",), "path": ("vx_main_pt_primary", "vx_main_pt_queue"),
+# the kernels of one frame (config 4: the one-kernel pt_kernel; under
+# RT_PT_QUEUE=1 two launches, pt_primary + pt_queue)
+IMAGE_OF = {"shadow": ("vx_main_rt_kernel",), "path": ("vx_main_pt_kernel",),
             "flat": ("vx_main_rt_flat",)}
 
 
@@ -53,8 +53,8 @@ def main():
     mode = mode_of(line)
     rows = {r["Name"]: r for r in csv.DictReader(open(a.stats))}
     knames = IMAGE_OF[mode]
-    if mode == "path" and "vx_main_pt_queue" not in rows:
-        knames = ("vx_main_pt_kernel",)
+    if mode == "path" and "vx_main_pt_queue" in rows and "vx_main_pt_kernel" not in rows:
+        knames = ("vx_main_pt_primary", "vx_main_pt_queue")
     for k in knames:
         if k not in rows:
             sys.exit(f"{k} not in {a.stats} (names: {sorted(rows)})")

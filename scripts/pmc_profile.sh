@@ -13,7 +13,7 @@ TAG=${TAG:-pmc}; mkdir -p gpurun_out/$TAG
 MODE=${MODE:-shadow}
 case $MODE in
   shadow) CO=rt_kernel.co; SZ=1024 ;;
-  path)   CO=pt_primary.co,pt_queue.co; SZ=1024 ;;  # one frame = both kernels
+  path)   CO=pt_kernel.co; SZ=1024 ;;  # RT_PT_QUEUE=1: CO=pt_primary.co,pt_queue.co
   flat)   CO=rt_flat.co;   SZ=256 ;;
   *) echo "bad MODE $MODE"; exit 2 ;;
 esac

@@ -45,8 +45,8 @@
 #else
 #define PT_BLOCK 64
 #endif
-#ifndef PT_ILP
-#define PT_ILP 0         // 1: a vertex's bounce walk and shadow-list scan in one loop
+#ifndef PT_COOP
+#define PT_COOP 1        // 32-pixel waves with the shadow lists: lane pairs per path
 #endif
 #ifndef PT_PAIR
 #define PT_PAIR 1        // 0: no paired-vertex code (the shadow lists never pair)
@@ -214,7 +214,7 @@ struct PathState {
 // The next vertex of a path whose bounce ray b from P hit triangle np at t:
 // albedo = the draw3d shader at the hit's MT barycentrics, T *= albedo
 __device__ __forceinline__ void path_hit(const Scene& S, PathState& st, const float P[3], const Ray& b,
-                                         int32_t np, float nt, Counters& cnt) {
+                                         int32_t np, float nt, Counters& cnt, bool counted = true) {
   float w0[3], f1[3], f2[3], b1, b2;
   load_tri(S, np, w0, f1, f2);
   mt_bary(b.o, b.d, w0, f1, f2, &b1, &b2);
@@ -222,9 +222,11 @@ __device__ __forceinline__ void path_hit(const Scene& S, PathState& st, const fl
   gfx::load_prim(S.A, S.prims + 128u * (uint32_t)np, p);
   const gfx::DcState dst = gfx::load_dcstate(S.A, S.dcs + 64u * p.dc());
 #ifdef RT_INSTRUMENT
-  ++cnt.shaded;
-  if (dst.flags & RT_DC_TEX)
-    cnt.texel_bytes += (dst.filter == VX_TEX_FILTER_BILINEAR ? 4u : 1u) * dst.stride;
+  if (counted) {
+    ++cnt.shaded;
+    if (dst.flags & RT_DC_TEX)
+      cnt.texel_bytes += (dst.filter == VX_TEX_FILTER_BILINEAR ? 4u : 1u) * dst.stride;
+  }
 #endif
   const uint32_t a = gfx::shade_weights(S.A, p, dst, gfx::fx_from_float_dev((1.0f - b1) - b2, 24),
                                         gfx::fx_from_float_dev(b1, 24));
@@ -244,10 +246,15 @@ __device__ __forceinline__ void path_hit(const Scene& S, PathState& st, const fl
 // One path vertex for an active lane: direct light through a shadow ray,
 // then (v < bounces) the bounce; returns whether the path continues (st then
 // describes the next vertex), else the pixel is final.  Every lane of the
-// wave calls it; `act` masks the work.
+// wave calls it; `act` masks the work.  COOP: the lane pairs of a 32-pixel
+// wave (lane l and l ^ 32 hold the same path, `hi` = the upper lane) trace
+// the shadow ray on its list and the bounce ray together (trace_coop,
+// occluded_list_coop); both lanes compute the rest, the lower one counts.
+template <bool COOP>
 __device__ __forceinline__ bool path_step(const Scene& S, int32_t* stack, PathState& st, uint32_t v,
-                                          bool act, Counters& cnt) {
+                                          bool act, Counters& cnt, bool hi = false) {
   const bool tie_high = (S.flags & RT_FLAG_TIE_HIGH) != 0;
+  const uint32_t one = hi ? 0u : 1u;  // per-path counters: the lower lane of a pair
   float v0[3], e1[3], e2[3], nrm[3], P[3];
   load_tri(S, act ? st.pid : 0, v0, e1, e2);
   tri_normal(e1, e2, st.d, nrm);
@@ -261,46 +268,13 @@ __device__ __forceinline__ bool path_step(const Scene& S, int32_t* stack, PathSt
   s.d[1] = S.light[1] - P[1];
   s.d[2] = S.light[2] - P[2];
   ray_setup(s);
-  cnt.shadow += act;
-#if PT_ILP
-  if (S.slist_on) {  // both rays of the vertex in one loop (trace_bounce_and_list)
-    bool alive = act && v < S.bounces;
-    Ray b;
-    b.o[0] = P[0]; b.o[1] = P[1]; b.o[2] = P[2];
-    b.d[0] = b.d[1] = b.d[2] = 1.0f;
-    if (alive) {
-      uint32_t x, y;
-      task_pixel(S, st.task, &x, &y);
-      bounce_dir(nrm, pt_key(S.seed, y * S.width + x, v), b.d);  // keyed by pixel, not task
-      cnt.bounce += 1;
-    }
-    ray_setup(b);
-    bool occ = false;
-    float nt = 0.0f;
-    const int32_t np = trace_bounce_and_list(S, b, st.pid, tie_high, &nt, stack, cnt, alive, s, st.pid,
-                                             act, &occ);
-    cnt.occluded += occ;
-    if (act && !occ) {
-      const float cosl = dot3(nrm, s.d) / sqrtf(dot3(s.d, s.d));
-      if (cosl > 0.0f) {
-#pragma unroll
-        for (int k = 0; k < 3; ++k) st.L[k] = fmaf(st.T[k], cosl, st.L[k]);
-      }
-    }
-    if (alive && np < 0) {
-#pragma unroll
-      for (int k = 0; k < 3; ++k) st.L[k] = fmaf(st.T[k], PT_SKY, st.L[k]);
-      alive = false;
-    }
-    if (alive) path_hit(S, st, P, b, np, nt, cnt);
-    return alive;
-  }
-#endif
+  cnt.shadow += act ? one : 0u;
   float ts;
   // the light-space lists when built (occluded_list), else the BVH
-  const bool occ = S.slist_on ? occluded_list(S, s, act, st.pid, cnt)
+  const bool occ = COOP ? occluded_list_coop(S, s, act, st.pid, hi, cnt)
+                 : S.slist_on ? occluded_list(S, s, act, st.pid, cnt)
                               : act && trace<true>(S, s, 0.0f, 1.0f, st.pid, tie_high, &ts, stack, cnt) >= 0;
-  cnt.occluded += occ;
+  cnt.occluded += occ ? one : 0u;
   if (act && !occ) {
     const float cosl = dot3(nrm, s.d) / sqrtf(dot3(s.d, s.d));
     if (cosl > 0.0f) {
@@ -318,15 +292,16 @@ __device__ __forceinline__ bool path_step(const Scene& S, int32_t* stack, PathSt
     task_pixel(S, st.task, &x, &y);
     bounce_dir(nrm, pt_key(S.seed, y * S.width + x, v), b.d);  // keyed by pixel, not task
     ray_setup(b);
-    cnt.bounce += 1;
-    np = trace<false>(S, b, 0.0f, INFINITY, st.pid, tie_high, &nt, stack, cnt);
+    cnt.bounce += one;
+    np = COOP ? trace_coop(S, b, st.pid, tie_high, &nt, stack, hi, cnt)
+              : trace<false>(S, b, 0.0f, INFINITY, st.pid, tie_high, &nt, stack, cnt);
     if (np < 0) {
 #pragma unroll
       for (int k = 0; k < 3; ++k) st.L[k] = fmaf(st.T[k], PT_SKY, st.L[k]);
       alive = false;
     }
   }
-  if (alive) path_hit(S, st, P, b, np, nt, cnt);
+  if (alive) path_hit(S, st, P, b, np, nt, cnt, !hi);
   return alive;
 }
 
@@ -476,7 +451,7 @@ __device__ __forceinline__ void vertex(const Scene& S, PtLds& L, int qi, uint32_
     st.L[k] = q.L[k][j];
   }
   int32_t* stack = &L.stack[threadIdx.x >> 6][0][lane_id()];
-  const bool alive = path_step(S, stack, st, v, act, cnt);
+  const bool alive = path_step<false>(S, stack, st, v, act, cnt);
   enqueue(L, qi ^ 1, alive, st.task, st.alpha, st.pid, st.t, st.o, st.d, st.T, st.L);
   if (act && !alive) store_path_pixel(S, st);
 }
@@ -536,7 +511,7 @@ __device__ __forceinline__ void queued_path(const vx_task_t& task, const Scene& 
     st.d[k] = r.d[k];
     st.L[k] = 0.0f;
   }
-  for (uint32_t v = 0; path_step(S, stack, st, v, true, cnt); ++v) {
+  for (uint32_t v = 0; path_step<false>(S, stack, st, v, true, cnt); ++v) {
   }
   store_path_pixel(S, st);
 }
@@ -550,10 +525,14 @@ __device__ __forceinline__ void lane_path(const vx_task_t& task, const Scene& S,
   uint32_t x, y, lb;
   task_pixel(S, t, &x, &y, &lb);
   const bool in = x < S.width && y < S.height;
-  // paired vertices (path_step_pair) when the whole wave is here and its
-  // upper 32 lanes hold no pixel -- wave-uniform; not with the light-space
-  // shadow lists (a list scan and a BVH walk cannot share one traversal loop)
-  const bool pair = PT_PAIR && !S.slist_on && __ballot(1) == ~0ull && (__ballot(in) >> 32) == 0;
+  // the whole wave is here and its upper 32 lanes hold no pixel (a 32-pixel
+  // wave of a geometry tile) -- wave-uniform: with the light-space shadow
+  // lists and the binary16 BVH4, lane pairs per path (path_step<true>);
+  // without the lists, paired vertices (path_step_pair: a list scan and a BVH
+  // walk cannot share one loop)
+  const bool split = __ballot(1) == ~0ull && (__ballot(in) >> 32) == 0;
+  const bool pair = PT_PAIR && !S.slist_on && split;
+  const bool coop = PT_COOP && S.slist_on && split && (RT_ONLY_BVH4H || (S.flags & RT_FLAG_BVH4H));
   cnt.primary += in;
   const bool tie_high = (S.flags & RT_FLAG_TIE_HIGH) != 0;
   // primary visibility: the raster's winner at this pixel (trace_primary)
@@ -566,7 +545,7 @@ __device__ __forceinline__ void lane_path(const vx_task_t& task, const Scene& S,
   const float th = hit >= 0 ? plane_t(S, r, hit) : 0.0f;
   const bool path = hit >= 0 && secondary_ok(th);  // a path starts at the winner's plane
   if (!path && in) store_pixel(S, t, x, y, color);
-  if (!path && !pair) return;
+  if (!path && !pair && !coop) return;
   const float k255 = 1.0f / 255.0f;
   PathState st;
   st.task = t;
@@ -590,7 +569,27 @@ __device__ __forceinline__ void lane_path(const vx_task_t& task, const Scene& S,
     if (own) store_path_pixel(S, st);
     return;
   }
-  for (uint32_t v = 0; path_step(S, stack, st, v, true, cnt); ++v) {
+  if (coop) {
+    // lane l + 32 takes lane l's path; both trace it, lane l stores it
+    const bool hi = lane_id() >= 32u;
+    const bool own = path && !hi;
+    bool act = xlow(path ? 1u : 0u) != 0u;
+    st.task = xlow(st.task);
+    st.alpha = xlow(st.alpha);
+    st.pid = (int32_t)xlow((uint32_t)st.pid);
+    st.t = xlowf(st.t);
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+      st.o[k] = xlowf(st.o[k]);
+      st.d[k] = xlowf(st.d[k]);
+      st.T[k] = xlowf(st.T[k]);
+    }
+    int32_t* pstack = hi ? stack - 32 : stack;  // the pair's stack: lane l's column
+    for (uint32_t v = 0; act; ++v) act = path_step<true>(S, pstack, st, v, act, cnt, hi);
+    if (own) store_path_pixel(S, st);
+    return;
+  }
+  for (uint32_t v = 0; path_step<false>(S, stack, st, v, true, cnt); ++v) {
   }
   store_path_pixel(S, st);
 }

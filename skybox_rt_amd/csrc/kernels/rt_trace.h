@@ -680,106 +680,208 @@ __device__ __forceinline__ bool occluded_list(const Scene& S, const Ray& s, bool
   return false;
 }
 
-// A path vertex's two rays in one per-lane loop (path tracer, light-space
-// lists, PT_ILP): the bounce ray's closest-hit walk of the binary16 BVH4
-// (trace_impl's per-lane sequence of node steps and leaf tests) and the
-// shadow ray's cell-list scan (occluded_list's sequence) advance one step
-// each per iteration, so a vertex costs the longer of the two instead of
-// their sum.  Each ray's visits, tests and result are its own walk's.
-// `bact` / `sact`: this lane traces a bounce / shadow ray; *occ = the shadow
-// verdict; returns the bounce hit (-1: none).
-__device__ __forceinline__ int32_t trace_bounce_and_list(const Scene& S, const Ray& r, int32_t skip,
-                                                         bool tie_high, float* t_out, int32_t* stack,
-                                                         Counters& cnt, bool bact, const Ray& sr,
-                                                         int32_t sskip, bool sact, bool* occ_out) {
-  // shadow list state (occluded_list)
-  uint32_t so = 0, sn = 0, sq = 0;
-  bool sdone = !sact, occ = false;
-  if (sact) {
-    const uint32_t cell = slist_cell(sr, S.slist_n);
-    so = S.slist + 48u * S.A.ld_u32(S.sidx + 8u * cell);
-    sn = S.A.ld_u32(S.sidx + 8u * cell + 4u);
-    sdone = sn == 0;
+// Cooperative walks for the path tracer's 32-pixel waves (pt_kernel
+// PT_COOP): the wave's upper 32 lanes hold no pixel, so lane l and its
+// partner l ^ 32 trace the same ray together -- the lower lane takes a BVH4
+// node's children 0-1 and a leaf's triangles 0-1, the upper lane children
+// 2-3 and triangles 2-3 (node4_step's four slab tests and four triangle
+// tests split two and two), a light-space list two records each per round.
+// The pair exchanges values with v_permlane32_swap (no LDS); both lanes hold
+// the same stack pointer, node and best hit throughout, so per ray the node
+// visits, the order of the stack and the result are the per-lane walk's
+// (trace_impl / occluded_list), and so are the counters (visits counted by
+// the lower lane, tests by the lane that made them).
+// the partner's value (lane l <-> l ^ 32)
+__device__ __forceinline__ uint32_t xpart(uint32_t v, bool hi) {
+  const auto r = __builtin_amdgcn_permlane32_swap(v, v, false, false);
+  return hi ? r[0] : r[1];
+}
+__device__ __forceinline__ float xpartf(float v, bool hi) {
+  return __uint_as_float(xpart(__float_as_uint(v), hi));
+}
+// the lower lane's value in both lanes of the pair
+__device__ __forceinline__ uint32_t xlow(uint32_t v) {
+  return __builtin_amdgcn_permlane32_swap(v, v, false, false)[0];
+}
+__device__ __forceinline__ float xlowf(float v) { return __uint_as_float(xlow(__float_as_uint(v))); }
+
+// node4_step<SCALAR, true> (closest hit) over a lane pair: the four hits in
+// the same sorting network (cx(0,1) | cx(2,3) within each lane, cx(0,2) and
+// cx(1,3) slot against slot across the pair, cx(1,2) the lower lane's slot 1
+// against the upper's slot 0), the hit children c[1..n-1] pushed at the rows
+// push_sorted gives them (the lower lane writes c[1], the upper c[2], c[3]),
+// the nearest returned to both lanes.  `mem` / `sp`: the pair's stack (the
+// lower lane's LDS column).
+template <bool SCALAR>
+__device__ __forceinline__ int32_t node4_coop(const Scene& S, uint32_t ref, const Ray& r, float lim,
+                                              bool hi, int32_t* mem, int& sp) {
+  auto ld = [&](uint32_t o) { return SCALAR ? S.A.sld_f4(o) : S.A.ld_f4(o); };
+  const uint32_t no = S.nodes4 + 128u * S.num_nodes4 + 64u * ref;
+  const float4 px = ld(no), py = ld(no + 16), pz = ld(no + 32), cf = ld(no + 48);
+  auto h2 = [](float w, float& a, float& b) {
+    const uint32_t u = __float_as_uint(w);
+    a = (float)__builtin_bit_cast(_Float16, (uint16_t)(u & 0xffffu));
+    b = (float)__builtin_bit_cast(_Float16, (uint16_t)(u >> 16));
+  };
+  float lx[2], hx[2], ly[2], hy[2], lz[2], hz[2];
+  h2(hi ? px.y : px.x, lx[0], lx[1]); h2(hi ? px.w : px.z, hx[0], hx[1]);
+  h2(hi ? py.y : py.x, ly[0], ly[1]); h2(hi ? py.w : py.z, hy[0], hy[1]);
+  h2(hi ? pz.y : pz.x, lz[0], lz[1]); h2(hi ? pz.w : pz.z, hz[0], hz[1]);
+  int32_t c[2] = {__float_as_int(hi ? cf.z : cf.x), __float_as_int(hi ? cf.w : cf.y)};
+  float k[2];
+  uint32_t nh = 0;
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    float tn = 0.0f;
+    const bool h = slab(lx[i], hx[i], ly[i], hy[i], lz[i], hz[i], r, 0.0f, lim, &tn) &
+                   (c[i] != RT_EMPTY_REF);
+    k[i] = h ? fminf(tn, 3.402823466e38f) : __builtin_inff();
+    nh += h ? 1u : 0u;
   }
-  // bounce walk state (trace_impl, closest hit)
-  LaneStack lst(stack);
-  int32_t ref = 0;
+  {  // cx(0,1) | cx(2,3)
+    const bool s = k[1] < k[0];
+    const float k0 = k[0], k1 = k[1];
+    const int32_t c0 = c[0], c1 = c[1];
+    k[0] = s ? k1 : k0; k[1] = s ? k0 : k1;
+    c[0] = s ? c1 : c0; c[1] = s ? c0 : c1;
+  }
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {  // cx(0,2), cx(1,3)
+    const float pk = xpartf(k[j], hi);
+    const int32_t pc = (int32_t)xpart((uint32_t)c[j], hi);
+    const bool s = hi ? k[j] < pk : pk < k[j];
+    k[j] = s ? pk : k[j];
+    c[j] = s ? pc : c[j];
+  }
+  {  // cx(1,2)
+    const float kx = hi ? k[0] : k[1];
+    const int32_t cv = hi ? c[0] : c[1];
+    const float pk = xpartf(kx, hi);
+    const int32_t pc = (int32_t)xpart((uint32_t)cv, hi);
+    const bool s = hi ? kx < pk : pk < kx;
+    if (hi) { c[0] = s ? pc : c[0]; }
+    else { c[1] = s ? pc : c[1]; }
+  }
+  const int n = (int)(nh + xpart(nh, hi));
+  if (n == 0) return RT_EMPTY_REF;
+  // entry c[j] at row sp + n - 1 - j (j < n, below RT_MAX_STACK)
+  const int r0 = sp + n - (hi ? 3 : 2), r1 = sp + n - 4;
+  if (r0 >= sp && r0 < RT_MAX_STACK) mem[64 * r0] = hi ? c[0] : c[1];
+  if (hi && r1 >= sp && r1 < RT_MAX_STACK) mem[64 * r1] = c[1];
+  const int top = sp + n - 1;
+  sp = top < RT_MAX_STACK ? top : RT_MAX_STACK;
+  return (int32_t)xlow((uint32_t)c[0]);
+}
+
+// trace<false> (closest hit from 0 below +inf, binary16 BVH4) by a lane pair;
+// both lanes return the hit and *t_out
+__device__ __forceinline__ int32_t trace_coop(const Scene& S, const Ray& r, int32_t skip, bool tie_high,
+                                              float* t_out, int32_t* mem, bool hi, Counters& cnt) {
+  if (S.num_nodes == 0) return -1;
+  int sp = 0;
   float bt = INFINITY;
   int32_t bpid = -1;
-  bool bdone = !bact || S.num_nodes == 0;
-  auto node_next = [&](bool uni, uint32_t at) -> int32_t {
 #ifdef RT_INSTRUMENT
-    ++cnt.visits;
+  cnt.visits += hi ? 0u : 1u;
 #endif
-    return uni ? node4_step<true, true>(S, at, r, 0.0f, bt, false, lst)
-               : node4_step<false, true>(S, at, r, 0.0f, bt, false, lst);
+  int32_t ref = node4_coop<true>(S, 0u, r, bt, hi, mem, sp);
+  if (ref == RT_EMPTY_REF) return -1;
+  auto pop = [&](int32_t& x) {
+    if (sp == 0) return false;
+    x = mem[64 * --sp];
+    return true;
   };
-  if (__ballot(!bdone)) {  // every bouncing lane starts at the root: one scalar step
-    const int32_t nx = node_next(true, 0u);
-    if (!bdone) {
-      if (nx == RT_EMPTY_REF) bdone = true;
-      else ref = nx;
-    }
-  }
-  while (!bdone || !sdone) {
-    if (!bdone) {
-      if (ref >= 0) {  // a node step
-        const int32_t nx = node_next(false, (uint32_t)ref);
-        if (nx != RT_EMPTY_REF) ref = nx;
-        else if (!lst.pop(ref)) bdone = true;
-      } else {  // a leaf's (up to 4) triangles
-        const uint32_t lr = (uint32_t)ref;
-        const uint32_t first = (lr >> 4) & 0x07ffffffu, count = (lr & 15u) + 1u;
-        const uint32_t to = S.tris + 48u * first;
-        float4 ta[4], tb[4], tc[4];
-#pragma unroll
-        for (uint32_t k = 0; k < 4; ++k) {
-          ta[k] = S.A.ld_f4(to + 48u * k);
-          tb[k] = S.A.ld_f4(to + 48u * k + 16);
-          tc[k] = S.A.ld_f4(to + 48u * k + 32);
-        }
-#pragma unroll
-        for (uint32_t k = 0; k < 4; ++k) {
-          if (k < count) {
-            const int32_t pid = __float_as_int(ta[k].w);
+  for (;;) {
+    bool dry = false;
+    while (ref >= 0) {  // while-while, as trace_impl
 #ifdef RT_INSTRUMENT
-            ++cnt.tests;
+      cnt.visits += hi ? 0u : 1u;
 #endif
-            float t;
-            if (pid != skip && mt_hit(r, ta[k], tb[k], tc[k], 0.0f, &t) && closer(t, pid, bt, bpid, tie_high)) {
-              bt = t;
-              bpid = pid;
-            }
-          }
-        }
-        if (!lst.pop(ref)) bdone = true;
-      }
+      const int32_t nx = node4_coop<false>(S, (uint32_t)ref, r, bt, hi, mem, sp);
+      if (nx != RT_EMPTY_REF) { ref = nx; continue; }
+      if (!pop(ref)) { dry = true; break; }
     }
-    if (!sdone) {  // two records of the cell list
-      float4 t[6];
+    if (dry) break;
+    {  // this lane's two of the leaf's (up to 4) triangles (padding records past the end)
+      const uint32_t lr = (uint32_t)ref;
+      const uint32_t first = (lr >> 4) & 0x07ffffffu, count = (lr & 15u) + 1u;
+      const uint32_t k0 = hi ? 2u : 0u;
+      const uint32_t to = S.tris + 48u * (first + k0);
+      float4 ta[2], tb[2], tc[2];
 #pragma unroll
-      for (int w = 0; w < 6; ++w) t[w] = S.A.ld_f4(so + 48u * sq + 16u * w);
+      for (uint32_t k = 0; k < 2; ++k) {
+        ta[k] = S.A.ld_f4(to + 48u * k);
+        tb[k] = S.A.ld_f4(to + 48u * k + 16);
+        tc[k] = S.A.ld_f4(to + 48u * k + 32);
+      }
 #pragma unroll
-      for (int e = 0; e < 2; ++e) {
-        if (!sdone && sq + e < sn) {
+      for (uint32_t k = 0; k < 2; ++k) {
+        if (k0 + k < count) {
+          const int32_t pid = __float_as_int(ta[k].w);
 #ifdef RT_INSTRUMENT
           ++cnt.tests;
 #endif
-          float th;
-          if (__float_as_int(t[3 * e].w) != sskip &&
-              mt_hit(sr, t[3 * e], t[3 * e + 1], t[3 * e + 2], 0.0f, &th) && th < 1.0f) {
-            occ = true;
-            sdone = true;
+          float t;
+          if (pid != skip && mt_hit(r, ta[k], tb[k], tc[k], 0.0f, &t) && closer(t, pid, bt, bpid, tie_high)) {
+            bt = t;
+            bpid = pid;
           }
         }
       }
-      sq += 2;
-      if (sq >= sn) sdone = true;
+      // the pair's best: closer() is a strict total order, so both lanes
+      // agree and it is the four tests' sequential result
+      const float pbt = xpartf(bt, hi);
+      const int32_t pb = (int32_t)xpart((uint32_t)bpid, hi);
+      if (pb >= 0 && closer(pbt, pb, bt, bpid, tie_high)) {
+        bt = pbt;
+        bpid = pb;
+      }
     }
+    if (!pop(ref)) break;
   }
-  *occ_out = occ;
   if (bpid >= 0) *t_out = bt;
   return bpid;
+}
+
+// occluded_list by a lane pair: rounds of four records, the lower lane
+// testing the first two, the upper the other two; the verdict is whether any
+// record occludes (order-free), the tests counted are the sequential scan's
+// (the upper lane's only when the lower lane's two did not occlude)
+__device__ __forceinline__ bool occluded_list_coop(const Scene& S, const Ray& s, bool act, int32_t skip,
+                                                   bool hi, Counters& cnt) {
+  if (!act) return false;
+  const uint32_t cell = slist_cell(s, S.slist_n);
+  const uint32_t off = S.A.ld_u32(S.sidx + 8u * cell), n = S.A.ld_u32(S.sidx + 8u * cell + 4u);
+  const uint32_t e0 = hi ? 2u : 0u;
+  uint32_t o = S.slist + 48u * (off + e0);
+  for (uint32_t q = 0; q < n; q += 4, o += 192u) {
+    bool hit = false;
+#ifdef RT_INSTRUMENT
+    uint32_t tests = 0;
+#endif
+    if (q + e0 < n) {  // 2 records (a padding one at the list's end)
+      float4 t[6];
+#pragma unroll
+      for (int w = 0; w < 6; ++w) t[w] = S.A.ld_f4(o + 16u * w);
+#pragma unroll
+      for (uint32_t e = 0; e < 2; ++e) {
+        if (!hit && q + e0 + e < n) {
+#ifdef RT_INSTRUMENT
+          ++tests;
+#endif
+          float th;
+          hit = __float_as_int(t[3 * e].w) != skip && mt_hit(s, t[3 * e], t[3 * e + 1], t[3 * e + 2], 0.0f, &th) &&
+                th < 1.0f;
+        }
+      }
+    }
+    const bool phit = xpart(hit ? 1u : 0u, hi) != 0u;
+#ifdef RT_INSTRUMENT
+    cnt.tests += (hi && phit) ? 0u : tests;
+#endif
+    if (hit || phit) return true;
+  }
+  return false;
 }
 
 template <bool ANY>

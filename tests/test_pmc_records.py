@@ -12,7 +12,7 @@ import pytest
 from skybox_rt_amd import _lib
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-IMAGES = {"shadow": ("rt_kernel.co",), "path": ("pt_primary.co", "pt_queue.co"),
+IMAGES = {"shadow": ("rt_kernel.co",), "path": ("pt_kernel.co",),
           "flat": ("rt_flat.co",)}
 
 
