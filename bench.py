@@ -298,34 +298,68 @@ class Run:
 
     def timed(self, steps, warmup, dist, render=True, exchange=True):
         """W untimed steps, then EXACTLY `steps` steps between barrier +
-        synchronize on both sides; returns (elapsed s, kernel ms avg, timed
-        launches).  render / exchange = False leave that half out of every
-        step (N > 1: the render and the frame exchange timed apart)."""
+        synchronize on both sides; returns the elapsed seconds.  The frames
+        carry no per-launch events (rt_render_set_timing 0: an event costs
+        the device an idle gap per timed launch), so they run back to back;
+        the kernel's duration comes from kernel_clock.  render / exchange =
+        False leave that half out of every step (N > 1: the render and the
+        frame exchange timed apart)."""
         import torch
-        for _ in range(warmup):
-            self.step(render, exchange)
-        self.drain()
-        if dist is not None:
-            dist.barrier()
-        torch.cuda.synchronize()
-        ms0, nt0, n0 = self.r.run_totals()
-        gc.disable()  # no collector pause inside the timed region
+        self.r.set_timing(False)
         try:
-            t0 = time.perf_counter()
-            for _ in range(steps):
+            for _ in range(warmup):
                 self.step(render, exchange)
-            self.drain()  # every frame rendered (and gathered + assembled) inside the region
-            torch.cuda.synchronize()
+            self.drain()
             if dist is not None:
                 dist.barrier()
-            elapsed = time.perf_counter() - t0
+            torch.cuda.synchronize()
+            _, _, n0 = self.r.run_totals()
+            gc.disable()  # no collector pause inside the timed region
+            try:
+                t0 = time.perf_counter()
+                for _ in range(steps):
+                    self.step(render, exchange)
+                self.drain()  # every frame rendered (and gathered + assembled) inside the region
+                torch.cuda.synchronize()
+                if dist is not None:
+                    dist.barrier()
+                elapsed = time.perf_counter() - t0
+            finally:
+                gc.enable()
+            _, _, n1 = self.r.run_totals()
         finally:
-            gc.enable()
-        ms1, nt1, n1 = self.r.run_totals()
-        if not render:
-            return elapsed, None, 0
-        assert n1 - n0 == steps and nt1 > nt0, (n0, n1, nt0, nt1)
-        return elapsed, (ms1 - ms0) / (nt1 - nt0), nt1 - nt0
+            self.r.set_timing(True)
+        assert n1 - n0 == (steps if render else 0), (n0, n1)
+        return elapsed
+
+
+    def kernel_clock(self, steps, warmup):
+        """Average kernel duration per frame over a back-to-back run: the
+        driver untimed (no per-launch events, no queue bound), `steps` frames
+        started back to back, bracketed by two HIP events recorded on the
+        driver's stream (the stream the kernel runs on): (stop - start) /
+        steps.  Per-launch events cost the timed launch an idle gap and start
+        it cold (rocprofv3 kernel trace: ~+1.5 us on a 24 us frame), so this,
+        not their average, is the duration the roofline divides by; it equals
+        rocprofv3's per-dispatch average of the same command."""
+        import torch
+        r = self.r
+        stream = torch.cuda.ExternalStream(r.device_stream())
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        r.set_timing(False)
+        try:
+            for _ in range(warmup):
+                r.start()
+            r.wait()
+            e0.record(stream)
+            for _ in range(steps):
+                r.start()
+            e1.record(stream)
+            r.wait()
+            e1.synchronize()
+        finally:
+            r.set_timing(True)
+        return e0.elapsed_time(e1) / steps
 
 
 def reduce_max_sum(dist, coll_dev, elapsed, rays):
@@ -455,7 +489,10 @@ def main():
     # frame (driver VX_HIP_QUEUE_DEPTH, default 2) so the host's launch and
     # completion-poll overhead overlaps the previous frame; every frame is
     # complete before the timed region ends
-    elapsed, avg_kernel_ms, timed_launches = run.timed(args.steps, args.warmup, dist)
+    elapsed = run.timed(args.steps, args.warmup, dist)
+    # the kernel's average duration: HIP events around a back-to-back run of
+    # the same frames on the driver's stream (Run.kernel_clock)
+    avg_kernel_ms = run.kernel_clock(max(50, min(args.steps, 1000)), max(5, min(args.warmup, 20)))
     st = r.stats()
     elapsed, rays_total = reduce_max_sum(dist, coll_dev, elapsed, run.rays_local)
     ms_per_step = elapsed / args.steps * 1e3
@@ -467,8 +504,8 @@ def main():
     split = None
     if use_gather:
         split_steps = max(20, min(args.steps, 500))
-        e_r, _, _ = run.timed(split_steps, 5, dist, exchange=False)
-        e_x, _, _ = run.timed(split_steps, 5, dist, render=False)
+        e_r = run.timed(split_steps, 5, dist, exchange=False)
+        e_x = run.timed(split_steps, 5, dist, render=False)
         e_r, _ = reduce_max_sum(dist, coll_dev, e_r, 0)
         e_x, _ = reduce_max_sum(dist, coll_dev, e_x, 0)
         split = {"steps": split_steps, "render_ms_per_step": round(e_r / split_steps * 1e3, 5),
@@ -496,7 +533,8 @@ def main():
                                 "same_as": "value"}
                 continue
             sr = make_run(s)
-            e2, k2, _ = sr.timed(series_steps, 10, dist)
+            e2 = sr.timed(series_steps, 10, dist)
+            k2 = sr.kernel_clock(series_steps, 5)
             e2, rays2 = reduce_max_sum(dist, coll_dev, e2, sr.rays_local)
             series[name] = {"side": s, "steps": series_steps,
                             "value": round(rays2 * series_steps / e2 / 1e6, 3),
@@ -591,9 +629,10 @@ def main():
             "rays_per_frame": int(rays_total),
             "mrays_per_s_per_gpu": round(value / n_gpus, 3),
             "kernel_ms": round(avg_kernel_ms, 5),
-            "frames": "queued (vx_start behind the in-flight frame, depth "
-                      f"{os.environ.get('VX_HIP_QUEUE_DEPTH', '2')}); kernel_ms = HIP events on "
-                      f"{timed_launches} of the {args.steps} timed launches",
+            "frames": "back to back (vx_start queues behind the in-flight frames; no per-launch "
+                      "events in the timed region); kernel_ms = two HIP events on the driver's "
+                      f"stream around {max(50, min(args.steps, 1000))} such frames after the "
+                      "timed region / frames (render only)",
             "sync_ms_per_step": round(sync_ms, 5) if sync_ms is not None else None,
             "kernel_mrays_per_s": round(run.rays_local / (avg_kernel_ms * 1e-3) / 1e6, 3),
             "counters": "off in the timed frames (rays per frame from the instrumented pre-run)",

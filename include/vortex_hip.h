@@ -49,6 +49,11 @@ typedef int (*vx_hip_set_counters_t)(vx_device_h hdevice, int enable);
  * counters of all its launches; then launches are single runs again.  Only
  * between groups (-1 inside one); never waits. */
 typedef int (*vx_hip_launch_group_t)(vx_device_h hdevice, uint32_t n);
+/* timed (1, the default: HIP events on one run in VX_HIP_TIME_EVERY, queue
+ * depth VX_HIP_QUEUE_DEPTH) or untimed (0: no events and no queue bound, so
+ * back-to-back starts reach the GPU without the idle gap an event costs --
+ * for timing a run of launches by a host clock).  Waits for the device. */
+typedef int (*vx_hip_set_timing_t)(vx_device_h hdevice, int timed);
 
 #ifdef __cplusplus
 }

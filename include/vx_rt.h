@@ -133,6 +133,11 @@ int rt_render_kernel_ms(rt_renderer_h r, double* kernel_ms);
  * one in VX_HIP_TIME_EVERY: kernel_ms_sum / timed is their average. */
 int rt_render_run_totals(rt_renderer_h r, double* kernel_ms_sum, uint64_t* timed,
                          uint64_t* launches);
+/* 1: launches timed by HIP events as above (the default); 0: untimed -- no
+ * events and no queue bound, so a run of rt_render_start calls reaches the
+ * GPU back to back (bench.py's stream clock: wall time of K such frames / K).
+ * Waits for the in-flight frames. */
+int rt_render_set_timing(rt_renderer_h r, int timed);
 /* linear W*H framebuffer (shard_count == 1) or compact tile buffer
  * (local_tiles * 1024 pixels in task order) */
 int rt_read_framebuffer(rt_renderer_h r, uint32_t* out, uint64_t count);

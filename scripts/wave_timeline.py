@@ -92,14 +92,16 @@ def main():
             "primary": float(rows[slow, 0].mean()), "shadow": float(rows[slow, 1].mean()),
             "primary_per_iter": float((rows[slow, 0] / pi).mean()),
             "shadow_per_iter": float((rows[slow, 1] / si).mean())}
-    if path:  # pt stamp image: 10 wave cycles (s_memtime), 4 paired-traversal cycles,
-        # 5 vertex steps, 6 post-traversal (bounce-hit shading) cycles
+    if path:  # pt stamp image: 10 wave cycles (s_memtime), 5 vertex steps, 6 bounce-hit
+        # shading cycles; lane pairs (path_step<true>): 4 shadow-list cycles, 2
+        # bounce-walk cycles; paired vertices: 4 paired-traversal cycles
         cyc = rows[:, 10].astype(np.float64)
         ghz = cyc[slow] / (dur[slow] * 10.0)
         out["slowest50"].update({
             "clock_ghz": float(ghz.mean()),
             "vertex_steps": float(rows[slow, 5].mean()),
             "traversal_frac": float((rows[slow, 4] / np.maximum(cyc[slow], 1)).mean()),
+            "bounce_walk_frac": float((rows[slow, 2] / np.maximum(cyc[slow], 1)).mean()),
             "shade_frac": float((rows[slow, 6] / np.maximum(cyc[slow], 1)).mean()),
             "node_loop_frac": float((rows[slow, 11] / np.maximum(cyc[slow], 1)).mean()),
             "node_iters": float(rows[slow, 9].mean()),

@@ -292,6 +292,7 @@ int rt_renderer_create(rt_scene_h s, const char* kernel_dir, rt_renderer_h* out)
   r->run_totals = (vx_hip_run_totals_t)vx_driver_symbol("vx_hip_run_totals");
   r->set_counters = (vx_hip_set_counters_t)vx_driver_symbol("vx_hip_set_counters");
   r->launch_group = (vx_hip_launch_group_t)vx_driver_symbol("vx_hip_launch_group");
+  r->set_timing = (vx_hip_set_timing_t)vx_driver_symbol("vx_hip_set_timing");
   // the two-kernel path tracer's images (binary16 BVH4 only; the others run
   // the one-kernel pt_kernel images), from the kernel directory itself: a
   // directory without them (e.g. lib/pt_compact) runs its own pt_kernel
@@ -1049,6 +1050,12 @@ int rt_render_kernel_ms(rt_renderer_h r, double* kernel_ms) {
   uint32_t grid = 0, block = 0;
   if (!r->last_run || r->last_run(r->dev, kernel_ms, &grid, &block) != 0)
     return fail("vx_hip_last_run failed");
+  return 0;
+}
+
+int rt_render_set_timing(rt_renderer_h r, int timed) {
+  if (!r) return fail("null argument");
+  if (!r->set_timing || r->set_timing(r->dev, timed) != 0) return fail("vx_hip_set_timing failed");
   return 0;
 }
 

@@ -67,6 +67,7 @@ struct rt_renderer {
   vx_hip_run_totals_t run_totals = nullptr;
   vx_hip_set_counters_t set_counters = nullptr;
   vx_hip_launch_group_t launch_group = nullptr;
+  vx_hip_set_timing_t set_timing = nullptr;
   std::string kdir;         // kernel directory (images missing there come from lib_dir)
   bool deep = false;        // generic RT/PT images (every BVH layout, 32-entry stack)
   // the primary rays' tree of the current configuration (rt_renderer_export_vis_tree;

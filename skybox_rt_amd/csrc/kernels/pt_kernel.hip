@@ -243,6 +243,18 @@ __device__ __forceinline__ void path_hit(const Scene& S, PathState& st, const fl
   st.t = nt;
 }
 
+#ifdef RT_STAMPS  // diagnostic image: per-wave cycle accumulators (scripts/wave_timeline.py)
+#define PT_CYC() __builtin_amdgcn_s_memtime()
+#define PT_ACC(slot, v)                                                            \
+  do {                                                                             \
+    if (lane_id() == (uint32_t)__builtin_ctzll(__ballot(1)))                      \
+      ((volatile uint32_t*)__vx_mpm_lds)[slot] += (uint32_t)(v);                  \
+  } while (0)
+#else
+#define PT_CYC() 0ull
+#define PT_ACC(slot, v) do {} while (0)
+#endif
+
 // One path vertex for an active lane: direct light through a shadow ray,
 // then (v < bounces) the bounce; returns whether the path continues (st then
 // describes the next vertex), else the pixel is final.  Every lane of the
@@ -270,11 +282,17 @@ __device__ __forceinline__ bool path_step(const Scene& S, int32_t* stack, PathSt
   ray_setup(s);
   cnt.shadow += act ? one : 0u;
   float ts;
+  const uint64_t c0 = PT_CYC();
   // the light-space lists when built (occluded_list), else the BVH
   const bool occ = COOP ? occluded_list_coop(S, s, act, st.pid, hi, cnt)
                  : S.slist_on ? occluded_list(S, s, act, st.pid, cnt)
                               : act && trace<true>(S, s, 0.0f, 1.0f, st.pid, tie_high, &ts, stack, cnt) >= 0;
   cnt.occluded += occ ? one : 0u;
+  const uint64_t c1 = PT_CYC();
+  if (COOP) {
+    PT_ACC(4, c1 - c0);  // cycles in the shadow-list scan
+    PT_ACC(5, 1);        // vertex steps
+  }
   if (act && !occ) {
     const float cosl = dot3(nrm, s.d) / sqrtf(dot3(s.d, s.d));
     if (cosl > 0.0f) {
@@ -301,7 +319,12 @@ __device__ __forceinline__ bool path_step(const Scene& S, int32_t* stack, PathSt
       alive = false;
     }
   }
+  const uint64_t c2 = PT_CYC();
   if (alive) path_hit(S, st, P, b, np, nt, cnt, !hi);
+  if (COOP) {
+    PT_ACC(2, c2 - c1);           // cycles in the bounce walk (and its setup)
+    PT_ACC(6, PT_CYC() - c2);     // cycles shading the bounce hit
+  }
   return alive;
 }
 
@@ -315,17 +338,6 @@ __device__ __forceinline__ bool path_step(const Scene& S, int32_t* stack, PathSt
 // (Shadow rays as wave packets, occluded_packet, then the bounce rays per
 // lane: 0.31 ms vs 0.22 ms, measured -- a path's later shadow rays are
 // incoherent and the two traversals no longer overlap.)
-#ifdef RT_STAMPS  // diagnostic image: per-wave cycle accumulators (scripts/wave_timeline.py)
-#define PT_CYC() __builtin_amdgcn_s_memtime()
-#define PT_ACC(slot, v)                                                            \
-  do {                                                                             \
-    if (lane_id() == (uint32_t)__builtin_ctzll(__ballot(1)))                      \
-      ((volatile uint32_t*)__vx_mpm_lds)[slot] += (uint32_t)(v);                  \
-  } while (0)
-#else
-#define PT_CYC() 0ull
-#define PT_ACC(slot, v) do {} while (0)
-#endif
 __device__ __forceinline__ bool path_step_pair(const Scene& S, int32_t* stack, PathState& st,
                                                uint32_t v, bool act, Counters& cnt) {
   const bool tie_high = (S.flags & RT_FLAG_TIE_HIGH) != 0;

@@ -343,8 +343,9 @@ __device__ __forceinline__ void flush(int slot, uint32_t v) { vx_mpm_add(RT_MPM_
 // 5 (71 VGPRs, 6-7 resident) 0.02574 ms, 7 0.02470, 8 (64 VGPRs, 39 SGPR
 // spills) 0.02532: the frame is latency-bound with the chip full of waves
 // (DESIGN 4.1), so more resident waves win until the spills cost more.
-// (r02: capping occupancy lower with LDS padding cost +27 / +80 %.)
-#if !defined(RT_WAVES_PER_EU) && !RT_FLAT
+// (r02: capping occupancy lower with LDS padding cost +27 / +80 %.)  The
+// deep images (every layout, 32-entry stack) keep the compiler's choice.
+#if !defined(RT_WAVES_PER_EU) && !RT_FLAT && RT_ONLY_BVH4H
 #define RT_WAVES_PER_EU 7
 #endif
 #ifdef RT_WAVES_PER_EU

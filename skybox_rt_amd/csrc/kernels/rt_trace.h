@@ -793,16 +793,22 @@ __device__ __forceinline__ int32_t trace_coop(const Scene& S, const Ray& r, int3
   };
   for (;;) {
     bool dry = false;
-    while (ref >= 0) {  // while-while, as trace_impl
+    {
+      RT_CYC_BEGIN();
+      while (ref >= 0) {  // while-while, as trace_impl
+        RT_WAVE_ITER(9);
 #ifdef RT_INSTRUMENT
-      cnt.visits += hi ? 0u : 1u;
+        cnt.visits += hi ? 0u : 1u;
 #endif
-      const int32_t nx = node4_coop<false>(S, (uint32_t)ref, r, bt, hi, mem, sp);
-      if (nx != RT_EMPTY_REF) { ref = nx; continue; }
-      if (!pop(ref)) { dry = true; break; }
+        const int32_t nx = node4_coop<false>(S, (uint32_t)ref, r, bt, hi, mem, sp);
+        if (nx != RT_EMPTY_REF) { ref = nx; continue; }
+        if (!pop(ref)) { dry = true; break; }
+      }
+      RT_CYC_END(11);
     }
     if (dry) break;
-    {  // this lane's two of the leaf's (up to 4) triangles (padding records past the end)
+    {
+      RT_WAVE_ITER(9);  // this lane's two of the leaf's (up to 4) triangles (padding records past the end)
       const uint32_t lr = (uint32_t)ref;
       const uint32_t first = (lr >> 4) & 0x07ffffffu, count = (lr & 15u) + 1u;
       const uint32_t k0 = hi ? 2u : 0u;

@@ -186,6 +186,7 @@ class vx_device {
     const uint64_t te = env_u64("VX_HIP_TIME_EVERY", 4);
     time_every_ = te < 1 ? 1 : te > 16 ? 16 : (int)te;
     launch_mode_ = (int)env_u64("VX_HIP_EXT_LAUNCH", 1);
+    launch_mode_timed_ = launch_mode_;
     counters_env_ = env_u64("VX_HIP_COUNTERS", 0) != 0;
     return 0;
   }
@@ -460,6 +461,14 @@ class vx_device {
     return 0;
   }
   void set_counters(bool on) { counters_ = on; }  // applies from the next start()
+  // timed (1: events on one run in time_every_, the default) or untimed (0:
+  // no events, no queue bound -- back-to-back launches for a host clock)
+  int set_timing(int timed) {
+    if (group_pos_ != 0) return -1;
+    wait_idle();
+    launch_mode_ = timed ? (launch_mode_timed_ == 2 ? 1 : launch_mode_timed_) : 2;
+    return 0;
+  }
   // the next n launches form one run (then single launches again)
   int launch_group(uint32_t n) {
     if (n < 1 || n > 4 || group_pos_ != 0) return -1;  // not inside a group
@@ -587,6 +596,7 @@ class vx_device {
   // 1: hipExtModuleLaunchKernel, start/stop timestamps on the dispatch packet;
   // 2: diagnostic -- every run untimed (no events, no queue bound)
   int launch_mode_ = 1;
+  int launch_mode_timed_ = 1;  // the mode set_timing(1) restores
   double run_ms_total_ = 0.0;
   uint64_t runs_total_ = 0;
   Module* last_module_ = nullptr;
@@ -736,6 +746,10 @@ __attribute__((visibility("default"))) int vx_hip_set_counters(vx_device_h hdevi
   if (hdevice == nullptr) return -1;
   ((vx_device*)hdevice)->set_counters(enable != 0);
   return 0;
+}
+__attribute__((visibility("default"))) int vx_hip_set_timing(vx_device_h hdevice, int timed) {
+  if (hdevice == nullptr) return -1;
+  return ((vx_device*)hdevice)->set_timing(timed);
 }
 __attribute__((visibility("default"))) int vx_hip_launch_group(vx_device_h hdevice, uint32_t n) {
   if (hdevice == nullptr) return -1;

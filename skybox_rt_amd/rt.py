@@ -125,6 +125,7 @@ def lib():
             "rt_render_kernel_ms": [vp, C.POINTER(C.c_double)],
             "rt_render_run_totals": [vp, C.POINTER(C.c_double), C.POINTER(C.c_uint64),
                                      C.POINTER(C.c_uint64)],
+            "rt_render_set_timing": [vp, C.c_int],
             "rt_read_framebuffer": [vp, vp, u64],
             "rt_read_depthbuffer": [vp, vp, u64],
             "rt_launch_rows": [vp, vp, u64, C.POINTER(u64)],
@@ -397,6 +398,12 @@ class Renderer:
         _check(lib().rt_render_run_totals(self._h, C.byref(ms), C.byref(nt), C.byref(n)),
                "rt_render_run_totals")
         return ms.value, nt.value, n.value
+
+    def set_timing(self, timed: bool) -> None:
+        """Events on the launches (True, the default) or none (False: no queue
+        bound either, back-to-back frames for a host clock); waits for the
+        in-flight frames."""
+        _check(lib().rt_render_set_timing(self._h, 1 if timed else 0), "rt_render_set_timing")
 
     def framebuffer(self) -> np.ndarray:
         p = self.params

@@ -289,6 +289,20 @@ def test_queued_frames_equal_synchronous_frames(path):
     assert n1 - n0 == 7 and nt1 > nt0 and ms1 > ms0
     assert np.array_equal(r.framebuffer(), ref)
     assert r.stats()["primary_rays"] == 512 * 512
+    # untimed (rt_render_set_timing 0: no events, no queue bound -- bench.py's
+    # kernel clock): 40 back-to-back frames, none timed, all complete
+    r.set_timing(False)
+    try:
+        for _ in range(40):
+            r.start()
+        r.wait()
+        ms2, nt2, n2 = r.run_totals()
+        assert n2 - n1 == 40 and nt2 == nt1 and ms2 == ms1
+        assert np.array_equal(r.framebuffer(), ref)
+    finally:
+        r.set_timing(True)
+    r.render()
+    assert r.run_totals()[1] == nt2 + 1      # timed again (a start on an idle queue)
 
 
 def test_rtapp_cli_against_golden():
