@@ -1231,17 +1231,16 @@ __device__ __forceinline__ bool secondary_ok(float t) { return t > 0.0f && t < I
 // order, each overwriting; draw3d/main.cpp:179 + gpu_sw.h:38-61); one
 // wave-uniform rt_vtri_t per step through the scalar cache.  Returns the pid
 // to shade (layer pid, or `spid` unchanged).
-__device__ __forceinline__ int32_t resolve_layers(const Scene& S, uint32_t px, uint32_t py, bool need,
-                                                  int32_t spid, Counters& cnt) {
+// `tests`: per lane, the layers it tested (the RT_INSTRUMENT count)
+__device__ __forceinline__ int32_t resolve_layers_n(const Scene& S, uint32_t px, uint32_t py, bool need,
+                                                    int32_t spid, uint32_t* tests) {
   uint64_t pend = __ballot(need);
   for (uint32_t k = 0; pend != 0 && k < S.num_layer; ++k) {
     uint4 lw[3];
     S.A.sld_u4n<3>(S.vlayers + 64u * k, lw);  // one pointer: merged wide s_loads
     const uint4 A = lw[0], B = lw[1], C = lw[2];
     const bool mine = (pend & (1ull << lane_id())) != 0;
-#ifdef RT_INSTRUMENT
-    cnt.layer_tests += mine;
-#endif
+    *tests += mine ? 1u : 0u;
     bool f = false;
     if (mine && rect_in(C.y, px) && rect_in(C.z, py)) {
       const int32_t e0[3] = {(int32_t)A.x, (int32_t)A.y, (int32_t)A.z};
@@ -1253,6 +1252,17 @@ __device__ __forceinline__ int32_t resolve_layers(const Scene& S, uint32_t px, u
     if (f) spid = (int32_t)C.w;
     pend &= ~__ballot(f);
   }
+  return spid;
+}
+__device__ __forceinline__ int32_t resolve_layers(const Scene& S, uint32_t px, uint32_t py, bool need,
+                                                  int32_t spid, Counters& cnt) {
+  uint32_t tests = 0;
+  spid = resolve_layers_n(S, px, py, need, spid, &tests);
+#ifdef RT_INSTRUMENT
+  cnt.layer_tests += tests;
+#else
+  (void)cnt;
+#endif
   return spid;
 }
 
