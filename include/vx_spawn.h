@@ -177,8 +177,11 @@ __device__ __forceinline__ uint32_t __vx_wave_sum(uint32_t v) {
  * rows (a wave-uniform constant): no cross-lane sums, no LDS atomics --
  * with the block barriers of VX_MAIN also gone then, config 3 measured
  * 0.02372 -> 0.01982 ms (A/B r03r). */
+#ifndef VX_ROWS_GATE
+#define VX_ROWS_GATE 1  /* 0: count and meet at the block barriers regardless */
+#endif
 __device__ __forceinline__ void vx_mpm_add(int slot, uint32_t v) {
-  if (!__vx_dcrs[VX_DCR_HIP_MPM_ROWS]) return;
+  if (VX_ROWS_GATE && !__vx_dcrs[VX_DCR_HIP_MPM_ROWS]) return;
   const uint32_t s = __vx_wave_sum(v);
   if ((threadIdx.x & 63u) == 0 && s && slot < VX_MPM_ROW) atomicAdd(&__vx_mpm_lds[slot], s);
 }
@@ -328,7 +331,7 @@ __device__ __forceinline__ int vx_spawn_chunks_block(uint32_t num_tasks, F kerne
     /* the block's counter row: only when the driver reads rows (then the   */    \
     /* block's waves meet at entry and exit; without, each wave runs and    */    \
     /* retires on its own)                                                  */    \
-    const bool rows_on = __vx_dcrs[VX_DCR_HIP_MPM_ROWS] != 0;                        \
+    const bool rows_on = !VX_ROWS_GATE || __vx_dcrs[VX_DCR_HIP_MPM_ROWS] != 0;       \
     if (rows_on) {                                                                   \
       if (threadIdx.x < VX_MPM_ROW) __vx_mpm_lds[threadIdx.x] = 0;                   \
       __syncthreads();                                                               \
@@ -338,7 +341,8 @@ __device__ __forceinline__ int vx_spawn_chunks_block(uint32_t num_tasks, F kerne
     (void)__vx_main_body(vx_ptr<ArgT>(a));                                           \
     if (rows_on) {                                                                   \
       __syncthreads();                                                               \
-      if (threadIdx.x < VX_MPM_ROW && blockIdx.x < VX_MAX_GRID)                      \
+      if (__vx_dcrs[VX_DCR_HIP_MPM_ROWS] && threadIdx.x < VX_MPM_ROW &&              \
+          blockIdx.x < VX_MAX_GRID)                                                  \
         __vx_state.mpm[blockIdx.x][threadIdx.x] = __vx_mpm_lds[threadIdx.x];         \
     }                                                                                \
   }                                                                                  \
