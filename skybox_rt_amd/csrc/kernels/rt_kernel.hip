@@ -90,31 +90,13 @@ __device__ __forceinline__ void kernel_body(const vx_task_t& task, const Scene& 
 #ifdef RT_STAMPS
   if (lane_id() == 0) __vx_mpm_lds[3] = (uint32_t)__builtin_amdgcn_s_memrealtime();
 #endif
-#ifndef RT_LAYERS_FIRST
-#define RT_LAYERS_FIRST 0
-#endif
-#if RT_LAYERS_FIRST
-  // the screen layers first, for every pixel in the image: their scalar
-  // record loads and tests no longer wait for the primary pass; a pixel
-  // keeps its layer only where no geometry wins (and counts the tests only
-  // there, as resolve_layers after the primary pass would)
-  uint32_t ltests = 0;
-  const int32_t lay = resolve_layers_n(S, x, y, in, -1, &ltests);
-#endif
   // primary visibility: the raster's winner at this pixel
   const int32_t hit = trace_primary(S, lb, x, y, in, tie_high, cnt);
 #ifdef RT_STAMPS
   if (lane_id() == 0) __vx_mpm_lds[14] = (uint32_t)__builtin_amdgcn_s_memrealtime();
 #endif
   cnt.hits += hit >= 0;
-#if RT_LAYERS_FIRST
-#ifdef RT_INSTRUMENT
-  cnt.layer_tests += (in && hit < 0) ? ltests : 0u;
-#endif
-  const int32_t spid = hit >= 0 ? hit : lay;
-#else
   const int32_t spid = resolve_layers(S, x, y, in && hit < 0, hit, cnt);
-#endif
 #ifdef RT_STAMPS
   if (lane_id() == 0) __vx_mpm_lds[4] = (uint32_t)__builtin_amdgcn_s_memrealtime();
 #endif
