@@ -33,6 +33,13 @@ namespace rtk {
 
 struct Counters {
   uint32_t primary = 0, shadow = 0, hits = 0, occluded = 0, bounce = 0;
+// RT_CNT(stmt): a counter update that only the instrumented images
+// (RT_INSTRUMENT, the *_stats kernels) compile
+#ifdef RT_INSTRUMENT
+#define RT_CNT(...) __VA_ARGS__
+#else
+#define RT_CNT(...)
+#endif
 #ifdef RT_INSTRUMENT
   uint32_t visits = 0, tests = 0, layer_tests = 0, shaded = 0, texel_bytes = 0;
   uint32_t rect_tests = 0, edge_tests = 0;  // flat image: work executed per wave
@@ -401,9 +408,7 @@ __device__ __forceinline__ int32_t trace_impl(const Scene& S, const Ray& r, floa
   // one node step: the next node to visit (nearest hit child), the other hit
   // children pushed farthest first; RT_EMPTY_REF when no child is hit
   auto node_next = [&](bool uni, int32_t r0) -> int32_t {
-#ifdef RT_INSTRUMENT
-    ++cnt.visits;
-#endif
+    RT_CNT(++cnt.visits;)
     const float lim = ANY ? tmax : bt;
     if (RT_ONLY_BVH4H || (S.flags & RT_FLAG_BVH4H))
       return uni ? node4_step<true, true>(S, (uint32_t)r0, r, tmin, lim, ANY, lst)
@@ -474,9 +479,7 @@ __device__ __forceinline__ int32_t trace_impl(const Scene& S, const Ray& r, floa
       for (uint32_t k = 0; k < 4; ++k) {
         if (k < count) {
           const int32_t pid = __float_as_int(ta[k].w);
-#ifdef RT_INSTRUMENT
-          ++cnt.tests;
-#endif
+          RT_CNT(++cnt.tests;)
           float t;
           if (pid != skip && mt_hit(r, ta[k], tb[k], tc[k], tmin, &t)) {
             if (ANY) {
@@ -541,9 +544,7 @@ __device__ __forceinline__ bool occluded_packet(const Scene& S, const Ray& r, bo
   for (;;) {
     const bool live = on && !done;
     if (ref >= 0) {
-#ifdef RT_INSTRUMENT
-      cnt.visits += live;
-#endif
+      RT_CNT(cnt.visits += live;)
       RT_WAVE_ITER(9);
       const uint32_t no = S.nodes4 + 128u * S.num_nodes4 + 64u * (uint32_t)ref;
       uint4 nw[4];
@@ -611,9 +612,7 @@ __device__ __forceinline__ bool occluded_packet(const Scene& S, const Ray& r, bo
 #pragma unroll
         for (uint32_t j = 0; j < H; ++j) {
           if (q0 + j < count) {
-#ifdef RT_INSTRUMENT
-            cnt.tests += lv;
-#endif
+            RT_CNT(cnt.tests += lv;)
             float t;
             if (lv && __float_as_int(ta[j].w) != skip && mt_hit(r, ta[j], tb[j], tc[j], 0.0f, &t) &&
                 t < tmax) {
@@ -668,9 +667,7 @@ __device__ __forceinline__ bool occluded_list(const Scene& S, const Ray& s, bool
 #pragma unroll
     for (int e = 0; e < 2; ++e) {
       if (q + e >= n) break;
-#ifdef RT_INSTRUMENT
-      ++cnt.tests;
-#endif
+      RT_CNT(++cnt.tests;)
       float th;
       if (__float_as_int(t[3 * e].w) != skip && mt_hit(s, t[3 * e], t[3 * e + 1], t[3 * e + 2], 0.0f, &th) &&
           th < 1.0f)
@@ -781,9 +778,7 @@ __device__ __forceinline__ int32_t trace_coop(const Scene& S, const Ray& r, int3
   int sp = 0;
   float bt = INFINITY;
   int32_t bpid = -1;
-#ifdef RT_INSTRUMENT
-  cnt.visits += hi ? 0u : 1u;
-#endif
+  RT_CNT(cnt.visits += hi ? 0u : 1u;)
   int32_t ref = node4_coop<true>(S, 0u, r, bt, hi, mem, sp);
   if (ref == RT_EMPTY_REF) return -1;
   auto pop = [&](int32_t& x) {
@@ -797,9 +792,7 @@ __device__ __forceinline__ int32_t trace_coop(const Scene& S, const Ray& r, int3
       RT_CYC_BEGIN();
       while (ref >= 0) {  // while-while, as trace_impl
         RT_WAVE_ITER(9);
-#ifdef RT_INSTRUMENT
-        cnt.visits += hi ? 0u : 1u;
-#endif
+        RT_CNT(cnt.visits += hi ? 0u : 1u;)
         const int32_t nx = node4_coop<false>(S, (uint32_t)ref, r, bt, hi, mem, sp);
         if (nx != RT_EMPTY_REF) { ref = nx; continue; }
         if (!pop(ref)) { dry = true; break; }
@@ -824,9 +817,7 @@ __device__ __forceinline__ int32_t trace_coop(const Scene& S, const Ray& r, int3
       for (uint32_t k = 0; k < 2; ++k) {
         if (k0 + k < count) {
           const int32_t pid = __float_as_int(ta[k].w);
-#ifdef RT_INSTRUMENT
-          ++cnt.tests;
-#endif
+          RT_CNT(++cnt.tests;)
           float t;
           if (pid != skip && mt_hit(r, ta[k], tb[k], tc[k], 0.0f, &t) && closer(t, pid, bt, bpid, tie_high)) {
             bt = t;
@@ -862,9 +853,7 @@ __device__ __forceinline__ bool occluded_list_coop(const Scene& S, const Ray& s,
   uint32_t o = S.slist + 48u * (off + e0);
   for (uint32_t q = 0; q < n; q += 4, o += 192u) {
     bool hit = false;
-#ifdef RT_INSTRUMENT
-    uint32_t tests = 0;
-#endif
+    RT_CNT(uint32_t tests = 0;)
     if (q + e0 < n) {  // 2 records (a padding one at the list's end)
       float4 t[6];
 #pragma unroll
@@ -872,9 +861,7 @@ __device__ __forceinline__ bool occluded_list_coop(const Scene& S, const Ray& s,
 #pragma unroll
       for (uint32_t e = 0; e < 2; ++e) {
         if (!hit && q + e0 + e < n) {
-#ifdef RT_INSTRUMENT
-          ++tests;
-#endif
+          RT_CNT(++tests;)
           float th;
           hit = __float_as_int(t[3 * e].w) != skip && mt_hit(s, t[3 * e], t[3 * e + 1], t[3 * e + 2], 0.0f, &th) &&
                 th < 1.0f;
@@ -882,9 +869,7 @@ __device__ __forceinline__ bool occluded_list_coop(const Scene& S, const Ray& s,
       }
     }
     const bool phit = xpart(hit ? 1u : 0u, hi) != 0u;
-#ifdef RT_INSTRUMENT
-    cnt.tests += (hi && phit) ? 0u : tests;
-#endif
+    RT_CNT(cnt.tests += (hi && phit) ? 0u : tests;)
     if (hit || phit) return true;
   }
   return false;
@@ -1080,9 +1065,7 @@ __device__ __forceinline__ int32_t trace_primary_packet(const Scene& S, uint32_t
   int32_t ref = 0;
   for (;;) {
     if (ref >= 0) {
-#ifdef RT_INSTRUMENT
-      cnt.visits += l0;
-#endif
+      RT_CNT(cnt.visits += l0;)
       RT_WAVE_ITER(7);
       const uint32_t o = S.vnodes + 64u * (uint32_t)ref;
       uint4 vw[4];
@@ -1145,9 +1128,7 @@ __device__ __forceinline__ int32_t trace_primary_packet(const Scene& S, uint32_t
 #pragma unroll
         for (uint32_t j = 0; j < H; ++j) {
           if (k0 + j < count) {
-#ifdef RT_INSTRUMENT
-            cnt.tests += l0;
-#endif
+            RT_CNT(cnt.tests += l0;)
             vis_test(A[j], B[j], C[j], D[j], px, py, tie_high, bz, bpid);
           }
         }
