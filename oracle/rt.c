@@ -83,6 +83,7 @@ typedef struct {
   uint32_t bl_nbx;
   uint32_t* sl_idx;               /* shadow_lists: per light-space cell (first entry, count) */
   int32_t* sl_ent;                /* per entry: geometry index (c->geom) */
+  float* sl_key;                  /* per entry: its sort key (sl_key) */
   int32_t* vpids;                 /* its leaf records' pids */
   uint32_t num_vnodes;
   int32_t* vhit;                  /* [W*H] primary winner per pixel (packet pre-pass) */
@@ -155,7 +156,7 @@ static int rt_prepare(rt_ctx_t* c, const orc_scene_t* s, const orc_rt_params_t* 
 static void rt_release(rt_ctx_t* c) {
   free(c->rp); free(c->rp_ok); free(c->prim_dc); free(c->tri); free(c->geom); free(c->dcst);
   free(c->bl_idx); free(c->bl_ent);
-  free(c->sl_idx); free(c->sl_ent);
+  free(c->sl_idx); free(c->sl_ent); free(c->sl_key);
   free(c->vis); free(c->vnodes); free(c->vpids); free(c->vhit);
   pthread_mutex_destroy(&c->mu);
 }
@@ -812,8 +813,12 @@ static uint32_t path_trace(const rt_ctx_t* c, uint32_t px, const float d0[3], fl
  * cell widened by SL_EPS.  Conservative: a triangle MT accepts for a ray meets
  * the ray's direction, which lies in the ray's cell, and the widening covers
  * fp32 rounding; the lists only narrow the candidates -- a ray's verdict is
- * the brute-force any-hit's.  A ray tests its cell's list in ascending
- * geometry index until the first occluder.  All arithmetic fp32, no
+ * the brute-force any-hit's.  A cell's list is ordered by (key, geometry
+ * index), key = the squared distance from the light to the triangle's
+ * bounding box (sl_key: a lower bound of |X - L|^2 over its points); a ray
+ * tests its cell's list in that order until the first occluder, or until a
+ * record whose key exceeds |L - P|^2 * 1.001 (that triangle has no point on
+ * the segment, nor has any after it).  All arithmetic fp32, no
  * contraction, the device's operation order. */
 #define SL_N 256
 #define SL_EPS (1.0f / 512.0f)
@@ -929,6 +934,26 @@ static void sl_pairs(const rt_ctx_t* c, const float L[3], uint32_t* cnt, uint32_
   }
 }
 
+/* rt_setup.hip sl_key: squared distance from L to the box of (v0, v0 + e1,
+ * v0 + e2) */
+static float sl_key(const float* t9, const float L[3]) {
+  float s = 0.0f;
+  for (int k = 0; k < 3; ++k) {
+    const float p = t9[k], q = t9[k] + t9[3 + k], u = t9[k] + t9[6 + k];
+    const float lo = fminf(p, fminf(q, u)), hi = fmaxf(p, fmaxf(q, u));
+    const float d = L[k] < lo ? lo - L[k] : (L[k] > hi ? L[k] - hi : 0.0f);
+    s = s + d * d;
+  }
+  return s;
+}
+static const float* sl_sort_keys;
+static int sl_cmp(const void* a, const void* b) {
+  const int32_t x = *(const int32_t*)a, y = *(const int32_t*)b;
+  const float kx = sl_sort_keys[x], ky = sl_sort_keys[y];
+  if (kx != ky) return kx < ky ? -1 : 1;
+  return x < y ? -1 : (x > y ? 1 : 0);
+}
+
 static void sl_build(rt_ctx_t* c) {
   uint32_t* cnt = (uint32_t*)calloc(SL_CELLS, sizeof(uint32_t));
   sl_pairs(c, c->p.light, cnt, NULL, NULL);
@@ -943,6 +968,16 @@ static void sl_build(rt_ctx_t* c) {
   }
   c->sl_ent = (int32_t*)malloc(sizeof(int32_t) * (tot ? tot : 1));
   sl_pairs(c, c->p.light, NULL, cur, c->sl_ent);  /* ascending k within each cell */
+  /* then by (key, k): nearest to the light first */
+  float* gk = (float*)malloc(sizeof(float) * (c->num_geom ? c->num_geom : 1));
+  for (int k = 0; k < c->num_geom; ++k) gk[k] = sl_key(c->tri + (size_t)c->geom[k] * 9, c->p.light);
+  sl_sort_keys = gk;
+  for (uint32_t i = 0; i < SL_CELLS; ++i)
+    if (c->sl_idx[2 * i + 1] > 1)
+      qsort(c->sl_ent + c->sl_idx[2 * i], c->sl_idx[2 * i + 1], sizeof(int32_t), sl_cmp);
+  c->sl_key = (float*)malloc(sizeof(float) * (tot ? tot : 1));
+  for (uint64_t e = 0; e < tot; ++e) c->sl_key[e] = gk[c->sl_ent[e]];
+  free(gk);
   free(cnt);
   free(cur);
 }
@@ -967,7 +1002,9 @@ static uint32_t sl_cell_of(const float sd[3]) {
 static int sl_occluded(const rt_ctx_t* c, const float so[3], const float sd[3], int skip, uint64_t* tests) {
   const uint32_t cell = sl_cell_of(sd);
   const uint32_t o = c->sl_idx[2 * cell], n = c->sl_idx[2 * cell + 1];
+  const float lim = (sd[0] * sd[0] + sd[1] * sd[1] + sd[2] * sd[2]) * 1.001f;
   for (uint32_t q = 0; q < n; ++q) {
+    if (c->sl_key[o + q] > lim) return 0;  /* this and every later record: off the segment */
     const int g = c->geom[c->sl_ent[o + q]];
     ++*tests;
     const float* t9 = c->tri + (size_t)g * 9;

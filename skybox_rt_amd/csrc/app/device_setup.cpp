@@ -276,7 +276,8 @@ int shadow_lists(rt_renderer* r, uint32_t* launches) {
   r->sl_entries = st[2];
   r->setup.slist_entries = st[2];
   if (!block_lists_fit(st[1], st[2])) return 0;  // the packet walk, as without lists
-  if (alloc_tmp(r, (uint64_t)st[2] * 4 + 4, &tmp) || alloc(r, ((uint64_t)st[2] + 1) * 48, &r->slist, &a.slist_addr))
+  // tmp: the entries' geometry indices, then their sort keys
+  if (alloc_tmp(r, (uint64_t)st[2] * 8 + 8, &tmp) || alloc(r, ((uint64_t)st[2] + 1) * 48, &r->slist, &a.slist_addr))
     return -1;
   g.btmp_addr = tmp.addr;
   g.slist_addr = a.slist_addr;

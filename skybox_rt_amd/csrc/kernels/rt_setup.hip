@@ -900,18 +900,43 @@ __device__ void phase_scount(const rt_setup_arg_t* a) {
   sl_for_cells(a, [&](uint32_t, uint32_t cell) { atomicAdd(&cnt[cell], 1u); });
 }
 
+// a list entry's sort key: a lower bound of |X - L|^2 over the triangle's
+// points X -- the squared distance from the light L to the triangle's
+// bounding box (corners v0, v0 + e1, v0 + e2); oracle/rt.c sl_key, the same
+// float operations in the same order (no contraction)
+__device__ __forceinline__ float sl_key(const rt_tri_t& r, const float L[3]) {
+  const float* t = reinterpret_cast<const float*>(&r);
+  float s = 0.0f;
+  for (int k = 0; k < 3; ++k) {
+    const float p = t[k], q = t[k] + t[4 + k], u = t[k] + t[8 + k];
+    const float lo = fminf(p, fminf(q, u)), hi = fmaxf(p, fmaxf(q, u));
+    const float d = L[k] < lo ? lo - L[k] : (L[k] > hi ? L[k] - hi : 0.0f);
+    s = s + d * d;
+  }
+  return s;
+}
+
 __device__ void phase_sfill(const rt_setup_arg_t* a) {
   uint32_t* cur = vx_ptr<uint32_t>(a->bcnt_addr);
   const uint2* sidx = vx_ptr<const uint2>(a->bidx_addr);
+  const rt_tri_t* geom = vx_ptr<const rt_tri_t>(a->geom_addr);
   uint32_t* tmp = vx_ptr<uint32_t>(a->btmp_addr);
-  sl_for_cells(a, [&](uint32_t j, uint32_t cell) { tmp[sidx[cell].x + atomicAdd(&cur[cell], 1u)] = j; });
+  uint32_t* key = tmp + a->blist_entries;  // the entries' sort keys (float bits)
+  sl_for_cells(a, [&](uint32_t j, uint32_t cell) {
+    const uint32_t pos = sidx[cell].x + atomicAdd(&cur[cell], 1u);
+    tmp[pos] = j;
+    key[pos] = __float_as_uint(sl_key(geom[j], a->light));
+  });
 }
 
-// a wave per cell: every entry's rank by geometry index (distinct), its
-// rt_tri_t copied to that position
+// a wave per cell: every entry's rank by (sort key, geometry index) -- the
+// nearest-to-the-light bounding boxes first, ties by index (distinct) -- its
+// rt_tri_t copied to that position with the key in the second word's w
+// (rt_tri_t e1.w, 0 in the geometry records), where the scan reads it
 __device__ void phase_ssort(const rt_setup_arg_t* a) {
   const uint2* sidx = vx_ptr<const uint2>(a->bidx_addr);
   const uint32_t* tmp = vx_ptr<const uint32_t>(a->btmp_addr);
+  const uint32_t* key = tmp + a->blist_entries;
   const uint4* geom = vx_ptr<const uint4>(a->geom_addr);
   uint4* out = vx_ptr<uint4>(a->slist_addr);
   const uint32_t waves = gridDim.x * (RTS_BLOCK / 64), l = lane_id();
@@ -921,11 +946,19 @@ __device__ void phase_ssort(const rt_setup_arg_t* a) {
     const uint2 oc = sload(sidx + c);
     for (uint32_t base = 0; base < oc.y; base += 64) {
       const uint32_t i = base + l;
-      const uint32_t me = tmp[oc.x + (i < oc.y ? i : 0u)];
+      const uint32_t me = tmp[oc.x + (i < oc.y ? i : 0u)], mk = key[oc.x + (i < oc.y ? i : 0u)];
       uint32_t rank = 0;
-      for (uint32_t q = 0; q < oc.y; ++q) rank += sload(tmp + oc.x + q) < me ? 1u : 0u;
-      if (i < oc.y)
-        for (int w = 0; w < 3; ++w) out[3ull * (oc.x + rank) + w] = geom[3ull * me + w];
+      for (uint32_t q = 0; q < oc.y; ++q) {
+        const uint32_t j = sload(tmp + oc.x + q), k = sload(key + oc.x + q);  // keys >= 0: bits order as floats
+        rank += (k < mk || (k == mk && j < me)) ? 1u : 0u;
+      }
+      if (i < oc.y) {
+        out[3ull * (oc.x + rank)] = geom[3ull * me];
+        uint4 w1 = geom[3ull * me + 1];
+        w1.w = mk;
+        out[3ull * (oc.x + rank) + 1] = w1;
+        out[3ull * (oc.x + rank) + 2] = geom[3ull * me + 2];
+      }
     }
   }
 }

@@ -654,11 +654,20 @@ __device__ __forceinline__ uint32_t slist_cell(const Ray& s, uint32_t N) {
   const int cy = min(max((int)floorf((uj / m + 1.0f) * hn), 0), (int)N - 1);
   return ((uint32_t)f * N + (uint32_t)cy) * N + (uint32_t)cx;
 }
+// The scan bound: a cell's records come nearest-to-the-light first (sort
+// key = squared distance from the light to the triangle's bounding box, in
+// the record's e1.w; rt_setup.hip SSORT); a triangle whose key exceeds
+// |light - origin|^2 (with a 0.1 % margin) has no point on the segment, nor
+// has any record after it, so the scan ends there, untested.
+__device__ __forceinline__ float slist_limit(const Ray& s) {
+  return (s.d[0] * s.d[0] + s.d[1] * s.d[1] + s.d[2] * s.d[2]) * 1.001f;
+}
 __device__ __forceinline__ bool occluded_list(const Scene& S, const Ray& s, bool act, int32_t skip,
                                               Counters& cnt) {
   if (!act) return false;
   const uint32_t cell = slist_cell(s, S.slist_n);
   const uint32_t off = S.A.ld_u32(S.sidx + 8u * cell), n = S.A.ld_u32(S.sidx + 8u * cell + 4u);
+  const float lim = slist_limit(s);
   uint32_t o = S.slist + 48u * off;
   for (uint32_t q = 0; q < n; q += 2, o += 96u) {
     float4 t[6];
@@ -667,6 +676,7 @@ __device__ __forceinline__ bool occluded_list(const Scene& S, const Ray& s, bool
 #pragma unroll
     for (int e = 0; e < 2; ++e) {
       if (q + e >= n) break;
+      if (t[3 * e + 1].w > lim) return false;
       RT_CNT(++cnt.tests;)
       float th;
       if (__float_as_int(t[3 * e].w) != skip && mt_hit(s, t[3 * e], t[3 * e + 1], t[3 * e + 2], 0.0f, &th) &&
@@ -850,9 +860,10 @@ __device__ __forceinline__ bool occluded_list_coop(const Scene& S, const Ray& s,
   const uint32_t cell = slist_cell(s, S.slist_n);
   const uint32_t off = S.A.ld_u32(S.sidx + 8u * cell), n = S.A.ld_u32(S.sidx + 8u * cell + 4u);
   const uint32_t e0 = hi ? 2u : 0u;
+  const float lim = slist_limit(s);
   uint32_t o = S.slist + 48u * (off + e0);
   for (uint32_t q = 0; q < n; q += 4, o += 192u) {
-    bool hit = false;
+    bool hit = false, end = false;  // end: a record past the bound (occluded_list)
     RT_CNT(uint32_t tests = 0;)
     if (q + e0 < n) {  // 2 records (a padding one at the list's end)
       float4 t[6];
@@ -860,17 +871,23 @@ __device__ __forceinline__ bool occluded_list_coop(const Scene& S, const Ray& s,
       for (int w = 0; w < 6; ++w) t[w] = S.A.ld_f4(o + 16u * w);
 #pragma unroll
       for (uint32_t e = 0; e < 2; ++e) {
-        if (!hit && q + e0 + e < n) {
-          RT_CNT(++tests;)
-          float th;
-          hit = __float_as_int(t[3 * e].w) != skip && mt_hit(s, t[3 * e], t[3 * e + 1], t[3 * e + 2], 0.0f, &th) &&
-                th < 1.0f;
+        if (!hit && !end && q + e0 + e < n) {
+          end = t[3 * e + 1].w > lim;
+          if (!end) {
+            RT_CNT(++tests;)
+            float th;
+            hit = __float_as_int(t[3 * e].w) != skip &&
+                  mt_hit(s, t[3 * e], t[3 * e + 1], t[3 * e + 2], 0.0f, &th) && th < 1.0f;
+          }
         }
       }
     }
-    const bool phit = xpart(hit ? 1u : 0u, hi) != 0u;
-    RT_CNT(cnt.tests += (hi && phit) ? 0u : tests;)
-    if (hit || phit) return true;
+    // the records are sorted: past the lower lane's bound the upper lane's
+    // are too, so the first event in list order decides
+    const uint32_t ev = (hit ? 1u : 0u) | (end ? 2u : 0u), pev = xpart(ev, hi);
+    RT_CNT(cnt.tests += (hi && pev != 0u) ? 0u : tests;)
+    if (((ev | pev) & 1u) != 0u) return true;
+    if (((ev | pev) & 2u) != 0u) return false;
   }
   return false;
 }

@@ -188,7 +188,9 @@ def test_configure_4096_with_lists_is_timed():
 @pytest.mark.parametrize("light", [(0.0, 60.0, 80.0), (30.0, -20.0, 95.0), (0.0, 0.0, 0.5)])
 def test_shadow_lists_equal_oracle(oracle_lib, name, light):
     """The device-built light-space lists == the oracle's (every cell's first
-    entry and count, every entry's triangle record in ascending pid order)."""
+    entry and count, every entry's triangle record in (key, index) order, the
+    key -- the squared distance from the light to the triangle's bounding box
+    -- in the record's e1.w word, equal to a float32 restatement)."""
     po = oracle_lib
     s = rt.Scene.load(scene_path(name))
     r = rt.Renderer(s)
@@ -201,7 +203,25 @@ def test_shadow_lists_equal_oracle(oracle_lib, name, light):
     assert np.array_equal(didx, idx)
     assert st["slist_entries"] == len(ent) and slist.shape == (len(ent) + 1, 12)
     geom = r.records("geom")
-    assert np.array_equal(slist[:-1].view(np.uint32), geom[ent].view(np.uint32))
+    got = slist[:-1].copy()
+    keys = got[:, 7].copy()
+    got[:, 7] = 0.0
+    assert np.array_equal(got.view(np.uint32), geom[ent].view(np.uint32))
+    # sl_key in float32, the kernels' operation order
+    g = geom[ent].astype(np.float32)
+    L = np.asarray(light, dtype=np.float32)
+    ks = np.zeros(len(ent), dtype=np.float32)
+    for k in range(3):
+        p, q, u = g[:, k], g[:, k] + g[:, 4 + k], g[:, k] + g[:, 8 + k]
+        lo = np.minimum(p, np.minimum(q, u))
+        hi = np.maximum(p, np.maximum(q, u))
+        d = np.where(L[k] < lo, lo - L[k], np.where(L[k] > hi, L[k] - hi, np.float32(0.0)))
+        ks = (ks + d * d).astype(np.float32)
+    assert np.array_equal(keys.view(np.uint32), ks.view(np.uint32))
+    # each cell ascending by key
+    n = idx.reshape(-1, 2)
+    for o, c in n[n[:, 1] > 1][:200]:
+        assert np.all(np.diff(keys[o:o + c]) >= 0)
     r.close()
     s.close()
 
