@@ -68,7 +68,7 @@ def algorithmic_bytes(st: dict, pixels: int, node_bytes: int = NODE_BYTES) -> in
 # the kernel images of one frame per workload (config 4: the one-kernel
 # pt_kernel; pt_primary + pt_queue under RT_PT_QUEUE=1)
 PMC_IMAGES = {"shadow": ("rt_kernel.co",), "path": ("pt_kernel.co",),
-              "flat": ("rt_flat.co",)}
+              "flat": ("rt_flat.co",), "bvh": ("rt_bvh.co",)}
 
 
 def pmc_record(mode: str, side: int, images=None):
@@ -94,6 +94,23 @@ def pmc_record(mode: str, side: int, images=None):
     if t.get("kernel_md5") != md5 or t.get("width") != side or t.get("height") != side:
         return None, True
     return t, False
+
+
+def issue_roofline(rec: dict, kernel_ms: float, mode: str):
+    """VALU issue rate of the timed image (the PMC record's SQ_INSTS_VALU over
+    the kernel's duration) against 1228.8 G wave-instructions/s, with the
+    record's wait / utilisation / hit ratios; None without SQ counters."""
+    if not rec or not rec.get("sq", {}).get("SQ_INSTS_VALU"):
+        return None
+    d = rec.get("derived", {})
+    gips = rec["sq"]["SQ_INSTS_VALU"] / (kernel_ms * 1e-3) / 1e9
+    return {"bound": "valu_issue", "achieved": round(gips, 2), "peak": VALU_ISSUE_PEAK_GIPS,
+            "unit": "G wave-instr/s", "frac": round(gips / VALU_ISSUE_PEAK_GIPS, 4),
+            "valu_insts_per_launch": int(rec["sq"]["SQ_INSTS_VALU"]),
+            **{k: d[k] for k in ("wait_any_frac", "wait_inst_any_frac", "active_inst_any_frac",
+                                 "active_inst_valu_frac", "valu_lane_utilisation",
+                                 "l1_hit_rate", "l2_hit_rate") if k in d},
+            "source": f"profiles/pmc_{mode}.json (rocprofv3 --pmc passes, scripts/pmc_profile.sh)"}
 
 
 def frame_side(n_gpus: int, base: int) -> int:
@@ -228,10 +245,10 @@ class Run:
     """One timed configuration of the renderer (+ the RCCL gather at N > 1)."""
 
     def __init__(self, r, rt, dist, coll_dev, rank, n_gpus, side, shadows, light, path, flat,
-                 bounces, use_gather):
+                 bounces, use_gather, bvh_walk=False):
         self.r, self.side, self.n = r, side, n_gpus
         self.kw = dict(shadows=shadows, light=light, shard_index=rank, shard_count=n_gpus,
-                       path=path, bounces=bounces, flat=flat)
+                       path=path, bounces=bounces, flat=flat, bvh_walk=bvh_walk)
         # algorithmic bytes per launch and rays per frame from the instrumented
         # variant (untimed; its counters equal the oracle's traversal,
         # tests/test_gpu_rt.py): the timed product image writes no counters
@@ -393,6 +410,9 @@ def main():
                          "path: config 4, 4-bounce diffuse path trace; "
                          "flat: config 2, 256^2 primary rays over the flat triangle list")
     ap.add_argument("--bounces", type=int, default=4)
+    ap.add_argument("--no-bvh-series", action="store_true",
+                    help="N=1 primary+shadow: skip the series entry timing the same frame by BVH "
+                         "traversal only (image rt_bvh)")
     ap.add_argument("--verify-gather", action="store_true",
                     help="N>1: rank 0 checks the gathered frame against its own full render")
     ap.add_argument("--plumbing-check", action="store_true",
@@ -464,9 +484,9 @@ def main():
     r = rt.Renderer(scene)
     bvh_st = r.bvh_stats()  # the renderer's tree, built on the device at creation
 
-    def make_run(s):
+    def make_run(s, bvh_walk=False):
         return Run(r, rt, dist, coll_dev, rank, n_gpus, s, shadows, light, path, flat,
-                   args.bounces, use_gather)
+                   args.bounces, use_gather, bvh_walk)
 
     run = make_run(side)
     setup_st = r.setup_stats()  # the timed configuration's records (configure)
@@ -540,6 +560,43 @@ def main():
                             "value": round(rays2 * series_steps / e2 / 1e6, 3),
                             "ms_per_step": round(e2 / series_steps * 1e3, 5),
                             "kernel_ms": round(k2, 5), "rays_per_frame": int(rays2)}
+    # BASELINE config 3 by BVH traversal only (RT_RENDER_BVH_WALK, image
+    # rt_bvh: primary visibility by the binary16-BVH4 packet walk, shadow
+    # rays by the shadow packet walk; no block or light-space lists): the
+    # same frame, steps and warm-up as `value`, with its own algorithmic
+    # bytes (node_visits > 0), kernel clock and PMC record
+    if n_gpus == 1 and not path and not flat and shadows and not args.no_bvh_series:
+        br = make_run(side, bvh_walk=True)
+        eb = br.timed(args.steps, args.warmup, dist)
+        kb = br.kernel_clock(max(50, min(args.steps, 1000)), max(5, min(args.warmup, 20)))
+        bi = br.inst
+        b_bytes = algorithmic_bytes(bi, bi["primary_rays"], (NODE4H_BYTES if r.bvh4_f16 else NODE4_BYTES)
+                                    if r.bvh4 else NODE_BYTES)
+        b_ach = b_bytes / (kb * 1e-3) / 1e9
+        b_rec, b_stale = pmc_record("bvh", side)
+        b_roof = {"bound": "hbm", "achieved": round(b_ach, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                  "frac": round(b_ach / HBM_PEAK_GBS, 4),
+                  "traffic": b_rec["traffic_bytes"] if b_rec else None,
+                  "algorithmic_bytes_per_launch": int(b_bytes),
+                  "counts": {k: int(bi[k]) for k in ("node_visits", "tri_tests", "layer_tests",
+                                                     "texel_bytes", "primary_rays", "shadow_rays",
+                                                     "bounce_rays")}}
+        if b_stale:
+            b_roof["traffic_stale"] = True
+        if b_rec:
+            b_roof["measured_hbm_frac"] = round(b_rec["traffic_bytes"] / (kb * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)
+            b_roof["pmc_source"] = "profiles/pmc_bvh.json"
+        series["bvh_walk"] = {
+            "workload": (f"{side}x{side} primary+shadow rays, tekkaman.cgltrace, BVH traversal only "
+                         f"(BASELINE config 3): primary visibility by a {bvh_kind} packet walk per "
+                         f"8x8-block wave (raster-exact leaf tests, node/leaf records through the "
+                         f"scalar cache, wave stack in one VGPR); shadow rays ballot/mbcnt-compacted "
+                         f"into full waves, each a {bvh_kind} any-hit packet walk"),
+            "image": "rt_bvh (entry vx_main_rt_bvh)", "side": side, "steps": args.steps,
+            "warmup": args.warmup, "value": round(br.rays_local * args.steps / eb / 1e6, 3),
+            "ms_per_step": round(eb / args.steps * 1e3, 5), "kernel_ms": round(kb, 5),
+            "rays_per_frame": int(br.rays_local), "roofline": b_roof,
+            "roofline_issue": issue_roofline(b_rec, kb, "bvh")}
     if rank != 0:
         dist.destroy_process_group()
         return
@@ -661,19 +718,10 @@ def main():
         out["roofline"]["measured_hbm_frac"] = round(traffic / (avg_kernel_ms * 1e-3) / 1e9
                                                      / HBM_PEAK_GBS, 4)
         out["roofline"]["pmc_source"] = f"profiles/pmc_{mode}.json"
-        d = rec.get("derived", {})
-        if rec.get("sq", {}).get("SQ_INSTS_VALU"):
-            # the binding resource: VALU issue (and what the waves wait on)
-            gips = rec["sq"]["SQ_INSTS_VALU"] / (avg_kernel_ms * 1e-3) / 1e9
-            out["roofline_issue"] = {
-                "bound": "valu_issue", "achieved": round(gips, 2), "peak": VALU_ISSUE_PEAK_GIPS,
-                "unit": "G wave-instr/s", "frac": round(gips / VALU_ISSUE_PEAK_GIPS, 4),
-                "valu_insts_per_launch": int(rec["sq"]["SQ_INSTS_VALU"]),
-                **{k: d[k] for k in ("wait_any_frac", "wait_inst_any_frac", "active_inst_any_frac",
-                                     "active_inst_valu_frac", "valu_lane_utilisation",
-                                     "l1_hit_rate", "l2_hit_rate") if k in d},
-                "source": f"profiles/pmc_{mode}.json (rocprofv3 --pmc passes, scripts/pmc_profile.sh)",
-            }
+        # the binding resource: VALU issue (and what the waves wait on)
+        ri = issue_roofline(rec, avg_kernel_ms, mode)
+        if ri is not None:
+            out["roofline_issue"] = ri
     if flat:
         # the flat list is read from LDS and the scalar cache, never from HBM,
         # and the kernel prunes with an integer rectangle test: its bound is

@@ -47,7 +47,10 @@ typedef int (*vx_hip_set_counters_t)(vx_device_h hdevice, int enable);
  * its first launch, stop event on its last: the frame's span), counted as
  * one run by vx_hip_run_totals / vx_hip_last_run, and vx_mpm_query sums the
  * counters of all its launches; then launches are single runs again.  Only
- * between groups (-1 inside one); never waits. */
+ * between groups (-1 inside one, or when (VX_HIP_QUEUE_DEPTH +
+ * VX_HIP_TIME_EVERY) * n exceeds the driver's 64 in-flight slots); never
+ * waits.  n = 0 abandons an open group after a failed launch inside it: the
+ * launches already issued retire as one untimed run. */
 typedef int (*vx_hip_launch_group_t)(vx_device_h hdevice, uint32_t n);
 /* timed (1, the default: HIP events on one run in VX_HIP_TIME_EVERY, queue
  * depth VX_HIP_QUEUE_DEPTH) or untimed (0: no events and no queue bound, so

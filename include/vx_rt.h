@@ -53,6 +53,13 @@ typedef struct {
 #define RT_RENDER_COVERAGE 0x1000u     /* with RT_RENDER_RASTER: the raster regression app's
                                           coverage image (tests/regression/raster/kernel.cpp:
                                           covered pixels 0xffffffff, no shading, no OM state) */
+#define RT_RENDER_BVH_WALK 0x2000u     /* primary+shadow / path frames without the per-block
+                                          and light-space lists: primary visibility by the BVH4
+                                          packet walk, shadow rays by the BVH (BASELINE config 3's
+                                          "full BVH traversal"); primary+shadow frames run their
+                                          own image (rt_bvh: entry vx_main_rt_bvh).  Env
+                                          RT_BLOCK_LISTS=0 RT_SHADOW_LISTS=0 give the same frames
+                                          on the default image */
 
 typedef struct {
   uint32_t width, height;
@@ -232,7 +239,7 @@ int rt_renderer_setup_stats(rt_renderer_h r, rt_setup_stats_t* stats);
 #define RT_REC_PTRIS 8u     /* rt_tri_t per primitive (clip v0 + pid, e1, e2) */
 #define RT_REC_GEOM 9u      /* rt_tri_t per geometry primitive */
 #define RT_REC_BIDX 10u     /* uint32[2] per local 8x8 block: first list entry, count */
-#define RT_REC_BLIST 11u    /* rt_bentry_t per list entry (+2 padding entries) */
+#define RT_REC_BLIST 11u    /* rt_bentry_t per list entry (+3 padding entries, RT_BLIST_PAD) */
 #define RT_REC_SIDX 12u     /* uint32[2] per light-space cell: first entry, count */
 #define RT_REC_SLIST 13u    /* rt_tri_t per light-space list entry (+1 padding record) */
 int rt_renderer_export_records(rt_renderer_h r, uint32_t which, void* out, uint64_t bytes,

@@ -115,7 +115,7 @@ typedef struct {
 
 typedef struct {
   uint64_t primary_rays, shadow_rays, geometry_hits, occluded;
-  uint64_t node_visits, tri_tests, layer_tests, shaded, texel_bytes;
+  uint64_t node_visits, tri_tests, layer_tests, shaded, texel_bytes;  /* layer_tests: per wave */
   uint64_t bounce_rays;
 } orc_rt_counters_t;
 

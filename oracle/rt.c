@@ -87,6 +87,7 @@ typedef struct {
   int32_t* vpids;                 /* its leaf records' pids */
   uint32_t num_vnodes;
   int32_t* vhit;                  /* [W*H] primary winner per pixel (packet pre-pass) */
+  uint32_t* lcnt;                 /* [W*H] screen layers the pixel's lane tested */
   int next_tile_row;
   float* tri;                     /* [num_prims][9] v0,e1,e2 (clip x,y,w) */
   int32_t* geom;                  /* geometry prim ids, ascending */
@@ -157,7 +158,7 @@ static void rt_release(rt_ctx_t* c) {
   free(c->rp); free(c->rp_ok); free(c->prim_dc); free(c->tri); free(c->geom); free(c->dcst);
   free(c->bl_idx); free(c->bl_ent);
   free(c->sl_idx); free(c->sl_ent); free(c->sl_key);
-  free(c->vis); free(c->vnodes); free(c->vpids); free(c->vhit);
+  free(c->vis); free(c->vnodes); free(c->vpids); free(c->vhit); free(c->lcnt);
   pthread_mutex_destroy(&c->mu);
 }
 
@@ -547,26 +548,36 @@ static void vis_scan_block(const rt_ctx_t* c, int n, const uint32_t* px, const u
 
 /* the primary pre-pass over one row of 32x32 tiles: every wave's packet
  * (8x8 blocks, or 8x4 halves in split tiles, the kernels' task_map) */
-static void vis_tile_row(rt_ctx_t* c, uint32_t ty, orc_rt_counters_t* k) {
+/* the in-image pixels of wave `wv` of tile (tx, ty): an 8x8 block, or an 8x4
+ * half in a split tile (the kernels' task_map); returns their number */
+static int wave_pixels(const rt_ctx_t* c, uint32_t tx, uint32_t ty, int split, int wv, uint32_t* px,
+                       uint32_t* py, int32_t* idx) {
   const uint32_t W = c->p.width, H = c->p.height;
+  const int lanes = split ? 32 : 64;
+  int n = 0;
+  for (int ln = 0; ln < lanes; ++ln) {
+    const uint32_t ti = split ? (((uint32_t)wv >> 1) << 6) + (uint32_t)ln + (((uint32_t)wv & 1u) << 5)
+                              : ((uint32_t)wv << 6) + (uint32_t)ln;
+    const uint32_t blk = ti >> 6, l = ti & 63u;
+    const uint32_t x = tx * 32 + (blk & 3u) * 8 + (l & 7u), y = ty * 32 + (blk >> 2) * 8 + (l >> 3);
+    if (x >= W || y >= H) continue;
+    px[n] = x; py[n] = y; idx[n] = (int32_t)(y * W + x);
+    ++n;
+  }
+  return n;
+}
+
+static void vis_tile_row(rt_ctx_t* c, uint32_t ty, orc_rt_counters_t* k) {
+  const uint32_t W = c->p.width;
   const uint32_t ntx = (W + 31) / 32;
   uint32_t px[PK_LANES], py[PK_LANES];
   int32_t out[PK_LANES];
   int32_t idx[PK_LANES];
   for (uint32_t tx = 0; tx < ntx; ++tx) {
     const int split = tile_split(c, tx, ty);
-    const int waves = split ? 32 : 16, lanes = split ? 32 : 64;
+    const int waves = split ? 32 : 16;
     for (int wv = 0; wv < waves; ++wv) {
-      int n = 0;
-      for (int ln = 0; ln < lanes; ++ln) {
-        const uint32_t ti = split ? (((uint32_t)wv >> 1) << 6) + (uint32_t)ln + (((uint32_t)wv & 1u) << 5)
-                                  : ((uint32_t)wv << 6) + (uint32_t)ln;
-        const uint32_t blk = ti >> 6, l = ti & 63u;
-        const uint32_t x = tx * 32 + (blk & 3u) * 8 + (l & 7u), y = ty * 32 + (blk >> 2) * 8 + (l >> 3);
-        if (x >= W || y >= H) continue;
-        px[n] = x; py[n] = y; idx[n] = (int32_t)(y * W + x);
-        ++n;
-      }
+      const int n = wave_pixels(c, tx, ty, split, wv, px, py, idx);
       if (n == 0) continue;
       if (c->bl_idx)
         vis_scan_block(c, n, px, py, out, &k->tri_tests);
@@ -1073,12 +1084,13 @@ static void rt_row(rt_ctx_t* c, uint32_t y, orc_rt_counters_t* k) {
       /* screen layers (depth_test off): painter order, the last drawn
        * (highest) covering pid, by draw3d's coverage rule */
       int lpid = -1;
+      uint32_t nl = 0;  /* layers this pixel's lane tests (layer_waves counts per wave) */
       for (int dd = s->num_drawcalls - 1; dd >= 0 && lpid < 0; --dd) {
         const orc_drawcall_t* dc = &s->drawcalls[dd];
         if (dc->depth_test) continue;
         for (int i = dc->prim_count - 1; i >= 0; --i) {
           const int g = dc->prim_offset + i;
-          ++k->layer_tests;
+          ++nl;
           const orc_vis_prim_t* v = &c->vis[g];
           if (!rect_in(v->rx, x) || !rect_in(v->ry, y)) continue;
           const orc_rast_prim_t* p = &c->rp[g];
@@ -1087,12 +1099,36 @@ static void rt_row(rt_ctx_t* c, uint32_t y, orc_rt_counters_t* k) {
         }
       }
       if (lpid >= 0) { col = shade_at(c, lpid, x, y, k); opid = lpid; }
+      c->lcnt[(uint64_t)y * W + x] = nl;
     }
     const uint64_t px = (uint64_t)y * W + x;
     c->color[px] = col;
     if (c->pid) c->pid[px] = opid;
     if (c->tout) c->tout[px] = hit >= 0 ? t : 0.0f;
   }
+}
+
+/* Screen-layer records fetched per frame: the kernels' resolve_layers loads
+ * layer k once per wave (wave-uniform, scalar cache) while some lane of the
+ * wave is still unresolved, so a wave fetches max over its lanes of the
+ * layers each lane tests -- counted once per wave, like the block lists' and
+ * packet walks' record tests. */
+static uint64_t layer_waves(const rt_ctx_t* c) {
+  const uint32_t ntx = (c->p.width + 31) / 32, nty = (c->p.height + 31) / 32;
+  uint32_t px[PK_LANES], py[PK_LANES];
+  int32_t idx[PK_LANES];
+  uint64_t tot = 0;
+  for (uint32_t ty = 0; ty < nty; ++ty)
+    for (uint32_t tx = 0; tx < ntx; ++tx) {
+      const int split = tile_split(c, tx, ty);
+      for (int wv = 0; wv < (split ? 32 : 16); ++wv) {
+        const int n = wave_pixels(c, tx, ty, split, wv, px, py, idx);
+        uint32_t m = 0;
+        for (int i = 0; i < n; ++i) m = c->lcnt[idx[i]] > m ? c->lcnt[idx[i]] : m;
+        tot += m;
+      }
+    }
+  return tot;
 }
 
 static void* rt_worker(void* arg) {
@@ -1128,6 +1164,7 @@ static int rt_run(const orc_scene_t* scene, const orc_bvh_t* bvh, const orc_rt_p
   /* (BVH mode only: the flat image's shadow rays test the whole list) */
   if (bvh && p->shadow_lists && (p->flags & (ORC_RT_PATH | ORC_RT_SHADOWS))) sl_build(&c);
   c.color = color; c.pid = pid; c.tout = t;
+  c.lcnt = (uint32_t*)calloc((size_t)p->width * p->height, sizeof(uint32_t));
   const uint32_t nt = p->nthreads > 1 ? p->nthreads : 1;
   if (bvh && !p->vis_per_lane && p->row_begin == 0 && p->row_end == 0 && p->row_step <= 1) {
     /* primary visibility as the kernels walk it: one packet per wave */
@@ -1151,6 +1188,7 @@ static int rt_run(const orc_scene_t* scene, const orc_bvh_t* bvh, const orc_rt_p
     for (uint32_t i = 0; i < nt; ++i) pthread_join(th[i], NULL);
     free(th);
   }
+  c.cnt.layer_tests = layer_waves(&c);
   if (counters) *counters = c.cnt;
   rt_release(&c);
   return 0;

@@ -18,6 +18,10 @@ Recomputed:
 and compared with the line (which uses the HIP-event average of its own timed
 launches): each must agree within --tol (default 5 %).
 
+The line's series entry `bvh_walk` (config 3 by BVH traversal, image rt_bvh)
+is checked the same way against the summary's vx_main_rt_bvh row and
+--pmc-bvh (profiles/pmc_bvh.json) when both are there.
+
 Usage: check_roofline.py <bench.json> <kernel_stats.csv> [--pmc profiles/pmc_shadow.json]"""
 import argparse
 import csv
@@ -47,6 +51,7 @@ def main():
     ap.add_argument("bench")
     ap.add_argument("stats")
     ap.add_argument("--pmc", default=None)
+    ap.add_argument("--pmc-bvh", default="profiles/pmc_bvh.json")
     ap.add_argument("--tol", type=float, default=0.05)
     a = ap.parse_args()
     line = load_line(a.bench)
@@ -84,6 +89,26 @@ def main():
     if issue is not None and issue.get("frac") is not None:
         check("roofline_issue.frac", pmc["sq"]["SQ_INSTS_VALU"] / dur_s / 1e9 / VALU_ISSUE_PEAK_GIPS,
               issue["frac"])
+    # the N=1 series entry timing config 3 by BVH traversal only (image rt_bvh)
+    sb = line.get("series", {}).get("bvh_walk")
+    if sb is not None and "vx_main_rt_bvh" in rows:
+        db = float(rows["vx_main_rt_bvh"]["AverageNs"]) * 1e-9
+        out["bvh_walk"] = {"rocprof_calls": int(rows["vx_main_rt_bvh"]["Calls"]),
+                           "rocprof_avg_ms": round(db * 1e3, 5), "line_kernel_ms": sb["kernel_ms"]}
+        br = sb["roofline"]
+        check("series.bvh_walk.roofline.frac", br["algorithmic_bytes_per_launch"] / db / 1e9 / HBM_PEAK_GBS,
+              br["frac"])
+        try:
+            pb = json.load(open(a.pmc_bvh))
+        except OSError:
+            pb = None
+        if pb is not None and br.get("measured_hbm_frac") is not None:
+            check("series.bvh_walk.roofline.measured_hbm_frac", pb["traffic_bytes"] / db / 1e9 / HBM_PEAK_GBS,
+                  br["measured_hbm_frac"])
+        bi = sb.get("roofline_issue")
+        if pb is not None and bi:
+            check("series.bvh_walk.roofline_issue.frac", pb["sq"]["SQ_INSTS_VALU"] / db / 1e9 / VALU_ISSUE_PEAK_GIPS,
+                  bi["frac"])
     out["ok"] = ok
     print(json.dumps(out, indent=1))
     sys.exit(0 if ok else 1)

@@ -5,7 +5,8 @@
 # scripts/prof_rt.py (the product configuration: counters off), reduced by
 # scripts/pmc_profile.py into gpurun_out/$TAG/pmc_<mode>.json over the timed
 # image's own entry (vx_main_<image>).
-# MODE = shadow (config 3, default), path (config 4) or flat (config 2).
+# MODE = shadow (config 3, default), path (config 4), flat (config 2) or bvh
+# (config 3 by BVH traversal only, image rt_bvh).
 set -o pipefail
 cd "$GRAFT_REPO_ROOT"
 export TMPDIR=/tmp
@@ -15,6 +16,7 @@ case $MODE in
   shadow) CO=rt_kernel.co; SZ=1024 ;;
   path)   CO=pt_kernel.co; SZ=1024 ;;  # RT_PT_QUEUE=1: CO=pt_primary.co,pt_queue.co
   flat)   CO=rt_flat.co;   SZ=256 ;;
+  bvh)    CO=rt_bvh.co;    SZ=1024 ;;  # config 3 by BVH traversal (bench series "bvh_walk")
   *) echo "bad MODE $MODE"; exit 2 ;;
 esac
 pass() {  # name, counters...

@@ -14,7 +14,8 @@ def main():
     ap.add_argument("--frames", type=int, default=20)
     ap.add_argument("--no-shadows", action="store_true")
     ap.add_argument("--kernel-dir", default=None)
-    ap.add_argument("--mode", choices=("shadow", "path", "flat"), default="shadow")
+    ap.add_argument("--mode", choices=("shadow", "path", "flat", "bvh"), default="shadow",
+                    help="bvh: config 3 by BVH traversal only (RT_RENDER_BVH_WALK, image rt_bvh)")
     ap.add_argument("--counters", action="store_true",
                     help="counter rows on (default off: the timed product configuration)")
     args = ap.parse_args()
@@ -25,7 +26,7 @@ def main():
     flat = args.mode == "flat"
     size = 256 if flat and args.size == 1024 else args.size   # bench.py's config-2 size
     r.configure(size, size, shadows=not (args.no_shadows or flat), path=args.mode == "path",
-                flat=flat, counters=args.counters)
+                flat=flat, counters=args.counters, bvh_walk=args.mode == "bvh")
     for _ in range(args.frames):
         r.render()
     print(r.stats(), file=sys.stderr)

@@ -9,6 +9,8 @@
 // and rt_app.cpp host_setup remain the host restatement (RT_SETUP=host) that
 // the GPU tests compare against bit for bit.
 #include <algorithm>
+#include <chrono>
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <vector>
@@ -22,10 +24,15 @@ namespace {
 // one setup launch: argument block, start, wait (the next launch and the
 // host's read-backs depend on it)
 int run(rt_renderer* r, DevBuf* argb, const rt_setup_arg_t& a, uint32_t* launches) {
+  static const bool trace = std::getenv("RT_SETUP_TRACE") != nullptr;  // per-launch phases to stderr
+  const auto t0 = std::chrono::steady_clock::now();
   if (vx_copy_to_dev(argb->h, &a, 0, sizeof(a)) != 0) return set_error("vx_copy_to_dev failed");
   if (vx_start(r->dev, r->setup_krnl, argb->h) != 0) return set_error("vx_start failed");
   if (vx_ready_wait(r->dev, VX_MAX_TIMEOUT) != 0) return set_error("vx_ready_wait failed");
   ++*launches;
+  if (trace)
+    std::fprintf(stderr, "rt_setup launch phases 0x%05x host %.1f us\n", a.phases,
+                 std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count());
   return 0;
 }
 
@@ -212,7 +219,7 @@ int device_setup(rt_renderer* r, bool raster, bool order_on, bool lists, uint32_
         continue;
       }
       const uint64_t total = st[2];
-      if (alloc_tmp(r, total * 16 + 16, &btmp) || alloc(r, (total + 2) * 16, &r->blist, &a.blist_addr))
+      if (alloc_tmp(r, total * 16 + 16, &btmp) || alloc(r, (total + RT_BLIST_PAD) * 16, &r->blist, &a.blist_addr))
         return -1;
       g.btmp_addr = btmp.addr;
       g.blist_addr = a.blist_addr;

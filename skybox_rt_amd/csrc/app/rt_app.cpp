@@ -308,6 +308,16 @@ int rt_renderer_create(rt_scene_h s, const char* kernel_dir, rt_renderer_h* out)
       for (int i = 0; i < 2; ++i)
         if (vx_upload_kernel_file(r->dev, (dir + "/" + pq_names[m][i]).c_str(), &r->krnl_pq[m][i]) != 0)
           return fail("cannot upload kernel " + dir + "/" + pq_names[m][i]);
+    // the BVH-walk primary+shadow images (RT_RENDER_BVH_WALK), from the
+    // kernel directory or the library's
+    const char* bvh_names[2] = {"rt_bvh.vxbin", "rt_bvh_stats.vxbin"};
+    for (int i = 0; i < 2; ++i) {
+      std::string path = dir + "/" + bvh_names[i];
+      if (FILE* f = std::fopen(path.c_str(), "rb")) std::fclose(f);
+      else path = lib_dir() + "/" + bvh_names[i];
+      if (vx_upload_kernel_file(r->dev, path.c_str(), &r->krnl_bvh[i]) != 0)
+        return fail("cannot upload kernel " + path);
+    }
   }
   rt_kernel_arg_t& a = r->arg;
   std::memset(&a, 0, sizeof(a));
@@ -450,7 +460,7 @@ int rt_renderer_export_records(rt_renderer_h r, uint32_t which, void* out, uint6
     case RT_REC_BIDX: b = a.blist_blocks ? r->bidx : nullptr; n = (uint64_t)a.blist_blocks * 8; break;
     case RT_REC_BLIST:
       b = a.blist_blocks ? r->blist : nullptr;
-      n = (r->setup.blist_entries + 2) * sizeof(rt_bentry_t);
+      n = (r->setup.blist_entries + RT_BLIST_PAD) * sizeof(rt_bentry_t);
       break;
     case RT_REC_SIDX: b = a.slist_on ? r->sidx : nullptr; n = 6ull * a.slist_n * a.slist_n * 8; break;
     case RT_REC_SLIST: b = a.slist_on ? r->slist : nullptr; n = (r->sl_entries + 1) * sizeof(rt_tri_t); break;
@@ -698,7 +708,7 @@ static int build_block_lists(rt_renderer* r, const std::vector<rt::VisPrim>& vis
   if (!rtapp::block_lists_fit(longest, total)) return 0;
   std::vector<rt_bentry_t> ent;
   std::vector<uint32_t> idx;
-  ent.reserve(total + 2);
+  ent.reserve(total + RT_BLIST_PAD);
   idx.reserve(2 * (size_t)nblk);
   for (auto& l : lists) {
     std::sort(l.begin(), l.end());
@@ -714,7 +724,8 @@ static int build_block_lists(rt_renderer* r, const std::vector<rt::VisPrim>& vis
       ent[base + i] = rt_bentry_t{l[i].second, x0 | (y0 << 16), x1 | (y1 << 16), l[i].first};
     }
   }
-  for (int i = 0; i < 2; ++i) ent.push_back(rt_bentry_t{0u, RT_BLIST_PAD_LO, RT_BLIST_PAD_HI, RT_VIS_ZMIN_NONE});
+  for (uint32_t i = 0; i < RT_BLIST_PAD; ++i)
+    ent.push_back(rt_bentry_t{0u, RT_BLIST_PAD_LO, RT_BLIST_PAD_HI, RT_VIS_ZMIN_NONE});
   if (upload(r->dev, ent.data(), ent.size() * sizeof(rt_bentry_t), &r->blist, &a.blist_addr) ||
       upload(r->dev, idx.data(), idx.size() * 4, &r->bidx, &a.bidx_addr))
     return -1;
@@ -902,7 +913,8 @@ int rt_renderer_configure(rt_renderer_h r, const rt_render_params_t* p) {
   // primary visibility of primary+shadow and path frames from per-block
   // candidate lists (rt_bentry_t; env RT_BLOCK_LISTS=0 keeps the tree walk)
   const char* bl = std::getenv("RT_BLOCK_LISTS");
-  const bool lists = !raster && !(p->flags & RT_RENDER_FLAT) && !(bl && std::atoi(bl) == 0) &&
+  const bool bvh_walk = (p->flags & RT_RENDER_BVH_WALK) != 0;
+  const bool lists = !raster && !(p->flags & RT_RENDER_FLAT) && !(bl && std::atoi(bl) == 0) && !bvh_walk &&
                      a.num_geom > 0 && r->local_tiles > 0;
   a.blist_blocks = 0;
   a.blist_addr = a.bidx_addr = 0;
@@ -923,7 +935,7 @@ int rt_renderer_configure(rt_renderer_h r, const rt_render_params_t* p) {
   r->setup.slist_entries = 0;
   const char* sle = std::getenv("RT_SHADOW_LISTS");
   if (device && !raster && !(p->flags & RT_RENDER_FLAT) && (p->flags & (RT_RENDER_SHADOWS | RT_RENDER_PATH)) &&
-      a.num_geom > 0 && !(sle && std::atoi(sle) == 0)) {
+      a.num_geom > 0 && !(sle && std::atoi(sle) == 0) && !bvh_walk) {
     if (rtapp::shadow_lists(r, &launches) != 0) return -1;
     a.slist_on = r->sl_built ? 1u : 0u;
   }
@@ -998,12 +1010,16 @@ int rt_render_start(rt_renderer_h r) {
   // a frame of the two-kernel path tracer is one launch group of 2
   if (mode == 1 && r->pq) {
     if (r->launch_group(r->dev, 2) != 0) return fail("vx_hip_launch_group failed");
-    return vx_start(r->dev, r->krnl_pq[0][k], r->args) == 0 &&
-                   vx_start(r->dev, r->krnl_pq[1][k], r->args) == 0
-               ? 0
-               : fail("vx_start failed");
+    if (vx_start(r->dev, r->krnl_pq[0][k], r->args) == 0 && vx_start(r->dev, r->krnl_pq[1][k], r->args) == 0)
+      return 0;
+    r->launch_group(r->dev, 0);  // abandon the half-issued group: later launches stand alone
+    return fail("vx_start failed");
   }
-  return vx_start(r->dev, r->krnl[mode][k], r->args) == 0 ? 0 : fail("vx_start failed");
+  // BVH-walk primary+shadow frames: their own image on the binary16 BVH4
+  // (the deep images walk every layout with the list code paths idle)
+  const bool bvh = mode == 0 && (f & RT_RENDER_BVH_WALK) && !r->deep && (r->arg.flags & RT_FLAG_BVH4H) &&
+                   r->krnl_bvh[k];
+  return vx_start(r->dev, bvh ? r->krnl_bvh[k] : r->krnl[mode][k], r->args) == 0 ? 0 : fail("vx_start failed");
 }
 
 int rt_render_wait(rt_renderer_h r) {

@@ -37,6 +37,9 @@ struct rt_renderer {
   // pt_primary (primary pass, path queue), [1] pt_queue (the queued paths);
   // [.][1] the instrumented images
   vx_buffer_h krnl_pq[2][2] = {};
+  // RT_RENDER_BVH_WALK primary+shadow frames (binary16 BVH4 images only):
+  // rt_bvh / rt_bvh_stats, the packet walks without the list code paths
+  vx_buffer_h krnl_bvh[2] = {};
   vx_buffer_h pathq = nullptr, pathq_ctr = nullptr;
   bool pq = false;          // the configuration runs the two-kernel path tracer
   vx_buffer_h nodes = nullptr, nodes4 = nullptr, tris = nullptr, layers = nullptr, dcs = nullptr, tex = nullptr;
@@ -88,7 +91,8 @@ struct rt_renderer {
                            &vgeom, &gather_recv, &gather_image, &prims, &cbuf, &args,
                            &setup_krnl, &verts, &pdc, &dcz, &layer_list, &geometry_list, &vis,
                            &blist, &bidx, &sidx, &slist, &krnl_pq[0][0], &krnl_pq[0][1],
-                           &krnl_pq[1][0], &krnl_pq[1][1], &pathq, &pathq_ctr};
+                           &krnl_pq[1][0], &krnl_pq[1][1], &pathq, &pathq_ctr,
+                           &krnl_bvh[0], &krnl_bvh[1]};
     for (auto* b : bufs) {
       if (*b) vx_mem_free(*b);
       *b = nullptr;

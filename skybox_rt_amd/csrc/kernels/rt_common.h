@@ -246,6 +246,10 @@ typedef struct {
   uint32_t lo, hi;         // union rectangle of this entry and the rest: corners x | y << 16
   uint32_t zmin;           // this entry's depth lower bound (the smallest of the rest)
 } rt_bentry_t;
+// padding entries after the last list: block_primary loads the next pair of
+// entries with each round's records, so the last round of an odd-length list
+// ending at the end of the array reads up to 3 entries past it
+#define RT_BLIST_PAD 3u
 #define RT_BLIST_PAD_LO 0xffffffffu   // padding entries: a rectangle no pixel is in
 #define RT_BLIST_PAD_HI 0xfffefffeu
 #define RT_BLIST_MAX_LIST 1024u       // longest list the device sort takes (else: tree walk)

@@ -4,8 +4,12 @@
 // the draw3d fixed-point coverage + 24-bit depth test decide), screen layers,
 // draw3d-exact shading of the winner, and an any-hit Möller–Trumbore shadow
 // ray per geometry hit, with the shadow rays compacted into full waves
-// (ballot + mbcnt into an LDS queue) and each full wave walking the binary16
-// BVH4 as one packet (occluded_packet).
+// (ballot + mbcnt into an LDS queue).  A full queue of shadow rays is traced
+// per lane over each ray's light-space cell list (occluded_list) when the
+// lists are built -- the default -- or as one packet walking the binary16
+// BVH4 (occluded_packet).  Image rt_bvh (RT_BVH_WALK) keeps only the BVH
+// walks: the packet walk of the tree for primary visibility and the shadow
+// packet (BASELINE config 3's "full BVH traversal").
 //
 // Launched by libvortex-hip.so (vx_start) as its entry (VX_ENTRY); the body
 // reads its rt_kernel_arg_t from the STARTUP_ARG DCRs and calls
@@ -20,7 +24,8 @@
 // every fused multiply-add is an explicit fmaf, everything else is compiled
 // with -ffp-contract=off, divisions are IEEE.
 //
-// Images (Makefile): rt_kernel (binary16 BVH4 only), rt_kernel_deep (every
+// Images (Makefile): rt_kernel (binary16 BVH4 only), rt_bvh (the same
+// without the list code paths), rt_kernel_deep (every
 // BVH layout: per-lane walks with a 32-entry LDS stack for the layouts the
 // packet walk does not read), rt_flat (RT_FLAT: BASELINE config 2, the flat
 // geometry list, no BVH).
@@ -172,7 +177,7 @@ __device__ __forceinline__ void shadow_drain(bool final, const Scene& S, WaveLds
     float ts;
     // the light-space lists when built (occluded_list), else the BVH: the
     // binary16 BVH4 as one packet, other layouts per lane (deep images)
-    const bool occ = S.slist_on ? occluded_list(S, s, active, w.q_pid[slot], cnt)
+    const bool occ = !RT_BVH_WALK && S.slist_on ? occluded_list(S, s, active, w.q_pid[slot], cnt)
                      : (RT_ONLY_BVH4H || (S.flags & RT_FLAG_BVH4H))
                          ? occluded_packet(S, s, active, w.q_pid[slot], 1.0f, cnt)
                          : active && trace<true>(S, s, 0.0f, 1.0f, w.q_pid[slot], tie_high, &ts,

@@ -754,7 +754,7 @@ __device__ void phase_bsort(const rt_setup_arg_t* a) {
   const uint4* btmp = vx_ptr<const uint4>(a->btmp_addr);
   uint4* blist = vx_ptr<uint4>(a->blist_addr);
   const uint32_t waves = gridDim.x * (RTS_BLOCK / 64), l = lane_id();
-  if (blockIdx.x == 0 && threadIdx.x < 2)  // the 2 padding entries (the kernels load pairs ahead)
+  if (blockIdx.x == 0 && threadIdx.x < RT_BLIST_PAD)  // padding entries (the kernels load pairs ahead)
     blist[a->blist_entries + threadIdx.x] = make_uint4(0u, RT_BLIST_PAD_LO, RT_BLIST_PAD_HI, RT_VIS_ZMIN_NONE);
   for (uint32_t lb = blockIdx.x * (RTS_BLOCK / 64) + (threadIdx.x >> 6); lb < a->nblk; lb += waves) {
     const uint2 oc = sload(bidx + lb);

@@ -14,6 +14,8 @@
 //                   images); 0: every layout (the deep images)
 //   RT_PUSH_UNCOND  per-lane BVH4 pushes as unconditional rows (path tracer)
 //   RT_LAZY_TASK_ARGS  task-map fields re-read from the argument block
+//   RT_BVH_WALK     the image walks the BVH for primary and shadow rays (no
+//                   block-list / light-space-list code: image rt_bvh)
 //   RT_INSTRUMENT   algorithmic counters (node visits, tests, texels)
 //   RT_STAMPS / RT_TRACE_CYCLES  diagnostic per-wave stamps
 #pragma once
@@ -26,6 +28,9 @@
 
 #ifndef RT_ONLY_BVH4H
 #define RT_ONLY_BVH4H 0
+#endif
+#ifndef RT_BVH_WALK
+#define RT_BVH_WALK 0  // 1: image rt_bvh -- primary and shadow rays walk the BVH, no list code
 #endif
 
 namespace rtk {
@@ -1071,7 +1076,9 @@ __device__ __forceinline__ void vis_test(const uint4& A, const uint4& B, const u
 // a pixel.
 __device__ __forceinline__ int32_t trace_primary_packet(const Scene& S, uint32_t px, uint32_t py,
                                                         bool act, bool tie_high, Counters& cnt) {
-  if (S.num_vnodes == 0) return -1;
+  // a wave with no pixel in the image (edge tiles overhang it) walks nothing
+  // (oracle/rt.c vis_tile_row skips it too)
+  if (S.num_vnodes == 0 || __ballot(act) == 0) return -1;
   if (!act) px = 0xffffffffu;  // in no rectangle
   const uint32_t pp = px > 0xffffu ? 0xffffffffu : px | (py << 16);  // packed pixel (rect2_in)
   int32_t vstk = 0;  // stack entry i in lane i of this VGPR
@@ -1178,7 +1185,7 @@ __device__ __forceinline__ int32_t block_primary(const Scene& S, uint32_t lb, ui
   uint32_t bz = VX_OM_DEPTH_MASK;
   int32_t bpid = -1;
   uint4 e[2];
-  S.A.sld_u4n<2>(S.blist + 16u * oc.x, e);  // the list carries 2 padding entries
+  S.A.sld_u4n<2>(S.blist + 16u * oc.x, e);  // the list array carries RT_BLIST_PAD padding entries
   for (uint32_t k = 0; k < oc.y; k += 2) {
     if (__ballot(rect2_in(e[0].y, e[0].z, pp) && e[0].w <= bz) == 0) break;
     uint4 r0[4], r1[4], en[2];
@@ -1200,7 +1207,7 @@ __device__ __forceinline__ int32_t block_primary(const Scene& S, uint32_t lb, ui
 // the host built lists (blist_blocks), else the packet walk of the tree
 __device__ __forceinline__ int32_t trace_primary(const Scene& S, uint32_t lb, uint32_t px, uint32_t py,
                                                  bool act, bool tie_high, Counters& cnt) {
-  if (S.blist_blocks) return block_primary(S, lb, px, py, act, tie_high, cnt);
+  if (!RT_BVH_WALK && S.blist_blocks) return block_primary(S, lb, px, py, act, tie_high, cnt);
   const int32_t h = trace_primary_packet(S, px, py, act, tie_high, cnt);
   return act ? h : -1;
 }
@@ -1229,16 +1236,20 @@ __device__ __forceinline__ bool secondary_ok(float t) { return t > 0.0f && t < I
 // order, each overwriting; draw3d/main.cpp:179 + gpu_sw.h:38-61); one
 // wave-uniform rt_vtri_t per step through the scalar cache.  Returns the pid
 // to shade (layer pid, or `spid` unchanged).
-// `tests`: per lane, the layers it tested (the RT_INSTRUMENT count)
+// `tests` (the RT_INSTRUMENT count): the layer records the wave fetched,
+// counted once per wave by its first active lane -- a record is one scalar
+// load for the whole wave, the rule block_primary's and the packet walks'
+// record tests follow (oracle/rt.c layer_waves: max over the wave's lanes)
 __device__ __forceinline__ int32_t resolve_layers_n(const Scene& S, uint32_t px, uint32_t py, bool need,
                                                     int32_t spid, uint32_t* tests) {
   uint64_t pend = __ballot(need);
+  const uint32_t lead = lane_id() == (uint32_t)__builtin_ctzll(__ballot(1)) ? 1u : 0u;
   for (uint32_t k = 0; pend != 0 && k < S.num_layer; ++k) {
     uint4 lw[3];
     S.A.sld_u4n<3>(S.vlayers + 64u * k, lw);  // one pointer: merged wide s_loads
     const uint4 A = lw[0], B = lw[1], C = lw[2];
     const bool mine = (pend & (1ull << lane_id())) != 0;
-    *tests += mine ? 1u : 0u;
+    *tests += lead;
     bool f = false;
     if (mine && rect_in(C.y, px) && rect_in(C.z, py)) {
       const int32_t e0[3] = {(int32_t)A.x, (int32_t)A.y, (int32_t)A.z};

@@ -469,9 +469,24 @@ class vx_device {
     launch_mode_ = timed ? (launch_mode_timed_ == 2 ? 1 : launch_mode_timed_) : 2;
     return 0;
   }
-  // the next n launches form one run (then single launches again)
+  // the next n launches form one run (then single launches again).  The
+  // event and slot arrays must hold every launch the queue bound lets into
+  // flight, (depth_ + time_every_ - 1) * n, plus the one being issued.
+  // n = 0 abandons an open group (a launch inside it failed): the launches
+  // already issued retire as one untimed run, and single launches resume.
   int launch_group(uint32_t n) {
-    if (n < 1 || n > 4 || group_pos_ != 0) return -1;  // not inside a group
+    if (n == 0) {
+      if (group_pos_ != 0) {
+        const int slot = (int)((issued_ + kMaxQueue - 1) % kMaxQueue);
+        group_last_[slot] = true;
+        timed_[slot] = false;
+      }
+      group_pos_ = 0;
+      group_n_ = 1;
+      return 0;
+    }
+    if (n > 4 || group_pos_ != 0) return -1;  // not inside a group
+    if ((uint64_t)(depth_ + time_every_) * n > (uint64_t)kMaxQueue) return -1;
     group_n_ = n;
     return 0;
   }

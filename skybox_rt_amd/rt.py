@@ -29,6 +29,7 @@ RT_RENDER_INSTRUMENTED = 0x100
 RT_RENDER_COMPACT = 0x200
 RT_RENDER_COUNTERS = 0x400
 RT_RENDER_HOST_SETUP = 0x800
+RT_RENDER_BVH_WALK = 0x2000
 # rt_renderer_export_records arrays: name -> (id, dtype, words per record)
 RECORDS = {"prims": (0, np.int32, 32), "bbox": (1, np.uint32, 2), "vis": (2, np.uint32, 4),
            "vnodes": (3, np.uint32, 16), "vtris": (4, np.int32, 16), "vlayers": (5, np.int32, 16),
@@ -254,7 +255,7 @@ class Renderer:
                   instrumented: bool = False, path: bool = False, bounces: int = 4,
                   seed: int = PT_SEED, flat: bool = False, raster: bool = False,
                   bvh_width: int = 0, compact: bool = False, counters: bool = True,
-                  host_setup: bool = False) -> None:
+                  host_setup: bool = False, bvh_walk: bool = False) -> None:
         """path=True: diffuse path trace (pt_kernel; `bounces` segments per
         path, RNG `seed`) instead of primary + shadow rays.  flat=True: the
         flat triangle list without BVH (BASELINE config 2).  raster=True:
@@ -265,14 +266,17 @@ class Renderer:
         counters=False: no per-workgroup counter rows (the timed product
         configuration; stats() then has the task count and kernel time only).
         host_setup=True: build the per-resolution records with the host loops
-        instead of on the device (kernels/rt_setup.hip)."""
+        instead of on the device (kernels/rt_setup.hip).  bvh_walk=True: no
+        per-block / light-space lists -- primary visibility by the BVH4 packet
+        walk, shadow rays by the BVH (BASELINE config 3's full BVH traversal;
+        primary+shadow frames run the rt_bvh image)."""
         p = RenderParams()
         p.width, p.height = width, height
         p.flags = ((RT_RENDER_SHADOWS if shadows else 0) | (RT_RENDER_INSTRUMENTED if instrumented else 0)
                    | (RT_RENDER_PATH if path else 0) | (RT_RENDER_FLAT if flat else 0)
                    | (RT_RENDER_RASTER if raster else 0) | (RT_RENDER_BVH2 if bvh_width == 2 else 0)
                    | (RT_RENDER_COMPACT if compact else 0) | (RT_RENDER_COUNTERS if counters else 0)
-                   | (RT_RENDER_HOST_SETUP if host_setup else 0))
+                   | (RT_RENDER_HOST_SETUP if host_setup else 0) | (RT_RENDER_BVH_WALK if bvh_walk else 0))
         p.bounces, p.seed = bounces, seed
         p.light[:] = [float(np.float32(x)) for x in light]
         p.clear_color = clear_color
@@ -295,7 +299,7 @@ class Renderer:
         """One per-resolution record array of the current configuration
         (RECORDS: prims, bbox, vis, vnodes, vtris, vlayers, vgeom, order,
         ptris, geom, bidx, blist -- the per-block candidate lists, blist with
-        its 2 padding entries), as [count, words]."""
+        its 3 padding entries), as [count, words]."""
         which, dt, words = RECORDS[name]
         n = C.c_uint64()
         _check(lib().rt_renderer_export_records(self._h, which, None, 0, C.byref(n)),

@@ -46,10 +46,10 @@ def _check_vs_oracle(po, name, r, w, h, index=0, count=1):
     bad = np.nonzero((idx != oidx).any(axis=1))[0]
     assert bad.size == 0, f"bidx: {bad.size} blocks differ, first {bad[:8]}"
     assert st["blist_entries"] == len(oent)
-    assert ent.shape == (len(oent) + 2, 4)
-    bad = np.nonzero((ent[:-2] != oent).any(axis=1))[0]
+    assert ent.shape == (len(oent) + 3, 4)
+    bad = np.nonzero((ent[:-3] != oent).any(axis=1))[0]
     assert bad.size == 0, f"blist: {bad.size} entries differ, first {bad[:8]}"
-    assert (ent[-2:] == PAD).all()
+    assert (ent[-3:] == PAD).all()
     assert st["blist_max"] == (int(oidx[:, 1].max()) if len(oidx) else 0)
 
 

@@ -205,31 +205,43 @@ def test_rt_tekkaman_1024_vs_reference_render(po):
 
 
 @pytest.mark.parametrize("name", ("tekkaman", "box", "scene", "carnival"))
-@pytest.mark.parametrize("path", (False, True))
-def test_rt_primary_matches_draw3d_golden_128(name, path):
+def test_rt_primary_matches_draw3d_golden_128(name):
     """RT kernel primary rays (no shadows) vs the reference's *_ref_128.png:
-    0 differing pixels.  The path tracer's primary pass is the same; its
-    frame differs only where paths start (checked against the oracle
-    elsewhere), so here only its non-geometry pixels are compared."""
+    0 differing pixels."""
     _, r = renderer(name)
-    if path:
-        r.configure(128, 128, shadows=False, path=True, bounces=0)
-    else:
-        r.configure(128, 128, shadows=False)
+    r.configure(128, 128, shadows=False)
     r.render()
     from oracle.py_oracle import argb_to_rgba_image, compare_images
     ref = _png(f"{GOLDEN}/draw3d/{name}_ref_128.png")
-    got = argb_to_rgba_image(r.framebuffer())
-    if not path:
-        assert compare_images(got, ref, tol=0) == 0
-    else:
-        # pixels with no geometry hit keep the raster colour in the path tracer
-        _, rr = renderer(name)
-        rr.configure(128, 128, shadows=False)
-        rr.render()
-        plain = argb_to_rgba_image(rr.framebuffer())
-        same = (plain == got).all(axis=-1)
-        assert compare_images(got[same], ref[same], tol=0) == 0
+    assert compare_images(argb_to_rgba_image(r.framebuffer()), ref, tol=0) == 0
+
+
+@pytest.mark.parametrize("name", ("tekkaman", "box", "scene", "carnival"))
+def test_pt_primary_pass_equals_oracle_128(po, name):
+    """The path tracer's primary pass at 0 bounces (pt_kernel: every path is
+    one shadow-ray vertex) == the oracle's path_trace(bounces=0) bit for bit,
+    counters included; and every pixel that starts no path (no geometry
+    hit) keeps the reference's raster colour (the *_ref_128.png golden)."""
+    s, r = renderer(name)
+    r.configure(128, 128, shadows=False, path=True, bounces=0, instrumented=True)
+    r.render()
+    st = r.stats()
+    fb = r.framebuffer()
+    c, _, tout, k = po.rt_render(oracle_scene(po, name),
+                                po.rt_params(128, 128, shadows=False, path=True, bounces=0, nthreads=4),
+                                bvh=s.bvh() + (s.bvh4(),))
+    assert np.array_equal(fb, c)
+    for key in ("primary_rays", "geometry_hits", "shadow_rays", "occluded", "bounce_rays", "node_visits",
+                "tri_tests", "layer_tests"):
+        assert st[key] == k[key], key
+    from oracle.py_oracle import argb_to_rgba_image, compare_images
+    ref = _png(f"{GOLDEN}/draw3d/{name}_ref_128.png")
+    # the oracle's t is 0 exactly where the primary ray has no geometry
+    # winner (rt.c rt_row); rows flipped like argb_to_rgba_image's
+    nogeo = (tout.reshape(128, 128) == 0.0)[::-1]
+    assert nogeo.sum() < 128 * 128 and (nogeo.any() or name == "carnival")  # carnival: all geometry
+    got = argb_to_rgba_image(fb)
+    assert compare_images(got[nogeo], ref[nogeo], tol=0) == 0
 
 
 @pytest.mark.parametrize("shards", (2, 3, 8))

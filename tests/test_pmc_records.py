@@ -13,7 +13,7 @@ from skybox_rt_amd import _lib
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 IMAGES = {"shadow": ("rt_kernel.co",), "path": ("pt_kernel.co",),
-          "flat": ("rt_flat.co",)}
+          "flat": ("rt_flat.co",), "bvh": ("rt_bvh.co",)}
 
 
 @pytest.mark.parametrize("mode", sorted(IMAGES))
