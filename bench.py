@@ -113,6 +113,64 @@ def issue_roofline(rec: dict, kernel_ms: float, mode: str):
             "source": f"profiles/pmc_{mode}.json (rocprofv3 --pmc passes, scripts/pmc_profile.sh)"}
 
 
+def moving_lights(k: int):
+    """k distinct point lights (clip x, y, w) circling above the model, the
+    metric's light (0, 60, 80) among them."""
+    return [(float(np.float32(40.0 * math.sin(2 * math.pi * i / k))),
+             float(np.float32(60.0 + 10.0 * (math.cos(2 * math.pi * i / k) - 1.0))),
+             float(np.float32(80.0 + 5.0 * math.sin(4 * math.pi * i / k)))) for i in range(k)]
+
+
+def moving_light_series(r, side, steps, warmup, kw):
+    """Every step moves the light (rt_renderer_set_light: the light-space
+    shadow lists rebuilt on the device, queued behind the previous frame)
+    and renders a frame -- the reference's per-render re-binning regime
+    (tests/regression/draw3d/main.cpp:179-211).  Frames back to back, no
+    per-launch events; the last frame is checked against a fresh configure
+    with its light.  Also the cost of one light change alone (set_light +
+    wait, median of 16: slist_build_ms)."""
+    import torch
+    lights = moving_lights(16)
+    r.configure(side, side, counters=False, **dict(kw, light=lights[0]))
+    r.render()
+    one = []
+    for L in lights[1:] + lights[:1]:
+        t0 = time.perf_counter()
+        r.set_light(L)
+        r.wait()
+        one.append((time.perf_counter() - t0) * 1e3)
+    r.set_timing(False)
+    try:
+        for i in range(warmup):
+            r.set_light(lights[i % 16])
+            r.start()
+        r.wait()
+        torch.cuda.synchronize()
+        _, _, n0 = r.run_totals()
+        t0 = time.perf_counter()
+        for i in range(steps):
+            r.set_light(lights[i % 16])
+            r.start()
+        r.wait()
+        torch.cuda.synchronize()
+        el = time.perf_counter() - t0
+        _, _, n1 = r.run_totals()
+    finally:
+        r.set_timing(True)
+    last = lights[(steps - 1) % 16]
+    fb = r.framebuffer().copy()
+    st = r.setup_stats()
+    r.configure(side, side, counters=False, **dict(kw, light=last))
+    r.render()
+    same = bool(np.array_equal(fb, r.framebuffer()))
+    return {"steps": steps, "lights": 16, "ms_per_step": round(el / steps * 1e3, 5),
+            "runs_per_step": round((n1 - n0) / steps, 3),
+            "slist_build_ms": round(float(np.median(one)), 4),
+            "slist_build_ms_min": round(float(min(one)), 4),
+            "slist_entries_last": int(st["slist_entries"]), "slist_on": int(st["slist_on"]),
+            "last_frame_equals_configured_render": same}
+
+
 def frame_side(n_gpus: int, base: int) -> int:
     return max(32, int(round(base * math.sqrt(n_gpus) / 32.0)) * 32)
 
@@ -253,6 +311,9 @@ class Run:
         # variant (untimed; its counters equal the oracle's traversal,
         # tests/test_gpu_rt.py): the timed product image writes no counters
         r.configure(side, side, instrumented=True, **self.kw)
+        # the renderer's first configure at this size and light: the cold
+        # per-resolution + per-light setup (records, lists, work order)
+        self.first_setup = r.setup_stats()
         r.render()
         self.inst = r.stats()
         self.rays_local = (self.inst["primary_rays"] + self.inst["shadow_rays"]
@@ -597,6 +658,16 @@ def main():
             "ms_per_step": round(eb / args.steps * 1e3, 5), "kernel_ms": round(kb, 5),
             "rays_per_frame": int(br.rays_local), "roofline": b_roof,
             "roofline_issue": issue_roofline(b_rec, kb, "bvh")}
+    # the moving light: a light change + a frame per step (N = 1)
+    moving = None
+    if n_gpus == 1 and not flat and (shadows or path) and not args.no_bvh_series:
+        mr = moving_light_series(r, side, args.steps, args.warmup,
+                                 dict(shadows=shadows, path=path, bounces=args.bounces))
+        mr["value"] = round(run.rays_local * mr["steps"] / (mr["ms_per_step"] * 1e-3 * mr["steps"]) / 1e6, 3)
+        mr["workload"] = (f"{side}x{side} {'path trace' if path else 'primary+shadow'} frames, the light "
+                          f"moved before every frame (rt_renderer_set_light: light-space shadow lists "
+                          f"rebuilt on the device, 6 stream-ordered setup launches, no host wait)")
+        series["moving_light"] = moving = mr
     if rank != 0:
         dist.destroy_process_group()
         return
@@ -679,6 +750,11 @@ def main():
             "bvh_build": {0: "device LBVH", 1: "device binned SAH (kernels/bvh_sah.hip)",
                           2: "host binned SAH"}.get(bvh_st["method"], "?"),
             "configure_ms": round(setup_st["configure_ms"], 3),
+            # the first configure of the renderer at this size and light:
+            # records, block lists, shadow lists, work order (cold)
+            "cold_configure_ms": round(run.first_setup["configure_ms"], 3),
+            "cold_configure_launches": int(run.first_setup["launches"]),
+            "slist_build_ms": moving["slist_build_ms"] if moving else None,
             "setup_ms": round(setup_st["setup_ms"], 3),
             "setup": ("device" if setup_st["device"] else "host") + f", {setup_st['launches']} launches",
             "block_list_entries": int(setup_st["blist_entries"]),

@@ -57,6 +57,19 @@ typedef int (*vx_hip_launch_group_t)(vx_device_h hdevice, uint32_t n);
  * back-to-back starts reach the GPU without the idle gap an event costs --
  * for timing a run of launches by a host clock).  Waits for the device. */
 typedef int (*vx_hip_set_timing_t)(vx_device_h hdevice, int timed);
+/* vx_copy_to_dev without the wait: the bytes (at most 4 KiB; larger copies,
+ * and copies into a kernel image, fall back to the synchronous copy) are
+ * staged in pinned host memory at once and copied when the driver's stream
+ * reaches the copy -- after every vx_start issued before it, before every
+ * one issued after it.  `src` may be reused when the call returns.  (simx's
+ * copies wait for the device, runtime/simx/vortex.cpp:174-176; a setup chain
+ * of dependent launches needs only stream order.) */
+typedef int (*vx_hip_copy_to_dev_async_t)(vx_buffer_h hbuf, const void* src, uint64_t off, uint64_t size);
+/* the kernel argument of the next vx_start (then 0 again): every image's
+ * entry takes one u32, `vx_launch_tag` in its VX_MAIN body (vx_spawn.h) --
+ * how the launches of a sequence sharing one argument block tell themselves
+ * apart without a device counter or a copy between them */
+typedef int (*vx_hip_set_launch_tag_t)(vx_device_h hdevice, uint32_t tag);
 
 #ifdef __cplusplus
 }

@@ -221,9 +221,24 @@ typedef struct {
   uint64_t slist_entries; /* light-space shadow list entries */
   uint32_t path_queue;    /* 1: RT_RENDER_PATH runs in two kernels (pt_primary + pt_queue: a
                              frame is one launch group of 2, vortex_hip.h) */
-  uint32_t pad;
+  uint32_t slist_built;   /* 1: the last configure / set_light built shadow lists for a new light
+                             (0: the lists of an unchanged light were kept) */
 } rt_setup_stats_t;
+/* (reads back the status of shadow lists queued by rt_renderer_set_light:
+ * waits for the device) */
 int rt_renderer_setup_stats(rt_renderer_h r, rt_setup_stats_t* stats);
+
+/* Move the point light of the current configuration (primary+shadow or path
+ * frames; clip (x, y, w)): the light in the render arguments and, when the
+ * configuration's shadow rays use the light-space lists, the lists for the
+ * new light -- a stream-ordered chain of setup launches (kernels/rt_setup.hip
+ * SPROJ .. SSORT) queued behind the frames already started, with no host
+ * wait; the frames started after it see the new light.  The lists' last
+ * launch decides on the device whether they fit (else those frames' shadow
+ * rays walk the BVH).  The reference re-bins its scene on the host for every
+ * render (tests/regression/draw3d/main.cpp:179-211 -> gfxutil.cpp:103-276);
+ * this is the per-frame rebuild of the only light-dependent structure. */
+int rt_renderer_set_light(rt_renderer_h r, const float light[3]);
 
 /* Read back one per-resolution record array of the current configuration
  * (layouts: kernels/rt_common.h; NO REFERENCE).  out NULL = size query

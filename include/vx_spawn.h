@@ -191,6 +191,28 @@ __device__ __forceinline__ void __vx_declare_tasks(uint32_t n) {
   if (blockIdx.x == 0 && threadIdx.x == 0) __vx_state.tasks = n;
 }
 
+/* The block whose chunks this hardware block runs.  VX_XCD_GROUP = g > 0:
+ * blocks are dealt round-robin over the 8 XCDs (b and b + 8 share one, each
+ * XCD its own L2; MI355X_MICROARCH.md "Workgroup dispatch, XCD placement"),
+ * so logical blocks are regrouped that g consecutive ones -- one 32x32 tile's
+ * chunks in the RT kernels -- run on one XCD, and the next 8 groups, one per
+ * XCD, start together (the work order's heaviest tiles spread over the
+ * XCDs).  A placement for speed only: every logical block runs once either
+ * way.  The tail of a grid that is not a multiple of 8 g keeps its ids. */
+#ifndef VX_XCD_GROUP
+#define VX_XCD_GROUP 0
+#endif
+__device__ __forceinline__ uint32_t __vx_logical_block() {
+#if VX_XCD_GROUP > 0
+  const uint32_t b = blockIdx.x, span = 8u * VX_XCD_GROUP;
+  if (b >= gridDim.x - gridDim.x % span) return b;
+  const uint32_t x = b & 7u, k = b >> 3;
+  return (k / VX_XCD_GROUP) * span + x * VX_XCD_GROUP + k % VX_XCD_GROUP;
+#else
+  return blockIdx.x;
+#endif
+}
+
 struct __vx_no_epilogue {
   template <typename Arg>
   __device__ __forceinline__ void operator()(bool, Arg*) const {}
@@ -221,7 +243,7 @@ __device__ __forceinline__ int vx_spawn_threads_ex(uint32_t dimension, const uin
   uint32_t ran = 0;
   vx_task_t task;
   task.threadIdx.x = task.threadIdx.y = task.threadIdx.z = 0;
-  for (uint32_t c = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6); c < nchunks;
+  for (uint32_t c = __vx_logical_block() * (blockDim.x >> 6) + (threadIdx.x >> 6); c < nchunks;
        c += nwaves) {
     const uint32_t t = c * VX_CHUNK + (threadIdx.x & 63u);
     if (t < num_groups) {
@@ -316,7 +338,10 @@ __device__ __forceinline__ int vx_spawn_chunks_block(uint32_t num_tasks, F kerne
  * defines the entry the driver launches with `block_threads` threads per
  * workgroup (must be a multiple of 64): `vx_main`, or the image's own name
  * vx_main_<image> given by -DVX_ENTRY (the driver finds it in the code
- * object's symbol table, so profiles tell the images apart). */
+ * object's symbol table, so profiles tell the images apart).  The body also
+ * sees `vx_launch_tag`, the launch's one kernel argument: 0, or the value an
+ * app set for this launch with vx_hip_set_launch_tag (vortex_hip.h) -- e.g.
+ * the step of a launch sequence sharing one argument block. */
 #define VX_MAIN(ArgT, argname, block_threads) \
   VX_MAIN_BOUNDS(ArgT, argname, __launch_bounds__(block_threads))
 /* same, asking the compiler for `waves_per_eu` resident waves per SIMD */
@@ -326,8 +351,8 @@ __device__ __forceinline__ int vx_spawn_chunks_block(uint32_t num_tasks, F kerne
 #define VX_ENTRY vx_main
 #endif
 #define VX_MAIN_BOUNDS(ArgT, argname, bounds)                                        \
-  static __device__ __forceinline__ int __vx_main_body(ArgT* argname);               \
-  extern "C" __global__ void bounds VX_ENTRY() {                                     \
+  static __device__ __forceinline__ int __vx_main_body(ArgT* argname, uint32_t vx_launch_tag); \
+  extern "C" __global__ void bounds VX_ENTRY(uint32_t __vx_tag) {                    \
     /* the block's counter row: only when the driver reads rows (then the   */    \
     /* block's waves meet at entry and exit; without, each wave runs and    */    \
     /* retires on its own)                                                  */    \
@@ -338,7 +363,7 @@ __device__ __forceinline__ int vx_spawn_chunks_block(uint32_t num_tasks, F kerne
     }                                                                                \
     const uint64_t a = ((uint64_t)__vx_dcrs[VX_DCR_BASE_STARTUP_ARG1] << 32) |       \
                        (uint64_t)__vx_dcrs[VX_DCR_BASE_STARTUP_ARG0];                \
-    (void)__vx_main_body(vx_ptr<ArgT>(a));                                           \
+    (void)__vx_main_body(vx_ptr<ArgT>(a), __vx_tag);                                 \
     if (rows_on) {                                                                   \
       __syncthreads();                                                               \
       if (__vx_dcrs[VX_DCR_HIP_MPM_ROWS] && threadIdx.x < VX_MPM_ROW &&              \
@@ -346,6 +371,6 @@ __device__ __forceinline__ int vx_spawn_chunks_block(uint32_t num_tasks, F kerne
         __vx_state.mpm[blockIdx.x][threadIdx.x] = __vx_mpm_lds[threadIdx.x];         \
     }                                                                                \
   }                                                                                  \
-  static __device__ __forceinline__ int __vx_main_body(ArgT* argname)
+  static __device__ __forceinline__ int __vx_main_body(ArgT* argname, uint32_t vx_launch_tag)
 
 #endif /* VX_SPAWN_H */

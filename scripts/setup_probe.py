@@ -6,7 +6,8 @@ Sequence (tekkaman, one renderer): 1024^2 with light A (cold: new
 resolution, new light), 1024^2 with light B (new light only: the shadow
 lists), light B again (nothing new), 4096^2 with light A (cold), then
 `--moving N` configures at 1024^2 with a new light each (the moving-light
-regime: only the shadow lists rebuild).  Prints one JSON line with every
+regime: only the shadow lists rebuild), then as many rt_renderer_set_light changes (each waited
+for and timed).  Prints one JSON line with every
 configure's setup_stats.  Run with RT_SETUP_TRACE=1 for the per-launch
 phases on stderr, under rocprofv3 --kernel-trace for their device times
 (vx_main_rt_setup dispatches in launch order)."""
@@ -44,6 +45,20 @@ def main():
     conf("cold_4096", 4096, la)
     for i in range(args.moving):
         conf(f"moving_{i}", 1024, (10.0 * (i % 5) - 20.0, 60.0 - i, 80.0 + 0.5 * i))
+    # set_light: the shadow lists alone, queued (then waited for, timed)
+    import time
+    r.configure(1024, 1024, shadows=True, light=la, counters=False)
+    r.render()
+    for i in range(args.moving):
+        L = (10.0 * (i % 5) - 20.0, 60.0 - i, 80.0 + 0.5 * i)
+        print(f"== set_light_{i}", file=sys.stderr, flush=True)
+        t0 = time.perf_counter()
+        r.set_light(L)
+        r.wait()
+        dt = (time.perf_counter() - t0) * 1e3
+        st = r.setup_stats()
+        out.append({"tag": f"set_light_{i}", "light": list(L), "set_light_wait_ms": round(dt, 4),
+                    "slist_entries": st["slist_entries"], "slist_on": st["slist_on"]})
     print(json.dumps(out))
     r.close()
     s.close()

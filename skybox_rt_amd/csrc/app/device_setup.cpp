@@ -12,6 +12,7 @@
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
+#include <cstddef>
 #include <cstring>
 #include <vector>
 
@@ -21,8 +22,7 @@
 namespace rtapp {
 namespace {
 
-// one setup launch: argument block, start, wait (the next launch and the
-// host's read-backs depend on it)
+// one setup launch (renderer creation): argument block, start, wait
 int run(rt_renderer* r, DevBuf* argb, const rt_setup_arg_t& a, uint32_t* launches) {
   static const bool trace = std::getenv("RT_SETUP_TRACE") != nullptr;  // per-launch phases to stderr
   const auto t0 = std::chrono::steady_clock::now();
@@ -108,63 +108,215 @@ int device_ingest(rt_renderer* r, bool records) {
   return run(r, &argb, g, &launches);
 }
 
-int device_setup(rt_renderer* r, bool raster, bool order_on, bool lists, uint32_t* heavy,
+namespace {
+
+// a persistent buffer holding at least `bytes`: kept while it is large
+// enough (vx_mem_access checks the range), else reallocated -- a free waits
+// for the device, so the setup's buffers only ever grow
+int ensure(rt_renderer* r, uint64_t bytes, vx_buffer_h* h, uint64_t* addr) {
+  const uint64_t b = bytes ? bytes : 64;
+  if (*h && vx_mem_access(*h, 0, b, VX_MEM_READ_WRITE) == 0)
+    return vx_mem_address(*h, addr) == 0 ? 0 : set_error("vx_mem_address failed");
+  return alloc(r, b, h, addr);
+}
+int ensure(rt_renderer* r, uint64_t bytes, DevScratch* d) { return ensure(r, bytes, &d->h, &d->addr); }
+
+// a launch sequence of the setup image (setup_common.h): launch i runs
+// ph[i] on every workgroup, then last[i] (the scans) on the last one
+struct Seq {
+  uint32_t ph[RTS_MAX_SEQ] = {}, last[RTS_MAX_SEQ] = {};
+  uint32_t n = 0;
+  void add(uint32_t p, uint32_t l = 0u) {
+    if (p == 0u && l == 0u) return;
+    ph[n] = p;
+    last[n] = l;
+    ++n;
+  }
+};
+
+// The argument block goes through the driver's stream (vx_hip_copy_to_dev_async)
+// and the n launches are queued behind it: no host wait before, between or
+// after them -- the caller reads the status words back when it needs them.
+int run_seq(rt_renderer* r, rt_setup_arg_t& g, const Seq& q, uint32_t* launches) {
+  static const bool trace = std::getenv("RT_SETUP_TRACE") != nullptr;  // the sequence to stderr
+  if (q.n == 0) return 0;
+  // a step's scans (one workgroup) read what the whole grid wrote in that
+  // step: they run as a launch of their own right behind it
+  Seq x;
+  for (uint32_t i = 0; i < q.n; ++i) {
+    x.add(q.ph[i]);
+    x.add(q.last[i]);
+  }
+  if (x.n > RTS_MAX_SEQ) return set_error("setup sequence too long");
+  g.phases = 0;
+  g.nseq = x.n;
+  for (uint32_t i = 0; i < RTS_MAX_SEQ; ++i) g.seq_phases[i] = i < x.n ? x.ph[i] : 0u;
+  if (ensure(r, sizeof(g), &r->su.args) != 0) return -1;
+  const int rc = r->copy_async ? r->copy_async(r->su.args.h, &g, 0, sizeof(g))
+                               : vx_copy_to_dev(r->su.args.h, &g, 0, sizeof(g));
+  if (rc != 0) return set_error("setup argument upload failed");
+  if (!r->set_tag) return set_error("the driver has no vx_hip_set_launch_tag");
+  for (uint32_t i = 0; i < x.n; ++i)
+    if (r->set_tag(r->dev, i) != 0 || vx_start(r->dev, r->setup_krnl, r->su.args.h) != 0)
+      return set_error("vx_start failed");
+  *launches += x.n;
+  if (trace)
+    for (uint32_t i = 0; i < x.n; ++i)
+      std::fprintf(stderr, "rt_setup seq launch %u/%u phases 0x%07x\n", i + 1, x.n, x.ph[i]);
+  return 0;
+}
+
+int read_status(rt_renderer* r, uint32_t st[RTS_STATUS_WORDS]) {
+  if (vx_copy_from_dev(st, r->su.status.h, 0, RTS_STATUS_WORDS * 4) != 0)
+    return set_error("vx_copy_from_dev failed");
+  return 0;
+}
+
+uint32_t slist_res() {
+  uint32_t N = RT_SLIST_N;
+  if (const char* e = std::getenv("RT_SLIST_N")) N = std::min(1024u, std::max(1u, (uint32_t)std::atoi(e)));
+  return N;
+}
+
+// the shadow-list fields of the setup argument block for the light in r->arg
+// (buffers grown to the light-space cells and the entry capacity r->su.scap)
+int slist_args(rt_renderer* r, rt_setup_arg_t* g) {
+  rt_kernel_arg_t& a = r->arg;
+  const uint32_t N = slist_res(), cells = 6u * N * N;
+  const uint32_t ncpart = (cells + RTS_BLOCKS_PER_PART - 1) / RTS_BLOCKS_PER_PART;
+  const uint64_t items = 6ull * r->sc->geometry.size();
+  if (r->su.scap == 0) {
+    // initial entry capacity (env RT_SETUP_SCAP: tests force the overflow refill)
+    r->su.scap = 1u << 19;
+    if (const char* e = std::getenv("RT_SETUP_SCAP")) r->su.scap = std::max(1u, (uint32_t)std::atoi(e));
+  }
+  if (ensure(r, (uint64_t)cells * 4, &r->su.scnt) || ensure(r, (uint64_t)ncpart * 4, &r->su.spart) ||
+      ensure(r, (uint64_t)cells * 8, &r->sidx, &a.sidx_addr) ||
+      ensure(r, items * RTS_SPROJ_WORDS * 4, &r->su.sproj) || ensure(r, (items + 1) * 4, &r->su.soff) ||
+      ensure(r, r->sc->geometry.size() * 4, &r->su.skey) ||
+      ensure(r, 3ull * r->su.scap * 4, &r->su.stmp) ||
+      ensure(r, ((uint64_t)r->su.scap + 1) * sizeof(rt_tri_t), &r->slist, &a.slist_addr))
+    return -1;
+  a.slist_n = N;
+  g->geom_addr = a.geom_addr;
+  g->slist_n = N;
+  for (int i = 0; i < 3; ++i) g->light[i] = a.light[i];
+  g->scnt_addr = r->su.scnt.addr;
+  g->spart_addr = r->su.spart.addr;
+  g->sidx_addr = a.sidx_addr;
+  g->sproj_addr = r->su.sproj.addr;
+  g->soff_addr = r->su.soff.addr;
+  g->skey_addr = r->su.skey.addr;
+  g->stmp_addr = r->su.stmp.addr;
+  g->slist_addr = a.slist_addr;
+  g->ncells = cells;
+  g->ncpart = ncpart;
+  g->scap = r->su.scap;
+  return 0;
+}
+
+// the lists' size limits (block_lists_fit) for the device's own verdict
+void list_limits(rt_setup_arg_t* g) {
+  g->max_list = RT_BLIST_MAX_LIST;
+  uint64_t cap = 16ull << 20;
+  if (const char* e = std::getenv("RT_BLIST_MAX_ENTRIES")) cap = std::strtoull(e, nullptr, 0);
+  g->max_entries = (uint32_t)std::min<uint64_t>(cap, 0xffffffffu);
+}
+
+// after a chain that built the shadow lists: their verdict from the status
+// words; an overflow of the entry capacity (only when the lists would be
+// used) grows it to the exact size and refills: cursors zeroed, SFILL, SSORT
+int slist_finish(rt_renderer* r, rt_setup_arg_t& g, uint32_t st[RTS_STATUS_WORDS], uint32_t* launches) {
+  r->sl_entries = st[5];
+  r->setup.slist_entries = st[5];
+  const bool fit = block_lists_fit(st[4], st[5]);
+  if (fit && st[7] != 0) {
+    r->su.scap = st[5];
+    if (slist_args(r, &g) != 0) return -1;
+    g.nfills = 0;
+    add_fill(&g, r->su.scnt.addr, g.ncells, 0u);
+    add_fill(&g, r->su.status.addr + 28, 1, 0u);  // the overflow word
+    Seq q;
+    q.add(RTS_FILL);
+    q.add(RTS_SFILL);
+    q.add(RTS_SSORT);
+    if (run_seq(r, g, q, launches) != 0 || read_status(r, st) != 0) return -1;
+    if (st[7] != 0) return set_error("shadow-list refill overflowed its exact capacity");
+  }
+  r->sl_pending = false;
+  r->sl_built = fit;
+  r->sl_rejected = !fit;
+  return 0;
+}
+
+}  // namespace
+
+int device_setup(rt_renderer* r, bool raster, bool order_on, bool lists, bool slists, uint32_t* heavy,
                  uint32_t* launches) {
   const rt_scene* s = r->sc;
   rt_kernel_arg_t& a = r->arg;
   *heavy = 0;
   *launches = 0;
+  r->setup.slist_built = 0;
+  if (r->sl_pending && settle_lists(r) != 0) return -1;  // lists queued by set_light
   const uint64_t np = s->scene.prims.size();
   uint64_t bbox_addr = 0;
-  if (alloc(r, np * sizeof(rt_prim_t), &r->prims, &a.prims_addr) ||
-      alloc(r, np * sizeof(rt_bbox_t), &r->bbox, &bbox_addr) ||
-      alloc(r, r->cbuf_bytes, &r->cbuf, &a.cbuf_addr))
-    return -1;
-  const uint32_t zero4[4] = {0, 0, 0, 0};
-  DevBuf argb, status;
-  if (alloc_tmp(r, sizeof(rt_setup_arg_t), &argb) || alloc_tmp(r, sizeof(zero4), &status, zero4))
+  if (ensure(r, np * sizeof(rt_prim_t), &r->prims, &a.prims_addr) ||
+      ensure(r, np * sizeof(rt_bbox_t), &r->bbox, &bbox_addr) ||
+      ensure(r, r->cbuf_bytes, &r->cbuf, &a.cbuf_addr) ||
+      ensure(r, RTS_STATUS_WORDS * 4, &r->su.status))
     return -1;
   rt_setup_arg_t g;
   base_arg(r, &g);
+  list_limits(&g);
   g.prims_addr = a.prims_addr;
   g.bbox_addr = bbox_addr;
-  g.status_addr = status.addr;
+  g.status_addr = r->su.status.addr;
   g.width = a.width;
   g.height = a.height;
   g.raster = raster ? 1u : 0u;
   // output buffer, cleared to the clear colour (draw3d/main.cpp:485-490)
   add_fill(&g, a.cbuf_addr, r->cbuf_bytes / 4, a.clear_color);
+  add_fill(&g, g.status_addr, RTS_STATUS_WORDS, 0u);
+  uint32_t st[RTS_STATUS_WORDS] = {};
   if (raster) {
     a.bbox_addr = bbox_addr;
-    if (alloc(r, (uint64_t)a.width * a.height * 4, &r->zbuf, &a.zbuf_addr)) return -1;
+    if (ensure(r, (uint64_t)a.width * a.height * 4, &r->zbuf, &a.zbuf_addr)) return -1;
     add_fill(&g, a.zbuf_addr, (uint64_t)a.width * a.height, 0xffffffffu);  // main.cpp:48
-    g.phases = RTS_FILL | RTS_PRIMVIS;
-    return run(r, &argb, g, launches);
+    Seq q;
+    q.add(RTS_FILL | RTS_PRIMVIS);
+    return run_seq(r, g, q, launches) != 0 || read_status(r, st) != 0 ? -1 : 0;
   }
   // primary-visibility records and the traversed tree's vnodes
   const bool bvh4 = r->use_bvh4;
   const uint32_t nn = bvh4 ? a.num_nodes4 : a.num_nodes;
   uint64_t vis_addr = 0;
-  if (alloc(r, np * 16, &r->vis, &vis_addr) ||
-      alloc(r, ((uint64_t)r->num_tris + 3) * sizeof(rt_vtri_t), &r->vtris, &a.vtris_addr) ||
-      alloc(r, s->layers.size() * sizeof(rt_vtri_t), &r->vlayers, &a.vlayers_addr) ||
-      alloc(r, s->geometry.size() * sizeof(rt_vtri_t), &r->vgeom, &a.vgeom_addr) ||
-      alloc(r, (uint64_t)nn * sizeof(rt_vnode_t), &r->vnodes, &a.vnodes_addr))
+  if (ensure(r, np * 16, &r->vis, &vis_addr) ||
+      ensure(r, ((uint64_t)r->num_tris + 3) * sizeof(rt_vtri_t), &r->vtris, &a.vtris_addr) ||
+      ensure(r, s->layers.size() * sizeof(rt_vtri_t), &r->vlayers, &a.vlayers_addr) ||
+      ensure(r, s->geometry.size() * sizeof(rt_vtri_t), &r->vgeom, &a.vgeom_addr) ||
+      ensure(r, (uint64_t)nn * sizeof(rt_vnode_t), &r->vnodes, &a.vnodes_addr) ||
+      ensure(r, (uint64_t)nn * 4, &r->su.parent) || ensure(r, (uint64_t)nn * 8, &r->su.count))
     return -1;
   a.num_vnodes = nn;
-  DevBuf parent, count, weight, hist, bcnt, bpart, btmp;
-  if (alloc_tmp(r, (uint64_t)nn * 4, &parent) || alloc_tmp(r, (uint64_t)nn * 8, &count)) return -1;
   // per-block candidate lists: one count / cursor word and one (first, count)
-  // pair per local 8x8 block, one partial sum per RTS_BLOCKS_PER_PART blocks
+  // pair per local 8x8 block, one partial sum per RTS_BLOCKS_PER_PART blocks;
+  // the entries at a capacity that only grows (the exact size after an overflow)
   const uint32_t nblk = lists ? r->local_tiles * 16u : 0u;
   const uint32_t nbpart = (nblk + RTS_BLOCKS_PER_PART - 1) / RTS_BLOCKS_PER_PART;
-  if (lists && (alloc_tmp(r, (uint64_t)nblk * 4, &bcnt) || alloc_tmp(r, (uint64_t)nbpart * 4, &bpart) ||
-                alloc(r, (uint64_t)nblk * 8, &r->bidx, &a.bidx_addr)))
-    return -1;
+  if (lists) {
+    uint64_t bcap0 = 2ull * nblk + 16ull * s->geometry.size();
+    if (const char* e = std::getenv("RT_SETUP_BCAP")) bcap0 = std::max(1ull, std::strtoull(e, nullptr, 0));  // tests
+    r->su.bcap = std::max<uint64_t>(r->su.bcap, bcap0);
+    if (ensure(r, (uint64_t)nblk * 4, &r->su.bcnt) || ensure(r, (uint64_t)nbpart * 4, &r->su.bpart) ||
+        ensure(r, (uint64_t)nblk * 8, &r->bidx, &a.bidx_addr) || ensure(r, r->su.bcap * 16, &r->su.btmp) ||
+        ensure(r, (r->su.bcap + RT_BLIST_PAD) * 16, &r->blist, &a.blist_addr))
+      return -1;
+  }
   const uint64_t wwords = (uint64_t)(a.tiles_x + 1) * (a.tiles_y + 1);
   const uint32_t nblocks = (r->local_tiles + RTS_ITEMS - 1) / RTS_ITEMS;
-  if (order_on && (alloc_tmp(r, wwords * 4, &weight) || alloc_tmp(r, 256ull * nblocks * 4, &hist) ||
-                   alloc(r, (uint64_t)r->local_tiles * 4, &r->order, &a.order_addr)))
+  if (order_on && (ensure(r, wwords * 4, &r->su.weight) || ensure(r, 256ull * nblocks * 4, &r->su.hist) ||
+                   ensure(r, (uint64_t)r->local_tiles * 4, &r->order, &a.order_addr)))
     return -1;
   g.vis_addr = vis_addr;
   g.tris_addr = a.tris_addr;
@@ -173,10 +325,10 @@ int device_setup(rt_renderer* r, bool raster, bool order_on, bool lists, uint32_
   g.vtris_addr = a.vtris_addr;
   g.vlayers_addr = a.vlayers_addr;
   g.vgeom_addr = a.vgeom_addr;
-  g.parent_addr = parent.addr;
-  g.count_addr = count.addr;
-  g.weight_addr = weight.addr;
-  g.hist_addr = hist.addr;
+  g.parent_addr = r->su.parent.addr;
+  g.count_addr = r->su.count.addr;
+  g.weight_addr = r->su.weight.addr;
+  g.hist_addr = r->su.hist.addr;
   g.order_addr = a.order_addr;
   g.num_tris = r->num_tris;
   g.num_nodes = nn;
@@ -189,114 +341,143 @@ int device_setup(rt_renderer* r, bool raster, bool order_on, bool lists, uint32_
   g.nblocks = nblocks;
   g.nblk = nblk;
   g.nbpart = nbpart;
-  g.bcnt_addr = bcnt.addr;
-  g.bpart_addr = bpart.addr;
+  g.bcnt_addr = r->su.bcnt.addr;
+  g.bpart_addr = r->su.bpart.addr;
   g.bidx_addr = a.bidx_addr;
-  add_fill(&g, parent.addr, nn, 0xffffffffu);
-  if (order_on) add_fill(&g, weight.addr, wwords, 0u);
-  if (lists) add_fill(&g, bcnt.addr, nblk, 0u);
-  const uint32_t ord = order_on ? 1u : 0u;
-  uint32_t bl = lists ? 1u : 0u;
-  const uint32_t steps[] = {
-      RTS_FILL | RTS_PRIMVIS,                                     // records, clears
-      RTS_VTRIS | (ord ? RTS_WEIGHT : 0u) | (bl ? RTS_BCOUNT : 0u),  // vtris; tile weights; block counts
-      RTS_LINK | (ord ? RTS_ROWSUM : 0u) | (bl ? RTS_BSUM : 0u),     // tree parents; rows; block sums
-      RTS_CLIMB | (ord ? RTS_COLSUM : 0u) | (bl ? RTS_BSCAN : 0u),   // vnodes; columns; sums scanned
-      (ord ? RTS_HIST : 0u) | (bl ? RTS_BOFF : 0u),                // tile histograms; list offsets
-      0u,                                                          // (list sizes read back here)
-      (ord ? RTS_SCAN : 0u) | (bl ? RTS_BFILL : 0u),               // digit scan; list entries
-      (ord ? RTS_SCATTER : 0u) | (bl ? RTS_BSORT : 0u)};           // tile order; lists sorted
-  uint32_t st[4] = {0, 0, 0, 0};
-  for (uint32_t ph : steps) {
-    if (ph == 0u && bl) {
-      // the list sizes: the longest list and the entries in total decide
-      // whether the lists are built (else the kernels walk the tree)
-      if (vx_copy_from_dev(st, status.h, 0, sizeof(st)) != 0) return set_error("vx_copy_from_dev failed");
-      r->setup.blist_max = st[1];
-      r->setup.blist_entries = st[2];
-      if (!rtapp::block_lists_fit(st[1], st[2])) {
-        bl = 0u;
-        continue;
-      }
-      const uint64_t total = st[2];
-      if (alloc_tmp(r, total * 16 + 16, &btmp) || alloc(r, (total + RT_BLIST_PAD) * 16, &r->blist, &a.blist_addr))
-        return -1;
-      g.btmp_addr = btmp.addr;
-      g.blist_addr = a.blist_addr;
-      g.blist_entries = st[2];
-      continue;
-    }
-    if (!bl) ph &= ~(RTS_BFILL | RTS_BSORT);
-    if (!ph) continue;
-    g.phases = ph;
-    if (run(r, &argb, g, launches) != 0) return -1;
+  g.btmp_addr = r->su.btmp.addr;
+  g.blist_addr = a.blist_addr;
+  g.bcap = lists ? (uint32_t)r->su.bcap : 0u;
+  add_fill(&g, g.parent_addr, nn, 0xffffffffu);
+  if (order_on) add_fill(&g, g.weight_addr, wwords, 0u);
+  if (lists) add_fill(&g, g.bcnt_addr, nblk, 0u);
+  // the shadow lists for this light unless the ones built (or found too
+  // large) for it are current
+  const uint32_t N = slist_res();
+  const bool sl_now = slists && !((r->sl_built || r->sl_rejected) && r->sl_n == N &&
+                                  std::memcmp(r->sl_light, a.light, sizeof(a.light)) == 0);
+  r->setup.slist_built = sl_now ? 1u : 0u;
+  if (sl_now) {
+    if (slist_args(r, &g) != 0) return -1;
+    add_fill(&g, g.scnt_addr, g.ncells, 0u);
   }
-  a.blist_blocks = bl ? nblk : 0u;
-  if (vx_copy_from_dev(st, status.h, 0, sizeof(st)) != 0) return set_error("vx_copy_from_dev failed");
+  const uint32_t ord = order_on ? 1u : 0u, bl = lists ? 1u : 0u, sl = sl_now ? 1u : 0u;
+  // the per-resolution records, the block lists, the work order and the
+  // shadow lists in one stream-ordered sequence: six launches, one
+  // read-back of the status words at the end
+  Seq q;
+  q.add(RTS_FILL | RTS_PRIMVIS | (sl ? RTS_SPROJ : 0u), sl ? RTS_SOSCAN : 0u);
+  q.add(RTS_VTRIS | (ord ? RTS_WEIGHT : 0u) | (bl ? RTS_BCOUNT : 0u) | (sl ? RTS_SCOUNT : 0u));
+  q.add(RTS_LINK | (ord ? RTS_ROWSUM : 0u) | (bl ? RTS_BSUM : 0u) | (sl ? RTS_SSUM : 0u),
+        (bl ? RTS_BSCAN : 0u) | (sl ? RTS_SSCAN : 0u));
+  q.add(RTS_CLIMB | (ord ? RTS_COLSUM : 0u) | (bl ? RTS_BOFF : 0u) | (sl ? RTS_SOFF : 0u));
+  q.add((ord ? RTS_HIST : 0u) | (bl ? RTS_BFILL : 0u) | (sl ? RTS_SFILL : 0u), ord ? RTS_SCAN : 0u);
+  q.add((ord ? RTS_SCATTER : 0u) | (bl ? RTS_BSORT : 0u) | (sl ? RTS_SSORT : 0u));
+  if (run_seq(r, g, q, launches) != 0 || read_status(r, st) != 0) return -1;
   if (st[0] & RTS_ERR_REF) return set_error("malformed BVH (reference out of range)");
   if (st[0] & RTS_ERR_PID) return set_error("malformed BVH (leaf pid out of range)");
   if (st[0] & RTS_ERR_CLIMB) return set_error("malformed BVH (deeper than 64 levels)");
-  // local tiles with weight > 0 = items whose digit is below 255 = the
-  // exclusive-scan offset of digit 255 in block 0
-  if (order_on &&
-      vx_copy_from_dev(heavy, hist.h, 255ull * nblocks * 4, 4) != 0)
-    return set_error("vx_copy_from_dev failed");
+  *heavy = order_on ? st[3] : 0u;
+  a.blist_blocks = 0;
+  if (lists) {
+    r->setup.blist_max = st[1];
+    r->setup.blist_entries = st[2];
+    const bool fit = block_lists_fit(st[1], st[2]);
+    if (fit && st[6] != 0) {
+      // more entries than the capacity: grow it to the exact size and refill
+      r->su.bcap = st[2];
+      if (ensure(r, r->su.bcap * 16, &r->su.btmp) ||
+          ensure(r, (r->su.bcap + RT_BLIST_PAD) * 16, &r->blist, &a.blist_addr))
+        return -1;
+      g.btmp_addr = r->su.btmp.addr;
+      g.blist_addr = a.blist_addr;
+      g.bcap = (uint32_t)r->su.bcap;
+      g.nfills = 0;
+      add_fill(&g, g.bcnt_addr, nblk, 0u);
+      add_fill(&g, g.status_addr + 24, 1, 0u);
+      Seq f;
+      f.add(RTS_FILL);
+      f.add(RTS_BFILL);
+      f.add(RTS_BSORT);
+      if (run_seq(r, g, f, launches) != 0 || read_status(r, st) != 0) return -1;
+      if (st[6] != 0) return set_error("block-list refill overflowed its exact capacity");
+    }
+    a.blist_blocks = fit ? nblk : 0u;
+  }
+  if (sl_now) {
+    std::memcpy(r->sl_light, a.light, sizeof(a.light));
+    r->sl_n = N;
+    if (slist_finish(r, g, st, launches) != 0) return -1;
+  } else if (slists) {
+    r->setup.slist_entries = r->sl_entries;
+    a.slist_n = N;
+  }
+  a.slist_on = slists && r->sl_built ? 1u : 0u;
   return 0;
 }
 
-int shadow_lists(rt_renderer* r, uint32_t* launches) {
+int set_light(rt_renderer* r, const float light[3], uint32_t* launches) {
   rt_kernel_arg_t& a = r->arg;
-  uint32_t N = RT_SLIST_N;
-  if (const char* e = std::getenv("RT_SLIST_N")) N = std::min(1024u, std::max(1u, (uint32_t)std::atoi(e)));
-  if (r->sl_built && std::memcmp(r->sl_light, a.light, sizeof(a.light)) == 0 && a.slist_n == N) {
-    r->setup.slist_entries = r->sl_entries;
-    return 0;
+  for (int i = 0; i < 3; ++i) {
+    a.light[i] = light[i];
+    r->params.light[i] = light[i];
   }
-  r->sl_built = false;
-  a.slist_on = 0;
-  a.slist_n = N;
-  const uint32_t cells = 6u * N * N, nbpart = (cells + RTS_BLOCKS_PER_PART - 1) / RTS_BLOCKS_PER_PART;
-  const uint32_t zero4[4] = {0, 0, 0, 0};
-  DevBuf argb, status, cnt, part, tmp;
-  if (alloc_tmp(r, sizeof(rt_setup_arg_t), &argb) || alloc_tmp(r, sizeof(zero4), &status, zero4) ||
-      alloc_tmp(r, (uint64_t)cells * 4, &cnt) || alloc_tmp(r, (uint64_t)nbpart * 4, &part) ||
-      alloc(r, (uint64_t)cells * 8, &r->sidx, &a.sidx_addr))
-    return -1;
+  // the render arguments' light, in stream order behind the queued frames
+  const int rc = r->copy_async
+                     ? r->copy_async(r->args, a.light, offsetof(rt_kernel_arg_t, light), sizeof(a.light))
+                     : vx_copy_to_dev(r->args, a.light, offsetof(rt_kernel_arg_t, light), sizeof(a.light));
+  if (rc != 0) return set_error("light upload failed");
+  if (!r->sl_mode) return 0;  // this configuration's shadow rays walk the BVH
+  // the shadow lists for the new light, queued behind it: the chain's last
+  // launch writes the render arguments' slist_on (the lists' own verdict),
+  // so no host wait anywhere; the status words are read when asked for
+  // (rt_renderer_setup_stats) or by the next configure
   rt_setup_arg_t g;
   base_arg(r, &g);
-  g.geom_addr = a.geom_addr;
-  g.status_addr = status.addr;
-  g.bcnt_addr = cnt.addr;
-  g.bpart_addr = part.addr;
-  g.bidx_addr = a.sidx_addr;
-  g.nblk = cells;
-  g.nbpart = nbpart;
-  g.slist_n = N;
-  for (int i = 0; i < 3; ++i) g.light[i] = a.light[i];
-  add_fill(&g, cnt.addr, cells, 0u);
-  for (uint32_t ph : {RTS_FILL, RTS_SCOUNT, RTS_BSUM, RTS_BSCAN, RTS_BOFF}) {
-    g.phases = ph;
-    if (run(r, &argb, g, launches) != 0) return -1;
-  }
-  uint32_t st[4];
-  if (vx_copy_from_dev(st, status.h, 0, sizeof(st)) != 0) return set_error("vx_copy_from_dev failed");
-  r->sl_entries = st[2];
-  r->setup.slist_entries = st[2];
-  if (!block_lists_fit(st[1], st[2])) return 0;  // the packet walk, as without lists
-  // tmp: the entries' geometry indices, then their sort keys
-  if (alloc_tmp(r, (uint64_t)st[2] * 8 + 8, &tmp) || alloc(r, ((uint64_t)st[2] + 1) * 48, &r->slist, &a.slist_addr))
-    return -1;
-  g.btmp_addr = tmp.addr;
-  g.slist_addr = a.slist_addr;
-  g.blist_entries = st[2];
-  g.nfills = 0;
-  for (uint32_t ph : {RTS_SFILL, RTS_SSORT}) {
-    g.phases = ph;
-    if (run(r, &argb, g, launches) != 0) return -1;
-  }
+  list_limits(&g);
+  g.status_addr = r->su.status.addr;
+  if (slist_args(r, &g) != 0) return -1;
+  uint64_t rargs = 0;
+  if (vx_mem_address(r->args, &rargs) != 0) return set_error("vx_mem_address failed");
+  g.rargs_addr = rargs;
+  add_fill(&g, g.scnt_addr, g.ncells, 0u);
+  add_fill(&g, g.status_addr + 16, 4, 0u);  // status words 4..7: the shadow lists
+  Seq q;
+  q.add(RTS_FILL | RTS_SPROJ, RTS_SOSCAN);
+  q.add(RTS_SCOUNT);
+  q.add(RTS_SSUM, RTS_SSCAN);
+  q.add(RTS_SOFF);
+  q.add(RTS_SFILL);
+  q.add(RTS_SSORT);
+  if (run_seq(r, g, q, launches) != 0) return -1;
   std::memcpy(r->sl_light, a.light, sizeof(a.light));
-  r->sl_built = true;
-  a.slist_on = 1;
+  r->sl_n = a.slist_n;
+  r->sl_pending = true;
+  return 0;
+}
+
+int settle_lists(rt_renderer* r) {
+  if (!r->sl_pending) return 0;
+  uint32_t st[RTS_STATUS_WORDS];
+  if (read_status(r, st) != 0) return -1;
+  rt_setup_arg_t g;
+  base_arg(r, &g);
+  list_limits(&g);
+  g.status_addr = r->su.status.addr;
+  uint64_t rargs = 0;
+  if (vx_mem_address(r->args, &rargs) != 0) return set_error("vx_mem_address failed");
+  g.rargs_addr = rargs;
+  uint32_t launches = 0;
+  const uint64_t sidx0 = r->arg.sidx_addr, slist0 = r->arg.slist_addr;
+  if (slist_finish(r, g, st, &launches) != 0) return -1;
+  r->arg.slist_on = r->sl_built ? 1u : 0u;
+  if (r->arg.sidx_addr != sidx0 || r->arg.slist_addr != slist0) {
+    // a refill moved the lists: the render arguments' addresses follow (the
+    // refill's SSORT wrote their slist_on)
+    const size_t o = offsetof(rt_kernel_arg_t, slist_n);
+    const size_t n = offsetof(rt_kernel_arg_t, slist_addr) + sizeof(uint64_t) - o;
+    if (vx_copy_to_dev(r->args, reinterpret_cast<const uint8_t*>(&r->arg) + o, o, n) != 0)
+      return set_error("vx_copy_to_dev failed");
+  }
   return 0;
 }
 

@@ -293,6 +293,8 @@ int rt_renderer_create(rt_scene_h s, const char* kernel_dir, rt_renderer_h* out)
   r->set_counters = (vx_hip_set_counters_t)vx_driver_symbol("vx_hip_set_counters");
   r->launch_group = (vx_hip_launch_group_t)vx_driver_symbol("vx_hip_launch_group");
   r->set_timing = (vx_hip_set_timing_t)vx_driver_symbol("vx_hip_set_timing");
+  r->copy_async = (vx_hip_copy_to_dev_async_t)vx_driver_symbol("vx_hip_copy_to_dev_async");
+  r->set_tag = (vx_hip_set_launch_tag_t)vx_driver_symbol("vx_hip_set_launch_tag");
   // the two-kernel path tracer's images (binary16 BVH4 only; the others run
   // the one-kernel pt_kernel images), from the kernel directory itself: a
   // directory without them (e.g. lib/pt_compact) runs its own pt_kernel
@@ -434,7 +436,20 @@ int rt_renderer_export_vis_tree(rt_renderer_h r, int32_t* refs, uint32_t* num_no
 int rt_renderer_setup_stats(rt_renderer_h r, rt_setup_stats_t* st) {
   if (!r || !st) return fail("null argument");
   if (!r->configured) return fail("renderer not configured");
+  if (rtapp::settle_lists(r) != 0) return -1;
+  r->setup.slist_on = r->arg.slist_on;
   *st = r->setup;
+  return 0;
+}
+
+int rt_renderer_set_light(rt_renderer_h r, const float light[3]) {
+  if (!r || !light) return fail("null argument");
+  if (!r->configured) return fail("renderer not configured");
+  if (!(r->params.flags & (RT_RENDER_SHADOWS | RT_RENDER_PATH)) || (r->params.flags & RT_RENDER_RASTER))
+    return fail("rt_renderer_set_light: the configuration traces no shadow rays");
+  uint32_t launches = 0;
+  if (rtapp::set_light(r, light, &launches) != 0) return -1;
+  r->setup.slist_built = r->sl_mode ? 1u : 0u;
   return 0;
 }
 
@@ -920,24 +935,23 @@ int rt_renderer_configure(rt_renderer_h r, const rt_render_params_t* p) {
   a.blist_addr = a.bidx_addr = 0;
   r->setup.blist_entries = 0;
   r->setup.blist_max = 0;
+  // shadow rays (primary+shadow frames, every path vertex): light-space
+  // lists (built on the device for this light; env RT_SHADOW_LISTS=0 keeps
+  // the BVH walks; the host setup path walks the BVH)
+  const char* sle = std::getenv("RT_SHADOW_LISTS");
+  const bool slists = device && !raster && !(p->flags & RT_RENDER_FLAT) &&
+                      (p->flags & (RT_RENDER_SHADOWS | RT_RENDER_PATH)) && a.num_geom > 0 &&
+                      !(sle && std::atoi(sle) == 0) && !bvh_walk;
+  r->sl_mode = slists;
+  a.slist_on = 0;
+  r->setup.slist_entries = 0;
   const auto t1 = std::chrono::steady_clock::now();
   if (device) {
     r->vis_refs.clear();
     r->vis_pids.clear();
-    if (rtapp::device_setup(r, raster, order_on, lists, &heavy, &launches) != 0) return -1;
+    if (rtapp::device_setup(r, raster, order_on, lists, slists, &heavy, &launches) != 0) return -1;
   } else if (host_setup(r, p, raster, order_on, lists, &heavy) != 0) {
     return -1;
-  }
-  // shadow rays (primary+shadow frames, every path vertex): light-space
-  // lists (built on the device for this light; env RT_SHADOW_LISTS=0 keeps
-  // the BVH walks; the host setup path walks the BVH)
-  a.slist_on = 0;
-  r->setup.slist_entries = 0;
-  const char* sle = std::getenv("RT_SHADOW_LISTS");
-  if (device && !raster && !(p->flags & RT_RENDER_FLAT) && (p->flags & (RT_RENDER_SHADOWS | RT_RENDER_PATH)) &&
-      a.num_geom > 0 && !(sle && std::atoi(sle) == 0) && !bvh_walk) {
-    if (rtapp::shadow_lists(r, &launches) != 0) return -1;
-    a.slist_on = r->sl_built ? 1u : 0u;
   }
   const double setup_ms = ms_since(t1);
   if (order_on) {

@@ -27,6 +27,28 @@ struct rt_scene {
   double parse_ms = 0, bvh_ms = 0;
 };
 
+// a device buffer of the setup that persists across configurations and only
+// grows (device_setup.cpp ensure)
+struct DevScratch {
+  vx_buffer_h h = nullptr;
+  uint64_t addr = 0;
+};
+// the device setup's argument block, status words and scratch arrays
+struct SetupScratch {
+  DevScratch args, status, parent, count, weight, hist, bcnt, bpart, btmp;
+  DevScratch scnt, spart, sproj, soff, skey, stmp;
+  uint64_t bcap = 0;   // block-list entry capacity of btmp / blist
+  uint32_t scap = 0;   // shadow-list entry capacity of stmp / slist
+  void release() {
+    for (DevScratch* d : {&args, &status, &parent, &count, &weight, &hist, &bcnt, &bpart, &btmp, &scnt, &spart,
+                          &sproj, &soff, &skey, &stmp})
+      if (d->h) {
+        vx_mem_free(d->h);
+        d->h = nullptr;
+      }
+  }
+};
+
 struct rt_renderer {
   rt_scene* sc = nullptr;
   vx_device_h dev = nullptr;
@@ -48,8 +70,15 @@ struct rt_renderer {
   vx_buffer_h vnodes = nullptr, vtris = nullptr, vlayers = nullptr, vgeom = nullptr;
   vx_buffer_h blist = nullptr, bidx = nullptr;  // per-block candidate lists (rt_bentry_t)
   vx_buffer_h sidx = nullptr, slist = nullptr;  // light-space shadow lists (built for sl_light)
+  bool sl_mode = false;     // this configuration's shadow rays use the light-space lists
+  bool sl_pending = false;  // lists queued by rt_renderer_set_light, status not read yet
+  SetupScratch su;
+  vx_hip_copy_to_dev_async_t copy_async = nullptr;
+  vx_hip_set_launch_tag_t set_tag = nullptr;
   float sl_light[3] = {0, 0, 0};
+  uint32_t sl_n = 0;        // the cube-map resolution they were built at
   bool sl_built = false;
+  bool sl_rejected = false;  // built for sl_light / sl_n and too large (block_lists_fit)
   uint64_t sl_entries = 0;
   vx_buffer_h gather_recv = nullptr, gather_image = nullptr;  // rank 0 of rt_render_gather
   vx_buffer_h prims = nullptr, cbuf = nullptr, args = nullptr;
@@ -97,6 +126,7 @@ struct rt_renderer {
       if (*b) vx_mem_free(*b);
       *b = nullptr;
     }
+    su.release();
     if (dev) vx_dev_close(dev);
   }
 };
@@ -128,15 +158,21 @@ int device_ingest(rt_renderer* r, bool records);
 // (+ bbox, zbuf clear for raster), vis / vtris / vlayers / vgeom / vnodes,
 // the tile order (heavy = local tiles with weight > 0), the cleared cbuf.
 // r->arg holds the layout fields (tiles, shard, flags, the tree); the
-// record buffers are (re)allocated here and their addresses set in r->arg.
+// record buffers grow as needed and their addresses are set in r->arg.
 // lists: also the per-block candidate lists (rt_bentry_t, the bidx / blist
-// buffers and arg.blist_blocks; 0 when they do not fit, block_lists_fit)
-int device_setup(rt_renderer* r, bool raster, bool order_on, bool lists, uint32_t* heavy,
+// buffers and arg.blist_blocks; 0 when they do not fit, block_lists_fit);
+// slists: the light-space shadow lists for a.light unless current (kept
+// while the light is unchanged; arg.slist_on 0 when they do not fit).  One
+// stream-ordered launch sequence, one status read-back.
+int device_setup(rt_renderer* r, bool raster, bool order_on, bool lists, bool slists, uint32_t* heavy,
                  uint32_t* launches);
-// the light-space shadow lists for a.light (rt_common.h; rt_setup.hip
-// SCOUNT .. SSORT), kept while the light is unchanged: arg.slist_on /
-// sidx_addr / slist_addr (slist_on 0 when they do not fit)
-int shadow_lists(rt_renderer* r, uint32_t* launches);
+// rt_renderer_set_light: the new light into the render arguments and, when
+// the configuration uses them, its shadow lists -- all queued on the
+// driver's stream behind the in-flight frames, no host wait
+int set_light(rt_renderer* r, const float light[3], uint32_t* launches);
+// read the status of lists queued by set_light (waits for the device): their
+// size, an overflow refill, r->sl_built
+int settle_lists(rt_renderer* r);
 // whether lists with this longest list and this many entries are built
 // (RT_BLIST_MAX_LIST, the device sort's limit; env RT_BLIST_MAX_ENTRIES,
 // default 16 M entries = 512 MiB of list and sort buffers)

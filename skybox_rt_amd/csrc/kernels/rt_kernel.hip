@@ -31,6 +31,14 @@
 // geometry list, no BVH).
 #include <hip/hip_runtime.h>
 
+#ifndef RT_BLOCK_THREADS
+#define RT_BLOCK_THREADS 64
+#endif
+// RT_XCD: a 32x32 tile's 16 one-chunk waves on one XCD (vx_spawn.h
+// VX_XCD_GROUP: blocks per tile)
+#if defined(RT_XCD) && RT_XCD && !defined(VX_XCD_GROUP)
+#define VX_XCD_GROUP (16 / (RT_BLOCK_THREADS / 64))
+#endif
 #include "rt_trace.h"
 
 #ifndef RT_FLAT

@@ -521,12 +521,9 @@ __device__ void phase_hist(const rt_setup_arg_t* a) {
   }
 }
 
-// exclusive scan of hist[256][nblocks] (digit-major) by workgroup 0
+// RTS_SCAN: exclusive scan of hist[256][nblocks] (digit-major) by one
+// workgroup (run_scans)
 __device__ void scan_excl(uint32_t* v, uint32_t n, uint32_t* total);
-__device__ void phase_scan(const rt_setup_arg_t* a) {
-  if (blockIdx.x != 0) return;
-  scan_excl(vx_ptr<uint32_t>(a->hist_addr), 256u * a->nblocks, nullptr);
-}
 
 // stable scatter of the local tile indices (rank = digit offset of the block
 // + earlier rounds + earlier waves + lanes below with the same digit)
@@ -639,25 +636,44 @@ __device__ __forceinline__ void block_sum_max(uint32_t xs, uint32_t xm, uint32_t
   __syncthreads();
 }
 
-// per RTS_BLOCKS_PER_PART blocks: their entry sum -> bpart, the longest list -> status[1]
-__device__ void phase_bsum(const rt_setup_arg_t* a) {
-  const uint32_t* bcnt = vx_ptr<const uint32_t>(a->bcnt_addr);
-  uint32_t* bpart = vx_ptr<uint32_t>(a->bpart_addr);
+// The count -> scan -> offsets steps of a set of lists: the 8x8 blocks'
+// candidate lists (status words 1, 2) or the light-space cells' shadow lists
+// (status words 4, 5)
+struct ListSet {
+  uint32_t* cnt;   // entries per list (then the fill cursors)
+  uint32_t* part;  // per RTS_BLOCKS_PER_PART lists their sum, then its exclusive scan
+  uint2* idx;      // per list (first entry, count)
+  uint32_t n, npart;
+  uint32_t* longest;  // status word: the longest list
+  uint32_t* total;    // status word: entries in total
+};
+__device__ __forceinline__ ListSet block_set(const rt_setup_arg_t* a) {
   uint32_t* status = vx_ptr<uint32_t>(a->status_addr);
+  return ListSet{vx_ptr<uint32_t>(a->bcnt_addr), vx_ptr<uint32_t>(a->bpart_addr), vx_ptr<uint2>(a->bidx_addr),
+                 a->nblk, a->nbpart, status + 1, status + 2};
+}
+__device__ __forceinline__ ListSet cell_set(const rt_setup_arg_t* a) {
+  uint32_t* status = vx_ptr<uint32_t>(a->status_addr);
+  return ListSet{vx_ptr<uint32_t>(a->scnt_addr), vx_ptr<uint32_t>(a->spart_addr), vx_ptr<uint2>(a->sidx_addr),
+                 a->ncells, a->ncpart, status + 4, status + 5};
+}
+
+// per RTS_BLOCKS_PER_PART lists: their entry sum -> part, the longest list -> *longest
+__device__ void phase_lsum(const ListSet& L) {
   constexpr uint32_t Q = RTS_BLOCKS_PER_PART / RTS_BLOCK;
-  for (uint32_t b = blockIdx.x; b < a->nbpart; b += gridDim.x) {
+  for (uint32_t b = blockIdx.x; b < L.npart; b += gridDim.x) {
     uint32_t sum = 0, mx = 0;
     for (uint32_t q = 0; q < Q; ++q) {
       const uint32_t lb = b * RTS_BLOCKS_PER_PART + threadIdx.x * Q + q;
-      const uint32_t c = lb < a->nblk ? bcnt[lb] : 0u;
+      const uint32_t c = lb < L.n ? L.cnt[lb] : 0u;
       sum += c;
       mx = max(mx, c);
     }
     uint32_t ts, tm;
     block_sum_max(sum, mx, &ts, &tm);
     if (threadIdx.x == 0) {
-      bpart[b] = ts;
-      atomicMax(&status[1], tm);
+      L.part[b] = ts;
+      atomicMax(L.longest, tm);
     }
   }
 }
@@ -686,24 +702,19 @@ __device__ void scan_excl(uint32_t* v, uint32_t n, uint32_t* total) {
   if (total && threadIdx.x == RTS_BLOCK - 1) *total = s[RTS_BLOCK - 1];
 }
 
-__device__ void phase_bscan(const rt_setup_arg_t* a) {
-  if (blockIdx.x != 0) return;
-  scan_excl(vx_ptr<uint32_t>(a->bpart_addr), a->nbpart, vx_ptr<uint32_t>(a->status_addr) + 2);
-}
+// (one workgroup) exclusive scan of the partial sums, the total -> *total
+__device__ void phase_lscan(const ListSet& L) { scan_excl(L.part, L.npart, L.total); }
 
-// per local block: (first entry, count) -> bidx; the count word zeroed (it
-// becomes the block's fill cursor)
-__device__ void phase_boff(const rt_setup_arg_t* a) {
-  uint32_t* bcnt = vx_ptr<uint32_t>(a->bcnt_addr);
-  const uint32_t* bpart = vx_ptr<const uint32_t>(a->bpart_addr);
-  uint2* bidx = vx_ptr<uint2>(a->bidx_addr);
+// per list: (first entry, count) -> idx; the count word zeroed (it becomes
+// the list's fill cursor)
+__device__ void phase_loff(const ListSet& L) {
   __shared__ uint32_t s[RTS_BLOCK];
   constexpr uint32_t Q = RTS_BLOCKS_PER_PART / RTS_BLOCK;
-  for (uint32_t b = blockIdx.x; b < a->nbpart; b += gridDim.x) {
+  for (uint32_t b = blockIdx.x; b < L.npart; b += gridDim.x) {
     const uint32_t lb0 = b * RTS_BLOCKS_PER_PART + threadIdx.x * Q;
     uint32_t c[Q], sum = 0;
     for (uint32_t q = 0; q < Q; ++q) {
-      c[q] = lb0 + q < a->nblk ? bcnt[lb0 + q] : 0u;
+      c[q] = lb0 + q < L.n ? L.cnt[lb0 + q] : 0u;
       sum += c[q];
     }
     s[threadIdx.x] = sum;
@@ -714,11 +725,11 @@ __device__ void phase_boff(const rt_setup_arg_t* a) {
       s[threadIdx.x] += y;
       __syncthreads();
     }
-    uint32_t run = bpart[b] + s[threadIdx.x] - sum;
+    uint32_t run = L.part[b] + s[threadIdx.x] - sum;
     for (uint32_t q = 0; q < Q; ++q) {
-      if (lb0 + q < a->nblk) {
-        bidx[lb0 + q] = make_uint2(run, c[q]);
-        bcnt[lb0 + q] = 0u;
+      if (lb0 + q < L.n) {
+        L.idx[lb0 + q] = make_uint2(run, c[q]);
+        L.cnt[lb0 + q] = 0u;
       }
       run += c[q];
     }
@@ -727,20 +738,23 @@ __device__ void phase_boff(const rt_setup_arg_t* a) {
 }
 
 // a wave per geometry primitive: its (depth bound, index, rectangle) in every
-// block it reaches, at the block's next free slot (order fixed by BSORT)
+// block it reaches, at the block's next free slot (order fixed by BSORT);
+// entries past the capacity bcap are dropped and flagged (status[6])
 __device__ void phase_bfill(const rt_setup_arg_t* a) {
   const int32_t* geometry = vx_ptr<const int32_t>(a->geometry_addr);
   const uint4* vis = vx_ptr<const uint4>(a->vis_addr);
   uint32_t* bcnt = vx_ptr<uint32_t>(a->bcnt_addr);
   const uint2* bidx = vx_ptr<const uint2>(a->bidx_addr);
   uint4* btmp = vx_ptr<uint4>(a->btmp_addr);
-  const uint32_t waves = gridDim.x * (RTS_BLOCK / 64);
+  uint32_t* status = vx_ptr<uint32_t>(a->status_addr);
+  const uint32_t waves = gridDim.x * (RTS_BLOCK / 64), cap = a->bcap;
   for (uint32_t j = blockIdx.x * (RTS_BLOCK / 64) + (threadIdx.x >> 6); j < a->num_geom; j += waves) {
     const uint4 v = vis[geometry[j]];
     if (!v.w) continue;
     for_blocks(a, v, [&](uint32_t lb) {
-      const uint32_t slot = atomicAdd(&bcnt[lb], 1u);
-      btmp[bidx[lb].x + slot] = make_uint4(v.z, j, v.x, v.y);
+      const uint32_t pos = bidx[lb].x + atomicAdd(&bcnt[lb], 1u);
+      if (pos < cap) btmp[pos] = make_uint4(v.z, j, v.x, v.y);
+      else atomicOr(&status[6], 1u);
     });
   }
 }
@@ -754,10 +768,12 @@ __device__ void phase_bsort(const rt_setup_arg_t* a) {
   const uint4* btmp = vx_ptr<const uint4>(a->btmp_addr);
   uint4* blist = vx_ptr<uint4>(a->blist_addr);
   const uint32_t waves = gridDim.x * (RTS_BLOCK / 64), l = lane_id();
-  if (blockIdx.x == 0 && threadIdx.x < RT_BLIST_PAD)  // padding entries (the kernels load pairs ahead)
-    blist[a->blist_entries + threadIdx.x] = make_uint4(0u, RT_BLIST_PAD_LO, RT_BLIST_PAD_HI, RT_VIS_ZMIN_NONE);
+  const uint32_t total = vx_ptr<const uint32_t>(a->status_addr)[2], cap = a->bcap;
+  if (blockIdx.x == 0 && threadIdx.x < RT_BLIST_PAD && total <= cap)  // padding entries (pairs loaded ahead)
+    blist[total + threadIdx.x] = make_uint4(0u, RT_BLIST_PAD_LO, RT_BLIST_PAD_HI, RT_VIS_ZMIN_NONE);
   for (uint32_t lb = blockIdx.x * (RTS_BLOCK / 64) + (threadIdx.x >> 6); lb < a->nblk; lb += waves) {
     const uint2 oc = sload(bidx + lb);
+    if (oc.x + oc.y > cap) continue;  // past the capacity (status[6]): the host refills
     for (uint32_t base = 0; base < oc.y; base += 64) {
       const uint32_t i = base + l;
       const uint4 me = btmp[oc.x + (i < oc.y ? i : 0u)];
@@ -849,57 +865,6 @@ __device__ __noinline__ bool sl_project(const rt_tri_t& r, const float L[3], int
   return F->x0 <= F->x1 && F->y0 <= F->y1;
 }
 
-// separating-axis test of the projected polygon against cell (cx, cy)
-// widened by RT_SLIST_EPS
-__device__ __forceinline__ bool sl_cell_meets(const SlFace& F, int cx, int cy, int N) {
-  if (F.n < 3) return true;
-  const float cw = 2.0f / (float)N;
-  const float rx0 = ((float)cx * cw - 1.0f) - RT_SLIST_EPS, rx1 = ((float)(cx + 1) * cw - 1.0f) + RT_SLIST_EPS;
-  const float ry0 = ((float)cy * cw - 1.0f) - RT_SLIST_EPS, ry1 = ((float)(cy + 1) * cw - 1.0f) + RT_SLIST_EPS;
-  for (int a = 0; a < F.n; ++a) {
-    const int b = a + 1 < F.n ? a + 1 : 0;
-    const float nx = F.pv[b] - F.pv[a], ny = F.pu[a] - F.pu[b];
-    float p0 = 0, p1 = 0;
-    for (int q = 0; q < F.n; ++q) {
-      const float d = nx * F.pu[q] + ny * F.pv[q];
-      if (q == 0 || d < p0) p0 = d;
-      if (q == 0 || d > p1) p1 = d;
-    }
-    const float c0 = nx * rx0 + ny * ry0, c1 = nx * rx1 + ny * ry0;
-    const float c2 = nx * rx0 + ny * ry1, c3 = nx * rx1 + ny * ry1;
-    const float r0 = fminf(fminf(c0, c1), fminf(c2, c3)), r1 = fmaxf(fmaxf(c0, c1), fmaxf(c2, c3));
-    if (p1 < r0 || p0 > r1) return false;
-  }
-  return true;
-}
-
-// a wave per geometry triangle: f(cell) for every cell of its projection on
-// every face (lanes split a face's cell range)
-template <typename Fn>
-__device__ __forceinline__ void sl_for_cells(const rt_setup_arg_t* a, Fn f) {
-  const rt_tri_t* geom = vx_ptr<const rt_tri_t>(a->geom_addr);
-  const uint32_t waves = gridDim.x * (RTS_BLOCK / 64);
-  const int N = (int)a->slist_n;
-  for (uint32_t j = blockIdx.x * (RTS_BLOCK / 64) + (threadIdx.x >> 6); j < a->num_geom; j += waves) {
-    const rt_tri_t r = geom[j];
-    for (int fc = 0; fc < 6; ++fc) {
-      SlFace F;
-      if (!sl_project(r, a->light, fc, N, &F)) continue;
-      const uint32_t w = (uint32_t)(F.x1 - F.x0 + 1), n = w * (uint32_t)(F.y1 - F.y0 + 1);
-      for (uint32_t q = lane_id(); q < n; q += 64) {
-        const int cx = F.x0 + (int)(q % w), cy = F.y0 + (int)(q / w);
-        if (!F.whole && !sl_cell_meets(F, cx, cy, N)) continue;
-        f(j, ((uint32_t)fc * (uint32_t)N + (uint32_t)cy) * (uint32_t)N + (uint32_t)cx);
-      }
-    }
-  }
-}
-
-__device__ void phase_scount(const rt_setup_arg_t* a) {
-  uint32_t* cnt = vx_ptr<uint32_t>(a->bcnt_addr);
-  sl_for_cells(a, [&](uint32_t, uint32_t cell) { atomicAdd(&cnt[cell], 1u); });
-}
-
 // a list entry's sort key: a lower bound of |X - L|^2 over the triangle's
 // points X -- the squared distance from the light L to the triangle's
 // bounding box (corners v0, v0 + e1, v0 + e2); oracle/rt.c sl_key, the same
@@ -916,50 +881,162 @@ __device__ __forceinline__ float sl_key(const rt_tri_t& r, const float L[3]) {
   return s;
 }
 
-__device__ void phase_sfill(const rt_setup_arg_t* a) {
-  uint32_t* cur = vx_ptr<uint32_t>(a->bcnt_addr);
-  const uint2* sidx = vx_ptr<const uint2>(a->bidx_addr);
+// thread per item (geometry triangle j, cube face f), item = 6 j + f: the
+// projection of the triangle on the face (sl_project) as an SPROJ record --
+// [0] the cell rectangle's corner x0 | y0 << 16, [1] its width, [2] the
+// separating axes n (0: every cell of the rectangle -- the polygon reaches
+// the light or has fewer than 3 vertices), [3] the face, then per polygon
+// edge a its axis (nx, ny) and the polygon's extent [p0, p1] along it, the
+// quantities oracle/rt.c sl_cell_meets derives for every cell, computed
+// once -- and the rectangle's cell count -> soff[item]; face 0 also stores
+// the triangle's sort key
+__device__ void phase_sproj(const rt_setup_arg_t* a) {
   const rt_tri_t* geom = vx_ptr<const rt_tri_t>(a->geom_addr);
-  uint32_t* tmp = vx_ptr<uint32_t>(a->btmp_addr);
-  uint32_t* key = tmp + a->blist_entries;  // the entries' sort keys (float bits)
-  sl_for_cells(a, [&](uint32_t j, uint32_t cell) {
+  uint4* rec = vx_ptr<uint4>(a->sproj_addr);
+  uint32_t* soff = vx_ptr<uint32_t>(a->soff_addr);
+  uint32_t* skey = vx_ptr<uint32_t>(a->skey_addr);
+  const int N = (int)a->slist_n;
+  const uint32_t items = 6u * a->num_geom;
+  for (uint32_t it = blockIdx.x * RTS_BLOCK + threadIdx.x; it < items; it += gridDim.x * RTS_BLOCK) {
+    const uint32_t j = it / 6u, f = it % 6u;
+    const rt_tri_t r = geom[j];
+    if (f == 0) skey[j] = __float_as_uint(sl_key(r, a->light));
+    SlFace F;
+    uint32_t cells = 0;
+    if (sl_project(r, a->light, (int)f, N, &F)) {
+      const uint32_t w = (uint32_t)(F.x1 - F.x0 + 1), h = (uint32_t)(F.y1 - F.y0 + 1);
+      const uint32_t n = (F.whole || F.n < 3) ? 0u : (uint32_t)F.n;
+      cells = w * h;
+      uint4* o = rec + (uint64_t)it * (RTS_SPROJ_WORDS / 4);
+      o[0] = make_uint4((uint32_t)F.x0 | ((uint32_t)F.y0 << 16), w, n, f);
+      for (uint32_t e = 0; e < n; ++e) {
+        const uint32_t e1 = e + 1 < n ? e + 1 : 0u;
+        const float nx = F.pv[e1] - F.pv[e], ny = F.pu[e] - F.pu[e1];
+        float p0 = 0, p1 = 0;
+        for (uint32_t q = 0; q < n; ++q) {
+          const float d = nx * F.pu[q] + ny * F.pv[q];
+          if (q == 0 || d < p0) p0 = d;
+          if (q == 0 || d > p1) p1 = d;
+        }
+        o[1 + e] = make_uint4(__float_as_uint(nx), __float_as_uint(ny), __float_as_uint(p0), __float_as_uint(p1));
+      }
+    }
+    soff[it] = cells;
+  }
+}
+
+// (one workgroup) exclusive scan of the items' cell counts, the total
+// candidates -> soff[items]
+__device__ void phase_soscan(const rt_setup_arg_t* a) {
+  const uint32_t items = 6u * a->num_geom;
+  uint32_t* soff = vx_ptr<uint32_t>(a->soff_addr);
+  scan_excl(soff, items, soff + items);
+}
+
+// Every candidate (item, cell of its rectangle), one per thread: q -> the
+// item whose scanned range holds q (binary search of soff), the cell, and
+// the separating-axis test of oracle/rt.c sl_cell_meets against the cell
+// widened by RT_SLIST_EPS (the same float operations: its p0 / p1 are the
+// record's); f(j, cell) for every cell the polygon meets
+template <typename Fn>
+__device__ __forceinline__ void sl_for_candidates(const rt_setup_arg_t* a, Fn f) {
+  const uint4* rec = vx_ptr<const uint4>(a->sproj_addr);
+  const uint32_t* soff = vx_ptr<const uint32_t>(a->soff_addr);
+  const uint32_t items = 6u * a->num_geom, total = soff[items];
+  const uint32_t N = a->slist_n;
+  const float cw = 2.0f / (float)N;
+  for (uint32_t q = blockIdx.x * RTS_BLOCK + threadIdx.x; q < total; q += gridDim.x * RTS_BLOCK) {
+    uint32_t lo = 0, hi = items;  // the last item with soff <= q
+    while (hi - lo > 1) {
+      const uint32_t mid = (lo + hi) >> 1;
+      if (soff[mid] <= q) lo = mid; else hi = mid;
+    }
+    const uint4* o = rec + (uint64_t)lo * (RTS_SPROJ_WORDS / 4);
+    const uint4 h = o[0];
+    const uint32_t li = q - soff[lo];
+    const int cx = (int)(h.x & 0xffffu) + (int)(li % h.y), cy = (int)(h.x >> 16) + (int)(li / h.y);
+    bool meets = true;
+    if (h.z != 0) {
+      const float rx0 = ((float)cx * cw - 1.0f) - RT_SLIST_EPS, rx1 = ((float)(cx + 1) * cw - 1.0f) + RT_SLIST_EPS;
+      const float ry0 = ((float)cy * cw - 1.0f) - RT_SLIST_EPS, ry1 = ((float)(cy + 1) * cw - 1.0f) + RT_SLIST_EPS;
+      for (uint32_t e = 0; e < h.z && meets; ++e) {
+        const uint4 ax = o[1 + e];
+        const float nx = __uint_as_float(ax.x), ny = __uint_as_float(ax.y);
+        const float p0 = __uint_as_float(ax.z), p1 = __uint_as_float(ax.w);
+        const float c0 = nx * rx0 + ny * ry0, c1 = nx * rx1 + ny * ry0;
+        const float c2 = nx * rx0 + ny * ry1, c3 = nx * rx1 + ny * ry1;
+        const float r0 = fminf(fminf(c0, c1), fminf(c2, c3)), r1 = fmaxf(fmaxf(c0, c1), fmaxf(c2, c3));
+        meets = !(p1 < r0 || p0 > r1);
+      }
+    }
+    if (meets) f(lo / 6u, (h.w * N + (uint32_t)cy) * N + (uint32_t)cx);
+  }
+}
+
+__device__ void phase_scount(const rt_setup_arg_t* a) {
+  uint32_t* cnt = vx_ptr<uint32_t>(a->scnt_addr);
+  sl_for_candidates(a, [&](uint32_t, uint32_t cell) { atomicAdd(&cnt[cell], 1u); });
+}
+
+// the entries at their cells' cursors: geometry index, key, cell (stmp);
+// entries past the capacity scap are dropped and flagged (status[7])
+__device__ void phase_sfill(const rt_setup_arg_t* a) {
+  uint32_t* cur = vx_ptr<uint32_t>(a->scnt_addr);
+  const uint2* sidx = vx_ptr<const uint2>(a->sidx_addr);
+  const uint32_t* skey = vx_ptr<const uint32_t>(a->skey_addr);
+  uint32_t* tj = vx_ptr<uint32_t>(a->stmp_addr);
+  uint32_t* status = vx_ptr<uint32_t>(a->status_addr);
+  const uint32_t cap = a->scap;
+  sl_for_candidates(a, [&](uint32_t j, uint32_t cell) {
     const uint32_t pos = sidx[cell].x + atomicAdd(&cur[cell], 1u);
-    tmp[pos] = j;
-    key[pos] = __float_as_uint(sl_key(geom[j], a->light));
+    if (pos < cap) {
+      tj[pos] = j;
+      tj[cap + pos] = skey[j];
+      tj[2u * cap + pos] = cell;
+    } else {
+      atomicOr(&status[7], 1u);
+    }
   });
 }
 
-// a wave per cell: every entry's rank by (sort key, geometry index) -- the
-// nearest-to-the-light bounding boxes first, ties by index (distinct) -- its
-// rt_tri_t copied to that position with the key in the second word's w
-// (rt_tri_t e1.w, 0 in the geometry records), where the scan reads it
+// thread per entry: its rank in its cell by (sort key, geometry index) --
+// the nearest-to-the-light bounding boxes first, ties by index (distinct) --
+// and its rt_tri_t copied to that position with the key in the second
+// word's w (rt_tri_t e1.w, 0 in the geometry records), where the scan reads
+// it; then (block 0) the render arguments' slist_on: the lists are used when
+// they all fit (no overflow, the longest within max_list, the total within
+// max_entries), else the frame's shadow rays walk the BVH
 __device__ void phase_ssort(const rt_setup_arg_t* a) {
-  const uint2* sidx = vx_ptr<const uint2>(a->bidx_addr);
-  const uint32_t* tmp = vx_ptr<const uint32_t>(a->btmp_addr);
-  const uint32_t* key = tmp + a->blist_entries;
+  const uint2* sidx = vx_ptr<const uint2>(a->sidx_addr);
+  const uint32_t* tj = vx_ptr<const uint32_t>(a->stmp_addr);
   const uint4* geom = vx_ptr<const uint4>(a->geom_addr);
   uint4* out = vx_ptr<uint4>(a->slist_addr);
-  const uint32_t waves = gridDim.x * (RTS_BLOCK / 64), l = lane_id();
-  if (blockIdx.x == 0 && threadIdx.x < 3)  // padding record (the kernels load pairs ahead)
-    out[3ull * a->blist_entries + threadIdx.x] = make_uint4(0u, 0u, 0u, 0u);
-  for (uint32_t c = blockIdx.x * (RTS_BLOCK / 64) + (threadIdx.x >> 6); c < a->nblk; c += waves) {
-    const uint2 oc = sload(sidx + c);
-    for (uint32_t base = 0; base < oc.y; base += 64) {
-      const uint32_t i = base + l;
-      const uint32_t me = tmp[oc.x + (i < oc.y ? i : 0u)], mk = key[oc.x + (i < oc.y ? i : 0u)];
-      uint32_t rank = 0;
-      for (uint32_t q = 0; q < oc.y; ++q) {
-        const uint32_t j = sload(tmp + oc.x + q), k = sload(key + oc.x + q);  // keys >= 0: bits order as floats
-        rank += (k < mk || (k == mk && j < me)) ? 1u : 0u;
-      }
-      if (i < oc.y) {
-        out[3ull * (oc.x + rank)] = geom[3ull * me];
-        uint4 w1 = geom[3ull * me + 1];
-        w1.w = mk;
-        out[3ull * (oc.x + rank) + 1] = w1;
-        out[3ull * (oc.x + rank) + 2] = geom[3ull * me + 2];
-      }
+  const uint32_t* status = vx_ptr<const uint32_t>(a->status_addr);
+  const uint32_t cap = a->scap, total = status[5], n = min(total, cap);
+  const uint32_t* tk = tj + cap;
+  const uint32_t* tc = tj + 2u * cap;
+  if (blockIdx.x == 0 && threadIdx.x < 3 && total <= cap)  // padding record (the kernels load pairs ahead)
+    out[3ull * total + threadIdx.x] = make_uint4(0u, 0u, 0u, 0u);
+  if (blockIdx.x == 0 && threadIdx.x == 0 && a->rargs_addr) {
+    const bool fit = status[7] == 0 && status[4] <= a->max_list && total <= a->max_entries;
+    __hip_atomic_store(&vx_ptr<rt_kernel_arg_t>(a->rargs_addr)->slist_on, fit ? 1u : 0u, __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);
+  }
+  for (uint32_t e = blockIdx.x * RTS_BLOCK + threadIdx.x; e < n; e += gridDim.x * RTS_BLOCK) {
+    const uint32_t me = tj[e], mk = tk[e];
+    const uint2 oc = sidx[tc[e]];
+    if (oc.x + oc.y > cap) continue;  // the cell's list overflowed (status[7]): the host refills
+    uint32_t rank = 0;
+    for (uint32_t q = oc.x; q < oc.x + oc.y; ++q) {
+      const uint32_t j = tj[q], k = tk[q];  // keys >= 0: bits order as floats
+      rank += (k < mk || (k == mk && j < me)) ? 1u : 0u;
     }
+    const uint64_t d = 3ull * (oc.x + rank);
+    out[d] = geom[3ull * me];
+    uint4 w1 = geom[3ull * me + 1];
+    w1.w = mk;
+    out[d + 1] = w1;
+    out[d + 2] = geom[3ull * me + 2];
   }
 }
 
@@ -994,12 +1071,11 @@ __device__ void phase_records(const rt_setup_arg_t* a) {
   }
 }
 
-}  // namespace
-
-VX_MAIN(rt_setup_arg_t, arg, RTS_BLOCK) {
-  const uint32_t ph = arg->phases;
+// the sub-phases of `ph` (each independent of the others in the same launch)
+__device__ void run_phases(const rt_setup_arg_t* arg, uint32_t ph) {
   if (ph & RTS_FILL) phase_fill(arg);
   if (ph & RTS_PRIMVIS) phase_primvis(arg);
+  if (ph & RTS_SPROJ) phase_sproj(arg);
   if (ph & RTS_VTRIS) phase_vtris(arg);
   if (ph & RTS_WEIGHT) phase_weight(arg);
   if (ph & RTS_LINK) phase_link(arg);
@@ -1007,17 +1083,48 @@ VX_MAIN(rt_setup_arg_t, arg, RTS_BLOCK) {
   if (ph & RTS_CLIMB) phase_climb(arg);
   if (ph & RTS_COLSUM) phase_colsum(arg);
   if (ph & RTS_HIST) phase_hist(arg);
-  if (ph & RTS_SCAN) phase_scan(arg);
   if (ph & RTS_SCATTER) phase_scatter(arg);
   if (ph & RTS_RECORDS) phase_records(arg);
   if (ph & RTS_BCOUNT) phase_bcount(arg);
-  if (ph & RTS_BSUM) phase_bsum(arg);
-  if (ph & RTS_BSCAN) phase_bscan(arg);
-  if (ph & RTS_BOFF) phase_boff(arg);
+  if (ph & RTS_BSUM) phase_lsum(block_set(arg));
+  if (ph & RTS_BOFF) phase_loff(block_set(arg));
   if (ph & RTS_BFILL) phase_bfill(arg);
   if (ph & RTS_BSORT) phase_bsort(arg);
   if (ph & RTS_SCOUNT) phase_scount(arg);
+  if (ph & RTS_SSUM) phase_lsum(cell_set(arg));
+  if (ph & RTS_SOFF) phase_loff(cell_set(arg));
   if (ph & RTS_SFILL) phase_sfill(arg);
   if (ph & RTS_SSORT) phase_ssort(arg);
+}
+// the one-workgroup sub-phases of `ph` (scans), run by one workgroup
+__device__ void run_scans(const rt_setup_arg_t* arg, uint32_t ph) {
+  if (ph & RTS_SOSCAN) { phase_soscan(arg); __syncthreads(); }
+  if (ph & RTS_BSCAN) { phase_lscan(block_set(arg)); __syncthreads(); }
+  if (ph & RTS_SSCAN) { phase_lscan(cell_set(arg)); __syncthreads(); }
+  if (ph & RTS_SCAN) {
+    scan_excl(vx_ptr<uint32_t>(arg->hist_addr), 256u * arg->nblocks, nullptr);
+    __syncthreads();
+    // local tiles with weight > 0 = items whose digit is below 255 = the
+    // exclusive-scan offset of digit 255 in block 0
+    if (threadIdx.x == 0)
+      vx_ptr<uint32_t>(arg->status_addr)[3] = vx_ptr<const uint32_t>(arg->hist_addr)[255u * arg->nblocks];
+  }
+}
+
+}  // namespace
+
+// A single launch runs `phases`; launch i of a sequence (nseq > 0, launch
+// tag i) runs seq_phases[i] -- the scans, one-workgroup phases, by
+// workgroup 0 in either case.  A sequence's dependent steps are launches
+// queued back to back on the driver's stream: the launch boundary makes
+// each step's stores visible to the next (per-XCD L2s are not coherent
+// within a launch), with no host round trip and no device-side counter.
+// Registers capped for 4 waves per SIMD (PRIMVIS alone would take 184 VGPRs;
+// at 120 nothing spills).
+VX_MAIN_OCC(rt_setup_arg_t, arg, RTS_BLOCK, 4) {
+  const uint32_t ph = arg->nseq == 0 ? arg->phases
+                      : vx_launch_tag < RTS_MAX_SEQ ? arg->seq_phases[vx_launch_tag] : 0u;
+  run_phases(arg, ph);
+  if (blockIdx.x == 0) run_scans(arg, ph);
   return 0;
 }

@@ -640,10 +640,14 @@ __device__ __forceinline__ bool occluded_packet(const Scene& S, const Ray& r, bo
 
 // A shadow segment's any-hit over its light-space cell list (rt_common.h;
 // oracle/rt.c sl_occluded): the cell of its direction from the light, then
-// the cell's triangles in ascending pid order until the first occluder
-// (t in (0, 1), the primary winner `skip` excluded).  Per lane: a lane's
-// chain is its own list, not the wave's union of BVH paths; the records are
-// copies in list order, loaded two ahead.  Tests count per lane.
+// the cell's triangles in the list's (key, geometry index) order -- nearest
+// to the light first, key = squared distance from the light to the
+// triangle's bounding box (in e1.w) -- until the first occluder (t in
+// (0, 1), the primary winner `skip` excluded) or the first record whose key
+// exceeds the segment's squared length (x 1.001: no later record can reach
+// the segment either).  Per lane: a lane's chain is its own list, not the
+// wave's union of BVH paths; the records are copies in list order, two per
+// load round.  Tests count per lane.
 __device__ __forceinline__ uint32_t slist_cell(const Ray& s, uint32_t N) {
   const float u0 = -s.d[0], u1 = -s.d[1], u2 = -s.d[2];
   int k = 0;

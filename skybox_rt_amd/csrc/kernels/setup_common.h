@@ -54,15 +54,33 @@
 #define RTS_BFILL    0x10000u // unsorted (zmin, k, rx, ry) per (block, primitive) -> btmp
 #define RTS_BSORT    0x20000u // wave per block: rank + suffix union -> blist (+2 pads)
 #define RTS_BLOCKS_PER_PART 1024u  // blocks summed per bpart word (4 per thread)
-// light-space shadow lists (rt_common.h): a wave per geometry triangle
-// visits the cells of its projection on each cube face; BSUM / BSCAN / BOFF
-// then run over the cells (bcnt = the cell counts, bidx = sidx)
-#define RTS_SCOUNT   0x40000u // atomic count per cell
-#define RTS_SFILL    0x80000u // geometry index per (cell, triangle) -> btmp (u32), unsorted
-#define RTS_SSORT    0x100000u // wave per cell: rank by geometry index -> slist (rt_tri_t copies, +1 pad)
+// light-space shadow lists (rt_common.h): SPROJ projects every (geometry
+// triangle, cube face) pair once -- the clipped polygon's cell rectangle and
+// its separating axes, precomputed -- and counts the rectangle's cells; the
+// candidates (item, cell of its rectangle) are then dealt one per thread
+// (binary search of the scanned counts), so a large projection is spread
+// over many waves instead of one.  SSUM / SSCAN / SOFF are BSUM / BSCAN /
+// BOFF over the cells.
+#define RTS_SCOUNT   0x40000u // thread per candidate: separating-axis test, atomic count per cell
+#define RTS_SFILL    0x80000u // thread per candidate: (geometry index, key, cell) at the cell's cursor
+#define RTS_SSORT    0x100000u // thread per entry: rank in its cell by (key, geometry index) -> slist
+                               // (rt_tri_t copies, the key -- squared light-to-bounding-box distance --
+                               // in e1.w; +1 pad); then the render arguments' slist fields
+#define RTS_SPROJ    0x200000u // thread per (triangle, face): projection record, cell count, key
+#define RTS_SOSCAN   0x400000u // exclusive scan of the per-item cell counts (one workgroup)
+#define RTS_SSUM     0x800000u // BSUM over the cells
+#define RTS_SSCAN    0x1000000u // BSCAN over the cells
+#define RTS_SOFF     0x2000000u // BOFF over the cells -> sidx
 
-// status words (u32 [4]): [0] malformed-input flags (RTS_ERR_*), [1] the
-// longest block list, [2] list entries in total, [3] spare
+// status words (u32 [RTS_STATUS_WORDS]): [0] malformed-input flags
+// (RTS_ERR_*), [1] the longest block list, [2] block-list entries in total,
+// [3] local tiles with weight > 0 (the scan of the tile order), [4] the
+// longest cell list, [5] cell-list entries in total, [6] block-list entries
+// beyond bcap (nonzero: the host refills at the exact size), [7] cell-list
+// entries beyond scap
+#define RTS_STATUS_WORDS 8
+#define RTS_SPROJ_WORDS 32u  // u32 per SPROJ record: header uint4 + 7 separating axes (nx, ny, p0, p1)
+#define RTS_MAX_SEQ 12
 #define RTS_ERR_REF   0x1u   // a tree reference out of range
 #define RTS_ERR_PID   0x2u   // a leaf record's pid out of range
 #define RTS_ERR_CLIMB 0x4u   // a climb longer than 64 levels
@@ -109,6 +127,25 @@ typedef struct {
   uint32_t nblk, nbpart, blist_entries;  // local 8x8 blocks, bpart words, list entries (BSORT)
   float light[3];          // shadow lists: the point light (clip x, y, w)
   uint32_t slist_n;        // shadow lists: cells per cube-face side
-  uint64_t slist_addr;     // shadow lists: rt_tri_t [entries + 1]
+  uint64_t slist_addr;     // shadow lists: rt_tri_t [scap + 1]
+  // shadow lists (the cell-level arrays, apart from the block lists' so one
+  // launch can build both)
+  uint64_t scnt_addr;      // u32 [ncells]: entries per cell (then the fill cursors)
+  uint64_t spart_addr;     // u32 [ncpart]: per RTS_BLOCKS_PER_PART cells their sum, then its scan
+  uint64_t sidx_addr;      // uint32[2] [ncells]: first entry, count
+  uint64_t sproj_addr;     // u32 [num_geom * 6][RTS_SPROJ_WORDS]: SPROJ records
+  uint64_t soff_addr;      // u32 [num_geom * 6 + 1]: cells per item, then their exclusive scan + total
+  uint64_t skey_addr;      // u32 [num_geom]: sl_key of each triangle (float bits)
+  uint64_t stmp_addr;      // u32 [3][scap]: unsorted entries -- geometry index, key, cell
+  uint64_t rargs_addr;     // the render arguments (rt_kernel_arg_t): SSORT writes their slist fields
+  uint32_t ncells, ncpart, scap, bcap;  // cells (6 N^2), spart words, entry capacities
+  uint32_t max_list;       // lists longer than this are not used (RT_BLIST_MAX_LIST)
+  uint32_t max_entries;    // nor more entries in total than this
+  // launch sequences: the host enqueues nseq launches of this one argument
+  // block back to back (no host wait between them), launch i with launch
+  // tag i (vx_hip_set_launch_tag: the entry's kernel argument); launch i
+  // runs seq_phases[i] -- its one-workgroup phases (the scans) by workgroup 0
+  uint32_t nseq, pad1;
+  uint32_t seq_phases[RTS_MAX_SEQ];
 
 } rt_setup_arg_t;

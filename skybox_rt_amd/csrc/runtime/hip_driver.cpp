@@ -154,6 +154,9 @@ class vx_device {
       if (ev_start_[i]) (void)hipEventDestroy(ev_start_[i]);
       if (ev_stop_[i]) (void)hipEventDestroy(ev_stop_[i]);
     }
+    for (int i = 0; i < kStageSlots; ++i)
+      if (stage_ev_[i]) (void)hipEventDestroy(stage_ev_[i]);
+    if (stage_) (void)hipHostFree(stage_);
     if (stream_) (void)hipStreamDestroy(stream_);
     if (arena_) (void)hipFree(arena_);
   }
@@ -181,6 +184,9 @@ class vx_device {
       HIP_CHECK(hipEventCreate(&ev_start_[i]));
       HIP_CHECK(hipEventCreate(&ev_stop_[i]));
     }
+    HIP_CHECK(hipHostMalloc((void**)&stage_, (size_t)kStageSlots * kStageSlot, hipHostMallocDefault));
+    for (int i = 0; i < kStageSlots; ++i)
+      HIP_CHECK(hipEventCreateWithFlags(&stage_ev_[i], hipEventDisableTiming));
     const uint64_t qd = env_u64("VX_HIP_QUEUE_DEPTH", 2);
     depth_ = qd < 1 ? 1 : qd > 16 ? 16 : (int)qd;
     const uint64_t te = env_u64("VX_HIP_TIME_EVERY", 4);
@@ -263,6 +269,27 @@ class vx_device {
     }
     return 0;
   }
+  // stream-ordered upload (vx_hip_copy_to_dev_async): the bytes are staged
+  // in a pinned slot at once and copied when the driver's stream reaches
+  // the copy, so the host does not wait for queued runs; a slot is reused
+  // once its copy has completed (its event).  Larger copies, and copies into
+  // a kernel image (whose host shadow must stay coherent), are synchronous.
+  int upload_async(uint64_t addr, const void* src, uint64_t size) {
+    if (addr + size > arena_size_) return -1;
+    if (size == 0) return 0;
+    bool image = false;
+    for (auto& kv : shadow_)
+      image |= addr < kv.first + kv.second.size() && kv.first < addr + size;
+    if (size > kStageSlot || image) return upload(addr, src, size);
+    const int slot = (int)(stage_next_++ % kStageSlots);
+    if (stage_busy_[slot]) HIP_CHECK(hipEventSynchronize(stage_ev_[slot]));
+    uint8_t* st = stage_ + (size_t)slot * kStageSlot;
+    std::memcpy(st, src, size);
+    HIP_CHECK(hipMemcpyAsync(arena_ + addr, st, size, hipMemcpyHostToDevice, stream_));
+    HIP_CHECK(hipEventRecord(stage_ev_[slot], stream_));
+    stage_busy_[slot] = true;
+    return 0;
+  }
   int download(void* dst, uint64_t addr, uint64_t size) {
     if (addr + size > arena_size_) return -1;
     if (size == 0) return 0;
@@ -311,6 +338,11 @@ class vx_device {
       HIP_CHECK(hipMemcpyHtoDAsync(m->dcrs, m->dcrs_sent, sizeof(dcrs_), stream_));
       m->dcrs_set = true;
     }
+    // the entry's one kernel argument (vx_spawn.h VX_MAIN: vx_launch_tag),
+    // copied into the dispatch's kernarg segment by the launch call
+    uint32_t tag = launch_tag_;
+    launch_tag_ = 0;
+    void* kparams[1] = {&tag};
     const int slot = (int)(issued_ % kMaxQueue);
     // a run is timed (events) when it starts on an idle queue -- every run of
     // a start + wait loop -- and then every time_every_-th run: an event
@@ -334,21 +366,21 @@ class vx_device {
     if (last) group_n_ = 1;  // a group covers the launches it was declared for
     if (!timed) {
       HIP_CHECK(hipExtModuleLaunchKernel(m->entry, m->grid * m->block, 1, 1, m->block, 1, 1, 0,
-                                         stream_, nullptr, nullptr, nullptr, nullptr, 0));
+                                         stream_, kparams, nullptr, nullptr, nullptr, 0));
     } else if (launch_mode_ == 2) {
       HIP_CHECK(hipExtModuleLaunchKernel(m->entry, m->grid * m->block, 1, 1, m->block, 1, 1, 0,
-                                         stream_, nullptr, nullptr, nullptr, nullptr, 0));
+                                         stream_, kparams, nullptr, nullptr, nullptr, 0));
     } else if (launch_mode_ == 1) {
       // the dispatch packet itself carries the start/stop timestamps: no
       // separate event packets between back-to-back frames
       HIP_CHECK(hipExtModuleLaunchKernel(m->entry, m->grid * m->block, 1, 1, m->block, 1, 1, 0,
-                                         stream_, nullptr, nullptr,
+                                         stream_, kparams, nullptr,
                                          first ? ev_start_[slot] : nullptr,
                                          last ? ev_stop_[slot] : nullptr, 0));
     } else {
       if (first) HIP_CHECK(hipEventRecord(ev_start_[slot], stream_));
       HIP_CHECK(hipModuleLaunchKernel(m->entry, m->grid, 1, 1, m->block, 1, 1, 0, stream_,
-                                      nullptr, nullptr));
+                                      kparams, nullptr));
       if (last) HIP_CHECK(hipEventRecord(ev_stop_[slot], stream_));
     }
     ++issued_;
@@ -490,6 +522,7 @@ class vx_device {
     group_n_ = n;
     return 0;
   }
+  void set_launch_tag(uint32_t tag) { launch_tag_ = tag; }  // the next start()'s kernel argument
   bool counters() const { return counters_ || counters_env_; }
   void* mem_ptr(uint64_t addr) { return arena_ + addr; }
   hipStream_t stream() const { return stream_; }
@@ -584,6 +617,14 @@ class vx_device {
   std::map<uint64_t, int> acl_;
   std::map<uint64_t, std::vector<uint8_t>> shadow_;
   std::map<uint64_t, Module> modules_;
+  // pinned staging slots of upload_async
+  static constexpr int kStageSlots = 64;
+  static constexpr uint64_t kStageSlot = 4096;
+  uint8_t* stage_ = nullptr;
+  hipEvent_t stage_ev_[kStageSlots] = {};
+  bool stage_busy_[kStageSlots] = {};
+  uint64_t stage_next_ = 0;
+  uint32_t launch_tag_ = 0;
   std::map<uint64_t, uint64_t> image_key_;  // image address -> module key
   hipStream_t stream_ = nullptr;
   static constexpr int kMaxQueue = 64;  // >= (depth_ + time_every_) * group_n_
@@ -769,6 +810,18 @@ __attribute__((visibility("default"))) int vx_hip_set_timing(vx_device_h hdevice
 __attribute__((visibility("default"))) int vx_hip_launch_group(vx_device_h hdevice, uint32_t n) {
   if (hdevice == nullptr) return -1;
   return ((vx_device*)hdevice)->launch_group(n);
+}
+__attribute__((visibility("default"))) int vx_hip_copy_to_dev_async(vx_buffer_h hbuf, const void* src,
+                                                                    uint64_t off, uint64_t size) {
+  if (hbuf == nullptr || (src == nullptr && size != 0)) return -1;
+  auto* b = (vx_buffer*)hbuf;
+  if (off + size > b->size) return -1;
+  return b->device->upload_async(b->addr + off, src, size);
+}
+__attribute__((visibility("default"))) int vx_hip_set_launch_tag(vx_device_h hdevice, uint32_t tag) {
+  if (hdevice == nullptr) return -1;
+  ((vx_device*)hdevice)->set_launch_tag(tag);
+  return 0;
 }
 __attribute__((visibility("default"))) int vx_hip_device_id(vx_device_h hdevice, int* id) {
   if (hdevice == nullptr || id == nullptr) return -1;

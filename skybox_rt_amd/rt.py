@@ -65,10 +65,10 @@ class SetupStats(C.Structure):
     _fields_ = [("device", C.c_uint32), ("launches", C.c_uint32), ("heavy_tiles", C.c_uint32),
                 ("blist_blocks", C.c_uint32), ("setup_ms", C.c_double), ("configure_ms", C.c_double),
                 ("blist_entries", C.c_uint64), ("blist_max", C.c_uint32), ("slist_on", C.c_uint32),
-                ("slist_entries", C.c_uint64), ("path_queue", C.c_uint32), ("pad", C.c_uint32)]
+                ("slist_entries", C.c_uint64), ("path_queue", C.c_uint32), ("slist_built", C.c_uint32)]
 
     def as_dict(self):
-        return {n: getattr(self, n) for n, _ in self._fields_ if n != "pad"}
+        return {n: getattr(self, n) for n, _ in self._fields_}
 
 
 class RenderParams(C.Structure):
@@ -139,6 +139,7 @@ def lib():
             "rt_device_caps": [vp, C.POINTER(u64)],
             "rt_render_gather": [vp, vp, vp],
             "rt_renderer_setup_stats": [vp, C.POINTER(SetupStats)],
+            "rt_renderer_set_light": [vp, C.POINTER(C.c_float)],
             "rt_renderer_export_records": [vp, u32, vp, u64, C.POINTER(u64)],
         }
         for name, argtypes in sig.items():
@@ -287,6 +288,15 @@ class Renderer:
                      and (not self.gpu_bvh or self.gpu_bvh4))
         # BVH4 node steps read 64-B binary16 nodes (rt_node4h_t) when the scene has them
         self.bvh4_f16 = self.bvh4 and (self.gpu_bvh or bool(self.scene.info()["bvh4_f16"]))
+
+    def set_light(self, light) -> None:
+        """Move the point light (clip x, y, w) of the current configuration:
+        the light and -- when the configuration uses them -- its light-space
+        shadow lists are rebuilt on the device, queued behind the frames
+        already started (rt_renderer_set_light: no host wait)."""
+        arr = (C.c_float * 3)(*[float(np.float32(x)) for x in light])
+        _check(lib().rt_renderer_set_light(self._h, arr), "rt_renderer_set_light")
+        self.params.light[:] = [float(np.float32(x)) for x in light]
 
     def setup_stats(self) -> dict:
         """How the last configure built its records (device / host, launches,
