@@ -108,6 +108,8 @@ typedef struct {
   uint32_t path_queue;              /* path trace in two kernels (pt_primary + pt_queue): the
                                        primary pass runs 8x8 blocks everywhere (no 32-pixel
                                        waves in geometry tiles) */
+  uint32_t split_log;               /* path trace: 2^split_log pixels per wave in the geometry
+                                       tiles (the renderer's split_log; 0 = 5, 32 pixels) */
 } orc_rt_params_t;
 
 #define ORC_RT_SHADOWS 0x1u

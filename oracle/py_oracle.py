@@ -53,7 +53,7 @@ class RtParamsC(C.Structure):
                 ("bounces", C.c_uint32), ("seed", C.c_uint32), ("nthreads", C.c_uint32),
                 ("row_begin", C.c_uint32), ("row_end", C.c_uint32), ("row_step", C.c_uint32),
                 ("vis_per_lane", C.c_uint32), ("vis_lists", C.c_uint32),
-                ("shadow_lists", C.c_uint32), ("path_queue", C.c_uint32)]
+                ("shadow_lists", C.c_uint32), ("path_queue", C.c_uint32), ("split_log", C.c_uint32)]
 
 
 class RtCountersC(C.Structure):
@@ -233,7 +233,7 @@ def shadow_lists(oscene: OracleScene, light=(0.0, 60.0, 80.0)):
 def rt_params(width, height, shadows=True, light=(0.0, 60.0, 80.0), nthreads=1,
               clear_color=CLEAR_COLOR, row_begin=0, row_end=0, row_step=0,
               path=False, bounces=4, seed=PT_SEED, vis_per_lane=False, vis_lists=None,
-              shadow_lists=None, path_queue=None):
+              shadow_lists=None, path_queue=None, split_log=0):
     p = RtParamsC()
     p.vis_per_lane = 1 if vis_per_lane else 0
     # the product resolves primary visibility from per-block candidate lists
@@ -246,6 +246,8 @@ def rt_params(width, height, shadows=True, light=(0.0, 60.0, 80.0), nthreads=1,
     # primary pass counts per 8x8 block everywhere); default the one-kernel
     # pt_kernel (32-pixel waves in geometry tiles)
     p.path_queue = int(bool(path_queue))
+    # path trace: pixels per wave in the geometry tiles, 2^split_log (0: 32)
+    p.split_log = int(split_log)
     p.width, p.height = width, height
     p.flags = (RT_SHADOWS if shadows else 0) | (RT_PATH if path else 0)
     p.bounces, p.seed = bounces, seed

@@ -548,15 +548,22 @@ static void vis_scan_block(const rt_ctx_t* c, int n, const uint32_t* px, const u
 
 /* the primary pre-pass over one row of 32x32 tiles: every wave's packet
  * (8x8 blocks, or 8x4 halves in split tiles, the kernels' task_map) */
-/* the in-image pixels of wave `wv` of tile (tx, ty): an 8x8 block, or an 8x4
- * half in a split tile (the kernels' task_map); returns their number */
+/* pixels per wave in a split tile: 2^split_log (the kernels' task_map) */
+static uint32_t split_pl(const rt_ctx_t* c) { return c->p.split_log ? c->p.split_log : 5u; }
+static int tile_waves(const rt_ctx_t* c, int split) { return split ? (int)(1024u >> split_pl(c)) : 16; }
+
+/* the in-image pixels of wave `wv` of tile (tx, ty): an 8x8 block, or in a
+ * split tile the 2^split_log-pixel part of one (8x4 halves by default; the
+ * kernels' task_map); returns their number */
 static int wave_pixels(const rt_ctx_t* c, uint32_t tx, uint32_t ty, int split, int wv, uint32_t* px,
                        uint32_t* py, int32_t* idx) {
   const uint32_t W = c->p.width, H = c->p.height;
-  const int lanes = split ? 32 : 64;
+  const uint32_t pl = split_pl(c), sub = 6u - pl;
+  const int lanes = split ? (1 << pl) : 64;
   int n = 0;
   for (int ln = 0; ln < lanes; ++ln) {
-    const uint32_t ti = split ? (((uint32_t)wv >> 1) << 6) + (uint32_t)ln + (((uint32_t)wv & 1u) << 5)
+    const uint32_t ti = split ? (((uint32_t)wv >> sub) << 6) + (((uint32_t)wv & ((1u << sub) - 1u)) << pl) +
+                                    (uint32_t)ln
                               : ((uint32_t)wv << 6) + (uint32_t)ln;
     const uint32_t blk = ti >> 6, l = ti & 63u;
     const uint32_t x = tx * 32 + (blk & 3u) * 8 + (l & 7u), y = ty * 32 + (blk >> 2) * 8 + (l >> 3);
@@ -575,7 +582,7 @@ static void vis_tile_row(rt_ctx_t* c, uint32_t ty, orc_rt_counters_t* k) {
   int32_t idx[PK_LANES];
   for (uint32_t tx = 0; tx < ntx; ++tx) {
     const int split = tile_split(c, tx, ty);
-    const int waves = split ? 32 : 16;
+    const int waves = tile_waves(c, split);
     for (int wv = 0; wv < waves; ++wv) {
       const int n = wave_pixels(c, tx, ty, split, wv, px, py, idx);
       if (n == 0) continue;
@@ -1121,7 +1128,7 @@ static uint64_t layer_waves(const rt_ctx_t* c) {
   for (uint32_t ty = 0; ty < nty; ++ty)
     for (uint32_t tx = 0; tx < ntx; ++tx) {
       const int split = tile_split(c, tx, ty);
-      for (int wv = 0; wv < (split ? 32 : 16); ++wv) {
+      for (int wv = 0; wv < tile_waves(c, split); ++wv) {
         const int n = wave_pixels(c, tx, ty, split, wv, px, py, idx);
         uint32_t m = 0;
         for (int i = 0; i < n; ++i) m = c->lcnt[idx[i]] > m ? c->lcnt[idx[i]] : m;

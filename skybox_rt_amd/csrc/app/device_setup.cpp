@@ -142,10 +142,19 @@ int run_seq(rt_renderer* r, rt_setup_arg_t& g, const Seq& q, uint32_t* launches)
   if (q.n == 0) return 0;
   // a step's scans (one workgroup) read what the whole grid wrote in that
   // step: they run as a launch of their own right behind it
+  // (env RT_SETUP_SPLIT=1, profiling: every sub-phase a launch of its own,
+  // in the same order -- rocprofv3 then times each; RT_SETUP_TRACE names them)
+  static const bool split = std::getenv("RT_SETUP_SPLIT") && std::atoi(std::getenv("RT_SETUP_SPLIT")) == 1;
   Seq x;
   for (uint32_t i = 0; i < q.n; ++i) {
-    x.add(q.ph[i]);
-    x.add(q.last[i]);
+    for (const uint32_t ph : {q.ph[i], q.last[i]}) {
+      if (!split) {
+        x.add(ph);
+        continue;
+      }
+      for (uint32_t b = 1; b != 0 && b <= ph; b <<= 1)
+        if (ph & b) x.add(b);
+    }
   }
   if (x.n > RTS_MAX_SEQ) return set_error("setup sequence too long");
   g.phases = 0;

@@ -881,6 +881,7 @@ int rt_renderer_configure(rt_renderer_h r, const rt_render_params_t* p) {
   a.order_addr = 0;
   a.split_tiles = 0;
   a.split_log = 5;
+  a.quad_tiles = 0;
   const bool order_on = !raster && r->local_tiles > 0 &&
                         !(std::getenv("RT_TILE_ORDER") && std::atoi(std::getenv("RT_TILE_ORDER")) == 0);
   bool use_bvh4 = !(p->flags & RT_RENDER_BVH2) && (!r->gpu_bvh || r->gpu_bvh4);
@@ -969,11 +970,17 @@ int rt_renderer_configure(rt_renderer_h r, const rt_render_params_t* p) {
     if (const char* e = std::getenv("RT_SPLIT_LOG")) a.split_log = std::min(6u, std::max(3u, (uint32_t)std::atoi(e)));
     const uint32_t extra = RT_TILE_PIXELS * ((64u >> a.split_log) - 1u);  // per split tile
     a.num_tasks += split * extra;
+    // the heaviest split tiles at 16 pixels per wave (a path on four lanes)
+    a.quad_tiles = 0;
+    if (const char* e = std::getenv("RT_QUAD_TILES")) a.quad_tiles = std::min<uint32_t>((uint32_t)std::atoi(e), split);
+    const uint32_t qextra = RT_TILE_PIXELS * 3u - extra;  // per quad tile beyond a split tile's
+    a.num_tasks += a.quad_tiles * qextra;
     // timing probe only (the frame is incomplete): render just the first n
     // tiles of the work order, e.g. the geometry tiles without the background
     if (const char* e = std::getenv("RT_TILE_LIMIT")) {
       const uint32_t n = std::min<uint32_t>((uint32_t)std::atoi(e), r->local_tiles);
-      a.num_tasks = std::min(a.num_tasks, n * RT_TILE_PIXELS + std::min(n, split) * extra);
+      a.num_tasks = std::min(a.num_tasks, n * RT_TILE_PIXELS + std::min(n, split) * extra +
+                                              std::min(n, a.quad_tiles) * qextra);
     }
   }
   uint64_t args_addr = 0;

@@ -51,6 +51,9 @@
 #ifndef PT_PAIR
 #define PT_PAIR 1        // 0: no paired-vertex code (the shadow lists never pair)
 #endif
+#ifndef PT_QUAD
+#define PT_QUAD 0        // 16-pixel waves (split_log 4) with the shadow lists: four lanes per path
+#endif
 #define PT_SKY 0.25f     // radiance of an escaped bounce ray (oracle ORC_PT_SKY)
 #define PT_TRIES 8u      // disk rejection-sampling attempts (ORC_PT_TRIES)
 
@@ -258,15 +261,18 @@ __device__ __forceinline__ void path_hit(const Scene& S, PathState& st, const fl
 // One path vertex for an active lane: direct light through a shadow ray,
 // then (v < bounces) the bounce; returns whether the path continues (st then
 // describes the next vertex), else the pixel is final.  Every lane of the
-// wave calls it; `act` masks the work.  COOP: the lane pairs of a 32-pixel
-// wave (lane l and l ^ 32 hold the same path, `hi` = the upper lane) trace
+// wave calls it; `act` masks the work.  CO 1: the lane pairs of a 32-pixel
+// wave (lane l and l ^ 32 hold the same path, role 1 = the upper lane) trace
 // the shadow ray on its list and the bounce ray together (trace_coop,
-// occluded_list_coop); both lanes compute the rest, the lower one counts.
-template <bool COOP>
+// occluded_list_coop); CO 2: the quads of a 16-pixel wave (lanes 4p ..
+// 4p + 3, role = lane & 3; trace_quad, occluded_list_quad).  Every lane of
+// the group computes the rest, role 0 counts.
+template <int CO>
 __device__ __forceinline__ bool path_step(const Scene& S, int32_t* stack, PathState& st, uint32_t v,
-                                          bool act, Counters& cnt, bool hi = false) {
+                                          bool act, Counters& cnt, uint32_t role = 0u) {
   const bool tie_high = (S.flags & RT_FLAG_TIE_HIGH) != 0;
-  const uint32_t one = hi ? 0u : 1u;  // per-path counters: the lower lane of a pair
+  const bool hi = role != 0u;
+  const uint32_t one = hi ? 0u : 1u;  // per-path counters: the group's first lane
   float v0[3], e1[3], e2[3], nrm[3], P[3];
   load_tri(S, act ? st.pid : 0, v0, e1, e2);
   tri_normal(e1, e2, st.d, nrm);
@@ -284,12 +290,13 @@ __device__ __forceinline__ bool path_step(const Scene& S, int32_t* stack, PathSt
   float ts;
   const uint64_t c0 = PT_CYC();
   // the light-space lists when built (occluded_list), else the BVH
-  const bool occ = COOP ? occluded_list_coop(S, s, act, st.pid, hi, cnt)
+  const bool occ = CO == 2 ? occluded_list_quad(S, s, act, st.pid, role, cnt)
+                 : CO == 1 ? occluded_list_coop(S, s, act, st.pid, hi, cnt)
                  : S.slist_on ? occluded_list(S, s, act, st.pid, cnt)
                               : act && trace<true>(S, s, 0.0f, 1.0f, st.pid, tie_high, &ts, stack, cnt) >= 0;
   cnt.occluded += occ ? one : 0u;
   const uint64_t c1 = PT_CYC();
-  if (COOP) {
+  if (CO) {
     PT_ACC(4, c1 - c0);  // cycles in the shadow-list scan
     PT_ACC(5, 1);        // vertex steps
   }
@@ -311,8 +318,9 @@ __device__ __forceinline__ bool path_step(const Scene& S, int32_t* stack, PathSt
     bounce_dir(nrm, pt_key(S.seed, y * S.width + x, v), b.d);  // keyed by pixel, not task
     ray_setup(b);
     cnt.bounce += one;
-    np = COOP ? trace_coop(S, b, st.pid, tie_high, &nt, stack, hi, cnt)
-              : trace<false>(S, b, 0.0f, INFINITY, st.pid, tie_high, &nt, stack, cnt);
+    np = CO == 2 ? trace_quad(S, b, st.pid, tie_high, &nt, stack, role, cnt)
+         : CO == 1 ? trace_coop(S, b, st.pid, tie_high, &nt, stack, hi, cnt)
+                   : trace<false>(S, b, 0.0f, INFINITY, st.pid, tie_high, &nt, stack, cnt);
     if (np < 0) {
 #pragma unroll
       for (int k = 0; k < 3; ++k) st.L[k] = fmaf(st.T[k], PT_SKY, st.L[k]);
@@ -321,7 +329,7 @@ __device__ __forceinline__ bool path_step(const Scene& S, int32_t* stack, PathSt
   }
   const uint64_t c2 = PT_CYC();
   if (alive) path_hit(S, st, P, b, np, nt, cnt, !hi);
-  if (COOP) {
+  if (CO) {
     PT_ACC(2, c2 - c1);           // cycles in the bounce walk (and its setup)
     PT_ACC(6, PT_CYC() - c2);     // cycles shading the bounce hit
   }
@@ -463,7 +471,7 @@ __device__ __forceinline__ void vertex(const Scene& S, PtLds& L, int qi, uint32_
     st.L[k] = q.L[k][j];
   }
   int32_t* stack = &L.stack[threadIdx.x >> 6][0][lane_id()];
-  const bool alive = path_step<false>(S, stack, st, v, act, cnt);
+  const bool alive = path_step<0>(S, stack, st, v, act, cnt);
   enqueue(L, qi ^ 1, alive, st.task, st.alpha, st.pid, st.t, st.o, st.d, st.T, st.L);
   if (act && !alive) store_path_pixel(S, st);
 }
@@ -523,7 +531,7 @@ __device__ __forceinline__ void queued_path(const vx_task_t& task, const Scene& 
     st.d[k] = r.d[k];
     st.L[k] = 0.0f;
   }
-  for (uint32_t v = 0; path_step<false>(S, stack, st, v, true, cnt); ++v) {
+  for (uint32_t v = 0; path_step<0>(S, stack, st, v, true, cnt); ++v) {
   }
   store_path_pixel(S, st);
 }
@@ -545,6 +553,8 @@ __device__ __forceinline__ void lane_path(const vx_task_t& task, const Scene& S,
   const bool split = __ballot(1) == ~0ull && (__ballot(in) >> 32) == 0;
   const bool pair = PT_PAIR && !S.slist_on && split;
   const bool coop = PT_COOP && S.slist_on && split && (RT_ONLY_BVH4H || (S.flags & RT_FLAG_BVH4H));
+  // a 16-pixel wave (split tiles at split_log 4): quads of lanes per path
+  const bool quad = PT_QUAD && coop && (__ballot(in) >> 16) == 0;
   cnt.primary += in;
   const bool tie_high = (S.flags & RT_FLAG_TIE_HIGH) != 0;
   // primary visibility: the raster's winner at this pixel (trace_primary)
@@ -558,6 +568,33 @@ __device__ __forceinline__ void lane_path(const vx_task_t& task, const Scene& S,
   const bool path = hit >= 0 && secondary_ok(th);  // a path starts at the winner's plane
   if (!path && in) store_pixel(S, t, x, y, color);
   if (!path && !pair && !coop) return;
+  if (quad) {
+    // lanes 4p .. 4p + 3 take pixel p's path (lane p); all four trace it,
+    // lane 4p stores it
+    const uint32_t src = lane_id() >> 2, j = lane_id() & 3u;
+    bool act = __shfl((int)path, (int)src) != 0;
+    const bool own = act && j == 0u;
+    PathState q;
+    q.task = (uint32_t)__shfl((int)t, (int)src);
+    q.alpha = (uint32_t)__shfl((int)(color & 0xff000000u), (int)src);
+    q.pid = __shfl(hit, (int)src);
+    q.t = __shfl(th, (int)src);
+    const float k255 = 1.0f / 255.0f;
+    const uint32_t qc = (uint32_t)__shfl((int)color, (int)src);
+    q.T[0] = (float)((qc >> 16) & 0xffu) * k255;
+    q.T[1] = (float)((qc >> 8) & 0xffu) * k255;
+    q.T[2] = (float)(qc & 0xffu) * k255;
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+      q.o[k] = __shfl(r.o[k], (int)src);
+      q.d[k] = __shfl(r.d[k], (int)src);
+      q.L[k] = 0.0f;
+    }
+    int32_t* qstack = stack - j;  // the quad's stack: lane 4p's column
+    for (uint32_t v = 0; act; ++v) act = path_step<2>(S, qstack, q, v, act, cnt, j);
+    if (own) store_path_pixel(S, q);
+    return;
+  }
   const float k255 = 1.0f / 255.0f;
   PathState st;
   st.task = t;
@@ -597,11 +634,11 @@ __device__ __forceinline__ void lane_path(const vx_task_t& task, const Scene& S,
       st.T[k] = xlowf(st.T[k]);
     }
     int32_t* pstack = hi ? stack - 32 : stack;  // the pair's stack: lane l's column
-    for (uint32_t v = 0; act; ++v) act = path_step<true>(S, pstack, st, v, act, cnt, hi);
+    for (uint32_t v = 0; act; ++v) act = path_step<1>(S, pstack, st, v, act, cnt, hi ? 1u : 0u);
     if (own) store_path_pixel(S, st);
     return;
   }
-  for (uint32_t v = 0; path_step<false>(S, stack, st, v, true, cnt); ++v) {
+  for (uint32_t v = 0; path_step<0>(S, stack, st, v, true, cnt); ++v) {
   }
   store_path_pixel(S, st);
 }

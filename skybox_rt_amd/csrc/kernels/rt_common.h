@@ -209,7 +209,8 @@ typedef struct {
                            // paths queued in segment i; RT_PQ_SEGS + g pt_queue waves done of
                            // group g; 2 * RT_PQ_SEGS groups done (the last zeroes them all)
   uint32_t pathq_seg_cap;  // entries per segment
-  uint32_t pad_pq;
+  uint32_t quad_tiles;     // the first quad_tiles of the split tiles run 16 pixels per wave
+                           // (the heaviest: a path on four lanes, pt_kernel.hip PT_QUAD)
 } rt_kernel_arg_t;
 // the path queue is split into segments (a primary chunk c appends to segment
 // c % RT_PQ_SEGS) so its atomics spread over that many counters: one

@@ -86,8 +86,13 @@ struct WaveLds {
 // 0.0302, 128 threads 0.0403.  The shadow rays read the MT records (rt_tri_t)
 // of S.geom.
 __shared__ uint4 s_geom[RT_FLAT_CAP];
+// RT_FLAT_SCALAR (A/B knob): no LDS staging, every rectangle word through
+// the scalar cache
+#ifndef RT_FLAT_SCALAR
+#define RT_FLAT_SCALAR 0
+#endif
 __device__ __forceinline__ const uint4* flat_list(const Scene& S) {
-  return S.num_geom <= RT_FLAT_CAP ? s_geom : nullptr;
+  return !RT_FLAT_SCALAR && S.num_geom <= RT_FLAT_CAP ? s_geom : nullptr;
 }
 #endif
 
@@ -379,7 +384,7 @@ VX_MAIN(rt_kernel_arg_t, arg, RT_BLOCK_THREADS) {
 #if RT_FLAT
   // stage the geometry list once per workgroup (workgroups past the last
   // task chunk have nothing to render and skip it)
-  if (S.num_geom <= RT_FLAT_CAP && blockIdx.x * VX_CHUNK < arg->num_tasks) {  // one chunk per step
+  if (!RT_FLAT_SCALAR && S.num_geom <= RT_FLAT_CAP && blockIdx.x * VX_CHUNK < arg->num_tasks) {
     for (uint32_t i = threadIdx.x; i < S.num_geom; i += blockDim.x)
       s_geom[i] = rect_corners(S.A.ld_u4(S.vgeom + 64u * i + 32u));
   }

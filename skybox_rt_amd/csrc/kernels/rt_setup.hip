@@ -166,9 +166,12 @@ __device__ void phase_fill(const rt_setup_arg_t* a) {
   }
 }
 
-// wave per primitive: every lane computes the setup (uniform values), lane 0
-// stores the records, the lanes split the rows of the covered-rectangle scan
-// (app/vis.cpp ComputeVisPrim)
+// workgroup per primitive: every thread computes the setup (uniform
+// values), thread 0 stores the records, the 256 threads split the rows of
+// the covered-rectangle scan (app/vis.cpp ComputeVisPrim) -- a screen-sized
+// layer triangle is 1024 rows at 1024^2, each three exact int64 row
+// solutions: 4 rows per thread instead of 16 per lane of one wave (the
+// phase's critical path) -- and the rectangle is reduced over the waves in LDS
 __device__ void phase_primvis(const rt_setup_arg_t* a) {
   const float* verts = vx_ptr<const float>(a->verts_addr);
   const uint32_t* pdc = vx_ptr<const uint32_t>(a->pdc_addr);
@@ -176,9 +179,9 @@ __device__ void phase_primvis(const rt_setup_arg_t* a) {
   rt_prim_t* prims = vx_ptr<rt_prim_t>(a->prims_addr);
   rt_bbox_t* bbox = vx_ptr<rt_bbox_t>(a->bbox_addr);
   uint4* vis = vx_ptr<uint4>(a->vis_addr);
-  const uint32_t W = a->width, H = a->height, l = lane_id();
-  const uint32_t waves = gridDim.x * (RTS_BLOCK / 64);
-  for (uint32_t g = blockIdx.x * (RTS_BLOCK / 64) + (threadIdx.x >> 6); g < a->num_prims; g += waves) {
+  const uint32_t W = a->width, H = a->height, l = lane_id(), wv = threadIdx.x >> 6;
+  __shared__ uint32_t red[RTS_BLOCK / 64][5];
+  for (uint32_t g = blockIdx.x; g < a->num_prims; g += gridDim.x) {
     float v[30];
     const float4* src = reinterpret_cast<const float4*>(verts + 32ull * g);
 #pragma unroll
@@ -193,7 +196,7 @@ __device__ void phase_primvis(const rt_setup_arg_t* a) {
     const uint32_t dc = pdc[g];
     Setup s;
     prim_setup(v, dc, dcz[2 * dc], dcz[2 * dc + 1], W, H, &s);
-    if (l == 0) {
+    if (threadIdx.x == 0) {
       const uint4* pr = reinterpret_cast<const uint4*>(&s.prim);
       uint4* dst = reinterpret_cast<uint4*>(prims + g);
 #pragma unroll
@@ -211,7 +214,7 @@ __device__ void phase_primvis(const rt_setup_arg_t* a) {
       const uint32_t Y0 = (T >> RT_TILE_LOG) << RT_TILE_LOG;
       const uint32_t Y1 = min(((B + 31u) >> RT_TILE_LOG) << RT_TILE_LOG, H);
       const int32_t* e = &s.prim.edges[0][0];
-      for (uint32_t y = Y0 + l; y < Y1; y += 64) {
+      for (uint32_t y = Y0 + threadIdx.x; y < Y1; y += RTS_BLOCK) {
         int64_t lo = X0, hi = (int64_t)X1 - 1, d[3] = {0, 0, 0};
         bool exact = true;
         for (int i = 0; i < 3 && exact; ++i) {
@@ -254,6 +257,15 @@ __device__ void phase_primvis(const rt_setup_arg_t* a) {
     xmax = wave_max_u32(xmax); ymax = wave_max_u32(ymax);
     all_zero = __ballot(all_zero) != 0;
     if (l == 0) {
+      red[wv][0] = xmin; red[wv][1] = xmax; red[wv][2] = ymin; red[wv][3] = ymax; red[wv][4] = all_zero;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      for (uint32_t k = 1; k < RTS_BLOCK / 64; ++k) {
+        xmin = min(xmin, red[k][0]); xmax = max(xmax, red[k][1]);
+        ymin = min(ymin, red[k][2]); ymax = max(ymax, red[k][3]);
+        all_zero |= red[k][4] != 0;
+      }
       const bool any = xmin != 0xffffffffu;
       uint4 rec = make_uint4(RT_VIS_EMPTY_RECT, RT_VIS_EMPTY_RECT, RT_VIS_ZMIN_NONE, 0u);
       if (any)
@@ -261,6 +273,7 @@ __device__ void phase_primvis(const rt_setup_arg_t* a) {
                          all_zero ? 0u : depth_lower_bound(s.prim.attribs[0]), 1u);
       vis[g] = rec;
     }
+    __syncthreads();  // red[] is reused by the next primitive
   }
 }
 
@@ -337,29 +350,6 @@ __device__ __forceinline__ void node_refs(const rt_setup_arg_t* a, uint32_t i, i
 
 // node references: > 0 internal node, < -1 leaf, -1 empty; 0 (the root is
 // nobody's child: the zero records of the device BVH4's absorbed nodes) empty
-__device__ void phase_link(const rt_setup_arg_t* a) {
-  int32_t* parent = vx_ptr<int32_t>(a->parent_addr);
-  uint32_t* count = vx_ptr<uint32_t>(a->count_addr);
-  uint32_t* status = vx_ptr<uint32_t>(a->status_addr);
-  const uint32_t nn = a->num_nodes;
-  for (uint32_t i = blockIdx.x * RTS_BLOCK + threadIdx.x; i < nn; i += gridDim.x * RTS_BLOCK) {
-    int32_t r[4];
-    node_refs(a, i, r);
-    uint32_t nint = 0;
-    for (int s = 0; s < 4; ++s) {
-      if (r[s] <= 0) continue;
-      if ((uint32_t)r[s] >= nn) {
-        atomicOr(&status[0], RTS_ERR_REF);
-        continue;
-      }
-      parent[r[s]] = (int32_t)(4 * i + s);
-      ++nint;
-    }
-    count[2 * i] = nint;
-    count[2 * i + 1] = 0;
-  }
-}
-
 struct Cover {
   uint32_t x0, x1, y0, y1, zmin;
   bool any;
@@ -375,13 +365,85 @@ __device__ __forceinline__ void cover_add(Cover* c, uint32_t rx, uint32_t ry, ui
 __device__ __forceinline__ void cover_add_corners(Cover* c, uint32_t lo, uint32_t hi, uint32_t zmin) {
   cover_add(c, (lo & 0xffffu) | (hi << 16), (lo >> 16) | (hi & 0xffff0000u), zmin);
 }
+// a leaf's cover: the covered rectangles / depth bounds of its (up to 4)
+// triangle records, their loads issued together
+__device__ __forceinline__ void leaf_cover(const rt_setup_arg_t* a, uint32_t lr, Cover* c) {
+  const rt_tri_t* tris = vx_ptr<const rt_tri_t>(a->tris_addr);
+  const uint4* vis = vx_ptr<const uint4>(a->vis_addr);
+  uint32_t* status = vx_ptr<uint32_t>(a->status_addr);
+  const uint32_t first = (lr >> 4) & 0x07ffffffu, cnt = (lr & 15u) + 1u;
+  int32_t pid[16];
+#pragma unroll
+  for (uint32_t k = 0; k < 16; ++k) {
+    if (k >= cnt) break;
+    pid[k] = first + k < a->num_tris ? tri_pid(tris, first + k) : -1;
+  }
+#pragma unroll
+  for (uint32_t k = 0; k < 16; ++k) {
+    if (k >= cnt) break;
+    if (pid[k] < 0 || (uint32_t)pid[k] >= a->num_prims) {
+      atomicOr(&status[0], RTS_ERR_PID);
+      continue;
+    }
+    const uint4 v = vis[pid[k]];
+    if (v.w) cover_add(c, v.x, v.y, v.z);
+  }
+}
+__device__ __forceinline__ void put_slot(rt_vnode_t& n, int s, const Cover& c, int32_t ref) {
+  n.lo[s] = c.any ? (c.x0 | (c.y0 << 16)) : RT_VIS_EMPTY_RECT;
+  n.hi[s] = c.any ? (c.x1 | (c.y1 << 16)) : RT_VIS_EMPTY_RECT;
+  n.zmin[s] = c.any ? c.zmin : RT_VIS_ZMIN_NONE;
+  n.child[s] = c.any ? ref : RT_EMPTY_REF;
+}
+
+// thread per node: the parent slot of each internal child and the node's
+// internal-child count (the climb's arrival target), and the node's vnode
+// record with its leaf and empty slots final (their covers computed here,
+// every node at once, so the climb only unions its children's slots)
+__device__ void phase_link(const rt_setup_arg_t* a) {
+  int32_t* parent = vx_ptr<int32_t>(a->parent_addr);
+  uint32_t* count = vx_ptr<uint32_t>(a->count_addr);
+  uint32_t* status = vx_ptr<uint32_t>(a->status_addr);
+  rt_vnode_t* vn = vx_ptr<rt_vnode_t>(a->vnodes_addr);
+  const uint32_t nn = a->num_nodes;
+  for (uint32_t i = blockIdx.x * RTS_BLOCK + threadIdx.x; i < nn; i += gridDim.x * RTS_BLOCK) {
+    int32_t r[4];
+    node_refs(a, i, r);
+    uint32_t nint = 0;
+    rt_vnode_t n;
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      if (r[s] > 0 && (uint32_t)r[s] < nn) {  // internal: written by the child's climb
+        parent[r[s]] = (int32_t)(4 * i + s);
+        ++nint;
+        n.lo[s] = n.hi[s] = RT_VIS_EMPTY_RECT;
+        n.zmin[s] = RT_VIS_ZMIN_NONE;
+        n.child[s] = RT_EMPTY_REF;
+        continue;
+      }
+      if (r[s] > 0) atomicOr(&status[0], RTS_ERR_REF);
+      Cover c = {0xffffu, 0u, 0xffffu, 0u, RT_VIS_ZMIN_NONE, false};
+      if (r[s] < RT_EMPTY_REF) leaf_cover(a, (uint32_t)r[s], &c);  // leaf: its triangle records
+      put_slot(n, s, c, r[s]);
+    }
+    vn[i] = n;
+    count[2 * i] = nint;
+    count[2 * i + 1] = 0;
+  }
+}
+
 
 // bottom-up vnode records (app/vis.cpp BuildVisNodes): each node's slots get
 // the union rectangle / minimum depth bound of the child's subtree; a node's
 // climbing thread computes its leaf slots, its internal slots were written by
 // the children's climbs, and it writes its own union into its parent's slot
-// before the agent-scope acq_rel arrival count -- the last child to arrive
-// climbs on (nobody waits)
+// before the acq_rel arrival count -- the last child to arrive climbs on
+// (nobody waits).  WG: the whole tree in one workgroup (trees up to
+// RTS_CLIMB_WG_NODES nodes, a one-workgroup phase): the arrivals are
+// workgroup-scope atomics, which cost no L2 write-back -- with the grid and
+// agent scope every climb step writes back the XCD's L2 (cross-XCD
+// visibility), ~55 us for tekkaman's 118-node tree at 1024^2
+template <bool WG>
 __device__ void phase_climb(const rt_setup_arg_t* a) {
   const int32_t* parent = vx_ptr<const int32_t>(a->parent_addr);
   uint32_t* count = vx_ptr<uint32_t>(a->count_addr);
@@ -390,7 +452,9 @@ __device__ void phase_climb(const rt_setup_arg_t* a) {
   rt_vnode_t* vn = vx_ptr<rt_vnode_t>(a->vnodes_addr);
   uint32_t* status = vx_ptr<uint32_t>(a->status_addr);
   const uint32_t nn = a->num_nodes;
-  for (uint32_t i = blockIdx.x * RTS_BLOCK + threadIdx.x; i < nn; i += gridDim.x * RTS_BLOCK) {
+  const uint32_t i0 = WG ? threadIdx.x : blockIdx.x * RTS_BLOCK + threadIdx.x;
+  const uint32_t step = WG ? RTS_BLOCK : gridDim.x * RTS_BLOCK;
+  for (uint32_t i = i0; i < nn; i += step) {
     if (count[2 * i] != 0) continue;
     uint32_t cur = i;
     for (int guard = 0;; ++guard) {
@@ -398,36 +462,16 @@ __device__ void phase_climb(const rt_setup_arg_t* a) {
         atomicOr(&status[0], RTS_ERR_CLIMB);
         break;
       }
-      int32_t r[4];
-      node_refs(a, cur, r);
+      // every slot of cur is final: its leaf / empty slots from LINK, its
+      // internal slots from the children's climbs -- one record read
+      const int32_t p = parent[cur];
       Cover u = {0xffffu, 0u, 0xffffu, 0u, RT_VIS_ZMIN_NONE, false};
-      for (int s = 0; s < 4; ++s) {
-        if (r[s] > 0 && (uint32_t)r[s] < nn) {  // written by the child's climb
-          if (vn[cur].child[s] != RT_EMPTY_REF) cover_add_corners(&u, vn[cur].lo[s], vn[cur].hi[s], vn[cur].zmin[s]);
-          continue;
-        }
-        Cover c = {0xffffu, 0u, 0xffffu, 0u, RT_VIS_ZMIN_NONE, false};
-        if (r[s] < RT_EMPTY_REF) {  // leaf: its triangle records
-          const uint32_t lr = (uint32_t)r[s], first = (lr >> 4) & 0x07ffffffu, cnt = (lr & 15u) + 1u;
-          for (uint32_t k = first; k < first + cnt; ++k) {
-            const int32_t pid = k < a->num_tris ? tri_pid(tris, k) : -1;
-            if (pid < 0 || (uint32_t)pid >= a->num_prims) {
-              atomicOr(&status[0], RTS_ERR_PID);
-              continue;
-            }
-            const uint4 v = vis[pid];
-            if (v.w) cover_add(&c, v.x, v.y, v.z);
-          }
-        }
-        vn[cur].lo[s] = c.any ? (c.x0 | (c.y0 << 16)) : RT_VIS_EMPTY_RECT;
-        vn[cur].hi[s] = c.any ? (c.x1 | (c.y1 << 16)) : RT_VIS_EMPTY_RECT;
-        vn[cur].zmin[s] = c.any ? c.zmin : RT_VIS_ZMIN_NONE;
-        vn[cur].child[s] = c.any ? r[s] : RT_EMPTY_REF;
-        if (c.any) cover_add_corners(&u, vn[cur].lo[s], vn[cur].hi[s], c.zmin);
-      }
-      // every slot of cur is final: ascending depth bound, stable (vis.cpp SortSlots)
       {
         rt_vnode_t n = vn[cur];
+#pragma unroll
+        for (int s = 0; s < 4; ++s)
+          if (n.child[s] != RT_EMPTY_REF) cover_add_corners(&u, n.lo[s], n.hi[s], n.zmin[s]);
+        // ascending depth bound, stable (vis.cpp SortSlots)
         for (int i = 1; i < 4; ++i)
           for (int j = i; j > 0 && n.zmin[j] < n.zmin[j - 1]; --j) {
             const uint32_t lo = n.lo[j], hi = n.hi[j], zm = n.zmin[j];
@@ -437,15 +481,15 @@ __device__ void phase_climb(const rt_setup_arg_t* a) {
           }
         vn[cur] = n;
       }
-      const int32_t p = parent[cur];
       if (p < 0) break;
       const uint32_t pn = (uint32_t)p >> 2, ps = (uint32_t)p & 3u;
       vn[pn].lo[ps] = u.any ? (u.x0 | (u.y0 << 16)) : RT_VIS_EMPTY_RECT;
       vn[pn].hi[ps] = u.any ? (u.x1 | (u.y1 << 16)) : RT_VIS_EMPTY_RECT;
       vn[pn].zmin[ps] = u.any ? u.zmin : RT_VIS_ZMIN_NONE;
       vn[pn].child[ps] = u.any ? (int32_t)cur : RT_EMPTY_REF;
-      const uint32_t old = __hip_atomic_fetch_add(&count[2 * pn + 1], 1u, __ATOMIC_ACQ_REL,
-                                                  __HIP_MEMORY_SCOPE_AGENT);
+      const uint32_t old =
+          WG ? __hip_atomic_fetch_add(&count[2 * pn + 1], 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_WORKGROUP)
+             : __hip_atomic_fetch_add(&count[2 * pn + 1], 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
       if (old + 1 != count[2 * pn]) break;
       cur = pn;
     }
@@ -472,28 +516,40 @@ __device__ void phase_weight(const rt_setup_arg_t* a) {
   }
 }
 
+// inclusive prefix sum of v[0], v[s], .., v[(n - 1) s] in place, 16 words
+// loaded per round before any is stored: a row / column of the difference
+// array is a few dependent memory round trips, not one per word (33 at
+// 1024^2, 129 at 4096^2)
+__device__ __forceinline__ void prefix_strided(uint32_t* v, uint32_t n, uint32_t s) {
+  constexpr uint32_t R = 16;
+  uint32_t run = 0;
+  for (uint32_t b = 0; b < n; b += R) {
+    uint32_t x[R];
+#pragma unroll
+    for (uint32_t k = 0; k < R; ++k) x[k] = b + k < n ? v[(b + k) * s] : 0u;
+#pragma unroll
+    for (uint32_t k = 0; k < R; ++k) {
+      run += x[k];
+      x[k] = run;
+    }
+#pragma unroll
+    for (uint32_t k = 0; k < R; ++k)
+      if (b + k < n) v[(b + k) * s] = x[k];
+  }
+}
+
 __device__ void phase_rowsum(const rt_setup_arg_t* a) {
   uint32_t* w = vx_ptr<uint32_t>(a->weight_addr);
   const uint32_t W1 = a->tiles_x + 1;
-  for (uint32_t r = blockIdx.x * RTS_BLOCK + threadIdx.x; r <= a->tiles_y; r += gridDim.x * RTS_BLOCK) {
-    uint32_t run = 0;
-    for (uint32_t x = 0; x < W1; ++x) {
-      run += w[r * W1 + x];
-      w[r * W1 + x] = run;
-    }
-  }
+  for (uint32_t r = blockIdx.x * RTS_BLOCK + threadIdx.x; r <= a->tiles_y; r += gridDim.x * RTS_BLOCK)
+    prefix_strided(w + r * W1, W1, 1u);
 }
 
 __device__ void phase_colsum(const rt_setup_arg_t* a) {
   uint32_t* w = vx_ptr<uint32_t>(a->weight_addr);
   const uint32_t W1 = a->tiles_x + 1;
-  for (uint32_t c = blockIdx.x * RTS_BLOCK + threadIdx.x; c < W1; c += gridDim.x * RTS_BLOCK) {
-    uint32_t run = 0;
-    for (uint32_t y = 0; y <= a->tiles_y; ++y) {
-      run += w[y * W1 + c];
-      w[y * W1 + c] = run;
-    }
-  }
+  for (uint32_t c = blockIdx.x * RTS_BLOCK + threadIdx.x; c < W1; c += gridDim.x * RTS_BLOCK)
+    prefix_strided(w + c, a->tiles_y + 1, W1);
 }
 
 // sort digit of local tile lt: 255 - min(weight, 255) (ascending digit =
@@ -795,23 +851,46 @@ __device__ void phase_bsort(const rt_setup_arg_t* a) {
 // ---- light-space shadow lists (rt_common.h; oracle/rt.c sl_build restates
 // them operation for operation: fp32, no contraction, IEEE division)
 
-// clip polygon `in` (n vertices) to s * x_k * (1 + eps) - sg * x_m >= 0
-__device__ __forceinline__ int sl_clip_plane(const float (*in)[3], int n, int k, float s, int m, float sg,
-                                             float (*out)[3]) {
+// The projection of a triangle on a cube face, in registers: polygons as
+// 8 static slots per coordinate (a triangle clipped by four planes has at
+// most 7 vertices); a vertex written at a dynamic position becomes selects
+// over the slots, so nothing goes to scratch memory.  Operation for
+// operation oracle/rt.c sl_clip_plane / sl_project (fp32, no contraction).
+struct SlPoly {
+  float c[3][8];  // c[axis][vertex]
+  int n;
+};
+__device__ __forceinline__ float sl_axis(const SlPoly& P, int q, int k) {
+  return k == 0 ? P.c[0][q] : (k == 1 ? P.c[1][q] : P.c[2][q]);
+}
+// clip `in` to s * x_k * (1 + eps) - sg * x_m >= 0
+__device__ __forceinline__ void sl_clip_plane(const SlPoly& in, int k, float s, int m, float sg, SlPoly& out) {
   const float ke = 1.0f + RT_SLIST_EPS;
   int o = 0;
-  for (int q = 0; q < n; ++q) {
-    const float* a = in[q];
-    const float* b = in[q + 1 < n ? q + 1 : 0];
-    const float da = (s * a[k]) * ke - sg * a[m], db = (s * b[k]) * ke - sg * b[m];
-    if (da >= 0.0f) { out[o][0] = a[0]; out[o][1] = a[1]; out[o][2] = a[2]; ++o; }
+  auto put = [&](float x, float y, float z) {
+#pragma unroll
+    for (int t = 0; t < 8; ++t)
+      if (t == o) { out.c[0][t] = x; out.c[1][t] = y; out.c[2][t] = z; }
+    ++o;
+  };
+#pragma unroll
+  for (int q = 0; q < 8; ++q) {
+    if (q >= in.n) break;
+    const bool wrap = q + 1 >= in.n;
+    const int qb = q + 1 < 8 ? q + 1 : 0;
+    const float ax = in.c[0][q], ay = in.c[1][q], az = in.c[2][q];
+    const float bx = wrap ? in.c[0][0] : in.c[0][qb], by = wrap ? in.c[1][0] : in.c[1][qb],
+                bz = wrap ? in.c[2][0] : in.c[2][qb];
+    const float ak = k == 0 ? ax : (k == 1 ? ay : az), am = m == 0 ? ax : (m == 1 ? ay : az);
+    const float bk = k == 0 ? bx : (k == 1 ? by : bz), bm = m == 0 ? bx : (m == 1 ? by : bz);
+    const float da = (s * ak) * ke - sg * am, db = (s * bk) * ke - sg * bm;
+    if (da >= 0.0f) put(ax, ay, az);
     if ((da >= 0.0f) != (db >= 0.0f)) {
       const float tq = da / (da - db);
-      for (int cc = 0; cc < 3; ++cc) out[o][cc] = a[cc] + (b[cc] - a[cc]) * tq;
-      ++o;
+      put(ax + (bx - ax) * tq, ay + (by - ay) * tq, az + (bz - az) * tq);
     }
   }
-  return o;
+  out.n = o;
 }
 
 struct SlFace {
@@ -822,25 +901,27 @@ struct SlFace {
 };
 
 // geometry triangle (rt_tri_t record r) on face f; false: nothing on the face
-__device__ __noinline__ bool sl_project(const rt_tri_t& r, const float L[3], int f, int N, SlFace* F) {
+__device__ __forceinline__ bool sl_project(const rt_tri_t& r, const float L[3], int f, int N, SlFace* F) {
   const int k = f >> 1, i = k == 0 ? 1 : 0, j = k == 2 ? 1 : 2;
   const float s = (f & 1) ? -1.0f : 1.0f;
-  float A[8][3], B[8][3];
+  SlPoly A, B;
   for (int cc = 0; cc < 3; ++cc) {
-    A[0][cc] = r.v[cc] - L[cc];
-    A[1][cc] = (r.v[cc] + r.v[4 + cc]) - L[cc];
-    A[2][cc] = (r.v[cc] + r.v[8 + cc]) - L[cc];
+    A.c[cc][0] = r.v[cc] - L[cc];
+    A.c[cc][1] = (r.v[cc] + r.v[4 + cc]) - L[cc];
+    A.c[cc][2] = (r.v[cc] + r.v[8 + cc]) - L[cc];
   }
-  int m = 3;
-  m = sl_clip_plane(A, m, k, s, i, 1.0f, B);
-  if (m) m = sl_clip_plane(B, m, k, s, i, -1.0f, A);
-  if (m) m = sl_clip_plane(A, m, k, s, j, 1.0f, B);
-  if (m) m = sl_clip_plane(B, m, k, s, j, -1.0f, A);
+  A.n = 3;
+  sl_clip_plane(A, k, s, i, 1.0f, B);
+  if (B.n) sl_clip_plane(B, k, s, i, -1.0f, A); else A.n = 0;
+  if (A.n) sl_clip_plane(A, k, s, j, 1.0f, B); else B.n = 0;
+  if (B.n) sl_clip_plane(B, k, s, j, -1.0f, A); else A.n = 0;
+  const int m = A.n;
   if (!m) return false;
   const float hn = (float)N * 0.5f;
   F->whole = 0;
-  for (int q = 0; q < m; ++q)
-    if (!(s * A[q][k] > 0.0f)) F->whole = 1;
+#pragma unroll
+  for (int q = 0; q < 8; ++q)
+    if (q < m && !(s * sl_axis(A, q, k) > 0.0f)) F->whole = 1;
   if (F->whole) {
     F->n = 0;
     F->x0 = F->y0 = 0;
@@ -848,10 +929,12 @@ __device__ __noinline__ bool sl_project(const rt_tri_t& r, const float L[3], int
     return true;
   }
   float u0 = 0, u1 = 0, v0 = 0, v1 = 0;
-  for (int q = 0; q < m; ++q) {
-    const float ck = s * A[q][k];
-    F->pu[q] = A[q][i] / ck;
-    F->pv[q] = A[q][j] / ck;
+#pragma unroll
+  for (int q = 0; q < 8; ++q) {
+    if (q >= m) break;
+    const float ck = s * sl_axis(A, q, k);
+    F->pu[q] = sl_axis(A, q, i) / ck;
+    F->pv[q] = sl_axis(A, q, j) / ck;
     if (q == 0 || F->pu[q] < u0) u0 = F->pu[q];
     if (q == 0 || F->pu[q] > u1) u1 = F->pu[q];
     if (q == 0 || F->pv[q] < v0) v0 = F->pv[q];
@@ -909,11 +992,16 @@ __device__ void phase_sproj(const rt_setup_arg_t* a) {
       cells = w * h;
       uint4* o = rec + (uint64_t)it * (RTS_SPROJ_WORDS / 4);
       o[0] = make_uint4((uint32_t)F.x0 | ((uint32_t)F.y0 << 16), w, n, f);
-      for (uint32_t e = 0; e < n; ++e) {
-        const uint32_t e1 = e + 1 < n ? e + 1 : 0u;
-        const float nx = F.pv[e1] - F.pv[e], ny = F.pu[e] - F.pu[e1];
+#pragma unroll
+      for (uint32_t e = 0; e < 7; ++e) {
+        if (e >= n) break;
+        const bool wrap = e + 1 >= n;
+        const float nx = (wrap ? F.pv[0] : F.pv[e + 1]) - F.pv[e];
+        const float ny = F.pu[e] - (wrap ? F.pu[0] : F.pu[e + 1]);
         float p0 = 0, p1 = 0;
-        for (uint32_t q = 0; q < n; ++q) {
+#pragma unroll
+        for (uint32_t q = 0; q < 7; ++q) {
+          if (q >= n) break;
           const float d = nx * F.pu[q] + ny * F.pv[q];
           if (q == 0 || d < p0) p0 = d;
           if (q == 0 || d > p1) p1 = d;
@@ -1080,7 +1168,7 @@ __device__ void run_phases(const rt_setup_arg_t* arg, uint32_t ph) {
   if (ph & RTS_WEIGHT) phase_weight(arg);
   if (ph & RTS_LINK) phase_link(arg);
   if (ph & RTS_ROWSUM) phase_rowsum(arg);
-  if (ph & RTS_CLIMB) phase_climb(arg);
+  if ((ph & RTS_CLIMB) && arg->num_nodes > RTS_CLIMB_WG_NODES) phase_climb<false>(arg);
   if (ph & RTS_COLSUM) phase_colsum(arg);
   if (ph & RTS_HIST) phase_hist(arg);
   if (ph & RTS_SCATTER) phase_scatter(arg);
@@ -1098,6 +1186,7 @@ __device__ void run_phases(const rt_setup_arg_t* arg, uint32_t ph) {
 }
 // the one-workgroup sub-phases of `ph` (scans), run by one workgroup
 __device__ void run_scans(const rt_setup_arg_t* arg, uint32_t ph) {
+  if ((ph & RTS_CLIMB) && arg->num_nodes <= RTS_CLIMB_WG_NODES) { phase_climb<true>(arg); __syncthreads(); }
   if (ph & RTS_SOSCAN) { phase_soscan(arg); __syncthreads(); }
   if (ph & RTS_BSCAN) { phase_lscan(block_set(arg)); __syncthreads(); }
   if (ph & RTS_SSCAN) { phase_lscan(cell_set(arg)); __syncthreads(); }
@@ -1112,6 +1201,11 @@ __device__ void run_scans(const rt_setup_arg_t* arg, uint32_t ph) {
 }
 
 }  // namespace
+
+// grid: 4 workgroups of 256 threads per CU (1024 on MI355X) -- the phases
+// are grid-stride loops, and a sequence's one-workgroup steps (the scans) or
+// small steps then pay the dispatch of 1024 workgroups instead of 4096
+__device__ __attribute__((used)) uint32_t __vx_grid_per_cu = 4;
 
 // A single launch runs `phases`; launch i of a sequence (nseq > 0, launch
 // tag i) runs seq_phases[i] -- the scans, one-workgroup phases, by

@@ -901,6 +901,171 @@ __device__ __forceinline__ bool occluded_list_coop(const Scene& S, const Ray& s,
   return false;
 }
 
+// Quad walks for the path tracer's 16-pixel waves (pt_kernel PT_QUAD): the
+// four lanes 4p .. 4p + 3 trace pixel p's ray together, lane j = lane & 3
+// taking a BVH4 node's child j, a leaf's triangle j and a list round's
+// record j.  The lanes exchange values within their quad by DPP quad_perm
+// moves (no LDS, no permlane): the node step's 5-exchange sorting network
+// (node4_step's: (0,1)(2,3) | (0,2)(1,3) | (1,2)) runs across the quad,
+// lane j ending with the j-th nearest hit child, so lane j pushes its child at
+// the row push_sorted gives it (one LDS column per quad); a leaf's best hit
+// and a list round's first event are quad reductions.  Per ray the node
+// visits, the stack's order and the result are the per-lane walk's
+// (trace_impl / occluded_list), and so are the counters (visits counted by
+// lane 0, tests by the lane that made them, a list round's only up to its
+// first event in list order).
+#define RT_QP_XOR1 0xB1  // quad_perm [1,0,3,2]
+#define RT_QP_XOR2 0x4E  // quad_perm [2,3,0,1]
+#define RT_QP_MID 0xD8   // quad_perm [0,2,1,3]
+#define RT_QP_B0 0x00    // quad_perm [0,0,0,0]
+template <int CTRL>
+__device__ __forceinline__ uint32_t qmov(uint32_t v) {
+  return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, CTRL, 0xF, 0xF, false);
+}
+template <int CTRL>
+__device__ __forceinline__ float qmovf(float v) { return __uint_as_float(qmov<CTRL>(__float_as_uint(v))); }
+// the quad's 4 bits of a wave mask (lane j of the quad = bit j)
+__device__ __forceinline__ uint32_t quad_bits(uint64_t m) {
+  return (uint32_t)(m >> (lane_id() & ~3u)) & 0xFu;
+}
+// one compare-exchange of the sorting network between quad lanes `lo` < `hi`
+// (CTRL: the permutation pairing them): the lower lane keeps the nearer
+// (strict <, node4_step's cx), the upper the farther, the child moving along
+template <int CTRL>
+__device__ __forceinline__ void qcx(float& k, int32_t& c, bool lower, bool part) {
+  const float pk = qmovf<CTRL>(k);
+  const int32_t pc = (int32_t)qmov<CTRL>((uint32_t)c);
+  if (!part) return;
+  const bool s = lower ? pk < k : k < pk;
+  k = s ? pk : k;
+  c = s ? pc : c;
+}
+
+template <bool SCALAR>
+__device__ __forceinline__ int32_t node4_quad(const Scene& S, uint32_t ref, const Ray& r, float lim,
+                                              uint32_t j, int32_t* mem, int& sp) {
+  auto ld = [&](uint32_t o) { return SCALAR ? S.A.sld_u4(o) : S.A.ld_u4(o); };
+  const uint32_t no = S.nodes4 + 128u * S.num_nodes4 + 64u * ref;
+  const uint4 px = ld(no), py = ld(no + 16), pz = ld(no + 32), cf = ld(no + 48);
+  // child j's planes: half j (lo) and half 4 + j (hi) of each axis' 16 B
+  const uint32_t sh = (j & 1u) * 16u;
+  auto half = [&](const uint4& w, bool upper) {
+    const uint32_t word = upper ? ((j >> 1) ? w.w : w.z) : ((j >> 1) ? w.y : w.x);
+    return (float)__builtin_bit_cast(_Float16, (uint16_t)((word >> sh) & 0xffffu));
+  };
+  const int32_t c0 = (int32_t)(j == 0 ? cf.x : j == 1 ? cf.y : j == 2 ? cf.z : cf.w);
+  float tn = 0.0f;
+  const bool h = slab(half(px, false), half(px, true), half(py, false), half(py, true), half(pz, false),
+                      half(pz, true), r, 0.0f, lim, &tn) &
+                 (c0 != RT_EMPTY_REF);
+  float k = h ? fminf(tn, 3.402823466e38f) : __builtin_inff();
+  int32_t c = c0;
+  const uint32_t n = (uint32_t)__popc(quad_bits(__ballot(h)));
+  qcx<RT_QP_XOR1>(k, c, (j & 1u) == 0u, true);  // (0,1) (2,3)
+  qcx<RT_QP_XOR2>(k, c, j < 2u, true);          // (0,2) (1,3)
+  qcx<RT_QP_MID>(k, c, j == 1u, j == 1u || j == 2u);  // (1,2)
+  if (n == 0) return RT_EMPTY_REF;
+  // lane j (1 <= j < n) holds the j-th nearest hit: row sp + n - 1 - j
+  const int row = sp + (int)n - 1 - (int)j;
+  if (j >= 1u && j < n && row < RT_MAX_STACK) mem[64 * row] = c;
+  const int top = sp + (int)n - 1;
+  sp = top < RT_MAX_STACK ? top : RT_MAX_STACK;
+  return (int32_t)qmov<RT_QP_B0>((uint32_t)c);
+}
+
+// trace<false> (closest hit from 0 below +inf, binary16 BVH4) by a quad;
+// every lane of the quad returns the hit and *t_out
+__device__ __forceinline__ int32_t trace_quad(const Scene& S, const Ray& r, int32_t skip, bool tie_high,
+                                              float* t_out, int32_t* mem, uint32_t j, Counters& cnt) {
+  if (S.num_nodes == 0) return -1;
+  int sp = 0;
+  float bt = INFINITY;
+  int32_t bpid = -1;
+  RT_CNT(cnt.visits += j == 0u ? 1u : 0u;)
+  int32_t ref = node4_quad<true>(S, 0u, r, bt, j, mem, sp);
+  if (ref == RT_EMPTY_REF) return -1;
+  auto pop = [&](int32_t& x) {
+    if (sp == 0) return false;
+    x = mem[64 * --sp];
+    return true;
+  };
+  for (;;) {
+    bool dry = false;
+    {
+      RT_CYC_BEGIN();
+      while (ref >= 0) {  // while-while, as trace_impl
+        RT_WAVE_ITER(9);
+        RT_CNT(cnt.visits += j == 0u ? 1u : 0u;)
+        const int32_t nx = node4_quad<false>(S, (uint32_t)ref, r, bt, j, mem, sp);
+        if (nx != RT_EMPTY_REF) { ref = nx; continue; }
+        if (!pop(ref)) { dry = true; break; }
+      }
+      RT_CYC_END(11);
+    }
+    if (dry) break;
+    {
+      RT_WAVE_ITER(9);  // this lane's triangle of the leaf (padding records past the end)
+      const uint32_t lr = (uint32_t)ref;
+      const uint32_t first = (lr >> 4) & 0x07ffffffu, count = (lr & 15u) + 1u;
+      const uint32_t to = S.tris + 48u * (first + j);
+      const float4 ta = S.A.ld_f4(to), tb = S.A.ld_f4(to + 16), tc = S.A.ld_f4(to + 32);
+      if (j < count) {
+        const int32_t pid = __float_as_int(ta.w);
+        RT_CNT(++cnt.tests;)
+        float t;
+        if (pid != skip && mt_hit(r, ta, tb, tc, 0.0f, &t) && closer(t, pid, bt, bpid, tie_high)) {
+          bt = t;
+          bpid = pid;
+        }
+      }
+      // the quad's best: closer() is a strict total order, so every lane
+      // ends with the four tests' sequential result
+      {
+        const float pt = qmovf<RT_QP_XOR1>(bt);
+        const int32_t pb = (int32_t)qmov<RT_QP_XOR1>((uint32_t)bpid);
+        if (pb >= 0 && closer(pt, pb, bt, bpid, tie_high)) { bt = pt; bpid = pb; }
+      }
+      {
+        const float pt = qmovf<RT_QP_XOR2>(bt);
+        const int32_t pb = (int32_t)qmov<RT_QP_XOR2>((uint32_t)bpid);
+        if (pb >= 0 && closer(pt, pb, bt, bpid, tie_high)) { bt = pt; bpid = pb; }
+      }
+    }
+    if (!pop(ref)) break;
+  }
+  if (bpid >= 0) *t_out = bt;
+  return bpid;
+}
+
+// occluded_list by a quad: rounds of four records, lane j testing record
+// q + j; the first event of the round in list order (an occluder, or a
+// record past the segment bound: occluded_list's two exits) decides, and the
+// tests counted are the sequential scan's (lanes before that event, and the
+// event's own lane when it is an occluder)
+__device__ __forceinline__ bool occluded_list_quad(const Scene& S, const Ray& s, bool act, int32_t skip,
+                                                   uint32_t j, Counters& cnt) {
+  if (!act) return false;
+  const uint32_t cell = slist_cell(s, S.slist_n);
+  const uint32_t off = S.A.ld_u32(S.sidx + 8u * cell), n = S.A.ld_u32(S.sidx + 8u * cell + 4u);
+  const float lim = slist_limit(s);
+  for (uint32_t q = 0; q < n; q += 4) {
+    const uint32_t e = q + j;
+    bool hit = false, end = false;
+    if (e < n) {
+      const uint32_t o = S.slist + 48u * (off + e);
+      const float4 a = S.A.ld_f4(o), b = S.A.ld_f4(o + 16), c = S.A.ld_f4(o + 32);
+      end = b.w > lim;
+      float th;
+      hit = !end && __float_as_int(a.w) != skip && mt_hit(s, a, b, c, 0.0f, &th) && th < 1.0f;
+    }
+    const uint32_t mh = quad_bits(__ballot(hit)), me = quad_bits(__ballot(end)), mev = mh | me;
+    const uint32_t first = mev ? (uint32_t)__builtin_ctz(mev) : 4u;
+    RT_CNT(cnt.tests += (e < n && (j < first || (j == first && ((mh >> j) & 1u)))) ? 1u : 0u;)
+    if (mev) return ((mh >> first) & 1u) != 0u;
+  }
+  return false;
+}
+
 template <bool ANY>
 __device__ __forceinline__ int32_t trace(const Scene& S, const Ray& r, float tmin, float tmax,
                                          int32_t skip, bool tie_high, float* t_out,
@@ -1299,7 +1464,7 @@ struct TaskPix {
 #define RT_LAZY_TASK_ARGS 1
 #endif
 struct TaskArgs {
-  uint32_t split_tiles, split_log, order, shard_index, shard_count, tiles_x;
+  uint32_t split_tiles, split_log, order, shard_index, shard_count, tiles_x, quad_tiles;
 };
 __device__ __forceinline__ TaskArgs task_args(const Scene& S) {
   TaskArgs t;
@@ -1310,26 +1475,43 @@ __device__ __forceinline__ TaskArgs task_args(const Scene& S) {
       (const __attribute__((address_space(4))) rt_kernel_arg_t*)p;
   t.split_tiles = a->split_tiles; t.split_log = a->split_log; t.order = (uint32_t)a->order_addr;
   t.shard_index = a->shard_index; t.shard_count = a->shard_count; t.tiles_x = a->tiles_x;
+  t.quad_tiles = a->quad_tiles;
 #else
   t.split_tiles = S.split_tiles; t.split_log = S.split_log; t.order = S.order;
   t.shard_index = S.shard_index; t.shard_count = S.shard_count; t.tiles_x = S.tiles_x;
+  t.quad_tiles = 0;
 #endif
   return t;
 }
+// Tiers: the first quad_tiles tiles of the order at 16 pixels per wave
+// (4096 tasks each), the rest of the split tiles at 2^split_log, then the
+// whole-block tiles.
 __device__ __forceinline__ TaskPix task_map(const Scene& S, const TaskArgs& T, uint32_t t) {
   TaskPix m;
-  const uint32_t pl = T.split_log;  // split tiles: 2^pl pixels per wave (pl <= 6)
+  uint32_t pl = T.split_log;         // split tiles: 2^pl pixels per wave (pl <= 6)
+  uint32_t base = 0, ns = T.split_tiles;
+  if (T.quad_tiles) {
+    const uint32_t hq = T.quad_tiles << 12;
+    if (t < hq) {
+      pl = 4u;
+      ns = T.quad_tiles;
+    } else {
+      t -= hq;
+      base = T.quad_tiles;
+      ns -= T.quad_tiles;
+    }
+  }
   const uint32_t cl = 16u - pl;      // log2 tasks per split tile (1024 >> pl chunks of 64)
-  const uint32_t hs = T.split_tiles << cl;
+  const uint32_t hs = ns << cl;
   uint32_t pos;
   if (t < hs) {
     const uint32_t sub = 6u - pl;    // log2 chunks per 8x8 block
     const uint32_t c = (t >> 6) & ((1024u >> pl) - 1u), ln = t & 63u;
-    pos = t >> cl;
+    pos = base + (t >> cl);
     m.idx = ((c >> sub) << 6) + ((c & ((1u << sub) - 1u)) << pl) + (ln & ((1u << pl) - 1u));
     m.live = ln < (1u << pl);
   } else {
-    pos = T.split_tiles + ((t - hs) >> 10);
+    pos = base + ns + ((t - hs) >> 10);
     m.idx = t & 1023u;
     m.live = true;
   }

@@ -80,7 +80,8 @@
 // entries beyond scap
 #define RTS_STATUS_WORDS 8
 #define RTS_SPROJ_WORDS 32u  // u32 per SPROJ record: header uint4 + 7 separating axes (nx, ny, p0, p1)
-#define RTS_MAX_SEQ 12
+#define RTS_MAX_SEQ 32
+#define RTS_CLIMB_WG_NODES 4096u  // trees this small climb in one workgroup (rt_setup.hip phase_climb)
 #define RTS_ERR_REF   0x1u   // a tree reference out of range
 #define RTS_ERR_PID   0x2u   // a leaf record's pid out of range
 #define RTS_ERR_CLIMB 0x4u   // a climb longer than 64 levels
