@@ -86,6 +86,15 @@ int orc_raster_render(const orc_scene_t* scene, uint32_t width, uint32_t height,
 int orc_raster_coverage(const orc_scene_t* scene, uint32_t width, uint32_t height,
                         uint32_t tile_logsize, uint32_t* color);
 
+/* The rasterizer's per-pixel coverage of one primitive over a w x h pixel
+ * window at (x0, y0): mask[j * w + i] = 1 iff all three edge values
+ * a*x + b*y + c (int32 wrap, graphics.cpp:640-642) at (x0 + i, y0 + j) are
+ * >= 0 (inclusive, no top-left rule, graphics.cpp:813-825).  `edges` holds
+ * (a, b, c) per edge.  The RTL raster slice's known-answer test
+ * (hw/unit_tests/raster_unit/raster_slice/testbench.cpp:53-66) pins it. */
+void orc_edge_cover(const int32_t edges[9], uint32_t x0, uint32_t y0, uint32_t w, uint32_t h,
+                    uint8_t* mask);
+
 /* ---- ray tracing -------------------------------------------------------- */
 typedef struct {
   uint32_t width, height;

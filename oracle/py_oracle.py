@@ -181,6 +181,18 @@ def raster_coverage(oscene: OracleScene, width: int, height: int, tile_logsize: 
     return color.reshape(height, width)
 
 
+def edge_cover(edges, x0: int, y0: int, w: int, h: int) -> np.ndarray:
+    """orc_edge_cover: the rasterizer's coverage of one primitive, (a, b, c)
+    per edge, over the w x h window at (x0, y0) -> uint8 [h, w]."""
+    L = lib()
+    L.orc_edge_cover.argtypes = [C.c_void_p, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32, C.c_void_p]
+    L.orc_edge_cover.restype = None
+    e = np.ascontiguousarray(np.asarray(edges, np.int64).reshape(9).astype(np.int32))
+    m = np.zeros(w * h, np.uint8)
+    L.orc_edge_cover(e.ctypes.data, x0, y0, w, h, m.ctypes.data)
+    return m.reshape(h, w)
+
+
 def vis_prims(oscene: OracleScene, width: int, height: int) -> np.ndarray:
     """uint32[P, 3]: every primitive's covered-pixel rectangle (x0|x1<<16,
     y0|y1<<16, inclusive) and depth-word lower bound, by brute force (vis.c)."""

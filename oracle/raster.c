@@ -102,6 +102,16 @@ int orc_raster_render(const orc_scene_t* scene, uint32_t width, uint32_t height,
   return raster_render(scene, width, height, tile_logsize, 0, color, depth, pid_out);
 }
 
+void orc_edge_cover(const int32_t edges[9], uint32_t x0, uint32_t y0, uint32_t w, uint32_t h,
+                    uint8_t* mask) {
+  for (uint32_t j = 0; j < h; ++j)
+    for (uint32_t i = 0; i < w; ++i) {
+      const uint32_t x = x0 + i, y = y0 + j;
+      mask[j * w + i] = orc_edge_eval(&edges[0], x, y) >= 0 && orc_edge_eval(&edges[3], x, y) >= 0 &&
+                        orc_edge_eval(&edges[6], x, y) >= 0;
+    }
+}
+
 int orc_raster_coverage(const orc_scene_t* scene, uint32_t width, uint32_t height,
                         uint32_t tile_logsize, uint32_t* color) {
   uint32_t dummy = 0;

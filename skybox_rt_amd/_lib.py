@@ -23,7 +23,7 @@ CSRC_DIR = os.path.join(PKG_DIR, "csrc")
 
 REQUIRED = ("libvortex.so", "libvortex-hip.so", "librtapp.so", "rtapp",
             "rt_kernel.vxbin", "rt_kernel_stats.vxbin", "rt_kernel_deep.vxbin",
-            "rt_kernel_deep_stats.vxbin", "spawn_test.vxbin", "pt_kernel.vxbin",
+            "rt_kernel_deep_stats.vxbin", "spawn_test.vxbin", "edge_kat.vxbin", "pt_kernel.vxbin",
             "pt_kernel_deep.vxbin", "pt_kernel_stats.vxbin", "pt_kernel_deep_stats.vxbin",
             "rt_flat.vxbin", "rt_flat_stats.vxbin", "raster_kernel.vxbin",
             "pt_compact/pt_kernel.vxbin", "pt_compact/pt_kernel_stats.vxbin",

@@ -195,6 +195,14 @@ __device__ __forceinline__ uint32_t mul8(int32_t d, uint32_t c) {
 __device__ __forceinline__ int32_t edge_eval(const int32_t* e, uint32_t x, uint32_t y) {
   return (int32_t)((uint32_t)e[0] * x + (uint32_t)e[1] * y + (uint32_t)e[2]);
 }
+// the rasterizer's coverage of pixel (x, y): all three edge values >= 0
+// (inclusive, no top-left rule, graphics.cpp:813-825); the values to `e`
+__device__ __forceinline__ bool covers(const int32_t* edges, uint32_t x, uint32_t y, int32_t e[3]) {
+  e[0] = edge_eval(edges, x, y);
+  e[1] = edge_eval(edges + 3, x, y);
+  e[2] = edge_eval(edges + 6, x, y);
+  return e[0] >= 0 && e[1] >= 0 && e[2] >= 0;
+}
 
 // The shader's tail from Q.24 barycentric weights dx (vertex 0), dy (vertex 1):
 // INTERPOLATE / TEXTURING / MODULATE (draw3d/kernel.cpp:48-79).  Path-trace

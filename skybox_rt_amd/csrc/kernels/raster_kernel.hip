@@ -159,12 +159,11 @@ __device__ __forceinline__ void render_tile(const Frame& F, uint32_t tile, RsLds
         for (uint32_t j = 0; j < 4; ++j) {
           if (j >= npx) break;
           const uint32_t x = qx + (j & 1u), y = qy + (j >> 1);
-          const int32_t e0 = gfx::edge_eval(p.edge(0), x, y);
-          const int32_t e1 = gfx::edge_eval(p.edge(1), x, y);
-          const int32_t e2 = gfx::edge_eval(p.edge(2), x, y);
+          int32_t e[3];
           // inclusive coverage, no top-left rule, viewport scissor
-          // (graphics.cpp:813-825)
-          bool in = x < F.width && y < F.height && e0 >= 0 && e1 >= 0 && e2 >= 0;
+          // (graphics.cpp:813-825; the edge KAT image tests gfx::covers)
+          bool in = gfx::covers(p.edge(0), x, y, e) && x < F.width && y < F.height;
+          const int32_t e0 = e[0], e1 = e[1], e2 = e[2];
           if (fine_bins)  // the pixel's own bin must be one the primitive was binned to
             in = in && bins_to(L.bb[k], x & ~pmask, (x & ~pmask) + pmask + 1u, y & ~pmask,
                                (y & ~pmask) + pmask + 1u);
