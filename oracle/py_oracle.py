@@ -222,7 +222,7 @@ def vis_block_lists(oscene: OracleScene, width: int, height: int, shard_index: i
     return idx[:nlb.value], ent[:tot.value]
 
 
-SL_N = 256  # rt.c SL_N, the kernels' RT_SLIST_N
+SL_N = 128  # rt.c SL_N, the kernels' RT_SLIST_N
 
 
 def shadow_lists(oscene: OracleScene, light=(0.0, 60.0, 80.0)):

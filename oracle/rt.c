@@ -838,7 +838,7 @@ static uint32_t path_trace(const rt_ctx_t* c, uint32_t px, const float d0[3], fl
  * record whose key exceeds |L - P|^2 * 1.001 (that triangle has no point on
  * the segment, nor has any after it).  All arithmetic fp32, no
  * contraction, the device's operation order. */
-#define SL_N 256
+#define SL_N 128
 #define SL_EPS (1.0f / 512.0f)
 #define SL_CELLS (6 * SL_N * SL_N)
 static const int sl_ax[3][2] = {{1, 2}, {0, 2}, {0, 1}};

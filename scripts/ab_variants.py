@@ -38,6 +38,7 @@ def main():
     ap.add_argument("--no-shadows", action="store_true")
     ap.add_argument("--mode", choices=("shadow", "path", "flat", "raster"), default="shadow")
     ap.add_argument("--bounces", type=int, default=4)
+    ap.add_argument("--bvh-walk", action="store_true", help="config 3 by BVH traversal only (rt_bvh)")
     args = ap.parse_args()
     import torch  # noqa: F401  (one HIP runtime)
     from skybox_rt_amd import rt
@@ -54,7 +55,7 @@ def main():
         sc = rt.Scene.load(args.scene) if any(k.startswith("RT_BVH_") for k in env) else scene
         r = rt.Renderer(sc, kernel_dir=lib if d == "default" else os.path.join(vdir, d))
         r.configure(args.size, args.size, shadows=not args.no_shadows, path=args.mode == "path",
-                    flat=args.mode == "flat", raster=args.mode == "raster", bounces=args.bounces,
+                    flat=args.mode == "flat", raster=args.mode == "raster", bounces=args.bounces, bvh_walk=args.bvh_walk,
                     counters=False)  # the timed product configuration
         r.render()  # the driver reads its launch env when it loads the image
         for k, v in saved.items():

@@ -18,22 +18,23 @@ sys.path.insert(0, ROOT)
 def main():
     size = int(sys.argv[1]) if len(sys.argv) > 1 else 1024
     path = len(sys.argv) > 2 and sys.argv[2] == "path"   # pt_kernel (variants/ptstamp)
+    bvh = len(sys.argv) > 2 and sys.argv[2] == "bvh"     # rt_bvh (variants/stamp): config 3 by BVH walks
     import torch  # noqa: F401
     from skybox_rt_amd import rt
     kdir = os.path.join(ROOT, "skybox_rt_amd/lib/variants", "ptstamp" if path else "stamp")
-    image = os.path.join(kdir, "pt_kernel.vxbin" if path else "rt_kernel.vxbin")
+    image = os.path.join(kdir, "pt_kernel.vxbin" if path else ("rt_bvh.vxbin" if bvh else "rt_kernel.vxbin"))
     if not os.path.exists(image):  # the renderer would fall back to the stamp-less product image
         sys.exit(f"wave_timeline: {image} missing (make -C skybox_rt_amd/csrc diag)")
     s = rt.Scene.load(os.path.join(ROOT, "tests/golden/scenes/tekkaman.cgltrace"))
     r = rt.Renderer(s, kernel_dir=kdir)
-    r.configure(size, size, shadows=True, path=path)
+    r.configure(size, size, shadows=True, path=path, bvh_walk=bvh)
     for _ in range(5):
         r.render()
     rows = r.launch_rows().astype(np.int64)
     kms = r.kernel_ms()
     # the same frame through the instrumented image: per-wave sums of the
     # lanes' node visits (slot 3 + RT_STAT_NODE_VISITS) and triangle tests
-    r.configure(size, size, shadows=True, path=path, instrumented=True)
+    r.configure(size, size, shadows=True, path=path, bvh_walk=bvh, instrumented=True)
     r.render()
     irows = r.launch_rows().astype(np.int64)
     base = rows[:, 12].min()

@@ -159,6 +159,9 @@ int run_seq(rt_renderer* r, rt_setup_arg_t& g, const Seq& q, uint32_t* launches)
   if (x.n > RTS_MAX_SEQ) return set_error("setup sequence too long");
   g.phases = 0;
   g.nseq = x.n;
+  // a launch's sub-phases side by side on slices of the grid (env RT_SETUP_PART=0: in turn)
+  const char* pe = std::getenv("RT_SETUP_PART");
+  g.part = (pe && std::atoi(pe) == 0) ? 0u : 1u;
   for (uint32_t i = 0; i < RTS_MAX_SEQ; ++i) g.seq_phases[i] = i < x.n ? x.ph[i] : 0u;
   if (ensure(r, sizeof(g), &r->su.args) != 0) return -1;
   const int rc = r->copy_async ? r->copy_async(r->su.args.h, &g, 0, sizeof(g))

@@ -229,7 +229,7 @@ typedef struct {
 // conservative, so any-hit over the list is the brute force's verdict.
 // Built on the device (rt_setup.hip SCOUNT .. SSORT); oracle/rt.c sl_build
 // restates it.
-#define RT_SLIST_N 256              // default cells per face side (the oracle's SL_N); A/B r03h: 128 0.02524 ms, 256 0.02476, 512 0.0259 (r03c)
+#define RT_SLIST_N 128              // default cells per face side (the oracle's SL_N); A/B r04g (nearest-first bounded lists): config 3 128 0.01836 / 256 0.0182 / 64 0.02072 ms, config 4 128 0.14286 / 256 0.14324; the lists build 4x fewer cells (set_light 0.137 -> 0.113 ms)
 #define RT_SLIST_EPS (1.0f / 512.0f)
 
 // ---- per-8x8-block candidate lists (primary visibility) -------------------

@@ -88,6 +88,11 @@ struct WaveLds {
 __shared__ uint4 s_geom[RT_FLAT_CAP];
 // RT_FLAT_SCALAR (A/B knob): no LDS staging, every rectangle word through
 // the scalar cache
+// RT_FLAT_BLOCK: entries against the chunk's 8x8 block, 64 per instruction,
+// before the per-pixel tests (flat_chunk); 0 = the one-level scan
+#ifndef RT_FLAT_BLOCK
+#define RT_FLAT_BLOCK 1
+#endif
 #ifndef RT_FLAT_SCALAR
 #define RT_FLAT_SCALAR 0
 #endif
@@ -259,6 +264,69 @@ __device__ __forceinline__ void flat_chunk(const vx_task_t& task, bool valid, co
   uint32_t bz = VX_OM_DEPTH_MASK;
   int32_t bp = -1;
   uint32_t k = k0;
+#if RT_FLAT_BLOCK
+  // Two levels: the wave's lanes take 64 of its entries at once and test
+  // each one's rectangle against the chunk's 8x8 block (packed corners:
+  // lo <= block hi and hi >= block lo, halfwise); then, for the entries that
+  // reach the block only, the per-pixel rectangle test and, where a lane
+  // lies in it, the edges and depth -- the records two at a time (one
+  // 64-B scalar load each, the second in flight while the first is tested).
+  // The same entries get the same tests as the one-level scan below (the
+  // block test only skips entries no pixel of the block lies in): identical
+  // winners and counts, with 1/64 of the rectangle-test instructions.  Wave w
+  // takes entries w, w + kWaves, ...: a region's triangles, often
+  // consecutive in the list, spread over the waves.
+  {
+    const uint32_t bx = (uint32_t)__builtin_amdgcn_readfirstlane(x) & ~7u;  // lane 0: the block's corner
+    const uint32_t by = (uint32_t)__builtin_amdgcn_readfirstlane(y) & ~7u;
+    const uint32_t blo = bx | (by << 16), bhi = (bx + 7u) | ((by + 7u) << 16);
+    const uint32_t mine = w < n ? (n - w + kWaves - 1) / kWaves : 0u;  // this wave's entries
+    for (uint32_t i = 0; i < mine; i += 64u) {
+      const uint32_t il = i + lane;
+      bool ov = false;
+      if (il < mine) {
+        const uint32_t kl = il * kWaves + w;
+        const uint4 C = lds ? lds[kl] : rect_corners(S.A.ld_u4(S.vgeom + 64u * kl + 32u));
+        // max(lo, block hi) == block hi and min(hi, block lo) == block lo
+        ov = rect2_clamp(C.y, 0xffffffffu, bhi) == bhi && rect2_clamp(0u, C.z, blo) == blo;
+      }
+      uint64_t m = __ballot(ov);
+#ifdef RT_INSTRUMENT
+      cnt.rect_tests += lane == 0 ? (mine - i < 64u ? mine - i : 64u) : 0u;
+#endif
+      while (m != 0) {
+        const uint32_t j0 = (uint32_t)__builtin_ctzll(m);
+        m &= m - 1;
+        const bool two = m != 0;
+        const uint32_t j1 = two ? (uint32_t)__builtin_ctzll(m) : j0;
+        if (two) m &= m - 1;
+        const uint32_t ka = (i + j0) * kWaves + w, kb = (i + j1) * kWaves + w;
+        uint4 ra[4], rb[4];
+        S.A.sld_u4n<4>(S.vgeom + 64u * ka, ra);
+        S.A.sld_u4n<4>(S.vgeom + 64u * kb, rb);
+        const uint4 Ca = rect_corners(ra[2]), Cb = rect_corners(rb[2]);
+        const bool ina = rect2_in(Ca.y, Ca.z, pp);
+        if (__ballot(ina) != 0) {  // wave-uniform
+#ifdef RT_INSTRUMENT
+          cnt.edge_tests += lane == 0 ? 1u : 0u;
+#endif
+          vis_test_in(ra[0], ra[1], ra[2], ra[3], ina, px, y, tie_high, bz, bp);
+        }
+        const bool inb = two && rect2_in(Cb.y, Cb.z, pp);
+        if (__ballot(inb) != 0) {
+#ifdef RT_INSTRUMENT
+          cnt.edge_tests += lane == 0 ? 1u : 0u;
+#endif
+          vis_test_in(rb[0], rb[1], rb[2], rb[3], inb, px, y, tie_high, bz, bp);
+        }
+      }
+    }
+#ifdef RT_INSTRUMENT
+    cnt.tests += in ? mine : 0u;  // the whole list per ray, summed over the waves
+#endif
+    k = k1;
+  }
+#endif
   // kFlatUnroll rectangle words in flight at once (their LDS reads
   // overlap), then the candidates among them in ascending order
   for (; k + kFlatUnroll <= k1; k += kFlatUnroll) {
@@ -297,12 +365,18 @@ __device__ __forceinline__ void flat_chunk(const vx_task_t& task, bool valid, co
     vis_test_in(flat_rec(S, lds, k, 0), flat_rec(S, lds, k, 1), C, flat_rec(S, lds, k, 3), inr, px,
                 y, tie_high, bz, bp);
   }
-#ifdef RT_INSTRUMENT
+#if defined(RT_INSTRUMENT) && !RT_FLAT_BLOCK
   cnt.tests += in ? k1 - k0 : 0u;  // the whole list per ray, summed over the waves
+#endif
+#ifdef RT_STAMPS  // 3: wave 0's list scan done, 4: the slowest wave's (after the barrier)
+  if (threadIdx.x == 0) __vx_mpm_lds[3] = (uint32_t)__builtin_amdgcn_s_memrealtime();
 #endif
   L.z[w][lane] = bz;
   L.pid[w][lane] = bp;
   __syncthreads();
+#ifdef RT_STAMPS
+  if (threadIdx.x == 0) __vx_mpm_lds[4] = (uint32_t)__builtin_amdgcn_s_memrealtime();
+#endif
   int32_t hit = -1;
   uint32_t hz = VX_OM_DEPTH_MASK;
   for (uint32_t i = 0; i < kWaves; ++i) {
@@ -318,6 +392,10 @@ __device__ __forceinline__ void flat_chunk(const vx_task_t& task, bool valid, co
     cnt.hits += hit >= 0;
     const int32_t spid = resolve_layers(S, x, y, in && hit < 0, hit, cnt);
     color = shade_wave(S, spid, x, y, S.clear_color, cnt);
+#ifdef RT_STAMPS  // 5: shaded (wave 0)
+    asm volatile("" : : "v"(color));  // the colour is complete before the stamp
+    if (threadIdx.x == 0) __vx_mpm_lds[5] = (uint32_t)__builtin_amdgcn_s_memrealtime();
+#endif
   }
   Ray r;
   primary_dir(S, x, y, r);
@@ -389,6 +467,9 @@ VX_MAIN(rt_kernel_arg_t, arg, RT_BLOCK_THREADS) {
       s_geom[i] = rect_corners(S.A.ld_u4(S.vgeom + 64u * i + 32u));
   }
   __syncthreads();
+#ifdef RT_STAMPS  // 11: list staged
+  if (threadIdx.x == 0) __vx_mpm_lds[11] = (uint32_t)__builtin_amdgcn_s_memrealtime();
+#endif
   __shared__ FlatLds s_flat;
   (void)w;
   const int rc = vx_spawn_chunks_block(

@@ -151,10 +151,17 @@ __device__ void prim_setup(const float* v, uint32_t dc, float zn, float zf, uint
 }
 
 // --- sub-phases -------------------------------------------------------------
+// Every wide sub-phase is a grid-stride loop over a slice of the launch's
+// workgroups: slice_b() = this workgroup's index in the slice, slice_n() = the slice's
+// size (run_phases: the sub-phases of one launch run side by side on
+// disjoint slices, or all on the whole grid one after the other).
+__shared__ uint32_t s_slice[2];
+__device__ __forceinline__ uint32_t slice_b() { return s_slice[0]; }
+__device__ __forceinline__ uint32_t slice_n() { return s_slice[1]; }
 
 __device__ void phase_fill(const rt_setup_arg_t* a) {
-  const uint64_t gid = (uint64_t)blockIdx.x * RTS_BLOCK + threadIdx.x;
-  const uint64_t gstride = (uint64_t)gridDim.x * RTS_BLOCK;
+  const uint64_t gid = (uint64_t)slice_b() * RTS_BLOCK + threadIdx.x;
+  const uint64_t gstride = (uint64_t)slice_n() * RTS_BLOCK;
   for (uint32_t f = 0; f < a->nfills && f < RTS_MAX_FILLS; ++f) {
     const rts_fill_t fl = a->fills[f];
     uint32_t* dst = vx_ptr<uint32_t>(fl.addr);
@@ -181,7 +188,7 @@ __device__ void phase_primvis(const rt_setup_arg_t* a) {
   uint4* vis = vx_ptr<uint4>(a->vis_addr);
   const uint32_t W = a->width, H = a->height, l = lane_id(), wv = threadIdx.x >> 6;
   __shared__ uint32_t red[RTS_BLOCK / 64][5];
-  for (uint32_t g = blockIdx.x; g < a->num_prims; g += gridDim.x) {
+  for (uint32_t g = slice_b(); g < a->num_prims; g += slice_n()) {
     float v[30];
     const float4* src = reinterpret_cast<const float4*>(verts + 32ull * g);
 #pragma unroll
@@ -315,7 +322,7 @@ __device__ void phase_vtris(const rt_setup_arg_t* a) {
   uint32_t* status = vx_ptr<uint32_t>(a->status_addr);
   const uint32_t nt = a->num_tris + 3, nl = a->num_layers, ng = a->num_geom;
   const uint32_t total = nt + nl + ng;
-  for (uint32_t i = blockIdx.x * RTS_BLOCK + threadIdx.x; i < total; i += gridDim.x * RTS_BLOCK) {
+  for (uint32_t i = slice_b() * RTS_BLOCK + threadIdx.x; i < total; i += slice_n() * RTS_BLOCK) {
     int32_t pid;
     rt_vtri_t* out;
     if (i < nt) {
@@ -406,7 +413,7 @@ __device__ void phase_link(const rt_setup_arg_t* a) {
   uint32_t* status = vx_ptr<uint32_t>(a->status_addr);
   rt_vnode_t* vn = vx_ptr<rt_vnode_t>(a->vnodes_addr);
   const uint32_t nn = a->num_nodes;
-  for (uint32_t i = blockIdx.x * RTS_BLOCK + threadIdx.x; i < nn; i += gridDim.x * RTS_BLOCK) {
+  for (uint32_t i = slice_b() * RTS_BLOCK + threadIdx.x; i < nn; i += slice_n() * RTS_BLOCK) {
     int32_t r[4];
     node_refs(a, i, r);
     uint32_t nint = 0;
@@ -452,8 +459,8 @@ __device__ void phase_climb(const rt_setup_arg_t* a) {
   rt_vnode_t* vn = vx_ptr<rt_vnode_t>(a->vnodes_addr);
   uint32_t* status = vx_ptr<uint32_t>(a->status_addr);
   const uint32_t nn = a->num_nodes;
-  const uint32_t i0 = WG ? threadIdx.x : blockIdx.x * RTS_BLOCK + threadIdx.x;
-  const uint32_t step = WG ? RTS_BLOCK : gridDim.x * RTS_BLOCK;
+  const uint32_t i0 = WG ? threadIdx.x : slice_b() * RTS_BLOCK + threadIdx.x;
+  const uint32_t step = WG ? RTS_BLOCK : slice_n() * RTS_BLOCK;
   for (uint32_t i = i0; i < nn; i += step) {
     if (count[2 * i] != 0) continue;
     uint32_t cur = i;
@@ -503,7 +510,7 @@ __device__ void phase_weight(const rt_setup_arg_t* a) {
   const uint4* vis = vx_ptr<const uint4>(a->vis_addr);
   uint32_t* w = vx_ptr<uint32_t>(a->weight_addr);
   const uint32_t W1 = a->tiles_x + 1;
-  for (uint32_t j = blockIdx.x * RTS_BLOCK + threadIdx.x; j < a->num_geom; j += gridDim.x * RTS_BLOCK) {
+  for (uint32_t j = slice_b() * RTS_BLOCK + threadIdx.x; j < a->num_geom; j += slice_n() * RTS_BLOCK) {
     const uint4 v = vis[geometry[j]];
     if (!v.w) continue;
     const uint32_t tx0 = (v.x & 0xffffu) >> RT_TILE_LOG, tx1 = min((v.x >> 16) >> RT_TILE_LOG, a->tiles_x - 1);
@@ -541,14 +548,14 @@ __device__ __forceinline__ void prefix_strided(uint32_t* v, uint32_t n, uint32_t
 __device__ void phase_rowsum(const rt_setup_arg_t* a) {
   uint32_t* w = vx_ptr<uint32_t>(a->weight_addr);
   const uint32_t W1 = a->tiles_x + 1;
-  for (uint32_t r = blockIdx.x * RTS_BLOCK + threadIdx.x; r <= a->tiles_y; r += gridDim.x * RTS_BLOCK)
+  for (uint32_t r = slice_b() * RTS_BLOCK + threadIdx.x; r <= a->tiles_y; r += slice_n() * RTS_BLOCK)
     prefix_strided(w + r * W1, W1, 1u);
 }
 
 __device__ void phase_colsum(const rt_setup_arg_t* a) {
   uint32_t* w = vx_ptr<uint32_t>(a->weight_addr);
   const uint32_t W1 = a->tiles_x + 1;
-  for (uint32_t c = blockIdx.x * RTS_BLOCK + threadIdx.x; c < W1; c += gridDim.x * RTS_BLOCK)
+  for (uint32_t c = slice_b() * RTS_BLOCK + threadIdx.x; c < W1; c += slice_n() * RTS_BLOCK)
     prefix_strided(w + c, a->tiles_y + 1, W1);
 }
 
@@ -564,7 +571,7 @@ __device__ void phase_hist(const rt_setup_arg_t* a) {
   const uint32_t* w = vx_ptr<const uint32_t>(a->weight_addr);
   uint32_t* hist = vx_ptr<uint32_t>(a->hist_addr);
   __shared__ uint32_t h[256];
-  for (uint32_t b = blockIdx.x; b < a->nblocks; b += gridDim.x) {
+  for (uint32_t b = slice_b(); b < a->nblocks; b += slice_n()) {
     h[threadIdx.x] = 0;
     __syncthreads();
     for (uint32_t i = 0; i < RTS_ITEMS / RTS_BLOCK; ++i) {
@@ -592,7 +599,7 @@ __device__ void phase_scatter(const rt_setup_arg_t* a) {
   __shared__ uint32_t wcnt[kW][256];
   const uint32_t wv = threadIdx.x >> 6, l = lane_id();
   const uint64_t lt_mask = (l == 0) ? 0ull : (~0ull >> (64 - l));
-  for (uint32_t b = blockIdx.x; b < a->nblocks; b += gridDim.x) {
+  for (uint32_t b = slice_b(); b < a->nblocks; b += slice_n()) {
     base[threadIdx.x] = hist[threadIdx.x * a->nblocks + b];
     for (uint32_t i = 0; i < kW; ++i) wcnt[i][threadIdx.x] = 0;
     __syncthreads();
@@ -666,8 +673,8 @@ __device__ void phase_bcount(const rt_setup_arg_t* a) {
   const int32_t* geometry = vx_ptr<const int32_t>(a->geometry_addr);
   const uint4* vis = vx_ptr<const uint4>(a->vis_addr);
   uint32_t* bcnt = vx_ptr<uint32_t>(a->bcnt_addr);
-  const uint32_t waves = gridDim.x * (RTS_BLOCK / 64);
-  for (uint32_t j = blockIdx.x * (RTS_BLOCK / 64) + (threadIdx.x >> 6); j < a->num_geom; j += waves) {
+  const uint32_t waves = slice_n() * (RTS_BLOCK / 64);
+  for (uint32_t j = slice_b() * (RTS_BLOCK / 64) + (threadIdx.x >> 6); j < a->num_geom; j += waves) {
     const uint4 v = vis[geometry[j]];
     if (!v.w) continue;
     for_blocks(a, v, [&](uint32_t lb) { atomicAdd(&bcnt[lb], 1u); });
@@ -717,7 +724,7 @@ __device__ __forceinline__ ListSet cell_set(const rt_setup_arg_t* a) {
 // per RTS_BLOCKS_PER_PART lists: their entry sum -> part, the longest list -> *longest
 __device__ void phase_lsum(const ListSet& L) {
   constexpr uint32_t Q = RTS_BLOCKS_PER_PART / RTS_BLOCK;
-  for (uint32_t b = blockIdx.x; b < L.npart; b += gridDim.x) {
+  for (uint32_t b = slice_b(); b < L.npart; b += slice_n()) {
     uint32_t sum = 0, mx = 0;
     for (uint32_t q = 0; q < Q; ++q) {
       const uint32_t lb = b * RTS_BLOCKS_PER_PART + threadIdx.x * Q + q;
@@ -766,7 +773,7 @@ __device__ void phase_lscan(const ListSet& L) { scan_excl(L.part, L.npart, L.tot
 __device__ void phase_loff(const ListSet& L) {
   __shared__ uint32_t s[RTS_BLOCK];
   constexpr uint32_t Q = RTS_BLOCKS_PER_PART / RTS_BLOCK;
-  for (uint32_t b = blockIdx.x; b < L.npart; b += gridDim.x) {
+  for (uint32_t b = slice_b(); b < L.npart; b += slice_n()) {
     const uint32_t lb0 = b * RTS_BLOCKS_PER_PART + threadIdx.x * Q;
     uint32_t c[Q], sum = 0;
     for (uint32_t q = 0; q < Q; ++q) {
@@ -803,8 +810,8 @@ __device__ void phase_bfill(const rt_setup_arg_t* a) {
   const uint2* bidx = vx_ptr<const uint2>(a->bidx_addr);
   uint4* btmp = vx_ptr<uint4>(a->btmp_addr);
   uint32_t* status = vx_ptr<uint32_t>(a->status_addr);
-  const uint32_t waves = gridDim.x * (RTS_BLOCK / 64), cap = a->bcap;
-  for (uint32_t j = blockIdx.x * (RTS_BLOCK / 64) + (threadIdx.x >> 6); j < a->num_geom; j += waves) {
+  const uint32_t waves = slice_n() * (RTS_BLOCK / 64), cap = a->bcap;
+  for (uint32_t j = slice_b() * (RTS_BLOCK / 64) + (threadIdx.x >> 6); j < a->num_geom; j += waves) {
     const uint4 v = vis[geometry[j]];
     if (!v.w) continue;
     for_blocks(a, v, [&](uint32_t lb) {
@@ -823,11 +830,11 @@ __device__ void phase_bsort(const rt_setup_arg_t* a) {
   const uint2* bidx = vx_ptr<const uint2>(a->bidx_addr);
   const uint4* btmp = vx_ptr<const uint4>(a->btmp_addr);
   uint4* blist = vx_ptr<uint4>(a->blist_addr);
-  const uint32_t waves = gridDim.x * (RTS_BLOCK / 64), l = lane_id();
+  const uint32_t waves = slice_n() * (RTS_BLOCK / 64), l = lane_id();
   const uint32_t total = vx_ptr<const uint32_t>(a->status_addr)[2], cap = a->bcap;
-  if (blockIdx.x == 0 && threadIdx.x < RT_BLIST_PAD && total <= cap)  // padding entries (pairs loaded ahead)
+  if (slice_b() == 0 && threadIdx.x < RT_BLIST_PAD && total <= cap)  // padding entries (pairs loaded ahead)
     blist[total + threadIdx.x] = make_uint4(0u, RT_BLIST_PAD_LO, RT_BLIST_PAD_HI, RT_VIS_ZMIN_NONE);
-  for (uint32_t lb = blockIdx.x * (RTS_BLOCK / 64) + (threadIdx.x >> 6); lb < a->nblk; lb += waves) {
+  for (uint32_t lb = slice_b() * (RTS_BLOCK / 64) + (threadIdx.x >> 6); lb < a->nblk; lb += waves) {
     const uint2 oc = sload(bidx + lb);
     if (oc.x + oc.y > cap) continue;  // past the capacity (status[6]): the host refills
     for (uint32_t base = 0; base < oc.y; base += 64) {
@@ -980,7 +987,7 @@ __device__ void phase_sproj(const rt_setup_arg_t* a) {
   uint32_t* skey = vx_ptr<uint32_t>(a->skey_addr);
   const int N = (int)a->slist_n;
   const uint32_t items = 6u * a->num_geom;
-  for (uint32_t it = blockIdx.x * RTS_BLOCK + threadIdx.x; it < items; it += gridDim.x * RTS_BLOCK) {
+  for (uint32_t it = slice_b() * RTS_BLOCK + threadIdx.x; it < items; it += slice_n() * RTS_BLOCK) {
     const uint32_t j = it / 6u, f = it % 6u;
     const rt_tri_t r = geom[j];
     if (f == 0) skey[j] = __float_as_uint(sl_key(r, a->light));
@@ -1033,7 +1040,7 @@ __device__ __forceinline__ void sl_for_candidates(const rt_setup_arg_t* a, Fn f)
   const uint32_t items = 6u * a->num_geom, total = soff[items];
   const uint32_t N = a->slist_n;
   const float cw = 2.0f / (float)N;
-  for (uint32_t q = blockIdx.x * RTS_BLOCK + threadIdx.x; q < total; q += gridDim.x * RTS_BLOCK) {
+  for (uint32_t q = slice_b() * RTS_BLOCK + threadIdx.x; q < total; q += slice_n() * RTS_BLOCK) {
     uint32_t lo = 0, hi = items;  // the last item with soff <= q
     while (hi - lo > 1) {
       const uint32_t mid = (lo + hi) >> 1;
@@ -1103,14 +1110,14 @@ __device__ void phase_ssort(const rt_setup_arg_t* a) {
   const uint32_t cap = a->scap, total = status[5], n = min(total, cap);
   const uint32_t* tk = tj + cap;
   const uint32_t* tc = tj + 2u * cap;
-  if (blockIdx.x == 0 && threadIdx.x < 3 && total <= cap)  // padding record (the kernels load pairs ahead)
+  if (slice_b() == 0 && threadIdx.x < 3 && total <= cap)  // padding record (the kernels load pairs ahead)
     out[3ull * total + threadIdx.x] = make_uint4(0u, 0u, 0u, 0u);
-  if (blockIdx.x == 0 && threadIdx.x == 0 && a->rargs_addr) {
+  if (slice_b() == 0 && threadIdx.x == 0 && a->rargs_addr) {
     const bool fit = status[7] == 0 && status[4] <= a->max_list && total <= a->max_entries;
     __hip_atomic_store(&vx_ptr<rt_kernel_arg_t>(a->rargs_addr)->slist_on, fit ? 1u : 0u, __ATOMIC_RELAXED,
                        __HIP_MEMORY_SCOPE_AGENT);
   }
-  for (uint32_t e = blockIdx.x * RTS_BLOCK + threadIdx.x; e < n; e += gridDim.x * RTS_BLOCK) {
+  for (uint32_t e = slice_b() * RTS_BLOCK + threadIdx.x; e < n; e += slice_n() * RTS_BLOCK) {
     const uint32_t me = tj[e], mk = tk[e];
     const uint2 oc = sidx[tc[e]];
     if (oc.x + oc.y > cap) continue;  // the cell's list overflowed (status[7]): the host refills
@@ -1153,44 +1160,88 @@ __device__ void phase_records(const rt_setup_arg_t* a) {
   rt_tri_t* ptris = vx_ptr<rt_tri_t>(a->ptris_addr);
   rt_tri_t* geom = vx_ptr<rt_tri_t>(a->geom_addr);
   const uint32_t total = a->num_prims + a->num_geom;
-  for (uint32_t i = blockIdx.x * RTS_BLOCK + threadIdx.x; i < total; i += gridDim.x * RTS_BLOCK) {
+  for (uint32_t i = slice_b() * RTS_BLOCK + threadIdx.x; i < total; i += slice_n() * RTS_BLOCK) {
     if (i < a->num_prims) tri_record(verts, i, ptris + i);
     else tri_record(verts, (uint32_t)geometry[i - a->num_prims], geom + (i - a->num_prims));
   }
 }
 
-// the sub-phases of `ph` (each independent of the others in the same launch)
-__device__ void run_phases(const rt_setup_arg_t* arg, uint32_t ph) {
-  if (ph & RTS_FILL) phase_fill(arg);
-  if (ph & RTS_PRIMVIS) phase_primvis(arg);
-  if (ph & RTS_SPROJ) phase_sproj(arg);
-  if (ph & RTS_VTRIS) phase_vtris(arg);
-  if (ph & RTS_WEIGHT) phase_weight(arg);
-  if (ph & RTS_LINK) phase_link(arg);
-  if (ph & RTS_ROWSUM) phase_rowsum(arg);
-  if ((ph & RTS_CLIMB) && arg->num_nodes > RTS_CLIMB_WG_NODES) phase_climb<false>(arg);
-  if (ph & RTS_COLSUM) phase_colsum(arg);
-  if (ph & RTS_HIST) phase_hist(arg);
-  if (ph & RTS_SCATTER) phase_scatter(arg);
-  if (ph & RTS_RECORDS) phase_records(arg);
-  if (ph & RTS_BCOUNT) phase_bcount(arg);
-  if (ph & RTS_BSUM) phase_lsum(block_set(arg));
-  if (ph & RTS_BOFF) phase_loff(block_set(arg));
-  if (ph & RTS_BFILL) phase_bfill(arg);
-  if (ph & RTS_BSORT) phase_bsort(arg);
-  if (ph & RTS_SCOUNT) phase_scount(arg);
-  if (ph & RTS_SSUM) phase_lsum(cell_set(arg));
-  if (ph & RTS_SOFF) phase_loff(cell_set(arg));
-  if (ph & RTS_SFILL) phase_sfill(arg);
-  if (ph & RTS_SSORT) phase_ssort(arg);
+// one wide sub-phase (on this workgroup's slice, slice_b() / slice_n())
+__device__ void run_phase(const rt_setup_arg_t* arg, uint32_t bit) {
+  switch (bit) {
+    case RTS_FILL: phase_fill(arg); break;
+    case RTS_PRIMVIS: phase_primvis(arg); break;
+    case RTS_SPROJ: phase_sproj(arg); break;
+    case RTS_VTRIS: phase_vtris(arg); break;
+    case RTS_WEIGHT: phase_weight(arg); break;
+    case RTS_LINK: phase_link(arg); break;
+    case RTS_ROWSUM: phase_rowsum(arg); break;
+    case RTS_CLIMB: phase_climb<false>(arg); break;
+    case RTS_COLSUM: phase_colsum(arg); break;
+    case RTS_HIST: phase_hist(arg); break;
+    case RTS_SCATTER: phase_scatter(arg); break;
+    case RTS_RECORDS: phase_records(arg); break;
+    case RTS_BCOUNT: phase_bcount(arg); break;
+    case RTS_BSUM: phase_lsum(block_set(arg)); break;
+    case RTS_BOFF: phase_loff(block_set(arg)); break;
+    case RTS_BFILL: phase_bfill(arg); break;
+    case RTS_BSORT: phase_bsort(arg); break;
+    case RTS_SCOUNT: phase_scount(arg); break;
+    case RTS_SSUM: phase_lsum(cell_set(arg)); break;
+    case RTS_SOFF: phase_loff(cell_set(arg)); break;
+    case RTS_SFILL: phase_sfill(arg); break;
+    case RTS_SSORT: phase_ssort(arg); break;
+    default: break;
+  }
 }
-// the one-workgroup sub-phases of `ph` (scans), run by one workgroup
+// the wide sub-phases in run order, with their shares of a partitioned
+// launch's workgroups (the per-primitive scan of PRIMVIS and the per-entry
+// list phases carry the longest per-workgroup chains)
+__constant__ const uint32_t kWide[22][2] = {
+    {RTS_FILL, 2},   {RTS_PRIMVIS, 8}, {RTS_SPROJ, 3},  {RTS_VTRIS, 1},  {RTS_WEIGHT, 1},  {RTS_LINK, 3},
+    {RTS_ROWSUM, 1}, {RTS_CLIMB, 3},   {RTS_COLSUM, 1}, {RTS_HIST, 1},   {RTS_SCATTER, 2}, {RTS_RECORDS, 2},
+    {RTS_BCOUNT, 2}, {RTS_BSUM, 1},    {RTS_BOFF, 1},   {RTS_BFILL, 2},  {RTS_BSORT, 4},   {RTS_SCOUNT, 3},
+    {RTS_SSUM, 1},   {RTS_SOFF, 2},    {RTS_SFILL, 3},  {RTS_SSORT, 3}};
+// the wide sub-phases of `ph` (each independent of the others in the same
+// launch).  part: each on its own slice of the grid, in proportion to its
+// share, so they run side by side (a launch then takes about its longest
+// sub-phase instead of their sum); otherwise each on the whole grid in turn.
+__device__ void run_phases(const rt_setup_arg_t* arg, uint32_t ph, bool part) {
+  if ((ph & RTS_CLIMB) && arg->num_nodes <= RTS_CLIMB_WG_NODES) ph &= ~RTS_CLIMB;  // one workgroup: run_scans
+  uint32_t total = 0;
+  for (int i = 0; i < 22; ++i) total += (ph & kWide[i][0]) ? kWide[i][1] : 0u;
+  if (total == 0) return;
+  const uint32_t G = gridDim.x;
+  uint32_t cum = 0;
+  for (int i = 0; i < 22; ++i) {
+    const uint32_t bit = kWide[i][0];
+    if (!(ph & bit)) continue;
+    uint32_t b0 = 0, b1 = G;
+    if (part) {
+      b0 = (uint32_t)((uint64_t)G * cum / total);
+      cum += kWide[i][1];
+      b1 = (uint32_t)((uint64_t)G * cum / total);
+      if (b1 <= b0) b1 = b0 + 1;  // at least one workgroup (G >= the sub-phase count)
+      if (blockIdx.x < b0 || blockIdx.x >= b1) continue;
+    }
+    __syncthreads();  // the previous sub-phase's reads of the slice are done
+    if (threadIdx.x == 0) {
+      s_slice[0] = blockIdx.x - b0;
+      s_slice[1] = b1 - b0;
+    }
+    __syncthreads();
+    run_phase(arg, bit);
+  }
+}
+// the one-workgroup sub-phases of `ph` (scans): the k-th present one by
+// workgroup k, so the scans of one launch run side by side
 __device__ void run_scans(const rt_setup_arg_t* arg, uint32_t ph) {
-  if ((ph & RTS_CLIMB) && arg->num_nodes <= RTS_CLIMB_WG_NODES) { phase_climb<true>(arg); __syncthreads(); }
-  if (ph & RTS_SOSCAN) { phase_soscan(arg); __syncthreads(); }
-  if (ph & RTS_BSCAN) { phase_lscan(block_set(arg)); __syncthreads(); }
-  if (ph & RTS_SSCAN) { phase_lscan(cell_set(arg)); __syncthreads(); }
-  if (ph & RTS_SCAN) {
+  uint32_t k = 0;
+  if ((ph & RTS_CLIMB) && arg->num_nodes <= RTS_CLIMB_WG_NODES && blockIdx.x == k++) phase_climb<true>(arg);
+  if ((ph & RTS_SOSCAN) && blockIdx.x == k++) phase_soscan(arg);
+  if ((ph & RTS_BSCAN) && blockIdx.x == k++) phase_lscan(block_set(arg));
+  if ((ph & RTS_SSCAN) && blockIdx.x == k++) phase_lscan(cell_set(arg));
+  if ((ph & RTS_SCAN) && blockIdx.x == k++) {
     scan_excl(vx_ptr<uint32_t>(arg->hist_addr), 256u * arg->nblocks, nullptr);
     __syncthreads();
     // local tiles with weight > 0 = items whose digit is below 255 = the
@@ -1218,7 +1269,7 @@ __device__ __attribute__((used)) uint32_t __vx_grid_per_cu = 4;
 VX_MAIN_OCC(rt_setup_arg_t, arg, RTS_BLOCK, 4) {
   const uint32_t ph = arg->nseq == 0 ? arg->phases
                       : vx_launch_tag < RTS_MAX_SEQ ? arg->seq_phases[vx_launch_tag] : 0u;
-  run_phases(arg, ph);
-  if (blockIdx.x == 0) run_scans(arg, ph);
+  run_phases(arg, ph, arg->nseq != 0 && arg->part != 0);
+  run_scans(arg, ph);
   return 0;
 }

@@ -145,8 +145,10 @@ typedef struct {
   // launch sequences: the host enqueues nseq launches of this one argument
   // block back to back (no host wait between them), launch i with launch
   // tag i (vx_hip_set_launch_tag: the entry's kernel argument); launch i
-  // runs seq_phases[i] -- its one-workgroup phases (the scans) by workgroup 0
-  uint32_t nseq, pad1;
+  // runs seq_phases[i] -- its one-workgroup phases (the scans) by workgroups
+  // 0, 1, ..; part: a launch's wide sub-phases on disjoint slices of the grid
+  // (rt_setup.hip run_phases)
+  uint32_t nseq, part;
   uint32_t seq_phases[RTS_MAX_SEQ];
 
 } rt_setup_arg_t;
