@@ -619,6 +619,25 @@ __device__ __forceinline__ void lane_path(const vx_task_t& task, const Scene& S,
     return;
   }
   if (coop) {
+#if RT_PAIR_ADJ
+    // lanes 2p, 2p + 1 take pixel p's path (lane p); both trace it, lane 2p
+    // stores it
+    const bool hi = (lane_id() & 1u) != 0u;
+    const int src = (int)(lane_id() >> 1);
+    bool act = __shfl((int)path, src) != 0;
+    const bool own = act && !hi;
+    st.task = (uint32_t)__shfl((int)st.task, src);
+    st.alpha = (uint32_t)__shfl((int)st.alpha, src);
+    st.pid = __shfl(st.pid, src);
+    st.t = __shfl(st.t, src);
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+      st.o[k] = __shfl(st.o[k], src);
+      st.d[k] = __shfl(st.d[k], src);
+      st.T[k] = __shfl(st.T[k], src);
+    }
+    int32_t* pstack = hi ? stack - 1 : stack;  // the pair's stack: lane 2p's column
+#else
     // lane l + 32 takes lane l's path; both trace it, lane l stores it
     const bool hi = lane_id() >= 32u;
     const bool own = path && !hi;
@@ -634,6 +653,7 @@ __device__ __forceinline__ void lane_path(const vx_task_t& task, const Scene& S,
       st.T[k] = xlowf(st.T[k]);
     }
     int32_t* pstack = hi ? stack - 32 : stack;  // the pair's stack: lane l's column
+#endif
     for (uint32_t v = 0; act; ++v) act = path_step<1>(S, pstack, st, v, act, cnt, hi ? 1u : 0u);
     if (own) store_path_pixel(S, st);
     return;

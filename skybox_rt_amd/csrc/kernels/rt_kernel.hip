@@ -441,8 +441,19 @@ __device__ __forceinline__ void flush(int slot, uint32_t v) { vx_mpm_add(RT_MPM_
 // (DESIGN 4.1), so more resident waves win until the spills cost more.
 // (r02: capping occupancy lower with LDS padding cost +27 / +80 %.)  The
 // deep images (every layout, 32-entry stack) keep the compiler's choice.
+// The BVH-walk image (rt_bvh: packet walks, no lists) is better at 5
+// (A/B r04f: 5 0.03644 ms, 6 0.03676, 7 0.03768, 8 0.03752).
 #if !defined(RT_WAVES_PER_EU) && !RT_FLAT && RT_ONLY_BVH4H
+#if RT_BVH_WALK
+#define RT_WAVES_PER_EU 5
+#else
 #define RT_WAVES_PER_EU 7
+#endif
+#endif
+#if RT_FLAT
+// config 2: 4 workgroups per CU (1 024 of 256 threads: one per 256^2 chunk,
+// each staging the list once) -- A/B r04i: 0.01084 ms vs 0.01108 at 16/CU
+__device__ __attribute__((used)) uint32_t __vx_grid_per_cu = 4;
 #endif
 #ifdef RT_WAVES_PER_EU
 VX_MAIN_OCC(rt_kernel_arg_t, arg, RT_BLOCK_THREADS, RT_WAVES_PER_EU) {

@@ -707,17 +707,37 @@ __device__ __forceinline__ bool occluded_list(const Scene& S, const Ray& s, bool
 // visits, the order of the stack and the result are the per-lane walk's
 // (trace_impl / occluded_list), and so are the counters (visits counted by
 // the lower lane, tests by the lane that made them).
-// the partner's value (lane l <-> l ^ 32)
+// 1: node4_coop exchanges once and sorts the four children in both lanes
+// (0: the network split over the pair, three exchange rounds); needs the
+// stack's slack rows (RT_PUSH_UNCOND)
+#ifndef RT_COOP_LOCAL_SORT
+#define RT_COOP_LOCAL_SORT 1
+#endif
+// RT_PAIR_ADJ = 1: the pair is lanes 2p, 2p + 1 (one DPP quad_perm move per
+// exchange, fused into its consumer) instead of l, l ^ 32 (permlane32_swap)
+#ifndef RT_PAIR_ADJ
+#define RT_PAIR_ADJ 1
+#endif
+// the partner's value (lane l <-> l ^ 32, or l ^ 1 with RT_PAIR_ADJ)
 __device__ __forceinline__ uint32_t xpart(uint32_t v, bool hi) {
+#if RT_PAIR_ADJ
+  (void)hi;
+  return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0xB1, 0xF, 0xF, false);  // quad_perm [1,0,3,2]
+#else
   const auto r = __builtin_amdgcn_permlane32_swap(v, v, false, false);
   return hi ? r[0] : r[1];
+#endif
 }
 __device__ __forceinline__ float xpartf(float v, bool hi) {
   return __uint_as_float(xpart(__float_as_uint(v), hi));
 }
 // the lower lane's value in both lanes of the pair
 __device__ __forceinline__ uint32_t xlow(uint32_t v) {
+#if RT_PAIR_ADJ
+  return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0xA0, 0xF, 0xF, false);  // quad_perm [0,0,2,2]
+#else
   return __builtin_amdgcn_permlane32_swap(v, v, false, false)[0];
+#endif
 }
 __device__ __forceinline__ float xlowf(float v) { return __uint_as_float(xlow(__float_as_uint(v))); }
 
@@ -754,6 +774,41 @@ __device__ __forceinline__ int32_t node4_coop(const Scene& S, uint32_t ref, cons
     k[i] = h ? fminf(tn, 3.402823466e38f) : __builtin_inff();
     nh += h ? 1u : 0u;
   }
+#if RT_COOP_LOCAL_SORT && RT_PUSH_UNCOND
+  // One exchange round: both lanes take the partner's two keys and children
+  // (four independent swaps), then run the whole network of node4_step
+  // locally in slot order -- the same comparisons, so the same order, ties
+  // included -- and push without branches: each lane writes two rows, an
+  // entry past the hit count to the slack row RT_MAX_STACK (RT_PUSH_UNCOND).
+  {
+    const float pk0 = xpartf(k[0], hi), pk1 = xpartf(k[1], hi);
+    const int32_t pc0 = (int32_t)xpart((uint32_t)c[0], hi), pc1 = (int32_t)xpart((uint32_t)c[1], hi);
+    float K[4] = {hi ? pk0 : k[0], hi ? pk1 : k[1], hi ? k[0] : pk0, hi ? k[1] : pk1};
+    int32_t C[4] = {hi ? pc0 : c[0], hi ? pc1 : c[1], hi ? c[0] : pc0, hi ? c[1] : pc1};
+    auto cx = [&](int a, int b) {  // node4_step's compare-exchange: swap iff K[b] < K[a]
+      const bool s = K[b] < K[a];
+      const float ka = K[a], kb = K[b];
+      const int32_t ca = C[a], cb = C[b];
+      K[a] = s ? kb : ka; K[b] = s ? ka : kb;
+      C[a] = s ? cb : ca; C[b] = s ? ca : cb;
+    };
+    cx(0, 1); cx(2, 3); cx(0, 2); cx(1, 3); cx(1, 2);
+    const int n = (int)(nh + xpart(nh, hi));
+    if (n == 0) return RT_EMPTY_REF;
+    // entry C[j] at row sp + n - 1 - j (0 < j < n, below RT_MAX_STACK): the
+    // lower lane writes C[1], the upper C[2] and C[3]
+    auto row = [&](int j) {
+      const int rr = sp + n - 1 - j;
+      return (j < n && rr < RT_MAX_STACK) ? rr : RT_MAX_STACK;
+    };
+    const int ra = row(hi ? 2 : 1), rb = hi ? row(3) : RT_MAX_STACK;
+    mem[64 * ra] = hi ? C[2] : C[1];
+    mem[64 * rb] = C[3];
+    const int top = sp + n - 1;
+    sp = top < RT_MAX_STACK ? top : RT_MAX_STACK;
+    return C[0];
+  }
+#endif
   {  // cx(0,1) | cx(2,3)
     const bool s = k[1] < k[0];
     const float k0 = k[0], k1 = k[1];
