@@ -52,6 +52,17 @@ typedef int (*vx_hip_set_counters_t)(vx_device_h hdevice, int enable);
  * waits.  n = 0 abandons an open group after a failed launch inside it: the
  * launches already issued retire as one untimed run. */
 typedef int (*vx_hip_launch_group_t)(vx_device_h hdevice, uint32_t n);
+/* n | VX_HIP_GROUP_UNTIMED: the group runs without events (no timing, no
+ * idle gap an event costs) and may hold up to 64 / (VX_HIP_QUEUE_DEPTH +
+ * VX_HIP_TIME_EVERY) launches (10 by default) -- a stream-ordered sequence
+ * such as the RT app's device setup (app/device_setup.cpp run_seq) */
+#define VX_HIP_GROUP_UNTIMED 0x80000000u
+/* the device's pinned host buffer (up to 64 KiB, allocated on first use,
+ * freed with the device), mapped for the device: *host for the host,
+ * *device_addr (a raw 64-bit device pointer, not an arena address) for
+ * kernels.  A kernel's stores to it are visible once the host has waited for
+ * the run (vx_ready_wait): small results come back without a copy. */
+typedef int (*vx_hip_host_mem_t)(vx_device_h hdevice, uint64_t size, void** host, uint64_t* device_addr);
 /* timed (1, the default: HIP events on one run in VX_HIP_TIME_EVERY, queue
  * depth VX_HIP_QUEUE_DEPTH) or untimed (0: no events and no queue bound, so
  * back-to-back starts reach the GPU without the idle gap an event costs --

@@ -159,6 +159,15 @@ int run_seq(rt_renderer* r, rt_setup_arg_t& g, const Seq& q, uint32_t* launches)
   if (x.n > RTS_MAX_SEQ) return set_error("setup sequence too long");
   g.phases = 0;
   g.nseq = x.n;
+  // the last launch leaves the status words in pinned host memory (read_status)
+  g.status_host = 0;
+  g.status_nonce = 0;
+  r->stat_pending = 0;
+  if (r->stat_host && x.n >= 2) {
+    g.status_host = r->stat_dev;
+    g.status_nonce = ++r->stat_nonce;
+    r->stat_pending = g.status_nonce;
+  }
   // a launch's sub-phases side by side on slices of the grid (env RT_SETUP_PART=0: in turn)
   const char* pe = std::getenv("RT_SETUP_PART");
   g.part = (pe && std::atoi(pe) == 0) ? 0u : 1u;
@@ -168,9 +177,15 @@ int run_seq(rt_renderer* r, rt_setup_arg_t& g, const Seq& q, uint32_t* launches)
                                : vx_copy_to_dev(r->su.args.h, &g, 0, sizeof(g));
   if (rc != 0) return set_error("setup argument upload failed");
   if (!r->set_tag) return set_error("the driver has no vx_hip_set_launch_tag");
+  // one untimed run: no timing events between the steps (each costs the
+  // device ~5 us idle) and no queue bound stalling the host mid-sequence
+  // (the driver refuses groups longer than its slots allow: then one run each)
+  const bool grouped = r->launch_group && r->launch_group(r->dev, x.n | VX_HIP_GROUP_UNTIMED) == 0;
   for (uint32_t i = 0; i < x.n; ++i)
-    if (r->set_tag(r->dev, i) != 0 || vx_start(r->dev, r->setup_krnl, r->su.args.h) != 0)
+    if (r->set_tag(r->dev, i) != 0 || vx_start(r->dev, r->setup_krnl, r->su.args.h) != 0) {
+      if (grouped) r->launch_group(r->dev, 0);  // abandon the half-issued group
       return set_error("vx_start failed");
+    }
   *launches += x.n;
   if (trace)
     for (uint32_t i = 0; i < x.n; ++i)
@@ -179,6 +194,24 @@ int run_seq(rt_renderer* r, rt_setup_arg_t& g, const Seq& q, uint32_t* launches)
 }
 
 int read_status(rt_renderer* r, uint32_t st[RTS_STATUS_WORDS]) {
+  // the last sequence's copy in pinned host memory: wait for the device,
+  // then read it (no copy back); else the device words
+  if (r->stat_pending != 0) {
+    // the last launch stores the words, fences, then the nonce: spin on the
+    // nonce (a host-memory read; no device sync, no wake-up latency) -- the
+    // launch's own sub-phases may still run, later work is stream-ordered
+    const auto t0 = std::chrono::steady_clock::now();
+    bool seen = false;
+    while (!(seen = r->stat_host[RTS_STATUS_WORDS] == r->stat_pending)) {
+      if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(2)) break;
+      __builtin_ia32_pause();
+    }
+    if (!seen && vx_ready_wait(r->dev, VX_MAX_TIMEOUT) != 0) return set_error("vx_ready_wait failed");
+    if (seen || r->stat_host[RTS_STATUS_WORDS] == r->stat_pending) {
+      for (int i = 0; i < RTS_STATUS_WORDS; ++i) st[i] = r->stat_host[i];
+      return 0;
+    }
+  }
   if (vx_copy_from_dev(st, r->su.status.h, 0, RTS_STATUS_WORDS * 4) != 0)
     return set_error("vx_copy_from_dev failed");
   return 0;

@@ -295,6 +295,11 @@ int rt_renderer_create(rt_scene_h s, const char* kernel_dir, rt_renderer_h* out)
   r->set_timing = (vx_hip_set_timing_t)vx_driver_symbol("vx_hip_set_timing");
   r->copy_async = (vx_hip_copy_to_dev_async_t)vx_driver_symbol("vx_hip_copy_to_dev_async");
   r->set_tag = (vx_hip_set_launch_tag_t)vx_driver_symbol("vx_hip_set_launch_tag");
+  r->host_mem = (vx_hip_host_mem_t)vx_driver_symbol("vx_hip_host_mem");
+  if (r->host_mem) {
+    void* h = nullptr;
+    if (r->host_mem(r->dev, 64, &h, &r->stat_dev) == 0) r->stat_host = (volatile uint32_t*)h;
+  }
   // the two-kernel path tracer's images (binary16 BVH4 only; the others run
   // the one-kernel pt_kernel images), from the kernel directory itself: a
   // directory without them (e.g. lib/pt_compact) runs its own pt_kernel
@@ -1006,7 +1011,13 @@ int rt_renderer_configure(rt_renderer_h r, const rt_render_params_t* p) {
   } else {
     a.pathq_addr = a.pathq_ctr_addr = 0;
   }
-  if (upload(r->dev, &a, sizeof(a), &r->args, &args_addr)) return -1;
+  // the render arguments: one buffer for the renderer's life (its address,
+  // the launches' STARTUP_ARG, stays put), rewritten in stream order behind
+  // the setup just queued -- no wait for the device
+  if (!r->args && upload(r->dev, nullptr, sizeof(a), &r->args, &args_addr)) return -1;
+  if (r->copy_async ? r->copy_async(r->args, &a, 0, sizeof(a)) != 0
+                    : vx_copy_to_dev(r->args, &a, 0, sizeof(a)) != 0)
+    return fail("render argument upload failed");
   r->setup.device = device ? 1u : 0u;
   r->setup.launches = launches;
   r->setup.heavy_tiles = heavy;

@@ -75,6 +75,11 @@ struct rt_renderer {
   SetupScratch su;
   vx_hip_copy_to_dev_async_t copy_async = nullptr;
   vx_hip_set_launch_tag_t set_tag = nullptr;
+  vx_hip_host_mem_t host_mem = nullptr;
+  volatile uint32_t* stat_host = nullptr;  // pinned status words (+ nonce) of the setup sequences
+  uint64_t stat_dev = 0;
+  uint32_t stat_nonce = 0;
+  uint32_t stat_pending = 0;  // nonce of the last sequence issued with the pinned status copy (0: none)
   float sl_light[3] = {0, 0, 0};
   uint32_t sl_n = 0;        // the cube-map resolution they were built at
   bool sl_built = false;

@@ -212,15 +212,23 @@ struct PathState {
   int32_t pid;
   float t;
   float o[3], d[3], T[3], L[3];
+  float n[3];  // PT_CARRY_NRM (lane pairs): the vertex's normal, from the hit that made it
 };
+// 1: the pair form carries the vertex normal from the hit (path_hit has the
+// triangle loaded) instead of loading the triangle again at the next vertex
+#ifndef PT_CARRY_NRM
+#define PT_CARRY_NRM 0
+#endif
 
 // The next vertex of a path whose bounce ray b from P hit triangle np at t:
 // albedo = the draw3d shader at the hit's MT barycentrics, T *= albedo
+template <bool NRM = false>
 __device__ __forceinline__ void path_hit(const Scene& S, PathState& st, const float P[3], const Ray& b,
                                          int32_t np, float nt, Counters& cnt, bool counted = true) {
   float w0[3], f1[3], f2[3], b1, b2;
   load_tri(S, np, w0, f1, f2);
   mt_bary(b.o, b.d, w0, f1, f2, &b1, &b2);
+  if (NRM) tri_normal(f1, f2, b.d, st.n);  // the next vertex's normal (path_step's)
   gfx::Prim p;
   gfx::load_prim(S.A, S.prims + 128u * (uint32_t)np, p);
   const gfx::DcState dst = gfx::load_dcstate(S.A, S.dcs + 64u * p.dc());
@@ -273,9 +281,16 @@ __device__ __forceinline__ bool path_step(const Scene& S, int32_t* stack, PathSt
   const bool tie_high = (S.flags & RT_FLAG_TIE_HIGH) != 0;
   const bool hi = role != 0u;
   const uint32_t one = hi ? 0u : 1u;  // per-path counters: the group's first lane
-  float v0[3], e1[3], e2[3], nrm[3], P[3];
-  load_tri(S, act ? st.pid : 0, v0, e1, e2);
-  tri_normal(e1, e2, st.d, nrm);
+  constexpr bool kNrm = PT_CARRY_NRM && CO == 1;
+  float nrm[3], P[3];
+  if (kNrm) {
+#pragma unroll
+    for (int k = 0; k < 3; ++k) nrm[k] = st.n[k];
+  } else {
+    float v0[3], e1[3], e2[3];
+    load_tri(S, act ? st.pid : 0, v0, e1, e2);
+    tri_normal(e1, e2, st.d, nrm);
+  }
   const float tt = st.t * 0.999755859375f;
 #pragma unroll
   for (int k = 0; k < 3; ++k) P[k] = fmaf(st.d[k], tt, st.o[k]);
@@ -328,7 +343,7 @@ __device__ __forceinline__ bool path_step(const Scene& S, int32_t* stack, PathSt
     }
   }
   const uint64_t c2 = PT_CYC();
-  if (alive) path_hit(S, st, P, b, np, nt, cnt, !hi);
+  if (alive) path_hit<kNrm>(S, st, P, b, np, nt, cnt, !hi);
   if (CO) {
     PT_ACC(2, c2 - c1);           // cycles in the bounce walk (and its setup)
     PT_ACC(6, PT_CYC() - c2);     // cycles shading the bounce hit
@@ -637,6 +652,13 @@ __device__ __forceinline__ void lane_path(const vx_task_t& task, const Scene& S,
       st.T[k] = __shfl(st.T[k], src);
     }
     int32_t* pstack = hi ? stack - 1 : stack;  // the pair's stack: lane 2p's column
+#if PT_CARRY_NRM
+    {
+      float v0[3], e1[3], e2[3];
+      load_tri(S, act ? st.pid : 0, v0, e1, e2);
+      tri_normal(e1, e2, st.d, st.n);
+    }
+#endif
 #else
     // lane l + 32 takes lane l's path; both trace it, lane l stores it
     const bool hi = lane_id() >= 32u;

@@ -1269,6 +1269,19 @@ __device__ __attribute__((used)) uint32_t __vx_grid_per_cu = 4;
 VX_MAIN_OCC(rt_setup_arg_t, arg, RTS_BLOCK, 4) {
   const uint32_t ph = arg->nseq == 0 ? arg->phases
                       : vx_launch_tag < RTS_MAX_SEQ ? arg->seq_phases[vx_launch_tag] : 0u;
+  // the last launch of a sequence starts after every earlier one has
+  // finished, and its sub-phases write no status word: the status is final
+  // (one thread: the words, a system-scope fence, then the nonce the host
+  // polls for -- it may return before this launch's own sub-phases finish,
+  // which later work follows in stream order anyway)
+  if (arg->status_host != 0 && arg->nseq >= 2 && vx_launch_tag + 1 == arg->nseq && blockIdx.x == 0 &&
+      threadIdx.x == 0) {
+    volatile uint32_t* h = reinterpret_cast<volatile uint32_t*>(arg->status_host);
+    const volatile uint32_t* st = vx_ptr<const uint32_t>(arg->status_addr);
+    for (int i = 0; i < RTS_STATUS_WORDS; ++i) h[i] = st[i];
+    __threadfence_system();
+    h[RTS_STATUS_WORDS] = arg->status_nonce;
+  }
   run_phases(arg, ph, arg->nseq != 0 && arg->part != 0);
   run_scans(arg, ph);
   return 0;

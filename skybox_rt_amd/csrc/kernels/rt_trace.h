@@ -713,6 +713,11 @@ __device__ __forceinline__ bool occluded_list(const Scene& S, const Ray& s, bool
 #ifndef RT_COOP_LOCAL_SORT
 #define RT_COOP_LOCAL_SORT 1
 #endif
+// RT_COOP_LEAF_IL = 1: trace_coop's leaf triangles dealt 0, 2 | 1, 3 over the
+// pair instead of 0, 1 | 2, 3
+#ifndef RT_COOP_LEAF_IL
+#define RT_COOP_LEAF_IL 1
+#endif
 // RT_PAIR_ADJ = 1: the pair is lanes 2p, 2p + 1 (one DPP quad_perm move per
 // exchange, fused into its consumer) instead of l, l ^ 32 (permlane32_swap)
 #ifndef RT_PAIR_ADJ
@@ -748,9 +753,16 @@ __device__ __forceinline__ float xlowf(float v) { return __uint_as_float(xlow(__
 // push_sorted gives them (the lower lane writes c[1], the upper c[2], c[3]),
 // the nearest returned to both lanes.  `mem` / `sp`: the pair's stack (the
 // lower lane's LDS column).
+// RT_COOP_TOPREG = 1 (local sort only): the pair keeps its stack's top entry
+// in a register (`top`, row sp - 1 of the logical stack): a pop takes it at
+// once and refills it from LDS off the critical path; a push spills the old
+// top.  The logical stack -- rows, order, depth -- is unchanged.
+#ifndef RT_COOP_TOPREG
+#define RT_COOP_TOPREG 0
+#endif
 template <bool SCALAR>
 __device__ __forceinline__ int32_t node4_coop(const Scene& S, uint32_t ref, const Ray& r, float lim,
-                                              bool hi, int32_t* mem, int& sp) {
+                                              bool hi, int32_t* mem, int& sp, int32_t& top) {
   auto ld = [&](uint32_t o) { return SCALAR ? S.A.sld_f4(o) : S.A.ld_f4(o); };
   const uint32_t no = S.nodes4 + 128u * S.num_nodes4 + 64u * ref;
   const float4 px = ld(no), py = ld(no + 16), pz = ld(no + 32), cf = ld(no + 48);
@@ -801,11 +813,24 @@ __device__ __forceinline__ int32_t node4_coop(const Scene& S, uint32_t ref, cons
       const int rr = sp + n - 1 - j;
       return (j < n && rr < RT_MAX_STACK) ? rr : RT_MAX_STACK;
     };
+#if RT_COOP_TOPREG
+    // rows: the old top back to sp - 1 (lower lane, when the push is not
+    // empty and the stack was not), C[2] (lower) and C[3] (upper) to theirs;
+    // C[1] becomes the top
+    const bool spill = n >= 2 && sp > 0 && sp - 1 < RT_MAX_STACK;
+    const int ra = hi ? row(3) : (spill ? sp - 1 : RT_MAX_STACK), rb = hi ? RT_MAX_STACK : row(2);
+    mem[64 * ra] = hi ? C[3] : top;
+    mem[64 * rb] = C[2];
+    if (n >= 2) top = C[1];
+    (void)row;
+#else
+    (void)top;
     const int ra = row(hi ? 2 : 1), rb = hi ? row(3) : RT_MAX_STACK;
     mem[64 * ra] = hi ? C[2] : C[1];
     mem[64 * rb] = C[3];
-    const int top = sp + n - 1;
-    sp = top < RT_MAX_STACK ? top : RT_MAX_STACK;
+#endif
+    const int nt = sp + n - 1;
+    sp = nt < RT_MAX_STACK ? nt : RT_MAX_STACK;
     return C[0];
   }
 #endif
@@ -833,14 +858,15 @@ __device__ __forceinline__ int32_t node4_coop(const Scene& S, uint32_t ref, cons
     if (hi) { c[0] = s ? pc : c[0]; }
     else { c[1] = s ? pc : c[1]; }
   }
+  (void)top;
   const int n = (int)(nh + xpart(nh, hi));
   if (n == 0) return RT_EMPTY_REF;
   // entry c[j] at row sp + n - 1 - j (j < n, below RT_MAX_STACK)
   const int r0 = sp + n - (hi ? 3 : 2), r1 = sp + n - 4;
   if (r0 >= sp && r0 < RT_MAX_STACK) mem[64 * r0] = hi ? c[0] : c[1];
   if (hi && r1 >= sp && r1 < RT_MAX_STACK) mem[64 * r1] = c[1];
-  const int top = sp + n - 1;
-  sp = top < RT_MAX_STACK ? top : RT_MAX_STACK;
+  const int nt = sp + n - 1;
+  sp = nt < RT_MAX_STACK ? nt : RT_MAX_STACK;
   return (int32_t)xlow((uint32_t)c[0]);
 }
 
@@ -850,14 +876,21 @@ __device__ __forceinline__ int32_t trace_coop(const Scene& S, const Ray& r, int3
                                               float* t_out, int32_t* mem, bool hi, Counters& cnt) {
   if (S.num_nodes == 0) return -1;
   int sp = 0;
+  int32_t top = RT_EMPTY_REF;  // RT_COOP_TOPREG: the stack's top entry
   float bt = INFINITY;
   int32_t bpid = -1;
   RT_CNT(cnt.visits += hi ? 0u : 1u;)
-  int32_t ref = node4_coop<true>(S, 0u, r, bt, hi, mem, sp);
+  int32_t ref = node4_coop<true>(S, 0u, r, bt, hi, mem, sp, top);
   if (ref == RT_EMPTY_REF) return -1;
   auto pop = [&](int32_t& x) {
     if (sp == 0) return false;
+#if RT_COOP_TOPREG && RT_COOP_LOCAL_SORT && RT_PUSH_UNCOND
+    x = top;
+    --sp;
+    top = mem[64 * (sp > 0 ? sp - 1 : RT_MAX_STACK)];  // refill (a slack row when empty)
+#else
     x = mem[64 * --sp];
+#endif
     return true;
   };
   for (;;) {
@@ -867,7 +900,7 @@ __device__ __forceinline__ int32_t trace_coop(const Scene& S, const Ray& r, int3
       while (ref >= 0) {  // while-while, as trace_impl
         RT_WAVE_ITER(9);
         RT_CNT(cnt.visits += hi ? 0u : 1u;)
-        const int32_t nx = node4_coop<false>(S, (uint32_t)ref, r, bt, hi, mem, sp);
+        const int32_t nx = node4_coop<false>(S, (uint32_t)ref, r, bt, hi, mem, sp, top);
         if (nx != RT_EMPTY_REF) { ref = nx; continue; }
         if (!pop(ref)) { dry = true; break; }
       }
@@ -878,18 +911,24 @@ __device__ __forceinline__ int32_t trace_coop(const Scene& S, const Ray& r, int3
       RT_WAVE_ITER(9);  // this lane's two of the leaf's (up to 4) triangles (padding records past the end)
       const uint32_t lr = (uint32_t)ref;
       const uint32_t first = (lr >> 4) & 0x07ffffffu, count = (lr & 15u) + 1u;
-      const uint32_t k0 = hi ? 2u : 0u;
+#if RT_COOP_LEAF_IL
+      // the lower lane triangles 0 and 2, the upper 1 and 3: a two-triangle
+      // leaf is one test per lane
+      const uint32_t k0 = hi ? 1u : 0u, ks = 2u;
+#else
+      const uint32_t k0 = hi ? 2u : 0u, ks = 1u;
+#endif
       const uint32_t to = S.tris + 48u * (first + k0);
       float4 ta[2], tb[2], tc[2];
 #pragma unroll
       for (uint32_t k = 0; k < 2; ++k) {
-        ta[k] = S.A.ld_f4(to + 48u * k);
-        tb[k] = S.A.ld_f4(to + 48u * k + 16);
-        tc[k] = S.A.ld_f4(to + 48u * k + 32);
+        ta[k] = S.A.ld_f4(to + 48u * ks * k);
+        tb[k] = S.A.ld_f4(to + 48u * ks * k + 16);
+        tc[k] = S.A.ld_f4(to + 48u * ks * k + 32);
       }
 #pragma unroll
       for (uint32_t k = 0; k < 2; ++k) {
-        if (k0 + k < count) {
+        if (k0 + ks * k < count) {
           const int32_t pid = __float_as_int(ta[k].w);
           RT_CNT(++cnt.tests;)
           float t;

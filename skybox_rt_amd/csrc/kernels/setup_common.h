@@ -150,5 +150,10 @@ typedef struct {
   // (rt_setup.hip run_phases)
   uint32_t nseq, part;
   uint32_t seq_phases[RTS_MAX_SEQ];
+  // the sequence's last launch copies the status words, then status_nonce,
+  // to this pinned host buffer (a raw device pointer; 0 = none): the host
+  // reads them there after waiting for the sequence
+  uint64_t status_host;
+  uint32_t status_nonce, pad2;
 
 } rt_setup_arg_t;

@@ -157,6 +157,7 @@ class vx_device {
     for (int i = 0; i < kStageSlots; ++i)
       if (stage_ev_[i]) (void)hipEventDestroy(stage_ev_[i]);
     if (stage_) (void)hipHostFree(stage_);
+    if (hostmem_) (void)hipHostFree(hostmem_);
     if (stream_) (void)hipStreamDestroy(stream_);
     if (arena_) (void)hipFree(arena_);
   }
@@ -352,7 +353,8 @@ class vx_device {
     // launch, the stop event on its last.
     const bool first = group_pos_ == 0, last = group_pos_ + 1 == group_n_;
     if (first) {
-      group_timed_ = launch_mode_ != 2 && (issued_ == retired_ || runs_issued_ % time_every_ == 0);
+      group_timed_ = !group_untimed_ && launch_mode_ != 2 &&
+                     (issued_ == retired_ || runs_issued_ % time_every_ == 0);
       group_slot_ = slot;
       group_mods_.clear();
       ++runs_issued_;
@@ -363,7 +365,10 @@ class vx_device {
     group_last_[slot] = last;
     group_first_slot_[slot] = group_slot_;
     group_pos_ = last ? 0 : group_pos_ + 1;
-    if (last) group_n_ = 1;  // a group covers the launches it was declared for
+    if (last) {  // a group covers the launches it was declared for
+      group_n_ = 1;
+      group_untimed_ = false;
+    }
     if (!timed) {
       HIP_CHECK(hipExtModuleLaunchKernel(m->entry, m->grid * m->block, 1, 1, m->block, 1, 1, 0,
                                          stream_, kparams, nullptr, nullptr, nullptr, 0));
@@ -507,6 +512,8 @@ class vx_device {
   // n = 0 abandons an open group (a launch inside it failed): the launches
   // already issued retire as one untimed run, and single launches resume.
   int launch_group(uint32_t n) {
+    const bool untimed = (n & VX_HIP_GROUP_UNTIMED) != 0;
+    n &= ~VX_HIP_GROUP_UNTIMED;
     if (n == 0) {
       if (group_pos_ != 0) {
         const int slot = (int)((issued_ + kMaxQueue - 1) % kMaxQueue);
@@ -515,14 +522,33 @@ class vx_device {
       }
       group_pos_ = 0;
       group_n_ = 1;
+      group_untimed_ = false;
       return 0;
     }
-    if (n > 4 || group_pos_ != 0) return -1;  // not inside a group
+    if ((n > 4 && !untimed) || group_pos_ != 0) return -1;  // not inside a group
     if ((uint64_t)(depth_ + time_every_) * n > (uint64_t)kMaxQueue) return -1;
     group_n_ = n;
+    group_untimed_ = untimed;
     return 0;
   }
   void set_launch_tag(uint32_t tag) { launch_tag_ = tag; }  // the next start()'s kernel argument
+  // one pinned host buffer mapped into the device's address space (allocated
+  // on first use, at most 64 KiB): kernels store to it, the host reads it
+  // after waiting for the device -- no copy back
+  int host_mem(uint64_t size, void** host, uint64_t* dev) {
+    if (size == 0 || size > 65536) return -1;
+    if (hostmem_ && size > hostmem_size_) return -1;
+    if (!hostmem_) {
+      HIP_CHECK(hipHostMalloc(&hostmem_, 65536, hipHostMallocMapped));
+      hostmem_size_ = 65536;
+      std::memset(hostmem_, 0, 65536);
+    }
+    void* d = nullptr;
+    HIP_CHECK(hipHostGetDevicePointer(&d, hostmem_, 0));
+    *host = hostmem_;
+    *dev = (uint64_t)(uintptr_t)d;
+    return 0;
+  }
   bool counters() const { return counters_ || counters_env_; }
   void* mem_ptr(uint64_t addr) { return arena_ + addr; }
   hipStream_t stream() const { return stream_; }
@@ -621,6 +647,8 @@ class vx_device {
   static constexpr int kStageSlots = 64;
   static constexpr uint64_t kStageSlot = 4096;
   uint8_t* stage_ = nullptr;
+  void* hostmem_ = nullptr;  // vx_hip_host_mem: pinned, device-mapped words
+  uint64_t hostmem_size_ = 0;
   hipEvent_t stage_ev_[kStageSlots] = {};
   bool stage_busy_[kStageSlots] = {};
   uint64_t stage_next_ = 0;
@@ -638,6 +666,7 @@ class vx_device {
     bool rows;
   };
   uint32_t group_n_ = 1, group_pos_ = 0;
+  bool group_untimed_ = false;  // the declared group runs without events
   uint64_t runs_issued_ = 0;
   bool group_timed_ = false;
   int group_slot_ = 0;
@@ -817,6 +846,11 @@ __attribute__((visibility("default"))) int vx_hip_copy_to_dev_async(vx_buffer_h 
   auto* b = (vx_buffer*)hbuf;
   if (off + size > b->size) return -1;
   return b->device->upload_async(b->addr + off, src, size);
+}
+__attribute__((visibility("default"))) int vx_hip_host_mem(vx_device_h hdevice, uint64_t size, void** host,
+                                                           uint64_t* device_addr) {
+  if (hdevice == nullptr || host == nullptr || device_addr == nullptr) return -1;
+  return ((vx_device*)hdevice)->host_mem(size, host, device_addr);
 }
 __attribute__((visibility("default"))) int vx_hip_set_launch_tag(vx_device_h hdevice, uint32_t tag) {
   if (hdevice == nullptr) return -1;
