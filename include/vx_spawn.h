@@ -137,6 +137,10 @@ struct vx_arena {
   __device__ __forceinline__ uint32_t ld_u32(uint32_t off) const {
     return __builtin_amdgcn_raw_buffer_load_b32(r, off, 0, 0);
   }
+  __device__ __forceinline__ uint2 ld_u2(uint32_t off) const {
+    const auto v = __builtin_amdgcn_raw_buffer_load_b64(r, off, 0, 0);
+    return make_uint2(v[0], v[1]);
+  }
   __device__ __forceinline__ uint32_t ld_u16(uint32_t off) const {
     return __builtin_amdgcn_raw_buffer_load_b16(r, off, 0, 0);
   }

@@ -22,12 +22,16 @@
 namespace rtapp {
 namespace {
 
-// one setup launch (renderer creation): argument block, start, wait
-int run(rt_renderer* r, DevBuf* argb, const rt_setup_arg_t& a, uint32_t* launches) {
+int ensure(rt_renderer* r, uint64_t bytes, DevScratch* d);
+
+// one setup launch (renderer creation): argument block, start, wait -- in
+// the buffer the configure sequences use, so their first launch finds the
+// image's start arguments unchanged (no constant re-upload before it)
+int run(rt_renderer* r, vx_buffer_h argb, const rt_setup_arg_t& a, uint32_t* launches) {
   static const bool trace = std::getenv("RT_SETUP_TRACE") != nullptr;  // per-launch phases to stderr
   const auto t0 = std::chrono::steady_clock::now();
-  if (vx_copy_to_dev(argb->h, &a, 0, sizeof(a)) != 0) return set_error("vx_copy_to_dev failed");
-  if (vx_start(r->dev, r->setup_krnl, argb->h) != 0) return set_error("vx_start failed");
+  if (vx_copy_to_dev(argb, &a, 0, sizeof(a)) != 0) return set_error("vx_copy_to_dev failed");
+  if (vx_start(r->dev, r->setup_krnl, argb) != 0) return set_error("vx_start failed");
   if (vx_ready_wait(r->dev, VX_MAX_TIMEOUT) != 0) return set_error("vx_ready_wait failed");
   ++*launches;
   if (trace)
@@ -38,10 +42,6 @@ int run(rt_renderer* r, DevBuf* argb, const rt_setup_arg_t& a, uint32_t* launche
 
 int alloc(rt_renderer* r, uint64_t bytes, vx_buffer_h* h, uint64_t* addr) {
   return upload(r->dev, nullptr, bytes, h, addr);
-}
-
-int alloc_tmp(rt_renderer* r, uint64_t bytes, DevBuf* b, const void* init = nullptr) {
-  return upload(r->dev, init, bytes, &b->h, &b->addr);
 }
 
 void base_arg(const rt_renderer* r, rt_setup_arg_t* g) {
@@ -102,10 +102,9 @@ int device_ingest(rt_renderer* r, bool records) {
   g.phases = RTS_RECORDS;
   g.ptris_addr = a.ptris_addr;
   g.geom_addr = a.geom_addr;
-  DevBuf argb;
   uint32_t launches = 0;
-  if (alloc_tmp(r, sizeof(g), &argb)) return -1;
-  return run(r, &argb, g, &launches);
+  if (ensure(r, sizeof(g), &r->su.args) != 0) return -1;
+  return run(r, r->su.args.h, g, &launches);
 }
 
 namespace {

@@ -713,6 +713,11 @@ __device__ __forceinline__ bool occluded_list(const Scene& S, const Ray& s, bool
 #ifndef RT_COOP_LOCAL_SORT
 #define RT_COOP_LOCAL_SORT 1
 #endif
+// RT_COOP_HALF_LOADS = 1: node4_coop's lanes load only their half of a node
+// (6 dword + 1 dword-pair loads) instead of all 64 B and a select per word
+#ifndef RT_COOP_HALF_LOADS
+#define RT_COOP_HALF_LOADS 1
+#endif
 // RT_COOP_LEAF_IL = 1: trace_coop's leaf triangles dealt 0, 2 | 1, 3 over the
 // pair instead of 0, 1 | 2, 3
 #ifndef RT_COOP_LEAF_IL
@@ -765,17 +770,30 @@ __device__ __forceinline__ int32_t node4_coop(const Scene& S, uint32_t ref, cons
                                               bool hi, int32_t* mem, int& sp, int32_t& top) {
   auto ld = [&](uint32_t o) { return SCALAR ? S.A.sld_f4(o) : S.A.ld_f4(o); };
   const uint32_t no = S.nodes4 + 128u * S.num_nodes4 + 64u * ref;
-  const float4 px = ld(no), py = ld(no + 16), pz = ld(no + 32), cf = ld(no + 48);
   auto h2 = [](float w, float& a, float& b) {
     const uint32_t u = __float_as_uint(w);
     a = (float)__builtin_bit_cast(_Float16, (uint16_t)(u & 0xffffu));
     b = (float)__builtin_bit_cast(_Float16, (uint16_t)(u >> 16));
   };
   float lx[2], hx[2], ly[2], hy[2], lz[2], hz[2];
-  h2(hi ? px.y : px.x, lx[0], lx[1]); h2(hi ? px.w : px.z, hx[0], hx[1]);
-  h2(hi ? py.y : py.x, ly[0], ly[1]); h2(hi ? py.w : py.z, hy[0], hy[1]);
-  h2(hi ? pz.y : pz.x, lz[0], lz[1]); h2(hi ? pz.w : pz.z, hz[0], hz[1]);
-  int32_t c[2] = {__float_as_int(hi ? cf.z : cf.x), __float_as_int(hi ? cf.w : cf.y)};
+  int32_t c[2];
+  if (RT_COOP_HALF_LOADS && !SCALAR) {
+    // each lane loads only its half: the planes of children 0-1 (lower
+    // lane) or 2-3 (upper) are every other dword, the child refs a pair
+    const uint32_t hb = no + (hi ? 4u : 0u);
+    const auto f = [&](uint32_t o) { return __uint_as_float(S.A.ld_u32(hb + o)); };
+    const uint2 cc = S.A.ld_u2(no + 48u + (hi ? 8u : 0u));
+    h2(f(0), lx[0], lx[1]); h2(f(8), hx[0], hx[1]);
+    h2(f(16), ly[0], ly[1]); h2(f(24), hy[0], hy[1]);
+    h2(f(32), lz[0], lz[1]); h2(f(40), hz[0], hz[1]);
+    c[0] = (int32_t)cc.x; c[1] = (int32_t)cc.y;
+  } else {
+    const float4 px = ld(no), py = ld(no + 16), pz = ld(no + 32), cf = ld(no + 48);
+    h2(hi ? px.y : px.x, lx[0], lx[1]); h2(hi ? px.w : px.z, hx[0], hx[1]);
+    h2(hi ? py.y : py.x, ly[0], ly[1]); h2(hi ? py.w : py.z, hy[0], hy[1]);
+    h2(hi ? pz.y : pz.x, lz[0], lz[1]); h2(hi ? pz.w : pz.z, hz[0], hz[1]);
+    c[0] = __float_as_int(hi ? cf.z : cf.x); c[1] = __float_as_int(hi ? cf.w : cf.y);
+  }
   float k[2];
   uint32_t nh = 0;
 #pragma unroll

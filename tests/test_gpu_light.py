@@ -169,7 +169,7 @@ def test_list_capacity_overflow_refills(oracle_lib, monkeypatch):
     s.close()
 
 
-@pytest.mark.parametrize("side,limit_ms", [(1024, 0.5), (4096, 2.0)])
+@pytest.mark.parametrize("side,limit_ms", [(1024, 0.25), (4096, 2.0)])
 def test_cold_configure_is_timed(side, limit_ms):
     """a cold configure -- new resolution, new light:
     records, block lists, shadow lists, work order, one stream-ordered
