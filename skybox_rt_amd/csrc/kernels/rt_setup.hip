@@ -31,12 +31,24 @@ __device__ __forceinline__ int32_t fixed_host(float f, int frac) {
   return cvt_x86(f * (float)(1u << frac));
 }
 
-__device__ __forceinline__ int64_t floor_div(int64_t a, int64_t b) {  // b > 0
-  int64_t q = a / b;
-  if (a % b != 0 && a < 0) --q;
+// floor(a / b) for b > 0 and |a| < 2^53 (the row solutions: |a| < 2^48,
+// 0 < b < 2^31): the IEEE double quotient of two exact integers is within
+// one of the exact one, so one integer correction makes it exact -- no
+// 64-bit integer divide (a ~100-instruction library sequence per call)
+__device__ __forceinline__ int64_t floor_div(int64_t a, int64_t b) {
+  int64_t q = (int64_t)floor((double)a / (double)b);
+  const int64_t r = a - q * b;
+  if (r < 0) --q;
+  else if (r >= b) ++q;
   return q;
 }
 __device__ __forceinline__ int64_t ceil_div(int64_t a, int64_t b) { return -floor_div(-a, b); }
+// b != 0: whether b divides a (then *q = a / b)
+__device__ __forceinline__ bool exact_div(int64_t a, int64_t b, int64_t* q) {
+  if (b < 0) { a = -a; b = -b; }
+  *q = floor_div(a, b);
+  return *q * b == a;
+}
 
 __device__ __forceinline__ int32_t edge_at(const int32_t* e, uint32_t x, uint32_t y) {
   return (int32_t)((uint32_t)e[0] * x + (uint32_t)e[1] * y + (uint32_t)e[2]);
@@ -253,10 +265,11 @@ __device__ void phase_primvis(const rt_setup_arg_t* a) {
         while (k < 3 && e[3 * k] == 0) ++k;
         if (k == 3) {
           all_zero |= d[0] == 0 && d[1] == 0 && d[2] == 0;
-        } else if ((-d[k]) % e[3 * k] == 0) {
-          const int64_t x = -d[k] / e[3 * k];
-          all_zero |= x >= lo && x <= hi && e[0] * x + d[0] == 0 && e[3] * x + d[1] == 0 &&
-                      e[6] * x + d[2] == 0;
+        } else {
+          int64_t x = 0;
+          if (exact_div(-d[k], e[3 * k], &x))
+            all_zero |= x >= lo && x <= hi && e[0] * x + d[0] == 0 && e[3] * x + d[1] == 0 &&
+                        e[6] * x + d[2] == 0;
         }
       }
     }
@@ -1198,7 +1211,7 @@ __device__ void run_phase(const rt_setup_arg_t* arg, uint32_t bit) {
 // launch's workgroups (the per-primitive scan of PRIMVIS and the per-entry
 // list phases carry the longest per-workgroup chains)
 __constant__ const uint32_t kWide[22][2] = {
-    {RTS_FILL, 2},   {RTS_PRIMVIS, 8}, {RTS_SPROJ, 3},  {RTS_VTRIS, 1},  {RTS_WEIGHT, 1},  {RTS_LINK, 3},
+    {RTS_FILL, 2},   {RTS_PRIMVIS, 16}, {RTS_SPROJ, 3},  {RTS_VTRIS, 1},  {RTS_WEIGHT, 1},  {RTS_LINK, 3},
     {RTS_ROWSUM, 1}, {RTS_CLIMB, 3},   {RTS_COLSUM, 1}, {RTS_HIST, 1},   {RTS_SCATTER, 2}, {RTS_RECORDS, 2},
     {RTS_BCOUNT, 2}, {RTS_BSUM, 1},    {RTS_BOFF, 1},   {RTS_BFILL, 2},  {RTS_BSORT, 4},   {RTS_SCOUNT, 3},
     {RTS_SSUM, 1},   {RTS_SOFF, 2},    {RTS_SFILL, 3},  {RTS_SSORT, 3}};
