@@ -133,6 +133,17 @@ struct Seq {
   }
 };
 
+// the scans the launches do themselves (setup_common.h RTS_FOLD_*): the list
+// and tile-order scans always, the candidate-count scan while its items fit
+// the workgroup's LDS copy
+uint32_t fold_flags(const rt_renderer* r) {
+  static const bool off = std::getenv("RT_SETUP_FOLD") && std::atoi(std::getenv("RT_SETUP_FOLD")) == 0;
+  if (off) return 0u;
+  uint32_t f = RTS_FOLD_LISTS | RTS_FOLD_ORDER;
+  if (6ull * r->sc->geometry.size() <= RTS_SOFF_LDS) f |= RTS_FOLD_SOFF;
+  return f;
+}
+
 // The argument block goes through the driver's stream (vx_hip_copy_to_dev_async)
 // and the n launches are queued behind it: no host wait before, between or
 // after them -- the caller reads the status words back when it needs them.
@@ -256,6 +267,7 @@ int slist_args(rt_renderer* r, rt_setup_arg_t* g) {
   g->ncells = cells;
   g->ncpart = ncpart;
   g->scap = r->su.scap;
+  g->fold = fold_flags(r);  // a refill reads the counts the way the chain left them
   return 0;
 }
 
@@ -408,13 +420,18 @@ int device_setup(rt_renderer* r, bool raster, bool order_on, bool lists, bool sl
   // the per-resolution records, the block lists, the work order and the
   // shadow lists in one stream-ordered sequence: six launches, one
   // read-back of the status words at the end
+  // the scans folded into the launches that read them (setup_common.h
+  // RTS_FOLD_*; env RT_SETUP_FOLD=0 keeps the one-workgroup scan launches)
+  g.fold = fold_flags(r);
+  const bool fl = (g.fold & RTS_FOLD_LISTS) != 0, fo = (g.fold & RTS_FOLD_ORDER) != 0,
+             fs = (g.fold & RTS_FOLD_SOFF) != 0;
   Seq q;
-  q.add(RTS_FILL | RTS_PRIMVIS | (sl ? RTS_SPROJ : 0u), sl ? RTS_SOSCAN : 0u);
+  q.add(RTS_FILL | RTS_PRIMVIS | (sl ? RTS_SPROJ : 0u), sl && !fs ? RTS_SOSCAN : 0u);
   q.add(RTS_VTRIS | (ord ? RTS_WEIGHT : 0u) | (bl ? RTS_BCOUNT : 0u) | (sl ? RTS_SCOUNT : 0u));
-  q.add(RTS_LINK | (ord ? RTS_ROWSUM : 0u) | (bl ? RTS_BSUM : 0u) | (sl ? RTS_SSUM : 0u),
+  q.add(RTS_LINK | (ord ? RTS_ROWSUM : 0u) | (bl ? RTS_BSUM : 0u) | (sl ? RTS_SSUM : 0u), fl ? 0u :
         (bl ? RTS_BSCAN : 0u) | (sl ? RTS_SSCAN : 0u));
   q.add(RTS_CLIMB | (ord ? RTS_COLSUM : 0u) | (bl ? RTS_BOFF : 0u) | (sl ? RTS_SOFF : 0u));
-  q.add((ord ? RTS_HIST : 0u) | (bl ? RTS_BFILL : 0u) | (sl ? RTS_SFILL : 0u), ord ? RTS_SCAN : 0u);
+  q.add((ord ? RTS_HIST : 0u) | (bl ? RTS_BFILL : 0u) | (sl ? RTS_SFILL : 0u), ord && !fo ? RTS_SCAN : 0u);
   q.add((ord ? RTS_SCATTER : 0u) | (bl ? RTS_BSORT : 0u) | (sl ? RTS_SSORT : 0u));
   if (run_seq(r, g, q, launches) != 0 || read_status(r, st) != 0) return -1;
   if (st[0] & RTS_ERR_REF) return set_error("malformed BVH (reference out of range)");
@@ -485,10 +502,11 @@ int set_light(rt_renderer* r, const float light[3], uint32_t* launches) {
   g.rargs_addr = rargs;
   add_fill(&g, g.scnt_addr, g.ncells, 0u);
   add_fill(&g, g.status_addr + 16, 4, 0u);  // status words 4..7: the shadow lists
+  g.fold = fold_flags(r);
   Seq q;
-  q.add(RTS_FILL | RTS_SPROJ, RTS_SOSCAN);
+  q.add(RTS_FILL | RTS_SPROJ, (g.fold & RTS_FOLD_SOFF) ? 0u : RTS_SOSCAN);
   q.add(RTS_SCOUNT);
-  q.add(RTS_SSUM, RTS_SSCAN);
+  q.add(RTS_SSUM, (g.fold & RTS_FOLD_LISTS) ? 0u : RTS_SSCAN);
   q.add(RTS_SOFF);
   q.add(RTS_SFILL);
   q.add(RTS_SSORT);

@@ -113,13 +113,15 @@ __device__ __forceinline__ void kernel_body(const vx_task_t& task, const Scene& 
 #ifdef RT_STAMPS
   if (lane_id() == 0) __vx_mpm_lds[3] = (uint32_t)__builtin_amdgcn_s_memrealtime();
 #endif
+  LayerPre lpre;
+  layer_prefetch(S, lpre);
   // primary visibility: the raster's winner at this pixel
   const int32_t hit = trace_primary(S, lb, x, y, in, tie_high, cnt);
 #ifdef RT_STAMPS
   if (lane_id() == 0) __vx_mpm_lds[14] = (uint32_t)__builtin_amdgcn_s_memrealtime();
 #endif
   cnt.hits += hit >= 0;
-  const int32_t spid = resolve_layers(S, x, y, in && hit < 0, hit, cnt);
+  const int32_t spid = resolve_layers(S, x, y, in && hit < 0, hit, cnt, &lpre);
 #ifdef RT_STAMPS
   if (lane_id() == 0) __vx_mpm_lds[4] = (uint32_t)__builtin_amdgcn_s_memrealtime();
 #endif

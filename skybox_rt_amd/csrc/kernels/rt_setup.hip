@@ -593,6 +593,12 @@ __device__ void phase_hist(const rt_setup_arg_t* a) {
     }
     __syncthreads();
     hist[threadIdx.x * a->nblocks + b] = h[threadIdx.x];
+    if ((a->fold & RTS_FOLD_ORDER) && threadIdx.x == 0) {
+      // tiles with weight > 0 (digit < 255): status word 3, SCAN's when not folded
+      uint32_t heavy = 0;
+      for (uint32_t d = 0; d < 255u; ++d) heavy += h[d];
+      if (heavy) atomicAdd(vx_ptr<uint32_t>(a->status_addr) + 3, heavy);
+    }
     __syncthreads();
   }
 }
@@ -612,8 +618,30 @@ __device__ void phase_scatter(const rt_setup_arg_t* a) {
   __shared__ uint32_t wcnt[kW][256];
   const uint32_t wv = threadIdx.x >> 6, l = lane_id();
   const uint64_t lt_mask = (l == 0) ? 0ull : (~0ull >> (64 - l));
+  const bool fold = (a->fold & RTS_FOLD_ORDER) != 0;
   for (uint32_t b = slice_b(); b < a->nblocks; b += slice_n()) {
-    base[threadIdx.x] = hist[threadIdx.x * a->nblocks + b];
+    if (fold) {
+      // SCAN's offset of (digit d = thread, block b) over the raw digit-major
+      // histogram: the digits below d in every block + digit d in blocks < b
+      uint32_t row = 0, part = 0;
+      for (uint32_t j = 0; j < a->nblocks; ++j) {
+        const uint32_t c = hist[threadIdx.x * a->nblocks + j];
+        row += c;
+        part += j < b ? c : 0u;
+      }
+      wcnt[0][threadIdx.x] = row;
+      __syncthreads();
+      for (uint32_t o = 1; o < 256u; o <<= 1) {  // inclusive scan of the row totals
+        const uint32_t y = threadIdx.x >= o ? wcnt[0][threadIdx.x - o] : 0u;
+        __syncthreads();
+        wcnt[0][threadIdx.x] += y;
+        __syncthreads();
+      }
+      base[threadIdx.x] = wcnt[0][threadIdx.x] - row + part;
+      __syncthreads();
+    } else {
+      base[threadIdx.x] = hist[threadIdx.x * a->nblocks + b];
+    }
     for (uint32_t i = 0; i < kW; ++i) wcnt[i][threadIdx.x] = 0;
     __syncthreads();
     for (uint32_t r = 0; r < RTS_ITEMS / RTS_BLOCK; ++r) {
@@ -783,10 +811,24 @@ __device__ void phase_lscan(const ListSet& L) { scan_excl(L.part, L.npart, L.tot
 
 // per list: (first entry, count) -> idx; the count word zeroed (it becomes
 // the list's fill cursor)
-__device__ void phase_loff(const ListSet& L) {
+__device__ void phase_loff(const ListSet& L, bool fold) {
   __shared__ uint32_t s[RTS_BLOCK];
   constexpr uint32_t Q = RTS_BLOCKS_PER_PART / RTS_BLOCK;
+  if (fold && slice_b() == 0) {  // the total (BSCAN / SSCAN's, folded)
+    uint32_t x = 0;
+    for (uint32_t i = threadIdx.x; i < L.npart; i += RTS_BLOCK) x += L.part[i];
+    uint32_t ts, tm;
+    block_sum_max(x, 0u, &ts, &tm);
+    if (threadIdx.x == 0) *L.total = ts;
+  }
   for (uint32_t b = slice_b(); b < L.npart; b += slice_n()) {
+    uint32_t pre = 0;  // folded: the exclusive prefix of the raw partial sums
+    if (fold) {
+      uint32_t x = 0;
+      for (uint32_t i = threadIdx.x; i < b; i += RTS_BLOCK) x += L.part[i];
+      uint32_t tm;
+      block_sum_max(x, 0u, &pre, &tm);
+    }
     const uint32_t lb0 = b * RTS_BLOCKS_PER_PART + threadIdx.x * Q;
     uint32_t c[Q], sum = 0;
     for (uint32_t q = 0; q < Q; ++q) {
@@ -801,7 +843,7 @@ __device__ void phase_loff(const ListSet& L) {
       s[threadIdx.x] += y;
       __syncthreads();
     }
-    uint32_t run = L.part[b] + s[threadIdx.x] - sum;
+    uint32_t run = (fold ? pre : L.part[b]) + s[threadIdx.x] - sum;
     for (uint32_t q = 0; q < Q; ++q) {
       if (lb0 + q < L.n) {
         L.idx[lb0 + q] = make_uint2(run, c[q]);
@@ -1046,11 +1088,38 @@ __device__ void phase_soscan(const rt_setup_arg_t* a) {
 // the separating-axis test of oracle/rt.c sl_cell_meets against the cell
 // widened by RT_SLIST_EPS (the same float operations: its p0 / p1 are the
 // record's); f(j, cell) for every cell the polygon meets
+__shared__ uint32_t s_soff[RTS_SOFF_LDS + 1];
 template <typename Fn>
 __device__ __forceinline__ void sl_for_candidates(const rt_setup_arg_t* a, Fn f) {
   const uint4* rec = vx_ptr<const uint4>(a->sproj_addr);
   const uint32_t* soff = vx_ptr<const uint32_t>(a->soff_addr);
-  const uint32_t items = 6u * a->num_geom, total = soff[items];
+  const uint32_t items = 6u * a->num_geom;
+  if (a->fold & RTS_FOLD_SOFF) {
+    // SOSCAN folded: this workgroup scans the raw counts into LDS
+    __shared__ uint32_t sp[RTS_BLOCK];
+    const uint32_t chunk = (items + RTS_BLOCK - 1) / RTS_BLOCK;
+    const uint32_t b0 = min(threadIdx.x * chunk, items), b1 = min(b0 + chunk, items);
+    uint32_t sum = 0;
+    for (uint32_t i = b0; i < b1; ++i) sum += soff[i];
+    sp[threadIdx.x] = sum;
+    __syncthreads();
+    for (uint32_t o = 1; o < RTS_BLOCK; o <<= 1) {
+      const uint32_t y = threadIdx.x >= o ? sp[threadIdx.x - o] : 0u;
+      __syncthreads();
+      sp[threadIdx.x] += y;
+      __syncthreads();
+    }
+    uint32_t run = sp[threadIdx.x] - sum;
+    for (uint32_t i = b0; i < b1; ++i) {
+      const uint32_t x = soff[i];
+      s_soff[i] = run;
+      run += x;
+    }
+    if (threadIdx.x == RTS_BLOCK - 1) s_soff[items] = sp[RTS_BLOCK - 1];
+    __syncthreads();
+    soff = s_soff;
+  }
+  const uint32_t total = soff[items];
   const uint32_t N = a->slist_n;
   const float cw = 2.0f / (float)N;
   for (uint32_t q = slice_b() * RTS_BLOCK + threadIdx.x; q < total; q += slice_n() * RTS_BLOCK) {
@@ -1196,12 +1265,12 @@ __device__ void run_phase(const rt_setup_arg_t* arg, uint32_t bit) {
     case RTS_RECORDS: phase_records(arg); break;
     case RTS_BCOUNT: phase_bcount(arg); break;
     case RTS_BSUM: phase_lsum(block_set(arg)); break;
-    case RTS_BOFF: phase_loff(block_set(arg)); break;
+    case RTS_BOFF: phase_loff(block_set(arg), (arg->fold & RTS_FOLD_LISTS) != 0); break;
     case RTS_BFILL: phase_bfill(arg); break;
     case RTS_BSORT: phase_bsort(arg); break;
     case RTS_SCOUNT: phase_scount(arg); break;
     case RTS_SSUM: phase_lsum(cell_set(arg)); break;
-    case RTS_SOFF: phase_loff(cell_set(arg)); break;
+    case RTS_SOFF: phase_loff(cell_set(arg), (arg->fold & RTS_FOLD_LISTS) != 0); break;
     case RTS_SFILL: phase_sfill(arg); break;
     case RTS_SSORT: phase_ssort(arg); break;
     default: break;

@@ -221,6 +221,30 @@ __device__ __forceinline__ bool mt_hit(const Ray& r, const float4& a, const floa
   return true;
 }
 
+// mt_hit without branches: the same operations in the same order, every
+// value computed, the verdict one predicate (a leaf's tests run without
+// exec-mask branching; *t_out is meaningful only when it returns true)
+__device__ __forceinline__ bool mt_hit_bf(const Ray& r, const float4& a, const float4& b,
+                                          const float4& c, float tmin, float* t_out) {
+  const float v0[3] = {a.x, a.y, a.z}, e1[3] = {b.x, b.y, b.z}, e2[3] = {c.x, c.y, c.z};
+  float pvec[3], tvec[3], qvec[3];
+  cross3(pvec, r.d, e2);
+  const float det = dot3(e1, pvec);
+  tvec[0] = r.o[0] - v0[0];
+  tvec[1] = r.o[1] - v0[1];
+  tvec[2] = r.o[2] - v0[2];
+  float u = dot3(tvec, pvec);
+  cross3(qvec, tvec, e1);
+  float v = dot3(r.d, qvec);
+  const bool neg = det < 0.0f;
+  const float adet = neg ? -det : det;
+  u = neg ? -u : u;
+  v = neg ? -v : v;
+  const float t = dot3(e2, qvec) / det;
+  *t_out = t;
+  return (adet > 0.0f) & !(u < 0.0f) & !(v < 0.0f) & !(u + v > adet) & (t > tmin);
+}
+
 // slab test of one child; box planes interleaved as in rt_node_t
 __device__ __forceinline__ bool slab(float lox, float hix, float loy, float hiy, float loz,
                                      float hiz, const Ray& r, float tmin, float tmax,
@@ -718,6 +742,14 @@ __device__ __forceinline__ bool occluded_list(const Scene& S, const Ray& s, bool
 #ifndef RT_COOP_HALF_LOADS
 #define RT_COOP_HALF_LOADS 1
 #endif
+// RT_COOP_LEAF_BF = 1: trace_coop's leaf tests without branches (mt_hit_bf)
+#ifndef RT_COOP_LEAF_BF
+#define RT_COOP_LEAF_BF 0
+#endif
+// RT_COOP_LIST_BF = 1: occluded_list_coop's round without branches
+#ifndef RT_COOP_LIST_BF
+#define RT_COOP_LIST_BF 0
+#endif
 // RT_COOP_LEAF_IL = 1: trace_coop's leaf triangles dealt 0, 2 | 1, 3 over the
 // pair instead of 0, 1 | 2, 3
 #ifndef RT_COOP_LEAF_IL
@@ -944,6 +976,21 @@ __device__ __forceinline__ int32_t trace_coop(const Scene& S, const Ray& r, int3
         tb[k] = S.A.ld_f4(to + 48u * ks * k + 16);
         tc[k] = S.A.ld_f4(to + 48u * ks * k + 32);
       }
+#if RT_COOP_LEAF_BF
+      // both tests computed, the best taken by selects (no branches)
+#pragma unroll
+      for (uint32_t k = 0; k < 2; ++k) {
+        const bool in = k0 + ks * k < count;
+        const int32_t pid = __float_as_int(ta[k].w);
+        RT_CNT(cnt.tests += in ? 1u : 0u;)
+        float t;
+        const bool h = mt_hit_bf(r, ta[k], tb[k], tc[k], 0.0f, &t);
+        const bool cl = (t < bt) | ((t == bt) & (tie_high ? pid > bpid : pid < bpid));
+        const bool take = in & (pid != skip) & h & cl;
+        bt = take ? t : bt;
+        bpid = take ? pid : bpid;
+      }
+#else
 #pragma unroll
       for (uint32_t k = 0; k < 2; ++k) {
         if (k0 + ks * k < count) {
@@ -956,6 +1003,7 @@ __device__ __forceinline__ int32_t trace_coop(const Scene& S, const Ray& r, int3
           }
         }
       }
+#endif
       // the pair's best: closer() is a strict total order, so both lanes
       // agree and it is the four tests' sequential result
       const float pbt = xpartf(bt, hi);
@@ -990,6 +1038,23 @@ __device__ __forceinline__ bool occluded_list_coop(const Scene& S, const Ray& s,
       float4 t[6];
 #pragma unroll
       for (int w = 0; w < 6; ++w) t[w] = S.A.ld_f4(o + 16u * w);
+#if RT_COOP_LIST_BF
+      // both records' tests computed; the sequential scan's verdict and
+      // count by predicates (record 1 only when record 0 neither occluded
+      // nor ended the list)
+      float th0, th1;
+      const bool m0 = mt_hit_bf(s, t[0], t[1], t[2], 0.0f, &th0);
+      const bool m1 = mt_hit_bf(s, t[3], t[4], t[5], 0.0f, &th1);
+      const bool end0 = t[1].w > lim;
+      const bool test0 = !end0;
+      const bool hit0 = test0 & (__float_as_int(t[0].w) != skip) & m0 & (th0 < 1.0f);
+      const bool do1 = !hit0 & !end0 & (q + e0 + 1u < n);
+      const bool end1 = do1 & (t[4].w > lim);
+      const bool test1 = do1 & !end1;
+      hit = hit0 | (test1 & (__float_as_int(t[3].w) != skip) & m1 & (th1 < 1.0f));
+      end = end0 | end1;
+      RT_CNT(tests += (test0 ? 1u : 0u) + (test1 ? 1u : 0u);)
+#else
 #pragma unroll
       for (uint32_t e = 0; e < 2; ++e) {
         if (!hit && !end && q + e0 + e < n) {
@@ -1002,6 +1067,7 @@ __device__ __forceinline__ bool occluded_list_coop(const Scene& S, const Ray& s,
           }
         }
       }
+#endif
     }
     // the records are sorted: past the lower lane's bound the upper lane's
     // are too, so the first event in list order decides
@@ -1521,13 +1587,29 @@ __device__ __forceinline__ bool secondary_ok(float t) { return t > 0.0f && t < I
 // counted once per wave by its first active lane -- a record is one scalar
 // load for the whole wave, the rule block_primary's and the packet walks'
 // record tests follow (oracle/rt.c layer_waves: max over the wave's lanes)
+// RT_PREFETCH_LAYER = 1: the first layer record is loaded (scalar cache) when
+// the wave starts, its latency hidden under the primary pass
+#ifndef RT_PREFETCH_LAYER
+#define RT_PREFETCH_LAYER 0
+#endif
+struct LayerPre {
+  uint4 w[3];
+};
+__device__ __forceinline__ void layer_prefetch(const Scene& S, LayerPre& L) {
+  if (RT_PREFETCH_LAYER && S.num_layer > 0) S.A.sld_u4n<3>(S.vlayers, L.w);
+}
 __device__ __forceinline__ int32_t resolve_layers_n(const Scene& S, uint32_t px, uint32_t py, bool need,
-                                                    int32_t spid, uint32_t* tests) {
+                                                    int32_t spid, uint32_t* tests,
+                                                    const LayerPre* pre = nullptr) {
   uint64_t pend = __ballot(need);
   const uint32_t lead = lane_id() == (uint32_t)__builtin_ctzll(__ballot(1)) ? 1u : 0u;
   for (uint32_t k = 0; pend != 0 && k < S.num_layer; ++k) {
     uint4 lw[3];
-    S.A.sld_u4n<3>(S.vlayers + 64u * k, lw);  // one pointer: merged wide s_loads
+    if (RT_PREFETCH_LAYER && pre && k == 0) {
+      lw[0] = pre->w[0]; lw[1] = pre->w[1]; lw[2] = pre->w[2];
+    } else {
+      S.A.sld_u4n<3>(S.vlayers + 64u * k, lw);  // one pointer: merged wide s_loads
+    }
     const uint4 A = lw[0], B = lw[1], C = lw[2];
     const bool mine = (pend & (1ull << lane_id())) != 0;
     *tests += lead;
@@ -1545,9 +1627,10 @@ __device__ __forceinline__ int32_t resolve_layers_n(const Scene& S, uint32_t px,
   return spid;
 }
 __device__ __forceinline__ int32_t resolve_layers(const Scene& S, uint32_t px, uint32_t py, bool need,
-                                                  int32_t spid, Counters& cnt) {
+                                                  int32_t spid, Counters& cnt,
+                                                  const LayerPre* pre = nullptr) {
   uint32_t tests = 0;
-  spid = resolve_layers_n(S, px, py, need, spid, &tests);
+  spid = resolve_layers_n(S, px, py, need, spid, &tests, pre);
 #ifdef RT_INSTRUMENT
   cnt.layer_tests += tests;
 #else

@@ -79,6 +79,10 @@
 // beyond bcap (nonzero: the host refills at the exact size), [7] cell-list
 // entries beyond scap
 #define RTS_STATUS_WORDS 8
+#define RTS_FOLD_LISTS 0x1u   // BOFF / SOFF sum the raw partial sums they need (no BSCAN / SSCAN)
+#define RTS_FOLD_ORDER 0x2u   // SCATTER scans the digit histogram itself, HIST counts the heavy tiles (no SCAN)
+#define RTS_FOLD_SOFF  0x4u   // SCOUNT / SFILL scan the candidate counts into LDS (no SOSCAN)
+#define RTS_SOFF_LDS 6144u    // candidate-count items (6 per geometry triangle) RTS_FOLD_SOFF holds
 #define RTS_SPROJ_WORDS 32u  // u32 per SPROJ record: header uint4 + 7 separating axes (nx, ny, p0, p1)
 #define RTS_MAX_SEQ 32
 #define RTS_CLIMB_WG_NODES 4096u  // trees this small climb in one workgroup (rt_setup.hip phase_climb)
@@ -154,6 +158,9 @@ typedef struct {
   // to this pinned host buffer (a raw device pointer; 0 = none): the host
   // reads them there after waiting for the sequence
   uint64_t status_host;
-  uint32_t status_nonce, pad2;
+  uint32_t status_nonce;
+  // RTS_FOLD_*: the scans done inside the launches that need them (each
+  // workgroup scans what it reads; no one-workgroup scan launch)
+  uint32_t fold;
 
 } rt_setup_arg_t;
