@@ -137,7 +137,8 @@ struct Seq {
 // and tile-order scans always, the candidate-count scan while its items fit
 // the workgroup's LDS copy
 uint32_t fold_flags(const rt_renderer* r) {
-  static const bool off = std::getenv("RT_SETUP_FOLD") && std::atoi(std::getenv("RT_SETUP_FOLD")) == 0;
+  const char* fe = std::getenv("RT_SETUP_FOLD");
+  const bool off = fe && std::atoi(fe) == 0;
   if (off) return 0u;
   uint32_t f = RTS_FOLD_LISTS | RTS_FOLD_ORDER;
   if (6ull * r->sc->geometry.size() <= RTS_SOFF_LDS) f |= RTS_FOLD_SOFF;

@@ -188,3 +188,34 @@ def test_cold_configure_is_timed(side, limit_ms):
           f"shadow-list entries)")
     assert best["configure_ms"] < limit_ms
     s.close()
+
+
+@pytest.mark.parametrize("env", [{"RT_SETUP_FOLD": "0"}, {"RT_SETUP_PART": "0"},
+                                 {"RT_SETUP_FOLD": "0", "RT_SETUP_PART": "0"}])
+def test_setup_sequence_forms_equal_oracle(oracle_lib, monkeypatch, env):
+    """The setup sequence's other forms -- the one-workgroup scan launches
+    instead of the folded scans (RT_SETUP_FOLD=0), every sub-phase on the
+    whole grid in turn instead of side by side (RT_SETUP_PART=0) -- build
+    the same block lists, shadow lists and frames as the oracle."""
+    po = oracle_lib
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
+    s = rt.Scene.load(scene_path("tekkaman"))
+    r = rt.Renderer(s)
+    r.configure(512, 512, shadows=True, light=LIGHTS[1], instrumented=True)
+    ss = r.setup_stats()
+    assert ss["slist_on"] == 1 and ss["blist_blocks"] > 0
+    oidx, oent = po.vis_block_lists(_oscene(po, "tekkaman"), 512, 512, 0, 1)
+    assert np.array_equal(r.records("bidx"), oidx)
+    assert np.array_equal(r.records("blist")[:-3], oent)
+    _lists_equal_oracle(po, r, LIGHTS[1])
+    r.render()
+    c, _, _, k = _oracle(po, s, 512, 512, LIGHTS[1])
+    assert np.array_equal(r.framebuffer(), c)
+    r.set_light(LIGHTS[2])
+    r.render()
+    c2, _, _, _ = _oracle(po, s, 512, 512, LIGHTS[2])
+    assert np.array_equal(r.framebuffer(), c2)
+    _lists_equal_oracle(po, r, LIGHTS[2])
+    r.close()
+    s.close()
