@@ -213,6 +213,7 @@ def test_setup_sequence_forms_equal_oracle(oracle_lib, monkeypatch, env):
     c, _, _, k = _oracle(po, s, 512, 512, LIGHTS[1])
     assert np.array_equal(r.framebuffer(), c)
     r.set_light(LIGHTS[2])
+    assert r.setup_stats()["slist_on"] == 1  # settles the lists (their entry count)
     r.render()
     c2, _, _, _ = _oracle(po, s, 512, 512, LIGHTS[2])
     assert np.array_equal(r.framebuffer(), c2)
