@@ -1343,14 +1343,20 @@ static int build_lbvh(rt_renderer_h r, rt_bvh_build_stats_t* st) {
 
 // The host builder (app/bvh.cpp) restated on the device (kernels/bvh_sah.hip):
 // the same binned-SAH tree, BVH4 collapse and binary16 planes bit for bit.
+// One stream-ordered launch sequence (launch i runs seq[i], its launch tag):
+// the init, one split launch per tree level for a level budget, then the
+// numbering, emission and collapse -- every count a launch needs is read on
+// the device, so the host waits once, for the control words.  A tree deeper
+// than the budget continues with the next levels and the finishing phases
+// again.  The image and the scratch arrays stay with the renderer (a free
+// waits for the device).  env RT_SAH_TRACE: every launch its own timed run,
+// per-launch times to stderr (scripts/sah_trace.py).
 static int build_sah(rt_renderer_h r, rt_bvh_build_stats_t* st) {
   rt_scene* s = r->sc;
   const uint32_t n = (uint32_t)s->geometry.size();
   const auto t0 = std::chrono::steady_clock::now();
-  vx_buffer_h krnl = nullptr;
-  if (load_image(r, "bvh_sah.vxbin", &krnl)) return -1;
-  DevBuf kimg;
-  kimg.h = krnl;
+  if (!r->set_tag) return fail("the driver has no vx_hip_set_launch_tag");
+  if (!r->sah_krnl && load_image(r, "bvh_sah.vxbin", &r->sah_krnl)) return -1;
   std::vector<float> verts((size_t)n * 12, 0.0f);
   for (uint32_t i = 0; i < n; ++i) {
     const auto& p = s->scene.prims[s->geometry[i]];
@@ -1360,100 +1366,112 @@ static int build_sah(rt_renderer_h r, rt_bvh_build_stats_t* st) {
       verts[(size_t)i * 12 + 4 * c + 2] = p[c].pos[3];
     }
   }
-  std::vector<uint32_t> ctl0(SAH_CTL_WORDS, 0u);
-  DevBuf vb, tbox, cen, idx[2], fin, segs[2], small[2], nrec, nbox, cnt, d0, parent, cs, is4, ctl, argb;
-  const uint64_t N = n;
-  if (alloc_buf(r->dev, verts.size() * 4, &vb, verts.data()) || alloc_buf(r->dev, N * 32, &tbox) ||
-      alloc_buf(r->dev, N * 16, &cen) || alloc_buf(r->dev, N * 4, &idx[0]) ||
-      alloc_buf(r->dev, N * 4, &idx[1]) || alloc_buf(r->dev, N * 4, &fin) ||
-      alloc_buf(r->dev, N * 16, &segs[0]) || alloc_buf(r->dev, N * 16, &segs[1]) ||
-      alloc_buf(r->dev, N * 16, &small[0]) || alloc_buf(r->dev, N * 16, &small[1]) ||
-      alloc_buf(r->dev, N * 16, &nrec) || alloc_buf(r->dev, N * 64, &nbox) ||
-      alloc_buf(r->dev, (N + 1) * 4, &cnt) || alloc_buf(r->dev, N * 4, &d0) ||
-      alloc_buf(r->dev, N * 4, &parent) || alloc_buf(r->dev, N * 32, &cs) ||
-      alloc_buf(r->dev, (N + 1) * 4, &is4) ||
-      alloc_buf(r->dev, ctl0.size() * 4, &ctl, ctl0.data()) ||
-      alloc_buf(r->dev, sizeof(sah_arg_t), &argb))
-    return -1;
   sah_arg_t a;
   std::memset(&a, 0, sizeof(a));
-  a.verts_addr = vb.addr;
-  a.geom_addr = r->arg.geom_addr;
-  a.tbox_addr = tbox.addr;
-  a.cen_addr = cen.addr;
-  a.idx_addr[0] = idx[0].addr;
-  a.idx_addr[1] = idx[1].addr;
-  a.final_addr = fin.addr;
-  a.segs_addr[0] = segs[0].addr;
-  a.segs_addr[1] = segs[1].addr;
-  a.small_addr[0] = small[0].addr;
-  a.small_addr[1] = small[1].addr;
-  a.nrec_addr = nrec.addr;
-  a.nbox_addr = nbox.addr;
-  a.cnt_addr = cnt.addr;
-  a.d0_addr = d0.addr;
-  a.parent_addr = parent.addr;
-  a.cs_addr = cs.addr;
-  a.is4_addr = is4.addr;
-  a.ctl_addr = ctl.addr;
-  a.n = n;
-  double kernel_ms = 0.0;
-  uint32_t launches = 0;
-  const bool trace = std::getenv("RT_SAH_TRACE") != nullptr;  // per-launch times to stderr
-  auto launch = [&](uint32_t phase) -> int {
-    a.phase = phase;
-    if (vx_copy_to_dev(argb.h, &a, 0, sizeof(a)) != 0) return fail("vx_copy_to_dev failed");
-    if (vx_start(r->dev, krnl, argb.h) != 0) return fail("vx_start failed");
-    if (vx_ready_wait(r->dev, VX_MAX_TIMEOUT) != 0) return fail("vx_ready_wait failed");
-    double ms = 0.0;
-    uint32_t g = 0, b = 0;
-    if (r->last_run && r->last_run(r->dev, &ms, &g, &b) == 0) kernel_ms += ms;
-    if (trace) std::fprintf(stderr, "sah phase %u level %u: %.4f ms\n", phase, a.level, ms);
-    ++launches;
-    return 0;
-  };
-  uint32_t c[SAH_CTL_WORDS];
-  auto read_ctl = [&]() -> int {
-    return vx_copy_from_dev(c, ctl.h, 0, sizeof(c)) == 0 ? 0 : fail("vx_copy_from_dev failed");
-  };
-  if (launch(SAH_INIT)) return -1;
-  // one launch per tree level, until a level creates no internal node
-  for (uint32_t L = 0;; ++L) {
-    if (L + 1 >= SAH_MAX_LEVELS) return fail("SAH build deeper than its level table");
-    a.level = L;
-    if (launch(SAH_SPLIT) || read_ctl()) return -1;
-    if (c[SAH_CTL_ERR]) return fail("SAH build overflowed its node / segment capacity");
-    if (c[SAH_CTL_SEG + L + 1] == 0 && c[SAH_CTL_SMALL + L + 1] == 0) break;
+  const uint64_t N = n;
+  // the arrays (sah_common.h), 256-B aligned in one scratch buffer
+  const std::pair<uint64_t*, uint64_t> parts[] = {
+      {&a.verts_addr, N * 48},     {&a.tbox_addr, N * 32},      {&a.cen_addr, N * 16},
+      {&a.idx_addr[0], N * 4},     {&a.idx_addr[1], N * 4},     {&a.final_addr, N * 4},
+      {&a.segs_addr[0], N * 16},   {&a.segs_addr[1], N * 16},   {&a.small_addr[0], N * 16},
+      {&a.small_addr[1], N * 16},  {&a.nrec_addr, N * 16},      {&a.nbox_addr, N * 64},
+      {&a.cnt_addr, (N + 1) * 4},  {&a.d0_addr, N * 4},         {&a.parent_addr, N * 4},
+      {&a.cs_addr, N * 32},        {&a.is4_addr, (N + 1) * 4},  {&a.ctl_addr, SAH_CTL_WORDS * 4}};
+  uint64_t total = 0;
+  for (const auto& pt : parts) total += (pt.second + 255) & ~255ull;
+  if (r->su.sah_bytes < total || !r->su.sah.h) {
+    if (upload(r->dev, nullptr, total, &r->su.sah.h, &r->su.sah.addr)) return -1;
+    r->su.sah_bytes = total;
   }
-  const uint32_t nn = c[SAH_CTL_NODES], depth = c[SAH_CTL_DEPTH];
-  if (depth > RT_STACK_DEEP) return fail("BVH deeper than RT_STACK_DEEP");
+  if (!r->su.sah_args.h && upload(r->dev, nullptr, sizeof(sah_arg_t), &r->su.sah_args.h, &r->su.sah_args.addr))
+    return -1;
+  uint64_t off = 0;
+  for (const auto& pt : parts) {
+    *pt.first = r->su.sah.addr + off;
+    off += (pt.second + 255) & ~255ull;
+  }
+  const uint64_t ctl_off = a.ctl_addr - r->su.sah.addr;
+  // the outputs, sized for the largest tree n triangles make (BFS ids < n)
   vx_buffer_h nodes_h = nullptr, tris_h = nullptr, nodes4_h = nullptr;
   uint64_t nodes_addr = 0, tris_addr = 0, nodes4_addr = 0;
   DevBuf nodes_out, tris_out, nodes4_out;  // owned here until handed to the renderer
-  if (upload(r->dev, nullptr, (uint64_t)nn * sizeof(rt_node_t), &nodes_h, &nodes_addr)) return -1;
+  const uint64_t nmax = std::max<uint64_t>(N, 1);
+  if (upload(r->dev, nullptr, nmax * sizeof(rt_node_t), &nodes_h, &nodes_addr)) return -1;
   nodes_out.h = nodes_h;
   if (upload(r->dev, nullptr, (N + 3) * sizeof(rt_tri_t), &tris_h, &tris_addr)) return -1;
   tris_out.h = tris_h;
-  a.nodes_addr = nodes_addr;
-  a.tris_addr = tris_addr;
-  a.nn = nn;
-  a.scan_addr = cnt.addr;
-  a.scan_count = n;
-  if (launch(SAH_NUMBER) || launch(SAH_SCAN) || launch(SAH_EMIT) || launch(SAH_CS) ||
-      launch(SAH_MARK))
-    return -1;
-  a.scan_addr = is4.addr;
-  a.scan_count = nn;
-  if (launch(SAH_SCAN)) return -1;
-  uint32_t nn4 = 0;
-  if (vx_copy_from_dev(&nn4, is4.h, (uint64_t)nn * 4, 4) != 0) return fail("vx_copy_from_dev failed");
-  if (upload(r->dev, nullptr, (uint64_t)nn4 * (sizeof(rt_node4_t) + sizeof(rt_node4h_t)), &nodes4_h,
-             &nodes4_addr))
+  if (upload(r->dev, nullptr, nmax * (sizeof(rt_node4_t) + sizeof(rt_node4h_t)), &nodes4_h, &nodes4_addr))
     return -1;
   nodes4_out.h = nodes4_h;
+  a.geom_addr = r->arg.geom_addr;
+  a.nodes_addr = nodes_addr;
+  a.tris_addr = tris_addr;
   a.nodes4_addr = nodes4_addr;
-  a.nn4 = nn4;
-  if (launch(SAH_EMIT4) || launch(SAH_HALF) || read_ctl()) return -1;
+  a.n = n;
+  auto copy = [&](vx_buffer_h h, const void* src, uint64_t o, uint64_t size) -> int {
+    const int rc = r->copy_async ? r->copy_async(h, src, o, size) : vx_copy_to_dev(h, src, o, size);
+    return rc == 0 ? 0 : fail("vx_copy_to_dev failed");
+  };
+  const std::vector<uint32_t> ctl0(SAH_CTL_WORDS, 0u);
+  if (copy(r->su.sah.h, verts.data(), a.verts_addr - r->su.sah.addr, verts.size() * 4) ||
+      copy(r->su.sah.h, ctl0.data(), ctl_off, ctl0.size() * 4))
+    return -1;
+  const bool trace = std::getenv("RT_SAH_TRACE") != nullptr;
+  double kernel_ms = 0.0;
+  uint32_t launches = 0;
+  auto run = [&](const std::vector<uint32_t>& seq) -> int {
+    if (seq.size() > SAH_MAX_SEQ) return fail("SAH build sequence too long");
+    a.nseq = (uint32_t)seq.size();
+    std::memset(a.seq, 0, sizeof(a.seq));
+    std::copy(seq.begin(), seq.end(), a.seq);
+    if (copy(r->su.sah_args.h, &a, 0, sizeof(a))) return -1;
+    for (uint32_t i = 0; i < a.nseq;) {
+      // untimed groups of up to 16 launches (the driver's queue slots bound a group)
+      uint32_t k = trace ? 1u : std::min<uint32_t>(16u, a.nseq - i);
+      bool grouped = false;
+      while (!trace && k > 1 && !(grouped = r->launch_group && r->launch_group(r->dev, k | VX_HIP_GROUP_UNTIMED) == 0))
+        k >>= 1;
+      for (uint32_t j = i; j < i + k; ++j) {
+        if (r->set_tag(r->dev, j) != 0 || vx_start(r->dev, r->sah_krnl, r->su.sah_args.h) != 0) {
+          if (grouped) r->launch_group(r->dev, 0);
+          return fail("vx_start failed");
+        }
+        ++launches;
+        if (trace) {
+          double ms = 0.0;
+          uint32_t g = 0, b = 0;
+          if (vx_ready_wait(r->dev, VX_MAX_TIMEOUT) != 0) return fail("vx_ready_wait failed");
+          if (r->last_run && r->last_run(r->dev, &ms, &g, &b) == 0) kernel_ms += ms;
+          std::fprintf(stderr, "sah phase %u level %u: %.4f ms\n", seq[j] & 0xffu, seq[j] >> 8, ms);
+        }
+      }
+      i += k;
+    }
+    return 0;
+  };
+  // the level budget: a binned-SAH tree over n triangles is rarely deeper
+  // than log2(n) + 6; a deeper one costs a second round trip
+  uint32_t lg = 0;
+  while ((1ull << lg) < N + 1) ++lg;
+  const uint32_t budget = lg + 6;
+  uint32_t c[SAH_CTL_WORDS];
+  std::vector<uint32_t> seq{SAH_SEQ(SAH_INIT, 0)};
+  for (uint32_t L = 0;;) {
+    const uint32_t lend = std::min<uint32_t>(L + budget, SAH_MAX_LEVELS - 1);
+    for (; L < lend; ++L) seq.push_back(SAH_SEQ(SAH_SPLIT, L));
+    for (const uint32_t ph : {SAH_NUMBER, SAH_SCAN, SAH_EMIT, SAH_CS, SAH_MARK, SAH_SCAN4, SAH_EMIT4, SAH_HALF})
+      seq.push_back(SAH_SEQ(ph, 0));
+    const auto tr = std::chrono::steady_clock::now();
+    if (run(seq) || vx_copy_from_dev(c, r->su.sah.h, ctl_off, sizeof(c)) != 0)
+      return fail("SAH build: launch or read-back failed");
+    if (!trace) kernel_ms += ms_since(tr);
+    if (c[SAH_CTL_ERR] & 1u) return fail("SAH build overflowed its node / segment capacity");
+    if (c[SAH_CTL_SEG + L] == 0 && c[SAH_CTL_SMALL + L] == 0) break;  // level L is empty: the tree is whole
+    if (L + 1 >= SAH_MAX_LEVELS) return fail("SAH build deeper than its level table");
+    seq.assign(1, SAH_SEQ(SAH_RESET, 0));
+  }
+  const uint32_t nn = c[SAH_CTL_NODES], depth = c[SAH_CTL_DEPTH], nn4 = c[SAH_CTL_NODES4];
+  if (depth > RT_STACK_DEEP) return fail("BVH deeper than RT_STACK_DEEP");
   if (c[SAH_CTL_ERR]) return fail("SAH build: BVH4 walk deeper than its path table");
   const uint32_t stack4 = c[SAH_CTL_STACK4];
   const bool use4 = stack4 <= RT_STACK_DEEP;

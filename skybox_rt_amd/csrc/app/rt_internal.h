@@ -37,11 +37,13 @@ struct DevScratch {
 struct SetupScratch {
   DevScratch args, status, parent, count, weight, hist, bcnt, bpart, btmp;
   DevScratch scnt, spart, sproj, soff, skey, stmp;
+  DevScratch sah, sah_args;  // the SAH build's arrays (one buffer) and argument block
   uint64_t bcap = 0;   // block-list entry capacity of btmp / blist
   uint32_t scap = 0;   // shadow-list entry capacity of stmp / slist
+  uint64_t sah_bytes = 0;
   void release() {
     for (DevScratch* d : {&args, &status, &parent, &count, &weight, &hist, &bcnt, &bpart, &btmp, &scnt, &spart,
-                          &sproj, &soff, &skey, &stmp})
+                          &sproj, &soff, &skey, &stmp, &sah, &sah_args})
       if (d->h) {
         vx_mem_free(d->h);
         d->h = nullptr;
@@ -62,6 +64,7 @@ struct rt_renderer {
   // RT_RENDER_BVH_WALK primary+shadow frames (binary16 BVH4 images only):
   // rt_bvh / rt_bvh_stats, the packet walks without the list code paths
   vx_buffer_h krnl_bvh[2] = {};
+  vx_buffer_h sah_krnl = nullptr;  // bvh_sah.vxbin, loaded by the first device build
   vx_buffer_h pathq = nullptr, pathq_ctr = nullptr;
   bool pq = false;          // the configuration runs the two-kernel path tracer
   vx_buffer_h nodes = nullptr, nodes4 = nullptr, tris = nullptr, layers = nullptr, dcs = nullptr, tex = nullptr;
@@ -126,7 +129,7 @@ struct rt_renderer {
                            &setup_krnl, &verts, &pdc, &dcz, &layer_list, &geometry_list, &vis,
                            &blist, &bidx, &sidx, &slist, &krnl_pq[0][0], &krnl_pq[0][1],
                            &krnl_pq[1][0], &krnl_pq[1][1], &pathq, &pathq_ctr,
-                           &krnl_bvh[0], &krnl_bvh[1]};
+                           &krnl_bvh[0], &krnl_bvh[1], &sah_krnl};
     for (auto* b : bufs) {
       if (*b) vx_mem_free(*b);
       *b = nullptr;

@@ -187,8 +187,8 @@ __device__ void sah_price(const uint32_t (*bin)[SAH_BINS][7], const float* cl, c
 // The node record of segment sg (split at b + nl; child boxes bx) and its
 // children: <= SAH_LEAF triangles a leaf, <= SAH_SMALL a segment of the
 // next level's wave list, else of its workgroup list (one thread)
-__device__ void emit_node(const sah_arg_t* a, const sah_seg_t& sg, uint32_t nl, const float (*bx)[6]) {
-  const uint32_t L = a->level;
+__device__ void emit_node(const sah_arg_t* a, uint32_t L, const sah_seg_t& sg, uint32_t nl,
+                          const float (*bx)[6]) {
   uint32_t* ctl = vx_ptr<uint32_t>(a->ctl_addr);
   sah_seg_t* next = vx_ptr<sah_seg_t>(a->segs_addr[(L + 1) & 1]);
   sah_seg_t* next_small = vx_ptr<sah_seg_t>(a->small_addr[(L + 1) & 1]);
@@ -238,8 +238,7 @@ __device__ __forceinline__ float wmax(float x) {
 // thousands of small nodes): a triangle per lane, wave reductions instead of
 // workgroup barriers, the bins in the wave's own LDS; the same decisions,
 // order and records as the workgroup path.
-__device__ void split_small(const sah_arg_t* a, SmallLds& W, uint32_t w, uint32_t l, uint64_t lt) {
-  const uint32_t L = a->level;
+__device__ void split_small(const sah_arg_t* a, uint32_t L, SmallLds& W, uint32_t w, uint32_t l, uint64_t lt) {
   const uint32_t nseg = vx_ptr<const uint32_t>(a->ctl_addr)[SAH_CTL_SMALL + L];
   const sah_seg_t* segs = vx_ptr<const sah_seg_t>(a->small_addr[L & 1]);
   const uint32_t* idx = vx_ptr<const uint32_t>(a->idx_addr[L & 1]);
@@ -308,13 +307,12 @@ __device__ void split_small(const sah_arg_t* a, SmallLds& W, uint32_t w, uint32_
         if (left ? leaf0 : leaf1) fin[i] = t;
       }
     }
-    if (l == 0) emit_node(a, sg, nl, bx);
+    if (l == 0) emit_node(a, L, sg, nl, bx);
     __builtin_amdgcn_wave_barrier();  // W is reused by the wave's next segment
   }
 }
 
-__device__ void phase_split(const sah_arg_t* a) {
-  const uint32_t L = a->level;
+__device__ void phase_split(const sah_arg_t* a, uint32_t L) {
   uint32_t* ctl = vx_ptr<uint32_t>(a->ctl_addr);
   const uint32_t nseg = ctl[SAH_CTL_SEG + L];
   const sah_seg_t* segs = vx_ptr<const sah_seg_t>(a->segs_addr[L & 1]);
@@ -465,11 +463,11 @@ __device__ void phase_split(const sah_arg_t* a) {
       }
     }
     // 5. the node record and the next level's segments
-    if (tid == 0) emit_node(a, sg, nl, S.dec.box);
+    if (tid == 0) emit_node(a, L, sg, nl, S.dec.box);
     __syncthreads();
   }
   __syncthreads();  // the union's other member from here on
-  split_small(a, U.small[w], w, l, lt);
+  split_small(a, L, U.small[w], w, l, lt);
 }
 
 // ---- preorder numbering ------------------------------------------------------
@@ -485,13 +483,11 @@ __device__ void phase_number(const sah_arg_t* a) {
   }
 }
 
-// exclusive scan of u32 [scan_count] in place, total at [scan_count]
-// (workgroup 0: contiguous chunks per thread, a workgroup scan of the chunk sums)
-__device__ void phase_scan(const sah_arg_t* a) {
+// exclusive scan of u32 [total] in place, total at [total] (workgroup 0:
+// contiguous chunks per thread, a workgroup scan of the chunk sums)
+__device__ void phase_scan(uint32_t* x, uint32_t total) {
   if (blockIdx.x != 0) return;
-  uint32_t* x = vx_ptr<uint32_t>(a->scan_addr);
   __shared__ uint32_t s[SAH_BLOCK];
-  const uint32_t total = a->scan_count;
   const uint32_t chunk = (total + SAH_BLOCK - 1) / SAH_BLOCK;
   const uint32_t b0 = min(threadIdx.x * chunk, total), b1 = min(b0 + chunk, total);
   uint32_t sum = 0;
@@ -593,7 +589,8 @@ __device__ __forceinline__ double child_area(const Child& c) {
 __device__ void phase_cs(const sah_arg_t* a) {
   const float* nodes = vx_ptr<const float>(a->nodes_addr);
   int32_t* cs = vx_ptr<int32_t>(a->cs_addr);
-  for (uint32_t p = blockIdx.x * SAH_BLOCK + threadIdx.x; p < a->nn; p += gridDim.x * SAH_BLOCK) {
+  const uint32_t nn = vx_ptr<const uint32_t>(a->ctl_addr)[SAH_CTL_NODES];
+  for (uint32_t p = blockIdx.x * SAH_BLOCK + threadIdx.x; p < nn; p += gridDim.x * SAH_BLOCK) {
     Child c[4];
     int m = 0;
     for (int ch = 0; ch < 2; ++ch) {
@@ -641,7 +638,8 @@ __device__ void phase_mark(const sah_arg_t* a) {
   const int32_t* cs = vx_ptr<const int32_t>(a->cs_addr);
   uint32_t* is4 = vx_ptr<uint32_t>(a->is4_addr);
   uint32_t* ctl = vx_ptr<uint32_t>(a->ctl_addr);
-  for (uint32_t m = blockIdx.x * SAH_BLOCK + threadIdx.x; m < a->nn; m += gridDim.x * SAH_BLOCK) {
+  const uint32_t nn = ctl[SAH_CTL_NODES];
+  for (uint32_t m = blockIdx.x * SAH_BLOCK + threadIdx.x; m < nn; m += gridDim.x * SAH_BLOCK) {
     int32_t path[SAH_MAX_LEVELS];
     int len = 0;
     int32_t x = (int32_t)m;
@@ -687,7 +685,8 @@ __device__ void phase_emit4(const sah_arg_t* a) {
   const int32_t* cs = vx_ptr<const int32_t>(a->cs_addr);
   const uint32_t* pre4 = vx_ptr<const uint32_t>(a->is4_addr);
   rt_node4_t* nodes4 = vx_ptr<rt_node4_t>(a->nodes4_addr);
-  for (uint32_t m = blockIdx.x * SAH_BLOCK + threadIdx.x; m < a->nn; m += gridDim.x * SAH_BLOCK) {
+  const uint32_t nn = vx_ptr<const uint32_t>(a->ctl_addr)[SAH_CTL_NODES];
+  for (uint32_t m = blockIdx.x * SAH_BLOCK + threadIdx.x; m < nn; m += gridDim.x * SAH_BLOCK) {
     if (pre4[m + 1] == pre4[m]) continue;  // not a BVH4 node
     float v[32];
     for (int i = 0; i < 32; ++i) v[i] = 0.0f;
@@ -711,25 +710,58 @@ __device__ void phase_emit4(const sah_arg_t* a) {
 }
 
 __device__ void phase_half(const sah_arg_t* a) {
+  const uint32_t nn = vx_ptr<const uint32_t>(a->ctl_addr)[SAH_CTL_NODES];
+  const uint32_t nn4 = vx_ptr<const uint32_t>(a->is4_addr)[nn];  // the membership scan's total
   rt_node4_t* nodes4 = vx_ptr<rt_node4_t>(a->nodes4_addr);
-  uint32_t* half = vx_ptr<uint32_t>(a->nodes4_addr + 128ull * (uint64_t)a->nn4);
-  for (uint32_t i = blockIdx.x * SAH_BLOCK + threadIdx.x; i < a->nn4; i += gridDim.x * SAH_BLOCK)
+  uint32_t* half = vx_ptr<uint32_t>(a->nodes4_addr + 128ull * (uint64_t)nn4);
+  if (blockIdx.x == 0 && threadIdx.x == 0) vx_ptr<uint32_t>(a->ctl_addr)[SAH_CTL_NODES4] = nn4;
+  for (uint32_t i = blockIdx.x * SAH_BLOCK + threadIdx.x; i < nn4; i += gridDim.x * SAH_BLOCK)
     half4_node(nodes4[i].v, half + 16 * i);
+}
+
+// the numbering's counters as SAH_INIT leaves them, and the collapse's
+// maxima (a sequence that ran its finishing phases before its last level)
+__device__ void phase_reset(const sah_arg_t* a) {
+  uint32_t* cnt = vx_ptr<uint32_t>(a->cnt_addr);
+  uint32_t* d0 = vx_ptr<uint32_t>(a->d0_addr);
+  for (uint32_t i = blockIdx.x * SAH_BLOCK + threadIdx.x; i <= a->n; i += gridDim.x * SAH_BLOCK) {
+    cnt[i] = 0;
+    if (i < a->n) d0[i] = 0xffffffffu;
+  }
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    uint32_t* ctl = vx_ptr<uint32_t>(a->ctl_addr);
+    ctl[SAH_CTL_DEPTH4] = 0;
+    ctl[SAH_CTL_STACK4] = 0;
+    ctl[SAH_CTL_ERR] &= ~2u;
+  }
 }
 
 }  // namespace
 
+// Launch i of the host's sequence runs seq[i] (its launch tag).  The
+// sequence's steps are launches queued back to back on the driver's stream:
+// each launch boundary makes one step's stores visible to the next (per-XCD
+// L2s are not coherent within a launch); counts a step needs (segments of a
+// level, nodes, BVH4 nodes) are read from device memory, never from the host.
 VX_MAIN(sah_arg_t, arg, SAH_BLOCK) {
-  switch (arg->phase) {
+  if (vx_launch_tag >= arg->nseq || vx_launch_tag >= SAH_MAX_SEQ) return 0;
+  const uint32_t e = arg->seq[vx_launch_tag];
+  const uint32_t L = e >> 8;
+  switch (e & 0xffu) {
     case SAH_INIT: phase_init(arg); break;
-    case SAH_SPLIT: phase_split(arg); break;
+    case SAH_SPLIT: phase_split(arg, L); break;
     case SAH_NUMBER: phase_number(arg); break;
-    case SAH_SCAN: phase_scan(arg); break;
+    case SAH_SCAN: phase_scan(vx_ptr<uint32_t>(arg->cnt_addr), arg->n); break;
     case SAH_EMIT: phase_emit(arg); break;
     case SAH_CS: phase_cs(arg); break;
     case SAH_MARK: phase_mark(arg); break;
     case SAH_EMIT4: phase_emit4(arg); break;
-    default: phase_half(arg); break;
+    case SAH_HALF: phase_half(arg); break;
+    case SAH_RESET: phase_reset(arg); break;
+    case SAH_SCAN4:
+      phase_scan(vx_ptr<uint32_t>(arg->is4_addr), vx_ptr<const uint32_t>(arg->ctl_addr)[SAH_CTL_NODES]);
+      break;
+    default: break;
   }
   return 0;
 }

@@ -6,6 +6,8 @@
 // of <= 4 triangles, stable partitions, boxes padded by 2^-16 of the scene
 // extent; the BVH4 collapse that repeatedly opens the largest-area internal
 // child; binary16 planes) that produces the host's arrays bit for bit:
+//   * one stream-ordered launch sequence (launch i runs seq[i]: its launch
+//     tag, vx_spawn.h), the host reading the control words once at the end;
 //   * top-down, one launch per tree level: a workgroup per node (segment of
 //     the triangle order; a wave per node of <= 64 triangles) computes the
 //     centroid bounds, the 3 x 16 bins in LDS, the SAH decision (45
@@ -28,6 +30,7 @@
 #define SAH_LEAF 4
 #define SAH_SMALL 64             // segments up to this many triangles: one wave each
 #define SAH_MAX_LEVELS 64
+#define SAH_MAX_SEQ 96           // launches of one sequence
 
 enum {
   SAH_INIT = 0,    // triangle boxes, centroids, extent; root segment; counters
@@ -39,7 +42,11 @@ enum {
   SAH_MARK = 6,    // BVH4 membership, depth, worst-case stack (root-path walks)
   SAH_EMIT4 = 7,   // rt_node4_t at BVH4 preorder indices
   SAH_HALF = 8,    // binary16 planes (rt_node4h_t behind the rt_node4_t array)
+  SAH_RESET = 9,   // the numbering's counters again (a sequence continued past its level budget)
+  SAH_SCAN4 = 10,  // exclusive scan of the BVH4 membership (is4, one word per BVH2 node)
 };
+// a sequence entry: the phase, and the tree level of a SAH_SPLIT
+#define SAH_SEQ(phase, level) ((uint32_t)(phase) | ((uint32_t)(level) << 8))
 
 // ctl words (u32)
 #define SAH_CTL_NODES 0    // BFS node ids allocated
@@ -48,6 +55,7 @@ enum {
 #define SAH_CTL_DEPTH4 3   // BVH4 depth
 #define SAH_CTL_STACK4 4   // BVH4 worst-case traversal stack
 #define SAH_CTL_ERR 5      // != 0: capacity / depth overflow
+#define SAH_CTL_NODES4 6   // BVH4 nodes (SAH_HALF: the membership scan's total)
 #define SAH_CTL_SEG 8      // [SAH_CTL_SEG + L]: workgroup segments of level L
 #define SAH_CTL_SMALL (SAH_CTL_SEG + SAH_MAX_LEVELS + 1)  // [.. + L]: wave segments of level L
 #define SAH_CTL_WORDS (SAH_CTL_SMALL + SAH_MAX_LEVELS + 1)
@@ -74,10 +82,9 @@ typedef struct {
   uint64_t cs_addr;       // i32 [n][8]: BVH4 expansion: 4 refs, 4 sources (node << 1 | slot)
   uint64_t is4_addr;      // u32 [n + 1]: BVH4 membership -> scan -> BVH4 preorder
   uint64_t ctl_addr;      // u32 [SAH_CTL_WORDS]
-  uint64_t scan_addr;     // SAH_SCAN input / output
-  uint64_t nodes_addr;    // rt_node_t [max(nn, 1)]
+  uint64_t nodes_addr;    // rt_node_t [max(n, 1)] (nn = ctl[SAH_CTL_NODES] used)
   uint64_t tris_addr;     // rt_tri_t [n + 3]
-  uint64_t nodes4_addr;   // rt_node4_t [nn4], then rt_node4h_t [nn4]
-  uint32_t n, phase, level, scan_count;
-  uint32_t nn, nn4, pad[2];
+  uint64_t nodes4_addr;   // rt_node4_t [nn4], then rt_node4h_t [nn4] (nn4 = is4[nn]; room for n each)
+  uint32_t n, nseq;
+  uint32_t seq[SAH_MAX_SEQ];  // SAH_SEQ entries, launch i runs seq[i]
 } sah_arg_t;

@@ -41,6 +41,23 @@ def make_scene(path: str, n: int, seed: int = 1, size: float = 0.03, w_range=(90
         verts[2] = tuple(np.concatenate([v0[:degenerate], v2[degenerate:]])
                          for v0, v2 in zip(verts[0], verts[2]))
     col = rng.uniform(0.2, 1.0, (n, 3))
+    return _write(path, verts, col)
+
+
+def make_chain_scene(path: str, n: int, ratio: float = 1.6, base: float = 1e-3) -> str:
+    """n small triangles whose x centres grow geometrically (base * ratio^k,
+    NDC): every binned-SAH split peels a few off the far end, so the tree is
+    about n / 5 levels deep -- deeper than the device build's level budget
+    (log2 n + 6) for n = 96."""
+    k = np.arange(n, dtype=np.float64)
+    w = np.full(n, 100.0)
+    cx = base * ratio ** k * w
+    verts = [(cx + dx * w, np.full(n, dy) * w, w * 0.5, w) for dx, dy in ((0.0, 0.0), (0.01, 0.0), (0.0, 0.01))]
+    return _write(path, verts, np.full((n, 3), 0.5))
+
+
+def _write(path, verts, col):
+    n = len(col)
     items = []
     for t in range(n):
         for k in range(3):

@@ -6,7 +6,12 @@ scene's host-built arrays bit for bit (BVH2 nodes in preorder, triangle
 records in leaf order, BVH4 nodes, rt_node4h_t records, depth, BVH4 depth
 and worst-case stack), on the reference's scenes and on synthetic ones
 (20k / 100k triangles: many levels and wide top-level segments; 3-9
-triangles: the small-root and median paths); frames over it == the oracle."""
+triangles: the small-root and median paths; chain96: a tree deeper than the
+build's level budget, so its launch sequence continues once); frames over it
+== the oracle.  The build is one launch sequence with one read-back: a
+rebuild (image resident) repeats the arrays exactly."""
+import math
+
 import numpy as np
 import pytest
 
@@ -22,7 +27,10 @@ _paths = {}
 def _scene(name, tmp_path_factory):
     if name in _paths:
         return _paths[name]
-    if name.startswith("synth"):
+    if name.startswith("chain"):
+        from synth_scene import make_chain_scene
+        path = make_chain_scene(str(tmp_path_factory.mktemp("sah") / f"{name}.cgltrace.gz"), int(name[5:]))
+    elif name.startswith("synth"):
         from synth_scene import make_scene
         n = int(name[5:].replace("k", "000"))
         path = make_scene(str(tmp_path_factory.mktemp("sah") / f"{name}.cgltrace.gz"), n, seed=n)
@@ -34,7 +42,7 @@ def _scene(name, tmp_path_factory):
 
 @pytest.mark.parametrize("name", ["tekkaman", "scene", "box", "carnival", "mouse", "vase",
                                   "evilskull", "polybump", "synth3", "synth4", "synth5",
-                                  "synth9", "synth20k", "synth100k"])
+                                  "synth9", "synth20k", "synth100k", "chain96"])
 def test_gpu_sah_equals_host_build(tmp_path_factory, name):
     s = rt.Scene.load(_scene(name, tmp_path_factory))
     info = s.info()
@@ -54,6 +62,13 @@ def test_gpu_sah_equals_host_build(tmp_path_factory, name):
     assert st["depth"] == info["bvh_depth"] and st["nodes"] == info["bvh_nodes"]
     assert st["nodes4"] == info["bvh4_nodes"] and st["depth4"] == info["bvh4_depth"]
     assert st["stack4"] == info["bvh4_stack"] and st["method"] == 1
+    # one sequence: the init, the level budget's split launches, 8 finishing
+    # launches -- and, past the budget, a reset, the next levels, 8 again
+    budget = math.ceil(math.log2(info["num_geometry"] + 1)) + 6
+    rounds = 1 if info["bvh_depth"] <= budget else 2
+    assert st["launches"] == 1 + min(rounds * budget, 63) + 8 * rounds + (rounds - 1)
+    if name == "chain96":
+        assert rounds == 2
     print(f"{name}: {info['num_geometry']} tris, {st['nodes']} nodes, {st['launches']} launches, "
           f"build {st['build_ms']:.2f} ms (kernels {st['kernel_ms']:.2f}), host {info['bvh_ms']:.2f} ms")
     r.close()
@@ -81,5 +96,28 @@ def test_frames_over_gpu_sah_equal_oracle(oracle_lib, mode):
     for key in ("node_visits", "tri_tests", "layer_tests", "shadow_rays", "occluded", "bounce_rays"):
         assert st[key] == host_st[key], key
     assert st["shadow_rays"] == k["shadow_rays"] and st["occluded"] == k["occluded"]
+    r.close()
+    s.close()
+
+
+def test_gpu_sah_rebuild(tmp_path_factory):
+    """A rebuild with the image and scratch resident: the same arrays every
+    time, in well under a millisecond for tekkaman (one launch sequence, one
+    read-back; the first build also loads the image)."""
+    s = rt.Scene.load(_scene("tekkaman", tmp_path_factory))
+    r = rt.Renderer(s)
+    first = r.bvh_stats()
+    ref = r.export_bvh(), r.export_bvh4(), r.export_bvh4h()
+    times = []
+    for _ in range(4):
+        st = r.build_bvh("sah")
+        times.append(st["build_ms"])
+        (n2, t2), n4, h4 = r.export_bvh(), r.export_bvh4(), r.export_bvh4h()
+        assert np.array_equal(n2.view(np.uint32), ref[0][0].view(np.uint32))
+        assert np.array_equal(t2.view(np.uint32), ref[0][1].view(np.uint32))
+        assert np.array_equal(n4.view(np.uint32), ref[1].view(np.uint32)) and np.array_equal(h4, ref[2])
+    print(f"tekkaman SAH build: first {first['build_ms']:.3f} ms, rebuilds {[round(t, 3) for t in times]} ms, "
+          f"{st['launches']} launches")
+    assert min(times) < 1.0
     r.close()
     s.close()
