@@ -15,6 +15,11 @@
 namespace {
 
 constexpr uint32_t kWaves = SAH_BLOCK / 64;
+// triangles per thread per pass of a workgroup segment's loops (their loads
+// in flight together; a partition round is SAH_ITEMS * SAH_BLOCK triangles,
+// whose counts fit the 16-bit halves of one word)
+#define SAH_ITEMS 4
+static_assert(SAH_ITEMS * SAH_BLOCK < 65536, "partition round counts in 16 bits");
 
 __device__ __forceinline__ uint32_t lane_id() {
   return __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
@@ -114,7 +119,7 @@ struct SplitLds {  // a workgroup's segment
   uint32_t bin[3][SAH_BINS][7];         // lo xyz, hi xyz (ordered), count
   uint32_t side[2][6];                  // child boxes by reduction (median / root)
   Decision dec;
-  uint32_t wl[kWaves], wr[kWaves], lbase, rbase;
+  uint32_t wsum[kWaves], lbase, rbase;  // partition round: per-wave (left | right << 16) counts
 };
 struct SmallLds {  // a wave's segment (<= SAH_SMALL triangles)
   uint32_t bin[3][SAH_BINS][7];
@@ -195,23 +200,37 @@ __device__ void emit_node(const sah_arg_t* a, uint32_t L, const sah_seg_t& sg, u
   int32_t ref[2];
   const uint32_t b = sg.b, e = sg.e;
   const uint32_t cb[2] = {b, b + nl}, ce[2] = {b + nl, e};
+  // the internal children's node ids and next-level slots: one atomic per
+  // counter per node, not per child (every segment of a level bumps the same
+  // few words); the tree depth is set per level (phase_split)
+  bool inner[2], small[2];
+  uint32_t nin = 0, nsmall = 0;
+  for (int q = 0; q < 2; ++q) {
+    const uint32_t m = ce[q] - cb[q];
+    inner[q] = m > SAH_LEAF;
+    small[q] = m <= SAH_SMALL;
+    nin += inner[q] ? 1u : 0u;
+    nsmall += inner[q] && small[q] ? 1u : 0u;
+  }
+  uint32_t id0 = 0, s_small = 0, s_big = 0;
+  if (nin) id0 = atomicAdd(&ctl[SAH_CTL_NODES], nin);
+  if (nsmall) s_small = atomicAdd(&ctl[SAH_CTL_SMALL + L + 1], nsmall);
+  if (nin > nsmall) s_big = atomicAdd(&ctl[SAH_CTL_SEG + L + 1], nin - nsmall);
   for (int q = 0; q < 2; ++q) {
     const uint32_t m = ce[q] - cb[q];
     if (m == 0) {
       ref[q] = RT_EMPTY_REF;  // only the small root's second child
-    } else if (m <= SAH_LEAF) {
+    } else if (!inner[q]) {
       ref[q] = (int32_t)(RT_LEAF_FLAG | (cb[q] << 4) | (m - 1));
     } else {
-      const bool small = m <= SAH_SMALL;
-      const uint32_t id = atomicAdd(&ctl[SAH_CTL_NODES], 1u);
-      const uint32_t slot = atomicAdd(&ctl[(small ? SAH_CTL_SMALL : SAH_CTL_SEG) + L + 1], 1u);
+      const uint32_t id = id0++;
+      const uint32_t slot = small[q] ? s_small++ : s_big++;
       if (id >= a->n || slot >= a->n || L + 2 >= SAH_MAX_LEVELS) {
         atomicOr(&ctl[SAH_CTL_ERR], 1u);
         ref[q] = RT_EMPTY_REF;
         continue;
       }
-      (small ? next_small : next)[slot] = sah_seg_t{cb[q], ce[q], id, sg.depth + 1};
-      atomicMax(&ctl[SAH_CTL_DEPTH], sg.depth + 1);
+      (small[q] ? next_small : next)[slot] = sah_seg_t{cb[q], ce[q], id, sg.depth + 1};
       ref[q] = (int32_t)id;
     }
   }
@@ -324,6 +343,8 @@ __device__ void phase_split(const sah_arg_t* a, uint32_t L) {
   __shared__ SplitShared U;
   SplitLds& S = U.big;
   const uint32_t tid = threadIdx.x, w = tid >> 6, l = lane_id();
+  // a level-L segment is a node of depth L + 1 (the root: level 0, depth 1)
+  if (blockIdx.x == 0 && tid == 0 && nseg + ctl[SAH_CTL_SMALL + L] > 0) atomicMax(&ctl[SAH_CTL_DEPTH], L + 1);
   const uint64_t lt = (l == 0) ? 0ull : (~0ull >> (64 - l));
   for (uint32_t si = blockIdx.x; si < nseg; si += gridDim.x) {
     const sah_seg_t sg = segs[si];
@@ -341,10 +362,19 @@ __device__ void phase_split(const sah_arg_t* a, uint32_t L) {
     }
     __syncthreads();
     float cl[3] = {INFINITY, INFINITY, INFINITY}, ch[3] = {-INFINITY, -INFINITY, -INFINITY};
-    for (uint32_t i = b + tid; i < e; i += SAH_BLOCK) {
-      const float4 c = cen[idx[i]];
-      cl[0] = fminf(cl[0], c.x); cl[1] = fminf(cl[1], c.y); cl[2] = fminf(cl[2], c.z);
-      ch[0] = fmaxf(ch[0], c.x); ch[1] = fmaxf(ch[1], c.y); ch[2] = fmaxf(ch[2], c.z);
+    // SAH_ITEMS triangles per thread per pass: their loads in flight together
+    for (uint32_t i0 = b + tid; i0 < e; i0 += SAH_ITEMS * SAH_BLOCK) {
+      uint32_t t[SAH_ITEMS];
+      float4 c[SAH_ITEMS];
+#pragma unroll
+      for (int j = 0; j < SAH_ITEMS; ++j) t[j] = idx[min(i0 + j * SAH_BLOCK, e - 1)];
+#pragma unroll
+      for (int j = 0; j < SAH_ITEMS; ++j) c[j] = cen[t[j]];
+#pragma unroll
+      for (int j = 0; j < SAH_ITEMS; ++j) {  // a clamped duplicate changes no min / max
+        cl[0] = fminf(cl[0], c[j].x); cl[1] = fminf(cl[1], c[j].y); cl[2] = fminf(cl[2], c[j].z);
+        ch[0] = fmaxf(ch[0], c[j].x); ch[1] = fmaxf(ch[1], c[j].y); ch[2] = fmaxf(ch[2], c[j].z);
+      }
     }
 #pragma unroll
     for (int k = 0; k < 3; ++k) {
@@ -367,16 +397,28 @@ __device__ void phase_split(const sah_arg_t* a, uint32_t L) {
     const bool split_node = n > SAH_LEAF;
     // 2. bins over every axis with extent (app/bvh.cpp split)
     if (split_node)
-      for (uint32_t i = b + tid; i < e; i += SAH_BLOCK) {
-        const uint32_t t = idx[i];
-        const float4 c = cen[t], lo = tbox[2 * t], hi = tbox[2 * t + 1];
-        for (int ax = 0; ax < 3; ++ax) {
-          const float ext = ch[ax] - cl[ax];
-          if (!(ext > 0.0f)) continue;
-          uint32_t* bn = S.bin[ax][bin_of(comp(c, ax), cl[ax], ext)];
-          atomicMin(&bn[0], ord(lo.x)); atomicMin(&bn[1], ord(lo.y)); atomicMin(&bn[2], ord(lo.z));
-          atomicMax(&bn[3], ord(hi.x)); atomicMax(&bn[4], ord(hi.y)); atomicMax(&bn[5], ord(hi.z));
-          atomicAdd(&bn[6], 1u);
+      for (uint32_t i0 = b + tid; i0 < e; i0 += SAH_ITEMS * SAH_BLOCK) {
+        uint32_t t[SAH_ITEMS];
+        float4 c[SAH_ITEMS], lo[SAH_ITEMS], hi[SAH_ITEMS];
+#pragma unroll
+        for (int j = 0; j < SAH_ITEMS; ++j) t[j] = idx[min(i0 + j * SAH_BLOCK, e - 1)];
+#pragma unroll
+        for (int j = 0; j < SAH_ITEMS; ++j) {
+          c[j] = cen[t[j]];
+          lo[j] = tbox[2 * t[j]];
+          hi[j] = tbox[2 * t[j] + 1];
+        }
+#pragma unroll
+        for (int j = 0; j < SAH_ITEMS; ++j) {
+          if (i0 + j * SAH_BLOCK >= e) break;  // (the count must not see the clamped duplicates)
+          for (int ax = 0; ax < 3; ++ax) {
+            const float ext = ch[ax] - cl[ax];
+            if (!(ext > 0.0f)) continue;
+            uint32_t* bn = S.bin[ax][bin_of(comp(c[j], ax), cl[ax], ext)];
+            atomicMin(&bn[0], ord(lo[j].x)); atomicMin(&bn[1], ord(lo[j].y)); atomicMin(&bn[2], ord(lo[j].z));
+            atomicMax(&bn[3], ord(hi[j].x)); atomicMax(&bn[4], ord(hi[j].y)); atomicMax(&bn[5], ord(hi[j].z));
+            atomicAdd(&bn[6], 1u);
+          }
         }
       }
     __syncthreads();
@@ -423,36 +465,56 @@ __device__ void phase_split(const sah_arg_t* a, uint32_t L) {
     //    (ballot ranks, rounds of SAH_BLOCK in order), else a copy; leaf
     //    ranges also go to the final order
     if (axis >= 0) {
+      // rounds of SAH_ITEMS * SAH_BLOCK triangles, thread tid holding the
+      // round's items SAH_ITEMS * tid .. + SAH_ITEMS - 1 (so thread order is
+      // triangle order): each thread's (left | right << 16) count, their
+      // exclusive prefix over the workgroup (a wave scan, then the waves'
+      // sums), the items placed in order from there
       const float ext = ch[axis] - cl[axis];
-      for (uint32_t r0 = b; r0 < e; r0 += SAH_BLOCK) {
-        const uint32_t i = r0 + tid;
-        const bool valid = i < e;
-        const uint32_t t = valid ? idx[i] : 0u;
-        const bool f = valid && (uint32_t)bin_of(comp(cen[t], axis), cl[axis], ext) < S.dec.s;
-        const bool g = valid && !f;
-        const uint64_t mL = __ballot(f), mR = __ballot(g);
-        if (l == 0) {
-          S.wl[w] = (uint32_t)__popcll(mL);
-          S.wr[w] = (uint32_t)__popcll(mR);
+      for (uint32_t r0 = b; r0 < e; r0 += SAH_ITEMS * SAH_BLOCK) {
+        const uint32_t i0 = r0 + SAH_ITEMS * tid;
+        uint32_t t[SAH_ITEMS];
+        float4 c[SAH_ITEMS];
+#pragma unroll
+        for (int j = 0; j < SAH_ITEMS; ++j) t[j] = idx[min(i0 + j, e - 1)];
+#pragma unroll
+        for (int j = 0; j < SAH_ITEMS; ++j) c[j] = cen[t[j]];
+        uint32_t fl = 0, cnt = 0;  // left bits; (left | right << 16)
+#pragma unroll
+        for (int j = 0; j < SAH_ITEMS; ++j) {
+          if (i0 + j >= e) break;
+          const bool f = (uint32_t)bin_of(comp(c[j], axis), cl[axis], ext) < S.dec.s;
+          fl |= f ? 1u << j : 0u;
+          cnt += f ? 1u : 0x10000u;
+        }
+        uint32_t inc = cnt;  // inclusive scan over the wave
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+          const uint32_t y = (uint32_t)__shfl_up((int)inc, o, 64);
+          if (l >= (uint32_t)o) inc += y;
+        }
+        if (l == 63) S.wsum[w] = inc;
+        __syncthreads();
+        uint32_t pre = inc - cnt, tot = 0;
+        for (uint32_t k = 0; k < kWaves; ++k) {
+          const uint32_t ws = S.wsum[k];
+          pre += k < w ? ws : 0u;
+          tot += ws;
+        }
+        uint32_t offL = b + S.lbase + (pre & 0xffffu), offR = b + nl + S.rbase + (pre >> 16);
+#pragma unroll
+        for (int j = 0; j < SAH_ITEMS; ++j) {
+          if (i0 + j >= e) break;
+          const bool f = (fl >> j) & 1u;
+          const uint32_t dst = f ? offL++ : offR++;
+          out[dst] = t[j];
+          if (f ? leaf0 : leaf1) fin[dst] = t[j];
         }
         __syncthreads();
-        uint32_t offL = S.lbase, offR = S.rbase;
-        for (uint32_t k = 0; k < w; ++k) {
-          offL += S.wl[k];
-          offR += S.wr[k];
+        if (tid == 0) {
+          S.lbase += tot & 0xffffu;
+          S.rbase += tot >> 16;
         }
-        if (valid) {
-          const uint32_t dst = f ? b + offL + (uint32_t)__popcll(mL & lt)
-                                 : b + nl + offR + (uint32_t)__popcll(mR & lt);
-          out[dst] = t;
-          if (f ? leaf0 : leaf1) fin[dst] = t;
-        }
-        __syncthreads();
-        if (tid == 0)
-          for (uint32_t k = 0; k < kWaves; ++k) {
-            S.lbase += S.wl[k];
-            S.rbase += S.wr[k];
-          }
         __syncthreads();
       }
     } else {
@@ -491,7 +553,15 @@ __device__ void phase_scan(uint32_t* x, uint32_t total) {
   const uint32_t chunk = (total + SAH_BLOCK - 1) / SAH_BLOCK;
   const uint32_t b0 = min(threadIdx.x * chunk, total), b1 = min(b0 + chunk, total);
   uint32_t sum = 0;
-  for (uint32_t i = b0; i < b1; ++i) sum += x[i];
+  uint32_t i = b0;
+  for (; i + 8 <= b1; i += 8) {  // eight loads in flight
+    uint32_t v[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] = x[i + j];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) sum += v[j];
+  }
+  for (; i < b1; ++i) sum += x[i];
   s[threadIdx.x] = sum;
   __syncthreads();
   for (uint32_t o = 1; o < SAH_BLOCK; o <<= 1) {
@@ -501,7 +571,17 @@ __device__ void phase_scan(uint32_t* x, uint32_t total) {
     __syncthreads();
   }
   uint32_t run = s[threadIdx.x] - sum;
-  for (uint32_t i = b0; i < b1; ++i) {
+  for (i = b0; i + 8 <= b1; i += 8) {
+    uint32_t v[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] = x[i + j];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      x[i + j] = run;
+      run += v[j];
+    }
+  }
+  for (; i < b1; ++i) {
     const uint32_t v = x[i];
     x[i] = run;
     run += v;
@@ -632,45 +712,55 @@ __device__ void phase_cs(const sah_arg_t* a) {
 
 // BVH4 membership: walk the node's root path down, following the BVH4 node
 // whose expansion the path is in; depth and the worst-case stack (the sum of
-// (children - 1) over the BVH4 nodes of the path) of every BVH4 node
+// (children - 1) over the BVH4 nodes of the path) of every BVH4 node.  The
+// path is kept as one bit per step (no per-thread array, which would live in
+// scratch memory): in preorder a node's first internal child is the node
+// right after it, so the way up records whether each step came from that
+// child (bit 0) or from the other one (bit 1, its id read from the parent's
+// record on the way down).
 __device__ void phase_mark(const sah_arg_t* a) {
   const int32_t* parent = vx_ptr<const int32_t>(a->parent_addr);
   const int32_t* cs = vx_ptr<const int32_t>(a->cs_addr);
+  const int32_t* nodes = vx_ptr<const int32_t>(a->nodes_addr);  // rt_node_t: refs at words 12, 13
   uint32_t* is4 = vx_ptr<uint32_t>(a->is4_addr);
   uint32_t* ctl = vx_ptr<uint32_t>(a->ctl_addr);
   const uint32_t nn = ctl[SAH_CTL_NODES];
   for (uint32_t m = blockIdx.x * SAH_BLOCK + threadIdx.x; m < nn; m += gridDim.x * SAH_BLOCK) {
-    int32_t path[SAH_MAX_LEVELS];
+    uint64_t bits = 0;
     int len = 0;
     int32_t x = (int32_t)m;
-    while (x >= 0 && len < SAH_MAX_LEVELS) {
-      path[len++] = x;
-      x = parent[x];
+    while (x > 0 && len < SAH_MAX_LEVELS - 1) {
+      const int32_t p = parent[x];
+      if (x != p + 1) bits |= 1ull << len;
+      ++len;
+      x = p;
     }
-    if (x >= 0) {
+    if (x != 0) {  // no root within the level table
       atomicOr(&ctl[SAH_CTL_ERR], 2u);
       is4[m] = 0;
       continue;
     }
-    auto nch = [&](int32_t p) {
-      int k = 0;
-      while (k < 4 && cs[8 * p + k] != RT_EMPTY_REF) ++k;
-      return (uint32_t)k;
+    // a BVH4 node's children: the expansion's refs (one 16-B load); their
+    // count = the refs before the first empty one
+    const int4* cs4 = reinterpret_cast<const int4*>(cs);
+    auto nch = [](const int4& r) {
+      return r.x == RT_EMPTY_REF ? 0u : r.y == RT_EMPTY_REF ? 1u : r.z == RT_EMPTY_REF ? 2u : r.w == RT_EMPTY_REF ? 3u : 4u;
     };
-    int32_t cur = path[len - 1];  // the root
-    uint32_t depth4 = 1, stack = nch(cur) > 0 ? nch(cur) - 1 : 0;
-    bool member = len == 1;
-    for (int k = len - 2; k >= 0; --k) {
-      const int32_t p = path[k];
-      bool in = false;
-      for (int i = 0; i < 4; ++i) in |= cs[8 * cur + i] == p;
+    int4 cc = cs4[0];  // the root's expansion
+    int32_t p = 0;
+    uint32_t depth4 = 1, stack = nch(cc) > 0 ? nch(cc) - 1 : 0;
+    bool member = len == 0;
+    for (int k = len - 1; k >= 0; --k) {
+      const int32_t c = ((bits >> k) & 1ull) ? nodes[16 * p + 13] : p + 1;
+      const bool in = cc.x == c || cc.y == c || cc.z == c || cc.w == c;
       if (in) {
-        cur = p;
+        cc = cs4[2 * c];
         ++depth4;
-        const uint32_t c = nch(p);
-        stack += c > 0 ? c - 1 : 0;
+        const uint32_t n4 = nch(cc);
+        stack += n4 > 0 ? n4 - 1 : 0;
       }
       if (k == 0) member = in;
+      p = c;
     }
     is4[m] = member ? 1u : 0u;
     if (member) {
