@@ -162,7 +162,9 @@ typedef struct {
                            RT/PT kernels), RT_BVH_STACK4_UNUSED if it exceeds the deep
                            images' stack and the BVH2 is traversed instead */
   double build_ms;      /* host wall time of the whole build (upload + launches) */
-  double kernel_ms;     /* sum of the build kernels' HIP-event times */
+  double kernel_ms;     /* LBVH: sum of the build kernels' HIP-event times; SAH: host wall time
+                           of the launch sequence and its one read-back (per-launch event
+                           times under env RT_SAH_TRACE) */
   uint32_t nodes4;      /* rt_node4_t records (LBVH: one per BVH2 index, zeros at absorbed nodes) */
   uint32_t depth4;      /* BVH4 depth (SAH build; 0 for the LBVH) */
   uint32_t method;      /* RT_BVH_BUILD_* */
@@ -172,8 +174,12 @@ int rt_renderer_build_bvh(rt_renderer_h r, rt_bvh_build_stats_t* stats);  /* = _
 /* RT_BVH_BUILD_LBVH: Morton codes + radix tree (kernels/bvh_build.hip, 19
  * launches, fastest build).  RT_BVH_BUILD_SAH: the host builder's binned-SAH
  * tree, BVH4 collapse and binary16 planes restated on the device
- * (kernels/bvh_sah.hip, one launch per level + 8): the same arrays as the
- * scene's host build, bit for bit. */
+ * (kernels/bvh_sah.hip): one stream-ordered launch sequence -- the init, a
+ * split launch per tree level for a budget of log2(n) + 6 levels, 7
+ * finishing launches -- with one read-back at the end (a deeper tree
+ * continues once per further budget); the same arrays as the scene's host
+ * build, bit for bit.  The build image and its scratch stay with the
+ * renderer, so a rebuild loads nothing. */
 #define RT_BVH_BUILD_LBVH 0u
 #define RT_BVH_BUILD_SAH 1u
 #define RT_BVH_BUILD_HOST 2u  /* the scene's host build (app/bvh.cpp) uploaded: env RT_BVH=host */

@@ -1345,7 +1345,7 @@ static int build_lbvh(rt_renderer_h r, rt_bvh_build_stats_t* st) {
 // the same binned-SAH tree, BVH4 collapse and binary16 planes bit for bit.
 // One stream-ordered launch sequence (launch i runs seq[i], its launch tag):
 // the init, one split launch per tree level for a level budget, then the
-// numbering, emission and collapse -- every count a launch needs is read on
+// numbering, emission and collapse (7 launches) -- every count a launch needs is read on
 // the device, so the host waits once, for the control words.  A tree deeper
 // than the budget continues with the next levels and the finishing phases
 // again.  The image and the scratch arrays stay with the renderer (a free
@@ -1459,7 +1459,7 @@ static int build_sah(rt_renderer_h r, rt_bvh_build_stats_t* st) {
   for (uint32_t L = 0;;) {
     const uint32_t lend = std::min<uint32_t>(L + budget, SAH_MAX_LEVELS - 1);
     for (; L < lend; ++L) seq.push_back(SAH_SEQ(SAH_SPLIT, L));
-    for (const uint32_t ph : {SAH_NUMBER, SAH_SCAN, SAH_EMIT, SAH_CS, SAH_MARK, SAH_SCAN4, SAH_EMIT4, SAH_HALF})
+    for (const uint32_t ph : {SAH_NUMBER, SAH_SCAN, SAH_EMIT, SAH_CS, SAH_MARK, SAH_SCAN4, SAH_EMIT4})
       seq.push_back(SAH_SEQ(ph, 0));
     const auto tr = std::chrono::steady_clock::now();
     if (run(seq) || vx_copy_from_dev(c, r->su.sah.h, ctl_off, sizeof(c)) != 0)

@@ -775,7 +775,12 @@ __device__ void phase_emit4(const sah_arg_t* a) {
   const int32_t* cs = vx_ptr<const int32_t>(a->cs_addr);
   const uint32_t* pre4 = vx_ptr<const uint32_t>(a->is4_addr);
   rt_node4_t* nodes4 = vx_ptr<rt_node4_t>(a->nodes4_addr);
-  const uint32_t nn = vx_ptr<const uint32_t>(a->ctl_addr)[SAH_CTL_NODES];
+  uint32_t* ctl = vx_ptr<uint32_t>(a->ctl_addr);
+  const uint32_t nn = ctl[SAH_CTL_NODES];
+  // the binary16 records (rt_node4h_t) follow the nn4 rt_node4_t records
+  const uint32_t nn4 = pre4[nn];  // the membership scan's total
+  uint32_t* half = vx_ptr<uint32_t>(a->nodes4_addr + 128ull * (uint64_t)nn4);
+  if (blockIdx.x == 0 && threadIdx.x == 0) ctl[SAH_CTL_NODES4] = nn4;
   for (uint32_t m = blockIdx.x * SAH_BLOCK + threadIdx.x; m < nn; m += gridDim.x * SAH_BLOCK) {
     if (pre4[m + 1] == pre4[m]) continue;  // not a BVH4 node
     float v[32];
@@ -794,19 +799,12 @@ __device__ void phase_emit4(const sah_arg_t* a) {
       }
       v[24 + i] = __int_as_float(ref);
     }
+    // the planes rounded outward to binary16 (in v: the fp32 record keeps
+    // the rounded planes too) and the half record
+    half4_node(v, half + 16ull * pre4[m]);
     float4* o = reinterpret_cast<float4*>(nodes4 + pre4[m]);
     for (int q = 0; q < 8; ++q) o[q] = make_float4(v[4 * q], v[4 * q + 1], v[4 * q + 2], v[4 * q + 3]);
   }
-}
-
-__device__ void phase_half(const sah_arg_t* a) {
-  const uint32_t nn = vx_ptr<const uint32_t>(a->ctl_addr)[SAH_CTL_NODES];
-  const uint32_t nn4 = vx_ptr<const uint32_t>(a->is4_addr)[nn];  // the membership scan's total
-  rt_node4_t* nodes4 = vx_ptr<rt_node4_t>(a->nodes4_addr);
-  uint32_t* half = vx_ptr<uint32_t>(a->nodes4_addr + 128ull * (uint64_t)nn4);
-  if (blockIdx.x == 0 && threadIdx.x == 0) vx_ptr<uint32_t>(a->ctl_addr)[SAH_CTL_NODES4] = nn4;
-  for (uint32_t i = blockIdx.x * SAH_BLOCK + threadIdx.x; i < nn4; i += gridDim.x * SAH_BLOCK)
-    half4_node(nodes4[i].v, half + 16 * i);
 }
 
 // the numbering's counters as SAH_INIT leaves them, and the collapse's
@@ -846,7 +844,6 @@ VX_MAIN(sah_arg_t, arg, SAH_BLOCK) {
     case SAH_CS: phase_cs(arg); break;
     case SAH_MARK: phase_mark(arg); break;
     case SAH_EMIT4: phase_emit4(arg); break;
-    case SAH_HALF: phase_half(arg); break;
     case SAH_RESET: phase_reset(arg); break;
     case SAH_SCAN4:
       phase_scan(vx_ptr<uint32_t>(arg->is4_addr), vx_ptr<const uint32_t>(arg->ctl_addr)[SAH_CTL_NODES]);

@@ -25,7 +25,9 @@
 
 #include <stdint.h>
 
+#ifndef SAH_BLOCK
 #define SAH_BLOCK 256
+#endif
 #define SAH_BINS 16
 #define SAH_LEAF 4
 #define SAH_SMALL 64             // segments up to this many triangles: one wave each
@@ -40,8 +42,9 @@ enum {
   SAH_EMIT = 4,    // rt_node_t at preorder indices, parents, rt_tri_t in leaf order
   SAH_CS = 5,      // BVH4 expansion of every BVH2 node
   SAH_MARK = 6,    // BVH4 membership, depth, worst-case stack (root-path walks)
-  SAH_EMIT4 = 7,   // rt_node4_t at BVH4 preorder indices
-  SAH_HALF = 8,    // binary16 planes (rt_node4h_t behind the rt_node4_t array)
+  SAH_EMIT4 = 7,   // rt_node4_t at BVH4 preorder indices, planes rounded outward to binary16,
+                   // and the rt_node4h_t records behind the rt_node4_t array
+                   // (8: the binary16 pass, folded into SAH_EMIT4 in r04)
   SAH_RESET = 9,   // the numbering's counters again (a sequence continued past its level budget)
   SAH_SCAN4 = 10,  // exclusive scan of the BVH4 membership (is4, one word per BVH2 node)
 };
@@ -55,7 +58,7 @@ enum {
 #define SAH_CTL_DEPTH4 3   // BVH4 depth
 #define SAH_CTL_STACK4 4   // BVH4 worst-case traversal stack
 #define SAH_CTL_ERR 5      // != 0: capacity / depth overflow
-#define SAH_CTL_NODES4 6   // BVH4 nodes (SAH_HALF: the membership scan's total)
+#define SAH_CTL_NODES4 6   // BVH4 nodes (SAH_EMIT4: the membership scan's total)
 #define SAH_CTL_SEG 8      // [SAH_CTL_SEG + L]: workgroup segments of level L
 #define SAH_CTL_SMALL (SAH_CTL_SEG + SAH_MAX_LEVELS + 1)  // [.. + L]: wave segments of level L
 #define SAH_CTL_WORDS (SAH_CTL_SMALL + SAH_MAX_LEVELS + 1)

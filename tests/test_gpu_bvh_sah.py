@@ -62,11 +62,11 @@ def test_gpu_sah_equals_host_build(tmp_path_factory, name):
     assert st["depth"] == info["bvh_depth"] and st["nodes"] == info["bvh_nodes"]
     assert st["nodes4"] == info["bvh4_nodes"] and st["depth4"] == info["bvh4_depth"]
     assert st["stack4"] == info["bvh4_stack"] and st["method"] == 1
-    # one sequence: the init, the level budget's split launches, 8 finishing
-    # launches -- and, past the budget, a reset, the next levels, 8 again
+    # one sequence: the init, the level budget's split launches, 7 finishing
+    # launches -- and, past the budget, a reset, the next levels, 7 again
     budget = math.ceil(math.log2(info["num_geometry"] + 1)) + 6
     rounds = 1 if info["bvh_depth"] <= budget else 2
-    assert st["launches"] == 1 + min(rounds * budget, 63) + 8 * rounds + (rounds - 1)
+    assert st["launches"] == 1 + min(rounds * budget, 63) + 7 * rounds + (rounds - 1)
     if name == "chain96":
         assert rounds == 2
     print(f"{name}: {info['num_geometry']} tris, {st['nodes']} nodes, {st['launches']} launches, "
