@@ -725,6 +725,9 @@ __device__ void phase_mark(const sah_arg_t* a) {
   uint32_t* is4 = vx_ptr<uint32_t>(a->is4_addr);
   uint32_t* ctl = vx_ptr<uint32_t>(a->ctl_addr);
   const uint32_t nn = ctl[SAH_CTL_NODES];
+  // the BVH4 depth and stack maxima: per lane over its nodes, then one
+  // atomic per wave (one per member node serialised on the two words)
+  uint32_t dmax = 0, smax = 0;
   for (uint32_t m = blockIdx.x * SAH_BLOCK + threadIdx.x; m < nn; m += gridDim.x * SAH_BLOCK) {
     uint64_t bits = 0;
     int len = 0;
@@ -764,9 +767,18 @@ __device__ void phase_mark(const sah_arg_t* a) {
     }
     is4[m] = member ? 1u : 0u;
     if (member) {
-      atomicMax(&ctl[SAH_CTL_DEPTH4], depth4);
-      atomicMax(&ctl[SAH_CTL_STACK4], stack);
+      dmax = max(dmax, depth4);
+      smax = max(smax, stack);
     }
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    dmax = max(dmax, (uint32_t)__shfl_xor((int)dmax, o, 64));
+    smax = max(smax, (uint32_t)__shfl_xor((int)smax, o, 64));
+  }
+  if (lane_id() == 0 && dmax != 0) {
+    atomicMax(&ctl[SAH_CTL_DEPTH4], dmax);
+    atomicMax(&ctl[SAH_CTL_STACK4], smax);
   }
 }
 
