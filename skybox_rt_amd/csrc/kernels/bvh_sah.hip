@@ -191,46 +191,46 @@ __device__ void sah_price(const uint32_t (*bin)[SAH_BINS][7], const float* cl, c
 
 // The node record of segment sg (split at b + nl; child boxes bx) and its
 // children: <= SAH_LEAF triangles a leaf, <= SAH_SMALL a segment of the
-// next level's wave list, else of its workgroup list (one thread)
-__device__ void emit_node(const sah_arg_t* a, uint32_t L, const sah_seg_t& sg, uint32_t nl,
-                          const float (*bx)[6]) {
+// next level's wave list, else of its workgroup list (one thread).  Node ids
+// and next-level slots come in blocks: `need` counts a node's internal
+// children (and the small ones among them), `emit_node_at` places them from
+// the bases the caller allocated -- every segment of a level bumps the same
+// few counter words, so they are bumped once per node (emit_node) or once
+// per workgroup round (split_small), and the tree depth once per level
+// (phase_split)
+__device__ __forceinline__ void node_needs(const sah_seg_t& sg, uint32_t nl, uint32_t* nin, uint32_t* nsmall) {
+  const uint32_t m[2] = {nl, sg.e - sg.b - nl};
+  *nin = *nsmall = 0;
+  for (int q = 0; q < 2; ++q)
+    if (m[q] > SAH_LEAF) {
+      ++*nin;
+      *nsmall += m[q] <= SAH_SMALL ? 1u : 0u;
+    }
+}
+__device__ void emit_node_at(const sah_arg_t* a, uint32_t L, const sah_seg_t& sg, uint32_t nl,
+                             const float (*bx)[6], uint32_t id0, uint32_t s_small, uint32_t s_big) {
   uint32_t* ctl = vx_ptr<uint32_t>(a->ctl_addr);
   sah_seg_t* next = vx_ptr<sah_seg_t>(a->segs_addr[(L + 1) & 1]);
   sah_seg_t* next_small = vx_ptr<sah_seg_t>(a->small_addr[(L + 1) & 1]);
   int32_t ref[2];
   const uint32_t b = sg.b, e = sg.e;
   const uint32_t cb[2] = {b, b + nl}, ce[2] = {b + nl, e};
-  // the internal children's node ids and next-level slots: one atomic per
-  // counter per node, not per child (every segment of a level bumps the same
-  // few words); the tree depth is set per level (phase_split)
-  bool inner[2], small[2];
-  uint32_t nin = 0, nsmall = 0;
-  for (int q = 0; q < 2; ++q) {
-    const uint32_t m = ce[q] - cb[q];
-    inner[q] = m > SAH_LEAF;
-    small[q] = m <= SAH_SMALL;
-    nin += inner[q] ? 1u : 0u;
-    nsmall += inner[q] && small[q] ? 1u : 0u;
-  }
-  uint32_t id0 = 0, s_small = 0, s_big = 0;
-  if (nin) id0 = atomicAdd(&ctl[SAH_CTL_NODES], nin);
-  if (nsmall) s_small = atomicAdd(&ctl[SAH_CTL_SMALL + L + 1], nsmall);
-  if (nin > nsmall) s_big = atomicAdd(&ctl[SAH_CTL_SEG + L + 1], nin - nsmall);
   for (int q = 0; q < 2; ++q) {
     const uint32_t m = ce[q] - cb[q];
     if (m == 0) {
       ref[q] = RT_EMPTY_REF;  // only the small root's second child
-    } else if (!inner[q]) {
+    } else if (m <= SAH_LEAF) {
       ref[q] = (int32_t)(RT_LEAF_FLAG | (cb[q] << 4) | (m - 1));
     } else {
+      const bool small = m <= SAH_SMALL;
       const uint32_t id = id0++;
-      const uint32_t slot = small[q] ? s_small++ : s_big++;
+      const uint32_t slot = small ? s_small++ : s_big++;
       if (id >= a->n || slot >= a->n || L + 2 >= SAH_MAX_LEVELS) {
         atomicOr(&ctl[SAH_CTL_ERR], 1u);
         ref[q] = RT_EMPTY_REF;
         continue;
       }
-      (small[q] ? next_small : next)[slot] = sah_seg_t{cb[q], ce[q], id, sg.depth + 1};
+      (small ? next_small : next)[slot] = sah_seg_t{cb[q], ce[q], id, sg.depth + 1};
       ref[q] = (int32_t)id;
     }
   }
@@ -240,6 +240,17 @@ __device__ void emit_node(const sah_arg_t* a, uint32_t L, const sah_seg_t& sg, u
   nb[1] = make_float4(bx[0][3], bx[0][4], bx[0][5], 0.0f);
   nb[2] = make_float4(bx[1][0], bx[1][1], bx[1][2], 0.0f);
   nb[3] = make_float4(bx[1][3], bx[1][4], bx[1][5], 0.0f);
+}
+__device__ void emit_node(const sah_arg_t* a, uint32_t L, const sah_seg_t& sg, uint32_t nl,
+                          const float (*bx)[6]) {
+  uint32_t* ctl = vx_ptr<uint32_t>(a->ctl_addr);
+  uint32_t nin, nsmall;
+  node_needs(sg, nl, &nin, &nsmall);
+  uint32_t id0 = 0, s_small = 0, s_big = 0;
+  if (nin) id0 = atomicAdd(&ctl[SAH_CTL_NODES], nin);
+  if (nsmall) s_small = atomicAdd(&ctl[SAH_CTL_SMALL + L + 1], nsmall);
+  if (nin > nsmall) s_big = atomicAdd(&ctl[SAH_CTL_SEG + L + 1], nin - nsmall);
+  emit_node_at(a, L, sg, nl, bx, id0, s_small, s_big);
 }
 
 __device__ __forceinline__ float wmin(float x) {
@@ -251,6 +262,28 @@ __device__ __forceinline__ float wmax(float x) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) x = fmaxf(x, __shfl_xor(x, o, 64));
   return x;
+}
+
+// one thread: the round's node ids and next-level slots for the workgroup's
+// waves (their needs in s_need), one atomic per counter
+__device__ __forceinline__ void small_alloc(uint32_t* ctl, uint32_t L, const uint32_t (*need)[2],
+                                            uint32_t (*base)[3]) {
+  uint32_t tin = 0, tsmall = 0;
+  for (uint32_t k = 0; k < kWaves; ++k) {
+    tin += need[k][0];
+    tsmall += need[k][1];
+  }
+  uint32_t id = tin ? atomicAdd(&ctl[SAH_CTL_NODES], tin) : 0u;
+  uint32_t ss = tsmall ? atomicAdd(&ctl[SAH_CTL_SMALL + L + 1], tsmall) : 0u;
+  uint32_t sb = tin > tsmall ? atomicAdd(&ctl[SAH_CTL_SEG + L + 1], tin - tsmall) : 0u;
+  for (uint32_t k = 0; k < kWaves; ++k) {
+    base[k][0] = id;
+    base[k][1] = ss;
+    base[k][2] = sb;
+    id += need[k][0];
+    ss += need[k][1];
+    sb += need[k][0] - need[k][1];
+  }
 }
 
 // Segments of <= SAH_SMALL (64) triangles, one per wave (the deep levels'
@@ -265,68 +298,88 @@ __device__ void split_small(const sah_arg_t* a, uint32_t L, SmallLds& W, uint32_
   uint32_t* fin = vx_ptr<uint32_t>(a->final_addr);
   const float4* cen = vx_ptr<const float4>(a->cen_addr);
   const float4* tbox = vx_ptr<const float4>(a->tbox_addr);
-  for (uint32_t si = blockIdx.x * kWaves + w; si < nseg; si += gridDim.x * kWaves) {
-    const sah_seg_t sg = segs[si];
-    const uint32_t b = sg.b, n = sg.e - sg.b;  // 5 .. SAH_SMALL
-    const bool valid = l < n;
-    const uint32_t i = b + l;
-    const uint32_t t = valid ? idx[i] : 0u;
-    const float4 c = cen[t], lo = tbox[2 * t], hi = tbox[2 * t + 1];
-    float cl[3], ch[3];
-    for (int k = 0; k < 3; ++k) {
-      cl[k] = wmin(valid ? comp(c, k) : INFINITY);
-      ch[k] = wmax(valid ? comp(c, k) : -INFINITY);
-    }
-    uint32_t* bins = &W.bin[0][0][0];
-    for (uint32_t k = l; k < 3 * SAH_BINS * 7; k += 64) {
-      const uint32_t f = k % 7;
-      bins[k] = f < 3 ? ord(INFINITY) : (f < 6 ? ord(-INFINITY) : 0u);
-    }
-    if (l == 0) W.dec.axis = -1;
-    __builtin_amdgcn_wave_barrier();  // (one wave: its LDS operations complete in order)
-    if (valid)
-      for (int ax = 0; ax < 3; ++ax) {
-        const float ext = ch[ax] - cl[ax];
-        if (!(ext > 0.0f)) continue;
-        uint32_t* bn = W.bin[ax][bin_of(comp(c, ax), cl[ax], ext)];
-        atomicMin(&bn[0], ord(lo.x)); atomicMin(&bn[1], ord(lo.y)); atomicMin(&bn[2], ord(lo.z));
-        atomicMax(&bn[3], ord(hi.x)); atomicMax(&bn[4], ord(hi.y)); atomicMax(&bn[5], ord(hi.z));
-        atomicAdd(&bn[6], 1u);
-      }
-    __builtin_amdgcn_wave_barrier();
-    sah_price(W.bin, cl, ch, l, &W.dec);
-    __builtin_amdgcn_wave_barrier();
-    const int axis = W.dec.axis;
-    const uint32_t nl = axis >= 0 ? W.dec.nl : n / 2;
-    const bool leaf0 = nl <= SAH_LEAF, leaf1 = n - nl <= SAH_LEAF;
+  // rounds of one segment per wave, the round's bound workgroup-uniform:
+  // the waves' node ids and next-level slots are allocated together
+  __shared__ uint32_t s_need[kWaves][2], s_base[kWaves][3];
+  uint32_t* ctl = vx_ptr<uint32_t>(a->ctl_addr);
+  for (uint32_t r0 = blockIdx.x * kWaves; r0 < nseg; r0 += gridDim.x * kWaves) {
+    const uint32_t si = r0 + w;
+    const bool have = si < nseg;  // wave-uniform: this wave has a segment this round
+    sah_seg_t sg{0, 0, 0, 0};
+    uint32_t nl = 0;
     float bx[2][6];
-    if (axis >= 0) {
-      for (int q = 0; q < 2; ++q)
-        for (int k = 0; k < 6; ++k) bx[q][k] = W.dec.box[q][k];
-      const float ext = ch[axis] - cl[axis];
-      const bool f = valid && (uint32_t)bin_of(comp(c, axis), cl[axis], ext) < W.dec.s;
-      const bool g = valid && !f;
-      const uint64_t mL = __ballot(f), mR = __ballot(g);
-      if (valid) {
-        const uint32_t dst = f ? b + (uint32_t)__popcll(mL & lt) : b + nl + (uint32_t)__popcll(mR & lt);
-        out[dst] = t;
-        if (f ? leaf0 : leaf1) fin[dst] = t;
+    if (have) {
+      sg = segs[si];
+      const uint32_t b = sg.b, n = sg.e - sg.b;  // 5 .. SAH_SMALL
+      const bool valid = l < n;
+      const uint32_t i = b + l;
+      const uint32_t t = valid ? idx[i] : 0u;
+      const float4 c = cen[t], lo = tbox[2 * t], hi = tbox[2 * t + 1];
+      float cl[3], ch[3];
+      for (int k = 0; k < 3; ++k) {
+        cl[k] = wmin(valid ? comp(c, k) : INFINITY);
+        ch[k] = wmax(valid ? comp(c, k) : -INFINITY);
       }
-    } else {  // the median: order unchanged, boxes of the two halves
-      const bool left = l < nl;
-      for (int q = 0; q < 2; ++q) {
-        const bool in = valid && (q == 0) == left;
-        for (int k = 0; k < 3; ++k) {
-          bx[q][k] = wmin(in ? comp(lo, k) : INFINITY);
-          bx[q][3 + k] = wmax(in ? comp(hi, k) : -INFINITY);
+      uint32_t* bins = &W.bin[0][0][0];
+      for (uint32_t k = l; k < 3 * SAH_BINS * 7; k += 64) {
+        const uint32_t f = k % 7;
+        bins[k] = f < 3 ? ord(INFINITY) : (f < 6 ? ord(-INFINITY) : 0u);
+      }
+      if (l == 0) W.dec.axis = -1;
+      __builtin_amdgcn_wave_barrier();  // (one wave: its LDS operations complete in order)
+      if (valid)
+        for (int ax = 0; ax < 3; ++ax) {
+          const float ext = ch[ax] - cl[ax];
+          if (!(ext > 0.0f)) continue;
+          uint32_t* bn = W.bin[ax][bin_of(comp(c, ax), cl[ax], ext)];
+          atomicMin(&bn[0], ord(lo.x)); atomicMin(&bn[1], ord(lo.y)); atomicMin(&bn[2], ord(lo.z));
+          atomicMax(&bn[3], ord(hi.x)); atomicMax(&bn[4], ord(hi.y)); atomicMax(&bn[5], ord(hi.z));
+          atomicAdd(&bn[6], 1u);
+        }
+      __builtin_amdgcn_wave_barrier();
+      sah_price(W.bin, cl, ch, l, &W.dec);
+      __builtin_amdgcn_wave_barrier();
+      const int axis = W.dec.axis;
+      nl = axis >= 0 ? W.dec.nl : n / 2;
+      const bool leaf0 = nl <= SAH_LEAF, leaf1 = n - nl <= SAH_LEAF;
+      if (axis >= 0) {
+        for (int q = 0; q < 2; ++q)
+          for (int k = 0; k < 6; ++k) bx[q][k] = W.dec.box[q][k];
+        const float ext = ch[axis] - cl[axis];
+        const bool f = valid && (uint32_t)bin_of(comp(c, axis), cl[axis], ext) < W.dec.s;
+        const bool g = valid && !f;
+        const uint64_t mL = __ballot(f), mR = __ballot(g);
+        if (valid) {
+          const uint32_t dst = f ? b + (uint32_t)__popcll(mL & lt) : b + nl + (uint32_t)__popcll(mR & lt);
+          out[dst] = t;
+          if (f ? leaf0 : leaf1) fin[dst] = t;
+        }
+      } else {  // the median: order unchanged, boxes of the two halves
+        const bool left = l < nl;
+        for (int q = 0; q < 2; ++q) {
+          const bool in = valid && (q == 0) == left;
+          for (int k = 0; k < 3; ++k) {
+            bx[q][k] = wmin(in ? comp(lo, k) : INFINITY);
+            bx[q][3 + k] = wmax(in ? comp(hi, k) : -INFINITY);
+          }
+        }
+        if (valid) {
+          out[i] = t;
+          if (left ? leaf0 : leaf1) fin[i] = t;
         }
       }
-      if (valid) {
-        out[i] = t;
-        if (left ? leaf0 : leaf1) fin[i] = t;
+    }
+    if (l == 0) {
+      if (have) {
+        node_needs(sg, nl, &s_need[w][0], &s_need[w][1]);
+      } else {
+        s_need[w][0] = s_need[w][1] = 0;
       }
     }
-    if (l == 0) emit_node(a, L, sg, nl, bx);
+    __syncthreads();
+    if (threadIdx.x == 0) small_alloc(ctl, L, s_need, s_base);
+    __syncthreads();
+    if (have && l == 0) emit_node_at(a, L, sg, nl, bx, s_base[w][0], s_base[w][1], s_base[w][2]);
     __builtin_amdgcn_wave_barrier();  // W is reused by the wave's next segment
   }
 }
