@@ -175,7 +175,7 @@ int rt_renderer_build_bvh(rt_renderer_h r, rt_bvh_build_stats_t* stats);  /* = _
  * launches, fastest build).  RT_BVH_BUILD_SAH: the host builder's binned-SAH
  * tree, BVH4 collapse and binary16 planes restated on the device
  * (kernels/bvh_sah.hip): one stream-ordered launch sequence -- the init, a
- * split launch per tree level for a budget of log2(n) + 6 levels, 7
+ * split launch per tree level for a budget of log2(n) + 4 levels, 7
  * finishing launches -- with one read-back at the end (a deeper tree
  * continues once per further budget); the same arrays as the scene's host
  * build, bit for bit.  The build image and its scratch stay with the

@@ -1450,10 +1450,11 @@ static int build_sah(rt_renderer_h r, rt_bvh_build_stats_t* st) {
     return 0;
   };
   // the level budget: a binned-SAH tree over n triangles is rarely deeper
-  // than log2(n) + 6; a deeper one costs a second round trip
+  // than log2(n) + 4 (r04: the deepest of the reference scenes is log2(n) + 3); a
+  // deeper one costs a second round trip
   uint32_t lg = 0;
   while ((1ull << lg) < N + 1) ++lg;
-  const uint32_t budget = lg + 6;
+  const uint32_t budget = lg + 4;
   uint32_t c[SAH_CTL_WORDS];
   std::vector<uint32_t> seq{SAH_SEQ(SAH_INIT, 0)};
   for (uint32_t L = 0;;) {

@@ -48,7 +48,7 @@ def make_chain_scene(path: str, n: int, ratio: float = 1.6, base: float = 1e-3) 
     """n small triangles whose x centres grow geometrically (base * ratio^k,
     NDC): every binned-SAH split peels a few off the far end, so the tree is
     about n / 5 levels deep -- deeper than the device build's level budget
-    (log2 n + 6) for n = 96."""
+    (log2 n + 4) for n = 96."""
     k = np.arange(n, dtype=np.float64)
     w = np.full(n, 100.0)
     cx = base * ratio ** k * w

@@ -64,7 +64,7 @@ def test_gpu_sah_equals_host_build(tmp_path_factory, name):
     assert st["stack4"] == info["bvh4_stack"] and st["method"] == 1
     # one sequence: the init, the level budget's split launches, 7 finishing
     # launches -- and, past the budget, a reset, the next levels, 7 again
-    budget = math.ceil(math.log2(info["num_geometry"] + 1)) + 6
+    budget = math.ceil(math.log2(info["num_geometry"] + 1)) + 4
     rounds = 1 if info["bvh_depth"] <= budget else 2
     assert st["launches"] == 1 + min(rounds * budget, 63) + 7 * rounds + (rounds - 1)
     if name == "chain96":
