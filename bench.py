@@ -4,7 +4,11 @@
 Workload at N = 1 (BASELINE.json configs[2], the metric's config):
 tekkaman.cgltrace, 1024x1024, one primary ray per pixel (raster-exact, from
 the per-8x8-block candidate lists built on the device) + one any-hit shadow
-ray per geometry hit (binary16 BVH4, wave packets, ballot/mbcnt-compacted).
+ray per geometry hit (ballot/mbcnt-compacted into full waves, each lane
+scanning its light-space cell list -- the cube map of triangle lists around
+the point light, built on the device -- nearest to the light first).  The
+same frame by BVH traversal only (binary16 BVH4 wave-packet walks, stack in
+one VGPR) is timed beside it as series.bvh_walk.
 A "step" is one full frame: vx_start of the RT kernel image through
 libvortex-hip.so (inputs already resident in HBM), every frame complete
 inside the timed region.
@@ -286,10 +290,17 @@ def cpu_baseline(shadows: bool, side: int, light, budget_s: float, path: bool = 
                              cpu_model)
     except OSError:
         pass
+    # the algorithm rt_params selects (oracle/py_oracle.py: vis_lists and
+    # shadow_lists on by default), the same as the GPU image's
+    if flat:
+        algo = "brute force over the geometry list"
+    else:
+        algo = ("primary: 8x8-block candidate lists; "
+                + ("shadow: light-space cell lists" if shadows or path else "no shadow rays")
+                + (f"; bounce rays: {'BVH4' if bvh4 else 'BVH2'} traversal" if path else ""))
     return {"value": float(np.median(runs)), "unit": "Mrays/s", "cores": threads, "kind": "port",
             "sample": f"median of 5 timed runs ({frames_total} full {side}x{side} frames of the same "
-                      f"workload in ~{budget_s:.0f} s; oracle/rt.c "
-                      f"{'brute force' if flat else ('BVH4' if bvh4 else 'BVH2') + ' traversal'}, "
+                      f"workload in ~{budget_s:.0f} s; oracle/rt.c {algo}, "
                       f"{threads} threads = every CPU granted to this process: {len(cpus)} in the "
                       f"affinity set, cgroup quota {quota}) after a warm-up frame",
             "runs_mrays_per_s": [round(x, 3) for x in runs],
@@ -676,7 +687,9 @@ def main():
                          f"(BASELINE config 3): primary visibility by a {bvh_kind} packet walk per "
                          f"8x8-block wave (raster-exact leaf tests, node/leaf records through the "
                          f"scalar cache, wave stack in one VGPR); shadow rays ballot/mbcnt-compacted "
-                         f"into full waves, each a {bvh_kind} any-hit packet walk"),
+                         f"into full waves, each a {bvh_kind} any-hit packet walk (its traversal stack "
+                         f"also in one VGPR, v_writelane/v_readlane, not LDS: measured neutral against "
+                         f"an LDS stack, DESIGN.md 4.1)"),
             "image": "rt_bvh (entry vx_main_rt_bvh)", "side": side, "steps": args.steps,
             "warmup": args.warmup, "value": round(br.rays_local * args.steps / eb / 1e6, 3),
             "ms_per_step": round(eb / args.steps * 1e3, 5), "kernel_ms": round(kb, 5),

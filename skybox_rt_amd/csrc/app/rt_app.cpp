@@ -461,6 +461,9 @@ int rt_renderer_set_light(rt_renderer_h r, const float light[3]) {
 int rt_renderer_export_records(rt_renderer_h r, uint32_t which, void* out, uint64_t bytes,
                                uint64_t* size) {
   if (!r || !r->configured) return fail("renderer not configured");
+  // lists queued by rt_renderer_set_light: their entry count (and slist_on)
+  // are known once their status is read, before the exports are sized
+  if ((which == RT_REC_SIDX || which == RT_REC_SLIST) && rtapp::settle_lists(r) != 0) return -1;
   const rt_kernel_arg_t& a = r->arg;
   const bool raster = (r->params.flags & RT_RENDER_RASTER) != 0;
   const uint64_t np = r->sc->scene.prims.size();
@@ -1460,8 +1463,10 @@ static int build_sah(rt_renderer_h r, rt_bvh_build_stats_t* st) {
   for (uint32_t L = 0;;) {
     const uint32_t lend = std::min<uint32_t>(L + budget, SAH_MAX_LEVELS - 1);
     for (; L < lend; ++L) seq.push_back(SAH_SEQ(SAH_SPLIT, L));
+    // the finishing phases carry level lend: on the device they do nothing
+    // while that level still holds segments (a partial tree, bvh_sah.hip)
     for (const uint32_t ph : {SAH_NUMBER, SAH_SCAN, SAH_EMIT, SAH_CS, SAH_MARK, SAH_SCAN4, SAH_EMIT4})
-      seq.push_back(SAH_SEQ(ph, 0));
+      seq.push_back(SAH_SEQ(ph, lend));
     const auto tr = std::chrono::steady_clock::now();
     if (run(seq) || vx_copy_from_dev(c, r->su.sah.h, ctl_off, sizeof(c)) != 0)
       return fail("SAH build: launch or read-back failed");

@@ -900,7 +900,17 @@ VX_MAIN(sah_arg_t, arg, SAH_BLOCK) {
   if (vx_launch_tag >= arg->nseq || vx_launch_tag >= SAH_MAX_SEQ) return 0;
   const uint32_t e = arg->seq[vx_launch_tag];
   const uint32_t L = e >> 8;
-  switch (e & 0xffu) {
+  const uint32_t ph = e & 0xffu;
+  // the finishing phases carry the level after the sequence's last split
+  // level: while that level still holds segments the tree is partial (deeper
+  // than the host's level budget) -- node ids of the last split level have no
+  // records yet -- so they do nothing; the host continues with SAH_RESET, the
+  // next levels and the finishing phases again
+  if (ph != SAH_INIT && ph != SAH_SPLIT && ph != SAH_RESET && L < SAH_MAX_LEVELS) {
+    const uint32_t* ctl = vx_ptr<const uint32_t>(arg->ctl_addr);
+    if (ctl[SAH_CTL_SEG + L] != 0 || ctl[SAH_CTL_SMALL + L] != 0) return 0;
+  }
+  switch (ph) {
     case SAH_INIT: phase_init(arg); break;
     case SAH_SPLIT: phase_split(arg, L); break;
     case SAH_NUMBER: phase_number(arg); break;

@@ -226,6 +226,30 @@ def test_shadow_lists_equal_oracle(oracle_lib, name, light):
     s.close()
 
 
+def test_shadow_list_export_right_after_set_light(oracle_lib):
+    """rt_renderer_set_light queues the new light's lists without waiting;
+    an export straight after it reads their status first, so the SLIST
+    export is sized by the NEW light's entry count."""
+    po = oracle_lib
+    s = rt.Scene.load(scene_path("tekkaman"))
+    r = rt.Renderer(s)
+    first, second = (0.0, 0.0, 0.5), (0.0, 60.0, 80.0)  # few entries, then many
+    r.configure(64, 64, shadows=True, light=first)
+    n_first = r.setup_stats()["slist_entries"]
+    r.set_light(second)
+    slist = r.records("slist")        # no setup_stats() in between
+    didx = r.records("sidx")
+    idx, ent = po.shadow_lists(_oscene(po, "tekkaman"), second)
+    assert len(ent) != n_first
+    assert slist.shape == (len(ent) + 1, 12) and np.array_equal(didx, idx)
+    geom = r.records("geom")
+    got = slist[:-1].copy()
+    got[:, 7] = 0.0
+    assert np.array_equal(got.view(np.uint32), geom[ent].view(np.uint32))
+    r.close()
+    s.close()
+
+
 @pytest.mark.parametrize("lists", [1, 0])
 @pytest.mark.parametrize("light", [(0.0, 60.0, 80.0), (-200.0, 150.0, 50.0), (5.0, 5.0, 99.5)])
 def test_shadow_lists_frames_equal_oracle_with_counts(oracle_lib, lists, light):

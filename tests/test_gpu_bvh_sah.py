@@ -100,6 +100,38 @@ def test_frames_over_gpu_sah_equal_oracle(oracle_lib, mode):
     s.close()
 
 
+def test_gpu_sah_deep_tree_on_stale_scratch(tmp_path_factory):
+    """A tree deeper than the level budget built in arena memory another
+    build has just left dirty: synth20k's SAH scratch is freed, chain96's
+    build reuses those addresses, and its first sequence's finishing phases
+    must not run on the partial tree (they skip on the device while the
+    level after the budget still holds segments, bvh_sah.hip) -- the arrays
+    still equal the host builder's."""
+    big = rt.Scene.load(_scene("synth20k", tmp_path_factory))
+    rb = rt.Renderer(big)
+    rb.build_bvh("sah")
+    rb.build_bvh("sah")
+    rb.close()
+    big.close()
+    s = rt.Scene.load(_scene("chain96", tmp_path_factory))
+    info = s.info()
+    host = rt.Renderer(s)
+    hn, ht = host.export_bvh()
+    h4, hh = host.export_bvh4(), host.export_bvh4h()
+    r = rt.Renderer(s)
+    for _ in range(2):
+        st = r.build_bvh("sah")
+        dn, dt = r.export_bvh()
+        assert np.array_equal(dn.view(np.uint32), hn.view(np.uint32))
+        assert np.array_equal(dt.view(np.uint32), ht.view(np.uint32))
+        assert np.array_equal(r.export_bvh4().view(np.uint32), h4.view(np.uint32))
+        assert np.array_equal(r.export_bvh4h(), hh)
+        assert st["depth"] == info["bvh_depth"] and st["stack4"] == info["bvh4_stack"]
+    r.close()
+    host.close()
+    s.close()
+
+
 def test_gpu_sah_rebuild(tmp_path_factory):
     """A rebuild with the image and scratch resident: the same arrays every
     time, in well under a millisecond for tekkaman (one launch sequence, one
