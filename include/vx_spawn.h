@@ -57,6 +57,9 @@
 typedef struct {
   uint32_t mpm[VX_MAX_GRID][VX_MPM_ROW];
   uint32_t tasks;
+  uint32_t pad;
+  uint64_t t0;  /* s_memrealtime (100 MHz) when block 0 started: the launch's start
+                 * for the completion kernel (VX_MAIN's <entry>_done) */
 } vx_state_t;
 
 /* Filled by the driver before every launch (hip_driver.cpp, start()). */
@@ -157,11 +160,23 @@ struct vx_arena {
   }
 };
 
+/* threads per workgroup: a compile-time constant when the kernel program
+ * defines VX_BLOCK_THREADS (its VX_MAIN block size) -- blockDim.x is a
+ * vector-memory load from the dispatch packet, on every wave's way to its
+ * first chunk */
+__device__ __forceinline__ uint32_t __vx_block_dim() {
+#ifdef VX_BLOCK_THREADS
+  return VX_BLOCK_THREADS;
+#else
+  return blockDim.x;
+#endif
+}
+
 /* hardware identity (vx_intrinsics.h vx_core_id/vx_warp_id/vx_thread_id) */
 __device__ __forceinline__ uint32_t vx_core_id() { return blockIdx.x; }
 __device__ __forceinline__ uint32_t vx_num_cores() { return gridDim.x; }
 __device__ __forceinline__ uint32_t vx_warp_id() { return threadIdx.x >> 6; }
-__device__ __forceinline__ uint32_t vx_num_warps() { return blockDim.x >> 6; }
+__device__ __forceinline__ uint32_t vx_num_warps() { return __vx_block_dim() >> 6; }
 __device__ __forceinline__ uint32_t vx_thread_id() { return threadIdx.x & 63u; }
 __device__ __forceinline__ uint32_t vx_num_threads() { return 64u; }
 __device__ __forceinline__ uint32_t vx_xcc_id() {
@@ -243,18 +258,23 @@ __device__ __forceinline__ int vx_spawn_threads_ex(uint32_t dimension, const uin
   if (group_size != 1) return -1;
   __vx_declare_tasks(num_groups);
   const uint32_t nchunks = (num_groups + VX_CHUNK - 1) / VX_CHUNK;
-  const uint32_t nwaves = gridDim.x * (blockDim.x >> 6);
+  const uint32_t nwaves = gridDim.x * (__vx_block_dim() >> 6);
   uint32_t ran = 0;
   vx_task_t task;
   task.threadIdx.x = task.threadIdx.y = task.threadIdx.z = 0;
-  for (uint32_t c = __vx_logical_block() * (blockDim.x >> 6) + (threadIdx.x >> 6); c < nchunks;
+  for (uint32_t c = __vx_logical_block() * (__vx_block_dim() >> 6) + (threadIdx.x >> 6); c < nchunks;
        c += nwaves) {
     const uint32_t t = c * VX_CHUNK + (threadIdx.x & 63u);
     if (t < num_groups) {
       task.task_id = t;
-      task.blockIdx.x = t % gd[0];
-      task.blockIdx.y = (t / gd[0]) % gd[1];
-      task.blockIdx.z = t / (gd[0] * gd[1]);
+      if (dimension <= 1) {  // t < num_groups = gd[0]: no division (vx_spawn_tasks)
+        task.blockIdx.x = t;
+        task.blockIdx.y = task.blockIdx.z = 0;
+      } else {
+        task.blockIdx.x = t % gd[0];
+        task.blockIdx.y = (t / gd[0]) % gd[1];
+        task.blockIdx.z = t / (gd[0] * gd[1]);
+      }
       kernel_func(task, arg);
       ++ran;
     }
@@ -293,14 +313,14 @@ __device__ __forceinline__ int vx_spawn_tasks_ex(uint32_t num_tasks, F kernel_fu
 template <typename F, typename E, typename Arg>
 __device__ __forceinline__ int vx_spawn_tasks_block(uint32_t num_tasks, F kernel_func,
                                                     E block_epilogue, Arg* arg) {
-  const uint32_t nsteps = (num_tasks + blockDim.x - 1) / blockDim.x;
+  const uint32_t nsteps = (num_tasks + __vx_block_dim() - 1) / __vx_block_dim();
   __vx_declare_tasks(num_tasks);
   uint32_t ran = 0;
   vx_task_t task;
   task.threadIdx.x = task.threadIdx.y = task.threadIdx.z = 0;
   task.blockIdx.y = task.blockIdx.z = 0;
   for (uint32_t st = blockIdx.x; st < nsteps; st += gridDim.x) {
-    const uint32_t t = st * blockDim.x + threadIdx.x;
+    const uint32_t t = st * __vx_block_dim() + threadIdx.x;
     task.task_id = t;
     task.blockIdx.x = t;
     const bool valid = t < num_tasks;
@@ -354,9 +374,35 @@ __device__ __forceinline__ int vx_spawn_chunks_block(uint32_t num_tasks, F kerne
 #ifndef VX_ENTRY
 #define VX_ENTRY vx_main
 #endif
+#define __VX_CAT2(a, b) a##b
+#define __VX_CAT(a, b) __VX_CAT2(a, b)
+/* <entry>_done(host, nonce): the completion kernel the driver queues right
+ * behind a launch started on an idle queue (hip_driver.cpp start: the
+ * synchronous start + wait of the reference's apps).  One lane stores the
+ * launch's start stamp (block 0's, vx_state_t::t0) and its own (the launch
+ * has completed: stream order), then `nonce` with a system-scope release, to
+ * the driver's pinned host words; vx_ready_wait spins on that word -- no HIP
+ * event or stream query between the frame and the host. */
+#define __VX_DONE_KERNEL                                                             \
+  extern "C" __global__ void __launch_bounds__(64) __VX_CAT(VX_ENTRY, _done)(uint64_t __vx_host, \
+                                                                        uint32_t __vx_nonce) { \
+    if (threadIdx.x == 0) {                                                          \
+      const uint64_t t1 = __builtin_amdgcn_s_memrealtime();                          \
+      const uint64_t t0 = __vx_state.t0;                                             \
+      uint32_t* h = reinterpret_cast<uint32_t*>(__vx_host);                          \
+      __hip_atomic_store(h + 2, (uint32_t)t0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM); \
+      __hip_atomic_store(h + 3, (uint32_t)(t0 >> 32), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM); \
+      __hip_atomic_store(h + 4, (uint32_t)t1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM); \
+      __hip_atomic_store(h + 5, (uint32_t)(t1 >> 32), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM); \
+      __hip_atomic_store(h, __vx_nonce, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);  \
+    }                                                                                \
+  }
 #define VX_MAIN_BOUNDS(ArgT, argname, bounds)                                        \
+  __VX_DONE_KERNEL                                                                   \
   static __device__ __forceinline__ int __vx_main_body(ArgT* argname, uint32_t vx_launch_tag); \
   extern "C" __global__ void bounds VX_ENTRY(uint32_t __vx_tag) {                    \
+    /* the launch's start stamp (one lane of block 0; <entry>_done reads it) */      \
+    if (blockIdx.x == 0 && threadIdx.x == 0) __vx_state.t0 = __builtin_amdgcn_s_memrealtime(); \
     /* the block's counter row: only when the driver reads rows (then the   */    \
     /* block's waves meet at entry and exit; without, each wave runs and    */    \
     /* retires on its own)                                                  */    \

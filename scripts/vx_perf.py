@@ -68,7 +68,7 @@ def collect(outdir, passes, cmd, kernel, timeout):
         for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
             with open(f) as fh:
                 for row in csv.DictReader(fh):
-                    if not row["Kernel_Name"].startswith(kernel):
+                    if not row["Kernel_Name"].startswith(kernel) or row["Kernel_Name"].endswith("_done"):
                         continue
                     per[row["Counter_Name"]] += float(row["Counter_Value"])
                     n.add(row["Dispatch_Id"])

@@ -279,24 +279,32 @@ class Builder {
   bool all_axes_;
 };
 
-// Collapse the BVH2 into a BVH4: a node's children are repeatedly replaced
-// by the children of its largest-area internal child (in place, so the order
-// stays left to right) until it has 4 or none is internal.  Boxes are copied
-// verbatim from the BVH2 nodes that stored them.
+// Collapse the BVH2 into a BVH4 (W = 4) or BVH8 (W = 8): a node's children
+// are repeatedly replaced by the children of its largest-area internal child
+// (in place, so the order stays left to right) until it has W or none is
+// internal.  Boxes are copied verbatim from the BVH2 nodes that stored them.
+// Nodes are numbered in preorder.  W = 4 fills nodes4 (rt_node4_t); W = 8
+// fills nodes8 (two rt_node4_t halves per node, children 0-3 and 4-7).
+template <int W>
 class Collapser {
  public:
   explicit Collapser(Bvh* b) : b_(b) {}
   void run() {
-    b_->nodes4.clear();
-    b_->depth4 = 0;
-    b_->stack4 = 0;
-    if (b_->nodes.empty()) return;
+    out().clear();
+    depth() = 0;
+    if (b_->nodes.empty()) {
+      stack() = 0;
+      return;
+    }
     uint32_t st = 0;
     collapse(0, 1, &st);
-    b_->stack4 = st;
+    stack() = st;
   }
 
  private:
+  std::vector<rt_node4_t>& out() { return W == 4 ? b_->nodes4 : b_->nodes8; }
+  uint32_t& depth() { return W == 4 ? b_->depth4 : b_->depth8; }
+  uint32_t& stack() { return W == 4 ? b_->stack4 : b_->stack8; }
   struct Child {
     float lo[3], hi[3];
     int32_t ref;
@@ -319,13 +327,13 @@ class Collapser {
   // returns the BVH4 index of BVH2 node n; *stack = worst-case stack
   // entries needed below (and including) this node
   uint32_t collapse(uint32_t n, uint32_t depth, uint32_t* stack) {
-    b_->depth4 = std::max(b_->depth4, depth);
+    this->depth() = std::max(this->depth(), depth);
     std::vector<Child> cs;
     for (int ch = 0; ch < 2; ++ch) {
       const Child c = child_of(n, ch);
       if (c.ref != RT_EMPTY_REF) cs.push_back(c);
     }
-    while (cs.size() < 4) {
+    while (cs.size() < (size_t)W) {
       int best = -1;
       double ba = -1.0;
       for (size_t i = 0; i < cs.size(); ++i)
@@ -340,8 +348,9 @@ class Collapser {
       cs.erase(cs.begin() + best);
       cs.insert(cs.begin() + best, sub.begin(), sub.end());
     }
-    const uint32_t idx = (uint32_t)b_->nodes4.size();
-    b_->nodes4.emplace_back();
+    constexpr int H = W / 4;  // rt_node4_t halves per node
+    const uint32_t idx = (uint32_t)(out().size() / H);
+    out().resize(out().size() + H);
     uint32_t below = 0;
     for (size_t i = 0; i < cs.size(); ++i)
       if (cs[i].ref >= 0) {
@@ -349,16 +358,19 @@ class Collapser {
         cs[i].ref = (int32_t)collapse((uint32_t)cs[i].ref, depth + 1, &st);
         below = std::max(below, st);
       }
-    rt_node4_t& o = b_->nodes4[idx];
-    std::memset(&o, 0, sizeof(o));
-    for (int i = 0; i < 4; ++i) {
-      const bool used = i < (int)cs.size();
-      for (int k = 0; k < 3; ++k) {
-        o.v[8 * k + i] = used ? cs[i].lo[k] : 0.0f;
-        o.v[8 * k + 4 + i] = used ? cs[i].hi[k] : 0.0f;
+    for (int h = 0; h < H; ++h) {
+      rt_node4_t& o = out()[(size_t)idx * H + h];
+      std::memset(&o, 0, sizeof(o));
+      for (int j = 0; j < 4; ++j) {
+        const int i = 4 * h + j;
+        const bool used = i < (int)cs.size();
+        for (int k = 0; k < 3; ++k) {
+          o.v[8 * k + j] = used ? cs[i].lo[k] : 0.0f;
+          o.v[8 * k + 4 + j] = used ? cs[i].hi[k] : 0.0f;
+        }
+        const int32_t ref = used ? cs[i].ref : RT_EMPTY_REF;
+        std::memcpy(&o.v[24 + j], &ref, 4);
       }
-      const int32_t ref = used ? cs[i].ref : RT_EMPTY_REF;
-      std::memcpy(&o.v[24 + i], &ref, 4);
     }
     // descending into one child pushes at most the other (cs.size() - 1)
     *stack = (uint32_t)(cs.empty() ? 0 : cs.size() - 1) + below;
@@ -398,7 +410,8 @@ int BuildBvhWith(const std::vector<BuildTri>& tris, const BvhParams& bp, Bvh* ou
   }
   Builder b(tris, out, bp);
   b.run();
-  Collapser(out).run();
+  Collapser<4>(out).run();
+  Collapser<8>(out).run();
   // binary16 box planes: round every BVH4 box outward (RT_BVH_F16=0 keeps
   // the fp32 planes, rt_node4h_t is then not uploaded), pack rt_node4h_t and
   // check that it decodes to exactly rt_node4_t's planes
@@ -423,6 +436,25 @@ int BuildBvhWith(const std::vector<BuildTri>& tris, const BvhParams& bp, Bvh* ou
         }
       std::memcpy(h.child, &o.v[24], 16);
     }
+    // the BVH8's halves the same way (from the same fp32 BVH2 boxes)
+    out->nodes8h.resize(out->nodes8.size() / 2);
+    for (size_t n = 0; n < out->nodes8.size(); ++n) {
+      rt_node4_t& o = out->nodes8[n];
+      rt_node4h_t& h = out->nodes8h[n / 2].half[n % 2];
+      for (int q = 0; q < 24; ++q) {
+        float& v = o.v[q];
+        v = HalfRound(v, (q & 4) ? +1 : -1);
+        h.b[q] = HalfBits(v);
+        if (HalfValue(h.b[q]) != v) {
+          if (error) *error = "binary16 box packing mismatch (BVH8)";
+          return -1;
+        }
+      }
+      std::memcpy(h.child, &o.v[24], 16);
+    }
+  } else {
+    out->nodes8.clear();  // the BVH8 exists in binary16 form only
+    out->depth8 = out->stack8 = 0;
   }
   if (out->depth > RT_STACK_DEEP) {
     if (error) *error = "BVH deeper than RT_STACK_DEEP";

@@ -719,18 +719,21 @@ __device__ __forceinline__ double child_area(const Child& c) {
   return 2.0 * (dx * dy + dy * dz + dz * dx);
 }
 
+// the expansion of every BVH2 node for a W-wide collapse (W = 4: cs, W = 8:
+// cs8): W refs, then W sources (node << 1 | slot)
+template <int W>
 __device__ void phase_cs(const sah_arg_t* a) {
   const float* nodes = vx_ptr<const float>(a->nodes_addr);
-  int32_t* cs = vx_ptr<int32_t>(a->cs_addr);
+  int32_t* cs = vx_ptr<int32_t>(W == 4 ? a->cs_addr : a->cs8_addr);
   const uint32_t nn = vx_ptr<const uint32_t>(a->ctl_addr)[SAH_CTL_NODES];
   for (uint32_t p = blockIdx.x * SAH_BLOCK + threadIdx.x; p < nn; p += gridDim.x * SAH_BLOCK) {
-    Child c[4];
+    Child c[W];
     int m = 0;
     for (int ch = 0; ch < 2; ++ch) {
       const Child x = child_of(nodes, p, ch);
       if (x.ref != RT_EMPTY_REF) c[m++] = x;
     }
-    while (m < 4) {
+    while (m < W) {
       int best = -1;
       double ba = -1.0;
       for (int i = 0; i < m; ++i)
@@ -746,8 +749,8 @@ __device__ void phase_cs(const sah_arg_t* a) {
         const Child x = child_of(nodes, q, ch);
         if (x.ref != RT_EMPTY_REF) sub[ns++] = x;
       }
-      // erase c[best], insert sub there (m - 1 + ns <= 4)
-      Child t[4];
+      // erase c[best], insert sub there (m - 1 + ns <= W)
+      Child t[W];
       int k = 0;
       for (int i = 0; i < best; ++i) t[k++] = c[i];
       for (int i = 0; i < ns; ++i) t[k++] = sub[i];
@@ -755,10 +758,10 @@ __device__ void phase_cs(const sah_arg_t* a) {
       for (int i = 0; i < k; ++i) c[i] = t[i];
       m = k;
     }
-    int32_t* o = cs + 8ull * p;
-    for (int i = 0; i < 4; ++i) {
+    int32_t* o = cs + 2ull * W * p;
+    for (int i = 0; i < W; ++i) {
       o[i] = i < m ? c[i].ref : RT_EMPTY_REF;
-      o[4 + i] = i < m ? c[i].src : -1;
+      o[W + i] = i < m ? c[i].src : -1;
     }
   }
 }
@@ -771,11 +774,13 @@ __device__ void phase_cs(const sah_arg_t* a) {
 // right after it, so the way up records whether each step came from that
 // child (bit 0) or from the other one (bit 1, its id read from the parent's
 // record on the way down).
+// (W = 8: the BVH8's membership, depth and stack the same way, is8 / cs8)
+template <int W>
 __device__ void phase_mark(const sah_arg_t* a) {
   const int32_t* parent = vx_ptr<const int32_t>(a->parent_addr);
-  const int32_t* cs = vx_ptr<const int32_t>(a->cs_addr);
+  const int32_t* cs = vx_ptr<const int32_t>(W == 4 ? a->cs_addr : a->cs8_addr);
   const int32_t* nodes = vx_ptr<const int32_t>(a->nodes_addr);  // rt_node_t: refs at words 12, 13
-  uint32_t* is4 = vx_ptr<uint32_t>(a->is4_addr);
+  uint32_t* is4 = vx_ptr<uint32_t>(W == 4 ? a->is4_addr : a->is8_addr);
   uint32_t* ctl = vx_ptr<uint32_t>(a->ctl_addr);
   const uint32_t nn = ctl[SAH_CTL_NODES];
   // the BVH4 depth and stack maxima: per lane over its nodes, then one
@@ -796,21 +801,43 @@ __device__ void phase_mark(const sah_arg_t* a) {
       is4[m] = 0;
       continue;
     }
-    // a BVH4 node's children: the expansion's refs (one 16-B load); their
-    // count = the refs before the first empty one
+    // a BVH4 (BVH8) node's children: the expansion's refs (one (two) 16-B
+    // loads); their count = the refs before the first empty one
     const int4* cs4 = reinterpret_cast<const int4*>(cs);
-    auto nch = [](const int4& r) {
+    auto nch4 = [](const int4& r) {
       return r.x == RT_EMPTY_REF ? 0u : r.y == RT_EMPTY_REF ? 1u : r.z == RT_EMPTY_REF ? 2u : r.w == RT_EMPTY_REF ? 3u : 4u;
     };
-    int4 cc = cs4[0];  // the root's expansion
+    constexpr int Q = W / 4;  // int4 words of refs per expansion
+    struct Refs {
+      int4 r[Q];
+    };
+    auto load = [&](int32_t node) {
+      Refs x;
+      for (int q = 0; q < Q; ++q) x.r[q] = cs4[(2 * W / 4) * node + q];
+      return x;
+    };
+    auto nch = [&](const Refs& x) {
+      uint32_t n = 0;
+      for (int q = 0; q < Q; ++q) {
+        const uint32_t k = nch4(x.r[q]);
+        n += (n == 4u * q) ? k : 0u;  // counts stop at the first empty ref
+      }
+      return n;
+    };
+    auto has = [&](const Refs& x, int32_t c) {
+      bool in = false;
+      for (int q = 0; q < Q; ++q) in = in || x.r[q].x == c || x.r[q].y == c || x.r[q].z == c || x.r[q].w == c;
+      return in;
+    };
+    Refs cc = load(0);  // the root's expansion
     int32_t p = 0;
     uint32_t depth4 = 1, stack = nch(cc) > 0 ? nch(cc) - 1 : 0;
     bool member = len == 0;
     for (int k = len - 1; k >= 0; --k) {
       const int32_t c = ((bits >> k) & 1ull) ? nodes[16 * p + 13] : p + 1;
-      const bool in = cc.x == c || cc.y == c || cc.z == c || cc.w == c;
+      const bool in = has(cc, c);
       if (in) {
-        cc = cs4[2 * c];
+        cc = load(c);
         ++depth4;
         const uint32_t n4 = nch(cc);
         stack += n4 > 0 ? n4 - 1 : 0;
@@ -830,8 +857,8 @@ __device__ void phase_mark(const sah_arg_t* a) {
     smax = max(smax, (uint32_t)__shfl_xor((int)smax, o, 64));
   }
   if (lane_id() == 0 && dmax != 0) {
-    atomicMax(&ctl[SAH_CTL_DEPTH4], dmax);
-    atomicMax(&ctl[SAH_CTL_STACK4], smax);
+    atomicMax(&ctl[W == 4 ? SAH_CTL_DEPTH4 : SAH_CTL_DEPTH8], dmax);
+    atomicMax(&ctl[W == 4 ? SAH_CTL_STACK4 : SAH_CTL_STACK8], smax);
   }
 }
 
@@ -872,6 +899,41 @@ __device__ void phase_emit4(const sah_arg_t* a) {
   }
 }
 
+// rt_node8h_t at BVH8 preorder indices: each half (children 0-3, 4-7) as
+// an rt_node4_t in registers, its planes rounded outward to binary16 and
+// packed as one rt_node4h_t (half4_node, the BVH4's rounding)
+__device__ void phase_emit8(const sah_arg_t* a) {
+  const float* nodes = vx_ptr<const float>(a->nodes_addr);
+  const int32_t* cs = vx_ptr<const int32_t>(a->cs8_addr);
+  const uint32_t* pre8 = vx_ptr<const uint32_t>(a->is8_addr);
+  uint32_t* out = vx_ptr<uint32_t>(a->nodes8_addr);
+  uint32_t* ctl = vx_ptr<uint32_t>(a->ctl_addr);
+  const uint32_t nn = ctl[SAH_CTL_NODES];
+  if (blockIdx.x == 0 && threadIdx.x == 0) ctl[SAH_CTL_NODES8] = pre8[nn];
+  for (uint32_t m = blockIdx.x * SAH_BLOCK + threadIdx.x; m < nn; m += gridDim.x * SAH_BLOCK) {
+    if (pre8[m + 1] == pre8[m]) continue;  // not a BVH8 node
+    for (int h = 0; h < 2; ++h) {
+      float v[32];
+      for (int i = 0; i < 32; ++i) v[i] = 0.0f;
+      for (int j = 0; j < 4; ++j) {
+        int32_t ref = cs[16 * m + 4 * h + j];
+        const int32_t src = cs[16 * m + 8 + 4 * h + j];
+        if (ref != RT_EMPTY_REF) {
+          const float* sn = nodes + 16ull * (uint32_t)(src >> 1);
+          const int ch = src & 1;
+          for (int k = 0; k < 3; ++k) {
+            v[8 * k + j] = sn[4 * k + 2 * ch];
+            v[8 * k + 4 + j] = sn[4 * k + 2 * ch + 1];
+          }
+          if (ref >= 0) ref = (int32_t)pre8[ref];
+        }
+        v[24 + j] = __int_as_float(ref);
+      }
+      half4_node(v, out + 32ull * pre8[m] + 16 * h);
+    }
+  }
+}
+
 // the numbering's counters as SAH_INIT leaves them, and the collapse's
 // maxima (a sequence that ran its finishing phases before its last level)
 __device__ void phase_reset(const sah_arg_t* a) {
@@ -885,6 +947,8 @@ __device__ void phase_reset(const sah_arg_t* a) {
     uint32_t* ctl = vx_ptr<uint32_t>(a->ctl_addr);
     ctl[SAH_CTL_DEPTH4] = 0;
     ctl[SAH_CTL_STACK4] = 0;
+    ctl[SAH_CTL_DEPTH8] = 0;
+    ctl[SAH_CTL_STACK8] = 0;
     ctl[SAH_CTL_ERR] &= ~2u;
   }
 }
@@ -916,13 +980,19 @@ VX_MAIN(sah_arg_t, arg, SAH_BLOCK) {
     case SAH_NUMBER: phase_number(arg); break;
     case SAH_SCAN: phase_scan(vx_ptr<uint32_t>(arg->cnt_addr), arg->n); break;
     case SAH_EMIT: phase_emit(arg); break;
-    case SAH_CS: phase_cs(arg); break;
-    case SAH_MARK: phase_mark(arg); break;
+    case SAH_CS: phase_cs<4>(arg); break;
+    case SAH_MARK: phase_mark<4>(arg); break;
     case SAH_EMIT4: phase_emit4(arg); break;
     case SAH_RESET: phase_reset(arg); break;
     case SAH_SCAN4:
       phase_scan(vx_ptr<uint32_t>(arg->is4_addr), vx_ptr<const uint32_t>(arg->ctl_addr)[SAH_CTL_NODES]);
       break;
+    case SAH_CS8: phase_cs<8>(arg); break;
+    case SAH_MARK8: phase_mark<8>(arg); break;
+    case SAH_SCAN8:
+      phase_scan(vx_ptr<uint32_t>(arg->is8_addr), vx_ptr<const uint32_t>(arg->ctl_addr)[SAH_CTL_NODES]);
+      break;
+    case SAH_EMIT8: phase_emit8(arg); break;
     default: break;
   }
   return 0;

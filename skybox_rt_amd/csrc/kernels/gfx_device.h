@@ -65,29 +65,26 @@ __device__ __forceinline__ void load_prim(const vx_arena& A, uint32_t off, Prim&
 
 // TFixed<F> <- float on the device: RISC-V fcvt.w.s (rtz, saturating,
 // NaN -> INT_MAX) semantics, as the reference's shader runs on RISC-V cores.
+// Branch-free (no exec-mask branches per call): the value clamped into
+// [-2^31, 2^31 - 128] (the largest float below 2^31) converts exactly as the
+// in-range branch did; out-of-range and NaN inputs are then selected.
 __device__ __forceinline__ int32_t fx_from_float_dev(float f, int frac) {
   const float x = f * (float)(1u << frac);
-  if (x != x) return INT32_MAX;
-  if (x >= 2147483648.0f) return INT32_MAX;
-  if (x < -2147483648.0f) return INT32_MIN;
-  return (int32_t)x;
+  const int32_t r = (int32_t)fminf(fmaxf(x, -2147483648.0f), 2147483520.0f);  // NaN -> -2^31
+  return (x >= 2147483648.0f || x != x) ? INT32_MAX : r;
 }
 __device__ __forceinline__ float fx_to_float(int32_t d, int frac) {
   return (float)d * (1.0f / (float)(1u << frac));
 }
 
-// TextureWrap (graphics.cpp:35-53) for TFixed<23>
+// TextureWrap (graphics.cpp:35-53) for TFixed<23>; the three modes
+// computed and selected (a wave-uniform mode: no branch per call)
 __device__ __forceinline__ int32_t tex_wrap(int32_t d, uint32_t wrap) {
   const int32_t MASK = (1 << VX_TEX_FXD_FRAC) - 1;
-  int32_t ret;
-  if (wrap == VX_TEX_WRAP_REPEAT) {
-    ret = d;
-  } else if (wrap == VX_TEX_WRAP_MIRROR) {
-    ret = d ^ ((int32_t)((uint32_t)d << (31 - VX_TEX_FXD_FRAC)) >> 31);
-  } else {
-    ret = d & -(int32_t)(d >= 0);
-    ret |= ((MASK - ret) >> 31);
-  }
+  const int32_t mir = d ^ ((int32_t)((uint32_t)d << (31 - VX_TEX_FXD_FRAC)) >> 31);
+  int32_t clp = d & -(int32_t)(d >= 0);
+  clp |= ((MASK - clp) >> 31);
+  const int32_t ret = wrap == VX_TEX_WRAP_REPEAT ? d : (wrap == VX_TEX_WRAP_MIRROR ? mir : clp);
   return ret & MASK;
 }
 
@@ -143,9 +140,73 @@ __device__ __forceinline__ uint32_t fetch_texel(const vx_arena& A, uint32_t base
   return A.ld_u8(base + idx);
 }
 
-// TextureSampler::read, lod 0 (graphics.cpp:253-314)
+// TextureSampler::read, lod 0 (graphics.cpp:253-314), for one texel format
+// known at compile time: its stride (setup.cpp FormatStride) and unpack
+// (unpack8888's case) are straight-line code, so a shade makes one format
+// switch (tex_read) instead of one per texel fetch and unpack
+template <uint32_t FMT>
+__device__ __forceinline__ uint32_t fmt_fetch(const vx_arena& A, uint32_t base, uint32_t idx) {
+  if constexpr (FMT == VX_TEX_FORMAT_A8R8G8B8) return A.ld_u32(base + 4 * idx);
+  else if constexpr (FMT == VX_TEX_FORMAT_L8 || FMT == VX_TEX_FORMAT_A8) return A.ld_u8(base + idx);
+  else return A.ld_u16(base + 2 * idx);
+}
+template <uint32_t FMT>
+__device__ __forceinline__ uint32_t tex_read_fmt(const vx_arena& A, const DcState& s, int32_t u, int32_t v) {
+  const uint32_t logw = s.logw, logh = s.logh;
+  if (s.filter == VX_TEX_FILTER_BILINEAR) {
+    const int32_t half = (1 << VX_TEX_FXD_FRAC) >> 1;
+    const int32_t dxh = half >> logw, dyh = half >> logh;
+    const uint32_t u0 = (uint32_t)tex_wrap((int32_t)((uint32_t)u - (uint32_t)dxh), s.wrapu);
+    const uint32_t u1 = (uint32_t)tex_wrap((int32_t)((uint32_t)u + (uint32_t)dxh), s.wrapu);
+    const uint32_t v0 = (uint32_t)tex_wrap((int32_t)((uint32_t)v - (uint32_t)dyh), s.wrapv);
+    const uint32_t v1 = (uint32_t)tex_wrap((int32_t)((uint32_t)v + (uint32_t)dyh), s.wrapv);
+    const uint32_t shu = VX_TEX_FXD_FRAC - logw, shv = VX_TEX_FXD_FRAC - logh;
+    const uint32_t x0s = (u0 << 8) >> shu, y0s = (v0 << 8) >> shv;
+    const uint32_t x0 = x0s >> 8, y0 = y0s >> 8, x1 = u1 >> shu, y1 = v1 >> shv;
+    const uint32_t t00 = fmt_fetch<FMT>(A, s.tex_off, x0 + (y0 << logw));
+    const uint32_t t01 = fmt_fetch<FMT>(A, s.tex_off, x1 + (y0 << logw));
+    const uint32_t t10 = fmt_fetch<FMT>(A, s.tex_off, x0 + (y1 << logw));
+    const uint32_t t11 = fmt_fetch<FMT>(A, s.tex_off, x1 + (y1 << logw));
+    const uint32_t alpha = x0s & 0xff, beta = y0s & 0xff;
+    uint32_t c0l, c0h, c1l, c1h, c2l, c2h, c3l, c3h;
+    unpack8888(FMT, t00, &c0l, &c0h);
+    unpack8888(FMT, t01, &c1l, &c1h);
+    const uint32_t c01l = lerp8888(c0l, c1l, alpha), c01h = lerp8888(c0h, c1h, alpha);
+    unpack8888(FMT, t10, &c2l, &c2h);
+    unpack8888(FMT, t11, &c3l, &c3h);
+    const uint32_t c23l = lerp8888(c2l, c3l, alpha), c23h = lerp8888(c2h, c3h, alpha);
+    const uint32_t cl = lerp8888(c01l, c23l, beta), ch = lerp8888(c01h, c23h, beta);
+    return (ch << 8) | cl;
+  }
+  const uint32_t uu = (uint32_t)tex_wrap(u, s.wrapu), vv = (uint32_t)tex_wrap(v, s.wrapv);
+  const uint32_t x = uu >> (VX_TEX_FXD_FRAC - logw), y = vv >> (VX_TEX_FXD_FRAC - logh);
+  uint32_t cl, ch;
+  unpack8888(FMT, fmt_fetch<FMT>(A, s.tex_off, x + (y << logw)), &cl, &ch);
+  return (ch << 8) | cl;
+}
+// any format: the record's own stride and the generic unpack (formats past
+// the seven named ones)
+__device__ __forceinline__ uint32_t tex_read_any(const vx_arena& A, const DcState& s, int32_t u,
+                                                 int32_t v);
 __device__ __forceinline__ uint32_t tex_read(const vx_arena& A, const DcState& s, int32_t u,
                                              int32_t v) {
+  if (s.stride == 4 - 2 * (s.format != VX_TEX_FORMAT_A8R8G8B8) -
+                     (s.format == VX_TEX_FORMAT_L8 || s.format == VX_TEX_FORMAT_A8)) {
+    switch (s.format) {
+    case VX_TEX_FORMAT_A8R8G8B8: return tex_read_fmt<VX_TEX_FORMAT_A8R8G8B8>(A, s, u, v);
+    case VX_TEX_FORMAT_R5G6B5: return tex_read_fmt<VX_TEX_FORMAT_R5G6B5>(A, s, u, v);
+    case VX_TEX_FORMAT_A1R5G5B5: return tex_read_fmt<VX_TEX_FORMAT_A1R5G5B5>(A, s, u, v);
+    case VX_TEX_FORMAT_A4R4G4B4: return tex_read_fmt<VX_TEX_FORMAT_A4R4G4B4>(A, s, u, v);
+    case VX_TEX_FORMAT_A8L8: return tex_read_fmt<VX_TEX_FORMAT_A8L8>(A, s, u, v);
+    case VX_TEX_FORMAT_L8: return tex_read_fmt<VX_TEX_FORMAT_L8>(A, s, u, v);
+    case VX_TEX_FORMAT_A8: return tex_read_fmt<VX_TEX_FORMAT_A8>(A, s, u, v);
+    default: break;
+    }
+  }
+  return tex_read_any(A, s, u, v);
+}
+__device__ __forceinline__ uint32_t tex_read_any(const vx_arena& A, const DcState& s, int32_t u,
+                                                 int32_t v) {
   const uint32_t logw = s.logw, logh = s.logh, fmt = s.format, stride = s.stride;
   if (s.filter == VX_TEX_FILTER_BILINEAR) {
     const int32_t half = (1 << VX_TEX_FXD_FRAC) >> 1;

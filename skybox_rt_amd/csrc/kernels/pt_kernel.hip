@@ -22,6 +22,15 @@
 // queue at ballot + mbcnt slots (wave64 compaction).
 #include <hip/hip_runtime.h>
 
+#ifndef PT_MODE
+#define PT_MODE 1
+#endif
+#if PT_MODE == 0
+#define PT_BLOCK 256
+#else
+#define PT_BLOCK 64
+#endif
+#define VX_BLOCK_THREADS PT_BLOCK  // vx_spawn.h: the workgroup size as a constant
 #include "rt_trace.h"
 
 // PT_MODE 1 (default image pt_kernel): every lane runs its own path to the
@@ -37,14 +46,6 @@
 // PT_MODE 2 (image pt_queue, with pt_primary): the second kernel of a
 // two-kernel frame -- the compacted path queue the first kernel filled, one
 // path per lane on full waves (rt_trace.h pathq_append).
-#ifndef PT_MODE
-#define PT_MODE 1
-#endif
-#if PT_MODE == 0
-#define PT_BLOCK 256
-#else
-#define PT_BLOCK 64
-#endif
 #ifndef PT_COOP
 #define PT_COOP 1        // 32-pixel waves with the shadow lists: lane pairs per path
 #endif
@@ -334,7 +335,8 @@ __device__ __forceinline__ bool path_step(const Scene& S, int32_t* stack, PathSt
     ray_setup(b);
     cnt.bounce += one;
     np = CO == 2 ? trace_quad(S, b, st.pid, tie_high, &nt, stack, role, cnt)
-         : CO == 1 ? trace_coop(S, b, st.pid, tie_high, &nt, stack, hi, cnt)
+         : CO == 1 ? (RT_BVH8 ? trace_coop8(S, b, st.pid, tie_high, &nt, stack, hi, cnt)
+                              : trace_coop(S, b, st.pid, tie_high, &nt, stack, hi, cnt))
                    : trace<false>(S, b, 0.0f, INFINITY, st.pid, tie_high, &nt, stack, cnt);
     if (np < 0) {
 #pragma unroll
@@ -721,7 +723,7 @@ VX_MAIN(rt_kernel_arg_t, arg, PT_BLOCK) {
   if (threadIdx.x == 0) { s_pt.n[0] = 0; s_pt.n[1] = 0; }
   __syncthreads();
   const int rc = vx_spawn_tasks_block(
-      arg->num_tasks,
+      S.num_tasks,
       [&](const vx_task_t& task, bool valid, const Scene* s) { primary(task, valid, *s, s_pt, cnt); },
       [&](uint32_t, const Scene* s) { bounces(*s, s_pt, cnt); }, &S);
 #elif PT_MODE == 2
@@ -744,8 +746,8 @@ VX_MAIN(rt_kernel_arg_t, arg, PT_BLOCK) {
   // counts the group, and the one completing the last group zeroes every
   // counter for the next frame -- by then every wave has read them.  Nobody
   // waits.
-  const uint32_t nwaves = gridDim.x * (blockDim.x >> 6);
-  const uint32_t wid = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+  const uint32_t nwaves = gridDim.x * (PT_BLOCK >> 6);
+  const uint32_t wid = blockIdx.x * (PT_BLOCK >> 6) + (threadIdx.x >> 6);
   const uint32_t grp = wid % RT_PQ_SEGS;
   const uint32_t in_grp = nwaves / RT_PQ_SEGS + (grp < nwaves % RT_PQ_SEGS ? 1u : 0u);
   const uint32_t ngrp = nwaves < RT_PQ_SEGS ? nwaves : RT_PQ_SEGS;
@@ -765,7 +767,7 @@ VX_MAIN(rt_kernel_arg_t, arg, PT_BLOCK) {
 #else
   int32_t* stack = &s_pt.stack[threadIdx.x >> 6][0][lane_id()];
   const int rc = vx_spawn_tasks(
-      arg->num_tasks,
+      S.num_tasks,
       [&](const vx_task_t& task, const Scene* s) { lane_path(task, *s, stack, cnt); }, &S);
 #endif
 #ifndef RT_STAMPS  // the stamp image keeps slots 4-6 for its cycle accumulators

@@ -34,6 +34,7 @@
 #ifndef RT_BLOCK_THREADS
 #define RT_BLOCK_THREADS 64
 #endif
+#define VX_BLOCK_THREADS RT_BLOCK_THREADS  // vx_spawn.h: the workgroup size as a constant
 // RT_XCD: a 32x32 tile's 16 one-chunk waves on one XCD (vx_spawn.h
 // VX_XCD_GROUP: blocks per tile)
 #if defined(RT_XCD) && RT_XCD && !defined(VX_XCD_GROUP)
@@ -68,7 +69,8 @@ struct WaveLds {
 #define RT_WSTACK(w, lane) ((int32_t*)nullptr)
 #endif
 #if !RT_FLAT
-  uint32_t q_task[RT_QUEUE];
+  uint32_t q_out[RT_QUEUE];  // framebuffer word (chunk_pixel)
+  uint32_t q_xy[RT_QUEUE];   // pixel x | y << 16
   float q_t[RT_QUEUE];
   int32_t q_pid[RT_QUEUE];
   uint32_t q_color[RT_QUEUE];
@@ -105,8 +107,11 @@ __device__ __forceinline__ const uint4* flat_list(const Scene& S) {
 __device__ __forceinline__ void kernel_body(const vx_task_t& task, const Scene& S, WaveLds& w,
                                             Counters& cnt) {
   const uint32_t t = task.blockIdx.x;
-  uint32_t x, y, lb;
-  task_pixel(S, t, &x, &y, &lb);
+  // the chunk's task map in scalar registers (every lane runs the same chunk)
+  const ChunkMap cm = chunk_map(S, task_args(S), (uint32_t)__builtin_amdgcn_readfirstlane(t) >> 6);
+  uint32_t x, y, out;
+  chunk_pixel(S, cm, t & 63u, &x, &y, &out);
+  const uint32_t lb = (cm.lt << 4) | cm.blk;
   const bool in = x < S.width && y < S.height;  // edge tiles overhang the image
   cnt.primary += in;
   const bool tie_high = (S.flags & RT_FLAG_TIE_HIGH) != 0;
@@ -137,7 +142,7 @@ __device__ __forceinline__ void kernel_body(const vx_task_t& task, const Scene& 
   // pixel is written by pt_queue when the path ends
   const bool path = hit >= 0 && secondary_ok(th);
   pathq_append(S, path, t, th, hit, color);
-  if (in && !path) store_pixel(S, t, x, y, color);
+  if (in && !path) store_out(S, out, color);
   (void)w;
   return;
 #endif
@@ -151,7 +156,8 @@ __device__ __forceinline__ void kernel_body(const vx_task_t& task, const Scene& 
       const uint32_t rank = __builtin_amdgcn_mbcnt_hi(
           (uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
       const uint32_t slot = base + rank;
-      w.q_task[slot] = t;
+      w.q_out[slot] = out;
+      w.q_xy[slot] = x | (y << 16);
       w.q_t[slot] = th;
       w.q_pid[slot] = hit;
       w.q_color[slot] = color;
@@ -160,7 +166,7 @@ __device__ __forceinline__ void kernel_body(const vx_task_t& task, const Scene& 
     if (lane_id() == 0) w.q_count = base + (uint32_t)__popcll(m);
     __builtin_amdgcn_wave_barrier();
   }
-  if (in && !shadow) store_pixel(S, t, x, y, color);
+  if (in && !shadow) store_out(S, out, color);
 #ifdef RT_STAMPS
   if (lane_id() == 0) __vx_mpm_lds[5] = (uint32_t)__builtin_amdgcn_s_memrealtime();
 #endif
@@ -186,11 +192,9 @@ __device__ __forceinline__ void shadow_drain(bool final, const Scene& S, WaveLds
     const uint32_t base = n - take;
     const bool active = lane < take;
     const uint32_t slot = base + lane;  // < RT_QUEUE for every lane
-    const uint32_t t = w.q_task[slot];
-    uint32_t x, y;
-    task_pixel(S, t, &x, &y);
+    const uint32_t xy = w.q_xy[slot];
     Ray p, s;
-    primary_dir(S, x, y, p);
+    primary_dir(S, xy & 0xffffu, xy >> 16, p);
     shadow_ray(S, p, w.q_t[slot], s);
     cnt.shadow += active;
     uint32_t color = w.q_color[slot];
@@ -198,6 +202,7 @@ __device__ __forceinline__ void shadow_drain(bool final, const Scene& S, WaveLds
     // the light-space lists when built (occluded_list), else the BVH: the
     // binary16 BVH4 as one packet, other layouts per lane (deep images)
     const bool occ = !RT_BVH_WALK && S.slist_on ? occluded_list(S, s, active, w.q_pid[slot], cnt)
+                     : (RT_BVH8 && S.num_nodes8 > 0) ? occluded_packet8(S, s, active, w.q_pid[slot], 1.0f, cnt)
                      : (RT_ONLY_BVH4H || (S.flags & RT_FLAG_BVH4H))
                          ? occluded_packet(S, s, active, w.q_pid[slot], 1.0f, cnt)
                          : active && trace<true>(S, s, 0.0f, 1.0f, w.q_pid[slot], tie_high, &ts,
@@ -206,7 +211,7 @@ __device__ __forceinline__ void shadow_drain(bool final, const Scene& S, WaveLds
       ++cnt.occluded;
       color = shadowed(color);
     }
-    if (active) store_pixel(S, t, x, y, color);
+    if (active) store_out(S, w.q_out[slot], color);
     n = base;
   }
   __builtin_amdgcn_wave_barrier();
@@ -254,8 +259,12 @@ __device__ __forceinline__ void flat_chunk(const vx_task_t& task, bool valid, co
                                            FlatLds& L, Counters& cnt) {
   const uint32_t w = threadIdx.x >> 6, lane = lane_id();
   const uint32_t t = task.blockIdx.x;
-  uint32_t x = 0, y = 0;
-  if (valid) task_pixel(S, t, &x, &y);
+  uint32_t x = 0, y = 0, out = 0;
+  if (valid) {
+    // the chunk's task map in scalar registers (block-uniform chunk)
+    const ChunkMap cm = chunk_map(S, task_args(S), (uint32_t)__builtin_amdgcn_readfirstlane(t) >> 6);
+    chunk_pixel(S, cm, t & 63u, &x, &y, &out);
+  }
   const bool in = valid && x < S.width && y < S.height;
   const uint32_t px = in ? x : 0xffffffffu;  // outside every pixel rectangle
   const uint32_t pp = in ? x | (y << 16) : 0xffffffffu;  // packed pixel (rect_corners)
@@ -425,7 +434,7 @@ __device__ __forceinline__ void flat_chunk(const vx_task_t& task, bool valid, co
         color = shadowed(color);
       }
     }
-    if (in) store_pixel(S, t, x, y, color);
+    if (in) store_out(S, out, color);
   }
 }
 #endif
@@ -475,8 +484,8 @@ VX_MAIN(rt_kernel_arg_t, arg, RT_BLOCK_THREADS) {
 #if RT_FLAT
   // stage the geometry list once per workgroup (workgroups past the last
   // task chunk have nothing to render and skip it)
-  if (!RT_FLAT_SCALAR && S.num_geom <= RT_FLAT_CAP && blockIdx.x * VX_CHUNK < arg->num_tasks) {
-    for (uint32_t i = threadIdx.x; i < S.num_geom; i += blockDim.x)
+  if (!RT_FLAT_SCALAR && S.num_geom <= RT_FLAT_CAP && blockIdx.x * VX_CHUNK < S.num_tasks) {
+    for (uint32_t i = threadIdx.x; i < S.num_geom; i += RT_BLOCK_THREADS)
       s_geom[i] = rect_corners(S.A.ld_u4(S.vgeom + 64u * i + 32u));
   }
   __syncthreads();
@@ -486,14 +495,14 @@ VX_MAIN(rt_kernel_arg_t, arg, RT_BLOCK_THREADS) {
   __shared__ FlatLds s_flat;
   (void)w;
   const int rc = vx_spawn_chunks_block(
-      arg->num_tasks,
+      S.num_tasks,
       [&](const vx_task_t& task, bool valid, const Scene* s) { flat_chunk(task, valid, *s, s_flat, cnt); },
       &S);
 #else
   if ((threadIdx.x & 63u) == 0) w.q_count = 0;
   __builtin_amdgcn_wave_barrier();
   const int rc = vx_spawn_tasks_ex(
-      arg->num_tasks,
+      S.num_tasks,
       [&](const vx_task_t& task, const Scene* s) { kernel_body(task, *s, w, cnt); },
       [&](bool final, const Scene* s) { shadow_drain(final, *s, w, cnt); }, &S);
 #endif

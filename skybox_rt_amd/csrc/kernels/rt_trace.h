@@ -32,6 +32,9 @@
 #ifndef RT_BVH_WALK
 #define RT_BVH_WALK 0  // 1: image rt_bvh -- primary and shadow rays walk the BVH, no list code
 #endif
+#ifndef RT_BVH8
+#define RT_BVH8 0  // 1: the BVH8 images -- shadow packets (rt_bvh8) and the pair walk (pt_kernel8) on rt_node8h_t
+#endif
 
 namespace rtk {
 
@@ -59,6 +62,8 @@ struct Scene {
   uint32_t vnodes, vtris, vlayers, vgeom, num_vnodes;  // primary visibility (rt_common.h)
   uint32_t num_nodes, num_nodes4, num_layer, num_geom, flags, width, height;
   uint32_t shard_index, shard_count, tiles_x, clear_color, bounces, seed, split_tiles, split_log;
+  uint32_t tiles_x_magic, num_tasks;
+  uint32_t nodes8, num_nodes8;  // BVH8 (rt_node8h_t; the RT_BVH8 images)
   float sx, sy, light[3];
   uint64_t argp;  // the argument block (constant address space), for lazy_args
   uint32_t blist, bidx, blist_blocks;  // per-block candidate lists (rt_bentry_t)
@@ -115,6 +120,10 @@ __device__ __forceinline__ Scene load_scene(const rt_kernel_arg_t* ga) {
   s.shard_index = a->shard_index;
   s.shard_count = a->shard_count;
   s.tiles_x = a->tiles_x;
+  s.tiles_x_magic = a->tiles_x_magic;
+  s.num_tasks = a->num_tasks;  // through the scalar cache (arg->num_tasks would be a flat load)
+  s.nodes8 = (uint32_t)a->nodes8_addr;
+  s.num_nodes8 = a->num_nodes8;
   s.clear_color = a->clear_color;
   s.sx = a->sx;
   s.sy = a->sy;
@@ -662,6 +671,126 @@ __device__ __forceinline__ bool occluded_packet(const Scene& S, const Ray& r, bo
   return occ;
 }
 
+// occluded_packet on the BVH8 (rt_node8h_t, RT_BVH8 images): the same
+// walk -- children in fixed slot order, a child entered when some unfinished
+// lane's ray hits its box and all its ancestors', the stack in one VGPR --
+// over 8 children per node (the node as two 64-B scalar loads, one per
+// rt_node4h_t half), so a root-to-leaf walk takes half as many dependent node
+// steps.  Restricted to one lane it is the per-lane any-hit walk of the BVH8
+// in slot order (oracle/rt.c bvh8_step), so verdicts and per-ray counts are
+// its.
+__device__ __forceinline__ bool occluded_packet8(const Scene& S, const Ray& r, bool act, int32_t skip,
+                                                 float tmax, Counters& cnt) {
+  bool done = !act, occ = false;
+  if (S.num_nodes8 == 0 || __ballot(!done) == 0) return false;
+  int32_t vstk = 0;  // stack entry i in lane i of this VGPR
+  int sp = 0;
+  int32_t ref = 0;
+  bool on = true;     // this lane's ray hit the current node's box (and its ancestors')
+  uint32_t onb = 0u;  // the same for the stack entries (bit sp)
+  static_assert(RT_MAX_STACK <= 32, "one bit per stack entry");
+  for (;;) {
+    const bool live = on && !done;
+    if (ref >= 0) {
+      RT_CNT(cnt.visits += live;)
+      RT_WAVE_ITER(9);
+      const uint32_t no = S.nodes8 + 128u * (uint32_t)ref;
+      uint4 nw[8];
+      RT_LD_BEGIN();
+      S.A.sld_u4n<8>(no, nw);  // two s_load_dwordx16
+      RT_LD_END(1);
+      int32_t c[8];
+      bool h[8];
+      uint32_t need = 0u;  // wave-uniform: children some live lane enters
+#pragma unroll
+      for (int hf = 0; hf < 2; ++hf) {
+        const uint4 px = nw[4 * hf], py = nw[4 * hf + 1], pz = nw[4 * hf + 2], cf = nw[4 * hf + 3];
+        float lx[4], hx[4], ly[4], hy[4], lz[4], hz[4];
+        auto h2 = [](uint32_t u, float& a, float& b) {
+          a = (float)__builtin_bit_cast(_Float16, (uint16_t)(u & 0xffffu));
+          b = (float)__builtin_bit_cast(_Float16, (uint16_t)(u >> 16));
+        };
+        h2(px.x, lx[0], lx[1]); h2(px.y, lx[2], lx[3]); h2(px.z, hx[0], hx[1]); h2(px.w, hx[2], hx[3]);
+        h2(py.x, ly[0], ly[1]); h2(py.y, ly[2], ly[3]); h2(py.z, hy[0], hy[1]); h2(py.w, hy[2], hy[3]);
+        h2(pz.x, lz[0], lz[1]); h2(pz.y, lz[2], lz[3]); h2(pz.z, hz[0], hz[1]); h2(pz.w, hz[2], hz[3]);
+        const int32_t cc[4] = {(int32_t)cf.x, (int32_t)cf.y, (int32_t)cf.z, (int32_t)cf.w};
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          float tn = 0.0f;
+          const bool hs = slab(lx[i], hx[i], ly[i], hy[i], lz[i], hz[i], r, 0.0f, tmax, &tn);
+          c[4 * hf + i] = cc[i];
+          h[4 * hf + i] = hs & live & (cc[i] != RT_EMPTY_REF);
+          need |= __ballot(h[4 * hf + i]) ? 1u << (4 * hf + i) : 0u;
+        }
+      }
+      if (need) {
+        // push the needed children after the first, last slot first
+#pragma unroll
+        for (int i = 7; i >= 1; --i) {
+          if ((need >> i) & 1u && (need & ((1u << i) - 1u))) {
+            if (sp < RT_MAX_STACK) {
+              vstk = vwritelane(vstk, c[i], sp);
+              onb = h[i] ? onb | (1u << sp) : onb & ~(1u << sp);
+              ++sp;
+            }
+          }
+        }
+        const int f = __builtin_ctz(need);
+        int32_t rf = c[0];
+        bool of = h[0];
+#pragma unroll
+        for (int i = 1; i < 8; ++i) {
+          rf = f == i ? c[i] : rf;
+          of = f == i ? h[i] : of;
+        }
+        ref = rf;
+        on = of;
+        continue;
+      }
+    } else {
+      const uint32_t lr = (uint32_t)ref;
+      const uint32_t first = (lr >> 4) & 0x07ffffffu, count = (lr & 15u) + 1u;
+      RT_WAVE_ITER(9);
+      bool lv = live;
+      constexpr uint32_t H = kLeafHoist;
+#pragma unroll
+      for (uint32_t q0 = 0; q0 < 4; q0 += H) {
+        if (q0 >= count) break;
+        float4 ta[H], tb[H], tc[H];
+        {
+          uint4 tw[3 * H];
+          RT_LD_BEGIN();
+          S.A.sld_u4n<3 * H>(S.tris + 48u * (first + q0), tw);
+          RT_LD_END(1);
+#pragma unroll
+          for (uint32_t j = 0; j < H; ++j) {
+            ta[j] = u4f(tw[3 * j]); tb[j] = u4f(tw[3 * j + 1]); tc[j] = u4f(tw[3 * j + 2]);
+          }
+        }
+#pragma unroll
+        for (uint32_t j = 0; j < H; ++j) {
+          if (q0 + j < count) {
+            RT_CNT(cnt.tests += lv;)
+            float t;
+            if (lv && __float_as_int(ta[j].w) != skip && mt_hit(r, ta[j], tb[j], tc[j], 0.0f, &t) &&
+                t < tmax) {
+              occ = true;
+              done = true;
+              lv = false;
+            }
+          }
+        }
+      }
+      if (__ballot(!done) == 0) break;
+    }
+    if (sp == 0) break;
+    --sp;
+    on = (onb >> sp) & 1u;
+    ref = __builtin_amdgcn_readlane(vstk, sp);
+  }
+  return occ;
+}
+
 // A shadow segment's any-hit over its light-space cell list (rt_common.h;
 // oracle/rt.c sl_occluded): the cell of its direction from the light, then
 // the cell's triangles in the list's (key, geometry index) order -- nearest
@@ -1019,6 +1148,160 @@ __device__ __forceinline__ int32_t trace_coop(const Scene& S, const Ray& r, int3
   return bpid;
 }
 
+// The BVH8 closest-hit step for a lane pair (pt_kernel8: RT_BVH8): the
+// lower lane reads half 0 of the rt_node8h_t (children 0-3), the upper half 1
+// (children 4-7); each slab-tests its four, the pair swaps the four keys and
+// children (DPP moves), and both lanes run bvh8_step's 19-comparator network
+// (oracle/rt.c: Batcher's odd-even merge sort, strict <, misses keyed +inf,
+// hit keys clamped to FLT_MAX) over slots 0-7, then push C[1..n-1] farthest
+// first with unconditional row stores (the lower lane C[1..3], the upper
+// C[4..7]; entries past the hit count to the slack row RT_MAX_STACK) and take
+// C[0].  Per ray: the per-lane BVH8 walk's visits, stack order and result.
+template <bool SCALAR>
+__device__ __forceinline__ int32_t node8_coop(const Scene& S, uint32_t ref, const Ray& r, float lim, bool hi,
+                                              int32_t* mem, int& sp) {
+  const uint32_t no = S.nodes8 + 128u * ref;
+  uint4 w[4];
+  if (SCALAR) {  // the root: both halves through the scalar cache, this lane's selected
+    uint4 nw[8];
+    S.A.sld_u4n<8>(no, nw);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) w[q] = hi ? nw[4 + q] : nw[q];
+  } else {
+    const uint32_t ho = no + (hi ? 64u : 0u);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) w[q] = S.A.ld_u4(ho + 16u * q);
+  }
+  auto h2 = [](uint32_t u, float& a, float& b) {
+    a = (float)__builtin_bit_cast(_Float16, (uint16_t)(u & 0xffffu));
+    b = (float)__builtin_bit_cast(_Float16, (uint16_t)(u >> 16));
+  };
+  float lx[4], hx[4], ly[4], hy[4], lz[4], hz[4];
+  h2(w[0].x, lx[0], lx[1]); h2(w[0].y, lx[2], lx[3]); h2(w[0].z, hx[0], hx[1]); h2(w[0].w, hx[2], hx[3]);
+  h2(w[1].x, ly[0], ly[1]); h2(w[1].y, ly[2], ly[3]); h2(w[1].z, hy[0], hy[1]); h2(w[1].w, hy[2], hy[3]);
+  h2(w[2].x, lz[0], lz[1]); h2(w[2].y, lz[2], lz[3]); h2(w[2].z, hz[0], hz[1]); h2(w[2].w, hz[2], hz[3]);
+  const int32_t c[4] = {(int32_t)w[3].x, (int32_t)w[3].y, (int32_t)w[3].z, (int32_t)w[3].w};
+  float k[4];
+  uint32_t nh = 0;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    float tn = 0.0f;
+    const bool h = slab(lx[i], hx[i], ly[i], hy[i], lz[i], hz[i], r, 0.0f, lim, &tn) & (c[i] != RT_EMPTY_REF);
+    k[i] = h ? fminf(tn, 3.402823466e38f) : __builtin_inff();
+    nh += h ? 1u : 0u;
+  }
+  float K[8];
+  int32_t C[8];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const float pk = xpartf(k[i], hi);
+    const int32_t pc = (int32_t)xpart((uint32_t)c[i], hi);
+    K[i] = hi ? pk : k[i];
+    K[4 + i] = hi ? k[i] : pk;
+    C[i] = hi ? pc : c[i];
+    C[4 + i] = hi ? c[i] : pc;
+  }
+  auto cx = [&](int a, int b) {  // swap iff K[b] < K[a]
+    const bool sw = K[b] < K[a];
+    const float ka = K[a], kb = K[b];
+    const int32_t ca = C[a], cb = C[b];
+    K[a] = sw ? kb : ka; K[b] = sw ? ka : kb;
+    C[a] = sw ? cb : ca; C[b] = sw ? ca : cb;
+  };
+  cx(0, 1); cx(2, 3); cx(4, 5); cx(6, 7);
+  cx(0, 2); cx(1, 3); cx(4, 6); cx(5, 7);
+  cx(1, 2); cx(5, 6);
+  cx(0, 4); cx(1, 5); cx(2, 6); cx(3, 7);
+  cx(2, 4); cx(3, 5);
+  cx(1, 2); cx(3, 4); cx(5, 6);
+  const int n = (int)(nh + xpart(nh, hi));
+  if (n == 0) return RT_EMPTY_REF;
+  auto row = [&](int j) {
+    const int rr = sp + n - 1 - j;
+    return (j < n && rr < RT_MAX_STACK) ? rr : RT_MAX_STACK;
+  };
+  if (hi) {
+    mem[64 * row(4)] = C[4];
+    mem[64 * row(5)] = C[5];
+    mem[64 * row(6)] = C[6];
+    mem[64 * row(7)] = C[7];
+  } else {
+    mem[64 * row(1)] = C[1];
+    mem[64 * row(2)] = C[2];
+    mem[64 * row(3)] = C[3];
+  }
+  const int nt = sp + n - 1;
+  sp = nt < RT_MAX_STACK ? nt : RT_MAX_STACK;
+  return C[0];
+}
+
+// trace_coop on the BVH8 (node8_coop; leaves as trace_coop's)
+__device__ __forceinline__ int32_t trace_coop8(const Scene& S, const Ray& r, int32_t skip, bool tie_high,
+                                               float* t_out, int32_t* mem, bool hi, Counters& cnt) {
+  if (S.num_nodes8 == 0) return trace_coop(S, r, skip, tie_high, t_out, mem, hi, cnt);
+  int sp = 0;
+  float bt = INFINITY;
+  int32_t bpid = -1;
+  RT_CNT(cnt.visits += hi ? 0u : 1u;)
+  int32_t ref = node8_coop<true>(S, 0u, r, bt, hi, mem, sp);
+  if (ref == RT_EMPTY_REF) return -1;
+  auto pop = [&](int32_t& x) {
+    if (sp == 0) return false;
+    x = mem[64 * --sp];
+    return true;
+  };
+  for (;;) {
+    bool dry = false;
+    {
+      RT_CYC_BEGIN();
+      while (ref >= 0) {  // while-while, as trace_impl
+        RT_WAVE_ITER(9);
+        RT_CNT(cnt.visits += hi ? 0u : 1u;)
+        const int32_t nx = node8_coop<false>(S, (uint32_t)ref, r, bt, hi, mem, sp);
+        if (nx != RT_EMPTY_REF) { ref = nx; continue; }
+        if (!pop(ref)) { dry = true; break; }
+      }
+      RT_CYC_END(11);
+    }
+    if (dry) break;
+    {
+      RT_WAVE_ITER(9);  // this lane's two of the leaf's (up to 4) triangles (padding records past the end)
+      const uint32_t lr = (uint32_t)ref;
+      const uint32_t first = (lr >> 4) & 0x07ffffffu, count = (lr & 15u) + 1u;
+      const uint32_t k0 = hi ? 1u : 0u, ks = 2u;  // the lower lane triangles 0 and 2, the upper 1 and 3
+      const uint32_t to = S.tris + 48u * (first + k0);
+      float4 ta[2], tb[2], tc[2];
+#pragma unroll
+      for (uint32_t k = 0; k < 2; ++k) {
+        ta[k] = S.A.ld_f4(to + 48u * ks * k);
+        tb[k] = S.A.ld_f4(to + 48u * ks * k + 16);
+        tc[k] = S.A.ld_f4(to + 48u * ks * k + 32);
+      }
+#pragma unroll
+      for (uint32_t k = 0; k < 2; ++k) {
+        if (k0 + ks * k < count) {
+          const int32_t pid = __float_as_int(ta[k].w);
+          RT_CNT(++cnt.tests;)
+          float t;
+          if (pid != skip && mt_hit(r, ta[k], tb[k], tc[k], 0.0f, &t) && closer(t, pid, bt, bpid, tie_high)) {
+            bt = t;
+            bpid = pid;
+          }
+        }
+      }
+      const float pbt = xpartf(bt, hi);
+      const int32_t pb = (int32_t)xpart((uint32_t)bpid, hi);
+      if (pb >= 0 && closer(pbt, pb, bt, bpid, tie_high)) {
+        bt = pbt;
+        bpid = pb;
+      }
+    }
+    if (!pop(ref)) break;
+  }
+  if (bpid >= 0) *t_out = bt;
+  return bpid;
+}
+
 // occluded_list by a lane pair: rounds of four records, the lower lane
 // testing the first two, the upper the other two; the verdict is whether any
 // record occludes (order-free), the tests counted are the sequential scan's
@@ -1333,7 +1616,28 @@ __device__ __forceinline__ uint32_t shade_wave(const Scene& S, int32_t spid, uin
     }
     return color;
   }
-  if (mine) color = shade_lane(S, spid, x, y, cnt);
+  // mixed primitives: each lane's primitive record per lane (vector loads,
+  // all in flight together), the drawcall state per distinct drawcall of the
+  // wave through the scalar cache (usually one or two: the model and the
+  // backdrop), so the sampler's format / filter / wrap switches are
+  // wave-uniform branches instead of exec-mask branches per lane
+  gfx::Prim p;
+  gfx::load_prim(S.A, S.prims + 128u * (uint32_t)(mine ? spid : p0), p);
+  const uint32_t dc = p.dc();
+  uint64_t pend = need;
+  while (pend != 0) {
+    const uint32_t d0 = (uint32_t)__builtin_amdgcn_readlane((int)dc, (int)__builtin_ctzll(pend));
+    const bool take = mine && dc == d0;
+    pend &= ~__ballot(take);
+    const gfx::DcState s = gfx::load_dcstate<true>(S.A, S.dcs + 64u * d0);
+    if (take) {
+#ifdef RT_INSTRUMENT
+      ++cnt.shaded;
+      if (s.flags & RT_DC_TEX) cnt.texel_bytes += (s.filter == VX_TEX_FILTER_BILINEAR ? 4u : 1u) * s.stride;
+#endif
+      color = gfx::shade(S.A, p, s, x, y);
+    }
+  }
   return color;
 }
 
@@ -1655,6 +1959,23 @@ __device__ __forceinline__ int32_t resolve_layers(const Scene& S, uint32_t px, u
 // 32 chunks of 64 tasks with only lanes 0-31 live, one 8x4 half-block each:
 // half as many divergent rays per wave where the per-wave union of BVH
 // paths is widest, which shortens the frame's critical path.
+// global tile gt -> (column, row) with no integer division: the row is
+// mulhi(gt, magic), magic = rt_tiles_x_magic(tiles_x) (rt_common.h), then at
+// most one correction either way (exact for every gt < 2^32 / tiles_x)
+__device__ __forceinline__ void tile_xy(uint32_t gt, uint32_t tiles_x, uint32_t magic, uint32_t* tx,
+                                        uint32_t* ty) {
+  uint32_t q = __umulhi(gt, magic);
+  int32_t r = (int32_t)(gt - q * tiles_x);
+  if (r < 0) {
+    --q;
+    r += (int32_t)tiles_x;
+  } else if (r >= (int32_t)tiles_x) {
+    ++q;
+    r -= (int32_t)tiles_x;
+  }
+  *tx = (uint32_t)r;
+  *ty = q;
+}
 struct TaskPix {
   uint32_t lt;   // shard-local tile
   uint32_t idx;  // pixel of the tile in block order: (8x8 block) * 64 + lane of the block
@@ -1667,7 +1988,7 @@ struct TaskPix {
 #define RT_LAZY_TASK_ARGS 1
 #endif
 struct TaskArgs {
-  uint32_t split_tiles, split_log, order, shard_index, shard_count, tiles_x, quad_tiles;
+  uint32_t split_tiles, split_log, order, shard_index, shard_count, tiles_x, quad_tiles, tiles_x_magic;
 };
 __device__ __forceinline__ TaskArgs task_args(const Scene& S) {
   TaskArgs t;
@@ -1678,11 +1999,11 @@ __device__ __forceinline__ TaskArgs task_args(const Scene& S) {
       (const __attribute__((address_space(4))) rt_kernel_arg_t*)p;
   t.split_tiles = a->split_tiles; t.split_log = a->split_log; t.order = (uint32_t)a->order_addr;
   t.shard_index = a->shard_index; t.shard_count = a->shard_count; t.tiles_x = a->tiles_x;
-  t.quad_tiles = a->quad_tiles;
+  t.quad_tiles = a->quad_tiles; t.tiles_x_magic = a->tiles_x_magic;
 #else
   t.split_tiles = S.split_tiles; t.split_log = S.split_log; t.order = S.order;
   t.shard_index = S.shard_index; t.shard_count = S.shard_count; t.tiles_x = S.tiles_x;
-  t.quad_tiles = 0;
+  t.quad_tiles = 0; t.tiles_x_magic = S.tiles_x_magic;
 #endif
   return t;
 }
@@ -1734,10 +2055,69 @@ __device__ __forceinline__ void task_pixel(const Scene& S, uint32_t t, uint32_t*
   const TaskPix m = task_map(S, T, t);
   if (lb) *lb = (uint32_t)__builtin_amdgcn_readfirstlane((m.lt << 4) | (m.idx >> 6));
   const uint32_t blk = m.idx >> 6, ln = m.idx & 63u;
-  const uint32_t gt = T.shard_index + m.lt * T.shard_count;
-  const uint32_t tx = gt % T.tiles_x, ty = gt / T.tiles_x;
+  uint32_t tx, ty;
+  tile_xy(T.shard_index + m.lt * T.shard_count, T.tiles_x, T.tiles_x_magic, &tx, &ty);
   *x = m.live ? (tx << RT_TILE_LOG) + ((blk & 3u) << 3) + (ln & 7u) : 0xffffffffu;  // dead lane:
   *y = (ty << RT_TILE_LOG) + ((blk >> 2) << 3) + (ln >> 3);                          // off-image
+}
+
+// The task map of one 64-task chunk, wave-uniform (every lane of a wave runs
+// the same chunk: vx_spawn deals whole chunks), all in scalar registers: the
+// chunk's tier (quad / split / whole-block tiles, task_map's rule), its
+// local tile (one scalar load of the work order), the tile's position
+// (tile_xy) and its 8x8 block; a lane's pixel is then a few VALU operations
+// (chunk_pixel).  Equals task_map / task_pixel for every task of the chunk.
+struct ChunkMap {
+  uint32_t lt, blk, part, pl, tx, ty;
+};
+__device__ __forceinline__ ChunkMap chunk_map(const Scene& S, const TaskArgs& T, uint32_t c) {
+  ChunkMap m;
+  uint32_t pl = T.split_log, base = 0, ns = T.split_tiles;
+  if (T.quad_tiles) {
+    const uint32_t hq = T.quad_tiles << 6;  // 4096 tasks = 64 chunks per quad tile
+    if (c < hq) {
+      pl = 4u;
+      ns = T.quad_tiles;
+    } else {
+      c -= hq;
+      base = T.quad_tiles;
+      ns -= T.quad_tiles;
+    }
+  }
+  const uint32_t ccl = 10u - pl;     // log2 chunks per split tile (1024 >> pl)
+  const uint32_t hs = ns << ccl;
+  uint32_t pos;
+  if (c < hs) {
+    const uint32_t sub = 6u - pl;    // log2 chunks per 8x8 block
+    const uint32_t ci = c & ((1u << ccl) - 1u);
+    pos = base + (c >> ccl);
+    m.blk = ci >> sub;
+    m.part = ci & ((1u << sub) - 1u);
+    m.pl = pl;
+  } else {
+    pos = base + ns + ((c - hs) >> 4);
+    m.blk = c & 15u;
+    m.part = 0;
+    m.pl = 6u;
+  }
+  m.lt = T.order ? S.A.sld<uint32_t>(T.order + 4u * pos) : pos;
+  tile_xy(T.shard_index + m.lt * T.shard_count, T.tiles_x, T.tiles_x_magic, &m.tx, &m.ty);
+  return m;
+}
+// lane `ln` of the chunk: its pixel (dead lanes of split chunks: x =
+// 0xffffffff, off-image) and its framebuffer word (store_out)
+__device__ __forceinline__ void chunk_pixel(const Scene& S, const ChunkMap& m, uint32_t ln, uint32_t* x,
+                                            uint32_t* y, uint32_t* out) {
+  const uint32_t ib = (m.part << m.pl) + (ln & ((1u << m.pl) - 1u));  // pixel of the 8x8 block
+  const bool live = ln < (1u << m.pl);
+  const uint32_t px = (m.tx << RT_TILE_LOG) + ((m.blk & 3u) << 3) + (ib & 7u);
+  *x = live ? px : 0xffffffffu;
+  *y = (m.ty << RT_TILE_LOG) + ((m.blk >> 2) << 3) + (ib >> 3);
+  // compact shard buffers: local-tile order, each tile row-major (store_pixel)
+  *out = (S.flags & RT_FLAG_COMPACT) ? (m.lt << 10) | ((*y & 31u) << 5) | (px & 31u) : *y * S.width + px;
+}
+__device__ __forceinline__ void store_out(const Scene& S, uint32_t out, uint32_t color) {
+  S.A.st_u32(S.cbuf + 4u * out, color);
 }
 
 __device__ __forceinline__ void primary_dir(const Scene& S, uint32_t x, uint32_t y, Ray& r) {

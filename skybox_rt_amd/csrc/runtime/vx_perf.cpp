@@ -76,7 +76,8 @@ State& St() {
 }
 
 bool IsMain(const std::string& name) {
-  return name.rfind("vx_main", 0) == 0;  // vx_main, vx_main_<image> (VX_ENTRY)
+  // vx_main, vx_main_<image> (VX_ENTRY); not an image's completion kernel <entry>_done
+  return name.rfind("vx_main", 0) == 0 && !(name.size() > 5 && name.compare(name.size() - 5, 5, "_done") == 0);
 }
 
 void CodeObjectCb(rocprofiler_callback_tracing_record_t rec, rocprofiler_user_data_t*, void*) {
