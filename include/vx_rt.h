@@ -243,6 +243,10 @@ typedef struct {
                              frame is one launch group of 2, vortex_hip.h) */
   uint32_t slist_built;   /* 1: the last configure / set_light built shadow lists for a new light
                              (0: the lists of an unchanged light were kept) */
+  uint32_t bvh8;          /* 1: the configured frames' BVH walks run the BVH8 images (rt_bvh8's
+                             shadow packets, pt_kernel8's pair walk): the tree has a BVH8 whose
+                             stack fits them and env RT_BVH8=1 */
+  uint32_t pad;
 } rt_setup_stats_t;
 /* (reads back the status of shadow lists queued by rt_renderer_set_light:
  * waits for the device) */

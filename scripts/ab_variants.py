@@ -1,6 +1,9 @@
 #!/usr/bin/env python3
 """Interleaved A/B timing of kernel-image variants in one process on one GPU
-(cdna_hip_programming.md section 5.4 rule 24).
+(cdna_hip_programming.md section 5.4 rule 24): per round each variant's
+back-to-back frames (the bench's kernel clock: events on the driver's stream
+around `frames` launches with per-launch timing off) and three synchronous
+frames' device times.
 
 A variant is `label=dir[:ENV=VAL[:ENV=VAL...]]`, where `dir` is `default`
 (skybox_rt_amd/lib) or a directory name under skybox_rt_amd/lib/variants and
@@ -73,15 +76,40 @@ def main():
         rs[label] = r
         names.append(label)
     times = {n: [] for n in names}
+    sync = {n: [] for n in names}
     for _ in range(args.rounds):
         for n in names:
             r = rs[n]
-            for _ in range(args.frames):
+            # back-to-back frames (no per-launch events, the bench's kernel
+            # clock): two events on the driver's stream around them / frames
+            times[n].append(back_to_back_ms(r, max(args.frames, 20)))
+            for _ in range(3):  # and a synchronous frame's device time (completion stamps)
                 r.render()
-                times[n].append(r.kernel_ms())
+                sync[n].append(r.kernel_ms())
     out = {n: {"median_ms": round(float(np.median(t)), 5), "min_ms": round(float(np.min(t)), 5),
+               "sync_median_ms": round(float(np.median(sync[n])), 5),
                "grid": rs[n].stats()["grid"]} for n, t in times.items()}
     print(json.dumps(out))
+
+
+def back_to_back_ms(r, frames):
+    import torch
+    stream = torch.cuda.ExternalStream(r.device_stream())
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    r.set_timing(False)
+    try:
+        for _ in range(3):
+            r.start()
+        r.wait()
+        e0.record(stream)
+        for _ in range(frames):
+            r.start()
+        e1.record(stream)
+        r.wait()
+        e1.synchronize()
+    finally:
+        r.set_timing(True)
+    return e0.elapsed_time(e1) / frames
 
 
 if __name__ == "__main__":

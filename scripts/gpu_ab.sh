@@ -10,3 +10,4 @@ fi
 if [ -n "$AB_SHADOW" ]; then timeout -k 10 300 python scripts/ab_variants.py --rounds ${ROUNDS:-8} --variants "$AB_SHADOW" > gpurun_out/${T}_shadow.json 2> gpurun_out/${T}_shadow.err || { tail -5 gpurun_out/${T}_shadow.err; exit 1; }; cat gpurun_out/${T}_shadow.json; fi
 if [ -n "$AB_PATH" ]; then timeout -k 10 300 python scripts/ab_variants.py --mode path --rounds ${ROUNDS:-8} --variants "$AB_PATH" > gpurun_out/${T}_path.json 2> gpurun_out/${T}_path.err || { tail -5 gpurun_out/${T}_path.err; exit 1; }; cat gpurun_out/${T}_path.json; fi
 if [ -n "$AB_FLAT" ]; then timeout -k 10 300 python scripts/ab_variants.py --mode flat --size 256 --no-shadows --rounds ${ROUNDS:-8} --variants "$AB_FLAT" > gpurun_out/${T}_flat.json 2> gpurun_out/${T}_flat.err || { tail -5 gpurun_out/${T}_flat.err; exit 1; }; cat gpurun_out/${T}_flat.json; fi
+if [ -n "$AB_BVH" ]; then timeout -k 10 300 python scripts/ab_variants.py --bvh-walk --rounds ${ROUNDS:-8} --variants "$AB_BVH" > gpurun_out/${T}_bvh.json 2> gpurun_out/${T}_bvh.err || { tail -5 gpurun_out/${T}_bvh.err; exit 1; }; cat gpurun_out/${T}_bvh.json; fi

@@ -868,6 +868,8 @@ static int host_setup(rt_renderer* r, const rt_render_params_t* p, bool raster, 
   return 0;
 }
 
+static bool use_bvh8(const rt_renderer* r);
+
 int rt_renderer_configure(rt_renderer_h r, const rt_render_params_t* p) {
   if (!r || !p) return fail("null argument");
   if (p->width == 0 || p->height == 0 || p->width > 32768 || p->height > 32768)
@@ -922,7 +924,8 @@ int rt_renderer_configure(rt_renderer_h r, const rt_render_params_t* p) {
   a.quad_tiles = 0;
   const bool order_on = !raster && r->local_tiles > 0 &&
                         !(std::getenv("RT_TILE_ORDER") && std::atoi(std::getenv("RT_TILE_ORDER")) == 0);
-  r->bvh8_env = !(std::getenv("RT_BVH8") && std::atoi(std::getenv("RT_BVH8")) == 0);
+  // the BVH8 images (rt_bvh8, pt_kernel8) on request: env RT_BVH8=1
+  r->bvh8_env = std::getenv("RT_BVH8") && std::atoi(std::getenv("RT_BVH8")) != 0;
   bool use_bvh4 = !(p->flags & RT_RENDER_BVH2) && (!r->gpu_bvh || r->gpu_bvh4);
   if (const char* e = std::getenv("RT_BVH_WIDTH")) use_bvh4 = use_bvh4 && std::atoi(e) != 2;
   r->use_bvh4 = use_bvh4;
@@ -1058,6 +1061,7 @@ int rt_renderer_configure(rt_renderer_h r, const rt_render_params_t* p) {
   r->setup.blist_blocks = a.blist_blocks;
   r->setup.slist_on = a.slist_on;
   r->setup.path_queue = r->pq ? 1u : 0u;
+  r->setup.bvh8 = use_bvh8(r) ? 1u : 0u;
   r->setup.setup_ms = setup_ms;
   r->setup.configure_ms = ms_since(t0);
   r->configured = true;

@@ -71,7 +71,7 @@ struct rt_renderer {
   vx_buffer_h krnl_bvh8[2] = {}, krnl_pt8[2] = {};
   vx_buffer_h nodes8 = nullptr;  // rt_node8h_t records
   uint32_t num_nodes8_built = 0;  // BVH8 records of the current tree (arg.num_nodes8: 0 when unused)
-  bool bvh8_env = true;           // env RT_BVH8 at the last configure (0: the BVH4 images)
+  bool bvh8_env = false;          // env RT_BVH8 at the last configure (1: the BVH8 images)
   vx_buffer_h sah_krnl = nullptr;  // bvh_sah.vxbin, loaded by the first device build
   vx_buffer_h pathq = nullptr, pathq_ctr = nullptr;
   bool pq = false;          // the configuration runs the two-kernel path tracer

@@ -210,6 +210,7 @@ __device__ __forceinline__ void primary(const vx_task_t& task, bool valid, const
 // throughput T and radiance L so far, its pixel task, the primary alpha.
 struct PathState {
   uint32_t task, alpha;
+  uint32_t xy, out;  // the pixel (x | y << 16: the bounce RNG key) and its framebuffer word, set once
   int32_t pid;
   float t;
   float o[3], d[3], T[3], L[3];
@@ -329,9 +330,7 @@ __device__ __forceinline__ bool path_step(const Scene& S, int32_t* stack, PathSt
   Ray b;
   if (alive) {
     b.o[0] = P[0]; b.o[1] = P[1]; b.o[2] = P[2];
-    uint32_t x, y;
-    task_pixel(S, st.task, &x, &y);
-    bounce_dir(nrm, pt_key(S.seed, y * S.width + x, v), b.d);  // keyed by pixel, not task
+    bounce_dir(nrm, pt_key(S.seed, (st.xy >> 16) * S.width + (st.xy & 0xffffu), v), b.d);  // keyed by pixel
     ray_setup(b);
     cnt.bounce += one;
     np = CO == 2 ? trace_quad(S, b, st.pid, tie_high, &nt, stack, role, cnt)
@@ -379,9 +378,7 @@ __device__ __forceinline__ bool path_step_pair(const Scene& S, int32_t* stack, P
   Ray b;
   b.o[0] = P[0]; b.o[1] = P[1]; b.o[2] = P[2];
   if (alive) {
-    uint32_t x, y;
-    task_pixel(S, st.task, &x, &y);
-    bounce_dir(nrm, pt_key(S.seed, y * S.width + x, v), b.d);  // keyed by pixel, not task
+    bounce_dir(nrm, pt_key(S.seed, (st.xy >> 16) * S.width + (st.xy & 0xffffu), v), b.d);  // keyed by pixel
   } else {
     b.d[0] = 1.0f; b.d[1] = 1.0f; b.d[2] = 1.0f;
   }
@@ -461,10 +458,18 @@ __device__ __forceinline__ bool path_step_pair(const Scene& S, int32_t* stack, P
 }
 
 __device__ __forceinline__ void store_path_pixel(const Scene& S, const PathState& st) {
+  store_out(S, st.out, st.alpha | (to8(st.L[0]) << 16) | (to8(st.L[1]) << 8) | to8(st.L[2]));
+}
+// st.xy / st.out from st.task (the queued forms: a path's pixel once, not per vertex)
+__device__ __forceinline__ void path_pixel(const Scene& S, PathState& st) {
   uint32_t x, y;
   task_pixel(S, st.task, &x, &y);
-  store_pixel(S, st.task, x, y,
-              st.alpha | (to8(st.L[0]) << 16) | (to8(st.L[1]) << 8) | to8(st.L[2]));
+  st.xy = x | (y << 16);
+  st.out = y * S.width + x;
+  if (S.flags & RT_FLAG_COMPACT) {
+    const TaskPix m = task_map(S, st.task);
+    st.out = (m.lt << 10) | ((y & 31u) << 5) | (x & 31u);
+  }
 }
 
 #if PT_MODE == 0
@@ -477,6 +482,7 @@ __device__ __forceinline__ void vertex(const Scene& S, PtLds& L, int qi, uint32_
   const uint32_t j = act ? i : 0u;
   PathState st;
   st.task = q.task[j];
+  path_pixel(S, st);
   st.alpha = q.alpha[j];
   st.pid = q.pid[j];
   st.t = q.t[j];
@@ -536,6 +542,12 @@ __device__ __forceinline__ void queued_path(const vx_task_t& task, const Scene& 
   const float k255 = 1.0f / 255.0f;
   PathState st;
   st.task = e.x;
+  st.xy = x | (y << 16);
+  st.out = y * S.width + x;
+  if (S.flags & RT_FLAG_COMPACT) {
+    const TaskPix m = task_map(S, e.x);
+    st.out = (m.lt << 10) | ((y & 31u) << 5) | (x & 31u);
+  }
   st.alpha = color & 0xff000000u;
   st.pid = (int32_t)e.z;
   st.t = __uint_as_float(e.y);
@@ -559,8 +571,11 @@ __device__ __forceinline__ void queued_path(const vx_task_t& task, const Scene& 
 __device__ __forceinline__ void lane_path(const vx_task_t& task, const Scene& S, int32_t* stack,
                                           Counters& cnt) {
   const uint32_t t = task.blockIdx.x;
-  uint32_t x, y, lb;
-  task_pixel(S, t, &x, &y, &lb);
+  // the chunk's task map in scalar registers (every lane runs the same chunk)
+  const ChunkMap cm = chunk_map(S, task_args(S), (uint32_t)__builtin_amdgcn_readfirstlane(t) >> 6);
+  uint32_t x, y, out;
+  chunk_pixel(S, cm, t & 63u, &x, &y, &out);
+  const uint32_t lb = (cm.lt << 4) | cm.blk;
   const bool in = x < S.width && y < S.height;
   // the whole wave is here and its upper 32 lanes hold no pixel (a 32-pixel
   // wave of a geometry tile) -- wave-uniform: with the light-space shadow
@@ -583,7 +598,7 @@ __device__ __forceinline__ void lane_path(const vx_task_t& task, const Scene& S,
   primary_dir(S, x, y, r);
   const float th = hit >= 0 ? plane_t(S, r, hit) : 0.0f;
   const bool path = hit >= 0 && secondary_ok(th);  // a path starts at the winner's plane
-  if (!path && in) store_pixel(S, t, x, y, color);
+  if (!path && in) store_out(S, out, color);
   if (!path && !pair && !coop) return;
   if (quad) {
     // lanes 4p .. 4p + 3 take pixel p's path (lane p); all four trace it,
@@ -593,6 +608,8 @@ __device__ __forceinline__ void lane_path(const vx_task_t& task, const Scene& S,
     const bool own = act && j == 0u;
     PathState q;
     q.task = (uint32_t)__shfl((int)t, (int)src);
+    q.xy = (uint32_t)__shfl((int)(x | (y << 16)), (int)src);
+    q.out = (uint32_t)__shfl((int)out, (int)src);
     q.alpha = (uint32_t)__shfl((int)(color & 0xff000000u), (int)src);
     q.pid = __shfl(hit, (int)src);
     q.t = __shfl(th, (int)src);
@@ -615,6 +632,8 @@ __device__ __forceinline__ void lane_path(const vx_task_t& task, const Scene& S,
   const float k255 = 1.0f / 255.0f;
   PathState st;
   st.task = t;
+  st.xy = x | (y << 16);
+  st.out = out;
   st.alpha = color & 0xff000000u;
   st.pid = hit;
   st.t = th;
@@ -644,6 +663,8 @@ __device__ __forceinline__ void lane_path(const vx_task_t& task, const Scene& S,
     bool act = __shfl((int)path, src) != 0;
     const bool own = act && !hi;
     st.task = (uint32_t)__shfl((int)st.task, src);
+    st.xy = (uint32_t)__shfl((int)st.xy, src);
+    st.out = (uint32_t)__shfl((int)st.out, src);
     st.alpha = (uint32_t)__shfl((int)st.alpha, src);
     st.pid = __shfl(st.pid, src);
     st.t = __shfl(st.t, src);
@@ -667,6 +688,8 @@ __device__ __forceinline__ void lane_path(const vx_task_t& task, const Scene& S,
     const bool own = path && !hi;
     bool act = xlow(path ? 1u : 0u) != 0u;
     st.task = xlow(st.task);
+    st.xy = xlow(st.xy);
+    st.out = xlow(st.out);
     st.alpha = xlow(st.alpha);
     st.pid = (int32_t)xlow((uint32_t)st.pid);
     st.t = xlowf(st.t);

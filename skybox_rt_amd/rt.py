@@ -67,10 +67,11 @@ class SetupStats(C.Structure):
     _fields_ = [("device", C.c_uint32), ("launches", C.c_uint32), ("heavy_tiles", C.c_uint32),
                 ("blist_blocks", C.c_uint32), ("setup_ms", C.c_double), ("configure_ms", C.c_double),
                 ("blist_entries", C.c_uint64), ("blist_max", C.c_uint32), ("slist_on", C.c_uint32),
-                ("slist_entries", C.c_uint64), ("path_queue", C.c_uint32), ("slist_built", C.c_uint32)]
+                ("slist_entries", C.c_uint64), ("path_queue", C.c_uint32), ("slist_built", C.c_uint32),
+                ("bvh8", C.c_uint32), ("pad", C.c_uint32)]
 
     def as_dict(self):
-        return {n: getattr(self, n) for n, _ in self._fields_}
+        return {n: getattr(self, n) for n, _ in self._fields_ if n != "pad"}
 
 
 class RenderParams(C.Structure):

@@ -11,6 +11,7 @@ build's level budget, so its launch sequence continues once); frames over it
 == the oracle.  The build is one launch sequence with one read-back: a
 rebuild (image resident) repeats the arrays exactly."""
 import math
+import os
 
 import numpy as np
 import pytest
@@ -22,6 +23,22 @@ pytestmark = pytest.mark.gpu
 from skybox_rt_amd import rt  # noqa: E402
 
 _paths = {}
+
+
+def _host_renderer(s):
+    """A renderer on the scene's host-built tree (app/bvh.cpp uploaded: env
+    RT_BVH=host while it is created) -- the arrays the device build must equal."""
+    old = os.environ.get("RT_BVH")
+    os.environ["RT_BVH"] = "host"
+    try:
+        r = rt.Renderer(s)
+    finally:
+        if old is None:
+            del os.environ["RT_BVH"]
+        else:
+            os.environ["RT_BVH"] = old
+    assert r.bvh_stats()["method"] == rt.RT_BVH_BUILD_HOST
+    return r
 
 
 def _scene(name, tmp_path_factory):
@@ -48,9 +65,10 @@ def test_gpu_sah_equals_host_build(tmp_path_factory, name):
     info = s.info()
     if info["num_geometry"] == 0:
         pytest.skip("no depth-tested geometry")
-    host = rt.Renderer(s)                     # the scene's host-built tree
+    host = _host_renderer(s)                  # the scene's host-built tree
     hn, ht = host.export_bvh()
     h4, hh = host.export_bvh4(), host.export_bvh4h()
+    h8 = host.export_bvh8h()
     r = rt.Renderer(s)
     st = r.build_bvh("sah")
     dn, dt = r.export_bvh()
@@ -59,14 +77,20 @@ def test_gpu_sah_equals_host_build(tmp_path_factory, name):
     d4 = r.export_bvh4()
     assert d4.shape == h4.shape and np.array_equal(d4.view(np.uint32), h4.view(np.uint32))
     assert np.array_equal(r.export_bvh4h(), hh)
+    # the BVH8 collapse (rt_node8h_t records) and its depth / stack
+    d8 = r.export_bvh8h()
+    assert d8.shape == h8.shape == (info["bvh8_nodes"], 128) and np.array_equal(d8, h8)
+    assert st["nodes8"] == info["bvh8_nodes"] and st["depth8"] == info["bvh8_depth"]
+    assert st["stack8"] == info["bvh8_stack"]
     assert st["depth"] == info["bvh_depth"] and st["nodes"] == info["bvh_nodes"]
     assert st["nodes4"] == info["bvh4_nodes"] and st["depth4"] == info["bvh4_depth"]
     assert st["stack4"] == info["bvh4_stack"] and st["method"] == 1
-    # one sequence: the init, the level budget's split launches, 7 finishing
-    # launches -- and, past the budget, a reset, the next levels, 7 again
+    # one sequence: the init, the level budget's split launches, 11 finishing
+    # launches (BVH2, BVH4, BVH8) -- and, past the budget, a reset, the next
+    # levels, 11 again
     budget = math.ceil(math.log2(info["num_geometry"] + 1)) + 4
     rounds = 1 if info["bvh_depth"] <= budget else 2
-    assert st["launches"] == 1 + min(rounds * budget, 63) + 7 * rounds + (rounds - 1)
+    assert st["launches"] == 1 + min(rounds * budget, 63) + 11 * rounds + (rounds - 1)
     if name == "chain96":
         assert rounds == 2
     print(f"{name}: {info['num_geometry']} tris, {st['nodes']} nodes, {st['launches']} launches, "
@@ -115,9 +139,10 @@ def test_gpu_sah_deep_tree_on_stale_scratch(tmp_path_factory):
     big.close()
     s = rt.Scene.load(_scene("chain96", tmp_path_factory))
     info = s.info()
-    host = rt.Renderer(s)
+    host = _host_renderer(s)
     hn, ht = host.export_bvh()
     h4, hh = host.export_bvh4(), host.export_bvh4h()
+    h8 = host.export_bvh8h()
     r = rt.Renderer(s)
     for _ in range(2):
         st = r.build_bvh("sah")
@@ -126,6 +151,7 @@ def test_gpu_sah_deep_tree_on_stale_scratch(tmp_path_factory):
         assert np.array_equal(dt.view(np.uint32), ht.view(np.uint32))
         assert np.array_equal(r.export_bvh4().view(np.uint32), h4.view(np.uint32))
         assert np.array_equal(r.export_bvh4h(), hh)
+        assert np.array_equal(r.export_bvh8h(), h8)
         assert st["depth"] == info["bvh_depth"] and st["stack4"] == info["bvh4_stack"]
     r.close()
     host.close()
