@@ -6,6 +6,7 @@
 #   ab      scripts/gpu_ab.sh with AB_SHADOW / AB_PATH / AB_FLAT variant lists
 #   prof    rocprofv3 --kernel-trace --stats of bench.py --no-cpu-baseline $BENCH_ARGS
 #   pmc     scripts/pmc_profile.sh for MODES (default: shadow)
+#   timeline scripts/wave_timeline.py 1024 $TL_MODE (stamp images, make diag)
 set -o pipefail
 cd "$GRAFT_REPO_ROOT"; mkdir -p gpurun_out; export TMPDIR=/tmp
 T=${TAG:-r05}
@@ -34,6 +35,10 @@ for s in ${STEPS:-tests bench}; do
         MODE=$m TAG=${T}_pmc bash scripts/pmc_profile.sh > gpurun_out/${T}_pmc_$m.log 2>&1 \
           || { tail -5 gpurun_out/${T}_pmc_$m.log; exit 1; }
       done ;;
+    timeline)
+      timeout -k 10 180 python scripts/wave_timeline.py 1024 ${TL_MODE:-} > gpurun_out/${T}_timeline.json \
+        2> gpurun_out/${T}_timeline.err || { tail -5 gpurun_out/${T}_timeline.err; exit 1; }
+      head -c 1500 gpurun_out/${T}_timeline.json; echo ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac
 done

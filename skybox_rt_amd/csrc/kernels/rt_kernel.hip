@@ -88,15 +88,19 @@ struct WaveLds {
 // 0.0302, 128 threads 0.0403.  The shadow rays read the MT records (rt_tri_t)
 // of S.geom.
 __shared__ uint4 s_geom[RT_FLAT_CAP];
-// RT_FLAT_SCALAR (A/B knob): no LDS staging, every rectangle word through
-// the scalar cache
+// RT_FLAT_SCALAR (default since r05): no LDS staging -- the block test
+// (RT_FLAT_BLOCK) reads its 64 rectangle words per instruction straight from
+// L2 with vector loads, so a workgroup starts on its chunk at once; A/B r05j
+// (256^2, median ms): staged 0.0101, unstaged 0.0096, unstaged with 512-thread
+// workgroups at 8 waves per SIMD 0.0090 (the default; 512 threads at 5 waves
+// per SIMD 0.0125, 128 threads 0.0122, 1024 threads 0.0204)
 // RT_FLAT_BLOCK: entries against the chunk's 8x8 block, 64 per instruction,
 // before the per-pixel tests (flat_chunk); 0 = the one-level scan
 #ifndef RT_FLAT_BLOCK
 #define RT_FLAT_BLOCK 1
 #endif
 #ifndef RT_FLAT_SCALAR
-#define RT_FLAT_SCALAR 0
+#define RT_FLAT_SCALAR 1
 #endif
 // RT_FLAT_VREC: the block test's candidates load their whole records as
 // vector loads, one round for the 64 entries, and each candidate is then
@@ -496,9 +500,13 @@ __device__ __forceinline__ void flush(int slot, uint32_t v) { vx_mpm_add(RT_MPM_
 #endif
 #endif
 #if RT_FLAT
-// config 2: 4 workgroups per CU (1 024 of 256 threads: one per 256^2 chunk,
-// each staging the list once) -- A/B r04i: 0.01084 ms vs 0.01108 at 16/CU
+// config 2: 4 workgroups per CU (1 024: one per 256^2 chunk) -- A/B r04i:
+// 0.01084 ms vs 0.01108 at 16/CU; registers for 8 waves per SIMD, so all
+// 1 024 workgroups of 512 threads are resident at once (r05j)
 __device__ __attribute__((used)) uint32_t __vx_grid_per_cu = 4;
+#ifndef RT_WAVES_PER_EU
+#define RT_WAVES_PER_EU 8
+#endif
 #endif
 #ifdef RT_WAVES_PER_EU
 VX_MAIN_OCC(rt_kernel_arg_t, arg, RT_BLOCK_THREADS, RT_WAVES_PER_EU) {
