@@ -722,12 +722,15 @@ def main():
     if flat:
         metric = (f"Mrays/sec per GPU + achieved HBM GB/s, {side}^2 primary rays, tekkaman flat "
                   f"triangle list, no BVH (BASELINE config 2)")
-        kind = "primary rays, flat triangle list (no BVH, LDS-staged)"
+        kind = "primary rays, flat triangle list (no BVH)"
     primary = ("primary: 8x8-block candidate lists built on the device (raster-exact)"
                if setup_st["blist_blocks"] else f"primary: {bvh_kind} packet walk (raster-exact)")
     if flat:
         workload = (f"{side}x{side} {kind}, tekkaman.cgltrace: every ray tests the whole geometry "
-                    f"list (rectangle words in LDS, wave-uniform rectangle skip, exact edge + depth test)")
+                    f"list -- a 512-thread workgroup per 64-pixel chunk splits the list 8 ways, each "
+                    f"wave tests 64 rectangle words per instruction (read from L2) against the "
+                    f"chunk's 8x8 block, then the entries reaching it per pixel (exact edge + depth "
+                    f"test, records through the scalar cache)")
     elif path and setup_st.get("path_queue"):
         shadow_how = ("light-space shadow lists" if setup_st["slist_on"] else f"{bvh_kind} walk")
         workload = (f"{side}x{side} {kind}, tekkaman.cgltrace, two kernels per frame: {primary}, "
@@ -738,8 +741,10 @@ def main():
         workload = (f"{side}x{side} {kind}, tekkaman.cgltrace, one kernel; {primary}; then each "
                     f"path on its lane(s): bounce rays a {bvh_kind} walk (LDS stack), shadow rays "
                     f"on the light-space shadow lists; in the 32-pixel waves of geometry tiles "
-                    f"two lanes per path (children / triangles / list records split two and two, "
-                    f"permlane32 exchanges)")
+                    f"two adjacent lanes per path (children / triangles / list records split two "
+                    f"and two, DPP exchanges); no wave64 compaction of live paths in the timed "
+                    f"kernel: the block-compacted (pt_compact) and queue-compacted "
+                    f"(RT_PT_QUEUE=1) forms measured slower, DESIGN.md 2.1")
     elif path:
         workload = (f"{side}x{side} {kind}, tekkaman.cgltrace; {primary}; bounce + shadow rays: "
                     f"per-lane {bvh_kind} walk, LDS stack, shadow/bounce lanes paired in the "

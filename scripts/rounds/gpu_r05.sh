@@ -6,7 +6,7 @@
 #   ab      scripts/gpu_ab.sh with AB_SHADOW / AB_PATH / AB_FLAT variant lists
 #   prof    rocprofv3 --kernel-trace --stats of bench.py --no-cpu-baseline $BENCH_ARGS
 #   pmc     scripts/pmc_profile.sh for MODES (default: shadow)
-#   timeline scripts/wave_timeline.py 1024 $TL_MODE (stamp images, make diag)
+#   timeline scripts/wave_timeline.py 1024 <mode> for TL_MODES (shadow, bvh, path; make diag)
 set -o pipefail
 cd "$GRAFT_REPO_ROOT"; mkdir -p gpurun_out; export TMPDIR=/tmp
 T=${TAG:-r05}
@@ -36,9 +36,11 @@ for s in ${STEPS:-tests bench}; do
           || { tail -5 gpurun_out/${T}_pmc_$m.log; exit 1; }
       done ;;
     timeline)
-      timeout -k 10 180 python scripts/wave_timeline.py 1024 ${TL_MODE:-} > gpurun_out/${T}_timeline.json \
-        2> gpurun_out/${T}_timeline.err || { tail -5 gpurun_out/${T}_timeline.err; exit 1; }
-      head -c 1500 gpurun_out/${T}_timeline.json; echo ;;
+      for m in ${TL_MODES:-shadow}; do
+        timeout -k 10 180 python scripts/wave_timeline.py 1024 $m > gpurun_out/${T}_timeline_$m.json \
+          2> gpurun_out/${T}_timeline_$m.err || { tail -5 gpurun_out/${T}_timeline_$m.err; exit 1; }
+        head -c 1500 gpurun_out/${T}_timeline_$m.json; echo
+      done ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac
 done
