@@ -1,10 +1,10 @@
 # Round 5 GPU calls.  STEPS = space-separated list, run in order, the first
 # failure ends the call; TAG names the outputs under gpurun_out/.
 #   tests   pytest -m gpu (FILES= to restrict to some test files)
-#   bench   python bench.py $BENCH_ARGS  (-> ${TAG}_bench.json)
+#   bench   python bench.py --workload W $BENCH_ARGS for W in WORKLOADS (-> ${TAG}_bench_W.json)
 #   host    scripts/host_overhead.py (start / wait / kernel split of a synchronous frame)
 #   ab      scripts/gpu_ab.sh with AB_SHADOW / AB_PATH / AB_FLAT variant lists
-#   prof    rocprofv3 --kernel-trace --stats of bench.py --no-cpu-baseline $BENCH_ARGS
+#   prof    rocprofv3 --kernel-trace --stats of bench.py --workload W --no-cpu-baseline $BENCH_ARGS
 #   pmc     scripts/pmc_profile.sh for MODES (default: shadow)
 #   timeline scripts/wave_timeline.py 1024 <mode> for TL_MODES (shadow, bvh, path; make diag)
 set -o pipefail
@@ -18,18 +18,22 @@ for s in ${STEPS:-tests bench}; do
         > gpurun_out/${T}_pytest_gpu.log 2>&1; rc=$?; tail -3 gpurun_out/${T}_pytest_gpu.log
       [ $rc -eq 0 ] || { grep -E "FAILED|Error|assert" gpurun_out/${T}_pytest_gpu.log | head -20; exit $rc; } ;;
     bench)
-      timeout -k 10 400 python bench.py $BENCH_ARGS > gpurun_out/${T}_bench.json 2> gpurun_out/${T}_bench.err \
-        || { tail -5 gpurun_out/${T}_bench.err; exit 1; }
-      python3 -c "import json;j=json.load(open('gpurun_out/${T}_bench.json'));c=j['config'];print(j['value'],j['ms_per_step'],c['kernel_ms'],c.get('sync_ms_per_step'),j['roofline']['frac'])" ;;
+      for w in ${WORKLOADS:-shadow}; do
+        timeout -k 10 400 python bench.py --workload $w $BENCH_ARGS > gpurun_out/${T}_bench_$w.json \
+          2> gpurun_out/${T}_bench_$w.err || { tail -5 gpurun_out/${T}_bench_$w.err; exit 1; }
+        python3 -c "import json;j=json.load(open('gpurun_out/${T}_bench_$w.json'));c=j['config'];print('$w',j['value'],j['ms_per_step'],c['kernel_ms'],c.get('sync_ms_per_step'),j['roofline']['frac'])"
+      done ;;
     host)
       timeout -k 10 120 python scripts/host_overhead.py > gpurun_out/${T}_host.json 2> gpurun_out/${T}_host.err \
         || { tail -5 gpurun_out/${T}_host.err; exit 1; }; cat gpurun_out/${T}_host.json ;;
     ab)
       TAG=${T}_ab FILES= bash scripts/gpu_ab.sh || exit 1 ;;
     prof)
-      timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/${T}_prof -o ${T} --output-format csv \
-        -- python3 bench.py --no-cpu-baseline $BENCH_ARGS > gpurun_out/${T}_prof.log 2>&1 \
-        || { tail -5 gpurun_out/${T}_prof.log; exit 1; } ;;
+      for w in ${WORKLOADS:-shadow}; do
+        timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/${T}_prof_$w -o ${T}_$w --output-format csv \
+          -- python3 bench.py --workload $w --no-cpu-baseline $BENCH_ARGS > gpurun_out/${T}_prof_$w.log 2>&1 \
+          || { tail -5 gpurun_out/${T}_prof_$w.log; exit 1; }
+      done ;;
     pmc)
       for m in ${MODES:-shadow}; do
         MODE=$m TAG=${T}_pmc bash scripts/pmc_profile.sh > gpurun_out/${T}_pmc_$m.log 2>&1 \
@@ -37,7 +41,8 @@ for s in ${STEPS:-tests bench}; do
       done ;;
     timeline)
       for m in ${TL_MODES:-shadow}; do
-        timeout -k 10 180 python scripts/wave_timeline.py 1024 $m > gpurun_out/${T}_timeline_$m.json \
+        if [ $m = flat ]; then tl="scripts/flat_timeline.py 256"; else tl="scripts/wave_timeline.py 1024 $m"; fi
+        timeout -k 10 180 python $tl > gpurun_out/${T}_timeline_$m.json \
           2> gpurun_out/${T}_timeline_$m.err || { tail -5 gpurun_out/${T}_timeline_$m.err; exit 1; }
         head -c 1500 gpurun_out/${T}_timeline_$m.json; echo
       done ;;

@@ -60,7 +60,14 @@ constexpr int kWaves = RT_BLOCK_THREADS / 64;
 // per-lane walks' stack[depth][lane] (deep images: layouts other than the
 // binary16 BVH4 walk per lane)
 #define RT_QUEUE 128
-#define RT_LANE_STACK (!RT_FLAT && !RT_ONLY_BVH4H)
+// RT_SHADOW_PERLANE = 1 (A/B knob): the queued shadow rays walk the BVH per
+// lane (trace<true>, LDS stack) instead of as one wave packet -- the
+// BVH-walk frame measured 0.0411 vs 0.0333 ms (r05n: 102 VGPRs and 35 KB of
+// LDS per workgroup, 4 waves per SIMD instead of 5)
+#ifndef RT_SHADOW_PERLANE
+#define RT_SHADOW_PERLANE 0
+#endif
+#define RT_LANE_STACK (!RT_FLAT && (!RT_ONLY_BVH4H || RT_SHADOW_PERLANE))
 struct WaveLds {
 #if RT_LANE_STACK
   int32_t stack[RT_STACK_ROWS][64];
@@ -213,7 +220,7 @@ __device__ __forceinline__ void shadow_drain(bool final, const Scene& S, WaveLds
     // binary16 BVH4 as one packet, other layouts per lane (deep images)
     const bool occ = !RT_BVH_WALK && S.slist_on ? occluded_list(S, s, active, w.q_pid[slot], cnt)
                      : (RT_BVH8 && S.num_nodes8 > 0) ? occluded_packet8(S, s, active, w.q_pid[slot], 1.0f, cnt)
-                     : (RT_ONLY_BVH4H || (S.flags & RT_FLAG_BVH4H))
+                     : (!RT_SHADOW_PERLANE && (RT_ONLY_BVH4H || (S.flags & RT_FLAG_BVH4H)))
                          ? occluded_packet(S, s, active, w.q_pid[slot], 1.0f, cnt)
                          : active && trace<true>(S, s, 0.0f, 1.0f, w.q_pid[slot], tie_high, &ts,
                                                  RT_WSTACK(w, lane), cnt) >= 0;

@@ -926,9 +926,26 @@ __device__ __forceinline__ float xlowf(float v) { return __uint_as_float(xlow(__
 #ifndef RT_COOP_TOPREG
 #define RT_COOP_TOPREG 0
 #endif
+// a lane's half of a binary16 BVH4 node as loaded (RT_COOP_HALF_LOADS): the
+// planes of children 0-1 (lower lane) or 2-3 (upper) -- every other dword --
+// and the child refs, a pair
+struct CoopHalf {
+  uint32_t w[6];
+  uint2 cc;
+};
+__device__ __forceinline__ CoopHalf coop_half_load(const Scene& S, uint32_t ref, bool hi) {
+  const uint32_t no = S.nodes4 + 128u * S.num_nodes4 + 64u * ref;
+  const uint32_t hb = no + (hi ? 4u : 0u);
+  CoopHalf h;
+#pragma unroll
+  for (int i = 0; i < 6; ++i) h.w[i] = S.A.ld_u32(hb + 8u * i);
+  h.cc = S.A.ld_u2(no + 48u + (hi ? 8u : 0u));
+  return h;
+}
 template <bool SCALAR>
 __device__ __forceinline__ int32_t node4_coop(const Scene& S, uint32_t ref, const Ray& r, float lim,
-                                              bool hi, int32_t* mem, int& sp, int32_t& top) {
+                                              bool hi, int32_t* mem, int& sp, int32_t& top,
+                                              const CoopHalf* pre = nullptr) {
   auto ld = [&](uint32_t o) { return SCALAR ? S.A.sld_f4(o) : S.A.ld_f4(o); };
   const uint32_t no = S.nodes4 + 128u * S.num_nodes4 + 64u * ref;
   auto h2 = [](float w, float& a, float& b) {
@@ -939,15 +956,14 @@ __device__ __forceinline__ int32_t node4_coop(const Scene& S, uint32_t ref, cons
   float lx[2], hx[2], ly[2], hy[2], lz[2], hz[2];
   int32_t c[2];
   if (RT_COOP_HALF_LOADS && !SCALAR) {
-    // each lane loads only its half: the planes of children 0-1 (lower
-    // lane) or 2-3 (upper) are every other dword, the child refs a pair
-    const uint32_t hb = no + (hi ? 4u : 0u);
-    const auto f = [&](uint32_t o) { return __uint_as_float(S.A.ld_u32(hb + o)); };
-    const uint2 cc = S.A.ld_u2(no + 48u + (hi ? 8u : 0u));
-    h2(f(0), lx[0], lx[1]); h2(f(8), hx[0], hx[1]);
-    h2(f(16), ly[0], ly[1]); h2(f(24), hy[0], hy[1]);
-    h2(f(32), lz[0], lz[1]); h2(f(40), hz[0], hz[1]);
-    c[0] = (int32_t)cc.x; c[1] = (int32_t)cc.y;
+    // each lane loads only its half (or has it already: `pre`, loaded while
+    // the pair tested a leaf -- trace_coop RT_COOP_LEAF_PF)
+    const CoopHalf hh = pre ? *pre : coop_half_load(S, ref, hi);
+    const auto f = [&](int i) { return __uint_as_float(hh.w[i]); };
+    h2(f(0), lx[0], lx[1]); h2(f(1), hx[0], hx[1]);
+    h2(f(2), ly[0], ly[1]); h2(f(3), hy[0], hy[1]);
+    h2(f(4), lz[0], lz[1]); h2(f(5), hz[0], hz[1]);
+    c[0] = (int32_t)hh.cc.x; c[1] = (int32_t)hh.cc.y;
   } else {
     const float4 px = ld(no), py = ld(no + 16), pz = ld(no + 32), cf = ld(no + 48);
     h2(hi ? px.y : px.x, lx[0], lx[1]); h2(hi ? px.w : px.z, hx[0], hx[1]);
@@ -1049,6 +1065,16 @@ __device__ __forceinline__ int32_t node4_coop(const Scene& S, uint32_t ref, cons
   return (int32_t)xlow((uint32_t)c[0]);
 }
 
+// RT_COOP_LEAF_PF = 1: after a leaf round's triangle loads are issued the pair
+// pops the next stack entry and, when it is a node, issues that node's loads
+// too, before the triangle tests; the node's step then runs on those
+// registers (its slab tests still use the best hit after the leaf).  The
+// same visits in the same order: only the load latency overlaps the tests.
+// A/B r05n (config 4, median kernel ms): 0.11599 vs 0.11786.
+#ifndef RT_COOP_LEAF_PF
+#define RT_COOP_LEAF_PF 1
+#endif
+
 // trace<false> (closest hit from 0 below +inf, binary16 BVH4) by a lane pair;
 // both lanes return the hit and *t_out
 __device__ __forceinline__ int32_t trace_coop(const Scene& S, const Ray& r, int32_t skip, bool tie_high,
@@ -1072,6 +1098,10 @@ __device__ __forceinline__ int32_t trace_coop(const Scene& S, const Ray& r, int3
 #endif
     return true;
   };
+  int32_t nref = RT_EMPTY_REF;  // RT_COOP_LEAF_PF: the entry popped during a leaf round
+  bool pf = false;              // ... a node, whose loads are in `pre`
+  CoopHalf pre;
+  (void)nref; (void)pf; (void)pre;
   for (;;) {
     bool dry = false;
     {
@@ -1105,6 +1135,14 @@ __device__ __forceinline__ int32_t trace_coop(const Scene& S, const Ray& r, int3
         tb[k] = S.A.ld_f4(to + 48u * ks * k + 16);
         tc[k] = S.A.ld_f4(to + 48u * ks * k + 32);
       }
+#if RT_COOP_LEAF_PF && RT_COOP_HALF_LOADS && RT_COOP_LOCAL_SORT && RT_PUSH_UNCOND && !RT_COOP_TOPREG
+      // the next entry and, for a node, its loads -- in flight during the tests
+      const bool more = sp > 0;
+      nref = more ? mem[64 * (sp - 1)] : RT_EMPTY_REF;
+      sp = more ? sp - 1 : sp;
+      pf = more && nref >= 0;
+      if (pf) pre = coop_half_load(S, (uint32_t)nref, hi);
+#endif
 #if RT_COOP_LEAF_BF
       // both tests computed, the best taken by selects (no branches)
 #pragma unroll
@@ -1142,7 +1180,20 @@ __device__ __forceinline__ int32_t trace_coop(const Scene& S, const Ray& r, int3
         bpid = pb;
       }
     }
+#if RT_COOP_LEAF_PF && RT_COOP_HALF_LOADS && RT_COOP_LOCAL_SORT && RT_PUSH_UNCOND && !RT_COOP_TOPREG
+    if (nref == RT_EMPTY_REF) break;  // the stack was empty
+    ref = nref;
+    if (pf) {
+      // the popped node's step on the registers loaded during the tests
+      // (node4_coop's own step: the same visit, the same pushes)
+      RT_CNT(cnt.visits += hi ? 0u : 1u;)
+      const int32_t nx = node4_coop<false>(S, (uint32_t)ref, r, bt, hi, mem, sp, top, &pre);
+      if (nx != RT_EMPTY_REF) ref = nx;
+      else if (!pop(ref)) break;
+    }
+#else
     if (!pop(ref)) break;
+#endif
   }
   if (bpid >= 0) *t_out = bt;
   return bpid;
