@@ -1070,16 +1070,13 @@ __device__ __forceinline__ int32_t node4_coop(const Scene& S, uint32_t ref, cons
 // too, before the triangle tests; the node's step then runs on those
 // registers (its slab tests still use the best hit after the leaf).  The
 // same visits in the same order: only the load latency overlaps the tests.
-// A/B r05n (config 4, median kernel ms): 0.11599 vs 0.11786.
+// A/B r05n (config 4, median kernel ms): 0.11599 vs 0.11786.  (Reading the
+// stack's top before every node step, so an empty step pops without an LDS
+// round trip, measured neutral: r05o 0.11613 vs 0.11603, not kept; the same
+// leaf-round prefetch in the wave-packet walks of the BVH-walk image cost 44
+// SGPR spills and measured slower: r05p 0.0350 vs 0.03325, not kept.)
 #ifndef RT_COOP_LEAF_PF
 #define RT_COOP_LEAF_PF 1
-#endif
-
-// RT_COOP_SPEC_POP = 1: each node step reads the stack's top entry before it
-// runs, so a step whose node has no hit child pops without an LDS round trip
-// of its own (the same pop, the same order)
-#ifndef RT_COOP_SPEC_POP
-#define RT_COOP_SPEC_POP 1
 #endif
 
 // trace<false> (closest hit from 0 below +inf, binary16 BVH4) by a lane pair;
@@ -1116,20 +1113,9 @@ __device__ __forceinline__ int32_t trace_coop(const Scene& S, const Ray& r, int3
       while (ref >= 0) {  // while-while, as trace_impl
         RT_WAVE_ITER(9);
         RT_CNT(cnt.visits += hi ? 0u : 1u;)
-#if RT_COOP_SPEC_POP && RT_COOP_LOCAL_SORT && RT_PUSH_UNCOND && !RT_COOP_TOPREG
-        // the stack's top entry read before the step: a step that hits no
-        // child pushes nothing, so it is the entry the pop takes
-        const int32_t spec = mem[64 * (sp > 0 ? sp - 1 : RT_MAX_STACK)];
-        const int32_t nx = node4_coop<false>(S, (uint32_t)ref, r, bt, hi, mem, sp, top);
-        if (nx != RT_EMPTY_REF) { ref = nx; continue; }
-        if (sp == 0) { dry = true; break; }
-        ref = spec;
-        --sp;
-#else
         const int32_t nx = node4_coop<false>(S, (uint32_t)ref, r, bt, hi, mem, sp, top);
         if (nx != RT_EMPTY_REF) { ref = nx; continue; }
         if (!pop(ref)) { dry = true; break; }
-#endif
       }
       RT_CYC_END(11);
     }
