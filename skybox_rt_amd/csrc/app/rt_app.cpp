@@ -1460,8 +1460,13 @@ static int build_sah(rt_renderer_h r, rt_bvh_build_stats_t* st) {
   if (upload(r->dev, nullptr, nmax * (sizeof(rt_node4_t) + sizeof(rt_node4h_t)), &nodes4_h, &nodes4_addr))
     return -1;
   nodes4_out.h = nodes4_h;
-  if (upload(r->dev, nullptr, nmax * sizeof(rt_node8h_t), &nodes8_h, &nodes8_addr)) return -1;
-  nodes8_out.h = nodes8_h;
+  // the BVH8 collapse only when the BVH8 images may run (env RT_BVH8=1 when
+  // the tree is built): its four phases are a quarter of a rebuild's launches
+  const bool want8 = std::getenv("RT_BVH8") && std::atoi(std::getenv("RT_BVH8")) != 0;
+  if (want8) {
+    if (upload(r->dev, nullptr, nmax * sizeof(rt_node8h_t), &nodes8_h, &nodes8_addr)) return -1;
+    nodes8_out.h = nodes8_h;
+  }
   a.nodes8_addr = nodes8_addr;
   a.geom_addr = r->arg.geom_addr;
   a.nodes_addr = nodes_addr;
@@ -1522,9 +1527,10 @@ static int build_sah(rt_renderer_h r, rt_bvh_build_stats_t* st) {
     for (; L < lend; ++L) seq.push_back(SAH_SEQ(SAH_SPLIT, L));
     // the finishing phases carry level lend: on the device they do nothing
     // while that level still holds segments (a partial tree, bvh_sah.hip)
-    for (const uint32_t ph : {SAH_NUMBER, SAH_SCAN, SAH_EMIT, SAH_CS, SAH_MARK, SAH_SCAN4, SAH_EMIT4,
-                              SAH_CS8, SAH_MARK8, SAH_SCAN8, SAH_EMIT8})
+    for (const uint32_t ph : {SAH_NUMBER, SAH_SCAN, SAH_EMIT, SAH_CS, SAH_MARK, SAH_SCAN4, SAH_EMIT4})
       seq.push_back(SAH_SEQ(ph, lend));
+    if (want8)
+      for (const uint32_t ph : {SAH_CS8, SAH_MARK8, SAH_SCAN8, SAH_EMIT8}) seq.push_back(SAH_SEQ(ph, lend));
     const auto tr = std::chrono::steady_clock::now();
     if (run(seq) || vx_copy_from_dev(c, r->su.sah.h, ctl_off, sizeof(c)) != 0)
       return fail("SAH build: launch or read-back failed");
@@ -1551,7 +1557,7 @@ static int build_sah(rt_renderer_h r, rt_bvh_build_stats_t* st) {
   r->nodes8 = nodes8_out.h;
   nodes_out.h = tris_out.h = nodes4_out.h = nodes8_out.h = nullptr;
   // the BVH8 for the BVH8 images when its stack fits them
-  const uint32_t nn8 = c[SAH_CTL_NODES8], stack8 = c[SAH_CTL_STACK8];
+  const uint32_t nn8 = want8 ? c[SAH_CTL_NODES8] : 0u, stack8 = want8 ? c[SAH_CTL_STACK8] : 0u;
   r->num_nodes8_built = nn8;
   r->arg.nodes8_addr = nodes8_addr;
   r->arg.num_nodes8 = stack8 <= RT_STACK_SHALLOW ? nn8 : 0u;
@@ -1574,7 +1580,7 @@ static int build_sah(rt_renderer_h r, rt_bvh_build_stats_t* st) {
     st->nodes4 = nn4;
     st->depth4 = c[SAH_CTL_DEPTH4];
     st->nodes8 = nn8;
-    st->depth8 = c[SAH_CTL_DEPTH8];
+    st->depth8 = want8 ? c[SAH_CTL_DEPTH8] : 0u;
     st->stack8 = stack8;
     st->method = RT_BVH_BUILD_SAH;
   }

@@ -41,6 +41,21 @@ def _host_renderer(s):
     return r
 
 
+class _bvh8_env:
+    """RT_BVH8=1 while a renderer builds its tree: the device SAH build then
+    also emits the BVH8 collapse (4 more finishing launches)."""
+
+    def __enter__(self):
+        self.old = os.environ.get("RT_BVH8")
+        os.environ["RT_BVH8"] = "1"
+
+    def __exit__(self, *exc):
+        if self.old is None:
+            del os.environ["RT_BVH8"]
+        else:
+            os.environ["RT_BVH8"] = self.old
+
+
 def _scene(name, tmp_path_factory):
     if name in _paths:
         return _paths[name]
@@ -69,8 +84,9 @@ def test_gpu_sah_equals_host_build(tmp_path_factory, name):
     hn, ht = host.export_bvh()
     h4, hh = host.export_bvh4(), host.export_bvh4h()
     h8 = host.export_bvh8h()
-    r = rt.Renderer(s)
-    st = r.build_bvh("sah")
+    with _bvh8_env():
+        r = rt.Renderer(s)
+        st = r.build_bvh("sah")
     dn, dt = r.export_bvh()
     assert dn.shape == hn.shape and np.array_equal(dn.view(np.uint32), hn.view(np.uint32))
     assert dt.shape == ht.shape and np.array_equal(dt.view(np.uint32), ht.view(np.uint32))
@@ -86,8 +102,8 @@ def test_gpu_sah_equals_host_build(tmp_path_factory, name):
     assert st["nodes4"] == info["bvh4_nodes"] and st["depth4"] == info["bvh4_depth"]
     assert st["stack4"] == info["bvh4_stack"] and st["method"] == 1
     # one sequence: the init, the level budget's split launches, 11 finishing
-    # launches (BVH2, BVH4, BVH8) -- and, past the budget, a reset, the next
-    # levels, 11 again
+    # launches (BVH2, BVH4, BVH8 under RT_BVH8) -- and, past the budget, a
+    # reset, the next levels, 11 again
     budget = math.ceil(math.log2(info["num_geometry"] + 1)) + 4
     rounds = 1 if info["bvh_depth"] <= budget else 2
     assert st["launches"] == 1 + min(rounds * budget, 63) + 11 * rounds + (rounds - 1)
@@ -143,9 +159,11 @@ def test_gpu_sah_deep_tree_on_stale_scratch(tmp_path_factory):
     hn, ht = host.export_bvh()
     h4, hh = host.export_bvh4(), host.export_bvh4h()
     h8 = host.export_bvh8h()
-    r = rt.Renderer(s)
+    with _bvh8_env():
+        r = rt.Renderer(s)
     for _ in range(2):
-        st = r.build_bvh("sah")
+        with _bvh8_env():
+            st = r.build_bvh("sah")
         dn, dt = r.export_bvh()
         assert np.array_equal(dn.view(np.uint32), hn.view(np.uint32))
         assert np.array_equal(dt.view(np.uint32), ht.view(np.uint32))
@@ -177,5 +195,8 @@ def test_gpu_sah_rebuild(tmp_path_factory):
     print(f"tekkaman SAH build: first {first['build_ms']:.3f} ms, rebuilds {[round(t, 3) for t in times]} ms, "
           f"{st['launches']} launches")
     assert min(times) < 1.0
+    # without RT_BVH8 the build stops at the BVH4: 7 finishing launches, no BVH8
+    budget = math.ceil(math.log2(s.info()["num_geometry"] + 1)) + 4
+    assert st["launches"] == 1 + budget + 7 and st["nodes8"] == 0 and r.export_bvh8h().shape[0] == 0
     r.close()
     s.close()

@@ -84,12 +84,16 @@ def test_bvh8_shadow_packets_equal_oracle_with_counts(oracle_lib, name, w, h):
     (oracle/rt.c bvh8_step); the frame equals the BVH4 image's."""
     po = oracle_lib
     s = rt.Scene.load(scene_path(name))
-    r = rt.Renderer(s)
-    r.configure(w, h, shadows=True, counters=False, bvh_walk=True)
-    r.render()
-    fb4 = r.framebuffer()
+    r4 = rt.Renderer(s)
+    r4.configure(w, h, shadows=True, counters=False, bvh_walk=True)
+    r4.render()
+    fb4 = r4.framebuffer()
+    r4.close()
+    # RT_BVH8=1 when the renderer builds its tree (the device SAH build then
+    # emits the BVH8) and when it is configured (the BVH8 images run)
     os.environ["RT_BVH8"] = "1"
     try:
+        r = rt.Renderer(s)
         r.configure(w, h, shadows=True, instrumented=True, bvh_walk=True)
         # a tree whose BVH8 walk could need more than the 24-entry stack
         # (scene: 27) keeps the BVH4 images (rt_app.cpp use_bvh8)

@@ -168,12 +168,16 @@ def test_pt_kernel8_bit_exact_vs_oracle_with_counts(po, name, size, bounces):
     (oracle/rt.c bvh8_step); the frame equals the BVH4 image's."""
     import os
     s, _, osc, bvh = setup(po, name)
-    r = rt.Renderer(s)  # fresh: a BVH2 frame on the cached one loaded the deep images for good
-    r.configure(size, size, path=True, bounces=bounces, counters=False)
-    r.render()
-    fb4 = r.framebuffer()
+    r4 = rt.Renderer(s)  # fresh: a BVH2 frame on the cached one loaded the deep images for good
+    r4.configure(size, size, path=True, bounces=bounces, counters=False)
+    r4.render()
+    fb4 = r4.framebuffer()
+    r4.close()
+    # RT_BVH8=1 when the renderer builds its tree (the device SAH build then
+    # emits the BVH8) and when it is configured (pt_kernel8 runs)
     os.environ["RT_BVH8"] = "1"
     try:
+        r = rt.Renderer(s)
         r.configure(size, size, path=True, bounces=bounces, instrumented=True)
         # past the 24-entry stack (scene's BVH8: 27) the BVH4 image stays
         on = s.info()["bvh8_stack"] <= 24
