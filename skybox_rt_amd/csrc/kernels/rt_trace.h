@@ -1074,7 +1074,9 @@ __device__ __forceinline__ int32_t node4_coop(const Scene& S, uint32_t ref, cons
 // stack's top before every node step, so an empty step pops without an LDS
 // round trip, measured neutral: r05o 0.11613 vs 0.11603, not kept; the same
 // leaf-round prefetch in the wave-packet walks of the BVH-walk image cost 44
-// SGPR spills and measured slower: r05p 0.0350 vs 0.03325, not kept.)
+// SGPR spills and measured slower: r05p 0.0350 vs 0.03325, not kept; so did
+// a branch-free push of the packet walks' children -- every slot written,
+// sp advanced by the push bit: r05s 0.03414 vs 0.03326, not kept.)
 #ifndef RT_COOP_LEAF_PF
 #define RT_COOP_LEAF_PF 1
 #endif
