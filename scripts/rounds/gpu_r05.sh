@@ -2,6 +2,7 @@
 # failure ends the call; TAG names the outputs under gpurun_out/.
 #   tests   pytest -m gpu (FILES= to restrict to some test files)
 #   bench   python bench.py --workload W $BENCH_ARGS for W in WORKLOADS (-> ${TAG}_bench_W.json)
+#   smoke   __graft_entry__.smoke()
 #   host    scripts/host_overhead.py (start / wait / kernel split of a synchronous frame)
 #   ab      scripts/gpu_ab.sh with AB_SHADOW / AB_PATH / AB_FLAT variant lists
 #   prof    rocprofv3 --kernel-trace --stats of bench.py --workload W --no-cpu-baseline $BENCH_ARGS
@@ -23,6 +24,9 @@ for s in ${STEPS:-tests bench}; do
           2> gpurun_out/${T}_bench_$w.err || { tail -5 gpurun_out/${T}_bench_$w.err; exit 1; }
         python3 -c "import json;j=json.load(open('gpurun_out/${T}_bench_$w.json'));c=j['config'];print('$w',j['value'],j['ms_per_step'],c['kernel_ms'],c.get('sync_ms_per_step'),j['roofline']['frac'])"
       done ;;
+    smoke)
+      timeout -k 10 300 python -c 'import __graft_entry__ as g; g.smoke()' > gpurun_out/${T}_smoke.log 2>&1 \
+        || { tail -5 gpurun_out/${T}_smoke.log; exit 1; }; tail -1 gpurun_out/${T}_smoke.log ;;
     host)
       timeout -k 10 120 python scripts/host_overhead.py > gpurun_out/${T}_host.json 2> gpurun_out/${T}_host.err \
         || { tail -5 gpurun_out/${T}_host.err; exit 1; }; cat gpurun_out/${T}_host.json ;;
