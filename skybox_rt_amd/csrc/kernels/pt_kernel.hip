@@ -335,8 +335,7 @@ __device__ __forceinline__ bool path_step(const Scene& S, int32_t* stack, PathSt
     cnt.bounce += one;
     np = CO == 2 ? trace_quad(S, b, st.pid, tie_high, &nt, stack, role, cnt)
          : CO == 1 ? (RT_BVH8 ? trace_coop8(S, b, st.pid, tie_high, &nt, stack, hi, cnt)
-                              : RT_COOP_2CUR ? trace_coop2(S, b, st.pid, tie_high, &nt, stack, hi, cnt)
-                                             : trace_coop(S, b, st.pid, tie_high, &nt, stack, hi, cnt))
+                              : trace_coop(S, b, st.pid, tie_high, &nt, stack, hi, cnt))
                    : trace<false>(S, b, 0.0f, INFINITY, st.pid, tie_high, &nt, stack, cnt);
     if (np < 0) {
 #pragma unroll

@@ -1076,7 +1076,10 @@ __device__ __forceinline__ int32_t node4_coop(const Scene& S, uint32_t ref, cons
 // leaf-round prefetch in the wave-packet walks of the BVH-walk image cost 44
 // SGPR spills and measured slower: r05p 0.0350 vs 0.03325, not kept; so did
 // a branch-free push of the packet walks' children -- every slot written,
-// sp advanced by the push bit: r05s 0.03414 vs 0.03326, not kept.)
+// sp advanced by the push bit: r05s 0.03414 vs 0.03326, not kept; and two
+// cursors per ray -- each lane of the pair a whole node or leaf from one
+// shared stack, the pair's best merged every iteration (same frames, more
+// visits): r05v 0.12505 vs 0.11556, not kept.)
 #ifndef RT_COOP_LEAF_PF
 #define RT_COOP_LEAF_PF 1
 #endif
@@ -1200,127 +1203,6 @@ __device__ __forceinline__ int32_t trace_coop(const Scene& S, const Ray& r, int3
 #else
     if (!pop(ref)) break;
 #endif
-  }
-  if (bpid >= 0) *t_out = bt;
-  return bpid;
-}
-
-// RT_COOP_2CUR = 1 (A/B knob): the pair walks with two cursors -- each lane
-// takes a whole node (four slab tests, the local sort) or a whole leaf from
-// one shared stack, instead of both lanes splitting one node or leaf two and
-// two.  The pair's best hit is merged every iteration and culls both
-// cursors, so the nearest hit is the same (closer() is a strict total order
-// and no box that holds it is ever culled); the visits differ.  The stack is
-// the pair's two LDS columns interleaved (logical row r: column r & 1, row
-// r >> 1), twice the one-cursor depth.
-#ifndef RT_COOP_2CUR
-#define RT_COOP_2CUR 0
-#endif
-static_assert(!RT_COOP_2CUR || RT_PAIR_ADJ, "two cursors use the pair's adjacent stack columns");
-__device__ __forceinline__ int32_t* c2row(int32_t* mem, int r) { return mem + 64 * (r >> 1) + (r & 1); }
-__device__ __forceinline__ int32_t trace_coop2(const Scene& S, const Ray& r, int32_t skip, bool tie_high,
-                                               float* t_out, int32_t* mem, bool hi, Counters& cnt) {
-  if (S.num_nodes == 0) return -1;
-  constexpr int CAP = 2 * RT_MAX_STACK;  // rows CAP.. (slack) absorb dropped pushes
-  float bt = INFINITY;
-  int32_t bpid = -1;
-  int sp = 0;
-  int32_t ref = hi ? RT_EMPTY_REF : 0;  // the lower lane starts at the root
-  auto h2 = [](float w, float& a, float& b) {
-    const uint32_t u = __float_as_uint(w);
-    a = (float)__builtin_bit_cast(_Float16, (uint16_t)(u & 0xffffu));
-    b = (float)__builtin_bit_cast(_Float16, (uint16_t)(u >> 16));
-  };
-  for (;;) {
-    const bool idle = ref == RT_EMPTY_REF;
-    if (idle && xpart(idle ? 1u : 0u, hi) != 0u && sp == 0) break;  // both cursors done
-    RT_WAVE_ITER(9);
-    float K[4];
-    int32_t C[4] = {RT_EMPTY_REF, RT_EMPTY_REF, RT_EMPTY_REF, RT_EMPTY_REF};
-    int n = 0;
-    if (ref >= 0) {
-      RT_CNT(++cnt.visits;)
-      const uint32_t no = S.nodes4 + 128u * S.num_nodes4 + 64u * (uint32_t)ref;
-      const float4 px = S.A.ld_f4(no), py = S.A.ld_f4(no + 16), pz = S.A.ld_f4(no + 32), cf = S.A.ld_f4(no + 48);
-      float lx[4], hx[4], ly[4], hy[4], lz[4], hz[4];
-      h2(px.x, lx[0], lx[1]); h2(px.y, lx[2], lx[3]); h2(px.z, hx[0], hx[1]); h2(px.w, hx[2], hx[3]);
-      h2(py.x, ly[0], ly[1]); h2(py.y, ly[2], ly[3]); h2(py.z, hy[0], hy[1]); h2(py.w, hy[2], hy[3]);
-      h2(pz.x, lz[0], lz[1]); h2(pz.y, lz[2], lz[3]); h2(pz.z, hz[0], hz[1]); h2(pz.w, hz[2], hz[3]);
-      const int32_t cc[4] = {__float_as_int(cf.x), __float_as_int(cf.y), __float_as_int(cf.z),
-                             __float_as_int(cf.w)};
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        float tn = 0.0f;
-        const bool h = slab(lx[i], hx[i], ly[i], hy[i], lz[i], hz[i], r, 0.0f, bt, &tn) &
-                       (cc[i] != RT_EMPTY_REF);
-        K[i] = h ? fminf(tn, 3.402823466e38f) : __builtin_inff();
-        C[i] = cc[i];
-        n += h ? 1 : 0;
-      }
-      auto cx = [&](int a, int b) {  // node4_step's compare-exchange: swap iff K[b] < K[a]
-        const bool sw = K[b] < K[a];
-        const float ka = K[a], kb = K[b];
-        const int32_t ca = C[a], cb = C[b];
-        K[a] = sw ? kb : ka; K[b] = sw ? ka : kb;
-        C[a] = sw ? cb : ca; C[b] = sw ? ca : cb;
-      };
-      cx(0, 1); cx(2, 3); cx(0, 2); cx(1, 3); cx(1, 2);
-    } else if (ref != RT_EMPTY_REF) {
-      const uint32_t lr = (uint32_t)ref;
-      const uint32_t first = (lr >> 4) & 0x07ffffffu, count = (lr & 15u) + 1u;
-      const uint32_t to = S.tris + 48u * first;
-      float4 ta[4], tb[4], tc[4];
-#pragma unroll
-      for (uint32_t k = 0; k < 4; ++k) {  // padding records past the end
-        ta[k] = S.A.ld_f4(to + 48u * k);
-        tb[k] = S.A.ld_f4(to + 48u * k + 16);
-        tc[k] = S.A.ld_f4(to + 48u * k + 32);
-      }
-#pragma unroll
-      for (uint32_t k = 0; k < 4; ++k) {
-        if (k < count) {
-          const int32_t pid = __float_as_int(ta[k].w);
-          RT_CNT(++cnt.tests;)
-          float t;
-          if (pid != skip && mt_hit(r, ta[k], tb[k], tc[k], 0.0f, &t) && closer(t, pid, bt, bpid, tie_high)) {
-            bt = t;
-            bpid = pid;
-          }
-        }
-      }
-    }
-    {  // the pair's best
-      const float pbt = xpartf(bt, hi);
-      const int32_t pb = (int32_t)xpart((uint32_t)bpid, hi);
-      if (pb >= 0 && closer(pbt, pb, bt, bpid, tie_high)) {
-        bt = pbt;
-        bpid = pb;
-      }
-    }
-    // pushes (the lower lane's run first): a node with hits goes on at C[0]
-    // and pushes C[1..n-1], C[1] on top of its run
-    const int np = n > 1 ? n - 1 : 0;
-    const int pnp = (int)xpart((uint32_t)np, hi);
-    const int base = sp + (hi ? pnp : 0);
-#pragma unroll
-    for (int j = 1; j < 4; ++j) {
-      if (j <= np) {
-        const int rr = base + np - j;
-        *c2row(mem, rr < CAP ? rr : CAP) = C[j];
-      }
-    }
-    sp = min(sp + np + pnp, CAP);
-    // the cursors without a next node pop, the lower lane first
-    int32_t nxt = n > 0 ? C[0] : RT_EMPTY_REF;
-    const bool want = n == 0;
-    const bool pwant = xpart(want ? 1u : 0u, hi) != 0u;
-    const bool lw = hi ? pwant : want, uw = hi ? want : pwant;
-    const int lp = (lw && sp > 0) ? 1 : 0;
-    const int up = (uw && sp - lp > 0) ? 1 : 0;
-    const int row = hi ? sp - 1 - lp : sp - 1;
-    if (want && (hi ? up : lp)) nxt = *c2row(mem, row);
-    sp -= lp + up;
-    ref = nxt;
   }
   if (bpid >= 0) *t_out = bt;
   return bpid;
