@@ -428,8 +428,15 @@ class Run:
                 t0 = time.perf_counter()
                 for _ in range(steps):
                     self.step(render, exchange)
-                self.drain()  # every frame rendered (and gathered + assembled) inside the region
+                # every frame rendered (and gathered + assembled) inside the
+                # region: the device synchronize first (it returns when the
+                # driver's stream is idle), then the driver's and the
+                # exchange's bookkeeping (instant for frames already done;
+                # host-staged gathers still block here)
                 torch.cuda.synchronize()
+                self.drain()
+                if self.fg is not None:
+                    torch.cuda.synchronize()
                 if dist is not None:
                     dist.barrier()
                 elapsed = time.perf_counter() - t0
