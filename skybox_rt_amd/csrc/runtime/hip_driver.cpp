@@ -743,6 +743,8 @@ class vx_device {
   std::map<uint64_t, uint64_t> image_key_;  // image address -> module key
   hipStream_t stream_ = nullptr;
   static constexpr int kMaxQueue = 64;  // >= (depth_ + time_every_) * group_n_
+  static_assert(kHostMemApp + (uint64_t)kMaxQueue * kTailSlot <= kHostMemBytes,
+                "a completion slot per queue slot in the pinned block");
   static_assert(kMaxQueue == 64, "tail_ / tail_nonce_slot_ are sized by it");
   static_assert(kHostMemApp + kMaxQueue * kTailSlot <= kHostMemBytes, "completion slots fit");
   hipEvent_t ev_start_[kMaxQueue] = {}, ev_stop_[kMaxQueue] = {};
