@@ -633,8 +633,9 @@ def main():
         e_x, _ = reduce_max_sum(dist, coll_dev, e_x, 0)
         split = {"steps": split_steps, "render_ms_per_step": round(e_r / split_steps * 1e3, 5),
                  "exchange_ms_per_step": round(e_x / split_steps * 1e3, 5),
-                 "exchange": "torch.distributed gather (RCCL) of the compact tile buffers + "
-                             "rt_frame_assemble on rank 0, pipelined over 4 slots"}
+                 "exchange": (f"torch.distributed gather ({'RCCL' if backend == 'nccl' else backend}) "
+                              f"of the compact tile buffers + rt_frame_assemble on rank 0, "
+                              f"pipelined over 4 slots")}
     gather_ok = None
     if use_gather and args.verify_gather:
         image = run.fg.image.cpu().numpy() if rank == 0 else None
