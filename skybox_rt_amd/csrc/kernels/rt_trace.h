@@ -1079,7 +1079,9 @@ __device__ __forceinline__ int32_t node4_coop(const Scene& S, uint32_t ref, cons
 // sp advanced by the push bit: r05s 0.03414 vs 0.03326, not kept; and two
 // cursors per ray -- each lane of the pair a whole node or leaf from one
 // shared stack, the pair's best merged every iteration (same frames, more
-// visits): r05v 0.12505 vs 0.11556, not kept.)
+// visits): r05v 0.12505 vs 0.11556, not kept; nor the BVH4 staged in LDS
+// by every pair-walking wave, the halves read from there: r05af 0.12778 vs
+// 0.11769 -- the copy and the lower occupancy cost more than L1 hits save.)
 #ifndef RT_COOP_LEAF_PF
 #define RT_COOP_LEAF_PF 1
 #endif
