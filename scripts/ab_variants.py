@@ -15,6 +15,7 @@ import argparse
 import json
 import os
 import sys
+import time
 
 import numpy as np
 
@@ -77,6 +78,7 @@ def main():
         names.append(label)
     times = {n: [] for n in names}
     sync = {n: [] for n in names}
+    host = {n: [] for n in names}
     for _ in range(args.rounds):
         for n in names:
             r = rs[n]
@@ -86,8 +88,13 @@ def main():
             for _ in range(3):  # and a synchronous frame's device time (completion stamps)
                 r.render()
                 sync[n].append(r.kernel_ms())
+            t0 = time.perf_counter()  # the host's view of 10 synchronous frames (start + wait)
+            for _ in range(10):
+                r.render()
+            host[n].append((time.perf_counter() - t0) / 10 * 1e3)
     out = {n: {"median_ms": round(float(np.median(t)), 5), "min_ms": round(float(np.min(t)), 5),
                "sync_median_ms": round(float(np.median(sync[n])), 5),
+               "sync_host_median_ms": round(float(np.median(host[n])), 5),
                "grid": rs[n].stats()["grid"]} for n, t in times.items()}
     print(json.dumps(out))
 
