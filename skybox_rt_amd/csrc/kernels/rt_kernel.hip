@@ -249,9 +249,17 @@ __device__ __forceinline__ void shadow_drain(bool final, const Scene& S, WaveLds
 // list order found by a min over the waves' first hits (which is also
 // brute_trace's test count).
 constexpr int kFlatUnroll = 8;  // rectangle words in flight at once
+// RT_FLAT_EARLY_OUT (no shadow rays): waves 1.. leave the chunk once their
+// winners are in LDS and wave 0 shades and stores with no second barrier --
+// the winners double-buffered by chunk parity, so a wave's next chunk never
+// overwrites words wave 0 is still reducing (it must pass the next chunk's
+// barrier, which wave 0 reaches only after its reduction)
+#ifndef RT_FLAT_EARLY_OUT
+#define RT_FLAT_EARLY_OUT 1
+#endif
 struct FlatLds {
-  uint32_t z[kWaves][64];
-  int32_t pid[kWaves][64];
+  uint32_t z[1 + RT_FLAT_EARLY_OUT][kWaves][64];
+  int32_t pid[1 + RT_FLAT_EARLY_OUT][kWaves][64];
   uint32_t first[kWaves][64];
 };
 
@@ -273,8 +281,10 @@ __device__ __forceinline__ uint4 flat_rec(const Scene& S, const uint4* lds, uint
 }
 
 __device__ __forceinline__ void flat_chunk(const vx_task_t& task, bool valid, const Scene& S,
-                                           FlatLds& L, Counters& cnt) {
+                                           FlatLds& L, uint32_t& par, Counters& cnt) {
   const uint32_t w = threadIdx.x >> 6, lane = lane_id();
+  const uint32_t pb = RT_FLAT_EARLY_OUT ? par : 0u;  // this chunk's winner buffer
+  par ^= 1u;
   const uint32_t t = task.blockIdx.x;
   uint32_t x = 0, y = 0, out = 0;
   if (valid) {
@@ -427,18 +437,20 @@ __device__ __forceinline__ void flat_chunk(const vx_task_t& task, bool valid, co
 #ifdef RT_STAMPS  // 3: wave 0's list scan done, 4: the slowest wave's (after the barrier)
   if (threadIdx.x == 0) __vx_mpm_lds[3] = (uint32_t)__builtin_amdgcn_s_memrealtime();
 #endif
-  L.z[w][lane] = bz;
-  L.pid[w][lane] = bp;
+  L.z[pb][w][lane] = bz;
+  L.pid[pb][w][lane] = bp;
   __syncthreads();
 #ifdef RT_STAMPS
   if (threadIdx.x == 0) __vx_mpm_lds[4] = (uint32_t)__builtin_amdgcn_s_memrealtime();
 #endif
+  const bool early = RT_FLAT_EARLY_OUT && (S.flags & RT_FLAG_SHADOWS) == 0;  // block-uniform
+  if (early && w != 0) return;
   int32_t hit = -1;
   uint32_t hz = VX_OM_DEPTH_MASK;
   for (uint32_t i = 0; i < kWaves; ++i) {
-    const int32_t p = L.pid[i][lane];
-    if (p >= 0 && vis_better(L.z[i][lane], p, hz, hit, tie_high)) {
-      hz = L.z[i][lane];
+    const int32_t p = L.pid[pb][i][lane];
+    if (p >= 0 && vis_better(L.z[pb][i][lane], p, hz, hit, tie_high)) {
+      hz = L.z[pb][i][lane];
       hit = p;
     }
   }
@@ -452,6 +464,10 @@ __device__ __forceinline__ void flat_chunk(const vx_task_t& task, bool valid, co
     asm volatile("" : : "v"(color));  // the colour is complete before the stamp
     if (threadIdx.x == 0) __vx_mpm_lds[5] = (uint32_t)__builtin_amdgcn_s_memrealtime();
 #endif
+  }
+  if (early) {  // wave 0 only: no shadow rays, no second barrier
+    if (in) store_out(S, out, color);
+    return;
   }
   Ray r;
   primary_dir(S, x, y, r);
@@ -543,9 +559,10 @@ VX_MAIN(rt_kernel_arg_t, arg, RT_BLOCK_THREADS) {
 #endif
   __shared__ FlatLds s_flat;
   (void)w;
+  uint32_t par = 0;
   const int rc = vx_spawn_chunks_block(
       S.num_tasks,
-      [&](const vx_task_t& task, bool valid, const Scene* s) { flat_chunk(task, valid, *s, s_flat, cnt); },
+      [&](const vx_task_t& task, bool valid, const Scene* s) { flat_chunk(task, valid, *s, s_flat, par, cnt); },
       &S);
 #else
   if ((threadIdx.x & 63u) == 0) w.q_count = 0;
