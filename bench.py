@@ -598,10 +598,15 @@ def main():
     alg_bytes = algorithmic_bytes(inst, inst["primary_rays"], (NODE4H_BYTES if r.bvh4_f16 else NODE4_BYTES)
                                   if r.bvh4 else NODE_BYTES)
     # synchronous frames first (start + wait per frame, simx's blocking
-    # start): reported beside the pipelined rate, not as `value`
+    # start): reported beside the pipelined rate, not as `value`.  200 frames
+    # (~5 ms) whatever --steps is: a steadier figure than a few frames, and
+    # the device reaches its working clocks before the timed region instead
+    # of inside it (at the driver's --steps 20 --warmup 5: 62.3-62.5 Grays/s
+    # after 20 of them, 64.2-64.3 after 200 -- DESIGN 6, r05at)
     sync_ms = None
+    sync_n = 0
     if not use_gather:
-        sync_n = max(5, min(args.steps, 50))
+        sync_n = int(os.environ.get("BENCH_SYNC_FRAMES", "0")) or 200
         for _ in range(2):
             r.render()
         t_s = time.perf_counter()
@@ -828,6 +833,8 @@ def main():
                       f"stream around {max(50, min(args.steps, 1000))} such frames after the "
                       "timed region / frames (render only)",
             "sync_ms_per_step": round(sync_ms, 5) if sync_ms is not None else None,
+            "sync_frames": (f"{sync_n} synchronous frames (vx_start + vx_ready_wait each), host "
+                            "clock, before the timed region") if sync_ms is not None else None,
             "kernel_mrays_per_s": round(run.rays_local / (avg_kernel_ms * 1e-3) / 1e6, 3),
             "counters": "off in the timed frames (rays per frame from the instrumented pre-run)",
         },
