@@ -28,7 +28,11 @@ def po(oracle_lib):
 
 @pytest.mark.parametrize("name,size,shadows", [("tekkaman", 256, False), ("tekkaman", 256, True),
                                                ("tekkaman", 100, True), ("triangle", 64, False),
-                                               ("box", 128, True), ("scene", 128, True)])
+                                               ("box", 128, True), ("scene", 128, True),
+                                               # more chunks than workgroups: each workgroup runs
+                                               # several chunks (the winner words' chunk-parity
+                                               # double buffer of the no-shadow early out)
+                                               ("tekkaman", 512, False), ("scene", 384, True)])
 def test_flat_bit_exact_vs_oracle_bruteforce(po, name, size, shadows):
     _, r, osc = setup(po, name)
     c, _, _, k = po.rt_render(osc, po.rt_params(size, size, shadows=shadows, nthreads=8))
