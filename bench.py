@@ -743,7 +743,9 @@ def main():
                     f"list -- a 512-thread workgroup per 64-pixel chunk splits the list 8 ways, each "
                     f"wave tests 64 rectangle words per instruction (read from L2) against the "
                     f"chunk's 8x8 block, then the entries reaching it per pixel (exact edge + depth "
-                    f"test, records through the scalar cache)")
+                    f"test, records through the scalar cache); the waves' winners meet in LDS and "
+                    f"wave 0 shades and stores the chunk (no shadow rays: the other waves leave "
+                    f"at the barrier)")
     elif path and setup_st.get("path_queue"):
         shadow_how = ("light-space shadow lists" if setup_st["slist_on"] else f"{bvh_kind} walk")
         workload = (f"{side}x{side} {kind}, tekkaman.cgltrace, two kernels per frame: {primary}, "
