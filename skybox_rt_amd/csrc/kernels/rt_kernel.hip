@@ -109,12 +109,6 @@ __shared__ uint4 s_geom[RT_FLAT_CAP];
 #ifndef RT_FLAT_SCALAR
 #define RT_FLAT_SCALAR 1
 #endif
-// RT_FLAT_VREC: the block test's candidates load their whole records as
-// vector loads, one round for the 64 entries, and each candidate is then
-// broadcast from its lane (v_readlane) -- no scalar-load round trip per pair
-#ifndef RT_FLAT_VREC
-#define RT_FLAT_VREC 0
-#endif
 __device__ __forceinline__ const uint4* flat_list(const Scene& S) {
   return !RT_FLAT_SCALAR && S.num_geom <= RT_FLAT_CAP ? s_geom : nullptr;
 }
@@ -332,35 +326,7 @@ __device__ __forceinline__ void flat_chunk(const vx_task_t& task, bool valid, co
 #ifdef RT_INSTRUMENT
       cnt.rect_tests += lane == 0 ? (mine - i < 64u ? mine - i : 64u) : 0u;
 #endif
-#if RT_FLAT_VREC
-      uint4 vr[4];
-      if (ov) {
-        const uint32_t o = S.vgeom + 64u * ((i + lane) * kWaves + w);
-#pragma unroll
-        for (int q = 0; q < 4; ++q) vr[q] = S.A.ld_u4(o + 16u * q);
-      }
       while (m != 0) {
-        const int j = (int)__builtin_ctzll(m);
-        m &= m - 1;
-        uint4 rc[4];
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          rc[q].x = (uint32_t)__builtin_amdgcn_readlane((int)vr[q].x, j);
-          rc[q].y = (uint32_t)__builtin_amdgcn_readlane((int)vr[q].y, j);
-          rc[q].z = (uint32_t)__builtin_amdgcn_readlane((int)vr[q].z, j);
-          rc[q].w = (uint32_t)__builtin_amdgcn_readlane((int)vr[q].w, j);
-        }
-        const uint4 Cc = rect_corners(rc[2]);
-        const bool inc = rect2_in(Cc.y, Cc.z, pp);
-        if (__ballot(inc) != 0) {  // wave-uniform
-#ifdef RT_INSTRUMENT
-          cnt.edge_tests += lane == 0 ? 1u : 0u;
-#endif
-          vis_test_in(rc[0], rc[1], rc[2], rc[3], inc, px, y, tie_high, bz, bp);
-        }
-      }
-#endif
-      while (!RT_FLAT_VREC && m != 0) {
         const uint32_t j0 = (uint32_t)__builtin_ctzll(m);
         m &= m - 1;
         const bool two = m != 0;
