@@ -28,3 +28,40 @@ def test_round_end_roofline_recomputes(workload):
     assert "timed dispatches" in out.get("rocprof_avg_of", ""), out
     line = json.load(open(bench))
     assert abs(out["rocprof_avg_ms"] - line["config"]["kernel_ms"]) <= 0.05 * line["config"]["kernel_ms"]
+
+
+def test_timed_region_picks_the_timed_dispatches(tmp_path):
+    """check_roofline.timed_region on a synthetic trace: sync frames (each
+    followed by the completion kernel), the warmup, a ~1 ms gap, the timed
+    frames with one host stall inside, a gap, the kernel-clock frames, then a
+    series of slower frames with setup launches between -- the average is the
+    timed frames' only."""
+    sys.path.insert(0, os.path.join(ROOT, "scripts"))
+    import check_roofline as cr
+    rows, t = [], 0
+
+    def k(name, dur, gap=0):
+        nonlocal t
+        t += gap
+        rows.append((t, t + dur, name))
+        t += dur
+
+    for _ in range(5):
+        k("vx_main_rt_kernel", 18000, 9000)
+        k("vx_main_rt_kernel_done", 1000)
+    for _ in range(5):
+        k("vx_main_rt_kernel", 17000, 500)
+    for i in range(20):
+        k("vx_main_rt_kernel", 16000, 1_000_000 if i == 0 else (40_000 if i == 7 else 0))
+    for i in range(10):
+        k("vx_main_rt_kernel", 16500, 130_000 if i == 0 else 0)
+    for _ in range(5):
+        k("vx_main_rt_setup", 2000, 1000)
+        k("vx_main_rt_kernel", 18000)
+    p = tmp_path / "trace.csv"
+    with open(p, "w") as f:
+        f.write('"Kernel_Name","Start_Timestamp","End_Timestamp"\n')
+        for st, en, nm in rows:
+            f.write(f'"{nm}",{st},{en}\n')
+    assert abs(cr.timed_region(str(p), "vx_main_rt_kernel", 20) - 16e-6) < 1e-12
+    assert cr.timed_region(str(p), "vx_main_rt_kernel", 50) is None
