@@ -7,7 +7,7 @@
 #include <string.h>
 
 /* ---- cocogfx ClipToHDC / ClipToScreen (inferred) ------------------------
- * Called by gfxutil.cpp:190-192 / :204-206 with (left,right,top,bottom) =
+ * Called by gfxutil.cpp:150-152 / :164-166 with (left,right,top,bottom) =
  * (0,width,0,height): HDC = (x_s*w, y_s*w, z_s*w, w) with
  * x_s = x/w * (r-l)/2 + (r+l)/2 and y measured from `top`, so framebuffer
  * row 0 is NDC y = -1 (confirmed by triangle_ref_8.png: apex at the top of
@@ -67,10 +67,10 @@ int orc_setup_prim(const float* v, uint32_t width, uint32_t height,
     clip_to_hdc(ph[i], p[i], 0.0f, (float)width, 0.0f, (float)height, znear, zfar);
   memset(out, 0, sizeof(*out));
   if (!edge_equation(e, ph[0], ph[1], ph[2]))
-    return 1;                                   /* gfxutil.cpp:195-199 */
+    return 1;                                   /* gfxutil.cpp:155-159 */
   for (int i = 0; i < 3; ++i)
     clip_to_screen(ps[i], p[i], 0.0f, (float)width, 0.0f, (float)height, znear, zfar);
-  {                                             /* gfxutil.cpp:209-232 */
+  {                                             /* gfxutil.cpp:168-192 */
     float l = ps[0][0], r = ps[0][0], t = ps[0][1], b = ps[0][1];
     for (int i = 1; i < 3; ++i) {
       l = fminf(l, ps[i][0]); r = fmaxf(r, ps[i][0]);
@@ -83,10 +83,10 @@ int orc_setup_prim(const float* v, uint32_t width, uint32_t height,
     bbox[2] = T > 0 ? T : 0;
     bbox[3] = B < (int32_t)height ? B : (int32_t)height;
   }
-  /* half-pixel offset, gfxutil.cpp:251-254 */
+  /* half-pixel offset, gfxutil.cpp:211-214 */
   for (int i = 0; i < 3; ++i)
     e[i][2] += e[i][0] * 0.5f + e[i][1] * 0.5f;
-  /* EdgeToFixed, gfxutil.cpp:119-136 */
+  /* EdgeToFixed, gfxutil.cpp:79-96 (called at :217) */
   {
     float m = fabsf(e[0][0]);
     const float c[5] = {fabsf(e[1][0]), fabsf(e[2][0]), fabsf(e[0][1]),
@@ -97,7 +97,7 @@ int orc_setup_prim(const float* v, uint32_t width, uint32_t height,
       for (int j = 0; j < 3; ++j)
         out->edges[i][j] = fx_from_float_host(e[i][j] * scale, 16);
   }
-  /* ATTRIBUTE_DELTA, gfxutil.cpp:244-270: z uses screen z, the rest raw */
+  /* ATTRIBUTE_DELTA, gfxutil.cpp:204-207,224-230: z uses screen z, the rest raw */
   {
     float a[7][3];
     for (int i = 0; i < 3; ++i) {

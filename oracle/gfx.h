@@ -52,7 +52,7 @@ enum {
 
 /* ---- cocogfx CGLTrace enums (inferred; pinned by goldens) ---------------
  * compare / stencil-op / blend-op: declaration order = the case order of
- * gfxutil.cpp:336-385 (GL order; depth_func 1 = LESS in tekkaman/box,
+ * gfxutil.cpp:296-346 (GL order; depth_func 1 = LESS in tekkaman/box,
  * 3 = LEQUAL in evilskull; blend 4/5 = SRC_ALPHA/ONE_MINUS_SRC_ALPHA).
  * pixel formats: 3 = A8L8 and 4 = R5G6B5 (2 B/texel), 5 = A8R8G8B8 (4 B/texel).
  * filter: NEAREST = 1 (tekkaman min=1, mag=2).  address: WRAP = 0.
@@ -62,19 +62,19 @@ enum {
 #define CGL_ADDRESS_WRAP 0
 #define CGL_ENVMODE_MODULATE 3
 
-static inline uint32_t cgl_to_vx_compare(int c) {   /* gfxutil.cpp:336-351 */
+static inline uint32_t cgl_to_vx_compare(int c) {   /* gfxutil.cpp:296-311 toVXCompare */
   static const uint32_t m[8] = {VX_OM_DEPTH_FUNC_NEVER, VX_OM_DEPTH_FUNC_LESS,
     VX_OM_DEPTH_FUNC_EQUAL, VX_OM_DEPTH_FUNC_LEQUAL, VX_OM_DEPTH_FUNC_GREATER,
     VX_OM_DEPTH_FUNC_NOTEQUAL, VX_OM_DEPTH_FUNC_GEQUAL, VX_OM_DEPTH_FUNC_ALWAYS};
   return (c >= 0 && c < 8) ? m[c] : VX_OM_DEPTH_FUNC_ALWAYS;
 }
-static inline uint32_t cgl_to_vx_stencil_op(int c) { /* gfxutil.cpp:353-366 */
+static inline uint32_t cgl_to_vx_stencil_op(int c) { /* gfxutil.cpp:313-326 toVXStencilOp */
   static const uint32_t m[6] = {VX_OM_STENCIL_OP_KEEP, VX_OM_STENCIL_OP_REPLACE,
     VX_OM_STENCIL_OP_INCR, VX_OM_STENCIL_OP_DECR, VX_OM_STENCIL_OP_ZERO,
     VX_OM_STENCIL_OP_INVERT};
   return (c >= 0 && c < 6) ? m[c] : VX_OM_STENCIL_OP_KEEP;
 }
-static inline uint32_t cgl_to_vx_blend(int c) {      /* gfxutil.cpp:368-386 */
+static inline uint32_t cgl_to_vx_blend(int c) {      /* gfxutil.cpp:328-346 toVXBlendFunc */
   static const uint32_t m[11] = {VX_OM_BLEND_FUNC_ZERO, VX_OM_BLEND_FUNC_ONE,
     VX_OM_BLEND_FUNC_SRC_RGB, VX_OM_BLEND_FUNC_ONE_MINUS_SRC_RGB,
     VX_OM_BLEND_FUNC_SRC_A, VX_OM_BLEND_FUNC_ONE_MINUS_SRC_A,
@@ -83,7 +83,7 @@ static inline uint32_t cgl_to_vx_blend(int c) {      /* gfxutil.cpp:368-386 */
     VX_OM_BLEND_FUNC_ALPHA_SAT};
   return (c >= 0 && c < 11) ? m[c] : VX_OM_BLEND_FUNC_ONE;
 }
-static inline int cgl_to_vx_format(int f) {          /* gfxutil.cpp:320-334 */
+static inline int cgl_to_vx_format(int f) {          /* gfxutil.cpp:280-294 toVXFormat */
   switch (f) {
   case 1: return VX_TEX_FORMAT_A8;
   case 2: return VX_TEX_FORMAT_L8;

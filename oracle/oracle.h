@@ -66,7 +66,7 @@ typedef struct {
   int32_t attribs[7][3];            /* Q7.24,  [z,r,g,b,a,u,v][x=a0-a2, y=a1-a2, z=a2] */
 } orc_rast_prim_t;
 
-/* Setup one primitive at W x H (gfxutil.cpp:171-274).  Returns 0 = ok,
+/* Setup one primitive at W x H (gfxutil.cpp:131-251).  Returns 0 = ok,
  * 1 = degenerate (rejected), 2 = outside the viewport (rejected by bbox).
  * bbox = {left, right, top, bottom} in pixels when status != 1. */
 int orc_setup_prim(const float* v /*[3][10]*/, uint32_t width, uint32_t height,

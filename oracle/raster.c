@@ -1,6 +1,6 @@
 /*
  * raster.c -- oracle restatement of the draw3d software path:
- * graphics::Binning (sim/common/gfxutil.cpp:143-316) + Rasterizer::render
+ * graphics::Binning (sim/common/gfxutil.cpp:103-276) + Rasterizer::render
  * (tests/regression/draw3d/gpu_sw.h:34-62, sim/common/graphics.cpp:715-843)
  * + shader_function_sw_rast_cb (draw3d/kernel.cpp:232-279) + OutputMerger.
  * TEST INFRASTRUCTURE ONLY (see oracle.h).
@@ -34,7 +34,7 @@ static int raster_render(const orc_scene_t* scene, uint32_t width, uint32_t heig
     int32_t* bb = (int32_t*)malloc(sizeof(int32_t) * 4 * (n ? n : 1));
     int* ok = (int*)malloc(sizeof(int) * (n ? n : 1));
     memset(tile_cnt, 0, sizeof(uint32_t) * (ntiles + 1));
-    /* Binning: per primitive bbox -> tile range (gfxutil.cpp:276-290) */
+    /* Binning: per primitive bbox -> tile range (gfxutil.cpp:237-250) */
     for (int i = 0; i < n; ++i) {
       const float* v = scene->prim_verts + (size_t)(dc->prim_offset + i) * 30;
       ok[i] = orc_setup_prim(v, width, height, dc->znear, dc->zfar, &rp[i], &bb[4 * i]) == 0;

@@ -8,7 +8,7 @@
  * parity of the RT-specific parts is unpinned; primary visibility is
  * cross-checked against the raster restatement (raster.c), which is pinned by
  * the reference's golden images.  Anchors used:
- *   - pixel centres / framebuffer orientation: gfxutil.cpp:190-214 and
+ *   - pixel centres / framebuffer orientation: gfxutil.cpp:150-152,164-166,211-214 and
  *     draw3d/main.cpp:385-386 (row 0 = NDC y = -1);
  *   - MT == homogeneous edge functions for eye rays: gfxutil.cpp:35-75;
  *   - inclusive coverage (no top-left rule): graphics.cpp:813-825;

@@ -2,7 +2,7 @@
 //
 // NO REFERENCE: the reference has no ray tracer; its
 // acceleration structure for the same scenes is the screen-tile binning of
-// gfxutil.cpp:237-290.  The BVH is built once per scene in clip (x, y, w)
+// gfxutil.cpp:237-250.  The BVH is built once per scene in clip (x, y, w)
 // space, so it is independent of the render resolution.  Boxes are padded by
 // 2^-16 of the scene extent so that fp32 slab tests are conservative for every
 // hit the (inclusive) Möller–Trumbore test can report.

@@ -810,7 +810,7 @@ static int host_setup(rt_renderer* r, const rt_render_params_t* p, bool raster, 
   if (upload(r->dev, prims.data(), prims.size() * sizeof(rt_prim_t), &r->prims, &a.prims_addr))
     return -1;
   // screen boxes (PrimBBox; degenerate / culled primitives get an empty box
-  // and are never binned, gfxutil.cpp:195-232) and primary visibility per
+  // and are never binned, gfxutil.cpp:155-192) and primary visibility per
   // primitive (app/vis.h): covered-pixel rectangle + depth bound
   std::vector<rt_bbox_t> bb(prims.size());
   std::vector<rt::VisPrim> vis(prims.size());

@@ -32,7 +32,7 @@ Viewport MakeViewport(uint32_t w, uint32_t h, float n, float f) {
 
 }  // namespace
 
-uint32_t ToVXCompare(int32_t c) {
+uint32_t ToVXCompare(int32_t c) {  // gfxutil.cpp:296-311
   static const uint32_t m[8] = {VX_OM_DEPTH_FUNC_NEVER,    VX_OM_DEPTH_FUNC_LESS,
                                 VX_OM_DEPTH_FUNC_EQUAL,    VX_OM_DEPTH_FUNC_LEQUAL,
                                 VX_OM_DEPTH_FUNC_GREATER,  VX_OM_DEPTH_FUNC_NOTEQUAL,
@@ -40,7 +40,7 @@ uint32_t ToVXCompare(int32_t c) {
   return (c >= 0 && c < 8) ? m[c] : VX_OM_DEPTH_FUNC_ALWAYS;
 }
 
-int32_t ToVXFormat(int32_t f) {
+int32_t ToVXFormat(int32_t f) {  // gfxutil.cpp:280-294
   switch (f) {
   case 1: return VX_TEX_FORMAT_A8;
   case 2: return VX_TEX_FORMAT_L8;
@@ -86,7 +86,7 @@ int PrimSetup(const std::array<Vertex, 3>& v, uint32_t width, uint32_t height, f
       for (float& x : row) x *= -1.0f;
   if (det == 0) return kSetupDegenerate;
   for (auto& row : e) row[2] += row[0] * 0.5f + row[1] * 0.5f;  // half-pixel offset
-  // EdgeToFixed (gfxutil.cpp:119-136)
+  // EdgeToFixed (gfxutil.cpp:79-96)
   float m = std::fabs(e[0][0]);
   const float c[5] = {std::fabs(e[1][0]), std::fabs(e[2][0]), std::fabs(e[0][1]),
                       std::fabs(e[1][1]), std::fabs(e[2][1])};
@@ -94,7 +94,7 @@ int PrimSetup(const std::array<Vertex, 3>& v, uint32_t width, uint32_t height, f
   const float scale = 1.0f / m;
   for (int i = 0; i < 3; ++i)
     for (int j = 0; j < 3; ++j) out->edges[i][j] = FixedHost(e[i][j] * scale, 16);
-  // ATTRIBUTE_DELTA (gfxutil.cpp:244-270): z from screen z, rest raw
+  // ATTRIBUTE_DELTA (gfxutil.cpp:204-207,224-230): z from screen z, rest raw
   float a[7][3];
   for (int i = 0; i < 3; ++i) {
     a[0][i] = sz[i];
@@ -172,13 +172,13 @@ int PrimBBox(const std::array<Vertex, 3>& v, uint32_t width, uint32_t height, rt
 }
 
 namespace {
-uint32_t ToVXStencilOp(int32_t c) {  // gfxutil.cpp:353-366
+uint32_t ToVXStencilOp(int32_t c) {  // gfxutil.cpp:313-326
   static const uint32_t m[6] = {VX_OM_STENCIL_OP_KEEP, VX_OM_STENCIL_OP_REPLACE,
                                 VX_OM_STENCIL_OP_INCR, VX_OM_STENCIL_OP_DECR,
                                 VX_OM_STENCIL_OP_ZERO, VX_OM_STENCIL_OP_INVERT};
   return (c >= 0 && c < 6) ? m[c] : VX_OM_STENCIL_OP_KEEP;
 }
-uint32_t ToVXBlend(int32_t c) {  // gfxutil.cpp:368-386
+uint32_t ToVXBlend(int32_t c) {  // gfxutil.cpp:328-346
   static const uint32_t m[11] = {VX_OM_BLEND_FUNC_ZERO, VX_OM_BLEND_FUNC_ONE,
                                  VX_OM_BLEND_FUNC_SRC_RGB, VX_OM_BLEND_FUNC_ONE_MINUS_SRC_RGB,
                                  VX_OM_BLEND_FUNC_SRC_A, VX_OM_BLEND_FUNC_ONE_MINUS_SRC_A,

@@ -1,7 +1,7 @@
 // setup.h -- host-side scene preparation for the RT kernel.
 //
 //  * PrimSetup: the per-primitive part of graphics::Binning
-//    (sim/common/gfxutil.cpp:171-274): clip -> 2D-homogeneous device
+//    (sim/common/gfxutil.cpp:131-251): clip -> 2D-homogeneous device
 //    coordinates, edge equations, half-pixel offset, Q15.16 edges, Q7.24
 //    attribute deltas -> rt_prim_t (the fixed-point shading record).
 //  * DrawcallState: the draw3d host state setup (draw3d/main.cpp:286-344)
@@ -18,7 +18,7 @@
 
 namespace rt {
 
-// CGLTrace -> VX enum mapping (gfxutil.cpp:320-386 case order)
+// CGLTrace -> VX enum mapping (gfxutil.cpp:280-346 case order)
 uint32_t ToVXCompare(int32_t cgl_compare);
 int32_t ToVXFormat(int32_t cgl_format);
 uint32_t FormatStride(int32_t vx_format);
@@ -36,7 +36,7 @@ int PrimSetup(const std::array<Vertex, 3>& v, uint32_t width, uint32_t height, f
 // Shading state of a drawcall (texture address filled by the caller).
 rt_dcstate_t DrawcallState(const DrawCall& dc, const Scene& scene);
 
-// Screen bounding box of a triangle at width x height (gfxutil.cpp:209-232);
+// Screen bounding box of a triangle at width x height (gfxutil.cpp:168-192);
 // returns kSetupCulled (and an empty box) when it misses the viewport.
 int PrimBBox(const std::array<Vertex, 3>& v, uint32_t width, uint32_t height, rt_bbox_t* out);
 

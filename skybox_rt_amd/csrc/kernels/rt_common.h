@@ -171,7 +171,7 @@ typedef struct {
   uint32_t pad[7];
 } rt_omstate_t;
 
-// screen bounding box of a primitive in pixels (gfxutil.cpp:209-232, clamped
+// screen bounding box of a primitive in pixels (gfxutil.cpp:168-192, clamped
 // to the viewport): x in [lo & 0xffff, lo >> 16), y in [hi & 0xffff, hi >> 16);
 // empty (x0 == x1) for degenerate or culled primitives
 typedef struct {
