@@ -6,9 +6,13 @@ tekkaman.cgltrace, 1024x1024, one primary ray per pixel (raster-exact, from
 the per-8x8-block candidate lists built on the device) + one any-hit shadow
 ray per geometry hit (ballot/mbcnt-compacted into full waves, each lane
 scanning its light-space cell list -- the cube map of triangle lists around
-the point light, built on the device -- nearest to the light first).  The
-same frame by BVH traversal only (binary16 BVH4 wave-packet walks, stack in
-one VGPR) is timed beside it as series.bvh_walk.
+the point light, built on the device -- nearest to the light first).  Timed beside it in the same command, each
+with its own kernel clock, roofline and PMC record (`series`): the same frame
+by BVH traversal only (binary16 BVH4 wave-packet walks; series.bvh_walk),
+config 4's 4-bounce path trace (series.path), config 2's 256^2 flat list
+(series.flat), config 5's 4096^2 frame on this one GPU (series.strong_4096:
+the N = 1 point of the multi-GPU curve) and frames whose light moves every
+step (series.moving_light).
 A "step" is one full frame: vx_start of the RT kernel image through
 libvortex-hip.so (inputs already resident in HBM), every frame complete
 inside the timed region.
@@ -18,10 +22,13 @@ BASELINE config 5: ONE 4096x4096 frame whose 32x32 tiles are dealt
 tile t -> rank t % N (sim/simx/raster_unit.cpp:109-111 striding), each step
 ending with an RCCL gather of the ranks' compact tile buffers to rank 0 and
 the frame assembly there -- strong scaling (fixed total
-work).  `--gpus N` without WORLD_SIZE launches the N ranks itself
-(torch.distributed.run, before anything touches a GPU).  Every line also
-carries `series`: the same render at 4096^2 on these N GPUs (strong) and at
-~1024^2 * sqrt(N) (weak, ~1M pixels per GPU).
+work).  `value` is then the whole job's rays/s (metric "Mrays/sec, all N
+GPUs"; per GPU in config.mrays_per_s_per_gpu).  `--gpus N` without
+WORLD_SIZE launches the N ranks itself (torch.distributed.run, before
+anything touches a GPU).  The communicator's start and the first gathers
+run under a watchdog (BENCH_DIST_TIMEOUT_S, default 240 s): a hang ends the
+rank with a message and the tracebacks on stderr.  The line also carries
+series.weak_1024_sqrtN (~1M pixels per GPU).
 
 Rank 0 prints one JSON line.  Everything else goes to stderr.
 """
@@ -82,11 +89,18 @@ def pmc_record(mode: str, side: int, images=None):
     the SQ/TCP counters.  Returns (record or None, stale): stale = a record
     exists but was taken on another kernel image or size."""
     import hashlib
-    path = os.path.join(ROOT, "profiles", f"pmc_{mode}.json")
-    try:
-        with open(path) as fh:
-            t = json.load(fh)
-    except (OSError, ValueError):
+    t = None
+    # profiles/pmc_<mode>.json at the mode's own size, pmc_<mode>_<side>.json
+    # at another (e.g. config 5's 4096^2 frame on one GPU)
+    for name in (f"pmc_{mode}.json", f"pmc_{mode}_{side}.json"):
+        try:
+            with open(os.path.join(ROOT, "profiles", name)) as fh:
+                c = json.load(fh)
+        except (OSError, ValueError):
+            continue
+        if t is None or (c.get("width") == side and t.get("width") != side):
+            t = dict(c, _path=name)
+    if t is None:
         return None, False
     try:
         h = hashlib.md5()  # the frame's images' bytes concatenated (scripts/pmc_profile.py)
@@ -114,7 +128,55 @@ def issue_roofline(rec: dict, kernel_ms: float, mode: str):
             **{k: d[k] for k in ("wait_any_frac", "wait_inst_any_frac", "active_inst_any_frac",
                                  "active_inst_valu_frac", "valu_lane_utilisation",
                                  "l1_hit_rate", "l2_hit_rate") if k in d},
-            "source": f"profiles/pmc_{mode}.json (rocprofv3 --pmc passes, scripts/pmc_profile.sh)"}
+            "source": f"profiles/{rec.get('_path', f'pmc_{mode}.json')} (rocprofv3 --pmc passes, "
+                      f"scripts/pmc_profile.sh)"}
+
+
+COUNT_KEYS = ("node_visits", "tri_tests", "layer_tests", "texel_bytes", "primary_rays", "shadow_rays",
+              "bounce_rays")
+
+
+def make_roofline(inst: dict, kernel_ms: float, mode: str, side: int, node_bytes: int, images=None,
+                  n_gpus: int = 1):
+    """(roofline, roofline_issue) of one timed configuration: algorithmic bytes
+    per launch (the instrumented pre-run's counts) over the kernel clock
+    against 8 TB/s, the PMC record's measured traffic beside it, and the VALU
+    issue roofline from the same record.  Config 2 (flat) reads its list from
+    L2 and the scalar cache and prunes with integer rectangle tests: its
+    roofline is the VALU-issue one, with the work executed per wave."""
+    rec, stale = pmc_record(mode, side, images) if n_gpus == 1 else (None, False)
+    traffic = rec["traffic_bytes"] if rec else None
+    counts = {k: int(inst[k]) for k in COUNT_KEYS}
+    alg = algorithmic_bytes(inst, inst["primary_rays"], node_bytes)
+    ach = alg / (kernel_ms * 1e-3) / 1e9
+    roof = {"bound": "hbm", "achieved": round(ach, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": traffic,
+            "algorithmic_bytes_per_launch": int(alg), "counts": counts}
+    if stale:
+        roof["traffic_stale"] = True
+    if rec:
+        roof["traffic_calibrated"] = bool(rec.get("traffic_calibrated", False))
+        if "traffic_bounds" in rec:
+            roof["traffic_bounds"] = rec["traffic_bounds"]
+        # measured HBM bytes per launch over the same kernel time: the share of
+        # the HBM peak the kernel physically uses (the scene is cache-resident)
+        roof["measured_hbm_gbs"] = round(traffic / (kernel_ms * 1e-3) / 1e9, 2)
+        roof["measured_hbm_frac"] = round(traffic / (kernel_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)
+        roof["pmc_source"] = f"profiles/{os.path.basename(rec.get('_path', f'pmc_{mode}.json'))}"
+    issue = issue_roofline(rec, kernel_ms, mode)
+    if mode == "flat":
+        work = {"rect_tests_per_wave": int(inst["rect_tests"]), "edge_tests_per_wave": int(inst["edge_tests"]),
+                "list_entries_per_ray_algorithmic": int(inst["tri_tests"])}
+        if issue is not None:
+            roof = {**issue, "traffic": traffic, "work_executed": work, "counts": counts}
+            if rec:
+                roof["measured_hbm_gbs"] = round(traffic / (kernel_ms * 1e-3) / 1e9, 2)
+            issue = None
+        else:
+            roof.pop("algorithmic_bytes_per_launch")
+            roof.update({"bound": "valu_issue", "achieved": None, "frac": None, "work_executed": work,
+                         "note": "no current PMC record"})
+    return roof, issue
 
 
 def moving_lights(k: int):
@@ -489,6 +551,67 @@ def reduce_max_sum(dist, coll_dev, elapsed, rays):
     return float(mx[0]), float(sm[1])
 
 
+def describe(side, mode, setup_st, shadows, bounces, bvh_kind):
+    """The workload text of one timed configuration (what the kernel runs)."""
+    if mode == "flat":
+        return (f"{side}x{side} primary rays, flat triangle list (no BVH), tekkaman.cgltrace: every "
+                f"ray tests the whole geometry list -- a 512-thread workgroup per 64-pixel chunk "
+                f"splits the list 8 ways, each wave tests 64 rectangle words per instruction (read "
+                f"from L2) against the chunk's 8x8 block, then the entries reaching it per pixel "
+                f"(exact edge + depth test, records through the scalar cache); the waves' winners "
+                f"meet in LDS and wave 0 shades and stores the chunk (no shadow rays: the other "
+                f"waves leave at the barrier)")
+    primary = ("primary: 8x8-block candidate lists built on the device (raster-exact)"
+               if setup_st["blist_blocks"] else f"primary: {bvh_kind} packet walk (raster-exact)")
+    if mode == "path":
+        kind = f"{bounces}-bounce diffuse path trace (primary + bounce + shadow rays)"
+        if setup_st.get("path_queue"):
+            shadow_how = ("light-space shadow lists" if setup_st["slist_on"] else f"{bvh_kind} walk")
+            return (f"{side}x{side} {kind}, tekkaman.cgltrace, two kernels per frame: {primary}, "
+                    f"path starts appended to a compacted queue (wave64: one atomic per wave, "
+                    f"ballot/mbcnt slots); then the queued paths on full waves: bounce rays a "
+                    f"per-lane {bvh_kind} walk (LDS stack), shadow rays on the {shadow_how}")
+        if setup_st["slist_on"]:
+            return (f"{side}x{side} {kind}, tekkaman.cgltrace, one kernel; {primary}; then each "
+                    f"path on its lane(s): bounce rays a {bvh_kind} walk (LDS stack), shadow rays "
+                    f"on the light-space shadow lists; in the 32-pixel waves of geometry tiles "
+                    f"two adjacent lanes per path (children / triangles / list records split two "
+                    f"and two, DPP exchanges); no wave64 compaction of live paths in the timed "
+                    f"kernel: the block-compacted (pt_compact) and queue-compacted "
+                    f"(RT_PT_QUEUE=1) forms measured slower, DESIGN.md 2.1")
+        return (f"{side}x{side} {kind}, tekkaman.cgltrace; {primary}; bounce + shadow rays: "
+                f"per-lane {bvh_kind} walk, LDS stack, shadow/bounce lanes paired in the "
+                f"32-pixel waves of geometry tiles")
+    shadow_how = ("per lane over its light-space cell list (cube map around the light, built "
+                  "on the device)" if setup_st["slist_on"]
+                  else f"each wave a {bvh_kind} packet walk (stack in one VGPR)")
+    return (f"{side}x{side} {'primary+shadow' if shadows else 'primary'} rays, "
+            f"tekkaman.cgltrace; {primary}; shadow rays: ballot/mbcnt-compacted into full "
+            f"waves, {shadow_how}")
+
+
+class Watchdog:
+    """N > 1: a phase that does not finish in `seconds` (a hung RCCL init or
+    first gather) ends the rank with a message and every thread's traceback
+    on stderr, exit status 1 (faulthandler), instead of hanging the driver's
+    run until its own limit."""
+
+    def __init__(self, on: bool, seconds: float):
+        self.on, self.seconds = on, seconds
+
+    def arm(self, what: str):
+        if not self.on:
+            return
+        import faulthandler
+        log(f"bench.py: rank {os.environ.get('RANK', '0')}: {what} (watchdog {self.seconds:.0f} s)")
+        faulthandler.dump_traceback_later(self.seconds, exit=True)
+
+    def disarm(self):
+        if self.on:
+            import faulthandler
+            faulthandler.cancel_dump_traceback_later()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -502,16 +625,15 @@ def main():
     ap.add_argument("--no-series", action="store_true",
                     help="skip the strong/weak scaling series runs (default at N>1)")
     ap.add_argument("--series", action="store_true",
-                    help="N=1: also run the series (4096^2 strong point, weak 1024^2); off by default "
-                         "so the timed image's rocprof average is the metric's frame size only")
+                    help="N=1: also run the weak-scaling series point (~1024^2 sqrt(N))")
     ap.add_argument("--workload", choices=("shadow", "path", "flat"), default="shadow",
                     help="shadow: BASELINE config 3 (the metric's config, default); "
                          "path: config 4, 4-bounce diffuse path trace; "
                          "flat: config 2, 256^2 primary rays over the flat triangle list")
     ap.add_argument("--bounces", type=int, default=4)
     ap.add_argument("--no-bvh-series", action="store_true",
-                    help="N=1 primary+shadow: skip the series entry timing the same frame by BVH "
-                         "traversal only (image rt_bvh)")
+                    help="N=1: skip the series entries beside the headline (the BVH-walk frame, "
+                         "configs 2 / 4 / 5's frame, the moving light)")
     ap.add_argument("--verify-gather", action="store_true",
                     help="N>1: rank 0 checks the gathered frame against its own full render")
     ap.add_argument("--plumbing-check", action="store_true",
@@ -533,6 +655,7 @@ def main():
     os.dup2(2, 1)
     path = args.workload == "path"
     flat = args.workload == "flat"
+    mode = "path" if path else ("flat" if flat else "shadow")
     n_gpus = max(world, 1)
     if args.size is None:
         args.size = 256 if flat else (CONFIG5_SIDE if n_gpus > 1 else 1024)
@@ -543,6 +666,7 @@ def main():
     # BENCH_FORCE_GATHER=1 (under torch.distributed.run): the N>1 exchange
     # path even at world size 1 -- RCCL on one GPU, to test its stream order
     use_gather = world > 1 or os.environ.get("BENCH_FORCE_GATHER") == "1" or args.plumbing_check
+    dog = Watchdog(use_gather, float(os.environ.get("BENCH_DIST_TIMEOUT_S", "240")))
     dist = None
     import torch
     # RCCL ("nccl") between the GPUs; BENCH_DIST_BACKEND=gloo rehearses the
@@ -551,19 +675,23 @@ def main():
     coll_dev = torch.device("cpu")
     ranks_seen = 1
     if use_gather:
+        import datetime
         import torch.distributed as dist
         ndev = torch.cuda.device_count()
         dev_index = local_rank % max(1, ndev)
         if ndev:
             torch.cuda.set_device(dev_index)
+        dog.arm(f"joining the {backend} communicator ({world} ranks)")
+        timeout = datetime.timedelta(seconds=dog.seconds)
         if backend == "nccl":
             coll_dev = torch.device("cuda", dev_index)
-            dist.init_process_group("nccl", device_id=coll_dev)
+            dist.init_process_group("nccl", device_id=coll_dev, timeout=timeout)
         else:
-            dist.init_process_group(backend)
+            dist.init_process_group(backend, timeout=timeout)
         one = torch.ones(1, dtype=torch.float64, device=coll_dev)
         dist.all_reduce(one)  # ranks the communicator actually connects
         ranks_seen = int(one.item())
+        dog.disarm()
         if ranks_seen != world:
             log(f"bench.py: communicator sees {ranks_seen} ranks, WORLD_SIZE={world}")
             sys.exit(3)
@@ -587,16 +715,19 @@ def main():
     bvh_rebuild_ms = min(r.build_bvh("sah")["build_ms"] for _ in range(3)) if bvh_st["method"] == 1 else None
     bvh_st = r.bvh_stats()
 
-    def make_run(s, bvh_walk=False):
-        return Run(r, rt, dist, coll_dev, rank, n_gpus, s, shadows, light, path, flat,
-                   args.bounces, use_gather, bvh_walk)
+    def make_run(s, bvh_walk=False, m=None, gather=None):
+        m = m or mode
+        g = use_gather if gather is None else gather
+        return Run(r, rt, dist, coll_dev, rank, n_gpus, s, shadows and m != "flat", light, m == "path",
+                   m == "flat", args.bounces, g, bvh_walk)
 
+    dog.arm("the first configure and gather set-up")
     run = make_run(side)
+    dog.disarm()
     setup_st = r.setup_stats()  # the timed configuration's records (configure)
     inst = run.inst
     bvh_kind = ("BVH4 (binary16 boxes)" if r.bvh4_f16 else "BVH4") if r.bvh4 else "BVH2"
-    alg_bytes = algorithmic_bytes(inst, inst["primary_rays"], (NODE4H_BYTES if r.bvh4_f16 else NODE4_BYTES)
-                                  if r.bvh4 else NODE_BYTES)
+    node_bytes = (NODE4H_BYTES if r.bvh4_f16 else NODE4_BYTES) if r.bvh4 else NODE_BYTES
     # synchronous frames first (start + wait per frame, simx's blocking
     # start): reported beside the pipelined rate, not as `value`.  200 frames
     # (~5 ms) whatever --steps is: a steadier figure than a few frames, and
@@ -616,16 +747,19 @@ def main():
     # a step = one frame: vx_start queues the launch behind the in-flight
     # frame (driver VX_HIP_QUEUE_DEPTH, default 2) so the host's launch and
     # completion-poll overhead overlaps the previous frame; every frame is
-    # complete before the timed region ends
+    # complete before the timed region ends.  N > 1: the first steps carry
+    # the first RCCL gathers (watchdog)
+    dog.arm("the timed steps (render + RCCL gather)")
     elapsed = run.timed(args.steps, args.warmup, dist)
+    dog.disarm()
     # the kernel's average duration: HIP events around a back-to-back run of
     # the same frames on the driver's stream (Run.kernel_clock)
-    avg_kernel_ms = run.kernel_clock(max(50, min(args.steps, 1000)), max(5, min(args.warmup, 20)))
+    clock_frames = max(50, min(args.steps, 1000))
+    avg_kernel_ms = run.kernel_clock(clock_frames, max(5, min(args.warmup, 20)))
     st = r.stats()
     elapsed, rays_total = reduce_max_sum(dist, coll_dev, elapsed, run.rays_local)
     ms_per_step = elapsed / args.steps * 1e3
     value = rays_total * args.steps / elapsed / 1e6
-    achieved = alg_bytes / (avg_kernel_ms * 1e-3) / 1e9
     # N > 1: the same steps with only the render, and with only the frame
     # exchange (gather of the last frame + assembly), max over ranks -- which
     # half sets the step time at this N
@@ -651,66 +785,64 @@ def main():
             full = r.framebuffer().reshape(-1).view(np.int32)
             gather_ok = bool(np.array_equal(image, full))
             log(f"gathered frame == full render: {gather_ok}")
-    # scaling series: the same render at 4096^2 on these N GPUs (strong) and
-    # at ~1024^2 * sqrt(N) (weak); short runs, reported beside `value`
     series = {}
+
+    def timed_series(name, s, m, image, bvh_walk=False, gather=None, note=None):
+        """One more configuration timed like `value` (same steps and warm-up),
+        with its own kernel clock, roofline and issue roofline (its own PMC
+        record); rays summed over the ranks, time the max over the ranks."""
+        sr = make_run(s, bvh_walk=bvh_walk, m=m, gather=gather)
+        sst = r.setup_stats()
+        e = sr.timed(args.steps, args.warmup, dist)
+        k = sr.kernel_clock(clock_frames, max(5, min(args.warmup, 20)))
+        e, rays = reduce_max_sum(dist, coll_dev, e, sr.rays_local)
+        roof, issue = make_roofline(sr.inst, k, "bvh" if bvh_walk else m, s, node_bytes, n_gpus=n_gpus)
+        ent = {"workload": describe(s, m, sst, shadows and m != "flat", args.bounces, bvh_kind),
+               "image": image, "side": s, "steps": args.steps, "warmup": args.warmup,
+               "value": round(rays * args.steps / e / 1e6, 3),
+               "ms_per_step": round(e / args.steps * 1e3, 5), "kernel_ms": round(k, 5),
+               "rays_per_frame": int(rays), "roofline": roof, "roofline_issue": issue}
+        if note:
+            ent["note"] = note
+        series[name] = ent
+        return ent
+
+    # N > 1: config 5's frame on these N GPUs is `value` itself; the weak
+    # point (~1M pixels per GPU) beside it.  N = 1 (`--series`): the weak point
     if not args.no_series and not flat and (n_gpus > 1 or args.series):
-        series_steps = max(20, min(args.steps, 200))
-        for name, s in (("strong_4096", CONFIG5_SIDE), ("weak_1024_sqrtN", frame_side(n_gpus, 1024))):
-            if s == side:
-                series[name] = {"side": s, "value": round(value, 3), "ms_per_step": round(ms_per_step, 5),
-                                "same_as": "value"}
-                continue
-            sr = make_run(s)
-            e2 = sr.timed(series_steps, 10, dist)
-            k2 = sr.kernel_clock(series_steps, 5)
-            e2, rays2 = reduce_max_sum(dist, coll_dev, e2, sr.rays_local)
-            series[name] = {"side": s, "steps": series_steps,
-                            "value": round(rays2 * series_steps / e2 / 1e6, 3),
-                            "ms_per_step": round(e2 / series_steps * 1e3, 5),
-                            "kernel_ms": round(k2, 5), "rays_per_frame": int(rays2)}
-    # BASELINE config 3 by BVH traversal only (RT_RENDER_BVH_WALK, image
-    # rt_bvh: primary visibility by the binary16-BVH4 packet walk, shadow
-    # rays by the shadow packet walk; no block or light-space lists): the
-    # same frame, steps and warm-up as `value`, with its own algorithmic
-    # bytes (node_visits > 0), kernel clock and PMC record
-    if n_gpus == 1 and not path and not flat and shadows and not args.no_bvh_series:
-        br = make_run(side, bvh_walk=True)
-        eb = br.timed(args.steps, args.warmup, dist)
-        kb = br.kernel_clock(max(50, min(args.steps, 1000)), max(5, min(args.warmup, 20)))
-        bi = br.inst
-        b_bytes = algorithmic_bytes(bi, bi["primary_rays"], (NODE4H_BYTES if r.bvh4_f16 else NODE4_BYTES)
-                                    if r.bvh4 else NODE_BYTES)
-        b_ach = b_bytes / (kb * 1e-3) / 1e9
-        b_rec, b_stale = pmc_record("bvh", side)
-        b_roof = {"bound": "hbm", "achieved": round(b_ach, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                  "frac": round(b_ach / HBM_PEAK_GBS, 4),
-                  "traffic": b_rec["traffic_bytes"] if b_rec else None,
-                  "algorithmic_bytes_per_launch": int(b_bytes),
-                  "counts": {k: int(bi[k]) for k in ("node_visits", "tri_tests", "layer_tests",
-                                                     "texel_bytes", "primary_rays", "shadow_rays",
-                                                     "bounce_rays")}}
-        if b_stale:
-            b_roof["traffic_stale"] = True
-        if b_rec:
-            b_roof["measured_hbm_frac"] = round(b_rec["traffic_bytes"] / (kb * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)
-            b_roof["pmc_source"] = "profiles/pmc_bvh.json"
-        series["bvh_walk"] = {
-            "workload": (f"{side}x{side} primary+shadow rays, tekkaman.cgltrace, BVH traversal only "
+        if side == CONFIG5_SIDE:
+            series["strong_4096"] = {"side": side, "value": round(value, 3),
+                                     "ms_per_step": round(ms_per_step, 5), "same_as": "value"}
+        s = frame_side(n_gpus, 1024)
+        if s != side:
+            timed_series("weak_1024_sqrtN", s, mode, "rt_kernel (entry vx_main_rt_kernel)")
+    extra = n_gpus == 1 and not args.no_bvh_series
+    if extra and mode == "shadow" and shadows:
+        # BASELINE config 3 by BVH traversal only (RT_RENDER_BVH_WALK, image
+        # rt_bvh: primary visibility by the binary16-BVH4 packet walk, shadow
+        # rays by the shadow packet walk; no block or light-space lists)
+        b = timed_series("bvh_walk", side, "shadow", "rt_bvh (entry vx_main_rt_bvh)", bvh_walk=True)
+        b["workload"] = (f"{side}x{side} primary+shadow rays, tekkaman.cgltrace, BVH traversal only "
                          f"(BASELINE config 3): primary visibility by a {bvh_kind} packet walk per "
                          f"8x8-block wave (raster-exact leaf tests, node/leaf records through the "
                          f"scalar cache, wave stack in one VGPR); shadow rays ballot/mbcnt-compacted "
                          f"into full waves, each a {bvh_kind} any-hit packet walk (its traversal stack "
-                         f"also in one VGPR, v_writelane/v_readlane, not LDS: measured neutral against "
-                         f"an LDS stack, DESIGN.md 4.1)"),
-            "image": "rt_bvh (entry vx_main_rt_bvh)", "side": side, "steps": args.steps,
-            "warmup": args.warmup, "value": round(br.rays_local * args.steps / eb / 1e6, 3),
-            "ms_per_step": round(eb / args.steps * 1e3, 5), "kernel_ms": round(kb, 5),
-            "rays_per_frame": int(br.rays_local), "roofline": b_roof,
-            "roofline_issue": issue_roofline(b_rec, kb, "bvh")}
+                         f"in VGPR lanes, v_writelane/v_readlane, not LDS: measured neutral against "
+                         f"an LDS stack, DESIGN.md 4.1)")
+        # every other single-GPU BASELINE config in the same command, each
+        # with its own kernel clock and PMC record (VERDICT r05 item 2): config
+        # 4 (path), config 2 (flat), and config 5's 4096^2 frame on this one
+        # GPU -- the N = 1 point of the driver's 4096^2 scaling curve
+        timed_series("path", 1024, "path", "pt_kernel (entry vx_main_pt_kernel)")
+        timed_series("flat", 256, "flat", "rt_flat (entry vx_main_rt_flat)")
+        timed_series("strong_4096", CONFIG5_SIDE, "shadow", "rt_kernel (entry vx_main_rt_kernel)",
+                     gather=True if os.environ.get("BENCH_FORCE_GATHER") == "1" else False,
+                     note="BASELINE config 5's frame (4096^2 primary+shadow) on one GPU, whole frame, "
+                          "no exchange: the N = 1 point of the --gpus N scaling curve, whose N > 1 "
+                          "lines render this frame tile-sharded")
     # the moving light: a light change + a frame per step (N = 1)
     moving = None
-    if n_gpus == 1 and not flat and (shadows or path) and not args.no_bvh_series:
+    if extra and not flat and (shadows or path):
         mr = moving_light_series(r, side, args.steps, args.warmup,
                                  dict(shadows=shadows, path=path, bounces=args.bounces))
         mr["value"] = round(run.rays_local * mr["steps"] / (mr["ms_per_step"] * 1e-3 * mr["steps"]) / 1e6, 3)
@@ -719,68 +851,33 @@ def main():
                           f"rebuilt on the device, 6 stream-ordered setup launches, no host wait)")
         series["moving_light"] = moving = mr
     cold = None
-    if n_gpus == 1 and not flat and not args.no_bvh_series:
+    if extra and not flat:
         cold = cold_configure_probe(rt, scene, side, dict(shadows=shadows, light=light, path=path,
                                                           bounces=args.bounces))
     if rank != 0:
         dist.destroy_process_group()
         return
     config5 = n_gpus > 1 and side == CONFIG5_SIDE
-    metric = "Mrays/sec per GPU + achieved HBM GB/s, 1024^2 primary+shadow tekkaman"
-    kind = "primary+shadow rays"
-    if path:
-        metric = (f"Mrays/sec per GPU + achieved HBM GB/s, 1024^2 {args.bounces}-bounce diffuse "
-                  f"path trace tekkaman (BASELINE config 4)")
-        kind = f"{args.bounces}-bounce diffuse path trace (primary + bounce + shadow rays)"
-    if flat:
-        metric = (f"Mrays/sec per GPU + achieved HBM GB/s, {side}^2 primary rays, tekkaman flat "
-                  f"triangle list, no BVH (BASELINE config 2)")
-        kind = "primary rays, flat triangle list (no BVH)"
-    primary = ("primary: 8x8-block candidate lists built on the device (raster-exact)"
-               if setup_st["blist_blocks"] else f"primary: {bvh_kind} packet walk (raster-exact)")
-    if flat:
-        workload = (f"{side}x{side} {kind}, tekkaman.cgltrace: every ray tests the whole geometry "
-                    f"list -- a 512-thread workgroup per 64-pixel chunk splits the list 8 ways, each "
-                    f"wave tests 64 rectangle words per instruction (read from L2) against the "
-                    f"chunk's 8x8 block, then the entries reaching it per pixel (exact edge + depth "
-                    f"test, records through the scalar cache); the waves' winners meet in LDS and "
-                    f"wave 0 shades and stores the chunk (no shadow rays: the other waves leave "
-                    f"at the barrier)")
-    elif path and setup_st.get("path_queue"):
-        shadow_how = ("light-space shadow lists" if setup_st["slist_on"] else f"{bvh_kind} walk")
-        workload = (f"{side}x{side} {kind}, tekkaman.cgltrace, two kernels per frame: {primary}, "
-                    f"path starts appended to a compacted queue (wave64: one atomic per wave, "
-                    f"ballot/mbcnt slots); then the queued paths on full waves: bounce rays a "
-                    f"per-lane {bvh_kind} walk (LDS stack), shadow rays on the {shadow_how}")
-    elif path and setup_st["slist_on"]:
-        workload = (f"{side}x{side} {kind}, tekkaman.cgltrace, one kernel; {primary}; then each "
-                    f"path on its lane(s): bounce rays a {bvh_kind} walk (LDS stack), shadow rays "
-                    f"on the light-space shadow lists; in the 32-pixel waves of geometry tiles "
-                    f"two adjacent lanes per path (children / triangles / list records split two "
-                    f"and two, DPP exchanges); no wave64 compaction of live paths in the timed "
-                    f"kernel: the block-compacted (pt_compact) and queue-compacted "
-                    f"(RT_PT_QUEUE=1) forms measured slower, DESIGN.md 2.1")
-    elif path:
-        workload = (f"{side}x{side} {kind}, tekkaman.cgltrace; {primary}; bounce + shadow rays: "
-                    f"per-lane {bvh_kind} walk, LDS stack, shadow/bounce lanes paired in the "
-                    f"32-pixel waves of geometry tiles")
+    what = {"shadow": f"{side}^2 primary+shadow tekkaman",
+            "path": f"{side}^2 {args.bounces}-bounce diffuse path trace tekkaman (BASELINE config 4)",
+            "flat": f"{side}^2 primary rays, tekkaman flat triangle list, no BVH (BASELINE config 2)"}[mode]
+    if n_gpus == 1:
+        # BASELINE.json's metric (config 3 at 1024^2)
+        metric = f"Mrays/sec per GPU + achieved HBM GB/s, {what}"
     else:
-        shadow_how = ("per lane over its light-space cell list (cube map around the light, built "
-                      "on the device)" if setup_st["slist_on"]
-                      else f"each wave a {bvh_kind} packet walk (stack in one VGPR)")
-        workload = (f"{side}x{side} {'primary+shadow' if shadows else 'primary'} rays, "
-                    f"tekkaman.cgltrace; {primary}; shadow rays: ballot/mbcnt-compacted into full "
-                    f"waves, {shadow_how}")
+        # `value` is the whole job's rays/s (all ranks' rays over the max
+        # rank's time); the per-GPU figure is config.mrays_per_s_per_gpu
+        metric = (f"Mrays/sec, all {n_gpus} GPUs (per GPU: config.mrays_per_s_per_gpu) + achieved HBM "
+                  f"GB/s, {what}" + (", tile-sharded (BASELINE config 5)" if config5 else ", tile-sharded"))
+    workload = describe(side, mode, setup_st, shadows, args.bounces, bvh_kind)
     if n_gpus > 1:
         workload += (f", tile-sharded over {n_gpus} GPUs (32x32 tile t -> rank t mod {n_gpus}) + "
                      f"{'RCCL' if backend == 'nccl' else backend} gather to rank 0"
                      + (" (BASELINE config 5)" if config5 else ""))
-    mode = "path" if path else ("flat" if flat else "shadow")
     images = None
     if path and setup_st.get("path_queue"):
         images = ("pt_primary.co", "pt_queue.co")  # the two-kernel form (RT_PT_QUEUE=1)
-    rec, stale = pmc_record(mode, side, images) if n_gpus == 1 else (None, False)
-    traffic = rec["traffic_bytes"] if rec else None
+    roof, issue = make_roofline(inst, avg_kernel_ms, mode, side, node_bytes, images, n_gpus)
     info = scene.info()  # (after the timed region: parse time, host-side counts)
     out = {
         "metric": metric,
@@ -791,7 +888,10 @@ def main():
         "warmup": args.warmup,
         "ms_per_step": round(ms_per_step, 5),
         "higher_is_better": True,
-        "scaling": "strong" if n_gpus > 1 else "weak",
+        # a fixed frame however many GPUs render it (N = 1: config 3's 1024^2
+        # frame; N > 1: config 5's 4096^2 frame dealt over the ranks, whose
+        # one-GPU point is series.strong_4096 of the N = 1 line)
+        "scaling": "strong",
         "vs_baseline": None,
         "dtype": "f32",
         "data": "tekkaman.cgltrace from the reference's regression data (tests/golden/scenes)",
@@ -832,7 +932,7 @@ def main():
             "kernel_ms": round(avg_kernel_ms, 5),
             "frames": "back to back (vx_start queues behind the in-flight frames; no per-launch "
                       "events in the timed region); kernel_ms = two HIP events on the driver's "
-                      f"stream around {max(50, min(args.steps, 1000))} such frames after the "
+                      f"stream around {clock_frames} such frames after the "
                       "timed region / frames (render only)",
             "sync_ms_per_step": round(sync_ms, 5) if sync_ms is not None else None,
             "sync_frames": (f"{sync_n} synchronous frames (vx_start + vx_ready_wait each), host "
@@ -841,52 +941,11 @@ def main():
             "counters": "off in the timed frames (rays per frame from the instrumented pre-run)",
         },
         "series": series,
-        "roofline": {
-            "bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-            "frac": round(achieved / HBM_PEAK_GBS, 4),
-            "traffic": traffic,
-            "algorithmic_bytes_per_launch": int(alg_bytes),
-            "counts": {k: int(inst[k]) for k in ("node_visits", "tri_tests", "layer_tests",
-                                                 "texel_bytes", "primary_rays", "shadow_rays",
-                                                 "bounce_rays")},
-        },
+        "roofline": roof,
         "cpu_baseline": None,
     }
-    if stale:
-        out["roofline"]["traffic_stale"] = True
-    if rec:
-        out["roofline"]["traffic_calibrated"] = bool(rec.get("traffic_calibrated", False))
-        if "traffic_bounds" in rec:
-            out["roofline"]["traffic_bounds"] = rec["traffic_bounds"]
-        # measured HBM bytes per launch over the same kernel time: the share of
-        # the HBM peak the kernel physically uses (the scene is cache-resident)
-        out["roofline"]["measured_hbm_gbs"] = round(traffic / (avg_kernel_ms * 1e-3) / 1e9, 2)
-        out["roofline"]["measured_hbm_frac"] = round(traffic / (avg_kernel_ms * 1e-3) / 1e9
-                                                     / HBM_PEAK_GBS, 4)
-        out["roofline"]["pmc_source"] = f"profiles/pmc_{mode}.json"
-        # the binding resource: VALU issue (and what the waves wait on)
-        ri = issue_roofline(rec, avg_kernel_ms, mode)
-        if ri is not None:
-            out["roofline_issue"] = ri
-    if flat:
-        # the flat list is read from LDS and the scalar cache, never from HBM,
-        # and the kernel prunes with an integer rectangle test: its bound is
-        # VALU issue (measured, profiles/pmc_flat.json).  The work executed per
-        # frame (instrumented image, per wave): rectangle words tested and the
-        # entries some lane lay in (edge + depth tests); the algorithmic list
-        # (every ray x every primitive) is reported beside it
-        work = {"rect_tests_per_wave": int(inst["rect_tests"]), "edge_tests_per_wave": int(inst["edge_tests"]),
-                "list_entries_per_ray_algorithmic": int(inst["tri_tests"])}
-        out["roofline"].pop("algorithmic_bytes_per_launch")
-        if "roofline_issue" in out:
-            ri = out.pop("roofline_issue")
-            out["roofline"] = {**ri, "traffic": traffic, "work_executed": work,
-                               "counts": out["roofline"]["counts"]}
-            if rec:
-                out["roofline"]["measured_hbm_gbs"] = round(traffic / (avg_kernel_ms * 1e-3) / 1e9, 2)
-        else:
-            out["roofline"].update({"bound": "valu_issue", "achieved": None, "frac": None,
-                                    "work_executed": work, "note": "no current PMC record"})
+    if issue is not None:
+        out["roofline_issue"] = issue
     if gather_ok is not None:
         out["config"]["gather_verified"] = gather_ok
     if split is not None:

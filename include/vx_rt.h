@@ -29,8 +29,6 @@ typedef struct {
   uint32_t bvh4_nodes, bvh4_depth, bvh4_stack;  /* the 4-wide BVH collapsed from it */
   uint32_t bvh4_f16;  /* 1: BVH4 boxes rounded outward to binary16, the kernel reads 64-B nodes */
   double parse_ms, bvh_ms;
-  uint32_t bvh8_nodes, bvh8_depth, bvh8_stack;  /* the 8-wide BVH collapsed from it (binary16) */
-  uint32_t pad8;
 } rt_scene_info_t;
 
 #define RT_RENDER_SHADOWS 0x1u
@@ -104,10 +102,6 @@ int rt_scene_export_prims(rt_scene_h scene, float* out, uint64_t count);
 int rt_scene_export_bvh(rt_scene_h scene, float* nodes, float* tris);
 /* 4-wide BVH nodes: float[bvh4_nodes][32] (rt_node4_t); leaves index the same tris */
 int rt_scene_export_bvh4(rt_scene_h scene, float* nodes4);
-/* 8-wide BVH nodes: float[bvh8_nodes][64] -- two rt_node4_t per node (children 0-3,
- * 4-7), the binary16-rounded planes as fp32; leaves index the same tris.  NO
- * REFERENCE (rt_common.h rt_node8h_t). */
-int rt_scene_export_bvh8(rt_scene_h scene, float* nodes8);
 /* fixed-point shading records (rt_prim_t) at width x height: int32[num_prims][32] */
 int rt_scene_setup_prims(rt_scene_h scene, uint32_t width, uint32_t height, int32_t* out,
                          uint64_t count);
@@ -175,11 +169,6 @@ typedef struct {
   uint32_t depth4;      /* BVH4 depth (SAH build; 0 for the LBVH) */
   uint32_t method;      /* RT_BVH_BUILD_* */
   uint32_t pad;
-  uint32_t nodes8;      /* rt_node8h_t records of the BVH8 collapse (0: none -- the LBVH) */
-  uint32_t depth8;      /* BVH8 depth */
-  uint32_t stack8;      /* its worst-case traversal stack; the BVH8 images walk it only when
-                           it fits their stack (RT_STACK_SHALLOW) */
-  uint32_t pad8;
 } rt_bvh_build_stats_t;
 int rt_renderer_build_bvh(rt_renderer_h r, rt_bvh_build_stats_t* stats);  /* = _ex(LBVH) */
 /* RT_BVH_BUILD_LBVH: Morton codes + radix tree (kernels/bvh_build.hip, 19
@@ -209,9 +198,6 @@ int rt_renderer_export_bvh4(rt_renderer_h r, float* nodes4, uint32_t* num_nodes4
 /* the same nodes as 64-B rt_node4h_t records (binary16 planes, the layout the
  * kernels read), num_nodes4 * 64 bytes */
 int rt_renderer_export_bvh4h(rt_renderer_h r, void* nodes4h, uint32_t* num_nodes4);
-/* the renderer's current BVH8 as 128-B rt_node8h_t records (the layout the
- * BVH8 images read), num_nodes8 * 128 bytes; *num_nodes8 = 0 without one */
-int rt_renderer_export_bvh8h(rt_renderer_h r, void* nodes8h, uint32_t* num_nodes8);
 /* the renderer's current BVH (float[num_nodes][16], float[num_tris][12]) */
 int rt_renderer_export_bvh(rt_renderer_h r, float* nodes, float* tris, uint32_t* num_nodes,
                            uint32_t* num_tris);
@@ -243,9 +229,6 @@ typedef struct {
                              frame is one launch group of 2, vortex_hip.h) */
   uint32_t slist_built;   /* 1: the last configure / set_light built shadow lists for a new light
                              (0: the lists of an unchanged light were kept) */
-  uint32_t bvh8;          /* 1: the configured frames' BVH walks run the BVH8 images (rt_bvh8's
-                             shadow packets, pt_kernel8's pair walk): the tree has a BVH8 whose
-                             stack fits them and env RT_BVH8=1 */
   uint32_t pad;
 } rt_setup_stats_t;
 /* (reads back the status of shadow lists queued by rt_renderer_set_light:

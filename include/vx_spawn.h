@@ -43,9 +43,6 @@
 #include "VX_types.h"
 
 #define VX_CHUNK 64          /* tasks per wave */
-#ifndef VX_SLD_PIN
-#define VX_SLD_PIN 0         /* 1: vx_arena::sld_u4n records complete in SGPRs at the load */
-#endif
 #define VX_MAX_GRID 32768    /* blocks per launch (rows of the counter slab) */
 
 /* per-launch device state: one 64-B row of the first VX_MPM_ROW u32 mpm
@@ -130,14 +127,9 @@ struct vx_arena {
         (const __attribute__((address_space(4))) uint4*)(base + o);
 #pragma unroll
     for (int i = 0; i < N; ++i) out[i] = p[i];
-#if VX_SLD_PIN
-    /* every word in an SGPR here: the compiler may not sink parts of the
-     * record's load into the branches that use them (which costs the walk
-     * one dependent scalar round trip per branch level) */
-#pragma unroll
-    for (int i = 0; i < N; ++i)
-      asm volatile("" : "+s"(out[i].x), "+s"(out[i].y), "+s"(out[i].z), "+s"(out[i].w));
-#endif
+    /* (pinning every word in SGPRs at the load, so the compiler cannot sink
+     * parts of it into the branches that use them, measured slower: r06a,
+     * config 3 0.0181 vs 0.0169 ms, BVH walk 0.0355 vs 0.0340) */
   }
   __device__ __forceinline__ float4 ld_f4(uint32_t off) const {
     const auto v = __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0);

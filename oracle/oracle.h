@@ -151,12 +151,6 @@ typedef struct {
   const int32_t* vis_refs;
   int32_t num_vis_leaves;
   const int32_t* vis_pids;
-  /* > 0: the BVH walks (shadow / bounce rays) traverse the 8-wide BVH instead
-   * of nodes4 (the product's RT_BVH8 images: rt_bvh8, pt_kernel8) -- per node
-   * two rt_node4_t halves, children 0-3 then 4-7 [num_nodes8][64]; the
-   * primary rays' packet walk keeps the BVH4 (its vnodes) */
-  int32_t num_nodes8;
-  const float* nodes8;
 } orc_bvh_t;
 
 /* Brute-force (no BVH) reference: closest hit over every geometry triangle,

@@ -70,8 +70,7 @@ class BvhC(C.Structure):
                 ("num_tris", C.c_int32), ("tris", C.POINTER(C.c_float)),
                 ("num_nodes4", C.c_int32), ("nodes4", C.POINTER(C.c_float)),
                 ("num_vis_nodes", C.c_int32), ("vis_refs", C.POINTER(C.c_int32)),
-                ("num_vis_leaves", C.c_int32), ("vis_pids", C.POINTER(C.c_int32)),
-                ("num_nodes8", C.c_int32), ("nodes8", C.POINTER(C.c_float))]
+                ("num_vis_leaves", C.c_int32), ("vis_pids", C.POINTER(C.c_int32))]
 
 
 def build():
@@ -273,10 +272,7 @@ def rt_params(width, height, shadows=True, light=(0.0, 60.0, 80.0), nthreads=1,
 
 def rt_render(oscene: OracleScene, params: RtParamsC, bvh=None, vis_tree=None):
     """bvh: None (brute force), (nodes float32[N,16], tris float32[M,12]) or
-    (nodes, tris, nodes4 float32[N4,32]) -- the last traverses the 4-wide BVH --
-    or (nodes, tris, nodes4, nodes8 float32[N8,64]): the BVH walks of shadow and
-    bounce rays traverse the 8-wide BVH (the RT_BVH8 images), primary packets
-    the BVH4.
+    (nodes, tris, nodes4 float32[N4,32]) -- the last traverses the 4-wide BVH.
     vis_tree: the primary rays' tree (refs int32[N,4], leaf pids int32[M]) as
     the product exports it (Renderer.export_vis_tree); None = walk the BVH
     (the frame is the same either way, the traversal counters are not)."""
@@ -296,9 +292,6 @@ def rt_render(oscene: OracleScene, params: RtParamsC, bvh=None, vis_tree=None):
         if len(bvh) > 2 and bvh[2] is not None:
             nodes4 = np.ascontiguousarray(bvh[2], np.float32)
             b.num_nodes4, b.nodes4 = nodes4.shape[0], _ptr(nodes4, C.c_float)
-        if len(bvh) > 3 and bvh[3] is not None:  # the BVH8 (RT_BVH8 images) for the BVH walks
-            nodes8 = np.ascontiguousarray(bvh[3], np.float32).reshape(-1, 64)
-            b.num_nodes8, b.nodes8 = nodes8.shape[0], _ptr(nodes8, C.c_float)
         if vis_tree is not None and len(vis_tree[0]):
             vrefs = np.ascontiguousarray(vis_tree[0], np.int32)
             vpids = np.ascontiguousarray(vis_tree[1], np.int32)

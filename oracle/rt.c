@@ -245,50 +245,6 @@ static int32_t bvh4_step(const float* n, const ray_pre_t* r, float tmin, float l
   return ref[0];
 }
 
-/* BVH8 node step (the RT_BVH8 images: rt_trace.h node8_coop -- the lane
- * pair's closest-hit step -- and occluded_packet8 -- the any-hit packet walk,
- * slot order): the same as bvh4_step over 8 children (two rt_node4_t halves,
- * children 0-3 and 4-7), the closest-hit keys ordered by Batcher's 19-
- * comparator odd-even merge sort network (strict <), the others pushed
- * farthest first. */
-static int32_t bvh8_step(const float* n, const ray_pre_t* r, float tmin, float lim, int anyhit,
-                         int32_t* stack, int* sp) {
-  float key[8];
-  int32_t ref[8];
-  int cnt = 0;
-  for (int i = 0; i < 8; ++i) {
-    const float* h = n + 32 * (i >> 2);
-    const int j = i & 3;
-    memcpy(&ref[i], &h[24 + j], 4);
-    float lo[3], hi[3];
-    for (int k = 0; k < 3; ++k) {
-      lo[k] = fmaf(h[8 * k + j], r->inv[k], -r->oi[k]);
-      hi[k] = fmaf(h[8 * k + 4 + j], r->inv[k], -r->oi[k]);
-    }
-    const float t0 = fminf(lo[0], hi[0]), t1 = fminf(lo[1], hi[1]), t2 = fminf(lo[2], hi[2]);
-    const float u0 = fmaxf(lo[0], hi[0]), u1 = fmaxf(lo[1], hi[1]), u2 = fmaxf(lo[2], hi[2]);
-    const float tn = fmaxf(fmaxf(t0, t1), fmaxf(t2, tmin));
-    const float tf = fminf(fminf(u0, u1), fminf(u2, lim));
-    const int hit = ref[i] != BVH_EMPTY && tn <= tf;
-    key[i] = hit ? (anyhit ? (float)i : fminf(tn, FLT_MAX)) : INFINITY;
-    cnt += hit;
-  }
-  static const int net[19][2] = {{0, 1}, {2, 3}, {4, 5}, {6, 7}, {0, 2}, {1, 3}, {4, 6},
-                                 {5, 7}, {1, 2}, {5, 6}, {0, 4}, {1, 5}, {2, 6}, {3, 7},
-                                 {2, 4}, {3, 5}, {1, 2}, {3, 4}, {5, 6}};
-  for (int e = 0; e < 19; ++e) {
-    const int a = net[e][0], b = net[e][1];
-    if (key[b] < key[a]) {
-      const float tk = key[a]; key[a] = key[b]; key[b] = tk;
-      const int32_t tr = ref[a]; ref[a] = ref[b]; ref[b] = tr;
-    }
-  }
-  if (cnt == 0) return BVH_EMPTY;
-  for (int i = cnt - 1; i >= 1; --i)
-    if (*sp < BVH_STACK) stack[(*sp)++] = ref[i];
-  return ref[0];
-}
-
 /* closest (anyhit=0) or any (anyhit=1) hit; returns hit pid or -1 */
 static int bvh_trace(const rt_ctx_t* c, const float o[3], const float d[3], float tmin,
                      float tmax, int anyhit, int skip_pid, float* t_out,
@@ -303,12 +259,7 @@ static int bvh_trace(const rt_ctx_t* c, const float o[3], const float d[3], floa
   float bt = tmax;
   int bpid = -1;
   for (;;) {
-    if (ref >= 0 && b->num_nodes8 > 0) {
-      ++*visits;
-      const int32_t nx = bvh8_step(b->nodes8 + (size_t)ref * 64, &rp, tmin, anyhit ? tmax : bt,
-                                   anyhit, stack, &sp);
-      if (nx != BVH_EMPTY) { ref = nx; continue; }
-    } else if (ref >= 0 && b->num_nodes4 > 0) {
+    if (ref >= 0 && b->num_nodes4 > 0) {
       ++*visits;
       const int32_t nx = bvh4_step(b->nodes4 + (size_t)ref * 32, &rp, tmin, anyhit ? tmax : bt,
                                    anyhit, stack, &sp);

@@ -18,9 +18,10 @@ Recomputed:
 and compared with the line (which uses the HIP-event average of its own timed
 launches): each must agree within --tol (default 5 %).
 
-The line's series entry `bvh_walk` (config 3 by BVH traversal, image rt_bvh)
-is checked the same way against the summary's vx_main_rt_bvh row and
---pmc-bvh (profiles/pmc_bvh.json) when both are there.
+The line's series entries (bvh_walk: config 3 by BVH traversal, image
+rt_bvh; path: config 4; flat: config 2; strong_4096: config 5's frame on one
+GPU) are checked the same way against their own images' dispatches and the
+PMC records they cite.
 
 Usage: check_roofline.py <bench.json> <kernel_stats.csv> [--pmc profiles/pmc_shadow.json]
        [--trace <kernel_trace.csv[.gz]>]  (default: the stats path with kernel_stats -> kernel_trace)"""
@@ -47,6 +48,25 @@ def load_line(path):
 def mode_of(line):
     m = line["metric"]
     return "path" if "path trace" in m else ("flat" if "flat" in m else "shadow")
+
+
+def timed_runs(path, kname, steps, max_gap_ns=100000):
+    """Every run of >= `steps` consecutive `kname` dispatches with no other
+    kernel between them and no idle gap of max_gap_ns or more (see
+    timed_region): the average duration (s) of each run's first `steps`."""
+    f = gzip.open(path, "rt") if path.endswith(".gz") else open(path)
+    ks = sorted(((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r["Kernel_Name"])
+                 for r in csv.DictReader(f)), key=lambda t: t[0])
+    runs, run = [], []
+    for st, en, nm in ks + [(0, 0, "")]:
+        if nm == kname and (not run or st - run[-1][1] < max_gap_ns):
+            run.append((st, en))
+            continue
+        if len(run) >= steps:
+            d = [e - b for b, e in run[:steps]]
+            runs.append(sum(d) / len(d) * 1e-9)
+        run = [(st, en)] if nm == kname else []
+    return runs
 
 
 def timed_region(path, kname, steps, max_gap_ns=100000):
@@ -79,7 +99,6 @@ def main():
     ap.add_argument("bench")
     ap.add_argument("stats")
     ap.add_argument("--pmc", default=None)
-    ap.add_argument("--pmc-bvh", default="profiles/pmc_bvh.json")
     ap.add_argument("--tol", type=float, default=0.05)
     ap.add_argument("--trace", default=None)
     a = ap.parse_args()
@@ -134,25 +153,47 @@ def main():
     if issue is not None and issue.get("frac") is not None:
         check("roofline_issue.frac", pmc["sq"]["SQ_INSTS_VALU"] / dur_s / 1e9 / VALU_ISSUE_PEAK_GIPS,
               issue["frac"])
-    # the N=1 series entry timing config 3 by BVH traversal only (image rt_bvh)
-    sb = line.get("series", {}).get("bvh_walk")
-    if sb is not None and "vx_main_rt_bvh" in rows:
-        db = float(rows["vx_main_rt_bvh"]["AverageNs"]) * 1e-9
-        out["bvh_walk"] = {"rocprof_calls": int(rows["vx_main_rt_bvh"]["Calls"]),
-                           "rocprof_avg_ms": round(db * 1e3, 5), "line_kernel_ms": sb["kernel_ms"]}
+    # the N = 1 series entries (bvh_walk, path, flat, strong_4096), each
+    # against its own image's dispatches: from the trace, the first run of
+    # the entry's steps within a factor 1.5 of its kernel clock (strong_4096
+    # shares rt_kernel with the headline: its 4096^2 frames are ~10x
+    # longer); without a trace, the summary row of an image no other entry
+    # uses
+    users = {}
+    for name, sb in line.get("series", {}).items():
+        if isinstance(sb, dict) and "image" in sb:
+            users.setdefault(sb["image"].split("entry ")[-1].rstrip(")"), []).append(name)
+    for name, sb in line.get("series", {}).items():
+        if not isinstance(sb, dict) or "roofline" not in sb or "image" not in sb:
+            continue
+        kn = sb["image"].split("entry ")[-1].rstrip(")")
+        if kn not in rows:
+            continue
+        db = None
+        if tpath != a.stats and os.path.exists(tpath):
+            near = [d for d in timed_runs(tpath, kn, int(sb["steps"]))
+                    if 1 / 1.5 < d * 1e3 / sb["kernel_ms"] < 1.5]
+            db = near[0] if near else None
+        if db is None and kn != knames[0] and len(users.get(kn, [])) == 1:
+            db = float(rows[kn]["AverageNs"]) * 1e-9
+        if db is None:
+            continue
+        out[name] = {"kernel": kn, "rocprof_avg_ms": round(db * 1e3, 5), "line_kernel_ms": sb["kernel_ms"]}
         br = sb["roofline"]
-        check("series.bvh_walk.roofline.frac", br["algorithmic_bytes_per_launch"] / db / 1e9 / HBM_PEAK_GBS,
-              br["frac"])
+        src = br.get("pmc_source") or (sb.get("roofline_issue") or {}).get("source", "").split(" ")[0]
         try:
-            pb = json.load(open(a.pmc_bvh))
+            pb = json.load(open(src)) if src else None
         except OSError:
             pb = None
-        if pb is not None and br.get("measured_hbm_frac") is not None:
-            check("series.bvh_walk.roofline.measured_hbm_frac", pb["traffic_bytes"] / db / 1e9 / HBM_PEAK_GBS,
-                  br["measured_hbm_frac"])
-        bi = sb.get("roofline_issue")
-        if pb is not None and bi:
-            check("series.bvh_walk.roofline_issue.frac", pb["sq"]["SQ_INSTS_VALU"] / db / 1e9 / VALU_ISSUE_PEAK_GIPS,
+        if br.get("bound") == "hbm":
+            check(f"series.{name}.roofline.frac", br["algorithmic_bytes_per_launch"] / db / 1e9 / HBM_PEAK_GBS,
+                  br["frac"])
+            if pb is not None and br.get("measured_hbm_frac") is not None:
+                check(f"series.{name}.roofline.measured_hbm_frac", pb["traffic_bytes"] / db / 1e9 / HBM_PEAK_GBS,
+                      br["measured_hbm_frac"])
+        bi = sb.get("roofline_issue") or (br if br.get("bound") == "valu_issue" else None)
+        if pb is not None and bi and bi.get("frac") is not None:
+            check(f"series.{name}.roofline_issue.frac", pb["sq"]["SQ_INSTS_VALU"] / db / 1e9 / VALU_ISSUE_PEAK_GIPS,
                   bi["frac"])
     out["ok"] = ok
     print(json.dumps(out, indent=1))

@@ -27,21 +27,28 @@ CSRC = os.path.join(ROOT, "skybox_rt_amd", "csrc")
 KDIR = os.path.join(CSRC, "kernels")
 FILES = ["rt_trace.h", "rt_kernel.hip", "pt_kernel.hip"]
 
-RT_DEFS = "-DRT_ONLY_BVH4H=1 -DRT_BLOCK_THREADS=256 -DRT_BLOCK_LIST=1"
-PT_DEFS = "-DRT_ONLY_BVH4H=1 -DRT_PUSH_UNCOND=1 -DRT_LAZY_TASK_ARGS=0"
-FLAT_DEFS = "-DRT_FLAT=1 -DRT_BLOCK_THREADS=256 -DRT_FLAT_RECT_LDS=1"
-# (source, defines) of every shipped image (Makefile IMAGES) and the
-# diagnostic stamp images (Makefile diag)
+# the shipped images' defines (skybox_rt_amd/csrc/Makefile: IMAGES and diag)
+RT_BASE = "-DRT_ONLY_BVH4H=1"
+RT_DEFS = RT_BASE + " -DRT_BLOCK_THREADS=128"
+BVH_DEFS = RT_BASE + " -DRT_BLOCK_THREADS=256 -DRT_BVH_WALK=1"
+PT_DEFS = "-DRT_ONLY_BVH4H=1 -DRT_PUSH_UNCOND=1 -DRT_LAZY_TASK_ARGS=0 -DVX_ROWS_GATE=0"
+FLAT_DEFS = "-DRT_FLAT=1 -DRT_BLOCK_THREADS=512"
+# (source, defines) of every shipped image and the diagnostic stamp images
 CONFIGS = []
 for inst in ("", " -DRT_INSTRUMENT"):
     CONFIGS += [
         ("rt_kernel.hip", RT_DEFS + inst),
-        ("rt_kernel.hip", "-DRT_MAX_STACK=32 -DRT_BLOCK_LIST=1" + inst),
+        ("rt_kernel.hip", BVH_DEFS + inst),
+        ("rt_kernel.hip", "-DRT_MAX_STACK=32" + inst),
         ("rt_kernel.hip", FLAT_DEFS + inst),
-        ("rt_kernel.hip", RT_DEFS + " -DRT_STAMPS -DRT_BLOCK_THREADS=64" + inst),
+        ("rt_kernel.hip", RT_DEFS + " -DRT_PATHQ=1" + inst),
+        ("rt_kernel.hip", RT_BASE + " -DRT_BLOCK_THREADS=64 -DRT_STAMPS" + inst),
+        ("rt_kernel.hip", RT_BASE + " -DRT_BLOCK_THREADS=64 -DRT_BVH_WALK=1 -DRT_STAMPS" + inst),
+        ("rt_kernel.hip", FLAT_DEFS + " -DRT_STAMPS" + inst),
         ("pt_kernel.hip", PT_DEFS + inst),
         ("pt_kernel.hip", "-DRT_MAX_STACK=32" + inst),
         ("pt_kernel.hip", "-DPT_MODE=0" + inst),
+        ("pt_kernel.hip", PT_DEFS + " -DPT_MODE=2 -DPT_PAIR=0" + inst),
         ("pt_kernel.hip", PT_DEFS + " -DRT_STAMPS -DRT_TRACE_CYCLES" + inst),
     ]
 

@@ -279,14 +279,16 @@ class Builder {
   bool all_axes_;
 };
 
-// Collapse the BVH2 into a BVH4 (W = 4) or BVH8 (W = 8): a node's children
-// are repeatedly replaced by the children of its largest-area internal child
-// (in place, so the order stays left to right) until it has W or none is
-// internal.  Boxes are copied verbatim from the BVH2 nodes that stored them.
-// Nodes are numbered in preorder.  W = 4 fills nodes4 (rt_node4_t); W = 8
-// fills nodes8 (two rt_node4_t halves per node, children 0-3 and 4-7).
+// Collapse the BVH2 into a BVH4 (W = 4): a node's children are repeatedly
+// replaced by the children of its largest-area internal child (in place, so
+// the order stays left to right) until it has W or none is internal.  Boxes
+// are copied verbatim from the BVH2 nodes that stored them.  Nodes are
+// numbered in preorder into nodes4 (rt_node4_t).  (An 8-wide collapse, walked
+// by opt-in BVH8 images, measured slower than the BVH4 everywhere in r05 and
+// was removed in r06: DESIGN.md 2.8.)
 template <int W>
 class Collapser {
+  static_assert(W == 4, "rt_node4_t: four children per node");
  public:
   explicit Collapser(Bvh* b) : b_(b) {}
   void run() {
@@ -302,9 +304,9 @@ class Collapser {
   }
 
  private:
-  std::vector<rt_node4_t>& out() { return W == 4 ? b_->nodes4 : b_->nodes8; }
-  uint32_t& depth() { return W == 4 ? b_->depth4 : b_->depth8; }
-  uint32_t& stack() { return W == 4 ? b_->stack4 : b_->stack8; }
+  std::vector<rt_node4_t>& out() { return b_->nodes4; }
+  uint32_t& depth() { return b_->depth4; }
+  uint32_t& stack() { return b_->stack4; }
   struct Child {
     float lo[3], hi[3];
     int32_t ref;
@@ -411,7 +413,6 @@ int BuildBvhWith(const std::vector<BuildTri>& tris, const BvhParams& bp, Bvh* ou
   Builder b(tris, out, bp);
   b.run();
   Collapser<4>(out).run();
-  Collapser<8>(out).run();
   // binary16 box planes: round every BVH4 box outward (RT_BVH_F16=0 keeps
   // the fp32 planes, rt_node4h_t is then not uploaded), pack rt_node4h_t and
   // check that it decodes to exactly rt_node4_t's planes
@@ -436,25 +437,6 @@ int BuildBvhWith(const std::vector<BuildTri>& tris, const BvhParams& bp, Bvh* ou
         }
       std::memcpy(h.child, &o.v[24], 16);
     }
-    // the BVH8's halves the same way (from the same fp32 BVH2 boxes)
-    out->nodes8h.resize(out->nodes8.size() / 2);
-    for (size_t n = 0; n < out->nodes8.size(); ++n) {
-      rt_node4_t& o = out->nodes8[n];
-      rt_node4h_t& h = out->nodes8h[n / 2].half[n % 2];
-      for (int q = 0; q < 24; ++q) {
-        float& v = o.v[q];
-        v = HalfRound(v, (q & 4) ? +1 : -1);
-        h.b[q] = HalfBits(v);
-        if (HalfValue(h.b[q]) != v) {
-          if (error) *error = "binary16 box packing mismatch (BVH8)";
-          return -1;
-        }
-      }
-      std::memcpy(h.child, &o.v[24], 16);
-    }
-  } else {
-    out->nodes8.clear();  // the BVH8 exists in binary16 form only
-    out->depth8 = out->stack8 = 0;
   }
   if (out->depth > RT_STACK_DEEP) {
     if (error) *error = "BVH deeper than RT_STACK_DEEP";

@@ -32,13 +32,6 @@ struct Bvh {
   std::vector<rt_node4h_t> nodes4h;  // the same nodes, binary16 boxes (the kernel's form)
   uint32_t depth4 = 0;
   uint32_t stack4 = 0;           // worst-case traversal stack entries (near-first, BVH4)
-  // BVH8 collapsed from `nodes` by the same rule (up to 8 children), binary16
-  // boxes only (f16_boxes): nodes8 = the fp32 planes as two rt_node4_t per
-  // node (children 0-3, 4-7; the oracle's input), nodes8h = the kernel's form
-  std::vector<rt_node4_t> nodes8;
-  std::vector<rt_node8h_t> nodes8h;
-  uint32_t depth8 = 0;
-  uint32_t stack8 = 0;           // worst-case traversal stack entries (BVH8)
 };
 
 constexpr uint32_t kBvhLeafSize = 4;   // the kernel fetches at most 4 triangles per leaf

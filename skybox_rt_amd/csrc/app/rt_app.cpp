@@ -171,9 +171,6 @@ int rt_scene_info(rt_scene_h s, rt_scene_info_t* info) {
   info->bvh4_f16 = s->bvh.nodes4h.empty() ? 0u : 1u;
   info->parse_ms = s->parse_ms;
   info->bvh_ms = s->bvh_ms;
-  info->bvh8_nodes = (uint32_t)s->bvh.nodes8h.size();
-  info->bvh8_depth = s->bvh.depth8;
-  info->bvh8_stack = s->bvh.stack8;
   return 0;
 }
 
@@ -203,13 +200,6 @@ int rt_scene_export_bvh4(rt_scene_h s, float* nodes4) {
   if (!s || !nodes4) return fail("null argument");
   if (rtapp::host_bvh(s) != 0) return -1;
   std::memcpy(nodes4, s->bvh.nodes4.data(), s->bvh.nodes4.size() * sizeof(rt_node4_t));
-  return 0;
-}
-
-int rt_scene_export_bvh8(rt_scene_h s, float* nodes8) {
-  if (!s || !nodes8) return fail("null argument");
-  if (rtapp::host_bvh(s) != 0) return -1;
-  std::memcpy(nodes8, s->bvh.nodes8.data(), s->bvh.nodes8.size() * sizeof(rt_node4_t));
   return 0;
 }
 
@@ -335,17 +325,6 @@ int rt_renderer_create(rt_scene_h s, const char* kernel_dir, rt_renderer_h* out)
       if (vx_upload_kernel_file(r->dev, path.c_str(), &r->krnl_bvh[i]) != 0)
         return fail("cannot upload kernel " + path);
     }
-    // the BVH8 images (kernel directory or the library's)
-    const char* b8_names[2][2] = {{"rt_bvh8.vxbin", "rt_bvh8_stats.vxbin"},
-                                  {"pt_kernel8.vxbin", "pt_kernel8_stats.vxbin"}};
-    for (int m = 0; m < 2; ++m)
-      for (int i = 0; i < 2; ++i) {
-        std::string path = dir + "/" + b8_names[m][i];
-        if (FILE* f = std::fopen(path.c_str(), "rb")) std::fclose(f);
-        else path = lib_dir() + "/" + b8_names[m][i];
-        if (vx_upload_kernel_file(r->dev, path.c_str(), m ? &r->krnl_pt8[i] : &r->krnl_bvh8[i]) != 0)
-          return fail("cannot upload kernel " + path);
-      }
   }
   rt_kernel_arg_t& a = r->arg;
   std::memset(&a, 0, sizeof(a));
@@ -369,11 +348,6 @@ int rt_renderer_create(rt_scene_h s, const char* kernel_dir, rt_renderer_h* out)
   a.num_nodes = (uint32_t)bvh.nodes.size();
   a.num_nodes4 = (uint32_t)bvh.nodes4.size();
   r->num_tris = (uint32_t)bvh.tris.size();
-  // the BVH8 (binary16 records) for the BVH8 images, when its stack fits them
-  if (upload(r->dev, bvh.nodes8h.data(), bvh.nodes8h.size() * sizeof(rt_node8h_t), &r->nodes8, &a.nodes8_addr))
-    return -1;
-  r->num_nodes8_built = (uint32_t)bvh.nodes8h.size();
-  a.num_nodes8 = bvh.stack8 <= RT_STACK_SHALLOW ? r->num_nodes8_built : 0u;
   a.num_geom = (uint32_t)s->geometry.size();
   // the resolution-independent device-setup inputs, and every primitive's
   // clip-space triangle by pid (path-trace bounce hits) + the geometry
@@ -433,9 +407,6 @@ int rt_renderer_create(rt_scene_h s, const char* kernel_dir, rt_renderer_h* out)
     r->bvh_stats.stack4 = bvh.stack4;
     r->bvh_stats.nodes4 = (uint32_t)bvh.nodes4.size();
     r->bvh_stats.depth4 = bvh.depth4;
-    r->bvh_stats.nodes8 = (uint32_t)bvh.nodes8h.size();
-    r->bvh_stats.depth8 = bvh.depth8;
-    r->bvh_stats.stack8 = bvh.stack8;
     r->bvh_stats.build_ms = s->bvh_ms;
     r->bvh_stats.method = RT_BVH_BUILD_HOST;
   }
@@ -868,8 +839,6 @@ static int host_setup(rt_renderer* r, const rt_render_params_t* p, bool raster, 
   return 0;
 }
 
-static bool use_bvh8(const rt_renderer* r);
-
 int rt_renderer_configure(rt_renderer_h r, const rt_render_params_t* p) {
   if (!r || !p) return fail("null argument");
   if (p->width == 0 || p->height == 0 || p->width > 32768 || p->height > 32768)
@@ -924,8 +893,6 @@ int rt_renderer_configure(rt_renderer_h r, const rt_render_params_t* p) {
   a.quad_tiles = 0;
   const bool order_on = !raster && r->local_tiles > 0 &&
                         !(std::getenv("RT_TILE_ORDER") && std::atoi(std::getenv("RT_TILE_ORDER")) == 0);
-  // the BVH8 images (rt_bvh8, pt_kernel8) on request: env RT_BVH8=1
-  r->bvh8_env = std::getenv("RT_BVH8") && std::atoi(std::getenv("RT_BVH8")) != 0;
   bool use_bvh4 = !(p->flags & RT_RENDER_BVH2) && (!r->gpu_bvh || r->gpu_bvh4);
   if (const char* e = std::getenv("RT_BVH_WIDTH")) use_bvh4 = use_bvh4 && std::atoi(e) != 2;
   r->use_bvh4 = use_bvh4;
@@ -1061,19 +1028,10 @@ int rt_renderer_configure(rt_renderer_h r, const rt_render_params_t* p) {
   r->setup.blist_blocks = a.blist_blocks;
   r->setup.slist_on = a.slist_on;
   r->setup.path_queue = r->pq ? 1u : 0u;
-  r->setup.bvh8 = use_bvh8(r) ? 1u : 0u;
   r->setup.setup_ms = setup_ms;
   r->setup.configure_ms = ms_since(t0);
   r->configured = true;
   return 0;
-}
-
-// the configured frame walks the BVH8 (RT_BVH8 images): the tree has one
-// whose stack fits them, the regular (binary16 BVH4) images are in use, and
-// env RT_BVH8 does not say 0
-static bool use_bvh8(const rt_renderer* r) {
-  return r->bvh8_env && r->arg.num_nodes8 > 0 && !r->deep && (r->arg.flags & RT_FLAG_BVH4H) && r->krnl_bvh8[0] &&
-         r->krnl_pt8[0];
 }
 
 int rt_render_start(rt_renderer_h r) {
@@ -1097,11 +1055,7 @@ int rt_render_start(rt_renderer_h r) {
   // (the deep images walk every layout with the list code paths idle)
   const bool bvh = mode == 0 && (f & RT_RENDER_BVH_WALK) && !r->deep && (r->arg.flags & RT_FLAG_BVH4H) &&
                    r->krnl_bvh[k];
-  // the BVH8 images when the tree has a usable BVH8 (rt_bvh8: the BVH-walk
-  // frame's shadow packets; pt_kernel8: the path tracer's pair walk)
-  const bool b8 = use_bvh8(r);
-  vx_buffer_h img = bvh ? (b8 ? r->krnl_bvh8[k] : r->krnl_bvh[k])
-                        : (mode == 1 && b8 ? r->krnl_pt8[k] : r->krnl[mode][k]);
+  vx_buffer_h img = bvh ? r->krnl_bvh[k] : r->krnl[mode][k];
   return vx_start(r->dev, img, r->args) == 0 ? 0 : fail("vx_start failed");
 }
 
@@ -1361,15 +1315,10 @@ static int build_lbvh(rt_renderer_h r, rt_bvh_build_stats_t* st) {
   if (r->nodes) vx_mem_free(r->nodes);
   if (r->tris) vx_mem_free(r->tris);
   if (r->nodes4) vx_mem_free(r->nodes4);
-  if (r->nodes8) vx_mem_free(r->nodes8);  // the LBVH has no BVH8: the BVH8 images are not used
   r->nodes = nodes_out.h;
   r->tris = tris_out.h;
   r->nodes4 = nodes4_out.h;
-  r->nodes8 = nullptr;
   nodes_out.h = tris_out.h = nodes4_out.h = nullptr;
-  r->num_nodes8_built = 0;
-  r->arg.nodes8_addr = 0;
-  r->arg.num_nodes8 = 0;
   r->arg.nodes_addr = nodes_addr;
   r->arg.tris_addr = tris_addr;
   r->arg.num_nodes = nn;
@@ -1432,8 +1381,7 @@ static int build_sah(rt_renderer_h r, rt_bvh_build_stats_t* st) {
       {&a.segs_addr[0], N * 16},   {&a.segs_addr[1], N * 16},   {&a.small_addr[0], N * 16},
       {&a.small_addr[1], N * 16},  {&a.nrec_addr, N * 16},      {&a.nbox_addr, N * 64},
       {&a.cnt_addr, (N + 1) * 4},  {&a.d0_addr, N * 4},         {&a.parent_addr, N * 4},
-      {&a.cs_addr, N * 32},        {&a.is4_addr, (N + 1) * 4},  {&a.ctl_addr, SAH_CTL_WORDS * 4},
-      {&a.cs8_addr, N * 64},       {&a.is8_addr, (N + 1) * 4}};
+      {&a.cs_addr, N * 32},        {&a.is4_addr, (N + 1) * 4},  {&a.ctl_addr, SAH_CTL_WORDS * 4}};
   uint64_t total = 0;
   for (const auto& pt : parts) total += (pt.second + 255) & ~255ull;
   if (r->su.sah_bytes < total || !r->su.sah.h) {
@@ -1449,9 +1397,9 @@ static int build_sah(rt_renderer_h r, rt_bvh_build_stats_t* st) {
   }
   const uint64_t ctl_off = a.ctl_addr - r->su.sah.addr;
   // the outputs, sized for the largest tree n triangles make (BFS ids < n)
-  vx_buffer_h nodes_h = nullptr, tris_h = nullptr, nodes4_h = nullptr, nodes8_h = nullptr;
-  uint64_t nodes_addr = 0, tris_addr = 0, nodes4_addr = 0, nodes8_addr = 0;
-  DevBuf nodes_out, tris_out, nodes4_out, nodes8_out;  // owned here until handed to the renderer
+  vx_buffer_h nodes_h = nullptr, tris_h = nullptr, nodes4_h = nullptr;
+  uint64_t nodes_addr = 0, tris_addr = 0, nodes4_addr = 0;
+  DevBuf nodes_out, tris_out, nodes4_out;  // owned here until handed to the renderer
   const uint64_t nmax = std::max<uint64_t>(N, 1);
   if (upload(r->dev, nullptr, nmax * sizeof(rt_node_t), &nodes_h, &nodes_addr)) return -1;
   nodes_out.h = nodes_h;
@@ -1460,14 +1408,6 @@ static int build_sah(rt_renderer_h r, rt_bvh_build_stats_t* st) {
   if (upload(r->dev, nullptr, nmax * (sizeof(rt_node4_t) + sizeof(rt_node4h_t)), &nodes4_h, &nodes4_addr))
     return -1;
   nodes4_out.h = nodes4_h;
-  // the BVH8 collapse only when the BVH8 images may run (env RT_BVH8=1 when
-  // the tree is built): its four phases are a quarter of a rebuild's launches
-  const bool want8 = std::getenv("RT_BVH8") && std::atoi(std::getenv("RT_BVH8")) != 0;
-  if (want8) {
-    if (upload(r->dev, nullptr, nmax * sizeof(rt_node8h_t), &nodes8_h, &nodes8_addr)) return -1;
-    nodes8_out.h = nodes8_h;
-  }
-  a.nodes8_addr = nodes8_addr;
   a.geom_addr = r->arg.geom_addr;
   a.nodes_addr = nodes_addr;
   a.tris_addr = tris_addr;
@@ -1529,8 +1469,6 @@ static int build_sah(rt_renderer_h r, rt_bvh_build_stats_t* st) {
     // while that level still holds segments (a partial tree, bvh_sah.hip)
     for (const uint32_t ph : {SAH_NUMBER, SAH_SCAN, SAH_EMIT, SAH_CS, SAH_MARK, SAH_SCAN4, SAH_EMIT4})
       seq.push_back(SAH_SEQ(ph, lend));
-    if (want8)
-      for (const uint32_t ph : {SAH_CS8, SAH_MARK8, SAH_SCAN8, SAH_EMIT8}) seq.push_back(SAH_SEQ(ph, lend));
     const auto tr = std::chrono::steady_clock::now();
     if (run(seq) || vx_copy_from_dev(c, r->su.sah.h, ctl_off, sizeof(c)) != 0)
       return fail("SAH build: launch or read-back failed");
@@ -1550,17 +1488,10 @@ static int build_sah(rt_renderer_h r, rt_bvh_build_stats_t* st) {
   if (r->nodes) vx_mem_free(r->nodes);
   if (r->tris) vx_mem_free(r->tris);
   if (r->nodes4) vx_mem_free(r->nodes4);
-  if (r->nodes8) vx_mem_free(r->nodes8);
   r->nodes = nodes_out.h;
   r->tris = tris_out.h;
   r->nodes4 = nodes4_out.h;
-  r->nodes8 = nodes8_out.h;
-  nodes_out.h = tris_out.h = nodes4_out.h = nodes8_out.h = nullptr;
-  // the BVH8 for the BVH8 images when its stack fits them
-  const uint32_t nn8 = want8 ? c[SAH_CTL_NODES8] : 0u, stack8 = want8 ? c[SAH_CTL_STACK8] : 0u;
-  r->num_nodes8_built = nn8;
-  r->arg.nodes8_addr = nodes8_addr;
-  r->arg.num_nodes8 = stack8 <= RT_STACK_SHALLOW ? nn8 : 0u;
+  nodes_out.h = tris_out.h = nodes4_out.h = nullptr;
   r->arg.nodes_addr = nodes_addr;
   r->arg.tris_addr = tris_addr;
   r->arg.num_nodes = nn;
@@ -1579,9 +1510,6 @@ static int build_sah(rt_renderer_h r, rt_bvh_build_stats_t* st) {
     st->build_ms = ms_since(t0);
     st->nodes4 = nn4;
     st->depth4 = c[SAH_CTL_DEPTH4];
-    st->nodes8 = nn8;
-    st->depth8 = want8 ? c[SAH_CTL_DEPTH8] : 0u;
-    st->stack8 = stack8;
     st->method = RT_BVH_BUILD_SAH;
   }
   if (r->configured) {
@@ -1627,15 +1555,6 @@ int rt_renderer_export_bvh4h(rt_renderer_h r, void* nodes4h, uint32_t* num_nodes
   const uint64_t n4 = r->arg.num_nodes4;
   if (nodes4h && n4 &&
       vx_copy_from_dev(nodes4h, r->nodes4, n4 * sizeof(rt_node4_t), n4 * sizeof(rt_node4h_t)) != 0)
-    return fail("vx_copy_from_dev failed");
-  return 0;
-}
-
-int rt_renderer_export_bvh8h(rt_renderer_h r, void* nodes8h, uint32_t* num_nodes8) {
-  if (!r) return fail("null argument");
-  const uint64_t n8 = r->num_nodes8_built;
-  if (num_nodes8) *num_nodes8 = (uint32_t)n8;
-  if (nodes8h && n8 && vx_copy_from_dev(nodes8h, r->nodes8, 0, n8 * sizeof(rt_node8h_t)) != 0)
     return fail("vx_copy_from_dev failed");
   return 0;
 }

@@ -64,14 +64,6 @@ struct rt_renderer {
   // RT_RENDER_BVH_WALK primary+shadow frames (binary16 BVH4 images only):
   // rt_bvh / rt_bvh_stats, the packet walks without the list code paths
   vx_buffer_h krnl_bvh[2] = {};
-  // the BVH8 images (kernels built with RT_BVH8: rt_bvh8 -- the BVH-walk
-  // primary+shadow frame with BVH8 shadow packets --, pt_kernel8 -- the path
-  // tracer's pair walk on the BVH8), used when the tree has a BVH8 whose
-  // stack fits them (env RT_BVH8=0: the BVH4 images)
-  vx_buffer_h krnl_bvh8[2] = {}, krnl_pt8[2] = {};
-  vx_buffer_h nodes8 = nullptr;  // rt_node8h_t records
-  uint32_t num_nodes8_built = 0;  // BVH8 records of the current tree (arg.num_nodes8: 0 when unused)
-  bool bvh8_env = false;          // env RT_BVH8 at the last configure (1: the BVH8 images)
   vx_buffer_h sah_krnl = nullptr;  // bvh_sah.vxbin, loaded by the first device build
   vx_buffer_h pathq = nullptr, pathq_ctr = nullptr;
   bool pq = false;          // the configuration runs the two-kernel path tracer
@@ -137,8 +129,7 @@ struct rt_renderer {
                            &setup_krnl, &verts, &pdc, &dcz, &layer_list, &geometry_list, &vis,
                            &blist, &bidx, &sidx, &slist, &krnl_pq[0][0], &krnl_pq[0][1],
                            &krnl_pq[1][0], &krnl_pq[1][1], &pathq, &pathq_ctr,
-                           &krnl_bvh[0], &krnl_bvh[1], &sah_krnl, &krnl_bvh8[0], &krnl_bvh8[1],
-                           &krnl_pt8[0], &krnl_pt8[1], &nodes8};
+                           &krnl_bvh[0], &krnl_bvh[1], &sah_krnl};
     for (auto* b : bufs) {
       if (*b) vx_mem_free(*b);
       *b = nullptr;

@@ -719,12 +719,12 @@ __device__ __forceinline__ double child_area(const Child& c) {
   return 2.0 * (dx * dy + dy * dz + dz * dx);
 }
 
-// the expansion of every BVH2 node for a W-wide collapse (W = 4: cs, W = 8:
-// cs8): W refs, then W sources (node << 1 | slot)
+// the expansion of every BVH2 node for a W-wide collapse (W = 4: cs): W
+// refs, then W sources (node << 1 | slot)
 template <int W>
 __device__ void phase_cs(const sah_arg_t* a) {
   const float* nodes = vx_ptr<const float>(a->nodes_addr);
-  int32_t* cs = vx_ptr<int32_t>(W == 4 ? a->cs_addr : a->cs8_addr);
+  int32_t* cs = vx_ptr<int32_t>(a->cs_addr);
   const uint32_t nn = vx_ptr<const uint32_t>(a->ctl_addr)[SAH_CTL_NODES];
   for (uint32_t p = blockIdx.x * SAH_BLOCK + threadIdx.x; p < nn; p += gridDim.x * SAH_BLOCK) {
     Child c[W];
@@ -774,13 +774,12 @@ __device__ void phase_cs(const sah_arg_t* a) {
 // right after it, so the way up records whether each step came from that
 // child (bit 0) or from the other one (bit 1, its id read from the parent's
 // record on the way down).
-// (W = 8: the BVH8's membership, depth and stack the same way, is8 / cs8)
 template <int W>
 __device__ void phase_mark(const sah_arg_t* a) {
   const int32_t* parent = vx_ptr<const int32_t>(a->parent_addr);
-  const int32_t* cs = vx_ptr<const int32_t>(W == 4 ? a->cs_addr : a->cs8_addr);
+  const int32_t* cs = vx_ptr<const int32_t>(a->cs_addr);
   const int32_t* nodes = vx_ptr<const int32_t>(a->nodes_addr);  // rt_node_t: refs at words 12, 13
-  uint32_t* is4 = vx_ptr<uint32_t>(W == 4 ? a->is4_addr : a->is8_addr);
+  uint32_t* is4 = vx_ptr<uint32_t>(a->is4_addr);
   uint32_t* ctl = vx_ptr<uint32_t>(a->ctl_addr);
   const uint32_t nn = ctl[SAH_CTL_NODES];
   // the BVH4 depth and stack maxima: per lane over its nodes, then one
@@ -857,8 +856,8 @@ __device__ void phase_mark(const sah_arg_t* a) {
     smax = max(smax, (uint32_t)__shfl_xor((int)smax, o, 64));
   }
   if (lane_id() == 0 && dmax != 0) {
-    atomicMax(&ctl[W == 4 ? SAH_CTL_DEPTH4 : SAH_CTL_DEPTH8], dmax);
-    atomicMax(&ctl[W == 4 ? SAH_CTL_STACK4 : SAH_CTL_STACK8], smax);
+    atomicMax(&ctl[SAH_CTL_DEPTH4], dmax);
+    atomicMax(&ctl[SAH_CTL_STACK4], smax);
   }
 }
 
@@ -899,41 +898,6 @@ __device__ void phase_emit4(const sah_arg_t* a) {
   }
 }
 
-// rt_node8h_t at BVH8 preorder indices: each half (children 0-3, 4-7) as
-// an rt_node4_t in registers, its planes rounded outward to binary16 and
-// packed as one rt_node4h_t (half4_node, the BVH4's rounding)
-__device__ void phase_emit8(const sah_arg_t* a) {
-  const float* nodes = vx_ptr<const float>(a->nodes_addr);
-  const int32_t* cs = vx_ptr<const int32_t>(a->cs8_addr);
-  const uint32_t* pre8 = vx_ptr<const uint32_t>(a->is8_addr);
-  uint32_t* out = vx_ptr<uint32_t>(a->nodes8_addr);
-  uint32_t* ctl = vx_ptr<uint32_t>(a->ctl_addr);
-  const uint32_t nn = ctl[SAH_CTL_NODES];
-  if (blockIdx.x == 0 && threadIdx.x == 0) ctl[SAH_CTL_NODES8] = pre8[nn];
-  for (uint32_t m = blockIdx.x * SAH_BLOCK + threadIdx.x; m < nn; m += gridDim.x * SAH_BLOCK) {
-    if (pre8[m + 1] == pre8[m]) continue;  // not a BVH8 node
-    for (int h = 0; h < 2; ++h) {
-      float v[32];
-      for (int i = 0; i < 32; ++i) v[i] = 0.0f;
-      for (int j = 0; j < 4; ++j) {
-        int32_t ref = cs[16 * m + 4 * h + j];
-        const int32_t src = cs[16 * m + 8 + 4 * h + j];
-        if (ref != RT_EMPTY_REF) {
-          const float* sn = nodes + 16ull * (uint32_t)(src >> 1);
-          const int ch = src & 1;
-          for (int k = 0; k < 3; ++k) {
-            v[8 * k + j] = sn[4 * k + 2 * ch];
-            v[8 * k + 4 + j] = sn[4 * k + 2 * ch + 1];
-          }
-          if (ref >= 0) ref = (int32_t)pre8[ref];
-        }
-        v[24 + j] = __int_as_float(ref);
-      }
-      half4_node(v, out + 32ull * pre8[m] + 16 * h);
-    }
-  }
-}
-
 // the numbering's counters as SAH_INIT leaves them, and the collapse's
 // maxima (a sequence that ran its finishing phases before its last level)
 __device__ void phase_reset(const sah_arg_t* a) {
@@ -947,8 +911,6 @@ __device__ void phase_reset(const sah_arg_t* a) {
     uint32_t* ctl = vx_ptr<uint32_t>(a->ctl_addr);
     ctl[SAH_CTL_DEPTH4] = 0;
     ctl[SAH_CTL_STACK4] = 0;
-    ctl[SAH_CTL_DEPTH8] = 0;
-    ctl[SAH_CTL_STACK8] = 0;
     ctl[SAH_CTL_ERR] &= ~2u;
   }
 }
@@ -987,12 +949,6 @@ VX_MAIN(sah_arg_t, arg, SAH_BLOCK) {
     case SAH_SCAN4:
       phase_scan(vx_ptr<uint32_t>(arg->is4_addr), vx_ptr<const uint32_t>(arg->ctl_addr)[SAH_CTL_NODES]);
       break;
-    case SAH_CS8: phase_cs<8>(arg); break;
-    case SAH_MARK8: phase_mark<8>(arg); break;
-    case SAH_SCAN8:
-      phase_scan(vx_ptr<uint32_t>(arg->is8_addr), vx_ptr<const uint32_t>(arg->ctl_addr)[SAH_CTL_NODES]);
-      break;
-    case SAH_EMIT8: phase_emit8(arg); break;
     default: break;
   }
   return 0;

@@ -46,14 +46,8 @@
 // PT_MODE 2 (image pt_queue, with pt_primary): the second kernel of a
 // two-kernel frame -- the compacted path queue the first kernel filled, one
 // path per lane on full waves (rt_trace.h pathq_append).
-#ifndef PT_COOP
-#define PT_COOP 1        // 32-pixel waves with the shadow lists: lane pairs per path
-#endif
 #ifndef PT_PAIR
 #define PT_PAIR 1        // 0: no paired-vertex code (the shadow lists never pair)
-#endif
-#ifndef PT_QUAD
-#define PT_QUAD 0        // 16-pixel waves (split_log 4) with the shadow lists: four lanes per path
 #endif
 #define PT_SKY 0.25f     // radiance of an escaped bounce ray (oracle ORC_PT_SKY)
 #define PT_TRIES 8u      // disk rejection-sampling attempts (ORC_PT_TRIES)
@@ -214,23 +208,17 @@ struct PathState {
   int32_t pid;
   float t;
   float o[3], d[3], T[3], L[3];
-  float n[3];  // PT_CARRY_NRM (lane pairs): the vertex's normal, from the hit that made it
 };
-// 1: the pair form carries the vertex normal from the hit (path_hit has the
-// triangle loaded) instead of loading the triangle again at the next vertex
-#ifndef PT_CARRY_NRM
-#define PT_CARRY_NRM 0
-#endif
+// (the pair form carrying the vertex normal from the hit instead of loading
+// the triangle again at the next vertex measured no gain, r05)
 
 // The next vertex of a path whose bounce ray b from P hit triangle np at t:
 // albedo = the draw3d shader at the hit's MT barycentrics, T *= albedo
-template <bool NRM = false>
 __device__ __forceinline__ void path_hit(const Scene& S, PathState& st, const float P[3], const Ray& b,
                                          int32_t np, float nt, Counters& cnt, bool counted = true) {
   float w0[3], f1[3], f2[3], b1, b2;
   load_tri(S, np, w0, f1, f2);
   mt_bary(b.o, b.d, w0, f1, f2, &b1, &b2);
-  if (NRM) tri_normal(f1, f2, b.d, st.n);  // the next vertex's normal (path_step's)
   gfx::Prim p;
   gfx::load_prim(S.A, S.prims + 128u * (uint32_t)np, p);
   const gfx::DcState dst = gfx::load_dcstate(S.A, S.dcs + 64u * p.dc());
@@ -272,23 +260,19 @@ __device__ __forceinline__ void path_hit(const Scene& S, PathState& st, const fl
 // then (v < bounces) the bounce; returns whether the path continues (st then
 // describes the next vertex), else the pixel is final.  Every lane of the
 // wave calls it; `act` masks the work.  CO 1: the lane pairs of a 32-pixel
-// wave (lane l and l ^ 32 hold the same path, role 1 = the upper lane) trace
-// the shadow ray on its list and the bounce ray together (trace_coop,
-// occluded_list_coop); CO 2: the quads of a 16-pixel wave (lanes 4p ..
-// 4p + 3, role = lane & 3; trace_quad, occluded_list_quad).  Every lane of
-// the group computes the rest, role 0 counts.
+// wave (lanes 2p and 2p + 1 hold the same path, role 1 = the upper lane)
+// trace the shadow ray on its list and the bounce ray together (trace_coop,
+// occluded_list_coop).  Every lane of the pair computes the rest, role 0
+// counts.  (Quads of four lanes per path in 16-pixel waves measured slower,
+// r04-r05, and were removed in r06.)
 template <int CO>
 __device__ __forceinline__ bool path_step(const Scene& S, int32_t* stack, PathState& st, uint32_t v,
                                           bool act, Counters& cnt, uint32_t role = 0u) {
   const bool tie_high = (S.flags & RT_FLAG_TIE_HIGH) != 0;
   const bool hi = role != 0u;
   const uint32_t one = hi ? 0u : 1u;  // per-path counters: the group's first lane
-  constexpr bool kNrm = PT_CARRY_NRM && CO == 1;
   float nrm[3], P[3];
-  if (kNrm) {
-#pragma unroll
-    for (int k = 0; k < 3; ++k) nrm[k] = st.n[k];
-  } else {
+  {
     float v0[3], e1[3], e2[3];
     load_tri(S, act ? st.pid : 0, v0, e1, e2);
     tri_normal(e1, e2, st.d, nrm);
@@ -307,8 +291,7 @@ __device__ __forceinline__ bool path_step(const Scene& S, int32_t* stack, PathSt
   float ts;
   const uint64_t c0 = PT_CYC();
   // the light-space lists when built (occluded_list), else the BVH
-  const bool occ = CO == 2 ? occluded_list_quad(S, s, act, st.pid, role, cnt)
-                 : CO == 1 ? occluded_list_coop(S, s, act, st.pid, hi, cnt)
+  const bool occ = CO == 1 ? occluded_list_coop(S, s, act, st.pid, hi, cnt)
                  : S.slist_on ? occluded_list(S, s, act, st.pid, cnt)
                               : act && trace<true>(S, s, 0.0f, 1.0f, st.pid, tie_high, &ts, stack, cnt) >= 0;
   cnt.occluded += occ ? one : 0u;
@@ -333,10 +316,8 @@ __device__ __forceinline__ bool path_step(const Scene& S, int32_t* stack, PathSt
     bounce_dir(nrm, pt_key(S.seed, (st.xy >> 16) * S.width + (st.xy & 0xffffu), v), b.d);  // keyed by pixel
     ray_setup(b);
     cnt.bounce += one;
-    np = CO == 2 ? trace_quad(S, b, st.pid, tie_high, &nt, stack, role, cnt)
-         : CO == 1 ? (RT_BVH8 ? trace_coop8(S, b, st.pid, tie_high, &nt, stack, hi, cnt)
-                              : trace_coop(S, b, st.pid, tie_high, &nt, stack, hi, cnt))
-                   : trace<false>(S, b, 0.0f, INFINITY, st.pid, tie_high, &nt, stack, cnt);
+    np = CO == 1 ? trace_coop(S, b, st.pid, tie_high, &nt, stack, hi, cnt)
+                 : trace<false>(S, b, 0.0f, INFINITY, st.pid, tie_high, &nt, stack, cnt);
     if (np < 0) {
 #pragma unroll
       for (int k = 0; k < 3; ++k) st.L[k] = fmaf(st.T[k], PT_SKY, st.L[k]);
@@ -344,7 +325,7 @@ __device__ __forceinline__ bool path_step(const Scene& S, int32_t* stack, PathSt
     }
   }
   const uint64_t c2 = PT_CYC();
-  if (alive) path_hit<kNrm>(S, st, P, b, np, nt, cnt, !hi);
+  if (alive) path_hit(S, st, P, b, np, nt, cnt, !hi);
   if (CO) {
     PT_ACC(2, c2 - c1);           // cycles in the bounce walk (and its setup)
     PT_ACC(6, PT_CYC() - c2);     // cycles shading the bounce hit
@@ -584,9 +565,7 @@ __device__ __forceinline__ void lane_path(const vx_task_t& task, const Scene& S,
   // walk cannot share one loop)
   const bool split = __ballot(1) == ~0ull && (__ballot(in) >> 32) == 0;
   const bool pair = PT_PAIR && !S.slist_on && split;
-  const bool coop = PT_COOP && S.slist_on && split && (RT_ONLY_BVH4H || (S.flags & RT_FLAG_BVH4H));
-  // a 16-pixel wave (split tiles at split_log 4): quads of lanes per path
-  const bool quad = PT_QUAD && coop && (__ballot(in) >> 16) == 0;
+  const bool coop = S.slist_on && split && (RT_ONLY_BVH4H || (S.flags & RT_FLAG_BVH4H));
   cnt.primary += in;
   const bool tie_high = (S.flags & RT_FLAG_TIE_HIGH) != 0;
   // primary visibility: the raster's winner at this pixel (trace_primary)
@@ -600,35 +579,6 @@ __device__ __forceinline__ void lane_path(const vx_task_t& task, const Scene& S,
   const bool path = hit >= 0 && secondary_ok(th);  // a path starts at the winner's plane
   if (!path && in) store_out(S, out, color);
   if (!path && !pair && !coop) return;
-  if (quad) {
-    // lanes 4p .. 4p + 3 take pixel p's path (lane p); all four trace it,
-    // lane 4p stores it
-    const uint32_t src = lane_id() >> 2, j = lane_id() & 3u;
-    bool act = __shfl((int)path, (int)src) != 0;
-    const bool own = act && j == 0u;
-    PathState q;
-    q.task = (uint32_t)__shfl((int)t, (int)src);
-    q.xy = (uint32_t)__shfl((int)(x | (y << 16)), (int)src);
-    q.out = (uint32_t)__shfl((int)out, (int)src);
-    q.alpha = (uint32_t)__shfl((int)(color & 0xff000000u), (int)src);
-    q.pid = __shfl(hit, (int)src);
-    q.t = __shfl(th, (int)src);
-    const float k255 = 1.0f / 255.0f;
-    const uint32_t qc = (uint32_t)__shfl((int)color, (int)src);
-    q.T[0] = (float)((qc >> 16) & 0xffu) * k255;
-    q.T[1] = (float)((qc >> 8) & 0xffu) * k255;
-    q.T[2] = (float)(qc & 0xffu) * k255;
-#pragma unroll
-    for (int k = 0; k < 3; ++k) {
-      q.o[k] = __shfl(r.o[k], (int)src);
-      q.d[k] = __shfl(r.d[k], (int)src);
-      q.L[k] = 0.0f;
-    }
-    int32_t* qstack = stack - j;  // the quad's stack: lane 4p's column
-    for (uint32_t v = 0; act; ++v) act = path_step<2>(S, qstack, q, v, act, cnt, j);
-    if (own) store_path_pixel(S, q);
-    return;
-  }
   const float k255 = 1.0f / 255.0f;
   PathState st;
   st.task = t;
@@ -655,7 +605,6 @@ __device__ __forceinline__ void lane_path(const vx_task_t& task, const Scene& S,
     return;
   }
   if (coop) {
-#if RT_PAIR_ADJ
     // lanes 2p, 2p + 1 take pixel p's path (lane p); both trace it, lane 2p
     // stores it
     const bool hi = (lane_id() & 1u) != 0u;
@@ -675,32 +624,6 @@ __device__ __forceinline__ void lane_path(const vx_task_t& task, const Scene& S,
       st.T[k] = __shfl(st.T[k], src);
     }
     int32_t* pstack = hi ? stack - 1 : stack;  // the pair's stack: lane 2p's column
-#if PT_CARRY_NRM
-    {
-      float v0[3], e1[3], e2[3];
-      load_tri(S, act ? st.pid : 0, v0, e1, e2);
-      tri_normal(e1, e2, st.d, st.n);
-    }
-#endif
-#else
-    // lane l + 32 takes lane l's path; both trace it, lane l stores it
-    const bool hi = lane_id() >= 32u;
-    const bool own = path && !hi;
-    bool act = xlow(path ? 1u : 0u) != 0u;
-    st.task = xlow(st.task);
-    st.xy = xlow(st.xy);
-    st.out = xlow(st.out);
-    st.alpha = xlow(st.alpha);
-    st.pid = (int32_t)xlow((uint32_t)st.pid);
-    st.t = xlowf(st.t);
-#pragma unroll
-    for (int k = 0; k < 3; ++k) {
-      st.o[k] = xlowf(st.o[k]);
-      st.d[k] = xlowf(st.d[k]);
-      st.T[k] = xlowf(st.T[k]);
-    }
-    int32_t* pstack = hi ? stack - 32 : stack;  // the pair's stack: lane l's column
-#endif
     for (uint32_t v = 0; act; ++v) act = path_step<1>(S, pstack, st, v, act, cnt, hi ? 1u : 0u);
     if (own) store_path_pixel(S, st);
     return;
@@ -730,11 +653,7 @@ __device__ __attribute__((used)) uint32_t __vx_grid_per_cu = PT_GRID_PER_CU;
 __device__ __attribute__((used)) uint32_t __vx_grid_per_cu = PT_GRID_PER_CU;
 #endif
 
-#ifdef PT_WAVES_PER_EU
-VX_MAIN_OCC(rt_kernel_arg_t, arg, PT_BLOCK, PT_WAVES_PER_EU) {
-#else
 VX_MAIN(rt_kernel_arg_t, arg, PT_BLOCK) {
-#endif
   __shared__ PtLds s_pt;
 #ifdef RT_STAMPS  // diagnostic image: per-wave start/end timestamps (scripts/wave_timeline.py)
   const uint64_t t_stamp0 = __builtin_amdgcn_s_memrealtime();

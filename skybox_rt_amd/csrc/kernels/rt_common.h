@@ -92,16 +92,6 @@ typedef struct { float v[32]; } rt_node4_t;
 // behind the rt_node4_t array (nodes4_addr + 128 * num_nodes4).
 typedef struct { uint16_t b[24]; int32_t child[4]; } rt_node4h_t;
 
-// rt_node8h_t (BVH8, 128 B): the BVH2 collapsed to 8 children per node by the
-// BVH4's rule (a node's children are repeatedly replaced by the children of
-// its largest-area internal child until it has 8), stored as two
-// rt_node4h_t halves -- children 0-3, then 4-7 (unused slots: empty refs,
-// zero planes) -- so a lane pair reads one half each (pt_kernel's pair walk)
-// and a wave packet reads the node as two 64-B scalar loads.  Planes rounded
-// outward to binary16 exactly as the BVH4's.  The kernels' BVH8 images
-// (RT_BVH8) walk it; the fp32 export (rt_scene_export_bvh8, the oracle's
-// input) is two rt_node4_t per node.
-typedef struct { rt_node4h_t half[2]; } rt_node8h_t;
 
 // rt_tri_t: (v0.x, v0.y, v0.w, pid), (e1.xyw, 0), (e2.xyw, 0) -- clip (x,y,w)
 typedef struct { float v[12]; } rt_tri_t;
@@ -221,9 +211,7 @@ typedef struct {
                            // group g; 2 * RT_PQ_SEGS groups done (the last zeroes them all)
   uint32_t pathq_seg_cap;  // entries per segment
   uint32_t quad_tiles;     // the first quad_tiles of the split tiles run 16 pixels per wave
-                           // (the heaviest: a path on four lanes, pt_kernel.hip PT_QUAD)
-  uint64_t nodes8_addr;    // rt_node8h_t BVH8 (the RT_BVH8 images' walks; 0 = none)
-  uint32_t num_nodes8;
+                           // (env RT_QUAD_TILES, a task-map probe; 0 by default)
   uint32_t tiles_x_magic;  // min(ceil(2^32 / tiles_x), 2^32 - 1): a tile's row is
                            // mulhi(tile, magic) plus at most one correction (rt_trace.h
                            // tile_row) -- no integer division in the kernels' task map

@@ -35,11 +35,6 @@
 #define RT_BLOCK_THREADS 64
 #endif
 #define VX_BLOCK_THREADS RT_BLOCK_THREADS  // vx_spawn.h: the workgroup size as a constant
-// RT_XCD: a 32x32 tile's 16 one-chunk waves on one XCD (vx_spawn.h
-// VX_XCD_GROUP: blocks per tile)
-#if defined(RT_XCD) && RT_XCD && !defined(VX_XCD_GROUP)
-#define VX_XCD_GROUP (16 / (RT_BLOCK_THREADS / 64))
-#endif
 #include "rt_trace.h"
 
 #ifndef RT_FLAT
@@ -48,7 +43,6 @@
 #ifndef RT_PATHQ
 #define RT_PATHQ 0  // 1: image pt_primary, the path tracer's first kernel (rt_trace.h pathq_append)
 #endif
-#define RT_FLAT_CAP 1024  // rectangle words staged in LDS (16 KB); longer lists stream via s_load
 
 namespace {
 
@@ -60,14 +54,9 @@ constexpr int kWaves = RT_BLOCK_THREADS / 64;
 // per-lane walks' stack[depth][lane] (deep images: layouts other than the
 // binary16 BVH4 walk per lane)
 #define RT_QUEUE 128
-// RT_SHADOW_PERLANE = 1 (A/B knob): the queued shadow rays walk the BVH per
-// lane (trace<true>, LDS stack) instead of as one wave packet -- the
-// BVH-walk frame measured 0.0411 vs 0.0333 ms (r05n: 102 VGPRs and 35 KB of
-// LDS per workgroup, 4 waves per SIMD instead of 5)
-#ifndef RT_SHADOW_PERLANE
-#define RT_SHADOW_PERLANE 0
-#endif
-#define RT_LANE_STACK (!RT_FLAT && (!RT_ONLY_BVH4H || RT_SHADOW_PERLANE))
+// (queued shadow rays walking the BVH per lane instead of as one packet:
+// BVH-walk frame 0.0411 vs 0.0333 ms, r05n -- 102 VGPRs, 4 waves per SIMD)
+#define RT_LANE_STACK (!RT_FLAT && !RT_ONLY_BVH4H)
 struct WaveLds {
 #if RT_LANE_STACK
   int32_t stack[RT_STACK_ROWS][64];
@@ -85,34 +74,12 @@ struct WaveLds {
 #endif
 };
 
-#if RT_FLAT
-// Only each record's rectangle word (16 B: the word the scan tests for every
-// entry) is staged in LDS, 12 KB for tekkaman, so 8 workgroups fit a CU; a
-// candidate's other three words come through the scalar cache (wave-uniform).
-// A/B (profiles/r02/ab_flat_rect_lds.json, 256^2): whole 64-B records in
-// 1024-thread workgroups (2 per CU by LDS) 0.0479 ms; rectangle words in
-// 256-thread workgroups (8 per CU, 4-way list split) 0.0280 ms; 512 threads
-// 0.0302, 128 threads 0.0403.  The shadow rays read the MT records (rt_tri_t)
-// of S.geom.
-__shared__ uint4 s_geom[RT_FLAT_CAP];
-// RT_FLAT_SCALAR (default since r05): no LDS staging -- the block test
-// (RT_FLAT_BLOCK) reads its 64 rectangle words per instruction straight from
-// L2 with vector loads, so a workgroup starts on its chunk at once; A/B r05j
-// (256^2, median ms): staged 0.0101, unstaged 0.0096, unstaged with 512-thread
-// workgroups at 8 waves per SIMD 0.0090 (the default; 512 threads at 5 waves
-// per SIMD 0.0125, 128 threads 0.0122, 1024 threads 0.0204)
-// RT_FLAT_BLOCK: entries against the chunk's 8x8 block, 64 per instruction,
-// before the per-pixel tests (flat_chunk); 0 = the one-level scan
-#ifndef RT_FLAT_BLOCK
-#define RT_FLAT_BLOCK 1
-#endif
-#ifndef RT_FLAT_SCALAR
-#define RT_FLAT_SCALAR 1
-#endif
-__device__ __forceinline__ const uint4* flat_list(const Scene& S) {
-  return !RT_FLAT_SCALAR && S.num_geom <= RT_FLAT_CAP ? s_geom : nullptr;
-}
-#endif
+// Config 2 reads the geometry list straight from L2: the block test reads
+// 64 rectangle words per instruction with vector loads, so a workgroup
+// starts on its chunk at once (r05j, 256^2, median ms: the rectangle words
+// staged in LDS 0.0101, unstaged 0.0096, unstaged with 512-thread workgroups
+// at 8 waves per SIMD 0.0090; r02: whole 64-B records in LDS 0.0479).  The
+// shadow rays read the MT records (rt_tri_t) of S.geom.
 
 #if !RT_FLAT
 __device__ __forceinline__ void kernel_body(const vx_task_t& task, const Scene& S, WaveLds& w,
@@ -129,15 +96,13 @@ __device__ __forceinline__ void kernel_body(const vx_task_t& task, const Scene& 
 #ifdef RT_STAMPS
   if (lane_id() == 0) __vx_mpm_lds[3] = (uint32_t)__builtin_amdgcn_s_memrealtime();
 #endif
-  LayerPre lpre;
-  layer_prefetch(S, lpre);
   // primary visibility: the raster's winner at this pixel
   const int32_t hit = trace_primary(S, lb, x, y, in, tie_high, cnt);
 #ifdef RT_STAMPS
   if (lane_id() == 0) __vx_mpm_lds[14] = (uint32_t)__builtin_amdgcn_s_memrealtime();
 #endif
   cnt.hits += hit >= 0;
-  const int32_t spid = resolve_layers(S, x, y, in && hit < 0, hit, cnt, &lpre);
+  const int32_t spid = resolve_layers(S, x, y, in && hit < 0, hit, cnt);
 #ifdef RT_STAMPS
   if (lane_id() == 0) __vx_mpm_lds[4] = (uint32_t)__builtin_amdgcn_s_memrealtime();
 #endif
@@ -213,9 +178,9 @@ __device__ __forceinline__ void shadow_drain(bool final, const Scene& S, WaveLds
     // the light-space lists when built (occluded_list), else the BVH: the
     // binary16 BVH4 as one packet, other layouts per lane (deep images)
     const bool occ = !RT_BVH_WALK && S.slist_on ? occluded_list(S, s, active, w.q_pid[slot], cnt)
-                     : (RT_BVH8 && S.num_nodes8 > 0) ? occluded_packet8(S, s, active, w.q_pid[slot], 1.0f, cnt)
-                     : (!RT_SHADOW_PERLANE && (RT_ONLY_BVH4H || (S.flags & RT_FLAG_BVH4H)))
-                         ? occluded_packet(S, s, active, w.q_pid[slot], 1.0f, cnt)
+                     : (RT_ONLY_BVH4H || (S.flags & RT_FLAG_BVH4H))
+                         ? (RT_SHADOW_MASKS ? occluded_packet_m(S, s, active, w.q_pid[slot], 1.0f, cnt)
+                                            : occluded_packet(S, s, active, w.q_pid[slot], 1.0f, cnt))
                          : active && trace<true>(S, s, 0.0f, 1.0f, w.q_pid[slot], tie_high, &ts,
                                                  RT_WSTACK(w, lane), cnt) >= 0;
     if (occ) {
@@ -234,34 +199,27 @@ __device__ __forceinline__ void shadow_drain(bool final, const Scene& S, WaveLds
 #if RT_FLAT
 // Config 2 with every ray's primitive list split across the workgroup's
 // waves: a workgroup step takes one 64-task chunk (vx_spawn_chunks_block),
-// wave w tests list entries [w*m, (w+1)*m) for the chunk's 64 pixels
-// (rt_vtri_t records from LDS: one broadcast 16-B read of a record's pixel
-// rectangle first, the edges and depth only when a lane of the wave lies in
-// it), the per-wave winners meet in LDS (vis_better is a strict order on
-// (depth word, pid), so the reduction order is immaterial) and wave 0
-// shades and stores; shadow rays split the same way, the first occluder in
-// list order found by a min over the waves' first hits (which is also
-// brute_trace's test count).
-constexpr int kFlatUnroll = 8;  // rectangle words in flight at once
-// RT_FLAT_EARLY_OUT (no shadow rays): waves 1.. leave the chunk once their
-// winners are in LDS and wave 0 shades and stores with no second barrier --
-// the winners double-buffered by chunk parity, so a wave's next chunk never
-// overwrites words wave 0 is still reducing (it must pass the next chunk's
-// barrier, which wave 0 reaches only after its reduction)
-#ifndef RT_FLAT_EARLY_OUT
-#define RT_FLAT_EARLY_OUT 1
-#endif
+// wave w tests the list entries w, w + kWaves, ... for the chunk's 64
+// pixels (flat_chunk), the per-wave winners meet in LDS (vis_better is a
+// strict order on (depth word, pid), so the reduction order is immaterial)
+// and wave 0 shades and stores; shadow rays split the list in ranges, the
+// first occluder in list order found by a min over the waves' first hits
+// (which is also brute_trace's test count).
+// Without shadow rays waves 1.. leave the chunk once their winners are in
+// LDS and wave 0 shades and stores with no second barrier -- the winners
+// double-buffered by chunk parity, so a wave's next chunk never overwrites
+// words wave 0 is still reducing (it must pass the next chunk's barrier,
+// which wave 0 reaches only after its reduction)
 struct FlatLds {
-  uint32_t z[1 + RT_FLAT_EARLY_OUT][kWaves][64];
-  int32_t pid[1 + RT_FLAT_EARLY_OUT][kWaves][64];
+  uint32_t z[2][kWaves][64];
+  int32_t pid[2][kWaves][64];
   uint32_t first[kWaves][64];
 };
 
 // a record's rectangle word with its rectangle as packed corners (lo = x0 |
 // y0 << 16, hi = x1 | y1 << 16 in .y / .z; an empty rectangle becomes
-// lo = 0xffffffff, hi = 0xfffefffe, which no pixel matches): the form staged
-// in LDS, so a wave's rectangle test is two packed 16-bit clamps and one
-// compare (rect2_in)
+// lo = 0xffffffff, hi = 0xfffefffe, which no pixel matches), so a wave's
+// rectangle test is two packed 16-bit clamps and one compare (rect2_in)
 __device__ __forceinline__ uint4 rect_corners(uint4 c) {
   const uint32_t rx = c.y, ry = c.z;
   const bool empty = (rx & 0xffffu) > (rx >> 16) || (ry & 0xffffu) > (ry >> 16);
@@ -269,15 +227,10 @@ __device__ __forceinline__ uint4 rect_corners(uint4 c) {
   c.z = empty ? 0xfffefffeu : (rx >> 16) | (ry & 0xffff0000u);
   return c;
 }
-__device__ __forceinline__ uint4 flat_rec(const Scene& S, const uint4* lds, uint32_t k, uint32_t q) {
-  if (q == 2) return lds ? lds[k] : rect_corners(S.A.sld_u4(S.vgeom + 64u * k + 32u));
-  return S.A.sld_u4(S.vgeom + 64u * k + 16u * q);
-}
-
 __device__ __forceinline__ void flat_chunk(const vx_task_t& task, bool valid, const Scene& S,
                                            FlatLds& L, uint32_t& par, Counters& cnt) {
   const uint32_t w = threadIdx.x >> 6, lane = lane_id();
-  const uint32_t pb = RT_FLAT_EARLY_OUT ? par : 0u;  // this chunk's winner buffer
+  const uint32_t pb = par;  // this chunk's winner buffer
   par ^= 1u;
   const uint32_t t = task.blockIdx.x;
   uint32_t x = 0, y = 0, out = 0;
@@ -292,22 +245,19 @@ __device__ __forceinline__ void flat_chunk(const vx_task_t& task, bool valid, co
   const bool tie_high = (S.flags & RT_FLAG_TIE_HIGH) != 0;
   const uint32_t n = S.num_geom, per = (n + kWaves - 1) / kWaves;
   const uint32_t k0 = w * per < n ? w * per : n, k1 = k0 + per < n ? k0 + per : n;
-  const uint4* lds = flat_list(S);
   uint32_t bz = VX_OM_DEPTH_MASK;
   int32_t bp = -1;
-  uint32_t k = k0;
-#if RT_FLAT_BLOCK
   // Two levels: the wave's lanes take 64 of its entries at once and test
   // each one's rectangle against the chunk's 8x8 block (packed corners:
   // lo <= block hi and hi >= block lo, halfwise); then, for the entries that
   // reach the block only, the per-pixel rectangle test and, where a lane
   // lies in it, the edges and depth -- the records two at a time (one
   // 64-B scalar load each, the second in flight while the first is tested).
-  // The same entries get the same tests as the one-level scan below (the
-  // block test only skips entries no pixel of the block lies in): identical
-  // winners and counts, with 1/64 of the rectangle-test instructions.  Wave w
-  // takes entries w, w + kWaves, ...: a region's triangles, often
-  // consecutive in the list, spread over the waves.
+  // The same entries get the same tests as a one-level scan of every entry
+  // per pixel (the block test only skips entries no pixel of the block lies
+  // in): identical winners and counts, with 1/64 of the rectangle-test
+  // instructions (r04).  Wave w takes entries w, w + kWaves, ...: a region's
+  // triangles, often consecutive in the list, spread over the waves.
   {
     const uint32_t bx = (uint32_t)__builtin_amdgcn_readfirstlane(x) & ~7u;  // lane 0: the block's corner
     const uint32_t by = (uint32_t)__builtin_amdgcn_readfirstlane(y) & ~7u;
@@ -318,7 +268,7 @@ __device__ __forceinline__ void flat_chunk(const vx_task_t& task, bool valid, co
       bool ov = false;
       if (il < mine) {
         const uint32_t kl = il * kWaves + w;
-        const uint4 C = lds ? lds[kl] : rect_corners(S.A.ld_u4(S.vgeom + 64u * kl + 32u));
+        const uint4 C = rect_corners(S.A.ld_u4(S.vgeom + 64u * kl + 32u));
         // max(lo, block hi) == block hi and min(hi, block lo) == block lo
         ov = rect2_clamp(C.y, 0xffffffffu, bhi) == bhi && rect2_clamp(0u, C.z, blo) == blo;
       }
@@ -356,50 +306,7 @@ __device__ __forceinline__ void flat_chunk(const vx_task_t& task, bool valid, co
 #ifdef RT_INSTRUMENT
     cnt.tests += in ? mine : 0u;  // the whole list per ray, summed over the waves
 #endif
-    k = k1;
   }
-#endif
-  // kFlatUnroll rectangle words in flight at once (their LDS reads
-  // overlap), then the candidates among them in ascending order
-  for (; k + kFlatUnroll <= k1; k += kFlatUnroll) {
-    uint4 C[kFlatUnroll];
-#pragma unroll
-    for (int j = 0; j < kFlatUnroll; ++j) C[j] = flat_rec(S, lds, k + j, 2);
-    uint32_t cand = 0u;
-    bool inr[kFlatUnroll];
-#ifdef RT_INSTRUMENT
-    cnt.rect_tests += lane == 0 ? (uint32_t)kFlatUnroll : 0u;
-#endif
-#pragma unroll
-    for (int j = 0; j < kFlatUnroll; ++j) {
-      inr[j] = rect2_in(C[j].y, C[j].z, pp);
-      cand |= mask_ueq(rect2_clamp(C[j].y, C[j].z, pp), pp) ? 1u << j : 0u;
-    }
-#ifdef RT_INSTRUMENT
-    cnt.edge_tests += lane == 0 ? (uint32_t)__popc(cand) : 0u;
-#endif
-#pragma unroll
-    for (int j = 0; j < kFlatUnroll; ++j)
-      if ((cand >> j) & 1u)  // wave-uniform
-        vis_test_in(flat_rec(S, lds, k + j, 0), flat_rec(S, lds, k + j, 1), C[j],
-                    flat_rec(S, lds, k + j, 3), inr[j], px, y, tie_high, bz, bp);
-  }
-  for (; k < k1; ++k) {
-    const uint4 C = flat_rec(S, lds, k, 2);
-    const bool inr = rect2_in(C.y, C.z, pp);
-#ifdef RT_INSTRUMENT
-    cnt.rect_tests += lane == 0 ? 1u : 0u;
-#endif
-    if (__ballot(inr) == 0) continue;  // wave-uniform skip
-#ifdef RT_INSTRUMENT
-    cnt.edge_tests += lane == 0 ? 1u : 0u;
-#endif
-    vis_test_in(flat_rec(S, lds, k, 0), flat_rec(S, lds, k, 1), C, flat_rec(S, lds, k, 3), inr, px,
-                y, tie_high, bz, bp);
-  }
-#if defined(RT_INSTRUMENT) && !RT_FLAT_BLOCK
-  cnt.tests += in ? k1 - k0 : 0u;  // the whole list per ray, summed over the waves
-#endif
 #ifdef RT_STAMPS  // 3: wave 0's list scan done, 4: the slowest wave's (after the barrier)
   if (threadIdx.x == 0) __vx_mpm_lds[3] = (uint32_t)__builtin_amdgcn_s_memrealtime();
 #endif
@@ -409,7 +316,7 @@ __device__ __forceinline__ void flat_chunk(const vx_task_t& task, bool valid, co
 #ifdef RT_STAMPS
   if (threadIdx.x == 0) __vx_mpm_lds[4] = (uint32_t)__builtin_amdgcn_s_memrealtime();
 #endif
-  const bool early = RT_FLAT_EARLY_OUT && (S.flags & RT_FLAG_SHADOWS) == 0;  // block-uniform
+  const bool early = (S.flags & RT_FLAG_SHADOWS) == 0;  // block-uniform
   if (early && w != 0) return;
   int32_t hit = -1;
   uint32_t hz = VX_OM_DEPTH_MASK;
@@ -493,9 +400,7 @@ __device__ __forceinline__ void flush(int slot, uint32_t v) { vx_mpm_add(RT_MPM_
 // 0.01084 ms vs 0.01108 at 16/CU; registers for 8 waves per SIMD, so all
 // 1 024 workgroups of 512 threads are resident at once (r05j)
 __device__ __attribute__((used)) uint32_t __vx_grid_per_cu = 4;
-#ifndef RT_WAVES_PER_EU
 #define RT_WAVES_PER_EU 8
-#endif
 #endif
 #ifdef RT_WAVES_PER_EU
 VX_MAIN_OCC(rt_kernel_arg_t, arg, RT_BLOCK_THREADS, RT_WAVES_PER_EU) {
@@ -513,14 +418,9 @@ VX_MAIN(rt_kernel_arg_t, arg, RT_BLOCK_THREADS) {
   if (threadIdx.x == 0) __vx_mpm_lds[10] = (uint32_t)__builtin_amdgcn_s_memrealtime();
 #endif
 #if RT_FLAT
-  // stage the geometry list once per workgroup (workgroups past the last
-  // task chunk have nothing to render and skip it)
-  if (!RT_FLAT_SCALAR && S.num_geom <= RT_FLAT_CAP && blockIdx.x * VX_CHUNK < S.num_tasks) {
-    for (uint32_t i = threadIdx.x; i < S.num_geom; i += RT_BLOCK_THREADS)
-      s_geom[i] = rect_corners(S.A.ld_u4(S.vgeom + 64u * i + 32u));
-  }
+  // the workgroup's waves start their first chunk together
   __syncthreads();
-#ifdef RT_STAMPS  // 11: list staged
+#ifdef RT_STAMPS  // 11: past the start barrier
   if (threadIdx.x == 0) __vx_mpm_lds[11] = (uint32_t)__builtin_amdgcn_s_memrealtime();
 #endif
   __shared__ FlatLds s_flat;

@@ -32,9 +32,6 @@
 #ifndef RT_BVH_WALK
 #define RT_BVH_WALK 0  // 1: image rt_bvh -- primary and shadow rays walk the BVH, no list code
 #endif
-#ifndef RT_BVH8
-#define RT_BVH8 0  // 1: the BVH8 images -- shadow packets (rt_bvh8) and the pair walk (pt_kernel8) on rt_node8h_t
-#endif
 
 namespace rtk {
 
@@ -63,7 +60,6 @@ struct Scene {
   uint32_t num_nodes, num_nodes4, num_layer, num_geom, flags, width, height;
   uint32_t shard_index, shard_count, tiles_x, clear_color, bounces, seed, split_tiles, split_log;
   uint32_t tiles_x_magic, num_tasks;
-  uint32_t nodes8, num_nodes8;  // BVH8 (rt_node8h_t; the RT_BVH8 images)
   float sx, sy, light[3];
   uint64_t argp;  // the argument block (constant address space), for lazy_args
   uint32_t blist, bidx, blist_blocks;  // per-block candidate lists (rt_bentry_t)
@@ -122,8 +118,6 @@ __device__ __forceinline__ Scene load_scene(const rt_kernel_arg_t* ga) {
   s.tiles_x = a->tiles_x;
   s.tiles_x_magic = a->tiles_x_magic;
   s.num_tasks = a->num_tasks;  // through the scalar cache (arg->num_tasks would be a flat load)
-  s.nodes8 = (uint32_t)a->nodes8_addr;
-  s.num_nodes8 = a->num_nodes8;
   s.clear_color = a->clear_color;
   s.sx = a->sx;
   s.sy = a->sy;
@@ -631,7 +625,8 @@ __device__ __forceinline__ bool occluded_packet(const Scene& S, const Ray& r, bo
       const uint32_t first = (lr >> 4) & 0x07ffffffu, count = (lr & 15u) + 1u;
       RT_WAVE_ITER(9);
       bool lv = live;
-      // kLeafHoist slots in flight at once (3 padding records)
+      // kLeafHoist slots in flight at once (3 padding records; 3 or 4
+      // measured no faster on the BVH-walk frame, r06b)
       constexpr uint32_t H = kLeafHoist;
 #pragma unroll
       for (uint32_t q0 = 0; q0 < 4; q0 += H) {
@@ -671,87 +666,76 @@ __device__ __forceinline__ bool occluded_packet(const Scene& S, const Ray& r, bo
   return occ;
 }
 
-// occluded_packet on the BVH8 (rt_node8h_t, RT_BVH8 images): the same
-// walk -- children in fixed slot order, a child entered when some unfinished
-// lane's ray hits its box and all its ancestors', the stack in one VGPR --
-// over 8 children per node (the node as two 64-B scalar loads, one per
-// rt_node4h_t half), so a root-to-leaf walk takes half as many dependent node
-// steps.  Restricted to one lane it is the per-lane any-hit walk of the BVH8
-// in slot order (oracle/rt.c bvh8_step), so verdicts and per-ray counts are
-// its.
-__device__ __forceinline__ bool occluded_packet8(const Scene& S, const Ray& r, bool act, int32_t skip,
-                                                 float tmax, Counters& cnt) {
-  bool done = !act, occ = false;
-  if (S.num_nodes8 == 0 || __ballot(!done) == 0) return false;
-  int32_t vstk = 0;  // stack entry i in lane i of this VGPR
+// occluded_packet with the walk's per-lane state as wave masks in SGPRs
+// (RT_SHADOW_MASKS): `live` (on the path and unfinished), `done`, and per
+// stack entry the mask of lanes on it (two more VGPRs of v_writelane /
+// v_readlane beside the ref) -- a child's lanes are one v_cmp of the slab's
+// near / far values ANDed with `live`, no per-lane booleans to materialise
+// and ballot again, no per-lane bit stack.  The leaf triangles are tested
+// branch-free (mt_hit_bf: mt_hit's operations, one predicate).  The same
+// walk: same nodes in the same order, same per-lane visits, tests and
+// verdicts.
+#define RT_SHADOW_MASKS 0  // 1: shadow packets walk as occluded_packet_m
+__device__ __forceinline__ bool occluded_packet_m(const Scene& S, const Ray& r, bool act, int32_t skip,
+                                                  float tmax, Counters& cnt) {
+  const uint64_t act_m = __ballot(act);
+  if (S.num_nodes4 == 0 || act_m == 0) return false;
+  uint64_t done_m = 0, live_m = act_m;  // live: on the current node's path and unfinished
+  int32_t vstk = 0, vmlo = 0, vmhi = 0;  // stack entry i in lane i: ref, lanes on it (lo, hi)
   int sp = 0;
   int32_t ref = 0;
-  bool on = true;     // this lane's ray hit the current node's box (and its ancestors')
-  uint32_t onb = 0u;  // the same for the stack entries (bit sp)
-  static_assert(RT_MAX_STACK <= 32, "one bit per stack entry");
+#ifdef RT_INSTRUMENT
+  const uint32_t lane = lane_id();
+#endif
   for (;;) {
-    const bool live = on && !done;
     if (ref >= 0) {
-      RT_CNT(cnt.visits += live;)
+      RT_CNT(cnt.visits += (uint32_t)(live_m >> lane) & 1u;)
       RT_WAVE_ITER(9);
-      const uint32_t no = S.nodes8 + 128u * (uint32_t)ref;
-      uint4 nw[8];
+      const uint32_t no = S.nodes4 + 128u * S.num_nodes4 + 64u * (uint32_t)ref;
+      uint4 nw[4];
       RT_LD_BEGIN();
-      S.A.sld_u4n<8>(no, nw);  // two s_load_dwordx16
+      S.A.sld_u4n<4>(no, nw);  // one s_load_dwordx16
       RT_LD_END(1);
-      int32_t c[8];
-      bool h[8];
-      uint32_t need = 0u;  // wave-uniform: children some live lane enters
+      const uint4 px = nw[0], py = nw[1], pz = nw[2], cf = nw[3];
+      float lx[4], hx[4], ly[4], hy[4], lz[4], hz[4];
+      auto h2 = [](uint32_t u, float& a, float& b) {
+        a = (float)__builtin_bit_cast(_Float16, (uint16_t)(u & 0xffffu));
+        b = (float)__builtin_bit_cast(_Float16, (uint16_t)(u >> 16));
+      };
+      h2(px.x, lx[0], lx[1]); h2(px.y, lx[2], lx[3]); h2(px.z, hx[0], hx[1]); h2(px.w, hx[2], hx[3]);
+      h2(py.x, ly[0], ly[1]); h2(py.y, ly[2], ly[3]); h2(py.z, hy[0], hy[1]); h2(py.w, hy[2], hy[3]);
+      h2(pz.x, lz[0], lz[1]); h2(pz.y, lz[2], lz[3]); h2(pz.z, hz[0], hz[1]); h2(pz.w, hz[2], hz[3]);
+      const int32_t c[4] = {(int32_t)cf.x, (int32_t)cf.y, (int32_t)cf.z, (int32_t)cf.w};
+      uint64_t hm[4];
+      uint32_t need = 0u;
 #pragma unroll
-      for (int hf = 0; hf < 2; ++hf) {
-        const uint4 px = nw[4 * hf], py = nw[4 * hf + 1], pz = nw[4 * hf + 2], cf = nw[4 * hf + 3];
-        float lx[4], hx[4], ly[4], hy[4], lz[4], hz[4];
-        auto h2 = [](uint32_t u, float& a, float& b) {
-          a = (float)__builtin_bit_cast(_Float16, (uint16_t)(u & 0xffffu));
-          b = (float)__builtin_bit_cast(_Float16, (uint16_t)(u >> 16));
-        };
-        h2(px.x, lx[0], lx[1]); h2(px.y, lx[2], lx[3]); h2(px.z, hx[0], hx[1]); h2(px.w, hx[2], hx[3]);
-        h2(py.x, ly[0], ly[1]); h2(py.y, ly[2], ly[3]); h2(py.z, hy[0], hy[1]); h2(py.w, hy[2], hy[3]);
-        h2(pz.x, lz[0], lz[1]); h2(pz.y, lz[2], lz[3]); h2(pz.z, hz[0], hz[1]); h2(pz.w, hz[2], hz[3]);
-        const int32_t cc[4] = {(int32_t)cf.x, (int32_t)cf.y, (int32_t)cf.z, (int32_t)cf.w};
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          float tn = 0.0f;
-          const bool hs = slab(lx[i], hx[i], ly[i], hy[i], lz[i], hz[i], r, 0.0f, tmax, &tn);
-          c[4 * hf + i] = cc[i];
-          h[4 * hf + i] = hs & live & (cc[i] != RT_EMPTY_REF);
-          need |= __ballot(h[4 * hf + i]) ? 1u << (4 * hf + i) : 0u;
-        }
+      for (int i = 0; i < 4; ++i) {
+        float tn, tf;
+        slab_nf(lx[i], hx[i], ly[i], hy[i], lz[i], hz[i], r, 0.0f, tmax, &tn, &tf);
+        hm[i] = c[i] != RT_EMPTY_REF ? mask_fle(tn, tf) & live_m : 0u;
+        need |= hm[i] ? 1u << i : 0u;
       }
       if (need) {
-        // push the needed children after the first, last slot first
 #pragma unroll
-        for (int i = 7; i >= 1; --i) {
+        for (int i = 3; i >= 1; --i) {
           if ((need >> i) & 1u && (need & ((1u << i) - 1u))) {
             if (sp < RT_MAX_STACK) {
               vstk = vwritelane(vstk, c[i], sp);
-              onb = h[i] ? onb | (1u << sp) : onb & ~(1u << sp);
+              vmlo = vwritelane(vmlo, (int32_t)(uint32_t)hm[i], sp);
+              vmhi = vwritelane(vmhi, (int32_t)(uint32_t)(hm[i] >> 32), sp);
               ++sp;
             }
           }
         }
         const int f = __builtin_ctz(need);
-        int32_t rf = c[0];
-        bool of = h[0];
-#pragma unroll
-        for (int i = 1; i < 8; ++i) {
-          rf = f == i ? c[i] : rf;
-          of = f == i ? h[i] : of;
-        }
-        ref = rf;
-        on = of;
+        ref = f == 0 ? c[0] : f == 1 ? c[1] : f == 2 ? c[2] : c[3];
+        live_m = f == 0 ? hm[0] : f == 1 ? hm[1] : f == 2 ? hm[2] : hm[3];
         continue;
       }
     } else {
       const uint32_t lr = (uint32_t)ref;
       const uint32_t first = (lr >> 4) & 0x07ffffffu, count = (lr & 15u) + 1u;
       RT_WAVE_ITER(9);
-      bool lv = live;
       constexpr uint32_t H = kLeafHoist;
 #pragma unroll
       for (uint32_t q0 = 0; q0 < 4; q0 += H) {
@@ -770,25 +754,26 @@ __device__ __forceinline__ bool occluded_packet8(const Scene& S, const Ray& r, b
 #pragma unroll
         for (uint32_t j = 0; j < H; ++j) {
           if (q0 + j < count) {
-            RT_CNT(cnt.tests += lv;)
+            RT_CNT(cnt.tests += (uint32_t)(live_m >> lane) & 1u;)
             float t;
-            if (lv && __float_as_int(ta[j].w) != skip && mt_hit(r, ta[j], tb[j], tc[j], 0.0f, &t) &&
-                t < tmax) {
-              occ = true;
-              done = true;
-              lv = false;
-            }
+            const bool hit = mt_hit_bf(r, ta[j], tb[j], tc[j], 0.0f, &t) && t < tmax &&
+                             __float_as_int(ta[j].w) != skip;
+            const uint64_t m = __ballot(hit) & live_m;
+            done_m |= m;
+            live_m &= ~m;
           }
         }
       }
-      if (__ballot(!done) == 0) break;
+      if ((act_m & ~done_m) == 0) break;
     }
     if (sp == 0) break;
     --sp;
-    on = (onb >> sp) & 1u;
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane(vmlo, sp);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane(vmhi, sp);
+    live_m = (((uint64_t)hi << 32) | lo) & ~done_m;
     ref = __builtin_amdgcn_readlane(vstk, sp);
   }
-  return occ;
+  return act && ((done_m >> lane_id()) & 1u);
 }
 
 // A shadow segment's any-hit over its light-space cell list (rt_common.h;
@@ -859,56 +844,26 @@ __device__ __forceinline__ bool occluded_list(const Scene& S, const Ray& s, bool
 // the same stack pointer, node and best hit throughout, so per ray the node
 // visits, the order of the stack and the result are the per-lane walk's
 // (trace_impl / occluded_list), and so are the counters (visits counted by
-// the lower lane, tests by the lane that made them).
-// 1: node4_coop exchanges once and sorts the four children in both lanes
-// (0: the network split over the pair, three exchange rounds); needs the
-// stack's slack rows (RT_PUSH_UNCOND)
-#ifndef RT_COOP_LOCAL_SORT
-#define RT_COOP_LOCAL_SORT 1
-#endif
-// RT_COOP_HALF_LOADS = 1: node4_coop's lanes load only their half of a node
-// (6 dword + 1 dword-pair loads) instead of all 64 B and a select per word
-#ifndef RT_COOP_HALF_LOADS
-#define RT_COOP_HALF_LOADS 1
-#endif
-// RT_COOP_LEAF_BF = 1: trace_coop's leaf tests without branches (mt_hit_bf)
-#ifndef RT_COOP_LEAF_BF
-#define RT_COOP_LEAF_BF 0
-#endif
-// RT_COOP_LIST_BF = 1: occluded_list_coop's round without branches
-#ifndef RT_COOP_LIST_BF
-#define RT_COOP_LIST_BF 0
-#endif
-// RT_COOP_LEAF_IL = 1: trace_coop's leaf triangles dealt 0, 2 | 1, 3 over the
-// pair instead of 0, 1 | 2, 3
-#ifndef RT_COOP_LEAF_IL
-#define RT_COOP_LEAF_IL 1
-#endif
-// RT_PAIR_ADJ = 1: the pair is lanes 2p, 2p + 1 (one DPP quad_perm move per
-// exchange, fused into its consumer) instead of l, l ^ 32 (permlane32_swap)
-#ifndef RT_PAIR_ADJ
-#define RT_PAIR_ADJ 1
-#endif
-// the partner's value (lane l <-> l ^ 32, or l ^ 1 with RT_PAIR_ADJ)
+// the lower lane, tests by the lane that made them).  The pair is lanes 2p,
+// 2p + 1: one DPP quad_perm move per exchange, fused into its consumer (r04;
+// the pair l, l ^ 32 exchanged by permlane32_swap was slower).  In the
+// images with the stack's slack rows (RT_PUSH_UNCOND) node4_coop exchanges
+// once and sorts the four children in both lanes; the others split the
+// network over the pair in three exchange rounds.  Measured and not kept
+// (r04-r05): branch-free leaf tests and list rounds, the
+// leaf's triangles dealt 0, 1 | 2, 3 instead of 0, 2 | 1, 3, the whole node
+// loaded by both lanes, the stack's top entry in a register.
+// the partner's value (lane l <-> l ^ 1)
 __device__ __forceinline__ uint32_t xpart(uint32_t v, bool hi) {
-#if RT_PAIR_ADJ
   (void)hi;
   return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0xB1, 0xF, 0xF, false);  // quad_perm [1,0,3,2]
-#else
-  const auto r = __builtin_amdgcn_permlane32_swap(v, v, false, false);
-  return hi ? r[0] : r[1];
-#endif
 }
 __device__ __forceinline__ float xpartf(float v, bool hi) {
   return __uint_as_float(xpart(__float_as_uint(v), hi));
 }
 // the lower lane's value in both lanes of the pair
 __device__ __forceinline__ uint32_t xlow(uint32_t v) {
-#if RT_PAIR_ADJ
   return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0xA0, 0xF, 0xF, false);  // quad_perm [0,0,2,2]
-#else
-  return __builtin_amdgcn_permlane32_swap(v, v, false, false)[0];
-#endif
 }
 __device__ __forceinline__ float xlowf(float v) { return __uint_as_float(xlow(__float_as_uint(v))); }
 
@@ -919,16 +874,10 @@ __device__ __forceinline__ float xlowf(float v) { return __uint_as_float(xlow(__
 // push_sorted gives them (the lower lane writes c[1], the upper c[2], c[3]),
 // the nearest returned to both lanes.  `mem` / `sp`: the pair's stack (the
 // lower lane's LDS column).
-// RT_COOP_TOPREG = 1 (local sort only): the pair keeps its stack's top entry
-// in a register (`top`, row sp - 1 of the logical stack): a pop takes it at
-// once and refills it from LDS off the critical path; a push spills the old
-// top.  The logical stack -- rows, order, depth -- is unchanged.
-#ifndef RT_COOP_TOPREG
-#define RT_COOP_TOPREG 0
-#endif
-// a lane's half of a binary16 BVH4 node as loaded (RT_COOP_HALF_LOADS): the
-// planes of children 0-1 (lower lane) or 2-3 (upper) -- every other dword --
-// and the child refs, a pair
+// A lane's half of a binary16 BVH4 node as loaded (6 dword + 1 dword-pair
+// loads instead of all 64 B and a select per word): the planes of children
+// 0-1 (lower lane) or 2-3 (upper) -- every other dword -- and the child
+// refs, a pair
 struct CoopHalf {
   uint32_t w[6];
   uint2 cc;
@@ -944,7 +893,7 @@ __device__ __forceinline__ CoopHalf coop_half_load(const Scene& S, uint32_t ref,
 }
 template <bool SCALAR>
 __device__ __forceinline__ int32_t node4_coop(const Scene& S, uint32_t ref, const Ray& r, float lim,
-                                              bool hi, int32_t* mem, int& sp, int32_t& top,
+                                              bool hi, int32_t* mem, int& sp,
                                               const CoopHalf* pre = nullptr) {
   auto ld = [&](uint32_t o) { return SCALAR ? S.A.sld_f4(o) : S.A.ld_f4(o); };
   const uint32_t no = S.nodes4 + 128u * S.num_nodes4 + 64u * ref;
@@ -955,9 +904,9 @@ __device__ __forceinline__ int32_t node4_coop(const Scene& S, uint32_t ref, cons
   };
   float lx[2], hx[2], ly[2], hy[2], lz[2], hz[2];
   int32_t c[2];
-  if (RT_COOP_HALF_LOADS && !SCALAR) {
+  if (!SCALAR) {
     // each lane loads only its half (or has it already: `pre`, loaded while
-    // the pair tested a leaf -- trace_coop RT_COOP_LEAF_PF)
+    // the pair tested a leaf -- trace_coop)
     const CoopHalf hh = pre ? *pre : coop_half_load(S, ref, hi);
     const auto f = [&](int i) { return __uint_as_float(hh.w[i]); };
     h2(f(0), lx[0], lx[1]); h2(f(1), hx[0], hx[1]);
@@ -981,7 +930,7 @@ __device__ __forceinline__ int32_t node4_coop(const Scene& S, uint32_t ref, cons
     k[i] = h ? fminf(tn, 3.402823466e38f) : __builtin_inff();
     nh += h ? 1u : 0u;
   }
-#if RT_COOP_LOCAL_SORT && RT_PUSH_UNCOND
+#if RT_PUSH_UNCOND
   // One exchange round: both lanes take the partner's two keys and children
   // (four independent swaps), then run the whole network of node4_step
   // locally in slot order -- the same comparisons, so the same order, ties
@@ -1008,22 +957,9 @@ __device__ __forceinline__ int32_t node4_coop(const Scene& S, uint32_t ref, cons
       const int rr = sp + n - 1 - j;
       return (j < n && rr < RT_MAX_STACK) ? rr : RT_MAX_STACK;
     };
-#if RT_COOP_TOPREG
-    // rows: the old top back to sp - 1 (lower lane, when the push is not
-    // empty and the stack was not), C[2] (lower) and C[3] (upper) to theirs;
-    // C[1] becomes the top
-    const bool spill = n >= 2 && sp > 0 && sp - 1 < RT_MAX_STACK;
-    const int ra = hi ? row(3) : (spill ? sp - 1 : RT_MAX_STACK), rb = hi ? RT_MAX_STACK : row(2);
-    mem[64 * ra] = hi ? C[3] : top;
-    mem[64 * rb] = C[2];
-    if (n >= 2) top = C[1];
-    (void)row;
-#else
-    (void)top;
     const int ra = row(hi ? 2 : 1), rb = hi ? row(3) : RT_MAX_STACK;
     mem[64 * ra] = hi ? C[2] : C[1];
     mem[64 * rb] = C[3];
-#endif
     const int nt = sp + n - 1;
     sp = nt < RT_MAX_STACK ? nt : RT_MAX_STACK;
     return C[0];
@@ -1053,7 +989,6 @@ __device__ __forceinline__ int32_t node4_coop(const Scene& S, uint32_t ref, cons
     if (hi) { c[0] = s ? pc : c[0]; }
     else { c[1] = s ? pc : c[1]; }
   }
-  (void)top;
   const int n = (int)(nh + xpart(nh, hi));
   if (n == 0) return RT_EMPTY_REF;
   // entry c[j] at row sp + n - 1 - j (j < n, below RT_MAX_STACK)
@@ -1065,8 +1000,8 @@ __device__ __forceinline__ int32_t node4_coop(const Scene& S, uint32_t ref, cons
   return (int32_t)xlow((uint32_t)c[0]);
 }
 
-// RT_COOP_LEAF_PF = 1: after a leaf round's triangle loads are issued the pair
-// pops the next stack entry and, when it is a node, issues that node's loads
+// With the slack rows (RT_PUSH_UNCOND), after a leaf round's triangle loads
+// are issued the pair pops the next stack entry and, when it is a node, issues that node's loads
 // too, before the triangle tests; the node's step then runs on those
 // registers (its slab tests still use the best hit after the leaf).  The
 // same visits in the same order: only the load latency overlaps the tests.
@@ -1082,9 +1017,6 @@ __device__ __forceinline__ int32_t node4_coop(const Scene& S, uint32_t ref, cons
 // visits): r05v 0.12505 vs 0.11556, not kept; nor the BVH4 staged in LDS
 // by every pair-walking wave, the halves read from there: r05af 0.12778 vs
 // 0.11769 -- the copy and the lower occupancy cost more than L1 hits save.)
-#ifndef RT_COOP_LEAF_PF
-#define RT_COOP_LEAF_PF 1
-#endif
 
 // trace<false> (closest hit from 0 below +inf, binary16 BVH4) by a lane pair;
 // both lanes return the hit and *t_out
@@ -1092,24 +1024,17 @@ __device__ __forceinline__ int32_t trace_coop(const Scene& S, const Ray& r, int3
                                               float* t_out, int32_t* mem, bool hi, Counters& cnt) {
   if (S.num_nodes == 0) return -1;
   int sp = 0;
-  int32_t top = RT_EMPTY_REF;  // RT_COOP_TOPREG: the stack's top entry
   float bt = INFINITY;
   int32_t bpid = -1;
   RT_CNT(cnt.visits += hi ? 0u : 1u;)
-  int32_t ref = node4_coop<true>(S, 0u, r, bt, hi, mem, sp, top);
+  int32_t ref = node4_coop<true>(S, 0u, r, bt, hi, mem, sp);
   if (ref == RT_EMPTY_REF) return -1;
   auto pop = [&](int32_t& x) {
     if (sp == 0) return false;
-#if RT_COOP_TOPREG && RT_COOP_LOCAL_SORT && RT_PUSH_UNCOND
-    x = top;
-    --sp;
-    top = mem[64 * (sp > 0 ? sp - 1 : RT_MAX_STACK)];  // refill (a slack row when empty)
-#else
     x = mem[64 * --sp];
-#endif
     return true;
   };
-  int32_t nref = RT_EMPTY_REF;  // RT_COOP_LEAF_PF: the entry popped during a leaf round
+  int32_t nref = RT_EMPTY_REF;  // the entry popped during a leaf round (RT_PUSH_UNCOND)
   bool pf = false;              // ... a node, whose loads are in `pre`
   CoopHalf pre;
   (void)nref; (void)pf; (void)pre;
@@ -1120,7 +1045,7 @@ __device__ __forceinline__ int32_t trace_coop(const Scene& S, const Ray& r, int3
       while (ref >= 0) {  // while-while, as trace_impl
         RT_WAVE_ITER(9);
         RT_CNT(cnt.visits += hi ? 0u : 1u;)
-        const int32_t nx = node4_coop<false>(S, (uint32_t)ref, r, bt, hi, mem, sp, top);
+        const int32_t nx = node4_coop<false>(S, (uint32_t)ref, r, bt, hi, mem, sp);
         if (nx != RT_EMPTY_REF) { ref = nx; continue; }
         if (!pop(ref)) { dry = true; break; }
       }
@@ -1131,13 +1056,9 @@ __device__ __forceinline__ int32_t trace_coop(const Scene& S, const Ray& r, int3
       RT_WAVE_ITER(9);  // this lane's two of the leaf's (up to 4) triangles (padding records past the end)
       const uint32_t lr = (uint32_t)ref;
       const uint32_t first = (lr >> 4) & 0x07ffffffu, count = (lr & 15u) + 1u;
-#if RT_COOP_LEAF_IL
       // the lower lane triangles 0 and 2, the upper 1 and 3: a two-triangle
       // leaf is one test per lane
       const uint32_t k0 = hi ? 1u : 0u, ks = 2u;
-#else
-      const uint32_t k0 = hi ? 2u : 0u, ks = 1u;
-#endif
       const uint32_t to = S.tris + 48u * (first + k0);
       float4 ta[2], tb[2], tc[2];
 #pragma unroll
@@ -1146,7 +1067,7 @@ __device__ __forceinline__ int32_t trace_coop(const Scene& S, const Ray& r, int3
         tb[k] = S.A.ld_f4(to + 48u * ks * k + 16);
         tc[k] = S.A.ld_f4(to + 48u * ks * k + 32);
       }
-#if RT_COOP_LEAF_PF && RT_COOP_HALF_LOADS && RT_COOP_LOCAL_SORT && RT_PUSH_UNCOND && !RT_COOP_TOPREG
+#if RT_PUSH_UNCOND
       // the next entry and, for a node, its loads -- in flight during the tests
       const bool more = sp > 0;
       nref = more ? mem[64 * (sp - 1)] : RT_EMPTY_REF;
@@ -1154,21 +1075,6 @@ __device__ __forceinline__ int32_t trace_coop(const Scene& S, const Ray& r, int3
       pf = more && nref >= 0;
       if (pf) pre = coop_half_load(S, (uint32_t)nref, hi);
 #endif
-#if RT_COOP_LEAF_BF
-      // both tests computed, the best taken by selects (no branches)
-#pragma unroll
-      for (uint32_t k = 0; k < 2; ++k) {
-        const bool in = k0 + ks * k < count;
-        const int32_t pid = __float_as_int(ta[k].w);
-        RT_CNT(cnt.tests += in ? 1u : 0u;)
-        float t;
-        const bool h = mt_hit_bf(r, ta[k], tb[k], tc[k], 0.0f, &t);
-        const bool cl = (t < bt) | ((t == bt) & (tie_high ? pid > bpid : pid < bpid));
-        const bool take = in & (pid != skip) & h & cl;
-        bt = take ? t : bt;
-        bpid = take ? pid : bpid;
-      }
-#else
 #pragma unroll
       for (uint32_t k = 0; k < 2; ++k) {
         if (k0 + ks * k < count) {
@@ -1181,7 +1087,6 @@ __device__ __forceinline__ int32_t trace_coop(const Scene& S, const Ray& r, int3
           }
         }
       }
-#endif
       // the pair's best: closer() is a strict total order, so both lanes
       // agree and it is the four tests' sequential result
       const float pbt = xpartf(bt, hi);
@@ -1191,174 +1096,20 @@ __device__ __forceinline__ int32_t trace_coop(const Scene& S, const Ray& r, int3
         bpid = pb;
       }
     }
-#if RT_COOP_LEAF_PF && RT_COOP_HALF_LOADS && RT_COOP_LOCAL_SORT && RT_PUSH_UNCOND && !RT_COOP_TOPREG
+#if RT_PUSH_UNCOND
     if (nref == RT_EMPTY_REF) break;  // the stack was empty
     ref = nref;
     if (pf) {
       // the popped node's step on the registers loaded during the tests
       // (node4_coop's own step: the same visit, the same pushes)
       RT_CNT(cnt.visits += hi ? 0u : 1u;)
-      const int32_t nx = node4_coop<false>(S, (uint32_t)ref, r, bt, hi, mem, sp, top, &pre);
+      const int32_t nx = node4_coop<false>(S, (uint32_t)ref, r, bt, hi, mem, sp, &pre);
       if (nx != RT_EMPTY_REF) ref = nx;
       else if (!pop(ref)) break;
     }
 #else
     if (!pop(ref)) break;
 #endif
-  }
-  if (bpid >= 0) *t_out = bt;
-  return bpid;
-}
-
-// The BVH8 closest-hit step for a lane pair (pt_kernel8: RT_BVH8): the
-// lower lane reads half 0 of the rt_node8h_t (children 0-3), the upper half 1
-// (children 4-7); each slab-tests its four, the pair swaps the four keys and
-// children (DPP moves), and both lanes run bvh8_step's 19-comparator network
-// (oracle/rt.c: Batcher's odd-even merge sort, strict <, misses keyed +inf,
-// hit keys clamped to FLT_MAX) over slots 0-7, then push C[1..n-1] farthest
-// first with unconditional row stores (the lower lane C[1..3], the upper
-// C[4..7]; entries past the hit count to the slack row RT_MAX_STACK) and take
-// C[0].  Per ray: the per-lane BVH8 walk's visits, stack order and result.
-template <bool SCALAR>
-__device__ __forceinline__ int32_t node8_coop(const Scene& S, uint32_t ref, const Ray& r, float lim, bool hi,
-                                              int32_t* mem, int& sp) {
-  const uint32_t no = S.nodes8 + 128u * ref;
-  uint4 w[4];
-  if (SCALAR) {  // the root: both halves through the scalar cache, this lane's selected
-    uint4 nw[8];
-    S.A.sld_u4n<8>(no, nw);
-#pragma unroll
-    for (int q = 0; q < 4; ++q) w[q] = hi ? nw[4 + q] : nw[q];
-  } else {
-    const uint32_t ho = no + (hi ? 64u : 0u);
-#pragma unroll
-    for (int q = 0; q < 4; ++q) w[q] = S.A.ld_u4(ho + 16u * q);
-  }
-  auto h2 = [](uint32_t u, float& a, float& b) {
-    a = (float)__builtin_bit_cast(_Float16, (uint16_t)(u & 0xffffu));
-    b = (float)__builtin_bit_cast(_Float16, (uint16_t)(u >> 16));
-  };
-  float lx[4], hx[4], ly[4], hy[4], lz[4], hz[4];
-  h2(w[0].x, lx[0], lx[1]); h2(w[0].y, lx[2], lx[3]); h2(w[0].z, hx[0], hx[1]); h2(w[0].w, hx[2], hx[3]);
-  h2(w[1].x, ly[0], ly[1]); h2(w[1].y, ly[2], ly[3]); h2(w[1].z, hy[0], hy[1]); h2(w[1].w, hy[2], hy[3]);
-  h2(w[2].x, lz[0], lz[1]); h2(w[2].y, lz[2], lz[3]); h2(w[2].z, hz[0], hz[1]); h2(w[2].w, hz[2], hz[3]);
-  const int32_t c[4] = {(int32_t)w[3].x, (int32_t)w[3].y, (int32_t)w[3].z, (int32_t)w[3].w};
-  float k[4];
-  uint32_t nh = 0;
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    float tn = 0.0f;
-    const bool h = slab(lx[i], hx[i], ly[i], hy[i], lz[i], hz[i], r, 0.0f, lim, &tn) & (c[i] != RT_EMPTY_REF);
-    k[i] = h ? fminf(tn, 3.402823466e38f) : __builtin_inff();
-    nh += h ? 1u : 0u;
-  }
-  float K[8];
-  int32_t C[8];
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const float pk = xpartf(k[i], hi);
-    const int32_t pc = (int32_t)xpart((uint32_t)c[i], hi);
-    K[i] = hi ? pk : k[i];
-    K[4 + i] = hi ? k[i] : pk;
-    C[i] = hi ? pc : c[i];
-    C[4 + i] = hi ? c[i] : pc;
-  }
-  auto cx = [&](int a, int b) {  // swap iff K[b] < K[a]
-    const bool sw = K[b] < K[a];
-    const float ka = K[a], kb = K[b];
-    const int32_t ca = C[a], cb = C[b];
-    K[a] = sw ? kb : ka; K[b] = sw ? ka : kb;
-    C[a] = sw ? cb : ca; C[b] = sw ? ca : cb;
-  };
-  cx(0, 1); cx(2, 3); cx(4, 5); cx(6, 7);
-  cx(0, 2); cx(1, 3); cx(4, 6); cx(5, 7);
-  cx(1, 2); cx(5, 6);
-  cx(0, 4); cx(1, 5); cx(2, 6); cx(3, 7);
-  cx(2, 4); cx(3, 5);
-  cx(1, 2); cx(3, 4); cx(5, 6);
-  const int n = (int)(nh + xpart(nh, hi));
-  if (n == 0) return RT_EMPTY_REF;
-  auto row = [&](int j) {
-    const int rr = sp + n - 1 - j;
-    return (j < n && rr < RT_MAX_STACK) ? rr : RT_MAX_STACK;
-  };
-  if (hi) {
-    mem[64 * row(4)] = C[4];
-    mem[64 * row(5)] = C[5];
-    mem[64 * row(6)] = C[6];
-    mem[64 * row(7)] = C[7];
-  } else {
-    mem[64 * row(1)] = C[1];
-    mem[64 * row(2)] = C[2];
-    mem[64 * row(3)] = C[3];
-  }
-  const int nt = sp + n - 1;
-  sp = nt < RT_MAX_STACK ? nt : RT_MAX_STACK;
-  return C[0];
-}
-
-// trace_coop on the BVH8 (node8_coop; leaves as trace_coop's)
-__device__ __forceinline__ int32_t trace_coop8(const Scene& S, const Ray& r, int32_t skip, bool tie_high,
-                                               float* t_out, int32_t* mem, bool hi, Counters& cnt) {
-  if (S.num_nodes8 == 0) return trace_coop(S, r, skip, tie_high, t_out, mem, hi, cnt);
-  int sp = 0;
-  float bt = INFINITY;
-  int32_t bpid = -1;
-  RT_CNT(cnt.visits += hi ? 0u : 1u;)
-  int32_t ref = node8_coop<true>(S, 0u, r, bt, hi, mem, sp);
-  if (ref == RT_EMPTY_REF) return -1;
-  auto pop = [&](int32_t& x) {
-    if (sp == 0) return false;
-    x = mem[64 * --sp];
-    return true;
-  };
-  for (;;) {
-    bool dry = false;
-    {
-      RT_CYC_BEGIN();
-      while (ref >= 0) {  // while-while, as trace_impl
-        RT_WAVE_ITER(9);
-        RT_CNT(cnt.visits += hi ? 0u : 1u;)
-        const int32_t nx = node8_coop<false>(S, (uint32_t)ref, r, bt, hi, mem, sp);
-        if (nx != RT_EMPTY_REF) { ref = nx; continue; }
-        if (!pop(ref)) { dry = true; break; }
-      }
-      RT_CYC_END(11);
-    }
-    if (dry) break;
-    {
-      RT_WAVE_ITER(9);  // this lane's two of the leaf's (up to 4) triangles (padding records past the end)
-      const uint32_t lr = (uint32_t)ref;
-      const uint32_t first = (lr >> 4) & 0x07ffffffu, count = (lr & 15u) + 1u;
-      const uint32_t k0 = hi ? 1u : 0u, ks = 2u;  // the lower lane triangles 0 and 2, the upper 1 and 3
-      const uint32_t to = S.tris + 48u * (first + k0);
-      float4 ta[2], tb[2], tc[2];
-#pragma unroll
-      for (uint32_t k = 0; k < 2; ++k) {
-        ta[k] = S.A.ld_f4(to + 48u * ks * k);
-        tb[k] = S.A.ld_f4(to + 48u * ks * k + 16);
-        tc[k] = S.A.ld_f4(to + 48u * ks * k + 32);
-      }
-#pragma unroll
-      for (uint32_t k = 0; k < 2; ++k) {
-        if (k0 + ks * k < count) {
-          const int32_t pid = __float_as_int(ta[k].w);
-          RT_CNT(++cnt.tests;)
-          float t;
-          if (pid != skip && mt_hit(r, ta[k], tb[k], tc[k], 0.0f, &t) && closer(t, pid, bt, bpid, tie_high)) {
-            bt = t;
-            bpid = pid;
-          }
-        }
-      }
-      const float pbt = xpartf(bt, hi);
-      const int32_t pb = (int32_t)xpart((uint32_t)bpid, hi);
-      if (pb >= 0 && closer(pbt, pb, bt, bpid, tie_high)) {
-        bt = pbt;
-        bpid = pb;
-      }
-    }
-    if (!pop(ref)) break;
   }
   if (bpid >= 0) *t_out = bt;
   return bpid;
@@ -1383,23 +1134,6 @@ __device__ __forceinline__ bool occluded_list_coop(const Scene& S, const Ray& s,
       float4 t[6];
 #pragma unroll
       for (int w = 0; w < 6; ++w) t[w] = S.A.ld_f4(o + 16u * w);
-#if RT_COOP_LIST_BF
-      // both records' tests computed; the sequential scan's verdict and
-      // count by predicates (record 1 only when record 0 neither occluded
-      // nor ended the list)
-      float th0, th1;
-      const bool m0 = mt_hit_bf(s, t[0], t[1], t[2], 0.0f, &th0);
-      const bool m1 = mt_hit_bf(s, t[3], t[4], t[5], 0.0f, &th1);
-      const bool end0 = t[1].w > lim;
-      const bool test0 = !end0;
-      const bool hit0 = test0 & (__float_as_int(t[0].w) != skip) & m0 & (th0 < 1.0f);
-      const bool do1 = !hit0 & !end0 & (q + e0 + 1u < n);
-      const bool end1 = do1 & (t[4].w > lim);
-      const bool test1 = do1 & !end1;
-      hit = hit0 | (test1 & (__float_as_int(t[3].w) != skip) & m1 & (th1 < 1.0f));
-      end = end0 | end1;
-      RT_CNT(tests += (test0 ? 1u : 0u) + (test1 ? 1u : 0u);)
-#else
 #pragma unroll
       for (uint32_t e = 0; e < 2; ++e) {
         if (!hit && !end && q + e0 + e < n) {
@@ -1412,7 +1146,6 @@ __device__ __forceinline__ bool occluded_list_coop(const Scene& S, const Ray& s,
           }
         }
       }
-#endif
     }
     // the records are sorted: past the lower lane's bound the upper lane's
     // are too, so the first event in list order decides
@@ -1420,171 +1153,6 @@ __device__ __forceinline__ bool occluded_list_coop(const Scene& S, const Ray& s,
     RT_CNT(cnt.tests += (hi && pev != 0u) ? 0u : tests;)
     if (((ev | pev) & 1u) != 0u) return true;
     if (((ev | pev) & 2u) != 0u) return false;
-  }
-  return false;
-}
-
-// Quad walks for the path tracer's 16-pixel waves (pt_kernel PT_QUAD): the
-// four lanes 4p .. 4p + 3 trace pixel p's ray together, lane j = lane & 3
-// taking a BVH4 node's child j, a leaf's triangle j and a list round's
-// record j.  The lanes exchange values within their quad by DPP quad_perm
-// moves (no LDS, no permlane): the node step's 5-exchange sorting network
-// (node4_step's: (0,1)(2,3) | (0,2)(1,3) | (1,2)) runs across the quad,
-// lane j ending with the j-th nearest hit child, so lane j pushes its child at
-// the row push_sorted gives it (one LDS column per quad); a leaf's best hit
-// and a list round's first event are quad reductions.  Per ray the node
-// visits, the stack's order and the result are the per-lane walk's
-// (trace_impl / occluded_list), and so are the counters (visits counted by
-// lane 0, tests by the lane that made them, a list round's only up to its
-// first event in list order).
-#define RT_QP_XOR1 0xB1  // quad_perm [1,0,3,2]
-#define RT_QP_XOR2 0x4E  // quad_perm [2,3,0,1]
-#define RT_QP_MID 0xD8   // quad_perm [0,2,1,3]
-#define RT_QP_B0 0x00    // quad_perm [0,0,0,0]
-template <int CTRL>
-__device__ __forceinline__ uint32_t qmov(uint32_t v) {
-  return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, CTRL, 0xF, 0xF, false);
-}
-template <int CTRL>
-__device__ __forceinline__ float qmovf(float v) { return __uint_as_float(qmov<CTRL>(__float_as_uint(v))); }
-// the quad's 4 bits of a wave mask (lane j of the quad = bit j)
-__device__ __forceinline__ uint32_t quad_bits(uint64_t m) {
-  return (uint32_t)(m >> (lane_id() & ~3u)) & 0xFu;
-}
-// one compare-exchange of the sorting network between quad lanes `lo` < `hi`
-// (CTRL: the permutation pairing them): the lower lane keeps the nearer
-// (strict <, node4_step's cx), the upper the farther, the child moving along
-template <int CTRL>
-__device__ __forceinline__ void qcx(float& k, int32_t& c, bool lower, bool part) {
-  const float pk = qmovf<CTRL>(k);
-  const int32_t pc = (int32_t)qmov<CTRL>((uint32_t)c);
-  if (!part) return;
-  const bool s = lower ? pk < k : k < pk;
-  k = s ? pk : k;
-  c = s ? pc : c;
-}
-
-template <bool SCALAR>
-__device__ __forceinline__ int32_t node4_quad(const Scene& S, uint32_t ref, const Ray& r, float lim,
-                                              uint32_t j, int32_t* mem, int& sp) {
-  auto ld = [&](uint32_t o) { return SCALAR ? S.A.sld_u4(o) : S.A.ld_u4(o); };
-  const uint32_t no = S.nodes4 + 128u * S.num_nodes4 + 64u * ref;
-  const uint4 px = ld(no), py = ld(no + 16), pz = ld(no + 32), cf = ld(no + 48);
-  // child j's planes: half j (lo) and half 4 + j (hi) of each axis' 16 B
-  const uint32_t sh = (j & 1u) * 16u;
-  auto half = [&](const uint4& w, bool upper) {
-    const uint32_t word = upper ? ((j >> 1) ? w.w : w.z) : ((j >> 1) ? w.y : w.x);
-    return (float)__builtin_bit_cast(_Float16, (uint16_t)((word >> sh) & 0xffffu));
-  };
-  const int32_t c0 = (int32_t)(j == 0 ? cf.x : j == 1 ? cf.y : j == 2 ? cf.z : cf.w);
-  float tn = 0.0f;
-  const bool h = slab(half(px, false), half(px, true), half(py, false), half(py, true), half(pz, false),
-                      half(pz, true), r, 0.0f, lim, &tn) &
-                 (c0 != RT_EMPTY_REF);
-  float k = h ? fminf(tn, 3.402823466e38f) : __builtin_inff();
-  int32_t c = c0;
-  const uint32_t n = (uint32_t)__popc(quad_bits(__ballot(h)));
-  qcx<RT_QP_XOR1>(k, c, (j & 1u) == 0u, true);  // (0,1) (2,3)
-  qcx<RT_QP_XOR2>(k, c, j < 2u, true);          // (0,2) (1,3)
-  qcx<RT_QP_MID>(k, c, j == 1u, j == 1u || j == 2u);  // (1,2)
-  if (n == 0) return RT_EMPTY_REF;
-  // lane j (1 <= j < n) holds the j-th nearest hit: row sp + n - 1 - j
-  const int row = sp + (int)n - 1 - (int)j;
-  if (j >= 1u && j < n && row < RT_MAX_STACK) mem[64 * row] = c;
-  const int top = sp + (int)n - 1;
-  sp = top < RT_MAX_STACK ? top : RT_MAX_STACK;
-  return (int32_t)qmov<RT_QP_B0>((uint32_t)c);
-}
-
-// trace<false> (closest hit from 0 below +inf, binary16 BVH4) by a quad;
-// every lane of the quad returns the hit and *t_out
-__device__ __forceinline__ int32_t trace_quad(const Scene& S, const Ray& r, int32_t skip, bool tie_high,
-                                              float* t_out, int32_t* mem, uint32_t j, Counters& cnt) {
-  if (S.num_nodes == 0) return -1;
-  int sp = 0;
-  float bt = INFINITY;
-  int32_t bpid = -1;
-  RT_CNT(cnt.visits += j == 0u ? 1u : 0u;)
-  int32_t ref = node4_quad<true>(S, 0u, r, bt, j, mem, sp);
-  if (ref == RT_EMPTY_REF) return -1;
-  auto pop = [&](int32_t& x) {
-    if (sp == 0) return false;
-    x = mem[64 * --sp];
-    return true;
-  };
-  for (;;) {
-    bool dry = false;
-    {
-      RT_CYC_BEGIN();
-      while (ref >= 0) {  // while-while, as trace_impl
-        RT_WAVE_ITER(9);
-        RT_CNT(cnt.visits += j == 0u ? 1u : 0u;)
-        const int32_t nx = node4_quad<false>(S, (uint32_t)ref, r, bt, j, mem, sp);
-        if (nx != RT_EMPTY_REF) { ref = nx; continue; }
-        if (!pop(ref)) { dry = true; break; }
-      }
-      RT_CYC_END(11);
-    }
-    if (dry) break;
-    {
-      RT_WAVE_ITER(9);  // this lane's triangle of the leaf (padding records past the end)
-      const uint32_t lr = (uint32_t)ref;
-      const uint32_t first = (lr >> 4) & 0x07ffffffu, count = (lr & 15u) + 1u;
-      const uint32_t to = S.tris + 48u * (first + j);
-      const float4 ta = S.A.ld_f4(to), tb = S.A.ld_f4(to + 16), tc = S.A.ld_f4(to + 32);
-      if (j < count) {
-        const int32_t pid = __float_as_int(ta.w);
-        RT_CNT(++cnt.tests;)
-        float t;
-        if (pid != skip && mt_hit(r, ta, tb, tc, 0.0f, &t) && closer(t, pid, bt, bpid, tie_high)) {
-          bt = t;
-          bpid = pid;
-        }
-      }
-      // the quad's best: closer() is a strict total order, so every lane
-      // ends with the four tests' sequential result
-      {
-        const float pt = qmovf<RT_QP_XOR1>(bt);
-        const int32_t pb = (int32_t)qmov<RT_QP_XOR1>((uint32_t)bpid);
-        if (pb >= 0 && closer(pt, pb, bt, bpid, tie_high)) { bt = pt; bpid = pb; }
-      }
-      {
-        const float pt = qmovf<RT_QP_XOR2>(bt);
-        const int32_t pb = (int32_t)qmov<RT_QP_XOR2>((uint32_t)bpid);
-        if (pb >= 0 && closer(pt, pb, bt, bpid, tie_high)) { bt = pt; bpid = pb; }
-      }
-    }
-    if (!pop(ref)) break;
-  }
-  if (bpid >= 0) *t_out = bt;
-  return bpid;
-}
-
-// occluded_list by a quad: rounds of four records, lane j testing record
-// q + j; the first event of the round in list order (an occluder, or a
-// record past the segment bound: occluded_list's two exits) decides, and the
-// tests counted are the sequential scan's (lanes before that event, and the
-// event's own lane when it is an occluder)
-__device__ __forceinline__ bool occluded_list_quad(const Scene& S, const Ray& s, bool act, int32_t skip,
-                                                   uint32_t j, Counters& cnt) {
-  if (!act) return false;
-  const uint32_t cell = slist_cell(s, S.slist_n);
-  const uint32_t off = S.A.ld_u32(S.sidx + 8u * cell), n = S.A.ld_u32(S.sidx + 8u * cell + 4u);
-  const float lim = slist_limit(s);
-  for (uint32_t q = 0; q < n; q += 4) {
-    const uint32_t e = q + j;
-    bool hit = false, end = false;
-    if (e < n) {
-      const uint32_t o = S.slist + 48u * (off + e);
-      const float4 a = S.A.ld_f4(o), b = S.A.ld_f4(o + 16), c = S.A.ld_f4(o + 32);
-      end = b.w > lim;
-      float th;
-      hit = !end && __float_as_int(a.w) != skip && mt_hit(s, a, b, c, 0.0f, &th) && th < 1.0f;
-    }
-    const uint32_t mh = quad_bits(__ballot(hit)), me = quad_bits(__ballot(end)), mev = mh | me;
-    const uint32_t first = mev ? (uint32_t)__builtin_ctz(mev) : 4u;
-    RT_CNT(cnt.tests += (e < n && (j < first || (j == first && ((mh >> j) & 1u)))) ? 1u : 0u;)
-    if (mev) return ((mh >> first) & 1u) != 0u;
   }
   return false;
 }
@@ -1889,9 +1457,6 @@ __device__ __forceinline__ int32_t trace_primary_packet(const Scene& S, uint32_t
 // count once per wave per record tested, as the packet walk's do.  Every
 // lane of the wave calls it with the wave's local block `lb` (uniform);
 // lanes with !act get -1.
-#ifndef RT_BLIST_SKIP0
-#define RT_BLIST_SKIP0 0
-#endif
 __device__ __forceinline__ int32_t block_primary(const Scene& S, uint32_t lb, uint32_t px, uint32_t py,
                                                  bool act, bool tie_high, Counters& cnt) {
   (void)cnt;
@@ -1900,11 +1465,8 @@ __device__ __forceinline__ int32_t block_primary(const Scene& S, uint32_t lb, ui
   const uint2 oc = S.A.sld<uint2>(S.bidx + 8u * lb);
   uint32_t bz = VX_OM_DEPTH_MASK;
   int32_t bpid = -1;
-  // RT_BLIST_SKIP0 = 1: a block no candidate reaches (the background's)
-  // skips the list load, whose scalar round trip holds up the wave's next
-  // scalar load (scalar loads complete out of order and are waited for
-  // together) -- measured 0.01868 vs 0.01836 ms (r04zj, noise), off
-  if (RT_BLIST_SKIP0 && oc.y == 0) return -1;
+  // (skipping the list load of a block no candidate reaches measured no
+  // gain, r04zj: the wave's next scalar load waits on it either way)
   uint4 e[2];
   S.A.sld_u4n<2>(S.blist + 16u * oc.x, e);  // the list array carries RT_BLIST_PAD padding entries
   for (uint32_t k = 0; k < oc.y; k += 2) {
@@ -1961,29 +1523,15 @@ __device__ __forceinline__ bool secondary_ok(float t) { return t > 0.0f && t < I
 // counted once per wave by its first active lane -- a record is one scalar
 // load for the whole wave, the rule block_primary's and the packet walks'
 // record tests follow (oracle/rt.c layer_waves: max over the wave's lanes)
-// RT_PREFETCH_LAYER = 1: the first layer record is loaded (scalar cache) when
-// the wave starts, its latency hidden under the primary pass
-#ifndef RT_PREFETCH_LAYER
-#define RT_PREFETCH_LAYER 0
-#endif
-struct LayerPre {
-  uint4 w[3];
-};
-__device__ __forceinline__ void layer_prefetch(const Scene& S, LayerPre& L) {
-  if (RT_PREFETCH_LAYER && S.num_layer > 0) S.A.sld_u4n<3>(S.vlayers, L.w);
-}
+// (loading the first layer record at wave start, its latency under the
+// primary pass, measured no gain: r04zj)
 __device__ __forceinline__ int32_t resolve_layers_n(const Scene& S, uint32_t px, uint32_t py, bool need,
-                                                    int32_t spid, uint32_t* tests,
-                                                    const LayerPre* pre = nullptr) {
+                                                    int32_t spid, uint32_t* tests) {
   uint64_t pend = __ballot(need);
   const uint32_t lead = lane_id() == (uint32_t)__builtin_ctzll(__ballot(1)) ? 1u : 0u;
   for (uint32_t k = 0; pend != 0 && k < S.num_layer; ++k) {
     uint4 lw[3];
-    if (RT_PREFETCH_LAYER && pre && k == 0) {
-      lw[0] = pre->w[0]; lw[1] = pre->w[1]; lw[2] = pre->w[2];
-    } else {
-      S.A.sld_u4n<3>(S.vlayers + 64u * k, lw);  // one pointer: merged wide s_loads
-    }
+    S.A.sld_u4n<3>(S.vlayers + 64u * k, lw);  // one pointer: merged wide s_loads
     const uint4 A = lw[0], B = lw[1], C = lw[2];
     const bool mine = (pend & (1ull << lane_id())) != 0;
     *tests += lead;
@@ -2001,10 +1549,9 @@ __device__ __forceinline__ int32_t resolve_layers_n(const Scene& S, uint32_t px,
   return spid;
 }
 __device__ __forceinline__ int32_t resolve_layers(const Scene& S, uint32_t px, uint32_t py, bool need,
-                                                  int32_t spid, Counters& cnt,
-                                                  const LayerPre* pre = nullptr) {
+                                                  int32_t spid, Counters& cnt) {
   uint32_t tests = 0;
-  spid = resolve_layers_n(S, px, py, need, spid, &tests, pre);
+  spid = resolve_layers_n(S, px, py, need, spid, &tests);
 #ifdef RT_INSTRUMENT
   cnt.layer_tests += tests;
 #else

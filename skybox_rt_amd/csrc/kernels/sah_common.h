@@ -20,8 +20,7 @@
 //     it is a prefix sum over positions plus the depth within the chain;
 //   * the BVH4 collapse per BVH2 node (its expansion), membership by a walk
 //     down the node's root path, BVH4 preorder = the BVH2 preorder
-//     restricted to BVH4 nodes (a prefix sum); the BVH8 the same way with up
-//     to 8 children (phases SAH_CS8 .. SAH_EMIT8).
+//     restricted to BVH4 nodes (a prefix sum).
 #pragma once
 
 #include <stdint.h>
@@ -48,11 +47,6 @@ enum {
                    // (8: the binary16 pass, folded into SAH_EMIT4 in r04)
   SAH_RESET = 9,   // the numbering's counters again (a sequence continued past its level budget)
   SAH_SCAN4 = 10,  // exclusive scan of the BVH4 membership (is4, one word per BVH2 node)
-  // the BVH8 (rt_node8h_t): the same collapse with up to 8 children
-  SAH_CS8 = 11,    // BVH8 expansion of every BVH2 node
-  SAH_MARK8 = 12,  // BVH8 membership, depth, worst-case stack
-  SAH_SCAN8 = 13,  // exclusive scan of the BVH8 membership (is8)
-  SAH_EMIT8 = 14,  // rt_node8h_t at BVH8 preorder indices (two rt_node4h_t halves)
 };
 // a sequence entry: the phase, and the tree level of a SAH_SPLIT
 #define SAH_SEQ(phase, level) ((uint32_t)(phase) | ((uint32_t)(level) << 8))
@@ -67,10 +61,7 @@ enum {
 #define SAH_CTL_NODES4 6   // BVH4 nodes (SAH_EMIT4: the membership scan's total)
 #define SAH_CTL_SEG 8      // [SAH_CTL_SEG + L]: workgroup segments of level L
 #define SAH_CTL_SMALL (SAH_CTL_SEG + SAH_MAX_LEVELS + 1)  // [.. + L]: wave segments of level L
-#define SAH_CTL_NODES8 7   // BVH8 nodes (SAH_EMIT8: the membership scan's total)
-#define SAH_CTL_DEPTH8 (SAH_CTL_SMALL + SAH_MAX_LEVELS + 1)  // BVH8 depth
-#define SAH_CTL_STACK8 (SAH_CTL_DEPTH8 + 1)                 // BVH8 worst-case traversal stack
-#define SAH_CTL_WORDS (SAH_CTL_STACK8 + 1)
+#define SAH_CTL_WORDS (SAH_CTL_SMALL + SAH_MAX_LEVELS + 1)
 
 typedef struct {
   uint32_t b, e, node, depth;
@@ -97,9 +88,6 @@ typedef struct {
   uint64_t nodes_addr;    // rt_node_t [max(n, 1)] (nn = ctl[SAH_CTL_NODES] used)
   uint64_t tris_addr;     // rt_tri_t [n + 3]
   uint64_t nodes4_addr;   // rt_node4_t [nn4], then rt_node4h_t [nn4] (nn4 = is4[nn]; room for n each)
-  uint64_t cs8_addr;      // i32 [n][16]: BVH8 expansion: 8 refs, 8 sources
-  uint64_t is8_addr;      // u32 [n + 1]: BVH8 membership -> scan -> BVH8 preorder
-  uint64_t nodes8_addr;   // rt_node8h_t [nn8] (room for n)
   uint32_t n, nseq;
   uint32_t seq[SAH_MAX_SEQ];  // SAH_SEQ entries, launch i runs seq[i]
 } sah_arg_t;

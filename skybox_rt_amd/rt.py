@@ -48,19 +48,17 @@ class SceneInfo(C.Structure):
         "num_drawcalls", "num_prims", "num_geometry", "num_layer", "num_textures",
         "bvh_nodes", "bvh_tris", "bvh_leaves", "bvh_depth", "bvh4_nodes", "bvh4_depth",
         "bvh4_stack", "bvh4_f16")] + [
-        ("parse_ms", C.c_double), ("bvh_ms", C.c_double)] + [
-        (n, C.c_uint32) for n in ("bvh8_nodes", "bvh8_depth", "bvh8_stack", "pad8")]
+        ("parse_ms", C.c_double), ("bvh_ms", C.c_double)]
 
 
 class BvhBuildStats(C.Structure):
     _fields_ = [("nodes", C.c_uint32), ("depth", C.c_uint32), ("launches", C.c_uint32),
                 ("stack4", C.c_uint32), ("build_ms", C.c_double), ("kernel_ms", C.c_double),
                 ("nodes4", C.c_uint32), ("depth4", C.c_uint32), ("method", C.c_uint32),
-                ("pad", C.c_uint32), ("nodes8", C.c_uint32), ("depth8", C.c_uint32),
-                ("stack8", C.c_uint32), ("pad8", C.c_uint32)]
+                ("pad", C.c_uint32)]
 
     def as_dict(self):
-        return {n: getattr(self, n) for n, _ in self._fields_ if n not in ("pad", "pad8")}
+        return {n: getattr(self, n) for n, _ in self._fields_ if n != "pad"}
 
 
 class SetupStats(C.Structure):
@@ -68,7 +66,7 @@ class SetupStats(C.Structure):
                 ("blist_blocks", C.c_uint32), ("setup_ms", C.c_double), ("configure_ms", C.c_double),
                 ("blist_entries", C.c_uint64), ("blist_max", C.c_uint32), ("slist_on", C.c_uint32),
                 ("slist_entries", C.c_uint64), ("path_queue", C.c_uint32), ("slist_built", C.c_uint32),
-                ("bvh8", C.c_uint32), ("pad", C.c_uint32)]
+                ("pad", C.c_uint32)]
 
     def as_dict(self):
         return {n: getattr(self, n) for n, _ in self._fields_ if n != "pad"}
@@ -112,8 +110,6 @@ def lib():
             "rt_scene_export_prims": [vp, vp, u64],
             "rt_scene_export_bvh": [vp, vp, vp],
             "rt_scene_export_bvh4": [vp, vp],
-            "rt_scene_export_bvh8": [vp, vp],
-            "rt_renderer_export_bvh8h": [vp, vp, C.POINTER(u32)],
             "rt_renderer_build_bvh": [vp, C.POINTER(BvhBuildStats)],
             "rt_renderer_build_bvh_ex": [vp, u32, C.POINTER(BvhBuildStats)],
             "rt_renderer_bvh_stats": [vp, C.POINTER(BvhBuildStats)],
@@ -197,14 +193,6 @@ class Scene:
         nodes4 = np.zeros((max(n, 1), 32), np.float32)
         _check(lib().rt_scene_export_bvh4(self._h, nodes4.ctypes.data), "rt_scene_export_bvh4")
         return nodes4[:n]
-
-    def bvh8(self):
-        """The 8-wide BVH nodes as fp32 (float32[N8, 64]: two rt_node4_t halves per
-        node, children 0-3 and 4-7, binary16-rounded planes); leaves index bvh()'s tris."""
-        n = self.info()["bvh8_nodes"]
-        nodes8 = np.zeros((max(n, 1), 64), np.float32)
-        _check(lib().rt_scene_export_bvh8(self._h, nodes8.ctypes.data), "rt_scene_export_bvh8")
-        return nodes8[:n]
 
     def setup_prims(self, width: int, height: int) -> np.ndarray:
         """rt_prim_t shading records (int32[P, 32]) at width x height."""
@@ -372,16 +360,6 @@ class Renderer:
         out = np.zeros((max(n.value, 1), 64), np.uint8)
         _check(lib().rt_renderer_export_bvh4h(self._h, out.ctypes.data, C.byref(n)),
                "rt_renderer_export_bvh4h")
-        return out[:n.value]
-
-    def export_bvh8h(self):
-        """The renderer's BVH8 as rt_node8h_t records (uint8[N8, 128]: two
-        rt_node4h_t halves) -- what the BVH8 images read; empty without one."""
-        n = C.c_uint32()
-        _check(lib().rt_renderer_export_bvh8h(self._h, None, C.byref(n)), "rt_renderer_export_bvh8h")
-        out = np.zeros((max(n.value, 1), 128), np.uint8)
-        _check(lib().rt_renderer_export_bvh8h(self._h, out.ctypes.data, C.byref(n)),
-               "rt_renderer_export_bvh8h")
         return out[:n.value]
 
     def export_vis_tree(self):

@@ -41,21 +41,6 @@ def _host_renderer(s):
     return r
 
 
-class _bvh8_env:
-    """RT_BVH8=1 while a renderer builds its tree: the device SAH build then
-    also emits the BVH8 collapse (4 more finishing launches)."""
-
-    def __enter__(self):
-        self.old = os.environ.get("RT_BVH8")
-        os.environ["RT_BVH8"] = "1"
-
-    def __exit__(self, *exc):
-        if self.old is None:
-            del os.environ["RT_BVH8"]
-        else:
-            os.environ["RT_BVH8"] = self.old
-
-
 def _scene(name, tmp_path_factory):
     if name in _paths:
         return _paths[name]
@@ -83,30 +68,23 @@ def test_gpu_sah_equals_host_build(tmp_path_factory, name):
     host = _host_renderer(s)                  # the scene's host-built tree
     hn, ht = host.export_bvh()
     h4, hh = host.export_bvh4(), host.export_bvh4h()
-    h8 = host.export_bvh8h()
-    with _bvh8_env():
-        r = rt.Renderer(s)
-        st = r.build_bvh("sah")
+    r = rt.Renderer(s)
+    st = r.build_bvh("sah")
     dn, dt = r.export_bvh()
     assert dn.shape == hn.shape and np.array_equal(dn.view(np.uint32), hn.view(np.uint32))
     assert dt.shape == ht.shape and np.array_equal(dt.view(np.uint32), ht.view(np.uint32))
     d4 = r.export_bvh4()
     assert d4.shape == h4.shape and np.array_equal(d4.view(np.uint32), h4.view(np.uint32))
     assert np.array_equal(r.export_bvh4h(), hh)
-    # the BVH8 collapse (rt_node8h_t records) and its depth / stack
-    d8 = r.export_bvh8h()
-    assert d8.shape == h8.shape == (info["bvh8_nodes"], 128) and np.array_equal(d8, h8)
-    assert st["nodes8"] == info["bvh8_nodes"] and st["depth8"] == info["bvh8_depth"]
-    assert st["stack8"] == info["bvh8_stack"]
     assert st["depth"] == info["bvh_depth"] and st["nodes"] == info["bvh_nodes"]
     assert st["nodes4"] == info["bvh4_nodes"] and st["depth4"] == info["bvh4_depth"]
     assert st["stack4"] == info["bvh4_stack"] and st["method"] == 1
-    # one sequence: the init, the level budget's split launches, 11 finishing
-    # launches (BVH2, BVH4, BVH8 under RT_BVH8) -- and, past the budget, a
-    # reset, the next levels, 11 again
+    # one sequence: the init, the level budget's split launches, 7 finishing
+    # launches (BVH2, BVH4) -- and, past the budget, a reset, the next levels,
+    # 7 again
     budget = math.ceil(math.log2(info["num_geometry"] + 1)) + 4
     rounds = 1 if info["bvh_depth"] <= budget else 2
-    assert st["launches"] == 1 + min(rounds * budget, 63) + 11 * rounds + (rounds - 1)
+    assert st["launches"] == 1 + min(rounds * budget, 63) + 7 * rounds + (rounds - 1)
     if name == "chain96":
         assert rounds == 2
     print(f"{name}: {info['num_geometry']} tris, {st['nodes']} nodes, {st['launches']} launches, "
@@ -158,18 +136,14 @@ def test_gpu_sah_deep_tree_on_stale_scratch(tmp_path_factory):
     host = _host_renderer(s)
     hn, ht = host.export_bvh()
     h4, hh = host.export_bvh4(), host.export_bvh4h()
-    h8 = host.export_bvh8h()
-    with _bvh8_env():
-        r = rt.Renderer(s)
+    r = rt.Renderer(s)
     for _ in range(2):
-        with _bvh8_env():
-            st = r.build_bvh("sah")
+        st = r.build_bvh("sah")
         dn, dt = r.export_bvh()
         assert np.array_equal(dn.view(np.uint32), hn.view(np.uint32))
         assert np.array_equal(dt.view(np.uint32), ht.view(np.uint32))
         assert np.array_equal(r.export_bvh4().view(np.uint32), h4.view(np.uint32))
         assert np.array_equal(r.export_bvh4h(), hh)
-        assert np.array_equal(r.export_bvh8h(), h8)
         assert st["depth"] == info["bvh_depth"] and st["stack4"] == info["bvh4_stack"]
     r.close()
     host.close()
@@ -195,8 +169,8 @@ def test_gpu_sah_rebuild(tmp_path_factory):
     print(f"tekkaman SAH build: first {first['build_ms']:.3f} ms, rebuilds {[round(t, 3) for t in times]} ms, "
           f"{st['launches']} launches")
     assert min(times) < 1.0
-    # without RT_BVH8 the build stops at the BVH4: 7 finishing launches, no BVH8
+    # the build stops at the BVH4: 7 finishing launches
     budget = math.ceil(math.log2(s.info()["num_geometry"] + 1)) + 4
-    assert st["launches"] == 1 + budget + 7 and st["nodes8"] == 0 and r.export_bvh8h().shape[0] == 0
+    assert st["launches"] == 1 + budget + 7
     r.close()
     s.close()

@@ -6,8 +6,6 @@ counter equal the oracle's restatement of the same walks (oracle/rt.c
 vis_trace_packet, bvh_trace with vis_lists / shadow_lists off); the frame
 equals the default (list) image's and, at 1024^2, the oracle's brute force.
 The bench's `series.bvh_walk` line times this image (bench.py)."""
-import os
-
 import numpy as np
 import pytest
 
@@ -27,7 +25,7 @@ def _oscene(po, name):
 
 
 @pytest.mark.parametrize("name,w,h", [("tekkaman", 1024, 1024), ("tekkaman", 257, 129),
-                                      ("carnival", 256, 256), ("scene", 200, 300)])
+                                      ("carnival", 256, 256), ("scene", 200, 300), ("box", 128, 128)])
 def test_bvh_walk_equals_oracle_with_counts(oracle_lib, name, w, h):
     po = oracle_lib
     s = rt.Scene.load(scene_path(name))
@@ -71,51 +69,5 @@ def test_bvh_walk_1024_equals_brute_force(oracle_lib):
     c, _, _, _ = po.rt_render(_oscene(po, "tekkaman"), po.rt_params(1024, 1024, shadows=True, nthreads=8),
                               bvh=None)
     assert np.array_equal(r.framebuffer(), c)
-    r.close()
-    s.close()
-
-
-@pytest.mark.parametrize("name,w,h", [("tekkaman", 1024, 1024), ("tekkaman", 257, 129),
-                                      ("carnival", 256, 256), ("scene", 200, 300), ("box", 128, 128)])
-def test_bvh8_shadow_packets_equal_oracle_with_counts(oracle_lib, name, w, h):
-    """Image rt_bvh8 (RT_BVH8=1): the shadow packets walk the BVH8
-    (rt_node8h_t, occluded_packet8) -- frame, node visits and every count
-    equal the oracle's per-lane any-hit walk of the same BVH8 in slot order
-    (oracle/rt.c bvh8_step); the frame equals the BVH4 image's."""
-    po = oracle_lib
-    s = rt.Scene.load(scene_path(name))
-    r4 = rt.Renderer(s)
-    r4.configure(w, h, shadows=True, counters=False, bvh_walk=True)
-    r4.render()
-    fb4 = r4.framebuffer()
-    r4.close()
-    # RT_BVH8=1 when the renderer builds its tree (the device SAH build then
-    # emits the BVH8) and when it is configured (the BVH8 images run)
-    os.environ["RT_BVH8"] = "1"
-    try:
-        r = rt.Renderer(s)
-        r.configure(w, h, shadows=True, instrumented=True, bvh_walk=True)
-        # a tree whose BVH8 walk could need more than the 24-entry stack
-        # (scene: 27) keeps the BVH4 images (rt_app.cpp use_bvh8)
-        on = s.info()["bvh8_stack"] <= 24
-        assert r.setup_stats()["bvh8"] == int(on)
-        r.render()
-        k_gpu = r.stats()
-        refs, pids = r.export_vis_tree()
-        c, _, _, k = po.rt_render(_oscene(po, name),
-                                  po.rt_params(w, h, shadows=True, nthreads=8, vis_lists=False,
-                                               shadow_lists=False),
-                                  bvh=s.bvh() + (s.bvh4(), s.bvh8() if on else None),
-                                  vis_tree=(refs, pids))
-        fb = r.framebuffer()
-        assert np.array_equal(fb, c) and np.array_equal(fb, fb4)
-        for key in ("node_visits", "tri_tests", "layer_tests", "shaded", "texel_bytes", "primary_rays",
-                    "shadow_rays", "geometry_hits", "occluded"):
-            assert k_gpu[key] == k[key], key
-        r.configure(w, h, shadows=True, counters=False, bvh_walk=True)
-        r.render()
-        assert np.array_equal(r.framebuffer(), fb)
-    finally:
-        del os.environ["RT_BVH8"]
     r.close()
     s.close()

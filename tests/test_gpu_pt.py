@@ -157,39 +157,3 @@ def test_pt_two_kernels_and_one_kernel_equal_oracle(po, queue, size, bounces):
         r.close()
     finally:
         del os.environ["RT_PT_QUEUE"]
-
-
-@pytest.mark.parametrize("name,size,bounces", [("tekkaman", 256, 4), ("tekkaman", 1024, 4), ("tekkaman", 333, 2),
-                                               ("box", 128, 4), ("scene", 256, 4), ("carnival", 128, 4)])
-def test_pt_kernel8_bit_exact_vs_oracle_with_counts(po, name, size, bounces):
-    """Image pt_kernel8 (RT_BVH8=1): the lane pairs' bounce walk on the BVH8
-    (node8_coop's 19-comparator network) -- frame and every counter,
-    node visits included, equal the oracle's per-lane walk of the same BVH8
-    (oracle/rt.c bvh8_step); the frame equals the BVH4 image's."""
-    import os
-    s, _, osc, bvh = setup(po, name)
-    r4 = rt.Renderer(s)  # fresh: a BVH2 frame on the cached one loaded the deep images for good
-    r4.configure(size, size, path=True, bounces=bounces, counters=False)
-    r4.render()
-    fb4 = r4.framebuffer()
-    r4.close()
-    # RT_BVH8=1 when the renderer builds its tree (the device SAH build then
-    # emits the BVH8) and when it is configured (pt_kernel8 runs)
-    os.environ["RT_BVH8"] = "1"
-    try:
-        r = rt.Renderer(s)
-        r.configure(size, size, path=True, bounces=bounces, instrumented=True)
-        # past the 24-entry stack (scene's BVH8: 27) the BVH4 image stays
-        on = s.info()["bvh8_stack"] <= 24
-        assert r.setup_stats()["bvh8"] == int(on)
-        r.render()
-        fb, st = r.framebuffer(), r.stats()
-        c, _, _, k = po.rt_render(osc, po.rt_params(size, size, path=True, bounces=bounces, nthreads=8),
-                                  bvh=bvh + (s.bvh8() if on else None,))
-        assert np.array_equal(fb, c) and np.array_equal(fb, fb4)
-        for key in ("primary_rays", "geometry_hits", "shadow_rays", "occluded", "bounce_rays", "node_visits",
-                    "tri_tests", "layer_tests", "shaded", "texel_bytes"):
-            assert st[key] == k[key], key
-    finally:
-        del os.environ["RT_BVH8"]
-    r.close()
