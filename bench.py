@@ -208,52 +208,67 @@ def cold_configure_probe(rt, scene, side, kw, n=3):
 
 
 def moving_light_series(r, side, steps, warmup, kw):
-    """Every step moves the light (rt_renderer_set_light: the light-space
-    shadow lists rebuilt on the device, queued behind the previous frame)
-    and renders a frame -- the reference's per-render re-binning regime
+    """Every step moves the light (rt_renderer_set_light) and renders a
+    frame -- the reference's per-render re-binning regime
     (tests/regression/draw3d/main.cpp:179-211).  Frames back to back, no
-    per-launch events; the last frame is checked against a fresh configure
-    with its light.  Also the cost of one light change alone (set_light +
-    wait, median of 16: slist_build_ms)."""
+    per-launch events, under the renderer's default list policy: a frame
+    whose light just moved traces its shadow rays by the BVH packet walk
+    (the same verdicts), the light-space lists are rebuilt only once a light
+    stays (rt_renderer_set_list_policy).  Beside it the same steps with the
+    lists rebuilt for every light before its frame (policy 0: 6 setup
+    launches queued behind the previous frame) and the cost of one such
+    rebuild alone (set_light + wait, median of 16: slist_build_ms).  The
+    last frame is checked against a fresh configure with its light."""
     import torch
     lights = moving_lights(16)
     r.configure(side, side, counters=False, **dict(kw, light=lights[0]))
     r.render()
+    r.set_list_policy(0)
     one = []
     for L in lights[1:] + lights[:1]:
         t0 = time.perf_counter()
         r.set_light(L)
         r.wait()
         one.append((time.perf_counter() - t0) * 1e3)
-    r.set_timing(False)
-    try:
-        for i in range(warmup):
-            r.set_light(lights[i % 16])
-            r.start()
-        r.wait()
-        torch.cuda.synchronize()
-        _, _, n0 = r.run_totals()
-        t0 = time.perf_counter()
-        for i in range(steps):
-            r.set_light(lights[i % 16])
-            r.start()
-        r.wait()
-        torch.cuda.synchronize()
-        el = time.perf_counter() - t0
-        _, _, n1 = r.run_totals()
-    finally:
-        r.set_timing(True)
+    defer = int(os.environ.get("RT_SLIST_DEFER", "8"))
+
+    def steps_ms(policy):
+        r.set_list_policy(policy)
+        r.set_timing(False)
+        try:
+            for i in range(warmup):
+                r.set_light(lights[i % 16])
+                r.start()
+            r.wait()
+            torch.cuda.synchronize()
+            _, _, n0 = r.run_totals()
+            t0 = time.perf_counter()
+            for i in range(steps):
+                r.set_light(lights[i % 16])
+                r.start()
+            r.wait()
+            torch.cuda.synchronize()
+            el = time.perf_counter() - t0
+            _, _, n1 = r.run_totals()
+        finally:
+            r.set_timing(True)
+        return el / steps * 1e3, (n1 - n0) / steps
+
+    rebuild_ms, rebuild_runs = steps_ms(0)
+    ms, runs = steps_ms(defer)
     last = lights[(steps - 1) % 16]
     fb = r.framebuffer().copy()
     st = r.setup_stats()
     r.configure(side, side, counters=False, **dict(kw, light=last))
     r.render()
     same = bool(np.array_equal(fb, r.framebuffer()))
-    return {"steps": steps, "lights": 16, "ms_per_step": round(el / steps * 1e3, 5),
-            "runs_per_step": round((n1 - n0) / steps, 3),
+    return {"steps": steps, "lights": 16, "ms_per_step": round(ms, 5), "runs_per_step": round(runs, 3),
+            "list_policy": f"lists deferred until a light stays {defer} frames (rt_renderer_set_list_policy)",
+            "slist_on_last": int(st["slist_on"]), "slist_stale_last": int(st["slist_stale"]),
+            "ms_per_step_lists_rebuilt_every_step": round(rebuild_ms, 5),
+            "runs_per_step_lists_rebuilt_every_step": round(rebuild_runs, 3),
             "slist_build_ms": round(float(np.median(one)), 4),
             "slist_build_ms_min": round(float(min(one)), 4),
-            "slist_entries_last": int(st["slist_entries"]), "slist_on": int(st["slist_on"]),
             "last_frame_equals_configured_render": same}
 
 
@@ -847,8 +862,11 @@ def main():
                                  dict(shadows=shadows, path=path, bounces=args.bounces))
         mr["value"] = round(run.rays_local * mr["steps"] / (mr["ms_per_step"] * 1e-3 * mr["steps"]) / 1e6, 3)
         mr["workload"] = (f"{side}x{side} {'path trace' if path else 'primary+shadow'} frames, the light "
-                          f"moved before every frame (rt_renderer_set_light: light-space shadow lists "
-                          f"rebuilt on the device, 6 stream-ordered setup launches, no host wait)")
+                          f"moved before every frame (rt_renderer_set_light, no host wait): the frames "
+                          f"trace their shadow rays by the BVH4 packet walk while the light moves and "
+                          f"the light-space lists are rebuilt on the device only once a light stays; "
+                          f"ms_per_step_lists_rebuilt_every_step = the lists rebuilt for every light "
+                          f"(6 stream-ordered setup launches before its frame)")
         series["moving_light"] = moving = mr
     cold = None
     if extra and not flat:

@@ -229,23 +229,34 @@ typedef struct {
                              frame is one launch group of 2, vortex_hip.h) */
   uint32_t slist_built;   /* 1: the last configure / set_light built shadow lists for a new light
                              (0: the lists of an unchanged light were kept) */
-  uint32_t pad;
+  uint32_t slist_stale;   /* 1: the light moved since its lists were built and none are queued:
+                             frames walk the BVH for their shadow rays (rt_renderer_set_list_policy) */
 } rt_setup_stats_t;
 /* (reads back the status of shadow lists queued by rt_renderer_set_light:
  * waits for the device) */
 int rt_renderer_setup_stats(rt_renderer_h r, rt_setup_stats_t* stats);
 
 /* Move the point light of the current configuration (primary+shadow or path
- * frames; clip (x, y, w)): the light in the render arguments and, when the
- * configuration's shadow rays use the light-space lists, the lists for the
- * new light -- a stream-ordered chain of setup launches (kernels/rt_setup.hip
- * SPROJ .. SSORT) queued behind the frames already started, with no host
- * wait; the frames started after it see the new light.  The lists' last
- * launch decides on the device whether they fit (else those frames' shadow
- * rays walk the BVH).  The reference re-bins its scene on the host for every
- * render (tests/regression/draw3d/main.cpp:179-211 -> gfxutil.cpp:103-276);
- * this is the per-frame rebuild of the only light-dependent structure. */
+ * frames; clip (x, y, w)): the light in the render arguments, queued behind
+ * the frames already started, with no host wait; the frames started after it
+ * see the new light.  When the configuration's shadow rays use the
+ * light-space lists, the lists for the new light are a stream-ordered chain
+ * of setup launches (kernels/rt_setup.hip SPROJ .. SSORT, ~0.1 ms at 1024^2)
+ * whose last launch decides on the device whether they fit (else the frames'
+ * shadow rays walk the BVH).  By default (rt_renderer_set_list_policy) the
+ * chain is deferred: the frames after the change trace their shadow rays by
+ * the BVH packet walk -- the same verdicts, no wait for lists -- and the
+ * lists are queued once the light has stayed for `defer_frames` frames.  The
+ * reference re-bins its scene on the host for every render
+ * (tests/regression/draw3d/main.cpp:179-211 -> gfxutil.cpp:103-276); this
+ * is the per-frame handling of the only light-dependent structure. */
 int rt_renderer_set_light(rt_renderer_h r, const float light[3]);
+/* When set_light queues a light's shadow lists: 0 = at once (set_light);
+ * n > 0 = before the (n + 1)-th frame started with that light, the n frames
+ * before walking the BVH for their shadow rays (default 8, env
+ * RT_SLIST_DEFER; a build costs about as much as that many frames save).
+ * NO REFERENCE. */
+int rt_renderer_set_list_policy(rt_renderer_h r, uint32_t defer_frames);
 
 /* Read back one per-resolution record array of the current configuration
  * (layouts: kernels/rt_common.h; NO REFERENCE).  out NULL = size query

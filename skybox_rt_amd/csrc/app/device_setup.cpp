@@ -489,7 +489,30 @@ int set_light(rt_renderer* r, const float light[3], uint32_t* launches) {
                      : vx_copy_to_dev(r->args, a.light, offsetof(rt_kernel_arg_t, light), sizeof(a.light));
   if (rc != 0) return set_error("light upload failed");
   if (!r->sl_mode) return 0;  // this configuration's shadow rays walk the BVH
-  // the shadow lists for the new light, queued behind it: the chain's last
+  if (r->sl_defer > 0) {
+    // the moving light: the next frames walk the BVH for their shadow rays
+    // (the same verdicts as the lists) and the lists wait until the light
+    // stays (queue_lists from rt_render_start).  A build still unsettled
+    // from before is settled first: its last launch writes slist_on.
+    if (r->sl_pending && settle_lists(r) != 0) return -1;
+    if (a.slist_on) {  // (a light moving every frame: one copy per change, the light's)
+      a.slist_on = 0;
+      const size_t o = offsetof(rt_kernel_arg_t, slist_on);
+      const int rs = r->copy_async ? r->copy_async(r->args, &a.slist_on, o, sizeof(a.slist_on))
+                                   : vx_copy_to_dev(r->args, &a.slist_on, o, sizeof(a.slist_on));
+      if (rs != 0) return set_error("slist_on upload failed");
+    }
+    r->sl_stale = true;
+    r->sl_static = 0;
+    return 0;
+  }
+  return queue_lists(r, launches);
+}
+
+int queue_lists(rt_renderer* r, uint32_t* launches) {
+  rt_kernel_arg_t& a = r->arg;
+  r->sl_stale = false;
+  // the shadow lists for the current light, queued behind it: the chain's last
   // launch writes the render arguments' slist_on (the lists' own verdict),
   // so no host wait anywhere; the status words are read when asked for
   // (rt_renderer_setup_stats) or by the next configure

@@ -294,6 +294,8 @@ int rt_renderer_create(rt_scene_h s, const char* kernel_dir, rt_renderer_h* out)
   r->launch_group = (vx_hip_launch_group_t)vx_driver_symbol("vx_hip_launch_group");
   r->set_timing = (vx_hip_set_timing_t)vx_driver_symbol("vx_hip_set_timing");
   r->copy_async = (vx_hip_copy_to_dev_async_t)vx_driver_symbol("vx_hip_copy_to_dev_async");
+  // the moving-light policy (rt_renderer_set_list_policy); env RT_SLIST_DEFER
+  if (const char* e = std::getenv("RT_SLIST_DEFER")) r->sl_defer = (uint32_t)std::atoi(e);
   r->set_tag = (vx_hip_set_launch_tag_t)vx_driver_symbol("vx_hip_set_launch_tag");
   r->host_mem = (vx_hip_host_mem_t)vx_driver_symbol("vx_hip_host_mem");
   if (r->host_mem) {
@@ -443,6 +445,7 @@ int rt_renderer_setup_stats(rt_renderer_h r, rt_setup_stats_t* st) {
   if (!r->configured) return fail("renderer not configured");
   if (rtapp::settle_lists(r) != 0) return -1;
   r->setup.slist_on = r->arg.slist_on;
+  r->setup.slist_stale = r->sl_stale ? 1u : 0u;
   *st = r->setup;
   return 0;
 }
@@ -953,6 +956,7 @@ int rt_renderer_configure(rt_renderer_h r, const rt_render_params_t* p) {
                       (p->flags & (RT_RENDER_SHADOWS | RT_RENDER_PATH)) && a.num_geom > 0 &&
                       !(sle && std::atoi(sle) == 0) && !bvh_walk;
   r->sl_mode = slists;
+  r->sl_stale = false;  // the configure builds the lists for its light
   a.slist_on = 0;
   r->setup.slist_entries = 0;
   const auto t1 = std::chrono::steady_clock::now();
@@ -1034,8 +1038,20 @@ int rt_renderer_configure(rt_renderer_h r, const rt_render_params_t* p) {
   return 0;
 }
 
+int rt_renderer_set_list_policy(rt_renderer_h r, uint32_t defer_frames) {
+  if (!r) return fail("null argument");
+  r->sl_defer = defer_frames;
+  return 0;
+}
+
 int rt_render_start(rt_renderer_h r) {
   if (!r || !r->configured) return fail("renderer not configured");
+  // the moving light: the lists of a light that stayed for sl_defer frames
+  // are queued before this frame (the frames before walked the BVH)
+  if (r->sl_stale && ++r->sl_static > r->sl_defer) {
+    uint32_t launches = 0;
+    if (rtapp::queue_lists(r, &launches) != 0) return -1;
+  }
   const uint32_t f = r->params.flags;
   const int mode = (f & RT_RENDER_PATH) ? 1 : (f & RT_RENDER_FLAT) ? 2 : (f & RT_RENDER_RASTER) ? 3 : 0;
   const int k = (f & RT_RENDER_INSTRUMENTED) && mode != 3 ? 1 : 0;

@@ -75,6 +75,13 @@ struct rt_renderer {
   vx_buffer_h sidx = nullptr, slist = nullptr;  // light-space shadow lists (built for sl_light)
   bool sl_mode = false;     // this configuration's shadow rays use the light-space lists
   bool sl_pending = false;  // lists queued by rt_renderer_set_light, status not read yet
+  // the moving light (rt_renderer_set_list_policy): after a light change the
+  // frames trace their shadow rays by the BVH packet walk (slist_on = 0, no
+  // wait for lists) until the light has stayed for sl_defer frames; then the
+  // lists are queued before the next frame.  0: set_light queues them at once
+  uint32_t sl_defer = 8;
+  bool sl_stale = false;    // the light moved since the lists were built; lists not queued yet
+  uint32_t sl_static = 0;   // frames started since that light change
   SetupScratch su;
   vx_hip_copy_to_dev_async_t copy_async = nullptr;
   vx_hip_set_launch_tag_t set_tag = nullptr;
@@ -178,6 +185,9 @@ int device_setup(rt_renderer* r, bool raster, bool order_on, bool lists, bool sl
 // the configuration uses them, its shadow lists -- all queued on the
 // driver's stream behind the in-flight frames, no host wait
 int set_light(rt_renderer* r, const float light[3], uint32_t* launches);
+// the shadow lists for the current light, queued on the driver's stream (the
+// set_light policy 0, or a deferred build once the light stays)
+int queue_lists(rt_renderer* r, uint32_t* launches);
 // read the status of lists queued by set_light (waits for the device): their
 // size, an overflow refill, r->sl_built
 int settle_lists(rt_renderer* r);

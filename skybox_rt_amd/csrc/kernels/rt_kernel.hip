@@ -179,8 +179,7 @@ __device__ __forceinline__ void shadow_drain(bool final, const Scene& S, WaveLds
     // binary16 BVH4 as one packet, other layouts per lane (deep images)
     const bool occ = !RT_BVH_WALK && S.slist_on ? occluded_list(S, s, active, w.q_pid[slot], cnt)
                      : (RT_ONLY_BVH4H || (S.flags & RT_FLAG_BVH4H))
-                         ? (RT_SHADOW_MASKS ? occluded_packet_m(S, s, active, w.q_pid[slot], 1.0f, cnt)
-                                            : occluded_packet(S, s, active, w.q_pid[slot], 1.0f, cnt))
+                         ? occluded_packet(S, s, active, w.q_pid[slot], 1.0f, cnt)
                          : active && trace<true>(S, s, 0.0f, 1.0f, w.q_pid[slot], tie_high, &ts,
                                                  RT_WSTACK(w, lane), cnt) >= 0;
     if (occ) {

@@ -138,7 +138,7 @@ __device__ __forceinline__ uint32_t lane_id() {
 #define RT_WAVE_ITER(slot)                                                         \
   do {                                                                             \
     if (lane_id() == (uint32_t)__builtin_ctzll(__ballot(1)))                      \
-      ((volatile uint32_t*)__vx_mpm_lds)[slot] += 1u;                             \
+      atomicAdd(&__vx_mpm_lds[slot], 1u);                                         \
   } while (0)
 // cycles from issuing a packet walk's record load to its data (rt stamp
 // image: slot 0 primary packets, slot 1 shadow packets; s_memtime, explicit
@@ -153,7 +153,7 @@ __device__ __forceinline__ uint32_t lane_id() {
     __builtin_amdgcn_s_waitcnt(0xC07F);                                            \
     const uint32_t rt_ldd = (uint32_t)(__builtin_amdgcn_s_memtime() - rt_ld0);     \
     if (lane_id() == (uint32_t)__builtin_ctzll(__ballot(1)))                      \
-      ((volatile uint32_t*)__vx_mpm_lds)[slot] += rt_ldd;                         \
+      atomicAdd(&__vx_mpm_lds[slot], rt_ldd);                                     \
   } while (0)
 #endif
 #else
@@ -169,7 +169,7 @@ __device__ __forceinline__ uint32_t lane_id() {
   do {                                                                                    \
     const uint32_t d = (uint32_t)(__builtin_amdgcn_s_memtime() - rt_cyc0);               \
     if (lane_id() == (uint32_t)__builtin_ctzll(__ballot(1)))                             \
-      ((volatile uint32_t*)__vx_mpm_lds)[slot] += d;                                      \
+      atomicAdd(&__vx_mpm_lds[slot], d);                                                  \
   } while (0)
 #else
 #define RT_CYC_BEGIN() do {} while (0)
@@ -539,14 +539,21 @@ __device__ __forceinline__ int32_t trace_impl(const Scene& S, const Ray& r, floa
 // finished.  Restricted to one lane, that is the per-lane any-hit walk
 // (trace<true>: same fixed order, same first occluder), so each lane's
 // verdict and its visit / test counts are the per-lane walk's: a lane counts
-// a node or triangle only while it is on the path (`on`: it hit the node's
-// box; per stack entry one bit of `onb`) and unfinished.  Measured (A/B,
-// tekkaman 1024^2 primary + shadow): -9 % kernel time vs per-lane walks
-// (0.0565 -> 0.0514 ms): the heavy tiles' shadow rays are coherent.  Every
-// active lane calls it (any EXEC mask).  The walk's (wave-uniform) stack
-// lives in one VGPR, entry i in lane i (v_writelane / v_readlane: no LDS
-// round trip on the pop -> node-load chain); a node (64 B) and a leaf's
-// records, two at a time, arrive through one pointer each as wide s_loads.
+// a node or triangle only while it is on the path (it hit the node's box and
+// its ancestors') and unfinished.  Measured (A/B, tekkaman 1024^2 primary +
+// shadow): -9 % kernel time vs per-lane walks (0.0565 -> 0.0514 ms, r02):
+// the heavy tiles' shadow rays are coherent.  Every active lane calls it
+// (any EXEC mask).  The walk's per-lane state is wave masks in SGPRs (r06):
+// `live` (on the path and unfinished), `done`, and per stack entry the mask
+// of the lanes on it -- a child's lanes are one v_cmp of the slab's near /
+// far values ANDed with `live`, no per-lane booleans materialised and
+// balloted again, no per-lane bit stack; BVH-walk frame 0.03436 -> 0.0324
+// ms, the heaviest tile alone 0.02919 -> 0.02756 (r06c).  The stack is
+// three VGPRs, entry i in lane i (v_writelane / v_readlane: no LDS round
+// trip on the pop -> node-load chain): the ref and the lane mask's halves.
+// A node (64 B) and a leaf's records, two at a time, arrive through one
+// pointer each as wide s_loads; the leaf triangles are tested branch-free
+// (mt_hit_bf: mt_hit's operations, one predicate).
 // Packet leaves load this many records before testing any (A/B,
 // profiles/r02/ab_packet_leaf_hoist.json: 1 0.0450 ms, 2 0.0426, 4 0.0436)
 constexpr uint32_t kLeafHoist = 2;
@@ -565,119 +572,6 @@ __device__ __forceinline__ float4 u4f(const uint4 u) {
 }
 __device__ __forceinline__ bool occluded_packet(const Scene& S, const Ray& r, bool act, int32_t skip,
                                                 float tmax, Counters& cnt) {
-  bool done = !act, occ = false;
-  if (S.num_nodes4 == 0 || __ballot(!done) == 0) return false;
-  int32_t vstk = 0;  // stack entry i in lane i of this VGPR
-  int sp = 0;
-  int32_t ref = 0;
-  bool on = true;     // this lane's ray hit the current node's box (and its ancestors')
-  uint32_t onb = 0u;  // the same for the stack entries (bit sp)
-  static_assert(RT_MAX_STACK <= 32, "one bit per stack entry");
-  for (;;) {
-    const bool live = on && !done;
-    if (ref >= 0) {
-      RT_CNT(cnt.visits += live;)
-      RT_WAVE_ITER(9);
-      const uint32_t no = S.nodes4 + 128u * S.num_nodes4 + 64u * (uint32_t)ref;
-      uint4 nw[4];
-      RT_LD_BEGIN();
-      S.A.sld_u4n<4>(no, nw);  // one s_load_dwordx16
-      RT_LD_END(1);
-      const uint4 px = nw[0], py = nw[1], pz = nw[2], cf = nw[3];
-      float lx[4], hx[4], ly[4], hy[4], lz[4], hz[4];
-      auto h2 = [](uint32_t u, float& a, float& b) {
-        a = (float)__builtin_bit_cast(_Float16, (uint16_t)(u & 0xffffu));
-        b = (float)__builtin_bit_cast(_Float16, (uint16_t)(u >> 16));
-      };
-      h2(px.x, lx[0], lx[1]); h2(px.y, lx[2], lx[3]); h2(px.z, hx[0], hx[1]); h2(px.w, hx[2], hx[3]);
-      h2(py.x, ly[0], ly[1]); h2(py.y, ly[2], ly[3]); h2(py.z, hy[0], hy[1]); h2(py.w, hy[2], hy[3]);
-      h2(pz.x, lz[0], lz[1]); h2(pz.y, lz[2], lz[3]); h2(pz.z, hz[0], hz[1]); h2(pz.w, hz[2], hz[3]);
-      const int32_t c[4] = {(int32_t)cf.x, (int32_t)cf.y, (int32_t)cf.z, (int32_t)cf.w};
-      bool h[4];
-      uint32_t need = 0u;  // wave-uniform: children some live lane enters
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        float tn = 0.0f;
-        // every lane evaluates the slab (no exec-mask branch per child)
-        const bool hs = slab(lx[i], hx[i], ly[i], hy[i], lz[i], hz[i], r, 0.0f, tmax, &tn);
-        h[i] = hs & live & (c[i] != RT_EMPTY_REF);
-        need |= __ballot(h[i]) ? 1u << i : 0u;
-      }
-      if (need) {
-        // push the needed children after the first, last slot first
-#pragma unroll
-        for (int i = 3; i >= 1; --i) {
-          if ((need >> i) & 1u && (need & ((1u << i) - 1u))) {
-            if (sp < RT_MAX_STACK) {
-              vstk = vwritelane(vstk, c[i], sp);
-              onb = h[i] ? onb | (1u << sp) : onb & ~(1u << sp);
-              ++sp;
-            }
-          }
-        }
-        const int f = __builtin_ctz(need);
-        ref = f == 0 ? c[0] : f == 1 ? c[1] : f == 2 ? c[2] : c[3];
-        on = f == 0 ? h[0] : f == 1 ? h[1] : f == 2 ? h[2] : h[3];
-        continue;
-      }
-    } else {
-      const uint32_t lr = (uint32_t)ref;
-      const uint32_t first = (lr >> 4) & 0x07ffffffu, count = (lr & 15u) + 1u;
-      RT_WAVE_ITER(9);
-      bool lv = live;
-      // kLeafHoist slots in flight at once (3 padding records; 3 or 4
-      // measured no faster on the BVH-walk frame, r06b)
-      constexpr uint32_t H = kLeafHoist;
-#pragma unroll
-      for (uint32_t q0 = 0; q0 < 4; q0 += H) {
-        if (q0 >= count) break;
-        float4 ta[H], tb[H], tc[H];
-        {  // the H consecutive records from one address (wide s_loads)
-          uint4 tw[3 * H];
-          RT_LD_BEGIN();
-          S.A.sld_u4n<3 * H>(S.tris + 48u * (first + q0), tw);
-          RT_LD_END(1);
-#pragma unroll
-          for (uint32_t j = 0; j < H; ++j) {
-            ta[j] = u4f(tw[3 * j]); tb[j] = u4f(tw[3 * j + 1]); tc[j] = u4f(tw[3 * j + 2]);
-          }
-        }
-#pragma unroll
-        for (uint32_t j = 0; j < H; ++j) {
-          if (q0 + j < count) {
-            RT_CNT(cnt.tests += lv;)
-            float t;
-            if (lv && __float_as_int(ta[j].w) != skip && mt_hit(r, ta[j], tb[j], tc[j], 0.0f, &t) &&
-                t < tmax) {
-              occ = true;
-              done = true;
-              lv = false;
-            }
-          }
-        }
-      }
-      if (__ballot(!done) == 0) break;
-    }
-    if (sp == 0) break;
-    --sp;
-    on = (onb >> sp) & 1u;
-    ref = __builtin_amdgcn_readlane(vstk, sp);
-  }
-  return occ;
-}
-
-// occluded_packet with the walk's per-lane state as wave masks in SGPRs
-// (RT_SHADOW_MASKS): `live` (on the path and unfinished), `done`, and per
-// stack entry the mask of lanes on it (two more VGPRs of v_writelane /
-// v_readlane beside the ref) -- a child's lanes are one v_cmp of the slab's
-// near / far values ANDed with `live`, no per-lane booleans to materialise
-// and ballot again, no per-lane bit stack.  The leaf triangles are tested
-// branch-free (mt_hit_bf: mt_hit's operations, one predicate).  The same
-// walk: same nodes in the same order, same per-lane visits, tests and
-// verdicts.
-#define RT_SHADOW_MASKS 0  // 1: shadow packets walk as occluded_packet_m
-__device__ __forceinline__ bool occluded_packet_m(const Scene& S, const Ray& r, bool act, int32_t skip,
-                                                  float tmax, Counters& cnt) {
   const uint64_t act_m = __ballot(act);
   if (S.num_nodes4 == 0 || act_m == 0) return false;
   uint64_t done_m = 0, live_m = act_m;  // live: on the current node's path and unfinished
@@ -1334,6 +1228,11 @@ __device__ __forceinline__ void vis_test_in(const uint4& A, const uint4& B, cons
     bpid = pid;
   }
 }
+// (vis_test_in without branches -- every lane evaluating the edges and the
+// depth word, one predicate deciding, so the compiler keeps the record's
+// loads in one scalar round trip instead of sinking them into the branches
+// -- measured slower: r06d, config 3 0.01646 vs 0.01621 ms, BVH walk
+// 0.03385 vs 0.03181; the division for every lane costs more)
 __device__ __forceinline__ void vis_test(const uint4& A, const uint4& B, const uint4& C, const uint4& D,
                                          uint32_t px, uint32_t py, bool tie_high, uint32_t& bz,
                                          int32_t& bpid) {
@@ -1389,9 +1288,11 @@ __device__ __forceinline__ int32_t trace_primary_packet(const Scene& S, uint32_t
         const rt_u16x2 cl = __builtin_elementwise_min(
             __builtin_elementwise_max(__builtin_bit_cast(rt_u16x2, pp), __builtin_bit_cast(rt_u16x2, alo[i])),
             __builtin_bit_cast(rt_u16x2, ahi[i]));
-        need |= (c[i] != RT_EMPTY_REF &&
-                 (mask_ueq(__builtin_bit_cast(uint32_t, cl), pp) & mask_ule(azm[i], bz)) != 0)
-                    ? 1u << i : 0u;
+        // (no short-circuit: a branch per child made the compiler sink the
+        // node's loads into three dependent scalar round trips; BVH walk
+        // 0.03181 -> 0.03132 ms, r06d)
+        const uint64_t m = mask_ueq(__builtin_bit_cast(uint32_t, cl), pp) & mask_ule(azm[i], bz);
+        need |= ((m != 0) & (c[i] != RT_EMPTY_REF)) ? 1u << i : 0u;
       }
       if (need != 0u) {
         // the slots are stored in ascending depth bound (vis.cpp SortSlots):

@@ -621,7 +621,17 @@ class vx_device {
     hostmem_dev_ = (uint64_t)(uintptr_t)d;
     return 0;
   }
+  // a run's completion word in the pinned block.  Guarded (r06, VERDICT r05
+  // item 5): the r05c / r05d work-in-progress trees died with SIGSEGV in
+  // rt_renderer_create while this block was being introduced -- the tree of
+  // those runs was never committed, and a completion word touched before the
+  // block existed (or past it) fits the trace; a slot outside the block or a
+  // block not yet allocated now ends the process with a message instead
   volatile uint32_t* tail_word(int slot) const {
+    if (!hostmem_ || slot < 0 || slot >= kMaxQueue) {
+      std::fprintf(stderr, "[VXDRV] completion slot %d outside the pinned block (%p)\n", slot, hostmem_);
+      std::abort();
+    }
     return reinterpret_cast<volatile uint32_t*>(static_cast<uint8_t*>(hostmem_) + kHostMemApp +
                                                 (uint64_t)slot * kTailSlot);
   }

@@ -66,7 +66,7 @@ class SetupStats(C.Structure):
                 ("blist_blocks", C.c_uint32), ("setup_ms", C.c_double), ("configure_ms", C.c_double),
                 ("blist_entries", C.c_uint64), ("blist_max", C.c_uint32), ("slist_on", C.c_uint32),
                 ("slist_entries", C.c_uint64), ("path_queue", C.c_uint32), ("slist_built", C.c_uint32),
-                ("pad", C.c_uint32)]
+                ("slist_stale", C.c_uint32)]
 
     def as_dict(self):
         return {n: getattr(self, n) for n, _ in self._fields_ if n != "pad"}
@@ -141,6 +141,7 @@ def lib():
             "rt_render_gather": [vp, vp, vp],
             "rt_renderer_setup_stats": [vp, C.POINTER(SetupStats)],
             "rt_renderer_set_light": [vp, C.POINTER(C.c_float)],
+            "rt_renderer_set_list_policy": [vp, u32],
             "rt_renderer_export_records": [vp, u32, vp, u64, C.POINTER(u64)],
         }
         for name, argtypes in sig.items():
@@ -291,13 +292,21 @@ class Renderer:
         self.bvh4_f16 = self.bvh4 and (self.gpu_bvh or bool(self.scene.info()["bvh4_f16"]))
 
     def set_light(self, light) -> None:
-        """Move the point light (clip x, y, w) of the current configuration:
-        the light and -- when the configuration uses them -- its light-space
-        shadow lists are rebuilt on the device, queued behind the frames
-        already started (rt_renderer_set_light: no host wait)."""
+        """Move the point light (clip x, y, w) of the current configuration,
+        queued behind the frames already started (rt_renderer_set_light: no
+        host wait).  When the configuration uses light-space shadow lists
+        they are rebuilt on the device -- at once, or (the default policy,
+        set_list_policy) once the light has stayed for a few frames, the
+        frames before tracing their shadow rays by the BVH packet walk."""
         arr = (C.c_float * 3)(*[float(np.float32(x)) for x in light])
         _check(lib().rt_renderer_set_light(self._h, arr), "rt_renderer_set_light")
         self.params.light[:] = [float(np.float32(x)) for x in light]
+
+    def set_list_policy(self, defer_frames: int) -> None:
+        """0: set_light queues the new light's shadow lists at once; n > 0:
+        before the (n + 1)-th frame with that light (rt_renderer_set_list_policy)."""
+        _check(lib().rt_renderer_set_list_policy(self._h, int(defer_frames)),
+               "rt_renderer_set_list_policy")
 
     def setup_stats(self) -> dict:
         """How the last configure built its records (device / host, launches,

@@ -6,8 +6,13 @@ here only the light-dependent structure, the light-space shadow lists, is
 rebuilt when the light moves, queued on the driver's stream behind the
 frames already started.
 
-* a frame after set_light equals the oracle for the new light, counters
-  included (the lists' own scan), and the device lists equal the oracle's;
+* set_light with the lists queued at once (set_list_policy(0)): a frame
+  after it equals the oracle for the new light, counters included (the
+  lists' own scan), and the device lists equal the oracle's;
+* the default policy (the moving light): the frames after a light change
+  trace their shadow rays by the BVH packet walk -- frame and counters the
+  oracle's BVH mode -- until the light has stayed for the policy's frames,
+  then the lists are queued and the frames scan them (list-mode counters);
 * frames started back to back with a light change between them: the last
   frame is the new light's (stream order, no host wait);
 * the path tracer's shadow rays follow the light too;
@@ -59,6 +64,7 @@ def test_set_light_frames_and_lists_equal_oracle(oracle_lib):
     s = rt.Scene.load(scene_path("tekkaman"))
     r = rt.Renderer(s)
     r.configure(512, 512, shadows=True, light=LIGHTS[0], instrumented=True)
+    r.set_list_policy(0)
     assert r.setup_stats()["slist_built"] == 1
     for L in LIGHTS[1:]:
         r.set_light(L)
@@ -78,13 +84,16 @@ def test_set_light_frames_and_lists_equal_oracle(oracle_lib):
     s.close()
 
 
-def test_set_light_between_queued_frames(oracle_lib):
+@pytest.mark.parametrize("defer", [0, 8])
+def test_set_light_between_queued_frames(oracle_lib, defer):
     """start(A) ; set_light(B) ; start ; set_light(C) ; start ; wait: the last
-    frame is C's, and the light changes never waited for the frames."""
+    frame is C's, and the light changes never waited for the frames (lists
+    queued at once, or deferred: the frames walk the BVH)."""
     po = oracle_lib
     s = rt.Scene.load(scene_path("tekkaman"))
     r = rt.Renderer(s)
     r.configure(1024, 1024, shadows=True, light=LIGHTS[0], counters=False)
+    r.set_list_policy(defer)
     r.render()
     for _ in range(3):
         for L in LIGHTS[1:4]:
@@ -94,7 +103,44 @@ def test_set_light_between_queued_frames(oracle_lib):
     r.wait()
     c, _, _, _ = _oracle(po, s, 1024, 1024, LIGHTS[3])
     assert np.array_equal(r.framebuffer(), c)
-    assert r.setup_stats()["slist_on"] == 1
+    ss = r.setup_stats()
+    assert (ss["slist_on"], ss["slist_stale"]) == ((1, 0) if defer == 0 else (0, 1)), ss
+    r.close()
+    s.close()
+
+
+@pytest.mark.parametrize("path", [False, True])
+def test_moving_light_defers_lists(oracle_lib, path):
+    """The default policy with 3 frames: after a light change the frames
+    trace their shadow rays by the BVH packet walk (frame, occlusions and
+    counters == the oracle's BVH mode) and no lists are built; the 4th frame
+    with the same light has its lists queued before it and scans them
+    (list-mode counters, lists == the oracle's)."""
+    po = oracle_lib
+    s = rt.Scene.load(scene_path("tekkaman"))
+    r = rt.Renderer(s)
+    kw = dict(path=True, bounces=2) if path else {}
+    r.configure(256, 256, shadows=True, light=LIGHTS[0], instrumented=True, **kw)
+    r.set_list_policy(3)
+    keys = ("tri_tests", "node_visits", "shadow_rays", "occluded") + (("bounce_rays",) if path else ())
+    for L in LIGHTS[1:3]:
+        r.set_light(L)
+        cb, _, _, kb = _oracle(po, s, 256, 256, L, shadow_lists=False, **kw)
+        for i in range(4):
+            r.render()
+            st, ss = r.stats(), r.setup_stats()
+            if i < 3:
+                assert ss["slist_on"] == 0 and ss["slist_stale"] == 1, (L, i, ss)
+                assert np.array_equal(r.framebuffer(), cb), (L, i)
+                for key in keys:
+                    assert st[key] == kb[key], (L, i, key)
+        assert ss["slist_on"] == 1 and ss["slist_stale"] == 0, ss
+        c, _, _, k = _oracle(po, s, 256, 256, L, **kw)
+        assert np.array_equal(r.framebuffer(), c) and np.array_equal(c, cb)
+        for key in keys:
+            assert st[key] == k[key], (L, key)
+        if not path:
+            _lists_equal_oracle(po, r, L)
     r.close()
     s.close()
 
@@ -104,6 +150,7 @@ def test_set_light_path_tracer(oracle_lib):
     s = rt.Scene.load(scene_path("tekkaman"))
     r = rt.Renderer(s)
     r.configure(256, 256, shadows=True, path=True, bounces=2, light=LIGHTS[0], instrumented=True)
+    r.set_list_policy(0)
     for L in LIGHTS[1:3]:
         r.set_light(L)
         r.render()
@@ -145,6 +192,7 @@ def test_list_capacity_overflow_refills(oracle_lib, monkeypatch):
     s = rt.Scene.load(scene_path("tekkaman"))
     r = rt.Renderer(s)
     r.configure(512, 512, shadows=True, light=LIGHTS[0], instrumented=True)
+    r.set_list_policy(0)
     ss = r.setup_stats()
     assert ss["blist_blocks"] > 0 and ss["blist_entries"] > 100 and ss["slist_on"] == 1, ss
     oidx, oent = po.vis_block_lists(_oscene(po, "tekkaman"), 512, 512, 0, 1)
@@ -212,6 +260,7 @@ def test_setup_sequence_forms_equal_oracle(oracle_lib, monkeypatch, env):
     r.render()
     c, _, _, k = _oracle(po, s, 512, 512, LIGHTS[1])
     assert np.array_equal(r.framebuffer(), c)
+    r.set_list_policy(0)
     r.set_light(LIGHTS[2])
     assert r.setup_stats()["slist_on"] == 1  # settles the lists (their entry count)
     r.render()
