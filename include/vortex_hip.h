@@ -77,10 +77,26 @@ typedef int (*vx_hip_set_timing_t)(vx_device_h hdevice, int timed);
  * of dependent launches needs only stream order.) */
 typedef int (*vx_hip_copy_to_dev_async_t)(vx_buffer_h hbuf, const void* src, uint64_t off, uint64_t size);
 /* the kernel argument of the next vx_start (then 0 again): every image's
- * entry takes one u32, `vx_launch_tag` in its VX_MAIN body (vx_spawn.h) --
+ * entry takes a u32 tag, `vx_launch_tag` in its VX_MAIN body (vx_spawn.h) --
  * how the launches of a sequence sharing one argument block tell themselves
  * apart without a device counter or a copy between them */
 typedef int (*vx_hip_set_launch_tag_t)(vx_device_h hdevice, uint32_t tag);
+/* which clock timed the runs vx_hip_last_run / vx_hip_run_totals report:
+ * `last_stamped` 1 when the last timed run was timed by its completion
+ * kernel's stamps (a run started on an idle queue: block 0's start to the
+ * completion kernel's start, so the kernel plus its launch boundary), 0 by
+ * HIP events on the dispatch (queued runs: the kernel alone); the counts of
+ * timed runs of each kind since the device opened (their sum is
+ * vx_hip_run_totals' timed count, and the total mixes both kinds when both
+ * are non-zero) */
+typedef int (*vx_hip_timing_source_t)(vx_device_h hdevice, int* last_stamped, uint64_t* stamped_runs,
+                                      uint64_t* event_runs);
+/* the four launch words of the next vx_start (then 0 again; n <= 4, the rest
+ * 0): carried in the dispatch's kernel arguments beside the tag,
+ * `vx_launch_words` in the VX_MAIN body -- per-launch values (a frame's light)
+ * that reach the kernel with its dispatch packet instead of through a copy
+ * queued between two launches */
+typedef int (*vx_hip_set_launch_words_t)(vx_device_h hdevice, const uint32_t* words, uint32_t n);
 
 #ifdef __cplusplus
 }

@@ -368,7 +368,13 @@ __device__ __forceinline__ int vx_spawn_chunks_block(uint32_t num_tasks, F kerne
  * object's symbol table, so profiles tell the images apart).  The body also
  * sees `vx_launch_tag`, the launch's one kernel argument: 0, or the value an
  * app set for this launch with vx_hip_set_launch_tag (vortex_hip.h) -- e.g.
- * the step of a launch sequence sharing one argument block. */
+ * the step of a launch sequence sharing one argument block -- and
+ * `vx_launch_words`, four more u32 set with vx_hip_set_launch_words (0
+ * unless set): per-launch values that travel in the dispatch packet's
+ * kernel arguments instead of a copy queued between two launches. */
+struct vx_launch_words_t {
+  uint32_t w[4];
+};
 #define VX_MAIN(ArgT, argname, block_threads) \
   VX_MAIN_BOUNDS(ArgT, argname, __launch_bounds__(block_threads))
 /* same, asking the compiler for `waves_per_eu` resident waves per SIMD */
@@ -402,8 +408,9 @@ __device__ __forceinline__ int vx_spawn_chunks_block(uint32_t num_tasks, F kerne
   }
 #define VX_MAIN_BOUNDS(ArgT, argname, bounds)                                        \
   __VX_DONE_KERNEL                                                                   \
-  static __device__ __forceinline__ int __vx_main_body(ArgT* argname, uint32_t vx_launch_tag); \
-  extern "C" __global__ void bounds VX_ENTRY(uint32_t __vx_tag) {                    \
+  static __device__ __forceinline__ int __vx_main_body(ArgT* argname, uint32_t vx_launch_tag, \
+                                                       vx_launch_words_t vx_launch_words); \
+  extern "C" __global__ void bounds VX_ENTRY(uint32_t __vx_tag, vx_launch_words_t __vx_words) { \
     /* the launch's start stamp (one lane of block 0; <entry>_done reads it) */      \
     if (blockIdx.x == 0 && threadIdx.x == 0) __vx_state.t0 = __builtin_amdgcn_s_memrealtime(); \
     /* the block's counter row: only when the driver reads rows (then the   */    \
@@ -416,7 +423,7 @@ __device__ __forceinline__ int vx_spawn_chunks_block(uint32_t num_tasks, F kerne
     }                                                                                \
     const uint64_t a = ((uint64_t)__vx_dcrs[VX_DCR_BASE_STARTUP_ARG1] << 32) |       \
                        (uint64_t)__vx_dcrs[VX_DCR_BASE_STARTUP_ARG0];                \
-    (void)__vx_main_body(vx_ptr<ArgT>(a), __vx_tag);                                 \
+    (void)__vx_main_body(vx_ptr<ArgT>(a), __vx_tag, __vx_words);                     \
     if (rows_on) {                                                                   \
       __syncthreads();                                                               \
       if (__vx_dcrs[VX_DCR_HIP_MPM_ROWS] && threadIdx.x < VX_MPM_ROW &&              \
@@ -424,6 +431,7 @@ __device__ __forceinline__ int vx_spawn_chunks_block(uint32_t num_tasks, F kerne
         __vx_state.mpm[blockIdx.x][threadIdx.x] = __vx_mpm_lds[threadIdx.x];         \
     }                                                                                \
   }                                                                                  \
-  static __device__ __forceinline__ int __vx_main_body(ArgT* argname, uint32_t vx_launch_tag)
+  static __device__ __forceinline__ int __vx_main_body(ArgT* argname, uint32_t vx_launch_tag, \
+                                                       vx_launch_words_t vx_launch_words)
 
 #endif /* VX_SPAWN_H */

@@ -483,8 +483,10 @@ int set_light(rt_renderer* r, const float light[3], uint32_t* launches) {
     a.light[i] = light[i];
     r->params.light[i] = light[i];
   }
-  // the render arguments' light, in stream order behind the queued frames
-  const int rc = r->copy_async
+  // the render arguments' light, in stream order behind the queued frames --
+  // unless every frame carries it in its launch words (rt_render_start)
+  const int rc = r->set_words ? 0
+                 : r->copy_async
                      ? r->copy_async(r->args, a.light, offsetof(rt_kernel_arg_t, light), sizeof(a.light))
                      : vx_copy_to_dev(r->args, a.light, offsetof(rt_kernel_arg_t, light), sizeof(a.light));
   if (rc != 0) return set_error("light upload failed");
@@ -495,13 +497,16 @@ int set_light(rt_renderer* r, const float light[3], uint32_t* launches) {
     // stays (queue_lists from rt_render_start).  A build still unsettled
     // from before is settled first: its last launch writes slist_on.
     if (r->sl_pending && settle_lists(r) != 0) return -1;
-    if (a.slist_on) {  // (a light moving every frame: one copy per change, the light's)
+    // the frames' launch words switch the stale lists off (RT_LW_NO_SLIST);
+    // without them the argument block's slist_on is cleared in stream order
+    if (a.slist_on && !r->set_words) {
       a.slist_on = 0;
       const size_t o = offsetof(rt_kernel_arg_t, slist_on);
       const int rs = r->copy_async ? r->copy_async(r->args, &a.slist_on, o, sizeof(a.slist_on))
                                    : vx_copy_to_dev(r->args, &a.slist_on, o, sizeof(a.slist_on));
       if (rs != 0) return set_error("slist_on upload failed");
     }
+    a.slist_on = 0;  // (the host's view: the lists are not in use)
     r->sl_stale = true;
     r->sl_static = 0;
     return 0;

@@ -297,6 +297,7 @@ int rt_renderer_create(rt_scene_h s, const char* kernel_dir, rt_renderer_h* out)
   // the moving-light policy (rt_renderer_set_list_policy); env RT_SLIST_DEFER
   if (const char* e = std::getenv("RT_SLIST_DEFER")) r->sl_defer = (uint32_t)std::atoi(e);
   r->set_tag = (vx_hip_set_launch_tag_t)vx_driver_symbol("vx_hip_set_launch_tag");
+  r->set_words = (vx_hip_set_launch_words_t)vx_driver_symbol("vx_hip_set_launch_words");
   r->host_mem = (vx_hip_host_mem_t)vx_driver_symbol("vx_hip_host_mem");
   if (r->host_mem) {
     void* h = nullptr;
@@ -1055,6 +1056,17 @@ int rt_render_start(rt_renderer_h r) {
   const uint32_t f = r->params.flags;
   const int mode = (f & RT_RENDER_PATH) ? 1 : (f & RT_RENDER_FLAT) ? 2 : (f & RT_RENDER_RASTER) ? 3 : 0;
   const int k = (f & RT_RENDER_INSTRUMENTED) && mode != 3 ? 1 : 0;
+  // every launch of the frame carries its light (and, while the lists wait
+  // for a light that stays, the switch to the BVH walk) in its launch words:
+  // rt_renderer_set_light queues no copy
+  uint32_t lw[4] = {0, 0, 0, 0};
+  if (r->set_words) {
+    std::memcpy(lw, r->arg.light, sizeof(r->arg.light));
+    lw[3] = RT_LW_LIGHT | (r->sl_stale ? RT_LW_NO_SLIST : 0u);
+  }
+  auto start = [&](vx_buffer_h img) {
+    return (!r->set_words || r->set_words(r->dev, lw, 4) == 0) && vx_start(r->dev, img, r->args) == 0;
+  };
   // counter rows only when the caller wants rt_render_stats' counts
   if (r->set_counters &&
       r->set_counters(r->dev, (f & (RT_RENDER_COUNTERS | RT_RENDER_INSTRUMENTED)) ? 1 : 0) != 0)
@@ -1062,8 +1074,7 @@ int rt_render_start(rt_renderer_h r) {
   // a frame of the two-kernel path tracer is one launch group of 2
   if (mode == 1 && r->pq) {
     if (r->launch_group(r->dev, 2) != 0) return fail("vx_hip_launch_group failed");
-    if (vx_start(r->dev, r->krnl_pq[0][k], r->args) == 0 && vx_start(r->dev, r->krnl_pq[1][k], r->args) == 0)
-      return 0;
+    if (start(r->krnl_pq[0][k]) && start(r->krnl_pq[1][k])) return 0;
     r->launch_group(r->dev, 0);  // abandon the half-issued group: later launches stand alone
     return fail("vx_start failed");
   }
@@ -1072,7 +1083,7 @@ int rt_render_start(rt_renderer_h r) {
   const bool bvh = mode == 0 && (f & RT_RENDER_BVH_WALK) && !r->deep && (r->arg.flags & RT_FLAG_BVH4H) &&
                    r->krnl_bvh[k];
   vx_buffer_h img = bvh ? r->krnl_bvh[k] : r->krnl[mode][k];
-  return vx_start(r->dev, img, r->args) == 0 ? 0 : fail("vx_start failed");
+  return start(img) ? 0 : fail("vx_start failed");
 }
 
 int rt_render_wait(rt_renderer_h r) {

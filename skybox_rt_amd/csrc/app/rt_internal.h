@@ -85,6 +85,7 @@ struct rt_renderer {
   SetupScratch su;
   vx_hip_copy_to_dev_async_t copy_async = nullptr;
   vx_hip_set_launch_tag_t set_tag = nullptr;
+  vx_hip_set_launch_words_t set_words = nullptr;  // a frame's light + flags (RT_LW_*)
   vx_hip_host_mem_t host_mem = nullptr;
   volatile uint32_t* stat_host = nullptr;  // pinned status words (+ nonce) of the setup sequences
   uint64_t stat_dev = 0;

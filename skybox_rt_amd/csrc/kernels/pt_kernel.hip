@@ -660,7 +660,7 @@ VX_MAIN(rt_kernel_arg_t, arg, PT_BLOCK) {
   const uint64_t t_cyc0 = __builtin_amdgcn_s_memtime();
 #endif
   Counters cnt;
-  Scene S = load_scene(arg);
+  Scene S = load_scene(arg, vx_launch_words);
 #if PT_MODE == 0
   if (threadIdx.x == 0) { s_pt.n[0] = 0; s_pt.n[1] = 0; }
   __syncthreads();

@@ -55,6 +55,13 @@
 #define RT_FLAG_BVH4H    0x80u   // BVH4 node steps read the binary16 rt_node4h_t form
 #define RT_FLAG_COVERAGE 0x100u  // raster mode: covered pixels white, no shading / OM
 
+// a render launch's words (vortex_hip.h vx_hip_set_launch_words, vx_spawn.h
+// vx_launch_words; rt_render_start sets them on every frame): w[0..2] the
+// frame's light (float bits), w[3] flags -- a moved light reaches the frame
+// in its dispatch packet, not through a copy into the argument block
+#define RT_LW_LIGHT    0x1u  // w[0..2] is the light (over arg.light)
+#define RT_LW_NO_SLIST 0x2u  // the light-space lists are stale: shadow rays walk the BVH
+
 #define RT_DC_DEPTH   0x1u
 #define RT_DC_COLOR   0x2u
 #define RT_DC_TEX     0x4u

@@ -40,6 +40,9 @@
 #ifndef RT_FLAT
 #define RT_FLAT 0
 #endif
+#ifndef RT_PRIO_TILES
+#define RT_PRIO_TILES 0
+#endif
 #ifndef RT_PATHQ
 #define RT_PATHQ 0  // 1: image pt_primary, the path tracer's first kernel (rt_trace.h pathq_append)
 #endif
@@ -85,6 +88,11 @@ struct WaveLds {
 __device__ __forceinline__ void kernel_body(const vx_task_t& task, const Scene& S, WaveLds& w,
                                             Counters& cnt) {
   const uint32_t t = task.blockIdx.x;
+#if RT_PRIO_TILES
+  // A/B: the waves of the first RT_PRIO_TILES tiles of the work order (the
+  // heaviest) issue ahead of the others on their SIMD
+  if (((uint32_t)__builtin_amdgcn_readfirstlane(t) >> 10) < RT_PRIO_TILES) __builtin_amdgcn_s_setprio(3);
+#endif
   // the chunk's task map in scalar registers (every lane runs the same chunk)
   const ChunkMap cm = chunk_map(S, task_args(S), (uint32_t)__builtin_amdgcn_readfirstlane(t) >> 6);
   uint32_t x, y, out;
@@ -412,7 +420,7 @@ VX_MAIN(rt_kernel_arg_t, arg, RT_BLOCK_THREADS) {
   const uint64_t t_stamp0 = __builtin_amdgcn_s_memrealtime();
 #endif
   Counters cnt;
-  Scene S = load_scene(arg);
+  Scene S = load_scene(arg, vx_launch_words);
 #ifdef RT_STAMPS
   if (threadIdx.x == 0) __vx_mpm_lds[10] = (uint32_t)__builtin_amdgcn_s_memrealtime();
 #endif

@@ -70,7 +70,10 @@ struct Scene {
 // space, wave-uniform address): the scene's fields then live in SGPRs, and
 // the traversal loops form node / triangle addresses in scalar registers
 // instead of VGPR + readfirstlane.
-__device__ __forceinline__ Scene load_scene(const rt_kernel_arg_t* ga) {
+//
+// The frame's launch words (rt_common.h RT_LW_*), kernel arguments like the
+// tag, override the block's light and switch stale lists off.
+__device__ __forceinline__ Scene load_scene(const rt_kernel_arg_t* ga, const vx_launch_words_t& lw) {
   const uint64_t p = (uint64_t)ga;
   // (readfirstlane returns int: through uint32_t, or the low word sign-extends)
   const uint32_t lo = (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)p);
@@ -124,6 +127,12 @@ __device__ __forceinline__ Scene load_scene(const rt_kernel_arg_t* ga) {
   s.light[0] = a->light[0];
   s.light[1] = a->light[1];
   s.light[2] = a->light[2];
+  if (lw.w[3] & RT_LW_LIGHT) {
+    s.light[0] = __builtin_bit_cast(float, lw.w[0]);
+    s.light[1] = __builtin_bit_cast(float, lw.w[1]);
+    s.light[2] = __builtin_bit_cast(float, lw.w[2]);
+  }
+  if (lw.w[3] & RT_LW_NO_SLIST) s.slist_on = 0;
   return s;
 }
 

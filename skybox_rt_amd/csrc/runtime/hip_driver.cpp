@@ -358,7 +358,11 @@ class vx_device {
     // copied into the dispatch's kernarg segment by the launch call
     uint32_t tag = launch_tag_;
     launch_tag_ = 0;
-    void* kparams[1] = {&tag};
+    // and its four launch words (vx_hip_set_launch_words), after the tag
+    uint32_t words[4];
+    std::memcpy(words, launch_words_, sizeof(words));
+    std::memset(launch_words_, 0, sizeof(launch_words_));
+    void* kparams[2] = {&tag, words};
     const int slot = (int)(issued_ % kMaxQueue);
     // a run is timed (events) when it starts on an idle queue -- every run of
     // a start + wait loop -- and then every time_every_-th run: an event
@@ -503,8 +507,10 @@ class vx_device {
         HIP_CHECK(hipEventElapsedTime(&ms, ev_start_[group_first_slot_[slot]], ev_stop_[slot]));
       }
       last_ms_ = ms;
+      last_stamped_ = tail_[slot];
       run_ms_total_ += ms;
       ++runs_timed_;
+      runs_stamped_ += tail_[slot] ? 1u : 0u;
     }
     return 0;
   }
@@ -602,6 +608,10 @@ class vx_device {
     return 0;
   }
   void set_launch_tag(uint32_t tag) { launch_tag_ = tag; }  // the next start()'s kernel argument
+  void set_launch_words(const uint32_t* w, uint32_t n) {       // and its launch words
+    std::memset(launch_words_, 0, sizeof(launch_words_));
+    std::memcpy(launch_words_, w, n * sizeof(uint32_t));
+  }
   // one pinned host buffer mapped into the device's address space (allocated
   // on first use, at most 64 KiB): kernels store to it, the host reads it
   // after waiting for the device -- no copy back
@@ -640,6 +650,14 @@ class vx_device {
   hipStream_t stream() const { return stream_; }
   int device_id() const { return device_id_; }
   double last_ms() const { return last_ms_; }
+  // which clock timed the runs: the completion kernel's stamps
+  // (a run started on an idle queue: kernel + launch boundary) or HIP events
+  // on the dispatch (queued runs: kernel only)
+  void timing_source(int* last_stamped, uint64_t* stamped, uint64_t* evented) const {
+    if (last_stamped) *last_stamped = last_stamped_ ? 1 : 0;
+    if (stamped) *stamped = runs_stamped_;
+    if (evented) *evented = runs_timed_ - runs_stamped_;
+  }
   void run_totals(double* ms, uint64_t* timed, uint64_t* runs) {
     wait_idle();
     if (ms) *ms = run_ms_total_;
@@ -750,6 +768,7 @@ class vx_device {
   bool stage_busy_[kStageSlots] = {};
   uint64_t stage_next_ = 0;
   uint32_t launch_tag_ = 0;
+  uint32_t launch_words_[4] = {};
   std::map<uint64_t, uint64_t> image_key_;  // image address -> module key
   hipStream_t stream_ = nullptr;
   static constexpr int kMaxQueue = 64;  // >= (depth_ + time_every_) * group_n_
@@ -789,6 +808,8 @@ class vx_device {
   bool mpm_dirty_ = false;
   bool counters_ = false, counters_env_ = false, last_rows_ = false;
   double last_ms_ = 0.0;
+  bool last_stamped_ = false;
+  uint64_t runs_stamped_ = 0;
   uint32_t last_grid_ = 0, last_block_ = 0;
   uint32_t dcrs_[VX_DCR_MIRROR_SIZE] = {};
   bool dcr_valid_[VX_DCR_MIRROR_SIZE] = {};
@@ -953,6 +974,20 @@ __attribute__((visibility("default"))) int vx_hip_host_mem(vx_device_h hdevice, 
   if (hdevice == nullptr || host == nullptr || device_addr == nullptr) return -1;
   return ((vx_device*)hdevice)->host_mem(size, host, device_addr);
 }
+__attribute__((visibility("default"))) int vx_hip_timing_source(vx_device_h hdevice, int* last_stamped,
+                                                                uint64_t* stamped_runs, uint64_t* event_runs) {
+  if (hdevice == nullptr) return -1;
+  ((vx_device*)hdevice)->timing_source(last_stamped, stamped_runs, event_runs);
+  return 0;
+}
+
+__attribute__((visibility("default"))) int vx_hip_set_launch_words(vx_device_h hdevice, const uint32_t* words,
+                                                                   uint32_t n) {
+  if (hdevice == nullptr || (n > 0 && words == nullptr) || n > 4) return -1;
+  ((vx_device*)hdevice)->set_launch_words(words, n);
+  return 0;
+}
+
 __attribute__((visibility("default"))) int vx_hip_set_launch_tag(vx_device_h hdevice, uint32_t tag) {
   if (hdevice == nullptr) return -1;
   ((vx_device*)hdevice)->set_launch_tag(tag);

@@ -49,7 +49,8 @@ def test_driver_exports_vx_dev_init_and_extensions():
     h = C.CDLL(os.path.join(_lib.LIB_DIR, "libvortex-hip.so"))
     for n in ("vx_dev_init", "vx_hip_mem_ptr", "vx_hip_stream", "vx_hip_last_run", "vx_hip_device_id",
               "vx_hip_run_totals", "vx_hip_mpm_rows", "vx_hip_set_counters", "vx_hip_set_timing",
-              "vx_hip_launch_group", "vx_hip_copy_to_dev_async", "vx_hip_set_launch_tag"):
+              "vx_hip_launch_group", "vx_hip_copy_to_dev_async", "vx_hip_set_launch_tag",
+              "vx_hip_set_launch_words", "vx_hip_timing_source"):
         assert hasattr(h, n)
 
 
