@@ -769,8 +769,12 @@ def main():
     dog.disarm()
     # the kernel's average duration: HIP events around a back-to-back run of
     # the same frames on the driver's stream (Run.kernel_clock)
-    clock_frames = max(50, min(args.steps, 1000))
-    avg_kernel_ms = run.kernel_clock(clock_frames, max(5, min(args.warmup, 20)))
+    # (at least 200 frames after 20 untimed ones: at the driver's 20-step
+    # command a 50-frame clock of a 0.03 ms frame is a 1.5 ms burst that
+    # still runs below the device's working clock)
+    clock_frames = max(200, min(args.steps, 1000))
+    clock_warmup = 20
+    avg_kernel_ms = run.kernel_clock(clock_frames, clock_warmup)
     st = r.stats()
     elapsed, rays_total = reduce_max_sum(dist, coll_dev, elapsed, run.rays_local)
     ms_per_step = elapsed / args.steps * 1e3
@@ -809,7 +813,7 @@ def main():
         sr = make_run(s, bvh_walk=bvh_walk, m=m, gather=gather)
         sst = r.setup_stats()
         e = sr.timed(args.steps, args.warmup, dist)
-        k = sr.kernel_clock(clock_frames, max(5, min(args.warmup, 20)))
+        k = sr.kernel_clock(clock_frames, clock_warmup)
         e, rays = reduce_max_sum(dist, coll_dev, e, sr.rays_local)
         roof, issue = make_roofline(sr.inst, k, "bvh" if bvh_walk else m, s, node_bytes, n_gpus=n_gpus)
         ent = {"workload": describe(s, m, sst, shadows and m != "flat", args.bounces, bvh_kind),

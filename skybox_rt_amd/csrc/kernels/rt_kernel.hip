@@ -40,9 +40,6 @@
 #ifndef RT_FLAT
 #define RT_FLAT 0
 #endif
-#ifndef RT_PRIO_TILES
-#define RT_PRIO_TILES 0
-#endif
 #ifndef RT_PATHQ
 #define RT_PATHQ 0  // 1: image pt_primary, the path tracer's first kernel (rt_trace.h pathq_append)
 #endif
@@ -88,11 +85,6 @@ struct WaveLds {
 __device__ __forceinline__ void kernel_body(const vx_task_t& task, const Scene& S, WaveLds& w,
                                             Counters& cnt) {
   const uint32_t t = task.blockIdx.x;
-#if RT_PRIO_TILES
-  // A/B: the waves of the first RT_PRIO_TILES tiles of the work order (the
-  // heaviest) issue ahead of the others on their SIMD
-  if (((uint32_t)__builtin_amdgcn_readfirstlane(t) >> 10) < RT_PRIO_TILES) __builtin_amdgcn_s_setprio(3);
-#endif
   // the chunk's task map in scalar registers (every lane runs the same chunk)
   const ChunkMap cm = chunk_map(S, task_args(S), (uint32_t)__builtin_amdgcn_readfirstlane(t) >> 6);
   uint32_t x, y, out;

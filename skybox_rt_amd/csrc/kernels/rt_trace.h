@@ -557,7 +557,13 @@ __device__ __forceinline__ int32_t trace_impl(const Scene& S, const Ray& r, floa
 // of the lanes on it -- a child's lanes are one v_cmp of the slab's near /
 // far values ANDed with `live`, no per-lane booleans materialised and
 // balloted again, no per-lane bit stack; BVH-walk frame 0.03436 -> 0.0324
-// ms, the heaviest tile alone 0.02919 -> 0.02756 (r06c).  The stack is
+// ms, the heaviest tile alone 0.02919 -> 0.02756 (r06c).  A node step has
+// no branch (r06f): every slot's box tested, empty slots dropped by a scalar
+// select, the pushes written unconditionally at the top with the top
+// advanced by need & (need - 1) -- a lone wave issues one instruction per
+// cycle slot, and a taken branch per slot cost more than the slot's work
+// (with the same for the primary packet walk: BVH-walk frame 0.03133 ->
+// 0.03087 ms, the heaviest tile alone 0.02644 -> 0.02526).  The stack is
 // three VGPRs, entry i in lane i (v_writelane / v_readlane: no LDS round
 // trip on the pop -> node-load chain): the ref and the lane mask's halves.
 // A node (64 B) and a leaf's records, two at a time, arrive through one
@@ -615,24 +621,39 @@ __device__ __forceinline__ bool occluded_packet(const Scene& S, const Ray& r, bo
       for (int i = 0; i < 4; ++i) {
         float tn, tf;
         slab_nf(lx[i], hx[i], ly[i], hy[i], lz[i], hz[i], r, 0.0f, tmax, &tn, &tf);
-        hm[i] = c[i] != RT_EMPTY_REF ? mask_fle(tn, tf) & live_m : 0u;
-        need |= hm[i] ? 1u << i : 0u;
+        // every slot's box tested, the empty slot's mask dropped by a scalar
+        // select afterwards: the volatile use pins the mask before the
+        // select, so no branch skips the VALU work of an empty slot
+        // (readfirstlane: an asm result counts as divergent, the mask is not);
+        // the slot's bit of `need` as integer arithmetic, min(popcount, 1):
+        // a bool here becomes a lane mask and a v_cndmask + readfirstlane
+        uint64_t m = mask_fle(tn, tf);
+        asm volatile("" : "+s"(m));
+        m = ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(m >> 32)) << 32) |
+            (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)m);
+        hm[i] = m & live_m & (c[i] == RT_EMPTY_REF ? 0ull : ~0ull);
+        const uint32_t pc = (uint32_t)__builtin_popcountll(hm[i]);
+        need |= (pc < 1u ? pc : 1u) << i;
       }
       if (need) {
+        // branch-free pushes: the slots after the first hit one, last slot
+        // first, each written at the top (the lanes at and above it are
+        // free) and kept by advancing the top -- no branch per slot
+        // (the pushed slots: need's bits but its lowest; the stack bound as
+        // a clamp -- at the bound the write lands on lane RT_MAX_STACK and
+        // the top stays, which is the bounded push's skip)
+        const uint32_t pm = need & (need - 1u);
 #pragma unroll
         for (int i = 3; i >= 1; --i) {
-          if ((need >> i) & 1u && (need & ((1u << i) - 1u))) {
-            if (sp < RT_MAX_STACK) {
-              vstk = vwritelane(vstk, c[i], sp);
-              vmlo = vwritelane(vmlo, (int32_t)(uint32_t)hm[i], sp);
-              vmhi = vwritelane(vmhi, (int32_t)(uint32_t)(hm[i] >> 32), sp);
-              ++sp;
-            }
-          }
+          vstk = vwritelane(vstk, c[i], sp);
+          vmlo = vwritelane(vmlo, (int32_t)(uint32_t)hm[i], sp);
+          vmhi = vwritelane(vmhi, (int32_t)(uint32_t)(hm[i] >> 32), sp);
+          const uint32_t nsp = (uint32_t)sp + ((pm >> i) & 1u);
+          sp = (int)(nsp < (uint32_t)RT_MAX_STACK ? nsp : (uint32_t)RT_MAX_STACK);
         }
-        const int f = __builtin_ctz(need);
-        ref = f == 0 ? c[0] : f == 1 ? c[1] : f == 2 ? c[2] : c[3];
-        live_m = f == 0 ? hm[0] : f == 1 ? hm[1] : f == 2 ? hm[2] : hm[3];
+        // the first hit slot by scalar selects
+        ref = (need & 1u) ? c[0] : (need & 2u) ? c[1] : (need & 4u) ? c[2] : c[3];
+        live_m = (need & 1u) ? hm[0] : (need & 2u) ? hm[1] : (need & 4u) ? hm[2] : hm[3];
         continue;
       }
     } else {
@@ -1304,18 +1325,17 @@ __device__ __forceinline__ int32_t trace_primary_packet(const Scene& S, uint32_t
         need |= ((m != 0) & (c[i] != RT_EMPTY_REF)) ? 1u << i : 0u;
       }
       if (need != 0u) {
-        // the slots are stored in ascending depth bound (vis.cpp SortSlots):
-        // the first needed slot is entered, the others pushed last slot first;
-        // unrolled over the slots so each c[i] is a fixed register
+        // branch-free pushes as in occluded_packet: every slot after the
+        // first needed one written at the top, the top advanced by its bit of
+        // need & (need - 1), clamped at the bound (the bounded push's skip)
+        const uint32_t pm = need & (need - 1u);
 #pragma unroll
         for (int i = 3; i >= 1; --i) {
-          if ((need >> i) & 1u && (need & ((1u << i) - 1u)) && sp < RT_MAX_STACK) {
-            vstk = vwritelane(vstk, c[i], sp);
-            ++sp;
-          }
+          vstk = vwritelane(vstk, c[i], sp);
+          const uint32_t nsp = (uint32_t)sp + ((pm >> i) & 1u);
+          sp = (int)(nsp < (uint32_t)RT_MAX_STACK ? nsp : (uint32_t)RT_MAX_STACK);
         }
-        const int f = __builtin_ctz(need);
-        ref = f == 0 ? c[0] : f == 1 ? c[1] : f == 2 ? c[2] : c[3];
+        ref = (need & 1u) ? c[0] : (need & 2u) ? c[1] : (need & 4u) ? c[2] : c[3];
         continue;
       }
     } else {
