@@ -8,6 +8,7 @@
 #   prof    rocprofv3 --kernel-trace --stats of bench.py --workload W --no-cpu-baseline $BENCH_ARGS
 #   pmc     scripts/pmc_profile.sh for MODES (default: shadow)
 #   timeline scripts/wave_timeline.py 1024 <mode> for TL_MODES (shadow, bvh, path; make diag)
+#   abtree  bench.py here against abtree/bench.py (another build), alternated ABTREE_ROUNDS times
 set -o pipefail
 cd "$GRAFT_REPO_ROOT"; mkdir -p gpurun_out; export TMPDIR=/tmp
 T=${TAG:-r05}
@@ -49,6 +50,18 @@ for s in ${STEPS:-tests bench}; do
         timeout -k 10 180 python $tl > gpurun_out/${T}_timeline_$m.json \
           2> gpurun_out/${T}_timeline_$m.err || { tail -5 gpurun_out/${T}_timeline_$m.err; exit 1; }
         head -c 1500 gpurun_out/${T}_timeline_$m.json; echo
+      done ;;
+    abtree)
+      # whole-bench A/B against another build staged in abtree/ (the
+      # previous commit's tree: a driver ABI change cannot be A/B'd as
+      # kernel-image variants), alternated ABTREE_ROUNDS times on this box
+      for i in $(seq ${ABTREE_ROUNDS:-2}); do
+        for side in new old; do
+          b=bench.py; [ $side = old ] && b=abtree/bench.py
+          timeout -k 10 300 python $b --no-cpu-baseline $BENCH_ARGS > gpurun_out/${T}_abtree_${side}_$i.json \
+            2> gpurun_out/${T}_abtree_${side}_$i.err || { tail -5 gpurun_out/${T}_abtree_${side}_$i.err; exit 1; }
+          python3 -c "import json;j=json.load(open('gpurun_out/${T}_abtree_${side}_$i.json'));c=j['config'];s=j.get('series',{});print('$side',$i,c['kernel_ms'],*[(k,v.get('kernel_ms'),v.get('ms_per_step')) for k,v in s.items()])"
+        done
       done ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac
