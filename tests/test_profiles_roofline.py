@@ -1,8 +1,10 @@
-"""The committed round-end evidence agrees with itself (CPU): for every bench
-workload, scripts/check_roofline.py recomputes the bench line's roofline
-fractions from the committed rocprofv3 summary + per-dispatch trace of the
-same command and the PMC record, and each agrees with the line within 5 %
-(the timed frames' rocprof average vs the line's kernel clock)."""
+"""The committed round-end evidence agrees with itself (CPU):
+scripts/check_roofline.py recomputes the round-end bench line's roofline
+fractions -- the headline's and every series entry's (the BVH walk, config
+4, config 2, the 4096^2 frame) -- from the committed rocprofv3 summary +
+per-dispatch trace of the same command and the PMC records, and each agrees
+with the line within 5 % (the timed frames' rocprof average vs the line's
+kernel clock)."""
 import json
 import os
 import subprocess
@@ -11,23 +13,27 @@ import sys
 import pytest
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-R05 = os.path.join(ROOT, "profiles", "r05")
+R06 = os.path.join(ROOT, "profiles", "r06")
 
 
-@pytest.mark.parametrize("workload", ["shadow", "path", "flat"])
-def test_round_end_roofline_recomputes(workload):
-    bench = os.path.join(R05, "final", f"bench_{workload}.json")
-    stats = os.path.join(R05, "prof", f"kernel_stats_{workload}.csv")
-    if not (os.path.exists(bench) and os.path.exists(stats)):
+def test_round_end_roofline_recomputes():
+    bench = os.path.join(R06, "final", "bench_under_rocprof.json")
+    stats = os.path.join(R06, "prof", "kernel_stats.csv")
+    trace = os.path.join(R06, "prof", "kernel_trace.csv.gz")
+    if not (os.path.exists(bench) and os.path.exists(stats) and os.path.exists(trace)):
         pytest.skip("round-end evidence not in this tree")
     p = subprocess.run([sys.executable, os.path.join(ROOT, "scripts", "check_roofline.py"), bench, stats,
-                        "--pmc", os.path.join(ROOT, "profiles", f"pmc_{workload}.json")],
-                       capture_output=True, text=True, cwd=ROOT, timeout=120)
+                        "--trace", trace], capture_output=True, text=True, cwd=ROOT, timeout=120)
     out = json.loads(p.stdout)
     assert out["ok"], out["checks"]
     assert "timed dispatches" in out.get("rocprof_avg_of", ""), out
     line = json.load(open(bench))
     assert abs(out["rocprof_avg_ms"] - line["config"]["kernel_ms"]) <= 0.05 * line["config"]["kernel_ms"]
+    # every HBM-bound series entry checked against its own image's dispatches
+    for name in ("bvh_walk", "path", "strong_4096"):
+        assert f"series.{name}.roofline.frac" in out["checks"], (name, sorted(out["checks"]))
+        assert name in out and out[name]["kernel"] == line["series"][name]["image"].split("entry ")[-1].rstrip(")")
+    assert "flat" in out
 
 
 def test_timed_region_picks_the_timed_dispatches(tmp_path):
