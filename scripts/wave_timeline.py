@@ -84,7 +84,9 @@ def main():
         out["slowest50"]["phases_us"] = {
             "to_primary": ph(12, 3), "primary": ph(3, 14), "layers": ph(14, 4), "shade": ph(4, 11),
             "plane_queue": ph(11, 5), "to_final_drain": ph(5, 15), "final_drain": ph(15, 13),
-            "nonfinal_drains": int((rows[slow, 6] > 0).sum())}
+            "nonfinal_drains": int((rows[slow, 6] > 0).sum()),
+            "final_drain_rays": float(rows[slow, 8].mean()),
+            "final_drain_rays_hist": np.histogram(rows[slow, 8], bins=[0, 1, 9, 17, 33, 49, 64])[0].tolist()}
         # s_memtime cycles waiting on the packet walks' record loads (slot 0
         # primary, 1 shadow) per wave, and per loop iteration
         pi = np.maximum(it[slow, 0] + it[slow, 1], 1)

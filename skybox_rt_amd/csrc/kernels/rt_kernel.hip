@@ -156,6 +156,7 @@ __device__ __forceinline__ void shadow_drain(bool final, const Scene& S, WaveLds
                                              Counters& cnt) {
 #ifdef RT_STAMPS
   if (final && lane_id() == 0) __vx_mpm_lds[15] = (uint32_t)__builtin_amdgcn_s_memrealtime();
+  if (final && lane_id() == 0) __vx_mpm_lds[8] = w.q_count;  // the final drain's shadow rays
   if (!final && w.q_count >= 64 && lane_id() == 0)
     __vx_mpm_lds[6] = (uint32_t)__builtin_amdgcn_s_memrealtime();
 #endif
